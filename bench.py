@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""bench.py — per-shard aggregation throughput on MI355X (BASELINE.json metric).
+
+Workload (default, `north_star`): terms(host){date_histogram(@timestamp,1h){stats(response_time_ms)}} over a
+1,000,000,000-doc synthetic log shard per GPU (BASELINE.md "north star": 1B docs / 1 shard / 1 GPU), columns
+HBM-resident before timing.  One step = one shard request: reset accumulators, collect the segment (fused gfx950
+kernel), postCollection + buildAggregation (top-k on the host, winners' rows gathered on the GPU), and the
+coordinator reduce (RCCL all-gather of the shard results across ranks when N > 1).
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  value = docs aggregated per second for the whole job (every rank owns one 1B-doc
+shard: weak scaling).  roofline = algorithmic HBM bytes of the collect kernel per launch / its HIP-event time.
+cpu_baseline = the oracle (line-by-line restatement of the reference Java collect loop, oracle/cpu_ref.cpp) on one
+host core over a bounded synthetic shard of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+WORKLOADS = {
+    # name: (fields, builder fn, filters fn, description, number_of_docs default)
+    "north_star": (("host", "@timestamp", "response_time_ms"), "terms(host){date_histogram(1h){stats(response_time_ms)}}"),
+    "config2": (("@timestamp", "response_time_ms"), "date_histogram(@timestamp,1h){extended_stats(response_time_ms)}"),
+    "config3": (("url",), "terms(url, size 10 => shard_size 80)"),
+    "config4": (("client_ip.hash",), "cardinality(client_ip.hash, precision_threshold 40000)"),
+    "config5": (("status", "bytes", "host", "@timestamp", "response_time_ms"),
+                "bool.filter[term(status:200), range(bytes:[1024,65536])] -> terms(host){date_histogram(1h){avg(response_time_ms)}}"),
+}
+
+
+def build_request(workload, world):
+    from elasticsearch_amd import AggregationBuilders as AB
+    from elasticsearch_amd import QueryBuilders as QB
+    if workload == "north_star":
+        return [AB.terms("hosts").field("host").size(10).subAggregation(
+            AB.dateHistogram("per_hour").field("@timestamp").interval("1h").subAggregation(
+                AB.stats("rt").field("response_time_ms")))], None
+    if workload == "config2":
+        return [AB.dateHistogram("per_hour").field("@timestamp").interval("1h").subAggregation(
+            AB.extendedStats("rt").field("response_time_ms"))], None
+    if workload == "config3":
+        return [AB.terms("urls").field("url").size(10)], None
+    if workload == "config4":
+        return [AB.cardinality("ips").field("client_ip.hash").precisionThreshold(40000)], None
+    if workload == "config5":
+        return ([AB.terms("hosts").field("host").size(10).subAggregation(
+            AB.dateHistogram("per_hour").field("@timestamp").interval("1h").subAggregation(AB.avg("rt").field("response_time_ms")))],
+            [QB.termQuery("status", 200), QB.rangeQuery("bytes").gte(1024).lte(65536)])
+    raise SystemExit(f"unknown workload {workload}")
+
+
+def cpu_baseline(workload, world, sample_docs):
+    """Oracle (cpu_ref restatement of the Java collect loop) on one host core over a sample_docs-doc synthetic shard."""
+    sys.path.insert(0, os.path.join(HERE, "oracle"))
+    sys.path.insert(0, os.path.join(HERE, "tests"))
+    import oracle as O
+    from helpers import synthetic_columns
+    fields = WORKLOADS[workload][0]
+    aggs, filters = build_request(workload, world)
+    cols = synthetic_columns(fields, sample_docs, shard=0)
+    _, secs = O.run([(cols, sample_docs)], aggs, filters=filters, number_of_shards=world, return_seconds=True)
+    return {"value": sample_docs / secs, "unit": "docs/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/cpu_ref.cpp single-threaded (one SEARCH thread per shard) over a {sample_docs:,}-doc "
+                      f"synthetic shard of the same request, collect+build timed ({secs:.2f} s)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--docs", type=int, default=1_000_000_000, help="docs per shard (one shard per GPU)")
+    ap.add_argument("--workload", default="north_star", choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-docs", type=int, default=64_000_000, help="CPU baseline sample size (0 = skip)")
+    ap.add_argument("--traffic", default=os.path.join(HERE, "profiles", "hbm_traffic.json"),
+                    help="PMC-derived HBM bytes per collect launch (profiles/), if measured for this workload")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        world = max(world, 1)
+
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+
+    import elasticsearch_amd as ea
+    engine = ea.Engine(local_rank if world > 1 else 0)
+    fields, desc = WORKLOADS[args.workload]
+    aggs, filters = build_request(args.workload, world)
+    seg = engine.synthetic_segment(args.docs, fields=fields, shard=rank)
+    plan = engine.plan(aggs, filters=filters, number_of_shards=world)
+    comm = None
+    if world > 1:
+        uid = [ea.Communicator.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = ea.Communicator(engine, world, rank, uid[0])
+
+    kernel_ms, kernel_bytes = [], 0
+    final = None
+
+    def step(record):
+        nonlocal final, kernel_bytes
+        plan.reset()
+        plan.collect(seg)
+        ms, nbytes, _ = plan.last_collect_stats()
+        if record:
+            kernel_ms.append(ms)
+            kernel_bytes = nbytes
+        res = plan.build()
+        final = comm.gather_reduce(res) if comm else ea.reduce([res])
+
+    for _ in range(args.warmup):
+        step(False)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ms_per_step = elapsed * 1000.0 / args.steps
+    value = args.docs * world / (elapsed / args.steps)
+    avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
+    achieved = kernel_bytes / (avg_kernel_ms / 1000.0) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic):
+        try:
+            with open(args.traffic) as f:
+                tr = json.load(f)
+            if tr.get("workload") == args.workload and tr.get("docs") == args.docs:
+                traffic = tr.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and args.cpu_docs > 0:
+            cpu = cpu_baseline(args.workload, world, args.cpu_docs)
+        out = {
+            "metric": "docs aggregated/sec (node) + achieved HBM GB/s, terms+date_histogram, 1B docs",
+            "value": value,
+            "unit": "docs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64/f64",
+            "data": "synthetic (deterministic splitmix64 log docs generated in HBM, seed 0x5EEDE1A5, shard = rank)",
+            "config": {"workload": args.workload, "request": desc, "docs_per_shard": args.docs, "shards": world,
+                       "parallelism": f"one shard per GPU x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+                         "kernel": "collect_kernel", "kernel_ms": avg_kernel_ms,
+                         "algorithmic_bytes_per_launch": kernel_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    plan.close()
+    seg.close()
+    if comm:
+        comm.close()
+    engine.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,390 @@
+"""Request builders mirroring the reference's Java API for this path.
+
+    AggregationBuilders.terms("keys").field("key").size(3).shardSize(3).order(Terms.Order.count(False))
+    AggregationBuilders.dateHistogram("histo").field("date").interval("1h").minDocCount(0)
+    QueryBuilders.termQuery("status", 200), QueryBuilders.rangeQuery("bytes").gte(1024).lte(65536)
+
+(core/src/main/java/org/elasticsearch/search/aggregations/AggregationBuilders.java and
+core/src/main/java/org/elasticsearch/index/query/QueryBuilders.java).  `flatten()` applies the parser defaults
+the reference applies before an AggregatorFactory exists (TermsParser.java:46-77 + BucketCountThresholds,
+DateHistogramParser.java:85-193, CardinalityParser.java:48-71, ExtendedStatsParser.java:57) and produces the
+flattened esgpu_agg_spec array of include/esgpu.h.
+"""
+import ctypes
+import re
+
+from . import _native as N
+
+# ---- DateHistogramParser.DATE_FIELD_UNITS (DateHistogramParser.java:50-69) ----
+DATE_FIELD_UNITS = {
+    "year": N.UNIT_YEAR, "1y": N.UNIT_YEAR, "quarter": N.UNIT_QUARTER, "1q": N.UNIT_QUARTER,
+    "month": N.UNIT_MONTH, "1M": N.UNIT_MONTH, "week": N.UNIT_WEEK, "1w": N.UNIT_WEEK,
+    "day": N.UNIT_DAY, "1d": N.UNIT_DAY, "hour": N.UNIT_HOUR, "1h": N.UNIT_HOUR,
+    "minute": N.UNIT_MINUTE, "1m": N.UNIT_MINUTE, "second": N.UNIT_SECOND, "1s": N.UNIT_SECOND,
+}
+
+_TIME_UNITS_MS = {"ms": 1, "s": 1000, "m": 60000, "h": 3600000, "d": 86400000, "w": 7 * 86400000}
+
+
+def parse_time_value(text):
+    """TimeValue.parseTimeValue subset: "<number><unit>" with unit in ms/s/m/h/d/w (plain numbers are millis)."""
+    m = re.fullmatch(r"\s*(-?\d+(?:\.\d+)?)\s*(ms|s|m|h|d|w)?\s*", str(text))
+    if not m:
+        raise ValueError(f"failed to parse time value [{text}]")
+    return int(float(m.group(1)) * _TIME_UNITS_MS[m.group(2) or "ms"])
+
+
+def parse_time_zone(tz):
+    """Fixed-offset time zones ("UTC", "+01:00", "-08:00", "-2") -> offset in ms.  DST zones are not supported."""
+    if tz is None or tz in ("UTC", "Z", "utc"):
+        return 0
+    m = re.fullmatch(r"([+-])?(\d{1,2})(?::?(\d{2}))?", tz)
+    if not m:
+        raise ValueError(f"only fixed-offset time zones are supported, got [{tz}]")
+    sign = -1 if m.group(1) == "-" else 1
+    return sign * (int(m.group(2)) * 3600000 + int(m.group(3) or 0) * 60000)
+
+
+class Order:
+    """Terms.Order (InternalOrder.java) and Histogram.Order."""
+
+    @staticmethod
+    def count(asc):
+        return N.ORDER_COUNT_ASC if asc else N.ORDER_COUNT_DESC
+
+    @staticmethod
+    def term(asc):
+        return N.ORDER_TERM_ASC if asc else N.ORDER_TERM_DESC
+
+    KEY_ASC = N.ORDER_KEY_ASC
+    KEY_DESC = N.ORDER_KEY_DESC
+    COUNT_ASC = N.ORDER_HCOUNT_ASC
+    COUNT_DESC = N.ORDER_HCOUNT_DESC
+
+
+class _Builder:
+    type = 0
+
+    def __init__(self, name):
+        self.name = name
+        self._field = None
+        self.subs = []
+
+    def field(self, f):
+        self._field = f
+        return self
+
+    def subAggregation(self, sub):  # noqa: N802 - mirrors the Java API
+        self.subs.append(sub)
+        return self
+
+    sub_aggregation = subAggregation
+
+
+class TermsBuilder(_Builder):
+    type = N.AGG_TERMS
+
+    def __init__(self, name):
+        super().__init__(name)
+        self._size, self._shard_size, self._min, self._shard_min = 10, -1, -1, -1
+        self._order = N.ORDER_COUNT_DESC
+        self._show_err = False
+
+    def size(self, n):
+        self._size = n
+        return self
+
+    def shardSize(self, n):  # noqa: N802
+        self._shard_size = n
+        return self
+
+    def minDocCount(self, n):  # noqa: N802
+        self._min = n
+        return self
+
+    def shardMinDocCount(self, n):  # noqa: N802
+        self._shard_min = n
+        return self
+
+    def order(self, o):
+        self._order = o
+        return self
+
+    def showTermDocCountError(self, b):  # noqa: N802
+        self._show_err = bool(b)
+        return self
+
+    shard_size = shardSize
+    min_doc_count = minDocCount
+
+
+class HistogramBuilder(_Builder):
+    type = N.AGG_HISTOGRAM
+
+    def __init__(self, name):
+        super().__init__(name)
+        self._interval = None
+        self._offset = 0
+        self._min = 0  # HistogramParser / DateHistogramParser: min_doc_count default 0
+        self._order = N.ORDER_KEY_ASC
+        self._keyed = False
+        self._bounds = (None, None)
+
+    def interval(self, i):
+        self._interval = i
+        return self
+
+    def offset(self, o):
+        self._offset = o
+        return self
+
+    def minDocCount(self, n):  # noqa: N802
+        self._min = n
+        return self
+
+    def order(self, o):
+        self._order = o
+        return self
+
+    def keyed(self, k):
+        self._keyed = bool(k)
+        return self
+
+    def extendedBounds(self, lo, hi):  # noqa: N802
+        self._bounds = (lo, hi)
+        return self
+
+    min_doc_count = minDocCount
+
+
+class DateHistogramBuilder(HistogramBuilder):
+    type = N.AGG_DATE_HISTOGRAM
+
+    def __init__(self, name):
+        super().__init__(name)
+        self._tz = None
+
+    def timeZone(self, tz):  # noqa: N802
+        self._tz = tz
+        return self
+
+    time_zone = timeZone
+
+
+class _MetricBuilder(_Builder):
+    def subAggregation(self, sub):  # noqa: N802
+        raise ValueError("Aggregator [%s] of type [%d] cannot accept sub-aggregations" % (self.name, self.type))
+
+
+class StatsBuilder(_MetricBuilder):
+    type = N.AGG_STATS
+
+
+class ExtendedStatsBuilder(_MetricBuilder):
+    type = N.AGG_EXTENDED_STATS
+
+    def __init__(self, name):
+        super().__init__(name)
+        self._sigma = 2.0
+
+    def sigma(self, s):
+        if s < 0:
+            raise ValueError("[sigma] must not be negative")
+        self._sigma = float(s)
+        return self
+
+
+class AvgBuilder(_MetricBuilder):
+    type = N.AGG_AVG
+
+
+class CardinalityBuilder(_MetricBuilder):
+    type = N.AGG_CARDINALITY
+
+    def __init__(self, name):
+        super().__init__(name)
+        self._threshold = -1
+
+    def precisionThreshold(self, t):  # noqa: N802
+        self._threshold = int(t)
+        return self
+
+    precision_threshold = precisionThreshold
+
+
+class AggregationBuilders:
+    terms = TermsBuilder
+    histogram = HistogramBuilder
+    dateHistogram = DateHistogramBuilder
+    date_histogram = DateHistogramBuilder
+    stats = StatsBuilder
+    extendedStats = ExtendedStatsBuilder
+    extended_stats = ExtendedStatsBuilder
+    avg = AvgBuilder
+    cardinality = CardinalityBuilder
+
+
+# ---- queries (bool.filter conjunction of term / range) ----
+class TermQuery:
+    def __init__(self, field, value):
+        self.field, self.value = field, value
+
+
+class RangeQuery:
+    def __init__(self, field):
+        self.field = field
+        self.lo = self.hi = None
+        self.include_lower = self.include_upper = True
+
+    def gte(self, v):
+        self.lo, self.include_lower = v, True
+        return self
+
+    def gt(self, v):
+        self.lo, self.include_lower = v, False
+        return self
+
+    def lte(self, v):
+        self.hi, self.include_upper = v, True
+        return self
+
+    def lt(self, v):
+        self.hi, self.include_upper = v, False
+        return self
+
+    def from_(self, v, include=True):
+        self.lo, self.include_lower = v, include
+        return self
+
+    def to(self, v, include=True):
+        self.hi, self.include_upper = v, include
+        return self
+
+
+class QueryBuilders:
+    @staticmethod
+    def termQuery(field, value):  # noqa: N802
+        return TermQuery(field, value)
+
+    @staticmethod
+    def rangeQuery(field):  # noqa: N802
+        return RangeQuery(field)
+
+    term_query = termQuery
+    range_query = rangeQuery
+
+
+# ---- flattening -------------------------------------------------------------------------------------------------
+def _rounding_params(b):
+    """-> (date_unit, interval, offset) with a fixed time-zone offset folded into OffsetRounding."""
+    if b.type == N.AGG_HISTOGRAM:
+        if b._interval is None or int(b._interval) < 1:
+            raise ValueError("[interval] must be 1 or greater for histogram aggregation [%s]" % b.name)
+        return N.UNIT_NONE, int(b._interval), int(b._offset)
+    if b._interval is None:
+        raise ValueError("Missing required field [interval] for histogram aggregation [%s]" % b.name)
+    off = b._offset if isinstance(b._offset, int) else parse_time_value(b._offset)
+    off -= parse_time_zone(b._tz)
+    unit = DATE_FIELD_UNITS.get(str(b._interval))
+    if unit is not None:
+        return unit, 0, off
+    return N.UNIT_NONE, parse_time_value(b._interval), off
+
+
+def _round_bound(unit, interval, offset, v):
+    """ExtendedBounds.round: the bound is rounded with the aggregation's rounding (affine roundings)."""
+    if v is None:
+        return None
+    if unit in (N.UNIT_NONE, N.UNIT_SECOND, N.UNIT_MINUTE, N.UNIT_HOUR, N.UNIT_DAY, N.UNIT_WEEK):
+        step = {N.UNIT_SECOND: 1000, N.UNIT_MINUTE: 60000, N.UNIT_HOUR: 3600000, N.UNIT_DAY: 86400000,
+                N.UNIT_WEEK: 7 * 86400000}.get(unit, interval)
+        off = offset - 3 * 86400000 if unit == N.UNIT_WEEK else offset
+        return ((v - off) // step) * step + off
+    raise ValueError("extended_bounds on calendar units are not supported")
+
+
+def thresholds(size, shard_size, min_doc_count, shard_min_doc_count, order, number_of_shards):
+    out = [ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int64()]
+    N.check(N.lib().esgpu_terms_thresholds(size, shard_size, min_doc_count, shard_min_doc_count, order,
+                                           number_of_shards, *[ctypes.byref(x) for x in out]))
+    return tuple(x.value for x in out)
+
+
+def flatten(aggs, number_of_shards=1):
+    """Builders -> ctypes array of AggSpec (parents before children, parser defaults applied)."""
+    specs = []
+    keep = []  # keep the encoded names alive
+
+    def enc(s):
+        b = s.encode("utf-8") if s is not None else None
+        keep.append(b)
+        return b
+
+    def visit(b, parent):
+        sp = N.AggSpec()
+        sp.type = b.type
+        sp.parent = parent
+        sp.name = enc(b.name)
+        sp.field = enc(b._field)
+        sp.sigma = 2.0
+        sp.precision_threshold = -1
+        if b.type == N.AGG_TERMS:
+            size, ssize, mn, smn = thresholds(b._size, b._shard_size, b._min, b._shard_min, b._order, number_of_shards)
+            sp.size, sp.shard_size, sp.min_doc_count, sp.shard_min_doc_count = size, ssize, mn, smn
+            sp.order = b._order
+            sp.show_term_doc_count_error = int(b._show_err)
+        elif b.type in (N.AGG_HISTOGRAM, N.AGG_DATE_HISTOGRAM):
+            unit, interval, off = _rounding_params(b)
+            sp.date_unit, sp.interval, sp.offset = unit, interval, off
+            sp.min_doc_count = b._min
+            sp.order = b._order
+            sp.keyed = int(b._keyed)
+            lo, hi = b._bounds
+            if lo is not None:
+                sp.has_extended_bounds_min = 1
+                sp.extended_bounds_min = _round_bound(unit, interval, off, lo)
+            if hi is not None:
+                sp.has_extended_bounds_max = 1
+                sp.extended_bounds_max = _round_bound(unit, interval, off, hi)
+        elif b.type == N.AGG_EXTENDED_STATS:
+            sp.sigma = b._sigma
+        elif b.type == N.AGG_CARDINALITY:
+            sp.precision_threshold = b._threshold
+        idx = len(specs)
+        specs.append(sp)
+        for s in b.subs:
+            visit(s, idx)
+
+    for a in aggs:
+        visit(a, -1)
+    arr = (N.AggSpec * max(len(specs), 1))(*specs)
+    return arr, len(specs), keep
+
+
+def flatten_filters(queries, ord_lookup=None):
+    """Queries -> ctypes array of Filter.  `ord_lookup(field, term) -> ordinal or -1` resolves keyword terms."""
+    out, keep = [], []
+    for q in queries or []:
+        f = N.Filter()
+        b = q.field.encode("utf-8")
+        keep.append(b)
+        f.field = b
+        if isinstance(q, TermQuery):
+            f.type = N.FILTER_TERM
+            v = q.value
+            if isinstance(v, str):
+                if ord_lookup is None:
+                    raise ValueError("keyword term filters need an ordinal lookup")
+                v = ord_lookup(q.field, v)
+            f.term = int(v)
+        else:
+            f.type = N.FILTER_RANGE
+            if q.lo is not None:
+                f.has_lower, f.include_lower = 1, int(q.include_lower)
+                f.lo_i, f.lo_d = int(q.lo) if float(q.lo).is_integer() else int(q.lo), float(q.lo)
+            if q.hi is not None:
+                f.has_upper, f.include_upper = 1, int(q.include_upper)
+                f.hi_i, f.hi_d = int(q.hi), float(q.hi)
+        out.append(f)
+    arr = (N.Filter * max(len(out), 1))(*out)
+    return arr, len(out), keep

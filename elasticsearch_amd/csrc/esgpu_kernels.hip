@@ -1,0 +1,641 @@
+// esgpu_kernels.hip — hand-written gfx950 kernels for the per-shard aggregation collection path.
+//
+//   zone_map_kernel      per-8192-doc-block min/max of an i64 column (segment upload, K11)
+//   synth_kernel         synthetic log-style shard generated in HBM (bench/test data)
+//   collect_kernel<...>  K1/K4/K5/K6/K7/K10 fused: filter predicates -> (term ord x rounded key) cell ->
+//                        doc count + stats/extended_stats/avg accumulators, LDS-privatised per workgroup with a
+//                        sliding key window over time-sorted blocks, flushed to HBM with coalesced atomics
+//   hll_kernel           K8: mix64 / murmur3-ord hashing, HLL++ register max + exact linear-counting set
+//   term_totals_kernel   outer-level doc counts from the [H][T] cell grid
+//   gather_rows_kernel   copies the surviving terms' rows (top shard_size) for the D2H build
+//
+// No MFMA: nothing on this path is a dense contraction.  Every kernel is an HBM stream; the per-doc work is
+// integer/LDS-atomic bound.  See DESIGN.md for the roofline accounting.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "es_common.hpp"
+#include "esgpu_kernels.hpp"
+
+namespace esgpu {
+
+// ------------------------------------------------------------------------------------------------------------
+// zone maps
+// ------------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void zone_map_kernel(const int64_t* __restrict__ v, const uint64_t* __restrict__ present,
+                                                       uint32_t n, int64_t* __restrict__ zmin, int64_t* __restrict__ zmax) {
+    const uint32_t block = blockIdx.x;
+    const uint32_t begin = block * kBlockDocs;
+    int64_t mn = INT64_MAX, mx = INT64_MIN;
+    for (uint32_t i = begin + threadIdx.x; i < begin + kBlockDocs && i < n; i += blockDim.x) {
+        if (present && !((present[i >> 6] >> (i & 63)) & 1)) continue;
+        const int64_t x = v[i];
+        mn = x < mn ? x : mn;
+        mx = x > mx ? x : mx;
+    }
+    __shared__ int64_t smn[256], smx[256];
+    smn[threadIdx.x] = mn;
+    smx[threadIdx.x] = mx;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            smn[threadIdx.x] = smn[threadIdx.x] < smn[threadIdx.x + s] ? smn[threadIdx.x] : smn[threadIdx.x + s];
+            smx[threadIdx.x] = smx[threadIdx.x] > smx[threadIdx.x + s] ? smx[threadIdx.x] : smx[threadIdx.x + s];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        zmin[block] = smn[0];
+        zmax[block] = smx[0];
+    }
+}
+
+void launch_zone_map(const int64_t* v, const uint64_t* present, uint32_t n, int64_t* zmin, int64_t* zmax,
+                     hipStream_t stream) {
+    const uint32_t nb = (n + kBlockDocs - 1) / kBlockDocs;
+    if (nb == 0) return;
+    hipLaunchKernelGGL(zone_map_kernel, dim3(nb), dim3(256), 0, stream, v, present, n, zmin, zmax);
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// synthetic shard
+// ------------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void synth_kernel(SynthParams P) {
+    const uint64_t sseed = shard_seed(P.seed, P.shard);
+    for (uint64_t d = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; d < P.n_pad; d += (uint64_t)gridDim.x * blockDim.x) {
+        const bool live = d < P.n;
+        if (P.ts) P.ts[d] = live ? synth_timestamp(sseed, d, P.n) : 0;
+        if (P.host) P.host[d] = live ? synth_host(sseed, d, P.host_cdf) : kMissingOrd;
+        if (P.url) P.url[d] = live ? synth_url(sseed, d, P.url_cdf) : kMissingOrd;
+        if (P.status) P.status[d] = live ? synth_status(sseed, d) : 0;
+        if (P.rt) P.rt[d] = live ? synth_rt(sseed, d, P.rt_cdf) : 0;
+        if (P.bytes) P.bytes[d] = live ? synth_bytes(sseed, d) : 0;
+        if (P.ip) P.ip[d] = live ? synth_ip_hash(sseed, d) : 0;
+        if (P.price) P.price[d] = live ? synth_price(sseed, d) : 0.0;
+    }
+}
+
+void launch_synth(const SynthParams& p, hipStream_t stream) {
+    hipLaunchKernelGGL(synth_kernel, dim3(4096), dim3(256), 0, stream, p);
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// collect
+// ------------------------------------------------------------------------------------------------------------
+constexpr int kWG = 512;                         // threads per workgroup (8 waves)
+constexpr int kVec = 4;                          // consecutive docs per thread per iteration
+constexpr int kIterDocs = kWG * kVec;            // 2048
+constexpr int kItersPerBlock = kBlockDocs / kIterDocs;  // 4
+
+struct Doc4 {
+    uint32_t ord[kVec];
+    int64_t hv[kVec];
+    double mv[kVec];
+    uint32_t ok;      // bit j: doc j passes filters / accept / bounds
+    uint32_t hpres;   // bit j: hist value present
+    uint32_t mpres;   // bit j: metric value present
+};
+
+__device__ __forceinline__ uint32_t bits4(const uint64_t* bm, uint32_t doc0) {
+    return (uint32_t)(bm[doc0 >> 6] >> (doc0 & 63)) & 0xFu;
+}
+
+__device__ __forceinline__ void load_i64x4(const int64_t* p, uint32_t doc0, int64_t out[4]) {
+    const longlong2 a = *reinterpret_cast<const longlong2*>(p + doc0);
+    const longlong2 b = *reinterpret_cast<const longlong2*>(p + doc0 + 2);
+    out[0] = a.x; out[1] = a.y; out[2] = b.x; out[3] = b.y;
+}
+__device__ __forceinline__ void load_f64x4(const double* p, uint32_t doc0, double out[4]) {
+    const double2 a = *reinterpret_cast<const double2*>(p + doc0);
+    const double2 b = *reinterpret_cast<const double2*>(p + doc0 + 2);
+    out[0] = a.x; out[1] = a.y; out[2] = b.x; out[3] = b.y;
+}
+__device__ __forceinline__ void load_u32x4(const uint32_t* p, uint32_t doc0, uint32_t out[4]) {
+    const uint4 a = *reinterpret_cast<const uint4*>(p + doc0);
+    out[0] = a.x; out[1] = a.y; out[2] = a.z; out[3] = a.w;
+}
+
+__device__ __forceinline__ uint32_t eval_pred(const PredDev& q, uint32_t doc0) {
+    uint32_t m = 0;
+    if (q.kind == PRED_ORD_EQ) {
+        uint32_t o[4];
+        load_u32x4((const uint32_t*)q.col, doc0, o);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m |= (uint32_t)((int64_t)o[j] == q.lo && o[j] != kMissingOrd) << j;
+    } else if (q.kind == PRED_F64_RANGE) {
+        double v[4];
+        load_f64x4((const double*)q.col, doc0, v);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool lo = q.lo_incl ? v[j] >= q.dlo : v[j] > q.dlo;
+            const bool hi = q.hi_incl ? v[j] <= q.dhi : v[j] < q.dhi;
+            m |= (uint32_t)(lo && hi) << j;
+        }
+    } else {  // PRED_I64_RANGE (term on a long is the degenerate range [t, t])
+        int64_t v[4];
+        load_i64x4((const int64_t*)q.col, doc0, v);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m |= (uint32_t)(v[j] >= q.lo && v[j] <= q.hi) << j;
+    }
+    if (q.present) m &= bits4(q.present, doc0);
+    return m;
+}
+
+template <bool ORD, bool HIST, int MET>
+__device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0, Doc4& d) {
+    uint32_t ok = 0xF;
+    if (doc0 + 4 > P.n_docs) ok = doc0 >= P.n_docs ? 0u : ((1u << (P.n_docs - doc0)) - 1u);
+    if (P.accept) ok &= bits4(P.accept, doc0);
+    for (int k = 0; k < P.npred; ++k) ok &= eval_pred(P.pred[k], doc0);
+    d.ok = ok;
+    if (ORD) load_u32x4(P.ord, doc0, d.ord);
+    if (HIST) {
+        load_i64x4(P.hv, doc0, d.hv);
+        d.hpres = P.hv_present ? bits4(P.hv_present, doc0) : 0xFu;
+    }
+    if (MET > 0) {
+        if (P.mv_f64) {
+            load_f64x4((const double*)P.mv, doc0, d.mv);
+        } else {
+            int64_t t[4];
+            load_i64x4((const int64_t*)P.mv, doc0, t);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) d.mv[j] = (double)t[j];  // FieldData.castToDouble
+        }
+        d.mpres = P.mv_present ? bits4(P.mv_present, doc0) : 0xFu;
+    }
+}
+
+// Accumulator views: either the workgroup's LDS window or the global cell grid.
+struct Acc {
+    uint32_t* cnt32;                // LDS
+    unsigned long long* cnt64;      // global
+    uint32_t* vcnt32;
+    unsigned long long* vcnt64;
+    double* sum;
+    unsigned long long* mn;
+    unsigned long long* mx;
+    double* sq;
+    uint32_t* ocnt32;
+    unsigned long long* ocnt64;
+};
+
+template <int MET, bool LDS>
+__device__ __forceinline__ void add_value(const Acc& a, uint32_t c, double x, bool has_vcnt) {
+    if (LDS) {
+        if (has_vcnt) atomicAdd(&a.vcnt32[c], 1u);
+    } else {
+        if (has_vcnt) atomicAdd(&a.vcnt64[c], 1ull);
+    }
+    atomicAdd(&a.sum[c], x);
+    if (MET >= 2) {
+        const bool nan = x != x;
+        const unsigned long long e = sortable(x);
+        const unsigned long long emn = nan ? 0ull : e;
+        const unsigned long long emx = nan ? ~0ull : e;
+        // read-check before the atomic: reads of one address broadcast, and min/max converge quickly
+        if (emn < a.mn[c]) atomicMin(&a.mn[c], emn);
+        if (emx > a.mx[c]) atomicMax(&a.mx[c], emx);
+    }
+    if (MET >= 3) atomicAdd(&a.sq[c], x * x);  // ExtendedStatsAggregator: sumOfSqr += value * value (no FMA)
+}
+
+// Per-doc update.  `slot` is the key index relative to the accumulator's first slot (window or grid).
+template <bool ORD, bool HIST, int MET, bool LDS>
+__device__ __forceinline__ void update_doc(const CollectParams& P, const Acc& a, uint32_t T, bool has_t, uint32_t t,
+                                           bool has_h, uint32_t slot, bool mpres, double x) {
+    if (P.ocnt_mode == OCNT_TERMS && has_t) {
+        if (LDS) atomicAdd(&a.ocnt32[t], 1u); else atomicAdd(&a.ocnt64[t], 1ull);
+    } else if (P.ocnt_mode == OCNT_HIST && has_h) {
+        if (LDS) atomicAdd(&a.ocnt32[slot], 1u); else atomicAdd(&a.ocnt64[slot], 1ull);
+    }
+    if (!(has_t && has_h)) return;
+    const uint32_t c = slot * T + t;
+    if (LDS) atomicAdd(&a.cnt32[c], 1u); else atomicAdd(&a.cnt64[c], 1ull);
+    if (MET > 0 && mpres) add_value<MET, LDS>(a, c, x, P.vcnt_mode != 0);
+}
+
+// Wave-level pre-aggregation for a cell shared by the whole wave (time-sorted data without a terms dimension):
+// one LDS atomic per quantity per wave instead of 256 conflicting ones.
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long w = __shfl_xor(v, o, 64);
+        v = w < v ? w : v;
+    }
+    return v;
+}
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long w = __shfl_xor(v, o, 64);
+        v = w > v ? w : v;
+    }
+    return v;
+}
+
+// key slot of a value relative to `base` (= value of the first slot); 32-bit magic division fast path
+__device__ __forceinline__ uint32_t slot_of(const CollectParams& P, int64_t v, int64_t base) {
+    if (P.fast32) return magic_div((uint32_t)((uint64_t)v - (uint64_t)base), P.mg_m, P.mg_s1, P.mg_s2, (uint32_t)P.interval);
+    return (uint32_t)(floor_div64(v - P.offset, P.interval) - floor_div64(base - P.offset, P.interval));
+}
+
+template <bool ORD, bool HIST, int MET, bool LDS>
+__device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, const Doc4& d, uint32_t T, int64_t base,
+                                         uint32_t W) {
+    uint32_t slot[kVec];
+    bool hv_ok[kVec];
+#pragma unroll
+    for (int j = 0; j < kVec; ++j) {
+        hv_ok[j] = true;
+        slot[j] = 0;
+        if (HIST) {
+            hv_ok[j] = (d.hpres >> j) & 1;
+            if (LDS) {
+                slot[j] = slot_of(P, d.hv[j], base);
+            } else {
+                const int64_t k = floor_div64(d.hv[j] - P.offset, P.interval) - P.key0;
+                hv_ok[j] = hv_ok[j] && k >= 0 && k < (int64_t)P.H;
+                slot[j] = (uint32_t)k;
+            }
+        }
+    }
+    if (LDS && !ORD && HIST && P.ocnt_mode == OCNT_NONE) {
+        // uniform-cell fast path: every valid doc of the wave maps to the same slot
+        uint32_t my = 0xFFFFFFFFu;
+        bool mixed = false;
+#pragma unroll
+        for (int j = 0; j < kVec; ++j) {
+            if (!((d.ok >> j) & 1) || !hv_ok[j]) continue;
+            if (my == 0xFFFFFFFFu) my = slot[j];
+            else mixed |= slot[j] != my;
+        }
+        const uint64_t has = __ballot(my != 0xFFFFFFFFu);
+        if (has == 0) return;
+        const int first = __ffsll((long long)has) - 1;
+        const uint32_t s0 = __shfl(my, first, 64);
+        const bool uniform = __all(!mixed && (my == 0xFFFFFFFFu || my == s0));
+        if (uniform && s0 < W) {
+            uint32_t cnt = 0, vc = 0;
+            double sum = 0.0, sq = 0.0;
+            unsigned long long mn = kMinInit, mx = kMaxInit;
+#pragma unroll
+            for (int j = 0; j < kVec; ++j) {
+                if (!((d.ok >> j) & 1) || !hv_ok[j]) continue;
+                ++cnt;
+                if (MET > 0 && ((d.mpres >> j) & 1)) {
+                    const double x = d.mv[j];
+                    ++vc;
+                    sum += x;
+                    if (MET >= 3) sq += x * x;
+                    if (MET >= 2) {
+                        const bool nan = x != x;
+                        const unsigned long long e = sortable(x);
+                        const unsigned long long emn = nan ? 0ull : e, emx = nan ? ~0ull : e;
+                        mn = emn < mn ? emn : mn;
+                        mx = emx > mx ? emx : mx;
+                    }
+                }
+            }
+            cnt = wave_sum_u32(cnt);
+            if (MET > 0) {
+                vc = wave_sum_u32(vc);
+                sum = wave_sum_f64(sum);
+                if (MET >= 2) { mn = wave_min_u64(mn); mx = wave_max_u64(mx); }
+                if (MET >= 3) sq = wave_sum_f64(sq);
+            }
+            if ((threadIdx.x & 63) == 0) {
+                const uint32_t c = s0;  // T == 1
+                atomicAdd(&a.cnt32[c], cnt);
+                if (MET > 0 && vc) {
+                    if (P.vcnt_mode) atomicAdd(&a.vcnt32[c], vc);
+                    atomicAdd(&a.sum[c], sum);
+                    if (MET >= 2) {
+                        if (mn < a.mn[c]) atomicMin(&a.mn[c], mn);
+                        if (mx > a.mx[c]) atomicMax(&a.mx[c], mx);
+                    }
+                    if (MET >= 3) atomicAdd(&a.sq[c], sq);
+                }
+            }
+            return;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kVec; ++j) {
+        if (!((d.ok >> j) & 1)) continue;
+        const uint32_t t = ORD ? d.ord[j] : 0u;
+        const bool has_t = ORD ? (t != kMissingOrd && t < T) : true;
+        update_doc<ORD, HIST, MET, LDS>(P, a, T, has_t, t, hv_ok[j], slot[j], MET > 0 && ((d.mpres >> j) & 1),
+                                        MET > 0 ? d.mv[j] : 0.0);
+    }
+}
+
+template <int MET>
+__device__ void flush_window(const CollectParams& P, const Acc& s, uint32_t T, uint32_t W, uint32_t win0) {
+    __syncthreads();
+    const uint32_t C = T * W;
+    for (uint32_t c = threadIdx.x; c < C; c += kWG) {
+        const uint32_t n = s.cnt32[c];
+        if (n == 0) continue;
+        const uint32_t local = c / T;
+        const uint32_t t = c - local * T;
+        const uint32_t slot = win0 + local;
+        if (slot >= P.H) continue;
+        const size_t g = (size_t)slot * T + t;
+        atomicAdd(&P.g_cnt[g], (unsigned long long)n);
+        s.cnt32[c] = 0;
+        if (MET > 0) {
+            if (P.vcnt_mode) { atomicAdd(&P.g_vcnt[g], (unsigned long long)s.vcnt32[c]); s.vcnt32[c] = 0; }
+            atomicAdd(&P.g_sum[g], s.sum[c]);
+            s.sum[c] = 0.0;
+            if (MET >= 2) {
+                const unsigned long long mn = s.mn[c], mx = s.mx[c];
+                if (mn != kMinInit) atomicMin(&P.g_min[g], mn);
+                if (mx != kMaxInit) atomicMax(&P.g_max[g], mx);
+                s.mn[c] = kMinInit;
+                s.mx[c] = kMaxInit;
+            }
+            if (MET >= 3) { atomicAdd(&P.g_sq[g], s.sq[c]); s.sq[c] = 0.0; }
+        }
+    }
+    if (P.ocnt_mode == OCNT_TERMS) {
+        for (uint32_t t = threadIdx.x; t < T; t += kWG) {
+            const uint32_t n = s.ocnt32[t];
+            if (n) { atomicAdd(&P.g_ocnt[t], (unsigned long long)n); s.ocnt32[t] = 0; }
+        }
+    } else if (P.ocnt_mode == OCNT_HIST) {
+        for (uint32_t l = threadIdx.x; l < W; l += kWG) {
+            const uint32_t n = s.ocnt32[l];
+            if (n && win0 + l < P.H) { atomicAdd(&P.g_ocnt[win0 + l], (unsigned long long)n); }
+            s.ocnt32[l] = 0;
+        }
+    }
+    __syncthreads();
+}
+
+template <bool ORD, bool HIST, int MET>
+__global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t T = ORD ? P.T : 1u;
+    const uint32_t W = HIST ? P.W : 1u;
+    const uint32_t C = T * W;
+
+    Acc g;  // global grid view
+    g.cnt32 = nullptr; g.vcnt32 = nullptr; g.ocnt32 = nullptr;
+    g.cnt64 = P.g_cnt; g.vcnt64 = P.g_vcnt; g.sum = P.g_sum; g.mn = P.g_min; g.mx = P.g_max; g.sq = P.g_sq;
+    g.ocnt64 = P.g_ocnt;
+
+    Acc s = g;  // LDS window view
+    if (P.lds_mode) {
+        size_t off = 0;
+        auto carve = [&](size_t bytes) { unsigned char* p = smem + off; off += (bytes + 15) & ~(size_t)15; return p; };
+        s.cnt32 = (uint32_t*)carve(sizeof(uint32_t) * C);
+        s.vcnt32 = P.vcnt_mode ? (uint32_t*)carve(sizeof(uint32_t) * C) : nullptr;
+        if (MET > 0) s.sum = (double*)carve(sizeof(double) * C);
+        if (MET >= 2) { s.mn = (unsigned long long*)carve(8 * C); s.mx = (unsigned long long*)carve(8 * C); }
+        if (MET >= 3) s.sq = (double*)carve(sizeof(double) * C);
+        if (P.ocnt_mode != OCNT_NONE) s.ocnt32 = (uint32_t*)carve(sizeof(uint32_t) * (P.ocnt_mode == OCNT_TERMS ? T : W));
+        for (uint32_t c = threadIdx.x; c < C; c += kWG) {
+            s.cnt32[c] = 0;
+            if (P.vcnt_mode) s.vcnt32[c] = 0;
+            if (MET > 0) s.sum[c] = 0.0;
+            if (MET >= 2) { s.mn[c] = kMinInit; s.mx[c] = kMaxInit; }
+            if (MET >= 3) s.sq[c] = 0.0;
+        }
+        if (P.ocnt_mode != OCNT_NONE)
+            for (uint32_t c = threadIdx.x; c < (P.ocnt_mode == OCNT_TERMS ? T : W); c += kWG) s.ocnt32[c] = 0;
+        __syncthreads();
+    }
+
+    const uint32_t b_begin = blockIdx.x * P.blocks_per_wg;
+    uint32_t b_end = b_begin + P.blocks_per_wg;
+    if (b_end > P.n_blocks) b_end = P.n_blocks;
+    if (b_begin >= b_end) return;
+
+    // window state (only meaningful with HIST && lds_mode)
+    uint32_t win0 = 0;
+    bool win_set = !(HIST && P.windowed);   // un-windowed: slot 0 of LDS == grid slot 0
+    bool dirty = false;
+    int64_t base = HIST ? P.key0 * P.interval + P.offset : 0;  // value of the first LDS slot
+
+    Doc4 cur;
+    const uint32_t tid4 = threadIdx.x * kVec;
+    load_docs<ORD, HIST, MET>(P, b_begin * kBlockDocs + tid4, cur);
+
+    for (uint32_t b = b_begin; b < b_end; ++b) {
+        // ---- per-block decision (wave-uniform: every lane reads the same zone-map words) ----
+        bool use_lds = P.lds_mode != 0;
+        if (use_lds && HIST && P.windowed) {
+            const int64_t zmn = P.zmin[b], zmx = P.zmax[b];
+            if (zmn <= zmx) {  // block has at least one timestamp
+                const int64_t kmn = floor_div64(zmn - P.offset, P.interval) - P.key0;
+                const int64_t kmx = floor_div64(zmx - P.offset, P.interval) - P.key0;
+                if (kmx - kmn + 1 > (int64_t)W) {
+                    use_lds = false;  // block spans more keys than the window: global atomics for this block
+                } else if (!win_set || kmn < (int64_t)win0 || kmx >= (int64_t)win0 + (int64_t)W) {
+                    if (dirty) flush_window<MET>(P, s, T, W, win0);
+                    dirty = false;
+                    win0 = (uint32_t)kmn;
+                    win_set = true;
+                    base = (P.key0 + (int64_t)win0) * P.interval + P.offset;
+                }
+            }
+        }
+        for (int it = 0; it < kItersPerBlock; ++it) {
+            // software pipeline: issue the next iteration's loads before this iteration's LDS updates
+            Doc4 nxt;
+            const bool last = (b + 1 == b_end) && (it + 1 == kItersPerBlock);
+            if (!last) {
+                const uint32_t nb = it + 1 == kItersPerBlock ? b + 1 : b;
+                const int nit = it + 1 == kItersPerBlock ? 0 : it + 1;
+                load_docs<ORD, HIST, MET>(P, nb * kBlockDocs + nit * kIterDocs + tid4, nxt);
+            }
+            if (use_lds) {
+                process4<ORD, HIST, MET, true>(P, s, cur, T, base, W);
+                dirty = true;
+            } else {
+                process4<ORD, HIST, MET, false>(P, g, cur, T, base, W);
+            }
+            if (!last) cur = nxt;
+        }
+    }
+    if (P.lds_mode && (dirty || !(HIST && P.windowed))) flush_window<MET>(P, s, T, W, win0);
+}
+
+template <bool ORD, bool HIST, int MET>
+static void launch_t(const CollectParams& p, uint32_t grid, size_t lds, hipStream_t st) {
+    hipLaunchKernelGGL((collect_kernel<ORD, HIST, MET>), dim3(grid), dim3(kWG), lds, st, p);
+}
+
+template <bool ORD, bool HIST>
+static void launch_m(const CollectParams& p, int met, uint32_t grid, size_t lds, hipStream_t st) {
+    switch (met) {
+        case 0: launch_t<ORD, HIST, 0>(p, grid, lds, st); break;
+        case 1: launch_t<ORD, HIST, 1>(p, grid, lds, st); break;
+        case 2: launch_t<ORD, HIST, 2>(p, grid, lds, st); break;
+        default: launch_t<ORD, HIST, 3>(p, grid, lds, st); break;
+    }
+}
+
+void launch_collect(const CollectParams& p, bool ord, bool hist, int met, uint32_t grid, size_t lds, hipStream_t st) {
+    if (ord && hist) launch_m<true, true>(p, met, grid, lds, st);
+    else if (ord) launch_m<true, false>(p, met, grid, lds, st);
+    else if (hist) launch_m<false, true>(p, met, grid, lds, st);
+    else launch_m<false, false>(p, met, grid, lds, st);
+}
+
+template <bool ORD, bool HIST, int MET>
+static int occ_t(size_t lds) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, collect_kernel<ORD, HIST, MET>, kWG, lds) != hipSuccess) n = 1;
+    return n;
+}
+template <bool ORD, bool HIST>
+static int occ_m(int met, size_t lds) {
+    switch (met) {
+        case 0: return occ_t<ORD, HIST, 0>(lds);
+        case 1: return occ_t<ORD, HIST, 1>(lds);
+        case 2: return occ_t<ORD, HIST, 2>(lds);
+        default: return occ_t<ORD, HIST, 3>(lds);
+    }
+}
+int collect_occupancy(bool ord, bool hist, int met, size_t lds) {
+    if (ord && hist) return occ_m<true, true>(met, lds);
+    if (ord) return occ_m<true, false>(met, lds);
+    if (hist) return occ_m<false, true>(met, lds);
+    return occ_m<false, false>(met, lds);
+}
+
+size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode) {
+    const size_t C = (size_t)T * W;
+    auto r = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    size_t bytes = r(4 * C);
+    if (vcnt_mode) bytes += r(4 * C);
+    if (met > 0) bytes += r(8 * C);
+    if (met >= 2) bytes += 2 * r(8 * C);
+    if (met >= 3) bytes += r(8 * C);
+    if (ocnt_mode == OCNT_TERMS) bytes += r(4 * (size_t)T);
+    if (ocnt_mode == OCNT_HIST) bytes += r(4 * (size_t)W);
+    return bytes;
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// HLL++ (K8)
+// ------------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void hll_kernel(HllParams P) {
+    const uint32_t gsz = gridDim.x * blockDim.x;
+    for (uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < P.n_docs; i0 += gsz * 4) {
+        // check the linear-counting overflow flag once per 4 docs (relaxed agent-scope load: sees other XCDs)
+        const bool lc_live = __hip_atomic_load(P.lc_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= P.lc_threshold;
+        uint64_t hv[4];
+        uint32_t ok = 0xF;
+        if (i0 + 4 > P.n_docs) ok = (1u << (P.n_docs - i0)) - 1u;
+        if (P.accept) ok &= bits4(P.accept, i0);
+        for (int k = 0; k < P.npred; ++k) ok &= eval_pred(P.pred[k], i0);
+        if (P.kind == HLL_ORD) {
+            uint32_t o[4];
+            load_u32x4((const uint32_t*)P.col, i0, o);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool valid = o[j] != kMissingOrd && o[j] < P.n_ords;
+                if (!valid) ok &= ~(1u << j);
+                hv[j] = valid ? P.ord_hash[o[j]] : 0;
+            }
+        } else {
+            int64_t v[4];
+            load_i64x4((const int64_t*)P.col, i0, v);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint64_t bits = (uint64_t)v[j];
+                if (P.kind == HLL_F64) {  // doubleToLongBits canonicalises NaN
+                    const double x = bits_dbl(bits);
+                    if (x != x) bits = 0x7ff8000000000000ULL;
+                }
+                hv[j] = mix64(bits);
+            }
+            if (P.present) ok &= bits4(P.present, i0);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (!((ok >> j) & 1)) continue;
+            const uint64_t h = hv[j];
+            const uint32_t idx = hll_index(h, P.p);
+            const uint32_t rl = hll_run_len(h, P.p);
+            if (rl > P.regs[idx]) atomicMax(&P.regs[idx], rl);
+            if (lc_live) {
+                const uint32_t enc = hll_encode(h, P.p);
+                uint32_t slot = (uint32_t)(mix64(enc) & P.lc_mask);
+                for (uint32_t probe = 0; probe <= P.lc_mask; ++probe) {
+                    const uint32_t cur = P.lc_set[slot];
+                    if (cur == enc) break;
+                    if (cur == 0) {
+                        const uint32_t prev = atomicCAS(&P.lc_set[slot], 0u, enc);
+                        if (prev == 0) { atomicAdd(P.lc_count, 1u); break; }
+                        if (prev == enc) break;
+                    }
+                    slot = (slot + 1) & P.lc_mask;
+                }
+            }
+        }
+    }
+}
+
+void launch_hll(const HllParams& p, hipStream_t st) {
+    uint32_t grid = (p.n_docs + 1023) / 1024;
+    if (grid > 8192) grid = 8192;
+    if (grid == 0) grid = 1;
+    hipLaunchKernelGGL(hll_kernel, dim3(grid), dim3(256), 0, st, p);
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// build helpers
+// ------------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void term_totals_kernel(const unsigned long long* __restrict__ cnt, uint32_t H, uint32_t T,
+                                                          unsigned long long* __restrict__ out) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    unsigned long long s = 0;
+    for (uint32_t h = 0; h < H; ++h) s += cnt[(size_t)h * T + t];
+    out[t] = s;
+}
+
+void launch_term_totals(const unsigned long long* cnt, uint32_t H, uint32_t T, unsigned long long* out, hipStream_t st) {
+    hipLaunchKernelGGL(term_totals_kernel, dim3((T + 255) / 256), dim3(256), 0, st, cnt, H, T, out);
+}
+
+// out[r][h] = src[h][rows[r]] for every column array (k rows x H slots)
+__global__ __launch_bounds__(256) void gather_rows_kernel(GatherParams P) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.k * P.H) return;
+    const uint32_t r = i / P.H, h = i - r * P.H;
+    const size_t src = (size_t)h * P.T + P.rows[r];
+    for (int a = 0; a < P.narrays; ++a) P.dst[a][i] = P.src[a][src];
+}
+
+void launch_gather_rows(const GatherParams& p, hipStream_t st) {
+    const uint32_t n = p.k * p.H;
+    if (n == 0) return;
+    hipLaunchKernelGGL(gather_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, st, p);
+}
+
+__global__ void fill_u64_kernel(unsigned long long* p, size_t n, unsigned long long v) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
+}
+void launch_fill_u64(unsigned long long* p, size_t n, unsigned long long v, hipStream_t st) {
+    if (n == 0) return;
+    size_t grid = (n + 255) / 256;
+    if (grid > 4096) grid = 4096;
+    hipLaunchKernelGGL(fill_u64_kernel, dim3((uint32_t)grid), dim3(256), 0, st, p, n, v);
+}
+
+}  // namespace esgpu

@@ -1,0 +1,115 @@
+// esgpu_kernels.hpp — launch interfaces between the host runtime (esgpu_runtime.cpp) and the gfx950 kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace esgpu {
+
+struct SynthParams {
+    uint64_t seed;
+    uint32_t shard;
+    uint32_t pad0;
+    uint64_t n;       // live docs
+    uint64_t n_pad;   // allocated (multiple of kBlockDocs)
+    int64_t* ts;
+    uint32_t* host;
+    uint32_t* url;
+    int64_t* status;
+    int64_t* rt;
+    int64_t* bytes;
+    uint64_t* ip;
+    double* price;
+    const double* host_cdf;
+    const double* url_cdf;
+    const double* rt_cdf;
+};
+
+enum PredKind : int32_t { PRED_ORD_EQ = 0, PRED_I64_RANGE = 1, PRED_F64_RANGE = 2 };
+
+struct PredDev {
+    const void* col;
+    const uint64_t* present;
+    int32_t kind;
+    int32_t lo_incl, hi_incl, pad;
+    int64_t lo, hi;    // ORD_EQ: lo = ordinal; I64_RANGE: inclusive [lo, hi]
+    double dlo, dhi;   // F64_RANGE with include flags
+};
+
+enum OcntMode : int32_t { OCNT_NONE = 0, OCNT_TERMS = 1, OCNT_HIST = 2 };
+
+struct CollectParams {
+    uint32_t n_docs, n_blocks, blocks_per_wg;
+    int32_t lds_mode;    // 1: LDS-privatised cells, 0: global atomics only
+    // terms dimension
+    const uint32_t* ord;
+    uint32_t T;
+    // histogram dimension
+    uint32_t H, W;
+    int32_t windowed;    // 1: W < H, slide a W-slot window using the zone maps
+    const int64_t* hv;
+    const uint64_t* hv_present;
+    int64_t interval, offset, key0;  // key index k of a value v: floor((v - offset) / interval) - key0
+    const int64_t* zmin;
+    const int64_t* zmax;
+    uint32_t mg_m, mg_s1, mg_s2;
+    int32_t fast32;
+    // metric
+    const void* mv;
+    const uint64_t* mv_present;
+    int32_t mv_f64;
+    int32_t vcnt_mode;   // separate value counts (metric column has missing values)
+    int32_t ocnt_mode;   // separate outer-level doc counts (inner dimension column has missing values)
+    int32_t npred;
+    PredDev pred[4];
+    const uint64_t* accept;
+    // global cell grid [H][T]
+    unsigned long long* g_cnt;
+    unsigned long long* g_ocnt;
+    unsigned long long* g_vcnt;
+    double* g_sum;
+    unsigned long long* g_min;
+    unsigned long long* g_max;
+    double* g_sq;
+};
+
+enum HllKind : int32_t { HLL_I64 = 0, HLL_F64 = 1, HLL_ORD = 2 };
+
+struct HllParams {
+    uint32_t n_docs;
+    int32_t p;
+    int32_t kind;
+    int32_t npred;
+    const void* col;
+    const uint64_t* present;
+    const uint64_t* ord_hash;   // HLL_ORD: murmur3 h1 of each term
+    uint64_t n_ords;            // HLL_ORD: entries of ord_hash (ordinals >= n_ords are treated as missing)
+    const uint64_t* accept;
+    PredDev pred[4];
+    unsigned int* regs;         // 2^p u32 registers
+    unsigned int* lc_set;       // open-addressing set of encoded hashes (0 = empty)
+    unsigned int* lc_count;
+    uint32_t lc_mask;
+    uint32_t lc_threshold;
+};
+
+struct GatherParams {
+    const uint32_t* rows;
+    uint32_t k, H, T;
+    int32_t narrays;
+    const unsigned long long* src[6];
+    unsigned long long* dst[6];
+};
+
+void launch_zone_map(const int64_t* v, const uint64_t* present, uint32_t n, int64_t* zmin, int64_t* zmax, hipStream_t s);
+void launch_synth(const SynthParams& p, hipStream_t s);
+void launch_collect(const CollectParams& p, bool ord, bool hist, int met, uint32_t grid, size_t lds, hipStream_t s);
+size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode);
+int collect_occupancy(bool ord, bool hist, int met, size_t lds);  // resident workgroups per CU
+void launch_hll(const HllParams& p, hipStream_t s);
+void launch_term_totals(const unsigned long long* cnt, uint32_t H, uint32_t T, unsigned long long* out, hipStream_t s);
+void launch_gather_rows(const GatherParams& p, hipStream_t s);
+void launch_fill_u64(unsigned long long* p, size_t n, unsigned long long v, hipStream_t s);
+
+}  // namespace esgpu

@@ -1,0 +1,1579 @@
+// esgpu_runtime.cpp — the C-ABI of libesgpu.so (include/esgpu.h): device contexts, HBM-resident segments,
+// aggregation plans compiled to gfx950 kernel launches, shard-level build, and the RCCL shard reduce.
+//
+// The plan mirrors the reference operator lifecycle (paths relative to
+// /root/reference/core/src/main/java/org/elasticsearch/search/aggregations/):
+//   esgpu_plan_create           AggregationPhase.preProcess / AggregatorFactories.createTopLevelAggregators
+//                               (AggregationPhase.java:69-94, AggregatorFactories.java:68-90)
+//   esgpu_plan_collect_segment  getLeafCollector + LeafBucketCollector.collect for every matching doc
+//                               (AggregatorBase.java:129-133, LeafBucketCollector.java:78-83)
+//   esgpu_plan_post_collection  postCollection (AggregatorBase.java:239-243)
+//   esgpu_plan_build            buildAggregation(0) (GlobalOrdinalsStringTermsAggregator.java:146-208,
+//                               HistogramAggregator.java:120-133, StatsAggegator.java:140-152, ...)
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/esgpu.h"
+#include "es_common.hpp"
+#include "esgpu_kernels.hpp"
+#include "esgpu_results.hpp"
+
+using namespace esgpu;
+
+// ------------------------------------------------------------------------------------------------------------
+// errors
+// ------------------------------------------------------------------------------------------------------------
+static thread_local std::string g_err;
+
+struct EsError : std::runtime_error {
+    int code;
+    EsError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIPX(expr)                                                                                            \
+    do {                                                                                                      \
+        hipError_t e_ = (expr);                                                                               \
+        if (e_ != hipSuccess)                                                                                 \
+            throw EsError(e_ == hipErrorOutOfMemory ? ESGPU_ERR_OOM : ESGPU_ERR_DEVICE,                       \
+                          std::string(#expr) + ": " + hipGetErrorString(e_));                                \
+    } while (0)
+
+template <class F>
+static int guarded(F&& f) {
+    try {
+        f();
+        return ESGPU_OK;
+    } catch (const EsError& e) {
+        g_err = e.what();
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        g_err = "host out of memory";
+        return ESGPU_ERR_OOM;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return ESGPU_ERR_INVALID;
+    }
+}
+
+static void require(bool c, int code, const std::string& msg) {
+    if (!c) throw EsError(code, msg);
+}
+
+extern "C" int esgpu_last_error(char* buf, size_t cap) {
+    if (buf && cap) {
+        const size_t n = std::min(cap - 1, g_err.size());
+        std::memcpy(buf, g_err.data(), n);
+        buf[n] = 0;
+    }
+    return (int)g_err.size();
+}
+extern "C" int esgpu_abi_version(void) { return ESGPU_ABI_VERSION; }
+
+// ------------------------------------------------------------------------------------------------------------
+// context + HBM accounting (the REQUEST/FIELDDATA circuit breakers' analogue, BigArrays.java:393-395)
+// ------------------------------------------------------------------------------------------------------------
+struct esgpu_ctx {
+    int device = 0;
+    int cus = 256;
+    uint64_t budget = 0;
+    std::atomic<uint64_t> used{0};
+    hipStream_t stream = nullptr;  // upload / generation stream
+    std::mutex mu;
+    // synthetic tables (device copies)
+    double* d_host_cdf = nullptr;
+    double* d_rt_cdf = nullptr;
+    double* d_url_cdf = nullptr;
+};
+
+struct DevBuf {
+    esgpu_ctx* ctx = nullptr;
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : ctx(o.ctx), p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+    DevBuf& operator=(DevBuf&& o) noexcept {
+        if (this != &o) {
+            release();
+            ctx = o.ctx; p = o.p; bytes = o.bytes;
+            o.p = nullptr; o.bytes = 0;
+        }
+        return *this;
+    }
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) {
+            (void)hipSetDevice(ctx->device);
+            (void)hipFree(p);
+            ctx->used -= bytes;
+            p = nullptr;
+            bytes = 0;
+        }
+    }
+    void alloc(esgpu_ctx* c, size_t n) {
+        release();
+        ctx = c;
+        if (n == 0) return;
+        if (c->used + n > c->budget)
+            throw EsError(ESGPU_ERR_OOM, "[request] Data too large: HBM budget of " + std::to_string(c->budget) +
+                                             " bytes would be exceeded by " + std::to_string(n) + " bytes");
+        HIPX(hipSetDevice(c->device));
+        HIPX(hipMalloc(&p, n));
+        bytes = n;
+        c->used += n;
+    }
+    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+extern "C" int esgpu_device_count(int* count) {
+    return guarded([&] {
+        int n = 0;
+        hipError_t e = hipGetDeviceCount(&n);
+        if (e != hipSuccess) n = 0;
+        *count = n;
+    });
+}
+
+extern "C" int esgpu_ctx_create(int device, uint64_t budget, esgpu_ctx** out) {
+    return guarded([&] {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+            throw EsError(ESGPU_ERR_NO_DEVICE, "no HIP device visible (libesgpu requires an MI355X / gfx950 GPU)");
+        require(device >= 0 && device < n, ESGPU_ERR_INVALID, "device ordinal out of range");
+        HIPX(hipSetDevice(device));
+        hipDeviceProp_t prop;
+        HIPX(hipGetDeviceProperties(&prop, device));
+        std::unique_ptr<esgpu_ctx> c(new esgpu_ctx());
+        c->device = device;
+        c->budget = budget ? budget : (uint64_t)(prop.totalGlobalMem * 0.9);
+        c->cus = prop.multiProcessorCount;
+        HIPX(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        *out = c.release();
+    });
+}
+
+extern "C" int esgpu_ctx_destroy(esgpu_ctx* c) {
+    return guarded([&] {
+        if (!c) return;
+        (void)hipSetDevice(c->device);
+        if (c->d_host_cdf) (void)hipFree(c->d_host_cdf);
+        if (c->d_rt_cdf) (void)hipFree(c->d_rt_cdf);
+        if (c->d_url_cdf) (void)hipFree(c->d_url_cdf);
+        if (c->stream) (void)hipStreamDestroy(c->stream);
+        delete c;
+    });
+}
+
+extern "C" int esgpu_ctx_hbm_used(const esgpu_ctx* c, uint64_t* bytes) {
+    return guarded([&] { *bytes = c->used.load(); });
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// synthetic data tables (host-computed once, identical for the host and device generators)
+// ------------------------------------------------------------------------------------------------------------
+static std::once_flag g_tables_once, g_url_once;
+static std::vector<double> g_host_cdf, g_rt_cdf, g_url_cdf;
+
+static void zipf_cdf(std::vector<double>& cdf, uint32_t n, double s) {
+    cdf.resize(n);
+    double total = 0;
+    for (uint32_t k = 1; k <= n; ++k) total += std::pow((double)k, -s);
+    double acc = 0;
+    for (uint32_t k = 1; k <= n; ++k) {
+        acc += std::pow((double)k, -s);
+        cdf[k - 1] = acc / total;
+    }
+    cdf[n - 1] = 1.0;
+}
+static void ensure_tables() {
+    std::call_once(g_tables_once, [] {
+        zipf_cdf(g_host_cdf, kHostTerms, 1.1);
+        g_rt_cdf.resize(kRtValues);
+        // response_time_ms: floor(lognormal(mu=4, sigma=1)) clamped to [0, 999]
+        for (uint32_t k = 0; k < kRtValues; ++k)
+            g_rt_cdf[k] = 0.5 * std::erfc(-(std::log((double)k + 1.0) - 4.0) / std::sqrt(2.0));
+        g_rt_cdf[kRtValues - 1] = 1.0;
+    });
+}
+static void ensure_url_table() {
+    std::call_once(g_url_once, [] { zipf_cdf(g_url_cdf, kUrlTerms, 1.0); });
+}
+
+static const char* synth_name(uint32_t bit) {
+    switch (bit) {
+        case ESGPU_SYNTH_TIMESTAMP: return "@timestamp";
+        case ESGPU_SYNTH_HOST: return "host";
+        case ESGPU_SYNTH_URL: return "url";
+        case ESGPU_SYNTH_STATUS: return "status";
+        case ESGPU_SYNTH_RESPONSE: return "response_time_ms";
+        case ESGPU_SYNTH_BYTES: return "bytes";
+        case ESGPU_SYNTH_CLIENT_IP: return "client_ip.hash";
+        case ESGPU_SYNTH_PRICE: return "price";
+    }
+    return nullptr;
+}
+
+extern "C" int esgpu_synthetic_term(uint32_t field_bit, uint64_t ord, char* buf, size_t cap) {
+    char tmp[32];
+    int n = 0;
+    if (field_bit == ESGPU_SYNTH_HOST) n = snprintf(tmp, sizeof tmp, "host-%04u", (unsigned)ord);
+    else if (field_bit == ESGPU_SYNTH_URL) n = snprintf(tmp, sizeof tmp, "/p/%08x", (unsigned)ord);
+    else return -1;
+    if (buf && cap) {
+        const size_t c = std::min((size_t)n, cap - 1);
+        std::memcpy(buf, tmp, c);
+        buf[c] = 0;
+    }
+    return n;
+}
+
+extern "C" int esgpu_synthetic_fill_host(uint64_t seed, uint32_t shard, uint32_t num_docs, uint32_t field_bit,
+                                         uint64_t start, uint64_t count, void* out) {
+    return guarded([&] {
+        ensure_tables();
+        if (field_bit == ESGPU_SYNTH_URL) ensure_url_table();
+        const uint64_t ss = shard_seed(seed, shard);
+        for (uint64_t i = 0; i < count; ++i) {
+            const uint64_t d = start + i;
+            switch (field_bit) {
+                case ESGPU_SYNTH_TIMESTAMP: ((int64_t*)out)[i] = synth_timestamp(ss, d, num_docs); break;
+                case ESGPU_SYNTH_HOST: ((uint32_t*)out)[i] = synth_host(ss, d, g_host_cdf.data()); break;
+                case ESGPU_SYNTH_URL: ((uint32_t*)out)[i] = synth_url(ss, d, g_url_cdf.data()); break;
+                case ESGPU_SYNTH_STATUS: ((int64_t*)out)[i] = synth_status(ss, d); break;
+                case ESGPU_SYNTH_RESPONSE: ((int64_t*)out)[i] = synth_rt(ss, d, g_rt_cdf.data()); break;
+                case ESGPU_SYNTH_BYTES: ((int64_t*)out)[i] = synth_bytes(ss, d); break;
+                case ESGPU_SYNTH_CLIENT_IP: ((uint64_t*)out)[i] = synth_ip_hash(ss, d); break;
+                case ESGPU_SYNTH_PRICE: ((double*)out)[i] = synth_price(ss, d); break;
+                default: throw EsError(ESGPU_ERR_INVALID, "unknown synthetic field");
+            }
+        }
+    });
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// segments
+// ------------------------------------------------------------------------------------------------------------
+struct DevColumn {
+    std::string name;
+    int32_t type = 0;
+    bool multi = false;
+    DevBuf values;   // padded to a multiple of kBlockDocs entries
+    DevBuf present;  // optional
+    DevBuf zmin, zmax;
+    int64_t vmin = INT64_MAX, vmax = INT64_MIN;  // over present values (I64 columns)
+    uint64_t value_count = 0;
+    // host dictionary (ORD): explicit bytes, or the synthetic formula
+    std::vector<uint8_t> dict_bytes;
+    std::vector<uint64_t> dict_offsets;
+    uint32_t synth_bit = 0;
+    DevBuf ord_hash;  // murmur3 h1 per term (built lazily for cardinality on keyword fields)
+
+    std::string term(uint64_t ord) const {
+        if (synth_bit) {
+            char b[32];
+            esgpu_synthetic_term(synth_bit, ord, b, sizeof b);
+            return b;
+        }
+        if (dict_offsets.empty()) return std::to_string(ord);
+        return std::string((const char*)dict_bytes.data() + dict_offsets[ord], (size_t)(dict_offsets[ord + 1] - dict_offsets[ord]));
+    }
+};
+
+struct esgpu_segment {
+    esgpu_ctx* ctx = nullptr;
+    uint32_t max_doc = 0;
+    uint32_t n_pad = 0;
+    std::map<std::string, std::unique_ptr<DevColumn>> cols;
+    const DevColumn* col(const char* name) const {
+        if (!name) return nullptr;
+        auto it = cols.find(name);
+        return it == cols.end() ? nullptr : it->second.get();
+    }
+};
+
+static uint32_t pad_docs(uint32_t n) { return (uint32_t)(((uint64_t)n + kBlockDocs - 1) / kBlockDocs * kBlockDocs); }
+
+static void build_zone_map(esgpu_ctx* c, DevColumn& col, uint32_t n) {
+    const uint32_t nb = (n + kBlockDocs - 1) / kBlockDocs;
+    col.zmin.alloc(c, (size_t)std::max(nb, 1u) * 8);
+    col.zmax.alloc(c, (size_t)std::max(nb, 1u) * 8);
+    launch_zone_map(col.values.as<int64_t>(), col.present.as<uint64_t>(), n, col.zmin.as<int64_t>(), col.zmax.as<int64_t>(),
+                    c->stream);
+    HIPX(hipGetLastError());
+    std::vector<int64_t> mn(nb), mx(nb);
+    if (nb) {
+        HIPX(hipMemcpyAsync(mn.data(), col.zmin.p, nb * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPX(hipMemcpyAsync(mx.data(), col.zmax.p, nb * 8, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPX(hipStreamSynchronize(c->stream));
+    for (uint32_t b = 0; b < nb; ++b) {
+        col.vmin = std::min(col.vmin, mn[b]);
+        col.vmax = std::max(col.vmax, mx[b]);
+    }
+}
+
+extern "C" int esgpu_segment_upload(esgpu_ctx* c, const esgpu_column_desc* cols, int32_t ncols, uint32_t max_doc,
+                                    esgpu_segment** out) {
+    return guarded([&] {
+        require(c && out && (ncols == 0 || cols), ESGPU_ERR_INVALID, "null argument");
+        require(max_doc <= 0x7FFFFFFFu, ESGPU_ERR_INVALID, "max_doc exceeds Lucene's int doc id space");
+        std::lock_guard<std::mutex> lk(c->mu);
+        HIPX(hipSetDevice(c->device));
+        std::unique_ptr<esgpu_segment> s(new esgpu_segment());
+        s->ctx = c;
+        s->max_doc = max_doc;
+        s->n_pad = pad_docs(max_doc);
+        for (int i = 0; i < ncols; ++i) {
+            const esgpu_column_desc& d = cols[i];
+            require(d.name && d.type >= ESGPU_COL_ORD_U32 && d.type <= ESGPU_COL_U64, ESGPU_ERR_INVALID, "bad column descriptor");
+            require(s->cols.find(d.name) == s->cols.end(), ESGPU_ERR_INVALID, std::string("duplicate column ") + d.name);
+            std::unique_ptr<DevColumn> col(new DevColumn());
+            col->name = d.name;
+            col->type = d.type;
+            col->value_count = d.value_count;
+            const size_t w = d.type == ESGPU_COL_ORD_U32 ? 4 : 8;
+            if (d.offsets) {
+                // multi-valued (SortedNumeric / SortedSet): kept host-free on device as CSR; the gfx950 collect
+                // kernels handle single-valued columns only in this version (plans over it are UNSUPPORTED).
+                col->multi = true;
+                const uint64_t nv = d.offsets[max_doc];
+                col->values.alloc(c, std::max<uint64_t>(nv, 1) * w);
+                if (nv) HIPX(hipMemcpyAsync(col->values.p, d.values, nv * w, hipMemcpyHostToDevice, c->stream));
+            } else {
+                col->values.alloc(c, (size_t)s->n_pad * w);
+                if (max_doc) HIPX(hipMemcpyAsync(col->values.p, d.values, (size_t)max_doc * w, hipMemcpyHostToDevice, c->stream));
+                if (s->n_pad > max_doc) {
+                    if (d.type == ESGPU_COL_ORD_U32)
+                        HIPX(hipMemsetAsync(col->values.as<uint8_t>() + (size_t)max_doc * w, 0xFF, (size_t)(s->n_pad - max_doc) * w, c->stream));
+                    else
+                        HIPX(hipMemsetAsync(col->values.as<uint8_t>() + (size_t)max_doc * w, 0, (size_t)(s->n_pad - max_doc) * w, c->stream));
+                }
+                if (d.present && d.type != ESGPU_COL_ORD_U32) {
+                    const size_t words = s->n_pad / 64;
+                    col->present.alloc(c, words * 8);
+                    HIPX(hipMemsetAsync(col->present.p, 0, words * 8, c->stream));
+                    HIPX(hipMemcpyAsync(col->present.p, d.present, ((size_t)max_doc + 63) / 64 * 8, hipMemcpyHostToDevice, c->stream));
+                }
+                if (d.type == ESGPU_COL_I64) build_zone_map(c, *col, max_doc);
+            }
+            if (d.type == ESGPU_COL_ORD_U32 && d.dict_bytes && d.dict_offsets) {
+                col->dict_offsets.assign(d.dict_offsets, d.dict_offsets + d.value_count + 1);
+                col->dict_bytes.assign(d.dict_bytes, d.dict_bytes + d.dict_offsets[d.value_count]);
+            }
+            s->cols[d.name] = std::move(col);
+        }
+        HIPX(hipStreamSynchronize(c->stream));
+        *out = s.release();
+    });
+}
+
+extern "C" int esgpu_segment_synthetic(esgpu_ctx* c, uint64_t seed, uint32_t shard, uint32_t num_docs, uint32_t mask,
+                                       esgpu_segment** out) {
+    return guarded([&] {
+        require(c && out, ESGPU_ERR_INVALID, "null argument");
+        require(num_docs <= 0x7FFFFFFFu, ESGPU_ERR_INVALID, "num_docs exceeds Lucene's int doc id space");
+        std::lock_guard<std::mutex> lk(c->mu);
+        HIPX(hipSetDevice(c->device));
+        ensure_tables();
+        if (!c->d_host_cdf) {
+            HIPX(hipMalloc(&c->d_host_cdf, kHostTerms * 8));
+            HIPX(hipMalloc(&c->d_rt_cdf, kRtValues * 8));
+            HIPX(hipMemcpy(c->d_host_cdf, g_host_cdf.data(), kHostTerms * 8, hipMemcpyHostToDevice));
+            HIPX(hipMemcpy(c->d_rt_cdf, g_rt_cdf.data(), kRtValues * 8, hipMemcpyHostToDevice));
+        }
+        if ((mask & ESGPU_SYNTH_URL) && !c->d_url_cdf) {
+            ensure_url_table();
+            HIPX(hipMalloc(&c->d_url_cdf, (size_t)kUrlTerms * 8));
+            HIPX(hipMemcpy(c->d_url_cdf, g_url_cdf.data(), (size_t)kUrlTerms * 8, hipMemcpyHostToDevice));
+        }
+        std::unique_ptr<esgpu_segment> s(new esgpu_segment());
+        s->ctx = c;
+        s->max_doc = num_docs;
+        s->n_pad = pad_docs(num_docs);
+        SynthParams p{};
+        p.seed = seed;
+        p.shard = shard;
+        p.n = num_docs;
+        p.n_pad = s->n_pad;
+        p.host_cdf = c->d_host_cdf;
+        p.rt_cdf = c->d_rt_cdf;
+        p.url_cdf = c->d_url_cdf;
+        for (uint32_t bit = 1; bit <= ESGPU_SYNTH_PRICE; bit <<= 1) {
+            if (!(mask & bit)) continue;
+            std::unique_ptr<DevColumn> col(new DevColumn());
+            col->name = synth_name(bit);
+            const bool ord = bit == ESGPU_SYNTH_HOST || bit == ESGPU_SYNTH_URL;
+            col->type = ord ? ESGPU_COL_ORD_U32 : bit == ESGPU_SYNTH_CLIENT_IP ? ESGPU_COL_U64
+                                                : bit == ESGPU_SYNTH_PRICE ? ESGPU_COL_F64 : ESGPU_COL_I64;
+            col->values.alloc(c, (size_t)s->n_pad * (ord ? 4 : 8));
+            if (ord) {
+                col->synth_bit = bit;
+                col->value_count = bit == ESGPU_SYNTH_HOST ? kHostTerms : kUrlTerms;
+            }
+            switch (bit) {
+                case ESGPU_SYNTH_TIMESTAMP: p.ts = col->values.as<int64_t>(); break;
+                case ESGPU_SYNTH_HOST: p.host = col->values.as<uint32_t>(); break;
+                case ESGPU_SYNTH_URL: p.url = col->values.as<uint32_t>(); break;
+                case ESGPU_SYNTH_STATUS: p.status = col->values.as<int64_t>(); break;
+                case ESGPU_SYNTH_RESPONSE: p.rt = col->values.as<int64_t>(); break;
+                case ESGPU_SYNTH_BYTES: p.bytes = col->values.as<int64_t>(); break;
+                case ESGPU_SYNTH_CLIENT_IP: p.ip = col->values.as<uint64_t>(); break;
+                case ESGPU_SYNTH_PRICE: p.price = col->values.as<double>(); break;
+            }
+            s->cols[col->name] = std::move(col);
+        }
+        launch_synth(p, c->stream);
+        HIPX(hipGetLastError());
+        HIPX(hipStreamSynchronize(c->stream));
+        for (auto& kv : s->cols)
+            if (kv.second->type == ESGPU_COL_I64) build_zone_map(c, *kv.second, num_docs);
+        *out = s.release();
+    });
+}
+
+extern "C" int esgpu_segment_destroy(esgpu_segment* s) {
+    return guarded([&] { delete s; });
+}
+
+extern "C" int esgpu_segment_max_doc(const esgpu_segment* s, uint32_t* max_doc) {
+    return guarded([&] { *max_doc = s->max_doc; });
+}
+
+extern "C" int esgpu_segment_read_column(const esgpu_segment* s, const char* field, uint64_t start, uint64_t count, void* out) {
+    return guarded([&] {
+        const DevColumn* col = s->col(field);
+        require(col != nullptr, ESGPU_ERR_INVALID, std::string("no such column: ") + (field ? field : "(null)"));
+        require(!col->multi && start + count <= s->max_doc, ESGPU_ERR_INVALID, "range out of bounds");
+        const size_t w = col->type == ESGPU_COL_ORD_U32 ? 4 : 8;
+        HIPX(hipSetDevice(s->ctx->device));
+        HIPX(hipMemcpy(out, col->values.as<uint8_t>() + start * w, count * w, hipMemcpyDeviceToHost));
+    });
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// parser helpers (TermsParser + BucketCountThresholds.ensureValidity, TermsAggregator.java:63-85,
+// BucketUtils.suggestShardSideQueueSize, bucket/BucketUtils.java:36-47)
+// ------------------------------------------------------------------------------------------------------------
+extern "C" int esgpu_terms_thresholds(int32_t size, int32_t shard_size, int64_t min_doc_count, int64_t shard_min_doc_count,
+                                      int32_t order, int32_t nshards, int32_t* o_size, int32_t* o_shard_size,
+                                      int64_t* o_min, int64_t* o_shard_min) {
+    return guarded([&] {
+        require(nshards >= 1, ESGPU_ERR_INVALID, "number_of_shards must be >= 1");
+        if (size < 0) size = 10;                    // TermsParametersParser.java:35 defaults
+        if (min_doc_count < 0) min_doc_count = 1;
+        if (shard_min_doc_count < 0) shard_min_doc_count = 0;
+        const bool term_order = order == ESGPU_ORDER_TERM_ASC || order == ESGPU_ORDER_TERM_DESC;
+        if (shard_size < 0) {
+            if (!term_order) {
+                if (nshards == 1) shard_size = size;
+                else {
+                    const int64_t sample = (int64_t)size * std::min(10, nshards);
+                    shard_size = (int32_t)std::min<int64_t>(INT32_MAX, std::max<int64_t>(10, sample));
+                }
+            } else {
+                shard_size = size;  // default shard_size (-1) with term order keeps -1 -> size below
+            }
+        }
+        if (shard_size == 0) shard_size = INT32_MAX;
+        if (size == 0) size = INT32_MAX;
+        if (shard_size < size) shard_size = size;
+        if (shard_min_doc_count > min_doc_count) shard_min_doc_count = min_doc_count;
+        require(size >= 0 && min_doc_count >= 0, ESGPU_ERR_INVALID,
+                "parameters [requiredSize] and [minDocCount] must be >=0 in terms aggregation.");
+        *o_size = size;
+        *o_shard_size = shard_size;
+        *o_min = min_doc_count;
+        *o_shard_min = shard_min_doc_count;
+    });
+}
+
+extern "C" int esgpu_murmur3_x64_128(const uint8_t* bytes, size_t len, int64_t seed, uint64_t* out2) {
+    return guarded([&] {
+        require(out2 && (bytes || len == 0), ESGPU_ERR_INVALID, "null argument");
+        murmur3_x64_128(bytes, (int)len, (uint64_t)seed, &out2[0], &out2[1]);
+    });
+}
+
+extern "C" int esgpu_precision_from_threshold(int64_t count, int32_t* precision) {
+    return guarded([&] { *precision = hll_precision_from_threshold(count); });
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// plans
+// ------------------------------------------------------------------------------------------------------------
+static bool is_bucket(int t) { return t == ESGPU_AGG_TERMS || t == ESGPU_AGG_HISTOGRAM || t == ESGPU_AGG_DATE_HISTOGRAM; }
+static bool is_metric(int t) { return t == ESGPU_AGG_STATS || t == ESGPU_AGG_EXTENDED_STATS || t == ESGPU_AGG_AVG; }
+
+struct SpecNode {
+    esgpu_agg_spec s;
+    std::string name, field;
+    std::vector<int> children;
+    int precision = 14;
+};
+
+// One top-level aggregation subtree compiled to one kernel pipeline.
+struct Pipeline {
+    int root = -1;             // spec index of the top-level aggregation
+    int kind = 0;              // 0 = cell grid (bucket / metric), 1 = cardinality
+    // cell grid shape
+    int outer = -1, inner = -1;      // bucket spec indices (inner may be -1)
+    int term_spec = -1, hist_spec = -1;
+    std::vector<int> metrics;        // metric specs at the deepest level
+    std::string ord_field, hist_field, metric_field;
+    int met = 0;                     // 0 none, 1 avg, 2 stats, 3 extended
+    int64_t interval = 1, offset = 0;
+    // device state
+    bool allocated = false;
+    uint32_t T = 1, H = 1;
+    uint64_t value_count = 1;        // terms: the global ordinal count (T is max(value_count, 1))
+    int64_t key0 = 0;
+    int vcnt_mode = 0, ocnt_mode = OCNT_NONE;
+    DevBuf g_cnt, g_ocnt, g_vcnt, g_sum, g_min, g_max, g_sq;
+    // cardinality state
+    int p = 14;
+    DevBuf regs, lc_set, lc_count;
+    uint32_t lc_mask = 0, lc_threshold = 0;
+    // post_collection products
+    std::vector<uint8_t> h_regs;
+    std::vector<uint32_t> h_lc;
+    int hll_mode = 0;
+    bool any_value = false;
+    // the segment the dictionary comes from (terms keys)
+    const DevColumn* ord_col = nullptr;
+};
+
+struct esgpu_plan {
+    esgpu_ctx* ctx = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::vector<SpecNode> specs;
+    std::vector<esgpu_filter> filters;
+    std::vector<std::string> filter_fields;
+    std::vector<Pipeline> pipes;
+    bool collected = false, posted = false;
+    double last_ms = 0;
+    uint64_t last_bytes = 0;
+    int32_t last_path = 0;
+    std::vector<const DevColumn*> dict_cols;  // keep dictionaries addressable after segment destroy: copy terms at build
+    std::map<std::string, std::vector<std::string>> term_cache;
+};
+
+static int metric_level(int t) { return t == ESGPU_AGG_AVG ? 1 : t == ESGPU_AGG_STATS ? 2 : 3; }
+
+static void affine_rounding(const esgpu_agg_spec& s, int64_t* interval, int64_t* offset) {
+    // HistogramAggregator keys as an affine map: key = floor((v - offset) / interval) * interval + offset
+    if (s.type == ESGPU_AGG_HISTOGRAM || s.date_unit == ESGPU_UNIT_NONE) {
+        require(s.interval >= 1, ESGPU_ERR_INVALID, "[interval] must be 1 or greater for histogram aggregation");
+        *interval = s.interval;
+        *offset = s.offset;
+        return;
+    }
+    switch (s.date_unit) {
+        case ESGPU_UNIT_SECOND: *interval = 1000; break;
+        case ESGPU_UNIT_MINUTE: *interval = 60000; break;
+        case ESGPU_UNIT_HOUR: *interval = 3600000; break;
+        case ESGPU_UNIT_DAY: *interval = 86400000; break;
+        case ESGPU_UNIT_WEEK: *interval = 7 * 86400000LL; *offset = s.offset - 3 * 86400000LL; return;  // Monday 00:00
+        default: throw EsError(ESGPU_ERR_UNSUPPORTED, "calendar date_histogram units (month/quarter/year) run on the CPU path");
+    }
+    *offset = s.offset;
+}
+
+extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int32_t nspecs, const esgpu_filter* filters,
+                                 int32_t nfilters, esgpu_plan** out) {
+    return guarded([&] {
+        require(c && out && (nspecs == 0 || specs), ESGPU_ERR_INVALID, "null argument");
+        require(nfilters >= 0 && nfilters <= 4, ESGPU_ERR_UNSUPPORTED, "at most 4 filter clauses run on the GPU path");
+        std::unique_ptr<esgpu_plan> p(new esgpu_plan());
+        p->ctx = c;
+        p->specs.resize(nspecs);
+        std::vector<int> tops;
+        for (int i = 0; i < nspecs; ++i) {
+            SpecNode& n = p->specs[i];
+            n.s = specs[i];
+            n.name = specs[i].name ? specs[i].name : "";
+            n.field = specs[i].field ? specs[i].field : "";
+            n.s.name = nullptr;
+            n.s.field = nullptr;
+            require(n.s.type >= ESGPU_AGG_TERMS && n.s.type <= ESGPU_AGG_VALUE_COUNT, ESGPU_ERR_INVALID, "unknown aggregation type");
+            if (n.s.parent < 0) tops.push_back(i);
+            else {
+                require(n.s.parent < i, ESGPU_ERR_INVALID, "parent must precede child");
+                require(is_bucket(p->specs[n.s.parent].s.type), ESGPU_ERR_INVALID, "metrics aggregations cannot have sub-aggregations");
+                p->specs[n.s.parent].children.push_back(i);
+            }
+            if (n.s.type >= ESGPU_AGG_SUM) throw EsError(ESGPU_ERR_UNSUPPORTED, "sum/min/max/value_count run on the CPU path");
+            if (n.s.type == ESGPU_AGG_TERMS) {
+                require(n.s.size >= 0 && n.s.min_doc_count >= 0, ESGPU_ERR_INVALID,
+                        "parameters [requiredSize] and [minDocCount] must be >=0 in terms aggregation.");
+                require(n.s.order >= ESGPU_ORDER_COUNT_DESC && n.s.order <= ESGPU_ORDER_TERM_DESC, ESGPU_ERR_UNSUPPORTED,
+                        "terms order by sub-aggregation runs on the CPU path");
+            }
+            if (n.s.type == ESGPU_AGG_CARDINALITY) {
+                if (n.s.precision_threshold >= 0) n.precision = hll_precision_from_threshold(n.s.precision_threshold);
+                else {
+                    int pr = 14;  // CardinalityAggregatorFactory.defaultPrecision
+                    for (int q = n.s.parent; q >= 0; q = p->specs[q].s.parent) if (is_bucket(p->specs[q].s.type)) pr -= 5;
+                    n.precision = std::max(pr, 4);
+                }
+            }
+        }
+        for (int k = 0; k < nfilters; ++k) {
+            require(filters[k].field != nullptr, ESGPU_ERR_INVALID, "filter without field");
+            p->filters.push_back(filters[k]);
+            p->filter_fields.push_back(filters[k].field);
+        }
+        // compile each top-level subtree into a pipeline
+        for (int r : tops) {
+            Pipeline pl;
+            pl.root = r;
+            const SpecNode& root = p->specs[r];
+            if (root.s.type == ESGPU_AGG_CARDINALITY) {
+                pl.kind = 1;
+                pl.p = root.precision;
+                pl.metric_field = root.field;
+                p->pipes.push_back(std::move(pl));
+                continue;
+            }
+            if (is_metric(root.s.type)) {
+                pl.metrics.push_back(r);
+            } else {
+                pl.outer = r;
+                std::vector<int> mets, buckets;
+                for (int ch : root.children) {
+                    const int t = p->specs[ch].s.type;
+                    if (is_metric(t)) mets.push_back(ch);
+                    else if (is_bucket(t)) buckets.push_back(ch);
+                    else throw EsError(ESGPU_ERR_UNSUPPORTED, "cardinality under a bucket aggregation runs on the CPU path");
+                }
+                require(buckets.size() <= 1, ESGPU_ERR_UNSUPPORTED, "more than one bucket sub-aggregation");
+                if (!buckets.empty()) {
+                    require(mets.empty(), ESGPU_ERR_UNSUPPORTED, "metrics beside a bucket sub-aggregation");
+                    pl.inner = buckets[0];
+                    for (int ch : p->specs[pl.inner].children) {
+                        const int t = p->specs[ch].s.type;
+                        require(is_metric(t), ESGPU_ERR_UNSUPPORTED, "bucket aggregations nested three levels deep");
+                        mets.push_back(ch);
+                    }
+                    const bool ot = p->specs[pl.outer].s.type == ESGPU_AGG_TERMS;
+                    const bool it = p->specs[pl.inner].s.type == ESGPU_AGG_TERMS;
+                    require(ot != it, ESGPU_ERR_UNSUPPORTED, "terms-under-terms and histogram-under-histogram");
+                }
+                pl.metrics = mets;
+            }
+            for (int b : {pl.outer, pl.inner}) {
+                if (b < 0) continue;
+                const SpecNode& n = p->specs[b];
+                if (n.s.type == ESGPU_AGG_TERMS) { pl.term_spec = b; pl.ord_field = n.field; }
+                else { pl.hist_spec = b; pl.hist_field = n.field; affine_rounding(n.s, &pl.interval, &pl.offset); }
+            }
+            for (int m : pl.metrics) {
+                const SpecNode& n = p->specs[m];
+                if (pl.metric_field.empty()) pl.metric_field = n.field;
+                require(pl.metric_field == n.field, ESGPU_ERR_UNSUPPORTED, "metrics on different fields at one level");
+                pl.met = std::max(pl.met, metric_level(n.s.type));
+            }
+            p->pipes.push_back(std::move(pl));
+        }
+        HIPX(hipSetDevice(c->device));
+        HIPX(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+        HIPX(hipEventCreate(&p->ev0));
+        HIPX(hipEventCreate(&p->ev1));
+        *out = p.release();
+    });
+}
+
+static void alloc_grid(esgpu_plan* p, Pipeline& pl) {
+    esgpu_ctx* c = p->ctx;
+    const size_t cells = (size_t)pl.T * pl.H;
+    pl.g_cnt.alloc(c, cells * 8);
+    HIPX(hipMemsetAsync(pl.g_cnt.p, 0, cells * 8, p->stream));
+    if (pl.ocnt_mode != OCNT_NONE) {
+        const size_t n = pl.ocnt_mode == OCNT_TERMS ? pl.T : pl.H;
+        pl.g_ocnt.alloc(c, n * 8);
+        HIPX(hipMemsetAsync(pl.g_ocnt.p, 0, n * 8, p->stream));
+    }
+    if (pl.met > 0) {
+        if (pl.vcnt_mode) { pl.g_vcnt.alloc(c, cells * 8); HIPX(hipMemsetAsync(pl.g_vcnt.p, 0, cells * 8, p->stream)); }
+        pl.g_sum.alloc(c, cells * 8);
+        HIPX(hipMemsetAsync(pl.g_sum.p, 0, cells * 8, p->stream));
+    }
+    if (pl.met >= 2) {
+        pl.g_min.alloc(c, cells * 8);
+        pl.g_max.alloc(c, cells * 8);
+        launch_fill_u64(pl.g_min.as<unsigned long long>(), cells, kMinInit, p->stream);
+        launch_fill_u64(pl.g_max.as<unsigned long long>(), cells, kMaxInit, p->stream);
+    }
+    if (pl.met >= 3) { pl.g_sq.alloc(c, cells * 8); HIPX(hipMemsetAsync(pl.g_sq.p, 0, cells * 8, p->stream)); }
+    pl.allocated = true;
+}
+
+// grow the key range of an allocated grid ([H][T] rows are contiguous, so a range extension is one copy)
+static void grow_keys(esgpu_plan* p, Pipeline& pl, int64_t kmin, int64_t kmax) {
+    const int64_t nk0 = std::min(pl.key0, kmin);
+    const int64_t nk1 = std::max(pl.key0 + (int64_t)pl.H - 1, kmax);
+    if (nk0 == pl.key0 && nk1 == pl.key0 + (int64_t)pl.H - 1) return;
+    require(nk1 - nk0 + 1 <= 64 * 1024 * 1024, ESGPU_ERR_UNSUPPORTED, "histogram key range too large for a dense grid");
+    const uint32_t oldH = pl.H;
+    const int64_t shift = pl.key0 - nk0;
+    struct { DevBuf g_cnt, g_ocnt, g_vcnt, g_sum, g_min, g_max, g_sq; } old;
+    old.g_cnt = std::move(pl.g_cnt);
+    old.g_ocnt = std::move(pl.g_ocnt);
+    old.g_vcnt = std::move(pl.g_vcnt);
+    old.g_sum = std::move(pl.g_sum);
+    old.g_min = std::move(pl.g_min);
+    old.g_max = std::move(pl.g_max);
+    old.g_sq = std::move(pl.g_sq);
+    pl.H = (uint32_t)(nk1 - nk0 + 1);
+    pl.key0 = nk0;
+    alloc_grid(p, pl);
+    const size_t row = (size_t)pl.T * 8;
+    auto cp = [&](DevBuf& dst, DevBuf& src, size_t rowb) {
+        if (src.p) HIPX(hipMemcpyAsync(dst.as<uint8_t>() + shift * rowb, src.p, (size_t)oldH * rowb, hipMemcpyDeviceToDevice, p->stream));
+    };
+    cp(pl.g_cnt, old.g_cnt, row);
+    cp(pl.g_vcnt, old.g_vcnt, row);
+    cp(pl.g_sum, old.g_sum, row);
+    cp(pl.g_min, old.g_min, row);
+    cp(pl.g_max, old.g_max, row);
+    cp(pl.g_sq, old.g_sq, row);
+    if (pl.ocnt_mode == OCNT_HIST) cp(pl.g_ocnt, old.g_ocnt, 8);
+    if (pl.ocnt_mode == OCNT_TERMS && old.g_ocnt.p)
+        HIPX(hipMemcpyAsync(pl.g_ocnt.p, old.g_ocnt.p, (size_t)pl.T * 8, hipMemcpyDeviceToDevice, p->stream));
+    HIPX(hipStreamSynchronize(p->stream));
+}
+
+static void set_preds(esgpu_plan* p, const esgpu_segment* s, PredDev* out, int32_t* npred, uint64_t* bytes_per_doc) {
+    *npred = 0;
+    for (size_t k = 0; k < p->filters.size(); ++k) {
+        const esgpu_filter& f = p->filters[k];
+        const DevColumn* col = s->col(p->filter_fields[k].c_str());
+        PredDev q{};
+        require(col != nullptr, ESGPU_ERR_UNSUPPORTED, "filter on a field missing from the segment");
+        require(!col->multi, ESGPU_ERR_UNSUPPORTED, "filters on multi-valued fields run on the CPU path");
+        q.col = col->values.p;
+        q.present = col->present.as<uint64_t>();
+        if (col->type == ESGPU_COL_ORD_U32) {
+            require(f.type == ESGPU_FILTER_TERM, ESGPU_ERR_UNSUPPORTED, "range filters on keyword fields run on the CPU path");
+            q.kind = PRED_ORD_EQ;
+            q.lo = f.term;
+            *bytes_per_doc += 4;
+        } else if (col->type == ESGPU_COL_F64) {
+            q.kind = PRED_F64_RANGE;
+            if (f.type == ESGPU_FILTER_TERM) { q.dlo = q.dhi = (double)f.term; q.lo_incl = q.hi_incl = 1; }
+            else {
+                q.dlo = f.has_lower ? f.lo_d : -INFINITY;
+                q.dhi = f.has_upper ? f.hi_d : INFINITY;
+                q.lo_incl = f.has_lower ? f.include_lower : 1;
+                q.hi_incl = f.has_upper ? f.include_upper : 1;
+            }
+            *bytes_per_doc += 8;
+        } else {
+            q.kind = PRED_I64_RANGE;
+            if (f.type == ESGPU_FILTER_TERM) { q.lo = q.hi = f.term; }
+            else {
+                int64_t lo = INT64_MIN, hi = INT64_MAX;
+                bool empty = false;
+                if (f.has_lower) {
+                    if (f.include_lower) lo = f.lo_i;
+                    else if (f.lo_i == INT64_MAX) empty = true;
+                    else lo = f.lo_i + 1;
+                }
+                if (f.has_upper) {
+                    if (f.include_upper) hi = f.hi_i;
+                    else if (f.hi_i == INT64_MIN) empty = true;
+                    else hi = f.hi_i - 1;
+                }
+                if (empty) { lo = 1; hi = 0; }
+                q.lo = lo;
+                q.hi = hi;
+            }
+            *bytes_per_doc += 8;
+        }
+        out[(*npred)++] = q;
+    }
+}
+
+static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
+    const bool ORD = pl.term_spec >= 0, HIST = pl.hist_spec >= 0;
+    const DevColumn* oc = ORD ? s->col(pl.ord_field.c_str()) : nullptr;
+    const DevColumn* hc = HIST ? s->col(pl.hist_field.c_str()) : nullptr;
+    const DevColumn* mc = pl.met > 0 ? s->col(pl.metric_field.c_str()) : nullptr;
+    // unmapped fields: a bucket aggregation over a missing field collects nothing (ValuesSource null)
+    if ((ORD && !oc) || (HIST && !hc)) return false;
+    if (oc) {
+        require(oc->type == ESGPU_COL_ORD_U32, ESGPU_ERR_UNSUPPORTED, "terms on numeric fields run on the CPU path");
+        require(!oc->multi, ESGPU_ERR_UNSUPPORTED, "multi-valued keyword fields run on the CPU path");
+    }
+    if (hc) {
+        require(hc->type == ESGPU_COL_I64, ESGPU_ERR_UNSUPPORTED, "histogram over non-long fields runs on the CPU path");
+        require(!hc->multi, ESGPU_ERR_UNSUPPORTED, "multi-valued numeric fields run on the CPU path");
+    }
+    if (mc) {
+        require(mc->type == ESGPU_COL_I64 || mc->type == ESGPU_COL_F64, ESGPU_ERR_UNSUPPORTED, "metric over non-numeric field");
+        require(!mc->multi, ESGPU_ERR_UNSUPPORTED, "multi-valued numeric fields run on the CPU path");
+    }
+    // an unmapped metric field collects nothing (ValuesSource null => NO_OP collector); counts stay separate
+    const int met_launch = mc ? pl.met : 0;
+    // ---- shape the grid ----
+    int64_t kmin = 0, kmax = 0;
+    bool has_keys = false;
+    if (HIST && hc->vmin <= hc->vmax) {
+        kmin = floor_div64(hc->vmin - pl.offset, pl.interval);
+        kmax = floor_div64(hc->vmax - pl.offset, pl.interval);
+        has_keys = true;
+    }
+    if (!pl.allocated) {
+        pl.T = ORD ? (uint32_t)std::max<uint64_t>(oc->value_count, 1) : 1;
+        pl.key0 = has_keys ? kmin : 0;
+        pl.H = HIST ? (uint32_t)(has_keys ? kmax - kmin + 1 : 1) : 1;
+        require(!HIST || !has_keys || kmax - kmin + 1 <= 64 * 1024 * 1024, ESGPU_ERR_UNSUPPORTED,
+                "histogram key range too large for a dense grid");
+        require((uint64_t)pl.T * pl.H <= (1ull << 31), ESGPU_ERR_UNSUPPORTED, "bucket grid too large");
+        pl.vcnt_mode = (pl.met > 0 && (!mc || mc->present.p)) ? 1 : 0;
+        pl.value_count = ORD ? oc->value_count : 1;
+        if (ORD && HIST) {
+            const bool terms_outer = pl.outer == pl.term_spec;
+            const bool inner_sparse = terms_outer ? (hc->present.p != nullptr) : true;  // ords may be missing
+            if (inner_sparse) pl.ocnt_mode = terms_outer ? OCNT_TERMS : OCNT_HIST;
+        }
+        pl.ord_col = oc;
+        alloc_grid(p, pl);
+    } else {
+        if (ORD) require(oc->value_count == pl.T || (oc->value_count == 0 && pl.T == 1), ESGPU_ERR_UNSUPPORTED,
+                         "segments with different global ordinal counts");
+        if (HIST && has_keys) grow_keys(p, pl, kmin, kmax);
+        if (pl.met > 0 && (!mc || mc->present.p) && !pl.vcnt_mode)
+            throw EsError(ESGPU_ERR_UNSUPPORTED, "metric field sparsity changed across segments");
+    }
+    // ---- launch configuration ----
+    CollectParams P{};
+    P.n_docs = s->max_doc;
+    P.n_blocks = s->n_pad / kBlockDocs;
+    if (P.n_blocks == 0) return false;
+    P.ord = oc ? oc->values.as<uint32_t>() : nullptr;
+    P.T = pl.T;
+    P.H = pl.H;
+    P.hv = hc ? hc->values.as<int64_t>() : nullptr;
+    P.hv_present = hc ? hc->present.as<uint64_t>() : nullptr;
+    P.interval = pl.interval;
+    P.offset = pl.offset;
+    P.key0 = pl.key0;
+    P.zmin = hc ? hc->zmin.as<int64_t>() : nullptr;
+    P.zmax = hc ? hc->zmax.as<int64_t>() : nullptr;
+    P.mv = mc ? mc->values.p : nullptr;
+    P.mv_present = mc ? mc->present.as<uint64_t>() : nullptr;
+    P.mv_f64 = mc && mc->type == ESGPU_COL_F64;
+    P.vcnt_mode = pl.vcnt_mode;
+    P.ocnt_mode = pl.ocnt_mode;
+    P.accept = d_accept;
+    uint64_t bytes_per_doc = (oc ? 4 : 0) + (hc ? 8 : 0) + (mc ? 8 : 0);
+    set_preds(p, s, P.pred, &P.npred, &bytes_per_doc);
+    P.g_cnt = pl.g_cnt.as<unsigned long long>();
+    P.g_ocnt = pl.g_ocnt.as<unsigned long long>();
+    P.g_vcnt = pl.g_vcnt.as<unsigned long long>();
+    P.g_sum = pl.g_sum.as<double>();
+    P.g_min = pl.g_min.as<unsigned long long>();
+    P.g_max = pl.g_max.as<unsigned long long>();
+    P.g_sq = pl.g_sq.as<double>();
+
+    // LDS sizing: the whole grid if it fits, else a sliding window over the key dimension (time-sorted data)
+    const size_t kLdsPair = 64 * 1024, kLdsMax = 150 * 1024;
+    uint32_t W = pl.H;
+    size_t lds = collect_lds_bytes(pl.T, W, met_launch, pl.vcnt_mode, pl.ocnt_mode);
+    P.lds_mode = 1;
+    P.windowed = 0;
+    if (lds > kLdsPair) {
+        if (HIST) {
+            uint32_t w = pl.H;
+            while (w > 1 && collect_lds_bytes(pl.T, w, met_launch, pl.vcnt_mode, pl.ocnt_mode) > kLdsPair) w = (w + 1) / 2;
+            if (collect_lds_bytes(pl.T, w, met_launch, pl.vcnt_mode, pl.ocnt_mode) > kLdsPair) w = 1;
+            W = w;
+            P.windowed = 1;
+            lds = collect_lds_bytes(pl.T, W, met_launch, pl.vcnt_mode, pl.ocnt_mode);
+        }
+        if (lds > kLdsMax) {
+            P.lds_mode = 0;
+            P.windowed = 0;
+            lds = 0;
+            W = pl.H;
+        }
+    }
+    P.W = W;
+    const uint64_t span = (uint64_t)pl.interval * (uint64_t)W;
+    P.fast32 = pl.interval < (1ll << 32) && span < (1ull << 32);
+    if (P.fast32) {
+        const MagicU32 mg = make_magic((uint32_t)pl.interval);
+        P.mg_m = mg.m; P.mg_s1 = mg.s1; P.mg_s2 = mg.s2;
+    }
+    const uint32_t wg_per_cu = (uint32_t)std::max(1, collect_occupancy(ORD, HIST, met_launch, lds));
+    const uint32_t target = (uint32_t)p->ctx->cus * wg_per_cu;
+    const uint32_t bpw = (P.n_blocks + target - 1) / target;
+    P.blocks_per_wg = std::max(1u, bpw);
+    const uint32_t grid = (P.n_blocks + P.blocks_per_wg - 1) / P.blocks_per_wg;
+    HIPX(hipEventRecord(p->ev0, p->stream));
+    launch_collect(P, ORD, HIST, met_launch, grid, lds, p->stream);
+    HIPX(hipGetLastError());
+    HIPX(hipEventRecord(p->ev1, p->stream));
+    p->last_bytes += bytes_per_doc * (uint64_t)s->max_doc + (d_accept ? ((uint64_t)s->max_doc + 7) / 8 : 0);
+    p->last_path = P.lds_mode ? (P.windowed ? 2 : 1) : 0;
+    return true;
+}
+
+static void ensure_ord_hash(esgpu_ctx* c, const DevColumn* col, hipStream_t st) {
+    DevColumn* mcol = const_cast<DevColumn*>(col);
+    if (mcol->ord_hash.p) return;
+    std::vector<uint64_t> h(std::max<uint64_t>(col->value_count, 1));
+    for (uint64_t o = 0; o < col->value_count; ++o) {
+        const std::string t = col->term(o);
+        uint64_t h1, h2;
+        murmur3_x64_128((const uint8_t*)t.data(), (int)t.size(), 0, &h1, &h2);
+        h[o] = h1;
+    }
+    mcol->ord_hash.alloc(c, h.size() * 8);
+    HIPX(hipMemcpyAsync(mcol->ord_hash.p, h.data(), h.size() * 8, hipMemcpyHostToDevice, st));
+    HIPX(hipStreamSynchronize(st));
+}
+
+static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
+    const DevColumn* col = s->col(pl.metric_field.c_str());
+    if (!col) return false;
+    require(!col->multi, ESGPU_ERR_UNSUPPORTED, "multi-valued fields run on the CPU path");
+    if (!pl.allocated) {
+        const uint32_t m = 1u << pl.p;
+        pl.regs.alloc(p->ctx, (size_t)m * 4);
+        HIPX(hipMemsetAsync(pl.regs.p, 0, (size_t)m * 4, p->stream));
+        pl.lc_threshold = (uint32_t)((float)(m / 4) * 0.75f);  // Hashset threshold (HyperLogLogPlusPlus.java:437-440)
+        uint32_t cap = 1024;
+        while (cap < 2 * (pl.lc_threshold + 1)) cap <<= 1;
+        pl.lc_mask = cap - 1;
+        pl.lc_set.alloc(p->ctx, (size_t)cap * 4);
+        HIPX(hipMemsetAsync(pl.lc_set.p, 0, (size_t)cap * 4, p->stream));
+        pl.lc_count.alloc(p->ctx, 16);
+        HIPX(hipMemsetAsync(pl.lc_count.p, 0, 16, p->stream));
+        pl.allocated = true;
+    }
+    HllParams H{};
+    H.n_docs = s->max_doc;
+    H.p = pl.p;
+    H.col = col->values.p;
+    H.present = col->present.as<uint64_t>();
+    H.accept = d_accept;
+    uint64_t bytes_per_doc = col->type == ESGPU_COL_ORD_U32 ? 4 : 8;
+    if (col->type == ESGPU_COL_ORD_U32) {
+        H.kind = HLL_ORD;
+        ensure_ord_hash(p->ctx, col, p->stream);
+        H.ord_hash = col->ord_hash.as<uint64_t>();
+        H.n_ords = col->value_count;
+    } else {
+        H.kind = col->type == ESGPU_COL_F64 ? HLL_F64 : HLL_I64;
+    }
+    set_preds(p, s, H.pred, &H.npred, &bytes_per_doc);
+    H.regs = pl.regs.as<unsigned int>();
+    H.lc_set = pl.lc_set.as<unsigned int>();
+    H.lc_count = pl.lc_count.as<unsigned int>();
+    H.lc_mask = pl.lc_mask;
+    H.lc_threshold = pl.lc_threshold;
+    if (H.n_docs == 0) return false;
+    HIPX(hipEventRecord(p->ev0, p->stream));
+    launch_hll(H, p->stream);
+    HIPX(hipGetLastError());
+    HIPX(hipEventRecord(p->ev1, p->stream));
+    p->last_bytes += bytes_per_doc * (uint64_t)s->max_doc;
+    p->last_path = 3;
+    return true;
+}
+
+extern "C" int esgpu_plan_collect_segment(esgpu_plan* p, const esgpu_segment* s, const uint64_t* accept_bits) {
+    return guarded([&] {
+        require(p && s, ESGPU_ERR_INVALID, "null argument");
+        require(!p->posted, ESGPU_ERR_STATE, "collect after postCollection");
+        require(s->ctx == p->ctx, ESGPU_ERR_INVALID, "segment belongs to another device context");
+        HIPX(hipSetDevice(p->ctx->device));
+        DevBuf accept;
+        if (accept_bits) {
+            const size_t words = s->n_pad / 64;
+            accept.alloc(p->ctx, std::max<size_t>(words, 1) * 8);
+            HIPX(hipMemsetAsync(accept.p, 0, std::max<size_t>(words, 1) * 8, p->stream));
+            HIPX(hipMemcpyAsync(accept.p, accept_bits, ((size_t)s->max_doc + 63) / 64 * 8, hipMemcpyHostToDevice, p->stream));
+        }
+        p->last_bytes = 0;
+        float total = 0;
+        for (Pipeline& pl : p->pipes) {
+            const bool launched = pl.kind == 1 ? collect_hll(p, pl, s, accept.as<uint64_t>())
+                                               : collect_grid(p, pl, s, accept.as<uint64_t>());
+            if (!launched) continue;
+            HIPX(hipEventSynchronize(p->ev1));
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, p->ev0, p->ev1) == hipSuccess) total += ms;
+        }
+        HIPX(hipStreamSynchronize(p->stream));
+        p->last_ms = total;
+        // keep dictionary terms reachable at build time even if the segment is destroyed first
+        for (Pipeline& pl : p->pipes) {
+            if (pl.term_spec < 0) continue;
+            const DevColumn* oc = s->col(pl.ord_field.c_str());
+            if (oc && p->term_cache.find(pl.ord_field) == p->term_cache.end() && !oc->synth_bit) {
+                auto& v = p->term_cache[pl.ord_field];
+                v.reserve(oc->value_count);
+                for (uint64_t o = 0; o < oc->value_count; ++o) v.push_back(oc->term(o));
+            }
+            if (oc && oc->synth_bit) p->term_cache[pl.ord_field + "#synth"] = {std::to_string(oc->synth_bit)};
+        }
+        p->collected = true;
+    });
+}
+
+extern "C" int esgpu_plan_last_collect_stats(const esgpu_plan* p, double* kernel_ms, uint64_t* bytes, int32_t* path) {
+    return guarded([&] {
+        if (kernel_ms) *kernel_ms = p->last_ms;
+        if (bytes) *bytes = p->last_bytes;
+        if (path) *path = p->last_path;
+    });
+}
+
+extern "C" int esgpu_plan_post_collection(esgpu_plan* p) {
+    return guarded([&] {
+        require(p != nullptr, ESGPU_ERR_INVALID, "null plan");
+        HIPX(hipSetDevice(p->ctx->device));
+        HIPX(hipStreamSynchronize(p->stream));
+        for (Pipeline& pl : p->pipes) {
+            if (pl.kind != 1 || !pl.allocated) continue;
+            uint32_t cnt = 0;
+            HIPX(hipMemcpy(&cnt, pl.lc_count.p, 4, hipMemcpyDeviceToHost));
+            const uint32_t m = 1u << pl.p;
+            pl.any_value = cnt > 0;
+            if (cnt <= pl.lc_threshold) {  // LINEAR_COUNTING: the distinct encoded hashes
+                pl.hll_mode = 0;
+                std::vector<uint32_t> set((size_t)pl.lc_mask + 1);
+                HIPX(hipMemcpy(set.data(), pl.lc_set.p, set.size() * 4, hipMemcpyDeviceToHost));
+                pl.h_lc.clear();
+                for (uint32_t v : set) if (v) pl.h_lc.push_back(v);
+                std::sort(pl.h_lc.begin(), pl.h_lc.end());
+            } else {  // HYPERLOGLOG
+                pl.hll_mode = 1;
+                std::vector<uint32_t> r(m);
+                HIPX(hipMemcpy(r.data(), pl.regs.p, (size_t)m * 4, hipMemcpyDeviceToHost));
+                pl.h_regs.resize(m);
+                for (uint32_t i = 0; i < m; ++i) pl.h_regs[i] = (uint8_t)r[i];
+            }
+        }
+        p->posted = true;
+    });
+}
+
+// ---- build ----------------------------------------------------------------------------------------------------
+static std::string plan_term(const esgpu_plan* p, const Pipeline& pl, uint64_t ord) {
+    auto syn = p->term_cache.find(pl.ord_field + "#synth");
+    if (syn != p->term_cache.end()) {
+        char b[32];
+        esgpu_synthetic_term((uint32_t)std::stoul(syn->second[0]), ord, b, sizeof b);
+        return b;
+    }
+    auto it = p->term_cache.find(pl.ord_field);
+    if (it != p->term_cache.end() && ord < it->second.size()) return it->second[ord];
+    return std::to_string(ord);
+}
+
+static RAgg empty_metric(const SpecNode& n) {
+    RAgg r;
+    r.type = n.s.type;
+    r.name = n.name;
+    r.count = 0; r.sum = 0.0; r.min = INFINITY; r.max = -INFINITY; r.sumsq = 0.0;
+    r.sigma = n.s.sigma;
+    return r;
+}
+
+static RAgg hist_base(const esgpu_plan* p, int spec, const std::vector<RAgg>& empty_subs) {
+    const SpecNode& n = p->specs[spec];
+    RAgg r;
+    r.type = n.s.type;
+    r.name = n.name;
+    r.order = n.s.order;
+    r.keyed = n.s.keyed;
+    r.min_doc_count = n.s.min_doc_count;
+    r.date_unit = n.s.type == ESGPU_AGG_DATE_HISTOGRAM ? n.s.date_unit : 0;
+    r.interval = n.s.interval;
+    r.offset = n.s.offset;
+    if (n.s.min_doc_count == 0) {  // EmptyBucketInfo
+        r.has_empty_info = true;
+        r.has_bmin = n.s.has_extended_bounds_min;
+        r.has_bmax = n.s.has_extended_bounds_max;
+        r.bmin = n.s.extended_bounds_min;
+        r.bmax = n.s.extended_bounds_max;
+        r.empty_subs = empty_subs;
+    }
+    return r;
+}
+
+static RAgg terms_base(const esgpu_plan* p, int spec) {
+    const SpecNode& n = p->specs[spec];
+    RAgg r;
+    r.type = ESGPU_AGG_TERMS;
+    r.name = n.name;
+    r.order = n.s.order;
+    r.required_size = n.s.size;
+    r.shard_size = n.s.shard_size;
+    r.min_doc_count = n.s.min_doc_count;
+    r.show_err = n.s.show_term_doc_count_error;
+    return r;
+}
+
+// host copies of one grid row set
+struct HostCells {
+    std::vector<unsigned long long> cnt, vcnt, mn, mx;
+    std::vector<double> sum, sq;
+};
+
+static std::vector<RAgg> metric_results(const esgpu_plan* p, const Pipeline& pl, const HostCells& h, size_t c) {
+    std::vector<RAgg> out;
+    for (int m : pl.metrics) {
+        const SpecNode& n = p->specs[m];
+        RAgg r = empty_metric(n);
+        const uint64_t vc = pl.vcnt_mode ? h.vcnt[c] : h.cnt[c];
+        r.count = (int64_t)vc;
+        if (vc > 0) {
+            r.sum = h.sum[c];
+            if (pl.met >= 2) {
+                const uint64_t emn = h.mn[c], emx = h.mx[c];
+                if (emn < kEncNegInf || emx > kEncPosInf) { r.min = NAN; r.max = NAN; }  // a NaN value was collected
+                else { r.min = unsortable(emn); r.max = unsortable(emx); }
+            }
+            if (pl.met >= 3) r.sumsq = h.sq[c];
+        }
+        if (n.s.type == ESGPU_AGG_AVG) { r.min = INFINITY; r.max = -INFINITY; r.sumsq = 0.0; }
+        if (n.s.type == ESGPU_AGG_STATS) r.sumsq = 0.0;
+        out.push_back(std::move(r));
+    }
+    return out;
+}
+
+static std::vector<RAgg> empty_metrics(const esgpu_plan* p, const Pipeline& pl) {
+    std::vector<RAgg> out;
+    for (int m : pl.metrics) out.push_back(empty_metric(p->specs[m]));
+    return out;
+}
+
+static void d2h(HostCells& h, const Pipeline& pl, size_t n, const unsigned long long* cnt, const unsigned long long* vcnt,
+                const double* sum, const unsigned long long* mn, const unsigned long long* mx, const double* sq, hipStream_t st) {
+    h.cnt.resize(n);
+    HIPX(hipMemcpyAsync(h.cnt.data(), cnt, n * 8, hipMemcpyDeviceToHost, st));
+    if (pl.vcnt_mode) { h.vcnt.resize(n); HIPX(hipMemcpyAsync(h.vcnt.data(), vcnt, n * 8, hipMemcpyDeviceToHost, st)); }
+    if (pl.met > 0) { h.sum.resize(n); HIPX(hipMemcpyAsync(h.sum.data(), sum, n * 8, hipMemcpyDeviceToHost, st)); }
+    if (pl.met >= 2) {
+        h.mn.resize(n); h.mx.resize(n);
+        HIPX(hipMemcpyAsync(h.mn.data(), mn, n * 8, hipMemcpyDeviceToHost, st));
+        HIPX(hipMemcpyAsync(h.mx.data(), mx, n * 8, hipMemcpyDeviceToHost, st));
+    }
+    if (pl.met >= 3) { h.sq.resize(n); HIPX(hipMemcpyAsync(h.sq.data(), sq, n * 8, hipMemcpyDeviceToHost, st)); }
+    HIPX(hipStreamSynchronize(st));
+}
+
+// GlobalOrdinalsStringTermsAggregator.buildAggregation candidate selection + PQ (:146-208)
+struct TermPick { uint32_t ord; int64_t count; };
+static std::vector<TermPick> select_terms(const esgpu_agg_spec& s, const unsigned long long* counts, uint32_t T, int64_t* other) {
+    std::vector<TermPick> cands;
+    int64_t oth = 0;
+    for (uint32_t g = 0; g < T; ++g) {
+        const int64_t c = (int64_t)counts[g];
+        if (s.min_doc_count > 0 && c == 0) continue;
+        oth += c;
+        if (s.shard_min_doc_count <= c) cands.push_back({g, c});
+    }
+    const size_t size = (size_t)std::min<int64_t>((int64_t)T, (int64_t)s.shard_size);
+    auto cmp = [&](const TermPick& a, const TermPick& b) {
+        switch (s.order) {
+            case ESGPU_ORDER_COUNT_DESC: if (a.count != b.count) return a.count > b.count; return a.ord < b.ord;
+            case ESGPU_ORDER_COUNT_ASC: if (a.count != b.count) return a.count < b.count; return a.ord < b.ord;
+            case ESGPU_ORDER_TERM_DESC: return a.ord > b.ord;
+            default: return a.ord < b.ord;
+        }
+    };
+    if (cands.size() > size) {
+        std::partial_sort(cands.begin(), cands.begin() + size, cands.end(), cmp);
+        cands.resize(size);
+    } else {
+        std::sort(cands.begin(), cands.end(), cmp);
+    }
+    for (auto& t : cands) oth -= t.count;
+    *other = oth;
+    return cands;
+}
+
+static RAgg build_grid(esgpu_plan* p, Pipeline& pl) {
+    hipStream_t st = p->stream;
+    const bool ORD = pl.term_spec >= 0, HIST = pl.hist_spec >= 0;
+    // ---- top-level metric ----
+    if (pl.outer < 0) {
+        const SpecNode& n = p->specs[pl.root];
+        if (!pl.allocated) return empty_metric(n);
+        HostCells h;
+        d2h(h, pl, 1, pl.g_cnt.as<unsigned long long>(), pl.g_vcnt.as<unsigned long long>(), pl.g_sum.as<double>(),
+            pl.g_min.as<unsigned long long>(), pl.g_max.as<unsigned long long>(), pl.g_sq.as<double>(), st);
+        return metric_results(p, pl, h, 0)[0];
+    }
+    const bool terms_outer = pl.outer == pl.term_spec;
+    // prototypes for empty sub-aggregations (bucketEmptyAggregations)
+    std::vector<RAgg> inner_empty;  // what an empty outer bucket carries
+    std::vector<RAgg> leaf_empty = empty_metrics(p, pl);
+    if (pl.inner >= 0) {
+        if (p->specs[pl.inner].s.type == ESGPU_AGG_TERMS) inner_empty.push_back(terms_base(p, pl.inner));
+        else inner_empty.push_back(hist_base(p, pl.inner, leaf_empty));
+    } else {
+        inner_empty = leaf_empty;
+    }
+    if (terms_outer) {
+        const SpecNode& tn = p->specs[pl.outer];
+        RAgg r = terms_base(p, pl.outer);
+        if (!pl.allocated) return r;  // unmapped: buildEmptyAggregation
+        const uint32_t T = pl.T, H = pl.H;
+        // outer doc counts per ordinal
+        std::vector<unsigned long long> tcnt(T);
+        DevBuf tmp;
+        const unsigned long long* dcnt = pl.g_cnt.as<unsigned long long>();
+        if (pl.ocnt_mode == OCNT_TERMS) dcnt = pl.g_ocnt.as<unsigned long long>();
+        else if (H > 1) {
+            tmp.alloc(p->ctx, (size_t)T * 8);
+            launch_term_totals(pl.g_cnt.as<unsigned long long>(), H, T, tmp.as<unsigned long long>(), st);
+            HIPX(hipGetLastError());
+            dcnt = tmp.as<unsigned long long>();
+        }
+        HIPX(hipMemcpyAsync(tcnt.data(), dcnt, (size_t)T * 8, hipMemcpyDeviceToHost, st));
+        HIPX(hipStreamSynchronize(st));
+        int64_t other = 0;
+        std::vector<TermPick> top = select_terms(tn.s, tcnt.data(), (uint32_t)pl.value_count, &other);
+        r.other_doc_count = other;
+        const uint32_t k = (uint32_t)top.size();
+        // gather the winners' rows [k][H] (GatherParams) and bring them back
+        HostCells h;
+        if (k > 0) {
+            std::vector<uint32_t> rows(k);
+            for (uint32_t i = 0; i < k; ++i) rows[i] = top[i].ord;
+            DevBuf drows, dst[6];
+            drows.alloc(p->ctx, (size_t)k * 4);
+            HIPX(hipMemcpyAsync(drows.p, rows.data(), (size_t)k * 4, hipMemcpyHostToDevice, st));
+            GatherParams G{};
+            G.rows = drows.as<uint32_t>();
+            G.k = k; G.H = H; G.T = T;
+            const unsigned long long* srcs[6] = {pl.g_cnt.as<unsigned long long>(), pl.g_vcnt.as<unsigned long long>(),
+                                                 (const unsigned long long*)pl.g_sum.p, pl.g_min.as<unsigned long long>(),
+                                                 pl.g_max.as<unsigned long long>(), (const unsigned long long*)pl.g_sq.p};
+            int slot_of_array[6];
+            for (int a = 0; a < 6; ++a) {
+                slot_of_array[a] = -1;
+                if (!srcs[a]) continue;
+                dst[a].alloc(p->ctx, (size_t)k * H * 8);
+                G.src[G.narrays] = srcs[a];
+                G.dst[G.narrays] = dst[a].as<unsigned long long>();
+                slot_of_array[a] = G.narrays++;
+            }
+            launch_gather_rows(G, st);
+            HIPX(hipGetLastError());
+            d2h(h, pl, (size_t)k * H, dst[0].as<unsigned long long>(), dst[1].as<unsigned long long>(), dst[2].as<double>(),
+                dst[3].as<unsigned long long>(), dst[4].as<unsigned long long>(), dst[5].as<double>(), st);
+            (void)slot_of_array;
+        }
+        for (uint32_t i = 0; i < k; ++i) {
+            RBucket b;
+            b.key = top[i].ord;
+            b.term = plan_term(p, pl, top[i].ord);
+            b.doc_count = top[i].count;
+            if (b.doc_count == 0) b.subs = inner_empty;  // bucketEmptyAggregations
+            else if (pl.inner < 0) b.subs = metric_results(p, pl, h, i);
+            else {
+                RAgg hr = hist_base(p, pl.inner, leaf_empty);
+                for (uint32_t s = 0; s < H; ++s) {
+                    const size_t c = (size_t)i * H + s;
+                    if (h.cnt[c] == 0) continue;
+                    RBucket hb;
+                    hb.key = (pl.key0 + (int64_t)s) * pl.interval + pl.offset;
+                    hb.doc_count = (int64_t)h.cnt[c];
+                    hb.subs = metric_results(p, pl, h, c);
+                    hr.buckets.push_back(std::move(hb));
+                }
+                b.subs.push_back(std::move(hr));
+            }
+            r.buckets.push_back(std::move(b));
+        }
+        return r;
+    }
+    // ---- histogram outer (optionally terms inner) ----
+    RAgg r = hist_base(p, pl.outer, inner_empty);
+    if (!pl.allocated) return r;
+    const uint32_t T = pl.T, H = pl.H;
+    HostCells h;
+    d2h(h, pl, (size_t)T * H, pl.g_cnt.as<unsigned long long>(), pl.g_vcnt.as<unsigned long long>(), pl.g_sum.as<double>(),
+        pl.g_min.as<unsigned long long>(), pl.g_max.as<unsigned long long>(), pl.g_sq.as<double>(), st);
+    std::vector<unsigned long long> ocnt;
+    if (pl.ocnt_mode == OCNT_HIST) {
+        ocnt.resize(H);
+        HIPX(hipMemcpy(ocnt.data(), pl.g_ocnt.p, (size_t)H * 8, hipMemcpyDeviceToHost));
+    }
+    for (uint32_t s = 0; s < H; ++s) {
+        uint64_t dc = 0;
+        if (!ORD) dc = h.cnt[s];
+        else if (pl.ocnt_mode == OCNT_HIST) dc = ocnt[s];
+        else for (uint32_t t = 0; t < T; ++t) dc += h.cnt[(size_t)s * T + t];
+        if (dc == 0) continue;
+        RBucket b;
+        b.key = (pl.key0 + (int64_t)s) * pl.interval + pl.offset;
+        b.doc_count = (int64_t)dc;
+        if (!ORD) b.subs = metric_results(p, pl, h, s);
+        else {
+            const SpecNode& tn = p->specs[pl.inner];
+            RAgg tr = terms_base(p, pl.inner);
+            int64_t other = 0;
+            std::vector<TermPick> top = select_terms(tn.s, h.cnt.data() + (size_t)s * T, (uint32_t)pl.value_count, &other);
+            tr.other_doc_count = other;
+            for (auto& tp : top) {
+                RBucket tb;
+                tb.key = tp.ord;
+                tb.term = plan_term(p, pl, tp.ord);
+                tb.doc_count = tp.count;
+                tb.subs = tp.count == 0 ? leaf_empty : metric_results(p, pl, h, (size_t)s * T + tp.ord);
+                tr.buckets.push_back(std::move(tb));
+            }
+            b.subs.push_back(std::move(tr));
+        }
+        r.buckets.push_back(std::move(b));
+    }
+    return r;
+}
+
+static RAgg build_cardinality(esgpu_plan* p, Pipeline& pl) {
+    const SpecNode& n = p->specs[pl.root];
+    RAgg r;
+    r.type = ESGPU_AGG_CARDINALITY;
+    r.name = n.name;
+    r.precision = pl.p;
+    if (!pl.allocated || !pl.any_value) return r;  // counts == null
+    r.hll_present = true;
+    r.hll_mode = pl.hll_mode;
+    r.lc = pl.h_lc;
+    r.registers = pl.h_regs;
+    if (hll_cardinality(r) == 0) { r.hll_present = false; r.lc.clear(); r.registers.clear(); }  // CardinalityAggregator:141-143
+    return r;
+}
+
+extern "C" int esgpu_plan_build(esgpu_plan* p, esgpu_result** out) {
+    return guarded([&] {
+        require(p && out, ESGPU_ERR_INVALID, "null argument");
+        if (!p->posted) {
+            int rc = esgpu_plan_post_collection(p);
+            if (rc != ESGPU_OK) throw EsError(rc, g_err);
+        }
+        HIPX(hipSetDevice(p->ctx->device));
+        std::unique_ptr<ResultHolder> h(new ResultHolder());
+        for (Pipeline& pl : p->pipes) h->aggs.push_back(pl.kind == 1 ? build_cardinality(p, pl) : build_grid(p, pl));
+        h->export_view();
+        *out = &h.release()->pub;
+    });
+}
+
+extern "C" int esgpu_plan_reset(esgpu_plan* p) {
+    return guarded([&] {
+        require(p != nullptr, ESGPU_ERR_INVALID, "null plan");
+        HIPX(hipSetDevice(p->ctx->device));
+        for (Pipeline& pl : p->pipes) {
+            if (!pl.allocated) continue;
+            if (pl.kind == 1) {
+                HIPX(hipMemsetAsync(pl.regs.p, 0, pl.regs.bytes, p->stream));
+                HIPX(hipMemsetAsync(pl.lc_set.p, 0, pl.lc_set.bytes, p->stream));
+                HIPX(hipMemsetAsync(pl.lc_count.p, 0, pl.lc_count.bytes, p->stream));
+                pl.h_lc.clear();
+                pl.h_regs.clear();
+                pl.any_value = false;
+                continue;
+            }
+            const size_t cells = (size_t)pl.T * pl.H;
+            HIPX(hipMemsetAsync(pl.g_cnt.p, 0, cells * 8, p->stream));
+            if (pl.g_ocnt.p) HIPX(hipMemsetAsync(pl.g_ocnt.p, 0, pl.g_ocnt.bytes, p->stream));
+            if (pl.g_vcnt.p) HIPX(hipMemsetAsync(pl.g_vcnt.p, 0, cells * 8, p->stream));
+            if (pl.g_sum.p) HIPX(hipMemsetAsync(pl.g_sum.p, 0, cells * 8, p->stream));
+            if (pl.g_min.p) launch_fill_u64(pl.g_min.as<unsigned long long>(), cells, kMinInit, p->stream);
+            if (pl.g_max.p) launch_fill_u64(pl.g_max.as<unsigned long long>(), cells, kMaxInit, p->stream);
+            if (pl.g_sq.p) HIPX(hipMemsetAsync(pl.g_sq.p, 0, cells * 8, p->stream));
+        }
+        HIPX(hipStreamSynchronize(p->stream));
+        p->posted = false;
+        p->collected = false;
+    });
+}
+
+extern "C" int esgpu_plan_destroy(esgpu_plan* p) {
+    return guarded([&] {
+        if (!p) return;
+        (void)hipSetDevice(p->ctx->device);
+        (void)hipStreamSynchronize(p->stream);
+        p->pipes.clear();
+        if (p->ev0) (void)hipEventDestroy(p->ev0);
+        if (p->ev1) (void)hipEventDestroy(p->ev1);
+        if (p->stream) (void)hipStreamDestroy(p->stream);
+        delete p;
+    });
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// results
+// ------------------------------------------------------------------------------------------------------------
+extern "C" int esgpu_result_free(esgpu_result* r) {
+    return guarded([&] { delete holder_of(r); });
+}
+
+extern "C" int esgpu_reduce(const esgpu_result* const* shards, int32_t n, esgpu_result** out) {
+    return guarded([&] {
+        require(out && n >= 1 && shards, ESGPU_ERR_INVALID, "reduce needs at least one shard result");
+        std::vector<const std::vector<RAgg>*> lists;
+        for (int i = 0; i < n; ++i) lists.push_back(&holder_of(shards[i])->aggs);
+        std::unique_ptr<ResultHolder> h(new ResultHolder());
+        h->aggs = reduce_lists(lists);
+        h->export_view();
+        *out = &h.release()->pub;
+    });
+}
+
+extern "C" int esgpu_cardinality_value(const esgpu_agg_result* r, int64_t* value) {
+    return guarded([&] {
+        require(r && value && r->type == ESGPU_AGG_CARDINALITY, ESGPU_ERR_INVALID, "not a cardinality result");
+        RAgg a;
+        a.hll_present = r->hll_present;
+        a.precision = r->precision;
+        a.hll_mode = r->hll_mode;
+        if (r->hll_mode && r->registers) a.registers.assign(r->registers, r->registers + ((size_t)1 << r->precision));
+        if (!r->hll_mode && r->lc_hashes) a.lc.assign(r->lc_hashes, r->lc_hashes + r->lc_size);
+        *value = hll_cardinality(a);
+    });
+}
+
+extern "C" int esgpu_result_to_json(const esgpu_result* r, char* buf, size_t cap, size_t* needed) {
+    return guarded([&] {
+        const std::string s = to_json(holder_of(r)->aggs);
+        if (needed) *needed = s.size() + 1;
+        if (buf && cap) {
+            const size_t c = std::min(cap - 1, s.size());
+            std::memcpy(buf, s.data(), c);
+            buf[c] = 0;
+        }
+    });
+}
+
+extern "C" int esgpu_result_serialize(const esgpu_result* r, uint8_t* buf, size_t cap, size_t* needed) {
+    return guarded([&] {
+        std::string s;
+        serialize(holder_of(r)->aggs, s);
+        if (needed) *needed = s.size();
+        if (buf) {
+            require(cap >= s.size(), ESGPU_ERR_INVALID, "buffer too small");
+            std::memcpy(buf, s.data(), s.size());
+        }
+    });
+}
+
+extern "C" int esgpu_result_deserialize(const uint8_t* buf, size_t len, esgpu_result** out) {
+    return guarded([&] {
+        std::unique_ptr<ResultHolder> h(new ResultHolder());
+        require(deserialize(buf, len, h->aggs), ESGPU_ERR_INVALID, "not an esgpu result stream");
+        h->export_view();
+        *out = &h.release()->pub;
+    });
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// RCCL shard reduce (one process per GPU)
+// ------------------------------------------------------------------------------------------------------------
+struct esgpu_comm {
+    esgpu_ctx* ctx = nullptr;
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+    hipStream_t stream = nullptr;
+};
+
+#define NCCLX(expr)                                                                                           \
+    do {                                                                                                      \
+        ncclResult_t r_ = (expr);                                                                             \
+        if (r_ != ncclSuccess) throw EsError(ESGPU_ERR_DEVICE, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+extern "C" int esgpu_comm_unique_id(uint8_t* id_out) {
+    return guarded([&] {
+        static_assert(sizeof(ncclUniqueId) == ESGPU_COMM_ID_BYTES, "ncclUniqueId size");
+        ncclUniqueId id;
+        NCCLX(ncclGetUniqueId(&id));
+        std::memcpy(id_out, &id, sizeof id);
+    });
+}
+
+extern "C" int esgpu_comm_init(esgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t* id, esgpu_comm** out) {
+    return guarded([&] {
+        require(c && id && out && nranks >= 1 && rank >= 0 && rank < nranks, ESGPU_ERR_INVALID, "bad communicator arguments");
+        HIPX(hipSetDevice(c->device));
+        std::unique_ptr<esgpu_comm> cm(new esgpu_comm());
+        cm->ctx = c;
+        cm->nranks = nranks;
+        cm->rank = rank;
+        ncclUniqueId uid;
+        std::memcpy(&uid, id, sizeof uid);
+        NCCLX(ncclCommInitRank(&cm->comm, nranks, uid, rank));
+        HIPX(hipStreamCreateWithFlags(&cm->stream, hipStreamNonBlocking));
+        *out = cm.release();
+    });
+}
+
+extern "C" int esgpu_comm_destroy(esgpu_comm* cm) {
+    return guarded([&] {
+        if (!cm) return;
+        (void)hipSetDevice(cm->ctx->device);
+        if (cm->comm) ncclCommDestroy(cm->comm);
+        if (cm->stream) (void)hipStreamDestroy(cm->stream);
+        delete cm;
+    });
+}
+
+extern "C" int esgpu_comm_gather_reduce(esgpu_comm* cm, const esgpu_result* local, esgpu_result** out) {
+    return guarded([&] {
+        require(cm && local && out, ESGPU_ERR_INVALID, "null argument");
+        HIPX(hipSetDevice(cm->ctx->device));
+        std::string mine;
+        serialize(holder_of(local)->aggs, mine);
+        // 1) all-gather the record sizes, 2) all-gather fixed-size padded records (shard order == rank order)
+        DevBuf dsz, dall, dmine;
+        dsz.alloc(cm->ctx, (size_t)cm->nranks * 8);
+        const uint64_t my = mine.size();
+        HIPX(hipMemcpy(dsz.as<uint8_t>() + (size_t)cm->rank * 8, &my, 8, hipMemcpyHostToDevice));
+        NCCLX(ncclAllGather(dsz.as<uint8_t>() + (size_t)cm->rank * 8, dsz.p, 8, ncclUint8, cm->comm, cm->stream));
+        std::vector<uint64_t> sizes(cm->nranks);
+        HIPX(hipMemcpyAsync(sizes.data(), dsz.p, (size_t)cm->nranks * 8, hipMemcpyDeviceToHost, cm->stream));
+        HIPX(hipStreamSynchronize(cm->stream));
+        const uint64_t rec = std::max<uint64_t>(*std::max_element(sizes.begin(), sizes.end()), 8);
+        dmine.alloc(cm->ctx, rec);
+        dall.alloc(cm->ctx, rec * cm->nranks);
+        HIPX(hipMemcpy(dmine.p, mine.data(), mine.size(), hipMemcpyHostToDevice));
+        NCCLX(ncclAllGather(dmine.p, dall.p, rec, ncclUint8, cm->comm, cm->stream));
+        std::vector<uint8_t> all(rec * cm->nranks);
+        HIPX(hipMemcpyAsync(all.data(), dall.p, all.size(), hipMemcpyDeviceToHost, cm->stream));
+        HIPX(hipStreamSynchronize(cm->stream));
+        std::vector<std::vector<RAgg>> shards(cm->nranks);
+        std::vector<const std::vector<RAgg>*> lists;
+        for (int r = 0; r < cm->nranks; ++r) {
+            require(deserialize(all.data() + rec * r, sizes[r], shards[r]), ESGPU_ERR_DEVICE, "corrupt shard record");
+            lists.push_back(&shards[r]);
+        }
+        std::unique_ptr<ResultHolder> h(new ResultHolder());
+        h->aggs = reduce_lists(lists);
+        h->export_view();
+        *out = &h.release()->pub;
+    });
+}

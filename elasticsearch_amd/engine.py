@@ -1,0 +1,311 @@
+"""Host-side driver of libesgpu.so: the Aggregator lifecycle of the reference, one shard per GPU.
+
+    engine = Engine(device=0)
+    seg = engine.synthetic_segment(num_docs=1 << 24, fields=("host", "@timestamp", "response_time_ms"))
+    plan = engine.plan([AggregationBuilders.terms("hosts").field("host")
+                        .subAggregation(AggregationBuilders.dateHistogram("h").field("@timestamp").interval("1h")
+                                        .subAggregation(AggregationBuilders.stats("rt").field("response_time_ms")))])
+    plan.collect(seg)                 # getLeafCollector + collect(doc) for every doc of the segment
+    shard = plan.build()              # postCollection + buildAggregation(0)
+    final = reduce([shard])           # InternalAggregations.reduce on the coordinating node
+    final.to_dict()
+
+Mirrors AggregationPhase / QueryPhase (core/src/main/java/org/elasticsearch/search/aggregations/AggregationPhase.java:69-168,
+core/src/main/java/org/elasticsearch/search/query/QueryPhase.java:254-258,312-314) and the coordinator reduce
+(core/src/main/java/org/elasticsearch/search/controller/SearchPhaseController.java:401-411).
+"""
+import ctypes
+import json
+
+import numpy as np
+
+from . import _native as N
+from .aggs import flatten, flatten_filters
+
+
+class ShardResult:
+    """An esgpu_result: the shard-level (or reduced) InternalAggregations."""
+
+    def __init__(self, ptr):
+        self._ptr = ptr
+
+    @property
+    def ptr(self):
+        return self._ptr
+
+    def __del__(self):
+        if getattr(self, "_ptr", None):
+            try:
+                N.lib().esgpu_result_free(self._ptr)
+            except Exception:
+                pass
+            self._ptr = None
+
+    def to_json(self):
+        needed = ctypes.c_size_t()
+        N.check(N.lib().esgpu_result_to_json(self._ptr, None, 0, ctypes.byref(needed)))
+        buf = ctypes.create_string_buffer(needed.value + 1)
+        N.check(N.lib().esgpu_result_to_json(self._ptr, buf, len(buf), ctypes.byref(needed)))
+        return buf.value.decode("utf-8")
+
+    def to_dict(self):
+        return json.loads(self.to_json())
+
+    def serialize(self):
+        needed = ctypes.c_size_t()
+        N.check(N.lib().esgpu_result_serialize(self._ptr, None, 0, ctypes.byref(needed)))
+        buf = (ctypes.c_uint8 * max(needed.value, 1))()
+        N.check(N.lib().esgpu_result_serialize(self._ptr, buf, needed.value, ctypes.byref(needed)))
+        return bytes(buf[: needed.value])
+
+    @staticmethod
+    def deserialize(data):
+        out = ctypes.POINTER(N.Result)()
+        buf = (ctypes.c_uint8 * max(len(data), 1)).from_buffer_copy(data if data else b"\0")
+        N.check(N.lib().esgpu_result_deserialize(buf, len(data), ctypes.byref(out)))
+        return ShardResult(out)
+
+    def aggregation(self, i=0):
+        return self._ptr.contents.aggs[i]
+
+    def registers(self, i=0):
+        a = self.aggregation(i)
+        if not a.hll_present or not a.hll_mode:
+            return None
+        return np.ctypeslib.as_array(a.registers, shape=(1 << a.precision,)).copy()
+
+
+def reduce(results):
+    """InternalAggregations.reduce over shard results in shard order (runs on the host, no GPU needed)."""
+    arr = (ctypes.POINTER(N.Result) * len(results))(*[r.ptr for r in results])
+    out = ctypes.POINTER(N.Result)()
+    N.check(N.lib().esgpu_reduce(arr, len(results), ctypes.byref(out)))
+    return ShardResult(out)
+
+
+class Segment:
+    def __init__(self, engine, ptr, dictionaries=None):
+        self.engine = engine
+        self._ptr = ptr
+        self.dictionaries = dictionaries or {}
+
+    @property
+    def ptr(self):
+        return self._ptr
+
+    @property
+    def max_doc(self):
+        v = ctypes.c_uint32()
+        N.check(N.lib().esgpu_segment_max_doc(self._ptr, ctypes.byref(v)))
+        return v.value
+
+    def read_column(self, field, start, count, dtype):
+        out = np.empty(count, dtype=dtype)
+        N.check(N.lib().esgpu_segment_read_column(self._ptr, field.encode(), start, count, out.ctypes.data))
+        return out
+
+    def ord_of(self, field, term):
+        d = self.dictionaries.get(field)
+        if d is None:
+            return -1
+        try:
+            return d.index(term)
+        except ValueError:
+            return -1
+
+    def close(self):
+        if self._ptr:
+            N.check(N.lib().esgpu_segment_destroy(self._ptr))
+            self._ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Plan:
+    def __init__(self, engine, aggs, filters=None, number_of_shards=1, ord_lookup=None):
+        self.engine = engine
+        self._specs, n, self._keep = flatten(aggs, number_of_shards)
+        self._filters, nf, self._fkeep = flatten_filters(filters, ord_lookup)
+        ptr = ctypes.c_void_p()
+        N.check(N.lib().esgpu_plan_create(engine.ptr, self._specs, n, self._filters, nf, ctypes.byref(ptr)))
+        self._ptr = ptr
+
+    def collect(self, segment, accept_bits=None):
+        bits = None
+        if accept_bits is not None:
+            bits = np.ascontiguousarray(accept_bits, dtype=np.uint64)
+        N.check(N.lib().esgpu_plan_collect_segment(self._ptr, segment.ptr, bits.ctypes.data if bits is not None else None))
+        return self
+
+    def post_collection(self):
+        N.check(N.lib().esgpu_plan_post_collection(self._ptr))
+
+    def build(self):
+        out = ctypes.POINTER(N.Result)()
+        N.check(N.lib().esgpu_plan_build(self._ptr, ctypes.byref(out)))
+        return ShardResult(out)
+
+    def reset(self):
+        N.check(N.lib().esgpu_plan_reset(self._ptr))
+
+    def last_collect_stats(self):
+        ms, nbytes, path = ctypes.c_double(), ctypes.c_uint64(), ctypes.c_int32()
+        N.check(N.lib().esgpu_plan_last_collect_stats(self._ptr, ctypes.byref(ms), ctypes.byref(nbytes), ctypes.byref(path)))
+        return ms.value, nbytes.value, path.value
+
+    def close(self):
+        if self._ptr:
+            N.check(N.lib().esgpu_plan_destroy(self._ptr))
+            self._ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Engine:
+    """One device context (one GPU); shards map one-per-GPU."""
+
+    def __init__(self, device=0, hbm_budget_bytes=0):
+        ptr = ctypes.c_void_p()
+        N.check(N.lib().esgpu_ctx_create(device, hbm_budget_bytes, ctypes.byref(ptr)))
+        self._ptr = ptr
+        self.device = device
+
+    @property
+    def ptr(self):
+        return self._ptr
+
+    def hbm_used(self):
+        v = ctypes.c_uint64()
+        N.check(N.lib().esgpu_ctx_hbm_used(self._ptr, ctypes.byref(v)))
+        return v.value
+
+    def synthetic_segment(self, num_docs, fields=("host", "@timestamp", "response_time_ms"), shard=0,
+                          seed=0x5EEDE1A5):
+        mask = 0
+        for f in fields:
+            mask |= N.SYNTH_FIELDS[f]
+        ptr = ctypes.c_void_p()
+        N.check(N.lib().esgpu_segment_synthetic(self._ptr, seed, shard, num_docs, mask, ctypes.byref(ptr)))
+        return Segment(self, ptr)
+
+    def upload_segment(self, columns, max_doc):
+        """columns: {name: dict(type=COL_*, values=np.array, offsets=None|np.uint64, present=None|np.uint64 bits,
+        terms=None|list[str|bytes])}.  Host arrays are copied once into HBM."""
+        descs, keep, dicts = [], [], {}
+        for name, c in columns.items():
+            d = N.ColumnDesc()
+            bname = name.encode("utf-8")
+            keep.append(bname)
+            d.name = bname
+            d.type = c["type"]
+            dtype = {N.COL_ORD_U32: np.uint32, N.COL_I64: np.int64, N.COL_F64: np.float64, N.COL_U64: np.uint64}[c["type"]]
+            vals = np.ascontiguousarray(c["values"], dtype=dtype)
+            keep.append(vals)
+            d.values = vals.ctypes.data if vals.size else None
+            if c.get("offsets") is not None:
+                offs = np.ascontiguousarray(c["offsets"], dtype=np.uint64)
+                keep.append(offs)
+                d.offsets = offs.ctypes.data
+            if c.get("present") is not None:
+                pres = np.ascontiguousarray(c["present"], dtype=np.uint64)
+                keep.append(pres)
+                d.present = pres.ctypes.data
+            terms = c.get("terms")
+            if c.get("terms_blob") is not None:
+                blob, offs = c["terms_blob"]
+                blob = np.ascontiguousarray(blob, dtype=np.uint8)
+                offs = np.ascontiguousarray(offs, dtype=np.uint64)
+                keep += [blob, offs]
+                d.dict_bytes = blob.ctypes.data
+                d.dict_offsets = offs.ctypes.data
+                d.value_count = len(offs) - 1
+            elif terms is not None:
+                tb = [t.encode("utf-8") if isinstance(t, str) else bytes(t) for t in terms]
+                blob = np.frombuffer(b"".join(tb), dtype=np.uint8) if tb and sum(map(len, tb)) else np.zeros(1, np.uint8)
+                offs = np.zeros(len(tb) + 1, dtype=np.uint64)
+                offs[1:] = np.cumsum([len(t) for t in tb]) if tb else []
+                blob = np.ascontiguousarray(blob)
+                keep += [blob, offs]
+                d.dict_bytes = blob.ctypes.data
+                d.dict_offsets = offs.ctypes.data
+                d.value_count = len(tb)
+                dicts[name] = [t.decode("utf-8", "replace") for t in tb]
+            else:
+                d.value_count = int(c.get("value_count", 0))
+            descs.append(d)
+        arr = (N.ColumnDesc * max(len(descs), 1))(*descs)
+        ptr = ctypes.c_void_p()
+        N.check(N.lib().esgpu_segment_upload(self._ptr, arr, len(descs), max_doc, ctypes.byref(ptr)))
+        return Segment(self, ptr, dicts)
+
+    def plan(self, aggs, filters=None, number_of_shards=1, ord_lookup=None):
+        return Plan(self, aggs, filters, number_of_shards, ord_lookup)
+
+    def close(self):
+        if self._ptr:
+            N.check(N.lib().esgpu_ctx_destroy(self._ptr))
+            self._ptr = None
+
+
+def device_count():
+    n = ctypes.c_int()
+    N.check(N.lib().esgpu_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def synthetic_host_column(field, num_docs, start=0, count=None, shard=0, seed=0x5EEDE1A5):
+    """The same synthetic values the device generator writes, computed on the CPU (oracle / CPU baseline input)."""
+    count = num_docs - start if count is None else count
+    dtype = {N.COL_ORD_U32: np.uint32, N.COL_I64: np.int64, N.COL_F64: np.float64, N.COL_U64: np.uint64}[N.SYNTH_TYPES[field]]
+    out = np.empty(count, dtype=dtype)
+    N.check(N.lib().esgpu_synthetic_fill_host(seed, shard, num_docs, N.SYNTH_FIELDS[field], start, count, out.ctypes.data))
+    return out
+
+
+def synthetic_terms(field, n):
+    buf = ctypes.create_string_buffer(64)
+    out = []
+    for o in range(n):
+        N.lib().esgpu_synthetic_term(N.SYNTH_FIELDS[field], o, buf, 64)
+        out.append(buf.value.decode())
+    return out
+
+
+def precision_from_threshold(t):
+    p = ctypes.c_int32()
+    N.check(N.lib().esgpu_precision_from_threshold(t, ctypes.byref(p)))
+    return p.value
+
+
+class Communicator:
+    """RCCL communicator over xGMI for the shard-level reduce (one process per GPU)."""
+
+    def __init__(self, engine, nranks, rank, unique_id):
+        ptr = ctypes.c_void_p()
+        idbuf = (ctypes.c_uint8 * N.COMM_ID_BYTES).from_buffer_copy(unique_id)
+        N.check(N.lib().esgpu_comm_init(engine.ptr, nranks, rank, idbuf, ctypes.byref(ptr)))
+        self._ptr = ptr
+
+    @staticmethod
+    def unique_id():
+        buf = (ctypes.c_uint8 * N.COMM_ID_BYTES)()
+        N.check(N.lib().esgpu_comm_unique_id(buf))
+        return bytes(buf)
+
+    def gather_reduce(self, shard_result):
+        out = ctypes.POINTER(N.Result)()
+        N.check(N.lib().esgpu_comm_gather_reduce(self._ptr, shard_result.ptr, ctypes.byref(out)))
+        return ShardResult(out)
+
+    def close(self):
+        if self._ptr:
+            N.check(N.lib().esgpu_comm_destroy(self._ptr))
+            self._ptr = None

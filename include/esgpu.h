@@ -1,0 +1,354 @@
+/*
+ * esgpu.h — C-ABI of libesgpu.so, the MI355X-native replacement for Elasticsearch's per-shard
+ * aggregation collection path (global-ordinal terms, histogram/date_histogram, stats/extended_stats/avg,
+ * HyperLogLog++ cardinality, term/range filters) and the shard-level InternalAggregation.reduce.
+ *
+ * Reference interfaces (paths relative to /root/reference/core/src/main/java/org/elasticsearch/):
+ *   AggregatorFactory.createInternal ............ search/aggregations/AggregatorFactory.java:88-103
+ *   Aggregator / BucketCollector ................. search/aggregations/Aggregator.java:38-107,
+ *                                                  search/aggregations/BucketCollector.java:34-117
+ *   getLeafCollector + LeafBucketCollector.collect search/aggregations/AggregatorBase.java:129-133,
+ *                                                  search/aggregations/LeafBucketCollector.java:78-83
+ *   postCollection / buildAggregation ............ search/aggregations/AggregatorBase.java:239-243
+ *   InternalAggregation.doReduce ................. search/aggregations/InternalAggregation.java:152-160,
+ *                                                  search/aggregations/InternalAggregations.java:133-161
+ *   AggregationStreams (writeTo / readFrom) ...... search/aggregations/AggregationStreams.java
+ *
+ * A JNI shim maps each Java call onto exactly one entry point below.  Every function
+ * returns an int status (ESGPU_OK = 0); esgpu_last_error() returns the thread-local message, which the
+ * shim turns into IOException / AggregationExecutionException / CircuitBreakingException.
+ *
+ * Nothing here takes or returns a torch/HIP type: plain pointers and sizes only.
+ */
+#ifndef ESGPU_H
+#define ESGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ESGPU_ABI_VERSION 1
+
+/* ---------------------------------------------------------------------------------------------------------
+ * Status codes.  Mapping used by the JNI shim (SURVEY §8(b) "Errors"):
+ *   ESGPU_ERR_INVALID     -> IllegalArgumentException / AggregationInitializationException (AggregationPhase.java:90-91)
+ *   ESGPU_ERR_UNSUPPORTED -> the plugin keeps the stock Java aggregator for this request (no GPU attempt made)
+ *   ESGPU_ERR_DEVICE      -> IOException from collect/build => QueryPhaseExecutionException => shard failure
+ *   ESGPU_ERR_OOM         -> CircuitBreakingException (BigArrays.java:393-395 accounting, here: HBM budget)
+ *   ESGPU_ERR_STATE       -> IllegalStateException (calls out of order)
+ * ------------------------------------------------------------------------------------------------------- */
+enum {
+    ESGPU_OK = 0,
+    ESGPU_ERR_INVALID = 1,
+    ESGPU_ERR_UNSUPPORTED = 2,
+    ESGPU_ERR_DEVICE = 3,
+    ESGPU_ERR_OOM = 4,
+    ESGPU_ERR_STATE = 5,
+    ESGPU_ERR_NO_DEVICE = 6
+};
+
+/* Copies the calling thread's last error message (NUL-terminated, truncated to cap). Returns its length. */
+int esgpu_last_error(char* buf, size_t cap);
+int esgpu_abi_version(void);
+
+/* ---------------------------------------------------------------------------------------------------------
+ * Device context: one per GPU, owns the HBM budget (REQUEST/FIELDDATA breaker analogue) and the streams.
+ * Thread-safe for segment upload; plans created from it are single-threaded (one SEARCH thread per shard
+ * request, SURVEY §8(b) "Threading").
+ * ------------------------------------------------------------------------------------------------------- */
+typedef struct esgpu_ctx esgpu_ctx;
+
+/* device: HIP ordinal. hbm_budget_bytes: 0 = 90% of device memory. */
+int esgpu_ctx_create(int device, uint64_t hbm_budget_bytes, esgpu_ctx** out);
+int esgpu_ctx_destroy(esgpu_ctx* ctx);
+int esgpu_ctx_hbm_used(const esgpu_ctx* ctx, uint64_t* bytes);
+int esgpu_device_count(int* count);
+
+/* ---------------------------------------------------------------------------------------------------------
+ * Segment = one Lucene LeafReaderContext exported from doc values (K11).
+ * Replaces ValuesSource.*Values(ctx) (search/aggregations/support/ValuesSource.java:60-152, 380-398).
+ *
+ * Column types (natural widths of SURVEY §8(d)):
+ *   ESGPU_COL_ORD_U32 : SORTED / SORTED_SET doc values as u32 global ordinals, 0xFFFFFFFF = missing
+ *                       (GlobalOrdinalsStringTermsAggregator.java:113-118; ord < 0 == missing)
+ *   ESGPU_COL_I64     : SORTED_NUMERIC longs / dates as epoch millis (DateFieldMapper.java:539)
+ *   ESGPU_COL_F64     : doubles (DoubleFieldMapper sortable-long already decoded to double)
+ *   ESGPU_COL_U64     : murmur3 field hashes (Murmur3FieldMapper.java:160-162), stored as the signed long bits
+ * Multi-valued columns are CSR: offsets[max_doc + 1] into values, values of one doc sorted ascending
+ * (SortedNumericDocValues / SortedSetDocValues contract).  Single-valued numerics may carry a
+ * `present` bitset (bit d set = doc d has a value); NULL = every doc has exactly one value.
+ * ------------------------------------------------------------------------------------------------------- */
+enum {
+    ESGPU_COL_ORD_U32 = 1,
+    ESGPU_COL_I64 = 2,
+    ESGPU_COL_F64 = 3,
+    ESGPU_COL_U64 = 4
+};
+
+typedef struct esgpu_column_desc {
+    const char* name;            /* field name as used by esgpu_agg_spec.field / esgpu_filter.field */
+    int32_t type;                /* ESGPU_COL_* */
+    int32_t reserved;
+    const void* values;          /* host memory (pinned recommended): max_doc entries, or offsets[max_doc] for CSR */
+    const uint64_t* offsets;     /* NULL = single valued; else max_doc+1 CSR offsets */
+    const uint64_t* present;     /* NULL = dense; else ceil(max_doc/64) words */
+    /* ORD_U32 only: the segment's term dictionary, terms sorted by unsigned bytes (Lucene BytesRef order).
+     * term i = dict_bytes[dict_offsets[i] .. dict_offsets[i+1]).  value_count = number of terms. */
+    const uint8_t* dict_bytes;
+    const uint64_t* dict_offsets;
+    uint64_t value_count;
+} esgpu_column_desc;
+
+typedef struct esgpu_segment esgpu_segment;
+
+/* K11: copies each column once into HBM (hipMemcpyAsync from the caller's buffers), builds per-block
+ * min/max zone maps for numeric columns, keeps the term dictionaries host-side for lookupOrd. */
+int esgpu_segment_upload(esgpu_ctx* ctx, const esgpu_column_desc* cols, int32_t ncols, uint32_t max_doc,
+                         esgpu_segment** out);
+int esgpu_segment_destroy(esgpu_segment* seg);
+int esgpu_segment_max_doc(const esgpu_segment* seg, uint32_t* max_doc);
+
+/* Synthetic log-style shard generated directly in HBM (bench/test data).
+ * fields_mask: bit set of ESGPU_SYNTH_* columns to materialise. */
+enum {
+    ESGPU_SYNTH_TIMESTAMP = 1 << 0,   /* "@timestamp"       I64  */
+    ESGPU_SYNTH_HOST = 1 << 1,        /* "host"             ORD  (1,000 terms, Zipf 1.1) */
+    ESGPU_SYNTH_URL = 1 << 2,         /* "url"              ORD  (10,000,000 terms, Zipf 1.0) */
+    ESGPU_SYNTH_STATUS = 1 << 3,      /* "status"           I64  */
+    ESGPU_SYNTH_RESPONSE = 1 << 4,    /* "response_time_ms" I64  in [0,999] */
+    ESGPU_SYNTH_BYTES = 1 << 5,       /* "bytes"            I64  in [0,1e6) */
+    ESGPU_SYNTH_CLIENT_IP = 1 << 6,   /* "client_ip.hash"   U64  murmur3 h1 of a dotted quad */
+    ESGPU_SYNTH_PRICE = 1 << 7        /* "price"            F64  non-integer doubles (float-stress) */
+};
+int esgpu_segment_synthetic(esgpu_ctx* ctx, uint64_t seed, uint32_t shard, uint32_t num_docs, uint32_t fields_mask,
+                            esgpu_segment** out);
+/* Host-side generation of the same values (doc range [start, start+count)), for the CPU oracle/baseline.
+ * out must hold count entries of the column's natural width (u32 for ORD columns, 8 bytes otherwise). */
+int esgpu_synthetic_fill_host(uint64_t seed, uint32_t shard, uint32_t num_docs, uint32_t field_bit, uint64_t start,
+                              uint64_t count, void* out);
+/* Term bytes of a synthetic dictionary term (host / url).  Returns length, writes at most cap bytes. */
+int esgpu_synthetic_term(uint32_t field_bit, uint64_t ord, char* buf, size_t cap);
+/* Copy a device column range back to host (tests compare device vs host generator). */
+int esgpu_segment_read_column(const esgpu_segment* seg, const char* field, uint64_t start, uint64_t count, void* out);
+
+/* ---------------------------------------------------------------------------------------------------------
+ * Aggregation plan = one AggregatorFactory tree for one shard request (AggregatorFactories.java:68-90).
+ * Specs are a flattened tree: spec[i].parent is the index of the enclosing bucket aggregation (-1 = top
+ * level); parents precede children.  Parameters already carry the parser defaults (a1, a10, a17):
+ *   terms:          size 10, shard_size from BucketUtils.suggestShardSideQueueSize, min_doc_count 1,
+ *                   shard_min_doc_count 0, order count desc (+ term asc tie-break)
+ *   date_histogram: min_doc_count 0, order key asc, unit/interval + offset (UTC or fixed tz offset folded in)
+ *   cardinality:    precision_threshold -1 = default precision (14, -5 per multi-bucket ancestor)
+ * esgpu_terms_thresholds() applies TermsParser + BucketCountThresholds.ensureValidity for callers that
+ * only have the raw request values.
+ * ------------------------------------------------------------------------------------------------------- */
+enum {
+    ESGPU_AGG_TERMS = 1,
+    ESGPU_AGG_HISTOGRAM = 2,
+    ESGPU_AGG_DATE_HISTOGRAM = 3,
+    ESGPU_AGG_STATS = 4,
+    ESGPU_AGG_EXTENDED_STATS = 5,
+    ESGPU_AGG_AVG = 6,
+    ESGPU_AGG_CARDINALITY = 7,
+    ESGPU_AGG_SUM = 8,
+    ESGPU_AGG_MIN = 9,
+    ESGPU_AGG_MAX = 10,
+    ESGPU_AGG_VALUE_COUNT = 11
+};
+
+/* terms order (InternalOrder.java:47-76; compound with _term asc tie-break for the count orders) */
+enum {
+    ESGPU_ORDER_COUNT_DESC = 0,
+    ESGPU_ORDER_COUNT_ASC = 1,
+    ESGPU_ORDER_TERM_ASC = 2,
+    ESGPU_ORDER_TERM_DESC = 3,
+    /* histogram orders (bucket/histogram/InternalOrder.java) */
+    ESGPU_ORDER_KEY_ASC = 4,
+    ESGPU_ORDER_KEY_DESC = 5,
+    ESGPU_ORDER_HCOUNT_ASC = 6,
+    ESGPU_ORDER_HCOUNT_DESC = 7
+};
+
+/* date_histogram calendar units (DateTimeUnit.java:36-43); ESGPU_UNIT_NONE = fixed interval in ms */
+enum {
+    ESGPU_UNIT_NONE = 0,
+    ESGPU_UNIT_WEEK = 1,
+    ESGPU_UNIT_YEAR = 2,
+    ESGPU_UNIT_QUARTER = 3,
+    ESGPU_UNIT_MONTH = 4,
+    ESGPU_UNIT_DAY = 5,
+    ESGPU_UNIT_HOUR = 6,
+    ESGPU_UNIT_MINUTE = 7,
+    ESGPU_UNIT_SECOND = 8
+};
+
+typedef struct esgpu_agg_spec {
+    int32_t type;                 /* ESGPU_AGG_* */
+    int32_t parent;               /* index of parent bucket agg, -1 = top level */
+    const char* name;
+    const char* field;
+    /* terms (TermsAggregator.BucketCountThresholds, TermsAggregator.java:63-85) */
+    int32_t size;
+    int32_t shard_size;
+    int64_t min_doc_count;
+    int64_t shard_min_doc_count;
+    int32_t order;                /* ESGPU_ORDER_* */
+    int32_t show_term_doc_count_error;
+    /* histogram / date_histogram (HistogramAggregator.java:60-75, DateHistogramParser.java:85-193) */
+    int32_t date_unit;            /* ESGPU_UNIT_*; NONE => `interval` in field units */
+    int32_t keyed;
+    int64_t interval;
+    int64_t offset;               /* OffsetRounding offset; a fixed time-zone offset is passed as -tz_offset_ms */
+    int32_t has_extended_bounds_min;
+    int32_t has_extended_bounds_max;
+    int64_t extended_bounds_min;  /* already rounded (ExtendedBounds.round) */
+    int64_t extended_bounds_max;
+    /* extended_stats (ExtendedStatsParser.java:57) */
+    double sigma;
+    /* cardinality (CardinalityParser.java:60-61) */
+    int64_t precision_threshold;
+} esgpu_agg_spec;
+
+/* Query filters: bool{filter:[...]} conjunction of term / range clauses. */
+enum {
+    ESGPU_FILTER_TERM = 1,        /* doc matches if any value == term (numeric: TermQuery on the prefix-coded long;
+                                     keyword: the term's ordinal; -1 = term not in dictionary => no match) */
+    ESGPU_FILTER_RANGE = 2        /* doc matches if any value in [lo,hi] with include flags (NumericRangeQuery) */
+};
+typedef struct esgpu_filter {
+    int32_t type;
+    int32_t include_lower;
+    int32_t include_upper;
+    int32_t has_lower;
+    int32_t has_upper;
+    int32_t reserved;
+    const char* field;
+    int64_t term;                 /* TERM on I64 / ORD columns */
+    int64_t lo_i, hi_i;           /* RANGE on I64 / U64 columns */
+    double lo_d, hi_d;            /* RANGE on F64 columns */
+} esgpu_filter;
+
+int esgpu_terms_thresholds(int32_t size, int32_t shard_size, int64_t min_doc_count, int64_t shard_min_doc_count,
+                           int32_t order, int32_t number_of_shards, int32_t* out_size, int32_t* out_shard_size,
+                           int64_t* out_min_doc_count, int64_t* out_shard_min_doc_count);
+int esgpu_precision_from_threshold(int64_t count, int32_t* precision);
+/* MurmurHash3_x64_128 (common/hash/MurmurHash3.java:62-157): the murmur3 field's index-time hash is out[0] (h1)
+ * (plugins/mapper-murmur3/.../Murmur3FieldMapper.java:152-165). */
+int esgpu_murmur3_x64_128(const uint8_t* bytes, size_t len, int64_t seed, uint64_t* out2);
+
+typedef struct esgpu_plan esgpu_plan;
+
+/* = AggregationPhase.preProcess + AggregatorFactories.createTopLevelAggregators (AggregationPhase.java:69-94). */
+int esgpu_plan_create(esgpu_ctx* ctx, const esgpu_agg_spec* specs, int32_t nspecs, const esgpu_filter* filters,
+                      int32_t nfilters, esgpu_plan** out);
+/* = getLeafCollector(ctx) + every collect(doc) of that segment.  accept_bits: optional live-docs / external
+ * query bitset (host memory, ceil(max_doc/64) words, bit d = doc d matches), AND-ed with the plan filters.
+ * Asynchronous on the plan's stream. */
+int esgpu_plan_collect_segment(esgpu_plan* plan, const esgpu_segment* seg, const uint64_t* accept_bits);
+/* = postCollection (AggregatorBase.java:239-243): LowCardinality remap, HLL LC/HLL decision; synchronises. */
+int esgpu_plan_post_collection(esgpu_plan* plan);
+/* = buildAggregation(0) on every top-level aggregator: returns the shard-level InternalAggregations. */
+typedef struct esgpu_result esgpu_result;
+int esgpu_plan_build(esgpu_plan* plan, esgpu_result** out);
+/* Zero the accumulators so the plan (and its compiled launch configuration) is reused for another request. */
+int esgpu_plan_reset(esgpu_plan* plan);
+int esgpu_plan_destroy(esgpu_plan* plan);
+/* Timing of the last collect_segment's dominant kernel (HIP events on the plan's stream), in milliseconds,
+ * and the algorithmic bytes it read (SURVEY §8(d) formula). */
+int esgpu_plan_last_collect_stats(const esgpu_plan* plan, double* kernel_ms, uint64_t* algorithmic_bytes,
+                                  int32_t* path);
+
+/* ---------------------------------------------------------------------------------------------------------
+ * Results: a tree of InternalAggregation values (StringTerms, InternalHistogram, InternalStats,
+ * InternalExtendedStats, InternalAvg, InternalCardinality ...).  Owned by the library.
+ * ------------------------------------------------------------------------------------------------------- */
+typedef struct esgpu_agg_result esgpu_agg_result;
+
+typedef struct esgpu_bucket {
+    int64_t key;                  /* histogram: rounded key; terms: ordinal within the producing shard */
+    const uint8_t* key_bytes;     /* terms: term bytes (StringTerms.Bucket.termBytes) */
+    int32_t key_len;
+    int32_t nsubs;
+    int64_t doc_count;
+    int64_t doc_count_error;
+    esgpu_agg_result* subs;       /* nsubs sub-aggregation results */
+} esgpu_bucket;
+
+struct esgpu_agg_result {
+    int32_t type;                 /* ESGPU_AGG_* */
+    int32_t order;
+    const char* name;
+    /* bucket aggs */
+    esgpu_bucket* buckets;
+    int64_t nbuckets;
+    int64_t doc_count_error;      /* InternalTerms.docCountError */
+    int64_t other_doc_count;      /* InternalTerms.otherDocCount */
+    int32_t required_size;
+    int32_t shard_size;
+    int64_t min_doc_count;
+    int32_t show_term_doc_count_error;
+    int32_t keyed;
+    /* histogram EmptyBucketInfo (InternalHistogram.java EmptyBucketInfo) */
+    int32_t has_empty_bucket_info;
+    int32_t date_unit;
+    int64_t interval;
+    int64_t offset;
+    int32_t has_extended_bounds_min;
+    int32_t has_extended_bounds_max;
+    int64_t extended_bounds_min;
+    int64_t extended_bounds_max;
+    esgpu_agg_result* empty_subs; /* sub-aggregation prototypes for empty buckets */
+    int32_t nempty_subs;
+    /* numeric metrics */
+    int32_t reserved;
+    int64_t count;
+    double sum, min, max, sum_of_squares, sigma;
+    /* cardinality (HyperLogLogPlusPlus state, HyperLogLogPlusPlus.java:519-555) */
+    int32_t hll_present;          /* 0 = InternalCardinality with counts == null (empty) */
+    int32_t precision;
+    int32_t hll_mode;             /* 0 = linear counting, 1 = hyperloglog */
+    int32_t reserved2;
+    uint8_t* registers;           /* 2^precision run lengths (hll_mode 1) */
+    uint32_t* lc_hashes;          /* encoded hashes (hll_mode 0), ascending */
+    int64_t lc_size;
+};
+
+struct esgpu_result {
+    esgpu_agg_result* aggs;
+    int32_t naggs;
+    int32_t reserved;
+};
+
+int esgpu_result_free(esgpu_result* r);
+/* InternalAggregations.reduce over shard results in shard order (InternalAggregations.java:133-161). */
+int esgpu_reduce(const esgpu_result* const* shard_results, int32_t n, esgpu_result** out);
+/* Cardinality value of a cardinality result (HyperLogLogPlusPlus.cardinality(0)). */
+int esgpu_cardinality_value(const esgpu_agg_result* r, int64_t* value);
+/* XContent-style JSON ({"<name>": {...}}), full double precision, Infinity/NaN as JSON tokens.
+ * Writes at most cap bytes (NUL-terminated) and returns the full length in *needed. */
+int esgpu_result_to_json(const esgpu_result* r, char* buf, size_t cap, size_t* needed);
+/* Stream (AggregationStreams writeTo / readFrom analogue) for moving shard results between processes. */
+int esgpu_result_serialize(const esgpu_result* r, uint8_t* buf, size_t cap, size_t* needed);
+int esgpu_result_deserialize(const uint8_t* buf, size_t len, esgpu_result** out);
+
+/* ---------------------------------------------------------------------------------------------------------
+ * Multi-GPU shard reduce over RCCL (one process per GPU; shards map one-per-GPU).
+ * The unique id (ESGPU_COMM_ID_BYTES bytes) is created on rank 0 and broadcast by the caller.
+ * esgpu_comm_gather_reduce: ncclAllGather of every rank's serialized shard result (fixed-size padded
+ * records, xGMI), then InternalAggregations.reduce in rank (= shard) order on every rank.
+ * ------------------------------------------------------------------------------------------------------- */
+#define ESGPU_COMM_ID_BYTES 128
+typedef struct esgpu_comm esgpu_comm;
+int esgpu_comm_unique_id(uint8_t* id_out);
+int esgpu_comm_init(esgpu_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t* id, esgpu_comm** out);
+int esgpu_comm_destroy(esgpu_comm* comm);
+int esgpu_comm_gather_reduce(esgpu_comm* comm, const esgpu_result* local, esgpu_result** out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ESGPU_H */

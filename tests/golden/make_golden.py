@@ -1,0 +1,287 @@
+#!/usr/bin/env python3
+"""Extract the reference's own known-answer vectors and fixtures for the aggregation path into JSON.
+
+Runs ONLY in the build container (it reads /root/reference as text, never executes it).  Outputs are
+committed as data under tests/golden/ and are what the oracle is pinned against:
+
+  kat.json          - known-answer vectors transcribed from the reference tests (each entry cites file:line)
+  hllpp_tables.json - the HyperLogLog++ empirical raw-estimate / bias / threshold tables (published
+                      appendix data of Heule et al. 2013, as held by HyperLogLogPlusPlus.java:84-152)
+
+It also renders hllpp_tables.json into the C include files used by the oracle and the product
+(oracle/hllpp_tables.inc, elasticsearch_amd/csrc/hllpp_tables.inc).
+
+Usage:  python tests/golden/make_golden.py [--reference /root/reference]
+"""
+import argparse
+import json
+import os
+import re
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+
+T = "core/src/test/java/org/elasticsearch/"
+G = "plugins/lang-groovy/src/test/java/org/elasticsearch/messy/tests/"
+A = "core/src/main/java/org/elasticsearch/search/aggregations/"
+
+
+def _read(ref, rel):
+    with open(os.path.join(ref, rel), encoding="utf-8") as f:
+        return f.read()
+
+
+def _line_of(text, needle):
+    idx = text.index(needle)
+    return text.count("\n", 0, idx) + 1
+
+
+def _s64(v):
+    """Java long literal (two's complement) -> signed python int."""
+    v &= (1 << 64) - 1
+    return v - (1 << 64) if v >> 63 else v
+
+
+def murmur3_vectors(ref):
+    rel = T + "common/hashing/MurmurHash3Tests.java"
+    text = _read(ref, rel)
+    out = []
+    pat = re.compile(r'assertHash\((0x[0-9a-fA-F]+)L, (0x[0-9a-fA-F]+)L, "([^"]*)", (\d+)\);')
+    for m in pat.finditer(text):
+        line = text.count("\n", 0, m.start()) + 1
+        out.append({"h1": _s64(int(m.group(1), 16)), "h2": _s64(int(m.group(2), 16)),
+                    "input": m.group(3), "seed": int(m.group(4)), "cite": f"{rel}:{line}"})
+    assert len(out) == 8, out
+    return out
+
+
+def precision_vectors(ref):
+    rel = T + "search/aggregations/metrics/cardinality/HyperLogLogPlusPlusTests.java"
+    text = _read(ref, rel)
+    out = []
+    pat = re.compile(r"assertEquals\((\d+), HyperLogLogPlusPlus\.precisionFromThreshold\((\d+)\)\);")
+    for m in pat.finditer(text):
+        line = text.count("\n", 0, m.start()) + 1
+        out.append({"threshold": int(m.group(2)), "precision": int(m.group(1)), "cite": f"{rel}:{line}"})
+    assert len(out) == 7, out
+    return out
+
+
+def _utc(s):
+    """ISO-8601 (UTC) -> epoch millis, proleptic Gregorian (joda ISOChronology UTC)."""
+    m = re.match(r"(\d{4})-(\d{2})-(\d{2})T(\d{1,2}):(\d{1,2}):(\d{2})(?:\.(\d{3}))?Z?$", s)
+    y, mo, d, hh, mm, ss = (int(m.group(i)) for i in range(1, 7))
+    ms = int(m.group(7) or 0)
+    # days from civil (Howard Hinnant)
+    y2 = y - (1 if mo <= 2 else 0)
+    era = (y2 if y2 >= 0 else y2 - 399) // 400
+    yoe = y2 - era * 400
+    doy = (153 * (mo + (-3 if mo > 2 else 9)) + 2) // 5 + d - 1
+    doe = yoe * 365 + yoe // 4 - yoe // 100 + doy
+    days = era * 146097 + doe - 719468
+    return ((days * 24 + hh) * 60 + mm) * 60000 + ss * 1000 + ms
+
+
+def rounding_vectors(ref):
+    """UTC / fixed-offset rounding KATs.  A fixed time zone offset tz is expressed as OffsetRounding(-tz), which is
+    what TimeUnitRounding/TimeIntervalRounding compute for fixed-offset zones (TimeZoneRounding.java:126-131,185-190).
+    Each case: rounding kind, parameters, then (input -> rounded value) and (value -> nextRoundingValue) pairs."""
+    rel = T + "common/rounding/TimeZoneRoundingTests.java"
+    text = _read(ref, rel)
+    H = 3600000
+    cases = []
+
+    def add(needle, kind, params, rounds, nexts):
+        cases.append({"kind": kind, **params,
+                      "round": [[_utc(a) if isinstance(a, str) else a, _utc(b) if isinstance(b, str) else b] for a, b in rounds],
+                      "next": [[_utc(a) if isinstance(a, str) else a, _utc(b) if isinstance(b, str) else b] for a, b in nexts],
+                      "cite": f"{rel}:{_line_of(text, needle)}"})
+
+    add("builder(DateTimeUnit.MONTH_OF_YEAR).build()", "unit", {"unit": "month", "offset": 0},
+        [("2009-02-03T01:01:01", "2009-02-01T00:00:00.000Z")], [("2009-02-01T00:00:00.000Z", "2009-03-01T00:00:00.000Z")])
+    add("builder(DateTimeUnit.WEEK_OF_WEEKYEAR).build()", "unit", {"unit": "week", "offset": 0},
+        [("2012-01-10T01:01:01", "2012-01-09T00:00:00.000Z")], [("2012-01-09T00:00:00.000Z", "2012-01-16T00:00:00.000Z")])
+    add("offset(-TimeValue.timeValueHours(24).millis())", "unit", {"unit": "week", "offset": -24 * H},
+        [("2012-01-10T01:01:01", "2012-01-08T00:00:00.000Z")], [("2012-01-08T00:00:00.000Z", "2012-01-15T00:00:00.000Z")])
+    add("builder(TimeValue.timeValueHours(12)).build()", "interval", {"interval": 12 * H, "offset": 0},
+        [("2009-02-03T01:01:01", "2009-02-03T00:00:00.000Z"), ("2009-02-03T13:01:01", "2009-02-03T12:00:00.000Z")],
+        [("2009-02-03T00:00:00.000Z", "2009-02-03T12:00:00.000Z"), ("2009-02-03T12:00:00.000Z", "2009-02-04T00:00:00.000Z")])
+    add("builder(TimeValue.timeValueHours(48)).build()", "interval", {"interval": 48 * H, "offset": 0},
+        [("2009-02-03T01:01:01", "2009-02-03T00:00:00.000Z"), ("2009-02-05T13:01:01", "2009-02-05T00:00:00.000Z")],
+        [("2009-02-03T00:00:00.000Z", "2009-02-05T00:00:00.000Z"), ("2009-02-05T00:00:00.000Z", "2009-02-07T00:00:00.000Z")])
+    # tz -01:00 => offset +1h
+    add("builder(TimeValue.timeValueHours(6)).timeZone(DateTimeZone.forOffsetHours(-1))", "interval",
+        {"interval": 6 * H, "offset": 1 * H},
+        [("2009-02-03T00:01:01", "2009-02-02T19:00:00.000Z"), ("2009-02-03T13:01:01", "2009-02-03T13:00:00.000Z")],
+        [("2009-02-02T19:00:00.000Z", "2009-02-03T01:00:00.000Z"), ("2009-02-03T13:00:00.000Z", "2009-02-03T19:00:00.000Z")])
+    # tz -08:00 => offset +8h
+    add("builder(TimeValue.timeValueHours(12)).timeZone(DateTimeZone.forOffsetHours(-8))", "interval",
+        {"interval": 12 * H, "offset": 8 * H},
+        [("2009-02-03T00:01:01", "2009-02-02T20:00:00.000Z"), ("2009-02-03T13:01:01", "2009-02-03T08:00:00.000Z")],
+        [("2009-02-02T20:00:00.000Z", "2009-02-03T08:00:00.000Z"), ("2009-02-03T08:00:00.000Z", "2009-02-03T20:00:00.000Z")])
+    # day unit, tz -2 => offset +2h ; round(0) == -22h
+    add("int timezoneOffset = -2;", "unit", {"unit": "day", "offset": 2 * H},
+        [(0, -22 * H), ("2009-02-03T01:01:01", "2009-02-02T02:00:00"), ("2009-02-03T02:01:01", "2009-02-03T02:00:00")],
+        [(-22 * H, 2 * H), ("2009-02-02T02:00:00", "2009-02-03T02:00:00"), ("2009-02-03T02:00:00", "2009-02-04T02:00:00")])
+    add('DateTimeUnit.DAY_OF_MONTH).timeZone(DateTimeZone.forID("-08:00"))', "unit", {"unit": "day", "offset": 8 * H},
+        [("2012-04-01T04:15:30Z", "2012-03-31T08:00:00Z")], [("2012-03-31T08:00:00Z", "2012-04-01T08:00:00Z")])
+    add('DateTimeUnit.MONTH_OF_YEAR).timeZone(DateTimeZone.forID("-08:00"))', "unit", {"unit": "month", "offset": 8 * H},
+        [("2012-04-01T04:15:30Z", "2012-03-01T08:00:00Z")], [("2012-03-01T08:00:00Z", "2012-04-01T08:00:00Z")])
+    add("DateTimeUnit.HOUR_OF_DAY).timeZone(DateTimeZone.forOffsetHours(-2)).build();", "unit", {"unit": "hour", "offset": 2 * H},
+        [(0, 0), ("2009-02-03T01:01:01", "2009-02-03T01:00:00")],
+        [(0, H), ("2009-02-03T01:00:00", "2009-02-03T02:00:00")])
+
+    rel2 = T + "common/rounding/RoundingTests.java"
+    text2 = _read(ref, rel2)
+    cases.append({"kind": "histogram", "interval": 10, "offset": 0, "round": [[24, 20]], "next": [],
+                  "keys": [[24, 2]], "cite": f"{rel2}:{_line_of(text2, 'public void testInterval()')}"})
+    cases.append({"kind": "histogram", "interval": 10, "offset": 7,
+                  "round": [[6, -3], [7, 7], [16, 7], [17, 17]], "next": [[-3, 7], [7, 17], [17, 27]],
+                  "keys": [[6, -1], [7, 0], [16, 0], [17, 1]],
+                  "cite": f"{rel2}:{_line_of(text2, 'public void testOffsetRounding()')}"})
+    return cases
+
+
+def stats_fixtures(ref):
+    """AbstractNumericTestCase fixture: 10 docs, value = i+1, values = [i+2, i+3]; ExtendedStatsTests expectations."""
+    rel = T + "search/aggregations/metrics/AbstractNumericTestCase.java"
+    text = _read(ref, rel)
+    rel_es = G + "ExtendedStatsTests.java"
+    text_es = _read(ref, rel_es)
+    value = [i + 1 for i in range(10)]
+    values = [[i + 2, i + 3] for i in range(10)]
+    flat = [v for vs in values for v in vs]
+
+    def ext(vals):
+        s = 0.0
+        sq = 0.0
+        for v in vals:
+            s += v
+            sq += v * v
+        var = (sq - ((s * s) / len(vals))) / len(vals)
+        return {"count": len(vals), "sum": s, "min": float(min(vals)), "max": float(max(vals)),
+                "avg": s / len(vals), "sum_of_squares": sq, "variance": var}
+
+    return {"docs": {"value": value, "values": values},
+            "cite_fixture": f"{rel}:{_line_of(text, 'final int numDocs = 10;')}",
+            "single": ext(value), "multi": ext(flat),
+            "cite_expect": f"{rel_es}:{_line_of(text_es, 'public void testSingleValuedField() throws Exception')}",
+            "empty_bucket_docs": [0, 2],
+            "cite_empty": f"{rel}:{_line_of(text, 'empty_bucket_idx')}"}
+
+
+def shard_size_fixture(ref):
+    rel = T + "search/aggregations/bucket/ShardSizeTestCase.java"
+    text = _read(ref, rel)
+    rel2 = T + "search/aggregations/bucket/ShardSizeTermsIT.java"
+    text2 = _read(ref, rel2)
+    shard1 = {}
+    shard2 = {}
+    for m in re.finditer(r'indexDoc\(routing(\d), "(\d)", (\d+)\)', text):
+        (shard1 if m.group(1) == "1" else shard2)[m.group(2)] = int(m.group(3))
+    assert shard1 == {"1": 5, "2": 4, "3": 3, "4": 2, "5": 1} and shard2 == {"1": 3, "2": 1, "3": 5, "4": 2, "5": 1}
+    return {"shards": [shard1, shard2],
+            "cite_fixture": f"{rel}:{_line_of(text, 'docs.addAll(indexDoc(routing1')}",
+            "cases": [
+                {"size": 3, "shard_size": None, "expect": {"1": 8, "3": 8, "2": 5},
+                 "cite": f"{rel2}:{_line_of(text2, 'public void noShardSize_string()')}"},
+                {"size": 3, "shard_size": 3, "expect": {"1": 8, "3": 8, "2": 4},
+                 "cite": f"{rel2}:{_line_of(text2, 'public void shardSizeEqualsSize_string()')}"},
+            ]}
+
+
+def rest_fixtures(ref):
+    rel = "rest-api-spec/src/main/resources/rest-api-spec/test/search.aggregation/10_histogram.yaml"
+    text = _read(ref, rel)
+    numbers = [int(x) for x in re.findall(r'body: \{ "number" : (\d+) \}', text)[:4]]
+    keys = [int(x) for x in re.findall(r"aggregations\.histo\.buckets\.\d\.key: (\d+)", text)[:4]]
+    rel2 = "plugins/mapper-murmur3/src/test/resources/rest-api-spec/test/mapper_murmur3/10_basic.yaml"
+    text2 = _read(ref, rel2)
+    foos = re.findall(r'body: \{ "foo": "([^"]+)" \}', text2)
+    values = [int(x) for x in re.findall(r"aggregations\.foo_count\.value: (\d+)", text2)]
+    return {"histogram": {"numbers": numbers, "interval": 50, "keys": keys, "doc_counts": [1, 1, 1, 1],
+                          "cite": f"{rel}:{_line_of(text, 'interval')}"},
+            "murmur3_cardinality": {"empty_value": values[0], "foo": foos, "value": values[1],
+                                    "cite": f"{rel2}:{_line_of(text2, 'foo_count')}"}}
+
+
+def date_histogram_fixture(ref):
+    rel = G + "DateHistogramTests.java"
+    text = _read(ref, rel)
+    docs = [(int(a), int(b), int(c)) for a, b, c in re.findall(r"indexDoc\((\d+), (\d+), (\d+)\)", text)[:6]]
+    dates = [_utc(f"2012-{m:02d}-{d:02d}T00:00:00") for m, d, _ in docs]
+    datess = [[_utc(f"2012-{m:02d}-{d:02d}T00:00:00"), _utc(f"2012-{m + 1:02d}-{d + 1:02d}T00:00:00")] for m, d, _ in docs]
+    return {"date": dates, "dates": datess, "value": [v for _, _, v in docs],
+            "cite_fixture": f"{rel}:{_line_of(text, 'indexDoc(1, 2, 1)')}",
+            "monthly": {"keys": [_utc("2012-01-01T00:00:00"), _utc("2012-02-01T00:00:00"), _utc("2012-03-01T00:00:00")],
+                        "doc_counts": [1, 2, 3], "cite": f"{rel}:{_line_of(text, 'public void singleValuedField() throws Exception')}"},
+            "daily_tz_plus1": {"offset": -3600000, "min_doc_count": 1,
+                               "keys": [_utc(s) for s in ["2012-01-01T23:00:00", "2012-02-01T23:00:00", "2012-02-14T23:00:00",
+                                                           "2012-03-01T23:00:00", "2012-03-14T23:00:00", "2012-03-22T23:00:00"]],
+                               "doc_counts": [1, 1, 1, 1, 1, 1],
+                               "cite": f"{rel}:{_line_of(text, 'public void singleValuedField_WithTimeZone()')}"}}
+
+
+def hll_tables(ref):
+    rel = A + "metrics/cardinality/HyperLogLogPlusPlus.java"
+    text = _read(ref, rel)
+
+    def table(name):
+        start = text.index(f"private static final double[][] {name} = {{")
+        end = text.index("};", start)
+        rows = re.findall(r"\{([^{}]*)\}", text[start + len(name) + 40:end])
+        return [[float(x) for x in r.split(",") if x.strip()] for r in rows]
+
+    raw = table("RAW_ESTIMATE_DATA")
+    bias = table("BIAS_DATA")
+    start = text.index("private static final long[] THRESHOLDS")
+    thr = [int(x) for x in re.findall(r"\d+", text[start:text.index("};", start)].split("{", 1)[1])]
+    assert len(raw) == 15 and len(bias) == 15 and len(thr) == 15
+    assert all(len(a) == len(b) for a, b in zip(raw, bias))
+    return {"source": f"{rel}:84-152 (HLL++ paper appendix data)", "raw_estimate": raw, "bias": bias, "thresholds": thr}
+
+
+def render_inc(tables, path):
+    with open(path, "w") as f:
+        f.write("/* Generated by tests/golden/make_golden.py from tests/golden/hllpp_tables.json.\n"
+                " * HyperLogLog++ empirical raw-estimate / bias tables for precisions 4..18 and the linear-counting\n"
+                " * thresholds (appendix data of Heule, Nunkesser, Hall 2013; held by the reference at\n"
+                " * HyperLogLogPlusPlus.java:84-152).  Data only. */\n")
+        n = [len(r) for r in tables["raw_estimate"]]
+        f.write("static const int HLLPP_TABLE_LEN[15] = {%s};\n" % ", ".join(map(str, n)))
+        for name, key in (("HLLPP_RAW", "raw_estimate"), ("HLLPP_BIAS", "bias")):
+            for p, row in enumerate(tables[key]):
+                f.write("static const double %s_%d[] = {%s};\n" % (name, p + 4, ", ".join(repr(x) for x in row)))
+            f.write("static const double* const %s[15] = {%s};\n" % (name, ", ".join(f"{name}_{p}" for p in range(4, 19))))
+        f.write("static const long long HLLPP_THRESHOLDS[15] = {%s};\n" % ", ".join(map(str, tables["thresholds"])))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reference", default="/root/reference")
+    args = ap.parse_args()
+    ref = args.reference
+    if not os.path.isdir(ref):
+        print("reference not present; committed fixtures are used as-is", file=sys.stderr)
+        return 0
+    kat = {"murmur3_x64_128": murmur3_vectors(ref),
+           "precision_from_threshold": precision_vectors(ref),
+           "rounding": rounding_vectors(ref),
+           "stats": stats_fixtures(ref),
+           "shard_size_terms": shard_size_fixture(ref),
+           "rest": rest_fixtures(ref),
+           "date_histogram": date_histogram_fixture(ref)}
+    with open(os.path.join(HERE, "kat.json"), "w") as f:
+        json.dump(kat, f, indent=1)
+    tables = hll_tables(ref)
+    with open(os.path.join(HERE, "hllpp_tables.json"), "w") as f:
+        json.dump(tables, f)
+    render_inc(tables, os.path.join(REPO, "oracle", "hllpp_tables.inc"))
+    render_inc(tables, os.path.join(REPO, "elasticsearch_amd", "csrc", "hllpp_tables.inc"))
+    print("wrote kat.json, hllpp_tables.json and the two hllpp_tables.inc files")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,86 @@
+"""Shared test utilities: synthetic host columns for the oracle, and the parity comparison rules.
+
+Parity bar (BASELINE.json north_star): bucket keys / counts / ordinals / HLL registers bit-exact; floating sums
+and averages within 1e-12 relative.  For integer-valued metrics (the synthetic response_time_ms, bytes) every
+partial sum is exact, so those comparisons are bit-exact too (`exact_floats=True`).
+"""
+import math
+
+import numpy as np
+
+from elasticsearch_amd import _native as N
+from elasticsearch_amd import synthetic_host_column
+
+REL_TOL = 1e-12
+
+
+def synthetic_dict(field):
+    """Term dictionary blob/offsets of a synthetic keyword field (host-%04d / /p/%08x)."""
+    if field == "host":
+        terms = [b"host-%04d" % i for i in range(1000)]
+        blob = np.frombuffer(b"".join(terms), dtype=np.uint8).copy()
+        offs = np.arange(0, 9 * 1001, 9, dtype=np.uint64)
+        return blob, offs
+    if field == "url":
+        n = 10_000_000
+        ids = np.arange(n, dtype=np.uint64)
+        digits = (ids[:, None] >> (np.arange(7, -1, -1, dtype=np.uint64) * 4)) & 15
+        hexchars = np.frombuffer(b"0123456789abcdef", dtype=np.uint8)[digits.astype(np.int64)]
+        out = np.empty((n, 11), dtype=np.uint8)
+        out[:, 0] = ord("/")
+        out[:, 1] = ord("p")
+        out[:, 2] = ord("/")
+        out[:, 3:] = hexchars
+        return out.reshape(-1), np.arange(0, 11 * (n + 1), 11, dtype=np.uint64)
+    raise KeyError(field)
+
+
+def synthetic_columns(fields, num_docs, shard=0, seed=0x5EEDE1A5):
+    """Host copies of a synthetic shard, in the column-dict format of Engine.upload_segment / oracle.run."""
+    cols = {}
+    for f in fields:
+        c = {"type": N.SYNTH_TYPES[f], "values": synthetic_host_column(f, num_docs, shard=shard, seed=seed)}
+        if f in ("host", "url"):
+            c["terms_blob"] = synthetic_dict(f)
+        cols[f] = c
+    return cols
+
+
+def _num_equal(a, b, exact):
+    if isinstance(a, bool) or isinstance(b, bool) or a is None or b is None:
+        return a == b
+    if isinstance(a, int) and isinstance(b, int):
+        return a == b
+    fa, fb = float(a), float(b)
+    if math.isnan(fa) or math.isnan(fb):
+        return math.isnan(fa) and math.isnan(fb)
+    if math.isinf(fa) or math.isinf(fb) or exact:
+        return fa == fb
+    return abs(fa - fb) <= REL_TOL * max(abs(fa), abs(fb)) or fa == fb
+
+
+def assert_same(got, want, path="", exact_floats=True):
+    """Deep comparison of two parsed result trees with the parity rules above."""
+    if isinstance(want, dict):
+        assert isinstance(got, dict), f"{path}: expected object, got {type(got).__name__}"
+        assert set(got) == set(want), f"{path}: keys differ: {sorted(set(got) ^ set(want))}"
+        for k in want:
+            assert_same(got[k], want[k], f"{path}.{k}", exact_floats)
+    elif isinstance(want, list):
+        assert isinstance(got, list), f"{path}: expected list"
+        assert len(got) == len(want), f"{path}: length {len(got)} != {len(want)}"
+        for i, (g, w) in enumerate(zip(got, want)):
+            assert_same(g, w, f"{path}[{i}]", exact_floats)
+    elif isinstance(want, str):
+        assert got == want, f"{path}: {got!r} != {want!r}"
+    else:
+        assert _num_equal(got, want, exact_floats), f"{path}: {got!r} != {want!r}"
+
+
+def bits_from_mask(mask):
+    """bool array -> u64 bitset words (bit d of word d // 64 set = doc d), the layout of include/esgpu.h."""
+    mask = np.asarray(mask, dtype=bool)
+    words = np.zeros(max((len(mask) + 63) // 64, 1), dtype=np.uint64)
+    idx = np.nonzero(mask)[0].astype(np.uint64)
+    np.bitwise_or.at(words, (idx // np.uint64(64)).astype(np.int64), np.left_shift(np.uint64(1), idx % np.uint64(64)))
+    return words

@@ -1,0 +1,204 @@
+"""GPU parity: the gfx950 path (through the C-ABI) against the CPU oracle on the same seeded inputs.
+
+Each case builds one request with the reference's builder API, runs it on the GPU (device-generated or uploaded
+segment) and through the oracle (host-generated copies of the same columns), and compares the shard-level and the
+reduced InternalAggregations with tests/helpers.assert_same (counts/keys/registers bit-exact, floats bit-exact for
+integer-valued metrics, 1e-12 relative otherwise).
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from elasticsearch_amd import AggregationBuilders as AB
+from elasticsearch_amd import Order, QueryBuilders as QB
+from elasticsearch_amd import _native as N
+from elasticsearch_amd import reduce, synthetic_host_column
+from helpers import assert_same, bits_from_mask, synthetic_columns
+
+pytestmark = pytest.mark.gpu
+
+
+def run_both(engine, aggs, fields, num_docs, shard=0, filters=None, exact=True, upload=False, accept=None):
+    cols = synthetic_columns(fields, num_docs, shard=shard)
+    want = O.run([(cols, num_docs)], aggs, filters=filters, accept=[accept] if accept is not None else None)
+    if upload:
+        seg = engine.upload_segment(cols, num_docs)
+    else:
+        seg = engine.synthetic_segment(num_docs, fields=fields, shard=shard)
+    plan = engine.plan(aggs, filters=filters)
+    plan.collect(seg, accept_bits=accept)
+    shard_res = plan.build()
+    got_shard = shard_res.to_dict()
+    got_red = reduce([shard_res]).to_dict()
+    assert_same(got_shard, want["shards"][0], "shard", exact)
+    assert_same(got_red, want["reduced"], "reduced", exact)
+    plan.close()
+    seg.close()
+    return got_red
+
+
+def test_device_generator_matches_host(engine):
+    n = 300_000
+    fields = ("@timestamp", "host", "status", "response_time_ms", "bytes", "client_ip.hash", "price")
+    seg = engine.synthetic_segment(n, fields=fields, shard=3)
+    for f in fields:
+        host = synthetic_host_column(f, n, shard=3)
+        dev = seg.read_column(f, 0, n, host.dtype)
+        assert np.array_equal(dev.view(np.uint8), host.view(np.uint8)), f
+    ts = synthetic_host_column("@timestamp", n, shard=3)
+    assert np.all(np.diff(ts) >= 0)
+
+
+def test_config1_terms_stats(engine):  # terms(host){stats(response_time_ms)} on 1M docs
+    aggs = [AB.terms("hosts").field("host").subAggregation(AB.stats("rt").field("response_time_ms"))]
+    run_both(engine, aggs, ("host", "response_time_ms"), 1_000_000)
+
+
+def test_config2_date_histogram_extended_stats(engine):  # date_histogram(1h){extended_stats}
+    aggs = [AB.dateHistogram("per_hour").field("@timestamp").interval("1h")
+            .subAggregation(AB.extendedStats("rt").field("response_time_ms"))]
+    r = run_both(engine, aggs, ("@timestamp", "response_time_ms"), 2_000_000)
+    assert len(r["per_hour"]["buckets"]) == 720
+
+
+def test_north_star_terms_date_histogram_stats(engine):  # terms(host){date_histogram(1h){stats}}
+    aggs = [AB.terms("hosts").field("host").size(10).subAggregation(
+        AB.dateHistogram("per_hour").field("@timestamp").interval("1h").subAggregation(AB.stats("rt").field("response_time_ms")))]
+    run_both(engine, aggs, ("host", "@timestamp", "response_time_ms"), 3_000_000)
+
+
+def test_north_star_windowed_many_terms(engine):  # shard_size 1000: every host, forces the LDS key window
+    aggs = [AB.terms("hosts").field("host").size(1000).subAggregation(
+        AB.dateHistogram("per_hour").field("@timestamp").interval("1h").subAggregation(
+            AB.extendedStats("rt").field("response_time_ms")))]
+    run_both(engine, aggs, ("host", "@timestamp", "response_time_ms"), 1_500_000)
+
+
+def test_config5_filtered_nested_avg(engine):  # bool.filter[term, range] -> terms{date_histogram{avg}}
+    aggs = [AB.terms("hosts").field("host").subAggregation(
+        AB.dateHistogram("per_hour").field("@timestamp").interval("1h").subAggregation(AB.avg("rt").field("response_time_ms")))]
+    filters = [QB.termQuery("status", 200), QB.rangeQuery("bytes").gte(1024).lte(65536)]
+    run_both(engine, aggs, ("host", "@timestamp", "response_time_ms", "status", "bytes"), 2_000_000, filters=filters)
+
+
+def test_config3_high_cardinality_terms(engine):  # terms(url) over 10M global ordinals, shard_size 80
+    aggs = [AB.terms("urls").field("url").size(10)]
+    cols = synthetic_columns(("url",), 3_000_000)
+    want = O.run([(cols, 3_000_000)], aggs, number_of_shards=8)
+    seg = engine.synthetic_segment(3_000_000, fields=("url",))
+    plan = engine.plan(aggs, number_of_shards=8)
+    plan.collect(seg)
+    got = plan.build().to_dict()
+    assert_same(got, want["shards"][0], "shard")
+
+
+@pytest.mark.parametrize("n", [1_000, 40_000, 2_000_000])
+def test_config4_cardinality(engine, n):  # cardinality(client_ip.hash, precision_threshold 40000): LC and HLL modes
+    aggs = [AB.cardinality("ips").field("client_ip.hash").precisionThreshold(40000)]
+    r = run_both(engine, aggs, ("client_ip.hash",), n)
+    assert r["ips"]["_internal"]["mode"] == ("lc" if n <= 40_000 else "hll")
+
+
+def test_cardinality_default_precision_keyword(engine):  # cardinality on a keyword field (murmur3 of term bytes)
+    run_both(engine, [AB.cardinality("hosts").field("host")], ("host",), 500_000)
+
+
+def test_float_stress_sums(engine):  # non-integer doubles: sums compared at 1e-12 relative
+    aggs = [AB.dateHistogram("d").field("@timestamp").interval("1d").subAggregation(AB.extendedStats("p").field("price")),
+            AB.terms("hosts").field("host").subAggregation(AB.stats("p").field("price"))]
+    run_both(engine, aggs, ("@timestamp", "host", "price"), 1_000_000, exact=False)
+
+
+def test_histogram_interval_offset_and_orders(engine):
+    aggs = [AB.histogram("rt_hist").field("response_time_ms").interval(50).offset(7).subAggregation(AB.avg("b").field("bytes")),
+            AB.terms("hosts_asc").field("host").size(7).order(Order.count(True)),
+            AB.terms("hosts_term").field("host").size(5).order(Order.term(False)),
+            AB.dateHistogram("tz").field("@timestamp").interval("1d").timeZone("+05:30").minDocCount(1)]
+    run_both(engine, aggs, ("host", "@timestamp", "response_time_ms", "bytes"), 800_000)
+
+
+def test_date_histogram_then_terms(engine):  # date_histogram(1d){terms(host){stats}}
+    aggs = [AB.dateHistogram("days").field("@timestamp").interval("1d").subAggregation(
+        AB.terms("hosts").field("host").size(3).subAggregation(AB.stats("rt").field("response_time_ms")))]
+    run_both(engine, aggs, ("host", "@timestamp", "response_time_ms"), 1_000_000)
+
+
+def test_missing_values_min_doc_count_zero_and_accept_bits(engine):
+    n = 200_003  # ragged: not a multiple of the 8192-doc block
+    rng = np.random.default_rng(11)
+    cols = synthetic_columns(("host", "@timestamp", "response_time_ms"), n)
+    host = cols["host"]["values"].copy()
+    host[rng.random(n) < 0.1] = 0xFFFFFFFF  # missing keyword values
+    cols["host"]["values"] = host
+    cols["@timestamp"]["present"] = bits_from_mask(rng.random(n) >= 0.05)
+    cols["response_time_ms"]["present"] = bits_from_mask(rng.random(n) >= 0.2)
+    accept = bits_from_mask(rng.random(n) < 0.7)
+    aggs = [AB.terms("hosts").field("host").size(20).minDocCount(0).subAggregation(
+                AB.dateHistogram("h").field("@timestamp").interval("6h").subAggregation(AB.stats("rt").field("response_time_ms"))),
+            AB.dateHistogram("days").field("@timestamp").interval("1d").extendedBounds(1440000000000, 1444000000000)
+            .subAggregation(AB.terms("hosts").field("host").size(2)),
+            AB.extendedStats("all_rt").field("response_time_ms"),
+            AB.cardinality("card").field("host")]
+    want = O.run([(cols, n)], aggs, accept=[accept])
+    seg = engine.upload_segment(cols, n)
+    plan = engine.plan(aggs)
+    plan.collect(seg, accept_bits=accept)
+    res = plan.build()
+    assert_same(res.to_dict(), want["shards"][0], "shard")
+    assert_same(reduce([res]).to_dict(), want["reduced"], "reduced")
+
+
+def test_empty_segment_and_unmapped_fields(engine):
+    cols = {"host": {"type": N.COL_ORD_U32, "values": np.zeros(0, np.uint32), "terms": []}}
+    aggs = [AB.terms("t").field("host"), AB.terms("unmapped").field("nope"), AB.stats("s").field("nope"),
+            AB.dateHistogram("d").field("nope").interval("1h"), AB.cardinality("c").field("nope")]
+    want = O.run([(cols, 0)], aggs)
+    seg = engine.upload_segment(cols, 0)
+    plan = engine.plan(aggs)
+    plan.collect(seg)
+    res = plan.build()
+    assert_same(res.to_dict(), want["shards"][0], "shard")
+    assert_same(reduce([res]).to_dict(), want["reduced"], "reduced")
+
+
+def test_multi_shard_reduce_matches_oracle(engine):  # 4 shards, one plan per shard, host-side coordinator reduce
+    n = 250_000
+    fields = ("host", "@timestamp", "response_time_ms", "client_ip.hash")
+    aggs = [AB.terms("hosts").field("host").size(5).subAggregation(
+                AB.dateHistogram("h").field("@timestamp").interval("1d").subAggregation(AB.stats("rt").field("response_time_ms"))),
+            AB.cardinality("ips").field("client_ip.hash").precisionThreshold(1000)]
+    shards = [(synthetic_columns(fields, n, shard=s), n) for s in range(4)]
+    want = O.run(shards, aggs, number_of_shards=4)
+    results = []
+    for s in range(4):
+        seg = engine.synthetic_segment(n, fields=fields, shard=s)
+        plan = engine.plan(aggs, number_of_shards=4)
+        plan.collect(seg)
+        r = plan.build()
+        assert_same(r.to_dict(), want["shards"][s], f"shard{s}")
+        results.append(r)
+    assert_same(reduce(results).to_dict(), want["reduced"], "reduced")
+
+
+def test_plan_reset_reuse_and_multi_segment(engine):  # two segments into one plan == oracle over the concatenation
+    n = 300_000
+    fields = ("host", "@timestamp", "response_time_ms")
+    cols = synthetic_columns(fields, 2 * n)
+    halves = []
+    for h in range(2):
+        part = {}
+        for f, c in cols.items():
+            d = dict(c)
+            d["values"] = c["values"][h * n:(h + 1) * n]
+            part[f] = d
+        halves.append(part)
+    aggs = [AB.terms("hosts").field("host").subAggregation(
+        AB.dateHistogram("h").field("@timestamp").interval("1h").subAggregation(AB.stats("rt").field("response_time_ms")))]
+    want = O.run([(cols, 2 * n)], aggs)
+    plan = engine.plan(aggs)
+    for rep in range(2):
+        segs = [engine.upload_segment(halves[h], n) for h in range(2)]
+        for s in segs:
+            plan.collect(s)
+        assert_same(plan.build().to_dict(), want["shards"][0], f"rep{rep}")
+        plan.reset()
