@@ -206,6 +206,8 @@ __device__ __forceinline__ void update_doc(const CollectParams& P, const Acc& a,
                                            bool has_h, uint32_t slot, bool mpres, double x) {
     if (P.ocnt_mode == OCNT_TERMS && has_t) {
         if (LDS) atomicAdd(&a.ocnt32[t], 1u); else atomicAdd(&a.ocnt64[t], 1ull);
+    } else if (!LDS && P.ocnt_mode == OCNT_TERMS_DERIVED && has_t && has_h) {
+        atomicAdd(&a.ocnt64[t], 1ull);
     } else if (P.ocnt_mode == OCNT_HIST && has_h) {
         if (LDS) atomicAdd(&a.ocnt32[slot], 1u); else atomicAdd(&a.ocnt64[slot], 1ull);
     }
@@ -218,6 +220,11 @@ __device__ __forceinline__ void update_doc(const CollectParams& P, const Acc& a,
 // Wave-level pre-aggregation for a cell shared by the whole wave (time-sorted data without a terms dimension):
 // one LDS atomic per quantity per wave instead of 256 conflicting ones.
 __device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
@@ -344,6 +351,14 @@ template <int MET>
 __device__ void flush_window(const CollectParams& P, const Acc& s, uint32_t T, uint32_t W, uint32_t win0) {
     __syncthreads();
     const uint32_t C = T * W;
+    if (P.ocnt_mode == OCNT_TERMS_DERIVED) {  // per-term totals of this window (one atomic per term)
+        for (uint32_t t = threadIdx.x; t < T; t += kWG) {
+            uint32_t tot = 0;
+            for (uint32_t l = 0; l < W; ++l) tot += s.cnt32[l * T + t];
+            if (tot) atomicAdd(&P.g_ocnt[t], (unsigned long long)tot);
+        }
+        __syncthreads();
+    }
     for (uint32_t c = threadIdx.x; c < C; c += kWG) {
         const uint32_t n = s.cnt32[c];
         if (n == 0) continue;
@@ -404,7 +419,8 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
         if (MET > 0) s.sum = (double*)carve(sizeof(double) * C);
         if (MET >= 2) { s.mn = (unsigned long long*)carve(8 * C); s.mx = (unsigned long long*)carve(8 * C); }
         if (MET >= 3) s.sq = (double*)carve(sizeof(double) * C);
-        if (P.ocnt_mode != OCNT_NONE) s.ocnt32 = (uint32_t*)carve(sizeof(uint32_t) * (P.ocnt_mode == OCNT_TERMS ? T : W));
+        if (P.ocnt_mode == OCNT_TERMS || P.ocnt_mode == OCNT_HIST)
+            s.ocnt32 = (uint32_t*)carve(sizeof(uint32_t) * (P.ocnt_mode == OCNT_TERMS ? T : W));
         for (uint32_t c = threadIdx.x; c < C; c += kWG) {
             s.cnt32[c] = 0;
             if (P.vcnt_mode) s.vcnt32[c] = 0;
@@ -412,7 +428,7 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
             if (MET >= 2) { s.mn[c] = kMinInit; s.mx[c] = kMaxInit; }
             if (MET >= 3) s.sq[c] = 0.0;
         }
-        if (P.ocnt_mode != OCNT_NONE)
+        if (P.ocnt_mode == OCNT_TERMS || P.ocnt_mode == OCNT_HIST)
             for (uint32_t c = threadIdx.x; c < (P.ocnt_mode == OCNT_TERMS ? T : W); c += kWG) s.ocnt32[c] = 0;
         __syncthreads();
     }
@@ -532,61 +548,100 @@ size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocn
 // ------------------------------------------------------------------------------------------------------------
 // HLL++ (K8)
 // ------------------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void hll_kernel(HllParams P) {
+// hashes of 4 consecutive docs (MurmurHash3Values.Long/Double: mix64; Bytes/ordinals: murmur3 h1 per term)
+__device__ __forceinline__ uint32_t hll_hash4(const HllParams& P, uint32_t i0, uint64_t hv[4]) {
+    uint32_t ok = 0xF;
+    if (i0 + 4 > P.n_docs) ok = (1u << (P.n_docs - i0)) - 1u;
+    if (P.accept) ok &= bits4(P.accept, i0);
+    for (int k = 0; k < P.npred; ++k) ok &= eval_pred(P.pred[k], i0);
+    if (P.kind == HLL_ORD) {
+        uint32_t o[4];
+        load_u32x4((const uint32_t*)P.col, i0, o);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool valid = o[j] != kMissingOrd && o[j] < P.n_ords;
+            if (!valid) ok &= ~(1u << j);
+            hv[j] = valid ? P.ord_hash[o[j]] : 0;
+        }
+    } else {
+        int64_t v[4];
+        load_i64x4((const int64_t*)P.col, i0, v);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint64_t bits = (uint64_t)v[j];
+            if (P.kind == HLL_F64) {  // doubleToLongBits canonicalises NaN
+                const double x = bits_dbl(bits);
+                if (x != x) bits = 0x7ff8000000000000ULL;
+            }
+            hv[j] = mix64(bits);
+        }
+        if (P.present) ok &= bits4(P.present, i0);
+    }
+    return ok;
+}
+
+// pass 1: HLL registers (max runLen per index).  Registers only grow, so a stale read-check costs at most an extra
+// atomic; after warm-up almost every doc is a read that finds a register already >= its run length.
+__global__ __launch_bounds__(256) void hll_registers_kernel(HllParams P) {
     const uint32_t gsz = gridDim.x * blockDim.x;
     for (uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < P.n_docs; i0 += gsz * 4) {
-        // check the linear-counting overflow flag once per 4 docs (relaxed agent-scope load: sees other XCDs)
-        const bool lc_live = __hip_atomic_load(P.lc_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= P.lc_threshold;
         uint64_t hv[4];
-        uint32_t ok = 0xF;
-        if (i0 + 4 > P.n_docs) ok = (1u << (P.n_docs - i0)) - 1u;
-        if (P.accept) ok &= bits4(P.accept, i0);
-        for (int k = 0; k < P.npred; ++k) ok &= eval_pred(P.pred[k], i0);
-        if (P.kind == HLL_ORD) {
-            uint32_t o[4];
-            load_u32x4((const uint32_t*)P.col, i0, o);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const bool valid = o[j] != kMissingOrd && o[j] < P.n_ords;
-                if (!valid) ok &= ~(1u << j);
-                hv[j] = valid ? P.ord_hash[o[j]] : 0;
-            }
-        } else {
-            int64_t v[4];
-            load_i64x4((const int64_t*)P.col, i0, v);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                uint64_t bits = (uint64_t)v[j];
-                if (P.kind == HLL_F64) {  // doubleToLongBits canonicalises NaN
-                    const double x = bits_dbl(bits);
-                    if (x != x) bits = 0x7ff8000000000000ULL;
-                }
-                hv[j] = mix64(bits);
-            }
-            if (P.present) ok &= bits4(P.present, i0);
-        }
+        const uint32_t ok = hll_hash4(P, i0, hv);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             if (!((ok >> j) & 1)) continue;
-            const uint64_t h = hv[j];
-            const uint32_t idx = hll_index(h, P.p);
-            const uint32_t rl = hll_run_len(h, P.p);
+            const uint32_t idx = hll_index(hv[j], P.p);
+            const uint32_t rl = hll_run_len(hv[j], P.p);
             if (rl > P.regs[idx]) atomicMax(&P.regs[idx], rl);
-            if (lc_live) {
-                const uint32_t enc = hll_encode(h, P.p);
-                uint32_t slot = (uint32_t)(mix64(enc) & P.lc_mask);
-                for (uint32_t probe = 0; probe <= P.lc_mask; ++probe) {
-                    const uint32_t cur = P.lc_set[slot];
-                    if (cur == enc) break;
-                    if (cur == 0) {
-                        const uint32_t prev = atomicCAS(&P.lc_set[slot], 0u, enc);
-                        if (prev == 0) { atomicAdd(P.lc_count, 1u); break; }
-                        if (prev == enc) break;
-                    }
-                    slot = (slot + 1) & P.lc_mask;
+        }
+    }
+}
+
+// number of non-zero registers: a lower bound on the number of distinct encoded hashes (distinct register indices
+// come from distinct encodeHash values), so nonzero > threshold proves the reference ends in HYPERLOGLOG mode.
+__global__ __launch_bounds__(1024) void hll_nonzero_kernel(const unsigned int* regs, uint32_t m, unsigned int* out) {
+    uint32_t n = 0;
+    for (uint32_t i = threadIdx.x; i < m; i += 1024) n += regs[i] != 0;
+    __shared__ uint32_t part[16];
+    n = wave_sum_u32(n);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = n;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < 16; ++w) t += part[w];
+        *out = t;
+    }
+}
+
+// pass 2 (only while nonzero <= threshold): the exact LINEAR_COUNTING set of encodeHash values.  Open addressing,
+// probes bounded by threshold+1 (a longer run proves > threshold distinct values), stops once the count passes
+// the threshold.  Final mode = LC iff count <= threshold, exactly as Hashset.add/upgradeToHll decide.
+__global__ __launch_bounds__(256) void hll_lc_kernel(HllParams P) {
+    if (*P.nonzero > P.lc_threshold) return;  // already proven HYPERLOGLOG
+    const uint32_t gsz = gridDim.x * blockDim.x;
+    for (uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < P.n_docs; i0 += gsz * 4) {
+        if (__hip_atomic_load(P.lc_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > P.lc_threshold) return;
+        uint64_t hv[4];
+        const uint32_t ok = hll_hash4(P, i0, hv);
+        uint32_t added = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (!((ok >> j) & 1)) continue;
+            const uint32_t enc = hll_encode(hv[j], P.p);
+            uint32_t slot = (uint32_t)(mix64(enc) & P.lc_mask);
+            for (uint32_t probe = 0; probe <= P.lc_threshold + 1; ++probe) {
+                const uint32_t cur = __hip_atomic_load(&P.lc_set[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (cur == enc) break;
+                if (cur == 0) {
+                    const uint32_t prev = atomicCAS(&P.lc_set[slot], 0u, enc);
+                    if (prev == 0) { ++added; break; }
+                    if (prev == enc) break;
                 }
+                if (probe == P.lc_threshold + 1) { added = P.lc_threshold + 1; break; }  // run longer than the set
+                slot = (slot + 1) & P.lc_mask;
             }
         }
+        if (added) atomicAdd(P.lc_count, added);
     }
 }
 
@@ -594,7 +649,9 @@ void launch_hll(const HllParams& p, hipStream_t st) {
     uint32_t grid = (p.n_docs + 1023) / 1024;
     if (grid > 8192) grid = 8192;
     if (grid == 0) grid = 1;
-    hipLaunchKernelGGL(hll_kernel, dim3(grid), dim3(256), 0, st, p);
+    hipLaunchKernelGGL(hll_registers_kernel, dim3(grid), dim3(256), 0, st, p);
+    hipLaunchKernelGGL(hll_nonzero_kernel, dim3(1), dim3(1024), 0, st, (const unsigned int*)p.regs, 1u << p.p, p.nonzero);
+    hipLaunchKernelGGL(hll_lc_kernel, dim3(grid), dim3(256), 0, st, p);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -636,6 +693,223 @@ void launch_fill_u64(unsigned long long* p, size_t n, unsigned long long v, hipS
     size_t grid = (n + 255) / 256;
     if (grid > 4096) grid = 4096;
     hipLaunchKernelGGL(fill_u64_kernel, dim3((uint32_t)grid), dim3(256), 0, st, p, n, v);
+}
+
+}  // namespace esgpu
+
+// ------------------------------------------------------------------------------------------------------------
+// K1 for high-cardinality terms (valueCount >> LDS): radix-partitioned counting.
+//   pass 1  part_hist     per-workgroup histogram of partitions (ord >> shift) in LDS
+//   pass 2  part_scan     exclusive scan of the [P][G] histogram -> per-(partition, workgroup) write cursors
+//   pass 3  part_scatter  each workgroup re-reads its docs and appends ordinals to its slice of every partition
+//   pass 4  part_count    one workgroup per (partition, <= chunk elements): LDS counters for the 2^shift ordinals of
+//                         the partition, flushed once -> no global atomic contention on hot (Zipf head) terms
+// ------------------------------------------------------------------------------------------------------------
+namespace esgpu {
+
+template <bool SCATTER>
+__global__ __launch_bounds__(kWG) void part_pass_kernel(PartParams P) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t* lds = (uint32_t*)smem;  // [P] histogram (pass 1) or write cursors (pass 3)
+    const uint32_t g = blockIdx.x;
+    for (uint32_t p = threadIdx.x; p < P.P; p += kWG) lds[p] = SCATTER ? P.wg_counts[(size_t)p * P.G + g] : 0u;
+    __syncthreads();
+    const uint32_t b_begin = g * P.blocks_per_wg;
+    const uint32_t b_end = min(b_begin + P.blocks_per_wg, P.n_blocks);
+    for (uint32_t b = b_begin; b < b_end; ++b) {
+        for (int it = 0; it < kItersPerBlock; ++it) {
+            const uint32_t doc0 = b * kBlockDocs + it * kIterDocs + threadIdx.x * kVec;
+            uint32_t ok = 0xF;
+            if (doc0 + 4 > P.n_docs) ok = doc0 >= P.n_docs ? 0u : ((1u << (P.n_docs - doc0)) - 1u);
+            if (P.accept) ok &= bits4(P.accept, doc0);
+            for (int k = 0; k < P.npred; ++k) ok &= eval_pred(P.pred[k], doc0);
+            uint32_t o[4];
+            load_u32x4(P.ord, doc0, o);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (!((ok >> j) & 1) || o[j] >= P.T) continue;  // missing ordinal (0xFFFFFFFF) or out of range
+                const uint32_t part = o[j] >> P.shift;
+                if (SCATTER) {
+                    const uint32_t pos = atomicAdd(&lds[part], 1u);
+                    P.pbuf[pos] = o[j];
+                } else {
+                    atomicAdd(&lds[part], 1u);
+                }
+            }
+        }
+    }
+    if (!SCATTER) {
+        __syncthreads();
+        for (uint32_t p = threadIdx.x; p < P.P; p += kWG) P.wg_counts[(size_t)p * P.G + g] = lds[p];
+    }
+}
+
+void launch_part_hist(const PartParams& p, hipStream_t s) {
+    hipLaunchKernelGGL((part_pass_kernel<false>), dim3(p.G), dim3(kWG), (size_t)p.P * 4, s, p);
+}
+void launch_part_scatter(const PartParams& p, hipStream_t s) {
+    hipLaunchKernelGGL((part_pass_kernel<true>), dim3(p.G), dim3(kWG), (size_t)p.P * 4, s, p);
+}
+
+// exclusive scan of wg_counts[P*G] (partition-major) in place; part_begin[p] = offset of (p, g = 0), [P] = total
+__global__ __launch_bounds__(1024) void part_scan_kernel(PartParams P) {
+    const size_t n = (size_t)P.P * P.G;
+    const size_t per = (n + 1023) / 1024;
+    const size_t b = threadIdx.x * per, e = min(b + per, n);
+    uint32_t local = 0;
+    for (size_t i = b; i < e; ++i) local += P.wg_counts[i];
+    __shared__ uint32_t sums[1024];
+    sums[threadIdx.x] = local;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan of the 1024 partial sums
+        const uint32_t v = threadIdx.x >= (unsigned)off ? sums[threadIdx.x - off] : 0u;
+        __syncthreads();
+        sums[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = threadIdx.x ? sums[threadIdx.x - 1] : 0u;
+    for (size_t i = b; i < e; ++i) {
+        const uint32_t c = P.wg_counts[i];
+        P.wg_counts[i] = run;
+        if (i % P.G == 0) P.part_begin[i / P.G] = run;
+        run += c;
+    }
+    if (threadIdx.x == 1023) P.part_begin[P.P] = sums[1023];
+}
+
+void launch_part_scan(const PartParams& p, hipStream_t s) {
+    hipLaunchKernelGGL(part_scan_kernel, dim3(1), dim3(1024), 0, s, p);
+}
+
+// item = {partition, begin, end, single}: count pbuf[begin, end) into the partition's 2^shift LDS counters
+__global__ __launch_bounds__(kWG) void part_count_kernel(PartParams P, const uint32_t* items) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t* cnt = (uint32_t*)smem;
+    const uint32_t S = 1u << P.shift;
+    const uint32_t part = items[blockIdx.x * 4 + 0];
+    const uint32_t begin = items[blockIdx.x * 4 + 1], end = items[blockIdx.x * 4 + 2];
+    const bool single = items[blockIdx.x * 4 + 3] != 0;
+    for (uint32_t i = threadIdx.x; i < S; i += kWG) cnt[i] = 0;
+    __syncthreads();
+    const uint32_t base = part << P.shift;
+    uint32_t i = begin + threadIdx.x;
+    for (; i + 3 * kWG < end; i += 4 * kWG) {  // 4 independent loads in flight per thread
+        const uint32_t a = P.pbuf[i], b = P.pbuf[i + kWG], c = P.pbuf[i + 2 * kWG], d = P.pbuf[i + 3 * kWG];
+        atomicAdd(&cnt[a - base], 1u);
+        atomicAdd(&cnt[b - base], 1u);
+        atomicAdd(&cnt[c - base], 1u);
+        atomicAdd(&cnt[d - base], 1u);
+    }
+    for (; i < end; i += kWG) atomicAdd(&cnt[P.pbuf[i] - base], 1u);
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < S; j += kWG) {
+        const uint32_t n = cnt[j];
+        if (n == 0 || base + j >= P.T) continue;
+        if (single) P.counts[base + j] += n;  // the only writer of this partition in this launch
+        else atomicAdd(&P.counts[base + j], (unsigned long long)n);
+    }
+}
+
+void launch_part_count(const PartParams& p, uint32_t n_items, const uint32_t* items, hipStream_t s) {
+    if (n_items == 0) return;
+    hipLaunchKernelGGL(part_count_kernel, dim3(n_items), dim3(kWG), (size_t)4 << p.shift, s, p, items);
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// K3: top shard_size of a count vector on the GPU (replaces BucketPriorityQueue over valueCount ordinals).
+// A candidate's key orders exactly like InternalOrder's comparator with the _term asc tie-break (larger = better);
+// key 0 = no candidate.  Pass 1: each workgroup keeps its best k keys (bitonic sort of 4096-key chunks in LDS +
+// bitonic merge with the running best); pass 2: one workgroup merges the candidates.
+// ------------------------------------------------------------------------------------------------------------
+__host__ __device__ __forceinline__ unsigned long long make_topk_key(int order, unsigned long long count, uint32_t ord) {
+    const unsigned long long flag = 1ull << 63;
+    switch (order) {
+        case 0: return flag | (count << 32) | (0xFFFFFFFFull - ord);                  // _count desc, _term asc
+        case 1: return flag | ((0x7FFFFFFFull - count) << 32) | (0xFFFFFFFFull - ord);  // _count asc, _term asc
+        case 2: return flag | (0xFFFFFFFFull - ord);                                  // _term asc
+        default: return flag | (unsigned long long)ord;                                // _term desc
+    }
+}
+uint64_t topk_key(int order, uint64_t count, uint32_t ord) { return make_topk_key(order, count, ord); }
+
+constexpr int kTopkChunk = 4096;
+
+// sort s[0..n) descending, n a power of two, 1024 threads
+__device__ void bitonic_sort_desc(unsigned long long* s, uint32_t n) {
+    for (uint32_t size = 2; size <= n; size <<= 1) {
+        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            __syncthreads();
+            for (uint32_t t = threadIdx.x; t < n / 2; t += 1024) {
+                const uint32_t i = 2 * t - (t & (stride - 1));
+                const uint32_t j = i + stride;
+                const bool desc = (i & size) == 0;
+                const unsigned long long a = s[i], b = s[j];
+                if ((a < b) == desc) { s[i] = b; s[j] = a; }
+            }
+        }
+    }
+    __syncthreads();
+}
+// s[0..n) holds a bitonic sequence; merge it into descending order
+__device__ void bitonic_merge_desc(unsigned long long* s, uint32_t n) {
+    for (uint32_t stride = n >> 1; stride > 0; stride >>= 1) {
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < n / 2; t += 1024) {
+            const uint32_t i = 2 * t - (t & (stride - 1));
+            const uint32_t j = i + stride;
+            const unsigned long long a = s[i], b = s[j];
+            if (a < b) { s[i] = b; s[j] = a; }
+        }
+    }
+    __syncthreads();
+}
+
+template <bool FROM_COUNTS>
+__global__ __launch_bounds__(1024) void topk_kernel(TopkParams P, const unsigned long long* src, uint32_t n, uint32_t per_wg,
+                                                    unsigned long long* out) {
+    __shared__ unsigned long long chunk[kTopkChunk];
+    __shared__ unsigned long long best[2 * kTopkMax];
+    uint32_t kp = 1;
+    while (kp < P.k) kp <<= 1;
+    for (uint32_t i = threadIdx.x; i < kp; i += 1024) best[i] = 0;
+    const uint32_t b = blockIdx.x * per_wg, e = min(b + per_wg, n);
+    unsigned long long sum = 0;
+    for (uint32_t c0 = b; c0 < e; c0 += kTopkChunk) {
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < kTopkChunk; t += 1024) {
+            const uint32_t i = c0 + t;
+            unsigned long long key = 0;
+            if (i < e) {
+                if (FROM_COUNTS) {
+                    const unsigned long long c = src[i];
+                    sum += c;
+                    const bool eligible = !(P.min_doc_count > 0 && c == 0) && (long long)c >= P.shard_min_doc_count;
+                    key = eligible ? make_topk_key(P.order, c, i) : 0ull;
+                } else {
+                    key = src[i];
+                }
+            }
+            chunk[t] = key;
+        }
+        bitonic_sort_desc(chunk, kTopkChunk);
+        // best (desc) ++ reverse(chunk[0..kp)) is bitonic; merge and keep the top kp
+        for (uint32_t t = threadIdx.x; t < kp; t += 1024) best[kp + t] = chunk[kp - 1 - t];
+        bitonic_merge_desc(best, 2 * kp);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < P.k; i += 1024) out[(size_t)blockIdx.x * P.k + i] = best[i];
+    if (FROM_COUNTS) {
+        sum = wave_sum_u64(sum);
+        if ((threadIdx.x & 63) == 0 && sum) atomicAdd(P.out_sum, sum);
+    }
+}
+
+void launch_topk(const TopkParams& p, hipStream_t s) {
+    const uint32_t per1 = (uint32_t)(((uint64_t)p.T + p.n_wg - 1) / p.n_wg);
+    hipLaunchKernelGGL((topk_kernel<true>), dim3(p.n_wg), dim3(1024), 0, s, p, p.counts, p.T, per1, p.cand);
+    const uint32_t nc = p.n_wg * p.k;
+    hipLaunchKernelGGL((topk_kernel<false>), dim3(1), dim3(1024), 0, s, p, (const unsigned long long*)p.cand, nc, nc,
+                       p.out_keys);
 }
 
 }  // namespace esgpu

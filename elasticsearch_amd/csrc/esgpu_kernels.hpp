@@ -37,7 +37,10 @@ struct PredDev {
     double dlo, dhi;   // F64_RANGE with include flags
 };
 
-enum OcntMode : int32_t { OCNT_NONE = 0, OCNT_TERMS = 1, OCNT_HIST = 2 };
+// separate outer-level doc counts: TERMS / HIST = counted per doc (the inner column has missing values);
+// TERMS_DERIVED = terms outer over a dense histogram column: the per-term totals are summed from the LDS window at
+// flush time (no per-doc cost) and counted per doc only on the global-atomic path.
+enum OcntMode : int32_t { OCNT_NONE = 0, OCNT_TERMS = 1, OCNT_HIST = 2, OCNT_TERMS_DERIVED = 3 };
 
 struct CollectParams {
     uint32_t n_docs, n_blocks, blocks_per_wg;
@@ -90,6 +93,7 @@ struct HllParams {
     unsigned int* regs;         // 2^p u32 registers
     unsigned int* lc_set;       // open-addressing set of encoded hashes (0 = empty)
     unsigned int* lc_count;
+    unsigned int* nonzero;      // written by the register pass: registers != 0
     uint32_t lc_mask;
     uint32_t lc_threshold;
 };
@@ -111,5 +115,46 @@ void launch_hll(const HllParams& p, hipStream_t s);
 void launch_term_totals(const unsigned long long* cnt, uint32_t H, uint32_t T, unsigned long long* out, hipStream_t s);
 void launch_gather_rows(const GatherParams& p, hipStream_t s);
 void launch_fill_u64(unsigned long long* p, size_t n, unsigned long long v, hipStream_t s);
+
+}  // namespace esgpu
+
+namespace esgpu {
+
+// ---- high-cardinality terms: radix-partitioned counting (T ordinals >> LDS) ----
+struct PartParams {
+    uint32_t n_docs, n_blocks, blocks_per_wg, G;   // G = workgroups of the histogram / scatter passes
+    const uint32_t* ord;
+    uint32_t T;
+    uint32_t shift;          // partition of an ordinal = ord >> shift
+    uint32_t P;              // number of partitions
+    int32_t npred;
+    PredDev pred[4];
+    const uint64_t* accept;
+    uint32_t* wg_counts;     // [P][G] docs of partition p seen by workgroup g (pass 1), exclusive offsets after the scan
+    uint32_t* part_begin;    // [P + 1] start of each partition in pbuf
+    uint32_t* pbuf;          // partitioned ordinals
+    unsigned long long* counts;  // [T] output doc counts
+    uint32_t chunk;          // max elements of one partition handled by one counting workgroup
+};
+void launch_part_hist(const PartParams& p, hipStream_t s);
+void launch_part_scan(const PartParams& p, hipStream_t s);
+void launch_part_scatter(const PartParams& p, hipStream_t s);
+void launch_part_count(const PartParams& p, uint32_t n_items, const uint32_t* items, hipStream_t s);
+
+// ---- GPU top-k over a count vector (BucketPriorityQueue replacement for large T) ----
+struct TopkParams {
+    const unsigned long long* counts;
+    uint32_t T;
+    int32_t order;           // ESGPU_ORDER_COUNT_DESC / COUNT_ASC / TERM_ASC / TERM_DESC
+    int64_t min_doc_count, shard_min_doc_count;
+    uint32_t k;              // <= kTopkMax
+    unsigned long long* cand;    // [n_wg][k] candidate keys from pass 1
+    uint32_t n_wg;
+    unsigned long long* out_keys;    // [k] winners (0 = none), best first
+    unsigned long long* out_sum;     // [1] sum of counts over min_doc_count-eligible terms
+};
+constexpr uint32_t kTopkMax = 1024;
+void launch_topk(const TopkParams& p, hipStream_t s);
+uint64_t topk_key(int order, uint64_t count, uint32_t ord);   // host mirror of the device key (for tests)
 
 }  // namespace esgpu

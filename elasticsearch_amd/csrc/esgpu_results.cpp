@@ -234,8 +234,17 @@ std::vector<RAgg> reduce_lists(const std::vector<const std::vector<RAgg>*>& list
 
 static RAgg reduce_one(const std::vector<const RAgg*>& aggs) {
     const RAgg& first = *aggs[0];
-    RAgg r = first;
-    r.buckets.clear();
+    RAgg r;  // header of the first aggregation (InternalX carries its request parameters); buckets rebuilt below
+    r.type = first.type; r.order = first.order; r.name = first.name;
+    r.doc_count_error = first.doc_count_error; r.other_doc_count = first.other_doc_count;
+    r.required_size = first.required_size; r.shard_size = first.shard_size; r.min_doc_count = first.min_doc_count;
+    r.show_err = first.show_err; r.keyed = first.keyed;
+    r.has_empty_info = first.has_empty_info; r.date_unit = first.date_unit; r.interval = first.interval;
+    r.offset = first.offset; r.has_bmin = first.has_bmin; r.has_bmax = first.has_bmax; r.bmin = first.bmin; r.bmax = first.bmax;
+    r.empty_subs = first.empty_subs;
+    r.count = first.count; r.sum = first.sum; r.min = first.min; r.max = first.max; r.sumsq = first.sumsq;
+    r.sigma = first.sigma;
+    r.hll_present = first.hll_present; r.precision = first.precision; r.hll_mode = first.hll_mode;
     switch (first.type) {
         case ESGPU_AGG_TERMS: {
             int64_t sumErr = 0, other = 0;

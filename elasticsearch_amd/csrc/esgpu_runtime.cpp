@@ -553,6 +553,41 @@ struct Pipeline {
     bool any_value = false;
     // the segment the dictionary comes from (terms keys)
     const DevColumn* ord_col = nullptr;
+    // timing of this pipeline's collect launch on the plan stream
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    bool timed = false;
+    uint64_t occ_key = ~0ull;   // cached occupancy of the last launch configuration
+    int occ = 1;
+};
+
+// pinned host staging buffer (D2H of build results without a pageable bounce)
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf&) = delete;
+    PinnedBuf& operator=(const PinnedBuf&) = delete;
+    ~PinnedBuf() { if (p) (void)hipHostFree(p); }
+    void* ensure(size_t n) {
+        if (n <= bytes) return p;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+        HIPX(hipHostMalloc(&p, n, hipHostMallocDefault));
+        bytes = n;
+        return p;
+    }
+    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+// device scratch that only grows: no hipMalloc/hipFree (and their implicit syncs) on the per-request path
+struct Scratch {
+    DevBuf buf;
+    void* ensure(esgpu_ctx* c, size_t n) {
+        if (n > buf.bytes) buf.alloc(c, n + n / 4);
+        return buf.p;
+    }
+    template <class T> T* as() const { return buf.as<T>(); }
 };
 
 struct esgpu_plan {
@@ -567,8 +602,13 @@ struct esgpu_plan {
     double last_ms = 0;
     uint64_t last_bytes = 0;
     int32_t last_path = 0;
-    std::vector<const DevColumn*> dict_cols;  // keep dictionaries addressable after segment destroy: copy terms at build
-    std::map<std::string, std::vector<std::string>> term_cache;
+    std::map<std::string, std::vector<std::string>> term_cache;  // terms reachable after the segment is destroyed
+    // per-request scratch, reused across requests
+    Scratch s_accept, s_tcnt, s_rows, s_dst[6];
+    Scratch s_wgc, s_pbeg, s_pbuf, s_items, s_cand, s_keys;  // partitioned counting + GPU top-k
+    PinnedBuf h_pbeg, h_items, h_keys;
+    hipEvent_t ev_mid = nullptr;
+    PinnedBuf h_tcnt, h_rows, h_dst[6];
 };
 
 static int metric_level(int t) { return t == ESGPU_AGG_AVG ? 1 : t == ESGPU_AGG_STATS ? 2 : 3; }
@@ -692,6 +732,11 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
         HIPX(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
         HIPX(hipEventCreate(&p->ev0));
         HIPX(hipEventCreate(&p->ev1));
+        HIPX(hipEventCreateWithFlags(&p->ev_mid, hipEventDisableTiming));
+        for (Pipeline& pl : p->pipes) {
+            HIPX(hipEventCreate(&pl.e0));
+            HIPX(hipEventCreate(&pl.e1));
+        }
         *out = p.release();
     });
 }
@@ -702,7 +747,7 @@ static void alloc_grid(esgpu_plan* p, Pipeline& pl) {
     pl.g_cnt.alloc(c, cells * 8);
     HIPX(hipMemsetAsync(pl.g_cnt.p, 0, cells * 8, p->stream));
     if (pl.ocnt_mode != OCNT_NONE) {
-        const size_t n = pl.ocnt_mode == OCNT_TERMS ? pl.T : pl.H;
+        const size_t n = pl.ocnt_mode == OCNT_HIST ? pl.H : pl.T;
         pl.g_ocnt.alloc(c, n * 8);
         HIPX(hipMemsetAsync(pl.g_ocnt.p, 0, n * 8, p->stream));
     }
@@ -751,7 +796,7 @@ static void grow_keys(esgpu_plan* p, Pipeline& pl, int64_t kmin, int64_t kmax) {
     cp(pl.g_max, old.g_max, row);
     cp(pl.g_sq, old.g_sq, row);
     if (pl.ocnt_mode == OCNT_HIST) cp(pl.g_ocnt, old.g_ocnt, 8);
-    if (pl.ocnt_mode == OCNT_TERMS && old.g_ocnt.p)
+    if ((pl.ocnt_mode == OCNT_TERMS || pl.ocnt_mode == OCNT_TERMS_DERIVED) && old.g_ocnt.p)
         HIPX(hipMemcpyAsync(pl.g_ocnt.p, old.g_ocnt.p, (size_t)pl.T * 8, hipMemcpyDeviceToDevice, p->stream));
     HIPX(hipStreamSynchronize(p->stream));
 }
@@ -807,6 +852,67 @@ static void set_preds(esgpu_plan* p, const esgpu_segment* s, PredDev* out, int32
     }
 }
 
+// K1 for valueCount >> LDS (e.g. 10M url ordinals): radix-partitioned counting instead of global atomics, which
+// serialise on the Zipf head terms.  Reads the ordinal column twice and the partitioned copy once (12 B/doc of
+// traffic for a 4 B/doc algorithmic stream); see DESIGN.md.
+static bool collect_partitioned(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const DevColumn* oc,
+                                const uint64_t* d_accept, const PredDev* pred, int npred) {
+    esgpu_ctx* c = p->ctx;
+    hipStream_t st = p->stream;
+    PartParams Q{};
+    Q.n_docs = s->max_doc;
+    Q.n_blocks = s->n_pad / kBlockDocs;
+    const uint32_t target = (uint32_t)c->cus * 2;
+    Q.blocks_per_wg = std::max(1u, (Q.n_blocks + target - 1) / target);
+    Q.G = (Q.n_blocks + Q.blocks_per_wg - 1) / Q.blocks_per_wg;
+    Q.ord = oc->values.as<uint32_t>();
+    Q.T = pl.T;
+    Q.shift = 14;  // 16384 ordinals per partition: 64 KB of LDS counters in the counting pass
+    Q.P = (uint32_t)(((uint64_t)pl.T + (1u << Q.shift) - 1) >> Q.shift);
+    require(Q.P <= 16384, ESGPU_ERR_UNSUPPORTED, "more than 2^28 ordinals");
+    Q.npred = npred;
+    for (int k = 0; k < npred; ++k) Q.pred[k] = pred[k];
+    Q.accept = d_accept;
+    Q.wg_counts = (uint32_t*)p->s_wgc.ensure(c, (size_t)Q.P * Q.G * 4);
+    Q.part_begin = (uint32_t*)p->s_pbeg.ensure(c, (size_t)(Q.P + 1) * 4);
+    Q.pbuf = (uint32_t*)p->s_pbuf.ensure(c, std::max<size_t>(s->max_doc, 1) * 4);
+    Q.counts = pl.g_cnt.as<unsigned long long>();
+    Q.chunk = 1u << 20;
+    HIPX(hipEventRecord(pl.e0, st));
+    launch_part_hist(Q, st);
+    launch_part_scan(Q, st);
+    uint32_t* hb = (uint32_t*)p->h_pbeg.ensure((size_t)(Q.P + 1) * 4);
+    HIPX(hipMemcpyAsync(hb, Q.part_begin, (size_t)(Q.P + 1) * 4, hipMemcpyDeviceToHost, st));
+    HIPX(hipEventRecord(p->ev_mid, st));
+    launch_part_scatter(Q, st);
+    HIPX(hipGetLastError());
+    HIPX(hipEventSynchronize(p->ev_mid));  // the scatter keeps running while the work items are built
+    std::vector<uint32_t> items;
+    for (uint32_t q = 0; q < Q.P; ++q) {
+        const uint32_t b = hb[q], e = hb[q + 1];
+        if (b == e) continue;
+        const uint32_t nch = (e - b + Q.chunk - 1) / Q.chunk;
+        for (uint32_t k = 0; k < nch; ++k) {
+            items.push_back(q);
+            items.push_back(b + k * Q.chunk);
+            items.push_back(std::min(e, b + (k + 1) * Q.chunk));
+            items.push_back(nch == 1);
+        }
+    }
+    const uint32_t n_items = (uint32_t)(items.size() / 4);
+    if (n_items) {
+        uint32_t* hi = (uint32_t*)p->h_items.ensure(items.size() * 4);
+        std::memcpy(hi, items.data(), items.size() * 4);
+        uint32_t* di = (uint32_t*)p->s_items.ensure(c, items.size() * 4);
+        HIPX(hipMemcpyAsync(di, hi, items.size() * 4, hipMemcpyHostToDevice, st));
+        launch_part_count(Q, n_items, di, st);
+        HIPX(hipGetLastError());
+    }
+    HIPX(hipEventRecord(pl.e1, st));
+    p->last_path = 4;
+    return true;
+}
+
 static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
     const bool ORD = pl.term_spec >= 0, HIST = pl.hist_spec >= 0;
     const DevColumn* oc = ORD ? s->col(pl.ord_field.c_str()) : nullptr;
@@ -849,6 +955,7 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
             const bool terms_outer = pl.outer == pl.term_spec;
             const bool inner_sparse = terms_outer ? (hc->present.p != nullptr) : true;  // ords may be missing
             if (inner_sparse) pl.ocnt_mode = terms_outer ? OCNT_TERMS : OCNT_HIST;
+            else pl.ocnt_mode = OCNT_TERMS_DERIVED;
         }
         pl.ord_col = oc;
         alloc_grid(p, pl);
@@ -913,21 +1020,30 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
         }
     }
     P.W = W;
+    if (!P.lds_mode && ORD && !HIST && met_launch == 0 && !pl.vcnt_mode && pl.ocnt_mode == OCNT_NONE) {
+        p->last_bytes += bytes_per_doc * (uint64_t)s->max_doc + (d_accept ? ((uint64_t)s->max_doc + 7) / 8 : 0);
+        return collect_partitioned(p, pl, s, oc, d_accept, P.pred, P.npred);
+    }
     const uint64_t span = (uint64_t)pl.interval * (uint64_t)W;
     P.fast32 = pl.interval < (1ll << 32) && span < (1ull << 32);
     if (P.fast32) {
         const MagicU32 mg = make_magic((uint32_t)pl.interval);
         P.mg_m = mg.m; P.mg_s1 = mg.s1; P.mg_s2 = mg.s2;
     }
-    const uint32_t wg_per_cu = (uint32_t)std::max(1, collect_occupancy(ORD, HIST, met_launch, lds));
+    const uint64_t occ_key = ((uint64_t)lds << 8) | ((uint64_t)met_launch << 2) | (ORD ? 2 : 0) | (HIST ? 1 : 0);
+    if (pl.occ_key != occ_key) {
+        pl.occ = std::max(1, collect_occupancy(ORD, HIST, met_launch, lds));
+        pl.occ_key = occ_key;
+    }
+    const uint32_t wg_per_cu = (uint32_t)pl.occ;
     const uint32_t target = (uint32_t)p->ctx->cus * wg_per_cu;
     const uint32_t bpw = (P.n_blocks + target - 1) / target;
     P.blocks_per_wg = std::max(1u, bpw);
     const uint32_t grid = (P.n_blocks + P.blocks_per_wg - 1) / P.blocks_per_wg;
-    HIPX(hipEventRecord(p->ev0, p->stream));
+    HIPX(hipEventRecord(pl.e0, p->stream));
     launch_collect(P, ORD, HIST, met_launch, grid, lds, p->stream);
     HIPX(hipGetLastError());
-    HIPX(hipEventRecord(p->ev1, p->stream));
+    HIPX(hipEventRecord(pl.e1, p->stream));
     p->last_bytes += bytes_per_doc * (uint64_t)s->max_doc + (d_accept ? ((uint64_t)s->max_doc + 7) / 8 : 0);
     p->last_path = P.lds_mode ? (P.windowed ? 2 : 1) : 0;
     return true;
@@ -957,8 +1073,8 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
         pl.regs.alloc(p->ctx, (size_t)m * 4);
         HIPX(hipMemsetAsync(pl.regs.p, 0, (size_t)m * 4, p->stream));
         pl.lc_threshold = (uint32_t)((float)(m / 4) * 0.75f);  // Hashset threshold (HyperLogLogPlusPlus.java:437-440)
-        uint32_t cap = 1024;
-        while (cap < 2 * (pl.lc_threshold + 1)) cap <<= 1;
+        uint32_t cap = 1024;  // load factor <= 1/16 while the set is within the threshold
+        while (cap < 16 * (pl.lc_threshold + 1)) cap <<= 1;
         pl.lc_mask = cap - 1;
         pl.lc_set.alloc(p->ctx, (size_t)cap * 4);
         HIPX(hipMemsetAsync(pl.lc_set.p, 0, (size_t)cap * 4, p->stream));
@@ -985,13 +1101,14 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
     H.regs = pl.regs.as<unsigned int>();
     H.lc_set = pl.lc_set.as<unsigned int>();
     H.lc_count = pl.lc_count.as<unsigned int>();
+    H.nonzero = pl.lc_count.as<unsigned int>() + 1;
     H.lc_mask = pl.lc_mask;
     H.lc_threshold = pl.lc_threshold;
     if (H.n_docs == 0) return false;
-    HIPX(hipEventRecord(p->ev0, p->stream));
+    HIPX(hipEventRecord(pl.e0, p->stream));
     launch_hll(H, p->stream);
     HIPX(hipGetLastError());
-    HIPX(hipEventRecord(p->ev1, p->stream));
+    HIPX(hipEventRecord(pl.e1, p->stream));
     p->last_bytes += bytes_per_doc * (uint64_t)s->max_doc;
     p->last_path = 3;
     return true;
@@ -1003,25 +1120,21 @@ extern "C" int esgpu_plan_collect_segment(esgpu_plan* p, const esgpu_segment* s,
         require(!p->posted, ESGPU_ERR_STATE, "collect after postCollection");
         require(s->ctx == p->ctx, ESGPU_ERR_INVALID, "segment belongs to another device context");
         HIPX(hipSetDevice(p->ctx->device));
-        DevBuf accept;
+        const uint64_t* d_accept = nullptr;
         if (accept_bits) {
-            const size_t words = s->n_pad / 64;
-            accept.alloc(p->ctx, std::max<size_t>(words, 1) * 8);
-            HIPX(hipMemsetAsync(accept.p, 0, std::max<size_t>(words, 1) * 8, p->stream));
-            HIPX(hipMemcpyAsync(accept.p, accept_bits, ((size_t)s->max_doc + 63) / 64 * 8, hipMemcpyHostToDevice, p->stream));
+            const size_t words = std::max<size_t>(s->n_pad / 64, 1);
+            void* a = p->s_accept.ensure(p->ctx, words * 8);
+            HIPX(hipMemsetAsync(a, 0, words * 8, p->stream));
+            HIPX(hipMemcpyAsync(a, accept_bits, ((size_t)s->max_doc + 63) / 64 * 8, hipMemcpyHostToDevice, p->stream));
+            // the caller may reuse its buffer as soon as we return
+            HIPX(hipStreamSynchronize(p->stream));
+            d_accept = (const uint64_t*)a;
         }
         p->last_bytes = 0;
-        float total = 0;
+        p->last_ms = -1;
         for (Pipeline& pl : p->pipes) {
-            const bool launched = pl.kind == 1 ? collect_hll(p, pl, s, accept.as<uint64_t>())
-                                               : collect_grid(p, pl, s, accept.as<uint64_t>());
-            if (!launched) continue;
-            HIPX(hipEventSynchronize(p->ev1));
-            float ms = 0;
-            if (hipEventElapsedTime(&ms, p->ev0, p->ev1) == hipSuccess) total += ms;
+            pl.timed = pl.kind == 1 ? collect_hll(p, pl, s, d_accept) : collect_grid(p, pl, s, d_accept);
         }
-        HIPX(hipStreamSynchronize(p->stream));
-        p->last_ms = total;
         // keep dictionary terms reachable at build time even if the segment is destroyed first
         for (Pipeline& pl : p->pipes) {
             if (pl.term_spec < 0) continue;
@@ -1037,8 +1150,20 @@ extern "C" int esgpu_plan_collect_segment(esgpu_plan* p, const esgpu_segment* s,
     });
 }
 
-extern "C" int esgpu_plan_last_collect_stats(const esgpu_plan* p, double* kernel_ms, uint64_t* bytes, int32_t* path) {
+extern "C" int esgpu_plan_last_collect_stats(const esgpu_plan* cp, double* kernel_ms, uint64_t* bytes, int32_t* path) {
     return guarded([&] {
+        esgpu_plan* p = const_cast<esgpu_plan*>(cp);
+        if (p->last_ms < 0) {  // resolve the HIP events of the last collect (synchronises with it)
+            float total = 0;
+            for (Pipeline& pl : p->pipes) {
+                if (!pl.timed) continue;
+                HIPX(hipEventSynchronize(pl.e1));
+                float ms = 0;
+                HIPX(hipEventElapsedTime(&ms, pl.e0, pl.e1));
+                total += ms;
+            }
+            p->last_ms = total;
+        }
         if (kernel_ms) *kernel_ms = p->last_ms;
         if (bytes) *bytes = p->last_bytes;
         if (path) *path = p->last_path;
@@ -1052,21 +1177,26 @@ extern "C" int esgpu_plan_post_collection(esgpu_plan* p) {
         HIPX(hipStreamSynchronize(p->stream));
         for (Pipeline& pl : p->pipes) {
             if (pl.kind != 1 || !pl.allocated) continue;
-            uint32_t cnt = 0;
-            HIPX(hipMemcpy(&cnt, pl.lc_count.p, 4, hipMemcpyDeviceToHost));
+            // [0] = distinct encoded hashes inserted (LC pass), [1] = non-zero registers (register pass)
+            uint32_t* cnt = (uint32_t*)p->h_tcnt.ensure(16);
+            HIPX(hipMemcpyAsync(cnt, pl.lc_count.p, 8, hipMemcpyDeviceToHost, p->stream));
+            HIPX(hipStreamSynchronize(p->stream));
             const uint32_t m = 1u << pl.p;
-            pl.any_value = cnt > 0;
-            if (cnt <= pl.lc_threshold) {  // LINEAR_COUNTING: the distinct encoded hashes
+            pl.any_value = cnt[0] > 0 || cnt[1] > 0;
+            if (cnt[1] <= pl.lc_threshold && cnt[0] <= pl.lc_threshold) {  // LINEAR_COUNTING: the distinct encoded hashes
                 pl.hll_mode = 0;
-                std::vector<uint32_t> set((size_t)pl.lc_mask + 1);
-                HIPX(hipMemcpy(set.data(), pl.lc_set.p, set.size() * 4, hipMemcpyDeviceToHost));
+                const size_t cap = (size_t)pl.lc_mask + 1;
+                uint32_t* set = (uint32_t*)p->h_dst[0].ensure(cap * 4);
+                HIPX(hipMemcpyAsync(set, pl.lc_set.p, cap * 4, hipMemcpyDeviceToHost, p->stream));
+                HIPX(hipStreamSynchronize(p->stream));
                 pl.h_lc.clear();
-                for (uint32_t v : set) if (v) pl.h_lc.push_back(v);
+                for (size_t i = 0; i < cap; ++i) if (set[i]) pl.h_lc.push_back(set[i]);
                 std::sort(pl.h_lc.begin(), pl.h_lc.end());
             } else {  // HYPERLOGLOG
                 pl.hll_mode = 1;
-                std::vector<uint32_t> r(m);
-                HIPX(hipMemcpy(r.data(), pl.regs.p, (size_t)m * 4, hipMemcpyDeviceToHost));
+                uint32_t* r = (uint32_t*)p->h_dst[0].ensure((size_t)m * 4);
+                HIPX(hipMemcpyAsync(r, pl.regs.p, (size_t)m * 4, hipMemcpyDeviceToHost, p->stream));
+                HIPX(hipStreamSynchronize(p->stream));
                 pl.h_regs.resize(m);
                 for (uint32_t i = 0; i < m; ++i) pl.h_regs[i] = (uint8_t)r[i];
             }
@@ -1132,10 +1262,14 @@ static RAgg terms_base(const esgpu_plan* p, int spec) {
     return r;
 }
 
-// host copies of one grid row set
+// host views (pinned staging buffers of the plan) of one grid row set
 struct HostCells {
-    std::vector<unsigned long long> cnt, vcnt, mn, mx;
-    std::vector<double> sum, sq;
+    const unsigned long long* cnt = nullptr;
+    const unsigned long long* vcnt = nullptr;
+    const unsigned long long* mn = nullptr;
+    const unsigned long long* mx = nullptr;
+    const double* sum = nullptr;
+    const double* sq = nullptr;
 };
 
 static std::vector<RAgg> metric_results(const esgpu_plan* p, const Pipeline& pl, const HostCells& h, size_t c) {
@@ -1167,19 +1301,25 @@ static std::vector<RAgg> empty_metrics(const esgpu_plan* p, const Pipeline& pl) 
     return out;
 }
 
-static void d2h(HostCells& h, const Pipeline& pl, size_t n, const unsigned long long* cnt, const unsigned long long* vcnt,
-                const double* sum, const unsigned long long* mn, const unsigned long long* mx, const double* sq, hipStream_t st) {
-    h.cnt.resize(n);
-    HIPX(hipMemcpyAsync(h.cnt.data(), cnt, n * 8, hipMemcpyDeviceToHost, st));
-    if (pl.vcnt_mode) { h.vcnt.resize(n); HIPX(hipMemcpyAsync(h.vcnt.data(), vcnt, n * 8, hipMemcpyDeviceToHost, st)); }
-    if (pl.met > 0) { h.sum.resize(n); HIPX(hipMemcpyAsync(h.sum.data(), sum, n * 8, hipMemcpyDeviceToHost, st)); }
-    if (pl.met >= 2) {
-        h.mn.resize(n); h.mx.resize(n);
-        HIPX(hipMemcpyAsync(h.mn.data(), mn, n * 8, hipMemcpyDeviceToHost, st));
-        HIPX(hipMemcpyAsync(h.mx.data(), mx, n * 8, hipMemcpyDeviceToHost, st));
+// device cell arrays -> the plan's pinned staging buffers (one stream sync)
+static void d2h(esgpu_plan* p, HostCells& h, const Pipeline& pl, size_t n, const void* cnt, const void* vcnt, const void* sum,
+                const void* mn, const void* mx, const void* sq) {
+    hipStream_t st = p->stream;
+    const void* src[6] = {cnt, pl.vcnt_mode ? vcnt : nullptr, pl.met > 0 ? sum : nullptr, pl.met >= 2 ? mn : nullptr,
+                          pl.met >= 2 ? mx : nullptr, pl.met >= 3 ? sq : nullptr};
+    void* dst[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    for (int a = 0; a < 6; ++a) {
+        if (!src[a]) continue;
+        dst[a] = p->h_dst[a].ensure(std::max<size_t>(n, 1) * 8);
+        HIPX(hipMemcpyAsync(dst[a], src[a], n * 8, hipMemcpyDeviceToHost, st));
     }
-    if (pl.met >= 3) { h.sq.resize(n); HIPX(hipMemcpyAsync(h.sq.data(), sq, n * 8, hipMemcpyDeviceToHost, st)); }
     HIPX(hipStreamSynchronize(st));
+    h.cnt = (const unsigned long long*)dst[0];
+    h.vcnt = (const unsigned long long*)dst[1];
+    h.sum = (const double*)dst[2];
+    h.mn = (const unsigned long long*)dst[3];
+    h.mx = (const unsigned long long*)dst[4];
+    h.sq = (const double*)dst[5];
 }
 
 // GlobalOrdinalsStringTermsAggregator.buildAggregation candidate selection + PQ (:146-208)
@@ -1221,8 +1361,7 @@ static RAgg build_grid(esgpu_plan* p, Pipeline& pl) {
         const SpecNode& n = p->specs[pl.root];
         if (!pl.allocated) return empty_metric(n);
         HostCells h;
-        d2h(h, pl, 1, pl.g_cnt.as<unsigned long long>(), pl.g_vcnt.as<unsigned long long>(), pl.g_sum.as<double>(),
-            pl.g_min.as<unsigned long long>(), pl.g_max.as<unsigned long long>(), pl.g_sq.as<double>(), st);
+        d2h(p, h, pl, 1, pl.g_cnt.p, pl.g_vcnt.p, pl.g_sum.p, pl.g_min.p, pl.g_max.p, pl.g_sq.p);
         return metric_results(p, pl, h, 0)[0];
     }
     const bool terms_outer = pl.outer == pl.term_spec;
@@ -1240,52 +1379,92 @@ static RAgg build_grid(esgpu_plan* p, Pipeline& pl) {
         RAgg r = terms_base(p, pl.outer);
         if (!pl.allocated) return r;  // unmapped: buildEmptyAggregation
         const uint32_t T = pl.T, H = pl.H;
-        // outer doc counts per ordinal
-        std::vector<unsigned long long> tcnt(T);
-        DevBuf tmp;
+        // outer doc counts per ordinal (term_totals over the [H][T] grid unless counted separately)
         const unsigned long long* dcnt = pl.g_cnt.as<unsigned long long>();
-        if (pl.ocnt_mode == OCNT_TERMS) dcnt = pl.g_ocnt.as<unsigned long long>();
+        if (pl.ocnt_mode == OCNT_TERMS || pl.ocnt_mode == OCNT_TERMS_DERIVED) dcnt = pl.g_ocnt.as<unsigned long long>();
         else if (H > 1) {
-            tmp.alloc(p->ctx, (size_t)T * 8);
-            launch_term_totals(pl.g_cnt.as<unsigned long long>(), H, T, tmp.as<unsigned long long>(), st);
+            unsigned long long* tmp = (unsigned long long*)p->s_tcnt.ensure(p->ctx, (size_t)T * 8);
+            launch_term_totals(pl.g_cnt.as<unsigned long long>(), H, T, tmp, st);
             HIPX(hipGetLastError());
-            dcnt = tmp.as<unsigned long long>();
+            dcnt = tmp;
         }
-        HIPX(hipMemcpyAsync(tcnt.data(), dcnt, (size_t)T * 8, hipMemcpyDeviceToHost, st));
-        HIPX(hipStreamSynchronize(st));
         int64_t other = 0;
-        std::vector<TermPick> top = select_terms(tn.s, tcnt.data(), (uint32_t)pl.value_count, &other);
-        r.other_doc_count = other;
+        std::vector<TermPick> top;
+        const uint64_t k_req = std::min<uint64_t>(pl.value_count, (uint64_t)std::max(tn.s.shard_size, 0));
+        const bool count_order = tn.s.order == ESGPU_ORDER_COUNT_DESC || tn.s.order == ESGPU_ORDER_COUNT_ASC;
+        const bool gpu_topk = pl.value_count > 65536 && k_req <= kTopkMax && (H == 1 || count_order);
+        if (gpu_topk) {
+            // K3 on the GPU: only the k winners (and the count total) cross PCIe
+            const uint32_t kk = (uint32_t)std::max<uint64_t>(k_req, 1);
+            TopkParams K{};
+            K.counts = dcnt;
+            K.T = (uint32_t)pl.value_count;
+            K.order = tn.s.order;
+            K.min_doc_count = tn.s.min_doc_count;
+            K.shard_min_doc_count = tn.s.shard_min_doc_count;
+            K.k = kk;
+            K.n_wg = std::min<uint32_t>(512, (K.T + 4095) / 4096);
+            K.cand = (unsigned long long*)p->s_cand.ensure(p->ctx, (size_t)K.n_wg * kk * 8);
+            unsigned long long* dk = (unsigned long long*)p->s_keys.ensure(p->ctx, ((size_t)kk + 1) * 8);
+            K.out_keys = dk;
+            K.out_sum = dk + kk;
+            HIPX(hipMemsetAsync(K.out_sum, 0, 8, st));
+            launch_topk(K, st);
+            HIPX(hipGetLastError());
+            unsigned long long* hk = (unsigned long long*)p->h_keys.ensure(((size_t)kk + 1) * 8);
+            HIPX(hipMemcpyAsync(hk, dk, ((size_t)kk + 1) * 8, hipMemcpyDeviceToHost, st));
+            HIPX(hipStreamSynchronize(st));
+            other = (int64_t)hk[kk];
+            for (uint32_t i = 0; i < (uint32_t)k_req; ++i) {
+                const unsigned long long key = hk[i];
+                if (key == 0) break;
+                TermPick tp;
+                const uint32_t lo = (uint32_t)key;
+                tp.ord = (tn.s.order == ESGPU_ORDER_TERM_DESC) ? lo : 0xFFFFFFFFu - lo;
+                const uint64_t hi = (key >> 32) & 0x7FFFFFFFull;
+                tp.count = tn.s.order == ESGPU_ORDER_COUNT_DESC ? (int64_t)hi
+                         : tn.s.order == ESGPU_ORDER_COUNT_ASC ? (int64_t)(0x7FFFFFFFull - hi) : -1;  // term orders: gathered below
+                top.push_back(tp);
+            }
+        } else {
+            unsigned long long* tcnt = (unsigned long long*)p->h_tcnt.ensure((size_t)T * 8);
+            HIPX(hipMemcpyAsync(tcnt, dcnt, (size_t)T * 8, hipMemcpyDeviceToHost, st));
+            HIPX(hipStreamSynchronize(st));
+            top = select_terms(tn.s, tcnt, (uint32_t)pl.value_count, &other);
+        }
         const uint32_t k = (uint32_t)top.size();
-        // gather the winners' rows [k][H] (GatherParams) and bring them back
+        // gather the winners' rows [k][H] on the GPU and bring back only those
         HostCells h;
         if (k > 0) {
-            std::vector<uint32_t> rows(k);
+            uint32_t* rows = (uint32_t*)p->h_rows.ensure((size_t)k * 4);
             for (uint32_t i = 0; i < k; ++i) rows[i] = top[i].ord;
-            DevBuf drows, dst[6];
-            drows.alloc(p->ctx, (size_t)k * 4);
-            HIPX(hipMemcpyAsync(drows.p, rows.data(), (size_t)k * 4, hipMemcpyHostToDevice, st));
+            void* drows = p->s_rows.ensure(p->ctx, (size_t)k * 4);
+            HIPX(hipMemcpyAsync(drows, rows, (size_t)k * 4, hipMemcpyHostToDevice, st));
             GatherParams G{};
-            G.rows = drows.as<uint32_t>();
+            G.rows = (const uint32_t*)drows;
             G.k = k; G.H = H; G.T = T;
-            const unsigned long long* srcs[6] = {pl.g_cnt.as<unsigned long long>(), pl.g_vcnt.as<unsigned long long>(),
-                                                 (const unsigned long long*)pl.g_sum.p, pl.g_min.as<unsigned long long>(),
-                                                 pl.g_max.as<unsigned long long>(), (const unsigned long long*)pl.g_sq.p};
-            int slot_of_array[6];
+            const void* srcs[6] = {pl.g_cnt.p, pl.vcnt_mode ? pl.g_vcnt.p : nullptr, pl.met > 0 ? pl.g_sum.p : nullptr,
+                                   pl.met >= 2 ? pl.g_min.p : nullptr, pl.met >= 2 ? pl.g_max.p : nullptr,
+                                   pl.met >= 3 ? pl.g_sq.p : nullptr};
+            void* dsts[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
             for (int a = 0; a < 6; ++a) {
-                slot_of_array[a] = -1;
                 if (!srcs[a]) continue;
-                dst[a].alloc(p->ctx, (size_t)k * H * 8);
-                G.src[G.narrays] = srcs[a];
-                G.dst[G.narrays] = dst[a].as<unsigned long long>();
-                slot_of_array[a] = G.narrays++;
+                dsts[a] = p->s_dst[a].ensure(p->ctx, (size_t)k * H * 8);
+                G.src[G.narrays] = (const unsigned long long*)srcs[a];
+                G.dst[G.narrays] = (unsigned long long*)dsts[a];
+                G.narrays++;
             }
             launch_gather_rows(G, st);
             HIPX(hipGetLastError());
-            d2h(h, pl, (size_t)k * H, dst[0].as<unsigned long long>(), dst[1].as<unsigned long long>(), dst[2].as<double>(),
-                dst[3].as<unsigned long long>(), dst[4].as<unsigned long long>(), dst[5].as<double>(), st);
-            (void)slot_of_array;
+            d2h(p, h, pl, (size_t)k * H, dsts[0], dsts[1], dsts[2], dsts[3], dsts[4], dsts[5]);
         }
+        if (gpu_topk) {  // otherDocCount = (sum of all counts) - (sum of the winners' counts)
+            for (uint32_t i = 0; i < k; ++i) {
+                if (top[i].count < 0) top[i].count = (int64_t)h.cnt[i];  // term orders (H == 1): count from the row
+                other -= top[i].count;
+            }
+        }
+        r.other_doc_count = other;
         for (uint32_t i = 0; i < k; ++i) {
             RBucket b;
             b.key = top[i].ord;
@@ -1315,8 +1494,7 @@ static RAgg build_grid(esgpu_plan* p, Pipeline& pl) {
     if (!pl.allocated) return r;
     const uint32_t T = pl.T, H = pl.H;
     HostCells h;
-    d2h(h, pl, (size_t)T * H, pl.g_cnt.as<unsigned long long>(), pl.g_vcnt.as<unsigned long long>(), pl.g_sum.as<double>(),
-        pl.g_min.as<unsigned long long>(), pl.g_max.as<unsigned long long>(), pl.g_sq.as<double>(), st);
+    d2h(p, h, pl, (size_t)T * H, pl.g_cnt.p, pl.g_vcnt.p, pl.g_sum.p, pl.g_min.p, pl.g_max.p, pl.g_sq.p);
     std::vector<unsigned long long> ocnt;
     if (pl.ocnt_mode == OCNT_HIST) {
         ocnt.resize(H);
@@ -1336,7 +1514,7 @@ static RAgg build_grid(esgpu_plan* p, Pipeline& pl) {
             const SpecNode& tn = p->specs[pl.inner];
             RAgg tr = terms_base(p, pl.inner);
             int64_t other = 0;
-            std::vector<TermPick> top = select_terms(tn.s, h.cnt.data() + (size_t)s * T, (uint32_t)pl.value_count, &other);
+            std::vector<TermPick> top = select_terms(tn.s, h.cnt + (size_t)s * T, (uint32_t)pl.value_count, &other);
             tr.other_doc_count = other;
             for (auto& tp : top) {
                 RBucket tb;
@@ -1407,7 +1585,6 @@ extern "C" int esgpu_plan_reset(esgpu_plan* p) {
             if (pl.g_max.p) launch_fill_u64(pl.g_max.as<unsigned long long>(), cells, kMaxInit, p->stream);
             if (pl.g_sq.p) HIPX(hipMemsetAsync(pl.g_sq.p, 0, cells * 8, p->stream));
         }
-        HIPX(hipStreamSynchronize(p->stream));
         p->posted = false;
         p->collected = false;
     });
@@ -1418,7 +1595,12 @@ extern "C" int esgpu_plan_destroy(esgpu_plan* p) {
         if (!p) return;
         (void)hipSetDevice(p->ctx->device);
         (void)hipStreamSynchronize(p->stream);
+        for (Pipeline& pl : p->pipes) {
+            if (pl.e0) (void)hipEventDestroy(pl.e0);
+            if (pl.e1) (void)hipEventDestroy(pl.e1);
+        }
         p->pipes.clear();
+        if (p->ev_mid) (void)hipEventDestroy(p->ev_mid);
         if (p->ev0) (void)hipEventDestroy(p->ev0);
         if (p->ev1) (void)hipEventDestroy(p->ev1);
         if (p->stream) (void)hipStreamDestroy(p->stream);
@@ -1499,6 +1681,8 @@ struct esgpu_comm {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
     hipStream_t stream = nullptr;
+    Scratch dsz, dall, dmine;   // grown on demand, reused across requests
+    PinnedBuf hsz, hall, hmine;
 };
 
 #define NCCLX(expr)                                                                                           \
@@ -1549,26 +1733,29 @@ extern "C" int esgpu_comm_gather_reduce(esgpu_comm* cm, const esgpu_result* loca
         std::string mine;
         serialize(holder_of(local)->aggs, mine);
         // 1) all-gather the record sizes, 2) all-gather fixed-size padded records (shard order == rank order)
-        DevBuf dsz, dall, dmine;
-        dsz.alloc(cm->ctx, (size_t)cm->nranks * 8);
-        const uint64_t my = mine.size();
-        HIPX(hipMemcpy(dsz.as<uint8_t>() + (size_t)cm->rank * 8, &my, 8, hipMemcpyHostToDevice));
-        NCCLX(ncclAllGather(dsz.as<uint8_t>() + (size_t)cm->rank * 8, dsz.p, 8, ncclUint8, cm->comm, cm->stream));
-        std::vector<uint64_t> sizes(cm->nranks);
-        HIPX(hipMemcpyAsync(sizes.data(), dsz.p, (size_t)cm->nranks * 8, hipMemcpyDeviceToHost, cm->stream));
+        const size_t n = (size_t)cm->nranks;
+        uint64_t* hsz = (uint64_t*)cm->hsz.ensure(n * 8);
+        uint8_t* dsz = (uint8_t*)cm->dsz.ensure(cm->ctx, n * 8);
+        hsz[cm->rank] = mine.size();
+        HIPX(hipMemcpyAsync(dsz + (size_t)cm->rank * 8, hsz + cm->rank, 8, hipMemcpyHostToDevice, cm->stream));
+        NCCLX(ncclAllGather(dsz + (size_t)cm->rank * 8, dsz, 8, ncclUint8, cm->comm, cm->stream));
+        HIPX(hipMemcpyAsync(hsz, dsz, n * 8, hipMemcpyDeviceToHost, cm->stream));
         HIPX(hipStreamSynchronize(cm->stream));
-        const uint64_t rec = std::max<uint64_t>(*std::max_element(sizes.begin(), sizes.end()), 8);
-        dmine.alloc(cm->ctx, rec);
-        dall.alloc(cm->ctx, rec * cm->nranks);
-        HIPX(hipMemcpy(dmine.p, mine.data(), mine.size(), hipMemcpyHostToDevice));
-        NCCLX(ncclAllGather(dmine.p, dall.p, rec, ncclUint8, cm->comm, cm->stream));
-        std::vector<uint8_t> all(rec * cm->nranks);
-        HIPX(hipMemcpyAsync(all.data(), dall.p, all.size(), hipMemcpyDeviceToHost, cm->stream));
+        std::vector<uint64_t> sizes(hsz, hsz + n);
+        const uint64_t rec = (std::max<uint64_t>(*std::max_element(sizes.begin(), sizes.end()), 8) + 15) & ~15ull;
+        uint8_t* hmine = (uint8_t*)cm->hmine.ensure(rec);
+        std::memcpy(hmine, mine.data(), mine.size());
+        uint8_t* dmine = (uint8_t*)cm->dmine.ensure(cm->ctx, rec);
+        uint8_t* dall = (uint8_t*)cm->dall.ensure(cm->ctx, rec * n);
+        HIPX(hipMemcpyAsync(dmine, hmine, rec, hipMemcpyHostToDevice, cm->stream));
+        NCCLX(ncclAllGather(dmine, dall, rec, ncclUint8, cm->comm, cm->stream));
+        uint8_t* all = (uint8_t*)cm->hall.ensure(rec * n);
+        HIPX(hipMemcpyAsync(all, dall, rec * n, hipMemcpyDeviceToHost, cm->stream));
         HIPX(hipStreamSynchronize(cm->stream));
         std::vector<std::vector<RAgg>> shards(cm->nranks);
         std::vector<const std::vector<RAgg>*> lists;
         for (int r = 0; r < cm->nranks; ++r) {
-            require(deserialize(all.data() + rec * r, sizes[r], shards[r]), ESGPU_ERR_DEVICE, "corrupt shard record");
+            require(deserialize(all + rec * r, sizes[r], shards[r]), ESGPU_ERR_DEVICE, "corrupt shard record");
             lists.push_back(&shards[r]);
         }
         std::unique_ptr<ResultHolder> h(new ResultHolder());

@@ -202,3 +202,28 @@ def test_plan_reset_reuse_and_multi_segment(engine):  # two segments into one pl
             plan.collect(s)
         assert_same(plan.build().to_dict(), want["shards"][0], f"rep{rep}")
         plan.reset()
+
+
+@pytest.mark.parametrize("order", [Order.count(False), Order.count(True), Order.term(True), Order.term(False)])
+def test_high_cardinality_partitioned_orders(engine, order):
+    """valueCount 70,000 (> LDS): partitioned counting + GPU top-k; a 40 % hot term spans several counting chunks."""
+    n, T = 3_000_000, 70_000
+    rng = np.random.default_rng(5)
+    ords = rng.integers(0, T, size=n, dtype=np.uint32)
+    ords[rng.random(n) < 0.4] = 5
+    ords[rng.random(n) < 0.05] = 0xFFFFFFFF  # missing
+    terms = ["t%06d" % i for i in range(T)]
+    status = rng.integers(0, 3, size=n).astype(np.int64)
+    cols = {"kw": {"type": N.COL_ORD_U32, "values": ords, "terms": terms},
+            "status": {"type": N.COL_I64, "values": status}}
+    aggs = [AB.terms("kw").field("kw").size(25).order(order),
+            AB.terms("kw0").field("kw").size(7).minDocCount(0).order(order)]
+    flt = [QB.rangeQuery("status").gte(1)]
+    want = O.run([(cols, n)], aggs, filters=flt)
+    seg = engine.upload_segment(cols, n)
+    plan = engine.plan(aggs, filters=flt)
+    plan.collect(seg)
+    _, _, path = plan.last_collect_stats()
+    res = plan.build()
+    assert_same(res.to_dict(), want["shards"][0], "shard")
+    assert_same(reduce([res]).to_dict(), want["reduced"], "reduced")

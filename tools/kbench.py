@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Kernel-level sweep: collect-kernel time and algorithmic GB/s for each §8 request shape on one synthetic shard.
+
+    python tools/kbench.py --docs 1000000000 --reps 5 [--only name,name]
+
+Prints one JSON line per variant: {"name", "kernel_ms", "bytes", "gbs", "frac", "path", "step_ms"}.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+import elasticsearch_amd as ea  # noqa: E402
+from elasticsearch_amd import AggregationBuilders as AB  # noqa: E402
+from elasticsearch_amd import QueryBuilders as QB  # noqa: E402
+
+
+def variants():
+    ns = lambda m: AB.terms("hosts").field("host").size(10).subAggregation(  # noqa: E731
+        AB.dateHistogram("h").field("@timestamp").interval("1h").subAggregation(m))
+    return {
+        "terms_host": ([AB.terms("hosts").field("host")], None),
+        "date_hist": ([AB.dateHistogram("h").field("@timestamp").interval("1h")], None),
+        "config2_dh_ext": ([AB.dateHistogram("h").field("@timestamp").interval("1h").subAggregation(
+            AB.extendedStats("rt").field("response_time_ms"))], None),
+        "terms_dh": ([AB.terms("hosts").field("host").subAggregation(AB.dateHistogram("h").field("@timestamp").interval("1h"))], None),
+        "config1_terms_stats": ([AB.terms("hosts").field("host").subAggregation(AB.stats("rt").field("response_time_ms"))], None),
+        "north_star": ([ns(AB.stats("rt").field("response_time_ms"))], None),
+        "ns_avg": ([ns(AB.avg("rt").field("response_time_ms"))], None),
+        "config5": ([ns(AB.avg("rt").field("response_time_ms"))],
+                    [QB.termQuery("status", 200), QB.rangeQuery("bytes").gte(1024).lte(65536)]),
+        "config4_card": ([AB.cardinality("ips").field("client_ip.hash").precisionThreshold(40000)], None),
+        "config3_url": ([AB.terms("urls").field("url").size(10)], None),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--docs", type=int, default=1_000_000_000)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    only = set(filter(None, args.only.split(",")))
+    e = ea.Engine(0)
+    vs = {k: v for k, v in variants().items() if not only or k in only}
+    fields = {"host", "@timestamp", "response_time_ms", "status", "bytes", "client_ip.hash"}
+    if "config3_url" in vs:
+        fields.add("url")
+    t = time.time()
+    seg = e.synthetic_segment(args.docs, fields=tuple(sorted(fields)))
+    print(json.dumps({"generated_s": time.time() - t, "hbm_gb": e.hbm_used() / 1e9}), flush=True)
+    for name, (aggs, flt) in vs.items():
+        plan = e.plan(aggs, filters=flt)
+        ms = []
+        steps = []
+        for r in range(args.reps + 1):
+            t0 = time.perf_counter()
+            plan.reset()
+            plan.collect(seg)
+            k, nbytes, path = plan.last_collect_stats()
+            res = plan.build()
+            ea.reduce([res])
+            dt = (time.perf_counter() - t0) * 1e3
+            if r:  # first is warmup
+                ms.append(k)
+                steps.append(dt)
+        kms = sorted(ms)[len(ms) // 2]
+        gbs = nbytes / (kms / 1e3) / 1e9
+        print(json.dumps({"name": name, "kernel_ms": round(kms, 4), "bytes": nbytes, "gbs": round(gbs, 1),
+                          "frac": round(gbs / 8000, 4), "path": path, "step_ms": round(sorted(steps)[len(steps) // 2], 3),
+                          "docs_per_s": args.docs / (kms / 1e3)}), flush=True)
+        plan.close()
+
+
+if __name__ == "__main__":
+    main()
