@@ -61,39 +61,34 @@ class Filter(ctypes.Structure):
     ]
 
 
-class AggResult(ctypes.Structure):
-    pass
+class AggBlock(ctypes.Structure):
+    """esgpu_agg_block: one aggregation spec for n_instances parent buckets, columnar (include/esgpu.h)."""
 
 
-class Bucket(ctypes.Structure):
-    _fields_ = [
-        ("key", ctypes.c_int64), ("key_bytes", ctypes.POINTER(ctypes.c_uint8)), ("key_len", ctypes.c_int32),
-        ("nsubs", ctypes.c_int32), ("doc_count", ctypes.c_int64), ("doc_count_error", ctypes.c_int64),
-        ("subs", ctypes.POINTER(AggResult)),
-    ]
-
-
-AggResult._fields_ = [
-    ("type", ctypes.c_int32), ("order", ctypes.c_int32), ("name", ctypes.c_char_p),
-    ("buckets", ctypes.POINTER(Bucket)), ("nbuckets", ctypes.c_int64),
-    ("doc_count_error", ctypes.c_int64), ("other_doc_count", ctypes.c_int64),
-    ("required_size", ctypes.c_int32), ("shard_size", ctypes.c_int32), ("min_doc_count", ctypes.c_int64),
-    ("show_term_doc_count_error", ctypes.c_int32), ("keyed", ctypes.c_int32),
-    ("has_empty_bucket_info", ctypes.c_int32), ("date_unit", ctypes.c_int32), ("interval", ctypes.c_int64),
-    ("offset", ctypes.c_int64), ("has_extended_bounds_min", ctypes.c_int32), ("has_extended_bounds_max", ctypes.c_int32),
-    ("extended_bounds_min", ctypes.c_int64), ("extended_bounds_max", ctypes.c_int64),
-    ("empty_subs", ctypes.POINTER(AggResult)), ("nempty_subs", ctypes.c_int32),
-    ("reserved", ctypes.c_int32), ("count", ctypes.c_int64),
-    ("sum", ctypes.c_double), ("min", ctypes.c_double), ("max", ctypes.c_double),
-    ("sum_of_squares", ctypes.c_double), ("sigma", ctypes.c_double),
-    ("hll_present", ctypes.c_int32), ("precision", ctypes.c_int32), ("hll_mode", ctypes.c_int32),
-    ("reserved2", ctypes.c_int32), ("registers", ctypes.POINTER(ctypes.c_uint8)),
-    ("lc_hashes", ctypes.POINTER(ctypes.c_uint32)), ("lc_size", ctypes.c_int64),
+_I32, _I64, _U64, _F64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
+AggBlock._fields_ = [
+    ("type", _I32), ("order", _I32), ("name", ctypes.c_char_p),
+    ("required_size", _I32), ("shard_size", _I32), ("min_doc_count", _I64),
+    ("show_term_doc_count_error", _I32), ("keyed", _I32),
+    ("has_empty_bucket_info", _I32), ("date_unit", _I32), ("interval", _I64), ("offset", _I64),
+    ("has_extended_bounds_min", _I32), ("has_extended_bounds_max", _I32),
+    ("extended_bounds_min", _I64), ("extended_bounds_max", _I64),
+    ("sigma", _F64), ("precision", _I32), ("nsubs", _I32), ("n_instances", _U64),
+    ("doc_count_error", ctypes.POINTER(_I64)), ("other_doc_count", ctypes.POINTER(_I64)),
+    ("bucket_offsets", ctypes.POINTER(_U64)), ("n_buckets", _U64),
+    ("keys", ctypes.POINTER(_I64)), ("term_offsets", ctypes.POINTER(_U64)), ("term_bytes", ctypes.POINTER(ctypes.c_uint8)),
+    ("doc_counts", ctypes.POINTER(_I64)), ("bucket_doc_count_errors", ctypes.POINTER(_I64)),
+    ("subs", ctypes.POINTER(AggBlock)), ("empty_subs", ctypes.POINTER(AggBlock)),
+    ("count", ctypes.POINTER(_I64)), ("sum", ctypes.POINTER(_F64)), ("min", ctypes.POINTER(_F64)),
+    ("max", ctypes.POINTER(_F64)), ("sum_of_squares", ctypes.POINTER(_F64)),
+    ("hll_present", ctypes.POINTER(_I32)), ("hll_mode", ctypes.POINTER(_I32)),
+    ("registers", ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8))),
+    ("lc_hashes", ctypes.POINTER(ctypes.POINTER(ctypes.c_uint32))), ("lc_sizes", ctypes.POINTER(_I64)),
 ]
 
 
 class Result(ctypes.Structure):
-    _fields_ = [("aggs", ctypes.POINTER(AggResult)), ("naggs", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+    _fields_ = [("aggs", ctypes.POINTER(AggBlock)), ("naggs", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 # every entry point declared in include/esgpu.h: (name, restype, argtypes)
@@ -131,7 +126,7 @@ SIGNATURES = [
     ("esgpu_result_free", ctypes.c_int, [ctypes.POINTER(Result)]),
     ("esgpu_reduce", ctypes.c_int, [ctypes.POINTER(ctypes.POINTER(Result)), ctypes.c_int32,
                                     ctypes.POINTER(ctypes.POINTER(Result))]),
-    ("esgpu_cardinality_value", ctypes.c_int, [ctypes.POINTER(AggResult), ctypes.POINTER(ctypes.c_int64)]),
+    ("esgpu_cardinality_value", ctypes.c_int, [ctypes.POINTER(AggBlock), ctypes.c_uint64, ctypes.POINTER(ctypes.c_int64)]),
     ("esgpu_result_to_json", ctypes.c_int, [ctypes.POINTER(Result), ctypes.c_char_p, ctypes.c_size_t,
                                             ctypes.POINTER(ctypes.c_size_t)]),
     ("esgpu_result_serialize", ctypes.c_int, [ctypes.POINTER(Result), _VP, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),

@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "es_common.hpp"
 #include "esgpu_kernels.hpp"
 
@@ -257,9 +259,47 @@ __device__ __forceinline__ uint32_t slot_of(const CollectParams& P, int64_t v, i
     return (uint32_t)(floor_div64(v - P.offset, P.interval) - floor_div64(base - P.offset, P.interval));
 }
 
+// Per-thread run accumulator for histogram-only plans over time-sorted data: a thread's consecutive docs share a
+// key slot, so their count / sum / min / max / sum-of-squares are combined in registers and reach LDS only when
+// the slot changes (an hour boundary) or at a window flush -- no per-doc LDS traffic.
+struct Run {
+    uint32_t slot;  // 0xFFFFFFFF = empty
+    uint32_t cnt, vc;
+    double sum, sq;
+    unsigned long long mn, mx;
+};
+
+__device__ __forceinline__ void run_reset(Run& r) {
+    r.slot = 0xFFFFFFFFu;
+    r.cnt = 0;
+    r.vc = 0;
+    r.sum = 0.0;
+    r.sq = 0.0;
+    r.mn = kMinInit;
+    r.mx = kMaxInit;
+}
+
+template <int MET>
+__device__ __forceinline__ void run_flush(const CollectParams& P, const Acc& a, Run& r) {
+    if (r.slot != 0xFFFFFFFFu) {
+        const uint32_t c = r.slot;  // T == 1: cell == slot
+        atomicAdd(&a.cnt32[c], r.cnt);
+        if (MET > 0 && r.vc) {
+            if (P.vcnt_mode) atomicAdd(&a.vcnt32[c], r.vc);
+            atomicAdd(&a.sum[c], r.sum);
+            if (MET >= 2) {
+                if (r.mn < a.mn[c]) atomicMin(&a.mn[c], r.mn);
+                if (r.mx > a.mx[c]) atomicMax(&a.mx[c], r.mx);
+            }
+            if (MET >= 3) atomicAdd(&a.sq[c], r.sq);
+        }
+    }
+    run_reset(r);
+}
+
 template <bool ORD, bool HIST, int MET, bool LDS>
 __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, const Doc4& d, uint32_t T, int64_t base,
-                                         uint32_t W) {
+                                         uint32_t W, Run& run) {
     uint32_t slot[kVec];
     bool hv_ok[kVec];
 #pragma unroll
@@ -277,65 +317,30 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
             }
         }
     }
-    if (LDS && !ORD && HIST && P.ocnt_mode == OCNT_NONE) {
-        // uniform-cell fast path: every valid doc of the wave maps to the same slot
-        uint32_t my = 0xFFFFFFFFu;
-        bool mixed = false;
+    if (LDS && !ORD) {  // ocnt_mode is OCNT_NONE without a terms dimension; without HIST the slot is always 0
 #pragma unroll
         for (int j = 0; j < kVec; ++j) {
             if (!((d.ok >> j) & 1) || !hv_ok[j]) continue;
-            if (my == 0xFFFFFFFFu) my = slot[j];
-            else mixed |= slot[j] != my;
-        }
-        const uint64_t has = __ballot(my != 0xFFFFFFFFu);
-        if (has == 0) return;
-        const int first = __ffsll((long long)has) - 1;
-        const uint32_t s0 = __shfl(my, first, 64);
-        const bool uniform = __all(!mixed && (my == 0xFFFFFFFFu || my == s0));
-        if (uniform && s0 < W) {
-            uint32_t cnt = 0, vc = 0;
-            double sum = 0.0, sq = 0.0;
-            unsigned long long mn = kMinInit, mx = kMaxInit;
-#pragma unroll
-            for (int j = 0; j < kVec; ++j) {
-                if (!((d.ok >> j) & 1) || !hv_ok[j]) continue;
-                ++cnt;
-                if (MET > 0 && ((d.mpres >> j) & 1)) {
-                    const double x = d.mv[j];
-                    ++vc;
-                    sum += x;
-                    if (MET >= 3) sq += x * x;
-                    if (MET >= 2) {
-                        const bool nan = x != x;
-                        const unsigned long long e = sortable(x);
-                        const unsigned long long emn = nan ? 0ull : e, emx = nan ? ~0ull : e;
-                        mn = emn < mn ? emn : mn;
-                        mx = emx > mx ? emx : mx;
-                    }
+            if (slot[j] != run.slot) {
+                run_flush<MET>(P, a, run);
+                run.slot = slot[j];
+            }
+            ++run.cnt;
+            if (MET > 0 && ((d.mpres >> j) & 1)) {
+                const double x = d.mv[j];
+                ++run.vc;
+                run.sum += x;
+                if (MET >= 3) run.sq += x * x;
+                if (MET >= 2) {
+                    const bool nan = x != x;
+                    const unsigned long long e = sortable(x);
+                    const unsigned long long emn = nan ? 0ull : e, emx = nan ? ~0ull : e;
+                    run.mn = emn < run.mn ? emn : run.mn;
+                    run.mx = emx > run.mx ? emx : run.mx;
                 }
             }
-            cnt = wave_sum_u32(cnt);
-            if (MET > 0) {
-                vc = wave_sum_u32(vc);
-                sum = wave_sum_f64(sum);
-                if (MET >= 2) { mn = wave_min_u64(mn); mx = wave_max_u64(mx); }
-                if (MET >= 3) sq = wave_sum_f64(sq);
-            }
-            if ((threadIdx.x & 63) == 0) {
-                const uint32_t c = s0;  // T == 1
-                atomicAdd(&a.cnt32[c], cnt);
-                if (MET > 0 && vc) {
-                    if (P.vcnt_mode) atomicAdd(&a.vcnt32[c], vc);
-                    atomicAdd(&a.sum[c], sum);
-                    if (MET >= 2) {
-                        if (mn < a.mn[c]) atomicMin(&a.mn[c], mn);
-                        if (mx > a.mx[c]) atomicMax(&a.mx[c], mx);
-                    }
-                    if (MET >= 3) atomicAdd(&a.sq[c], sq);
-                }
-            }
-            return;
         }
+        return;
     }
 #pragma unroll
     for (int j = 0; j < kVec; ++j) {
@@ -444,6 +449,8 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
     bool dirty = false;
     int64_t base = HIST ? P.key0 * P.interval + P.offset : 0;  // value of the first LDS slot
 
+    Run run;
+    run_reset(run);
     Doc4 cur;
     const uint32_t tid4 = threadIdx.x * kVec;
     load_docs<ORD, HIST, MET>(P, b_begin * kBlockDocs + tid4, cur);
@@ -459,7 +466,10 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
                 if (kmx - kmn + 1 > (int64_t)W) {
                     use_lds = false;  // block spans more keys than the window: global atomics for this block
                 } else if (!win_set || kmn < (int64_t)win0 || kmx >= (int64_t)win0 + (int64_t)W) {
-                    if (dirty) flush_window<MET>(P, s, T, W, win0);
+                    if (dirty) {
+                        if (!ORD) run_flush<MET>(P, s, run);
+                        flush_window<MET>(P, s, T, W, win0);
+                    }
                     dirty = false;
                     win0 = (uint32_t)kmn;
                     win_set = true;
@@ -477,15 +487,18 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
                 load_docs<ORD, HIST, MET>(P, nb * kBlockDocs + nit * kIterDocs + tid4, nxt);
             }
             if (use_lds) {
-                process4<ORD, HIST, MET, true>(P, s, cur, T, base, W);
+                process4<ORD, HIST, MET, true>(P, s, cur, T, base, W, run);
                 dirty = true;
             } else {
-                process4<ORD, HIST, MET, false>(P, g, cur, T, base, W);
+                process4<ORD, HIST, MET, false>(P, g, cur, T, base, W, run);
             }
             if (!last) cur = nxt;
         }
     }
-    if (P.lds_mode && (dirty || !(HIST && P.windowed))) flush_window<MET>(P, s, T, W, win0);
+    if (P.lds_mode && (dirty || !(HIST && P.windowed))) {
+        if (!ORD) run_flush<MET>(P, s, run);
+        flush_window<MET>(P, s, T, W, win0);
+    }
 }
 
 template <bool ORD, bool HIST, int MET>
@@ -582,18 +595,38 @@ __device__ __forceinline__ uint32_t hll_hash4(const HllParams& P, uint32_t i0, u
 
 // pass 1: HLL registers (max runLen per index).  Registers only grow, so a stale read-check costs at most an extra
 // atomic; after warm-up almost every doc is a read that finds a register already >= its run length.
-__global__ __launch_bounds__(256) void hll_registers_kernel(HllParams P) {
+// `floor` is a lower bound of every register (min over registers after the previous phase): a hash whose run
+// length is <= floor cannot raise any register, so it needs no register read at all.
+__global__ __launch_bounds__(256) void hll_registers_kernel(HllParams P, uint32_t d_begin, uint32_t d_end,
+                                                            const unsigned int* floor_ptr) {
+    const uint32_t floor = floor_ptr ? *floor_ptr : 0u;
     const uint32_t gsz = gridDim.x * blockDim.x;
-    for (uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < P.n_docs; i0 += gsz * 4) {
+    for (uint32_t i0 = d_begin + (blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < d_end; i0 += gsz * 4) {
         uint64_t hv[4];
         const uint32_t ok = hll_hash4(P, i0, hv);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             if (!((ok >> j) & 1)) continue;
-            const uint32_t idx = hll_index(hv[j], P.p);
             const uint32_t rl = hll_run_len(hv[j], P.p);
+            if (rl <= floor) continue;
+            const uint32_t idx = hll_index(hv[j], P.p);
             if (rl > P.regs[idx]) atomicMax(&P.regs[idx], rl);
         }
+    }
+}
+
+__global__ __launch_bounds__(1024) void hll_floor_kernel(const unsigned int* regs, uint32_t m, unsigned int* out) {
+    uint32_t mn = 0xFFFFFFFFu;
+    for (uint32_t i = threadIdx.x; i < m; i += 1024) mn = min(mn, regs[i]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+    __shared__ uint32_t part[16];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = mn;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = part[0];
+        for (int w = 1; w < 16; ++w) t = min(t, part[w]);
+        *out = t;
     }
 }
 
@@ -649,7 +682,23 @@ void launch_hll(const HllParams& p, hipStream_t st) {
     uint32_t grid = (p.n_docs + 1023) / 1024;
     if (grid > 8192) grid = 8192;
     if (grid == 0) grid = 1;
-    hipLaunchKernelGGL(hll_registers_kernel, dim3(grid), dim3(256), 0, st, p);
+    // phases over [0, n/64), [n/64, n/8), [n/8, n): the register floor from each phase prunes the next one
+    const uint32_t n = p.n_docs;
+    uint32_t cuts[4] = {0, 0, 0, n};
+    if (n >= 64u * 65536u) {
+        cuts[1] = (n / 64) & ~3u;
+        cuts[2] = (n / 8) & ~3u;
+    }
+    const uint32_t m = 1u << p.p;
+    for (int ph = 0; ph < 3; ++ph) {
+        if (cuts[ph + 1] <= cuts[ph]) continue;
+        const uint32_t span = cuts[ph + 1] - cuts[ph];
+        const uint32_t g = std::max(1u, std::min(grid, (span + 1023) / 1024));
+        hipLaunchKernelGGL(hll_registers_kernel, dim3(g), dim3(256), 0, st, p, cuts[ph], cuts[ph + 1],
+                           ph == 0 ? (const unsigned int*)nullptr : (const unsigned int*)p.floor);
+        if (ph < 2 && cuts[ph + 1] < n)
+            hipLaunchKernelGGL(hll_floor_kernel, dim3(1), dim3(1024), 0, st, (const unsigned int*)p.regs, m, p.floor);
+    }
     hipLaunchKernelGGL(hll_nonzero_kernel, dim3(1), dim3(1024), 0, st, (const unsigned int*)p.regs, 1u << p.p, p.nonzero);
     hipLaunchKernelGGL(hll_lc_kernel, dim3(grid), dim3(256), 0, st, p);
 }

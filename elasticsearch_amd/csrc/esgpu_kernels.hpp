@@ -94,6 +94,7 @@ struct HllParams {
     unsigned int* lc_set;       // open-addressing set of encoded hashes (0 = empty)
     unsigned int* lc_count;
     unsigned int* nonzero;      // written by the register pass: registers != 0
+    unsigned int* floor;        // scratch: min register after a phase
     uint32_t lc_mask;
     uint32_t lc_threshold;
 };

@@ -17,6 +17,7 @@
 #include <cstring>
 #include <map>
 #include <stdexcept>
+#include <string_view>
 #include <unordered_map>
 
 namespace esgpu {
@@ -134,17 +135,16 @@ static double estimate_bias(int p, double e) {  // :378-405
     return bs / ws;
 }
 
-int64_t hll_cardinality(const RAgg& a) {  // :270-307
-    if (!a.hll_present) return 0;
-    const int p = a.precision;
-    if (a.hll_mode == 0) return linear_counting(1LL << kP2, (1LL << kP2) - (int64_t)a.lc.size());
+int64_t hll_cardinality(int p, bool present, int mode, const uint8_t* regs, size_t nlc) {  // :270-307
+    if (!present) return 0;
+    if (mode == 0) return linear_counting(1LL << kP2, (1LL << kP2) - (int64_t)nlc);
     const int m = 1 << p;
     const double alpha = p == 4 ? 0.673 : p == 5 ? 0.697 : 0.7213 / (1 + 1.079 / m);
     const double alphaMM = alpha * m * m;
     double inv = 0;
     int zeros = 0;
     for (int i = 0; i < m; ++i) {
-        const int rl = a.registers[i];
+        const int rl = regs[i];
         inv += 1. / (double)(1LL << rl);
         if (rl == 0) ++zeros;
     }
@@ -164,210 +164,444 @@ static uint32_t dec_index(uint32_t enc, int p) {
     const uint32_t idx = (enc & 1) ? (enc >> 7) : (enc >> 1);
     return idx >> (kP2 - p);
 }
-static void upgrade_to_hll(RAgg& a) {  // :309-322
-    a.registers.assign((size_t)1 << a.precision, 0);
-    for (uint32_t e : a.lc) {
-        uint8_t& r = a.registers[dec_index(e, a.precision)];
-        r = (uint8_t)std::max<uint32_t>(r, dec_run_len(e, a.precision));
+// HyperLogLogPlusPlus.merge (:201-230) on one instance's state: (mode, registers, lc)
+struct HllState {
+    int p = 14;
+    bool present = false;
+    int mode = 0;
+    std::vector<uint8_t> regs;
+    std::vector<uint32_t> lc;
+    void upgrade() {  // upgradeToHll (:309-322)
+        regs.assign((size_t)1 << p, 0);
+        for (uint32_t e : lc) {
+            uint8_t& r = regs[dec_index(e, p)];
+            r = (uint8_t)std::max<uint32_t>(r, dec_run_len(e, p));
+        }
+        lc.clear();
+        mode = 1;
     }
-    a.lc.clear();
-    a.hll_mode = 1;
+    void merge(int op, int omode, const std::vector<uint8_t>& oregs, const std::vector<uint32_t>& olc) {
+        if (p != op) throw std::invalid_argument("cardinality precision mismatch");
+        const int m = 1 << p;
+        const size_t threshold = (size_t)((float)(m / 4) * 0.75f);
+        if (omode == 0) {
+            for (uint32_t e : olc) {
+                if (mode == 0) {
+                    auto it = std::lower_bound(lc.begin(), lc.end(), e);
+                    if (it == lc.end() || *it != e) {
+                        lc.insert(it, e);
+                        if (lc.size() > threshold) upgrade();
+                    }
+                } else {
+                    uint8_t& r = regs[dec_index(e, p)];
+                    r = (uint8_t)std::max<uint32_t>(r, dec_run_len(e, p));
+                }
+            }
+        } else {
+            if (mode == 0) upgrade();
+            for (int i = 0; i < m; ++i) regs[i] = std::max(regs[i], oregs[i]);
+        }
+    }
+};
+
+// ------------------------------------------------------------------------------------------------------------
+// Block structure helpers
+// ------------------------------------------------------------------------------------------------------------
+Block Block::like() const {
+    Block b;
+    b.type = type; b.order = order; b.name = name;
+    b.required_size = required_size; b.shard_size = shard_size; b.min_doc_count = min_doc_count;
+    b.show_err = show_err; b.keyed = keyed;
+    b.has_empty_info = has_empty_info; b.date_unit = date_unit; b.interval = interval; b.offset = offset;
+    b.has_bmin = has_bmin; b.has_bmax = has_bmax; b.bmin = bmin; b.bmax = bmax;
+    b.sigma = sigma; b.precision = precision;
+    b.n = 0;
+    if (is_bucket()) {
+        b.boff.assign(1, 0);
+        b.term_off.assign(1, 0);
+        for (const Block& s : subs) b.subs.push_back(s.like());
+        b.empty_subs = empty_subs;
+    }
+    return b;
 }
 
-void hll_merge(RAgg& into, const RAgg& other) {  // HyperLogLogPlusPlus.merge (:201-230)
-    if (!other.hll_present) return;
-    if (into.precision != other.precision) throw std::invalid_argument("cardinality precision mismatch");
-    const int m = 1 << into.precision;
-    const size_t threshold = (size_t)((float)(m / 4) * 0.75f);
-    if (other.hll_mode == 0) {
-        for (uint32_t e : other.lc) {
-            if (into.hll_mode == 0) {
-                auto it = std::lower_bound(into.lc.begin(), into.lc.end(), e);
-                if (it == into.lc.end() || *it != e) {
-                    into.lc.insert(it, e);
-                    if (into.lc.size() > threshold) upgrade_to_hll(into);
-                }
-            } else {
-                uint8_t& r = into.registers[dec_index(e, into.precision)];
-                r = (uint8_t)std::max<uint32_t>(r, dec_run_len(e, into.precision));
+void Block::append_instance(const Block& src, uint64_t i) {
+    ++n;
+    if (is_bucket()) {
+        doc_count_error.push_back(src.doc_count_error[i]);
+        other_doc_count.push_back(src.other_doc_count[i]);
+        const uint64_t b0 = src.boff[i], b1 = src.boff[i + 1];
+        for (uint64_t k = b0; k < b1; ++k) {
+            key.push_back(src.key[k]);
+            term_pool.append(src.term_pool, src.term_off[k], src.term_off[k + 1] - src.term_off[k]);
+            term_off.push_back(term_pool.size());
+            bcount.push_back(src.bcount[k]);
+            berr.push_back(src.berr[k]);
+        }
+        boff.push_back(boff.back() + (b1 - b0));
+        for (size_t j = 0; j < subs.size(); ++j)
+            for (uint64_t k = b0; k < b1; ++k) subs[j].append_instance(src.subs[j], k);
+    } else if (type == ESGPU_AGG_CARDINALITY) {
+        hll_present.push_back(src.hll_present[i]);
+        hll_mode.push_back(src.hll_mode[i]);
+        regs.push_back(src.regs[i]);
+        lc.push_back(src.lc[i]);
+    } else {
+        count.push_back(src.count[i]);
+        sum.push_back(src.sum[i]);
+        min.push_back(src.min[i]);
+        max.push_back(src.max[i]);
+        sumsq.push_back(src.sumsq[i]);
+    }
+}
+
+void Block::append_empty() {  // buildEmptyAggregation
+    ++n;
+    if (is_bucket()) {
+        doc_count_error.push_back(0);
+        other_doc_count.push_back(0);
+        boff.push_back(boff.back());
+    } else if (type == ESGPU_AGG_CARDINALITY) {
+        hll_present.push_back(0);
+        hll_mode.push_back(0);
+        regs.emplace_back();
+        lc.emplace_back();
+    } else {
+        count.push_back(0);
+        sum.push_back(0.0);
+        min.push_back(INFINITY);
+        max.push_back(-INFINITY);
+        sumsq.push_back(0.0);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// reduce: one output instance per group of input instances (shard order inside a group)
+//
+// All bookkeeping is flat: a level's groups are ranges into one Ref pool, so a reduce allocates O(depth) vectors,
+// not O(buckets).
+// ------------------------------------------------------------------------------------------------------------
+namespace {
+
+struct Ref {
+    const Block* b;
+    uint64_t i;
+};
+struct Group {
+    uint32_t begin, end;    // range in the level's Ref pool
+    bool verbatim = false;  // an empty histogram bucket's prototype sub-aggregation: copied, not reduced
+};
+struct Level {
+    std::vector<Ref> pool;
+    std::vector<Group> groups;
+    void add(const Ref* r, size_t n, bool verbatim) {
+        Group g{(uint32_t)pool.size(), (uint32_t)(pool.size() + n), verbatim};
+        pool.insert(pool.end(), r, r + n);
+        groups.push_back(g);
+    }
+};
+
+void reduce_level(const Level& lv, Block& out);
+
+inline std::string_view term_of(const Block& b, uint64_t k) {
+    return std::string_view(b.term_pool.data() + b.term_off[k], b.term_off[k + 1] - b.term_off[k]);
+}
+
+int cmp_terms(int order, int64_t ca, int64_t cb, std::string_view ta, std::string_view tb) {
+    switch (order) {
+        case ESGPU_ORDER_COUNT_DESC: if (ca != cb) return ca > cb ? -1 : 1; return ta.compare(tb);
+        case ESGPU_ORDER_COUNT_ASC: if (ca != cb) return ca < cb ? -1 : 1; return ta.compare(tb);
+        case ESGPU_ORDER_TERM_DESC: return -ta.compare(tb);
+        default: return ta.compare(tb);
+    }
+}
+
+// emitted bucket: its contributing (block, bucket) pairs are contrib[c0, c1) of the group's scratch
+struct OutBucket {
+    int64_t key;
+    const Block* tb;  // where the term bytes live (terms)
+    uint64_t tk;
+    int64_t count;
+    int64_t err;
+    uint32_t c0, c1;
+    bool empty;
+};
+
+struct Scratch {
+    std::vector<Ref> contrib;
+    std::vector<OutBucket> buckets, filled;
+    std::vector<uint32_t> ids, start;
+    std::unordered_map<std::string_view, uint32_t> index;
+    std::vector<Ref> child;
+};
+
+void emit_buckets(Block& out, const std::vector<OutBucket>& buckets, const Scratch& sc, std::vector<Level>& child) {
+    for (const OutBucket& ob : buckets) {
+        out.key.push_back(ob.key);
+        if (ob.tb) {
+            const std::string_view t = term_of(*ob.tb, ob.tk);
+            out.term_pool.append(t.data(), t.size());
+        }
+        out.term_off.push_back(out.term_pool.size());
+        out.bcount.push_back(ob.count);
+        out.berr.push_back(ob.err);
+        for (size_t j = 0; j < out.subs.size(); ++j) {
+            Level& lv = child[j];
+            if (ob.empty) {
+                const Ref r{&out.empty_subs[j], 0};
+                lv.add(&r, 1, true);
+                continue;
             }
+            Group g{(uint32_t)lv.pool.size(), 0, false};
+            for (uint32_t c = ob.c0; c < ob.c1; ++c) lv.pool.push_back({&sc.contrib[c].b->subs[j], sc.contrib[c].i});
+            g.end = (uint32_t)lv.pool.size();
+            lv.groups.push_back(g);
+        }
+    }
+    out.boff.push_back(out.boff.back() + buckets.size());
+}
+
+void reduce_terms(const Ref* refs, size_t nrefs, Block& out, Scratch& sc, std::vector<Level>& child) {  // InternalTerms.doReduce
+    int64_t sumErr = 0, other = 0;
+    sc.buckets.clear();
+    sc.contrib.clear();
+    sc.ids.clear();
+    sc.index.clear();
+    std::vector<Ref>& entries = sc.child;  // (block, bucket) in shard order
+    entries.clear();
+    for (size_t x = 0; x < nrefs; ++x) {
+        const Ref& r = refs[x];
+        const Block& t = *r.b;
+        other += t.other_doc_count[r.i];
+        const uint64_t b0 = t.boff[r.i], b1 = t.boff[r.i + 1];
+        int64_t thisErr;
+        if ((int64_t)(b1 - b0) < out.shard_size || out.order == ESGPU_ORDER_TERM_ASC || out.order == ESGPU_ORDER_TERM_DESC) thisErr = 0;
+        else if (out.order == ESGPU_ORDER_COUNT_DESC) thisErr = t.bcount[b1 - 1];
+        else thisErr = -1;
+        if (sumErr != -1) sumErr = thisErr == -1 ? -1 : sumErr + thisErr;
+        for (uint64_t k = b0; k < b1; ++k) {
+            uint32_t id;
+            if (nrefs == 1) {  // one shard: its terms are distinct
+                id = (uint32_t)sc.buckets.size();
+                sc.buckets.push_back(OutBucket{t.key[k], &t, k, 0, 0, 0, 0, false});
+            } else {
+                auto ins = sc.index.try_emplace(term_of(t, k), (uint32_t)sc.buckets.size());
+                if (ins.second) sc.buckets.push_back(OutBucket{t.key[k], &t, k, 0, 0, 0, 0, false});
+                id = ins.first->second;
+            }
+            OutBucket& ob = sc.buckets[id];
+            ob.count += t.bcount[k];
+            if (ob.err != -1) ob.err = thisErr == -1 ? -1 : ob.err + thisErr;  // Bucket.reduce of per-shard errors
+            ob.c1++;  // contribution count for now
+            sc.ids.push_back(id);
+            entries.push_back({&t, k});
+        }
+    }
+    // contributions grouped by bucket, shard order kept (counting sort)
+    const uint32_t nb = (uint32_t)sc.buckets.size();
+    sc.start.assign(nb + 1, 0);
+    for (uint32_t id = 0; id < nb; ++id) sc.start[id + 1] = sc.start[id] + sc.buckets[id].c1;
+    for (uint32_t id = 0; id < nb; ++id) { sc.buckets[id].c0 = sc.start[id]; sc.buckets[id].c1 = sc.start[id]; }
+    sc.contrib.resize(entries.size());
+    for (size_t e = 0; e < entries.size(); ++e) sc.contrib[sc.buckets[sc.ids[e]].c1++] = entries[e];
+    // per-bucket error relative to the summed shard error, min_doc_count filter (in place)
+    size_t m = 0;
+    for (uint32_t id = 0; id < nb; ++id) {
+        OutBucket ob = sc.buckets[id];
+        if (ob.err != -1) ob.err = sumErr == -1 ? -1 : sumErr - ob.err;
+        if (ob.count >= out.min_doc_count) sc.buckets[m++] = ob;
+    }
+    sc.buckets.resize(m);
+    const size_t size = std::min<size_t>((size_t)std::max(out.required_size, 0), nb);
+    auto less = [&](const OutBucket& a, const OutBucket& b) {
+        return cmp_terms(out.order, a.count, b.count, term_of(*a.tb, a.tk), term_of(*b.tb, b.tk)) < 0;
+    };
+    if (sc.buckets.size() > size) {
+        std::partial_sort(sc.buckets.begin(), sc.buckets.begin() + size, sc.buckets.end(), less);
+        for (size_t i = size; i < sc.buckets.size(); ++i) other += sc.buckets[i].count;
+        sc.buckets.resize(size);
+    } else {
+        std::sort(sc.buckets.begin(), sc.buckets.end(), less);
+    }
+    ++out.n;
+    out.doc_count_error.push_back(sumErr == -1 ? -1 : (nrefs == 1 ? 0 : sumErr));
+    out.other_doc_count.push_back(other);
+    emit_buckets(out, sc.buckets, sc, child);
+}
+
+void reduce_histogram(const Ref* refs, size_t nrefs, Block& out, Scratch& sc, std::vector<Level>& child) {  // InternalHistogram.doReduce
+    std::vector<OutBucket>& list = sc.buckets;
+    list.clear();
+    sc.contrib.clear();
+    if (nrefs == 1) {  // one shard: already key-sorted, nothing to merge
+        const Block& h = *refs[0].b;
+        const uint64_t i = refs[0].i;
+        for (uint64_t k = h.boff[i]; k < h.boff[i + 1]; ++k) {
+            if (h.bcount[k] < out.min_doc_count) continue;
+            const uint32_t c = (uint32_t)sc.contrib.size();
+            sc.contrib.push_back({&h, k});
+            list.push_back(OutBucket{h.key[k], nullptr, 0, h.bcount[k], 0, c, c + 1, false});
         }
     } else {
-        if (into.hll_mode == 0) upgrade_to_hll(into);
-        for (int i = 0; i < m; ++i) into.registers[i] = std::max(into.registers[i], other.registers[i]);
+        std::vector<Ref>& all = sc.child;
+        all.clear();
+        for (size_t x = 0; x < nrefs; ++x)
+            for (uint64_t k = refs[x].b->boff[refs[x].i]; k < refs[x].b->boff[refs[x].i + 1]; ++k) all.push_back({refs[x].b, k});
+        std::stable_sort(all.begin(), all.end(), [](const Ref& a, const Ref& b) { return a.b->key[a.i] < b.b->key[b.i]; });
+        sc.contrib = all;
+        for (size_t x = 0; x < all.size();) {
+            const int64_t key = all[x].b->key[all[x].i];
+            OutBucket ob{key, nullptr, 0, 0, 0, (uint32_t)x, 0, false};
+            size_t y = x;
+            for (; y < all.size() && all[y].b->key[all[y].i] == key; ++y) ob.count += all[y].b->bcount[all[y].i];
+            ob.c1 = (uint32_t)y;
+            if (ob.count >= out.min_doc_count) list.push_back(ob);
+            x = y;
+        }
+    }
+    if (out.min_doc_count == 0 && out.has_empty_info) {  // addEmptyBuckets (InternalHistogram.java:395-449)
+        auto next = [&](int64_t k) { return rounding_next(out.type, out.date_unit, out.interval, out.offset, k); };
+        auto empty = [](int64_t k) { return OutBucket{k, nullptr, 0, 0, 0, 0, 0, true}; };
+        std::vector<OutBucket>& filled = sc.filled;
+        filled.clear();
+        if (list.empty()) {
+            if (out.has_bmin && out.has_bmax)
+                for (int64_t k = out.bmin; k <= out.bmax; k = next(k)) filled.push_back(empty(k));
+        } else {
+            if (out.has_bmin)
+                for (int64_t k = out.bmin; k < list[0].key; k = next(k)) filled.push_back(empty(k));
+            for (size_t i = 0; i < list.size(); ++i) {
+                if (i > 0)
+                    for (int64_t k = next(list[i - 1].key); k < list[i].key; k = next(k)) filled.push_back(empty(k));
+                filled.push_back(list[i]);
+            }
+            const int64_t last = filled.back().key;
+            if (out.has_bmax && out.bmax > last)
+                for (int64_t k = next(last); k <= out.bmax; k = next(k)) filled.push_back(empty(k));
+        }
+        list.swap(filled);
+    }
+    if (out.order == ESGPU_ORDER_KEY_DESC) std::reverse(list.begin(), list.end());
+    else if (out.order == ESGPU_ORDER_HCOUNT_ASC || out.order == ESGPU_ORDER_HCOUNT_DESC) {
+        const bool asc = out.order == ESGPU_ORDER_HCOUNT_ASC;
+        std::stable_sort(list.begin(), list.end(), [&](const OutBucket& a, const OutBucket& b) {
+            if (a.count != b.count) return asc ? a.count < b.count : a.count > b.count;
+            return a.key < b.key;
+        });
+    }
+    ++out.n;
+    out.doc_count_error.push_back(0);
+    out.other_doc_count.push_back(0);
+    emit_buckets(out, list, sc, child);
+}
+
+// copy a prototype instance; its sub-aggregations stay verbatim too (queued in bucket order)
+void copy_verbatim(const Ref& r, Block& out, std::vector<Level>& child) {
+    const Block& src = *r.b;
+    const uint64_t i = r.i;
+    ++out.n;
+    out.doc_count_error.push_back(src.doc_count_error[i]);
+    out.other_doc_count.push_back(src.other_doc_count[i]);
+    for (uint64_t k = src.boff[i]; k < src.boff[i + 1]; ++k) {
+        out.key.push_back(src.key[k]);
+        const std::string_view t = term_of(src, k);
+        out.term_pool.append(t.data(), t.size());
+        out.term_off.push_back(out.term_pool.size());
+        out.bcount.push_back(src.bcount[k]);
+        out.berr.push_back(src.berr[k]);
+        for (size_t j = 0; j < out.subs.size(); ++j) {
+            const Ref c{&src.subs[j], k};
+            child[j].add(&c, 1, true);
+        }
+    }
+    out.boff.push_back(out.boff.back() + (src.boff[i + 1] - src.boff[i]));
+}
+
+void reduce_level(const Level& lv, Block& out) {
+    if (out.is_bucket()) {
+        std::vector<Level> child(out.subs.size());
+        Scratch sc;
+        for (const Group& g : lv.groups) {
+            const Ref* refs = lv.pool.data() + g.begin;
+            const size_t n = g.end - g.begin;
+            if (g.verbatim) copy_verbatim(refs[0], out, child);
+            else if (out.type == ESGPU_AGG_TERMS) reduce_terms(refs, n, out, sc, child);
+            else reduce_histogram(refs, n, out, sc, child);
+        }
+        for (size_t j = 0; j < out.subs.size(); ++j) reduce_level(child[j], out.subs[j]);
+        return;
+    }
+    for (const Group& g : lv.groups) {
+        const Ref* refs = lv.pool.data() + g.begin;
+        const size_t n = g.end - g.begin;
+        if (g.verbatim) {
+            out.append_instance(*refs[0].b, refs[0].i);
+            continue;
+        }
+        if (out.type == ESGPU_AGG_CARDINALITY) {  // InternalCardinality.doReduce (:103-121)
+            HllState st;
+            bool any = false;
+            for (size_t x = 0; x < n; ++x) {
+                const Ref& r = refs[x];
+                if (!r.b->hll_present[r.i]) continue;
+                if (!any) { any = true; st.present = true; st.p = r.b->precision; st.mode = 0; }
+                st.merge(r.b->precision, r.b->hll_mode[r.i], r.b->regs[r.i], r.b->lc[r.i]);
+            }
+            if (!any) { out.append_instance(*refs[0].b, refs[0].i); continue; }  // all empty: the first one
+            ++out.n;
+            out.hll_present.push_back(1);
+            out.hll_mode.push_back(st.mode);
+            out.regs.push_back(std::move(st.regs));
+            out.lc.push_back(std::move(st.lc));
+            continue;
+        }
+        // InternalStats / InternalExtendedStats / InternalAvg .doReduce: sums in shard order, Math.min / Math.max
+        int64_t count = 0;
+        double mn = INFINITY, mx = -INFINITY, sum = 0, sq = 0;
+        for (size_t x = 0; x < n; ++x) {
+            const Ref& r = refs[x];
+            count += r.b->count[r.i];
+            mn = jmin(mn, r.b->min[r.i]);
+            mx = jmax(mx, r.b->max[r.i]);
+            sum += r.b->sum[r.i];
+            sq += r.b->sumsq[r.i];
+        }
+        ++out.n;
+        out.count.push_back(count);
+        out.min.push_back(mn);
+        out.max.push_back(mx);
+        out.sum.push_back(sum);
+        out.sumsq.push_back(sq);
     }
 }
 
-// ------------------------------------------------------------------------------------------------------------
-// reduce
-// ------------------------------------------------------------------------------------------------------------
-static int terms_cmp(int order, const RBucket& a, const RBucket& b) {
-    auto keycmp = [&]() {
-        const int c = std::memcmp(a.term.data(), b.term.data(), std::min(a.term.size(), b.term.size()));
-        if (c != 0) return c < 0 ? -1 : 1;
-        return a.term.size() < b.term.size() ? -1 : a.term.size() > b.term.size() ? 1 : 0;
-    };
-    switch (order) {
-        case ESGPU_ORDER_COUNT_DESC: if (a.doc_count != b.doc_count) return a.doc_count > b.doc_count ? -1 : 1; return keycmp();
-        case ESGPU_ORDER_COUNT_ASC: if (a.doc_count != b.doc_count) return a.doc_count < b.doc_count ? -1 : 1; return keycmp();
-        case ESGPU_ORDER_TERM_DESC: return -keycmp();
-        default: return keycmp();
-    }
+}  // namespace
+
+// shard results of one request share the aggregation tree (types, sub-aggregation lists, sketch precision)
+static bool same_shape(const Block& a, const Block& b) {
+    if (a.type != b.type || a.subs.size() != b.subs.size() || a.empty_subs.size() != b.empty_subs.size()) return false;
+    if (a.type == ESGPU_AGG_CARDINALITY && a.precision != b.precision) return false;
+    for (size_t j = 0; j < a.subs.size(); ++j) if (!same_shape(a.subs[j], b.subs[j])) return false;
+    return true;
 }
 
-static RAgg reduce_one(const std::vector<const RAgg*>& aggs);
-
-std::vector<RAgg> reduce_lists(const std::vector<const std::vector<RAgg>*>& lists) {
-    std::vector<RAgg> out;
+std::vector<Block> reduce_lists(const std::vector<const std::vector<Block>*>& lists) {
+    std::vector<Block> out;
     if (lists.empty()) return out;
     const size_t n = lists[0]->size();
-    for (size_t i = 0; i < n; ++i) {
-        std::vector<const RAgg*> same;
+    for (size_t a = 0; a < n; ++a) {
+        Level lv;
         for (auto* l : lists) {
             if (l->size() != n) throw std::invalid_argument("shard results have different aggregation lists");
-            same.push_back(&(*l)[i]);
+            if (!same_shape((*l)[a], (*lists[0])[a])) throw std::invalid_argument("aggregation trees differ across shards");
+            lv.pool.push_back({&(*l)[a], 0});
         }
-        out.push_back(reduce_one(same));
+        lv.groups.push_back(Group{0, (uint32_t)lv.pool.size(), false});
+        Block b = (*lists[0])[a].like();
+        reduce_level(lv, b);
+        out.push_back(std::move(b));
     }
     return out;
-}
-
-static RAgg reduce_one(const std::vector<const RAgg*>& aggs) {
-    const RAgg& first = *aggs[0];
-    RAgg r;  // header of the first aggregation (InternalX carries its request parameters); buckets rebuilt below
-    r.type = first.type; r.order = first.order; r.name = first.name;
-    r.doc_count_error = first.doc_count_error; r.other_doc_count = first.other_doc_count;
-    r.required_size = first.required_size; r.shard_size = first.shard_size; r.min_doc_count = first.min_doc_count;
-    r.show_err = first.show_err; r.keyed = first.keyed;
-    r.has_empty_info = first.has_empty_info; r.date_unit = first.date_unit; r.interval = first.interval;
-    r.offset = first.offset; r.has_bmin = first.has_bmin; r.has_bmax = first.has_bmax; r.bmin = first.bmin; r.bmax = first.bmax;
-    r.empty_subs = first.empty_subs;
-    r.count = first.count; r.sum = first.sum; r.min = first.min; r.max = first.max; r.sumsq = first.sumsq;
-    r.sigma = first.sigma;
-    r.hll_present = first.hll_present; r.precision = first.precision; r.hll_mode = first.hll_mode;
-    switch (first.type) {
-        case ESGPU_AGG_TERMS: {
-            int64_t sumErr = 0, other = 0;
-            std::unordered_map<std::string, size_t> index;
-            std::vector<std::vector<std::pair<const RBucket*, int64_t>>> groups;  // (bucket, its shard's error)
-            for (const RAgg* t : aggs) {
-                other += t->other_doc_count;
-                int64_t thisErr;
-                if ((int64_t)t->buckets.size() < first.shard_size || first.order == ESGPU_ORDER_TERM_ASC ||
-                    first.order == ESGPU_ORDER_TERM_DESC) thisErr = 0;
-                else if (first.order == ESGPU_ORDER_COUNT_DESC) thisErr = t->buckets.back().doc_count;
-                else thisErr = -1;
-                if (sumErr != -1) sumErr = thisErr == -1 ? -1 : sumErr + thisErr;
-                for (const RBucket& b : t->buckets) {
-                    auto it = index.find(b.term);
-                    if (it == index.end()) { index.emplace(b.term, groups.size()); groups.push_back({}); it = index.find(b.term); }
-                    groups[it->second].push_back({&b, thisErr});
-                }
-            }
-            std::vector<RBucket> cands;
-            for (auto& g : groups) {
-                RBucket nb;
-                nb.term = g[0].first->term;
-                nb.key = g[0].first->key;
-                int64_t err = 0;
-                std::vector<const std::vector<RAgg>*> subl;
-                for (auto& pr : g) {
-                    nb.doc_count += pr.first->doc_count;
-                    if (err != -1) err = pr.second == -1 ? -1 : err + pr.second;
-                    subl.push_back(&pr.first->subs);
-                }
-                nb.subs = reduce_lists(subl);
-                nb.doc_count_error = err;
-                if (nb.doc_count_error != -1) nb.doc_count_error = sumErr == -1 ? -1 : sumErr - nb.doc_count_error;
-                if (nb.doc_count >= first.min_doc_count) cands.push_back(std::move(nb));
-            }
-            const size_t size = std::min<size_t>((size_t)std::max(first.required_size, 0), groups.size());
-            std::stable_sort(cands.begin(), cands.end(),
-                             [&](const RBucket& a, const RBucket& b) { return terms_cmp(first.order, a, b) < 0; });
-            for (size_t i = size; i < cands.size(); ++i) other += cands[i].doc_count;
-            if (cands.size() > size) cands.resize(size);
-            r.buckets = std::move(cands);
-            r.doc_count_error = sumErr == -1 ? -1 : (aggs.size() == 1 ? 0 : sumErr);
-            r.other_doc_count = other;
-            return r;
-        }
-        case ESGPU_AGG_HISTOGRAM:
-        case ESGPU_AGG_DATE_HISTOGRAM: {
-            std::map<int64_t, std::vector<const RBucket*>> byKey;
-            for (const RAgg* a : aggs) for (const RBucket& b : a->buckets) byKey[b.key].push_back(&b);
-            std::vector<RBucket> list;
-            for (auto& kv : byKey) {
-                RBucket nb;
-                nb.key = kv.first;
-                std::vector<const std::vector<RAgg>*> subl;
-                for (const RBucket* b : kv.second) { nb.doc_count += b->doc_count; subl.push_back(&b->subs); }
-                nb.subs = reduce_lists(subl);
-                if (nb.doc_count >= first.min_doc_count) list.push_back(std::move(nb));
-            }
-            if (first.min_doc_count == 0 && first.has_empty_info) {
-                auto next = [&](int64_t k) { return rounding_next(first.type, first.date_unit, first.interval, first.offset, k); };
-                auto empty = [&](int64_t k) { RBucket e; e.key = k; e.subs = first.empty_subs; return e; };
-                std::vector<RBucket> out;
-                if (list.empty()) {
-                    if (first.has_bmin && first.has_bmax)
-                        for (int64_t k = first.bmin; k <= first.bmax; k = next(k)) out.push_back(empty(k));
-                } else {
-                    if (first.has_bmin)
-                        for (int64_t k = first.bmin; k < list[0].key; k = next(k)) out.push_back(empty(k));
-                    for (size_t i = 0; i < list.size(); ++i) {
-                        if (i > 0) for (int64_t k = next(list[i - 1].key); k < list[i].key; k = next(k)) out.push_back(empty(k));
-                        out.push_back(list[i]);
-                    }
-                    if (first.has_bmax && first.bmax > list.back().key)
-                        for (int64_t k = next(list.back().key); k <= first.bmax; k = next(k)) out.push_back(empty(k));
-                }
-                list = std::move(out);
-            }
-            if (first.order == ESGPU_ORDER_KEY_DESC) std::reverse(list.begin(), list.end());
-            else if (first.order == ESGPU_ORDER_HCOUNT_ASC || first.order == ESGPU_ORDER_HCOUNT_DESC) {
-                const bool asc = first.order == ESGPU_ORDER_HCOUNT_ASC;
-                std::stable_sort(list.begin(), list.end(), [&](const RBucket& a, const RBucket& b) {
-                    if (a.doc_count != b.doc_count) return asc ? a.doc_count < b.doc_count : a.doc_count > b.doc_count;
-                    return a.key < b.key;
-                });
-            }
-            r.buckets = std::move(list);
-            return r;
-        }
-        case ESGPU_AGG_STATS:
-        case ESGPU_AGG_EXTENDED_STATS:
-        case ESGPU_AGG_AVG: {
-            int64_t count = 0;
-            double mn = INFINITY, mx = -INFINITY, sum = 0, sq = 0;
-            for (const RAgg* a : aggs) {
-                count += a->count;
-                mn = jmin(mn, a->min);
-                mx = jmax(mx, a->max);
-                sum += a->sum;
-                sq += a->sumsq;
-            }
-            r.count = count; r.min = mn; r.max = mx; r.sum = sum; r.sumsq = sq;
-            return r;
-        }
-        case ESGPU_AGG_CARDINALITY: {
-            bool any = false;
-            for (const RAgg* a : aggs) {
-                if (!a->hll_present) continue;
-                if (!any) {
-                    any = true;
-                    r.hll_present = true;
-                    r.precision = a->precision;
-                    r.hll_mode = 0;
-                    r.lc.clear();
-                    r.registers.clear();
-                }
-                hll_merge(r, *a);
-            }
-            if (!any) return first;
-            return r;
-        }
-    }
-    throw std::invalid_argument("reduce: unknown aggregation type");
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -377,16 +611,18 @@ namespace {
 struct J {
     std::string s;
     void raw(const char* t) { s += t; }
-    void str(const std::string& v) {
+    void str(const char* p, size_t n) {
         s += '"';
-        for (unsigned char c : v) {
+        for (size_t i = 0; i < n; ++i) {
+            const unsigned char c = (unsigned char)p[i];
             if (c == '"' || c == '\\') { s += '\\'; s += (char)c; }
             else if (c < 0x20) { char b[8]; snprintf(b, sizeof b, "\\u%04x", c); s += b; }
             else s += (char)c;
         }
         s += '"';
     }
-    void i64(int64_t v) { s += std::to_string(v); }
+    void str(const std::string& v) { str(v.data(), v.size()); }
+    void i64(int64_t v) { char b[24]; snprintf(b, sizeof b, "%lld", (long long)v); s += b; }
     void dbl(double v) {
         if (v != v) { s += "NaN"; return; }
         if (std::isinf(v)) { s += v > 0 ? "Infinity" : "-Infinity"; return; }
@@ -413,21 +649,30 @@ uint64_t fnv1a(const uint8_t* p, size_t n) {
     for (size_t i = 0; i < n; ++i) { h ^= p[i]; h *= 0x100000001b3ULL; }
     return h;
 }
-void write_list(J& j, const std::vector<RAgg>& aggs);
-void write_agg(J& j, const RAgg& a) {
+
+void write_instance(J& j, const Block& a, uint64_t i);
+
+void write_subs(J& j, const Block& a, uint64_t k) {
+    for (const Block& s : a.subs) {
+        j.raw(",");
+        j.key(s.name);
+        write_instance(j, s, k);
+    }
+}
+
+void write_instance(J& j, const Block& a, uint64_t i) {
     j.raw("{");
     switch (a.type) {
         case ESGPU_AGG_TERMS:
-            j.key("doc_count_error_upper_bound"); j.i64(a.doc_count_error); j.raw(",");
-            j.key("sum_other_doc_count"); j.i64(a.other_doc_count); j.raw(",");
+            j.key("doc_count_error_upper_bound"); j.i64(a.doc_count_error[i]); j.raw(",");
+            j.key("sum_other_doc_count"); j.i64(a.other_doc_count[i]); j.raw(",");
             j.key("buckets"); j.raw("[");
-            for (size_t i = 0; i < a.buckets.size(); ++i) {
-                const RBucket& b = a.buckets[i];
-                if (i) j.raw(",");
-                j.raw("{"); j.key("key"); j.str(b.term); j.raw(",");
-                j.key("doc_count"); j.i64(b.doc_count);
-                if (a.show_err) { j.raw(","); j.key("doc_count_error_upper_bound"); j.i64(b.doc_count_error); }
-                if (!b.subs.empty()) { j.raw(","); write_list(j, b.subs); }
+            for (uint64_t k = a.boff[i]; k < a.boff[i + 1]; ++k) {
+                if (k != a.boff[i]) j.raw(",");
+                j.raw("{"); j.key("key"); j.str(a.term_pool.data() + a.term_off[k], a.term_off[k + 1] - a.term_off[k]); j.raw(",");
+                j.key("doc_count"); j.i64(a.bcount[k]);
+                if (a.show_err) { j.raw(","); j.key("doc_count_error_upper_bound"); j.i64(a.berr[k]); }
+                write_subs(j, a, k);
                 j.raw("}");
             }
             j.raw("]");
@@ -435,36 +680,37 @@ void write_agg(J& j, const RAgg& a) {
         case ESGPU_AGG_HISTOGRAM:
         case ESGPU_AGG_DATE_HISTOGRAM:
             j.key("buckets"); j.raw("[");
-            for (size_t i = 0; i < a.buckets.size(); ++i) {
-                const RBucket& b = a.buckets[i];
-                if (i) j.raw(",");
+            for (uint64_t k = a.boff[i]; k < a.boff[i + 1]; ++k) {
+                if (k != a.boff[i]) j.raw(",");
                 j.raw("{");
-                if (a.type == ESGPU_AGG_DATE_HISTOGRAM) { j.key("key_as_string"); j.str(iso8601(b.key)); j.raw(","); }
-                j.key("key"); j.i64(b.key); j.raw(",");
-                j.key("doc_count"); j.i64(b.doc_count);
-                if (!b.subs.empty()) { j.raw(","); write_list(j, b.subs); }
+                if (a.type == ESGPU_AGG_DATE_HISTOGRAM) { j.key("key_as_string"); j.str(iso8601(a.key[k])); j.raw(","); }
+                j.key("key"); j.i64(a.key[k]); j.raw(",");
+                j.key("doc_count"); j.i64(a.bcount[k]);
+                write_subs(j, a, k);
                 j.raw("}");
             }
             j.raw("]");
             break;
         case ESGPU_AGG_AVG:
-            j.key("value"); j.opt(a.count != 0, a.sum / (double)a.count);
-            j.raw(","); j.key("_internal"); j.raw("{"); j.key("count"); j.i64(a.count); j.raw(",");
-            j.key("sum"); j.dbl(a.sum); j.raw("}");
+            j.key("value"); j.opt(a.count[i] != 0, a.sum[i] / (double)a.count[i]);
+            j.raw(","); j.key("_internal"); j.raw("{"); j.key("count"); j.i64(a.count[i]); j.raw(",");
+            j.key("sum"); j.dbl(a.sum[i]); j.raw("}");
             break;
         case ESGPU_AGG_STATS:
         case ESGPU_AGG_EXTENDED_STATS: {
-            const bool c = a.count != 0;
-            const double avg = a.sum / (double)a.count;
-            j.key("count"); j.i64(a.count); j.raw(",");
-            j.key("min"); j.opt(c, a.min); j.raw(",");
-            j.key("max"); j.opt(c, a.max); j.raw(",");
+            const int64_t cnt = a.count[i];
+            const double sum = a.sum[i], mn = a.min[i], mx = a.max[i], sq = a.sumsq[i];
+            const bool c = cnt != 0;
+            const double avg = sum / (double)cnt;
+            j.key("count"); j.i64(cnt); j.raw(",");
+            j.key("min"); j.opt(c, mn); j.raw(",");
+            j.key("max"); j.opt(c, mx); j.raw(",");
             j.key("avg"); j.opt(c, avg); j.raw(",");
-            j.key("sum"); j.opt(c, a.sum);
-            if (a.type == ESGPU_AGG_EXTENDED_STATS) {
-                const double var = (a.sumsq - ((a.sum * a.sum) / (double)a.count)) / (double)a.count;
+            j.key("sum"); j.opt(c, sum);
+            if (a.type == ESGPU_AGG_EXTENDED_STATS) {  // InternalExtendedStats.getVariance / getStdDeviationBound
+                const double var = (sq - ((sum * sum) / (double)cnt)) / (double)cnt;
                 const double sd = std::sqrt(var);
-                j.raw(","); j.key("sum_of_squares"); j.opt(c, a.sumsq);
+                j.raw(","); j.key("sum_of_squares"); j.opt(c, sq);
                 j.raw(","); j.key("variance"); j.opt(c, var);
                 j.raw(","); j.key("std_deviation"); j.opt(c, sd);
                 j.raw(","); j.key("std_deviation_bounds"); j.raw("{");
@@ -472,28 +718,30 @@ void write_agg(J& j, const RAgg& a) {
                 j.key("lower"); j.opt(c, avg - (sd * a.sigma)); j.raw("}");
             }
             j.raw(","); j.key("_internal"); j.raw("{");
-            j.key("count"); j.i64(a.count); j.raw(",");
-            j.key("sum"); j.dbl(a.sum); j.raw(",");
-            j.key("min"); j.dbl(a.min); j.raw(",");
-            j.key("max"); j.dbl(a.max);
-            if (a.type == ESGPU_AGG_EXTENDED_STATS) { j.raw(","); j.key("sum_of_squares"); j.dbl(a.sumsq); }
+            j.key("count"); j.i64(cnt); j.raw(",");
+            j.key("sum"); j.dbl(sum); j.raw(",");
+            j.key("min"); j.dbl(mn); j.raw(",");
+            j.key("max"); j.dbl(mx);
+            if (a.type == ESGPU_AGG_EXTENDED_STATS) { j.raw(","); j.key("sum_of_squares"); j.dbl(sq); }
             j.raw("}");
             break;
         }
         case ESGPU_AGG_CARDINALITY: {
-            j.key("value"); j.i64(hll_cardinality(a));
+            const bool present = a.hll_present[i];
+            const int mode = a.hll_mode[i];
+            j.key("value"); j.i64(hll_cardinality(a.precision, present, mode, a.regs[i].data(), a.lc[i].size()));
             j.raw(","); j.key("_internal"); j.raw("{");
-            j.key("present"); j.i64(a.hll_present ? 1 : 0);
-            if (a.hll_present) {
+            j.key("present"); j.i64(present ? 1 : 0);
+            if (present) {
                 char b[32];
                 j.raw(","); j.key("precision"); j.i64(a.precision);
-                j.raw(","); j.key("mode"); j.str(a.hll_mode ? "hll" : "lc");
-                if (a.hll_mode) {
-                    snprintf(b, sizeof b, "%016llx", (unsigned long long)fnv1a(a.registers.data(), a.registers.size()));
+                j.raw(","); j.key("mode"); j.str(mode ? "hll" : "lc");
+                if (mode) {
+                    snprintf(b, sizeof b, "%016llx", (unsigned long long)fnv1a(a.regs[i].data(), a.regs[i].size()));
                     j.raw(","); j.key("registers_fnv1a64"); j.str(b);
                 } else {
-                    j.raw(","); j.key("lc_size"); j.i64((int64_t)a.lc.size());
-                    snprintf(b, sizeof b, "%016llx", (unsigned long long)fnv1a((const uint8_t*)a.lc.data(), a.lc.size() * 4));
+                    j.raw(","); j.key("lc_size"); j.i64((int64_t)a.lc[i].size());
+                    snprintf(b, sizeof b, "%016llx", (unsigned long long)fnv1a((const uint8_t*)a.lc[i].data(), a.lc[i].size() * 4));
                     j.raw(","); j.key("lc_fnv1a64"); j.str(b);
                 }
             }
@@ -503,31 +751,32 @@ void write_agg(J& j, const RAgg& a) {
     }
     j.raw("}");
 }
-void write_list(J& j, const std::vector<RAgg>& aggs) {
+}  // namespace
+
+std::string to_json(const std::vector<Block>& aggs) {
+    J j;
+    j.raw("{");
     for (size_t i = 0; i < aggs.size(); ++i) {
         if (i) j.raw(",");
         j.key(aggs[i].name);
-        write_agg(j, aggs[i]);
+        write_instance(j, aggs[i], 0);
     }
-}
-}  // namespace
-
-std::string to_json(const std::vector<RAgg>& aggs) {
-    J j;
-    j.raw("{");
-    write_list(j, aggs);
     j.raw("}");
     return j.s;
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// stream format (AggregationStreams analogue): little-endian, length-prefixed, versioned
+// stream format (AggregationStreams analogue): little-endian, versioned, one record per block
 // ------------------------------------------------------------------------------------------------------------
 namespace {
 struct W {
     std::string& o;
     template <class T> void pod(const T& v) { o.append((const char*)&v, sizeof v); }
-    void str(const std::string& s) { pod<uint32_t>((uint32_t)s.size()); o.append(s); }
+    void str(const std::string& s) { pod<uint64_t>(s.size()); o.append(s); }
+    template <class T> void vec(const std::vector<T>& v) {
+        pod<uint64_t>(v.size());
+        if (!v.empty()) o.append((const char*)v.data(), v.size() * sizeof(T));
+    }
 };
 struct R {
     const uint8_t* p;
@@ -540,82 +789,112 @@ struct R {
         return v;
     }
     std::string str() {
-        const uint32_t len = pod<uint32_t>();
-        if (i + len > n) throw std::runtime_error("truncated stream");
-        std::string s((const char*)p + i, len);
+        const uint64_t len = pod<uint64_t>();
+        if (len > n - i) throw std::runtime_error("truncated stream");
+        std::string s((const char*)p + i, (size_t)len);
         i += len;
         return s;
     }
+    template <class T> void vec(std::vector<T>& v) {
+        const uint64_t len = pod<uint64_t>();
+        if (len > (n - i) / sizeof(T)) throw std::runtime_error("truncated stream");
+        v.resize(len);
+        if (len) std::memcpy(v.data(), p + i, len * sizeof(T));
+        i += len * sizeof(T);
+    }
 };
-void w_list(W& w, const std::vector<RAgg>& l);
-void w_agg(W& w, const RAgg& a) {
+void w_blocks(W& w, const std::vector<Block>& l);
+void w_block(W& w, const Block& a) {
     w.pod(a.type); w.pod(a.order); w.str(a.name);
-    w.pod(a.doc_count_error); w.pod(a.other_doc_count); w.pod(a.required_size); w.pod(a.shard_size);
-    w.pod(a.min_doc_count); w.pod(a.show_err); w.pod(a.keyed);
+    w.pod(a.required_size); w.pod(a.shard_size); w.pod(a.min_doc_count); w.pod(a.show_err); w.pod(a.keyed);
     w.pod<uint8_t>(a.has_empty_info); w.pod(a.date_unit); w.pod(a.interval); w.pod(a.offset);
     w.pod<uint8_t>(a.has_bmin); w.pod<uint8_t>(a.has_bmax); w.pod(a.bmin); w.pod(a.bmax);
-    w_list(w, a.empty_subs);
-    w.pod(a.count); w.pod(a.sum); w.pod(a.min); w.pod(a.max); w.pod(a.sumsq); w.pod(a.sigma);
-    w.pod<uint8_t>(a.hll_present); w.pod(a.precision); w.pod(a.hll_mode);
-    w.pod<uint64_t>(a.registers.size()); w.o.append((const char*)a.registers.data(), a.registers.size());
-    w.pod<uint64_t>(a.lc.size()); w.o.append((const char*)a.lc.data(), a.lc.size() * 4);
-    w.pod<uint64_t>(a.buckets.size());
-    for (const RBucket& b : a.buckets) {
-        w.pod(b.key); w.str(b.term); w.pod(b.doc_count); w.pod(b.doc_count_error);
-        w_list(w, b.subs);
-    }
+    w.pod(a.sigma); w.pod(a.precision); w.pod(a.n);
+    w.vec(a.doc_count_error); w.vec(a.other_doc_count); w.vec(a.boff); w.vec(a.key); w.vec(a.term_off);
+    w.str(a.term_pool); w.vec(a.bcount); w.vec(a.berr);
+    w_blocks(w, a.subs);
+    w_blocks(w, a.empty_subs);
+    w.vec(a.count); w.vec(a.sum); w.vec(a.min); w.vec(a.max); w.vec(a.sumsq);
+    w.vec(a.hll_present); w.vec(a.hll_mode);
+    w.pod<uint64_t>(a.regs.size());
+    for (auto& r : a.regs) w.vec(r);
+    w.pod<uint64_t>(a.lc.size());
+    for (auto& l : a.lc) w.vec(l);
 }
-void w_list(W& w, const std::vector<RAgg>& l) {
+void w_blocks(W& w, const std::vector<Block>& l) {
     w.pod<uint32_t>((uint32_t)l.size());
-    for (const RAgg& a : l) w_agg(w, a);
+    for (const Block& a : l) w_block(w, a);
 }
-void r_list(R& r, std::vector<RAgg>& l);
-void r_agg(R& r, RAgg& a) {
+void r_blocks(R& r, std::vector<Block>& l, int depth);
+void r_block(R& r, Block& a, int depth) {
+    if (depth > 64) throw std::runtime_error("stream nests too deep");
     a.type = r.pod<int32_t>(); a.order = r.pod<int32_t>(); a.name = r.str();
-    a.doc_count_error = r.pod<int64_t>(); a.other_doc_count = r.pod<int64_t>();
-    a.required_size = r.pod<int32_t>(); a.shard_size = r.pod<int32_t>();
-    a.min_doc_count = r.pod<int64_t>(); a.show_err = r.pod<int32_t>(); a.keyed = r.pod<int32_t>();
+    a.required_size = r.pod<int32_t>(); a.shard_size = r.pod<int32_t>(); a.min_doc_count = r.pod<int64_t>();
+    a.show_err = r.pod<int32_t>(); a.keyed = r.pod<int32_t>();
     a.has_empty_info = r.pod<uint8_t>(); a.date_unit = r.pod<int32_t>(); a.interval = r.pod<int64_t>();
     a.offset = r.pod<int64_t>();
     a.has_bmin = r.pod<uint8_t>(); a.has_bmax = r.pod<uint8_t>(); a.bmin = r.pod<int64_t>(); a.bmax = r.pod<int64_t>();
-    r_list(r, a.empty_subs);
-    a.count = r.pod<int64_t>(); a.sum = r.pod<double>(); a.min = r.pod<double>(); a.max = r.pod<double>();
-    a.sumsq = r.pod<double>(); a.sigma = r.pod<double>();
-    a.hll_present = r.pod<uint8_t>(); a.precision = r.pod<int32_t>(); a.hll_mode = r.pod<int32_t>();
-    const uint64_t nr = r.pod<uint64_t>();
-    if (r.i + nr > r.n) throw std::runtime_error("truncated stream");
-    a.registers.assign(r.p + r.i, r.p + r.i + nr); r.i += nr;
-    const uint64_t nl = r.pod<uint64_t>();
-    if (r.i + nl * 4 > r.n) throw std::runtime_error("truncated stream");
-    a.lc.resize(nl); std::memcpy(a.lc.data(), r.p + r.i, nl * 4); r.i += nl * 4;
-    const uint64_t nb = r.pod<uint64_t>();
-    a.buckets.resize(nb);
-    for (RBucket& b : a.buckets) {
-        b.key = r.pod<int64_t>(); b.term = r.str(); b.doc_count = r.pod<int64_t>(); b.doc_count_error = r.pod<int64_t>();
-        r_list(r, b.subs);
+    a.sigma = r.pod<double>(); a.precision = r.pod<int32_t>(); a.n = r.pod<uint64_t>();
+    r.vec(a.doc_count_error); r.vec(a.other_doc_count); r.vec(a.boff); r.vec(a.key); r.vec(a.term_off);
+    a.term_pool = r.str(); r.vec(a.bcount); r.vec(a.berr);
+    r_blocks(r, a.subs, depth + 1);
+    r_blocks(r, a.empty_subs, depth + 1);
+    r.vec(a.count); r.vec(a.sum); r.vec(a.min); r.vec(a.max); r.vec(a.sumsq);
+    r.vec(a.hll_present); r.vec(a.hll_mode);
+    a.regs.resize(r.pod<uint64_t>());
+    for (auto& x : a.regs) r.vec(x);
+    a.lc.resize(r.pod<uint64_t>());
+    for (auto& x : a.lc) r.vec(x);
+    // structural validation: a corrupt record must not produce out-of-bounds views
+    const bool bucket = a.is_bucket();
+    if (bucket) {
+        const uint64_t nb = a.boff.empty() ? 0 : a.boff.back();
+        if (a.boff.size() != a.n + 1 || a.key.size() != nb || a.bcount.size() != nb || a.berr.size() != nb ||
+            a.term_off.size() != nb + 1 || a.doc_count_error.size() != a.n || a.other_doc_count.size() != a.n ||
+            (nb && a.term_off.back() != a.term_pool.size()))
+            throw std::runtime_error("inconsistent bucket block");
+        for (size_t k = 0; k + 1 < a.boff.size(); ++k) if (a.boff[k] > a.boff[k + 1]) throw std::runtime_error("bad offsets");
+        for (size_t k = 0; k + 1 < a.term_off.size(); ++k) if (a.term_off[k] > a.term_off[k + 1]) throw std::runtime_error("bad offsets");
+        for (const Block& s : a.subs) if (s.n != nb) throw std::runtime_error("sub-aggregation instance count mismatch");
+        if (a.has_empty_info && a.empty_subs.size() != a.subs.size()) throw std::runtime_error("missing empty-bucket prototypes");
+        for (size_t j = 0; j < a.empty_subs.size(); ++j)
+            if (a.empty_subs[j].n != 1 || a.empty_subs[j].type != a.subs[j].type) throw std::runtime_error("bad empty-bucket prototype");
+    } else if (a.type == ESGPU_AGG_CARDINALITY) {
+        if (a.hll_present.size() != a.n || a.hll_mode.size() != a.n || a.regs.size() != a.n || a.lc.size() != a.n)
+            throw std::runtime_error("inconsistent cardinality block");
+        if (a.precision < 4 || a.precision > 18) throw std::runtime_error("bad precision");
+        for (uint64_t i = 0; i < a.n; ++i)
+            if (a.hll_present[i] && a.hll_mode[i] && a.regs[i].size() != ((size_t)1 << a.precision))
+                throw std::runtime_error("bad register array");
+    } else if (a.count.size() != a.n || a.sum.size() != a.n || a.min.size() != a.n || a.max.size() != a.n ||
+               a.sumsq.size() != a.n) {
+        throw std::runtime_error("inconsistent metric block");
     }
 }
-void r_list(R& r, std::vector<RAgg>& l) {
+void r_blocks(R& r, std::vector<Block>& l, int depth) {
     const uint32_t n = r.pod<uint32_t>();
+    if (n > 4096) throw std::runtime_error("too many aggregations");
     l.resize(n);
-    for (RAgg& a : l) r_agg(r, a);
+    for (Block& a : l) r_block(r, a, depth);
 }
 const uint32_t kStreamMagic = 0x45534750;  // "ESGP"
+const uint32_t kStreamVersion = 2;
 }  // namespace
 
-void serialize(const std::vector<RAgg>& aggs, std::string& out) {
+void serialize(const std::vector<Block>& aggs, std::string& out) {
     out.clear();
     W w{out};
     w.pod(kStreamMagic);
-    w.pod<uint32_t>(ESGPU_ABI_VERSION);
-    w_list(w, aggs);
+    w.pod(kStreamVersion);
+    w_blocks(w, aggs);
 }
 
-bool deserialize(const uint8_t* p, size_t n, std::vector<RAgg>& out) {
+bool deserialize(const uint8_t* p, size_t n, std::vector<Block>& out) {
     R r{p, n};
-    if (r.pod<uint32_t>() != kStreamMagic) return false;
-    if (r.pod<uint32_t>() != ESGPU_ABI_VERSION) return false;
-    r_list(r, out);
+    if (n < 8 || r.pod<uint32_t>() != kStreamMagic) return false;
+    if (r.pod<uint32_t>() != kStreamVersion) return false;
+    r_blocks(r, out, 0);
+    for (const Block& b : out) if (b.n != 1) throw std::runtime_error("top-level aggregations carry one instance");
     return true;
 }
 
@@ -624,15 +903,16 @@ bool deserialize(const uint8_t* p, size_t n, std::vector<RAgg>& out) {
 // ------------------------------------------------------------------------------------------------------------
 ResultHolder* holder_of(const esgpu_result* r) { return reinterpret_cast<ResultHolder*>(const_cast<esgpu_result*>(r)); }
 
-static void export_list(ResultHolder& h, std::vector<RAgg>& src, esgpu_agg_result** out, int32_t* n);
+namespace {
+template <class T> const T* ptr(const std::vector<T>& v) { return v.empty() ? nullptr : v.data(); }
 
-static void export_agg(ResultHolder& h, RAgg& a, esgpu_agg_result& o) {
+const esgpu_agg_block* export_blocks(ResultHolder& h, const std::vector<Block>& src);
+
+void export_block(ResultHolder& h, const Block& a, esgpu_agg_block& o) {
     std::memset(&o, 0, sizeof o);
     o.type = a.type;
     o.order = a.order;
     o.name = a.name.c_str();
-    o.doc_count_error = a.doc_count_error;
-    o.other_doc_count = a.other_doc_count;
     o.required_size = a.required_size;
     o.shard_size = a.shard_size;
     o.min_doc_count = a.min_doc_count;
@@ -646,53 +926,68 @@ static void export_agg(ResultHolder& h, RAgg& a, esgpu_agg_result& o) {
     o.has_extended_bounds_max = a.has_bmax;
     o.extended_bounds_min = a.bmin;
     o.extended_bounds_max = a.bmax;
-    export_list(h, a.empty_subs, &o.empty_subs, &o.nempty_subs);
-    o.count = a.count;
-    o.sum = a.sum;
-    o.min = a.min;
-    o.max = a.max;
-    o.sum_of_squares = a.sumsq;
     o.sigma = a.sigma;
-    o.hll_present = a.hll_present;
     o.precision = a.precision;
-    o.hll_mode = a.hll_mode;
-    o.registers = a.registers.empty() ? nullptr : a.registers.data();
-    o.lc_hashes = a.lc.empty() ? nullptr : a.lc.data();
-    o.lc_size = (int64_t)a.lc.size();
-    o.nbuckets = (int64_t)a.buckets.size();
-    if (!a.buckets.empty()) {
-        std::unique_ptr<esgpu_bucket[]> bb(new esgpu_bucket[a.buckets.size()]);
-        for (size_t i = 0; i < a.buckets.size(); ++i) {
-            RBucket& b = a.buckets[i];
-            esgpu_bucket& ob = bb[i];
-            std::memset(&ob, 0, sizeof ob);
-            ob.key = b.key;
-            ob.key_bytes = (const uint8_t*)b.term.data();
-            ob.key_len = (int32_t)b.term.size();
-            ob.doc_count = b.doc_count;
-            ob.doc_count_error = b.doc_count_error;
-            export_list(h, b.subs, &ob.subs, &ob.nsubs);
+    o.nsubs = (int32_t)a.subs.size();
+    o.n_instances = a.n;
+    o.doc_count_error = ptr(a.doc_count_error);
+    o.other_doc_count = ptr(a.other_doc_count);
+    o.bucket_offsets = ptr(a.boff);
+    o.n_buckets = a.nbuckets();
+    o.keys = ptr(a.key);
+    o.term_offsets = ptr(a.term_off);
+    o.term_bytes = (const uint8_t*)a.term_pool.data();
+    o.doc_counts = ptr(a.bcount);
+    o.bucket_doc_count_errors = ptr(a.berr);
+    o.subs = export_blocks(h, a.subs);
+    o.empty_subs = export_blocks(h, a.empty_subs);
+    o.count = ptr(a.count);
+    o.sum = ptr(a.sum);
+    o.min = ptr(a.min);
+    o.max = ptr(a.max);
+    o.sum_of_squares = ptr(a.sumsq);
+    if (a.type == ESGPU_AGG_CARDINALITY && a.n) {
+        std::unique_ptr<int32_t[]> pres(new int32_t[a.n]);
+        std::unique_ptr<const uint8_t*[]> rp(new const uint8_t*[a.n]);
+        std::unique_ptr<const uint32_t*[]> lp(new const uint32_t*[a.n]);
+        std::unique_ptr<int64_t[]> ls(new int64_t[a.n]);
+        for (uint64_t i = 0; i < a.n; ++i) {
+            pres[i] = a.hll_present[i];
+            rp[i] = a.regs[i].empty() ? nullptr : a.regs[i].data();
+            lp[i] = a.lc[i].empty() ? nullptr : a.lc[i].data();
+            ls[i] = (int64_t)a.lc[i].size();
         }
-        o.buckets = bb.get();
-        h.bucket_blocks.push_back(std::move(bb));
+        o.hll_present = pres.get();
+        o.hll_mode = ptr(a.hll_mode);
+        o.registers = rp.get();
+        o.lc_hashes = lp.get();
+        o.lc_sizes = ls.get();
+        h.present32.push_back(std::move(pres));
+        h.reg_ptrs.push_back(std::move(rp));
+        h.lc_ptrs.push_back(std::move(lp));
+        h.lc_sizes.push_back(std::move(ls));
     }
 }
 
-static void export_list(ResultHolder& h, std::vector<RAgg>& src, esgpu_agg_result** out, int32_t* n) {
-    *n = (int32_t)src.size();
-    *out = nullptr;
-    if (src.empty()) return;
-    std::unique_ptr<esgpu_agg_result[]> blk(new esgpu_agg_result[src.size()]);
-    for (size_t i = 0; i < src.size(); ++i) export_agg(h, src[i], blk[i]);
-    *out = blk.get();
-    h.agg_blocks.push_back(std::move(blk));
+const esgpu_agg_block* export_blocks(ResultHolder& h, const std::vector<Block>& src) {
+    if (src.empty()) return nullptr;
+    std::unique_ptr<esgpu_agg_block[]> blk(new esgpu_agg_block[src.size()]);
+    for (size_t i = 0; i < src.size(); ++i) export_block(h, src[i], blk[i]);
+    const esgpu_agg_block* p = blk.get();
+    h.views.push_back(std::move(blk));
+    return p;
 }
+}  // namespace
 
 void ResultHolder::export_view() {
-    agg_blocks.clear();
-    bucket_blocks.clear();
+    views.clear();
+    reg_ptrs.clear();
+    lc_ptrs.clear();
+    lc_sizes.clear();
+    present32.clear();
     std::memset(&pub, 0, sizeof pub);
-    export_list(*this, aggs, &pub.aggs, &pub.naggs);
+    pub.aggs = export_blocks(*this, aggs);
+    pub.naggs = (int32_t)aggs.size();
 }
 
 }  // namespace esgpu

@@ -1,5 +1,11 @@
-// esgpu_results.hpp — host-side InternalAggregation model of libesgpu.so (StringTerms, InternalHistogram,
-// InternalStats, InternalExtendedStats, InternalAvg, InternalCardinality), its reduce, JSON and stream formats.
+// esgpu_results.hpp — columnar InternalAggregations of libesgpu.so and their reduce / JSON / stream formats.
+//
+// A Block holds ONE aggregation (one spec of the request) for `n` parent buckets at once: instance i is the
+// InternalAggregation that the reference would build for parent bucket i (StringTerms, InternalHistogram,
+// InternalStats, InternalExtendedStats, InternalAvg, InternalCardinality).  Bucket aggregations keep their buckets
+// in flat arrays ([boff[i], boff[i+1]) belong to instance i) and every sub-aggregation is again a Block with one
+// instance per bucket.  The north-star result (10 terms x 720 hours x stats) is 3 blocks of flat arrays instead of
+// ~7,200 objects, which keeps build / reduce / transport in the tens of microseconds.
 #pragma once
 
 #include <stdint.h>
@@ -12,70 +18,86 @@
 
 namespace esgpu {
 
-struct RAgg;
-
-struct RBucket {
-    int64_t key = 0;          // histogram key / terms ordinal in its shard
-    std::string term;         // terms key bytes
-    int64_t doc_count = 0;
-    int64_t doc_count_error = 0;
-    std::vector<RAgg> subs;
-};
-
-struct RAgg {
+struct Block {
+    // ---- request parameters (shared by every instance of the spec) ----
     int32_t type = 0;
     int32_t order = 0;
     std::string name;
-    // bucket aggregations
-    std::vector<RBucket> buckets;
-    int64_t doc_count_error = 0;
-    int64_t other_doc_count = 0;
     int32_t required_size = 10;
     int32_t shard_size = 10;
     int64_t min_doc_count = 1;
     int32_t show_err = 0;
     int32_t keyed = 0;
-    // histogram EmptyBucketInfo
-    bool has_empty_info = false;
+    bool has_empty_info = false;  // histogram EmptyBucketInfo (min_doc_count == 0)
     int32_t date_unit = 0;
     int64_t interval = 1;
     int64_t offset = 0;
     bool has_bmin = false, has_bmax = false;
     int64_t bmin = 0, bmax = 0;
-    std::vector<RAgg> empty_subs;
-    // metrics
-    int64_t count = 0;
-    double sum = 0.0, min = 0.0, max = 0.0, sumsq = 0.0, sigma = 2.0;
-    // cardinality
-    bool hll_present = false;
+    double sigma = 2.0;
     int32_t precision = 14;
-    int32_t hll_mode = 0;            // 0 linear counting, 1 hyperloglog
-    std::vector<uint8_t> registers;  // 2^precision
-    std::vector<uint32_t> lc;        // distinct encoded hashes, ascending
+
+    uint64_t n = 0;  // instances
+
+    // ---- bucket aggregations ----
+    std::vector<int64_t> doc_count_error;  // [n]
+    std::vector<int64_t> other_doc_count;  // [n]
+    std::vector<uint64_t> boff;            // [n + 1]
+    std::vector<int64_t> key;              // [nb] histogram key / terms ordinal in the producing shard
+    std::vector<uint64_t> term_off;        // [nb + 1] (terms)
+    std::string term_pool;
+    std::vector<int64_t> bcount;           // [nb] doc_count
+    std::vector<int64_t> berr;             // [nb] bucket doc_count_error
+    std::vector<Block> subs;               // each with n == nb
+    std::vector<Block> empty_subs;         // prototypes, n == 1
+
+    // ---- numeric metrics [n] ----
+    std::vector<int64_t> count;
+    std::vector<double> sum, min, max, sumsq;
+
+    // ---- cardinality [n] ----
+    std::vector<uint8_t> hll_present;
+    std::vector<int32_t> hll_mode;
+    std::vector<std::vector<uint8_t>> regs;
+    std::vector<std::vector<uint32_t>> lc;  // ascending encoded hashes
+
+    bool is_bucket() const { return type == ESGPU_AGG_TERMS || type == ESGPU_AGG_HISTOGRAM || type == ESGPU_AGG_DATE_HISTOGRAM; }
+    uint64_t nbuckets() const { return boff.empty() ? 0 : boff.back(); }
+    std::string term(uint64_t b) const { return term_pool.substr(term_off[b], term_off[b + 1] - term_off[b]); }
+
+    // an empty block with this block's parameters and sub-structure (no instances)
+    Block like() const;
+    // append instance `i` of `src` (same spec) to this block, deep (sub-blocks included)
+    void append_instance(const Block& src, uint64_t i);
+    // append an empty instance (buildEmptyAggregation) of this spec
+    void append_empty();
 };
 
-// rounding helpers for EmptyBucketInfo (common/rounding/*)
+// rounding helper for EmptyBucketInfo (common/rounding/*)
 int64_t rounding_next(int32_t type, int32_t date_unit, int64_t interval, int64_t offset, int64_t value);
 
 // HyperLogLogPlusPlus
 int hll_precision_from_threshold(int64_t count);
-int64_t hll_cardinality(const RAgg& a);
-void hll_merge(RAgg& into, const RAgg& other);  // InternalCardinality.merge (into has hll_present)
+int64_t hll_cardinality(int precision, bool present, int mode, const uint8_t* regs, size_t nlc);
 
 // InternalAggregations.reduce over shard lists in shard order
-std::vector<RAgg> reduce_lists(const std::vector<const std::vector<RAgg>*>& lists);
+std::vector<Block> reduce_lists(const std::vector<const std::vector<Block>*>& lists);
 
-std::string to_json(const std::vector<RAgg>& aggs);
-void serialize(const std::vector<RAgg>& aggs, std::string& out);
-bool deserialize(const uint8_t* p, size_t n, std::vector<RAgg>& out);
+std::string to_json(const std::vector<Block>& aggs);
+void serialize(const std::vector<Block>& aggs, std::string& out);
+bool deserialize(const uint8_t* p, size_t n, std::vector<Block>& out);
 
 // owning wrapper behind the public esgpu_result (pub must stay the first member)
 struct ResultHolder {
     esgpu_result pub;
-    std::vector<RAgg> aggs;
-    // storage for the exported C view
-    std::vector<std::unique_ptr<esgpu_agg_result[]>> agg_blocks;
-    std::vector<std::unique_ptr<esgpu_bucket[]>> bucket_blocks;
+    std::vector<Block> aggs;
+    std::vector<std::unique_ptr<esgpu_agg_block[]>> views;
+    std::vector<std::unique_ptr<const uint8_t*[]>> reg_ptrs;
+    std::vector<std::unique_ptr<const uint32_t*[]>> lc_ptrs;
+    std::vector<std::unique_ptr<int64_t[]>> lc_sizes;
+    std::vector<std::unique_ptr<int32_t[]>> present32;
+    std::string json;  // rendered on first esgpu_result_to_json
+    bool json_valid = false;
     void export_view();
 };
 

@@ -1102,6 +1102,7 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
     H.lc_set = pl.lc_set.as<unsigned int>();
     H.lc_count = pl.lc_count.as<unsigned int>();
     H.nonzero = pl.lc_count.as<unsigned int>() + 1;
+    H.floor = pl.lc_count.as<unsigned int>() + 2;
     H.lc_mask = pl.lc_mask;
     H.lc_threshold = pl.lc_threshold;
     if (H.n_docs == 0) return false;
@@ -1218,18 +1219,19 @@ static std::string plan_term(const esgpu_plan* p, const Pipeline& pl, uint64_t o
     return std::to_string(ord);
 }
 
-static RAgg empty_metric(const SpecNode& n) {
-    RAgg r;
+// ---- result blocks (columnar InternalAggregations, see esgpu_results.hpp) ----
+static Block metric_shell(const SpecNode& n) {
+    Block r;
     r.type = n.s.type;
     r.name = n.name;
-    r.count = 0; r.sum = 0.0; r.min = INFINITY; r.max = -INFINITY; r.sumsq = 0.0;
     r.sigma = n.s.sigma;
     return r;
 }
 
-static RAgg hist_base(const esgpu_plan* p, int spec, const std::vector<RAgg>& empty_subs) {
+// histogram spec with the given sub-aggregation prototypes (each an n == 1 empty instance)
+static Block hist_shell(const esgpu_plan* p, int spec, const std::vector<Block>& protos) {
     const SpecNode& n = p->specs[spec];
-    RAgg r;
+    Block r;
     r.type = n.s.type;
     r.name = n.name;
     r.order = n.s.order;
@@ -1238,20 +1240,23 @@ static RAgg hist_base(const esgpu_plan* p, int spec, const std::vector<RAgg>& em
     r.date_unit = n.s.type == ESGPU_AGG_DATE_HISTOGRAM ? n.s.date_unit : 0;
     r.interval = n.s.interval;
     r.offset = n.s.offset;
+    r.boff.assign(1, 0);
+    r.term_off.assign(1, 0);
+    for (const Block& b : protos) r.subs.push_back(b.like());
     if (n.s.min_doc_count == 0) {  // EmptyBucketInfo
         r.has_empty_info = true;
         r.has_bmin = n.s.has_extended_bounds_min;
         r.has_bmax = n.s.has_extended_bounds_max;
         r.bmin = n.s.extended_bounds_min;
         r.bmax = n.s.extended_bounds_max;
-        r.empty_subs = empty_subs;
+        r.empty_subs = protos;
     }
     return r;
 }
 
-static RAgg terms_base(const esgpu_plan* p, int spec) {
+static Block terms_shell(const esgpu_plan* p, int spec, const std::vector<Block>& protos) {
     const SpecNode& n = p->specs[spec];
-    RAgg r;
+    Block r;
     r.type = ESGPU_AGG_TERMS;
     r.name = n.name;
     r.order = n.s.order;
@@ -1259,7 +1264,24 @@ static RAgg terms_base(const esgpu_plan* p, int spec) {
     r.shard_size = n.s.shard_size;
     r.min_doc_count = n.s.min_doc_count;
     r.show_err = n.s.show_term_doc_count_error;
+    r.boff.assign(1, 0);
+    r.term_off.assign(1, 0);
+    for (const Block& b : protos) r.subs.push_back(b.like());
     return r;
+}
+
+static void begin_instance(Block& b, int64_t other) {
+    ++b.n;
+    b.doc_count_error.push_back(0);
+    b.other_doc_count.push_back(other);
+}
+static void end_instance(Block& b) { b.boff.push_back(b.key.size()); }
+static void push_bucket(Block& b, int64_t key, const std::string* term, int64_t count) {
+    b.key.push_back(key);
+    if (term) b.term_pool += *term;
+    b.term_off.push_back(b.term_pool.size());
+    b.bcount.push_back(count);
+    b.berr.push_back(0);
 }
 
 // host views (pinned staging buffers of the plan) of one grid row set
@@ -1272,32 +1294,37 @@ struct HostCells {
     const double* sq = nullptr;
 };
 
-static std::vector<RAgg> metric_results(const esgpu_plan* p, const Pipeline& pl, const HostCells& h, size_t c) {
-    std::vector<RAgg> out;
-    for (int m : pl.metrics) {
-        const SpecNode& n = p->specs[m];
-        RAgg r = empty_metric(n);
+// one instance of every leaf metric of the pipeline, from grid cell c, appended to blocks[0..]
+static void append_metrics(const esgpu_plan* p, const Pipeline& pl, const HostCells& h, size_t c, std::vector<Block>& blocks) {
+    for (size_t j = 0; j < pl.metrics.size(); ++j) {
+        const int32_t type = p->specs[pl.metrics[j]].s.type;
+        Block& r = blocks[j];
         const uint64_t vc = pl.vcnt_mode ? h.vcnt[c] : h.cnt[c];
-        r.count = (int64_t)vc;
+        double sum = 0.0, mn = INFINITY, mx = -INFINITY, sq = 0.0;
         if (vc > 0) {
-            r.sum = h.sum[c];
-            if (pl.met >= 2) {
+            sum = h.sum[c];
+            if (pl.met >= 2 && type != ESGPU_AGG_AVG) {
                 const uint64_t emn = h.mn[c], emx = h.mx[c];
-                if (emn < kEncNegInf || emx > kEncPosInf) { r.min = NAN; r.max = NAN; }  // a NaN value was collected
-                else { r.min = unsortable(emn); r.max = unsortable(emx); }
+                if (emn < kEncNegInf || emx > kEncPosInf) { mn = NAN; mx = NAN; }  // a NaN value was collected
+                else { mn = unsortable(emn); mx = unsortable(emx); }
             }
-            if (pl.met >= 3) r.sumsq = h.sq[c];
+            if (pl.met >= 3 && type == ESGPU_AGG_EXTENDED_STATS) sq = h.sq[c];
         }
-        if (n.s.type == ESGPU_AGG_AVG) { r.min = INFINITY; r.max = -INFINITY; r.sumsq = 0.0; }
-        if (n.s.type == ESGPU_AGG_STATS) r.sumsq = 0.0;
-        out.push_back(std::move(r));
+        ++r.n;
+        r.count.push_back((int64_t)vc);
+        r.sum.push_back(sum);
+        r.min.push_back(mn);
+        r.max.push_back(mx);
+        r.sumsq.push_back(sq);
     }
-    return out;
 }
 
-static std::vector<RAgg> empty_metrics(const esgpu_plan* p, const Pipeline& pl) {
-    std::vector<RAgg> out;
-    for (int m : pl.metrics) out.push_back(empty_metric(p->specs[m]));
+static std::vector<Block> metric_protos(const esgpu_plan* p, const Pipeline& pl) {
+    std::vector<Block> out;
+    for (int m : pl.metrics) {
+        out.push_back(metric_shell(p->specs[m]));
+        out.back().append_empty();
+    }
     return out;
 }
 
@@ -1353,31 +1380,34 @@ static std::vector<TermPick> select_terms(const esgpu_agg_spec& s, const unsigne
     return cands;
 }
 
-static RAgg build_grid(esgpu_plan* p, Pipeline& pl) {
+static Block build_grid(esgpu_plan* p, Pipeline& pl) {
     hipStream_t st = p->stream;
-    const bool ORD = pl.term_spec >= 0, HIST = pl.hist_spec >= 0;
+    const bool ORD = pl.term_spec >= 0;
+    const std::vector<Block> leaf = metric_protos(p, pl);  // empty metric instances (n == 1)
     // ---- top-level metric ----
     if (pl.outer < 0) {
-        const SpecNode& n = p->specs[pl.root];
-        if (!pl.allocated) return empty_metric(n);
+        Block r = leaf[0].like();
+        if (!pl.allocated) { r.append_empty(); return r; }
         HostCells h;
         d2h(p, h, pl, 1, pl.g_cnt.p, pl.g_vcnt.p, pl.g_sum.p, pl.g_min.p, pl.g_max.p, pl.g_sq.p);
-        return metric_results(p, pl, h, 0)[0];
+        std::vector<Block> one{std::move(r)};
+        append_metrics(p, pl, h, 0, one);
+        return std::move(one[0]);
     }
     const bool terms_outer = pl.outer == pl.term_spec;
-    // prototypes for empty sub-aggregations (bucketEmptyAggregations)
-    std::vector<RAgg> inner_empty;  // what an empty outer bucket carries
-    std::vector<RAgg> leaf_empty = empty_metrics(p, pl);
+    // what an outer bucket carries as sub-aggregations (prototypes = bucketEmptyAggregations)
+    std::vector<Block> inner_protos;
     if (pl.inner >= 0) {
-        if (p->specs[pl.inner].s.type == ESGPU_AGG_TERMS) inner_empty.push_back(terms_base(p, pl.inner));
-        else inner_empty.push_back(hist_base(p, pl.inner, leaf_empty));
+        Block in = p->specs[pl.inner].s.type == ESGPU_AGG_TERMS ? terms_shell(p, pl.inner, leaf) : hist_shell(p, pl.inner, leaf);
+        in.append_empty();
+        inner_protos.push_back(std::move(in));
     } else {
-        inner_empty = leaf_empty;
+        inner_protos = leaf;
     }
     if (terms_outer) {
         const SpecNode& tn = p->specs[pl.outer];
-        RAgg r = terms_base(p, pl.outer);
-        if (!pl.allocated) return r;  // unmapped: buildEmptyAggregation
+        Block r = terms_shell(p, pl.outer, inner_protos);
+        if (!pl.allocated) { r.append_empty(); return r; }  // unmapped: buildEmptyAggregation
         const uint32_t T = pl.T, H = pl.H;
         // outer doc counts per ordinal (term_totals over the [H][T] grid unless counted separately)
         const unsigned long long* dcnt = pl.g_cnt.as<unsigned long long>();
@@ -1464,34 +1494,32 @@ static RAgg build_grid(esgpu_plan* p, Pipeline& pl) {
                 other -= top[i].count;
             }
         }
-        r.other_doc_count = other;
+        begin_instance(r, other);
         for (uint32_t i = 0; i < k; ++i) {
-            RBucket b;
-            b.key = top[i].ord;
-            b.term = plan_term(p, pl, top[i].ord);
-            b.doc_count = top[i].count;
-            if (b.doc_count == 0) b.subs = inner_empty;  // bucketEmptyAggregations
-            else if (pl.inner < 0) b.subs = metric_results(p, pl, h, i);
-            else {
-                RAgg hr = hist_base(p, pl.inner, leaf_empty);
+            const std::string term = plan_term(p, pl, top[i].ord);
+            push_bucket(r, top[i].ord, &term, top[i].count);
+            if (top[i].count == 0) {  // bucketEmptyAggregations
+                for (Block& sb : r.subs) sb.append_empty();
+            } else if (pl.inner < 0) {
+                append_metrics(p, pl, h, i, r.subs);
+            } else {
+                Block& hr = r.subs[0];
+                begin_instance(hr, 0);
                 for (uint32_t s = 0; s < H; ++s) {
                     const size_t c = (size_t)i * H + s;
                     if (h.cnt[c] == 0) continue;
-                    RBucket hb;
-                    hb.key = (pl.key0 + (int64_t)s) * pl.interval + pl.offset;
-                    hb.doc_count = (int64_t)h.cnt[c];
-                    hb.subs = metric_results(p, pl, h, c);
-                    hr.buckets.push_back(std::move(hb));
+                    push_bucket(hr, (pl.key0 + (int64_t)s) * pl.interval + pl.offset, nullptr, (int64_t)h.cnt[c]);
+                    append_metrics(p, pl, h, c, hr.subs);
                 }
-                b.subs.push_back(std::move(hr));
+                end_instance(hr);
             }
-            r.buckets.push_back(std::move(b));
         }
+        end_instance(r);
         return r;
     }
     // ---- histogram outer (optionally terms inner) ----
-    RAgg r = hist_base(p, pl.outer, inner_empty);
-    if (!pl.allocated) return r;
+    Block r = hist_shell(p, pl.outer, inner_protos);
+    if (!pl.allocated) { r.append_empty(); return r; }
     const uint32_t T = pl.T, H = pl.H;
     HostCells h;
     d2h(p, h, pl, (size_t)T * H, pl.g_cnt.p, pl.g_vcnt.p, pl.g_sum.p, pl.g_min.p, pl.g_max.p, pl.g_sq.p);
@@ -1500,49 +1528,49 @@ static RAgg build_grid(esgpu_plan* p, Pipeline& pl) {
         ocnt.resize(H);
         HIPX(hipMemcpy(ocnt.data(), pl.g_ocnt.p, (size_t)H * 8, hipMemcpyDeviceToHost));
     }
+    begin_instance(r, 0);
     for (uint32_t s = 0; s < H; ++s) {
         uint64_t dc = 0;
         if (!ORD) dc = h.cnt[s];
         else if (pl.ocnt_mode == OCNT_HIST) dc = ocnt[s];
         else for (uint32_t t = 0; t < T; ++t) dc += h.cnt[(size_t)s * T + t];
         if (dc == 0) continue;
-        RBucket b;
-        b.key = (pl.key0 + (int64_t)s) * pl.interval + pl.offset;
-        b.doc_count = (int64_t)dc;
-        if (!ORD) b.subs = metric_results(p, pl, h, s);
-        else {
-            const SpecNode& tn = p->specs[pl.inner];
-            RAgg tr = terms_base(p, pl.inner);
-            int64_t other = 0;
-            std::vector<TermPick> top = select_terms(tn.s, h.cnt + (size_t)s * T, (uint32_t)pl.value_count, &other);
-            tr.other_doc_count = other;
-            for (auto& tp : top) {
-                RBucket tb;
-                tb.key = tp.ord;
-                tb.term = plan_term(p, pl, tp.ord);
-                tb.doc_count = tp.count;
-                tb.subs = tp.count == 0 ? leaf_empty : metric_results(p, pl, h, (size_t)s * T + tp.ord);
-                tr.buckets.push_back(std::move(tb));
-            }
-            b.subs.push_back(std::move(tr));
+        push_bucket(r, (pl.key0 + (int64_t)s) * pl.interval + pl.offset, nullptr, (int64_t)dc);
+        if (!ORD) {
+            append_metrics(p, pl, h, s, r.subs);
+            continue;
         }
-        r.buckets.push_back(std::move(b));
+        const SpecNode& tn = p->specs[pl.inner];
+        Block& tr = r.subs[0];
+        int64_t other = 0;
+        std::vector<TermPick> top = select_terms(tn.s, h.cnt + (size_t)s * T, (uint32_t)pl.value_count, &other);
+        begin_instance(tr, other);
+        for (auto& tp : top) {
+            const std::string term = plan_term(p, pl, tp.ord);
+            push_bucket(tr, tp.ord, &term, tp.count);
+            if (tp.count == 0) for (Block& sb : tr.subs) sb.append_empty();
+            else append_metrics(p, pl, h, (size_t)s * T + tp.ord, tr.subs);
+        }
+        end_instance(tr);
     }
+    end_instance(r);
     return r;
 }
 
-static RAgg build_cardinality(esgpu_plan* p, Pipeline& pl) {
+static Block build_cardinality(esgpu_plan* p, Pipeline& pl) {
     const SpecNode& n = p->specs[pl.root];
-    RAgg r;
+    Block r;
     r.type = ESGPU_AGG_CARDINALITY;
     r.name = n.name;
     r.precision = pl.p;
-    if (!pl.allocated || !pl.any_value) return r;  // counts == null
-    r.hll_present = true;
-    r.hll_mode = pl.hll_mode;
-    r.lc = pl.h_lc;
-    r.registers = pl.h_regs;
-    if (hll_cardinality(r) == 0) { r.hll_present = false; r.lc.clear(); r.registers.clear(); }  // CardinalityAggregator:141-143
+    r.append_empty();  // counts == null
+    if (!pl.allocated || !pl.any_value) return r;
+    // CardinalityAggregator:141-143 — an all-zero sketch is reported as "no counts"
+    if (hll_cardinality(pl.p, true, pl.hll_mode, pl.h_regs.data(), pl.h_lc.size()) == 0) return r;
+    r.hll_present[0] = 1;
+    r.hll_mode[0] = pl.hll_mode;
+    r.lc[0] = pl.h_lc;
+    r.regs[0] = pl.h_regs;
     return r;
 }
 
@@ -1618,7 +1646,7 @@ extern "C" int esgpu_result_free(esgpu_result* r) {
 extern "C" int esgpu_reduce(const esgpu_result* const* shards, int32_t n, esgpu_result** out) {
     return guarded([&] {
         require(out && n >= 1 && shards, ESGPU_ERR_INVALID, "reduce needs at least one shard result");
-        std::vector<const std::vector<RAgg>*> lists;
+        std::vector<const std::vector<Block>*> lists;
         for (int i = 0; i < n; ++i) lists.push_back(&holder_of(shards[i])->aggs);
         std::unique_ptr<ResultHolder> h(new ResultHolder());
         h->aggs = reduce_lists(lists);
@@ -1627,22 +1655,29 @@ extern "C" int esgpu_reduce(const esgpu_result* const* shards, int32_t n, esgpu_
     });
 }
 
-extern "C" int esgpu_cardinality_value(const esgpu_agg_result* r, int64_t* value) {
+extern "C" int esgpu_cardinality_value(const esgpu_agg_block* b, uint64_t instance, int64_t* value) {
     return guarded([&] {
-        require(r && value && r->type == ESGPU_AGG_CARDINALITY, ESGPU_ERR_INVALID, "not a cardinality result");
-        RAgg a;
-        a.hll_present = r->hll_present;
-        a.precision = r->precision;
-        a.hll_mode = r->hll_mode;
-        if (r->hll_mode && r->registers) a.registers.assign(r->registers, r->registers + ((size_t)1 << r->precision));
-        if (!r->hll_mode && r->lc_hashes) a.lc.assign(r->lc_hashes, r->lc_hashes + r->lc_size);
-        *value = hll_cardinality(a);
+        require(b && value && b->type == ESGPU_AGG_CARDINALITY && instance < b->n_instances, ESGPU_ERR_INVALID,
+                "not a cardinality block instance");
+        require(b->precision >= 4 && b->precision <= 18, ESGPU_ERR_INVALID, "precision out of range");
+        const bool present = b->hll_present && b->hll_present[instance];
+        const int mode = b->hll_mode ? b->hll_mode[instance] : 0;
+        const uint8_t* regs = b->registers ? b->registers[instance] : nullptr;
+        const size_t nlc = b->lc_sizes ? (size_t)b->lc_sizes[instance] : 0;
+        require(!(present && mode && !regs), ESGPU_ERR_INVALID, "missing registers");
+        *value = hll_cardinality(b->precision, present, mode, regs, nlc);
     });
 }
 
 extern "C" int esgpu_result_to_json(const esgpu_result* r, char* buf, size_t cap, size_t* needed) {
     return guarded([&] {
-        const std::string s = to_json(holder_of(r)->aggs);
+        require(r != nullptr, ESGPU_ERR_INVALID, "null result");
+        ResultHolder* h = holder_of(r);
+        if (!h->json_valid) {  // results are immutable: render once (callers size the buffer, then fill it)
+            h->json = to_json(h->aggs);
+            h->json_valid = true;
+        }
+        const std::string& s = h->json;
         if (needed) *needed = s.size() + 1;
         if (buf && cap) {
             const size_t c = std::min(cap - 1, s.size());
@@ -1752,8 +1787,8 @@ extern "C" int esgpu_comm_gather_reduce(esgpu_comm* cm, const esgpu_result* loca
         uint8_t* all = (uint8_t*)cm->hall.ensure(rec * n);
         HIPX(hipMemcpyAsync(all, dall, rec * n, hipMemcpyDeviceToHost, cm->stream));
         HIPX(hipStreamSynchronize(cm->stream));
-        std::vector<std::vector<RAgg>> shards(cm->nranks);
-        std::vector<const std::vector<RAgg>*> lists;
+        std::vector<std::vector<Block>> shards(cm->nranks);
+        std::vector<const std::vector<Block>*> lists;
         for (int r = 0; r < cm->nranks; ++r) {
             require(deserialize(all + rec * r, sizes[r], shards[r]), ESGPU_ERR_DEVICE, "corrupt shard record");
             lists.push_back(&shards[r]);

@@ -69,10 +69,16 @@ class ShardResult:
         return self._ptr.contents.aggs[i]
 
     def registers(self, i=0):
+        """HLL registers of top-level cardinality aggregation i (None unless it is in hyperloglog mode)."""
         a = self.aggregation(i)
-        if not a.hll_present or not a.hll_mode:
+        if a.type != N.AGG_CARDINALITY or not a.hll_present[0] or not a.hll_mode[0]:
             return None
-        return np.ctypeslib.as_array(a.registers, shape=(1 << a.precision,)).copy()
+        return np.ctypeslib.as_array(a.registers[0], shape=(1 << a.precision,)).copy()
+
+    def cardinality(self, i=0):
+        v = ctypes.c_int64()
+        N.check(N.lib().esgpu_cardinality_value(ctypes.byref(self.aggregation(i)), 0, ctypes.byref(v)))
+        return v.value
 
 
 def reduce(results):

@@ -262,37 +262,26 @@ int esgpu_plan_last_collect_stats(const esgpu_plan* plan, double* kernel_ms, uin
                                   int32_t* path);
 
 /* ---------------------------------------------------------------------------------------------------------
- * Results: a tree of InternalAggregation values (StringTerms, InternalHistogram, InternalStats,
- * InternalExtendedStats, InternalAvg, InternalCardinality ...).  Owned by the library.
+ * Results: columnar InternalAggregations, owned by the library.
+ * An esgpu_agg_block holds ONE aggregation of the request for n_instances parent buckets: instance i is the
+ * InternalAggregation the reference builds for parent bucket i (StringTerms, InternalHistogram / InternalDateHistogram,
+ * InternalStats, InternalExtendedStats, InternalAvg, InternalCardinality).  Top-level blocks have one instance.
+ * A bucket aggregation's instance i owns buckets [bucket_offsets[i], bucket_offsets[i+1]); each sub-aggregation is a
+ * block with one instance per bucket.  A JNI shim builds the Java objects from these arrays with bulk copies.
  * ------------------------------------------------------------------------------------------------------- */
-typedef struct esgpu_agg_result esgpu_agg_result;
+typedef struct esgpu_agg_block esgpu_agg_block;
 
-typedef struct esgpu_bucket {
-    int64_t key;                  /* histogram: rounded key; terms: ordinal within the producing shard */
-    const uint8_t* key_bytes;     /* terms: term bytes (StringTerms.Bucket.termBytes) */
-    int32_t key_len;
-    int32_t nsubs;
-    int64_t doc_count;
-    int64_t doc_count_error;
-    esgpu_agg_result* subs;       /* nsubs sub-aggregation results */
-} esgpu_bucket;
-
-struct esgpu_agg_result {
+struct esgpu_agg_block {
     int32_t type;                 /* ESGPU_AGG_* */
     int32_t order;
     const char* name;
-    /* bucket aggs */
-    esgpu_bucket* buckets;
-    int64_t nbuckets;
-    int64_t doc_count_error;      /* InternalTerms.docCountError */
-    int64_t other_doc_count;      /* InternalTerms.otherDocCount */
+    /* request parameters shared by all instances */
     int32_t required_size;
     int32_t shard_size;
     int64_t min_doc_count;
     int32_t show_term_doc_count_error;
     int32_t keyed;
-    /* histogram EmptyBucketInfo (InternalHistogram.java EmptyBucketInfo) */
-    int32_t has_empty_bucket_info;
+    int32_t has_empty_bucket_info;          /* histogram EmptyBucketInfo (InternalHistogram.java) */
     int32_t date_unit;
     int64_t interval;
     int64_t offset;
@@ -300,24 +289,38 @@ struct esgpu_agg_result {
     int32_t has_extended_bounds_max;
     int64_t extended_bounds_min;
     int64_t extended_bounds_max;
-    esgpu_agg_result* empty_subs; /* sub-aggregation prototypes for empty buckets */
-    int32_t nempty_subs;
-    /* numeric metrics */
-    int32_t reserved;
-    int64_t count;
-    double sum, min, max, sum_of_squares, sigma;
-    /* cardinality (HyperLogLogPlusPlus state, HyperLogLogPlusPlus.java:519-555) */
-    int32_t hll_present;          /* 0 = InternalCardinality with counts == null (empty) */
+    double sigma;
     int32_t precision;
-    int32_t hll_mode;             /* 0 = linear counting, 1 = hyperloglog */
-    int32_t reserved2;
-    uint8_t* registers;           /* 2^precision run lengths (hll_mode 1) */
-    uint32_t* lc_hashes;          /* encoded hashes (hll_mode 0), ascending */
-    int64_t lc_size;
+    int32_t nsubs;
+    uint64_t n_instances;
+    /* bucket aggregations */
+    const int64_t* doc_count_error;         /* [n_instances] InternalTerms.docCountError */
+    const int64_t* other_doc_count;         /* [n_instances] InternalTerms.otherDocCount */
+    const uint64_t* bucket_offsets;         /* [n_instances + 1] */
+    uint64_t n_buckets;
+    const int64_t* keys;                    /* [n_buckets] histogram key; terms: ordinal in the producing shard */
+    const uint64_t* term_offsets;           /* [n_buckets + 1] terms key bytes in term_bytes */
+    const uint8_t* term_bytes;
+    const int64_t* doc_counts;              /* [n_buckets] */
+    const int64_t* bucket_doc_count_errors; /* [n_buckets] */
+    const esgpu_agg_block* subs;            /* nsubs blocks, each with n_instances == n_buckets */
+    const esgpu_agg_block* empty_subs;      /* nsubs prototypes (n_instances == 1) for empty histogram buckets */
+    /* numeric metrics [n_instances] */
+    const int64_t* count;
+    const double* sum;
+    const double* min;
+    const double* max;
+    const double* sum_of_squares;
+    /* cardinality [n_instances] (HyperLogLogPlusPlus state, HyperLogLogPlusPlus.java:519-555) */
+    const int32_t* hll_present;             /* 0 = InternalCardinality with counts == null */
+    const int32_t* hll_mode;                /* 0 = linear counting, 1 = hyperloglog */
+    const uint8_t* const* registers;        /* 2^precision run lengths (hll_mode 1) */
+    const uint32_t* const* lc_hashes;       /* encoded hashes, ascending (hll_mode 0) */
+    const int64_t* lc_sizes;
 };
 
 struct esgpu_result {
-    esgpu_agg_result* aggs;
+    const esgpu_agg_block* aggs;
     int32_t naggs;
     int32_t reserved;
 };
@@ -325,8 +328,8 @@ struct esgpu_result {
 int esgpu_result_free(esgpu_result* r);
 /* InternalAggregations.reduce over shard results in shard order (InternalAggregations.java:133-161). */
 int esgpu_reduce(const esgpu_result* const* shard_results, int32_t n, esgpu_result** out);
-/* Cardinality value of a cardinality result (HyperLogLogPlusPlus.cardinality(0)). */
-int esgpu_cardinality_value(const esgpu_agg_result* r, int64_t* value);
+/* Cardinality value of instance i of a cardinality block (HyperLogLogPlusPlus.cardinality(0)). */
+int esgpu_cardinality_value(const esgpu_agg_block* block, uint64_t instance, int64_t* value);
 /* XContent-style JSON ({"<name>": {...}}), full double precision, Infinity/NaN as JSON tokens.
  * Writes at most cap bytes (NUL-terminated) and returns the full length in *needed. */
 int esgpu_result_to_json(const esgpu_result* r, char* buf, size_t cap, size_t* needed);

@@ -1,0 +1,76 @@
+"""CPU parity of the product's shard-level reduce (esgpu_reduce) and JSON rendering against the oracle, per request
+shape, without a GPU.
+
+The oracle collects several synthetic shards and reduces them the way the coordinating node does
+(InternalAggregations.reduce).  Its shard-level results are re-encoded into the library's stream format
+(tests/result_stream.py), decoded by esgpu_result_deserialize, rendered back (must equal the oracle's shard JSON),
+and reduced by esgpu_reduce (must equal the oracle's reduced JSON).  This covers terms error bounds / other counts,
+histogram empty-bucket filling with prototypes, order variants and nested sub-aggregation reduce at every level.
+"""
+import pytest
+
+import oracle as O
+from elasticsearch_amd import AggregationBuilders as AB
+from elasticsearch_amd import Order, ShardResult, reduce
+from helpers import assert_same, synthetic_columns
+from result_stream import encode, from_shard_json
+
+DOCS = 12_000
+DAY = 86_400_000
+T0 = 1441065600000
+
+
+def _ns(metric):
+    return [AB.terms("hosts").field("host").size(10).subAggregation(
+        AB.dateHistogram("per_hour").field("@timestamp").interval("1h").subAggregation(metric))]
+
+
+CASES = {
+    "north_star": (_ns(AB.stats("rt").field("response_time_ms")), ("host", "@timestamp", "response_time_ms")),
+    "config5_avg": (_ns(AB.avg("rt").field("response_time_ms")), ("host", "@timestamp", "response_time_ms")),
+    "config2_ext_bounds": ([AB.dateHistogram("h").field("@timestamp").interval("1h").minDocCount(0)
+                            .extendedBounds(T0 - DAY, T0 + 2 * DAY)
+                            .subAggregation(AB.extendedStats("rt").field("response_time_ms").sigma(3.0))],
+                           ("@timestamp", "response_time_ms")),
+    "hist_terms_mdc0": ([AB.histogram("b").field("bytes").interval(50_000).minDocCount(0)
+                         .subAggregation(AB.terms("st").field("status").size(3)
+                                         .subAggregation(AB.avg("rt").field("response_time_ms")))],
+                        ("bytes", "status", "response_time_ms")),
+    "terms_small_shard_size": ([AB.terms("hosts").field("host").size(5).shardSize(6)
+                                .showTermDocCountError(True)], ("host",)),
+    "terms_count_asc": ([AB.terms("hosts").field("host").size(7).order(Order.count(True))], ("host",)),
+    "terms_term_desc": ([AB.terms("hosts").field("host").size(7).order(Order.term(False))], ("host",)),
+    "hist_key_desc": ([AB.histogram("rt").field("response_time_ms").interval(25).order(Order.KEY_DESC)
+                       .subAggregation(AB.stats("b").field("bytes"))], ("response_time_ms", "bytes")),
+    "hist_count_asc": ([AB.histogram("rt").field("response_time_ms").interval(100).order(Order.COUNT_ASC)],
+                       ("response_time_ms",)),
+    "day_hist_terms": ([AB.dateHistogram("d").field("@timestamp").interval("1d")
+                        .subAggregation(AB.terms("hosts").field("host").size(4))], ("@timestamp", "host")),
+    "top_metrics": ([AB.stats("s").field("response_time_ms"), AB.extendedStats("e").field("bytes"),
+                     AB.avg("a").field("response_time_ms")], ("response_time_ms", "bytes")),
+}
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+@pytest.mark.parametrize("nshards", [1, 3])
+def test_reduce_matches_oracle(name, nshards):
+    aggs, fields = CASES[name]
+    shards = [(synthetic_columns(fields, DOCS + 997 * s, shard=s), DOCS + 997 * s) for s in range(nshards)]
+    want = O.run(shards, aggs, number_of_shards=nshards)
+    results = []
+    for s, sj in enumerate(want["shards"]):
+        r = ShardResult.deserialize(encode(from_shard_json(aggs, sj, nshards)))
+        assert_same(r.to_dict(), sj, f"shard{s}")  # columnar blocks render the reference's shard JSON
+        results.append(r)
+    assert_same(reduce(results).to_dict(), want["reduced"], "reduced")
+    # the reduce consumed the shard results read-only: reducing again gives the same answer
+    assert reduce(results).to_json() == reduce(results).to_json()
+
+
+def test_reduce_rejects_mismatched_trees():
+    a = encode(from_shard_json([AB.stats("x").field("f")], {"x": {"_internal": {"count": 1, "sum": 2.0, "min": 2.0,
+                                                                                  "max": 2.0}}}))
+    b = encode([{"type": 1, "name": "x", "buckets": []}])
+    from elasticsearch_amd import _native as N
+    with pytest.raises(N.EsGpuError):
+        reduce([ShardResult.deserialize(a), ShardResult.deserialize(b)])

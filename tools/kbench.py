@@ -57,22 +57,32 @@ def main():
         plan = e.plan(aggs, filters=flt)
         ms = []
         steps = []
+        parts = {"reset": [], "collect_call": [], "kernel_wait": [], "build": [], "reduce": []}
         for r in range(args.reps + 1):
             t0 = time.perf_counter()
             plan.reset()
+            t1 = time.perf_counter()
             plan.collect(seg)
+            t2 = time.perf_counter()
             k, nbytes, path = plan.last_collect_stats()
+            t3 = time.perf_counter()
             res = plan.build()
+            t4 = time.perf_counter()
             ea.reduce([res])
-            dt = (time.perf_counter() - t0) * 1e3
+            t5 = time.perf_counter()
+            dt = (t5 - t0) * 1e3
             if r:  # first is warmup
                 ms.append(k)
                 steps.append(dt)
+                for key, a, b in (("reset", t0, t1), ("collect_call", t1, t2), ("kernel_wait", t2, t3),
+                                  ("build", t3, t4), ("reduce", t4, t5)):
+                    parts[key].append((b - a) * 1e3)
         kms = sorted(ms)[len(ms) // 2]
         gbs = nbytes / (kms / 1e3) / 1e9
         print(json.dumps({"name": name, "kernel_ms": round(kms, 4), "bytes": nbytes, "gbs": round(gbs, 1),
                           "frac": round(gbs / 8000, 4), "path": path, "step_ms": round(sorted(steps)[len(steps) // 2], 3),
-                          "docs_per_s": args.docs / (kms / 1e3)}), flush=True)
+                          "docs_per_s": args.docs / (kms / 1e3),
+                          "parts_ms": {k: round(sorted(v)[len(v) // 2], 3) for k, v in parts.items()}}), flush=True)
         plan.close()
 
 
