@@ -1,0 +1,37 @@
+#!/bin/bash
+# One gpurun session: GPU parity tests, kernel sweep, bench, rocprofv3 kernel-trace stats and PMC HBM-traffic passes.
+#   gpurun --timeout 1200 -- bash tools/gpu_check.sh <tag> [steps...]
+# steps: tests kbench bench prof pmc (default: all).  Every GPU step has its own time limit; the first failure ends it.
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${1:-r1}
+shift || true
+STEPS=${*:-tests kbench bench prof pmc}
+OUT=$R/gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+run() {  # name seconds cmd...
+    local name=$1 secs=$2
+    shift 2
+    echo "== $name $(date +%T)"
+    timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc $(date +%T)"
+    tail -5 "$OUT/$name.log"
+    [ $rc -eq 0 ] || exit $rc
+}
+for s in $STEPS; do
+    case $s in
+        tests) run pytest_gpu 900 python3 -m pytest "$R/tests" -m gpu -x -q -p no:cacheprovider ;;
+        kbench) run kbench 600 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 ;;
+        bench) run bench 600 python3 "$R/bench.py" ;;
+        prof) cd /tmp && run rocprof_stats 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench -- \
+                  python3 "$R/bench.py" --steps 10 --warmup 3 --cpu-docs 0 ;;
+        pmc) cd /tmp && run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o bench -- \
+                 python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-docs 0 &&
+             run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o bench -- \
+                 python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-docs 0 ;;
+        *) echo "unknown step $s"; exit 2 ;;
+    esac
+done
+echo "== done"
