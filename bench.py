@@ -80,7 +80,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--docs", type=int, default=1_000_000_000, help="docs per shard (one shard per GPU)")
     ap.add_argument("--workload", default="north_star", choices=sorted(WORKLOADS))
-    ap.add_argument("--cpu-docs", type=int, default=64_000_000, help="CPU baseline sample size (0 = skip)")
+    ap.add_argument("--cpu-docs", type=int, default=320_000_000, help="CPU baseline sample size (0 = skip)")
     ap.add_argument("--traffic", default=os.path.join(HERE, "profiles", "hbm_traffic.json"),
                     help="PMC-derived HBM bytes per collect launch (profiles/), if measured for this workload")
     args = ap.parse_args()

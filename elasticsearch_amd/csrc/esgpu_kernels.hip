@@ -604,14 +604,18 @@ __global__ __launch_bounds__(256) void hll_registers_kernel(HllParams P, uint32_
     for (uint32_t i0 = d_begin + (blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < d_end; i0 += gsz * 4) {
         uint64_t hv[4];
         const uint32_t ok = hll_hash4(P, i0, hv);
+        // all register reads first, then the atomics: registers only grow, so a read that races with another
+        // thread's atomicMax can only cause a redundant atomic, never a missed one
+        uint32_t rl[4], idx[4], cur[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            if (!((ok >> j) & 1)) continue;
-            const uint32_t rl = hll_run_len(hv[j], P.p);
-            if (rl <= floor) continue;
-            const uint32_t idx = hll_index(hv[j], P.p);
-            if (rl > P.regs[idx]) atomicMax(&P.regs[idx], rl);
+            rl[j] = ((ok >> j) & 1) ? hll_run_len(hv[j], P.p) : 0u;
+            idx[j] = hll_index(hv[j], P.p);
+            cur[j] = rl[j] > floor ? P.regs[idx[j]] : 0xFFu;
         }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (rl[j] > cur[j]) atomicMax(&P.regs[idx[j]], rl[j]);
     }
 }
 
@@ -756,112 +760,281 @@ void launch_fill_u64(unsigned long long* p, size_t n, unsigned long long v, hipS
 // ------------------------------------------------------------------------------------------------------------
 namespace esgpu {
 
-template <bool SCATTER>
-__global__ __launch_bounds__(kWG) void part_pass_kernel(PartParams P) {
+// pass 1: per-workgroup partition histogram
+__global__ __launch_bounds__(kWG) void part_hist_kernel(PartParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint32_t* lds = (uint32_t*)smem;  // [P] histogram (pass 1) or write cursors (pass 3)
+    uint32_t* lds = (uint32_t*)smem;  // [P]
     const uint32_t g = blockIdx.x;
-    for (uint32_t p = threadIdx.x; p < P.P; p += kWG) lds[p] = SCATTER ? P.wg_counts[(size_t)p * P.G + g] : 0u;
+    for (uint32_t p = threadIdx.x; p < P.P; p += kWG) lds[p] = 0u;
     __syncthreads();
     const uint32_t b_begin = g * P.blocks_per_wg;
     const uint32_t b_end = min(b_begin + P.blocks_per_wg, P.n_blocks);
     for (uint32_t b = b_begin; b < b_end; ++b) {
+        uint32_t o[kItersPerBlock][4], ok[kItersPerBlock];
+#pragma unroll
+        for (int it = 0; it < kItersPerBlock; ++it) {  // all 16 loads in flight before the first atomic
+            const uint32_t doc0 = b * kBlockDocs + it * kIterDocs + threadIdx.x * kVec;
+            load_u32x4(P.ord, doc0, o[it]);
+            ok[it] = 0xF;
+            if (doc0 + 4 > P.n_docs) ok[it] = doc0 >= P.n_docs ? 0u : ((1u << (P.n_docs - doc0)) - 1u);
+            if (P.accept) ok[it] &= bits4(P.accept, doc0);
+            for (int k = 0; k < P.npred; ++k) ok[it] &= eval_pred(P.pred[k], doc0);
+        }
+#pragma unroll
+        for (int it = 0; it < kItersPerBlock; ++it)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (((ok[it] >> j) & 1) && o[it][j] < P.T) atomicAdd(&lds[o[it][j] >> P.shift], 1u);
+    }
+    __syncthreads();
+    for (uint32_t p = threadIdx.x; p < P.P; p += kWG) P.wg_counts[(size_t)p * P.G + g] = lds[p];
+}
+
+// exclusive scan of v[0, n) in LDS by one workgroup (n <= kPartMaxStaged); returns the total
+__device__ uint32_t block_exclusive_scan(uint32_t* v, uint32_t n, uint32_t* wave_tot) {
+    const uint32_t per = (n + kWG - 1) / kWG;
+    const uint32_t b = threadIdx.x * per, e = min(b + per, n);
+    uint32_t local = 0;
+    for (uint32_t i = b; i < e; ++i) local += v[i];
+    // inclusive scan of `local` across the wave (wave64), then across the 8 waves
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = local;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) wave_tot[wave] = x;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < kWG / 64; ++w) {
+        const uint32_t t = wave_tot[w];
+        if (w < wave) before += t;
+        total += t;
+    }
+    uint32_t run = before + x - local;
+    for (uint32_t i = b; i < e; ++i) {
+        const uint32_t c = v[i];
+        v[i] = run;
+        run += c;
+    }
+    return total;
+}
+
+// pass 3: scatter through an LDS-staged tile.  Every 8192-doc block is counting-sorted by partition in LDS first, so
+// the global writes are runs of consecutive 16-bit partition-local offsets instead of 8192 scattered words.
+__global__ __launch_bounds__(kWG) void part_scatter_kernel(PartParams P) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t* cursor = (uint32_t*)smem;      // [P] next write position of (partition, this workgroup)
+    uint32_t* tcnt = cursor + P.P;           // [P] elements of the tile per partition
+    uint32_t* toff = tcnt + P.P;             // [P] their exclusive offsets inside the tile
+    uint32_t* stage = toff + P.P;            // [kBlockDocs] the tile, sorted by partition
+    __shared__ uint32_t wave_tot[kWG / 64];
+    const uint32_t g = blockIdx.x;
+    const uint32_t mask = (1u << P.shift) - 1u;
+    for (uint32_t p = threadIdx.x; p < P.P; p += kWG) {
+        cursor[p] = P.wg_counts[(size_t)p * P.G + g];
+        tcnt[p] = 0u;
+    }
+    __syncthreads();
+    const uint32_t b_begin = g * P.blocks_per_wg;
+    const uint32_t b_end = min(b_begin + P.blocks_per_wg, P.n_blocks);
+    for (uint32_t b = b_begin; b < b_end; ++b) {
+        uint32_t o[kItersPerBlock][4], ok[kItersPerBlock], rank[kItersPerBlock][4];
+#pragma unroll
         for (int it = 0; it < kItersPerBlock; ++it) {
             const uint32_t doc0 = b * kBlockDocs + it * kIterDocs + threadIdx.x * kVec;
-            uint32_t ok = 0xF;
-            if (doc0 + 4 > P.n_docs) ok = doc0 >= P.n_docs ? 0u : ((1u << (P.n_docs - doc0)) - 1u);
-            if (P.accept) ok &= bits4(P.accept, doc0);
-            for (int k = 0; k < P.npred; ++k) ok &= eval_pred(P.pred[k], doc0);
-            uint32_t o[4];
-            load_u32x4(P.ord, doc0, o);
+            load_u32x4(P.ord, doc0, o[it]);
+            ok[it] = 0xF;
+            if (doc0 + 4 > P.n_docs) ok[it] = doc0 >= P.n_docs ? 0u : ((1u << (P.n_docs - doc0)) - 1u);
+            if (P.accept) ok[it] &= bits4(P.accept, doc0);
+            for (int k = 0; k < P.npred; ++k) ok[it] &= eval_pred(P.pred[k], doc0);
+        }
+#pragma unroll
+        for (int it = 0; it < kItersPerBlock; ++it)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                if (!((ok >> j) & 1) || o[j] >= P.T) continue;  // missing ordinal (0xFFFFFFFF) or out of range
-                const uint32_t part = o[j] >> P.shift;
-                if (SCATTER) {
-                    const uint32_t pos = atomicAdd(&lds[part], 1u);
-                    P.pbuf[pos] = o[j];
-                } else {
-                    atomicAdd(&lds[part], 1u);
-                }
+                const bool v = ((ok[it] >> j) & 1) && o[it][j] < P.T;
+                rank[it][j] = v ? atomicAdd(&tcnt[o[it][j] >> P.shift], 1u) : 0xFFFFFFFFu;
             }
-        }
-    }
-    if (!SCATTER) {
         __syncthreads();
-        for (uint32_t p = threadIdx.x; p < P.P; p += kWG) P.wg_counts[(size_t)p * P.G + g] = lds[p];
+        for (uint32_t p = threadIdx.x; p < P.P; p += kWG) toff[p] = tcnt[p];
+        __syncthreads();
+        const uint32_t n_tile = block_exclusive_scan(toff, P.P, wave_tot);
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < kItersPerBlock; ++it)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (rank[it][j] != 0xFFFFFFFFu) stage[toff[o[it][j] >> P.shift] + rank[it][j]] = o[it][j];
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < n_tile; i += kWG) {
+            const uint32_t v = stage[i];
+            const uint32_t p = v >> P.shift;
+            P.pbuf[cursor[p] + (i - toff[p])] = (uint16_t)(v & mask);
+        }
+        __syncthreads();
+        for (uint32_t p = threadIdx.x; p < P.P; p += kWG) {
+            cursor[p] += tcnt[p];
+            tcnt[p] = 0u;
+        }
+        __syncthreads();
     }
 }
 
 void launch_part_hist(const PartParams& p, hipStream_t s) {
-    hipLaunchKernelGGL((part_pass_kernel<false>), dim3(p.G), dim3(kWG), (size_t)p.P * 4, s, p);
+    hipLaunchKernelGGL(part_hist_kernel, dim3(p.G), dim3(kWG), (size_t)p.P * 4, s, p);
 }
 void launch_part_scatter(const PartParams& p, hipStream_t s) {
-    hipLaunchKernelGGL((part_pass_kernel<true>), dim3(p.G), dim3(kWG), (size_t)p.P * 4, s, p);
+    hipLaunchKernelGGL(part_scatter_kernel, dim3(p.G), dim3(kWG), ((size_t)p.P * 3 + kBlockDocs) * 4, s, p);
+}
+size_t part_scatter_lds_bytes(uint32_t n_parts) { return ((size_t)n_parts * 3 + kBlockDocs) * 4; }
+
+// exclusive scan of wg_counts[P*G] (partition-major) in place; part_begin[p] = offset of (p, g = 0), [P] = total.
+// Three launches over 4096-element tiles (tile sums, scan of the tile sums, tile-local scans), all coalesced.
+constexpr uint32_t kScanTile = kWG * 8;
+
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    return x;
 }
 
-// exclusive scan of wg_counts[P*G] (partition-major) in place; part_begin[p] = offset of (p, g = 0), [P] = total
-__global__ __launch_bounds__(1024) void part_scan_kernel(PartParams P) {
-    const size_t n = (size_t)P.P * P.G;
-    const size_t per = (n + 1023) / 1024;
-    const size_t b = threadIdx.x * per, e = min(b + per, n);
+__global__ __launch_bounds__(kWG) void scan_tile_sums_kernel(const uint32_t* v, uint32_t n, uint32_t* tile_sums) {
+    const uint32_t base = blockIdx.x * kScanTile;
     uint32_t local = 0;
-    for (size_t i = b; i < e; ++i) local += P.wg_counts[i];
-    __shared__ uint32_t sums[1024];
-    sums[threadIdx.x] = local;
+    for (uint32_t i = base + threadIdx.x; i < min(n, base + kScanTile); i += kWG) local += v[i];
+    local = wave_sum_u32(local);
+    __shared__ uint32_t part[kWG / 64];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = local;
     __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan of the 1024 partial sums
-        const uint32_t v = threadIdx.x >= (unsigned)off ? sums[threadIdx.x - off] : 0u;
-        __syncthreads();
-        sums[threadIdx.x] += v;
-        __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < kWG / 64; ++w) t += part[w];
+        tile_sums[blockIdx.x] = t;
     }
-    uint32_t run = threadIdx.x ? sums[threadIdx.x - 1] : 0u;
-    for (size_t i = b; i < e; ++i) {
-        const uint32_t c = P.wg_counts[i];
-        P.wg_counts[i] = run;
-        if (i % P.G == 0) P.part_begin[i / P.G] = run;
-        run += c;
+}
+
+// one workgroup: exclusive scan of the tile sums (ntiles <= kScanTile)
+__global__ __launch_bounds__(kWG) void scan_tile_offsets_kernel(uint32_t* tile_sums, uint32_t ntiles) {
+    __shared__ uint32_t wave_tot[kWG / 64];
+    __shared__ uint32_t buf[kScanTile];
+    for (uint32_t i = threadIdx.x; i < kScanTile; i += kWG) buf[i] = i < ntiles ? tile_sums[i] : 0u;
+    __syncthreads();
+    block_exclusive_scan(buf, kScanTile, wave_tot);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < ntiles; i += kWG) tile_sums[i] = buf[i];
+}
+
+__global__ __launch_bounds__(kWG) void scan_tiles_kernel(PartParams P, const uint32_t* tile_offsets, uint32_t n) {
+    __shared__ uint32_t wave_tot[kWG / 64];
+    __shared__ uint32_t buf[kScanTile];
+    const uint32_t base = blockIdx.x * kScanTile;
+    const uint32_t cnt = min(kScanTile, n - base);
+    for (uint32_t i = threadIdx.x; i < kScanTile; i += kWG) buf[i] = i < cnt ? P.wg_counts[base + i] : 0u;
+    __syncthreads();
+    const uint32_t tile_total = block_exclusive_scan(buf, kScanTile, wave_tot);
+    __syncthreads();
+    const uint32_t off = tile_offsets[blockIdx.x];
+    for (uint32_t i = threadIdx.x; i < cnt; i += kWG) {
+        const uint32_t gi = base + i;
+        const uint32_t x = off + buf[i];
+        P.wg_counts[gi] = x;
+        if (gi % P.G == 0) P.part_begin[gi / P.G] = x;
     }
-    if (threadIdx.x == 1023) P.part_begin[P.P] = sums[1023];
+    if (base + cnt == n && threadIdx.x == 0) P.part_begin[P.P] = off + tile_total;
 }
 
 void launch_part_scan(const PartParams& p, hipStream_t s) {
-    hipLaunchKernelGGL(part_scan_kernel, dim3(1), dim3(1024), 0, s, p);
+    const uint32_t n = p.P * p.G;
+    const uint32_t ntiles = (n + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL(scan_tile_sums_kernel, dim3(ntiles), dim3(kWG), 0, s, (const uint32_t*)p.wg_counts, n, p.tile_sums);
+    hipLaunchKernelGGL(scan_tile_offsets_kernel, dim3(1), dim3(kWG), 0, s, p.tile_sums, ntiles);
+    hipLaunchKernelGGL(scan_tiles_kernel, dim3(ntiles), dim3(kWG), 0, s, p, (const uint32_t*)p.tile_sums, n);
+}
+uint32_t part_scan_tiles(uint32_t n) { return (n + kScanTile - 1) / kScanTile; }
+
+// pass 4: workgroup w counts the partitioned elements [w*chunk, (w+1)*chunk) — hot partitions are thereby split
+// across many workgroups, and no host round trip is needed.  Each partition piece is counted in 2^shift LDS
+// counters; a thread merges runs of equal offsets in registers first (the Zipf head term dominates its partition).
+__device__ __forceinline__ void count_run(uint32_t* cnt, uint32_t& cur, uint32_t& n, uint32_t v) {
+    if (v == cur) { ++n; return; }
+    if (n) atomicAdd(&cnt[cur], n);
+    cur = v;
+    n = 1;
 }
 
-// item = {partition, begin, end, single}: count pbuf[begin, end) into the partition's 2^shift LDS counters
-__global__ __launch_bounds__(kWG) void part_count_kernel(PartParams P, const uint32_t* items) {
+__global__ __launch_bounds__(kWG) void part_count_kernel(PartParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t* cnt = (uint32_t*)smem;
     const uint32_t S = 1u << P.shift;
-    const uint32_t part = items[blockIdx.x * 4 + 0];
-    const uint32_t begin = items[blockIdx.x * 4 + 1], end = items[blockIdx.x * 4 + 2];
-    const bool single = items[blockIdx.x * 4 + 3] != 0;
-    for (uint32_t i = threadIdx.x; i < S; i += kWG) cnt[i] = 0;
-    __syncthreads();
-    const uint32_t base = part << P.shift;
-    uint32_t i = begin + threadIdx.x;
-    for (; i + 3 * kWG < end; i += 4 * kWG) {  // 4 independent loads in flight per thread
-        const uint32_t a = P.pbuf[i], b = P.pbuf[i + kWG], c = P.pbuf[i + 2 * kWG], d = P.pbuf[i + 3 * kWG];
-        atomicAdd(&cnt[a - base], 1u);
-        atomicAdd(&cnt[b - base], 1u);
-        atomicAdd(&cnt[c - base], 1u);
-        atomicAdd(&cnt[d - base], 1u);
+    const uint32_t total = P.part_begin[P.P];
+    const uint64_t e0l = (uint64_t)blockIdx.x * P.chunk;
+    if (e0l >= total) return;
+    const uint32_t e0 = (uint32_t)e0l, e1 = (uint32_t)min<uint64_t>(e0l + P.chunk, total);
+    // first partition with part_begin[q + 1] > e0
+    uint32_t lo = 0, hi = P.P - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (P.part_begin[mid + 1] <= e0) lo = mid + 1;
+        else hi = mid;
     }
-    for (; i < end; i += kWG) atomicAdd(&cnt[P.pbuf[i] - base], 1u);
-    __syncthreads();
-    for (uint32_t j = threadIdx.x; j < S; j += kWG) {
-        const uint32_t n = cnt[j];
-        if (n == 0 || base + j >= P.T) continue;
-        if (single) P.counts[base + j] += n;  // the only writer of this partition in this launch
-        else atomicAdd(&P.counts[base + j], (unsigned long long)n);
+    for (uint32_t q = lo; q < P.P; ++q) {
+        const uint32_t qb = P.part_begin[q], qe = P.part_begin[q + 1];
+        if (qb >= e1) break;
+        const uint32_t s0 = max(e0, qb), s1 = min(e1, qe);
+        if (s0 >= s1) continue;
+        for (uint32_t i = threadIdx.x; i < S; i += kWG) cnt[i] = 0;
+        __syncthreads();
+        uint32_t cur = 0, n = 0;
+        uint32_t i0 = s0;
+        const uint32_t a0 = min(s1, (s0 + 7u) & ~7u);  // head up to a 16-byte boundary
+        for (uint32_t i = i0 + threadIdx.x; i < a0; i += kWG) count_run(cnt, cur, n, P.pbuf[i]);
+        const uint32_t nvec = (s1 - a0) / 8;
+        const uint4* v8 = reinterpret_cast<const uint4*>(P.pbuf + a0);
+        uint32_t k = threadIdx.x;
+        for (; k + kWG < nvec; k += 2 * kWG) {  // two 16-byte loads (16 offsets) in flight per thread
+            const uint4 x = v8[k], y = v8[k + kWG];
+            const uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                count_run(cnt, cur, n, w[t] & 0xFFFFu);
+                count_run(cnt, cur, n, w[t] >> 16);
+            }
+        }
+        for (; k < nvec; k += kWG) {
+            const uint4 x = v8[k];
+            const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                count_run(cnt, cur, n, w[t] & 0xFFFFu);
+                count_run(cnt, cur, n, w[t] >> 16);
+            }
+        }
+        for (uint32_t i = a0 + nvec * 8 + threadIdx.x; i < s1; i += kWG) count_run(cnt, cur, n, P.pbuf[i]);
+        if (n) atomicAdd(&cnt[cur], n);
+        __syncthreads();
+        const bool whole = s0 == qb && s1 == qe;  // the only writer of this partition in this launch
+        const uint32_t base = q << P.shift;
+        for (uint32_t j = threadIdx.x; j < S; j += kWG) {
+            const uint32_t c = cnt[j];
+            if (c == 0 || base + j >= P.T) continue;
+            if (whole) P.counts[base + j] += c;
+            else atomicAdd(&P.counts[base + j], (unsigned long long)c);
+        }
+        __syncthreads();
     }
 }
 
-void launch_part_count(const PartParams& p, uint32_t n_items, const uint32_t* items, hipStream_t s) {
-    if (n_items == 0) return;
-    hipLaunchKernelGGL(part_count_kernel, dim3(n_items), dim3(kWG), (size_t)4 << p.shift, s, p, items);
+void launch_part_count(const PartParams& p, hipStream_t s) {
+    const uint32_t grid = (uint32_t)(((uint64_t)p.n_docs + p.chunk - 1) / p.chunk);
+    if (grid == 0) return;
+    hipLaunchKernelGGL(part_count_kernel, dim3(grid), dim3(kWG), (size_t)4 << p.shift, s, p);
 }
 
 // ------------------------------------------------------------------------------------------------------------

@@ -133,14 +133,19 @@ struct PartParams {
     const uint64_t* accept;
     uint32_t* wg_counts;     // [P][G] docs of partition p seen by workgroup g (pass 1), exclusive offsets after the scan
     uint32_t* part_begin;    // [P + 1] start of each partition in pbuf
-    uint32_t* pbuf;          // partitioned ordinals
+    uint16_t* pbuf;          // partitioned ordinals as partition-local offsets (ord & (2^shift - 1))
     unsigned long long* counts;  // [T] output doc counts
-    uint32_t chunk;          // max elements of one partition handled by one counting workgroup
+    uint32_t chunk;          // partitioned elements per counting workgroup
+    uint32_t* tile_sums;     // scratch of the scan: part_scan_tiles(P * G) entries
 };
+constexpr uint32_t kPartShift = 14;        // 16384 ordinals per partition
+constexpr uint32_t kPartMaxStaged = 2048;  // partitions the LDS-staged scatter handles (2^25 ordinals at shift 14)
 void launch_part_hist(const PartParams& p, hipStream_t s);
 void launch_part_scan(const PartParams& p, hipStream_t s);
 void launch_part_scatter(const PartParams& p, hipStream_t s);
-void launch_part_count(const PartParams& p, uint32_t n_items, const uint32_t* items, hipStream_t s);
+void launch_part_count(const PartParams& p, hipStream_t s);
+size_t part_scatter_lds_bytes(uint32_t n_parts);
+uint32_t part_scan_tiles(uint32_t n);
 
 // ---- GPU top-k over a count vector (BucketPriorityQueue replacement for large T) ----
 struct TopkParams {

@@ -605,8 +605,8 @@ struct esgpu_plan {
     std::map<std::string, std::vector<std::string>> term_cache;  // terms reachable after the segment is destroyed
     // per-request scratch, reused across requests
     Scratch s_accept, s_tcnt, s_rows, s_dst[6];
-    Scratch s_wgc, s_pbeg, s_pbuf, s_items, s_cand, s_keys;  // partitioned counting + GPU top-k
-    PinnedBuf h_pbeg, h_items, h_keys;
+    Scratch s_wgc, s_pbeg, s_pbuf, s_tiles, s_cand, s_keys;  // partitioned counting + GPU top-k
+    PinnedBuf h_keys;
     hipEvent_t ev_mid = nullptr;
     PinnedBuf h_tcnt, h_rows, h_dst[6];
 };
@@ -853,8 +853,8 @@ static void set_preds(esgpu_plan* p, const esgpu_segment* s, PredDev* out, int32
 }
 
 // K1 for valueCount >> LDS (e.g. 10M url ordinals): radix-partitioned counting instead of global atomics, which
-// serialise on the Zipf head terms.  Reads the ordinal column twice and the partitioned copy once (12 B/doc of
-// traffic for a 4 B/doc algorithmic stream); see DESIGN.md.
+// serialise on the Zipf head terms.  Reads the ordinal column twice (4 + 4 B/doc), writes and re-reads a 2 B/doc
+// partition-local copy: 12 B/doc of traffic for the 4 B/doc algorithmic stream.  Fully asynchronous.
 static bool collect_partitioned(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const DevColumn* oc,
                                 const uint64_t* d_accept, const PredDev* pred, int npred) {
     esgpu_ctx* c = p->ctx;
@@ -867,47 +867,28 @@ static bool collect_partitioned(esgpu_plan* p, Pipeline& pl, const esgpu_segment
     Q.G = (Q.n_blocks + Q.blocks_per_wg - 1) / Q.blocks_per_wg;
     Q.ord = oc->values.as<uint32_t>();
     Q.T = pl.T;
-    Q.shift = 14;  // 16384 ordinals per partition: 64 KB of LDS counters in the counting pass
+    Q.shift = kPartShift;  // 16384 ordinals per partition: 64 KB of LDS counters in the counting pass
     Q.P = (uint32_t)(((uint64_t)pl.T + (1u << Q.shift) - 1) >> Q.shift);
-    require(Q.P <= 16384, ESGPU_ERR_UNSUPPORTED, "more than 2^28 ordinals");
+    require(Q.P >= 1 && Q.P <= kPartMaxStaged, ESGPU_ERR_INVALID, "partition count out of range");
     Q.npred = npred;
     for (int k = 0; k < npred; ++k) Q.pred[k] = pred[k];
     Q.accept = d_accept;
     Q.wg_counts = (uint32_t*)p->s_wgc.ensure(c, (size_t)Q.P * Q.G * 4);
     Q.part_begin = (uint32_t*)p->s_pbeg.ensure(c, (size_t)(Q.P + 1) * 4);
-    Q.pbuf = (uint32_t*)p->s_pbuf.ensure(c, std::max<size_t>(s->max_doc, 1) * 4);
+    const uint32_t ntiles = part_scan_tiles(Q.P * Q.G);
+    require(ntiles <= 4096, ESGPU_ERR_INVALID, "partition scan too large");
+    Q.tile_sums = (uint32_t*)p->s_tiles.ensure(c, (size_t)ntiles * 4);
+    Q.pbuf = (uint16_t*)p->s_pbuf.ensure(c, (std::max<size_t>(s->max_doc, 1) + 8) * 2);
     Q.counts = pl.g_cnt.as<unsigned long long>();
-    Q.chunk = 1u << 20;
+    // ~4 counting workgroups per CU; each covers `chunk` partitioned elements (a multiple of 8: 16-byte loads)
+    const uint64_t want = (uint64_t)c->cus * 4;
+    Q.chunk = (uint32_t)std::max<uint64_t>(1u << 16, (((uint64_t)s->max_doc + want - 1) / want + 7) & ~7ull);
     HIPX(hipEventRecord(pl.e0, st));
     launch_part_hist(Q, st);
     launch_part_scan(Q, st);
-    uint32_t* hb = (uint32_t*)p->h_pbeg.ensure((size_t)(Q.P + 1) * 4);
-    HIPX(hipMemcpyAsync(hb, Q.part_begin, (size_t)(Q.P + 1) * 4, hipMemcpyDeviceToHost, st));
-    HIPX(hipEventRecord(p->ev_mid, st));
     launch_part_scatter(Q, st);
+    launch_part_count(Q, st);
     HIPX(hipGetLastError());
-    HIPX(hipEventSynchronize(p->ev_mid));  // the scatter keeps running while the work items are built
-    std::vector<uint32_t> items;
-    for (uint32_t q = 0; q < Q.P; ++q) {
-        const uint32_t b = hb[q], e = hb[q + 1];
-        if (b == e) continue;
-        const uint32_t nch = (e - b + Q.chunk - 1) / Q.chunk;
-        for (uint32_t k = 0; k < nch; ++k) {
-            items.push_back(q);
-            items.push_back(b + k * Q.chunk);
-            items.push_back(std::min(e, b + (k + 1) * Q.chunk));
-            items.push_back(nch == 1);
-        }
-    }
-    const uint32_t n_items = (uint32_t)(items.size() / 4);
-    if (n_items) {
-        uint32_t* hi = (uint32_t*)p->h_items.ensure(items.size() * 4);
-        std::memcpy(hi, items.data(), items.size() * 4);
-        uint32_t* di = (uint32_t*)p->s_items.ensure(c, items.size() * 4);
-        HIPX(hipMemcpyAsync(di, hi, items.size() * 4, hipMemcpyHostToDevice, st));
-        launch_part_count(Q, n_items, di, st);
-        HIPX(hipGetLastError());
-    }
     HIPX(hipEventRecord(pl.e1, st));
     p->last_path = 4;
     return true;
@@ -1020,7 +1001,8 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
         }
     }
     P.W = W;
-    if (!P.lds_mode && ORD && !HIST && met_launch == 0 && !pl.vcnt_mode && pl.ocnt_mode == OCNT_NONE) {
+    if (!P.lds_mode && ORD && !HIST && met_launch == 0 && !pl.vcnt_mode && pl.ocnt_mode == OCNT_NONE &&
+        (((uint64_t)pl.T + (1u << kPartShift) - 1) >> kPartShift) <= kPartMaxStaged) {
         p->last_bytes += bytes_per_doc * (uint64_t)s->max_doc + (d_accept ? ((uint64_t)s->max_doc + 7) / 8 : 0);
         return collect_partitioned(p, pl, s, oc, d_accept, P.pred, P.npred);
     }

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun session: GPU parity tests, kernel sweep, bench, rocprofv3 kernel-trace stats and PMC HBM-traffic passes.
 #   gpurun --timeout 1200 -- bash tools/gpu_check.sh <tag> [steps...]
-# steps: tests kbench bench prof pmc (default: all).  Every GPU step has its own time limit; the first failure ends it.
+# steps: tests kbench bench prof profk pmc (default: tests kbench bench prof pmc).  Every GPU step has its own time limit; the first failure ends it.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r1}
@@ -25,11 +25,13 @@ for s in $STEPS; do
         tests) run pytest_gpu 900 python3 -m pytest "$R/tests" -m gpu -x -q -p no:cacheprovider ;;
         kbench) run kbench 600 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 ;;
         bench) run bench 600 python3 "$R/bench.py" ;;
-        prof) cd /tmp && run rocprof_stats 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench -- \
+        prof) cd /tmp && run rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
                   python3 "$R/bench.py" --steps 10 --warmup 3 --cpu-docs 0 ;;
-        pmc) cd /tmp && run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o bench -- \
+        profk) cd /tmp && run rocprof_kbench 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profk" -o kbench -- \
+                   python3 "$R/tools/kbench.py" --docs 1000000000 --reps 3 ;;
+        pmc) cd /tmp && run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o bench -- \
                  python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-docs 0 &&
-             run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o bench -- \
+             run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o bench -- \
                  python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-docs 0 ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
