@@ -58,19 +58,42 @@ def build_request(workload, world):
     raise SystemExit(f"unknown workload {workload}")
 
 
-def cpu_baseline(workload, world, sample_docs):
-    """Oracle (cpu_ref restatement of the Java collect loop) on one host core over a sample_docs-doc synthetic shard."""
+def cpu_baseline(workload, world, sample_docs, threads):
+    """The oracle (cpu_ref: the reference's Java collect/build loops restated in C++) on the host cores, one shard per
+    thread as Elasticsearch runs one SEARCH thread per shard.  `threads` shards of
+    sample_docs / threads docs each, generated and collected concurrently; the wall time of the collect+build
+    phase over all of them gives the node-level CPU rate."""
+    import threading
     sys.path.insert(0, os.path.join(HERE, "oracle"))
     sys.path.insert(0, os.path.join(HERE, "tests"))
     import oracle as O
     from helpers import synthetic_columns
     fields = WORKLOADS[workload][0]
     aggs, filters = build_request(workload, world)
-    cols = synthetic_columns(fields, sample_docs, shard=0)
-    _, secs = O.run([(cols, sample_docs)], aggs, filters=filters, number_of_shards=world, return_seconds=True)
-    return {"value": sample_docs / secs, "unit": "docs/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/cpu_ref.cpp single-threaded (one SEARCH thread per shard) over a {sample_docs:,}-doc "
-                      f"synthetic shard of the same request, collect+build timed ({secs:.2f} s)"}
+    per = max(sample_docs // threads, 1)
+    cols = [None] * threads
+    secs = [0.0] * threads
+
+    def gen(i):
+        cols[i] = synthetic_columns(fields, per, shard=i)
+
+    def work(i):
+        _, secs[i] = O.run([(cols[i], per)], aggs, filters=filters, number_of_shards=world, return_seconds=True)
+
+    for fn in (gen, work):
+        ts = [threading.Thread(target=fn, args=(i,)) for i in range(threads)]
+        t0 = time.perf_counter()
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        wall = time.perf_counter() - t0
+    core_rate = per / (sum(secs) / threads)
+    return {"value": per * threads / wall, "unit": "docs/s", "cores": threads, "kind": "port",
+            "single_core_value": core_rate,
+            "sample": f"oracle/cpu_ref.cpp (the reference's Java collect+build loops restated), {threads} synthetic "
+                      f"shards x {per:,} docs of the same request, one host thread per shard, run concurrently "
+                      f"({wall:.2f} s wall; {core_rate / 1e6:.1f}M docs/s per core)"}
 
 
 def main():
@@ -80,7 +103,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--docs", type=int, default=1_000_000_000, help="docs per shard (one shard per GPU)")
     ap.add_argument("--workload", default="north_star", choices=sorted(WORKLOADS))
-    ap.add_argument("--cpu-docs", type=int, default=320_000_000, help="CPU baseline sample size (0 = skip)")
+    ap.add_argument("--cpu-docs", type=int, default=640_000_000, help="CPU baseline sample size (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=min(16, int(os.environ.get("OMP_NUM_THREADS", "0")) or
+                                                              os.cpu_count() or 1),
+                    help="host threads of the CPU baseline (one shard each)")
     ap.add_argument("--traffic", default=os.path.join(HERE, "profiles", "hbm_traffic.json"),
                     help="PMC-derived HBM bytes per collect launch (profiles/), if measured for this workload")
     args = ap.parse_args()
@@ -159,7 +185,7 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and args.cpu_docs > 0:
-            cpu = cpu_baseline(args.workload, world, args.cpu_docs)
+            cpu = cpu_baseline(args.workload, world, args.cpu_docs, max(1, args.cpu_threads))
         out = {
             "metric": "docs aggregated/sec (node) + achieved HBM GB/s, terms+date_histogram, 1B docs",
             "value": value,

@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libesgpu.so")
+# ESGPU_LIBRARY selects an alternative build of the same library (kernel-variant experiments, tools/kbench.py)
+LIB_PATH = os.environ.get("ESGPU_LIBRARY") or os.path.join(_HERE, "libesgpu.so")
 
 # ---- constants (include/esgpu.h) ----
 OK, ERR_INVALID, ERR_UNSUPPORTED, ERR_DEVICE, ERR_OOM, ERR_STATE, ERR_NO_DEVICE = range(7)

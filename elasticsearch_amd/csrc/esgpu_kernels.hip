@@ -84,10 +84,14 @@ void launch_synth(const SynthParams& p, hipStream_t stream) {
 // ------------------------------------------------------------------------------------------------------------
 // collect
 // ------------------------------------------------------------------------------------------------------------
+#ifndef ESGPU_PREFETCH
+#define ESGPU_PREFETCH 2
+#endif
 constexpr int kWG = 512;                         // threads per workgroup (8 waves)
 constexpr int kVec = 4;                          // consecutive docs per thread per iteration
 constexpr int kIterDocs = kWG * kVec;            // 2048
 constexpr int kItersPerBlock = kBlockDocs / kIterDocs;  // 4
+constexpr int kPrefetch = ESGPU_PREFETCH;             // iterations of loads in flight per thread
 
 struct Doc4 {
     uint32_t ord[kVec];
@@ -415,17 +419,24 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
     g.cnt64 = P.g_cnt; g.vcnt64 = P.g_vcnt; g.sum = P.g_sum; g.mn = P.g_min; g.mx = P.g_max; g.sq = P.g_sq;
     g.ocnt64 = P.g_ocnt;
 
-    Acc s = g;  // LDS window view
-    if (P.lds_mode) {
+    // LDS window view.  Every pointer is derived from `smem` alone -- never merged with a global pointer -- so the
+    // compiler keeps them in the LDS address space (ds_* instructions).  A generic pointer would compile to flat_*
+    // accesses, and each flat load waits for vmcnt(0): the prefetched loads of the next iteration.
+    Acc s;
+    {
         size_t off = 0;
         auto carve = [&](size_t bytes) { unsigned char* p = smem + off; off += (bytes + 15) & ~(size_t)15; return p; };
+        s.cnt64 = nullptr; s.vcnt64 = nullptr; s.ocnt64 = nullptr;
         s.cnt32 = (uint32_t*)carve(sizeof(uint32_t) * C);
-        s.vcnt32 = P.vcnt_mode ? (uint32_t*)carve(sizeof(uint32_t) * C) : nullptr;
-        if (MET > 0) s.sum = (double*)carve(sizeof(double) * C);
-        if (MET >= 2) { s.mn = (unsigned long long*)carve(8 * C); s.mx = (unsigned long long*)carve(8 * C); }
-        if (MET >= 3) s.sq = (double*)carve(sizeof(double) * C);
-        if (P.ocnt_mode == OCNT_TERMS || P.ocnt_mode == OCNT_HIST)
-            s.ocnt32 = (uint32_t*)carve(sizeof(uint32_t) * (P.ocnt_mode == OCNT_TERMS ? T : W));
+        s.vcnt32 = (uint32_t*)carve(P.vcnt_mode ? sizeof(uint32_t) * C : 0);
+        s.sum = (double*)carve(MET > 0 ? sizeof(double) * C : 0);
+        s.mn = (unsigned long long*)carve(MET >= 2 ? 8 * C : 0);
+        s.mx = (unsigned long long*)carve(MET >= 2 ? 8 * C : 0);
+        s.sq = (double*)carve(MET >= 3 ? sizeof(double) * C : 0);
+        s.ocnt32 = (uint32_t*)carve(P.ocnt_mode == OCNT_TERMS ? sizeof(uint32_t) * T
+                                    : P.ocnt_mode == OCNT_HIST ? sizeof(uint32_t) * W : 0);
+    }
+    if (P.lds_mode) {
         for (uint32_t c = threadIdx.x; c < C; c += kWG) {
             s.cnt32[c] = 0;
             if (P.vcnt_mode) s.vcnt32[c] = 0;
@@ -451,49 +462,55 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
 
     Run run;
     run_reset(run);
-    Doc4 cur;
+    // software pipeline, kPrefetch iterations deep: the loads of iteration i + kPrefetch are issued before the LDS
+    // updates of iteration i (bytes in flight per CU are what bound a streaming kernel at 2 workgroups per CU)
     const uint32_t tid4 = threadIdx.x * kVec;
-    load_docs<ORD, HIST, MET>(P, b_begin * kBlockDocs + tid4, cur);
+    const uint32_t n_it = (b_end - b_begin) * kItersPerBlock;
+    auto doc_of = [&](uint32_t i) {
+        return (b_begin + i / kItersPerBlock) * kBlockDocs + (i % kItersPerBlock) * kIterDocs + tid4;
+    };
+    Doc4 q[kPrefetch];
+#pragma unroll
+    for (int k = 0; k < kPrefetch; ++k)
+        if ((uint32_t)k < n_it) load_docs<ORD, HIST, MET>(P, doc_of(k), q[k]);
 
-    for (uint32_t b = b_begin; b < b_end; ++b) {
-        // ---- per-block decision (wave-uniform: every lane reads the same zone-map words) ----
-        bool use_lds = P.lds_mode != 0;
-        if (use_lds && HIST && P.windowed) {
-            const int64_t zmn = P.zmin[b], zmx = P.zmax[b];
-            if (zmn <= zmx) {  // block has at least one timestamp
-                const int64_t kmn = floor_div64(zmn - P.offset, P.interval) - P.key0;
-                const int64_t kmx = floor_div64(zmx - P.offset, P.interval) - P.key0;
-                if (kmx - kmn + 1 > (int64_t)W) {
-                    use_lds = false;  // block spans more keys than the window: global atomics for this block
-                } else if (!win_set || kmn < (int64_t)win0 || kmx >= (int64_t)win0 + (int64_t)W) {
-                    if (dirty) {
-                        if (!ORD) run_flush<MET>(P, s, run);
-                        flush_window<MET>(P, s, T, W, win0);
+    bool use_lds = P.lds_mode != 0;
+    for (uint32_t i = 0; i < n_it; ++i) {
+        if (i % kItersPerBlock == 0) {
+            // ---- per-block decision (wave-uniform: every lane reads the same zone-map words) ----
+            const uint32_t b = b_begin + i / kItersPerBlock;
+            use_lds = P.lds_mode != 0;
+            if (use_lds && HIST && P.windowed) {
+                const int64_t zmn = P.zmin[b], zmx = P.zmax[b];
+                if (zmn <= zmx) {  // block has at least one timestamp
+                    const int64_t kmn = floor_div64(zmn - P.offset, P.interval) - P.key0;
+                    const int64_t kmx = floor_div64(zmx - P.offset, P.interval) - P.key0;
+                    if (kmx - kmn + 1 > (int64_t)W) {
+                        use_lds = false;  // block spans more keys than the window: global atomics for this block
+                    } else if (!win_set || kmn < (int64_t)win0 || kmx >= (int64_t)win0 + (int64_t)W) {
+                        if (dirty) {
+                            if (!ORD) run_flush<MET>(P, s, run);
+                            flush_window<MET>(P, s, T, W, win0);
+                        }
+                        dirty = false;
+                        win0 = (uint32_t)kmn;
+                        win_set = true;
+                        base = (P.key0 + (int64_t)win0) * P.interval + P.offset;
                     }
-                    dirty = false;
-                    win0 = (uint32_t)kmn;
-                    win_set = true;
-                    base = (P.key0 + (int64_t)win0) * P.interval + P.offset;
                 }
             }
         }
-        for (int it = 0; it < kItersPerBlock; ++it) {
-            // software pipeline: issue the next iteration's loads before this iteration's LDS updates
-            Doc4 nxt;
-            const bool last = (b + 1 == b_end) && (it + 1 == kItersPerBlock);
-            if (!last) {
-                const uint32_t nb = it + 1 == kItersPerBlock ? b + 1 : b;
-                const int nit = it + 1 == kItersPerBlock ? 0 : it + 1;
-                load_docs<ORD, HIST, MET>(P, nb * kBlockDocs + nit * kIterDocs + tid4, nxt);
-            }
-            if (use_lds) {
-                process4<ORD, HIST, MET, true>(P, s, cur, T, base, W, run);
-                dirty = true;
-            } else {
-                process4<ORD, HIST, MET, false>(P, g, cur, T, base, W, run);
-            }
-            if (!last) cur = nxt;
+        Doc4 nxt;
+        if (i + kPrefetch < n_it) load_docs<ORD, HIST, MET>(P, doc_of(i + kPrefetch), nxt);
+        if (use_lds) {
+            process4<ORD, HIST, MET, true>(P, s, q[0], T, base, W, run);
+            dirty = true;
+        } else {
+            process4<ORD, HIST, MET, false>(P, g, q[0], T, base, W, run);
         }
+#pragma unroll
+        for (int k = 0; k + 1 < kPrefetch; ++k) q[k] = q[k + 1];
+        q[kPrefetch - 1] = nxt;
     }
     if (P.lds_mode && (dirty || !(HIST && P.windowed))) {
         if (!ORD) run_flush<MET>(P, s, run);

@@ -1,7 +1,8 @@
 #!/bin/bash
 # One gpurun session: GPU parity tests, kernel sweep, bench, rocprofv3 kernel-trace stats and PMC HBM-traffic passes.
 #   gpurun --timeout 1200 -- bash tools/gpu_check.sh <tag> [steps...]
-# steps: tests kbench bench prof profk pmc (default: tests kbench bench prof pmc).  Every GPU step has its own time limit; the first failure ends it.
+# steps: tests kbench bench prof profk pmc variants (default: tests kbench bench prof pmc)
+# KBENCH_ONLY=name,name restricts the kbench sweeps; variants = every build/variants/libesgpu_*.so via ESGPU_LIBRARY.  Every GPU step has its own time limit; the first failure ends it.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r1}
@@ -23,7 +24,7 @@ run() {  # name seconds cmd...
 for s in $STEPS; do
     case $s in
         tests) run pytest_gpu 900 python3 -m pytest "$R/tests" -m gpu -x -q -p no:cacheprovider ;;
-        kbench) run kbench 600 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 ;;
+        kbench) run kbench 600 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 ${KBENCH_ONLY:+--only $KBENCH_ONLY} ;;
         bench) run bench 600 python3 "$R/bench.py" ;;
         prof) cd /tmp && run rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
                   python3 "$R/bench.py" --steps 10 --warmup 3 --cpu-docs 0 ;;
@@ -33,6 +34,11 @@ for s in $STEPS; do
                  python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-docs 0 &&
              run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o bench -- \
                  python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-docs 0 ;;
+        variants) for so in "$R"/build/variants/libesgpu_*.so; do
+                      v=$(basename "$so" .so)
+                      ESGPU_LIBRARY=$so run "kbench_$v" 600 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 \
+                          ${KBENCH_ONLY:+--only $KBENCH_ONLY}
+                  done ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done
