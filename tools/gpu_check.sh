@@ -27,13 +27,13 @@ for s in $STEPS; do
         kbench) run kbench 600 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 ${KBENCH_ONLY:+--only $KBENCH_ONLY} ;;
         bench) run bench 600 python3 "$R/bench.py" ;;
         prof) cd /tmp && run rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
-                  python3 "$R/bench.py" --steps 10 --warmup 3 --cpu-docs 0 ;;
+                  python3 "$R/bench.py" --steps 10 --warmup 3 --cpu-docs 0 --inflight 1 ;;
         profk) cd /tmp && run rocprof_kbench 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profk" -o kbench -- \
                    python3 "$R/tools/kbench.py" --docs 1000000000 --reps 3 ;;
         pmc) cd /tmp && run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o bench -- \
-                 python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-docs 0 &&
+                 python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-docs 0 --inflight 1 &&
              run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o bench -- \
-                 python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-docs 0 ;;
+                 python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-docs 0 --inflight 1 ;;
         variants) for so in "$R"/build/variants/libesgpu_*.so; do
                       v=$(basename "$so" .so)
                       ESGPU_LIBRARY=$so run "kbench_$v" 600 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 \
