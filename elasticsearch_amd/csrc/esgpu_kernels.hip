@@ -15,6 +15,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <vector>
 
 #include "es_common.hpp"
 #include "esgpu_kernels.hpp"
@@ -579,26 +580,44 @@ size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocn
 // HLL++ (K8)
 // ------------------------------------------------------------------------------------------------------------
 // hashes of 4 consecutive docs (MurmurHash3Values.Long/Double: mix64; Bytes/ordinals: murmur3 h1 per term)
-__device__ __forceinline__ uint32_t hll_hash4(const HllParams& P, uint32_t i0, uint64_t hv[4]) {
-    uint32_t ok = 0xF;
-    if (i0 + 4 > P.n_docs) ok = (1u << (P.n_docs - i0)) - 1u;
-    if (P.accept) ok &= bits4(P.accept, i0);
-    for (int k = 0; k < P.npred; ++k) ok &= eval_pred(P.pred[k], i0);
+
+// pass 1: HLL registers (max runLen per index).  Registers only grow, so a stale read-check costs at most an extra
+// atomic; after warm-up almost every doc is a read that finds a register already >= its run length.
+// `floor` is a lower bound of every register (min over registers after the previous phase): a hash whose run
+// length is <= floor cannot raise any register, so it needs no register read at all.
+// Each workgroup owns a contiguous doc range and prefetches the next 1024 docs' raw words while it hashes the
+// current ones (mix64 runs at processing time, so the prefetch is never drained early).
+constexpr int kHllWG = 256;
+constexpr uint32_t kHllIter = kHllWG * 4;
+
+__device__ __forceinline__ void hll_load_raw(const HllParams& P, uint32_t i0, uint64_t raw[4]) {
     if (P.kind == HLL_ORD) {
         uint32_t o[4];
         load_u32x4((const uint32_t*)P.col, i0, o);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const bool valid = o[j] != kMissingOrd && o[j] < P.n_ords;
-            if (!valid) ok &= ~(1u << j);
-            hv[j] = valid ? P.ord_hash[o[j]] : 0;
-        }
+        for (int j = 0; j < 4; ++j) raw[j] = o[j];
     } else {
-        int64_t v[4];
-        load_i64x4((const int64_t*)P.col, i0, v);
+        load_i64x4((const int64_t*)P.col, i0, (int64_t*)raw);
+    }
+}
+
+__device__ __forceinline__ uint32_t hll_hash_raw(const HllParams& P, uint32_t i0, const uint64_t raw[4], uint64_t hv[4]) {
+    uint32_t ok = 0xF;
+    if (i0 + 4 > P.n_docs) ok = i0 >= P.n_docs ? 0u : (1u << (P.n_docs - i0)) - 1u;
+    if (P.accept) ok &= bits4(P.accept, i0);
+    for (int k = 0; k < P.npred; ++k) ok &= eval_pred(P.pred[k], i0);
+    if (P.kind == HLL_ORD) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            uint64_t bits = (uint64_t)v[j];
+            const uint32_t o = (uint32_t)raw[j];
+            const bool valid = o != kMissingOrd && o < P.n_ords;
+            if (!valid) ok &= ~(1u << j);
+            hv[j] = valid ? P.ord_hash[o] : 0;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint64_t bits = raw[j];
             if (P.kind == HLL_F64) {  // doubleToLongBits canonicalises NaN
                 const double x = bits_dbl(bits);
                 if (x != x) bits = 0x7ff8000000000000ULL;
@@ -610,35 +629,45 @@ __device__ __forceinline__ uint32_t hll_hash4(const HllParams& P, uint32_t i0, u
     return ok;
 }
 
-// pass 1: HLL registers (max runLen per index).  Registers only grow, so a stale read-check costs at most an extra
-// atomic; after warm-up almost every doc is a read that finds a register already >= its run length.
-// `floor` is a lower bound of every register (min over registers after the previous phase): a hash whose run
-// length is <= floor cannot raise any register, so it needs no register read at all.
-__global__ __launch_bounds__(256) void hll_registers_kernel(HllParams P, uint32_t d_begin, uint32_t d_end,
-                                                            const unsigned int* floor_ptr) {
+__global__ __launch_bounds__(kHllWG) void hll_registers_kernel(HllParams P, uint32_t d_begin, uint32_t d_end,
+                                                               uint32_t per_wg, const unsigned int* floor_ptr) {
     const uint32_t floor = floor_ptr ? *floor_ptr : 0u;
-    const uint32_t gsz = gridDim.x * blockDim.x;
-    for (uint32_t i0 = d_begin + (blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < d_end; i0 += gsz * 4) {
-        uint64_t hv[4];
-        const uint32_t ok = hll_hash4(P, i0, hv);
-        // all register reads first, then the atomics: registers only grow, so a read that races with another
-        // thread's atomicMax can only cause a redundant atomic, never a missed one
-        uint32_t rl[4], idx[4], cur[4];
+    const uint32_t w0 = d_begin + blockIdx.x * per_wg;
+    const uint32_t w1 = min(d_end, w0 + per_wg);
+    if (w0 >= w1) return;
+    const uint32_t t4 = threadIdx.x * 4;
+    uint64_t cur_raw[4] = {0, 0, 0, 0};
+    if (w0 + t4 < w1) hll_load_raw(P, w0 + t4, cur_raw);
+    for (uint32_t base = w0; base < w1; base += kHllIter) {
+        const uint32_t i0 = base + t4, nx = i0 + kHllIter;
+        uint64_t nxt_raw[4] = {0, 0, 0, 0};
+        if (nx < w1) hll_load_raw(P, nx, nxt_raw);
+        if (i0 < w1) {
+            uint64_t hv[4];
+            uint32_t ok = hll_hash_raw(P, i0, cur_raw, hv);
+            if (i0 + 4 > w1) ok &= (1u << (w1 - i0)) - 1u;
+            // all register reads first, then the atomics: registers only grow, so a read that races with another
+            // thread's atomicMax can only cause a redundant atomic, never a missed one
+            uint32_t rl[4], idx[4], cur[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            rl[j] = ((ok >> j) & 1) ? hll_run_len(hv[j], P.p) : 0u;
-            idx[j] = hll_index(hv[j], P.p);
-            cur[j] = rl[j] > floor ? P.regs[idx[j]] : 0xFFu;
+            for (int j = 0; j < 4; ++j) {
+                rl[j] = ((ok >> j) & 1) ? hll_run_len(hv[j], P.p) : 0u;
+                idx[j] = hll_index(hv[j], P.p);
+                cur[j] = rl[j] > floor ? P.regs[idx[j]] : 0xFFu;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (rl[j] > cur[j]) atomicMax(&P.regs[idx[j]], rl[j]);
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if (rl[j] > cur[j]) atomicMax(&P.regs[idx[j]], rl[j]);
+        for (int j = 0; j < 4; ++j) cur_raw[j] = nxt_raw[j];
     }
 }
 
+// min over the registers -> *out (initialised to ~0 by the launcher); one read of the 2^p words by 64 workgroups
 __global__ __launch_bounds__(1024) void hll_floor_kernel(const unsigned int* regs, uint32_t m, unsigned int* out) {
     uint32_t mn = 0xFFFFFFFFu;
-    for (uint32_t i = threadIdx.x; i < m; i += 1024) mn = min(mn, regs[i]);
+    for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < m; i += gridDim.x * 1024) mn = min(mn, regs[i]);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
     __shared__ uint32_t part[16];
@@ -647,7 +676,7 @@ __global__ __launch_bounds__(1024) void hll_floor_kernel(const unsigned int* reg
     if (threadIdx.x == 0) {
         uint32_t t = part[0];
         for (int w = 1; w < 16; ++w) t = min(t, part[w]);
-        *out = t;
+        atomicMin(out, t);
     }
 }
 
@@ -655,7 +684,7 @@ __global__ __launch_bounds__(1024) void hll_floor_kernel(const unsigned int* reg
 // come from distinct encodeHash values), so nonzero > threshold proves the reference ends in HYPERLOGLOG mode.
 __global__ __launch_bounds__(1024) void hll_nonzero_kernel(const unsigned int* regs, uint32_t m, unsigned int* out) {
     uint32_t n = 0;
-    for (uint32_t i = threadIdx.x; i < m; i += 1024) n += regs[i] != 0;
+    for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < m; i += gridDim.x * 1024) n += regs[i] != 0;
     __shared__ uint32_t part[16];
     n = wave_sum_u32(n);
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = n;
@@ -663,7 +692,7 @@ __global__ __launch_bounds__(1024) void hll_nonzero_kernel(const unsigned int* r
     if (threadIdx.x == 0) {
         uint32_t t = 0;
         for (int w = 0; w < 16; ++w) t += part[w];
-        *out = t;
+        if (t) atomicAdd(out, t);  // *out is zeroed with the plan's accumulators
     }
 }
 
@@ -675,8 +704,9 @@ __global__ __launch_bounds__(256) void hll_lc_kernel(HllParams P) {
     const uint32_t gsz = gridDim.x * blockDim.x;
     for (uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < P.n_docs; i0 += gsz * 4) {
         if (__hip_atomic_load(P.lc_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > P.lc_threshold) return;
-        uint64_t hv[4];
-        const uint32_t ok = hll_hash4(P, i0, hv);
+        uint64_t raw[4], hv[4];
+        hll_load_raw(P, i0, raw);
+        const uint32_t ok = hll_hash_raw(P, i0, raw, hv);
         uint32_t added = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -699,28 +729,39 @@ __global__ __launch_bounds__(256) void hll_lc_kernel(HllParams P) {
     }
 }
 
-void launch_hll(const HllParams& p, hipStream_t st) {
-    uint32_t grid = (p.n_docs + 1023) / 1024;
+void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
+    const uint32_t n = p.n_docs;
+    const uint32_t m = 1u << p.p;
+    // phases [0, 16m), then x4 each: every register has seen ~16 hashes after the first cut, so the floor (min
+    // register) starts to rise, and each later phase reads registers only for hashes longer than the floor
+    std::vector<uint32_t> cuts{0};
+    uint64_t c = (uint64_t)m * 16;
+    while (c < n) {
+        cuts.push_back((uint32_t)c & ~3u);
+        c *= 4;
+    }
+    cuts.push_back(n);
+    const uint32_t wgs_max = cus * 8;  // 8 workgroups of 256 threads per CU
+    const uint32_t floor_grid = std::max(1u, std::min(64u, m / 4096));
+    for (size_t ph = 0; ph + 1 < cuts.size(); ++ph) {
+        const uint32_t span = cuts[ph + 1] - cuts[ph];
+        if (span == 0) continue;
+        // contiguous range per workgroup, a multiple of 4 docs, at least 16 iterations of 1024 docs
+        uint32_t wgs = std::max(1u, std::min(wgs_max, span / (kHllIter * 16)));
+        const uint32_t per = ((span + wgs - 1) / wgs + 3) & ~3u;
+        wgs = (span + per - 1) / per;
+        hipLaunchKernelGGL(hll_registers_kernel, dim3(wgs), dim3(kHllWG), 0, st, p, cuts[ph], cuts[ph + 1], per,
+                           ph == 0 ? (const unsigned int*)nullptr : (const unsigned int*)p.floor);
+        if (ph + 2 < cuts.size()) {
+            (void)hipMemsetAsync(p.floor, 0xFF, 4, st);
+            hipLaunchKernelGGL(hll_floor_kernel, dim3(floor_grid), dim3(1024), 0, st, (const unsigned int*)p.regs, m, p.floor);
+        }
+    }
+    (void)hipMemsetAsync(p.nonzero, 0, 4, st);  // recount over the registers (they accumulate across segments)
+    hipLaunchKernelGGL(hll_nonzero_kernel, dim3(floor_grid), dim3(1024), 0, st, (const unsigned int*)p.regs, m, p.nonzero);
+    uint32_t grid = (n + 1023) / 1024;
     if (grid > 8192) grid = 8192;
     if (grid == 0) grid = 1;
-    // phases over [0, n/64), [n/64, n/8), [n/8, n): the register floor from each phase prunes the next one
-    const uint32_t n = p.n_docs;
-    uint32_t cuts[4] = {0, 0, 0, n};
-    if (n >= 64u * 65536u) {
-        cuts[1] = (n / 64) & ~3u;
-        cuts[2] = (n / 8) & ~3u;
-    }
-    const uint32_t m = 1u << p.p;
-    for (int ph = 0; ph < 3; ++ph) {
-        if (cuts[ph + 1] <= cuts[ph]) continue;
-        const uint32_t span = cuts[ph + 1] - cuts[ph];
-        const uint32_t g = std::max(1u, std::min(grid, (span + 1023) / 1024));
-        hipLaunchKernelGGL(hll_registers_kernel, dim3(g), dim3(256), 0, st, p, cuts[ph], cuts[ph + 1],
-                           ph == 0 ? (const unsigned int*)nullptr : (const unsigned int*)p.floor);
-        if (ph < 2 && cuts[ph + 1] < n)
-            hipLaunchKernelGGL(hll_floor_kernel, dim3(1), dim3(1024), 0, st, (const unsigned int*)p.regs, m, p.floor);
-    }
-    hipLaunchKernelGGL(hll_nonzero_kernel, dim3(1), dim3(1024), 0, st, (const unsigned int*)p.regs, 1u << p.p, p.nonzero);
     hipLaunchKernelGGL(hll_lc_kernel, dim3(grid), dim3(256), 0, st, p);
 }
 
@@ -758,6 +799,14 @@ void launch_gather_rows(const GatherParams& p, hipStream_t st) {
 __global__ void fill_u64_kernel(unsigned long long* p, size_t n, unsigned long long v) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
 }
+__global__ void pack_u8_kernel(const unsigned int* src, uint32_t n, uint8_t* dst) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) dst[i] = (uint8_t)src[i];
+}
+void launch_pack_u8(const unsigned int* src, uint32_t n, uint8_t* dst, hipStream_t st) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(pack_u8_kernel, dim3(std::min<uint32_t>(1024, (n + 255) / 256)), dim3(256), 0, st, src, n, dst);
+}
+
 void launch_fill_u64(unsigned long long* p, size_t n, unsigned long long v, hipStream_t st) {
     if (n == 0) return;
     size_t grid = (n + 255) / 256;
@@ -839,17 +888,25 @@ __device__ uint32_t block_exclusive_scan(uint32_t* v, uint32_t n, uint32_t* wave
     return total;
 }
 
-// pass 3: scatter through an LDS-staged tile.  Every 8192-doc block is counting-sorted by partition in LDS first, so
-// the global writes are runs of consecutive 16-bit partition-local offsets instead of 8192 scattered words.
+// pass 3: scatter through an LDS-staged tile.  Every tile (kScatterTB 8192-doc blocks) is counting-sorted by
+// partition in LDS first, so the global writes are runs of consecutive 16-bit partition-local offsets instead of
+// scattered words; the larger the tile, the longer the runs and the fewer partially written lines leave L2.
+#ifndef ESGPU_SCATTER_TB
+#define ESGPU_SCATTER_TB 4
+#endif
+constexpr int kScatterTB = ESGPU_SCATTER_TB;
+constexpr uint32_t kScatterTile = kScatterTB * kBlockDocs;
+
 __global__ __launch_bounds__(kWG) void part_scatter_kernel(PartParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t* cursor = (uint32_t*)smem;      // [P] next write position of (partition, this workgroup)
     uint32_t* tcnt = cursor + P.P;           // [P] elements of the tile per partition
     uint32_t* toff = tcnt + P.P;             // [P] their exclusive offsets inside the tile
-    uint32_t* stage = toff + P.P;            // [kBlockDocs] the tile, sorted by partition
+    uint32_t* stage = toff + P.P;            // [kScatterTile] the tile, sorted by partition
     __shared__ uint32_t wave_tot[kWG / 64];
     const uint32_t g = blockIdx.x;
     const uint32_t mask = (1u << P.shift) - 1u;
+    constexpr int kIt = kScatterTB * kItersPerBlock;
     for (uint32_t p = threadIdx.x; p < P.P; p += kWG) {
         cursor[p] = P.wg_counts[(size_t)p * P.G + g];
         tcnt[p] = 0u;
@@ -857,19 +914,24 @@ __global__ __launch_bounds__(kWG) void part_scatter_kernel(PartParams P) {
     __syncthreads();
     const uint32_t b_begin = g * P.blocks_per_wg;
     const uint32_t b_end = min(b_begin + P.blocks_per_wg, P.n_blocks);
-    for (uint32_t b = b_begin; b < b_end; ++b) {
-        uint32_t o[kItersPerBlock][4], ok[kItersPerBlock], rank[kItersPerBlock][4];
+    for (uint32_t b = b_begin; b < b_end; b += kScatterTB) {
+        uint32_t o[kIt][4], ok[kIt], rank[kIt][4];
 #pragma unroll
-        for (int it = 0; it < kItersPerBlock; ++it) {
-            const uint32_t doc0 = b * kBlockDocs + it * kIterDocs + threadIdx.x * kVec;
-            load_u32x4(P.ord, doc0, o[it]);
-            ok[it] = 0xF;
-            if (doc0 + 4 > P.n_docs) ok[it] = doc0 >= P.n_docs ? 0u : ((1u << (P.n_docs - doc0)) - 1u);
-            if (P.accept) ok[it] &= bits4(P.accept, doc0);
-            for (int k = 0; k < P.npred; ++k) ok[it] &= eval_pred(P.pred[k], doc0);
+        for (int it = 0; it < kIt; ++it) {
+            const uint32_t blk = b + it / kItersPerBlock;
+            const uint32_t doc0 = blk * kBlockDocs + (it % kItersPerBlock) * kIterDocs + threadIdx.x * kVec;
+            ok[it] = 0u;
+            o[it][0] = o[it][1] = o[it][2] = o[it][3] = 0u;
+            if (blk < b_end) {
+                load_u32x4(P.ord, doc0, o[it]);
+                ok[it] = 0xF;
+                if (doc0 + 4 > P.n_docs) ok[it] = doc0 >= P.n_docs ? 0u : ((1u << (P.n_docs - doc0)) - 1u);
+                if (P.accept) ok[it] &= bits4(P.accept, doc0);
+                for (int k = 0; k < P.npred; ++k) ok[it] &= eval_pred(P.pred[k], doc0);
+            }
         }
 #pragma unroll
-        for (int it = 0; it < kItersPerBlock; ++it)
+        for (int it = 0; it < kIt; ++it)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const bool v = ((ok[it] >> j) & 1) && o[it][j] < P.T;
@@ -881,7 +943,7 @@ __global__ __launch_bounds__(kWG) void part_scatter_kernel(PartParams P) {
         const uint32_t n_tile = block_exclusive_scan(toff, P.P, wave_tot);
         __syncthreads();
 #pragma unroll
-        for (int it = 0; it < kItersPerBlock; ++it)
+        for (int it = 0; it < kIt; ++it)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 if (rank[it][j] != 0xFFFFFFFFu) stage[toff[o[it][j] >> P.shift] + rank[it][j]] = o[it][j];
@@ -904,9 +966,16 @@ void launch_part_hist(const PartParams& p, hipStream_t s) {
     hipLaunchKernelGGL(part_hist_kernel, dim3(p.G), dim3(kWG), (size_t)p.P * 4, s, p);
 }
 void launch_part_scatter(const PartParams& p, hipStream_t s) {
-    hipLaunchKernelGGL(part_scatter_kernel, dim3(p.G), dim3(kWG), ((size_t)p.P * 3 + kBlockDocs) * 4, s, p);
+    hipLaunchKernelGGL(part_scatter_kernel, dim3(p.G), dim3(kWG), part_scatter_lds_bytes(p.P), s, p);
 }
-size_t part_scatter_lds_bytes(uint32_t n_parts) { return ((size_t)n_parts * 3 + kBlockDocs) * 4; }
+size_t part_scatter_lds_bytes(uint32_t n_parts) { return ((size_t)n_parts * 3 + kScatterTile) * 4; }
+uint32_t part_wg_per_cu() {  // the staged tile takes most of the LDS: one scatter workgroup per CU
+#ifdef ESGPU_PART_WG_PER_CU
+    return ESGPU_PART_WG_PER_CU;
+#else
+    return 1;
+#endif
+}
 
 // exclusive scan of wg_counts[P*G] (partition-major) in place; part_begin[p] = offset of (p, g = 0), [P] = total.
 // Three launches over 4096-element tiles (tile sums, scan of the tile sums, tile-local scans), all coalesced.
@@ -1143,7 +1212,108 @@ __global__ __launch_bounds__(1024) void topk_kernel(TopkParams P, const unsigned
     }
 }
 
+// Count-ordered top-k by selection instead of sorting every ordinal (10M counts -> two streaming passes):
+//   topk_hist      log-scale histogram of the eligible counts (32 sub-bins per power of two, 2048 bins, monotone in
+//                  the key) + the sum of all counts
+//   topk_thresh    one workgroup: the highest bin b* such that bins >= b* hold at least k candidates
+//   topk_compact   every eligible ordinal whose bin >= b* -> candidate keys (wave-aggregated append)
+//   topk_final     one workgroup: chunked bitonic top-k over the candidates (usually a few hundred)
+constexpr uint32_t kTopkBins = 2048;
+
+__device__ __forceinline__ uint32_t count_bin(int order, unsigned long long c) {
+    uint32_t b;
+    if (c < 32) {
+        b = (uint32_t)c;
+    } else {
+        const uint32_t e = 63u - (uint32_t)__clzll((long long)c);  // >= 5
+        b = (e - 4) * 32 + (uint32_t)((c >> (e - 5)) & 31u);       // 32 sub-bins per octave, >= 32
+    }
+    b = min(b, kTopkBins - 1);
+    return order == 0 ? b : kTopkBins - 1 - b;  // COUNT_ASC: fewer docs = better
+}
+
+__device__ __forceinline__ bool topk_eligible(const TopkParams& P, unsigned long long c) {
+    return !(P.min_doc_count > 0 && c == 0) && (long long)c >= P.shard_min_doc_count;
+}
+
+__global__ __launch_bounds__(1024) void topk_hist_kernel(TopkParams P) {
+    __shared__ uint32_t hist[kTopkBins];
+    for (uint32_t i = threadIdx.x; i < kTopkBins; i += 1024) hist[i] = 0;
+    __syncthreads();
+    unsigned long long sum = 0;
+    for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < P.T; i += gridDim.x * 1024) {
+        const unsigned long long c = P.counts[i];
+        sum += c;
+        if (topk_eligible(P, c)) atomicAdd(&hist[count_bin(P.order, c)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < kTopkBins; i += 1024)
+        if (hist[i]) atomicAdd(&P.hist[i], hist[i]);
+    sum = wave_sum_u64(sum);
+    if ((threadIdx.x & 63) == 0 && sum) atomicAdd(P.out_sum, sum);
+}
+
+__global__ __launch_bounds__(64) void topk_thresh_kernel(TopkParams P) {
+    if (threadIdx.x != 0) return;
+    uint32_t acc = 0, b = kTopkBins;
+    while (b > 0 && acc < P.k) acc += P.hist[--b];
+    P.sel[0] = b;  // bins >= b hold >= k candidates (or every candidate)
+    P.sel[1] = 0;  // candidate counter for topk_compact
+}
+
+__global__ __launch_bounds__(1024) void topk_compact_kernel(TopkParams P) {
+    const uint32_t tb = P.sel[0];
+    const int lane = threadIdx.x & 63;
+    for (uint32_t i0 = blockIdx.x * 1024; i0 < P.T; i0 += gridDim.x * 1024) {
+        const uint32_t i = i0 + threadIdx.x;
+        bool take = false;
+        unsigned long long key = 0;
+        if (i < P.T) {
+            const unsigned long long c = P.counts[i];
+            take = topk_eligible(P, c) && count_bin(P.order, c) >= tb;
+            if (take) key = make_topk_key(P.order, c, i);
+        }
+        const unsigned long long m = __ballot(take);
+        if (m == 0) continue;
+        uint32_t base = 0;
+        if (lane == __ffsll((long long)m) - 1) base = atomicAdd(&P.sel[1], (uint32_t)__popcll(m));
+        base = __shfl(base, __ffsll((long long)m) - 1, 64);
+        if (take) P.cand[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = key;
+    }
+}
+
+// one workgroup: best k of the n = sel[1] candidate keys, chunked bitonic sort + merge (chunk = pow2 >= n, <= 4096)
+__global__ __launch_bounds__(1024) void topk_final_kernel(TopkParams P) {
+    __shared__ unsigned long long chunk[kTopkChunk];
+    __shared__ unsigned long long best[2 * kTopkMax];
+    const uint32_t n = P.sel[1];
+    uint32_t kp = 1;
+    while (kp < P.k) kp <<= 1;
+    uint32_t cs = 64;
+    while (cs < n && cs < kTopkChunk) cs <<= 1;
+    if (cs < kp) cs = kp;
+    for (uint32_t i = threadIdx.x; i < kp; i += 1024) best[i] = 0;
+    for (uint32_t c0 = 0; c0 < max(n, 1u); c0 += cs) {
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < cs; t += 1024) chunk[t] = c0 + t < n ? P.cand[c0 + t] : 0ull;
+        bitonic_sort_desc(chunk, cs);
+        for (uint32_t t = threadIdx.x; t < kp; t += 1024) best[kp + t] = chunk[kp - 1 - t];
+        bitonic_merge_desc(best, 2 * kp);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < P.k; i += 1024) P.out_keys[i] = best[i];
+}
+
 void launch_topk(const TopkParams& p, hipStream_t s) {
+    if (p.order == 0 || p.order == 1) {  // count orders: select, then sort the few candidates
+        const uint32_t g = std::max(1u, std::min(p.n_wg, (p.T + 1023) / 1024));
+        (void)hipMemsetAsync(p.hist, 0, kTopkBins * 4, s);
+        hipLaunchKernelGGL(topk_hist_kernel, dim3(g), dim3(1024), 0, s, p);
+        hipLaunchKernelGGL(topk_thresh_kernel, dim3(1), dim3(64), 0, s, p);
+        hipLaunchKernelGGL(topk_compact_kernel, dim3(g), dim3(1024), 0, s, p);
+        hipLaunchKernelGGL(topk_final_kernel, dim3(1), dim3(1024), 0, s, p);
+        return;
+    }
     const uint32_t per1 = (uint32_t)(((uint64_t)p.T + p.n_wg - 1) / p.n_wg);
     hipLaunchKernelGGL((topk_kernel<true>), dim3(p.n_wg), dim3(1024), 0, s, p, p.counts, p.T, per1, p.cand);
     const uint32_t nc = p.n_wg * p.k;

@@ -112,7 +112,8 @@ void launch_synth(const SynthParams& p, hipStream_t s);
 void launch_collect(const CollectParams& p, bool ord, bool hist, int met, uint32_t grid, size_t lds, hipStream_t s);
 size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode);
 int collect_occupancy(bool ord, bool hist, int met, size_t lds);  // resident workgroups per CU
-void launch_hll(const HllParams& p, hipStream_t s);
+void launch_hll(const HllParams& p, uint32_t cus, hipStream_t s);
+void launch_pack_u8(const unsigned int* src, uint32_t n, uint8_t* dst, hipStream_t s);
 void launch_term_totals(const unsigned long long* cnt, uint32_t H, uint32_t T, unsigned long long* out, hipStream_t s);
 void launch_gather_rows(const GatherParams& p, hipStream_t s);
 void launch_fill_u64(unsigned long long* p, size_t n, unsigned long long v, hipStream_t s);
@@ -145,6 +146,7 @@ void launch_part_scan(const PartParams& p, hipStream_t s);
 void launch_part_scatter(const PartParams& p, hipStream_t s);
 void launch_part_count(const PartParams& p, hipStream_t s);
 size_t part_scatter_lds_bytes(uint32_t n_parts);
+uint32_t part_wg_per_cu();  // workgroups per CU of the histogram / scatter passes
 uint32_t part_scan_tiles(uint32_t n);
 
 // ---- GPU top-k over a count vector (BucketPriorityQueue replacement for large T) ----
@@ -154,7 +156,9 @@ struct TopkParams {
     int32_t order;           // ESGPU_ORDER_COUNT_DESC / COUNT_ASC / TERM_ASC / TERM_DESC
     int64_t min_doc_count, shard_min_doc_count;
     uint32_t k;              // <= kTopkMax
-    unsigned long long* cand;    // [n_wg][k] candidate keys from pass 1
+    unsigned long long* cand;    // candidate keys: [n_wg][k] (term orders) or up to T (count orders)
+    uint32_t* hist;              // count orders: [2048] count histogram
+    uint32_t* sel;               // count orders: [2] threshold bin, candidate counter
     uint32_t n_wg;
     unsigned long long* out_keys;    // [k] winners (0 = none), best first
     unsigned long long* out_sum;     // [1] sum of counts over min_doc_count-eligible terms

@@ -605,7 +605,7 @@ struct esgpu_plan {
     std::map<std::string, std::vector<std::string>> term_cache;  // terms reachable after the segment is destroyed
     // per-request scratch, reused across requests
     Scratch s_accept, s_tcnt, s_rows, s_dst[6];
-    Scratch s_wgc, s_pbeg, s_pbuf, s_tiles, s_cand, s_keys;  // partitioned counting + GPU top-k
+    Scratch s_wgc, s_pbeg, s_pbuf, s_tiles, s_cand, s_keys, s_hist;  // partitioned counting + GPU top-k
     PinnedBuf h_keys;
     hipEvent_t ev_mid = nullptr;
     PinnedBuf h_tcnt, h_rows, h_dst[6];
@@ -862,7 +862,7 @@ static bool collect_partitioned(esgpu_plan* p, Pipeline& pl, const esgpu_segment
     PartParams Q{};
     Q.n_docs = s->max_doc;
     Q.n_blocks = s->n_pad / kBlockDocs;
-    const uint32_t target = (uint32_t)c->cus * 2;
+    const uint32_t target = (uint32_t)c->cus * part_wg_per_cu();
     Q.blocks_per_wg = std::max(1u, (Q.n_blocks + target - 1) / target);
     Q.G = (Q.n_blocks + Q.blocks_per_wg - 1) / Q.blocks_per_wg;
     Q.ord = oc->values.as<uint32_t>();
@@ -1089,7 +1089,7 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
     H.lc_threshold = pl.lc_threshold;
     if (H.n_docs == 0) return false;
     HIPX(hipEventRecord(pl.e0, p->stream));
-    launch_hll(H, p->stream);
+    launch_hll(H, (uint32_t)p->ctx->cus, p->stream);
     HIPX(hipGetLastError());
     HIPX(hipEventRecord(pl.e1, p->stream));
     p->last_bytes += bytes_per_doc * (uint64_t)s->max_doc;
@@ -1177,11 +1177,14 @@ extern "C" int esgpu_plan_post_collection(esgpu_plan* p) {
                 std::sort(pl.h_lc.begin(), pl.h_lc.end());
             } else {  // HYPERLOGLOG
                 pl.hll_mode = 1;
-                uint32_t* r = (uint32_t*)p->h_dst[0].ensure((size_t)m * 4);
-                HIPX(hipMemcpyAsync(r, pl.regs.p, (size_t)m * 4, hipMemcpyDeviceToHost, p->stream));
+                // registers are u32 on the device (atomicMax); pack to the reference's byte array before the copy
+                uint8_t* d8 = (uint8_t*)p->s_dst[0].ensure(p->ctx, m);
+                launch_pack_u8(pl.regs.as<unsigned int>(), m, d8, p->stream);
+                HIPX(hipGetLastError());
+                uint8_t* r = (uint8_t*)p->h_dst[0].ensure(m);
+                HIPX(hipMemcpyAsync(r, d8, m, hipMemcpyDeviceToHost, p->stream));
                 HIPX(hipStreamSynchronize(p->stream));
-                pl.h_regs.resize(m);
-                for (uint32_t i = 0; i < m; ++i) pl.h_regs[i] = (uint8_t)r[i];
+                pl.h_regs.assign(r, r + m);
             }
         }
         p->posted = true;
@@ -1416,7 +1419,11 @@ static Block build_grid(esgpu_plan* p, Pipeline& pl) {
             K.shard_min_doc_count = tn.s.shard_min_doc_count;
             K.k = kk;
             K.n_wg = std::min<uint32_t>(512, (K.T + 4095) / 4096);
-            K.cand = (unsigned long long*)p->s_cand.ensure(p->ctx, (size_t)K.n_wg * kk * 8);
+            const bool select = K.order == ESGPU_ORDER_COUNT_DESC || K.order == ESGPU_ORDER_COUNT_ASC;
+            K.cand = (unsigned long long*)p->s_cand.ensure(p->ctx, (select ? (size_t)K.T : (size_t)K.n_wg * kk) * 8);
+            uint32_t* hs = (uint32_t*)p->s_hist.ensure(p->ctx, (2048 + 2) * 4);
+            K.hist = hs;
+            K.sel = hs + 2048;
             unsigned long long* dk = (unsigned long long*)p->s_keys.ensure(p->ctx, ((size_t)kk + 1) * 8);
             K.out_keys = dk;
             K.out_sum = dk + kk;
@@ -1547,8 +1554,9 @@ static Block build_cardinality(esgpu_plan* p, Pipeline& pl) {
     r.precision = pl.p;
     r.append_empty();  // counts == null
     if (!pl.allocated || !pl.any_value) return r;
-    // CardinalityAggregator:141-143 — an all-zero sketch is reported as "no counts"
-    if (hll_cardinality(pl.p, true, pl.hll_mode, pl.h_regs.data(), pl.h_lc.size()) == 0) return r;
+    // CardinalityAggregator:141-143 — a sketch whose cardinality is 0 is reported as "no counts".  That is exactly
+    // an empty linear-counting set: HYPERLOGLOG mode implies more than threshold distinct hashes.
+    if (pl.hll_mode == 0 && pl.h_lc.empty()) return r;
     r.hll_present[0] = 1;
     r.hll_mode[0] = pl.hll_mode;
     r.lc[0] = pl.h_lc;

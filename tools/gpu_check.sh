@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun session: GPU parity tests, kernel sweep, bench, rocprofv3 kernel-trace stats and PMC HBM-traffic passes.
 #   gpurun --timeout 1200 -- bash tools/gpu_check.sh <tag> [steps...]
-# steps: tests kbench bench prof profk pmc variants (default: tests kbench bench prof pmc)
+# steps: tests kbench bench prof profk pmc pmck variants (default: tests kbench bench prof pmc)
 # KBENCH_ONLY=name,name restricts the kbench sweeps; variants = every build/variants/libesgpu_*.so via ESGPU_LIBRARY.  Every GPU step has its own time limit; the first failure ends it.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -34,6 +34,14 @@ for s in $STEPS; do
                  python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-docs 0 --inflight 1 &&
              run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o bench -- \
                  python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-docs 0 --inflight 1 ;;
+        pmck) # counters for the kbench shapes in KBENCH_ONLY (default config3_url), one counter group per pass
+              for grp in FETCH_SIZE WRITE_SIZE "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
+                         "SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT"; do
+                  tag=$(echo "$grp" | cut -d' ' -f1)
+                  cd /tmp && run "pmck_$tag" 600 rocprofv3 --pmc $grp --kernel-trace --output-format csv \
+                      -d "$OUT/pmck_$tag" -o kb -- python3 "$R/tools/kbench.py" --docs 1000000000 --reps 1 \
+                      --only "${KBENCH_ONLY:-config3_url}"
+              done ;;
         variants) for so in "$R"/build/variants/libesgpu_*.so; do
                       v=$(basename "$so" .so)
                       ESGPU_LIBRARY=$so run "kbench_$v" 600 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 \
