@@ -110,6 +110,11 @@ SIGNATURES = [
                                                  ctypes.c_uint64, ctypes.c_uint64, _VP]),
     ("esgpu_synthetic_term", ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_size_t]),
     ("esgpu_segment_read_column", ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64, _VP]),
+    ("esgpu_ordinal_map_build", ctypes.c_int, [_VP, ctypes.POINTER(_VP), ctypes.c_int32, ctypes.c_char_p,
+                                               ctypes.POINTER(_VP)]),
+    ("esgpu_ordinal_map_value_count", ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_uint64)]),
+    ("esgpu_ordinal_map_lookup", ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int64)]),
+    ("esgpu_ordinal_map_destroy", ctypes.c_int, [_VP]),
     ("esgpu_terms_thresholds", ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
                                               ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
                                               ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),

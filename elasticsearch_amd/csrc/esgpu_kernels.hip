@@ -799,6 +799,25 @@ void launch_gather_rows(const GatherParams& p, hipStream_t st) {
 __global__ void fill_u64_kernel(unsigned long long* p, size_t n, unsigned long long v) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
 }
+// global ordinals: out[d] = map[in[d]] (ordinals outside the segment dictionary, incl. missing, stay missing)
+__global__ void remap_ords_kernel(const uint32_t* in, uint32_t n, const uint32_t* map, uint32_t map_n, uint32_t* out) {
+    for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += gridDim.x * blockDim.x * 4) {
+        uint32_t o[4];
+        load_u32x4(in, i, o);  // n is a multiple of kBlockDocs
+        uint4 r;
+        r.x = o[0] < map_n ? map[o[0]] : kMissingOrd;
+        r.y = o[1] < map_n ? map[o[1]] : kMissingOrd;
+        r.z = o[2] < map_n ? map[o[2]] : kMissingOrd;
+        r.w = o[3] < map_n ? map[o[3]] : kMissingOrd;
+        *reinterpret_cast<uint4*>(out + i) = r;
+    }
+}
+void launch_remap_ords(const uint32_t* in, uint32_t n, const uint32_t* map, uint32_t map_n, uint32_t* out, hipStream_t st) {
+    if (n == 0) return;
+    const uint32_t grid = std::min<uint32_t>(4096, (n / 4 + 255) / 256);
+    hipLaunchKernelGGL(remap_ords_kernel, dim3(grid), dim3(256), 0, st, in, n, map, map_n, out);
+}
+
 __global__ void pack_u8_kernel(const unsigned int* src, uint32_t n, uint8_t* dst) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) dst[i] = (uint8_t)src[i];
 }

@@ -113,6 +113,7 @@ void launch_collect(const CollectParams& p, bool ord, bool hist, int met, uint32
 size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode);
 int collect_occupancy(bool ord, bool hist, int met, size_t lds);  // resident workgroups per CU
 void launch_hll(const HllParams& p, uint32_t cus, hipStream_t s);
+void launch_remap_ords(const uint32_t* in, uint32_t n, const uint32_t* map, uint32_t map_n, uint32_t* out, hipStream_t s);
 void launch_pack_u8(const unsigned int* src, uint32_t n, uint8_t* dst, hipStream_t s);
 void launch_term_totals(const unsigned long long* cnt, uint32_t H, uint32_t T, unsigned long long* out, hipStream_t s);
 void launch_gather_rows(const GatherParams& p, hipStream_t s);

@@ -19,6 +19,8 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <queue>
+#include <string_view>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -266,6 +268,16 @@ extern "C" int esgpu_synthetic_fill_host(uint64_t seed, uint32_t shard, uint32_t
 // ------------------------------------------------------------------------------------------------------------
 // segments
 // ------------------------------------------------------------------------------------------------------------
+// Global term dictionary of one keyword field over the segments of a reader (Lucene OrdinalMap).
+struct GlobalDict {
+    std::vector<uint8_t> bytes;
+    std::vector<uint64_t> offsets;  // count + 1
+    uint64_t count() const { return offsets.empty() ? 0 : offsets.size() - 1; }
+    std::string term(uint64_t g) const {
+        return std::string((const char*)bytes.data() + offsets[g], (size_t)(offsets[g + 1] - offsets[g]));
+    }
+};
+
 struct DevColumn {
     std::string name;
     int32_t type = 0;
@@ -280,6 +292,13 @@ struct DevColumn {
     std::vector<uint64_t> dict_offsets;
     uint32_t synth_bit = 0;
     DevBuf ord_hash;  // murmur3 h1 per term (built lazily for cardinality on keyword fields)
+    // global ordinals (esgpu_ordinal_map_build): the segment's ordinals remapped into the reader-wide dictionary
+    std::shared_ptr<const GlobalDict> gdict;
+    DevBuf gvalues;
+
+    const DevBuf& ords() const { return gdict ? gvalues : values; }       // what terms aggregations count by
+    uint64_t ord_count() const { return gdict ? gdict->count() : value_count; }
+    std::string ord_term(uint64_t ord) const { return gdict ? gdict->term(ord) : term(ord); }
 
     std::string term(uint64_t ord) const {
         if (synth_bit) {
@@ -461,6 +480,129 @@ extern "C" int esgpu_segment_read_column(const esgpu_segment* s, const char* fie
         HIPX(hipSetDevice(s->ctx->device));
         HIPX(hipMemcpy(out, col->values.as<uint8_t>() + start * w, count * w, hipMemcpyDeviceToHost));
     });
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Global ordinals across the segments of a reader (GlobalOrdinalsBuilder.build -> Lucene OrdinalMap,
+// GlobalOrdinalsBuilder.java:45-70, GlobalOrdinalMapping.java:51-58).  Segment dictionaries are sorted by unsigned
+// bytes; their union in that order defines the global ordinals.  The dictionaries are merged on the host (once per
+// reader, as Lucene does), then every segment's ordinal column is remapped on the GPU.
+// ------------------------------------------------------------------------------------------------------------
+struct esgpu_ordinal_map {
+    std::shared_ptr<const GlobalDict> dict;
+};
+
+static std::string_view dict_view(const DevColumn* c, uint64_t o, std::string& scratch) {
+    if (c->synth_bit) {
+        char b[32];
+        esgpu_synthetic_term(c->synth_bit, o, b, sizeof b);
+        scratch = b;
+        return scratch;
+    }
+    return std::string_view((const char*)c->dict_bytes.data() + c->dict_offsets[o],
+                            (size_t)(c->dict_offsets[o + 1] - c->dict_offsets[o]));
+}
+
+extern "C" int esgpu_ordinal_map_build(esgpu_ctx* ctx, esgpu_segment* const* segs, int32_t nsegs, const char* field,
+                                       esgpu_ordinal_map** out) {
+    return guarded([&] {
+        require(ctx && segs && nsegs >= 1 && field && out, ESGPU_ERR_INVALID, "bad ordinal map arguments");
+        HIPX(hipSetDevice(ctx->device));
+        std::vector<DevColumn*> cols;
+        for (int i = 0; i < nsegs; ++i) {
+            require(segs[i] != nullptr, ESGPU_ERR_INVALID, "null segment");
+            auto it = segs[i]->cols.find(field);
+            if (it == segs[i]->cols.end()) { cols.push_back(nullptr); continue; }  // unmapped in this segment
+            DevColumn* c = it->second.get();
+            require(c->type == ESGPU_COL_ORD_U32 && !c->multi, ESGPU_ERR_UNSUPPORTED, "ordinal maps cover single-valued keyword columns");
+            require(c->synth_bit || c->dict_offsets.size() == c->value_count + 1, ESGPU_ERR_INVALID,
+                    std::string("no term dictionary for ") + field);
+            cols.push_back(c);
+        }
+        // k-way merge of the sorted segment dictionaries (unsigned byte order, BytesRef.compareTo)
+        auto g = std::make_shared<GlobalDict>();
+        g->offsets.push_back(0);
+        std::vector<std::vector<uint32_t>> maps(cols.size());
+        std::vector<uint64_t> pos(cols.size(), 0);
+        std::vector<std::string> cur(cols.size()), scratch(cols.size());
+        using Item = std::pair<std::string_view, int>;
+        auto cmp = [](const Item& a, const Item& b) { return b.first < a.first || (a.first == b.first && b.second < a.second); };
+        std::priority_queue<Item, std::vector<Item>, decltype(cmp)> heap(cmp);
+        for (size_t k = 0; k < cols.size(); ++k) {
+            if (!cols[k]) continue;
+            maps[k].resize(cols[k]->value_count);
+            if (cols[k]->value_count) heap.push({dict_view(cols[k], 0, scratch[k]), (int)k});
+        }
+        std::string last;
+        bool have_last = false;
+        while (!heap.empty()) {
+            const auto [term, k] = heap.top();
+            heap.pop();
+            if (!have_last || term != std::string_view(last)) {
+                last.assign(term.data(), term.size());
+                have_last = true;
+                g->bytes.insert(g->bytes.end(), last.begin(), last.end());
+                g->offsets.push_back(g->bytes.size());
+                require(g->count() < 0xFFFFFFFFull, ESGPU_ERR_UNSUPPORTED, "more than 2^32-1 global ordinals");
+            }
+            const uint64_t o = pos[k]++;
+            maps[k][o] = (uint32_t)(g->count() - 1);
+            if (pos[k] < cols[k]->value_count) {
+                const std::string_view nx = dict_view(cols[k], pos[k], scratch[k]);  // last == this segment's term
+                require(std::string_view(last) < nx, ESGPU_ERR_INVALID, "segment dictionary not strictly sorted");
+                heap.push({nx, k});
+            }
+        }
+        // remap every segment's column on the GPU: gvalues[d] = map[values[d]] (missing stays missing)
+        for (size_t k = 0; k < cols.size(); ++k) {
+            DevColumn* c = cols[k];
+            if (!c) continue;
+            DevBuf dmap;
+            dmap.alloc(ctx, std::max<size_t>(maps[k].size(), 1) * 4);
+            if (!maps[k].empty()) HIPX(hipMemcpy(dmap.p, maps[k].data(), maps[k].size() * 4, hipMemcpyHostToDevice));
+            DevBuf gv;
+            gv.alloc(ctx, c->values.bytes);
+            launch_remap_ords(c->values.as<uint32_t>(), (uint32_t)(c->values.bytes / 4), dmap.as<uint32_t>(),
+                              (uint32_t)maps[k].size(), gv.as<uint32_t>(), nullptr);
+            HIPX(hipGetLastError());
+            HIPX(hipDeviceSynchronize());
+            c->gvalues = std::move(gv);
+            c->gdict = g;
+        }
+        std::unique_ptr<esgpu_ordinal_map> m(new esgpu_ordinal_map());
+        m->dict = g;
+        *out = m.release();
+    });
+}
+
+extern "C" int esgpu_ordinal_map_value_count(const esgpu_ordinal_map* m, uint64_t* count) {
+    return guarded([&] {
+        require(m && count, ESGPU_ERR_INVALID, "null argument");
+        *count = m->dict->count();
+    });
+}
+
+extern "C" int esgpu_ordinal_map_lookup(const esgpu_ordinal_map* m, const uint8_t* term, size_t len, int64_t* ord) {
+    return guarded([&] {
+        require(m && ord && (term || len == 0), ESGPU_ERR_INVALID, "null argument");
+        const GlobalDict& d = *m->dict;
+        const std::string_view key((const char*)term, len);
+        uint64_t lo = 0, hi = d.count();
+        while (lo < hi) {  // lower bound in unsigned byte order
+            const uint64_t mid = (lo + hi) / 2;
+            const std::string_view t((const char*)d.bytes.data() + d.offsets[mid], (size_t)(d.offsets[mid + 1] - d.offsets[mid]));
+            if (t < key) lo = mid + 1; else hi = mid;
+        }
+        *ord = -1;
+        if (lo < d.count()) {
+            const std::string_view t((const char*)d.bytes.data() + d.offsets[lo], (size_t)(d.offsets[lo + 1] - d.offsets[lo]));
+            if (t == key) *ord = (int64_t)lo;
+        }
+    });
+}
+
+extern "C" int esgpu_ordinal_map_destroy(esgpu_ordinal_map* m) {
+    return guarded([&] { delete m; });  // segments keep the dictionary they were remapped into
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -809,7 +951,7 @@ static void set_preds(esgpu_plan* p, const esgpu_segment* s, PredDev* out, int32
         PredDev q{};
         require(col != nullptr, ESGPU_ERR_UNSUPPORTED, "filter on a field missing from the segment");
         require(!col->multi, ESGPU_ERR_UNSUPPORTED, "filters on multi-valued fields run on the CPU path");
-        q.col = col->values.p;
+        q.col = col->type == ESGPU_COL_ORD_U32 ? col->ords().p : col->values.p;  // keyword terms: global ordinal
         q.present = col->present.as<uint64_t>();
         if (col->type == ESGPU_COL_ORD_U32) {
             require(f.type == ESGPU_FILTER_TERM, ESGPU_ERR_UNSUPPORTED, "range filters on keyword fields run on the CPU path");
@@ -865,7 +1007,7 @@ static bool collect_partitioned(esgpu_plan* p, Pipeline& pl, const esgpu_segment
     const uint32_t target = (uint32_t)c->cus * part_wg_per_cu();
     Q.blocks_per_wg = std::max(1u, (Q.n_blocks + target - 1) / target);
     Q.G = (Q.n_blocks + Q.blocks_per_wg - 1) / Q.blocks_per_wg;
-    Q.ord = oc->values.as<uint32_t>();
+    Q.ord = oc->ords().as<uint32_t>();
     Q.T = pl.T;
     Q.shift = kPartShift;  // 16384 ordinals per partition: 64 KB of LDS counters in the counting pass
     Q.P = (uint32_t)(((uint64_t)pl.T + (1u << Q.shift) - 1) >> Q.shift);
@@ -924,14 +1066,14 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
         has_keys = true;
     }
     if (!pl.allocated) {
-        pl.T = ORD ? (uint32_t)std::max<uint64_t>(oc->value_count, 1) : 1;
+        pl.T = ORD ? (uint32_t)std::max<uint64_t>(oc->ord_count(), 1) : 1;
         pl.key0 = has_keys ? kmin : 0;
         pl.H = HIST ? (uint32_t)(has_keys ? kmax - kmin + 1 : 1) : 1;
         require(!HIST || !has_keys || kmax - kmin + 1 <= 64 * 1024 * 1024, ESGPU_ERR_UNSUPPORTED,
                 "histogram key range too large for a dense grid");
         require((uint64_t)pl.T * pl.H <= (1ull << 31), ESGPU_ERR_UNSUPPORTED, "bucket grid too large");
         pl.vcnt_mode = (pl.met > 0 && (!mc || mc->present.p)) ? 1 : 0;
-        pl.value_count = ORD ? oc->value_count : 1;
+        pl.value_count = ORD ? oc->ord_count() : 1;
         if (ORD && HIST) {
             const bool terms_outer = pl.outer == pl.term_spec;
             const bool inner_sparse = terms_outer ? (hc->present.p != nullptr) : true;  // ords may be missing
@@ -941,7 +1083,7 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
         pl.ord_col = oc;
         alloc_grid(p, pl);
     } else {
-        if (ORD) require(oc->value_count == pl.T || (oc->value_count == 0 && pl.T == 1), ESGPU_ERR_UNSUPPORTED,
+        if (ORD) require(oc->ord_count() == pl.T || (oc->ord_count() == 0 && pl.T == 1), ESGPU_ERR_UNSUPPORTED,
                          "segments with different global ordinal counts");
         if (HIST && has_keys) grow_keys(p, pl, kmin, kmax);
         if (pl.met > 0 && (!mc || mc->present.p) && !pl.vcnt_mode)
@@ -952,7 +1094,7 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
     P.n_docs = s->max_doc;
     P.n_blocks = s->n_pad / kBlockDocs;
     if (P.n_blocks == 0) return false;
-    P.ord = oc ? oc->values.as<uint32_t>() : nullptr;
+    P.ord = oc ? oc->ords().as<uint32_t>() : nullptr;
     P.T = pl.T;
     P.H = pl.H;
     P.hv = hc ? hc->values.as<int64_t>() : nullptr;
@@ -1122,12 +1264,13 @@ extern "C" int esgpu_plan_collect_segment(esgpu_plan* p, const esgpu_segment* s,
         for (Pipeline& pl : p->pipes) {
             if (pl.term_spec < 0) continue;
             const DevColumn* oc = s->col(pl.ord_field.c_str());
-            if (oc && p->term_cache.find(pl.ord_field) == p->term_cache.end() && !oc->synth_bit) {
+            const bool synth = oc && oc->synth_bit && !oc->gdict;
+            if (oc && p->term_cache.find(pl.ord_field) == p->term_cache.end() && !synth) {
                 auto& v = p->term_cache[pl.ord_field];
-                v.reserve(oc->value_count);
-                for (uint64_t o = 0; o < oc->value_count; ++o) v.push_back(oc->term(o));
+                v.reserve(oc->ord_count());
+                for (uint64_t o = 0; o < oc->ord_count(); ++o) v.push_back(oc->ord_term(o));
             }
-            if (oc && oc->synth_bit) p->term_cache[pl.ord_field + "#synth"] = {std::to_string(oc->synth_bit)};
+            if (synth) p->term_cache[pl.ord_field + "#synth"] = {std::to_string(oc->synth_bit)};
         }
         p->collected = true;
     });

@@ -89,6 +89,31 @@ def reduce(results):
     return ShardResult(out)
 
 
+class OrdinalMap:
+    """Global ordinals of one keyword field over a reader's segments (GlobalOrdinalsBuilder / Lucene OrdinalMap)."""
+
+    def __init__(self, ptr):
+        self._ptr = ptr
+
+    @property
+    def value_count(self):
+        v = ctypes.c_uint64()
+        N.check(N.lib().esgpu_ordinal_map_value_count(self._ptr, ctypes.byref(v)))
+        return v.value
+
+    def lookup(self, term):
+        """global ordinal of `term` (str or bytes), -1 if no segment holds it"""
+        b = term.encode("utf-8") if isinstance(term, str) else bytes(term)
+        v = ctypes.c_int64()
+        N.check(N.lib().esgpu_ordinal_map_lookup(self._ptr, b, len(b), ctypes.byref(v)))
+        return v.value
+
+    def close(self):
+        if self._ptr:
+            N.check(N.lib().esgpu_ordinal_map_destroy(self._ptr))
+            self._ptr = None
+
+
 class Segment:
     def __init__(self, engine, ptr, dictionaries=None):
         self.engine = engine
@@ -201,6 +226,13 @@ class Engine:
         ptr = ctypes.c_void_p()
         N.check(N.lib().esgpu_segment_synthetic(self._ptr, seed, shard, num_docs, mask, ctypes.byref(ptr)))
         return Segment(self, ptr)
+
+    def ordinal_map(self, segments, field):
+        """Build global ordinals of `field` over `segments` and remap their ordinal columns on the GPU."""
+        arr = (ctypes.c_void_p * len(segments))(*[sg.ptr for sg in segments])
+        out = ctypes.c_void_p()
+        N.check(N.lib().esgpu_ordinal_map_build(self._ptr, arr, len(segments), field.encode(), ctypes.byref(out)))
+        return OrdinalMap(out)
 
     def upload_segment(self, columns, max_doc):
         """columns: {name: dict(type=COL_*, values=np.array, offsets=None|np.uint64, present=None|np.uint64 bits,

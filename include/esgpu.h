@@ -134,6 +134,20 @@ int esgpu_synthetic_term(uint32_t field_bit, uint64_t ord, char* buf, size_t cap
 /* Copy a device column range back to host (tests compare device vs host generator). */
 int esgpu_segment_read_column(const esgpu_segment* seg, const char* field, uint64_t start, uint64_t count, void* out);
 
+/* Global ordinals over the segments of one reader = GlobalOrdinalsBuilder.build / Lucene OrdinalMap
+ * (core/.../index/fielddata/ordinals/GlobalOrdinalsBuilder.java:45-70, GlobalOrdinalMapping.java:51-58).
+ * Merges the segments' term dictionaries of `field` (each sorted by unsigned bytes, as Lucene stores them) into
+ * global ordinals and remaps every segment's ordinal column on the GPU.  From then on, terms aggregations and
+ * keyword term filters on these segments use global ordinals and resolve terms through the global dictionary
+ * (until a segment is destroyed or remapped by another map).  Segments without the field are skipped. */
+typedef struct esgpu_ordinal_map esgpu_ordinal_map;
+int esgpu_ordinal_map_build(esgpu_ctx* ctx, esgpu_segment* const* segs, int32_t nsegs, const char* field,
+                            esgpu_ordinal_map** out);
+int esgpu_ordinal_map_value_count(const esgpu_ordinal_map* map, uint64_t* count);
+/* global ordinal of a term, or -1 (TermQuery resolution for keyword term filters) */
+int esgpu_ordinal_map_lookup(const esgpu_ordinal_map* map, const uint8_t* term, size_t len, int64_t* ord);
+int esgpu_ordinal_map_destroy(esgpu_ordinal_map* map);
+
 /* ---------------------------------------------------------------------------------------------------------
  * Aggregation plan = one AggregatorFactory tree for one shard request (AggregatorFactories.java:68-90).
  * Specs are a flattened tree: spec[i].parent is the index of the enclosing bucket aggregation (-1 = top

@@ -227,3 +227,61 @@ def test_high_cardinality_partitioned_orders(engine, order):
     res = plan.build()
     assert_same(res.to_dict(), want["shards"][0], "shard")
     assert_same(reduce([res]).to_dict(), want["reduced"], "reduced")
+
+
+def test_multi_segment_global_ordinals(engine):
+    """Three segments with different term dictionaries (GlobalOrdinalsBuilder / OrdinalMap): the
+    GPU-remapped global ordinals give the same shard result as one segment over the concatenated docs with the
+    merged dictionary; a keyword term filter resolves its term through the global dictionary."""
+    rng = np.random.default_rng(11)
+    universe = sorted("kw-%05d-%s" % (i, "x" * (i % 3)) for i in range(4000))
+    sizes = [200_000, 150_001, 250_003]
+    segs_cols, dicts, concat = [], [], {"kw": [], "@timestamp": [], "response_time_ms": []}
+    t0 = 1441065600000
+    for k, n in enumerate(sizes):
+        d = sorted(rng.choice(universe, size=1500 + 400 * k, replace=False).tolist())
+        ranks = np.minimum(rng.zipf(1.3, size=n) - 1, len(d) - 1).astype(np.uint32)
+        ords = rng.permutation(len(d)).astype(np.uint32)[ranks]
+        ords[rng.random(n) < 0.03] = 0xFFFFFFFF  # missing
+        ts = np.sort(rng.integers(t0, t0 + 3 * 86_400_000, size=n)).astype(np.int64)
+        rt = rng.integers(0, 1000, size=n).astype(np.int64)
+        segs_cols.append({"kw": {"type": N.COL_ORD_U32, "values": ords, "terms": d},
+                          "@timestamp": {"type": N.COL_I64, "values": ts},
+                          "response_time_ms": {"type": N.COL_I64, "values": rt}})
+        dicts.append(d)
+        concat["kw"].append([d[o] if o != 0xFFFFFFFF else None for o in ords])
+        concat["@timestamp"].append(ts)
+        concat["response_time_ms"].append(rt)
+    gdict = sorted(set().union(*dicts))
+    gindex = {t: i for i, t in enumerate(gdict)}
+    gords = np.array([gindex[t] if t is not None else 0xFFFFFFFF for part in concat["kw"] for t in part], dtype=np.uint32)
+    total = sum(sizes)
+    one = {"kw": {"type": N.COL_ORD_U32, "values": gords, "terms": gdict},
+           "@timestamp": {"type": N.COL_I64, "values": np.concatenate(concat["@timestamp"])},
+           "response_time_ms": {"type": N.COL_I64, "values": np.concatenate(concat["response_time_ms"])}}
+    segs = [engine.upload_segment(c, n) for c, n in zip(segs_cols, sizes)]
+    omap = engine.ordinal_map(segs, "kw")
+    assert omap.value_count == len(gdict)
+    probe = dicts[1][7]
+    assert omap.lookup(probe) == gindex[probe] and omap.lookup("no-such-term") == -1
+    requests = [
+        ([AB.terms("t").field("kw").size(15).subAggregation(
+            AB.dateHistogram("h").field("@timestamp").interval("1h").subAggregation(AB.stats("rt").field("response_time_ms")))],
+         None),
+        ([AB.terms("t").field("kw").size(5).order(Order.term(False)).subAggregation(AB.avg("a").field("response_time_ms"))],
+         None),
+        ([AB.dateHistogram("h").field("@timestamp").interval("6h").subAggregation(AB.terms("t").field("kw").size(3))],
+         [QB.termQuery("kw", probe)]),
+    ]
+    for aggs, flt in requests:
+        want = O.run([(one, total)], aggs, filters=flt, ord_lookup=lambda f, t: gindex.get(t, -1))
+        plan = engine.plan(aggs, filters=flt, ord_lookup=lambda f, t: omap.lookup(t))
+        for s in segs:
+            plan.collect(s)
+        shard = plan.build()
+        assert_same(shard.to_dict(), want["shards"][0], "shard")
+        assert_same(reduce([shard]).to_dict(), want["reduced"], "reduced")
+        plan.close()
+    omap.close()
+    for s in segs:
+        s.close()
