@@ -50,6 +50,8 @@ class AggSpec(ctypes.Structure):
         ("has_extended_bounds_min", ctypes.c_int32), ("has_extended_bounds_max", ctypes.c_int32),
         ("extended_bounds_min", ctypes.c_int64), ("extended_bounds_max", ctypes.c_int64),
         ("sigma", ctypes.c_double), ("precision_threshold", ctypes.c_int64),
+        ("tz_starts", ctypes.POINTER(ctypes.c_int64)), ("tz_offsets_ms", ctypes.POINTER(ctypes.c_int64)),
+        ("tz_count", ctypes.c_int32), ("reserved_tz", ctypes.c_int32),
     ]
 
 
@@ -119,6 +121,8 @@ SIGNATURES = [
                                               ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
                                               ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     ("esgpu_precision_from_threshold", ctypes.c_int, [ctypes.c_int64, ctypes.POINTER(ctypes.c_int32)]),
+    ("esgpu_date_rounding", ctypes.c_int, [ctypes.POINTER(AggSpec), ctypes.c_int32, ctypes.c_int64,
+                                           ctypes.POINTER(ctypes.c_int64)]),
     ("esgpu_murmur3_x64_128", ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int64, ctypes.POINTER(ctypes.c_uint64)]),
     ("esgpu_plan_create", ctypes.c_int, [_VP, ctypes.POINTER(AggSpec), ctypes.c_int32, ctypes.POINTER(Filter),
                                          ctypes.c_int32, _PP]),

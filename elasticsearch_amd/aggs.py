@@ -11,6 +11,7 @@ DateHistogramParser.java:85-193, CardinalityParser.java:48-71, ExtendedStatsPars
 flattened esgpu_agg_spec array of include/esgpu.h.
 """
 import ctypes
+import functools
 import re
 
 from . import _native as N
@@ -35,14 +36,59 @@ def parse_time_value(text):
 
 
 def parse_time_zone(tz):
-    """Fixed-offset time zones ("UTC", "+01:00", "-08:00", "-2") -> offset in ms.  DST zones are not supported."""
+    """DateTimeZone.forID: fixed offsets ("UTC", "+01:00", "-08:00", "-2") -> offset in ms; a region id
+    ("Europe/Berlin", "America/Chicago", "CET") -> its offset history (tz_history)."""
     if tz is None or tz in ("UTC", "Z", "utc"):
         return 0
     m = re.fullmatch(r"([+-])?(\d{1,2})(?::?(\d{2}))?", tz)
     if not m:
-        raise ValueError(f"only fixed-offset time zones are supported, got [{tz}]")
+        return tz_history(tz)
     sign = -1 if m.group(1) == "-" else 1
     return sign * (int(m.group(2)) * 3600000 + int(m.group(3) or 0) * 60000)
+
+
+@functools.lru_cache(maxsize=64)
+def tz_history(name, first_year=1900, last_year=2100):
+    """Offset history of an IANA zone as the C-ABI takes it (esgpu_agg_spec.tz_starts / tz_offsets_ms): offset
+    offs[i] applies from UTC instant starts[i] on (starts[0] = -infinity).  What a JNI caller reads from joda's
+    DateTimeZone (getOffset / nextTransition), read here from the IANA database behind Python's zoneinfo: the offset
+    is sampled every 6 hours over [first_year, last_year) and each change is bisected to the second."""
+    import datetime as _dt
+    import zoneinfo
+    try:
+        z = zoneinfo.ZoneInfo(name)
+    except (zoneinfo.ZoneInfoNotFoundError, ValueError) as e:
+        raise ValueError(f"The datetime zone id '{name}' is not recognised") from e
+    epoch = _dt.datetime(1970, 1, 1, tzinfo=_dt.timezone.utc)
+
+    def off(sec):
+        return int((epoch + _dt.timedelta(seconds=sec)).astimezone(z).utcoffset().total_seconds() * 1000)
+
+    lo = int((_dt.datetime(first_year, 1, 1, tzinfo=_dt.timezone.utc) - epoch).total_seconds())
+    hi = int((_dt.datetime(last_year, 1, 1, tzinfo=_dt.timezone.utc) - epoch).total_seconds())
+    step = 6 * 3600
+    starts, offs = [-(1 << 63)], [off(lo)]
+    prev = offs[0]
+    t = lo
+    while t < hi:
+        nxt = t + step
+        o = off(nxt)
+        if o != prev:
+            a, b = t, nxt  # off(a) == prev != off(b): the transition instant is in (a, b]
+            while b - a > 1:
+                mid = (a + b) // 2
+                if off(mid) == prev:
+                    a = mid
+                else:
+                    b = mid
+            starts.append(b * 1000)
+            offs.append(off(b))
+            prev = offs[-1]
+            if o != prev:  # two changes inside one step: rescan from the transition
+                t = b
+                continue
+        t = nxt
+    return tuple(starts), tuple(offs)
 
 
 class Order:
@@ -276,31 +322,34 @@ class QueryBuilders:
 
 # ---- flattening -------------------------------------------------------------------------------------------------
 def _rounding_params(b):
-    """-> (date_unit, interval, offset) with a fixed time-zone offset folded into OffsetRounding."""
+    """-> (date_unit, interval, offset, zone) with a fixed time-zone offset folded into OffsetRounding; zone is None
+    or the (starts, offsets) history of a region zone (DateHistogramParser.java:178-187)."""
     if b.type == N.AGG_HISTOGRAM:
         if b._interval is None or int(b._interval) < 1:
             raise ValueError("[interval] must be 1 or greater for histogram aggregation [%s]" % b.name)
-        return N.UNIT_NONE, int(b._interval), int(b._offset)
+        return N.UNIT_NONE, int(b._interval), int(b._offset), None
     if b._interval is None:
         raise ValueError("Missing required field [interval] for histogram aggregation [%s]" % b.name)
     off = b._offset if isinstance(b._offset, int) else parse_time_value(b._offset)
-    off -= parse_time_zone(b._tz)
+    tz = parse_time_zone(b._tz)
+    zone = None
+    if isinstance(tz, tuple):
+        zone = tz
+    else:
+        off -= tz
     unit = DATE_FIELD_UNITS.get(str(b._interval))
     if unit is not None:
-        return unit, 0, off
-    return N.UNIT_NONE, parse_time_value(b._interval), off
+        return unit, 0, off, zone
+    return N.UNIT_NONE, parse_time_value(b._interval), off, zone
 
 
-def _round_bound(unit, interval, offset, v):
-    """ExtendedBounds.round: the bound is rounded with the aggregation's rounding (affine roundings)."""
+def _round_bound(spec, v):
+    """ExtendedBounds.round: the bound is rounded with the aggregation's own Rounding (esgpu_date_rounding)."""
     if v is None:
         return None
-    if unit in (N.UNIT_NONE, N.UNIT_SECOND, N.UNIT_MINUTE, N.UNIT_HOUR, N.UNIT_DAY, N.UNIT_WEEK):
-        step = {N.UNIT_SECOND: 1000, N.UNIT_MINUTE: 60000, N.UNIT_HOUR: 3600000, N.UNIT_DAY: 86400000,
-                N.UNIT_WEEK: 7 * 86400000}.get(unit, interval)
-        off = offset - 3 * 86400000 if unit == N.UNIT_WEEK else offset
-        return ((v - off) // step) * step + off
-    raise ValueError("extended_bounds on calendar units are not supported")
+    out = ctypes.c_int64()
+    N.check(N.lib().esgpu_date_rounding(ctypes.byref(spec), 0, int(v), ctypes.byref(out)))
+    return out.value
 
 
 def thresholds(size, shard_size, min_doc_count, shard_min_doc_count, order, number_of_shards):
@@ -334,18 +383,25 @@ def flatten(aggs, number_of_shards=1):
             sp.order = b._order
             sp.show_term_doc_count_error = int(b._show_err)
         elif b.type in (N.AGG_HISTOGRAM, N.AGG_DATE_HISTOGRAM):
-            unit, interval, off = _rounding_params(b)
+            unit, interval, off, zone = _rounding_params(b)
             sp.date_unit, sp.interval, sp.offset = unit, interval, off
+            if zone is not None:
+                starts = (ctypes.c_int64 * len(zone[0]))(*zone[0])
+                offs = (ctypes.c_int64 * len(zone[1]))(*zone[1])
+                keep.extend([starts, offs])
+                sp.tz_starts = ctypes.cast(starts, ctypes.POINTER(ctypes.c_int64))
+                sp.tz_offsets_ms = ctypes.cast(offs, ctypes.POINTER(ctypes.c_int64))
+                sp.tz_count = len(zone[0])
             sp.min_doc_count = b._min
             sp.order = b._order
             sp.keyed = int(b._keyed)
             lo, hi = b._bounds
             if lo is not None:
                 sp.has_extended_bounds_min = 1
-                sp.extended_bounds_min = _round_bound(unit, interval, off, lo)
+                sp.extended_bounds_min = _round_bound(sp, lo)
             if hi is not None:
                 sp.has_extended_bounds_max = 1
-                sp.extended_bounds_max = _round_bound(unit, interval, off, hi)
+                sp.extended_bounds_max = _round_bound(sp, hi)
         elif b.type == N.AGG_EXTENDED_STATS:
             sp.sigma = b._sigma
         elif b.type == N.AGG_CARDINALITY:

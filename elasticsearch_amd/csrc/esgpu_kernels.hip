@@ -258,6 +258,19 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
     return v;
 }
 
+// grid key index of a value: affine roundings divide, table roundings (calendar units, DST zones) search the bucket
+// start instants; values outside the grid give an index outside [0, H)
+__device__ __forceinline__ int64_t key_index(const CollectParams& P, int64_t v) {
+    if (!P.kstart) return floor_div64(v - P.offset, P.interval) - P.key0;
+    if (v < P.kstart[0]) return -1;
+    uint32_t lo = 0, hi = P.H;  // kstart[lo] <= v < kstart[hi] (kstart[H] = +inf)
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (P.kstart[mid] <= v) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
 // key slot of a value relative to `base` (= value of the first slot); 32-bit magic division fast path
 __device__ __forceinline__ uint32_t slot_of(const CollectParams& P, int64_t v, int64_t base) {
     if (P.fast32) return magic_div((uint32_t)((uint64_t)v - (uint64_t)base), P.mg_m, P.mg_s1, P.mg_s2, (uint32_t)P.interval);
@@ -304,7 +317,7 @@ __device__ __forceinline__ void run_flush(const CollectParams& P, const Acc& a, 
 
 template <bool ORD, bool HIST, int MET, bool LDS>
 __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, const Doc4& d, uint32_t T, int64_t base,
-                                         uint32_t W, Run& run) {
+                                         uint32_t win0, Run& run) {
     uint32_t slot[kVec];
     bool hv_ok[kVec];
 #pragma unroll
@@ -314,9 +327,9 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
         if (HIST) {
             hv_ok[j] = (d.hpres >> j) & 1;
             if (LDS) {
-                slot[j] = slot_of(P, d.hv[j], base);
+                slot[j] = P.kstart ? (uint32_t)(key_index(P, d.hv[j]) - (int64_t)win0) : slot_of(P, d.hv[j], base);
             } else {
-                const int64_t k = floor_div64(d.hv[j] - P.offset, P.interval) - P.key0;
+                const int64_t k = key_index(P, d.hv[j]);
                 hv_ok[j] = hv_ok[j] && k >= 0 && k < (int64_t)P.H;
                 slot[j] = (uint32_t)k;
             }
@@ -484,8 +497,8 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
             if (use_lds && HIST && P.windowed) {
                 const int64_t zmn = P.zmin[b], zmx = P.zmax[b];
                 if (zmn <= zmx) {  // block has at least one timestamp
-                    const int64_t kmn = floor_div64(zmn - P.offset, P.interval) - P.key0;
-                    const int64_t kmx = floor_div64(zmx - P.offset, P.interval) - P.key0;
+                    const int64_t kmn = key_index(P, zmn);
+                    const int64_t kmx = key_index(P, zmx);
                     if (kmx - kmn + 1 > (int64_t)W) {
                         use_lds = false;  // block spans more keys than the window: global atomics for this block
                     } else if (!win_set || kmn < (int64_t)win0 || kmx >= (int64_t)win0 + (int64_t)W) {
@@ -504,10 +517,10 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
         Doc4 nxt;
         if (i + kPrefetch < n_it) load_docs<ORD, HIST, MET>(P, doc_of(i + kPrefetch), nxt);
         if (use_lds) {
-            process4<ORD, HIST, MET, true>(P, s, q[0], T, base, W, run);
+            process4<ORD, HIST, MET, true>(P, s, q[0], T, base, win0, run);
             dirty = true;
         } else {
-            process4<ORD, HIST, MET, false>(P, g, q[0], T, base, W, run);
+            process4<ORD, HIST, MET, false>(P, g, q[0], T, base, win0, run);
         }
 #pragma unroll
         for (int k = 0; k + 1 < kPrefetch; ++k) q[k] = q[k + 1];

@@ -54,6 +54,7 @@ struct CollectParams {
     const int64_t* hv;
     const uint64_t* hv_present;
     int64_t interval, offset, key0;  // key index k of a value v: floor((v - offset) / interval) - key0
+    const int64_t* kstart;           // non-affine roundings: bucket start instants [H] (key index = last start <= v)
     const int64_t* zmin;
     const int64_t* zmax;
     uint32_t mg_m, mg_s1, mg_s2;

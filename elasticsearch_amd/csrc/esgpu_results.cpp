@@ -46,56 +46,17 @@ static inline int64_t jround(double a) {
 }
 static inline int64_t fdiv(int64_t a, int64_t b) { return a < 0 ? (a - b + 1) / b : a / b; }
 
-// ------------------------------------------------------------------------------------------------------------
-// calendar (joda ISOChronology UTC) for EmptyBucketInfo.rounding.nextRoundingValue
-// ------------------------------------------------------------------------------------------------------------
-static int64_t days_from_civil(int64_t y, int m, int d) {
-    y -= m <= 2;
-    const int64_t era = (y >= 0 ? y : y - 399) / 400;
-    const int64_t yoe = y - era * 400;
-    const int64_t doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
-    const int64_t doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
-    return era * 146097 + doe - 719468;
-}
-static void civil_from_days(int64_t z, int64_t* y, int* m, int* d) {
-    z += 719468;
-    const int64_t era = (z >= 0 ? z : z - 146096) / 146097;
-    const int64_t doe = z - era * 146097;
-    const int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
-    const int64_t doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
-    const int64_t mp = (5 * doy + 2) / 153;
-    *d = (int)(doy - (153 * mp + 2) / 5 + 1);
-    *m = (int)(mp < 10 ? mp + 3 : mp - 9);
-    *y = yoe + era * 400 + (*m <= 2);
-}
-static const int64_t kDay = 86400000LL;
-
-int64_t rounding_next(int32_t type, int32_t unit, int64_t interval, int64_t offset, int64_t v) {
-    if (type == ESGPU_AGG_HISTOGRAM || unit == ESGPU_UNIT_NONE) return v + interval;  // Interval / TimeIntervalRounding
-    const int64_t t = v - offset;  // OffsetRounding.nextRoundingValue
-    int64_t r;
-    switch (unit) {
-        case ESGPU_UNIT_SECOND: r = t + 1000; break;
-        case ESGPU_UNIT_MINUTE: r = t + 60000; break;
-        case ESGPU_UNIT_HOUR: r = t + 3600000; break;
-        case ESGPU_UNIT_DAY: r = t + kDay; break;
-        case ESGPU_UNIT_WEEK: r = t + 7 * kDay; break;
-        default: {
-            const int64_t days = fdiv(t, kDay);
-            const int64_t rem = t - days * kDay;
-            int64_t y; int m, d;
-            civil_from_days(days, &y, &m, &d);
-            const int add = unit == ESGPU_UNIT_MONTH ? 1 : unit == ESGPU_UNIT_QUARTER ? 3 : 12;
-            const int64_t mm = (int64_t)(m - 1) + add;
-            y += mm / 12;
-            m = (int)(mm % 12) + 1;
-            static const int md[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
-            const int dim = md[m - 1] + ((m == 2 && ((y % 4 == 0 && y % 100 != 0) || y % 400 == 0)) ? 1 : 0);
-            if (d > dim) d = dim;
-            r = days_from_civil(y, m, d) * kDay + rem;
-        }
-    }
-    return r + offset;
+// EmptyBucketInfo.rounding (InternalHistogram.java:395-449): the spec's Rounding, time zone included
+Rounding Block::rounding() const {
+    esgpu_agg_spec sp{};
+    sp.type = type;
+    sp.date_unit = date_unit;
+    sp.interval = interval;
+    sp.offset = offset;
+    sp.tz_count = (int32_t)tz_starts.size();
+    sp.tz_starts = tz_starts.data();
+    sp.tz_offsets_ms = tz_offs.data();
+    return Rounding::from_spec(sp);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -213,6 +174,7 @@ Block Block::like() const {
     b.required_size = required_size; b.shard_size = shard_size; b.min_doc_count = min_doc_count;
     b.show_err = show_err; b.keyed = keyed;
     b.has_empty_info = has_empty_info; b.date_unit = date_unit; b.interval = interval; b.offset = offset;
+    b.tz_starts = tz_starts; b.tz_offs = tz_offs;
     b.has_bmin = has_bmin; b.has_bmax = has_bmax; b.bmin = bmin; b.bmax = bmax;
     b.sigma = sigma; b.precision = precision;
     b.n = 0;
@@ -460,7 +422,8 @@ void reduce_histogram(const Ref* refs, size_t nrefs, Block& out, Scratch& sc, st
         }
     }
     if (out.min_doc_count == 0 && out.has_empty_info) {  // addEmptyBuckets (InternalHistogram.java:395-449)
-        auto next = [&](int64_t k) { return rounding_next(out.type, out.date_unit, out.interval, out.offset, k); };
+        const Rounding rnd = out.rounding();
+        auto next = [&](int64_t k) { return rnd.next_rounding_value(k); };
         auto empty = [](int64_t k) { return OutBucket{k, nullptr, 0, 0, 0, 0, 0, true}; };
         std::vector<OutBucket>& filled = sc.filled;
         filled.clear();
@@ -635,10 +598,10 @@ struct J {
     void opt(bool c, double v) { if (c) dbl(v); else raw("null"); }
 };
 std::string iso8601(int64_t ms) {
-    const int64_t days = fdiv(ms, kDay);
-    const int64_t rem = ms - days * kDay;
+    const int64_t days = fdiv(ms, kMsDay);
+    const int64_t rem = ms - days * kMsDay;
     int64_t y; int m, d;
-    civil_from_days(days, &y, &m, &d);
+    r_civil_from_days(days, &y, &m, &d);
     char b[64];
     snprintf(b, sizeof b, "%04lld-%02d-%02dT%02d:%02d:%02d.%03dZ", (long long)y, m, d, (int)(rem / 3600000),
              (int)(rem / 60000 % 60), (int)(rem / 1000 % 60), (int)(rem % 1000));
@@ -808,6 +771,7 @@ void w_block(W& w, const Block& a) {
     w.pod(a.type); w.pod(a.order); w.str(a.name);
     w.pod(a.required_size); w.pod(a.shard_size); w.pod(a.min_doc_count); w.pod(a.show_err); w.pod(a.keyed);
     w.pod<uint8_t>(a.has_empty_info); w.pod(a.date_unit); w.pod(a.interval); w.pod(a.offset);
+    w.vec(a.tz_starts); w.vec(a.tz_offs);
     w.pod<uint8_t>(a.has_bmin); w.pod<uint8_t>(a.has_bmax); w.pod(a.bmin); w.pod(a.bmax);
     w.pod(a.sigma); w.pod(a.precision); w.pod(a.n);
     w.vec(a.doc_count_error); w.vec(a.other_doc_count); w.vec(a.boff); w.vec(a.key); w.vec(a.term_off);
@@ -833,6 +797,8 @@ void r_block(R& r, Block& a, int depth) {
     a.show_err = r.pod<int32_t>(); a.keyed = r.pod<int32_t>();
     a.has_empty_info = r.pod<uint8_t>(); a.date_unit = r.pod<int32_t>(); a.interval = r.pod<int64_t>();
     a.offset = r.pod<int64_t>();
+    r.vec(a.tz_starts); r.vec(a.tz_offs);
+    if (a.tz_starts.size() != a.tz_offs.size()) throw std::runtime_error("bad time zone table");
     a.has_bmin = r.pod<uint8_t>(); a.has_bmax = r.pod<uint8_t>(); a.bmin = r.pod<int64_t>(); a.bmax = r.pod<int64_t>();
     a.sigma = r.pod<double>(); a.precision = r.pod<int32_t>(); a.n = r.pod<uint64_t>();
     r.vec(a.doc_count_error); r.vec(a.other_doc_count); r.vec(a.boff); r.vec(a.key); r.vec(a.term_off);
@@ -878,7 +844,7 @@ void r_blocks(R& r, std::vector<Block>& l, int depth) {
     for (Block& a : l) r_block(r, a, depth);
 }
 const uint32_t kStreamMagic = 0x45534750;  // "ESGP"
-const uint32_t kStreamVersion = 2;
+const uint32_t kStreamVersion = 3;
 }  // namespace
 
 void serialize(const std::vector<Block>& aggs, std::string& out) {

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../include/esgpu.h"
+#include "es_rounding.hpp"
 
 namespace esgpu {
 
@@ -32,6 +33,7 @@ struct Block {
     int32_t date_unit = 0;
     int64_t interval = 1;
     int64_t offset = 0;
+    std::vector<int64_t> tz_starts, tz_offs;  // date_histogram time zone (empty = UTC / folded fixed offset)
     bool has_bmin = false, has_bmax = false;
     int64_t bmin = 0, bmax = 0;
     double sigma = 2.0;
@@ -61,6 +63,7 @@ struct Block {
     std::vector<std::vector<uint8_t>> regs;
     std::vector<std::vector<uint32_t>> lc;  // ascending encoded hashes
 
+    Rounding rounding() const;  // histogram specs: the request's Rounding (EmptyBucketInfo)
     bool is_bucket() const { return type == ESGPU_AGG_TERMS || type == ESGPU_AGG_HISTOGRAM || type == ESGPU_AGG_DATE_HISTOGRAM; }
     uint64_t nbuckets() const { return boff.empty() ? 0 : boff.back(); }
     std::string term(uint64_t b) const { return term_pool.substr(term_off[b], term_off[b + 1] - term_off[b]); }
@@ -73,8 +76,6 @@ struct Block {
     void append_empty();
 };
 
-// rounding helper for EmptyBucketInfo (common/rounding/*)
-int64_t rounding_next(int32_t type, int32_t date_unit, int64_t interval, int64_t offset, int64_t value);
 
 // HyperLogLogPlusPlus
 int hll_precision_from_threshold(int64_t count);

@@ -29,6 +29,7 @@
 
 #include "../../include/esgpu.h"
 #include "es_common.hpp"
+#include "es_rounding.hpp"
 #include "esgpu_kernels.hpp"
 #include "esgpu_results.hpp"
 
@@ -649,6 +650,21 @@ extern "C" int esgpu_murmur3_x64_128(const uint8_t* bytes, size_t len, int64_t s
     });
 }
 
+extern "C" int esgpu_date_rounding(const esgpu_agg_spec* spec, int32_t op, int64_t value, int64_t* out) {
+    return guarded([&] {
+        require(spec && out && op >= 0 && op <= 2, ESGPU_ERR_INVALID, "bad rounding arguments");
+        require(spec->type == ESGPU_AGG_HISTOGRAM || spec->type == ESGPU_AGG_DATE_HISTOGRAM, ESGPU_ERR_INVALID,
+                "not a histogram spec");
+        Rounding r;
+        try {
+            r = Rounding::from_spec(*spec);
+        } catch (const std::invalid_argument& e) {
+            throw EsError(ESGPU_ERR_INVALID, e.what());
+        }
+        *out = op == 0 ? r.round(value) : op == 1 ? r.next_rounding_value(value) : r.round_key(value);
+    });
+}
+
 extern "C" int esgpu_precision_from_threshold(int64_t count, int32_t* precision) {
     return guarded([&] { *precision = hll_precision_from_threshold(count); });
 }
@@ -664,6 +680,14 @@ struct SpecNode {
     std::string name, field;
     std::vector<int> children;
     int precision = 14;
+    std::vector<int64_t> tz_starts, tz_offs;  // owned copy of the spec's time zone table
+    Rounding rounding() const {               // histogram specs (Rounding.java / TimeZoneRounding.java)
+        esgpu_agg_spec sp = s;
+        sp.tz_count = (int32_t)tz_starts.size();
+        sp.tz_starts = tz_starts.data();
+        sp.tz_offsets_ms = tz_offs.data();
+        return Rounding::from_spec(sp);
+    }
 };
 
 // One top-level aggregation subtree compiled to one kernel pipeline.
@@ -676,7 +700,12 @@ struct Pipeline {
     std::vector<int> metrics;        // metric specs at the deepest level
     std::string ord_field, hist_field, metric_field;
     int met = 0;                     // 0 none, 1 avg, 2 stats, 3 extended
-    int64_t interval = 1, offset = 0;
+    int64_t interval = 1, offset = 0;  // affine roundings: key = floor((v - offset) / interval) * interval + offset
+    Rounding rnd;                    // the histogram spec's rounding
+    bool ktable = false;             // non-affine rounding: bucket start table instead of the affine map
+    int64_t kt_lo = 0, kt_hi = -1;   // value range the table covers
+    std::vector<int64_t> kt_start, kt_key;  // [H] bucket start instants and keys
+    DevBuf d_kstart;                 // device copy of kt_start
     // device state
     bool allocated = false;
     uint32_t T = 1, H = 1;
@@ -755,23 +784,8 @@ struct esgpu_plan {
 
 static int metric_level(int t) { return t == ESGPU_AGG_AVG ? 1 : t == ESGPU_AGG_STATS ? 2 : 3; }
 
-static void affine_rounding(const esgpu_agg_spec& s, int64_t* interval, int64_t* offset) {
-    // HistogramAggregator keys as an affine map: key = floor((v - offset) / interval) * interval + offset
-    if (s.type == ESGPU_AGG_HISTOGRAM || s.date_unit == ESGPU_UNIT_NONE) {
-        require(s.interval >= 1, ESGPU_ERR_INVALID, "[interval] must be 1 or greater for histogram aggregation");
-        *interval = s.interval;
-        *offset = s.offset;
-        return;
-    }
-    switch (s.date_unit) {
-        case ESGPU_UNIT_SECOND: *interval = 1000; break;
-        case ESGPU_UNIT_MINUTE: *interval = 60000; break;
-        case ESGPU_UNIT_HOUR: *interval = 3600000; break;
-        case ESGPU_UNIT_DAY: *interval = 86400000; break;
-        case ESGPU_UNIT_WEEK: *interval = 7 * 86400000LL; *offset = s.offset - 3 * 86400000LL; return;  // Monday 00:00
-        default: throw EsError(ESGPU_ERR_UNSUPPORTED, "calendar date_histogram units (month/quarter/year) run on the CPU path");
-    }
-    *offset = s.offset;
+static int64_t key_value(const Pipeline& pl, uint32_t slot) {
+    return pl.ktable ? pl.kt_key[slot] : (pl.key0 + (int64_t)slot) * pl.interval + pl.offset;
 }
 
 extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int32_t nspecs, const esgpu_filter* filters,
@@ -790,6 +804,14 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
             n.field = specs[i].field ? specs[i].field : "";
             n.s.name = nullptr;
             n.s.field = nullptr;
+            if (is_bucket(n.s.type) && n.s.type != ESGPU_AGG_TERMS && specs[i].tz_count > 0) {
+                require(specs[i].tz_starts && specs[i].tz_offsets_ms, ESGPU_ERR_INVALID, "time zone table without arrays");
+                n.tz_starts.assign(specs[i].tz_starts, specs[i].tz_starts + specs[i].tz_count);
+                n.tz_offs.assign(specs[i].tz_offsets_ms, specs[i].tz_offsets_ms + specs[i].tz_count);
+            }
+            n.s.tz_starts = nullptr;
+            n.s.tz_offsets_ms = nullptr;
+            n.s.tz_count = 0;
             require(n.s.type >= ESGPU_AGG_TERMS && n.s.type <= ESGPU_AGG_VALUE_COUNT, ESGPU_ERR_INVALID, "unknown aggregation type");
             if (n.s.parent < 0) tops.push_back(i);
             else {
@@ -860,7 +882,16 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
                 if (b < 0) continue;
                 const SpecNode& n = p->specs[b];
                 if (n.s.type == ESGPU_AGG_TERMS) { pl.term_spec = b; pl.ord_field = n.field; }
-                else { pl.hist_spec = b; pl.hist_field = n.field; affine_rounding(n.s, &pl.interval, &pl.offset); }
+                else {
+                    pl.hist_spec = b;
+                    pl.hist_field = n.field;
+                    try {
+                        pl.rnd = n.rounding();
+                    } catch (const std::invalid_argument& e) {
+                        throw EsError(ESGPU_ERR_INVALID, std::string(e.what()) + " for histogram aggregation [" + n.name + "]");
+                    }
+                    pl.ktable = !pl.rnd.affine(&pl.interval, &pl.offset);
+                }
             }
             for (int m : pl.metrics) {
                 const SpecNode& n = p->specs[m];
@@ -908,14 +939,10 @@ static void alloc_grid(esgpu_plan* p, Pipeline& pl) {
     pl.allocated = true;
 }
 
-// grow the key range of an allocated grid ([H][T] rows are contiguous, so a range extension is one copy)
-static void grow_keys(esgpu_plan* p, Pipeline& pl, int64_t kmin, int64_t kmax) {
-    const int64_t nk0 = std::min(pl.key0, kmin);
-    const int64_t nk1 = std::max(pl.key0 + (int64_t)pl.H - 1, kmax);
-    if (nk0 == pl.key0 && nk1 == pl.key0 + (int64_t)pl.H - 1) return;
-    require(nk1 - nk0 + 1 <= 64 * 1024 * 1024, ESGPU_ERR_UNSUPPORTED, "histogram key range too large for a dense grid");
+// re-shape an allocated grid to newH key rows, the old rows landing at row `shift` ([H][T] rows are contiguous, so a
+// key-range extension is one copy per array)
+static void regrid(esgpu_plan* p, Pipeline& pl, uint32_t newH, int64_t shift) {
     const uint32_t oldH = pl.H;
-    const int64_t shift = pl.key0 - nk0;
     struct { DevBuf g_cnt, g_ocnt, g_vcnt, g_sum, g_min, g_max, g_sq; } old;
     old.g_cnt = std::move(pl.g_cnt);
     old.g_ocnt = std::move(pl.g_ocnt);
@@ -924,8 +951,7 @@ static void grow_keys(esgpu_plan* p, Pipeline& pl, int64_t kmin, int64_t kmax) {
     old.g_min = std::move(pl.g_min);
     old.g_max = std::move(pl.g_max);
     old.g_sq = std::move(pl.g_sq);
-    pl.H = (uint32_t)(nk1 - nk0 + 1);
-    pl.key0 = nk0;
+    pl.H = newH;
     alloc_grid(p, pl);
     const size_t row = (size_t)pl.T * 8;
     auto cp = [&](DevBuf& dst, DevBuf& src, size_t rowb) {
@@ -941,6 +967,45 @@ static void grow_keys(esgpu_plan* p, Pipeline& pl, int64_t kmin, int64_t kmax) {
     if ((pl.ocnt_mode == OCNT_TERMS || pl.ocnt_mode == OCNT_TERMS_DERIVED) && old.g_ocnt.p)
         HIPX(hipMemcpyAsync(pl.g_ocnt.p, old.g_ocnt.p, (size_t)pl.T * 8, hipMemcpyDeviceToDevice, p->stream));
     HIPX(hipStreamSynchronize(p->stream));
+}
+
+// grow the key range of an allocated affine grid to cover key indices [kmin, kmax]
+static void grow_keys(esgpu_plan* p, Pipeline& pl, int64_t kmin, int64_t kmax) {
+    const int64_t nk0 = std::min(pl.key0, kmin);
+    const int64_t nk1 = std::max(pl.key0 + (int64_t)pl.H - 1, kmax);
+    if (nk0 == pl.key0 && nk1 == pl.key0 + (int64_t)pl.H - 1) return;
+    require(nk1 - nk0 + 1 <= 64 * 1024 * 1024, ESGPU_ERR_UNSUPPORTED, "histogram key range too large for a dense grid");
+    const int64_t shift = pl.key0 - nk0;
+    pl.key0 = nk0;
+    regrid(p, pl, (uint32_t)(nk1 - nk0 + 1), shift);
+}
+
+// (re)build the bucket table of a non-affine rounding so that it covers [lo, hi]; returns the row shift of the
+// previous table's buckets (0 on first build)
+static constexpr size_t kMaxTableBuckets = 16u << 20;
+static int64_t build_key_table(esgpu_plan* p, Pipeline& pl, int64_t lo, int64_t hi) {
+    if (pl.kt_lo <= pl.kt_hi) {
+        if (lo >= pl.kt_lo && hi <= pl.kt_hi) return 0;
+        lo = std::min(lo, pl.kt_lo);
+        hi = std::max(hi, pl.kt_hi);
+    }
+    std::vector<int64_t> starts, keys;
+    require(pl.rnd.key_table(lo, hi, kMaxTableBuckets, starts, keys), ESGPU_ERR_UNSUPPORTED,
+            "date_histogram rounding produces too many or non-monotone buckets for a dense grid");
+    int64_t shift = 0;
+    if (!pl.kt_key.empty()) {
+        auto it = std::lower_bound(keys.begin(), keys.end(), pl.kt_key.front());
+        require(it != keys.end() && *it == pl.kt_key.front(), ESGPU_ERR_DEVICE, "bucket table is not a superset");
+        shift = it - keys.begin();
+    }
+    pl.kt_lo = lo;
+    pl.kt_hi = hi;
+    pl.kt_start = std::move(starts);
+    pl.kt_key = std::move(keys);
+    pl.d_kstart.alloc(p->ctx, std::max<size_t>(pl.kt_start.size(), 1) * 8);
+    if (!pl.kt_start.empty())
+        HIPX(hipMemcpyAsync(pl.d_kstart.p, pl.kt_start.data(), pl.kt_start.size() * 8, hipMemcpyHostToDevice, p->stream));
+    return shift;
 }
 
 static void set_preds(esgpu_plan* p, const esgpu_segment* s, PredDev* out, int32_t* npred, uint64_t* bytes_per_doc) {
@@ -1060,9 +1125,17 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
     // ---- shape the grid ----
     int64_t kmin = 0, kmax = 0;
     bool has_keys = false;
+    int64_t table_shift = 0;
+    const uint32_t H_before = pl.H;
     if (HIST && hc->vmin <= hc->vmax) {
-        kmin = floor_div64(hc->vmin - pl.offset, pl.interval);
-        kmax = floor_div64(hc->vmax - pl.offset, pl.interval);
+        if (pl.ktable) {
+            table_shift = build_key_table(p, pl, hc->vmin, hc->vmax);
+            kmin = 0;
+            kmax = (int64_t)pl.kt_key.size() - 1;
+        } else {
+            kmin = floor_div64(hc->vmin - pl.offset, pl.interval);
+            kmax = floor_div64(hc->vmax - pl.offset, pl.interval);
+        }
         has_keys = true;
     }
     if (!pl.allocated) {
@@ -1085,7 +1158,10 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
     } else {
         if (ORD) require(oc->ord_count() == pl.T || (oc->ord_count() == 0 && pl.T == 1), ESGPU_ERR_UNSUPPORTED,
                          "segments with different global ordinal counts");
-        if (HIST && has_keys) grow_keys(p, pl, kmin, kmax);
+        if (HIST && has_keys) {
+            if (!pl.ktable) grow_keys(p, pl, kmin, kmax);
+            else if ((uint32_t)pl.kt_key.size() != H_before || table_shift != 0) regrid(p, pl, (uint32_t)pl.kt_key.size(), table_shift);
+        }
         if (pl.met > 0 && (!mc || mc->present.p) && !pl.vcnt_mode)
             throw EsError(ESGPU_ERR_UNSUPPORTED, "metric field sparsity changed across segments");
     }
@@ -1102,6 +1178,7 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
     P.interval = pl.interval;
     P.offset = pl.offset;
     P.key0 = pl.key0;
+    P.kstart = (HIST && pl.ktable) ? pl.d_kstart.as<int64_t>() : nullptr;
     P.zmin = hc ? hc->zmin.as<int64_t>() : nullptr;
     P.zmax = hc ? hc->zmax.as<int64_t>() : nullptr;
     P.mv = mc ? mc->values.p : nullptr;
@@ -1149,7 +1226,7 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
         return collect_partitioned(p, pl, s, oc, d_accept, P.pred, P.npred);
     }
     const uint64_t span = (uint64_t)pl.interval * (uint64_t)W;
-    P.fast32 = pl.interval < (1ll << 32) && span < (1ull << 32);
+    P.fast32 = !P.kstart && pl.interval < (1ll << 32) && span < (1ull << 32);
     if (P.fast32) {
         const MagicU32 mg = make_magic((uint32_t)pl.interval);
         P.mg_m = mg.m; P.mg_s1 = mg.s1; P.mg_s2 = mg.s2;
@@ -1368,6 +1445,8 @@ static Block hist_shell(const esgpu_plan* p, int spec, const std::vector<Block>&
     r.date_unit = n.s.type == ESGPU_AGG_DATE_HISTOGRAM ? n.s.date_unit : 0;
     r.interval = n.s.interval;
     r.offset = n.s.offset;
+    r.tz_starts = n.tz_starts;
+    r.tz_offs = n.tz_offs;
     r.boff.assign(1, 0);
     r.term_off.assign(1, 0);
     for (const Block& b : protos) r.subs.push_back(b.like());
@@ -1640,7 +1719,7 @@ static Block build_grid(esgpu_plan* p, Pipeline& pl) {
                 for (uint32_t s = 0; s < H; ++s) {
                     const size_t c = (size_t)i * H + s;
                     if (h.cnt[c] == 0) continue;
-                    push_bucket(hr, (pl.key0 + (int64_t)s) * pl.interval + pl.offset, nullptr, (int64_t)h.cnt[c]);
+                    push_bucket(hr, key_value(pl, s), nullptr, (int64_t)h.cnt[c]);
                     append_metrics(p, pl, h, c, hr.subs);
                 }
                 end_instance(hr);
@@ -1667,7 +1746,7 @@ static Block build_grid(esgpu_plan* p, Pipeline& pl) {
         else if (pl.ocnt_mode == OCNT_HIST) dc = ocnt[s];
         else for (uint32_t t = 0; t < T; ++t) dc += h.cnt[(size_t)s * T + t];
         if (dc == 0) continue;
-        push_bucket(r, (pl.key0 + (int64_t)s) * pl.interval + pl.offset, nullptr, (int64_t)dc);
+        push_bucket(r, key_value(pl, s), nullptr, (int64_t)dc);
         if (!ORD) {
             append_metrics(p, pl, h, s, r.subs);
             continue;

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define ESGPU_ABI_VERSION 1
+#define ESGPU_ABI_VERSION 2
 
 /* ---------------------------------------------------------------------------------------------------------
  * Status codes.  Mapping used by the JNI shim (SURVEY §8(b) "Errors"):
@@ -224,6 +224,16 @@ typedef struct esgpu_agg_spec {
     double sigma;
     /* cardinality (CardinalityParser.java:60-61) */
     int64_t precision_threshold;
+    /* date_histogram time zone (ValuesSourceParser timezone -> TimeZoneRounding.Builder.timeZone,
+     * DateHistogramParser.java:185-187).  tz_count == 0: UTC, or a fixed offset already folded into `offset`.
+     * Otherwise the zone's offset history as joda's DateTimeZone reports it: offset tz_offsets_ms[i] applies from the
+     * UTC instant tz_starts[i] on (tz_starts[0] is taken as -infinity), ascending, covering the field's value range.
+     * Calendar units (month / quarter / year) and zones with transitions are bucketed through a per-segment table of
+     * bucket start instants (es_rounding.hpp); everything else is affine on the GPU. */
+    const int64_t* tz_starts;
+    const int64_t* tz_offsets_ms;
+    int32_t tz_count;
+    int32_t reserved_tz;
 } esgpu_agg_spec;
 
 /* Query filters: bool{filter:[...]} conjunction of term / range clauses. */
@@ -249,6 +259,10 @@ int esgpu_terms_thresholds(int32_t size, int32_t shard_size, int64_t min_doc_cou
                            int32_t order, int32_t number_of_shards, int32_t* out_size, int32_t* out_shard_size,
                            int64_t* out_min_doc_count, int64_t* out_shard_min_doc_count);
 int esgpu_precision_from_threshold(int64_t count, int32_t* precision);
+/* The histogram / date_histogram spec's Rounding (Rounding.java, TimeZoneRounding.java incl. its time zone):
+ * op 0 = round(value), 1 = nextRoundingValue(value), 2 = roundKey(value).  Callers use it for ExtendedBounds.round
+ * (ExtendedBounds.java) before filling esgpu_agg_spec.extended_bounds_*. */
+int esgpu_date_rounding(const esgpu_agg_spec* spec, int32_t op, int64_t value, int64_t* out);
 /* MurmurHash3_x64_128 (common/hash/MurmurHash3.java:62-157): the murmur3 field's index-time hash is out[0] (h1)
  * (plugins/mapper-murmur3/.../Murmur3FieldMapper.java:152-165). */
 int esgpu_murmur3_x64_128(const uint8_t* bytes, size_t len, int64_t seed, uint64_t* out2);

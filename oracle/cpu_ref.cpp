@@ -163,28 +163,89 @@ static void civil_from_days(int64_t z, int64_t* y, int* m, int* d) {
 static const int64_t MS_DAY = 86400000LL;
 
 // ------------------------------------------------------------------------------------------------------------
-// Rounding (common/rounding/Rounding.java, TimeZoneRounding.java).  Fixed time-zone offsets are folded into
-// OffsetRounding by the caller (see include/esgpu.h esgpu_agg_spec.offset).
+// joda-time 2.8.2 DateTimeZone (third-party, not in /root/reference): getOffset / nextTransition over an offset
+// history (offs[i] from UTC instant starts[i] on), convertUTCToLocal, and both convertLocalToUTC overloads, restated
+// from joda's published DateTimeZone.java.  Pinned by TimeZoneRoundingTests' DST cases (kat.json "rounding_tz").
+// An empty table is UTC.
+// ------------------------------------------------------------------------------------------------------------
+struct Zone {
+    std::vector<int64_t> starts, offs;
+    int64_t getOffset(int64_t instant) const {  // starts[0] is -infinity
+        if (starts.empty()) return 0;
+        size_t lo = 0, hi = starts.size();  // last i with starts[i] <= instant (i = 0 always qualifies)
+        while (hi - lo > 1) {
+            const size_t mid = (lo + hi) / 2;
+            if (starts[mid] <= instant) lo = mid; else hi = mid;
+        }
+        return offs[lo];
+    }
+    int64_t nextTransition(int64_t instant) const {
+        for (size_t lo = 1, hi = starts.size(); lo < hi;) {  // first i >= 1 with starts[i] > instant
+            const size_t mid = (lo + hi) / 2;
+            if (starts[mid] > instant) hi = mid; else lo = mid + 1;
+            if (lo == hi) return lo < starts.size() ? starts[lo] : instant;
+        }
+        return instant;
+    }
+    int64_t convertUTCToLocal(int64_t utc) const { return utc + getOffset(utc); }
+    int64_t convertLocalToUTC(int64_t instantLocal, bool strict) const {
+        const int64_t offsetLocal = getOffset(instantLocal);
+        int64_t offset = getOffset(instantLocal - offsetLocal);
+        if (offsetLocal != offset) {
+            if (strict || offsetLocal < 0) {
+                int64_t nextLocal = nextTransition(instantLocal - offsetLocal);
+                if (nextLocal == (instantLocal - offsetLocal)) nextLocal = INT64_MAX;
+                int64_t nextAdjusted = nextTransition(instantLocal - offset);
+                if (nextAdjusted == (instantLocal - offset)) nextAdjusted = INT64_MAX;
+                if (nextLocal != nextAdjusted) {
+                    if (strict) throw std::runtime_error("IllegalInstantException");
+                    offset = offsetLocal;
+                }
+            }
+        }
+        return instantLocal - offset;
+    }
+    int64_t convertLocalToUTC(int64_t instantLocal, bool strict, int64_t originalInstantUTC) const {
+        const int64_t offsetOriginal = getOffset(originalInstantUTC);
+        const int64_t instantUTC = instantLocal - offsetOriginal;
+        const int64_t offsetLocalFromOriginal = getOffset(instantUTC);
+        if (offsetLocalFromOriginal == offsetOriginal) return instantUTC;
+        return convertLocalToUTC(instantLocal, strict);
+    }
+};
+
+// ------------------------------------------------------------------------------------------------------------
+// Rounding (common/rounding/Rounding.java, TimeZoneRounding.java:101-217).  A fixed time-zone offset given without a
+// zone table is folded into OffsetRounding by the caller (see include/esgpu.h esgpu_agg_spec.offset).
 // ------------------------------------------------------------------------------------------------------------
 struct Rounding {
-    int kind = 0;       // 0 = Interval (histogram), 1 = TimeUnitRounding (UTC), 2 = TimeIntervalRounding (UTC)
+    int kind = 0;       // 0 = Interval (histogram), 1 = TimeUnitRounding, 2 = TimeIntervalRounding
     int unit = 0;       // ESGPU_UNIT_*
     int64_t interval = 1;
     int64_t offset = 0; // OffsetRounding (Rounding.java:205-236); 0 = not wrapped
+    Zone tz;            // TimeZoneRounding's timeZone (empty = UTC)
 
     int64_t inner_round_key(int64_t v) const {
         switch (kind) {
             case 0: return floor_div(v, interval);                  // Rounding.Interval.roundKey
-            case 2: return floor_div(v, interval) * interval;       // TimeIntervalRounding.roundKey (UTC)
-            default: return unit_floor(v);                          // TimeUnitRounding.roundKey (UTC)
+            case 2: {                                               // TimeIntervalRounding.roundKey
+                const int64_t timeLocal = tz.convertUTCToLocal(v);
+                const int64_t rounded = floor_div(timeLocal, interval) * interval;
+                return tz.convertLocalToUTC(rounded, false);
+            }
+            default: {                                              // TimeUnitRounding.roundKey
+                const int64_t timeLocal = tz.convertUTCToLocal(v);
+                const int64_t rounded = unit_floor(timeLocal);
+                return tz.convertLocalToUTC(rounded, false, v);
+            }
         }
     }
     int64_t inner_value_for_key(int64_t k) const { return kind == 0 ? k * interval : k; }
     int64_t inner_next(int64_t v) const {
         switch (kind) {
             case 0: return v + interval;
-            case 2: return v + interval;
-            default: return unit_add(v);
+            case 2: return tz.convertLocalToUTC(tz.convertUTCToLocal(v) + interval, false);
+            default: return tz.convertLocalToUTC(unit_add(tz.convertUTCToLocal(v)), false);
         }
     }
     int64_t unit_floor(int64_t t) const {  // joda DateTimeField.roundFloor in ISOChronology UTC
@@ -250,6 +311,10 @@ static Rounding make_rounding(const esgpu_agg_spec& s) {
         r.interval = s.interval;
     }
     r.offset = s.offset;
+    if (r.kind != 0 && s.tz_count > 0) {
+        r.tz.starts.assign(s.tz_starts, s.tz_starts + s.tz_count);
+        r.tz.offs.assign(s.tz_offsets_ms, s.tz_offsets_ms + s.tz_count);
+    }
     if (r.kind != 1 && r.interval < 1) throw std::invalid_argument("interval must be >= 1");
     return r;
 }
@@ -1361,6 +1426,19 @@ int64_t oracle_index(uint64_t h, int32_t p) { return oracle::hll_index(h, p); }
 int32_t oracle_run_len(uint64_t h, int32_t p) { return oracle::run_len(h, p); }
 
 /* Rounding KATs: kind 0 histogram Interval, 1 date unit, 2 date interval; returns round(v) / next(v) / roundKey(v) */
+int64_t oracle_rounding_tz(int32_t kind, int32_t unit, int64_t interval, int64_t offset, const int64_t* tz_starts,
+                           const int64_t* tz_offs, int32_t tz_count, int32_t op, int64_t v) {
+    oracle::Rounding r;
+    r.kind = kind; r.unit = unit; r.interval = interval; r.offset = offset;
+    if (tz_count > 0) {
+        r.tz.starts.assign(tz_starts, tz_starts + tz_count);
+        r.tz.offs.assign(tz_offs, tz_offs + tz_count);
+    }
+    if (op == 0) return r.round(v);
+    if (op == 1) return r.next_rounding_value(v);
+    return r.round_key(v);
+}
+
 int64_t oracle_rounding(int32_t kind, int32_t unit, int64_t interval, int64_t offset, int32_t op, int64_t v) {
     oracle::Rounding r;
     r.kind = kind; r.unit = unit; r.interval = interval; r.offset = offset;

@@ -143,6 +143,68 @@ def rounding_vectors(ref):
     return cases
 
 
+def _zone_time(s, zone):
+    """ISODateTimeFormat.dateOptionalTimeParser().withZone(zone).parseMillis(s) for the non-ambiguous local times the
+    DST tests use (zone "UTC" or an IANA id, read through Python's zoneinfo)."""
+    import datetime as dt
+    import zoneinfo
+    m = re.match(r"(\d{4})-(\d{2})-(\d{2})T(\d{2}):(\d{2}):(\d{2})(?:\.(\d{3}))?$", s)
+    y, mo, d, hh, mm, ss = (int(m.group(i)) for i in range(1, 7))
+    ms = int(m.group(7) or 0)
+    tz = dt.timezone.utc if zone == "UTC" else zoneinfo.ZoneInfo(zone)
+    t = dt.datetime(y, mo, d, hh, mm, ss, tzinfo=tz)
+    return int(t.timestamp()) * 1000 + ms
+
+
+def rounding_tz_vectors(ref):
+    """DST-zone rounding KATs (TimeZoneRoundingTests.testTimeUnitRoundingDST / testAmbiguousHoursAfterDSTSwitch):
+    the rounding's zone id, its unit, and (input -> round(input)) pairs in UTC millis.  The zone tables themselves are
+    built at test time from the same zone ids (elasticsearch_amd.aggs.tz_history)."""
+    rel = T + "common/rounding/TimeZoneRoundingTests.java"
+    text = _read(ref, rel)
+    units = {"HOUR_OF_DAY": "hour", "DAY_OF_MONTH": "day", "MONTH_OF_YEAR": "month", "YEAR_OF_CENTURY": "year",
+             "WEEK_OF_WEEKYEAR": "week", "QUARTER": "quarter", "MINUTES_OF_HOUR": "minute", "SECOND_OF_MINUTE": "second"}
+    consts = {"JERUSALEM_TIMEZONE": "Asia/Jerusalem", "DateTimeZone.UTC": "UTC"}
+
+    def zone_of(expr):
+        expr = expr.strip()
+        m = re.fullmatch(r'DateTimeZone\.forID\("([^"]+)"\)', expr)
+        return m.group(1) if m else consts[expr]
+
+    cases = []
+    for method in ("testTimeUnitRoundingDST", "testAmbiguousHoursAfterDSTSwitch"):
+        start = text.index("public void " + method)
+        end = text.index("@Test", start)
+        body = text[start:end]
+        builder = re.compile(r"TimeZoneRounding\.builder\(DateTimeUnit\.(\w+)\)\.timeZone\(([^;]+?)\)\.build\(\);")
+        check = re.compile(r'assertThat\(tzRounding\.round\(time\("([^"]+)",\s*([^)]+\)?)\)\),\s*'
+                           r'equalTo\(time\("([^"]+)",\s*([^)]+\)?)\)\)\);', re.S)
+        cur = None
+        pos = 0
+        events = sorted([(m.start(), "b", m) for m in builder.finditer(body)] + [(m.start(), "c", m) for m in check.finditer(body)],
+                        key=lambda e: e[0])
+        for off, kind, m in events:
+            if kind == "b":
+                cur = {"unit": units[m.group(1)], "zone": zone_of(m.group(2)), "round": [],
+                       "cite": f"{rel}:{text.count(chr(10), 0, start + off) + 1}"}
+                cases.append(cur)
+            else:
+                cur["round"].append([_zone_time(m.group(1), zone_of(m.group(2))), _zone_time(m.group(3), zone_of(m.group(4)))])
+    cases = [c for c in cases if c["round"]]
+    assert sum(len(c["round"]) for c in cases) == 19, cases
+    # "Double buckets" (#9491): two instants of one year in different offsets round to the same key
+    m = re.search(r'assertThat\(tzRounding\.round\(time\("([^"]+)", JERUSALEM_TIMEZONE\)\),\s*'
+                  r'equalTo\(tzRounding\.round\(time\("([^"]+)", JERUSALEM_TIMEZONE\)\)\)\);', text)
+    cases.append({"unit": "year", "zone": "Asia/Jerusalem", "round": [],
+                  "same": [[_zone_time(m.group(1), "Asia/Jerusalem"), _zone_time(m.group(2), "Asia/Jerusalem")]],
+                  "cite": f"{rel}:{text.count(chr(10), 0, m.start()) + 1}"})
+    # testLenientConversionDST: nextRoundingValue(t) > t for every minute across a DST start (property, not values)
+    lenient = {"zone": "America/Sao_Paulo", "start": _zone_time("2014-10-18T20:50:00.000", "America/Sao_Paulo"),
+               "end": _zone_time("2014-10-19T01:00:00.000", "America/Sao_Paulo"), "step": 60000,
+               "cite": f"{rel}:{_line_of(text, 'public void testLenientConversionDST')}"}
+    return {"cases": cases, "lenient": lenient}
+
+
 def stats_fixtures(ref):
     """AbstractNumericTestCase fixture: 10 docs, value = i+1, values = [i+2, i+3]; ExtendedStatsTests expectations."""
     rel = T + "search/aggregations/metrics/AbstractNumericTestCase.java"
@@ -268,6 +330,7 @@ def main():
     kat = {"murmur3_x64_128": murmur3_vectors(ref),
            "precision_from_threshold": precision_vectors(ref),
            "rounding": rounding_vectors(ref),
+           "rounding_tz": rounding_tz_vectors(ref),
            "stats": stats_fixtures(ref),
            "shard_size_terms": shard_size_fixture(ref),
            "rest": rest_fixtures(ref),

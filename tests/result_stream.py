@@ -1,4 +1,4 @@
-"""Test-side encoder of the libesgpu shard-result stream (esgpu_result_serialize format, version 2, esgpu_results.cpp).
+"""Test-side encoder of the libesgpu shard-result stream (esgpu_result_serialize format, version 3, esgpu_results.cpp).
 
 Lets CPU tests hand-build shard-level InternalAggregations (the way the reference's unit tests construct
 StringTerms / InternalHistogram / InternalCardinality objects) and push them through esgpu_result_deserialize +
@@ -10,7 +10,7 @@ import struct
 from elasticsearch_amd import _native as N
 
 MAGIC = 0x45534750
-VERSION = 2
+VERSION = 3
 BUCKET_TYPES = (N.AGG_TERMS, N.AGG_HISTOGRAM, N.AGG_DATE_HISTOGRAM)
 
 
@@ -33,6 +33,8 @@ def _block(b, insts):
     b += struct.pack("<iiqii", a.get("required_size", 10), a.get("shard_size", 10), a.get("min_doc_count", 1),
                      a.get("show_err", 0), a.get("keyed", 0))
     b += struct.pack("<Biqq", a.get("has_empty_info", 0), a.get("date_unit", 0), a.get("interval", 1), a.get("offset", 0))
+    _vec(b, "q", a.get("tz_starts", []))
+    _vec(b, "q", a.get("tz_offs", []))
     b += struct.pack("<BBqq", a.get("has_bmin", 0), a.get("has_bmax", 0), a.get("bmin", 0), a.get("bmax", 0))
     b += struct.pack("<diQ", a.get("sigma", 2.0), a.get("precision", 14), len(insts))
     bucket = t in BUCKET_TYPES
@@ -89,6 +91,8 @@ def _empty_block(b, spec):
     b += struct.pack("<iiqii", s.get("required_size", 10), s.get("shard_size", 10), s.get("min_doc_count", 1),
                      s.get("show_err", 0), s.get("keyed", 0))
     b += struct.pack("<Biqq", s.get("has_empty_info", 0), s.get("date_unit", 0), s.get("interval", 1), s.get("offset", 0))
+    _vec(b, "q", s.get("tz_starts", []))
+    _vec(b, "q", s.get("tz_offs", []))
     b += struct.pack("<BBqq", s.get("has_bmin", 0), s.get("has_bmax", 0), s.get("bmin", 0), s.get("bmax", 0))
     b += struct.pack("<diQ", s.get("sigma", 2.0), s.get("precision", 14), 0)
     bucket = t in BUCKET_TYPES

@@ -1,0 +1,117 @@
+"""GPU parity of date_histogram roundings that are not affine: calendar units (month / quarter / year) and time zones
+with DST transitions (TimeZoneRounding.TimeUnitRounding / TimeIntervalRounding over a joda zone).
+
+The kernel buckets these through a per-segment table of bucket start instants built on the host
+(es_rounding.hpp key_table); the oracle evaluates the reference's roundKey per value.  Timestamps span two years so
+every zone crosses several transitions; sorted data exercises the LDS window, shuffled data the global-atomic path.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from elasticsearch_amd import AggregationBuilders as AB
+from elasticsearch_amd import _native as N
+from elasticsearch_amd import reduce
+from helpers import assert_same
+
+pytestmark = pytest.mark.gpu
+
+T0 = 1388534400000  # 2014-01-01T00:00:00Z
+SPAN = 2 * 365 * 86_400_000
+
+
+def columns(n, seed, sorted_ts=True, lo=T0, span=SPAN):
+    rng = np.random.default_rng(seed)
+    ts = rng.integers(lo, lo + span, size=n).astype(np.int64)
+    if sorted_ts:
+        ts.sort()
+    host = np.minimum(rng.zipf(1.5, size=n) - 1, 199).astype(np.uint32)
+    rt = rng.integers(0, 1000, size=n).astype(np.int64)
+    return {"@timestamp": {"type": N.COL_I64, "values": ts},
+            "host": {"type": N.COL_ORD_U32, "values": host, "terms": ["h%03d" % i for i in range(200)]},
+            "response_time_ms": {"type": N.COL_I64, "values": rt}}
+
+
+def check(engine, aggs, cols, n):
+    want = O.run([(cols, n)], aggs)
+    seg = engine.upload_segment(cols, n)
+    plan = engine.plan(aggs)
+    plan.collect(seg)
+    res = plan.build()
+    assert_same(res.to_dict(), want["shards"][0], "shard")
+    assert_same(reduce([res]).to_dict(), want["reduced"], "reduced")
+    plan.close()
+    seg.close()
+    return want["reduced"]
+
+
+CALENDAR = [
+    AB.dateHistogram("month").field("@timestamp").interval("month").subAggregation(AB.stats("rt").field("response_time_ms")),
+    AB.dateHistogram("quarter").field("@timestamp").interval("quarter"),
+    AB.dateHistogram("year").field("@timestamp").interval("1y").subAggregation(AB.extendedStats("rt").field("response_time_ms")),
+    AB.dateHistogram("month_off").field("@timestamp").interval("1M").offset("6h").timeZone("-03:00"),
+]
+
+ZONED = [
+    AB.dateHistogram("day_chicago").field("@timestamp").interval("1d").timeZone("America/Chicago")
+    .subAggregation(AB.avg("rt").field("response_time_ms")),
+    AB.dateHistogram("hour_berlin").field("@timestamp").interval("1h").timeZone("Europe/Berlin"),
+    AB.dateHistogram("m90_jerusalem").field("@timestamp").interval("90m").timeZone("Asia/Jerusalem"),
+    AB.dateHistogram("week_lord_howe").field("@timestamp").interval("week").timeZone("Australia/Lord_Howe"),
+    AB.dateHistogram("month_sao_paulo").field("@timestamp").interval("month").timeZone("America/Sao_Paulo").offset("1h"),
+]
+
+
+@pytest.mark.parametrize("sorted_ts", [True, False])
+def test_calendar_units(engine, sorted_ts):
+    r = check(engine, CALENDAR, columns(1_500_000, 1, sorted_ts), 1_500_000)
+    assert len(r["month"]["buckets"]) == 24 and len(r["quarter"]["buckets"]) == 8 and len(r["year"]["buckets"]) == 2
+
+
+@pytest.mark.parametrize("sorted_ts", [True, False])
+def test_dst_zones(engine, sorted_ts):
+    check(engine, ZONED, columns(1_500_000, 2, sorted_ts), 1_500_000)
+
+
+def test_dst_nested_under_terms_and_over_terms(engine):
+    aggs = [AB.terms("hosts").field("host").size(20).subAggregation(
+                AB.dateHistogram("d").field("@timestamp").interval("day").timeZone("Europe/Berlin")
+                .subAggregation(AB.stats("rt").field("response_time_ms"))),
+            AB.dateHistogram("m").field("@timestamp").interval("month").timeZone("America/Chicago")
+            .subAggregation(AB.terms("hosts").field("host").size(5))]
+    check(engine, aggs, columns(1_000_000, 3), 1_000_000)
+
+
+def test_calendar_extended_bounds_empty_buckets(engine):
+    """min_doc_count 0 with extended_bounds outside the data: ExtendedBounds.round and the empty-bucket fill both use
+    the zoned calendar rounding (nextRoundingValue across DST)."""
+    lo, hi = T0 + 100 * 86_400_000, T0 + 160 * 86_400_000
+    cols = columns(200_000, 4, lo=lo, span=hi - lo)
+    aggs = [AB.dateHistogram("d").field("@timestamp").interval("day").timeZone("America/Chicago").minDocCount(0)
+            .extendedBounds(T0 + 60 * 86_400_000, T0 + 200 * 86_400_000),
+            AB.dateHistogram("m").field("@timestamp").interval("month").timeZone("Europe/Berlin").minDocCount(0)
+            .extendedBounds(T0, T0 + 300 * 86_400_000)]
+    r = check(engine, aggs, cols, 200_000)
+    assert len(r["m"]["buckets"]) == 10
+
+
+def test_table_grows_across_segments(engine):
+    """Two segments whose time ranges do not overlap: the second one extends the bucket table on both sides' union
+    and the grid rows of the first are shifted, not lost."""
+    n1, n2 = 300_000, 200_000
+    a = columns(n1, 5, lo=T0 + 400 * 86_400_000, span=100 * 86_400_000)
+    b = columns(n2, 6, lo=T0, span=90 * 86_400_000)
+    one = {k: {**a[k], "values": np.concatenate([a[k]["values"], b[k]["values"]])} for k in a}
+    aggs = [AB.dateHistogram("m").field("@timestamp").interval("month").timeZone("America/Chicago")
+            .subAggregation(AB.avg("rt").field("response_time_ms")),
+            AB.terms("hosts").field("host").size(5).subAggregation(
+                AB.dateHistogram("w").field("@timestamp").interval("week").timeZone("Europe/Berlin"))]
+    want = O.run([(one, n1 + n2)], aggs)
+    segs = [engine.upload_segment(a, n1), engine.upload_segment(b, n2)]
+    plan = engine.plan(aggs)
+    for s in segs:
+        plan.collect(s)
+    assert_same(plan.build().to_dict(), want["shards"][0], "shard")
+    plan.close()
+    for s in segs:
+        s.close()

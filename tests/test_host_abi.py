@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
     for name in names:
         assert hasattr(lib, name), name
     assert {n for n, _, _ in N.SIGNATURES} == set(names)
-    assert lib.esgpu_abi_version() == 1
+    assert lib.esgpu_abi_version() == 2
 
 
 def test_no_silent_cpu_fallback():
@@ -195,3 +195,78 @@ def test_stream_roundtrip_and_json():
     assert d["c"]["value"] == 0 and d["c"]["_internal"]["present"] == 0
     with pytest.raises(N.EsGpuError):
         ShardResult.deserialize(b"garbage!")
+
+
+# ---- date rounding (esgpu_date_rounding: Rounding / TimeZoneRounding with joda zone arithmetic) ----
+def _date_spec(unit, interval=0, offset=0, zone=None):
+    from elasticsearch_amd.aggs import tz_history
+    sp = N.AggSpec()
+    sp.type = N.AGG_DATE_HISTOGRAM
+    sp.date_unit = unit
+    sp.interval = interval
+    sp.offset = offset
+    keep = []
+    if zone and zone != "UTC":
+        starts, offs = tz_history(zone)
+        st = (ctypes.c_int64 * len(starts))(*starts)
+        of = (ctypes.c_int64 * len(offs))(*offs)
+        keep += [st, of]
+        sp.tz_starts = ctypes.cast(st, ctypes.POINTER(ctypes.c_int64))
+        sp.tz_offsets_ms = ctypes.cast(of, ctypes.POINTER(ctypes.c_int64))
+        sp.tz_count = len(starts)
+    return sp, keep
+
+
+def product_round(sp, op, v):
+    out = ctypes.c_int64()
+    N.check(N.lib().esgpu_date_rounding(ctypes.byref(sp), op, v, ctypes.byref(out)))
+    return out.value
+
+
+UNITS_BY_NAME = {"hour": N.UNIT_HOUR, "day": N.UNIT_DAY, "month": N.UNIT_MONTH, "year": N.UNIT_YEAR, "minute": N.UNIT_MINUTE,
+                 "week": N.UNIT_WEEK}
+
+
+def test_date_rounding_known_values(kat):  # the product's rounding on TimeZoneRoundingTests' UTC, fixed and DST KATs
+    for c in kat["rounding"]:
+        if c["kind"] == "histogram":
+            continue
+        unit = UNITS_BY_NAME[c["unit"]] if c["kind"] == "unit" else N.UNIT_NONE
+        sp, _ = _date_spec(unit, c.get("interval", 0), c["offset"])
+        for v, expect in c["round"]:
+            assert product_round(sp, 0, v) == expect, c["cite"]
+        for v, expect in c["next"]:
+            assert product_round(sp, 1, v) == expect, c["cite"]
+    for c in kat["rounding_tz"]["cases"]:
+        sp, keep = _date_spec(UNITS_BY_NAME[c["unit"]], zone=c["zone"])
+        for v, expect in c["round"]:
+            assert product_round(sp, 0, v) == expect, c["cite"]
+        for a, b in c.get("same", []):
+            assert product_round(sp, 0, a) == product_round(sp, 0, b), c["cite"]
+    c = kat["rounding_tz"]["lenient"]
+    sp, keep = _date_spec(N.UNIT_MINUTE, zone=c["zone"])
+    sp2, keep2 = _date_spec(N.UNIT_NONE, 60000, zone=c["zone"])
+    for t in range(c["start"], c["end"], c["step"]):
+        assert product_round(sp, 1, t) > t and product_round(sp2, 1, t) > t, c["cite"]
+
+
+def test_date_rounding_matches_oracle_across_zones():
+    """Product Rounding (es_rounding.hpp) == oracle Rounding (cpu_ref.cpp), two independent restatements, on random
+    instants around DST transitions, for every unit, fixed intervals and offsets."""
+    from test_oracle_kat import oracle_round_tz
+    rng = np.random.default_rng(5)
+    zones = ["Europe/Berlin", "America/Chicago", "Asia/Jerusalem", "America/Sao_Paulo", "Australia/Lord_Howe",
+             "Asia/Kolkata", "UTC"]
+    for i in range(1500):
+        zone = zones[i % len(zones)]
+        if i % 3 == 2:
+            kind, unit, interval = 2, N.UNIT_NONE, int(rng.choice([60000, 900000, 5400000, 3600000 * 7, 86400000]))
+        else:
+            kind, unit, interval = 1, int(rng.integers(1, 9)), 0
+        offset = int(rng.choice([0, 0, 3600000, -1800000]))
+        base = int(rng.integers(0, 2 * 10**12))
+        sp, keep = _date_spec(unit, interval, offset, zone)
+        for v in (base, base - base % 3600000, base - base % 86400000 + 3600000 * int(rng.integers(0, 4))):
+            for op in (0, 1, 2):
+                assert product_round(sp, op, v) == oracle_round_tz(kind, unit, interval, offset, zone, op, v), \
+                    (zone, kind, unit, interval, offset, op, v)

@@ -80,6 +80,54 @@ def test_rounding_known_values(kat):  # RoundingTests / TimeZoneRoundingTests (U
             assert L.oracle_rounding(kind, unit, interval, c["offset"], 2, v) == expect, c["cite"]
 
 
+TZ_UNITS = {"hour": N.UNIT_HOUR, "day": N.UNIT_DAY, "month": N.UNIT_MONTH, "year": N.UNIT_YEAR, "minute": N.UNIT_MINUTE}
+
+
+def oracle_round_tz(kind, unit, interval, offset, zone, op, v):
+    from elasticsearch_amd.aggs import tz_history
+    starts, offs = tz_history(zone) if zone != "UTC" else ((-(1 << 63),), (0,))
+    st = (ctypes.c_int64 * len(starts))(*starts)
+    of = (ctypes.c_int64 * len(offs))(*offs)
+    L = O.lib()
+    L.oracle_rounding_tz.restype = ctypes.c_int64
+    L.oracle_rounding_tz.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64,
+                                     ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), ctypes.c_int32,
+                                     ctypes.c_int32, ctypes.c_int64]
+    return L.oracle_rounding_tz(kind, unit, interval, offset, st, of, len(starts), op, v)
+
+
+def test_rounding_dst_known_values(kat):  # TimeZoneRoundingTests.testTimeUnitRoundingDST / testAmbiguousHoursAfterDSTSwitch
+    cases = kat["rounding_tz"]["cases"]
+    assert sum(len(c["round"]) for c in cases) == 19
+    for c in cases:
+        for v, expect in c["round"]:
+            got = oracle_round_tz(1, TZ_UNITS[c["unit"]], 0, 0, c["zone"], 0, v)
+            assert got == expect, (c["cite"], v, got, expect)
+        for a, b in c.get("same", []):
+            assert oracle_round_tz(1, TZ_UNITS[c["unit"]], 0, 0, c["zone"], 0, a) == \
+                oracle_round_tz(1, TZ_UNITS[c["unit"]], 0, 0, c["zone"], 0, b), c["cite"]
+
+
+def test_rounding_dst_lenient_conversion(kat):  # TimeZoneRoundingTests.testLenientConversionDST
+    c = kat["rounding_tz"]["lenient"]
+    for t in range(c["start"], c["end"], c["step"]):
+        assert oracle_round_tz(1, N.UNIT_MINUTE, 0, 0, c["zone"], 1, t) > t, c["cite"]
+        assert oracle_round_tz(2, 0, 60000, 0, c["zone"], 1, t) > t, c["cite"]
+
+
+def test_rounding_tz_random_properties():  # TimeZoneRoundingTests.testTimeZoneRoundingRandom with DST zones
+    rng = np.random.default_rng(77)
+    for i in range(600):
+        zone = ["Europe/Berlin", "America/Chicago", "Asia/Jerusalem", "America/Sao_Paulo", "Australia/Lord_Howe"][i % 5]
+        unit = int(rng.integers(1, 9))
+        date = int(rng.integers(0, 10**12))
+        r = oracle_round_tz(1, unit, 0, 0, zone, 0, date)
+        nxt = oracle_round_tz(1, unit, 0, 0, zone, 1, r)
+        assert r <= date, (zone, unit, date)
+        assert oracle_round_tz(1, unit, 0, 0, zone, 0, r) == r, (zone, unit, date)
+        assert nxt > r, (zone, unit, date)
+
+
 def _i64(vals):
     return {"type": N.COL_I64, "values": np.array(vals, dtype=np.int64)}
 
