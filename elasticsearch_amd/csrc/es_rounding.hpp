@@ -217,23 +217,30 @@ struct Rounding {
         return true;
     }
 
-    // Bucket table of a non-affine rounding over the values [lo, hi]: starts[b] = first value of bucket b,
-    // keys[b] = its key (value_for_key).  round_key is a step function whose steps can only sit at a zone transition or
-    // at a local-time unit / interval boundary, so walking those points visits every bucket exactly once.
-    // Returns false when the buckets are not monotone in the value (no such zone in the IANA data) or exceed max_buckets.
-    bool key_table(int64_t lo, int64_t hi, size_t max_buckets, std::vector<int64_t>& starts, std::vector<int64_t>& keys) const {
+    // Bucket table of a non-affine rounding over the values [lo, hi].  round_key is a step function whose steps can only
+    // sit at a zone transition or at a local-time unit / interval boundary, so walking those points visits every step:
+    //   starts[j]  first value of step j (ascending)          keys[b]  distinct bucket keys, ascending
+    //   slot[j]    bucket of step j (empty when step j == bucket j, i.e. the keys rise with the value)
+    // TimeIntervalRounding maps the repeated local hour of a DST fall-back to its first occurrence
+    // (convertLocalToUTC without the original instant), so there a later step can return to an earlier bucket.
+    // Returns false when the table would exceed max_steps.
+    bool key_table(int64_t lo, int64_t hi, size_t max_steps, std::vector<int64_t>& starts, std::vector<int64_t>& keys,
+                   std::vector<uint32_t>& slot) const {
         starts.clear();
         keys.clear();
+        slot.clear();
         if (lo > hi) return true;
+        std::vector<int64_t> step_key;
+        bool monotone = true;
         int64_t u = lo - offset;
         const int64_t uhi = hi - offset;
         for (;;) {
-            const int64_t k = inner_round_key(u);
-            if (keys.empty() || k != keys.back() - offset) {
-                if (!keys.empty() && k < keys.back() - offset) return false;
-                if (keys.size() >= max_buckets) return false;
+            const int64_t k = inner_round_key(u) + offset;
+            if (step_key.empty() || k != step_key.back()) {
+                if (!step_key.empty() && k < step_key.back()) monotone = false;
+                if (step_key.size() >= max_steps) return false;
                 starts.push_back(u + offset);
-                keys.push_back(k + offset);
+                step_key.push_back(k);
             }
             const int64_t o = tz.offset(u);
             const int64_t local = u + o;
@@ -245,6 +252,16 @@ struct Rounding {
             if (cand > uhi) break;
             u = cand;
         }
+        if (monotone) {
+            keys = std::move(step_key);
+            return true;
+        }
+        keys = step_key;
+        std::sort(keys.begin(), keys.end());
+        keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+        slot.resize(step_key.size());
+        for (size_t j = 0; j < step_key.size(); ++j)
+            slot[j] = (uint32_t)(std::lower_bound(keys.begin(), keys.end(), step_key[j]) - keys.begin());
         return true;
     }
 };

@@ -260,15 +260,16 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
 
 // grid key index of a value: affine roundings divide, table roundings (calendar units, DST zones) search the bucket
 // start instants; values outside the grid give an index outside [0, H)
+template <bool KT>
 __device__ __forceinline__ int64_t key_index(const CollectParams& P, int64_t v) {
-    if (!P.kstart) return floor_div64(v - P.offset, P.interval) - P.key0;
+    if (!KT) return floor_div64(v - P.offset, P.interval) - P.key0;
     if (v < P.kstart[0]) return -1;
-    uint32_t lo = 0, hi = P.H;  // kstart[lo] <= v < kstart[hi] (kstart[H] = +inf)
+    uint32_t lo = 0, hi = P.nsteps;  // kstart[lo] <= v < kstart[hi] (kstart[nsteps] = +inf)
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (P.kstart[mid] <= v) lo = mid; else hi = mid;
     }
-    return lo;
+    return P.kslot ? P.kslot[lo] : lo;
 }
 
 // key slot of a value relative to `base` (= value of the first slot); 32-bit magic division fast path
@@ -315,7 +316,7 @@ __device__ __forceinline__ void run_flush(const CollectParams& P, const Acc& a, 
     run_reset(r);
 }
 
-template <bool ORD, bool HIST, int MET, bool LDS>
+template <bool ORD, bool HIST, int MET, bool LDS, bool KT>
 __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, const Doc4& d, uint32_t T, int64_t base,
                                          uint32_t win0, Run& run) {
     uint32_t slot[kVec];
@@ -327,9 +328,9 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
         if (HIST) {
             hv_ok[j] = (d.hpres >> j) & 1;
             if (LDS) {
-                slot[j] = P.kstart ? (uint32_t)(key_index(P, d.hv[j]) - (int64_t)win0) : slot_of(P, d.hv[j], base);
+                slot[j] = KT ? (uint32_t)(key_index<KT>(P, d.hv[j]) - (int64_t)win0) : slot_of(P, d.hv[j], base);
             } else {
-                const int64_t k = key_index(P, d.hv[j]);
+                const int64_t k = key_index<KT>(P, d.hv[j]);
                 hv_ok[j] = hv_ok[j] && k >= 0 && k < (int64_t)P.H;
                 slot[j] = (uint32_t)k;
             }
@@ -421,8 +422,11 @@ __device__ void flush_window(const CollectParams& P, const Acc& s, uint32_t T, u
     __syncthreads();
 }
 
-template <bool ORD, bool HIST, int MET>
+// HK: 0 = no histogram dimension, 1 = affine rounding, 2 = bucket table (calendar units / DST zones)
+template <bool ORD, int HK, int MET>
 __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
+    constexpr bool HIST = HK != 0;
+    constexpr bool KT = HK == 2;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t T = ORD ? P.T : 1u;
     const uint32_t W = HIST ? P.W : 1u;
@@ -497,8 +501,8 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
             if (use_lds && HIST && P.windowed) {
                 const int64_t zmn = P.zmin[b], zmx = P.zmax[b];
                 if (zmn <= zmx) {  // block has at least one timestamp
-                    const int64_t kmn = key_index(P, zmn);
-                    const int64_t kmx = key_index(P, zmx);
+                    const int64_t kmn = key_index<KT>(P, zmn);
+                    const int64_t kmx = key_index<KT>(P, zmx);
                     if (kmx - kmn + 1 > (int64_t)W) {
                         use_lds = false;  // block spans more keys than the window: global atomics for this block
                     } else if (!win_set || kmn < (int64_t)win0 || kmx >= (int64_t)win0 + (int64_t)W) {
@@ -517,10 +521,10 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
         Doc4 nxt;
         if (i + kPrefetch < n_it) load_docs<ORD, HIST, MET>(P, doc_of(i + kPrefetch), nxt);
         if (use_lds) {
-            process4<ORD, HIST, MET, true>(P, s, q[0], T, base, win0, run);
+            process4<ORD, HIST, MET, true, KT>(P, s, q[0], T, base, win0, run);
             dirty = true;
         } else {
-            process4<ORD, HIST, MET, false>(P, g, q[0], T, base, win0, run);
+            process4<ORD, HIST, MET, false, KT>(P, g, q[0], T, base, win0, run);
         }
 #pragma unroll
         for (int k = 0; k + 1 < kPrefetch; ++k) q[k] = q[k + 1];
@@ -532,48 +536,52 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
     }
 }
 
-template <bool ORD, bool HIST, int MET>
+template <bool ORD, int HK, int MET>
 static void launch_t(const CollectParams& p, uint32_t grid, size_t lds, hipStream_t st) {
-    hipLaunchKernelGGL((collect_kernel<ORD, HIST, MET>), dim3(grid), dim3(kWG), lds, st, p);
+    hipLaunchKernelGGL((collect_kernel<ORD, HK, MET>), dim3(grid), dim3(kWG), lds, st, p);
 }
 
-template <bool ORD, bool HIST>
+template <bool ORD, int HK>
 static void launch_m(const CollectParams& p, int met, uint32_t grid, size_t lds, hipStream_t st) {
     switch (met) {
-        case 0: launch_t<ORD, HIST, 0>(p, grid, lds, st); break;
-        case 1: launch_t<ORD, HIST, 1>(p, grid, lds, st); break;
-        case 2: launch_t<ORD, HIST, 2>(p, grid, lds, st); break;
-        default: launch_t<ORD, HIST, 3>(p, grid, lds, st); break;
+        case 0: launch_t<ORD, HK, 0>(p, grid, lds, st); break;
+        case 1: launch_t<ORD, HK, 1>(p, grid, lds, st); break;
+        case 2: launch_t<ORD, HK, 2>(p, grid, lds, st); break;
+        default: launch_t<ORD, HK, 3>(p, grid, lds, st); break;
     }
 }
 
 void launch_collect(const CollectParams& p, bool ord, bool hist, int met, uint32_t grid, size_t lds, hipStream_t st) {
-    if (ord && hist) launch_m<true, true>(p, met, grid, lds, st);
-    else if (ord) launch_m<true, false>(p, met, grid, lds, st);
-    else if (hist) launch_m<false, true>(p, met, grid, lds, st);
-    else launch_m<false, false>(p, met, grid, lds, st);
-}
-
-template <bool ORD, bool HIST, int MET>
-static int occ_t(size_t lds) {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, collect_kernel<ORD, HIST, MET>, kWG, lds) != hipSuccess) n = 1;
-    return n;
-}
-template <bool ORD, bool HIST>
-static int occ_m(int met, size_t lds) {
-    switch (met) {
-        case 0: return occ_t<ORD, HIST, 0>(lds);
-        case 1: return occ_t<ORD, HIST, 1>(lds);
-        case 2: return occ_t<ORD, HIST, 2>(lds);
-        default: return occ_t<ORD, HIST, 3>(lds);
+    const int hk = hist ? (p.kstart ? 2 : 1) : 0;
+    if (ord) {
+        if (hk == 2) launch_m<true, 2>(p, met, grid, lds, st);
+        else if (hk == 1) launch_m<true, 1>(p, met, grid, lds, st);
+        else launch_m<true, 0>(p, met, grid, lds, st);
+    } else {
+        if (hk == 2) launch_m<false, 2>(p, met, grid, lds, st);
+        else if (hk == 1) launch_m<false, 1>(p, met, grid, lds, st);
+        else launch_m<false, 0>(p, met, grid, lds, st);
     }
 }
-int collect_occupancy(bool ord, bool hist, int met, size_t lds) {
-    if (ord && hist) return occ_m<true, true>(met, lds);
-    if (ord) return occ_m<true, false>(met, lds);
-    if (hist) return occ_m<false, true>(met, lds);
-    return occ_m<false, false>(met, lds);
+
+template <bool ORD, int HK, int MET>
+static int occ_t(size_t lds) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, collect_kernel<ORD, HK, MET>, kWG, lds) != hipSuccess) n = 1;
+    return n;
+}
+template <bool ORD, int HK>
+static int occ_m(int met, size_t lds) {
+    switch (met) {
+        case 0: return occ_t<ORD, HK, 0>(lds);
+        case 1: return occ_t<ORD, HK, 1>(lds);
+        case 2: return occ_t<ORD, HK, 2>(lds);
+        default: return occ_t<ORD, HK, 3>(lds);
+    }
+}
+int collect_occupancy(bool ord, int hk, int met, size_t lds) {
+    if (ord) return hk == 2 ? occ_m<true, 2>(met, lds) : hk == 1 ? occ_m<true, 1>(met, lds) : occ_m<true, 0>(met, lds);
+    return hk == 2 ? occ_m<false, 2>(met, lds) : hk == 1 ? occ_m<false, 1>(met, lds) : occ_m<false, 0>(met, lds);
 }
 
 size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode) {

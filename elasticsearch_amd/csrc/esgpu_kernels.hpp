@@ -54,7 +54,9 @@ struct CollectParams {
     const int64_t* hv;
     const uint64_t* hv_present;
     int64_t interval, offset, key0;  // key index k of a value v: floor((v - offset) / interval) - key0
-    const int64_t* kstart;           // non-affine roundings: bucket start instants [H] (key index = last start <= v)
+    const int64_t* kstart;           // non-affine roundings: step start instants [nsteps] (step = last start <= v)
+    const uint32_t* kslot;           // bucket of each step (null: step j is bucket j)
+    uint32_t nsteps;
     const int64_t* zmin;
     const int64_t* zmax;
     uint32_t mg_m, mg_s1, mg_s2;
@@ -112,7 +114,7 @@ void launch_zone_map(const int64_t* v, const uint64_t* present, uint32_t n, int6
 void launch_synth(const SynthParams& p, hipStream_t s);
 void launch_collect(const CollectParams& p, bool ord, bool hist, int met, uint32_t grid, size_t lds, hipStream_t s);
 size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode);
-int collect_occupancy(bool ord, bool hist, int met, size_t lds);  // resident workgroups per CU
+int collect_occupancy(bool ord, int hk, int met, size_t lds);  // resident workgroups per CU (hk: 0 none, 1 affine, 2 table)
 void launch_hll(const HllParams& p, uint32_t cus, hipStream_t s);
 void launch_remap_ords(const uint32_t* in, uint32_t n, const uint32_t* map, uint32_t map_n, uint32_t* out, hipStream_t s);
 void launch_pack_u8(const unsigned int* src, uint32_t n, uint8_t* dst, hipStream_t s);

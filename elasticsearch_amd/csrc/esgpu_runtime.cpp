@@ -704,8 +704,9 @@ struct Pipeline {
     Rounding rnd;                    // the histogram spec's rounding
     bool ktable = false;             // non-affine rounding: bucket start table instead of the affine map
     int64_t kt_lo = 0, kt_hi = -1;   // value range the table covers
-    std::vector<int64_t> kt_start, kt_key;  // [H] bucket start instants and keys
-    DevBuf d_kstart;                 // device copy of kt_start
+    std::vector<int64_t> kt_start, kt_key;  // step start instants, [H] bucket keys (es_rounding.hpp key_table)
+    std::vector<uint32_t> kt_slot;   // bucket of each step (empty: steps are buckets)
+    DevBuf d_kstart, d_kslot;        // device copies
     // device state
     bool allocated = false;
     uint32_t T = 1, H = 1;
@@ -990,8 +991,9 @@ static int64_t build_key_table(esgpu_plan* p, Pipeline& pl, int64_t lo, int64_t 
         hi = std::max(hi, pl.kt_hi);
     }
     std::vector<int64_t> starts, keys;
-    require(pl.rnd.key_table(lo, hi, kMaxTableBuckets, starts, keys), ESGPU_ERR_UNSUPPORTED,
-            "date_histogram rounding produces too many or non-monotone buckets for a dense grid");
+    std::vector<uint32_t> slot;
+    require(pl.rnd.key_table(lo, hi, kMaxTableBuckets, starts, keys, slot), ESGPU_ERR_UNSUPPORTED,
+            "date_histogram rounding produces too many buckets for a dense grid");
     int64_t shift = 0;
     if (!pl.kt_key.empty()) {
         auto it = std::lower_bound(keys.begin(), keys.end(), pl.kt_key.front());
@@ -1002,9 +1004,15 @@ static int64_t build_key_table(esgpu_plan* p, Pipeline& pl, int64_t lo, int64_t 
     pl.kt_hi = hi;
     pl.kt_start = std::move(starts);
     pl.kt_key = std::move(keys);
+    pl.kt_slot = std::move(slot);
     pl.d_kstart.alloc(p->ctx, std::max<size_t>(pl.kt_start.size(), 1) * 8);
     if (!pl.kt_start.empty())
         HIPX(hipMemcpyAsync(pl.d_kstart.p, pl.kt_start.data(), pl.kt_start.size() * 8, hipMemcpyHostToDevice, p->stream));
+    pl.d_kslot.release();
+    if (!pl.kt_slot.empty()) {
+        pl.d_kslot.alloc(p->ctx, pl.kt_slot.size() * 4);
+        HIPX(hipMemcpyAsync(pl.d_kslot.p, pl.kt_slot.data(), pl.kt_slot.size() * 4, hipMemcpyHostToDevice, p->stream));
+    }
     return shift;
 }
 
@@ -1179,6 +1187,8 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
     P.offset = pl.offset;
     P.key0 = pl.key0;
     P.kstart = (HIST && pl.ktable) ? pl.d_kstart.as<int64_t>() : nullptr;
+    P.kslot = P.kstart ? pl.d_kslot.as<uint32_t>() : nullptr;
+    P.nsteps = (uint32_t)pl.kt_start.size();
     P.zmin = hc ? hc->zmin.as<int64_t>() : nullptr;
     P.zmax = hc ? hc->zmax.as<int64_t>() : nullptr;
     P.mv = mc ? mc->values.p : nullptr;
@@ -1204,7 +1214,7 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
     P.lds_mode = 1;
     P.windowed = 0;
     if (lds > kLdsPair) {
-        if (HIST) {
+        if (HIST && !P.kslot) {  // the key window needs buckets that rise with the value (zone-map ranges)
             uint32_t w = pl.H;
             while (w > 1 && collect_lds_bytes(pl.T, w, met_launch, pl.vcnt_mode, pl.ocnt_mode) > kLdsPair) w = (w + 1) / 2;
             if (collect_lds_bytes(pl.T, w, met_launch, pl.vcnt_mode, pl.ocnt_mode) > kLdsPair) w = 1;
@@ -1231,9 +1241,10 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
         const MagicU32 mg = make_magic((uint32_t)pl.interval);
         P.mg_m = mg.m; P.mg_s1 = mg.s1; P.mg_s2 = mg.s2;
     }
-    const uint64_t occ_key = ((uint64_t)lds << 8) | ((uint64_t)met_launch << 2) | (ORD ? 2 : 0) | (HIST ? 1 : 0);
+    const int hk = HIST ? (P.kstart ? 2 : 1) : 0;
+    const uint64_t occ_key = ((uint64_t)lds << 8) | ((uint64_t)met_launch << 4) | ((uint64_t)hk << 1) | (ORD ? 1 : 0);
     if (pl.occ_key != occ_key) {
-        pl.occ = std::max(1, collect_occupancy(ORD, HIST, met_launch, lds));
+        pl.occ = std::max(1, collect_occupancy(ORD, hk, met_launch, lds));
         pl.occ_key = occ_key;
     }
     const uint32_t wg_per_cu = (uint32_t)pl.occ;
