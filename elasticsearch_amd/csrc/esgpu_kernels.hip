@@ -1362,3 +1362,252 @@ void launch_topk(const TopkParams& p, hipStream_t s) {
 }
 
 }  // namespace esgpu
+
+// ------------------------------------------------------------------------------------------------------------
+// Multi-valued doc values (SortedSetDocValues / SortedNumericDocValues as CSR: offsets[doc] .. offsets[doc+1]).
+//   GlobalOrdinalsStringTermsAggregator (multi-valued ords, :100-112): every ordinal of the doc is a bucket
+//   HistogramAggregator.collect (:95-117): keys of the doc's sorted values, equal consecutive keys collected once
+//   StatsAggegator / ExtendedStats / Avg collect: count += valueCount, sums[b] += (local sum of the doc's values)
+// One doc per thread; the cells of the doc are the cross product of its ordinals and its deduplicated keys.  The grid
+// lives in LDS when it fits (flushed like the single-valued kernel), else updates go to HBM with global atomics.
+// ------------------------------------------------------------------------------------------------------------
+namespace esgpu {
+
+__device__ __forceinline__ bool bit_at(const uint64_t* bm, uint32_t d) { return (bm[d >> 6] >> (d & 63)) & 1; }
+
+// values [b, e) of doc d in a column (single valued: [d, d+1) when present)
+__device__ __forceinline__ void value_range(const uint64_t* off, const uint64_t* present, uint32_t d, uint64_t& b,
+                                            uint64_t& e) {
+    if (off) {
+        b = off[d];
+        e = off[d + 1];
+    } else {
+        b = d;
+        e = (uint64_t)d + ((present && !bit_at(present, d)) ? 0 : 1);
+    }
+}
+
+__device__ bool pred_doc(const PredDev& q, uint32_t d) {
+    uint64_t b, e;
+    value_range(q.offsets, q.present, d, b, e);
+    for (uint64_t i = b; i < e; ++i) {
+        bool m;
+        if (q.kind == PRED_ORD_EQ) {
+            const uint32_t o = ((const uint32_t*)q.col)[i];
+            m = o != kMissingOrd && (int64_t)o == q.lo;
+        } else if (q.kind == PRED_F64_RANGE) {
+            const double v = ((const double*)q.col)[i];
+            m = (q.lo_incl ? v >= q.dlo : v > q.dlo) && (q.hi_incl ? v <= q.dhi : v < q.dhi);
+        } else {
+            const int64_t v = ((const int64_t*)q.col)[i];
+            m = v >= q.lo && v <= q.hi;
+        }
+        if (m) return true;
+    }
+    return false;
+}
+
+template <bool ORD, int HK, int MET>
+__global__ __launch_bounds__(kWG) void collect_multi_kernel(CollectParams P) {
+    constexpr bool HIST = HK != 0;
+    constexpr bool KT = HK == 2;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t T = ORD ? P.T : 1u;
+    const uint32_t H = HIST ? P.H : 1u;
+    const uint32_t C = T * H;
+    Acc g;
+    g.cnt32 = nullptr; g.vcnt32 = nullptr; g.ocnt32 = nullptr;
+    g.cnt64 = P.g_cnt; g.vcnt64 = P.g_vcnt; g.sum = P.g_sum; g.mn = P.g_min; g.mx = P.g_max; g.sq = P.g_sq;
+    g.ocnt64 = P.g_ocnt;
+    Acc s;
+    {
+        size_t off = 0;
+        auto carve = [&](size_t bytes) { unsigned char* p = smem + off; off += (bytes + 15) & ~(size_t)15; return p; };
+        s.cnt64 = nullptr; s.vcnt64 = nullptr; s.ocnt64 = nullptr;
+        s.cnt32 = (uint32_t*)carve(sizeof(uint32_t) * C);
+        s.vcnt32 = (uint32_t*)carve(P.vcnt_mode ? sizeof(uint32_t) * C : 0);
+        s.sum = (double*)carve(MET > 0 ? sizeof(double) * C : 0);
+        s.mn = (unsigned long long*)carve(MET >= 2 ? 8 * C : 0);
+        s.mx = (unsigned long long*)carve(MET >= 2 ? 8 * C : 0);
+        s.sq = (double*)carve(MET >= 3 ? sizeof(double) * C : 0);
+        s.ocnt32 = (uint32_t*)carve(P.ocnt_mode == OCNT_TERMS ? sizeof(uint32_t) * T : P.ocnt_mode == OCNT_HIST ? sizeof(uint32_t) * H : 0);
+    }
+    if (P.lds_mode) {
+        for (uint32_t c = threadIdx.x; c < C; c += kWG) {
+            s.cnt32[c] = 0;
+            if (P.vcnt_mode) s.vcnt32[c] = 0;
+            if (MET > 0) s.sum[c] = 0.0;
+            if (MET >= 2) { s.mn[c] = kMinInit; s.mx[c] = kMaxInit; }
+            if (MET >= 3) s.sq[c] = 0.0;
+        }
+        if (P.ocnt_mode == OCNT_TERMS || P.ocnt_mode == OCNT_HIST)
+            for (uint32_t c = threadIdx.x; c < (P.ocnt_mode == OCNT_TERMS ? T : H); c += kWG) s.ocnt32[c] = 0;
+        __syncthreads();
+    }
+    for (uint32_t d = blockIdx.x * kWG + threadIdx.x; d < P.n_docs; d += gridDim.x * kWG) {
+        if (P.accept && !bit_at(P.accept, d)) continue;
+        // the doc's metric values, aggregated once (StatsAggegator.collect: local sum, then sums[b] += sum)
+        uint32_t nm = 0;
+        double msum = 0.0, msq = 0.0;
+        unsigned long long emn = kMinInit, emx = kMaxInit;
+        if (MET > 0) {
+            uint64_t b, e;
+            value_range(P.mv_off, P.mv_present, d, b, e);
+            for (uint64_t i = b; i < e; ++i) {
+                const double x = P.mv_f64 ? ((const double*)P.mv)[i] : (double)((const int64_t*)P.mv)[i];
+                msum += x;
+                if (MET >= 3) msq += x * x;
+                if (MET >= 2) {
+                    const bool nan = x != x;
+                    const unsigned long long en = sortable(x);
+                    const unsigned long long a = nan ? 0ull : en, z = nan ? ~0ull : en;
+                    emn = a < emn ? a : emn;
+                    emx = z > emx ? z : emx;
+                }
+                ++nm;
+            }
+        }
+        uint64_t ob = 0, oe = 1, hb = 0, he = 1;
+        if (ORD) value_range(P.ord_off, nullptr, d, ob, oe);
+        if (HIST) value_range(P.hv_off, P.hv_present, d, hb, he);
+        if (HIST && P.ocnt_mode == OCNT_HIST) {  // outer histogram doc counts: once per distinct key
+            bool first = true;
+            int64_t prev = 0;
+            for (uint64_t h = hb; h < he; ++h) {
+                const int64_t k = key_index<KT>(P, ((const int64_t*)P.hv)[h]);
+                if (!first && k == prev) continue;
+                first = false;
+                prev = k;
+                if (k < 0 || k >= (int64_t)H) continue;
+                if (P.lds_mode) atomicAdd(&s.ocnt32[k], 1u); else atomicAdd(&g.ocnt64[k], 1ull);
+            }
+        }
+        for (uint64_t o = ob; o < oe; ++o) {
+            const uint32_t t = ORD ? P.ord[o] : 0u;
+            if (ORD && (t == kMissingOrd || t >= T)) continue;
+            if (ORD && P.ocnt_mode == OCNT_TERMS) {
+                if (P.lds_mode) atomicAdd(&s.ocnt32[t], 1u); else atomicAdd(&g.ocnt64[t], 1ull);
+            }
+            bool first = true;
+            int64_t prev = 0;
+            for (uint64_t h = hb; h < he; ++h) {
+                uint32_t slot = 0;
+                if (HIST) {
+                    const int64_t k = key_index<KT>(P, ((const int64_t*)P.hv)[h]);
+                    if (!first && k == prev) continue;
+                    first = false;
+                    prev = k;
+                    if (k < 0 || k >= (int64_t)H) continue;
+                    slot = (uint32_t)k;
+                }
+                const uint32_t c = slot * T + t;
+                const Acc& a = P.lds_mode ? s : g;
+                if (P.lds_mode) atomicAdd(&s.cnt32[c], 1u); else atomicAdd(&g.cnt64[c], 1ull);
+                if (MET > 0 && nm) {
+                    if (P.vcnt_mode) {
+                        if (P.lds_mode) atomicAdd(&s.vcnt32[c], nm); else atomicAdd(&g.vcnt64[c], (unsigned long long)nm);
+                    }
+                    atomicAdd(&a.sum[c], msum);
+                    if (MET >= 2) {
+                        if (emn < a.mn[c]) atomicMin(&a.mn[c], emn);
+                        if (emx > a.mx[c]) atomicMax(&a.mx[c], emx);
+                    }
+                    if (MET >= 3) atomicAdd(&a.sq[c], msq);
+                }
+            }
+        }
+    }
+    if (P.lds_mode) flush_window<MET>(P, s, T, H, 0);
+}
+
+template <bool ORD, int HK, int MET>
+static void launch_multi_t(const CollectParams& p, uint32_t grid, size_t lds, hipStream_t st) {
+    hipLaunchKernelGGL((collect_multi_kernel<ORD, HK, MET>), dim3(grid), dim3(kWG), lds, st, p);
+}
+template <bool ORD, int HK>
+static void launch_multi_m(const CollectParams& p, int met, uint32_t grid, size_t lds, hipStream_t st) {
+    switch (met) {
+        case 0: launch_multi_t<ORD, HK, 0>(p, grid, lds, st); break;
+        case 1: launch_multi_t<ORD, HK, 1>(p, grid, lds, st); break;
+        case 2: launch_multi_t<ORD, HK, 2>(p, grid, lds, st); break;
+        default: launch_multi_t<ORD, HK, 3>(p, grid, lds, st); break;
+    }
+}
+void launch_collect_multi(const CollectParams& p, bool ord, bool hist, int met, uint32_t grid, size_t lds, hipStream_t st) {
+    const int hk = hist ? (p.kstart ? 2 : 1) : 0;
+    if (ord) {
+        if (hk == 2) launch_multi_m<true, 2>(p, met, grid, lds, st);
+        else if (hk == 1) launch_multi_m<true, 1>(p, met, grid, lds, st);
+        else launch_multi_m<true, 0>(p, met, grid, lds, st);
+    } else {
+        if (hk == 2) launch_multi_m<false, 2>(p, met, grid, lds, st);
+        else if (hk == 1) launch_multi_m<false, 1>(p, met, grid, lds, st);
+        else launch_multi_m<false, 0>(p, met, grid, lds, st);
+    }
+}
+
+struct FilterBitsArgs {
+    uint32_t n_docs;
+    int32_t npred;
+    const uint64_t* accept;
+    uint64_t* out;
+    PredDev pred[4];
+};
+// one thread per 64-doc word: no atomics
+__global__ __launch_bounds__(256) void filter_bits_kernel(FilterBitsArgs A) {
+    const uint32_t nw = (A.n_docs + 63) / 64;
+    for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += gridDim.x * blockDim.x) {
+        uint64_t bits = A.accept ? A.accept[w] : ~0ull;
+        const uint32_t d0 = w * 64;
+        if (d0 + 64 > A.n_docs) bits &= (1ull << (A.n_docs - d0)) - 1ull;
+        for (int j = 0; j < 64; ++j) {
+            if (!((bits >> j) & 1)) continue;
+            for (int k = 0; k < A.npred; ++k)
+                if (!pred_doc(A.pred[k], d0 + j)) { bits &= ~(1ull << j); break; }
+        }
+        A.out[w] = bits;
+    }
+}
+void launch_filter_bits(uint32_t n_docs, const uint64_t* accept, const PredDev* preds, int npred, uint64_t* out,
+                        hipStream_t st) {
+    FilterBitsArgs A{};
+    A.n_docs = n_docs;
+    A.npred = npred;
+    A.accept = accept;
+    A.out = out;
+    for (int k = 0; k < npred && k < 4; ++k) A.pred[k] = preds[k];
+    const uint32_t nw = (n_docs + 63) / 64;
+    if (nw == 0) return;
+    hipLaunchKernelGGL(filter_bits_kernel, dim3(std::min<uint32_t>(4096, (nw + 255) / 256)), dim3(256), 0, st, A);
+}
+
+__global__ __launch_bounds__(256) void expand_bits_kernel(uint32_t n_docs, const uint64_t* doc_bits, const uint64_t* off,
+                                                         uint64_t* out) {
+    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < n_docs; d += gridDim.x * blockDim.x) {
+        if (!bit_at(doc_bits, d)) continue;
+        for (uint64_t i = off[d]; i < off[d + 1]; ++i) atomicOr(&out[i >> 6], 1ull << (i & 63));
+    }
+}
+void launch_expand_bits(uint32_t n_docs, const uint64_t* doc_bits, const uint64_t* offsets, uint64_t n_values,
+                        uint64_t* out, hipStream_t st) {
+    (void)hipMemsetAsync(out, 0, (n_values + 63) / 64 * 8, st);
+    if (n_docs == 0) return;
+    hipLaunchKernelGGL(expand_bits_kernel, dim3(std::min<uint32_t>(4096, (n_docs + 255) / 256)), dim3(256), 0, st, n_docs,
+                       doc_bits, offsets, out);
+}
+
+__global__ __launch_bounds__(256) void minmax_i64_kernel(const int64_t* v, uint64_t n, int64_t* out) {
+    int64_t mn = INT64_MAX, mx = INT64_MIN;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        mn = v[i] < mn ? v[i] : mn;
+        mx = v[i] > mx ? v[i] : mx;
+    }
+    atomicMin((long long*)&out[0], (long long)mn);
+    atomicMax((long long*)&out[1], (long long)mx);
+}
+void launch_minmax_i64(const int64_t* v, uint64_t n, int64_t* out, hipStream_t st) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(minmax_i64_kernel, dim3((uint32_t)std::min<uint64_t>(1024, (n + 255) / 256)), dim3(256), 0, st, v, n, out);
+}
+
+}  // namespace esgpu

@@ -31,6 +31,7 @@ enum PredKind : int32_t { PRED_ORD_EQ = 0, PRED_I64_RANGE = 1, PRED_F64_RANGE = 
 struct PredDev {
     const void* col;
     const uint64_t* present;
+    const uint64_t* offsets;   // multi-valued column: CSR offsets [n_docs + 1] (doc matches if any value matches)
     int32_t kind;
     int32_t lo_incl, hi_incl, pad;
     int64_t lo, hi;    // ORD_EQ: lo = ordinal; I64_RANGE: inclusive [lo, hi]
@@ -70,6 +71,10 @@ struct CollectParams {
     int32_t npred;
     PredDev pred[4];
     const uint64_t* accept;
+    // multi-valued columns (collect_multi_kernel): CSR offsets [n_docs + 1], null = single valued
+    const uint64_t* ord_off;
+    const uint64_t* hv_off;
+    const uint64_t* mv_off;
     // global cell grid [H][T]
     unsigned long long* g_cnt;
     unsigned long long* g_ocnt;
@@ -116,6 +121,19 @@ void launch_collect(const CollectParams& p, bool ord, bool hist, int met, uint32
 size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode);
 int collect_occupancy(bool ord, int hk, int met, size_t lds);  // resident workgroups per CU (hk: 0 none, 1 affine, 2 table)
 void launch_hll(const HllParams& p, uint32_t cus, hipStream_t s);
+
+// ---- multi-valued (CSR) columns, esgpu_kernels_multi.hip ----
+// K1/K4/K5/K6/K7 for SortedSet / SortedNumeric doc values: one doc per thread, every (ordinal x deduplicated key)
+// pair of the doc is a cell update, metrics aggregate all of the doc's values once (StatsAggegator's local sum).
+void launch_collect_multi(const CollectParams& p, bool ord, bool hist, int met, uint32_t grid, size_t lds, hipStream_t s);
+// doc bitset of (accept AND every predicate); multi-valued predicate columns match if any value matches
+void launch_filter_bits(uint32_t n_docs, const uint64_t* accept, const PredDev* preds, int npred, uint64_t* out,
+                        hipStream_t s);
+// per-value bitset from a doc bitset over a CSR column (out zeroed by the launcher, words for n_values)
+void launch_expand_bits(uint32_t n_docs, const uint64_t* doc_bits, const uint64_t* offsets, uint64_t n_values,
+                        uint64_t* out, hipStream_t s);
+// min / max over a value array (multi-valued i64 columns: key range of a histogram), out[0] = min, out[1] = max
+void launch_minmax_i64(const int64_t* v, uint64_t n, int64_t* out, hipStream_t s);
 void launch_remap_ords(const uint32_t* in, uint32_t n, const uint32_t* map, uint32_t map_n, uint32_t* out, hipStream_t s);
 void launch_pack_u8(const unsigned int* src, uint32_t n, uint8_t* dst, hipStream_t s);
 void launch_term_totals(const unsigned long long* cnt, uint32_t H, uint32_t T, unsigned long long* out, hipStream_t s);

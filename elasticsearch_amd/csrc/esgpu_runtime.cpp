@@ -285,6 +285,8 @@ struct DevColumn {
     bool multi = false;
     DevBuf values;   // padded to a multiple of kBlockDocs entries
     DevBuf present;  // optional
+    DevBuf offsets;  // multi-valued: CSR offsets [max_doc + 1] (values hold n_values entries, padded)
+    uint64_t n_values = 0;
     DevBuf zmin, zmax;
     int64_t vmin = INT64_MAX, vmax = INT64_MIN;  // over present values (I64 columns)
     uint64_t value_count = 0;
@@ -366,12 +368,33 @@ extern "C" int esgpu_segment_upload(esgpu_ctx* c, const esgpu_column_desc* cols,
             col->value_count = d.value_count;
             const size_t w = d.type == ESGPU_COL_ORD_U32 ? 4 : 8;
             if (d.offsets) {
-                // multi-valued (SortedNumeric / SortedSet): kept host-free on device as CSR; the gfx950 collect
-                // kernels handle single-valued columns only in this version (plans over it are UNSUPPORTED).
+                // multi-valued (SortedNumeric / SortedSet): CSR on the device, values padded like a doc column
                 col->multi = true;
+                require(d.offsets[0] == 0, ESGPU_ERR_INVALID, "CSR offsets must start at 0");
+                for (uint32_t k = 0; k < max_doc; ++k)
+                    require(d.offsets[k] <= d.offsets[k + 1], ESGPU_ERR_INVALID, "CSR offsets must be non-decreasing");
                 const uint64_t nv = d.offsets[max_doc];
-                col->values.alloc(c, std::max<uint64_t>(nv, 1) * w);
+                require(nv < 0xFFFFFFFFull - kBlockDocs, ESGPU_ERR_UNSUPPORTED, "more than 2^32 values in one segment");
+                col->n_values = nv;
+                const uint64_t nv_pad = pad_docs((uint32_t)nv);
+                col->values.alloc(c, std::max<uint64_t>(nv_pad, kBlockDocs) * w);
+                HIPX(hipMemsetAsync(col->values.p, d.type == ESGPU_COL_ORD_U32 ? 0xFF : 0, col->values.bytes, c->stream));
                 if (nv) HIPX(hipMemcpyAsync(col->values.p, d.values, nv * w, hipMemcpyHostToDevice, c->stream));
+                col->offsets.alloc(c, ((size_t)max_doc + 1) * 8);
+                HIPX(hipMemcpyAsync(col->offsets.p, d.offsets, ((size_t)max_doc + 1) * 8, hipMemcpyHostToDevice, c->stream));
+                if (d.type == ESGPU_COL_I64 && nv) {  // key range of a histogram over the field
+                    DevBuf mm;
+                    mm.alloc(c, 16);
+                    const int64_t init[2] = {INT64_MAX, INT64_MIN};
+                    HIPX(hipMemcpyAsync(mm.p, init, 16, hipMemcpyHostToDevice, c->stream));
+                    launch_minmax_i64(col->values.as<int64_t>(), nv, mm.as<int64_t>(), c->stream);
+                    HIPX(hipGetLastError());
+                    int64_t r[2];
+                    HIPX(hipMemcpyAsync(r, mm.p, 16, hipMemcpyDeviceToHost, c->stream));
+                    HIPX(hipStreamSynchronize(c->stream));
+                    col->vmin = r[0];
+                    col->vmax = r[1];
+                }
             } else {
                 col->values.alloc(c, (size_t)s->n_pad * w);
                 if (max_doc) HIPX(hipMemcpyAsync(col->values.p, d.values, (size_t)max_doc * w, hipMemcpyHostToDevice, c->stream));
@@ -515,7 +538,7 @@ extern "C" int esgpu_ordinal_map_build(esgpu_ctx* ctx, esgpu_segment* const* seg
             auto it = segs[i]->cols.find(field);
             if (it == segs[i]->cols.end()) { cols.push_back(nullptr); continue; }  // unmapped in this segment
             DevColumn* c = it->second.get();
-            require(c->type == ESGPU_COL_ORD_U32 && !c->multi, ESGPU_ERR_UNSUPPORTED, "ordinal maps cover single-valued keyword columns");
+            require(c->type == ESGPU_COL_ORD_U32, ESGPU_ERR_INVALID, "ordinal maps cover keyword columns");
             require(c->synth_bit || c->dict_offsets.size() == c->value_count + 1, ESGPU_ERR_INVALID,
                     std::string("no term dictionary for ") + field);
             cols.push_back(c);
@@ -778,6 +801,7 @@ struct esgpu_plan {
     // per-request scratch, reused across requests
     Scratch s_accept, s_tcnt, s_rows, s_dst[6];
     Scratch s_wgc, s_pbeg, s_pbuf, s_tiles, s_cand, s_keys, s_hist;  // partitioned counting + GPU top-k
+    Scratch s_fbits, s_vbits;  // doc bitset of multi-valued filters, per-value bitset of a multi-valued HLL field
     PinnedBuf h_keys;
     hipEvent_t ev_mid = nullptr;
     PinnedBuf h_tcnt, h_rows, h_dst[6];
@@ -1023,9 +1047,9 @@ static void set_preds(esgpu_plan* p, const esgpu_segment* s, PredDev* out, int32
         const DevColumn* col = s->col(p->filter_fields[k].c_str());
         PredDev q{};
         require(col != nullptr, ESGPU_ERR_UNSUPPORTED, "filter on a field missing from the segment");
-        require(!col->multi, ESGPU_ERR_UNSUPPORTED, "filters on multi-valued fields run on the CPU path");
         q.col = col->type == ESGPU_COL_ORD_U32 ? col->ords().p : col->values.p;  // keyword terms: global ordinal
         q.present = col->present.as<uint64_t>();
+        q.offsets = col->multi ? col->offsets.as<uint64_t>() : nullptr;
         if (col->type == ESGPU_COL_ORD_U32) {
             require(f.type == ESGPU_FILTER_TERM, ESGPU_ERR_UNSUPPORTED, "range filters on keyword fields run on the CPU path");
             q.kind = PRED_ORD_EQ;
@@ -1109,6 +1133,49 @@ static bool collect_partitioned(esgpu_plan* p, Pipeline& pl, const esgpu_segment
     return true;
 }
 
+// algorithmic bytes of one referenced column over a segment: natural width per value, plus the CSR
+// offsets (8 B per doc) of a multi-valued column
+static uint64_t column_bytes(const DevColumn* c, uint32_t max_doc) {
+    if (!c) return 0;
+    const uint64_t w = c->type == ESGPU_COL_ORD_U32 ? 4 : 8;
+    return c->multi ? w * c->n_values + 8ull * max_doc : w * max_doc;
+}
+
+// K1/K4-K7 over multi-valued columns: collect_multi_kernel (one doc per thread, CSR), filters folded into a doc bitset
+static bool collect_multi(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, CollectParams& P, const DevColumn* oc,
+                          const DevColumn* hc, const DevColumn* mc, int met_launch, const uint64_t* d_accept) {
+    esgpu_ctx* c = p->ctx;
+    const bool ORD = oc != nullptr, HIST = hc != nullptr;
+    uint64_t bytes = column_bytes(oc, s->max_doc) + column_bytes(hc, s->max_doc) + column_bytes(mc, s->max_doc);
+    if (d_accept) bytes += ((uint64_t)s->max_doc + 7) / 8;
+    for (const std::string& f : p->filter_fields) bytes += column_bytes(s->col(f.c_str()), s->max_doc);
+    HIPX(hipEventRecord(pl.e0, p->stream));
+    if (P.npred > 0) {
+        uint64_t* bits = (uint64_t*)p->s_fbits.ensure(c, std::max<size_t>(s->n_pad / 64, 1) * 8);
+        launch_filter_bits(s->max_doc, d_accept, P.pred, P.npred, bits, p->stream);
+        HIPX(hipGetLastError());
+        P.accept = bits;
+        P.npred = 0;
+    }
+    P.ord_off = (oc && oc->multi) ? oc->offsets.as<uint64_t>() : nullptr;
+    P.hv_off = (hc && hc->multi) ? hc->offsets.as<uint64_t>() : nullptr;
+    P.mv_off = (mc && mc->multi) ? mc->offsets.as<uint64_t>() : nullptr;
+    if (P.ocnt_mode == OCNT_TERMS_DERIVED) P.ocnt_mode = OCNT_TERMS;  // outer counts per doc, never from the cells
+    P.W = pl.H;
+    P.windowed = 0;
+    size_t lds = collect_lds_bytes(pl.T, pl.H, met_launch, pl.vcnt_mode, P.ocnt_mode);
+    P.lds_mode = lds <= 64 * 1024 ? 1 : 0;
+    if (!P.lds_mode) lds = 0;
+    const uint32_t want = (s->max_doc + 511) / 512;
+    const uint32_t grid = std::max(1u, std::min(want, (uint32_t)c->cus * 4));
+    launch_collect_multi(P, ORD, HIST, met_launch, grid, lds, p->stream);
+    HIPX(hipGetLastError());
+    HIPX(hipEventRecord(pl.e1, p->stream));
+    p->last_bytes += bytes;
+    p->last_path = 5;
+    return true;
+}
+
 static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
     const bool ORD = pl.term_spec >= 0, HIST = pl.hist_spec >= 0;
     const DevColumn* oc = ORD ? s->col(pl.ord_field.c_str()) : nullptr;
@@ -1116,17 +1183,14 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
     const DevColumn* mc = pl.met > 0 ? s->col(pl.metric_field.c_str()) : nullptr;
     // unmapped fields: a bucket aggregation over a missing field collects nothing (ValuesSource null)
     if ((ORD && !oc) || (HIST && !hc)) return false;
-    if (oc) {
-        require(oc->type == ESGPU_COL_ORD_U32, ESGPU_ERR_UNSUPPORTED, "terms on numeric fields run on the CPU path");
-        require(!oc->multi, ESGPU_ERR_UNSUPPORTED, "multi-valued keyword fields run on the CPU path");
-    }
-    if (hc) {
-        require(hc->type == ESGPU_COL_I64, ESGPU_ERR_UNSUPPORTED, "histogram over non-long fields runs on the CPU path");
-        require(!hc->multi, ESGPU_ERR_UNSUPPORTED, "multi-valued numeric fields run on the CPU path");
-    }
-    if (mc) {
-        require(mc->type == ESGPU_COL_I64 || mc->type == ESGPU_COL_F64, ESGPU_ERR_UNSUPPORTED, "metric over non-numeric field");
-        require(!mc->multi, ESGPU_ERR_UNSUPPORTED, "multi-valued numeric fields run on the CPU path");
+    if (oc) require(oc->type == ESGPU_COL_ORD_U32, ESGPU_ERR_UNSUPPORTED, "terms on numeric fields run on the CPU path");
+    if (hc) require(hc->type == ESGPU_COL_I64, ESGPU_ERR_UNSUPPORTED, "histogram over non-long fields runs on the CPU path");
+    if (mc) require(mc->type == ESGPU_COL_I64 || mc->type == ESGPU_COL_F64, ESGPU_ERR_UNSUPPORTED, "metric over non-numeric field");
+    // any multi-valued column (aggregated field or filter field) takes the CSR kernel
+    bool multi = (oc && oc->multi) || (hc && hc->multi) || (mc && mc->multi);
+    for (const std::string& f : p->filter_fields) {
+        const DevColumn* fc = s->col(f.c_str());
+        if (fc && fc->multi) multi = true;
     }
     // an unmapped metric field collects nothing (ValuesSource null => NO_OP collector); counts stay separate
     const int met_launch = mc ? pl.met : 0;
@@ -1153,11 +1217,12 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
         require(!HIST || !has_keys || kmax - kmin + 1 <= 64 * 1024 * 1024, ESGPU_ERR_UNSUPPORTED,
                 "histogram key range too large for a dense grid");
         require((uint64_t)pl.T * pl.H <= (1ull << 31), ESGPU_ERR_UNSUPPORTED, "bucket grid too large");
-        pl.vcnt_mode = (pl.met > 0 && (!mc || mc->present.p)) ? 1 : 0;
+        pl.vcnt_mode = (pl.met > 0 && (!mc || mc->present.p || mc->multi)) ? 1 : 0;
         pl.value_count = ORD ? oc->ord_count() : 1;
         if (ORD && HIST) {
             const bool terms_outer = pl.outer == pl.term_spec;
-            const bool inner_sparse = terms_outer ? (hc->present.p != nullptr) : true;  // ords may be missing
+            // ords may be missing; a doc may have several keys: the outer counts cannot be summed from the cells
+            const bool inner_sparse = terms_outer ? (hc->present.p != nullptr || hc->multi) : true;
             if (inner_sparse) pl.ocnt_mode = terms_outer ? OCNT_TERMS : OCNT_HIST;
             else pl.ocnt_mode = OCNT_TERMS_DERIVED;
         }
@@ -1170,8 +1235,10 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
             if (!pl.ktable) grow_keys(p, pl, kmin, kmax);
             else if ((uint32_t)pl.kt_key.size() != H_before || table_shift != 0) regrid(p, pl, (uint32_t)pl.kt_key.size(), table_shift);
         }
-        if (pl.met > 0 && (!mc || mc->present.p) && !pl.vcnt_mode)
+        if (pl.met > 0 && (!mc || mc->present.p || mc->multi) && !pl.vcnt_mode)
             throw EsError(ESGPU_ERR_UNSUPPORTED, "metric field sparsity changed across segments");
+        if (ORD && HIST && pl.outer == pl.term_spec && hc->multi && pl.ocnt_mode == OCNT_NONE)
+            throw EsError(ESGPU_ERR_UNSUPPORTED, "histogram field became multi-valued across segments");
     }
     // ---- launch configuration ----
     CollectParams P{};
@@ -1206,6 +1273,7 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
     P.g_min = pl.g_min.as<unsigned long long>();
     P.g_max = pl.g_max.as<unsigned long long>();
     P.g_sq = pl.g_sq.as<double>();
+    if (multi) return collect_multi(p, pl, s, P, oc, hc, mc, met_launch, d_accept);
 
     // LDS sizing: the whole grid if it fits, else a sliding window over the key dimension (time-sorted data)
     const size_t kLdsPair = 64 * 1024, kLdsMax = 150 * 1024;
@@ -1279,7 +1347,6 @@ static void ensure_ord_hash(esgpu_ctx* c, const DevColumn* col, hipStream_t st) 
 static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
     const DevColumn* col = s->col(pl.metric_field.c_str());
     if (!col) return false;
-    require(!col->multi, ESGPU_ERR_UNSUPPORTED, "multi-valued fields run on the CPU path");
     if (!pl.allocated) {
         const uint32_t m = 1u << pl.p;
         pl.regs.alloc(p->ctx, (size_t)m * 4);
@@ -1310,6 +1377,34 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
         H.kind = col->type == ESGPU_COL_F64 ? HLL_F64 : HLL_I64;
     }
     set_preds(p, s, H.pred, &H.npred, &bytes_per_doc);
+    bool multi_pred = false;
+    for (int k = 0; k < H.npred; ++k) multi_pred |= H.pred[k].offsets != nullptr;
+    uint64_t bytes = bytes_per_doc * (uint64_t)s->max_doc;
+    if (col->multi || multi_pred) {
+        // MurmurHash3Values iterates every value of an accepted doc: fold accept + filters into a doc bitset, then
+        // (multi-valued field) expand it to a per-value bitset and run the register passes over the value array
+        bytes = column_bytes(col, s->max_doc) + (d_accept ? ((uint64_t)s->max_doc + 7) / 8 : 0);
+        for (const std::string& f : p->filter_fields) bytes += column_bytes(s->col(f.c_str()), s->max_doc);
+        const uint64_t* doc_bits = d_accept;
+        if (H.npred > 0) {
+            uint64_t* b = (uint64_t*)p->s_fbits.ensure(p->ctx, std::max<size_t>(s->n_pad / 64, 1) * 8);
+            launch_filter_bits(s->max_doc, d_accept, H.pred, H.npred, b, p->stream);
+            HIPX(hipGetLastError());
+            doc_bits = b;
+            H.npred = 0;
+        }
+        H.accept = doc_bits;
+        if (col->multi) {
+            H.n_docs = (uint32_t)col->n_values;
+            H.present = nullptr;
+            if (doc_bits) {
+                uint64_t* vb = (uint64_t*)p->s_vbits.ensure(p->ctx, (col->values.bytes / (col->type == ESGPU_COL_ORD_U32 ? 4 : 8) + 63) / 64 * 8);
+                launch_expand_bits(s->max_doc, doc_bits, col->offsets.as<uint64_t>(), col->n_values, vb, p->stream);
+                HIPX(hipGetLastError());
+                H.accept = vb;
+            }
+        }
+    }
     H.regs = pl.regs.as<unsigned int>();
     H.lc_set = pl.lc_set.as<unsigned int>();
     H.lc_count = pl.lc_count.as<unsigned int>();
@@ -1322,7 +1417,7 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
     launch_hll(H, (uint32_t)p->ctx->cus, p->stream);
     HIPX(hipGetLastError());
     HIPX(hipEventRecord(pl.e1, p->stream));
-    p->last_bytes += bytes_per_doc * (uint64_t)s->max_doc;
+    p->last_bytes += bytes;
     p->last_path = 3;
     return true;
 }
