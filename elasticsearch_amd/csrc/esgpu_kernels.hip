@@ -1596,6 +1596,143 @@ void launch_expand_bits(uint32_t n_docs, const uint64_t* doc_bits, const uint64_
                        doc_bits, offsets, out);
 }
 
+// ---- cardinality per bucket ----
+__device__ __forceinline__ void reg_max_u8(uint8_t* regs, size_t idx, uint32_t rl) {
+    uint32_t* w = (uint32_t*)(regs + (idx & ~(size_t)3));
+    const int sh = (int)(idx & 3) * 8;
+    uint32_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (((old >> sh) & 0xFFu) < rl) {
+        const uint32_t nw = (old & ~(0xFFu << sh)) | (rl << sh);
+        const uint32_t prev = atomicCAS(w, old, nw);
+        if (prev == old) break;
+        old = prev;
+    }
+}
+
+__device__ __forceinline__ bool card_hash(const CardParams& C, uint64_t i, uint64_t& h) {
+    if (C.kind == HLL_ORD) {
+        const uint32_t o = ((const uint32_t*)C.col)[i];
+        if (o == kMissingOrd || o >= C.n_ords) return false;
+        h = C.ord_hash[o];
+        return true;
+    }
+    uint64_t bits = ((const uint64_t*)C.col)[i];
+    if (C.kind == HLL_F64) {  // MurmurHash3Values.Double: doubleToLongBits (canonical NaN)
+        const double x = bits_dbl(bits);
+        if (x != x) bits = 0x7ff8000000000000ULL;
+    }
+    h = mix64(bits);
+    return true;
+}
+
+template <bool ORD, int HK>
+__global__ __launch_bounds__(256) void card_kernel(CardParams C, int pass) {
+    constexpr bool HIST = HK != 0;
+    constexpr bool KT = HK == 2;
+    const CollectParams& P = C.G;
+    const uint32_t T = ORD ? P.T : 1u;
+    const uint32_t H = HIST ? P.H : 1u;
+    const uint32_t m = 1u << C.p;
+    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < P.n_docs; d += gridDim.x * blockDim.x) {
+        if (P.accept && !bit_at(P.accept, d)) continue;
+        uint64_t vb, ve;
+        value_range(C.off, C.present, d, vb, ve);
+        if (vb == ve) continue;
+        uint64_t ob = 0, oe = 1, hb = 0, he = 1;
+        if (ORD) value_range(P.ord_off, nullptr, d, ob, oe);
+        if (HIST) value_range(P.hv_off, P.hv_present, d, hb, he);
+        for (uint64_t o = ob; o < oe; ++o) {
+            const uint32_t t = ORD ? P.ord[o] : 0u;
+            if (ORD && (t == kMissingOrd || t >= T)) continue;
+            bool first = true;
+            int64_t prev = 0;
+            for (uint64_t hh = hb; hh < he; ++hh) {
+                uint32_t slot = 0;
+                if (HIST) {
+                    const int64_t k = key_index<KT>(P, ((const int64_t*)P.hv)[hh]);
+                    if (!first && k == prev) continue;
+                    first = false;
+                    prev = k;
+                    if (k < 0 || k >= (int64_t)H) continue;
+                    slot = (uint32_t)k;
+                }
+                const size_t b = (size_t)slot * T + t;
+                if (pass == 1 && (C.nonzero[b] > C.thr ||
+                                  __hip_atomic_load(&C.set_cnt[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > C.thr))
+                    continue;  // this bucket already ends in HYPERLOGLOG
+                for (uint64_t i = vb; i < ve; ++i) {
+                    uint64_t h;
+                    if (!card_hash(C, i, h)) continue;
+                    if (pass == 0) {
+                        reg_max_u8(C.regs, b * m + hll_index(h, C.p), hll_run_len(h, C.p));
+                        continue;
+                    }
+                    const uint32_t enc = hll_encode(h, C.p);
+                    uint32_t* set = C.sets + b * C.cap;
+                    uint32_t sl = (uint32_t)(mix64(enc) & (C.cap - 1));
+                    uint32_t probe = 0;
+                    for (; probe < C.cap; ++probe) {
+                        const uint32_t cur = __hip_atomic_load(&set[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (cur == enc) break;
+                        if (cur == 0) {
+                            const uint32_t was = atomicCAS(&set[sl], 0u, enc);
+                            if (was == 0) { atomicAdd(&C.set_cnt[b], 1u); break; }
+                            if (was == enc) break;
+                        }
+                        sl = (sl + 1) & (C.cap - 1);
+                    }
+                    if (probe == C.cap) atomicAdd(&C.set_cnt[b], C.cap);  // full: more than cap distinct hashes
+                }
+            }
+        }
+    }
+}
+
+void launch_card(const CardParams& c, bool ord, bool hist, int pass, uint32_t grid, hipStream_t st) {
+    const int hk = hist ? (c.G.kstart ? 2 : 1) : 0;
+    if (ord) {
+        if (hk == 2) hipLaunchKernelGGL((card_kernel<true, 2>), dim3(grid), dim3(256), 0, st, c, pass);
+        else if (hk == 1) hipLaunchKernelGGL((card_kernel<true, 1>), dim3(grid), dim3(256), 0, st, c, pass);
+        else hipLaunchKernelGGL((card_kernel<true, 0>), dim3(grid), dim3(256), 0, st, c, pass);
+    } else {
+        if (hk == 2) hipLaunchKernelGGL((card_kernel<false, 2>), dim3(grid), dim3(256), 0, st, c, pass);
+        else if (hk == 1) hipLaunchKernelGGL((card_kernel<false, 1>), dim3(grid), dim3(256), 0, st, c, pass);
+        else hipLaunchKernelGGL((card_kernel<false, 0>), dim3(grid), dim3(256), 0, st, c, pass);
+    }
+}
+
+__global__ __launch_bounds__(256) void card_nonzero_kernel(const uint32_t* regs, uint64_t n_words, uint32_t words_per_bucket,
+                                                          uint32_t* nonzero) {
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < n_words; w += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t v = regs[w];
+        const uint32_t n = ((v & 0xFFu) != 0) + ((v & 0xFF00u) != 0) + ((v & 0xFF0000u) != 0) + ((v & 0xFF000000u) != 0);
+        if (n) atomicAdd(&nonzero[w / words_per_bucket], n);
+    }
+}
+void launch_card_nonzero(const uint8_t* regs, uint64_t n_buckets, int p, uint32_t* nonzero, hipStream_t st) {
+    (void)hipMemsetAsync(nonzero, 0, n_buckets * 4, st);
+    const uint32_t wpb = (1u << p) / 4;
+    const uint64_t n_words = n_buckets * wpb;
+    if (n_words == 0) return;
+    hipLaunchKernelGGL(card_nonzero_kernel, dim3((uint32_t)std::min<uint64_t>(8192, (n_words + 255) / 256)), dim3(256), 0, st,
+                       (const uint32_t*)regs, n_words, wpb, nonzero);
+}
+
+__global__ __launch_bounds__(256) void gather_bytes_kernel(const uint32_t* cells, uint32_t n, uint32_t row, const uint8_t* src,
+                                                          uint8_t* dst) {
+    const uint32_t wpr = row / 4;  // rows are multiples of 4 bytes
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (uint64_t)n * wpr; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t r = i / wpr, w = i - r * wpr;
+        ((uint32_t*)dst)[i] = ((const uint32_t*)(src + (size_t)cells[r] * row))[w];
+    }
+}
+void launch_gather_bytes(const uint32_t* cells, uint32_t n, uint32_t row_bytes, const uint8_t* src, uint8_t* dst, hipStream_t st) {
+    const uint64_t total = (uint64_t)n * (row_bytes / 4);
+    if (total == 0) return;
+    hipLaunchKernelGGL(gather_bytes_kernel, dim3((uint32_t)std::min<uint64_t>(8192, (total + 255) / 256)), dim3(256), 0, st, cells,
+                       n, row_bytes, src, dst);
+}
+
 __global__ __launch_bounds__(256) void minmax_i64_kernel(const int64_t* v, uint64_t n, int64_t* out) {
     int64_t mn = INT64_MAX, mx = INT64_MIN;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {

@@ -132,6 +132,30 @@ void launch_filter_bits(uint32_t n_docs, const uint64_t* accept, const PredDev* 
 // per-value bitset from a doc bitset over a CSR column (out zeroed by the launcher, words for n_values)
 void launch_expand_bits(uint32_t n_docs, const uint64_t* doc_bits, const uint64_t* offsets, uint64_t n_values,
                         uint64_t* out, hipStream_t s);
+// ---- cardinality under a bucket aggregation (HyperLogLogPlusPlus with one sketch per bucket ordinal) ----
+// The buckets are the cells of the parent grid (cell = key slot * T + ordinal).  Pass 0 raises the u8 run-length
+// registers [B][m]; nonzero counts them per bucket; pass 1 inserts the encoded hashes of the buckets that can still end
+// in LINEAR_COUNTING (nonzero <= threshold) into per-bucket open-addressing sets [B][cap].
+struct CardParams {
+    CollectParams G;             // bucket dimensions: ord / hv columns, key mapping, T, H, accept (filters folded in)
+    const void* col;             // the cardinality field
+    const uint64_t* off;         // CSR offsets (multi-valued) or null
+    const uint64_t* present;
+    int32_t kind;                // HLL_I64 / HLL_F64 / HLL_ORD
+    int32_t p;
+    const uint64_t* ord_hash;    // HLL_ORD: murmur3 h1 per term
+    uint64_t n_ords;
+    uint8_t* regs;               // [B][2^p]
+    uint32_t* sets;              // [B][cap]
+    uint32_t* set_cnt;           // [B]
+    uint32_t* nonzero;           // [B]
+    uint32_t cap, thr;
+};
+void launch_card(const CardParams& c, bool ord, bool hist, int pass, uint32_t grid, hipStream_t s);
+void launch_card_nonzero(const uint8_t* regs, uint64_t n_buckets, int p, uint32_t* nonzero, hipStream_t s);
+// out[i*row ... ] = src[cells[i]*row ...] (bytes), for the cells of the emitted buckets
+void launch_gather_bytes(const uint32_t* cells, uint32_t n, uint32_t row_bytes, const uint8_t* src, uint8_t* dst, hipStream_t s);
+
 // min / max over a value array (multi-valued i64 columns: key range of a histogram), out[0] = min, out[1] = max
 void launch_minmax_i64(const int64_t* v, uint64_t n, int64_t* out, hipStream_t s);
 void launch_remap_ords(const uint32_t* in, uint32_t n, const uint32_t* map, uint32_t map_n, uint32_t* out, hipStream_t s);

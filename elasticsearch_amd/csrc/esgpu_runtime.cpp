@@ -713,6 +713,18 @@ struct SpecNode {
     }
 };
 
+// cardinality under a bucket aggregation: one HyperLogLogPlusPlus sketch per bucket cell of the pipeline's grid
+struct CardState {
+    int spec = -1;
+    int p = 9;
+    std::string field;
+    uint32_t m = 0, cap = 0, thr = 0;
+    DevBuf regs, sets, cnt, nonzero;  // [B][m] u8, [B][cap] u32, [B], [B]
+    // gathered rows of the emitted buckets (build)
+    std::vector<uint8_t> h_regs;
+    std::vector<uint32_t> h_sets, h_cnt, h_nz;
+};
+
 // One top-level aggregation subtree compiled to one kernel pipeline.
 struct Pipeline {
     int root = -1;             // spec index of the top-level aggregation
@@ -720,7 +732,8 @@ struct Pipeline {
     // cell grid shape
     int outer = -1, inner = -1;      // bucket spec indices (inner may be -1)
     int term_spec = -1, hist_spec = -1;
-    std::vector<int> metrics;        // metric specs at the deepest level
+    std::vector<int> metrics;        // leaf specs at the deepest level, in request order (numeric metrics + cardinality)
+    std::vector<CardState> cards;    // cardinality leaves (spec order)
     std::string ord_field, hist_field, metric_field;
     int met = 0;                     // 0 none, 1 avg, 2 stats, 3 extended
     int64_t interval = 1, offset = 0;  // affine roundings: key = floor((v - offset) / interval) * interval + offset
@@ -884,9 +897,9 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
                 std::vector<int> mets, buckets;
                 for (int ch : root.children) {
                     const int t = p->specs[ch].s.type;
-                    if (is_metric(t)) mets.push_back(ch);
+                    if (is_metric(t) || t == ESGPU_AGG_CARDINALITY) mets.push_back(ch);
                     else if (is_bucket(t)) buckets.push_back(ch);
-                    else throw EsError(ESGPU_ERR_UNSUPPORTED, "cardinality under a bucket aggregation runs on the CPU path");
+                    else throw EsError(ESGPU_ERR_UNSUPPORTED, "aggregation type not on the GPU path");
                 }
                 require(buckets.size() <= 1, ESGPU_ERR_UNSUPPORTED, "more than one bucket sub-aggregation");
                 if (!buckets.empty()) {
@@ -894,7 +907,8 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
                     pl.inner = buckets[0];
                     for (int ch : p->specs[pl.inner].children) {
                         const int t = p->specs[ch].s.type;
-                        require(is_metric(t), ESGPU_ERR_UNSUPPORTED, "bucket aggregations nested three levels deep");
+                        require(is_metric(t) || t == ESGPU_AGG_CARDINALITY, ESGPU_ERR_UNSUPPORTED,
+                                "bucket aggregations nested three levels deep");
                         mets.push_back(ch);
                     }
                     const bool ot = p->specs[pl.outer].s.type == ESGPU_AGG_TERMS;
@@ -920,6 +934,18 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
             }
             for (int m : pl.metrics) {
                 const SpecNode& n = p->specs[m];
+                if (n.s.type == ESGPU_AGG_CARDINALITY) {
+                    CardState cs;
+                    cs.spec = m;
+                    cs.p = n.precision;
+                    cs.field = n.field;
+                    cs.m = 1u << cs.p;
+                    cs.thr = (uint32_t)((float)(cs.m / 4) * 0.75f);  // Hashset threshold (HyperLogLogPlusPlus.java:437-440)
+                    cs.cap = 16;
+                    while (cs.cap < 4 * (cs.thr + 1)) cs.cap <<= 1;
+                    pl.cards.push_back(std::move(cs));
+                    continue;
+                }
                 if (pl.metric_field.empty()) pl.metric_field = n.field;
                 require(pl.metric_field == n.field, ESGPU_ERR_UNSUPPORTED, "metrics on different fields at one level");
                 pl.met = std::max(pl.met, metric_level(n.s.type));
@@ -961,6 +987,18 @@ static void alloc_grid(esgpu_plan* p, Pipeline& pl) {
         launch_fill_u64(pl.g_max.as<unsigned long long>(), cells, kMaxInit, p->stream);
     }
     if (pl.met >= 3) { pl.g_sq.alloc(c, cells * 8); HIPX(hipMemsetAsync(pl.g_sq.p, 0, cells * 8, p->stream)); }
+    for (CardState& cs : pl.cards) {
+        require((double)cells * (cs.m + 4.0 * cs.cap) <= 4.0 * (1ull << 30), ESGPU_ERR_UNSUPPORTED,
+                "cardinality sketches for every bucket exceed the 4 GiB per-request budget");
+        cs.regs.alloc(c, cells * cs.m);
+        cs.sets.alloc(c, cells * cs.cap * 4);
+        cs.cnt.alloc(c, cells * 4);
+        cs.nonzero.alloc(c, cells * 4);
+        HIPX(hipMemsetAsync(cs.regs.p, 0, cs.regs.bytes, p->stream));
+        HIPX(hipMemsetAsync(cs.sets.p, 0, cs.sets.bytes, p->stream));
+        HIPX(hipMemsetAsync(cs.cnt.p, 0, cs.cnt.bytes, p->stream));
+        HIPX(hipMemsetAsync(cs.nonzero.p, 0, cs.nonzero.bytes, p->stream));
+    }
     pl.allocated = true;
 }
 
@@ -968,6 +1006,12 @@ static void alloc_grid(esgpu_plan* p, Pipeline& pl) {
 // key-range extension is one copy per array)
 static void regrid(esgpu_plan* p, Pipeline& pl, uint32_t newH, int64_t shift) {
     const uint32_t oldH = pl.H;
+    std::vector<CardState> old_cards(pl.cards.size());
+    for (size_t i = 0; i < pl.cards.size(); ++i) {
+        old_cards[i].regs = std::move(pl.cards[i].regs);
+        old_cards[i].sets = std::move(pl.cards[i].sets);
+        old_cards[i].cnt = std::move(pl.cards[i].cnt);
+    }
     struct { DevBuf g_cnt, g_ocnt, g_vcnt, g_sum, g_min, g_max, g_sq; } old;
     old.g_cnt = std::move(pl.g_cnt);
     old.g_ocnt = std::move(pl.g_ocnt);
@@ -991,6 +1035,12 @@ static void regrid(esgpu_plan* p, Pipeline& pl, uint32_t newH, int64_t shift) {
     if (pl.ocnt_mode == OCNT_HIST) cp(pl.g_ocnt, old.g_ocnt, 8);
     if ((pl.ocnt_mode == OCNT_TERMS || pl.ocnt_mode == OCNT_TERMS_DERIVED) && old.g_ocnt.p)
         HIPX(hipMemcpyAsync(pl.g_ocnt.p, old.g_ocnt.p, (size_t)pl.T * 8, hipMemcpyDeviceToDevice, p->stream));
+    for (size_t i = 0; i < pl.cards.size(); ++i) {
+        CardState& cs = pl.cards[i];
+        cp(cs.regs, old_cards[i].regs, (size_t)pl.T * cs.m);
+        cp(cs.sets, old_cards[i].sets, (size_t)pl.T * cs.cap * 4);
+        cp(cs.cnt, old_cards[i].cnt, (size_t)pl.T * 4);
+    }
     HIPX(hipStreamSynchronize(p->stream));
 }
 
@@ -1176,7 +1226,83 @@ static bool collect_multi(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, C
     return true;
 }
 
+static void ensure_ord_hash(esgpu_ctx* c, const DevColumn* col, hipStream_t st);
+
+// cardinality leaves of a bucket pipeline: register pass, nonzero recount, linear-counting pass (per segment, in
+// order, so a bucket's set holds every encoded hash of every segment while it can still end in LINEAR_COUNTING)
+static void collect_cards(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
+    const bool ORD = pl.term_spec >= 0, HIST = pl.hist_spec >= 0;
+    const DevColumn* oc = ORD ? s->col(pl.ord_field.c_str()) : nullptr;
+    const DevColumn* hc = HIST ? s->col(pl.hist_field.c_str()) : nullptr;
+    CollectParams G{};
+    G.n_docs = s->max_doc;
+    G.ord = oc ? oc->ords().as<uint32_t>() : nullptr;
+    G.ord_off = (oc && oc->multi) ? oc->offsets.as<uint64_t>() : nullptr;
+    G.T = pl.T;
+    G.H = pl.H;
+    G.hv = hc ? hc->values.as<int64_t>() : nullptr;
+    G.hv_present = hc ? hc->present.as<uint64_t>() : nullptr;
+    G.hv_off = (hc && hc->multi) ? hc->offsets.as<uint64_t>() : nullptr;
+    G.interval = pl.interval;
+    G.offset = pl.offset;
+    G.key0 = pl.key0;
+    G.kstart = (HIST && pl.ktable) ? pl.d_kstart.as<int64_t>() : nullptr;
+    G.kslot = G.kstart ? pl.d_kslot.as<uint32_t>() : nullptr;
+    G.nsteps = (uint32_t)pl.kt_start.size();
+    G.accept = d_accept;
+    PredDev pred[4];
+    int npred = 0;
+    uint64_t fbytes = 0;
+    set_preds(p, s, pred, &npred, &fbytes);
+    if (npred > 0) {
+        uint64_t* bits = (uint64_t*)p->s_fbits.ensure(p->ctx, std::max<size_t>(s->n_pad / 64, 1) * 8);
+        launch_filter_bits(s->max_doc, d_accept, pred, npred, bits, p->stream);
+        HIPX(hipGetLastError());
+        G.accept = bits;
+    }
+    const uint64_t B = (uint64_t)pl.T * pl.H;
+    const uint32_t grid = std::max(1u, std::min((s->max_doc + 255) / 256, (uint32_t)p->ctx->cus * 8));
+    for (CardState& cs : pl.cards) {
+        const DevColumn* col = s->col(cs.field.c_str());
+        if (!col || s->max_doc == 0) continue;  // unmapped in this segment: no values
+        CardParams C{};
+        C.G = G;
+        C.col = col->values.p;
+        C.off = col->multi ? col->offsets.as<uint64_t>() : nullptr;
+        C.present = col->present.as<uint64_t>();
+        C.p = cs.p;
+        if (col->type == ESGPU_COL_ORD_U32) {
+            C.kind = HLL_ORD;
+            ensure_ord_hash(p->ctx, col, p->stream);
+            C.ord_hash = col->ord_hash.as<uint64_t>();
+            C.n_ords = col->value_count;
+        } else {
+            C.kind = col->type == ESGPU_COL_F64 ? HLL_F64 : HLL_I64;
+        }
+        C.regs = cs.regs.as<uint8_t>();
+        C.sets = cs.sets.as<uint32_t>();
+        C.set_cnt = cs.cnt.as<uint32_t>();
+        C.nonzero = cs.nonzero.as<uint32_t>();
+        C.cap = cs.cap;
+        C.thr = cs.thr;
+        launch_card(C, ORD, HIST, 0, grid, p->stream);
+        launch_card_nonzero(C.regs, B, cs.p, C.nonzero, p->stream);
+        launch_card(C, ORD, HIST, 1, grid, p->stream);
+        HIPX(hipGetLastError());
+        p->last_bytes += column_bytes(col, s->max_doc);
+    }
+    HIPX(hipEventRecord(pl.e1, p->stream));
+}
+
+static bool collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept);
+
 static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
+    const bool done = collect_grid_cells(p, pl, s, d_accept);
+    if (done && !pl.cards.empty()) collect_cards(p, pl, s, d_accept);
+    return done;
+}
+
+static bool collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
     const bool ORD = pl.term_spec >= 0, HIST = pl.hist_spec >= 0;
     const DevColumn* oc = ORD ? s->col(pl.ord_field.c_str()) : nullptr;
     const DevColumn* hc = HIST ? s->col(pl.hist_field.c_str()) : nullptr;
@@ -1607,11 +1733,68 @@ struct HostCells {
     const double* sq = nullptr;
 };
 
+// the cardinality sketches of the given bucket cells, gathered to the host in that order (rows index like HostCells)
+static void gather_cards(esgpu_plan* p, Pipeline& pl, const std::vector<uint32_t>& cells) {
+    if (pl.cards.empty()) return;
+    hipStream_t st = p->stream;
+    const uint32_t n = (uint32_t)cells.size();
+    uint32_t* dcells = nullptr;
+    if (n) {
+        dcells = (uint32_t*)p->s_rows.ensure(p->ctx, (size_t)n * 4);
+        HIPX(hipMemcpyAsync(dcells, cells.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
+    }
+    for (CardState& cs : pl.cards) {
+        cs.h_regs.resize((size_t)n * cs.m);
+        cs.h_sets.resize((size_t)n * cs.cap);
+        cs.h_cnt.resize(n);
+        cs.h_nz.resize(n);
+        if (!n) continue;
+        struct { const DevBuf* src; uint32_t row; void* host; } parts[4] = {
+            {&cs.regs, cs.m, cs.h_regs.data()}, {&cs.sets, cs.cap * 4, cs.h_sets.data()},
+            {&cs.cnt, 4, cs.h_cnt.data()}, {&cs.nonzero, 4, cs.h_nz.data()}};
+        for (auto& pt : parts) {
+            uint8_t* d = (uint8_t*)p->s_dst[5].ensure(p->ctx, (size_t)n * pt.row);
+            launch_gather_bytes(dcells, n, pt.row, pt.src->as<uint8_t>(), d, st);
+            HIPX(hipGetLastError());
+            HIPX(hipMemcpyAsync(pt.host, d, (size_t)n * pt.row, hipMemcpyDeviceToHost, st));
+            HIPX(hipStreamSynchronize(st));  // s_dst[5] is reused by the next part
+        }
+    }
+}
+
+// one instance of cardinality leaf `cs` from gathered row c (CardinalityAggregator.buildAggregation: a sketch whose
+// cardinality is 0 is reported as "no counts"; HYPERLOGLOG iff more than threshold distinct encoded hashes)
+static void append_card(const CardState& cs, size_t c, Block& r) {
+    const uint32_t nz = cs.h_nz[c], cnt = cs.h_cnt[c];
+    r.append_empty();
+    if (nz == 0 && cnt == 0) return;
+    const size_t i = r.n - 1;
+    r.hll_present[i] = 1;
+    if (nz > cs.thr || cnt > cs.thr) {
+        r.hll_mode[i] = 1;
+        r.regs[i].assign(cs.h_regs.begin() + c * cs.m, cs.h_regs.begin() + (c + 1) * cs.m);
+    } else {
+        r.hll_mode[i] = 0;
+        std::vector<uint32_t>& lc = r.lc[i];
+        for (size_t k = 0; k < cs.cap; ++k) {
+            const uint32_t e = cs.h_sets[c * cs.cap + k];
+            if (e) lc.push_back(e);
+        }
+        std::sort(lc.begin(), lc.end());
+        if (lc.empty()) r.hll_present[i] = 0;
+    }
+}
+
 // one instance of every leaf metric of the pipeline, from grid cell c, appended to blocks[0..]
 static void append_metrics(const esgpu_plan* p, const Pipeline& pl, const HostCells& h, size_t c, std::vector<Block>& blocks) {
+    size_t card = 0;
     for (size_t j = 0; j < pl.metrics.size(); ++j) {
         const int32_t type = p->specs[pl.metrics[j]].s.type;
         Block& r = blocks[j];
+        if (type == ESGPU_AGG_CARDINALITY) {
+            append_card(pl.cards[card++], c, r);
+            continue;
+        }
         const uint64_t vc = pl.vcnt_mode ? h.vcnt[c] : h.cnt[c];
         double sum = 0.0, mn = INFINITY, mx = -INFINITY, sq = 0.0;
         if (vc > 0) {
@@ -1636,6 +1819,7 @@ static std::vector<Block> metric_protos(const esgpu_plan* p, const Pipeline& pl)
     std::vector<Block> out;
     for (int m : pl.metrics) {
         out.push_back(metric_shell(p->specs[m]));
+        if (p->specs[m].s.type == ESGPU_AGG_CARDINALITY) out.back().precision = p->specs[m].precision;
         out.back().append_empty();
     }
     return out;
@@ -1805,6 +1989,12 @@ static Block build_grid(esgpu_plan* p, Pipeline& pl) {
             HIPX(hipGetLastError());
             d2h(p, h, pl, (size_t)k * H, dsts[0], dsts[1], dsts[2], dsts[3], dsts[4], dsts[5]);
         }
+        if (!pl.cards.empty()) {
+            std::vector<uint32_t> cells((size_t)k * H);
+            for (uint32_t i = 0; i < k; ++i)
+                for (uint32_t s2 = 0; s2 < H; ++s2) cells[(size_t)i * H + s2] = s2 * T + top[i].ord;
+            gather_cards(p, pl, cells);
+        }
         if (gpu_topk) {  // otherDocCount = (sum of all counts) - (sum of the winners' counts)
             for (uint32_t i = 0; i < k; ++i) {
                 if (top[i].count < 0) top[i].count = (int64_t)h.cnt[i];  // term orders (H == 1): count from the row
@@ -1840,6 +2030,11 @@ static Block build_grid(esgpu_plan* p, Pipeline& pl) {
     const uint32_t T = pl.T, H = pl.H;
     HostCells h;
     d2h(p, h, pl, (size_t)T * H, pl.g_cnt.p, pl.g_vcnt.p, pl.g_sum.p, pl.g_min.p, pl.g_max.p, pl.g_sq.p);
+    if (!pl.cards.empty()) {
+        std::vector<uint32_t> cells((size_t)T * H);
+        for (size_t i = 0; i < cells.size(); ++i) cells[i] = (uint32_t)i;
+        gather_cards(p, pl, cells);
+    }
     std::vector<unsigned long long> ocnt;
     if (pl.ocnt_mode == OCNT_HIST) {
         ocnt.resize(H);
@@ -1923,6 +2118,12 @@ extern "C" int esgpu_plan_reset(esgpu_plan* p) {
                 continue;
             }
             const size_t cells = (size_t)pl.T * pl.H;
+            for (CardState& cs : pl.cards) {
+                HIPX(hipMemsetAsync(cs.regs.p, 0, cs.regs.bytes, p->stream));
+                HIPX(hipMemsetAsync(cs.sets.p, 0, cs.sets.bytes, p->stream));
+                HIPX(hipMemsetAsync(cs.cnt.p, 0, cs.cnt.bytes, p->stream));
+                HIPX(hipMemsetAsync(cs.nonzero.p, 0, cs.nonzero.bytes, p->stream));
+            }
             HIPX(hipMemsetAsync(pl.g_cnt.p, 0, cells * 8, p->stream));
             if (pl.g_ocnt.p) HIPX(hipMemsetAsync(pl.g_ocnt.p, 0, pl.g_ocnt.bytes, p->stream));
             if (pl.g_vcnt.p) HIPX(hipMemsetAsync(pl.g_vcnt.p, 0, cells * 8, p->stream));
