@@ -178,6 +178,9 @@ def lib():
             raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
         handle = ctypes.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
+            fn = getattr(handle, name, None)
+            if fn is None and os.environ.get("ESGPU_LIBRARY"):  # an older variant build for A/B timing
+                continue
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args

@@ -31,7 +31,7 @@ def check_synthetic(engine, aggs, fields, n, filters=None):
 
 
 def test_terms_cardinality_default_precision(engine):  # p = 9 under one bucket level: head hosts HLL, tail hosts LC
-    aggs = [AB.terms("hosts").field("host").size(200).subAggregation(AB.cardinality("ips").field("client_ip.hash"))]
+    aggs = [AB.terms("hosts").field("host").size(1000).subAggregation(AB.cardinality("ips").field("client_ip.hash"))]
     r = check_synthetic(engine, aggs, ("host", "client_ip.hash"), 1_000_000)
     modes = {b["ips"]["_internal"]["mode"] for b in r["hosts"]["buckets"]}
     assert modes == {"lc", "hll"}
