@@ -685,6 +685,91 @@ __global__ __launch_bounds__(kHllWG) void hll_registers_kernel(HllParams P, uint
     }
 }
 
+// Unfiltered dense columns (no accept bits, no predicates, no present bitset): the register pass without the generic
+// per-doc branches.  A hash can raise a register only if its run length exceeds the floor, i.e. only if the `floor`
+// bits below the index bits are all zero -- one 64-bit AND decides that before any clz / index / register read.
+template <int KIND>
+__device__ __forceinline__ uint64_t hll_fast_hash(const HllParams& P, uint64_t raw) {
+    if (KIND == HLL_ORD) {
+        const uint32_t o = (uint32_t)raw;
+        return (o != kMissingOrd && o < P.n_ords) ? P.ord_hash[o] : 0ull;
+    }
+    uint64_t bits = raw;
+    if (KIND == HLL_F64) {  // doubleToLongBits canonicalises NaN
+        const double x = bits_dbl(bits);
+        if (x != x) bits = 0x7ff8000000000000ULL;
+    }
+    return mix64(bits);
+}
+
+constexpr uint32_t kHllGroup = 64;       // registers per group floor
+constexpr uint32_t kHllMaxGroups = 4096;  // 2^18 / 64
+
+template <int KIND>
+__global__ __launch_bounds__(kHllWG) void hll_registers_fast_kernel(HllParams P, uint32_t d_begin, uint32_t d_end,
+                                                                    uint32_t per_wg, const unsigned int* floor_ptr) {
+    const uint32_t floor = floor_ptr ? min(*floor_ptr, 64u - (uint32_t)P.p) : 0u;
+    // rl > floor  <=>  bits [64 - p - floor, 64 - p) of the hash are zero
+    const uint64_t zmask = floor == 0 ? 0ull : (((1ull << floor) - 1ull) << (64 - P.p - floor));
+    // per-group floors (min of 64 registers) rise faster than the global one: most survivors of the mask test stop here
+    __shared__ unsigned char gf[kHllMaxGroups];
+    const uint32_t m = 1u << P.p;
+    const uint32_t ngroups = m >= kHllGroup ? m / kHllGroup : 1u;
+    const uint32_t gshift = m >= kHllGroup ? 6u : (uint32_t)P.p;
+    for (uint32_t i = threadIdx.x; i < ngroups; i += kHllWG) gf[i] = floor_ptr ? P.gfloor[i] : 0;
+    __syncthreads();
+    const uint32_t w0 = d_begin + blockIdx.x * per_wg;
+    const uint32_t w1 = min(d_end, w0 + per_wg);
+    if (w0 >= w1) return;
+    const uint32_t t4 = threadIdx.x * 4;
+    uint64_t cur_raw[4] = {0, 0, 0, 0};
+    if (w0 + t4 < w1) hll_load_raw(P, w0 + t4, cur_raw);
+    for (uint32_t base = w0; base < w1; base += kHllIter) {
+        const uint32_t i0 = base + t4, nx = i0 + kHllIter;
+        uint64_t nxt_raw[4] = {0, 0, 0, 0};
+        if (nx < w1) hll_load_raw(P, nx, nxt_raw);
+        if (i0 < w1) {
+            const uint32_t lim = w1 - i0;  // docs of this thread inside the range (>= 1)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint64_t h = hll_fast_hash<KIND>(P, cur_raw[j]);
+                bool live = (uint32_t)j < lim && (h & zmask) == 0;
+                if (KIND == HLL_ORD) live = live && (uint32_t)cur_raw[j] != kMissingOrd && (uint32_t)cur_raw[j] < P.n_ords;
+                if (live) {
+                    const uint32_t rl = hll_run_len(h, P.p);
+                    const uint32_t idx = hll_index(h, P.p);
+                    if (rl > gf[idx >> gshift] && rl > P.regs[idx]) atomicMax(&P.regs[idx], rl);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cur_raw[j] = nxt_raw[j];
+    }
+}
+
+// group floors: one wave per group of 64 registers; the global floor is their min (*out initialised to ~0), one
+// atomic per workgroup of 16 groups
+__global__ __launch_bounds__(1024) void hll_group_floor_kernel(const unsigned int* regs, uint32_t m, unsigned char* gfloor,
+                                                               unsigned int* out) {
+    __shared__ uint32_t wmin[16];
+    const uint32_t gsz = m >= kHllGroup ? kHllGroup : m;
+    const uint32_t g = blockIdx.x * 16 + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t v = (g * gsz < m && lane < gsz) ? regs[g * gsz + lane] : 0xFFFFFFFFu;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    if (lane == 0) {
+        if (g * gsz < m) gfloor[g] = (unsigned char)min(v, 255u);
+        wmin[threadIdx.x >> 6] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = wmin[0];
+        for (int w = 1; w < 16; ++w) t = min(t, wmin[w]);
+        atomicMin(out, t);
+    }
+}
+
 // min over the registers -> *out (initialised to ~0 by the launcher); one read of the 2^p words by 64 workgroups
 __global__ __launch_bounds__(1024) void hll_floor_kernel(const unsigned int* regs, uint32_t m, unsigned int* out) {
     uint32_t mn = 0xFFFFFFFFu;
@@ -763,19 +848,34 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
     }
     cuts.push_back(n);
     const uint32_t wgs_max = cus * 8;  // 8 workgroups of 256 threads per CU
+    const bool fast = !p.accept && p.npred == 0 && !p.present;
     const uint32_t floor_grid = std::max(1u, std::min(64u, m / 4096));
     for (size_t ph = 0; ph + 1 < cuts.size(); ++ph) {
         const uint32_t span = cuts[ph + 1] - cuts[ph];
         if (span == 0) continue;
-        // contiguous range per workgroup, a multiple of 4 docs, at least 16 iterations of 1024 docs
-        uint32_t wgs = std::max(1u, std::min(wgs_max, span / (kHllIter * 16)));
+        // contiguous range per workgroup, a multiple of 4 docs, at least 4 iterations of 1024 docs (the first phase is
+        // small and latency-bound: every hash reads a register there, so it needs the whole chip)
+        uint32_t wgs = std::max(1u, std::min(wgs_max, span / (kHllIter * 4)));
         const uint32_t per = ((span + wgs - 1) / wgs + 3) & ~3u;
         wgs = (span + per - 1) / per;
-        hipLaunchKernelGGL(hll_registers_kernel, dim3(wgs), dim3(kHllWG), 0, st, p, cuts[ph], cuts[ph + 1], per,
-                           ph == 0 ? (const unsigned int*)nullptr : (const unsigned int*)p.floor);
+        const unsigned int* fl = ph == 0 ? (const unsigned int*)nullptr : (const unsigned int*)p.floor;
+        if (fast && p.kind == HLL_I64)
+            hipLaunchKernelGGL(hll_registers_fast_kernel<HLL_I64>, dim3(wgs), dim3(kHllWG), 0, st, p, cuts[ph], cuts[ph + 1], per, fl);
+        else if (fast && p.kind == HLL_F64)
+            hipLaunchKernelGGL(hll_registers_fast_kernel<HLL_F64>, dim3(wgs), dim3(kHllWG), 0, st, p, cuts[ph], cuts[ph + 1], per, fl);
+        else if (fast)
+            hipLaunchKernelGGL(hll_registers_fast_kernel<HLL_ORD>, dim3(wgs), dim3(kHllWG), 0, st, p, cuts[ph], cuts[ph + 1], per, fl);
+        else
+            hipLaunchKernelGGL(hll_registers_kernel, dim3(wgs), dim3(kHllWG), 0, st, p, cuts[ph], cuts[ph + 1], per, fl);
         if (ph + 2 < cuts.size()) {
             (void)hipMemsetAsync(p.floor, 0xFF, 4, st);
-            hipLaunchKernelGGL(hll_floor_kernel, dim3(floor_grid), dim3(1024), 0, st, (const unsigned int*)p.regs, m, p.floor);
+            if (fast) {
+                const uint32_t ng = m >= kHllGroup ? m / kHllGroup : 1u;
+                hipLaunchKernelGGL(hll_group_floor_kernel, dim3((ng + 15) / 16), dim3(1024), 0, st, (const unsigned int*)p.regs, m,
+                                   p.gfloor, p.floor);
+            } else {
+                hipLaunchKernelGGL(hll_floor_kernel, dim3(floor_grid), dim3(1024), 0, st, (const unsigned int*)p.regs, m, p.floor);
+            }
         }
     }
     (void)hipMemsetAsync(p.nonzero, 0, 4, st);  // recount over the registers (they accumulate across segments)

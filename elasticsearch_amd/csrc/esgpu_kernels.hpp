@@ -103,6 +103,7 @@ struct HllParams {
     unsigned int* lc_count;
     unsigned int* nonzero;      // written by the register pass: registers != 0
     unsigned int* floor;        // scratch: min register after a phase
+    unsigned char* gfloor;      // scratch: min register of each group of 64 registers after a phase ([max(m / 64, 1)])
     uint32_t lc_mask;
     uint32_t lc_threshold;
 };

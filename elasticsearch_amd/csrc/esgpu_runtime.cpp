@@ -1483,7 +1483,7 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
         pl.lc_mask = cap - 1;
         pl.lc_set.alloc(p->ctx, (size_t)cap * 4);
         HIPX(hipMemsetAsync(pl.lc_set.p, 0, (size_t)cap * 4, p->stream));
-        pl.lc_count.alloc(p->ctx, 16);
+        pl.lc_count.alloc(p->ctx, 16 + std::max<size_t>(m / 64, 1));  // counters, then the group floors
         HIPX(hipMemsetAsync(pl.lc_count.p, 0, 16, p->stream));
         pl.allocated = true;
     }
@@ -1536,6 +1536,7 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
     H.lc_count = pl.lc_count.as<unsigned int>();
     H.nonzero = pl.lc_count.as<unsigned int>() + 1;
     H.floor = pl.lc_count.as<unsigned int>() + 2;
+    H.gfloor = pl.lc_count.as<unsigned char>() + 16;
     H.lc_mask = pl.lc_mask;
     H.lc_threshold = pl.lc_threshold;
     if (H.n_docs == 0) return false;
