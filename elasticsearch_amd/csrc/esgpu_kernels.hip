@@ -107,18 +107,32 @@ __device__ __forceinline__ uint32_t bits4(const uint64_t* bm, uint32_t doc0) {
     return (uint32_t)(bm[doc0 >> 6] >> (doc0 & 63)) & 0xFu;
 }
 
+// Column streams are read once per request: ESGPU_NT=1 marks them non-temporal (nt) so they do not displace the
+// cell grid and the zone maps in L2 / MALL.
+#ifndef ESGPU_NT
+#define ESGPU_NT 0
+#endif
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4_t load16(const void* p) {
+#if ESGPU_NT
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+#else
+    return *reinterpret_cast<const u32x4_t*>(p);
+#endif
+}
+__device__ __forceinline__ uint64_t join64(uint32_t lo, uint32_t hi) { return (uint64_t)lo | ((uint64_t)hi << 32); }
 __device__ __forceinline__ void load_i64x4(const int64_t* p, uint32_t doc0, int64_t out[4]) {
-    const longlong2 a = *reinterpret_cast<const longlong2*>(p + doc0);
-    const longlong2 b = *reinterpret_cast<const longlong2*>(p + doc0 + 2);
-    out[0] = a.x; out[1] = a.y; out[2] = b.x; out[3] = b.y;
+    const u32x4_t a = load16(p + doc0), b = load16(p + doc0 + 2);
+    out[0] = (int64_t)join64(a.x, a.y); out[1] = (int64_t)join64(a.z, a.w);
+    out[2] = (int64_t)join64(b.x, b.y); out[3] = (int64_t)join64(b.z, b.w);
 }
 __device__ __forceinline__ void load_f64x4(const double* p, uint32_t doc0, double out[4]) {
-    const double2 a = *reinterpret_cast<const double2*>(p + doc0);
-    const double2 b = *reinterpret_cast<const double2*>(p + doc0 + 2);
-    out[0] = a.x; out[1] = a.y; out[2] = b.x; out[3] = b.y;
+    const u32x4_t a = load16(p + doc0), b = load16(p + doc0 + 2);
+    out[0] = bits_dbl(join64(a.x, a.y)); out[1] = bits_dbl(join64(a.z, a.w));
+    out[2] = bits_dbl(join64(b.x, b.y)); out[3] = bits_dbl(join64(b.z, b.w));
 }
 __device__ __forceinline__ void load_u32x4(const uint32_t* p, uint32_t doc0, uint32_t out[4]) {
-    const uint4 a = *reinterpret_cast<const uint4*>(p + doc0);
+    const u32x4_t a = load16(p + doc0);
     out[0] = a.x; out[1] = a.y; out[2] = a.z; out[3] = a.w;
 }
 
