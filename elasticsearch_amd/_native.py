@@ -61,6 +61,8 @@ class Filter(ctypes.Structure):
         ("has_lower", ctypes.c_int32), ("has_upper", ctypes.c_int32), ("reserved", ctypes.c_int32),
         ("field", ctypes.c_char_p), ("term", ctypes.c_int64), ("lo_i", ctypes.c_int64), ("hi_i", ctypes.c_int64),
         ("lo_d", ctypes.c_double), ("hi_d", ctypes.c_double),
+        ("lo_term", ctypes.c_char_p), ("hi_term", ctypes.c_char_p), ("lo_term_len", ctypes.c_uint64),
+        ("hi_term_len", ctypes.c_uint64),
     ]
 
 

@@ -437,10 +437,20 @@ def flatten_filters(queries, ord_lookup=None):
             f.type = N.FILTER_RANGE
             if q.lo is not None:
                 f.has_lower, f.include_lower = 1, int(q.include_lower)
-                f.lo_i, f.lo_d = int(q.lo) if float(q.lo).is_integer() else int(q.lo), float(q.lo)
+                if isinstance(q.lo, (str, bytes)):  # TermRangeQuery on a keyword field
+                    b = q.lo.encode("utf-8") if isinstance(q.lo, str) else bytes(q.lo)
+                    keep.append(b)
+                    f.lo_term, f.lo_term_len = b, len(b)
+                else:
+                    f.lo_i, f.lo_d = int(q.lo), float(q.lo)
             if q.hi is not None:
                 f.has_upper, f.include_upper = 1, int(q.include_upper)
-                f.hi_i, f.hi_d = int(q.hi), float(q.hi)
+                if isinstance(q.hi, (str, bytes)):
+                    b = q.hi.encode("utf-8") if isinstance(q.hi, str) else bytes(q.hi)
+                    keep.append(b)
+                    f.hi_term, f.hi_term_len = b, len(b)
+                else:
+                    f.hi_i, f.hi_d = int(q.hi), float(q.hi)
         out.append(f)
     arr = (N.Filter * max(len(out), 1))(*out)
     return arr, len(out), keep

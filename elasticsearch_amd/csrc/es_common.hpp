@@ -135,6 +135,14 @@ ES_HD uint32_t magic_div(uint32_t n, uint32_t m, uint32_t s1, uint32_t s2, uint3
     return (t + ((n - t) >> s1)) >> s2;
 }
 
+// Java (long) of a double (FieldData.castToLong / JLS 5.1.3): NaN -> 0, saturating, truncation toward zero
+ES_HD int64_t java_long(double v) {
+    if (v != v) return 0;
+    if (v >= 9.2233720368547758e18) return INT64_MAX;
+    if (v <= -9.2233720368547758e18) return INT64_MIN;
+    return (int64_t)v;
+}
+
 ES_HD int64_t floor_div64(int64_t a, int64_t b) {  // Rounding.Interval.roundKey (common/rounding/Rounding.java:92-98)
     return a < 0 ? (a - b + 1) / b : a / b;
 }

@@ -26,13 +26,14 @@ namespace esgpu {
 // zone maps
 // ------------------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void zone_map_kernel(const int64_t* __restrict__ v, const uint64_t* __restrict__ present,
-                                                       uint32_t n, int64_t* __restrict__ zmin, int64_t* __restrict__ zmax) {
+                                                       uint32_t n, int64_t* __restrict__ zmin, int64_t* __restrict__ zmax,
+                                                       int f64) {
     const uint32_t block = blockIdx.x;
     const uint32_t begin = block * kBlockDocs;
     int64_t mn = INT64_MAX, mx = INT64_MIN;
     for (uint32_t i = begin + threadIdx.x; i < begin + kBlockDocs && i < n; i += blockDim.x) {
         if (present && !((present[i >> 6] >> (i & 63)) & 1)) continue;
-        const int64_t x = v[i];
+        const int64_t x = f64 ? java_long(bits_dbl((uint64_t)v[i])) : v[i];
         mn = x < mn ? x : mn;
         mx = x > mx ? x : mx;
     }
@@ -53,11 +54,11 @@ __global__ __launch_bounds__(256) void zone_map_kernel(const int64_t* __restrict
     }
 }
 
-void launch_zone_map(const int64_t* v, const uint64_t* present, uint32_t n, int64_t* zmin, int64_t* zmax,
+void launch_zone_map(const int64_t* v, const uint64_t* present, uint32_t n, int64_t* zmin, int64_t* zmax, bool f64,
                      hipStream_t stream) {
     const uint32_t nb = (n + kBlockDocs - 1) / kBlockDocs;
     if (nb == 0) return;
-    hipLaunchKernelGGL(zone_map_kernel, dim3(nb), dim3(256), 0, stream, v, present, n, zmin, zmax);
+    hipLaunchKernelGGL(zone_map_kernel, dim3(nb), dim3(256), 0, stream, v, present, n, zmin, zmax, f64 ? 1 : 0);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -138,11 +139,11 @@ __device__ __forceinline__ void load_u32x4(const uint32_t* p, uint32_t doc0, uin
 
 __device__ __forceinline__ uint32_t eval_pred(const PredDev& q, uint32_t doc0) {
     uint32_t m = 0;
-    if (q.kind == PRED_ORD_EQ) {
+    if (q.kind == PRED_ORD_EQ || q.kind == PRED_ORD_RANGE) {  // a term is the range [ord, ord]
         uint32_t o[4];
         load_u32x4((const uint32_t*)q.col, doc0, o);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) m |= (uint32_t)((int64_t)o[j] == q.lo && o[j] != kMissingOrd) << j;
+        for (int j = 0; j < 4; ++j) m |= (uint32_t)((int64_t)o[j] >= q.lo && (int64_t)o[j] <= q.hi && o[j] != kMissingOrd) << j;
     } else if (q.kind == PRED_F64_RANGE) {
         double v[4];
         load_f64x4((const double*)q.col, doc0, v);
@@ -172,6 +173,10 @@ __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0,
     if (ORD) load_u32x4(P.ord, doc0, d.ord);
     if (HIST) {
         load_i64x4(P.hv, doc0, d.hv);
+        if (P.hv_f64) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) d.hv[j] = java_long(bits_dbl((uint64_t)d.hv[j]));
+        }
         d.hpres = P.hv_present ? bits4(P.hv_present, doc0) : 0xFu;
     }
     if (MET > 0) {
@@ -1489,6 +1494,12 @@ namespace esgpu {
 
 __device__ __forceinline__ bool bit_at(const uint64_t* bm, uint32_t d) { return (bm[d >> 6] >> (d & 63)) & 1; }
 
+// histogram field value i as a long (a double field is cast, ValuesSource.Numeric.longValues)
+__device__ __forceinline__ int64_t hv_at(const CollectParams& P, uint64_t i) {
+    const int64_t x = P.hv[i];
+    return P.hv_f64 ? java_long(bits_dbl((uint64_t)x)) : x;
+}
+
 // values [b, e) of doc d in a column (single valued: [d, d+1) when present)
 __device__ __forceinline__ void value_range(const uint64_t* off, const uint64_t* present, uint32_t d, uint64_t& b,
                                             uint64_t& e) {
@@ -1506,9 +1517,9 @@ __device__ bool pred_doc(const PredDev& q, uint32_t d) {
     value_range(q.offsets, q.present, d, b, e);
     for (uint64_t i = b; i < e; ++i) {
         bool m;
-        if (q.kind == PRED_ORD_EQ) {
+        if (q.kind == PRED_ORD_EQ || q.kind == PRED_ORD_RANGE) {
             const uint32_t o = ((const uint32_t*)q.col)[i];
-            m = o != kMissingOrd && (int64_t)o == q.lo;
+            m = o != kMissingOrd && (int64_t)o >= q.lo && (int64_t)o <= q.hi;
         } else if (q.kind == PRED_F64_RANGE) {
             const double v = ((const double*)q.col)[i];
             m = (q.lo_incl ? v >= q.dlo : v > q.dlo) && (q.hi_incl ? v <= q.dhi : v < q.dhi);
@@ -1588,7 +1599,7 @@ __global__ __launch_bounds__(kWG) void collect_multi_kernel(CollectParams P) {
             bool first = true;
             int64_t prev = 0;
             for (uint64_t h = hb; h < he; ++h) {
-                const int64_t k = key_index<KT>(P, ((const int64_t*)P.hv)[h]);
+                const int64_t k = key_index<KT>(P, hv_at(P, h));
                 if (!first && k == prev) continue;
                 first = false;
                 prev = k;
@@ -1607,7 +1618,7 @@ __global__ __launch_bounds__(kWG) void collect_multi_kernel(CollectParams P) {
             for (uint64_t h = hb; h < he; ++h) {
                 uint32_t slot = 0;
                 if (HIST) {
-                    const int64_t k = key_index<KT>(P, ((const int64_t*)P.hv)[h]);
+                    const int64_t k = key_index<KT>(P, hv_at(P, h));
                     if (!first && k == prev) continue;
                     first = false;
                     prev = k;
@@ -1763,7 +1774,7 @@ __global__ __launch_bounds__(256) void card_kernel(CardParams C, int pass) {
             for (uint64_t hh = hb; hh < he; ++hh) {
                 uint32_t slot = 0;
                 if (HIST) {
-                    const int64_t k = key_index<KT>(P, ((const int64_t*)P.hv)[hh]);
+                    const int64_t k = key_index<KT>(P, hv_at(P, hh));
                     if (!first && k == prev) continue;
                     first = false;
                     prev = k;
@@ -1847,18 +1858,20 @@ void launch_gather_bytes(const uint32_t* cells, uint32_t n, uint32_t row_bytes, 
                        n, row_bytes, src, dst);
 }
 
-__global__ __launch_bounds__(256) void minmax_i64_kernel(const int64_t* v, uint64_t n, int64_t* out) {
+__global__ __launch_bounds__(256) void minmax_i64_kernel(const int64_t* v, uint64_t n, int64_t* out, int f64) {
     int64_t mn = INT64_MAX, mx = INT64_MIN;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        mn = v[i] < mn ? v[i] : mn;
-        mx = v[i] > mx ? v[i] : mx;
+        const int64_t x = f64 ? java_long(bits_dbl((uint64_t)v[i])) : v[i];
+        mn = x < mn ? x : mn;
+        mx = x > mx ? x : mx;
     }
     atomicMin((long long*)&out[0], (long long)mn);
     atomicMax((long long*)&out[1], (long long)mx);
 }
-void launch_minmax_i64(const int64_t* v, uint64_t n, int64_t* out, hipStream_t st) {
+void launch_minmax_i64(const int64_t* v, uint64_t n, int64_t* out, bool f64, hipStream_t st) {
     if (n == 0) return;
-    hipLaunchKernelGGL(minmax_i64_kernel, dim3((uint32_t)std::min<uint64_t>(1024, (n + 255) / 256)), dim3(256), 0, st, v, n, out);
+    hipLaunchKernelGGL(minmax_i64_kernel, dim3((uint32_t)std::min<uint64_t>(1024, (n + 255) / 256)), dim3(256), 0, st, v, n, out,
+                       f64 ? 1 : 0);
 }
 
 }  // namespace esgpu

@@ -26,7 +26,7 @@ struct SynthParams {
     const double* rt_cdf;
 };
 
-enum PredKind : int32_t { PRED_ORD_EQ = 0, PRED_I64_RANGE = 1, PRED_F64_RANGE = 2 };
+enum PredKind : int32_t { PRED_ORD_EQ = 0, PRED_I64_RANGE = 1, PRED_F64_RANGE = 2, PRED_ORD_RANGE = 3 };
 
 struct PredDev {
     const void* col;
@@ -34,7 +34,7 @@ struct PredDev {
     const uint64_t* offsets;   // multi-valued column: CSR offsets [n_docs + 1] (doc matches if any value matches)
     int32_t kind;
     int32_t lo_incl, hi_incl, pad;
-    int64_t lo, hi;    // ORD_EQ: lo = ordinal; I64_RANGE: inclusive [lo, hi]
+    int64_t lo, hi;    // ORD_EQ: lo = ordinal; I64_RANGE / ORD_RANGE: inclusive [lo, hi]
     double dlo, dhi;   // F64_RANGE with include flags
 };
 
@@ -52,8 +52,9 @@ struct CollectParams {
     // histogram dimension
     uint32_t H, W;
     int32_t windowed;    // 1: W < H, slide a W-slot window using the zone maps
-    const int64_t* hv;
+    const int64_t* hv;               // histogram field values (i64, or f64 bits when hv_f64)
     const uint64_t* hv_present;
+    int32_t hv_f64;                  // double field: keys from (long) value (ValuesSource.Numeric.longValues, castToLong)
     int64_t interval, offset, key0;  // key index k of a value v: floor((v - offset) / interval) - key0
     const int64_t* kstart;           // non-affine roundings: step start instants [nsteps] (step = last start <= v)
     const uint32_t* kslot;           // bucket of each step (null: step j is bucket j)
@@ -116,7 +117,9 @@ struct GatherParams {
     unsigned long long* dst[6];
 };
 
-void launch_zone_map(const int64_t* v, const uint64_t* present, uint32_t n, int64_t* zmin, int64_t* zmax, hipStream_t s);
+// per-8192-doc-block min / max; f64 = the column holds doubles, taken as (long) casts (FieldData.castToLong)
+void launch_zone_map(const int64_t* v, const uint64_t* present, uint32_t n, int64_t* zmin, int64_t* zmax, bool f64,
+                     hipStream_t s);
 void launch_synth(const SynthParams& p, hipStream_t s);
 void launch_collect(const CollectParams& p, bool ord, bool hist, int met, uint32_t grid, size_t lds, hipStream_t s);
 size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode);
@@ -158,7 +161,7 @@ void launch_card_nonzero(const uint8_t* regs, uint64_t n_buckets, int p, uint32_
 void launch_gather_bytes(const uint32_t* cells, uint32_t n, uint32_t row_bytes, const uint8_t* src, uint8_t* dst, hipStream_t s);
 
 // min / max over a value array (multi-valued i64 columns: key range of a histogram), out[0] = min, out[1] = max
-void launch_minmax_i64(const int64_t* v, uint64_t n, int64_t* out, hipStream_t s);
+void launch_minmax_i64(const int64_t* v, uint64_t n, int64_t* out, bool f64, hipStream_t s);
 void launch_remap_ords(const uint32_t* in, uint32_t n, const uint32_t* map, uint32_t map_n, uint32_t* out, hipStream_t s);
 void launch_pack_u8(const unsigned int* src, uint32_t n, uint8_t* dst, hipStream_t s);
 void launch_term_totals(const unsigned long long* cnt, uint32_t H, uint32_t T, unsigned long long* out, hipStream_t s);

@@ -333,6 +333,7 @@ static void build_zone_map(esgpu_ctx* c, DevColumn& col, uint32_t n) {
     col.zmin.alloc(c, (size_t)std::max(nb, 1u) * 8);
     col.zmax.alloc(c, (size_t)std::max(nb, 1u) * 8);
     launch_zone_map(col.values.as<int64_t>(), col.present.as<uint64_t>(), n, col.zmin.as<int64_t>(), col.zmax.as<int64_t>(),
+                    col.type == ESGPU_COL_F64,
                     c->stream);
     HIPX(hipGetLastError());
     std::vector<int64_t> mn(nb), mx(nb);
@@ -382,12 +383,12 @@ extern "C" int esgpu_segment_upload(esgpu_ctx* c, const esgpu_column_desc* cols,
                 if (nv) HIPX(hipMemcpyAsync(col->values.p, d.values, nv * w, hipMemcpyHostToDevice, c->stream));
                 col->offsets.alloc(c, ((size_t)max_doc + 1) * 8);
                 HIPX(hipMemcpyAsync(col->offsets.p, d.offsets, ((size_t)max_doc + 1) * 8, hipMemcpyHostToDevice, c->stream));
-                if (d.type == ESGPU_COL_I64 && nv) {  // key range of a histogram over the field
+                if ((d.type == ESGPU_COL_I64 || d.type == ESGPU_COL_F64) && nv) {  // key range of a histogram over the field
                     DevBuf mm;
                     mm.alloc(c, 16);
                     const int64_t init[2] = {INT64_MAX, INT64_MIN};
                     HIPX(hipMemcpyAsync(mm.p, init, 16, hipMemcpyHostToDevice, c->stream));
-                    launch_minmax_i64(col->values.as<int64_t>(), nv, mm.as<int64_t>(), c->stream);
+                    launch_minmax_i64(col->values.as<int64_t>(), nv, mm.as<int64_t>(), d.type == ESGPU_COL_F64, c->stream);
                     HIPX(hipGetLastError());
                     int64_t r[2];
                     HIPX(hipMemcpyAsync(r, mm.p, 16, hipMemcpyDeviceToHost, c->stream));
@@ -410,7 +411,7 @@ extern "C" int esgpu_segment_upload(esgpu_ctx* c, const esgpu_column_desc* cols,
                     HIPX(hipMemsetAsync(col->present.p, 0, words * 8, c->stream));
                     HIPX(hipMemcpyAsync(col->present.p, d.present, ((size_t)max_doc + 63) / 64 * 8, hipMemcpyHostToDevice, c->stream));
                 }
-                if (d.type == ESGPU_COL_I64) build_zone_map(c, *col, max_doc);
+                if (d.type == ESGPU_COL_I64 || d.type == ESGPU_COL_F64) build_zone_map(c, *col, max_doc);
             }
             if (d.type == ESGPU_COL_ORD_U32 && d.dict_bytes && d.dict_offsets) {
                 col->dict_offsets.assign(d.dict_offsets, d.dict_offsets + d.value_count + 1);
@@ -482,7 +483,7 @@ extern "C" int esgpu_segment_synthetic(esgpu_ctx* c, uint64_t seed, uint32_t sha
         HIPX(hipGetLastError());
         HIPX(hipStreamSynchronize(c->stream));
         for (auto& kv : s->cols)
-            if (kv.second->type == ESGPU_COL_I64) build_zone_map(c, *kv.second, num_docs);
+            if (kv.second->type == ESGPU_COL_I64 || kv.second->type == ESGPU_COL_F64) build_zone_map(c, *kv.second, num_docs);
         *out = s.release();
     });
 }
@@ -1101,9 +1102,33 @@ static void set_preds(esgpu_plan* p, const esgpu_segment* s, PredDev* out, int32
         q.present = col->present.as<uint64_t>();
         q.offsets = col->multi ? col->offsets.as<uint64_t>() : nullptr;
         if (col->type == ESGPU_COL_ORD_U32) {
-            require(f.type == ESGPU_FILTER_TERM, ESGPU_ERR_UNSUPPORTED, "range filters on keyword fields run on the CPU path");
-            q.kind = PRED_ORD_EQ;
-            q.lo = f.term;
+            if (f.type == ESGPU_FILTER_TERM) {
+                q.kind = PRED_ORD_EQ;
+                q.lo = q.hi = f.term;
+            } else {  // TermRangeQuery: the dictionary is sorted by unsigned bytes, so the range is an ordinal range
+                q.kind = PRED_ORD_RANGE;
+                const uint64_t n = col->ord_count();
+                auto bound = [&](const uint8_t* t, uint64_t len, bool upper) {  // first ord with term > t (upper) / >= t
+                    const std::string key((const char*)t, (size_t)len);
+                    uint64_t lo = 0, hi = n;
+                    while (lo < hi) {
+                        const uint64_t mid = (lo + hi) / 2;
+                        const std::string m = col->ord_term(mid);
+                        if (upper ? !(key < m) : m < key) lo = mid + 1; else hi = mid;
+                    }
+                    return (int64_t)lo;
+                };
+                q.lo = 0;
+                q.hi = (int64_t)n - 1;
+                if (f.has_lower) {
+                    require(f.lo_term || f.lo_term_len == 0, ESGPU_ERR_INVALID, "keyword range without lower term bytes");
+                    q.lo = bound(f.lo_term, f.lo_term_len, !f.include_lower);
+                }
+                if (f.has_upper) {
+                    require(f.hi_term || f.hi_term_len == 0, ESGPU_ERR_INVALID, "keyword range without upper term bytes");
+                    q.hi = bound(f.hi_term, f.hi_term_len, f.include_upper) - 1;
+                }
+            }
             *bytes_per_doc += 4;
         } else if (col->type == ESGPU_COL_F64) {
             q.kind = PRED_F64_RANGE;
@@ -1243,6 +1268,7 @@ static void collect_cards(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, c
     G.hv = hc ? hc->values.as<int64_t>() : nullptr;
     G.hv_present = hc ? hc->present.as<uint64_t>() : nullptr;
     G.hv_off = (hc && hc->multi) ? hc->offsets.as<uint64_t>() : nullptr;
+    G.hv_f64 = hc && hc->type == ESGPU_COL_F64;
     G.interval = pl.interval;
     G.offset = pl.offset;
     G.key0 = pl.key0;
@@ -1310,7 +1336,8 @@ static bool collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment*
     // unmapped fields: a bucket aggregation over a missing field collects nothing (ValuesSource null)
     if ((ORD && !oc) || (HIST && !hc)) return false;
     if (oc) require(oc->type == ESGPU_COL_ORD_U32, ESGPU_ERR_UNSUPPORTED, "terms on numeric fields run on the CPU path");
-    if (hc) require(hc->type == ESGPU_COL_I64, ESGPU_ERR_UNSUPPORTED, "histogram over non-long fields runs on the CPU path");
+    if (hc) require(hc->type == ESGPU_COL_I64 || hc->type == ESGPU_COL_F64, ESGPU_ERR_UNSUPPORTED,
+                    "histogram over a keyword field runs on the CPU path");
     if (mc) require(mc->type == ESGPU_COL_I64 || mc->type == ESGPU_COL_F64, ESGPU_ERR_UNSUPPORTED, "metric over non-numeric field");
     // any multi-valued column (aggregated field or filter field) takes the CSR kernel
     bool multi = (oc && oc->multi) || (hc && hc->multi) || (mc && mc->multi);
@@ -1376,6 +1403,7 @@ static bool collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment*
     P.H = pl.H;
     P.hv = hc ? hc->values.as<int64_t>() : nullptr;
     P.hv_present = hc ? hc->present.as<uint64_t>() : nullptr;
+    P.hv_f64 = hc && hc->type == ESGPU_COL_F64;
     P.interval = pl.interval;
     P.offset = pl.offset;
     P.key0 = pl.key0;

@@ -240,7 +240,8 @@ typedef struct esgpu_agg_spec {
 enum {
     ESGPU_FILTER_TERM = 1,        /* doc matches if any value == term (numeric: TermQuery on the prefix-coded long;
                                      keyword: the term's ordinal; -1 = term not in dictionary => no match) */
-    ESGPU_FILTER_RANGE = 2        /* doc matches if any value in [lo,hi] with include flags (NumericRangeQuery) */
+    ESGPU_FILTER_RANGE = 2        /* doc matches if any value in [lo,hi] with include flags (NumericRangeQuery; on a
+                                     keyword field TermRangeQuery over the term bytes lo_term / hi_term) */
 };
 typedef struct esgpu_filter {
     int32_t type;
@@ -253,6 +254,9 @@ typedef struct esgpu_filter {
     int64_t term;                 /* TERM on I64 / ORD columns */
     int64_t lo_i, hi_i;           /* RANGE on I64 / U64 columns */
     double lo_d, hi_d;            /* RANGE on F64 columns */
+    const uint8_t* lo_term;       /* RANGE on ORD columns: bounds as term bytes, compared as unsigned bytes (BytesRef) */
+    const uint8_t* hi_term;
+    uint64_t lo_term_len, hi_term_len;
 } esgpu_filter;
 
 int esgpu_terms_thresholds(int32_t size, int32_t shard_size, int64_t min_doc_count, int64_t shard_min_doc_count,

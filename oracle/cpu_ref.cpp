@@ -1328,6 +1328,15 @@ static bool doc_matches(const Segment& seg, uint32_t doc, const esgpu_filter* fl
         for (int i = 0; i < n && !any; ++i) {
             if (flt[k].type == ESGPU_FILTER_TERM) {
                 any = c->d->type == ESGPU_COL_ORD_U32 ? (int64_t)c->ord_at(doc, i) == flt[k].term : c->long_at(doc, i) == flt[k].term;
+            } else if (c->d->type == ESGPU_COL_ORD_U32) {  // TermRangeQuery: BytesRef (unsigned byte) order
+                const uint32_t o = c->ord_at(doc, i);
+                if (o == 0xFFFFFFFFu) continue;
+                const std::string t = c->term(o);
+                const std::string lo((const char*)flt[k].lo_term, flt[k].lo_term ? (size_t)flt[k].lo_term_len : 0);
+                const std::string hi((const char*)flt[k].hi_term, flt[k].hi_term ? (size_t)flt[k].hi_term_len : 0);
+                const bool lo_ok = !flt[k].has_lower || (flt[k].include_lower ? term_compare(t, lo) >= 0 : term_compare(t, lo) > 0);
+                const bool hi_ok = !flt[k].has_upper || (flt[k].include_upper ? term_compare(t, hi) <= 0 : term_compare(t, hi) < 0);
+                any = lo_ok && hi_ok;
             } else if (c->d->type == ESGPU_COL_F64) {
                 const double v = c->double_at(doc, i);
                 bool lo = !flt[k].has_lower || (flt[k].include_lower ? v >= flt[k].lo_d : v > flt[k].lo_d);

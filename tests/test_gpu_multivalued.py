@@ -149,3 +149,14 @@ def test_multi_valued_accept_bits_and_global_ordinals(engine):
     omap.close()
     for sg in segs:
         sg.close()
+
+
+def test_multi_valued_double_histogram(engine):
+    aggs = [AB.histogram("p").field("prices").interval(50).subAggregation(AB.avg("c").field("codes")),
+            AB.terms("tags").field("tags").size(5).subAggregation(AB.histogram("p").field("prices").interval(250))]
+    check(engine, aggs, segment(N_DOCS, 12), N_DOCS)
+
+
+def test_multi_valued_keyword_range(engine):  # a doc matches if any of its terms is in the range
+    aggs = [AB.terms("host").field("host").size(10), AB.cardinality("c").field("codes")]
+    check(engine, aggs, segment(N_DOCS, 13), N_DOCS, filters=[QB.rangeQuery("tags").gte("tag-050").lt("tag-060")])

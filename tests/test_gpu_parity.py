@@ -285,3 +285,57 @@ def test_multi_segment_global_ordinals(engine):
     omap.close()
     for s in segs:
         s.close()
+
+
+def test_histogram_over_double_field(engine):
+    """HistogramAggregator over a double field buckets (long) value (ValuesSource.Numeric.longValues ->
+    FieldData.castToLong): truncation toward zero, NaN -> 0."""
+    n = 400_000
+    rng = np.random.default_rng(21)
+    x = (rng.standard_normal(n) * 300.0).astype(np.float64)
+    x[rng.random(n) < 0.001] = np.nan
+    x[:3] = [-0.5, 0.5, -99.99]
+    present = rng.random(n) < 0.9
+    cols = {"x": {"type": N.COL_F64, "values": x, "present": bits_from_mask(present)},
+            "rt": {"type": N.COL_I64, "values": rng.integers(0, 1000, size=n).astype(np.int64)}}
+    aggs = [AB.histogram("hx").field("x").interval(25).offset(3).subAggregation(AB.stats("rt").field("rt")),
+            AB.histogram("hx0").field("x").interval(100).minDocCount(0).subAggregation(AB.extendedStats("x").field("x"))]
+    want = O.run([(cols, n)], aggs)
+    seg = engine.upload_segment(cols, n)
+    plan = engine.plan(aggs)
+    plan.collect(seg)
+    res = plan.build()
+    assert_same(res.to_dict(), want["shards"][0], "shard", False)
+    assert_same(reduce([res]).to_dict(), want["reduced"], "reduced", False)
+    plan.close()
+    seg.close()
+
+
+def test_keyword_range_filters(engine):
+    """RangeQuery on a keyword field (TermRangeQuery over BytesRef order) becomes an ordinal range of the sorted
+    dictionary: inclusive / exclusive / open bounds, bounds that are not terms, an empty range, and the partitioned
+    high-cardinality path."""
+    n = 600_000
+    fields = ("host", "@timestamp", "response_time_ms", "url")
+    cases = [
+        [QB.rangeQuery("host").gte("host-0100").lt("host-0500")],
+        [QB.rangeQuery("host").gt("host-0100").lte("host-0500x")],
+        [QB.rangeQuery("host").gt("host-09")],
+        [QB.rangeQuery("host").lt("host-0002"), QB.termQuery("host", "host-0001")],
+        [QB.rangeQuery("host").gte("zzz")],
+        [QB.rangeQuery("url").gte("/p/00100000").lt("/p/00800000")],
+    ]
+    aggs = [AB.terms("hosts").field("host").size(20).subAggregation(AB.stats("rt").field("response_time_ms")),
+            AB.dateHistogram("d").field("@timestamp").interval("1d"),
+            AB.terms("urls").field("url").size(10)]
+    cols = synthetic_columns(fields, n)
+    hosts = ["host-%04d" % i for i in range(1000)]
+    lookup = lambda f, t: hosts.index(t) if f == "host" and t in hosts else -1  # noqa: E731
+    seg = engine.synthetic_segment(n, fields=fields)
+    for flt in cases:
+        want = O.run([(cols, n)], aggs, filters=flt, ord_lookup=lookup)
+        plan = engine.plan(aggs, filters=flt, ord_lookup=lookup)
+        plan.collect(seg)
+        assert_same(plan.build().to_dict(), want["shards"][0], "shard")
+        plan.close()
+    seg.close()
