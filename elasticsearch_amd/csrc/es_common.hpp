@@ -64,6 +64,76 @@ ES_HD void murmur3_x64_128(const uint8_t* key, int len, uint64_t seed, uint64_t*
     *out_h2 = h2;
 }
 
+// MurmurHash3_x86_32 as Lucene's StringHelper.murmurhash3_x86_32 (third-party, Lucene 5.4; seed 0 for routing):
+// little-endian 4-byte blocks, tail of 1-3 bytes, fmix32.  Murmur3HashFunction.hash(routing) feeds it the UTF-16LE
+// bytes of the routing string (cluster/routing/Murmur3HashFunction.java:31-41).
+ES_HD uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+ES_HD uint32_t murmur3_x86_32(const uint8_t* data, int len, uint32_t seed) {
+    const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
+    uint32_t h1 = seed;
+    const int rounded = len & ~3;
+    for (int i = 0; i < rounded; i += 4) {
+        uint32_t k1 = (uint32_t)data[i] | ((uint32_t)data[i + 1] << 8) | ((uint32_t)data[i + 2] << 16) | ((uint32_t)data[i + 3] << 24);
+        k1 *= c1;
+        k1 = rotl32(k1, 15);
+        k1 *= c2;
+        h1 ^= k1;
+        h1 = rotl32(h1, 13);
+        h1 = h1 * 5 + 0xe6546b64u;
+    }
+    uint32_t k1 = 0;
+    switch (len & 3) {
+        case 3: k1 = (uint32_t)data[rounded + 2] << 16;  // fallthrough
+        case 2: k1 |= (uint32_t)data[rounded + 1] << 8;  // fallthrough
+        case 1:
+            k1 |= data[rounded];
+            k1 *= c1;
+            k1 = rotl32(k1, 15);
+            k1 *= c2;
+            h1 ^= k1;
+    }
+    h1 ^= (uint32_t)len;
+    h1 ^= h1 >> 16;
+    h1 *= 0x85ebca6bu;
+    h1 ^= h1 >> 13;
+    h1 *= 0xc2b2ae35u;
+    h1 ^= h1 >> 16;
+    return h1;
+}
+// the same over the UTF-16LE bytes of n UTF-16 code units (a Java String's chars): two chars per 4-byte block
+ES_HD uint32_t murmur3_x86_32_utf16(const uint16_t* c, int n, uint32_t seed) {
+    const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
+    uint32_t h1 = seed;
+    for (int i = 0; i + 1 < n; i += 2) {
+        uint32_t k1 = (uint32_t)c[i] | ((uint32_t)c[i + 1] << 16);
+        k1 *= c1;
+        k1 = rotl32(k1, 15);
+        k1 *= c2;
+        h1 ^= k1;
+        h1 = rotl32(h1, 13);
+        h1 = h1 * 5 + 0xe6546b64u;
+    }
+    if (n & 1) {  // two tail bytes
+        uint32_t k1 = c[n - 1];
+        k1 *= c1;
+        k1 = rotl32(k1, 15);
+        k1 *= c2;
+        h1 ^= k1;
+    }
+    h1 ^= (uint32_t)(2 * n);
+    h1 ^= h1 >> 16;
+    h1 *= 0x85ebca6bu;
+    h1 ^= h1 >> 13;
+    h1 *= 0xc2b2ae35u;
+    h1 ^= h1 >> 16;
+    return h1;
+}
+// OperationRouting.shardId for indices created on or after 2.0: MathUtils.mod(hash, numberOfShards)
+ES_HD int32_t routing_shard(int32_t hash, int32_t nshards) {
+    const int32_t r = hash % nshards;
+    return r < 0 ? r + nshards : r;
+}
+
 // ---- HyperLogLog++ register math (A/metrics/cardinality/HyperLogLogPlusPlus.java:335-375) ----------------------
 constexpr int kP2 = 25;
 ES_HD int clz64(uint64_t x) {

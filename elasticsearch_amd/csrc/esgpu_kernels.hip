@@ -1858,6 +1858,34 @@ void launch_gather_bytes(const uint32_t* cells, uint32_t n, uint32_t row_bytes, 
                        n, row_bytes, src, dst);
 }
 
+// ---- index-time hashing: one value per thread ----
+__global__ __launch_bounds__(256) void route_kernel(const uint16_t* chars, const uint64_t* off, uint64_t n, int32_t nshards,
+                                                   int32_t* hash_out, int32_t* shard_out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const int32_t h = (int32_t)murmur3_x86_32_utf16(chars + off[i], (int)(off[i + 1] - off[i]), 0);
+        if (hash_out) hash_out[i] = h;
+        shard_out[i] = routing_shard(h, nshards);
+    }
+}
+void launch_route(const uint16_t* chars, const uint64_t* offsets, uint64_t n, int32_t nshards, int32_t* hash_out,
+                  int32_t* shard_out, hipStream_t st) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(route_kernel, dim3((uint32_t)std::min<uint64_t>(8192, (n + 255) / 256)), dim3(256), 0, st, chars, offsets, n,
+                       nshards, hash_out, shard_out);
+}
+__global__ __launch_bounds__(256) void murmur3_field_kernel(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint64_t* h1_out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t h1, h2;
+        murmur3_x64_128(bytes + off[i], (int)(off[i + 1] - off[i]), 0, &h1, &h2);
+        h1_out[i] = h1;
+    }
+}
+void launch_murmur3_field(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint64_t* h1_out, hipStream_t st) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(murmur3_field_kernel, dim3((uint32_t)std::min<uint64_t>(8192, (n + 255) / 256)), dim3(256), 0, st, bytes,
+                       offsets, n, h1_out);
+}
+
 __global__ __launch_bounds__(256) void minmax_i64_kernel(const int64_t* v, uint64_t n, int64_t* out, int f64) {
     int64_t mn = INT64_MAX, mx = INT64_MIN;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {

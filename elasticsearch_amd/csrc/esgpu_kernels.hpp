@@ -160,6 +160,13 @@ void launch_card_nonzero(const uint8_t* regs, uint64_t n_buckets, int p, uint32_
 // out[i*row ... ] = src[cells[i]*row ...] (bytes), for the cells of the emitted buckets
 void launch_gather_bytes(const uint32_t* cells, uint32_t n, uint32_t row_bytes, const uint8_t* src, uint8_t* dst, hipStream_t s);
 
+// ---- index-time hashing (bulk ingest helpers) ----
+// shard of each _id / routing value: MathUtils.mod(murmur3_x86_32(UTF-16LE(id)), nshards) (OperationRouting.java:238-258)
+void launch_route(const uint16_t* chars, const uint64_t* offsets, uint64_t n, int32_t nshards, int32_t* hash_out,
+                  int32_t* shard_out, hipStream_t s);
+// murmur3 field values: MurmurHash3.hash128(utf8 bytes, seed 0).h1 per value (Murmur3FieldMapper.java:152-165)
+void launch_murmur3_field(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint64_t* h1_out, hipStream_t s);
+
 // min / max over a value array (multi-valued i64 columns: key range of a histogram), out[0] = min, out[1] = max
 void launch_minmax_i64(const int64_t* v, uint64_t n, int64_t* out, bool f64, hipStream_t s);
 void launch_remap_ords(const uint32_t* in, uint32_t n, const uint32_t* map, uint32_t map_n, uint32_t* out, hipStream_t s);

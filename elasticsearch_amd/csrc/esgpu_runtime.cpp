@@ -689,6 +689,66 @@ extern "C" int esgpu_date_rounding(const esgpu_agg_spec* spec, int32_t op, int64
     });
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// index-time hashing (bulk ingest helpers)
+// ------------------------------------------------------------------------------------------------------------
+extern "C" int esgpu_routing_hash(const uint16_t* chars, size_t nchars, int32_t* hash) {
+    return guarded([&] {
+        require(hash && (chars || nchars == 0), ESGPU_ERR_INVALID, "null argument");
+        require(nchars < (1u << 30), ESGPU_ERR_INVALID, "routing value too long");
+        *hash = (int32_t)murmur3_x86_32_utf16(chars, (int)nchars, 0);
+    });
+}
+
+// host CSR arrays -> device, kernel, results -> host (one synchronous round trip per batch)
+template <class In, class Out, class Launch>
+static void batch_hash(esgpu_ctx* c, const In* data, const uint64_t* offsets, uint64_t n, Out* out, Out* out2, Launch&& launch) {
+    require(offsets && out && (data || n == 0), ESGPU_ERR_INVALID, "null argument");
+    require(offsets[0] == 0, ESGPU_ERR_INVALID, "CSR offsets must start at 0");
+    for (uint64_t i = 0; i < n; ++i) {
+        require(offsets[i] <= offsets[i + 1], ESGPU_ERR_INVALID, "CSR offsets must be non-decreasing");
+        require(offsets[i + 1] - offsets[i] < (1u << 30), ESGPU_ERR_INVALID, "value too long");
+    }
+    if (n == 0) return;
+    HIPX(hipSetDevice(c->device));
+    const uint64_t units = offsets[n];
+    DevBuf d_data, d_off, d_out, d_out2;
+    d_data.alloc(c, std::max<uint64_t>(units, 1) * sizeof(In));
+    d_off.alloc(c, (n + 1) * 8);
+    d_out.alloc(c, n * sizeof(Out));
+    if (out2) d_out2.alloc(c, n * sizeof(Out));
+    if (units) HIPX(hipMemcpyAsync(d_data.p, data, units * sizeof(In), hipMemcpyHostToDevice, c->stream));
+    HIPX(hipMemcpyAsync(d_off.p, offsets, (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    launch(d_data.as<In>(), d_off.as<uint64_t>(), d_out.as<Out>(), out2 ? d_out2.as<Out>() : nullptr);
+    HIPX(hipGetLastError());
+    HIPX(hipMemcpyAsync(out, d_out.p, n * sizeof(Out), hipMemcpyDeviceToHost, c->stream));
+    if (out2) HIPX(hipMemcpyAsync(out2, d_out2.p, n * sizeof(Out), hipMemcpyDeviceToHost, c->stream));
+    HIPX(hipStreamSynchronize(c->stream));
+}
+
+extern "C" int esgpu_route_shards(esgpu_ctx* c, const uint16_t* chars, const uint64_t* offsets, uint64_t n, int32_t nshards,
+                                  int32_t* hashes_out, int32_t* shards_out) {
+    return guarded([&] {
+        require(c != nullptr && nshards >= 1, ESGPU_ERR_INVALID, "bad routing arguments");
+        std::lock_guard<std::mutex> lk(c->mu);
+        batch_hash<uint16_t, int32_t>(c, chars, offsets, n, shards_out, hashes_out,
+                                      [&](const uint16_t* d, const uint64_t* o, int32_t* shards, int32_t* hashes) {
+                                          launch_route(d, o, n, nshards, hashes, shards, c->stream);
+                                      });
+    });
+}
+
+extern "C" int esgpu_murmur3_field(esgpu_ctx* c, const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint64_t* h1_out) {
+    return guarded([&] {
+        require(c != nullptr, ESGPU_ERR_INVALID, "null context");
+        std::lock_guard<std::mutex> lk(c->mu);
+        batch_hash<uint8_t, uint64_t>(c, bytes, offsets, n, h1_out, (uint64_t*)nullptr,
+                                      [&](const uint8_t* d, const uint64_t* o, uint64_t* h1, uint64_t*) {
+                                          launch_murmur3_field(d, o, n, h1, c->stream);
+                                      });
+    });
+}
+
 extern "C" int esgpu_precision_from_threshold(int64_t count, int32_t* precision) {
     return guarded([&] { *precision = hll_precision_from_threshold(count); });
 }

@@ -287,6 +287,28 @@ class Engine:
     def plan(self, aggs, filters=None, number_of_shards=1, ord_lookup=None):
         return Plan(self, aggs, filters, number_of_shards, ord_lookup)
 
+    def route_shards(self, ids, number_of_shards, with_hashes=False):
+        """Shard of each _id / routing string (OperationRouting.shardId, Murmur3HashFunction), computed on the GPU."""
+        units = [np.frombuffer(s.encode("utf-16-le"), dtype=np.uint16) for s in ids]
+        offs = np.zeros(len(ids) + 1, dtype=np.uint64)
+        offs[1:] = np.cumsum([len(u) for u in units]) if units else []
+        chars = np.ascontiguousarray(np.concatenate(units) if units else np.zeros(1, np.uint16))
+        shards = np.zeros(max(len(ids), 1), dtype=np.int32)
+        hashes = np.zeros(max(len(ids), 1), dtype=np.int32)
+        N.check(N.lib().esgpu_route_shards(self._ptr, chars.ctypes.data, offs.ctypes.data, len(ids), number_of_shards,
+                                           hashes.ctypes.data if with_hashes else None, shards.ctypes.data))
+        return (shards[:len(ids)], hashes[:len(ids)]) if with_hashes else shards[:len(ids)]
+
+    def murmur3_field(self, values):
+        """The murmur3 field's indexed long of each string value (MurmurHash3.hash128(utf8, 0).h1), on the GPU."""
+        b = [v.encode("utf-8") if isinstance(v, str) else bytes(v) for v in values]
+        offs = np.zeros(len(b) + 1, dtype=np.uint64)
+        offs[1:] = np.cumsum([len(x) for x in b]) if b else []
+        blob = np.frombuffer(b"".join(b) or b"\0", dtype=np.uint8).copy()
+        out = np.zeros(max(len(b), 1), dtype=np.uint64)
+        N.check(N.lib().esgpu_murmur3_field(self._ptr, blob.ctypes.data, offs.ctypes.data, len(b), out.ctypes.data))
+        return out[:len(b)]
+
     def close(self):
         if self._ptr:
             N.check(N.lib().esgpu_ctx_destroy(self._ptr))
@@ -315,6 +337,14 @@ def synthetic_terms(field, n):
         N.lib().esgpu_synthetic_term(N.SYNTH_FIELDS[field], o, buf, 64)
         out.append(buf.value.decode())
     return out
+
+
+def routing_hash(routing):
+    """Murmur3HashFunction.hash(routing): murmur3_x86_32 of the string's UTF-16LE bytes (host, no GPU needed)."""
+    u = np.frombuffer(routing.encode("utf-16-le"), dtype=np.uint16).copy()
+    out = ctypes.c_int32()
+    N.check(N.lib().esgpu_routing_hash(u.ctypes.data if u.size else None, u.size, ctypes.byref(out)))
+    return out.value
 
 
 def precision_from_threshold(t):

@@ -271,6 +271,22 @@ int esgpu_date_rounding(const esgpu_agg_spec* spec, int32_t op, int64_t value, i
  * (plugins/mapper-murmur3/.../Murmur3FieldMapper.java:152-165). */
 int esgpu_murmur3_x64_128(const uint8_t* bytes, size_t len, int64_t seed, uint64_t* out2);
 
+/* ---------------------------------------------------------------------------------------------------------
+ * Index-time hashing for bulk ingest: the shard a document routes to, and the murmur3 field value
+ * stored for it, so that shards built outside Elasticsearch match the ones it would build from the same _ids / values.
+ *   esgpu_routing_hash: Murmur3HashFunction.hash(routing) = StringHelper.murmurhash3_x86_32 over the UTF-16LE bytes of
+ *                       the string (cluster/routing/Murmur3HashFunction.java:31-41); chars = Java UTF-16 code units.
+ *   esgpu_route_shards: for n strings (CSR over UTF-16 units, host memory) the shard
+ *                       MathUtils.mod(hash, number_of_shards) (cluster/routing/OperationRouting.java:238-258), on the GPU;
+ *                       hashes_out may be NULL.
+ *   esgpu_murmur3_field: for n values (CSR over UTF-8 bytes, host memory) MurmurHash3.hash128(bytes, 0).h1, the long
+ *                       the murmur3 field mapper indexes (plugins/mapper-murmur3/.../Murmur3FieldMapper.java:152-165).
+ * ------------------------------------------------------------------------------------------------------- */
+int esgpu_routing_hash(const uint16_t* chars, size_t nchars, int32_t* hash);
+int esgpu_route_shards(esgpu_ctx* ctx, const uint16_t* chars, const uint64_t* offsets, uint64_t n, int32_t number_of_shards,
+                       int32_t* hashes_out, int32_t* shards_out);
+int esgpu_murmur3_field(esgpu_ctx* ctx, const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint64_t* h1_out);
+
 typedef struct esgpu_plan esgpu_plan;
 
 /* = AggregationPhase.preProcess + AggregatorFactories.createTopLevelAggregators (AggregationPhase.java:69-94). */

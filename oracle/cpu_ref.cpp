@@ -1435,6 +1435,38 @@ int64_t oracle_index(uint64_t h, int32_t p) { return oracle::hll_index(h, p); }
 int32_t oracle_run_len(uint64_t h, int32_t p) { return oracle::run_len(h, p); }
 
 /* Rounding KATs: kind 0 histogram Interval, 1 date unit, 2 date interval; returns round(v) / next(v) / roundKey(v) */
+/* Lucene StringHelper.murmurhash3_x86_32 (third-party, Lucene 5.4) over the UTF-16LE bytes of a Java string, as
+ * Murmur3HashFunction.hash (cluster/routing/Murmur3HashFunction.java:31-41); pinned by Murmur3HashFunctionTests. */
+int32_t oracle_routing_hash(const uint16_t* chars, int32_t n) {
+    std::vector<uint8_t> b((size_t)n * 2);
+    for (int32_t i = 0; i < n; ++i) { b[2 * i] = (uint8_t)chars[i]; b[2 * i + 1] = (uint8_t)(chars[i] >> 8); }
+    const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
+    uint32_t h1 = 0;
+    const int len = (int)b.size(), rounded = len & ~3;
+    for (int i = 0; i < rounded; i += 4) {
+        uint32_t k1 = (b[i] & 0xff) | ((b[i + 1] & 0xff) << 8) | ((b[i + 2] & 0xff) << 16) | ((uint32_t)b[i + 3] << 24);
+        k1 *= c1; k1 = (k1 << 15) | (k1 >> 17); k1 *= c2;
+        h1 ^= k1; h1 = (h1 << 13) | (h1 >> 19); h1 = h1 * 5 + 0xe6546b64u;
+    }
+    uint32_t k1 = 0;
+    const int tail = len & 3;
+    if (tail == 3) k1 = (uint32_t)(b[rounded + 2] & 0xff) << 16;
+    if (tail >= 2) k1 |= (uint32_t)(b[rounded + 1] & 0xff) << 8;
+    if (tail >= 1) {
+        k1 |= (b[rounded] & 0xff);
+        k1 *= c1; k1 = (k1 << 15) | (k1 >> 17); k1 *= c2; h1 ^= k1;
+    }
+    h1 ^= (uint32_t)len;
+    h1 ^= h1 >> 16; h1 *= 0x85ebca6bu; h1 ^= h1 >> 13; h1 *= 0xc2b2ae35u; h1 ^= h1 >> 16;
+    return (int32_t)h1;
+}
+/* OperationRouting.shardId (indices created on or after 2.0): MathUtils.mod(hash, numberOfShards) */
+int32_t oracle_shard_id(int32_t hash, int32_t nshards) {
+    int32_t r = hash % nshards;
+    if (r < 0) r += nshards;
+    return r;
+}
+
 int64_t oracle_rounding_tz(int32_t kind, int32_t unit, int64_t interval, int64_t offset, const int64_t* tz_starts,
                            const int64_t* tz_offs, int32_t tz_count, int32_t op, int64_t v) {
     oracle::Rounding r;

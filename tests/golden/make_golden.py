@@ -56,6 +56,19 @@ def murmur3_vectors(ref):
     return out
 
 
+def routing_vectors(ref):
+    """Murmur3HashFunction.hash known values (Murmur3HashFunctionTests.testKnownValues)."""
+    rel = T + "cluster/routing/operation/hash/murmur3/Murmur3HashFunctionTests.java"
+    text = _read(ref, rel)
+    out = []
+    for m in re.finditer(r'assertHash\((0x[0-9a-fA-F]+), "([^"]*)"\);', text):
+        v = int(m.group(1), 16)
+        out.append({"input": m.group(2), "hash": v - (1 << 32) if v >> 31 else v,
+                    "cite": f"{rel}:{text.count(chr(10), 0, m.start()) + 1}"})
+    assert len(out) == 7, out
+    return out
+
+
 def precision_vectors(ref):
     rel = T + "search/aggregations/metrics/cardinality/HyperLogLogPlusPlusTests.java"
     text = _read(ref, rel)
@@ -329,6 +342,7 @@ def main():
         return 0
     kat = {"murmur3_x64_128": murmur3_vectors(ref),
            "precision_from_threshold": precision_vectors(ref),
+           "routing_murmur3_x86_32": routing_vectors(ref),
            "rounding": rounding_vectors(ref),
            "rounding_tz": rounding_tz_vectors(ref),
            "stats": stats_fixtures(ref),

@@ -339,3 +339,27 @@ def test_keyword_range_filters(engine):
         assert_same(plan.build().to_dict(), want["shards"][0], "shard")
         plan.close()
     seg.close()
+
+
+def test_index_time_hashing(engine):
+    """Bulk ingest helpers on the GPU: shard routing of _ids (Murmur3HashFunction + MathUtils.mod) against the oracle,
+    and murmur3 field values against MurmurHash3.hash128(...).h1 -- the device-generated client_ip.hash column is the
+    murmur3 field of the generated IP strings."""
+    import ctypes
+    from test_oracle_kat import oracle_routing_hash, oracle_shard_id
+    rng = np.random.default_rng(17)
+    ids = ["doc-%d-%s" % (i, "x" * int(rng.integers(0, 9))) for i in range(20_000)] + ["", "é中\U0001F600"]
+    for nshards in (1, 5, 8):
+        shards, hashes = engine.route_shards(ids, nshards, with_hashes=True)
+        for i in range(0, len(ids), 97):
+            h = oracle_routing_hash(ids[i])
+            assert hashes[i] == h and shards[i] == oracle_shard_id(h, nshards), ids[i]
+        assert shards.min() >= 0 and shards.max() < nshards
+    vals = ["10.%d.%d.%d" % tuple(rng.integers(0, 256, size=3)) for _ in range(5000)] + ["", "a" * 37]
+    got = engine.murmur3_field(vals)
+    L = O.lib()
+    for i, v in enumerate(vals):
+        b = v.encode()
+        h1, h2 = ctypes.c_uint64(), ctypes.c_uint64()
+        L.oracle_murmur3_128(b, len(b), 0, ctypes.byref(h1), ctypes.byref(h2))
+        assert int(got[i]) == h1.value, v

@@ -270,3 +270,17 @@ def test_date_rounding_matches_oracle_across_zones():
             for op in (0, 1, 2):
                 assert product_round(sp, op, v) == oracle_round_tz(kind, unit, interval, offset, zone, op, v), \
                     (zone, kind, unit, interval, offset, op, v)
+
+
+def test_routing_hash_matches_kats_and_oracle(kat):
+    """Product Murmur3HashFunction (host path) == the reference's KATs, and == the oracle on random strings including
+    odd lengths, non-ASCII and surrogate pairs (UTF-16 code units, as Java's String.charAt)."""
+    from elasticsearch_amd import routing_hash
+    from test_oracle_kat import oracle_routing_hash
+    for v in kat["routing_murmur3_x86_32"]:
+        assert routing_hash(v["input"]) == v["hash"], v["cite"]
+    rng = np.random.default_rng(3)
+    alphabet = list("abcdefghijklmnopqrstuvwxyz0123456789-_") + ["é", "ß", "中", "文", "\U0001F600"]
+    for i in range(400):
+        s = "".join(rng.choice(alphabet, size=int(rng.integers(0, 40))))
+        assert routing_hash(s) == oracle_routing_hash(s), s

@@ -212,3 +212,24 @@ def test_date_histogram_fixture(kat):  # DateHistogramTests.singleValuedField / 
     res = O.run([(cols, 6)], [AB.dateHistogram("histo").field("date").interval("day").minDocCount(1).timeZone("+01:00")])
     b = res["reduced"]["histo"]["buckets"]
     assert [x["key"] for x in b] == tz["keys"] and [x["doc_count"] for x in b] == tz["doc_counts"]
+
+
+def oracle_routing_hash(s):
+    L = O.lib()
+    L.oracle_routing_hash.restype = ctypes.c_int32
+    L.oracle_routing_hash.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+    u = np.frombuffer(s.encode("utf-16-le"), dtype=np.uint16).copy()
+    return L.oracle_routing_hash(u.ctypes.data if u.size else None, u.size)
+
+
+def oracle_shard_id(h, n):
+    L = O.lib()
+    L.oracle_shard_id.restype = ctypes.c_int32
+    L.oracle_shard_id.argtypes = [ctypes.c_int32, ctypes.c_int32]
+    return L.oracle_shard_id(h, n)
+
+
+def test_routing_murmur3_known_values(kat):  # Murmur3HashFunctionTests.testKnownValues
+    for v in kat["routing_murmur3_x86_32"]:
+        assert oracle_routing_hash(v["input"]) == v["hash"], v["cite"]
+    assert oracle_shard_id(-7, 5) == 3 and oracle_shard_id(7, 5) == 2  # MathUtils.mod: floor modulo
