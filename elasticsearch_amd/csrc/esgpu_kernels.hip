@@ -199,11 +199,12 @@ struct Acc {
     uint32_t* vcnt32;
     unsigned long long* vcnt64;
     double* sum;
-    unsigned long long* mn;
+    unsigned long long* mn;         // LDS: min / max interleaved (mx == mn + 1, stride 2): one ds_read2_b64 per check
     unsigned long long* mx;
     double* sq;
     uint32_t* ocnt32;
     unsigned long long* ocnt64;
+    uint32_t mstride;               // 2 in LDS, 1 in the global grid
 };
 
 template <int MET, bool LDS>
@@ -220,8 +221,10 @@ __device__ __forceinline__ void add_value(const Acc& a, uint32_t c, double x, bo
         const unsigned long long emn = nan ? 0ull : e;
         const unsigned long long emx = nan ? ~0ull : e;
         // read-check before the atomic: reads of one address broadcast, and min/max converge quickly
-        if (emn < a.mn[c]) atomicMin(&a.mn[c], emn);
-        if (emx > a.mx[c]) atomicMax(&a.mx[c], emx);
+        constexpr uint32_t st = LDS ? 2 : 1;
+        const unsigned long long cmn = a.mn[c * st], cmx = a.mx[c * st];
+        if (emn < cmn) atomicMin(&a.mn[c * st], emn);
+        if (emx > cmx) atomicMax(&a.mx[c * st], emx);
     }
     if (MET >= 3) atomicAdd(&a.sq[c], x * x);  // ExtendedStatsAggregator: sumOfSqr += value * value (no FMA)
 }
@@ -326,8 +329,9 @@ __device__ __forceinline__ void run_flush(const CollectParams& P, const Acc& a, 
             if (P.vcnt_mode) atomicAdd(&a.vcnt32[c], r.vc);
             atomicAdd(&a.sum[c], r.sum);
             if (MET >= 2) {
-                if (r.mn < a.mn[c]) atomicMin(&a.mn[c], r.mn);
-                if (r.mx > a.mx[c]) atomicMax(&a.mx[c], r.mx);
+                const unsigned long long cmn = a.mn[2 * c], cmx = a.mx[2 * c];  // LDS, interleaved
+                if (r.mn < cmn) atomicMin(&a.mn[2 * c], r.mn);
+                if (r.mx > cmx) atomicMax(&a.mx[2 * c], r.mx);
             }
             if (MET >= 3) atomicAdd(&a.sq[c], r.sq);
         }
@@ -417,11 +421,11 @@ __device__ void flush_window(const CollectParams& P, const Acc& s, uint32_t T, u
             atomicAdd(&P.g_sum[g], s.sum[c]);
             s.sum[c] = 0.0;
             if (MET >= 2) {
-                const unsigned long long mn = s.mn[c], mx = s.mx[c];
+                const unsigned long long mn = s.mn[2 * c], mx = s.mx[2 * c];
                 if (mn != kMinInit) atomicMin(&P.g_min[g], mn);
                 if (mx != kMaxInit) atomicMax(&P.g_max[g], mx);
-                s.mn[c] = kMinInit;
-                s.mx[c] = kMaxInit;
+                s.mn[2 * c] = kMinInit;
+                s.mx[2 * c] = kMaxInit;
             }
             if (MET >= 3) { atomicAdd(&P.g_sq[g], s.sq[c]); s.sq[c] = 0.0; }
         }
@@ -454,6 +458,7 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
     Acc g;  // global grid view
     g.cnt32 = nullptr; g.vcnt32 = nullptr; g.ocnt32 = nullptr;
     g.cnt64 = P.g_cnt; g.vcnt64 = P.g_vcnt; g.sum = P.g_sum; g.mn = P.g_min; g.mx = P.g_max; g.sq = P.g_sq;
+    g.mstride = 1;
     g.ocnt64 = P.g_ocnt;
 
     // LDS window view.  Every pointer is derived from `smem` alone -- never merged with a global pointer -- so the
@@ -467,8 +472,9 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
         s.cnt32 = (uint32_t*)carve(sizeof(uint32_t) * C);
         s.vcnt32 = (uint32_t*)carve(P.vcnt_mode ? sizeof(uint32_t) * C : 0);
         s.sum = (double*)carve(MET > 0 ? sizeof(double) * C : 0);
-        s.mn = (unsigned long long*)carve(MET >= 2 ? 8 * C : 0);
-        s.mx = (unsigned long long*)carve(MET >= 2 ? 8 * C : 0);
+        s.mn = (unsigned long long*)carve(MET >= 2 ? 16 * C : 0);
+        s.mx = s.mn + 1;
+        s.mstride = 2;
         s.sq = (double*)carve(MET >= 3 ? sizeof(double) * C : 0);
         s.ocnt32 = (uint32_t*)carve(P.ocnt_mode == OCNT_TERMS ? sizeof(uint32_t) * T
                                     : P.ocnt_mode == OCNT_HIST ? sizeof(uint32_t) * W : 0);
@@ -478,7 +484,7 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
             s.cnt32[c] = 0;
             if (P.vcnt_mode) s.vcnt32[c] = 0;
             if (MET > 0) s.sum[c] = 0.0;
-            if (MET >= 2) { s.mn[c] = kMinInit; s.mx[c] = kMaxInit; }
+            if (MET >= 2) { s.mn[2 * c] = kMinInit; s.mx[2 * c] = kMaxInit; }
             if (MET >= 3) s.sq[c] = 0.0;
         }
         if (P.ocnt_mode == OCNT_TERMS || P.ocnt_mode == OCNT_HIST)
@@ -609,7 +615,7 @@ size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocn
     size_t bytes = r(4 * C);
     if (vcnt_mode) bytes += r(4 * C);
     if (met > 0) bytes += r(8 * C);
-    if (met >= 2) bytes += 2 * r(8 * C);
+    if (met >= 2) bytes += r(16 * C);
     if (met >= 3) bytes += r(8 * C);
     if (ocnt_mode == OCNT_TERMS) bytes += r(4 * (size_t)T);
     if (ocnt_mode == OCNT_HIST) bytes += r(4 * (size_t)W);
@@ -1543,6 +1549,7 @@ __global__ __launch_bounds__(kWG) void collect_multi_kernel(CollectParams P) {
     Acc g;
     g.cnt32 = nullptr; g.vcnt32 = nullptr; g.ocnt32 = nullptr;
     g.cnt64 = P.g_cnt; g.vcnt64 = P.g_vcnt; g.sum = P.g_sum; g.mn = P.g_min; g.mx = P.g_max; g.sq = P.g_sq;
+    g.mstride = 1;
     g.ocnt64 = P.g_ocnt;
     Acc s;
     {
@@ -1552,8 +1559,9 @@ __global__ __launch_bounds__(kWG) void collect_multi_kernel(CollectParams P) {
         s.cnt32 = (uint32_t*)carve(sizeof(uint32_t) * C);
         s.vcnt32 = (uint32_t*)carve(P.vcnt_mode ? sizeof(uint32_t) * C : 0);
         s.sum = (double*)carve(MET > 0 ? sizeof(double) * C : 0);
-        s.mn = (unsigned long long*)carve(MET >= 2 ? 8 * C : 0);
-        s.mx = (unsigned long long*)carve(MET >= 2 ? 8 * C : 0);
+        s.mn = (unsigned long long*)carve(MET >= 2 ? 16 * C : 0);
+        s.mx = s.mn + 1;
+        s.mstride = 2;
         s.sq = (double*)carve(MET >= 3 ? sizeof(double) * C : 0);
         s.ocnt32 = (uint32_t*)carve(P.ocnt_mode == OCNT_TERMS ? sizeof(uint32_t) * T : P.ocnt_mode == OCNT_HIST ? sizeof(uint32_t) * H : 0);
     }
@@ -1562,7 +1570,7 @@ __global__ __launch_bounds__(kWG) void collect_multi_kernel(CollectParams P) {
             s.cnt32[c] = 0;
             if (P.vcnt_mode) s.vcnt32[c] = 0;
             if (MET > 0) s.sum[c] = 0.0;
-            if (MET >= 2) { s.mn[c] = kMinInit; s.mx[c] = kMaxInit; }
+            if (MET >= 2) { s.mn[2 * c] = kMinInit; s.mx[2 * c] = kMaxInit; }
             if (MET >= 3) s.sq[c] = 0.0;
         }
         if (P.ocnt_mode == OCNT_TERMS || P.ocnt_mode == OCNT_HIST)
@@ -1634,8 +1642,8 @@ __global__ __launch_bounds__(kWG) void collect_multi_kernel(CollectParams P) {
                     }
                     atomicAdd(&a.sum[c], msum);
                     if (MET >= 2) {
-                        if (emn < a.mn[c]) atomicMin(&a.mn[c], emn);
-                        if (emx > a.mx[c]) atomicMax(&a.mx[c], emx);
+                        if (emn < a.mn[c * a.mstride]) atomicMin(&a.mn[c * a.mstride], emn);
+                        if (emx > a.mx[c * a.mstride]) atomicMax(&a.mx[c * a.mstride], emx);
                     }
                     if (MET >= 3) atomicAdd(&a.sq[c], msq);
                 }
