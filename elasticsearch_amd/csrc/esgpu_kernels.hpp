@@ -105,6 +105,7 @@ struct HllParams {
     unsigned int* nonzero;      // written by the register pass: registers != 0
     unsigned int* floor;        // scratch: min register after a phase
     unsigned char* gfloor;      // scratch: min register of each group of 64 registers after a phase ([max(m / 64, 1)])
+    unsigned char* snap;        // scratch: registers as 4-bit lower bounds over the floor ([2^p / 2], 16-byte aligned)
     uint32_t lc_mask;
     uint32_t lc_threshold;
 };

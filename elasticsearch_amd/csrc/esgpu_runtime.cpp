@@ -1558,6 +1558,8 @@ static void ensure_ord_hash(esgpu_ctx* c, const DevColumn* col, hipStream_t st) 
     HIPX(hipStreamSynchronize(st));
 }
 
+static size_t hll_snap_offset(uint32_t m) { return (16 + std::max<size_t>(m / 64, 1) + 15) & ~(size_t)15; }
+
 static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
     const DevColumn* col = s->col(pl.metric_field.c_str());
     if (!col) return false;
@@ -1571,7 +1573,8 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
         pl.lc_mask = cap - 1;
         pl.lc_set.alloc(p->ctx, (size_t)cap * 4);
         HIPX(hipMemsetAsync(pl.lc_set.p, 0, (size_t)cap * 4, p->stream));
-        pl.lc_count.alloc(p->ctx, 16 + std::max<size_t>(m / 64, 1));  // counters, then the group floors
+        // counters, then the group floors, then the packed register snapshot (16-byte aligned)
+        pl.lc_count.alloc(p->ctx, hll_snap_offset(m) + std::max<size_t>(m / 2, 16));
         HIPX(hipMemsetAsync(pl.lc_count.p, 0, 16, p->stream));
         pl.allocated = true;
     }
@@ -1625,6 +1628,7 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
     H.nonzero = pl.lc_count.as<unsigned int>() + 1;
     H.floor = pl.lc_count.as<unsigned int>() + 2;
     H.gfloor = pl.lc_count.as<unsigned char>() + 16;
+    H.snap = pl.lc_count.as<unsigned char>() + hll_snap_offset(1u << pl.p);
     H.lc_mask = pl.lc_mask;
     H.lc_threshold = pl.lc_threshold;
     if (H.n_docs == 0) return false;
