@@ -15,6 +15,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #include "es_common.hpp"
@@ -163,7 +164,9 @@ __device__ __forceinline__ uint32_t eval_pred(const PredDev& q, uint32_t doc0) {
     return m;
 }
 
-template <bool ORD, bool HIST, int MET>
+// VK (value kinds, compile time): bit 0 = the histogram column holds doubles (keys are (long) casts), bit 1 = the
+// metric column holds doubles (else longs cast to double).  A runtime branch on these cost the north-star kernel ~6 %.
+template <bool ORD, bool HIST, int MET, int VK>
 __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0, Doc4& d) {
     uint32_t ok = 0xF;
     if (doc0 + 4 > P.n_docs) ok = doc0 >= P.n_docs ? 0u : ((1u << (P.n_docs - doc0)) - 1u);
@@ -173,14 +176,14 @@ __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0,
     if (ORD) load_u32x4(P.ord, doc0, d.ord);
     if (HIST) {
         load_i64x4(P.hv, doc0, d.hv);
-        if (P.hv_f64) {
+        if (VK & 1) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) d.hv[j] = java_long(bits_dbl((uint64_t)d.hv[j]));
         }
         d.hpres = P.hv_present ? bits4(P.hv_present, doc0) : 0xFu;
     }
     if (MET > 0) {
-        if (P.mv_f64) {
+        if (VK & 2) {
             load_f64x4((const double*)P.mv, doc0, d.mv);
         } else {
             int64_t t[4];
@@ -446,7 +449,7 @@ __device__ void flush_window(const CollectParams& P, const Acc& s, uint32_t T, u
 }
 
 // HK: 0 = no histogram dimension, 1 = affine rounding, 2 = bucket table (calendar units / DST zones)
-template <bool ORD, int HK, int MET>
+template <bool ORD, int HK, int MET, int VK>
 __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
     constexpr bool HIST = HK != 0;
     constexpr bool KT = HK == 2;
@@ -518,7 +521,7 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
     Doc4 q[kPrefetch];
 #pragma unroll
     for (int k = 0; k < kPrefetch; ++k)
-        if ((uint32_t)k < n_it) load_docs<ORD, HIST, MET>(P, doc_of(k), q[k]);
+        if ((uint32_t)k < n_it) load_docs<ORD, HIST, MET, VK>(P, doc_of(k), q[k]);
 
     bool use_lds = P.lds_mode != 0;
     for (uint32_t i = 0; i < n_it; ++i) {
@@ -547,7 +550,7 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
             }
         }
         Doc4 nxt;
-        if (i + kPrefetch < n_it) load_docs<ORD, HIST, MET>(P, doc_of(i + kPrefetch), nxt);
+        if (i + kPrefetch < n_it) load_docs<ORD, HIST, MET, VK>(P, doc_of(i + kPrefetch), nxt);
         if (use_lds) {
             process4<ORD, HIST, MET, true, KT, kMS>(P, s, q[0], T, base, win0, run);
             dirty = true;
@@ -564,9 +567,33 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
     }
 }
 
+// calls f(std::integral_constant<int, VK>) for the value kinds the plan uses; bits that cannot matter (no histogram
+// dimension, no metric) are never instantiated
+template <int HK, int MET, class F>
+static auto with_vk(bool hv_f64, bool mv_f64, F f) {
+    const bool hf = HK != 0 && hv_f64, mf = MET > 0 && mv_f64;
+    if constexpr (HK != 0 && MET > 0) {
+        if (hf && mf) return f(std::integral_constant<int, 3>{});
+        if (hf) return f(std::integral_constant<int, 1>{});
+        if (mf) return f(std::integral_constant<int, 2>{});
+        return f(std::integral_constant<int, 0>{});
+    } else if constexpr (HK != 0) {
+        if (hf) return f(std::integral_constant<int, 1>{});
+        return f(std::integral_constant<int, 0>{});
+    } else if constexpr (MET > 0) {
+        if (mf) return f(std::integral_constant<int, 2>{});
+        return f(std::integral_constant<int, 0>{});
+    } else {
+        return f(std::integral_constant<int, 0>{});
+    }
+}
+
 template <bool ORD, int HK, int MET>
 static void launch_t(const CollectParams& p, uint32_t grid, size_t lds, hipStream_t st) {
-    hipLaunchKernelGGL((collect_kernel<ORD, HK, MET>), dim3(grid), dim3(kWG), lds, st, p);
+    with_vk<HK, MET>(p.hv_f64 != 0, p.mv_f64 != 0, [&](auto vk) {
+        hipLaunchKernelGGL((collect_kernel<ORD, HK, MET, decltype(vk)::value>), dim3(grid), dim3(kWG), lds, st, p);
+        return 0;
+    });
 }
 
 template <bool ORD, int HK>
@@ -593,23 +620,27 @@ void launch_collect(const CollectParams& p, bool ord, bool hist, int met, uint32
 }
 
 template <bool ORD, int HK, int MET>
-static int occ_t(size_t lds) {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, collect_kernel<ORD, HK, MET>, kWG, lds) != hipSuccess) n = 1;
-    return n;
+static int occ_t(size_t lds, int vkbits) {
+    return with_vk<HK, MET>((vkbits & 1) != 0, (vkbits & 2) != 0, [&](auto vk) {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, collect_kernel<ORD, HK, MET, decltype(vk)::value>, kWG, lds) !=
+            hipSuccess)
+            n = 1;
+        return n;
+    });
 }
 template <bool ORD, int HK>
-static int occ_m(int met, size_t lds) {
+static int occ_m(int met, size_t lds, int vk) {
     switch (met) {
-        case 0: return occ_t<ORD, HK, 0>(lds);
-        case 1: return occ_t<ORD, HK, 1>(lds);
-        case 2: return occ_t<ORD, HK, 2>(lds);
-        default: return occ_t<ORD, HK, 3>(lds);
+        case 0: return occ_t<ORD, HK, 0>(lds, vk);
+        case 1: return occ_t<ORD, HK, 1>(lds, vk);
+        case 2: return occ_t<ORD, HK, 2>(lds, vk);
+        default: return occ_t<ORD, HK, 3>(lds, vk);
     }
 }
-int collect_occupancy(bool ord, int hk, int met, size_t lds) {
-    if (ord) return hk == 2 ? occ_m<true, 2>(met, lds) : hk == 1 ? occ_m<true, 1>(met, lds) : occ_m<true, 0>(met, lds);
-    return hk == 2 ? occ_m<false, 2>(met, lds) : hk == 1 ? occ_m<false, 1>(met, lds) : occ_m<false, 0>(met, lds);
+int collect_occupancy(bool ord, int hk, int met, size_t lds, int vk) {
+    if (ord) return hk == 2 ? occ_m<true, 2>(met, lds, vk) : hk == 1 ? occ_m<true, 1>(met, lds, vk) : occ_m<true, 0>(met, lds, vk);
+    return hk == 2 ? occ_m<false, 2>(met, lds, vk) : hk == 1 ? occ_m<false, 1>(met, lds, vk) : occ_m<false, 0>(met, lds, vk);
 }
 
 size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode) {

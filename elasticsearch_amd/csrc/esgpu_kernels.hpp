@@ -124,7 +124,8 @@ void launch_zone_map(const int64_t* v, const uint64_t* present, uint32_t n, int6
 void launch_synth(const SynthParams& p, hipStream_t s);
 void launch_collect(const CollectParams& p, bool ord, bool hist, int met, uint32_t grid, size_t lds, hipStream_t s);
 size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode);
-int collect_occupancy(bool ord, int hk, int met, size_t lds);  // resident workgroups per CU (hk: 0 none, 1 affine, 2 table)
+// resident workgroups per CU (hk: 0 none, 1 affine, 2 table; vk: bit 0 double histogram column, bit 1 double metric)
+int collect_occupancy(bool ord, int hk, int met, size_t lds, int vk);
 void launch_hll(const HllParams& p, uint32_t cus, hipStream_t s);
 
 // ---- multi-valued (CSR) columns, esgpu_kernels_multi.hip ----

@@ -1524,9 +1524,11 @@ static bool collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment*
         P.mg_m = mg.m; P.mg_s1 = mg.s1; P.mg_s2 = mg.s2;
     }
     const int hk = HIST ? (P.kstart ? 2 : 1) : 0;
-    const uint64_t occ_key = ((uint64_t)lds << 8) | ((uint64_t)met_launch << 4) | ((uint64_t)hk << 1) | (ORD ? 1 : 0);
+    const int vk = (P.hv_f64 ? 1 : 0) | (P.mv_f64 ? 2 : 0);
+    const uint64_t occ_key = ((uint64_t)lds << 10) | ((uint64_t)vk << 8) | ((uint64_t)met_launch << 4) | ((uint64_t)hk << 1) |
+                             (ORD ? 1 : 0);
     if (pl.occ_key != occ_key) {
-        pl.occ = std::max(1, collect_occupancy(ORD, hk, met_launch, lds));
+        pl.occ = std::max(1, collect_occupancy(ORD, hk, met_launch, lds, vk));
         pl.occ_key = occ_key;
     }
     const uint32_t wg_per_cu = (uint32_t)pl.occ;
