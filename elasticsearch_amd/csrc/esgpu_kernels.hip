@@ -511,23 +511,27 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
 
     Run run;
     run_reset(run);
-    // software pipeline, kPrefetch iterations deep: the loads of iteration i + kPrefetch are issued before the LDS
-    // updates of iteration i (bytes in flight per CU are what bound a streaming kernel at 2 workgroups per CU)
+    // software pipeline over two buffers: each is reloaded (iteration i + 2) right after it is processed, so one
+    // buffer's loads are in flight while the other is processed.  Loads are unconditional (past the end: the last
+    // iteration's docs again, never processed) and no loaded register is copied: a conditional load or a register
+    // copy of a load's result makes the compiler wait vmcnt(0), which drains the other buffer's loads as well.
     const uint32_t tid4 = threadIdx.x * kVec;
-    const uint32_t n_it = (b_end - b_begin) * kItersPerBlock;
+    const uint32_t n_it = (b_end - b_begin) * kItersPerBlock;  // a multiple of kItersPerBlock (even)
     auto doc_of = [&](uint32_t i) {
+        i = min(i, n_it - 1);
         return (b_begin + i / kItersPerBlock) * kBlockDocs + (i % kItersPerBlock) * kIterDocs + tid4;
     };
-    Doc4 q[kPrefetch];
-#pragma unroll
-    for (int k = 0; k < kPrefetch; ++k)
-        if ((uint32_t)k < n_it) load_docs<ORD, HIST, MET, VK>(P, doc_of(k), q[k]);
+    Doc4 qa, qb;
+    load_docs<ORD, HIST, MET, VK>(P, doc_of(0), qa);
+    load_docs<ORD, HIST, MET, VK>(P, doc_of(1), qb);
 
     bool use_lds = P.lds_mode != 0;
-    for (uint32_t i = 0; i < n_it; ++i) {
+    auto step = [&](uint32_t i, Doc4& q) {
         if (i % kItersPerBlock == 0) {
             // ---- per-block decision (wave-uniform: every lane reads the same zone-map words) ----
-            const uint32_t b = b_begin + i / kItersPerBlock;
+            // readfirstlane: the zone-map words become scalar loads (lgkmcnt), not vector loads whose vmcnt wait
+            // would drain the prefetched buffers
+            const uint32_t b = __builtin_amdgcn_readfirstlane(b_begin + i / kItersPerBlock);
             use_lds = P.lds_mode != 0;
             if (use_lds && HIST && P.windowed) {
                 const int64_t zmn = P.zmin[b], zmx = P.zmax[b];
@@ -549,17 +553,17 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
                 }
             }
         }
-        Doc4 nxt;
-        if (i + kPrefetch < n_it) load_docs<ORD, HIST, MET, VK>(P, doc_of(i + kPrefetch), nxt);
         if (use_lds) {
-            process4<ORD, HIST, MET, true, KT, kMS>(P, s, q[0], T, base, win0, run);
+            process4<ORD, HIST, MET, true, KT, kMS>(P, s, q, T, base, win0, run);
             dirty = true;
         } else {
-            process4<ORD, HIST, MET, false, KT, kMS>(P, g, q[0], T, base, win0, run);
+            process4<ORD, HIST, MET, false, KT, kMS>(P, g, q, T, base, win0, run);
         }
-#pragma unroll
-        for (int k = 0; k + 1 < kPrefetch; ++k) q[k] = q[k + 1];
-        q[kPrefetch - 1] = nxt;
+        load_docs<ORD, HIST, MET, VK>(P, doc_of(i + 2), q);
+    };
+    for (uint32_t i = 0; i < n_it; i += 2) {
+        step(i, qa);
+        step(i + 1, qb);
     }
     if (P.lds_mode && (dirty || !(HIST && P.windowed))) {
         if (!ORD) run_flush<MET, kMS>(P, s, run);
@@ -972,7 +976,10 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
     // phases [0, 16m), then x4 each: every register has seen ~16 hashes after the first cut, so the floor (min
     // register) starts to rise, and each later phase reads registers only for hashes longer than the floor
     std::vector<uint32_t> cuts{0};
-    uint64_t c = (uint64_t)m * 16;
+#ifndef ESGPU_HLL_CUT0
+#define ESGPU_HLL_CUT0 4  // measured: 4 beats 16 by 3-4 % (phase 0 reads and raises registers for every hash)
+#endif
+    uint64_t c = (uint64_t)m * ESGPU_HLL_CUT0;
     while (c < n) {
         cuts.push_back((uint32_t)c & ~3u);
         c *= 4;

@@ -363,3 +363,24 @@ def test_index_time_hashing(engine):
         h1, h2 = ctypes.c_uint64(), ctypes.c_uint64()
         L.oracle_murmur3_128(b, len(b), 0, ctypes.byref(h1), ctypes.byref(h2))
         assert int(got[i]) == h1.value, v
+
+
+def test_rccl_gather_reduce_single_rank(engine):  # the bench's N > 1 exchange (esgpu_comm_*) on a one-rank communicator
+    from elasticsearch_amd import Communicator
+    n = 200_000
+    fields = ("host", "@timestamp", "response_time_ms", "client_ip.hash")
+    aggs = [AB.terms("hosts").field("host").size(5).subAggregation(
+                AB.dateHistogram("h").field("@timestamp").interval("1d").subAggregation(AB.stats("rt").field("response_time_ms"))),
+            AB.cardinality("ips").field("client_ip.hash").precisionThreshold(1000)]
+    want = O.run([(synthetic_columns(fields, n), n)], aggs)
+    comm = Communicator(engine, 1, 0, Communicator.unique_id())
+    seg = engine.synthetic_segment(n, fields=fields)
+    plan = engine.plan(aggs)
+    for _ in range(2):  # communicator buffers are reused across requests
+        plan.reset()
+        plan.collect(seg)
+        got = comm.gather_reduce(plan.build()).to_dict()
+        assert_same(got, want["reduced"], "rccl reduced")
+    plan.close()
+    seg.close()
+    comm.close()
