@@ -1378,23 +1378,33 @@ __global__ __launch_bounds__(kWG) void part_count_kernel(PartParams P) {
         for (uint32_t i = i0 + threadIdx.x; i < a0; i += kWG) count_run(cnt, cur, n, P.pbuf[i]);
         const uint32_t nvec = (s1 - a0) / 8;
         const uint4* v8 = reinterpret_cast<const uint4*>(P.pbuf + a0);
-        uint32_t k = threadIdx.x;
-        for (; k + kWG < nvec; k += 2 * kWG) {  // two 16-byte loads (16 offsets) in flight per thread
-            const uint4 x = v8[k], y = v8[k + kWG];
-            const uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+        // two buffers of 2 x 16 bytes (16 offsets), each reloaded right after it is counted; loads are unconditional
+        // (clamped to the last vector, counted only when in range) so the compiler waits with counted vmcnt
+        if (nvec > 0) {
+            auto ld = [&](uint32_t k, uint4 v[2]) {
+                v[0] = v8[min(k, nvec - 1)];
+                v[1] = v8[min(k + kWG, nvec - 1)];
+            };
+            auto count8 = [&](uint32_t k, const uint4 v[2]) {
 #pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                count_run(cnt, cur, n, w[t] & 0xFFFFu);
-                count_run(cnt, cur, n, w[t] >> 16);
-            }
-        }
-        for (; k < nvec; k += kWG) {
-            const uint4 x = v8[k];
-            const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+                for (int h = 0; h < 2; ++h) {
+                    if (k + h * kWG >= nvec) break;
+                    const uint32_t w[4] = {v[h].x, v[h].y, v[h].z, v[h].w};
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                count_run(cnt, cur, n, w[t] & 0xFFFFu);
-                count_run(cnt, cur, n, w[t] >> 16);
+                    for (int t = 0; t < 4; ++t) {
+                        count_run(cnt, cur, n, w[t] & 0xFFFFu);
+                        count_run(cnt, cur, n, w[t] >> 16);
+                    }
+                }
+            };
+            uint4 va[2], vb[2];
+            ld(threadIdx.x, va);
+            ld(threadIdx.x + 2 * kWG, vb);
+            for (uint32_t k = threadIdx.x; k < nvec; k += 4 * kWG) {
+                count8(k, va);
+                ld(k + 4 * kWG, va);
+                count8(k + 2 * kWG, vb);
+                ld(k + 6 * kWG, vb);
             }
         }
         for (uint32_t i = a0 + nvec * 8 + threadIdx.x; i < s1; i += kWG) count_run(cnt, cur, n, P.pbuf[i]);
