@@ -976,13 +976,16 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
     // phases [0, 16m), then x4 each: every register has seen ~16 hashes after the first cut, so the floor (min
     // register) starts to rise, and each later phase reads registers only for hashes longer than the floor
     std::vector<uint32_t> cuts{0};
+#ifndef ESGPU_HLL_GROW
+#define ESGPU_HLL_GROW 4
+#endif
 #ifndef ESGPU_HLL_CUT0
 #define ESGPU_HLL_CUT0 4  // measured: 4 beats 16 by 3-4 % (phase 0 reads and raises registers for every hash)
 #endif
     uint64_t c = (uint64_t)m * ESGPU_HLL_CUT0;
     while (c < n) {
         cuts.push_back((uint32_t)c & ~3u);
-        c *= 4;
+        c *= ESGPU_HLL_GROW;
     }
     cuts.push_back(n);
     const uint32_t wgs_max = cus * 8;  // 8 workgroups of 256 threads per CU
