@@ -25,7 +25,7 @@ SYNTH_TYPES = {
     "response_time_ms": COL_I64, "bytes": COL_I64, "client_ip.hash": COL_U64, "price": COL_F64,
 }
 AGG_TERMS, AGG_HISTOGRAM, AGG_DATE_HISTOGRAM, AGG_STATS, AGG_EXTENDED_STATS, AGG_AVG, AGG_CARDINALITY = 1, 2, 3, 4, 5, 6, 7
-AGG_SUM, AGG_MIN, AGG_MAX, AGG_VALUE_COUNT = 8, 9, 10, 11
+AGG_SUM, AGG_MIN, AGG_MAX, AGG_VALUE_COUNT, AGG_FILTER = 8, 9, 10, 11, 12
 ORDER_COUNT_DESC, ORDER_COUNT_ASC, ORDER_TERM_ASC, ORDER_TERM_DESC = 0, 1, 2, 3
 ORDER_KEY_ASC, ORDER_KEY_DESC, ORDER_HCOUNT_ASC, ORDER_HCOUNT_DESC = 4, 5, 6, 7
 UNIT_NONE, UNIT_WEEK, UNIT_YEAR, UNIT_QUARTER, UNIT_MONTH, UNIT_DAY, UNIT_HOUR, UNIT_MINUTE, UNIT_SECOND = range(9)
@@ -58,7 +58,7 @@ class AggSpec(ctypes.Structure):
 class Filter(ctypes.Structure):
     _fields_ = [
         ("type", ctypes.c_int32), ("include_lower", ctypes.c_int32), ("include_upper", ctypes.c_int32),
-        ("has_lower", ctypes.c_int32), ("has_upper", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("has_lower", ctypes.c_int32), ("has_upper", ctypes.c_int32), ("owner", ctypes.c_int32),
         ("field", ctypes.c_char_p), ("term", ctypes.c_int64), ("lo_i", ctypes.c_int64), ("hi_i", ctypes.c_int64),
         ("lo_d", ctypes.c_double), ("hi_d", ctypes.c_double),
         ("lo_term", ctypes.c_char_p), ("hi_term", ctypes.c_char_p), ("lo_term_len", ctypes.c_uint64),

@@ -258,8 +258,29 @@ class CardinalityBuilder(_MetricBuilder):
     precision_threshold = precisionThreshold
 
 
+class FilterBuilder(_Builder):
+    """filter aggregation (FilterAggregator / InternalFilter): one bucket of the docs matching `query` -- a TermQuery,
+    a RangeQuery or a list of them (bool.filter conjunction) -- with sub-aggregations.  Top level on the GPU path."""
+    type = N.AGG_FILTER
+
+    def __init__(self, name, query=None):
+        super().__init__(name)
+        self._query = query
+
+    def filter(self, query):
+        self._query = query
+        return self
+
+    def clauses(self):
+        q = self._query
+        if q is None:
+            raise ValueError("[filter] aggregation [%s] requires a filter" % self.name)
+        return list(q) if isinstance(q, (list, tuple)) else [q]
+
+
 class AggregationBuilders:
     terms = TermsBuilder
+    filter = FilterBuilder
     histogram = HistogramBuilder
     dateHistogram = DateHistogramBuilder
     date_histogram = DateHistogramBuilder
@@ -417,11 +438,31 @@ def flatten(aggs, number_of_shards=1):
     return arr, len(specs), keep
 
 
-def flatten_filters(queries, ord_lookup=None):
-    """Queries -> ctypes array of Filter.  `ord_lookup(field, term) -> ordinal or -1` resolves keyword terms."""
+def _preorder(aggs):
+    """(builder, spec index) in flatten()'s order (parents before children, depth first)."""
+    out = []
+
+    def visit(b):
+        out.append(b)
+        for s in b.subs:
+            visit(s)
+
+    for a in aggs or []:
+        visit(a)
+    return [(b, i) for i, b in enumerate(out)]
+
+
+def flatten_filters(queries, ord_lookup=None, aggs=None):
+    """Queries -> ctypes array of Filter.  `ord_lookup(field, term) -> ordinal or -1` resolves keyword terms.  With
+    `aggs`, the clauses of every filter aggregation follow, each tagged with its owner (spec index + 1)."""
     out, keep = [], []
-    for q in queries or []:
+    tagged = [(q, 0) for q in queries or []]
+    for b, i in _preorder(aggs):
+        if b.type == N.AGG_FILTER:
+            tagged += [(q, i + 1) for q in b.clauses()]
+    for q, owner in tagged:
         f = N.Filter()
+        f.owner = owner
         b = q.field.encode("utf-8")
         keep.append(b)
         f.field = b

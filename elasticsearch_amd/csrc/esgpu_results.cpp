@@ -183,6 +183,8 @@ Block Block::like() const {
         b.term_off.assign(1, 0);
         for (const Block& s : subs) b.subs.push_back(s.like());
         b.empty_subs = empty_subs;
+    } else if (type == ESGPU_AGG_FILTER) {
+        for (const Block& s : subs) b.subs.push_back(s.like());
     }
     return b;
 }
@@ -203,6 +205,9 @@ void Block::append_instance(const Block& src, uint64_t i) {
         boff.push_back(boff.back() + (b1 - b0));
         for (size_t j = 0; j < subs.size(); ++j)
             for (uint64_t k = b0; k < b1; ++k) subs[j].append_instance(src.subs[j], k);
+    } else if (type == ESGPU_AGG_FILTER) {
+        count.push_back(src.count[i]);
+        for (size_t j = 0; j < subs.size(); ++j) subs[j].append_instance(src.subs[j], i);
     } else if (type == ESGPU_AGG_CARDINALITY) {
         hll_present.push_back(src.hll_present[i]);
         hll_mode.push_back(src.hll_mode[i]);
@@ -223,6 +228,9 @@ void Block::append_empty() {  // buildEmptyAggregation
         doc_count_error.push_back(0);
         other_doc_count.push_back(0);
         boff.push_back(boff.back());
+    } else if (type == ESGPU_AGG_FILTER) {
+        count.push_back(0);
+        for (Block& s : subs) s.append_empty();
     } else if (type == ESGPU_AGG_CARDINALITY) {
         hll_present.push_back(0);
         hll_mode.push_back(0);
@@ -494,6 +502,25 @@ void reduce_level(const Level& lv, Block& out) {
         for (size_t j = 0; j < out.subs.size(); ++j) reduce_level(child[j], out.subs[j]);
         return;
     }
+    if (out.type == ESGPU_AGG_FILTER) {  // InternalFilter (InternalSingleBucketAggregation.doReduce): Σ doc_count, subs
+        std::vector<Level> child(out.subs.size());
+        std::vector<Ref> rs;
+        for (const Group& g : lv.groups) {
+            const Ref* refs = lv.pool.data() + g.begin;
+            const size_t n = g.end - g.begin;
+            int64_t dc = 0;
+            for (size_t x = 0; x < n; ++x) dc += refs[x].b->count[refs[x].i];
+            ++out.n;
+            out.count.push_back(dc);
+            for (size_t j = 0; j < out.subs.size(); ++j) {
+                rs.clear();
+                for (size_t x = 0; x < n; ++x) rs.push_back({&refs[x].b->subs[j], refs[x].i});
+                child[j].add(rs.data(), rs.size(), g.verbatim);
+            }
+        }
+        for (size_t j = 0; j < out.subs.size(); ++j) reduce_level(child[j], out.subs[j]);
+        return;
+    }
     for (const Group& g : lv.groups) {
         const Ref* refs = lv.pool.data() + g.begin;
         const size_t n = g.end - g.begin;
@@ -653,6 +680,10 @@ void write_instance(J& j, const Block& a, uint64_t i) {
                 j.raw("}");
             }
             j.raw("]");
+            break;
+        case ESGPU_AGG_FILTER:  // InternalSingleBucketAggregation.doXContentBody: doc_count, then the sub-aggregations
+            j.key("doc_count"); j.i64(a.count[i]);
+            write_subs(j, a, i);
             break;
         case ESGPU_AGG_AVG:
             j.key("value"); j.opt(a.count[i] != 0, a.sum[i] / (double)a.count[i]);
@@ -825,6 +856,9 @@ void r_block(R& r, Block& a, int depth) {
         if (a.has_empty_info && a.empty_subs.size() != a.subs.size()) throw std::runtime_error("missing empty-bucket prototypes");
         for (size_t j = 0; j < a.empty_subs.size(); ++j)
             if (a.empty_subs[j].n != 1 || a.empty_subs[j].type != a.subs[j].type) throw std::runtime_error("bad empty-bucket prototype");
+    } else if (a.type == ESGPU_AGG_FILTER) {
+        if (a.count.size() != a.n) throw std::runtime_error("inconsistent filter block");
+        for (const Block& s : a.subs) if (s.n != a.n) throw std::runtime_error("sub-aggregation instance count mismatch");
     } else if (a.type == ESGPU_AGG_CARDINALITY) {
         if (a.hll_present.size() != a.n || a.hll_mode.size() != a.n || a.regs.size() != a.n || a.lc.size() != a.n)
             throw std::runtime_error("inconsistent cardinality block");

@@ -788,8 +788,10 @@ struct CardState {
 
 // One top-level aggregation subtree compiled to one kernel pipeline.
 struct Pipeline {
-    int root = -1;             // spec index of the top-level aggregation
+    int root = -1;             // spec index of the top-level aggregation (for a filter's children: the child)
     int kind = 0;              // 0 = cell grid (bucket / metric), 1 = cardinality
+    int fspec = -1;            // enclosing filter aggregation (FilterAggregator): its clauses apply too; -1 = none
+    bool count_only = false;   // the filter aggregation's own doc_count (one cell, no metric)
     // cell grid shape
     int outer = -1, inner = -1;      // bucket spec indices (inner may be -1)
     int term_spec = -1, hist_spec = -1;
@@ -866,6 +868,9 @@ struct esgpu_plan {
     std::vector<SpecNode> specs;
     std::vector<esgpu_filter> filters;
     std::vector<std::string> filter_fields;
+    std::vector<int> filter_owner;             // -1 = query clause (bool.filter); k = clause of filter aggregation spec k
+    std::vector<std::string> filter_lo, filter_hi;  // owned copies of keyword range bounds (the caller's may not outlive create)
+    std::vector<int> tops;                     // top-level spec indices in request order
     std::vector<Pipeline> pipes;
     bool collected = false, posted = false;
     double last_ms = 0;
@@ -891,7 +896,7 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
                                  int32_t nfilters, esgpu_plan** out) {
     return guarded([&] {
         require(c && out && (nspecs == 0 || specs), ESGPU_ERR_INVALID, "null argument");
-        require(nfilters >= 0 && nfilters <= 4, ESGPU_ERR_UNSUPPORTED, "at most 4 filter clauses run on the GPU path");
+        require(nfilters >= 0, ESGPU_ERR_INVALID, "negative filter count");
         std::unique_ptr<esgpu_plan> p(new esgpu_plan());
         p->ctx = c;
         p->specs.resize(nspecs);
@@ -911,14 +916,18 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
             n.s.tz_starts = nullptr;
             n.s.tz_offsets_ms = nullptr;
             n.s.tz_count = 0;
-            require(n.s.type >= ESGPU_AGG_TERMS && n.s.type <= ESGPU_AGG_VALUE_COUNT, ESGPU_ERR_INVALID, "unknown aggregation type");
+            require(n.s.type >= ESGPU_AGG_TERMS && n.s.type <= ESGPU_AGG_FILTER, ESGPU_ERR_INVALID, "unknown aggregation type");
+            if (n.s.type == ESGPU_AGG_FILTER)
+                require(n.s.parent < 0, ESGPU_ERR_UNSUPPORTED, "filter aggregation under another aggregation runs on the CPU path");
             if (n.s.parent < 0) tops.push_back(i);
             else {
                 require(n.s.parent < i, ESGPU_ERR_INVALID, "parent must precede child");
-                require(is_bucket(p->specs[n.s.parent].s.type), ESGPU_ERR_INVALID, "metrics aggregations cannot have sub-aggregations");
+                const int pt = p->specs[n.s.parent].s.type;
+                require(is_bucket(pt) || pt == ESGPU_AGG_FILTER, ESGPU_ERR_INVALID, "metrics aggregations cannot have sub-aggregations");
                 p->specs[n.s.parent].children.push_back(i);
             }
-            if (n.s.type >= ESGPU_AGG_SUM) throw EsError(ESGPU_ERR_UNSUPPORTED, "sum/min/max/value_count run on the CPU path");
+            if (n.s.type >= ESGPU_AGG_SUM && n.s.type <= ESGPU_AGG_VALUE_COUNT)
+                throw EsError(ESGPU_ERR_UNSUPPORTED, "sum/min/max/value_count run on the CPU path");
             if (n.s.type == ESGPU_AGG_TERMS) {
                 require(n.s.size >= 0 && n.s.min_doc_count >= 0, ESGPU_ERR_INVALID,
                         "parameters [requiredSize] and [minDocCount] must be >=0 in terms aggregation.");
@@ -934,22 +943,48 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
                 }
             }
         }
+        p->filter_lo.resize(nfilters);
+        p->filter_hi.resize(nfilters);
         for (int k = 0; k < nfilters; ++k) {
             require(filters[k].field != nullptr, ESGPU_ERR_INVALID, "filter without field");
+            const int owner = filters[k].owner - 1;  // 0 = query clause, k + 1 = clause of filter aggregation spec k
+            require(owner >= -1 && owner < nspecs && (owner < 0 || p->specs[owner].s.type == ESGPU_AGG_FILTER), ESGPU_ERR_INVALID,
+                    "filter clause owner is not a filter aggregation");
             p->filters.push_back(filters[k]);
             p->filter_fields.push_back(filters[k].field);
+            p->filter_owner.push_back(owner);
+            esgpu_filter& f = p->filters.back();
+            if (f.lo_term) { p->filter_lo[k].assign((const char*)f.lo_term, (size_t)f.lo_term_len); f.lo_term = (const uint8_t*)p->filter_lo[k].data(); }
+            if (f.hi_term) { p->filter_hi[k].assign((const char*)f.hi_term, (size_t)f.hi_term_len); f.hi_term = (const uint8_t*)p->filter_hi[k].data(); }
+            f.field = nullptr;  // filter_fields[k] holds it
         }
-        // compile each top-level subtree into a pipeline
+        // every pipeline evaluates the query clauses plus those of its filter aggregation: at most 4 predicates
+        int nquery = 0;
+        for (int o : p->filter_owner) nquery += o < 0;
+        require(nquery <= 4, ESGPU_ERR_UNSUPPORTED, "at most 4 filter clauses run on the GPU path");
         for (int r : tops) {
+            if (p->specs[r].s.type != ESGPU_AGG_FILTER) continue;
+            int own = 0;
+            for (int o : p->filter_owner) own += o == r;
+            require(own >= 1, ESGPU_ERR_INVALID, "filter aggregation without a filter clause");
+            require(nquery + own <= 4, ESGPU_ERR_UNSUPPORTED, "at most 4 filter clauses run on the GPU path");
+            for (int ch : p->specs[r].children)
+                require(p->specs[ch].s.type != ESGPU_AGG_FILTER, ESGPU_ERR_UNSUPPORTED, "nested filter aggregations");
+        }
+        p->tops = tops;
+        // compile each top-level subtree into a pipeline; a filter aggregation (FilterAggregator) becomes one
+        // counting pipeline for its doc_count plus one pipeline per sub-aggregation, all under its clauses
+        auto compile = [&](int r, int fspec) {
             Pipeline pl;
             pl.root = r;
+            pl.fspec = fspec;
             const SpecNode& root = p->specs[r];
             if (root.s.type == ESGPU_AGG_CARDINALITY) {
                 pl.kind = 1;
                 pl.p = root.precision;
                 pl.metric_field = root.field;
                 p->pipes.push_back(std::move(pl));
-                continue;
+                return;
             }
             if (is_metric(root.s.type)) {
                 pl.metrics.push_back(r);
@@ -1012,6 +1047,15 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
                 pl.met = std::max(pl.met, metric_level(n.s.type));
             }
             p->pipes.push_back(std::move(pl));
+        };
+        for (int r : tops) {
+            if (p->specs[r].s.type != ESGPU_AGG_FILTER) { compile(r, -1); continue; }
+            Pipeline cnt;
+            cnt.root = r;
+            cnt.fspec = r;
+            cnt.count_only = true;
+            p->pipes.push_back(std::move(cnt));
+            for (int ch : p->specs[r].children) compile(ch, r);
         }
         HIPX(hipSetDevice(c->device));
         HIPX(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
@@ -1151,9 +1195,16 @@ static int64_t build_key_table(esgpu_plan* p, Pipeline& pl, int64_t lo, int64_t 
     return shift;
 }
 
-static void set_preds(esgpu_plan* p, const esgpu_segment* s, PredDev* out, int32_t* npred, uint64_t* bytes_per_doc) {
+// the query clauses and those of the pipeline's filter aggregation
+static bool applies(const esgpu_plan* p, const Pipeline& pl, size_t k) {
+    return p->filter_owner[k] < 0 || p->filter_owner[k] == pl.fspec;
+}
+
+static void set_preds(esgpu_plan* p, const Pipeline& pl, const esgpu_segment* s, PredDev* out, int32_t* npred,
+                      uint64_t* bytes_per_doc) {
     *npred = 0;
     for (size_t k = 0; k < p->filters.size(); ++k) {
+        if (!applies(p, pl, k)) continue;
         const esgpu_filter& f = p->filters[k];
         const DevColumn* col = s->col(p->filter_fields[k].c_str());
         PredDev q{};
@@ -1283,7 +1334,8 @@ static bool collect_multi(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, C
     const bool ORD = oc != nullptr, HIST = hc != nullptr;
     uint64_t bytes = column_bytes(oc, s->max_doc) + column_bytes(hc, s->max_doc) + column_bytes(mc, s->max_doc);
     if (d_accept) bytes += ((uint64_t)s->max_doc + 7) / 8;
-    for (const std::string& f : p->filter_fields) bytes += column_bytes(s->col(f.c_str()), s->max_doc);
+    for (size_t k = 0; k < p->filter_fields.size(); ++k)
+        if (applies(p, pl, k)) bytes += column_bytes(s->col(p->filter_fields[k].c_str()), s->max_doc);
     HIPX(hipEventRecord(pl.e0, p->stream));
     if (P.npred > 0) {
         uint64_t* bits = (uint64_t*)p->s_fbits.ensure(c, std::max<size_t>(s->n_pad / 64, 1) * 8);
@@ -1339,7 +1391,7 @@ static void collect_cards(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, c
     PredDev pred[4];
     int npred = 0;
     uint64_t fbytes = 0;
-    set_preds(p, s, pred, &npred, &fbytes);
+    set_preds(p, pl, s, pred, &npred, &fbytes);
     if (npred > 0) {
         uint64_t* bits = (uint64_t*)p->s_fbits.ensure(p->ctx, std::max<size_t>(s->n_pad / 64, 1) * 8);
         launch_filter_bits(s->max_doc, d_accept, pred, npred, bits, p->stream);
@@ -1401,8 +1453,8 @@ static bool collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment*
     if (mc) require(mc->type == ESGPU_COL_I64 || mc->type == ESGPU_COL_F64, ESGPU_ERR_UNSUPPORTED, "metric over non-numeric field");
     // any multi-valued column (aggregated field or filter field) takes the CSR kernel
     bool multi = (oc && oc->multi) || (hc && hc->multi) || (mc && mc->multi);
-    for (const std::string& f : p->filter_fields) {
-        const DevColumn* fc = s->col(f.c_str());
+    for (size_t k = 0; k < p->filter_fields.size(); ++k) {
+        const DevColumn* fc = applies(p, pl, k) ? s->col(p->filter_fields[k].c_str()) : nullptr;
         if (fc && fc->multi) multi = true;
     }
     // an unmapped metric field collects nothing (ValuesSource null => NO_OP collector); counts stay separate
@@ -1479,7 +1531,7 @@ static bool collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment*
     P.ocnt_mode = pl.ocnt_mode;
     P.accept = d_accept;
     uint64_t bytes_per_doc = (oc ? 4 : 0) + (hc ? 8 : 0) + (mc ? 8 : 0);
-    set_preds(p, s, P.pred, &P.npred, &bytes_per_doc);
+    set_preds(p, pl, s, P.pred, &P.npred, &bytes_per_doc);
     P.g_cnt = pl.g_cnt.as<unsigned long long>();
     P.g_ocnt = pl.g_ocnt.as<unsigned long long>();
     P.g_vcnt = pl.g_vcnt.as<unsigned long long>();
@@ -1595,7 +1647,7 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
     } else {
         H.kind = col->type == ESGPU_COL_F64 ? HLL_F64 : HLL_I64;
     }
-    set_preds(p, s, H.pred, &H.npred, &bytes_per_doc);
+    set_preds(p, pl, s, H.pred, &H.npred, &bytes_per_doc);
     bool multi_pred = false;
     for (int k = 0; k < H.npred; ++k) multi_pred |= H.pred[k].offsets != nullptr;
     uint64_t bytes = bytes_per_doc * (uint64_t)s->max_doc;
@@ -1603,7 +1655,8 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
         // MurmurHash3Values iterates every value of an accepted doc: fold accept + filters into a doc bitset, then
         // (multi-valued field) expand it to a per-value bitset and run the register passes over the value array
         bytes = column_bytes(col, s->max_doc) + (d_accept ? ((uint64_t)s->max_doc + 7) / 8 : 0);
-        for (const std::string& f : p->filter_fields) bytes += column_bytes(s->col(f.c_str()), s->max_doc);
+        for (size_t k = 0; k < p->filter_fields.size(); ++k)
+        if (applies(p, pl, k)) bytes += column_bytes(s->col(p->filter_fields[k].c_str()), s->max_doc);
         const uint64_t* doc_bits = d_accept;
         if (H.npred > 0) {
             uint64_t* b = (uint64_t*)p->s_fbits.ensure(p->ctx, std::max<size_t>(s->n_pad / 64, 1) * 8);
@@ -2191,7 +2244,28 @@ extern "C" int esgpu_plan_build(esgpu_plan* p, esgpu_result** out) {
         }
         HIPX(hipSetDevice(p->ctx->device));
         std::unique_ptr<ResultHolder> h(new ResultHolder());
-        for (Pipeline& pl : p->pipes) h->aggs.push_back(pl.kind == 1 ? build_cardinality(p, pl) : build_grid(p, pl));
+        // top-level aggregations in request order; a filter aggregation (InternalFilter, FilterAggregator.java:72-80)
+        // is its counting pipeline's doc_count plus its sub-aggregations' pipelines, in the order compile() made them
+        size_t k = 0;
+        auto build_one = [&](Pipeline& pl) { return pl.kind == 1 ? build_cardinality(p, pl) : build_grid(p, pl); };
+        for (int r : p->tops) {
+            if (p->specs[r].s.type != ESGPU_AGG_FILTER) { h->aggs.push_back(build_one(p->pipes[k++])); continue; }
+            Pipeline& cnt = p->pipes[k++];
+            Block fb;
+            fb.type = ESGPU_AGG_FILTER;
+            fb.name = p->specs[r].name;
+            fb.n = 1;
+            uint64_t dc = 0;
+            if (cnt.allocated) {
+                uint64_t* hc = (uint64_t*)p->h_tcnt.ensure(16);
+                HIPX(hipMemcpyAsync(hc, cnt.g_cnt.p, 8, hipMemcpyDeviceToHost, p->stream));
+                HIPX(hipStreamSynchronize(p->stream));
+                dc = hc[0];
+            }
+            fb.count.push_back((int64_t)dc);
+            for (size_t j = 0; j < p->specs[r].children.size(); ++j) fb.subs.push_back(build_one(p->pipes[k++]));
+            h->aggs.push_back(std::move(fb));
+        }
         h->export_view();
         *out = &h.release()->pub;
     });

@@ -160,7 +160,7 @@ class Plan:
     def __init__(self, engine, aggs, filters=None, number_of_shards=1, ord_lookup=None):
         self.engine = engine
         self._specs, n, self._keep = flatten(aggs, number_of_shards)
-        self._filters, nf, self._fkeep = flatten_filters(filters, ord_lookup)
+        self._filters, nf, self._fkeep = flatten_filters(filters, ord_lookup, aggs)
         ptr = ctypes.c_void_p()
         N.check(N.lib().esgpu_plan_create(engine.ptr, self._specs, n, self._filters, nf, ctypes.byref(ptr)))
         self._ptr = ptr

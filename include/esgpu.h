@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define ESGPU_ABI_VERSION 2
+#define ESGPU_ABI_VERSION 3
 
 /* ---------------------------------------------------------------------------------------------------------
  * Status codes.  Mapping used by the JNI shim (SURVEY §8(b) "Errors"):
@@ -170,7 +170,9 @@ enum {
     ESGPU_AGG_SUM = 8,
     ESGPU_AGG_MIN = 9,
     ESGPU_AGG_MAX = 10,
-    ESGPU_AGG_VALUE_COUNT = 11
+    ESGPU_AGG_VALUE_COUNT = 11,
+    ESGPU_AGG_FILTER = 12         /* FilterAggregator: single bucket of the docs matching its clauses (esgpu_filter.owner);
+                                     top level only; result block: count[i] = doc_count, subs = its sub-aggregations */
 };
 
 /* terms order (InternalOrder.java:47-76; compound with _term asc tie-break for the count orders) */
@@ -249,7 +251,8 @@ typedef struct esgpu_filter {
     int32_t include_upper;
     int32_t has_lower;
     int32_t has_upper;
-    int32_t reserved;
+    int32_t owner;                /* 0 = query clause (applies to every aggregation); k + 1 = clause of the filter
+                                     aggregation spec[k] (FilterAggregator: conjunction of its clauses) */
     const char* field;
     int64_t term;                 /* TERM on I64 / ORD columns */
     int64_t lo_i, hi_i;           /* RANGE on I64 / U64 columns */

@@ -563,6 +563,8 @@ struct Internal {
     double sum = 0, min = INFINITY, max = -INFINITY, sumsq = 0, sigma = 2.0;
     // cardinality
     std::shared_ptr<HLLPP> hll;
+    // filter (InternalSingleBucketAggregation): doc_count in `count`, sub-aggregations here
+    InternalList subs;
 };
 
 // ---- comparators (A/bucket/terms/InternalOrder.java:47-76, CompoundOrder with _term asc tie-break) ----
@@ -621,6 +623,7 @@ struct Aggregator {
 struct Factory {
     esgpu_agg_spec spec;
     std::string name, field;
+    std::vector<esgpu_filter> clauses;  // filter aggregation: its query (conjunction of term / range clauses)
     std::vector<std::unique_ptr<Factory>> children;
     const Factory* parent = nullptr;
     int precision = 14;
@@ -940,6 +943,35 @@ struct CardinalityAgg : Aggregator {
     InternalPtr build_empty() override { return make(nullptr); }
 };
 
+// FilterAggregator (A/bucket/filter/FilterAggregator.java:57-81): a SingleBucketAggregator; collect(doc, bucket) counts
+// the doc into docCounts[bucket] and collects the sub-aggregators iff the doc matches the filter's query.  Not wrapped
+// by asMultiBucketAggregator (it keeps one doc count per owning bucket itself).
+struct FilterAgg : Aggregator {
+    const Segment* seg = nullptr;
+    std::vector<int64_t> docCounts;
+    void set_leaf(const Segment& s) override { seg = &s; Aggregator::set_leaf(s); }
+    void collect(uint32_t doc, int64_t bucket) override;
+    InternalPtr make(int64_t bucket, bool empty) {
+        auto r = std::make_shared<Internal>();
+        r->type = ESGPU_AGG_FILTER;
+        r->name = f->name;
+        r->count = (!empty && bucket < (int64_t)docCounts.size()) ? docCounts[bucket] : 0;
+        r->subs = empty ? bucket_empty_aggs() : bucket_aggs(bucket);
+        return r;
+    }
+    InternalPtr build(int64_t bucket) override { return make(bucket, false); }
+    InternalPtr build_empty() override { return make(0, true); }
+};
+
+static bool doc_matches(const Segment& seg, uint32_t doc, const esgpu_filter* flt, int nf, const uint64_t* accept);
+
+void FilterAgg::collect(uint32_t doc, int64_t bucket) {
+    if (!doc_matches(*seg, doc, f->clauses.data(), (int)f->clauses.size(), nullptr)) return;
+    if ((int64_t)docCounts.size() <= bucket) docCounts.resize((size_t)bucket + 1, 0);
+    ++docCounts[bucket];  // collectBucket
+    collect_subs(doc, bucket);
+}
+
 std::unique_ptr<Aggregator> Factory::create_one() const {
     std::unique_ptr<Aggregator> a;
     switch (spec.type) {
@@ -961,6 +993,7 @@ std::unique_ptr<Aggregator> Factory::create_one() const {
             break;
         }
         case ESGPU_AGG_CARDINALITY: a.reset(new CardinalityAgg()); break;
+        case ESGPU_AGG_FILTER: a.reset(new FilterAgg()); break;
         default: throw std::invalid_argument("unsupported aggregation type " + std::to_string(spec.type));
     }
     a->f = this;
@@ -981,6 +1014,14 @@ static InternalPtr reduce_one(const InternalList& aggs) {
     const Internal& first = *aggs[0];
     auto r = std::make_shared<Internal>(first);
     switch (first.type) {
+        case ESGPU_AGG_FILTER: {  // InternalSingleBucketAggregation.doReduce (A/bucket/InternalSingleBucketAggregation.java:85-95)
+            int64_t dc = 0;
+            std::vector<InternalList> lists;
+            for (auto& a : aggs) { dc += a->count; lists.push_back(a->subs); }
+            r->count = dc;
+            r->subs = reduce_list(lists);
+            return r;
+        }
         case ESGPU_AGG_TERMS: {  // InternalTerms.doReduce (A/bucket/terms/InternalTerms.java:165-246)
             std::map<std::string, std::vector<const Bucket*>> groups;  // iteration order irrelevant (strict order)
             std::vector<std::string> key_order;
@@ -1178,6 +1219,10 @@ static void write_list(Json& j, const InternalList& aggs);
 static void write_agg(Json& j, const Internal& a) {
     j.raw("{");
     switch (a.type) {
+        case ESGPU_AGG_FILTER:  // InternalSingleBucketAggregation.doXContentBody (:130-134)
+            j.key("doc_count"); j.i64(a.count);
+            if (!a.subs.empty()) { j.raw(","); write_list(j, a.subs); }
+            break;
         case ESGPU_AGG_TERMS: {
             j.key("doc_count_error_upper_bound"); j.i64(a.doc_count_error); j.raw(",");
             j.key("sum_other_doc_count"); j.i64(a.other_doc_count); j.raw(",");
@@ -1288,7 +1333,8 @@ static void write_list(Json& j, const InternalList& aggs) {
 // (A/AggregationPhase.java:69-168; C/search/query/QueryPhase.java:254-258,312-314) and the coordinator reduce
 // (C/search/controller/SearchPhaseController.java:401-411).
 // ------------------------------------------------------------------------------------------------------------
-static std::vector<std::unique_ptr<Factory>> build_factories(const esgpu_agg_spec* specs, int n, std::vector<Factory*>& top) {
+static std::vector<std::unique_ptr<Factory>> build_factories(const esgpu_agg_spec* specs, int n, std::vector<Factory*>& top,
+                                                             const esgpu_filter* flt, int nf) {
     std::vector<std::unique_ptr<Factory>> owned;
     std::vector<Factory*> all(n, nullptr);
     for (int i = 0; i < n; ++i) {
@@ -1303,6 +1349,13 @@ static std::vector<std::unique_ptr<Factory>> build_factories(const esgpu_agg_spe
             f->parent = all[specs[i].parent];
             all[specs[i].parent]->children.push_back(std::move(f));
         }
+    }
+    // filter aggregations own the clauses whose owner names them (esgpu_filter.owner = spec index + 1)
+    for (int k = 0; k < nf; ++k) {
+        const int o = flt[k].owner - 1;
+        if (o < 0) continue;
+        if (o >= n || all[o]->spec.type != ESGPU_AGG_FILTER) throw std::invalid_argument("filter clause owner is not a filter aggregation");
+        all[o]->clauses.push_back(flt[k]);
     }
     // cardinality precision: CardinalityAggregatorFactory.precision / defaultPrecision (:43-77)
     for (int i = 0; i < n; ++i) {
@@ -1385,14 +1438,16 @@ int oracle_run(const oracle_shard* shards, int32_t nshards, const esgpu_agg_spec
             seg.max_doc = shards[s].max_doc;
             for (int c = 0; c < shards[s].ncols; ++c) seg.cols[shards[s].cols[c].name].d = &shards[s].cols[c];
             std::vector<Factory*> top;
-            auto owned = build_factories(specs, nspecs, top);
+            auto owned = build_factories(specs, nspecs, top, filters, nfilters);
+            std::vector<esgpu_filter> query;  // bool.filter clauses (owner 0); the rest belong to filter aggregations
+            for (int k = 0; k < nfilters; ++k) if (filters[k].owner == 0) query.push_back(filters[k]);
             std::vector<std::unique_ptr<Aggregator>> aggs;
             for (Factory* f : top) aggs.push_back(f->create(true));
             struct timespec t0, t1;
             clock_gettime(CLOCK_MONOTONIC, &t0);
             for (auto& a : aggs) a->set_leaf(seg);
             for (uint32_t doc = 0; doc < seg.max_doc; ++doc) {
-                if (!doc_matches(seg, doc, filters, nfilters, shards[s].accept_bits)) continue;
+                if (!doc_matches(seg, doc, query.data(), (int)query.size(), shards[s].accept_bits)) continue;
                 for (auto& a : aggs) a->collect(doc, 0);
             }
             for (auto& a : aggs) a->post_collection();

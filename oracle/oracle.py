@@ -122,7 +122,7 @@ def run(shards, aggs, filters=None, number_of_shards=None, accept=None, ord_look
     L = lib()
     number_of_shards = number_of_shards or len(shards)
     specs, nspecs, k1 = flatten(aggs, number_of_shards)
-    flt, nf, k2 = flatten_filters(filters, ord_lookup)
+    flt, nf, k2 = flatten_filters(filters, ord_lookup, aggs)
     oshards, keep = [], [k1, k2]
     for i, (cols, max_doc) in enumerate(shards):
         arr, n, k = _columns(cols)

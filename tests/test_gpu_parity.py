@@ -384,3 +384,17 @@ def test_rccl_gather_reduce_single_rank(engine):  # the bench's N > 1 exchange (
     plan.close()
     seg.close()
     comm.close()
+
+
+def test_filter_aggregation(engine):  # FilterAggregator: top-level filter{...} beside unfiltered siblings, under a query
+    n = 300_001
+    fields = ("host", "@timestamp", "response_time_ms", "status", "bytes", "client_ip.hash")
+    aggs = [AB.filter("ok_small", [QB.termQuery("status", 200), QB.rangeQuery("bytes").gte(1024).lte(65536)]).subAggregation(
+                AB.terms("hosts").field("host").size(5).subAggregation(
+                    AB.dateHistogram("h").field("@timestamp").interval("1d").subAggregation(AB.avg("rt").field("response_time_ms")))
+            ).subAggregation(AB.stats("rt_all").field("response_time_ms")).subAggregation(
+                AB.cardinality("ips").field("client_ip.hash").precisionThreshold(100)),
+            AB.filter("errors", QB.rangeQuery("status").gte(500)),
+            AB.terms("all_hosts").field("host").size(3)]
+    run_both(engine, aggs, fields, n, filters=[QB.rangeQuery("response_time_ms").lt(900)])
+    run_both(engine, aggs, fields, n)  # no query clauses: only the filters' own

@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
     for name in names:
         assert hasattr(lib, name), name
     assert {n for n, _, _ in N.SIGNATURES} == set(names)
-    assert lib.esgpu_abi_version() == 2
+    assert lib.esgpu_abi_version() == 3
 
 
 def test_no_silent_cpu_fallback():
@@ -284,3 +284,19 @@ def test_routing_hash_matches_kats_and_oracle(kat):
     for i in range(400):
         s = "".join(rng.choice(alphabet, size=int(rng.integers(0, 40))))
         assert routing_hash(s) == oracle_routing_hash(s), s
+
+
+def test_filter_aggregation_plan_validation():
+    """Filter aggregations compile on the GPU path at the top level only; clause owners must name filter specs."""
+    from elasticsearch_amd import AggregationBuilders as AB
+    from elasticsearch_amd import QueryBuilders as QB
+    from elasticsearch_amd.aggs import flatten, flatten_filters
+    aggs = [AB.filter("f", [QB.termQuery("status", 200)]).subAggregation(AB.avg("a").field("x")),
+            AB.terms("t").field("host")]
+    specs, n, _k1 = flatten(aggs)
+    flt, nf, _k2 = flatten_filters([QB.rangeQuery("bytes").gte(1)], None, aggs)
+    assert n == 3 and nf == 2
+    assert [flt[i].owner for i in range(nf)] == [0, 1]  # query clause, then the clause of spec 0
+    assert specs[0].type == N.AGG_FILTER and specs[1].parent == 0
+    with pytest.raises(ValueError):
+        flatten_filters(None, None, [AB.filter("nofilter")])

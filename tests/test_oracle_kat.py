@@ -233,3 +233,20 @@ def test_routing_murmur3_known_values(kat):  # Murmur3HashFunctionTests.testKnow
     for v in kat["routing_murmur3_x86_32"]:
         assert oracle_routing_hash(v["input"]) == v["hash"], v["cite"]
     assert oracle_shard_id(-7, 5) == 3 and oracle_shard_id(7, 5) == 2  # MathUtils.mod: floor modulo
+
+
+@pytest.mark.parametrize("num_docs,num_tag1", [(5, 1), (12, 7), (20, 19)])
+def test_filter_aggregation_fixture(num_docs, num_tag1):  # FilterIT.simple / withSubAggregation (FilterIT.java:95-146)
+    """FilterIT's index: docs 0..numTag1Docs-1 {value: i+1, tag: tag1}, the rest {value: i, tag: tag2}.
+    filter(termQuery(tag, tag1)) has doc_count numTag1Docs and avg(value) = sum(1..numTag1Docs) / numTag1Docs."""
+    from elasticsearch_amd import QueryBuilders as QB
+    tags = ["tag1" if i < num_tag1 else "tag2" for i in range(num_docs)]
+    vals = [i + 1 if i < num_tag1 else i for i in range(num_docs)]
+    cols = {"tag": _terms_col(tags), "value": _i64(vals)}
+    lookup = {"tag1": 0, "tag2": 1}
+    aggs = [AB.filter("tag1", QB.termQuery("tag", "tag1")).subAggregation(AB.avg("avg_value").field("value")),
+            AB.filter("plain", QB.termQuery("tag", "tag1"))]
+    res = O.run([(cols, num_docs)], aggs, ord_lookup=lambda f, t: lookup.get(t, -1))["reduced"]
+    assert res["tag1"]["doc_count"] == num_tag1 and res["plain"]["doc_count"] == num_tag1
+    assert res["tag1"]["avg_value"]["value"] == sum(range(1, num_tag1 + 1)) / num_tag1
+    assert list(res["plain"].keys()) == ["doc_count"]
