@@ -87,14 +87,13 @@ void launch_synth(const SynthParams& p, hipStream_t stream) {
 // ------------------------------------------------------------------------------------------------------------
 // collect
 // ------------------------------------------------------------------------------------------------------------
-#ifndef ESGPU_PREFETCH
-#define ESGPU_PREFETCH 2
-#endif
 constexpr int kWG = 512;                         // threads per workgroup (8 waves)
 constexpr int kVec = 4;                          // consecutive docs per thread per iteration
 constexpr int kIterDocs = kWG * kVec;            // 2048
 constexpr int kItersPerBlock = kBlockDocs / kIterDocs;  // 4
-constexpr int kPrefetch = ESGPU_PREFETCH;             // iterations of loads in flight per thread
+#ifndef ESGPU_NBUF_NARROW  // load buffers in flight per thread for shapes reading one narrow column
+#define ESGPU_NBUF_NARROW 2  // measured: 4 no faster for terms(host), 4 % slower for date_histogram
+#endif
 
 struct Doc4 {
     uint32_t ord[kVec];
@@ -521,9 +520,13 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
         i = min(i, n_it - 1);
         return (b_begin + i / kItersPerBlock) * kBlockDocs + (i % kItersPerBlock) * kIterDocs + tid4;
     };
-    Doc4 qa, qb;
-    load_docs<ORD, HIST, MET, VK>(P, doc_of(0), qa);
-    load_docs<ORD, HIST, MET, VK>(P, doc_of(1), qb);
+    // shapes that read few bytes per doc (one ordinal or one key column) keep 4 buffers in flight, the rest 2 (their
+    // buffers are 5x larger; 4 would cost occupancy).  kItersPerBlock (4) is a multiple of either.
+    constexpr int kBuf = (MET == 0 && !(ORD && HIST)) ? ESGPU_NBUF_NARROW : 2;
+    static_assert(kItersPerBlock % kBuf == 0, "buffers per block");
+    Doc4 q[kBuf];
+#pragma unroll
+    for (int k = 0; k < kBuf; ++k) load_docs<ORD, HIST, MET, VK>(P, doc_of(k), q[k]);
 
     bool use_lds = P.lds_mode != 0;
     auto step = [&](uint32_t i, Doc4& q) {
@@ -559,11 +562,11 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
         } else {
             process4<ORD, HIST, MET, false, KT, kMS>(P, g, q, T, base, win0, run);
         }
-        load_docs<ORD, HIST, MET, VK>(P, doc_of(i + 2), q);
+        load_docs<ORD, HIST, MET, VK>(P, doc_of(i + kBuf), q);
     };
-    for (uint32_t i = 0; i < n_it; i += 2) {
-        step(i, qa);
-        step(i + 1, qb);
+    for (uint32_t i = 0; i < n_it; i += kBuf) {
+#pragma unroll
+        for (int k = 0; k < kBuf; ++k) step(i + k, q[k]);
     }
     if (P.lds_mode && (dirty || !(HIST && P.windowed))) {
         if (!ORD) run_flush<MET, kMS>(P, s, run);
