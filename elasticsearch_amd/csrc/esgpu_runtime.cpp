@@ -1292,7 +1292,7 @@ static bool collect_partitioned(esgpu_plan* p, Pipeline& pl, const esgpu_segment
     Q.G = (Q.n_blocks + Q.blocks_per_wg - 1) / Q.blocks_per_wg;
     Q.ord = oc->ords().as<uint32_t>();
     Q.T = pl.T;
-    Q.shift = kPartShift;  // 16384 ordinals per partition: 64 KB of LDS counters in the counting pass
+    Q.shift = kPartShift;  // 32768 ordinals per partition: 128 KB of LDS counters in the counting pass
     Q.P = (uint32_t)(((uint64_t)pl.T + (1u << Q.shift) - 1) >> Q.shift);
     require(Q.P >= 1 && Q.P <= kPartMaxStaged, ESGPU_ERR_INVALID, "partition count out of range");
     Q.npred = npred;
