@@ -1356,7 +1356,12 @@ __device__ __forceinline__ void count_run(uint32_t* cnt, uint32_t& cur, uint32_t
     n = 1;
 }
 
-__global__ __launch_bounds__(kWG) void part_count_kernel(PartParams P) {
+#ifndef ESGPU_COUNT_WG
+#define ESGPU_COUNT_WG 512
+#endif
+constexpr int kCountWG = ESGPU_COUNT_WG;  // one counting workgroup per CU at 128 KB of LDS counters
+
+__global__ __launch_bounds__(kCountWG) void part_count_kernel(PartParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t* cnt = (uint32_t*)smem;
     const uint32_t S = 1u << P.shift;
@@ -1376,12 +1381,12 @@ __global__ __launch_bounds__(kWG) void part_count_kernel(PartParams P) {
         if (qb >= e1) break;
         const uint32_t s0 = max(e0, qb), s1 = min(e1, qe);
         if (s0 >= s1) continue;
-        for (uint32_t i = threadIdx.x; i < S; i += kWG) cnt[i] = 0;
+        for (uint32_t i = threadIdx.x; i < S; i += kCountWG) cnt[i] = 0;
         __syncthreads();
         uint32_t cur = 0, n = 0;
         uint32_t i0 = s0;
         const uint32_t a0 = min(s1, (s0 + 7u) & ~7u);  // head up to a 16-byte boundary
-        for (uint32_t i = i0 + threadIdx.x; i < a0; i += kWG) count_run(cnt, cur, n, P.pbuf[i]);
+        for (uint32_t i = i0 + threadIdx.x; i < a0; i += kCountWG) count_run(cnt, cur, n, P.pbuf[i]);
         const uint32_t nvec = (s1 - a0) / 8;
         const uint4* v8 = reinterpret_cast<const uint4*>(P.pbuf + a0);
         // two buffers of 2 x 16 bytes (16 offsets), each reloaded right after it is counted; loads are unconditional
@@ -1389,12 +1394,12 @@ __global__ __launch_bounds__(kWG) void part_count_kernel(PartParams P) {
         if (nvec > 0) {
             auto ld = [&](uint32_t k, uint4 v[2]) {
                 v[0] = v8[min(k, nvec - 1)];
-                v[1] = v8[min(k + kWG, nvec - 1)];
+                v[1] = v8[min(k + kCountWG, nvec - 1)];
             };
             auto count8 = [&](uint32_t k, const uint4 v[2]) {
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    if (k + h * kWG >= nvec) break;
+                    if (k + h * kCountWG >= nvec) break;
                     const uint32_t w[4] = {v[h].x, v[h].y, v[h].z, v[h].w};
 #pragma unroll
                     for (int t = 0; t < 4; ++t) {
@@ -1405,20 +1410,20 @@ __global__ __launch_bounds__(kWG) void part_count_kernel(PartParams P) {
             };
             uint4 va[2], vb[2];
             ld(threadIdx.x, va);
-            ld(threadIdx.x + 2 * kWG, vb);
-            for (uint32_t k = threadIdx.x; k < nvec; k += 4 * kWG) {
+            ld(threadIdx.x + 2 * kCountWG, vb);
+            for (uint32_t k = threadIdx.x; k < nvec; k += 4 * kCountWG) {
                 count8(k, va);
-                ld(k + 4 * kWG, va);
-                count8(k + 2 * kWG, vb);
-                ld(k + 6 * kWG, vb);
+                ld(k + 4 * kCountWG, va);
+                count8(k + 2 * kCountWG, vb);
+                ld(k + 6 * kCountWG, vb);
             }
         }
-        for (uint32_t i = a0 + nvec * 8 + threadIdx.x; i < s1; i += kWG) count_run(cnt, cur, n, P.pbuf[i]);
+        for (uint32_t i = a0 + nvec * 8 + threadIdx.x; i < s1; i += kCountWG) count_run(cnt, cur, n, P.pbuf[i]);
         if (n) atomicAdd(&cnt[cur], n);
         __syncthreads();
         const bool whole = s0 == qb && s1 == qe;  // the only writer of this partition in this launch
         const uint32_t base = q << P.shift;
-        for (uint32_t j = threadIdx.x; j < S; j += kWG) {
+        for (uint32_t j = threadIdx.x; j < S; j += kCountWG) {
             const uint32_t c = cnt[j];
             if (c == 0 || base + j >= P.T) continue;
             if (whole) P.counts[base + j] += c;
@@ -1431,7 +1436,7 @@ __global__ __launch_bounds__(kWG) void part_count_kernel(PartParams P) {
 void launch_part_count(const PartParams& p, hipStream_t s) {
     const uint32_t grid = (uint32_t)(((uint64_t)p.n_docs + p.chunk - 1) / p.chunk);
     if (grid == 0) return;
-    hipLaunchKernelGGL(part_count_kernel, dim3(grid), dim3(kWG), (size_t)4 << p.shift, s, p);
+    hipLaunchKernelGGL(part_count_kernel, dim3(grid), dim3(kCountWG), (size_t)4 << p.shift, s, p);
 }
 
 // ------------------------------------------------------------------------------------------------------------
