@@ -207,16 +207,18 @@ struct Acc {
     uint32_t* ocnt32;
     unsigned long long* ocnt64;
     uint32_t mstride;               // LDS min/max stride; 1 in the global grid
+    uint32_t coff;                  // this lane's copy of the additive LDS cells (CollectParams.ncopies); 0 in the grid
 };
 
 template <int MET, bool LDS, int MS>
 __device__ __forceinline__ void add_value(const Acc& a, uint32_t c, double x, bool has_vcnt) {
+    const uint32_t ca = LDS ? c + a.coff : c;  // additive cell (lane copy)
     if (LDS) {
-        if (has_vcnt) atomicAdd(&a.vcnt32[c], 1u);
+        if (has_vcnt) atomicAdd(&a.vcnt32[ca], 1u);
     } else {
         if (has_vcnt) atomicAdd(&a.vcnt64[c], 1ull);
     }
-    atomicAdd(&a.sum[c], x);
+    atomicAdd(&a.sum[ca], x);
     if (MET >= 2) {
         const bool nan = x != x;
         const unsigned long long e = sortable(x);
@@ -228,7 +230,7 @@ __device__ __forceinline__ void add_value(const Acc& a, uint32_t c, double x, bo
         if (emn < cmn) atomicMin(&a.mn[c * st], emn);
         if (emx > cmx) atomicMax(&a.mx[c * st], emx);
     }
-    if (MET >= 3) atomicAdd(&a.sq[c], x * x);  // ExtendedStatsAggregator: sumOfSqr += value * value (no FMA)
+    if (MET >= 3) atomicAdd(&a.sq[ca], x * x);  // ExtendedStatsAggregator: sumOfSqr += value * value (no FMA)
 }
 
 // Per-doc update.  `slot` is the key index relative to the accumulator's first slot (window or grid).
@@ -244,7 +246,7 @@ __device__ __forceinline__ void update_doc(const CollectParams& P, const Acc& a,
     }
     if (!(has_t && has_h)) return;
     const uint32_t c = slot * T + t;
-    if (LDS) atomicAdd(&a.cnt32[c], 1u); else atomicAdd(&a.cnt64[c], 1ull);
+    if (LDS) atomicAdd(&a.cnt32[c + a.coff], 1u); else atomicAdd(&a.cnt64[c], 1ull);
     if (MET > 0 && mpres) add_value<MET, LDS, MS>(a, c, x, P.vcnt_mode != 0);
 }
 
@@ -397,7 +399,7 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
 }
 
 template <int MET, int MS>
-__device__ void flush_window(const CollectParams& P, const Acc& s, uint32_t T, uint32_t W, uint32_t win0) {
+__device__ void flush_window(const CollectParams& P, const Acc& s, uint32_t T, uint32_t W, uint32_t win0, uint32_t ncp = 1) {
     __syncthreads();
     const uint32_t C = T * W;
     if (P.ocnt_mode == OCNT_TERMS_DERIVED) {  // per-term totals of this window (one atomic per term)
@@ -409,7 +411,8 @@ __device__ void flush_window(const CollectParams& P, const Acc& s, uint32_t T, u
         __syncthreads();
     }
     for (uint32_t c = threadIdx.x; c < C; c += kWG) {
-        const uint32_t n = s.cnt32[c];
+        uint32_t n = 0;
+        for (uint32_t k = 0; k < ncp; ++k) n += s.cnt32[k * C + c];
         if (n == 0) continue;
         const uint32_t local = c / T;
         const uint32_t t = c - local * T;
@@ -417,11 +420,16 @@ __device__ void flush_window(const CollectParams& P, const Acc& s, uint32_t T, u
         if (slot >= P.H) continue;
         const size_t g = (size_t)slot * T + t;
         atomicAdd(&P.g_cnt[g], (unsigned long long)n);
-        s.cnt32[c] = 0;
+        for (uint32_t k = 0; k < ncp; ++k) s.cnt32[k * C + c] = 0;
         if (MET > 0) {
-            if (P.vcnt_mode) { atomicAdd(&P.g_vcnt[g], (unsigned long long)s.vcnt32[c]); s.vcnt32[c] = 0; }
-            atomicAdd(&P.g_sum[g], s.sum[c]);
-            s.sum[c] = 0.0;
+            if (P.vcnt_mode) {
+                uint32_t vc = 0;
+                for (uint32_t k = 0; k < ncp; ++k) { vc += s.vcnt32[k * C + c]; s.vcnt32[k * C + c] = 0; }
+                atomicAdd(&P.g_vcnt[g], (unsigned long long)vc);
+            }
+            double sum = 0.0;
+            for (uint32_t k = 0; k < ncp; ++k) { sum += s.sum[k * C + c]; s.sum[k * C + c] = 0.0; }
+            atomicAdd(&P.g_sum[g], sum);
             if (MET >= 2) {
                 const unsigned long long mn = s.mn[MS * c], mx = s.mx[MS * c];
                 if (mn != kMinInit) atomicMin(&P.g_min[g], mn);
@@ -429,7 +437,11 @@ __device__ void flush_window(const CollectParams& P, const Acc& s, uint32_t T, u
                 s.mn[MS * c] = kMinInit;
                 s.mx[MS * c] = kMaxInit;
             }
-            if (MET >= 3) { atomicAdd(&P.g_sq[g], s.sq[c]); s.sq[c] = 0.0; }
+            if (MET >= 3) {
+                double sq = 0.0;
+                for (uint32_t k = 0; k < ncp; ++k) { sq += s.sq[k * C + c]; s.sq[k * C + c] = 0.0; }
+                atomicAdd(&P.g_sq[g], sq);
+            }
         }
     }
     if (P.ocnt_mode == OCNT_TERMS) {
@@ -464,7 +476,9 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
     g.cnt32 = nullptr; g.vcnt32 = nullptr; g.ocnt32 = nullptr;
     g.cnt64 = P.g_cnt; g.vcnt64 = P.g_vcnt; g.sum = P.g_sum; g.mn = P.g_min; g.mx = P.g_max; g.sq = P.g_sq;
     g.mstride = 1;
+    g.coff = 0;
     g.ocnt64 = P.g_ocnt;
+    const uint32_t ncp = (ORD && !HIST) ? max(P.ncopies, 1u) : 1u;  // additive cell copies (terms-only grids)
 
     // LDS window view.  Every pointer is derived from `smem` alone -- never merged with a global pointer -- so the
     // compiler keeps them in the LDS address space (ds_* instructions).  A generic pointer would compile to flat_*
@@ -474,24 +488,26 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
         size_t off = 0;
         auto carve = [&](size_t bytes) { unsigned char* p = smem + off; off += (bytes + 15) & ~(size_t)15; return p; };
         s.cnt64 = nullptr; s.vcnt64 = nullptr; s.ocnt64 = nullptr;
-        s.cnt32 = (uint32_t*)carve(sizeof(uint32_t) * C);
-        s.vcnt32 = (uint32_t*)carve(P.vcnt_mode ? sizeof(uint32_t) * C : 0);
-        s.sum = (double*)carve(MET > 0 ? sizeof(double) * C : 0);
+        s.cnt32 = (uint32_t*)carve(sizeof(uint32_t) * C * ncp);
+        s.vcnt32 = (uint32_t*)carve(P.vcnt_mode ? sizeof(uint32_t) * C * ncp : 0);
+        s.sum = (double*)carve(MET > 0 ? sizeof(double) * C * ncp : 0);
         s.mn = (unsigned long long*)carve(MET >= 2 ? 16 * C : 0);
         s.mx = s.mn + (kMS == 2 ? 1 : C);
         s.mstride = kMS;
-        s.sq = (double*)carve(MET >= 3 ? sizeof(double) * C : 0);
+        s.sq = (double*)carve(MET >= 3 ? sizeof(double) * C * ncp : 0);
+        s.coff = ((threadIdx.x & 63) % ncp) * C;
         s.ocnt32 = (uint32_t*)carve(P.ocnt_mode == OCNT_TERMS ? sizeof(uint32_t) * T
                                     : P.ocnt_mode == OCNT_HIST ? sizeof(uint32_t) * W : 0);
     }
     if (P.lds_mode) {
-        for (uint32_t c = threadIdx.x; c < C; c += kWG) {
+        for (uint32_t c = threadIdx.x; c < C * ncp; c += kWG) {
             s.cnt32[c] = 0;
             if (P.vcnt_mode) s.vcnt32[c] = 0;
             if (MET > 0) s.sum[c] = 0.0;
-            if (MET >= 2) { s.mn[kMS * c] = kMinInit; s.mx[kMS * c] = kMaxInit; }
             if (MET >= 3) s.sq[c] = 0.0;
         }
+        for (uint32_t c = threadIdx.x; c < C; c += kWG)
+            if (MET >= 2) { s.mn[kMS * c] = kMinInit; s.mx[kMS * c] = kMaxInit; }
         if (P.ocnt_mode == OCNT_TERMS || P.ocnt_mode == OCNT_HIST)
             for (uint32_t c = threadIdx.x; c < (P.ocnt_mode == OCNT_TERMS ? T : W); c += kWG) s.ocnt32[c] = 0;
         __syncthreads();
@@ -546,7 +562,7 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
                     } else if (!win_set || kmn < (int64_t)win0 || kmx >= (int64_t)win0 + (int64_t)W) {
                         if (dirty) {
                             if (!ORD) run_flush<MET, kMS>(P, s, run);
-                            flush_window<MET, kMS>(P, s, T, W, win0);
+                            flush_window<MET, kMS>(P, s, T, W, win0, ncp);
                         }
                         dirty = false;
                         win0 = (uint32_t)kmn;
@@ -570,7 +586,7 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
     }
     if (P.lds_mode && (dirty || !(HIST && P.windowed))) {
         if (!ORD) run_flush<MET, kMS>(P, s, run);
-        flush_window<MET, kMS>(P, s, T, W, win0);
+        flush_window<MET, kMS>(P, s, T, W, win0, ncp);
     }
 }
 
@@ -650,14 +666,15 @@ int collect_occupancy(bool ord, int hk, int met, size_t lds, int vk) {
     return hk == 2 ? occ_m<false, 2>(met, lds, vk) : hk == 1 ? occ_m<false, 1>(met, lds, vk) : occ_m<false, 0>(met, lds, vk);
 }
 
-size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode) {
+size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode, uint32_t ncopies) {
     const size_t C = (size_t)T * W;
+    const size_t n = std::max(ncopies, 1u);
     auto r = [](size_t b) { return (b + 15) & ~(size_t)15; };
-    size_t bytes = r(4 * C);
-    if (vcnt_mode) bytes += r(4 * C);
-    if (met > 0) bytes += r(8 * C);
+    size_t bytes = r(4 * C * n);
+    if (vcnt_mode) bytes += r(4 * C * n);
+    if (met > 0) bytes += r(8 * C * n);
     if (met >= 2) bytes += r(16 * C);
-    if (met >= 3) bytes += r(8 * C);
+    if (met >= 3) bytes += r(8 * C * n);
     if (ocnt_mode == OCNT_TERMS) bytes += r(4 * (size_t)T);
     if (ocnt_mode == OCNT_HIST) bytes += r(4 * (size_t)W);
     return bytes;
@@ -1740,6 +1757,7 @@ __global__ __launch_bounds__(kWG) void collect_multi_kernel(CollectParams P) {
     g.cnt32 = nullptr; g.vcnt32 = nullptr; g.ocnt32 = nullptr;
     g.cnt64 = P.g_cnt; g.vcnt64 = P.g_vcnt; g.sum = P.g_sum; g.mn = P.g_min; g.mx = P.g_max; g.sq = P.g_sq;
     g.mstride = 1;
+    g.coff = 0;
     g.ocnt64 = P.g_ocnt;
     Acc s;
     {
@@ -1752,6 +1770,7 @@ __global__ __launch_bounds__(kWG) void collect_multi_kernel(CollectParams P) {
         s.mn = (unsigned long long*)carve(MET >= 2 ? 16 * C : 0);
         s.mx = s.mn + 1;
         s.mstride = 2;
+        s.coff = 0;
         s.sq = (double*)carve(MET >= 3 ? sizeof(double) * C : 0);
         s.ocnt32 = (uint32_t*)carve(P.ocnt_mode == OCNT_TERMS ? sizeof(uint32_t) * T : P.ocnt_mode == OCNT_HIST ? sizeof(uint32_t) * H : 0);
     }

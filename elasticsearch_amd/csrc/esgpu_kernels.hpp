@@ -69,6 +69,8 @@ struct CollectParams {
     int32_t mv_f64;
     int32_t vcnt_mode;   // separate value counts (metric column has missing values)
     int32_t ocnt_mode;   // separate outer-level doc counts (inner dimension column has missing values)
+    uint32_t ncopies;    // terms-only LDS grids: copies of the additive cells (count, value count, sum, sum of squares);
+                         // lane l adds into copy l % ncopies, so hot terms collide on ncopies addresses, not one
     int32_t npred;
     PredDev pred[4];
     const uint64_t* accept;
@@ -123,7 +125,7 @@ void launch_zone_map(const int64_t* v, const uint64_t* present, uint32_t n, int6
                      hipStream_t s);
 void launch_synth(const SynthParams& p, hipStream_t s);
 void launch_collect(const CollectParams& p, bool ord, bool hist, int met, uint32_t grid, size_t lds, hipStream_t s);
-size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode);
+size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode, uint32_t ncopies = 1);
 // resident workgroups per CU (hk: 0 none, 1 affine, 2 table; vk: bit 0 double histogram column, bit 1 double metric)
 int collect_occupancy(bool ord, int hk, int met, size_t lds, int vk);
 void launch_hll(const HllParams& p, uint32_t cus, hipStream_t s);

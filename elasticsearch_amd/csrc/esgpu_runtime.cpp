@@ -1440,6 +1440,11 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
     return done;
 }
 
+#ifndef ESGPU_TERMS_COPIES
+#define ESGPU_TERMS_COPIES 4
+#endif
+static constexpr uint32_t kTermsCopies = ESGPU_TERMS_COPIES;
+
 static bool collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
     const bool ORD = pl.term_spec >= 0, HIST = pl.hist_spec >= 0;
     const DevColumn* oc = ORD ? s->col(pl.ord_field.c_str()) : nullptr;
@@ -1564,6 +1569,15 @@ static bool collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment*
         }
     }
     P.W = W;
+    // terms-only grids: lane-rotated copies of the additive cells while they still fit two workgroups per CU (the
+    // Zipf-head terms otherwise serialise a wave's LDS atomics on one address)
+    P.ncopies = 1;
+    if (P.lds_mode && ORD && !HIST) {
+        for (uint32_t nc = kTermsCopies; nc > 1; nc /= 2) {
+            const size_t b = collect_lds_bytes(pl.T, W, met_launch, pl.vcnt_mode, pl.ocnt_mode, nc);
+            if (b <= kLdsPair) { P.ncopies = nc; lds = b; break; }
+        }
+    }
     if (!P.lds_mode && ORD && !HIST && met_launch == 0 && !pl.vcnt_mode && pl.ocnt_mode == OCNT_NONE &&
         (((uint64_t)pl.T + (1u << kPartShift) - 1) >> kPartShift) <= kPartMaxStaged) {
         p->last_bytes += bytes_per_doc * (uint64_t)s->max_doc + (d_accept ? ((uint64_t)s->max_doc + 7) / 8 : 0);
