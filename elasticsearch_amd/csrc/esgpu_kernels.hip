@@ -405,7 +405,8 @@ __device__ void flush_window(const CollectParams& P, const Acc& s, uint32_t T, u
     if (P.ocnt_mode == OCNT_TERMS_DERIVED) {  // per-term totals of this window (one atomic per term)
         for (uint32_t t = threadIdx.x; t < T; t += kWG) {
             uint32_t tot = 0;
-            for (uint32_t l = 0; l < W; ++l) tot += s.cnt32[l * T + t];
+            for (uint32_t k = 0; k < ncp; ++k)
+                for (uint32_t l = 0; l < W; ++l) tot += s.cnt32[k * C + l * T + t];
             if (tot) atomicAdd(&P.g_ocnt[t], (unsigned long long)tot);
         }
         __syncthreads();
@@ -478,7 +479,7 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
     g.mstride = 1;
     g.coff = 0;
     g.ocnt64 = P.g_ocnt;
-    const uint32_t ncp = (ORD && !HIST) ? max(P.ncopies, 1u) : 1u;  // additive cell copies (terms-only grids)
+    const uint32_t ncp = ORD ? max(P.ncopies, 1u) : 1u;  // additive cell copies (grids with a terms dimension)
 
     // LDS window view.  Every pointer is derived from `smem` alone -- never merged with a global pointer -- so the
     // compiler keeps them in the LDS address space (ds_* instructions).  A generic pointer would compile to flat_*

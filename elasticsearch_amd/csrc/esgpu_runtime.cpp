@@ -1443,6 +1443,9 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
 #ifndef ESGPU_TERMS_COPIES
 #define ESGPU_TERMS_COPIES 4
 #endif
+#ifndef ESGPU_COPIES_HIST
+#define ESGPU_COPIES_HIST 0  // terms x histogram grids: copies measured within noise
+#endif
 static constexpr uint32_t kTermsCopies = ESGPU_TERMS_COPIES;
 
 static bool collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
@@ -1569,10 +1572,10 @@ static bool collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment*
         }
     }
     P.W = W;
-    // terms-only grids: lane-rotated copies of the additive cells while they still fit two workgroups per CU (the
-    // Zipf-head terms otherwise serialise a wave's LDS atomics on one address)
+    // grids with a terms dimension: lane-rotated copies of the additive cells while they still fit two workgroups per
+    // CU (the Zipf-head terms otherwise serialise a wave's LDS atomics on one address)
     P.ncopies = 1;
-    if (P.lds_mode && ORD && !HIST) {
+    if (P.lds_mode && ORD && (!HIST || ESGPU_COPIES_HIST)) {
         for (uint32_t nc = kTermsCopies; nc > 1; nc /= 2) {
             const size_t b = collect_lds_bytes(pl.T, W, met_launch, pl.vcnt_mode, pl.ocnt_mode, nc);
             if (b <= kLdsPair) { P.ncopies = nc; lds = b; break; }
