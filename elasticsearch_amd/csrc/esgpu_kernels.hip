@@ -840,6 +840,13 @@ __global__ __launch_bounds__(kHllWG) void hll_registers_fast_kernel(HllParams P,
 // still a lower bound (registers only grow, and every nibble written came with an atomicMax of at least its value).
 constexpr uint32_t kHllLdsWG = 1024;
 constexpr uint32_t kHllLdsIter = kHllLdsWG * 4;
+#ifndef ESGPU_HLL_BITS
+#define ESGPU_HLL_BITS 4
+#endif
+constexpr uint32_t kHllBits = ESGPU_HLL_BITS;            // bits per register bound in the snapshot (4: 128 KB at p = 18)
+constexpr uint32_t kHllPerByte = 8 / kHllBits;
+constexpr uint32_t kHllMaxDelta = (1u << kHllBits) - 1;
+__host__ __device__ constexpr uint32_t hll_snap_bytes(uint32_t m) { return m / kHllPerByte; }
 
 template <int KIND>
 __global__ __launch_bounds__(kHllLdsWG) void hll_registers_lds_kernel(HllParams P, uint32_t d_begin, uint32_t d_end,
@@ -847,7 +854,7 @@ __global__ __launch_bounds__(kHllLdsWG) void hll_registers_lds_kernel(HllParams 
     extern __shared__ __attribute__((aligned(16))) unsigned char nib[];  // [2^p / 2] packed nibbles
     const uint32_t F = min(*floor_ptr, 64u - (uint32_t)P.p);
     const uint64_t zmask = F == 0 ? 0ull : (((1ull << F) - 1ull) << (64 - P.p - F));  // rl > F <=> these bits are 0
-    const uint32_t nbytes = (1u << P.p) >> 1;
+    const uint32_t nbytes = hll_snap_bytes(1u << P.p);
     if ((nbytes & 15u) == 0) {
         for (uint32_t i = threadIdx.x * 16; i < nbytes; i += kHllLdsWG * 16)
             *reinterpret_cast<u32x4_t*>(nib + i) = load16(P.snap + i);
@@ -872,11 +879,12 @@ __global__ __launch_bounds__(kHllLdsWG) void hll_registers_lds_kernel(HllParams 
             if ((uint32_t)j < lim && (h & zmask) == 0) {
                 const uint32_t rl = hll_run_len(h, P.p);
                 const uint32_t idx = hll_index(h, P.p);
-                const uint32_t byte = nib[idx >> 1];
-                const uint32_t sh = (idx & 1u) * 4u;
-                if (rl > F + ((byte >> sh) & 15u)) {
+                const uint32_t bi = idx / kHllPerByte;
+                const uint32_t byte = nib[bi];
+                const uint32_t sh = (idx % kHllPerByte) * kHllBits;
+                if (rl > F + ((byte >> sh) & kHllMaxDelta)) {
                     atomicMax(&P.regs[idx], rl);
-                    nib[idx >> 1] = (unsigned char)((byte & ~(15u << sh)) | (min(rl - F, 15u) << sh));
+                    nib[bi] = (unsigned char)((byte & ~(kHllMaxDelta << sh)) | (min(rl - F, kHllMaxDelta) << sh));
                 }
             }
         }
@@ -898,9 +906,11 @@ __global__ __launch_bounds__(256) void hll_snapshot_kernel(const unsigned int* r
                                                            unsigned char* snap) {
     const uint32_t F = *floor_ptr;
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (2 * i >= m) return;
-    const uint32_t lo = min(regs[2 * i] - F, 15u), hi = min(regs[2 * i + 1] - F, 15u);
-    snap[i] = (unsigned char)(lo | (hi << 4));
+    if (kHllPerByte * i >= m) return;
+    uint32_t b = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kHllPerByte; ++k) b |= min(regs[kHllPerByte * i + k] - F, kHllMaxDelta) << (k * kHllBits);
+    snap[i] = (unsigned char)b;
 }
 
 // group floors: one wave per group of 64 registers; the global floor is their min (*out initialised to ~0), one
@@ -1027,14 +1037,14 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
         const unsigned int* fl = ph == 0 ? (const unsigned int*)nullptr : (const unsigned int*)p.floor;
         if (lds && ph > 0) {
             // one 1024-thread workgroup per CU (128 KB of nibbles at p = 18), more for smaller p
-            const uint32_t per_cu = std::max(1u, std::min(4u, (uint32_t)(160u * 1024u / (m / 2 + 1024u))));
+            const uint32_t per_cu = std::max(1u, std::min(4u, (uint32_t)(160u * 1024u / (hll_snap_bytes(m) + 1024u))));
             uint32_t lw = std::max(1u, std::min(cus * per_cu, span / (kHllLdsIter * 4)));
             const uint32_t lper = ((span + lw - 1) / lw + 3) & ~3u;
             lw = (span + lper - 1) / lper;
             if (p.kind == HLL_I64)
-                hipLaunchKernelGGL(hll_registers_lds_kernel<HLL_I64>, dim3(lw), dim3(kHllLdsWG), m / 2, st, p, cuts[ph], cuts[ph + 1], lper, fl);
+                hipLaunchKernelGGL(hll_registers_lds_kernel<HLL_I64>, dim3(lw), dim3(kHllLdsWG), hll_snap_bytes(m), st, p, cuts[ph], cuts[ph + 1], lper, fl);
             else
-                hipLaunchKernelGGL(hll_registers_lds_kernel<HLL_F64>, dim3(lw), dim3(kHllLdsWG), m / 2, st, p, cuts[ph], cuts[ph + 1], lper, fl);
+                hipLaunchKernelGGL(hll_registers_lds_kernel<HLL_F64>, dim3(lw), dim3(kHllLdsWG), hll_snap_bytes(m), st, p, cuts[ph], cuts[ph + 1], lper, fl);
         } else if (fast && p.kind == HLL_I64)
             hipLaunchKernelGGL(hll_registers_fast_kernel<HLL_I64>, dim3(wgs), dim3(kHllWG), 0, st, p, cuts[ph], cuts[ph + 1], per, fl);
         else if (fast && p.kind == HLL_F64)
@@ -1050,7 +1060,7 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
                 hipLaunchKernelGGL(hll_group_floor_kernel, dim3((ng + 15) / 16), dim3(1024), 0, st, (const unsigned int*)p.regs, m,
                                    p.gfloor, p.floor);
                 if (lds)
-                    hipLaunchKernelGGL(hll_snapshot_kernel, dim3((m / 2 + 255) / 256), dim3(256), 0, st, (const unsigned int*)p.regs, m,
+                    hipLaunchKernelGGL(hll_snapshot_kernel, dim3((hll_snap_bytes(m) + 255) / 256), dim3(256), 0, st, (const unsigned int*)p.regs, m,
                                        (const unsigned int*)p.floor, p.snap);
             } else {
                 hipLaunchKernelGGL(hll_floor_kernel, dim3(floor_grid), dim3(1024), 0, st, (const unsigned int*)p.regs, m, p.floor);
