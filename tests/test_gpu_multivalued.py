@@ -160,3 +160,14 @@ def test_multi_valued_double_histogram(engine):
 def test_multi_valued_keyword_range(engine):  # a doc matches if any of its terms is in the range
     aggs = [AB.terms("host").field("host").size(10), AB.cardinality("c").field("codes")]
     check(engine, aggs, segment(N_DOCS, 13), N_DOCS, filters=[QB.rangeQuery("tags").gte("tag-050").lt("tag-060")])
+
+
+def test_filter_aggregation_over_multi_valued_fields(engine):  # FilterAggregator on CSR columns (a doc matches if any value does)
+    cols = segment(N_DOCS, 11)
+    aggs = [AB.filter("tagged", [QB.termQuery("tags", "tag-007"), QB.rangeQuery("codes").gte(100).lt(300)])
+            .subAggregation(AB.terms("tags").field("tags").size(10).subAggregation(AB.avg("p").field("prices")))
+            .subAggregation(AB.dateHistogram("d").field("dates").interval("1d"))
+            .subAggregation(AB.cardinality("c").field("codes").precisionThreshold(200)),
+            AB.stats("all_prices").field("prices")]
+    got = check(engine, aggs, cols, N_DOCS, filters=[QB.rangeQuery("response_time_ms").lt(700)])
+    assert got["tagged"]["doc_count"] > 0
