@@ -863,9 +863,18 @@ void r_block(R& r, Block& a, int depth) {
         if (a.hll_present.size() != a.n || a.hll_mode.size() != a.n || a.regs.size() != a.n || a.lc.size() != a.n)
             throw std::runtime_error("inconsistent cardinality block");
         if (a.precision < 4 || a.precision > 18) throw std::runtime_error("bad precision");
-        for (uint64_t i = 0; i < a.n; ++i)
+        // every value the reduce decodes must stay in range: unflagged encoded hashes carry a 25-bit index
+        // (dec_index < 2^p), flagged ones a run length of at most 64 - 25 + 1, registers at most 64 - p + 1
+        const uint32_t max_rl = (uint32_t)(64 - a.precision + 1);
+        for (uint64_t i = 0; i < a.n; ++i) {
             if (a.hll_present[i] && a.hll_mode[i] && a.regs[i].size() != ((size_t)1 << a.precision))
                 throw std::runtime_error("bad register array");
+            for (uint8_t r : a.regs[i]) if (r > max_rl) throw std::runtime_error("bad register value");
+            for (uint32_t e : a.lc[i]) {
+                if (e & 1) { if (((e >> 1) & 0x3F) > 64 - kP2 + 1) throw std::runtime_error("bad encoded hash"); }
+                else if (e >= (1u << (kP2 + 1))) throw std::runtime_error("bad encoded hash");
+            }
+        }
     } else if (a.count.size() != a.n || a.sum.size() != a.n || a.min.size() != a.n || a.max.size() != a.n ||
                a.sumsq.size() != a.n) {
         throw std::runtime_error("inconsistent metric block");

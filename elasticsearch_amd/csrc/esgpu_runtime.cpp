@@ -269,15 +269,54 @@ extern "C" int esgpu_synthetic_fill_host(uint64_t seed, uint32_t shard, uint32_t
 // ------------------------------------------------------------------------------------------------------------
 // segments
 // ------------------------------------------------------------------------------------------------------------
-// Global term dictionary of one keyword field over the segments of a reader (Lucene OrdinalMap).
-struct GlobalDict {
+// An immutable term dictionary (ordinal -> term bytes, sorted by unsigned bytes): a segment's own SortedSet dictionary,
+// the synthetic formula, or the reader-wide global dictionary of an ordinal map (Lucene OrdinalMap).  Shared by the
+// segments that use it and by the plans that resolve winners through it, so a plan never copies a dictionary and a
+// destroyed segment never invalidates a plan's terms.  `identity` is a content hash: two dictionaries with equal
+// identity number their terms the same way, so their ordinals may be counted into one grid.
+struct TermDict {
+    uint32_t synth_bit = 0;          // synthetic formula (esgpu_synthetic_term)
+    bool numbered = false;           // no term bytes given: term(ord) = decimal ordinal
+    uint64_t n = 0;
     std::vector<uint8_t> bytes;
-    std::vector<uint64_t> offsets;  // count + 1
-    uint64_t count() const { return offsets.empty() ? 0 : offsets.size() - 1; }
-    std::string term(uint64_t g) const {
-        return std::string((const char*)bytes.data() + offsets[g], (size_t)(offsets[g + 1] - offsets[g]));
+    std::vector<uint64_t> offsets;   // n + 1 (explicit dictionaries)
+    uint64_t identity = 0;
+    uint64_t count() const { return n; }
+    std::string_view view(uint64_t o, std::string& scratch) const {
+        if (synth_bit) {
+            char b[32];
+            esgpu_synthetic_term(synth_bit, o, b, sizeof b);
+            scratch = b;
+            return scratch;
+        }
+        if (numbered) {
+            scratch = std::to_string(o);
+            return scratch;
+        }
+        return std::string_view((const char*)bytes.data() + offsets[o], (size_t)(offsets[o + 1] - offsets[o]));
+    }
+    std::string term(uint64_t o) const {
+        std::string s;
+        return std::string(view(o, s));
+    }
+    void seal() {  // FNV-1a over (kind, count, offsets, bytes)
+        uint64_t h = 0xcbf29ce484222325ULL;
+        auto mix = [&](const void* p, size_t len) {
+            const uint8_t* b = (const uint8_t*)p;
+            for (size_t i = 0; i < len; ++i) { h ^= b[i]; h *= 0x100000001b3ULL; }
+        };
+        const uint32_t kind = synth_bit ? synth_bit : numbered ? 0x80000000u : 0x40000000u;
+        mix(&kind, sizeof kind);
+        mix(&n, sizeof n);
+        if (!offsets.empty()) mix(offsets.data(), offsets.size() * 8);
+        if (!bytes.empty()) mix(bytes.data(), bytes.size());
+        identity = h;
     }
 };
+
+static bool same_dict(const std::shared_ptr<const TermDict>& a, const std::shared_ptr<const TermDict>& b) {
+    return a == b || (a && b && a->n == b->n && a->identity == b->identity);
+}
 
 struct DevColumn {
     std::string name;
@@ -290,28 +329,17 @@ struct DevColumn {
     DevBuf zmin, zmax;
     int64_t vmin = INT64_MAX, vmax = INT64_MIN;  // over present values (I64 columns)
     uint64_t value_count = 0;
-    // host dictionary (ORD): explicit bytes, or the synthetic formula
-    std::vector<uint8_t> dict_bytes;
-    std::vector<uint64_t> dict_offsets;
-    uint32_t synth_bit = 0;
+    std::shared_ptr<const TermDict> dict;   // ORD: the segment's own dictionary (value_count terms)
     DevBuf ord_hash;  // murmur3 h1 per term (built lazily for cardinality on keyword fields)
     // global ordinals (esgpu_ordinal_map_build): the segment's ordinals remapped into the reader-wide dictionary
-    std::shared_ptr<const GlobalDict> gdict;
+    std::shared_ptr<const TermDict> gdict;
     DevBuf gvalues;
 
     const DevBuf& ords() const { return gdict ? gvalues : values; }       // what terms aggregations count by
     uint64_t ord_count() const { return gdict ? gdict->count() : value_count; }
-    std::string ord_term(uint64_t ord) const { return gdict ? gdict->term(ord) : term(ord); }
-
-    std::string term(uint64_t ord) const {
-        if (synth_bit) {
-            char b[32];
-            esgpu_synthetic_term(synth_bit, ord, b, sizeof b);
-            return b;
-        }
-        if (dict_offsets.empty()) return std::to_string(ord);
-        return std::string((const char*)dict_bytes.data() + dict_offsets[ord], (size_t)(dict_offsets[ord + 1] - dict_offsets[ord]));
-    }
+    const std::shared_ptr<const TermDict>& ord_dict() const { return gdict ? gdict : dict; }
+    std::string ord_term(uint64_t ord) const { return ord_dict()->term(ord); }
+    std::string term(uint64_t ord) const { return dict->term(ord); }
 };
 
 struct esgpu_segment {
@@ -325,6 +353,22 @@ struct esgpu_segment {
         return it == cols.end() ? nullptr : it->second.get();
     }
 };
+
+// the synthetic dictionaries (host-%04d / /p/%08x) are formulas: one shared instance per field
+static std::shared_ptr<const TermDict> synth_dict(uint32_t bit, uint64_t n) {
+    static std::mutex mu;
+    static std::map<uint32_t, std::shared_ptr<const TermDict>> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    auto& d = cache[bit];
+    if (!d) {
+        auto td = std::make_shared<TermDict>();
+        td->synth_bit = bit;
+        td->n = n;
+        td->seal();
+        d = td;
+    }
+    return d;
+}
 
 static uint32_t pad_docs(uint32_t n) { return (uint32_t)(((uint64_t)n + kBlockDocs - 1) / kBlockDocs * kBlockDocs); }
 
@@ -413,9 +457,20 @@ extern "C" int esgpu_segment_upload(esgpu_ctx* c, const esgpu_column_desc* cols,
                 }
                 if (d.type == ESGPU_COL_I64 || d.type == ESGPU_COL_F64) build_zone_map(c, *col, max_doc);
             }
-            if (d.type == ESGPU_COL_ORD_U32 && d.dict_bytes && d.dict_offsets) {
-                col->dict_offsets.assign(d.dict_offsets, d.dict_offsets + d.value_count + 1);
-                col->dict_bytes.assign(d.dict_bytes, d.dict_bytes + d.dict_offsets[d.value_count]);
+            if (d.type == ESGPU_COL_ORD_U32) {
+                auto td = std::make_shared<TermDict>();
+                td->n = d.value_count;
+                if (d.dict_bytes && d.dict_offsets) {
+                    require(d.dict_offsets[0] == 0, ESGPU_ERR_INVALID, "dictionary offsets must start at 0");
+                    for (uint64_t k = 0; k < d.value_count; ++k)
+                        require(d.dict_offsets[k] <= d.dict_offsets[k + 1], ESGPU_ERR_INVALID, "dictionary offsets must be non-decreasing");
+                    td->offsets.assign(d.dict_offsets, d.dict_offsets + d.value_count + 1);
+                    td->bytes.assign(d.dict_bytes, d.dict_bytes + d.dict_offsets[d.value_count]);
+                } else {
+                    td->numbered = true;
+                }
+                td->seal();
+                col->dict = std::move(td);
             }
             s->cols[d.name] = std::move(col);
         }
@@ -464,8 +519,8 @@ extern "C" int esgpu_segment_synthetic(esgpu_ctx* c, uint64_t seed, uint32_t sha
                                                 : bit == ESGPU_SYNTH_PRICE ? ESGPU_COL_F64 : ESGPU_COL_I64;
             col->values.alloc(c, (size_t)s->n_pad * (ord ? 4 : 8));
             if (ord) {
-                col->synth_bit = bit;
                 col->value_count = bit == ESGPU_SYNTH_HOST ? kHostTerms : kUrlTerms;
+                col->dict = synth_dict(bit, col->value_count);
             }
             switch (bit) {
                 case ESGPU_SYNTH_TIMESTAMP: p.ts = col->values.as<int64_t>(); break;
@@ -514,19 +569,10 @@ extern "C" int esgpu_segment_read_column(const esgpu_segment* s, const char* fie
 // reader, as Lucene does), then every segment's ordinal column is remapped on the GPU.
 // ------------------------------------------------------------------------------------------------------------
 struct esgpu_ordinal_map {
-    std::shared_ptr<const GlobalDict> dict;
+    std::shared_ptr<const TermDict> dict;
 };
 
-static std::string_view dict_view(const DevColumn* c, uint64_t o, std::string& scratch) {
-    if (c->synth_bit) {
-        char b[32];
-        esgpu_synthetic_term(c->synth_bit, o, b, sizeof b);
-        scratch = b;
-        return scratch;
-    }
-    return std::string_view((const char*)c->dict_bytes.data() + c->dict_offsets[o],
-                            (size_t)(c->dict_offsets[o + 1] - c->dict_offsets[o]));
-}
+static std::string_view dict_view(const DevColumn* c, uint64_t o, std::string& scratch) { return c->dict->view(o, scratch); }
 
 extern "C" int esgpu_ordinal_map_build(esgpu_ctx* ctx, esgpu_segment* const* segs, int32_t nsegs, const char* field,
                                        esgpu_ordinal_map** out) {
@@ -540,12 +586,11 @@ extern "C" int esgpu_ordinal_map_build(esgpu_ctx* ctx, esgpu_segment* const* seg
             if (it == segs[i]->cols.end()) { cols.push_back(nullptr); continue; }  // unmapped in this segment
             DevColumn* c = it->second.get();
             require(c->type == ESGPU_COL_ORD_U32, ESGPU_ERR_INVALID, "ordinal maps cover keyword columns");
-            require(c->synth_bit || c->dict_offsets.size() == c->value_count + 1, ESGPU_ERR_INVALID,
-                    std::string("no term dictionary for ") + field);
+            require(c->dict && !c->dict->numbered, ESGPU_ERR_INVALID, std::string("no term dictionary for ") + field);
             cols.push_back(c);
         }
         // k-way merge of the sorted segment dictionaries (unsigned byte order, BytesRef.compareTo)
-        auto g = std::make_shared<GlobalDict>();
+        auto g = std::make_shared<TermDict>();
         g->offsets.push_back(0);
         std::vector<std::vector<uint32_t>> maps(cols.size());
         std::vector<uint64_t> pos(cols.size(), 0);
@@ -568,6 +613,7 @@ extern "C" int esgpu_ordinal_map_build(esgpu_ctx* ctx, esgpu_segment* const* seg
                 have_last = true;
                 g->bytes.insert(g->bytes.end(), last.begin(), last.end());
                 g->offsets.push_back(g->bytes.size());
+                g->n++;
                 require(g->count() < 0xFFFFFFFFull, ESGPU_ERR_UNSUPPORTED, "more than 2^32-1 global ordinals");
             }
             const uint64_t o = pos[k]++;
@@ -578,6 +624,7 @@ extern "C" int esgpu_ordinal_map_build(esgpu_ctx* ctx, esgpu_segment* const* seg
                 heap.push({nx, k});
             }
         }
+        g->seal();
         // remap every segment's column on the GPU: gvalues[d] = map[values[d]] (missing stays missing)
         for (size_t k = 0; k < cols.size(); ++k) {
             DevColumn* c = cols[k];
@@ -610,7 +657,7 @@ extern "C" int esgpu_ordinal_map_value_count(const esgpu_ordinal_map* m, uint64_
 extern "C" int esgpu_ordinal_map_lookup(const esgpu_ordinal_map* m, const uint8_t* term, size_t len, int64_t* ord) {
     return guarded([&] {
         require(m && ord && (term || len == 0), ESGPU_ERR_INVALID, "null argument");
-        const GlobalDict& d = *m->dict;
+        const TermDict& d = *m->dict;
         const std::string_view key((const char*)term, len);
         uint64_t lo = 0, hi = d.count();
         while (lo < hi) {  // lower bound in unsigned byte order
@@ -811,6 +858,7 @@ struct Pipeline {
     uint32_t T = 1, H = 1;
     uint64_t value_count = 1;        // terms: the global ordinal count (T is max(value_count, 1))
     int64_t key0 = 0;
+    bool keyed = false;              // the key range has been taken from a segment's values (else H == 1, key0 == 0)
     int vcnt_mode = 0, ocnt_mode = OCNT_NONE;
     DevBuf g_cnt, g_ocnt, g_vcnt, g_sum, g_min, g_max, g_sq;
     // cardinality state
@@ -822,8 +870,10 @@ struct Pipeline {
     std::vector<uint32_t> h_lc;
     int hll_mode = 0;
     bool any_value = false;
-    // the segment the dictionary comes from (terms keys)
-    const DevColumn* ord_col = nullptr;
+    // the term dictionary the terms keys resolve through (the first collected segment's; every later segment must
+    // number its terms the same way) -- shared, so it outlives the segments
+    std::shared_ptr<const TermDict> tdict;
+    bool fresh = true;               // no segment collected since create / reset: the grid shape is (re)derived
     // timing of this pipeline's collect launch on the plan stream
     hipEvent_t e0 = nullptr, e1 = nullptr;
     bool timed = false;
@@ -876,7 +926,6 @@ struct esgpu_plan {
     double last_ms = 0;
     uint64_t last_bytes = 0;
     int32_t last_path = 0;
-    std::map<std::string, std::vector<std::string>> term_cache;  // terms reachable after the segment is destroyed
     // per-request scratch, reused across requests
     Scratch s_accept, s_tcnt, s_rows, s_dst[6];
     Scratch s_wgc, s_pbeg, s_pbuf, s_tiles, s_cand, s_keys, s_hist;  // partitioned counting + GPU top-k
@@ -1073,6 +1122,12 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
 static void alloc_grid(esgpu_plan* p, Pipeline& pl) {
     esgpu_ctx* c = p->ctx;
     const size_t cells = (size_t)pl.T * pl.H;
+    pl.g_ocnt.release();  // arrays the (new) shape does not use
+    pl.g_vcnt.release();
+    pl.g_sum.release();
+    pl.g_min.release();
+    pl.g_max.release();
+    pl.g_sq.release();
     pl.g_cnt.alloc(c, cells * 8);
     HIPX(hipMemsetAsync(pl.g_cnt.p, 0, cells * 8, p->stream));
     if (pl.ocnt_mode != OCNT_NONE) {
@@ -1116,6 +1171,7 @@ static void regrid(esgpu_plan* p, Pipeline& pl, uint32_t newH, int64_t shift) {
         old_cards[i].regs = std::move(pl.cards[i].regs);
         old_cards[i].sets = std::move(pl.cards[i].sets);
         old_cards[i].cnt = std::move(pl.cards[i].cnt);
+        old_cards[i].nonzero = std::move(pl.cards[i].nonzero);
     }
     struct { DevBuf g_cnt, g_ocnt, g_vcnt, g_sum, g_min, g_max, g_sq; } old;
     old.g_cnt = std::move(pl.g_cnt);
@@ -1145,6 +1201,7 @@ static void regrid(esgpu_plan* p, Pipeline& pl, uint32_t newH, int64_t shift) {
         cp(cs.regs, old_cards[i].regs, (size_t)pl.T * cs.m);
         cp(cs.sets, old_cards[i].sets, (size_t)pl.T * cs.cap * 4);
         cp(cs.cnt, old_cards[i].cnt, (size_t)pl.T * 4);
+        cp(cs.nonzero, old_cards[i].nonzero, (size_t)pl.T * 4);
     }
     HIPX(hipStreamSynchronize(p->stream));
 }
@@ -1468,6 +1525,13 @@ static bool collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment*
     // an unmapped metric field collects nothing (ValuesSource null => NO_OP collector); counts stay separate
     const int met_launch = mc ? pl.met : 0;
     // ---- shape the grid ----
+    if (pl.fresh) {  // first segment since create / reset: the grid shape and the dictionary are taken from it
+        pl.kt_lo = 0;
+        pl.kt_hi = -1;
+        pl.kt_start.clear();
+        pl.kt_key.clear();
+        pl.kt_slot.clear();
+    }
     int64_t kmin = 0, kmax = 0;
     bool has_keys = false;
     int64_t table_shift = 0;
@@ -1483,35 +1547,58 @@ static bool collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment*
         }
         has_keys = true;
     }
-    if (!pl.allocated) {
-        pl.T = ORD ? (uint32_t)std::max<uint64_t>(oc->ord_count(), 1) : 1;
-        pl.key0 = has_keys ? kmin : 0;
-        pl.H = HIST ? (uint32_t)(has_keys ? kmax - kmin + 1 : 1) : 1;
+    const bool sparse_metric = pl.met > 0 && (!mc || mc->present.p || mc->multi);
+    const bool terms_outer = pl.outer == pl.term_spec;
+    // ords may be missing; a doc may have several keys: then the outer counts cannot be summed from the cells
+    const bool inner_sparse = ORD && HIST && (terms_outer ? (hc->present.p != nullptr || hc->multi) : true);
+    if (!pl.allocated || pl.fresh) {
+        const uint32_t T = ORD ? (uint32_t)std::max<uint64_t>(oc->ord_count(), 1) : 1;
+        const int64_t key0 = has_keys ? kmin : 0;
         require(!HIST || !has_keys || kmax - kmin + 1 <= 64 * 1024 * 1024, ESGPU_ERR_UNSUPPORTED,
                 "histogram key range too large for a dense grid");
-        require((uint64_t)pl.T * pl.H <= (1ull << 31), ESGPU_ERR_UNSUPPORTED, "bucket grid too large");
-        pl.vcnt_mode = (pl.met > 0 && (!mc || mc->present.p || mc->multi)) ? 1 : 0;
+        const uint32_t H = HIST ? (uint32_t)(has_keys ? kmax - kmin + 1 : 1) : 1;
+        require((uint64_t)T * H <= (1ull << 31), ESGPU_ERR_UNSUPPORTED, "bucket grid too large");
+        const int vcnt = sparse_metric ? 1 : 0;
+        int ocnt = OCNT_NONE;
+        if (ORD && HIST) ocnt = inner_sparse ? (terms_outer ? OCNT_TERMS : OCNT_HIST) : OCNT_TERMS_DERIVED;
+        // a reset plan keeps its buffers (already zeroed) when the new request's first segment has the same shape
+        const bool same = pl.allocated && T == pl.T && H == pl.H && key0 == pl.key0 && vcnt == pl.vcnt_mode &&
+                          ocnt == pl.ocnt_mode;
+        pl.T = T;
+        pl.H = H;
+        pl.key0 = key0;
+        pl.vcnt_mode = vcnt;
+        pl.ocnt_mode = ocnt;
+        pl.keyed = has_keys;
         pl.value_count = ORD ? oc->ord_count() : 1;
-        if (ORD && HIST) {
-            const bool terms_outer = pl.outer == pl.term_spec;
-            // ords may be missing; a doc may have several keys: the outer counts cannot be summed from the cells
-            const bool inner_sparse = terms_outer ? (hc->present.p != nullptr || hc->multi) : true;
-            if (inner_sparse) pl.ocnt_mode = terms_outer ? OCNT_TERMS : OCNT_HIST;
-            else pl.ocnt_mode = OCNT_TERMS_DERIVED;
-        }
-        pl.ord_col = oc;
-        alloc_grid(p, pl);
+        pl.tdict = ORD ? oc->ord_dict() : nullptr;
+        if (!same) alloc_grid(p, pl);
+        pl.fresh = false;
     } else {
-        if (ORD) require(oc->ord_count() == pl.T || (oc->ord_count() == 0 && pl.T == 1), ESGPU_ERR_UNSUPPORTED,
-                         "segments with different global ordinal counts");
-        if (HIST && has_keys) {
+        if (ORD) require(same_dict(oc->ord_dict(), pl.tdict), ESGPU_ERR_INVALID,
+                         "segments number the terms of [" + pl.ord_field + "] differently: build an ordinal map "
+                         "(esgpu_ordinal_map_build) over the reader's segments first");
+        if (HIST && has_keys && !pl.keyed) {
+            // the earlier segments had no histogram values: their single placeholder row is empty
+            require(kmax - kmin + 1 <= 64 * 1024 * 1024, ESGPU_ERR_UNSUPPORTED, "histogram key range too large for a dense grid");
+            pl.key0 = kmin;
+            regrid(p, pl, (uint32_t)(kmax - kmin + 1), 0);
+            pl.keyed = true;
+        } else if (HIST && has_keys) {
             if (!pl.ktable) grow_keys(p, pl, kmin, kmax);
             else if ((uint32_t)pl.kt_key.size() != H_before || table_shift != 0) regrid(p, pl, (uint32_t)pl.kt_key.size(), table_shift);
         }
-        if (pl.met > 0 && (!mc || mc->present.p || mc->multi) && !pl.vcnt_mode)
-            throw EsError(ESGPU_ERR_UNSUPPORTED, "metric field sparsity changed across segments");
-        if (ORD && HIST && pl.outer == pl.term_spec && hc->multi && pl.ocnt_mode == OCNT_NONE)
-            throw EsError(ESGPU_ERR_UNSUPPORTED, "histogram field became multi-valued across segments");
+        if (sparse_metric && !pl.vcnt_mode) {
+            // the metric field turns sparse in this segment: value counts split from doc counts, which they equalled
+            // so far (every earlier doc had exactly one value)
+            const size_t cells = (size_t)pl.T * pl.H;
+            pl.g_vcnt.alloc(p->ctx, cells * 8);
+            HIPX(hipMemcpyAsync(pl.g_vcnt.p, pl.g_cnt.p, cells * 8, hipMemcpyDeviceToDevice, p->stream));
+            pl.vcnt_mode = 1;
+        }
+        // the histogram field turns sparse / multi-valued: outer counts are counted per doc from here on (the derived
+        // counts of the earlier segments are already in g_ocnt)
+        if (inner_sparse && pl.ocnt_mode == OCNT_TERMS_DERIVED) pl.ocnt_mode = OCNT_TERMS;
     }
     // ---- launch configuration ----
     CollectParams P{};
@@ -1738,18 +1825,6 @@ extern "C" int esgpu_plan_collect_segment(esgpu_plan* p, const esgpu_segment* s,
         for (Pipeline& pl : p->pipes) {
             pl.timed = pl.kind == 1 ? collect_hll(p, pl, s, d_accept) : collect_grid(p, pl, s, d_accept);
         }
-        // keep dictionary terms reachable at build time even if the segment is destroyed first
-        for (Pipeline& pl : p->pipes) {
-            if (pl.term_spec < 0) continue;
-            const DevColumn* oc = s->col(pl.ord_field.c_str());
-            const bool synth = oc && oc->synth_bit && !oc->gdict;
-            if (oc && p->term_cache.find(pl.ord_field) == p->term_cache.end() && !synth) {
-                auto& v = p->term_cache[pl.ord_field];
-                v.reserve(oc->ord_count());
-                for (uint64_t o = 0; o < oc->ord_count(); ++o) v.push_back(oc->ord_term(o));
-            }
-            if (synth) p->term_cache[pl.ord_field + "#synth"] = {std::to_string(oc->synth_bit)};
-        }
         p->collected = true;
     });
 }
@@ -1813,16 +1888,8 @@ extern "C" int esgpu_plan_post_collection(esgpu_plan* p) {
 }
 
 // ---- build ----------------------------------------------------------------------------------------------------
-static std::string plan_term(const esgpu_plan* p, const Pipeline& pl, uint64_t ord) {
-    auto syn = p->term_cache.find(pl.ord_field + "#synth");
-    if (syn != p->term_cache.end()) {
-        char b[32];
-        esgpu_synthetic_term((uint32_t)std::stoul(syn->second[0]), ord, b, sizeof b);
-        return b;
-    }
-    auto it = p->term_cache.find(pl.ord_field);
-    if (it != p->term_cache.end() && ord < it->second.size()) return it->second[ord];
-    return std::to_string(ord);
+static std::string plan_term(const esgpu_plan*, const Pipeline& pl, uint64_t ord) {
+    return pl.tdict ? pl.tdict->term(ord) : std::to_string(ord);
 }
 
 // ---- result blocks (columnar InternalAggregations, see esgpu_results.hpp) ----
@@ -2297,6 +2364,9 @@ extern "C" int esgpu_plan_reset(esgpu_plan* p) {
         require(p != nullptr, ESGPU_ERR_INVALID, "null plan");
         HIPX(hipSetDevice(p->ctx->device));
         for (Pipeline& pl : p->pipes) {
+            // the next request takes its grid shape and term dictionary from its own first segment
+            pl.fresh = true;
+            pl.tdict.reset();
             if (!pl.allocated) continue;
             if (pl.kind == 1) {
                 HIPX(hipMemsetAsync(pl.regs.p, 0, pl.regs.bytes, p->stream));
