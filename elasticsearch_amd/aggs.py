@@ -28,11 +28,29 @@ _TIME_UNITS_MS = {"ms": 1, "s": 1000, "m": 60000, "h": 3600000, "d": 86400000, "
 
 
 def parse_time_value(text):
-    """TimeValue.parseTimeValue subset: "<number><unit>" with unit in ms/s/m/h/d/w (plain numbers are millis)."""
-    m = re.fullmatch(r"\s*(-?\d+(?:\.\d+)?)\s*(ms|s|m|h|d|w)?\s*", str(text))
+    """TimeValue.parseTimeValue (common/unit/TimeValue.java:232-272): the lower-cased text's suffix picks the unit
+    (ms, s, m, h, d, w in that order of tests), a bare number is milliseconds.  As in Java, seconds truncate the
+    number before scaling ((long) 1.5 * 1000 = 1000); the other units scale, then truncate."""
+    t = str(text).lower().strip()
+    m = re.fullmatch(r"(-?\d+(?:\.\d*)?|-?\.\d+)(ms|s|m|h|d|w)?", t)
     if not m:
-        raise ValueError(f"failed to parse time value [{text}]")
-    return int(float(m.group(1)) * _TIME_UNITS_MS[m.group(2) or "ms"])
+        raise ValueError(f"Failed to parse [{text}]")
+    num, unit = m.group(1), m.group(2)
+    if unit is None:
+        if "." in num:
+            raise ValueError(f"Failed to parse [{text}]")
+        return int(num)
+    if unit == "s":
+        return int(float(num)) * 1000
+    return int(float(num) * _TIME_UNITS_MS[unit])
+
+
+def parse_offset(text):
+    """DateHistogramParser.parseOffset: "-" negates, "+" is dropped, the rest is a TimeValue."""
+    t = str(text)
+    if t.startswith("-"):
+        return -parse_time_value(t[1:])
+    return parse_time_value(t[1:] if t.startswith("+") else t)
 
 
 def parse_time_zone(tz):
@@ -351,7 +369,7 @@ def _rounding_params(b):
         return N.UNIT_NONE, int(b._interval), int(b._offset), None
     if b._interval is None:
         raise ValueError("Missing required field [interval] for histogram aggregation [%s]" % b.name)
-    off = b._offset if isinstance(b._offset, int) else parse_time_value(b._offset)
+    off = b._offset if isinstance(b._offset, int) else parse_offset(b._offset)
     tz = parse_time_zone(b._tz)
     zone = None
     if isinstance(tz, tuple):

@@ -13,9 +13,11 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(_HERE))
+sys.path.insert(0, _HERE)
 
 from elasticsearch_amd import _native as N  # noqa: E402  (struct layouts of include/esgpu.h)
-from elasticsearch_amd.aggs import flatten, flatten_filters  # noqa: E402
+
+import oracle_request  # noqa: E402  (the oracle's own request lowering: no product code)
 
 LIB_PATH = os.path.join(_HERE, "libesoracle.so")
 
@@ -63,6 +65,10 @@ def lib():
         L.oracle_rounding.restype = ctypes.c_int64
         L.oracle_rounding.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
                                       ctypes.c_int64]
+        L.oracle_rounding_tz.restype = ctypes.c_int64
+        L.oracle_rounding_tz.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64,
+                                         ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), ctypes.c_int32,
+                                         ctypes.c_int32, ctypes.c_int64]
         L.oracle_hll_collect.restype = ctypes.c_int64
         L.oracle_hll_collect.argtypes = [ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int64,
                                          ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_uint64)]
@@ -121,8 +127,8 @@ def run(shards, aggs, filters=None, number_of_shards=None, accept=None, ord_look
     """shards: list of (columns_dict, max_doc).  Returns {"shards": [...], "reduced": {...}} (parsed JSON)."""
     L = lib()
     number_of_shards = number_of_shards or len(shards)
-    specs, nspecs, k1 = flatten(aggs, number_of_shards)
-    flt, nf, k2 = flatten_filters(filters, ord_lookup, aggs)
+    specs, nspecs, k1 = oracle_request.lower(L, aggs, number_of_shards)
+    flt, nf, k2 = oracle_request.lower_filters(filters, ord_lookup, aggs)
     oshards, keep = [], [k1, k2]
     for i, (cols, max_doc) in enumerate(shards):
         arr, n, k = _columns(cols)

@@ -84,16 +84,12 @@ TZ_UNITS = {"hour": N.UNIT_HOUR, "day": N.UNIT_DAY, "month": N.UNIT_MONTH, "year
 
 
 def oracle_round_tz(kind, unit, interval, offset, zone, op, v):
-    from elasticsearch_amd.aggs import tz_history
-    starts, offs = tz_history(zone) if zone != "UTC" else ((-(1 << 63),), (0,))
+    """The oracle's Rounding with the oracle's own zone table (TZif transitions + POSIX footer, oracle_request.py)."""
+    import oracle_request
+    starts, offs = oracle_request.zone_table(zone) or ((-(1 << 63),), (0,))
     st = (ctypes.c_int64 * len(starts))(*starts)
     of = (ctypes.c_int64 * len(offs))(*offs)
-    L = O.lib()
-    L.oracle_rounding_tz.restype = ctypes.c_int64
-    L.oracle_rounding_tz.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64,
-                                     ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), ctypes.c_int32,
-                                     ctypes.c_int32, ctypes.c_int64]
-    return L.oracle_rounding_tz(kind, unit, interval, offset, st, of, len(starts), op, v)
+    return O.lib().oracle_rounding_tz(kind, unit, interval, offset, st, of, len(starts), op, v)
 
 
 def test_rounding_dst_known_values(kat):  # TimeZoneRoundingTests.testTimeUnitRoundingDST / testAmbiguousHoursAfterDSTSwitch
