@@ -58,11 +58,27 @@ def build_request(workload, world):
     raise SystemExit(f"unknown workload {workload}")
 
 
-def cpu_baseline(workload, world, sample_docs, threads):
+def host_cpu():
+    """(model name, logical CPUs visible to this process) -- what `lscpu` reports for the box."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return model, n
+
+
+def cpu_baseline(workload, world, sample_docs, threads, single_docs):
     """The oracle (cpu_ref: the reference's Java collect/build loops restated in C++) on the host cores, one shard per
     thread as Elasticsearch runs one SEARCH thread per shard.  `threads` shards of
     sample_docs / threads docs each, generated and collected concurrently; the wall time of the collect+build
-    phase over all of them gives the node-level CPU rate."""
+    phase over all of them gives the node-level CPU rate.  A separate single-thread run over one shard of
+    `single_docs` docs gives the one-core rate (the reference's per-shard latency path)."""
     import threading
     sys.path.insert(0, os.path.join(HERE, "oracle"))
     sys.path.insert(0, os.path.join(HERE, "tests"))
@@ -75,7 +91,7 @@ def cpu_baseline(workload, world, sample_docs, threads):
     secs = [0.0] * threads
 
     def gen(i):
-        cols[i] = synthetic_columns(fields, per, shard=i)
+        cols[i] = synthetic_columns(fields, per, shard=i, threads=1)
 
     def work(i):
         _, secs[i] = O.run([(cols[i], per)], aggs, filters=filters, number_of_shards=world, return_seconds=True)
@@ -88,12 +104,57 @@ def cpu_baseline(workload, world, sample_docs, threads):
         for t in ts:
             t.join()
         wall = time.perf_counter() - t0
-    core_rate = per / (sum(secs) / threads)
-    return {"value": per * threads / wall, "unit": "docs/s", "cores": threads, "kind": "port",
-            "single_core_value": core_rate,
+    cols = None
+    one = synthetic_columns(fields, single_docs, shard=0)
+    _, one_secs = O.run([(one, single_docs)], aggs, filters=filters, number_of_shards=world, return_seconds=True)
+    one = None
+    model, visible = host_cpu()
+    value = per * threads / wall
+    return {"value": value, "unit": "docs/s", "cores": threads, "kind": "port",
+            "single_core_value": single_docs / one_secs,
+            "cpu_model": model, "host_cpus_visible": visible,
             "sample": f"oracle/cpu_ref.cpp (the reference's Java collect+build loops restated), {threads} synthetic "
-                      f"shards x {per:,} docs of the same request, one host thread per shard, run concurrently "
-                      f"({wall:.2f} s wall; {core_rate / 1e6:.1f}M docs/s per core)"}
+                      f"shards x {per:,} docs of the same request, one host thread per shard, run concurrently on the "
+                      f"{threads} cores this job is allotted ({wall:.2f} s wall), plus one shard of {single_docs:,} docs "
+                      f"on one thread ({single_docs / one_secs / 1e6:.1f}M docs/s); {model}, {visible} logical CPUs "
+                      f"visible"}
+
+
+def self_check(workload, res, docs_total, matching=None):
+    """Size-independent properties of the timed request's final result (outside the timed region): every counted doc
+    is in a bucket or in sum_other_doc_count, a term's hour buckets add up to its doc count, each bucket's metric count
+    equals its doc count (dense metric column), and the cardinality estimate is within 5 % of the distinct values the
+    generator can produce.  Returns (ok, details)."""
+    errs = []
+    expect = docs_total if matching is None else matching
+    if workload in ("north_star", "config5", "config3"):
+        t = res["hosts"] if workload != "config3" else res["urls"]
+        total = sum(b["doc_count"] for b in t["buckets"]) + t["sum_other_doc_count"]
+        if total != expect:
+            errs.append(f"sum(doc_count) + sum_other_doc_count = {total} != {expect}")
+        for b in t["buckets"] if workload != "config3" else []:
+            hours = b["per_hour"]["buckets"]
+            if sum(h["doc_count"] for h in hours) != b["doc_count"]:
+                errs.append(f"term {b['key']}: hour buckets do not add up")
+            for h in hours:
+                cnt = h["rt"]["count"] if workload == "north_star" else h["rt"]["_internal"]["count"]
+                if cnt != h["doc_count"]:
+                    errs.append(f"term {b['key']} hour {h['key']}: metric count {cnt} != doc_count {h['doc_count']}")
+                    break
+    elif workload == "config2":
+        hours = res["per_hour"]["buckets"]
+        if sum(h["doc_count"] for h in hours) != expect:
+            errs.append("hour buckets do not add up to the docs")
+        if any(h["rt"]["count"] != h["doc_count"] for h in hours):
+            errs.append("metric count != doc_count")
+    elif workload == "config4":
+        import math
+        pool = 1 << 27  # client_ip.hash draws from 2^27 distinct IPs
+        distinct = pool * (1.0 - math.exp(-docs_total / pool))
+        v = res["ips"]["value"]
+        if abs(v - distinct) > 0.05 * distinct or res["ips"]["_internal"]["mode"] != "hll":
+            errs.append(f"cardinality {v} vs ~{distinct:.0f} expected distinct")
+    return not errs, errs
 
 
 def main():
@@ -104,9 +165,10 @@ def main():
     ap.add_argument("--docs", type=int, default=1_000_000_000, help="docs per shard (one shard per GPU)")
     ap.add_argument("--workload", default="north_star", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-docs", type=int, default=640_000_000, help="CPU baseline sample size (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=min(16, int(os.environ.get("OMP_NUM_THREADS", "0")) or
-                                                              os.cpu_count() or 1),
-                    help="host threads of the CPU baseline (one shard each)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="host threads of the CPU baseline, one shard each (0 = every CPU this job is allotted: its "
+                         "affinity, capped by OMP_NUM_THREADS)")
+    ap.add_argument("--cpu-single-docs", type=int, default=20_000_000, help="docs of the single-thread CPU shard")
     ap.add_argument("--inflight", type=int, default=2, choices=(1, 2),
                     help="requests in flight (2: build/reduce of one request overlaps the next collect)")
     ap.add_argument("--traffic", default=os.path.join(HERE, "profiles", "hbm_traffic.json"),
@@ -192,6 +254,19 @@ def main():
     # (measured here, where no two requests' kernels overlap on the GPU)
     elapsed_seq = timed(1, True) if len(plans) > 1 else elapsed
 
+    # self-check of the last timed request's final result (outside the timed region)
+    matching = None
+    if args.workload == "config5":  # docs the query matches: a filter aggregation over the same clauses, per shard
+        fp = engine.plan([ea.AggregationBuilders.filter("m", filters)], number_of_shards=world)
+        fp.collect(seg)
+        matching = fp.build().to_dict()["m"]["doc_count"]
+        fp.close()
+        if dist:
+            t = torch.tensor([matching], dtype=torch.int64, device=f"cuda:{local_rank}")
+            dist.all_reduce(t)
+            matching = int(t.item())
+    checked, check_errors = self_check(args.workload, final.to_dict(), args.docs * world, matching)
+
     ms_per_step = elapsed * 1000.0 / args.steps
     value = args.docs * world / (elapsed / args.steps)
     avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
@@ -209,7 +284,10 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and args.cpu_docs > 0:
-            cpu = cpu_baseline(args.workload, world, args.cpu_docs, max(1, args.cpu_threads))
+            sys.path.insert(0, os.path.join(HERE, "tests"))
+            from helpers import host_threads
+            threads = args.cpu_threads if args.cpu_threads > 0 else host_threads()
+            cpu = cpu_baseline(args.workload, world, args.cpu_docs, threads, args.cpu_single_docs)
         out = {
             "metric": "docs aggregated/sec (node) + achieved HBM GB/s, terms+date_histogram, 1B docs",
             "value": value,
@@ -232,6 +310,8 @@ def main():
                          "kernel": "collect_kernel", "kernel_ms": avg_kernel_ms,
                          "algorithmic_bytes_per_launch": kernel_bytes},
             "cpu_baseline": cpu,
+            "checked": checked,
+            "check_errors": check_errors[:5],
         }
         print(json.dumps(out), flush=True)
     for p in plans:

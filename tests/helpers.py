@@ -40,11 +40,32 @@ def synthetic_dict(field):
     raise KeyError(field)
 
 
-def synthetic_columns(fields, num_docs, shard=0, seed=0x5EEDE1A5):
+def _host_column(field, num_docs, shard, seed, threads):
+    """synthetic_host_column in `threads` concurrent chunks (the C generator releases the GIL)."""
+    if threads <= 1 or num_docs < (1 << 22):
+        return synthetic_host_column(field, num_docs, shard=shard, seed=seed)
+    from concurrent.futures import ThreadPoolExecutor
+    bounds = [num_docs * i // threads for i in range(threads + 1)]
+    with ThreadPoolExecutor(threads) as ex:
+        parts = list(ex.map(lambda i: synthetic_host_column(field, num_docs, start=bounds[i], count=bounds[i + 1] - bounds[i],
+                                                            shard=shard, seed=seed), range(threads)))
+    return np.concatenate(parts)
+
+
+def host_threads():
+    """Host threads this job may use: its CPU affinity, capped by OMP_NUM_THREADS (the GPU box allots 16)."""
+    import os
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n, omp) if omp > 0 else n)
+
+
+def synthetic_columns(fields, num_docs, shard=0, seed=0x5EEDE1A5, threads=None):
     """Host copies of a synthetic shard, in the column-dict format of Engine.upload_segment / oracle.run."""
+    threads = host_threads() if threads is None else threads
     cols = {}
     for f in fields:
-        c = {"type": N.SYNTH_TYPES[f], "values": synthetic_host_column(f, num_docs, shard=shard, seed=seed)}
+        c = {"type": N.SYNTH_TYPES[f], "values": _host_column(f, num_docs, shard, seed, threads)}
         if f in ("host", "url"):
             c["terms_blob"] = synthetic_dict(f)
         cols[f] = c

@@ -23,7 +23,7 @@ run() {  # name seconds cmd...
 }
 for s in $STEPS; do
     case $s in
-        tests) run pytest_gpu 900 python3 -m pytest "$R/tests" -m gpu -x -q -p no:cacheprovider ;;
+        tests) run pytest_gpu 1100 python3 -u -m pytest "$R/tests" -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         kbench) run kbench 600 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 ${KBENCH_ONLY:+--only $KBENCH_ONLY} ;;
         bench) run bench 600 python3 "$R/bench.py" ;;
         prof) cd /tmp && run rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
