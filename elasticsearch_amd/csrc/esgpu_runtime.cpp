@@ -32,47 +32,9 @@
 #include "es_rounding.hpp"
 #include "esgpu_kernels.hpp"
 #include "esgpu_results.hpp"
+#include "esgpu_internal.hpp"
 
 using namespace esgpu;
-
-// ------------------------------------------------------------------------------------------------------------
-// errors
-// ------------------------------------------------------------------------------------------------------------
-static thread_local std::string g_err;
-
-struct EsError : std::runtime_error {
-    int code;
-    EsError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
-};
-
-#define HIPX(expr)                                                                                            \
-    do {                                                                                                      \
-        hipError_t e_ = (expr);                                                                               \
-        if (e_ != hipSuccess)                                                                                 \
-            throw EsError(e_ == hipErrorOutOfMemory ? ESGPU_ERR_OOM : ESGPU_ERR_DEVICE,                       \
-                          std::string(#expr) + ": " + hipGetErrorString(e_));                                \
-    } while (0)
-
-template <class F>
-static int guarded(F&& f) {
-    try {
-        f();
-        return ESGPU_OK;
-    } catch (const EsError& e) {
-        g_err = e.what();
-        return e.code;
-    } catch (const std::bad_alloc&) {
-        g_err = "host out of memory";
-        return ESGPU_ERR_OOM;
-    } catch (const std::exception& e) {
-        g_err = e.what();
-        return ESGPU_ERR_INVALID;
-    }
-}
-
-static void require(bool c, int code, const std::string& msg) {
-    if (!c) throw EsError(code, msg);
-}
 
 extern "C" int esgpu_last_error(char* buf, size_t cap) {
     if (buf && cap) {
@@ -83,63 +45,6 @@ extern "C" int esgpu_last_error(char* buf, size_t cap) {
     return (int)g_err.size();
 }
 extern "C" int esgpu_abi_version(void) { return ESGPU_ABI_VERSION; }
-
-// ------------------------------------------------------------------------------------------------------------
-// context + HBM accounting (the REQUEST/FIELDDATA circuit breakers' analogue, BigArrays.java:393-395)
-// ------------------------------------------------------------------------------------------------------------
-struct esgpu_ctx {
-    int device = 0;
-    int cus = 256;
-    uint64_t budget = 0;
-    std::atomic<uint64_t> used{0};
-    hipStream_t stream = nullptr;  // upload / generation stream
-    std::mutex mu;
-    // synthetic tables (device copies)
-    double* d_host_cdf = nullptr;
-    double* d_rt_cdf = nullptr;
-    double* d_url_cdf = nullptr;
-};
-
-struct DevBuf {
-    esgpu_ctx* ctx = nullptr;
-    void* p = nullptr;
-    size_t bytes = 0;
-    DevBuf() = default;
-    DevBuf(const DevBuf&) = delete;
-    DevBuf& operator=(const DevBuf&) = delete;
-    DevBuf(DevBuf&& o) noexcept : ctx(o.ctx), p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
-    DevBuf& operator=(DevBuf&& o) noexcept {
-        if (this != &o) {
-            release();
-            ctx = o.ctx; p = o.p; bytes = o.bytes;
-            o.p = nullptr; o.bytes = 0;
-        }
-        return *this;
-    }
-    ~DevBuf() { release(); }
-    void release() {
-        if (p) {
-            (void)hipSetDevice(ctx->device);
-            (void)hipFree(p);
-            ctx->used -= bytes;
-            p = nullptr;
-            bytes = 0;
-        }
-    }
-    void alloc(esgpu_ctx* c, size_t n) {
-        release();
-        ctx = c;
-        if (n == 0) return;
-        if (c->used + n > c->budget)
-            throw EsError(ESGPU_ERR_OOM, "[request] Data too large: HBM budget of " + std::to_string(c->budget) +
-                                             " bytes would be exceeded by " + std::to_string(n) + " bytes");
-        HIPX(hipSetDevice(c->device));
-        HIPX(hipMalloc(&p, n));
-        bytes = n;
-        c->used += n;
-    }
-    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
-};
 
 extern "C" int esgpu_device_count(int* count) {
     return guarded([&] {
@@ -879,36 +784,6 @@ struct Pipeline {
     bool timed = false;
     uint64_t occ_key = ~0ull;   // cached occupancy of the last launch configuration
     int occ = 1;
-};
-
-// pinned host staging buffer (D2H of build results without a pageable bounce)
-struct PinnedBuf {
-    void* p = nullptr;
-    size_t bytes = 0;
-    PinnedBuf() = default;
-    PinnedBuf(const PinnedBuf&) = delete;
-    PinnedBuf& operator=(const PinnedBuf&) = delete;
-    ~PinnedBuf() { if (p) (void)hipHostFree(p); }
-    void* ensure(size_t n) {
-        if (n <= bytes) return p;
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        bytes = 0;
-        HIPX(hipHostMalloc(&p, n, hipHostMallocDefault));
-        bytes = n;
-        return p;
-    }
-    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
-};
-
-// device scratch that only grows: no hipMalloc/hipFree (and their implicit syncs) on the per-request path
-struct Scratch {
-    DevBuf buf;
-    void* ensure(esgpu_ctx* c, size_t n) {
-        if (n > buf.bytes) buf.alloc(c, n + n / 4);
-        return buf.p;
-    }
-    template <class T> T* as() const { return buf.as<T>(); }
 };
 
 struct esgpu_plan {
