@@ -162,7 +162,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--docs", type=int, default=1_000_000_000, help="docs per shard (one shard per GPU)")
+    ap.add_argument("--docs", type=int, default=1_000_000_000, help="docs per shard")
+    ap.add_argument("--shards", type=int, default=0,
+                    help="shards of the job, shards / GPUs per GPU, collected in turn (0 = one shard per GPU: weak "
+                         "scaling; S > 0 fixes the job's size: strong scaling, e.g. --shards 8 --docs 125000000 is "
+                         "BASELINE configs 3-5's 1B docs in 8 shards)")
     ap.add_argument("--workload", default="north_star", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-docs", type=int, default=640_000_000, help="CPU baseline sample size (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -170,7 +174,7 @@ def main():
                          "affinity, capped by OMP_NUM_THREADS)")
     ap.add_argument("--cpu-single-docs", type=int, default=20_000_000, help="docs of the single-thread CPU shard")
     ap.add_argument("--inflight", type=int, default=2, choices=(1, 2),
-                    help="requests in flight (2: build/reduce of one request overlaps the next collect)")
+                    help="plans in flight (2: the host build of one shard result overlaps the next collect)")
     ap.add_argument("--traffic", default=os.path.join(HERE, "profiles", "hbm_traffic.json"),
                     help="PMC-derived HBM bytes per collect launch (profiles/), if measured for this workload")
     args = ap.parse_args()
@@ -178,8 +182,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        world = max(world, 1)
+    world = max(world, 1)
+    shards = args.shards if args.shards > 0 else world
+    if shards % world:
+        raise SystemExit(f"--shards {shards} must be a multiple of the {world} GPUs")
+    per_gpu = shards // world
 
     import torch
     dist = None
@@ -192,45 +199,56 @@ def main():
     import elasticsearch_amd as ea
     engine = ea.Engine(local_rank if world > 1 else 0)
     fields, desc = WORKLOADS[args.workload]
-    aggs, filters = build_request(args.workload, world)
-    seg = engine.synthetic_segment(args.docs, fields=fields, shard=rank)
-    plan = engine.plan(aggs, filters=filters, number_of_shards=world)
+    aggs, filters = build_request(args.workload, shards)
+    # this rank's shards: global shards rank * per_gpu ... (rank-major = the reduce's shard order)
+    segs = [engine.synthetic_segment(args.docs, fields=fields, shard=rank * per_gpu + i) for i in range(per_gpu)]
+    plans = [engine.plan(aggs, filters=filters, number_of_shards=shards) for _ in range(args.inflight)]
+    # fixed-shape requests (no terms): this GPU's shards are collected into one plan, one build per request; terms
+    # requests build one shard result per shard (per-shard top-k) and reduce them with the other ranks'
+    merged = plans[0].shard_mergeable() and per_gpu > 1
+    units_per_request = 1 if merged or per_gpu == 1 else per_gpu
     comm = None
     if world > 1:
         uid = [ea.Communicator.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         comm = ea.Communicator(engine, world, rank, uid[0])
 
-    kernel_ms, kernel_bytes = [], 0
+    kernel_ms, kernel_bytes = [0.0], [0]
     final = None
-    # --inflight 2: two plans (two request contexts, each with its own HIP stream) alternate, so the host-side
-    # buildAggregation + reduce of request i overlaps the collect kernel of request i + 1 -- how a node serves a
-    # stream of search requests.  Every request still runs reset -> collect -> build -> reduce in full.
-    plans = [plan] + [engine.plan(aggs, filters=filters, number_of_shards=world) for _ in range(args.inflight - 1)]
+    partial = []
 
-    def launch(p):
+    def launch(p, unit, record):
         p.reset()
-        p.collect(seg)
+        for seg in (segs if merged or per_gpu == 1 else [segs[unit]]):
+            p.collect(seg)
+            if record:  # HIP-event time of this collect (synchronises: sequential phase only)
+                ms, nbytes, _ = p.last_collect_stats()
+                kernel_ms[0] += ms
+                kernel_bytes[0] += nbytes
 
-    def finish(p, record):
-        nonlocal final, kernel_bytes
-        ms, nbytes, _ = p.last_collect_stats()
-        if record:
-            kernel_ms.append(ms)
-            kernel_bytes = nbytes
-        res = p.build()
-        final = comm.gather_reduce(res) if comm else ea.reduce([res])
+    def finish(p, unit):
+        nonlocal final, partial
+        partial.append(p.build())
+        if unit == units_per_request - 1:
+            final = comm.reduce(partial) if comm else ea.reduce(partial)
+            partial = []
 
-    def run(n, record, depth):
+    # one unit = one collect (+ build) of a shard, or of all this GPU's shards of a fixed-shape request; with two plans
+    # the host build + reduce of one unit overlaps the collect kernel of the next -- how a node serves a stream of
+    # search requests.  Every request still runs reset -> collect -> build -> reduce in full.
+    def run(n_requests, record, depth):
         pend = []
-        for i in range(n):
-            p = plans[i % depth]
-            launch(p)
-            pend.append(p)
-            if len(pend) == depth:
-                finish(pend.pop(0), record)
+        k = 0
+        for _ in range(n_requests):
+            for unit in range(units_per_request):
+                p = plans[k % depth]
+                k += 1
+                launch(p, unit, record)
+                pend.append((p, unit))
+                if len(pend) == depth:
+                    finish(*pend.pop(0))
         while pend:
-            finish(pend.pop(0), record)
+            finish(*pend.pop(0))
 
     def timed(depth, record):
         if dist:
@@ -250,27 +268,37 @@ def main():
 
     run(args.warmup, False, len(plans))
     elapsed = timed(len(plans), len(plans) == 1)
-    # one request at a time: the sequential rate, reported alongside, and the collect kernel's HIP-event time
-    # (measured here, where no two requests' kernels overlap on the GPU)
+    # one unit at a time: the sequential rate, reported alongside, and the collect kernels' HIP-event time (measured
+    # here, where no two collects overlap on the GPU)
     elapsed_seq = timed(1, True) if len(plans) > 1 else elapsed
+    exchange = None
+    if comm:
+        ar, ag, ncoll = comm.last_exchange()
+        exchange = {"allreduce_bytes": ar, "allgather_bytes": ag, "collectives": ncoll}
 
     # self-check of the last timed request's final result (outside the timed region)
     matching = None
     if args.workload == "config5":  # docs the query matches: a filter aggregation over the same clauses, per shard
-        fp = engine.plan([ea.AggregationBuilders.filter("m", filters)], number_of_shards=world)
-        fp.collect(seg)
-        matching = fp.build().to_dict()["m"]["doc_count"]
+        fp = engine.plan([ea.AggregationBuilders.filter("m", filters)], number_of_shards=shards)
+        matching = 0
+        for seg in segs:
+            fp.reset()
+            fp.collect(seg)
+            matching += fp.build().to_dict()["m"]["doc_count"]
         fp.close()
         if dist:
             t = torch.tensor([matching], dtype=torch.int64, device=f"cuda:{local_rank}")
             dist.all_reduce(t)
             matching = int(t.item())
-    checked, check_errors = self_check(args.workload, final.to_dict(), args.docs * world, matching)
+    docs_total = args.docs * shards
+    checked, check_errors = self_check(args.workload, final.to_dict(), docs_total, matching)
 
     ms_per_step = elapsed * 1000.0 / args.steps
-    value = args.docs * world / (elapsed / args.steps)
-    avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
-    achieved = kernel_bytes / (avg_kernel_ms / 1000.0) / 1e9
+    value = docs_total / (elapsed / args.steps)
+    avg_kernel_ms = kernel_ms[0] / args.steps
+    bytes_per_step = kernel_bytes[0] // args.steps
+    achieved = bytes_per_step / (avg_kernel_ms / 1000.0) / 1e9
+    launches = args.steps * (per_gpu if per_gpu > 1 else 1)
     traffic = None
     if os.path.exists(args.traffic):
         try:
@@ -287,7 +315,7 @@ def main():
             sys.path.insert(0, os.path.join(HERE, "tests"))
             from helpers import host_threads
             threads = args.cpu_threads if args.cpu_threads > 0 else host_threads()
-            cpu = cpu_baseline(args.workload, world, args.cpu_docs, threads, args.cpu_single_docs)
+            cpu = cpu_baseline(args.workload, shards, args.cpu_docs, threads, args.cpu_single_docs)
         out = {
             "metric": "docs aggregated/sec (node) + achieved HBM GB/s, terms+date_histogram, 1B docs",
             "value": value,
@@ -299,16 +327,19 @@ def main():
             "inflight_requests": len(plans),
             "ms_per_step_sequential": elapsed_seq * 1000.0 / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.shards > 0 else "weak",
             "vs_baseline": None,
             "dtype": "int64/f64",
-            "data": "synthetic (deterministic splitmix64 log docs generated in HBM, seed 0x5EEDE1A5, shard = rank)",
-            "config": {"workload": args.workload, "request": desc, "docs_per_shard": args.docs, "shards": world,
-                       "parallelism": f"one shard per GPU x{world}"},
+            "data": "synthetic (deterministic splitmix64 log docs generated in HBM, seed 0x5EEDE1A5, shard = global shard id)",
+            "config": {"workload": args.workload, "request": desc, "docs_per_shard": args.docs, "shards": shards,
+                       "shards_per_gpu": per_gpu, "docs_total": docs_total,
+                       "collect": "merged (one plan per GPU)" if merged else "per shard",
+                       "parallelism": f"{per_gpu} shard(s) per GPU x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
-                         "kernel": "collect_kernel", "kernel_ms": avg_kernel_ms,
-                         "algorithmic_bytes_per_launch": kernel_bytes},
+                         "kernel": "collect_kernel", "kernel_ms": avg_kernel_ms * args.steps / launches,
+                         "algorithmic_bytes_per_launch": kernel_bytes[0] // launches},
+            "exchange": exchange,
             "cpu_baseline": cpu,
             "checked": checked,
             "check_errors": check_errors[:5],
@@ -316,7 +347,8 @@ def main():
         print(json.dumps(out), flush=True)
     for p in plans:
         p.close()
-    seg.close()
+    for seg in segs:
+        seg.close()
     if comm:
         comm.close()
     engine.close()

@@ -31,6 +31,8 @@ ORDER_KEY_ASC, ORDER_KEY_DESC, ORDER_HCOUNT_ASC, ORDER_HCOUNT_DESC = 4, 5, 6, 7
 UNIT_NONE, UNIT_WEEK, UNIT_YEAR, UNIT_QUARTER, UNIT_MONTH, UNIT_DAY, UNIT_HOUR, UNIT_MINUTE, UNIT_SECOND = range(9)
 FILTER_TERM, FILTER_RANGE = 1, 2
 COMM_ID_BYTES = 128
+DT_U8, DT_I64, DT_U64, DT_F64 = 0, 1, 2, 3
+RED_SUM, RED_MIN, RED_MAX = 0, 1, 2
 
 
 class ColumnDesc(ctypes.Structure):
@@ -96,6 +98,16 @@ class Result(ctypes.Structure):
     _fields_ = [("aggs", ctypes.POINTER(AggBlock)), ("naggs", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32,
+                                ctypes.c_int32)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)
+
+
+class HostTransport(ctypes.Structure):
+    """esgpu_host_transport: a caller's collectives for esgpu_comm_init_host."""
+    _fields_ = [("user", ctypes.c_void_p), ("allreduce", ALLREDUCE_FN), ("allgather", ALLGATHER_FN)]
+
+
 # every entry point declared in include/esgpu.h: (name, restype, argtypes)
 _VP = ctypes.c_void_p
 _PP = ctypes.POINTER(ctypes.c_void_p)
@@ -138,6 +150,7 @@ SIGNATURES = [
     ("esgpu_plan_destroy", ctypes.c_int, [_VP]),
     ("esgpu_plan_last_collect_stats", ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64),
                                                      ctypes.POINTER(ctypes.c_int32)]),
+    ("esgpu_plan_shard_mergeable", ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_int32)]),
     ("esgpu_result_free", ctypes.c_int, [ctypes.POINTER(Result)]),
     ("esgpu_reduce", ctypes.c_int, [ctypes.POINTER(ctypes.POINTER(Result)), ctypes.c_int32,
                                     ctypes.POINTER(ctypes.POINTER(Result))]),
@@ -148,8 +161,13 @@ SIGNATURES = [
     ("esgpu_result_deserialize", ctypes.c_int, [_VP, ctypes.c_size_t, ctypes.POINTER(ctypes.POINTER(Result))]),
     ("esgpu_comm_unique_id", ctypes.c_int, [_VP]),
     ("esgpu_comm_init", ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_int32, _VP, _PP]),
+    ("esgpu_comm_init_host", ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(HostTransport), _PP]),
     ("esgpu_comm_destroy", ctypes.c_int, [_VP]),
+    ("esgpu_comm_reduce", ctypes.c_int, [_VP, ctypes.POINTER(ctypes.POINTER(Result)), ctypes.c_int32,
+                                         ctypes.POINTER(ctypes.POINTER(Result))]),
     ("esgpu_comm_gather_reduce", ctypes.c_int, [_VP, ctypes.POINTER(Result), ctypes.POINTER(ctypes.POINTER(Result))]),
+    ("esgpu_comm_last_exchange", ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                                ctypes.POINTER(ctypes.c_int32)]),
 ]
 
 

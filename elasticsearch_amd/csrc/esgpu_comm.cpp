@@ -1,0 +1,176 @@
+// esgpu_comm.cpp — the shard reduce across ranks (include/esgpu.h "Shard reduce across ranks"): collectives over
+// RCCL / xGMI (one process per GPU) or over a caller's host transport, driving reduce_across (esgpu_results.cpp).
+//
+// Reference: the coordinating reduce SearchPhaseController.merge -> InternalAggregations.reduce
+// (core/src/main/java/org/elasticsearch/search/controller/SearchPhaseController.java:401-411) over shard results
+// that travel as AggregationStreams records; here fixed-shape partials travel as ncclAllReduce operands instead.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "../../include/esgpu.h"
+#include "esgpu_internal.hpp"
+#include "esgpu_results.hpp"
+
+using namespace esgpu;
+
+#define NCCLX(expr)                                                                                           \
+    do {                                                                                                      \
+        ncclResult_t r_ = (expr);                                                                             \
+        if (r_ != ncclSuccess) throw EsError(ESGPU_ERR_DEVICE, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+namespace {
+
+size_t dt_size(int dt) { return dt == ESGPU_DT_U8 ? 1 : 8; }
+
+// RCCL over xGMI: host operands staged through pinned memory into a device buffer, reduced in place on the
+// communicator's stream.  The operands are small (KB for histograms, 2^p bytes of registers, shard records).
+struct RcclCollective : Collective {
+    esgpu_ctx* ctx = nullptr;
+    ncclComm_t comm = nullptr;
+    hipStream_t stream = nullptr;
+    Scratch d_in, d_out;
+    PinnedBuf h_in, h_out;
+    ~RcclCollective() override {
+        if (ctx) (void)hipSetDevice(ctx->device);
+        if (comm) ncclCommDestroy(comm);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+    void allreduce(void* buf, uint64_t count, int dt, int op) override {
+        if (!count) return;
+        const size_t bytes = count * dt_size(dt);
+        HIPX(hipSetDevice(ctx->device));
+        void* h = h_in.ensure(bytes);
+        std::memcpy(h, buf, bytes);
+        void* d = d_in.ensure(ctx, bytes);
+        HIPX(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream));
+        const ncclDataType_t t = dt == ESGPU_DT_U8 ? ncclUint8 : dt == ESGPU_DT_I64 ? ncclInt64 : dt == ESGPU_DT_U64 ? ncclUint64 : ncclFloat64;
+        const ncclRedOp_t o = op == ESGPU_RED_SUM ? ncclSum : op == ESGPU_RED_MIN ? ncclMin : ncclMax;
+        NCCLX(ncclAllReduce(d, d, count, t, o, comm, stream));
+        HIPX(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, stream));
+        HIPX(hipStreamSynchronize(stream));
+        std::memcpy(buf, h, bytes);
+        allreduce_bytes += bytes;
+        ++collectives;
+    }
+    void allgather(const void* in, void* out, uint64_t bytes) override {
+        HIPX(hipSetDevice(ctx->device));
+        const size_t total = (size_t)bytes * nranks;
+        void* hi = h_in.ensure(std::max<size_t>(bytes, 1));
+        std::memcpy(hi, in, bytes);
+        uint8_t* di = (uint8_t*)d_in.ensure(ctx, std::max<size_t>(bytes, 1));
+        uint8_t* dout = (uint8_t*)d_out.ensure(ctx, std::max<size_t>(total, 1));
+        HIPX(hipMemcpyAsync(di, hi, bytes, hipMemcpyHostToDevice, stream));
+        NCCLX(ncclAllGather(di, dout, bytes, ncclUint8, comm, stream));
+        void* ho = h_out.ensure(std::max<size_t>(total, 1));
+        HIPX(hipMemcpyAsync(ho, dout, total, hipMemcpyDeviceToHost, stream));
+        HIPX(hipStreamSynchronize(stream));
+        std::memcpy(out, ho, total);
+        allgather_bytes += total;
+        ++collectives;
+    }
+};
+
+// a caller's transport (esgpu_comm_init_host)
+struct HostCollective : Collective {
+    esgpu_host_transport t{};
+    void allreduce(void* buf, uint64_t count, int dt, int op) override {
+        if (!count) return;
+        require(t.allreduce(t.user, buf, count, dt, op) == 0, ESGPU_ERR_DEVICE, "host transport all-reduce failed");
+        allreduce_bytes += count * dt_size(dt);
+        ++collectives;
+    }
+    void allgather(const void* in, void* out, uint64_t bytes) override {
+        require(t.allgather(t.user, in, out, bytes) == 0, ESGPU_ERR_DEVICE, "host transport all-gather failed");
+        allgather_bytes += bytes * nranks;
+        ++collectives;
+    }
+};
+
+}  // namespace
+
+struct esgpu_comm {
+    std::unique_ptr<Collective> coll;
+};
+
+extern "C" int esgpu_comm_unique_id(uint8_t* id_out) {
+    return guarded([&] {
+        static_assert(sizeof(ncclUniqueId) == ESGPU_COMM_ID_BYTES, "ncclUniqueId size");
+        require(id_out != nullptr, ESGPU_ERR_INVALID, "null argument");
+        ncclUniqueId id;
+        NCCLX(ncclGetUniqueId(&id));
+        std::memcpy(id_out, &id, sizeof id);
+    });
+}
+
+extern "C" int esgpu_comm_init(esgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t* id, esgpu_comm** out) {
+    return guarded([&] {
+        require(c && id && out && nranks >= 1 && rank >= 0 && rank < nranks, ESGPU_ERR_INVALID, "bad communicator arguments");
+        HIPX(hipSetDevice(c->device));
+        std::unique_ptr<RcclCollective> r(new RcclCollective());
+        r->ctx = c;
+        r->nranks = nranks;
+        r->rank = rank;
+        ncclUniqueId uid;
+        std::memcpy(&uid, id, sizeof uid);
+        NCCLX(ncclCommInitRank(&r->comm, nranks, uid, rank));
+        HIPX(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
+        std::unique_ptr<esgpu_comm> cm(new esgpu_comm());
+        cm->coll = std::move(r);
+        *out = cm.release();
+    });
+}
+
+extern "C" int esgpu_comm_init_host(int32_t nranks, int32_t rank, const esgpu_host_transport* t, esgpu_comm** out) {
+    return guarded([&] {
+        require(t && t->allreduce && t->allgather && out && nranks >= 1 && rank >= 0 && rank < nranks, ESGPU_ERR_INVALID,
+                "bad communicator arguments");
+        std::unique_ptr<HostCollective> h(new HostCollective());
+        h->t = *t;
+        h->nranks = nranks;
+        h->rank = rank;
+        std::unique_ptr<esgpu_comm> cm(new esgpu_comm());
+        cm->coll = std::move(h);
+        *out = cm.release();
+    });
+}
+
+extern "C" int esgpu_comm_destroy(esgpu_comm* cm) {
+    return guarded([&] { delete cm; });
+}
+
+static int comm_reduce(esgpu_comm* cm, const esgpu_result* const* locals, int32_t n, esgpu_result** out, bool gather_only) {
+    return guarded([&] {
+        require(cm && locals && n >= 1 && out, ESGPU_ERR_INVALID, "comm reduce needs at least one local shard result");
+        std::vector<const std::vector<Block>*> lists;
+        for (int i = 0; i < n; ++i) {
+            require(locals[i] != nullptr, ESGPU_ERR_INVALID, "null shard result");
+            lists.push_back(&holder_of(locals[i])->aggs);
+        }
+        std::unique_ptr<ResultHolder> h(new ResultHolder());
+        h->aggs = reduce_across(*cm->coll, lists, gather_only);
+        h->export_view();
+        *out = &h.release()->pub;
+    });
+}
+
+extern "C" int esgpu_comm_reduce(esgpu_comm* cm, const esgpu_result* const* locals, int32_t n, esgpu_result** out) {
+    return comm_reduce(cm, locals, n, out, false);
+}
+
+extern "C" int esgpu_comm_gather_reduce(esgpu_comm* cm, const esgpu_result* local, esgpu_result** out) {
+    return comm_reduce(cm, &local, 1, out, true);
+}
+
+extern "C" int esgpu_comm_last_exchange(const esgpu_comm* cm, uint64_t* ar, uint64_t* ag, int32_t* n) {
+    return guarded([&] {
+        require(cm != nullptr, ESGPU_ERR_INVALID, "null communicator");
+        if (ar) *ar = cm->coll->allreduce_bytes;
+        if (ag) *ag = cm->coll->allgather_bytes;
+        if (n) *n = cm->coll->collectives;
+    });
+}

@@ -12,6 +12,7 @@
 #include "esgpu_results.hpp"
 
 #include <algorithm>
+#include <iterator>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -146,14 +147,24 @@ struct HllState {
         const int m = 1 << p;
         const size_t threshold = (size_t)((float)(m / 4) * 0.75f);
         if (omode == 0) {
-            for (uint32_t e : olc) {
-                if (mode == 0) {
-                    auto it = std::lower_bound(lc.begin(), lc.end(), e);
-                    if (it == lc.end() || *it != e) {
-                        lc.insert(it, e);
-                        if (lc.size() > threshold) upgrade();
-                    }
-                } else {
+            if (mode == 0) {
+                // Hashset adds with an upgrade once the set exceeds the threshold: the upgraded registers are the
+                // maxima over the union, so the sorted union (then one upgrade if it is too large) is the same state
+                std::vector<uint32_t> sorted_olc;
+                const std::vector<uint32_t>* o = &olc;
+                if (!std::is_sorted(olc.begin(), olc.end())) {
+                    sorted_olc = olc;
+                    std::sort(sorted_olc.begin(), sorted_olc.end());
+                    o = &sorted_olc;
+                }
+                std::vector<uint32_t> u;
+                u.reserve(lc.size() + o->size());
+                std::set_union(lc.begin(), lc.end(), o->begin(), o->end(), std::back_inserter(u));
+                u.erase(std::unique(u.begin(), u.end()), u.end());
+                lc.swap(u);
+                if (lc.size() > threshold) upgrade();
+            } else {
+                for (uint32_t e : olc) {
                     uint8_t& r = regs[dec_index(e, p)];
                     r = (uint8_t)std::max<uint32_t>(r, dec_run_len(e, p));
                 }
@@ -568,7 +579,7 @@ void reduce_level(const Level& lv, Block& out) {
 }  // namespace
 
 // shard results of one request share the aggregation tree (types, sub-aggregation lists, sketch precision)
-static bool same_shape(const Block& a, const Block& b) {
+bool same_shape(const Block& a, const Block& b) {
     if (a.type != b.type || a.subs.size() != b.subs.size() || a.empty_subs.size() != b.empty_subs.size()) return false;
     if (a.type == ESGPU_AGG_CARDINALITY && a.precision != b.precision) return false;
     for (size_t j = 0; j < a.subs.size(); ++j) if (!same_shape(a.subs[j], b.subs[j])) return false;
@@ -997,6 +1008,333 @@ void ResultHolder::export_view() {
     std::memset(&pub, 0, sizeof pub);
     pub.aggs = export_blocks(*this, aggs);
     pub.naggs = (int32_t)aggs.size();
+}
+
+
+// ------------------------------------------------------------------------------------------------------------
+// reduce across ranks: all-reduce for fixed-shape partials, all-gather of shard records for the rest
+// ------------------------------------------------------------------------------------------------------------
+namespace {
+
+// order-preserving image of a double (Java Math.min / Math.max order: -0.0 < +0.0); NaN wins both reductions
+inline uint64_t enc_dbl(double x) {
+    uint64_t b;
+    std::memcpy(&b, &x, 8);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ULL);
+}
+inline double dec_dbl(uint64_t e) {
+    const uint64_t b = (e >> 63) ? (e & 0x7FFFFFFFFFFFFFFFULL) : ~e;
+    double x;
+    std::memcpy(&x, &b, 8);
+    return x;
+}
+inline uint64_t enc_min(double x) { return x != x ? 0 : enc_dbl(x); }
+inline uint64_t enc_max(double x) { return x != x ? ~0ULL : enc_dbl(x); }
+inline double dec_min(uint64_t e) { return e == 0 ? NAN : dec_dbl(e); }
+inline double dec_max(uint64_t e) { return e == ~0ULL ? NAN : dec_dbl(e); }
+
+bool is_numeric_metric(int t) { return t == ESGPU_AGG_STATS || t == ESGPU_AGG_EXTENDED_STATS || t == ESGPU_AGG_AVG; }
+
+// a top-level aggregation whose shard partials have a fixed shape once the bucket keys are agreed on
+bool fixed_shape(const Block& b) {
+    if (is_numeric_metric(b.type) || b.type == ESGPU_AGG_CARDINALITY) return true;
+    if (b.type == ESGPU_AGG_HISTOGRAM || b.type == ESGPU_AGG_DATE_HISTOGRAM) {
+        for (const Block& s : b.subs) if (!is_numeric_metric(s.type)) return false;
+        return true;
+    }
+    return false;
+}
+
+// all-gather of one variable-size byte message per rank: sizes first, then padded records
+std::vector<std::string> gather_messages(Collective& c, const std::string& mine) {
+    std::vector<uint64_t> sizes(c.nranks);
+    const uint64_t my = mine.size();
+    c.allgather(&my, sizes.data(), 8);
+    const uint64_t rec = (std::max<uint64_t>(*std::max_element(sizes.begin(), sizes.end()), 8) + 15) & ~15ull;
+    std::string padded(mine);
+    padded.resize(rec, '\0');
+    std::string all((size_t)(rec * c.nranks), '\0');
+    c.allgather(padded.data(), &all[0], rec);
+    std::vector<std::string> out(c.nranks);
+    for (int r = 0; r < c.nranks; ++r) out[r] = all.substr((size_t)(rec * r), (size_t)sizes[r]);
+    return out;
+}
+
+std::string pack_lists(const std::vector<std::vector<Block>>& lists) {
+    std::string out;
+    const uint32_t n = (uint32_t)lists.size();
+    out.append((const char*)&n, 4);
+    for (const auto& l : lists) {
+        std::string rec;
+        serialize(l, rec);
+        const uint64_t len = rec.size();
+        out.append((const char*)&len, 8);
+        out += rec;
+    }
+    return out;
+}
+
+void unpack_lists(const std::string& msg, std::vector<std::vector<Block>>& out) {
+    size_t i = 0;
+    auto need = [&](size_t k) { if (i + k > msg.size()) throw std::runtime_error("corrupt shard message"); };
+    need(4);
+    uint32_t n;
+    std::memcpy(&n, msg.data(), 4);
+    i = 4;
+    if (n > 65536) throw std::runtime_error("corrupt shard message");
+    for (uint32_t k = 0; k < n; ++k) {
+        need(8);
+        uint64_t len;
+        std::memcpy(&len, msg.data() + i, 8);
+        i += 8;
+        need((size_t)len);
+        out.emplace_back();
+        if (!deserialize((const uint8_t*)msg.data() + i, (size_t)len, out.back())) throw std::runtime_error("corrupt shard record");
+        i += (size_t)len;
+    }
+}
+
+}  // namespace
+
+std::vector<Block> reduce_across(Collective& c, const std::vector<const std::vector<Block>*>& locals, bool gather_only) {
+    if (locals.empty()) throw std::invalid_argument("every rank reduces at least one local shard result");
+    c.allreduce_bytes = c.allgather_bytes = 0;
+    c.collectives = 0;
+    const std::vector<Block>& first = *locals[0];
+    const size_t naggs = first.size();
+    for (auto* l : locals) {
+        if (l->size() != naggs) throw std::invalid_argument("shard results have different aggregation lists");
+        for (size_t a = 0; a < naggs; ++a)
+            if (!same_shape((*l)[a], first[a])) throw std::invalid_argument("aggregation trees differ across shards");
+    }
+    std::vector<int> fixed, gathered;
+    for (size_t a = 0; a < naggs; ++a) (!gather_only && fixed_shape(first[a]) ? fixed : gathered).push_back((int)a);
+    std::vector<Block> out(naggs);
+
+    // ---- all-gather path: every rank's shard records, reduced in global shard order (rank-major) ----
+    if (!gathered.empty()) {
+        std::vector<std::vector<Block>> mine;
+        for (auto* l : locals) {
+            mine.emplace_back();
+            for (int a : gathered) mine.back().push_back((*l)[a]);
+        }
+        std::vector<std::string> msgs = gather_messages(c, pack_lists(mine));
+        std::vector<std::vector<Block>> shards;
+        for (const std::string& m : msgs) unpack_lists(m, shards);
+        std::vector<const std::vector<Block>*> lists;
+        for (auto& s : shards) lists.push_back(&s);
+        std::vector<Block> red = reduce_lists(lists);
+        for (size_t k = 0; k < gathered.size(); ++k) out[gathered[k]] = std::move(red[k]);
+    }
+
+    // ---- fixed-shape path ----
+    // (1) bucket keys of the top-level histograms: the union over every rank's shards (all-gather of the key lists)
+    std::vector<int> hists, metrics, cards;
+    for (int a : fixed) {
+        const int t = first[a].type;
+        if (t == ESGPU_AGG_CARDINALITY) cards.push_back(a);
+        else if (t == ESGPU_AGG_HISTOGRAM || t == ESGPU_AGG_DATE_HISTOGRAM) hists.push_back(a);
+        else metrics.push_back(a);
+    }
+    std::vector<std::vector<int64_t>> keys(naggs);
+    if (!hists.empty()) {
+        std::vector<int64_t> msg;  // [count per histogram] [keys of histogram 0] ...
+        std::vector<std::vector<int64_t>> local(hists.size());
+        for (size_t h = 0; h < hists.size(); ++h) {
+            for (auto* l : locals) {
+                const Block& b = (*l)[hists[h]];
+                local[h].insert(local[h].end(), b.key.begin() + (int64_t)b.boff[0], b.key.begin() + (int64_t)b.boff[1]);
+            }
+            std::sort(local[h].begin(), local[h].end());
+            local[h].erase(std::unique(local[h].begin(), local[h].end()), local[h].end());
+            msg.push_back((int64_t)local[h].size());
+        }
+        for (auto& v : local) msg.insert(msg.end(), v.begin(), v.end());
+        const std::vector<std::string> msgs = gather_messages(c, std::string((const char*)msg.data(), msg.size() * 8));
+        for (const std::string& m : msgs) {
+            const int64_t* p = (const int64_t*)m.data();
+            const size_t n = m.size() / 8;
+            if (n < hists.size()) throw std::runtime_error("corrupt key message");
+            size_t pos = hists.size();
+            for (size_t h = 0; h < hists.size(); ++h) {
+                const size_t cnt = (size_t)p[h];
+                if (pos + cnt > n) throw std::runtime_error("corrupt key message");
+                keys[hists[h]].insert(keys[hists[h]].end(), p + pos, p + pos + cnt);
+                pos += cnt;
+            }
+        }
+        for (int a : hists) {
+            std::sort(keys[a].begin(), keys[a].end());
+            keys[a].erase(std::unique(keys[a].begin(), keys[a].end()), keys[a].end());
+        }
+    }
+    // (2) dense partials: per slot (histogram bucket, or the one metric instance) the doc count, and per numeric metric
+    //     its value count (u64 sums), sum and sum of squares (f64 sums), min and max (u64 min / max of encodings)
+    struct Layout { int agg; size_t slots, nmet, u64, f64, mn, mx; };
+    std::vector<Layout> lay;
+    size_t nu = 0, nf = 0, nmn = 0, nmx = 0;
+    for (int a : fixed) {
+        const Block& b = first[a];
+        if (b.type == ESGPU_AGG_CARDINALITY) continue;
+        const bool hist = b.is_bucket();
+        Layout L{a, hist ? keys[a].size() : 1, hist ? b.subs.size() : 1, nu, nf, nmn, nmx};
+        nu += L.slots * ((hist ? 1 : 0) + L.nmet);
+        nf += L.slots * L.nmet * 2;
+        nmn += L.slots * L.nmet;
+        nmx += L.slots * L.nmet;
+        lay.push_back(L);
+    }
+    if (!lay.empty()) {
+        std::vector<uint64_t> U(nu, 0), MN(nmn, ~0ULL), MX(nmx, 0);
+        std::vector<double> F(nf, 0.0);
+        for (const Layout& L : lay) {
+            const bool hist = first[L.agg].is_bucket();
+            const size_t du = hist ? 1 : 0;
+            for (auto* l : locals) {  // local shards in shard order
+                const Block& b = (*l)[L.agg];
+                const uint64_t k0 = hist ? b.boff[0] : 0, k1 = hist ? b.boff[1] : 1;
+                for (uint64_t k = k0; k < k1; ++k) {
+                    size_t slot = 0;
+                    if (hist) {
+                        slot = (size_t)(std::lower_bound(keys[L.agg].begin(), keys[L.agg].end(), b.key[k]) - keys[L.agg].begin());
+                        U[L.u64 + slot * (du + L.nmet)] += (uint64_t)b.bcount[k];
+                    }
+                    for (size_t j = 0; j < L.nmet; ++j) {
+                        const Block& m = hist ? b.subs[j] : b;
+                        const uint64_t i = hist ? k : 0;
+                        U[L.u64 + slot * (du + L.nmet) + du + j] += (uint64_t)m.count[i];
+                        F[L.f64 + (slot * L.nmet + j) * 2] += m.sum[i];
+                        F[L.f64 + (slot * L.nmet + j) * 2 + 1] += m.sumsq[i];
+                        uint64_t& mn = MN[L.mn + slot * L.nmet + j];
+                        uint64_t& mx = MX[L.mx + slot * L.nmet + j];
+                        mn = std::min(mn, enc_min(m.min[i]));
+                        mx = std::max(mx, enc_max(m.max[i]));
+                    }
+                }
+            }
+        }
+        if (nu) c.allreduce(U.data(), nu, ESGPU_DT_U64, ESGPU_RED_SUM);
+        if (nf) c.allreduce(F.data(), nf, ESGPU_DT_F64, ESGPU_RED_SUM);
+        if (nmn) c.allreduce(MN.data(), nmn, ESGPU_DT_U64, ESGPU_RED_MIN);
+        if (nmx) c.allreduce(MX.data(), nmx, ESGPU_DT_U64, ESGPU_RED_MAX);
+        // (3) one merged shard result per aggregation, then the reference's own single-shard reduce on it (min_doc_count,
+        //     empty-bucket fill, order)
+        for (const Layout& L : lay) {
+            const Block& proto = first[L.agg];
+            const bool hist = proto.is_bucket();
+            const size_t du = hist ? 1 : 0;
+            Block m = proto.like();
+            auto put_metric = [&](Block& dst, size_t slot, size_t j) {
+                ++dst.n;
+                dst.count.push_back((int64_t)U[L.u64 + slot * (du + L.nmet) + du + j]);
+                dst.sum.push_back(F[L.f64 + (slot * L.nmet + j) * 2]);
+                dst.sumsq.push_back(F[L.f64 + (slot * L.nmet + j) * 2 + 1]);
+                dst.min.push_back(dec_min(MN[L.mn + slot * L.nmet + j]));
+                dst.max.push_back(dec_max(MX[L.mx + slot * L.nmet + j]));
+            };
+            if (!hist) {
+                put_metric(m, 0, 0);
+            } else {
+                ++m.n;
+                m.doc_count_error.push_back(0);
+                m.other_doc_count.push_back(0);
+                for (size_t slot = 0; slot < L.slots; ++slot) {
+                    const uint64_t dc = U[L.u64 + slot * (du + L.nmet)];
+                    if (dc == 0) continue;
+                    m.key.push_back(keys[L.agg][slot]);
+                    m.term_off.push_back(m.term_pool.size());
+                    m.bcount.push_back((int64_t)dc);
+                    m.berr.push_back(0);
+                    for (size_t j = 0; j < L.nmet; ++j) put_metric(m.subs[j], slot, j);
+                }
+                m.boff.push_back(m.key.size());
+            }
+            std::vector<Block> one;
+            one.push_back(std::move(m));
+            out[L.agg] = std::move(reduce_lists({&one})[0]);
+        }
+    }
+    // (4) cardinality: local merge (shard order), then register max over the ranks -- or, while every rank is still in
+    //     LINEAR_COUNTING, the union of the encoded-hash sets (HyperLogLogPlusPlus.merge, :201-230; the merged state
+    //     depends only on the union of encoded hashes and the register maxima)
+    if (!cards.empty()) {
+        std::vector<HllState> st(cards.size());
+        std::vector<uint64_t> flags(cards.size() * 2, 0);  // present, hll mode
+        for (size_t k = 0; k < cards.size(); ++k) {
+            for (auto* l : locals) {
+                const Block& b = (*l)[cards[k]];
+                if (!b.hll_present[0]) continue;
+                if (!st[k].present) { st[k].present = true; st[k].p = b.precision; st[k].mode = 0; }
+                st[k].merge(b.precision, b.hll_mode[0], b.regs[0], b.lc[0]);
+            }
+            flags[2 * k] = st[k].present;
+            flags[2 * k + 1] = st[k].mode;
+        }
+        c.allreduce(flags.data(), flags.size(), ESGPU_DT_U64, ESGPU_RED_MAX);
+        std::vector<int> to_union;
+        for (size_t k = 0; k < cards.size(); ++k) {
+            const Block& proto = first[cards[k]];
+            if (!flags[2 * k]) {  // no rank collected a value: the empty sketch
+                Block m = proto.like();
+                m.append_empty();
+                out[cards[k]] = std::move(m);
+                continue;
+            }
+            if (!flags[2 * k + 1]) { to_union.push_back((int)k); continue; }
+            HllState& s = st[k];
+            s.p = proto.precision;
+            if (!s.present) s.regs.assign((size_t)1 << s.p, 0);
+            else if (s.mode == 0) s.upgrade();
+            c.allreduce(s.regs.data(), s.regs.size(), ESGPU_DT_U8, ESGPU_RED_MAX);
+            Block m = proto.like();
+            ++m.n;
+            m.hll_present.push_back(1);
+            m.hll_mode.push_back(1);
+            m.regs.push_back(std::move(s.regs));
+            m.lc.emplace_back();
+            out[cards[k]] = std::move(m);
+        }
+        if (!to_union.empty()) {  // every rank in LINEAR_COUNTING: all-gather the sets, union, upgrade past threshold
+            std::string msg;
+            for (int k : to_union) {
+                const uint64_t n = st[k].lc.size();
+                msg.append((const char*)&n, 8);
+                msg.append((const char*)st[k].lc.data(), n * 4);
+            }
+            const std::vector<std::string> msgs = gather_messages(c, msg);
+            for (size_t u = 0; u < to_union.size(); ++u) {
+                const int k = to_union[u];
+                const Block& proto = first[cards[k]];
+                HllState s;
+                s.p = proto.precision;
+                s.present = true;
+                for (const std::string& mm : msgs) {  // rank order; the result only depends on the union
+                    size_t pos = 0;
+                    for (size_t v = 0; v <= u; ++v) {
+                        if (pos + 8 > mm.size()) throw std::runtime_error("corrupt set message");
+                        uint64_t n;
+                        std::memcpy(&n, mm.data() + pos, 8);
+                        pos += 8;
+                        if (pos + n * 4 > mm.size()) throw std::runtime_error("corrupt set message");
+                        if (v == u) {
+                            std::vector<uint32_t> lc(n);
+                            std::memcpy(lc.data(), mm.data() + pos, n * 4);
+                            s.merge(s.p, 0, {}, lc);
+                        }
+                        pos += n * 4;
+                    }
+                }
+                Block m = proto.like();
+                ++m.n;
+                m.hll_present.push_back(1);
+                m.hll_mode.push_back(s.mode);
+                m.regs.push_back(std::move(s.regs));
+                m.lc.push_back(std::move(s.lc));
+                out[cards[k]] = std::move(m);
+            }
+        }
+    }
+    return out;
 }
 
 }  // namespace esgpu

@@ -84,6 +84,27 @@ int64_t hll_cardinality(int precision, bool present, int mode, const uint8_t* re
 // InternalAggregations.reduce over shard lists in shard order
 std::vector<Block> reduce_lists(const std::vector<const std::vector<Block>*>& lists);
 
+// ---- the shard reduce across ranks (one process per GPU) ----
+// Host-memory collectives among the ranks of one reduce; RCCL over xGMI (esgpu_comm_init) or a caller transport
+// (esgpu_comm_init_host).  dtype / op values are include/esgpu.h's ESGPU_DT_* / ESGPU_RED_*.
+struct Collective {
+    int nranks = 1, rank = 0;
+    uint64_t allreduce_bytes = 0, allgather_bytes = 0;  // per reduce call (statistics)
+    int32_t collectives = 0;
+    virtual ~Collective() {}
+    virtual void allreduce(void* buf, uint64_t count, int dtype, int op) = 0;  // in place
+    virtual void allgather(const void* in, void* out, uint64_t bytes) = 0;     // out: nranks * bytes, rank order
+};
+// InternalAggregations.reduce over every rank's shard results, the shards in rank-major order (rank r's `locals` are
+// global shards r * n_local ...).  Fixed-shape partials are combined by all-reduce: top-level histograms with numeric
+// metric sub-aggregations (bucket keys all-gathered, then sum of doc counts / metric counts / sums / sums of squares,
+// min / max of order-preserving encodings), top-level numeric metrics, and top-level cardinality (register max over
+// 2^p bytes, or the union of the linear-counting sets while every rank is still in LINEAR_COUNTING).  Everything
+// else (terms at any level: per-shard top-k then merge) is all-gathered as shard records and reduced in shard order.
+std::vector<Block> reduce_across(Collective& c, const std::vector<const std::vector<Block>*>& locals,
+                                 bool gather_only = false);
+bool same_shape(const Block& a, const Block& b);
+
 std::string to_json(const std::vector<Block>& aggs);
 void serialize(const std::vector<Block>& aggs, std::string& out);
 bool deserialize(const uint8_t* p, size_t n, std::vector<Block>& out);

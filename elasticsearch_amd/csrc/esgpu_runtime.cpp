@@ -11,7 +11,6 @@
 //   esgpu_plan_build            buildAggregation(0) (GlobalOrdinalsStringTermsAggregator.java:146-208,
 //                               HistogramAggregator.java:120-133, StatsAggegator.java:140-152, ...)
 #include <hip/hip_runtime.h>
-#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <atomic>
@@ -1704,6 +1703,15 @@ extern "C" int esgpu_plan_collect_segment(esgpu_plan* p, const esgpu_segment* s,
     });
 }
 
+extern "C" int esgpu_plan_shard_mergeable(const esgpu_plan* p, int32_t* mergeable) {
+    return guarded([&] {
+        require(p && mergeable, ESGPU_ERR_INVALID, "null argument");
+        int32_t m = 1;
+        for (const SpecNode& n : p->specs) if (n.s.type == ESGPU_AGG_TERMS) m = 0;
+        *mergeable = m;
+    });
+}
+
 extern "C" int esgpu_plan_last_collect_stats(const esgpu_plan* cp, double* kernel_ms, uint64_t* bytes, int32_t* path) {
     return guarded([&] {
         esgpu_plan* p = const_cast<esgpu_plan*>(cp);
@@ -2362,94 +2370,3 @@ extern "C" int esgpu_result_deserialize(const uint8_t* buf, size_t len, esgpu_re
     });
 }
 
-// ------------------------------------------------------------------------------------------------------------
-// RCCL shard reduce (one process per GPU)
-// ------------------------------------------------------------------------------------------------------------
-struct esgpu_comm {
-    esgpu_ctx* ctx = nullptr;
-    ncclComm_t comm = nullptr;
-    int nranks = 1, rank = 0;
-    hipStream_t stream = nullptr;
-    Scratch dsz, dall, dmine;   // grown on demand, reused across requests
-    PinnedBuf hsz, hall, hmine;
-};
-
-#define NCCLX(expr)                                                                                           \
-    do {                                                                                                      \
-        ncclResult_t r_ = (expr);                                                                             \
-        if (r_ != ncclSuccess) throw EsError(ESGPU_ERR_DEVICE, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
-    } while (0)
-
-extern "C" int esgpu_comm_unique_id(uint8_t* id_out) {
-    return guarded([&] {
-        static_assert(sizeof(ncclUniqueId) == ESGPU_COMM_ID_BYTES, "ncclUniqueId size");
-        ncclUniqueId id;
-        NCCLX(ncclGetUniqueId(&id));
-        std::memcpy(id_out, &id, sizeof id);
-    });
-}
-
-extern "C" int esgpu_comm_init(esgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t* id, esgpu_comm** out) {
-    return guarded([&] {
-        require(c && id && out && nranks >= 1 && rank >= 0 && rank < nranks, ESGPU_ERR_INVALID, "bad communicator arguments");
-        HIPX(hipSetDevice(c->device));
-        std::unique_ptr<esgpu_comm> cm(new esgpu_comm());
-        cm->ctx = c;
-        cm->nranks = nranks;
-        cm->rank = rank;
-        ncclUniqueId uid;
-        std::memcpy(&uid, id, sizeof uid);
-        NCCLX(ncclCommInitRank(&cm->comm, nranks, uid, rank));
-        HIPX(hipStreamCreateWithFlags(&cm->stream, hipStreamNonBlocking));
-        *out = cm.release();
-    });
-}
-
-extern "C" int esgpu_comm_destroy(esgpu_comm* cm) {
-    return guarded([&] {
-        if (!cm) return;
-        (void)hipSetDevice(cm->ctx->device);
-        if (cm->comm) ncclCommDestroy(cm->comm);
-        if (cm->stream) (void)hipStreamDestroy(cm->stream);
-        delete cm;
-    });
-}
-
-extern "C" int esgpu_comm_gather_reduce(esgpu_comm* cm, const esgpu_result* local, esgpu_result** out) {
-    return guarded([&] {
-        require(cm && local && out, ESGPU_ERR_INVALID, "null argument");
-        HIPX(hipSetDevice(cm->ctx->device));
-        std::string mine;
-        serialize(holder_of(local)->aggs, mine);
-        // 1) all-gather the record sizes, 2) all-gather fixed-size padded records (shard order == rank order)
-        const size_t n = (size_t)cm->nranks;
-        uint64_t* hsz = (uint64_t*)cm->hsz.ensure(n * 8);
-        uint8_t* dsz = (uint8_t*)cm->dsz.ensure(cm->ctx, n * 8);
-        hsz[cm->rank] = mine.size();
-        HIPX(hipMemcpyAsync(dsz + (size_t)cm->rank * 8, hsz + cm->rank, 8, hipMemcpyHostToDevice, cm->stream));
-        NCCLX(ncclAllGather(dsz + (size_t)cm->rank * 8, dsz, 8, ncclUint8, cm->comm, cm->stream));
-        HIPX(hipMemcpyAsync(hsz, dsz, n * 8, hipMemcpyDeviceToHost, cm->stream));
-        HIPX(hipStreamSynchronize(cm->stream));
-        std::vector<uint64_t> sizes(hsz, hsz + n);
-        const uint64_t rec = (std::max<uint64_t>(*std::max_element(sizes.begin(), sizes.end()), 8) + 15) & ~15ull;
-        uint8_t* hmine = (uint8_t*)cm->hmine.ensure(rec);
-        std::memcpy(hmine, mine.data(), mine.size());
-        uint8_t* dmine = (uint8_t*)cm->dmine.ensure(cm->ctx, rec);
-        uint8_t* dall = (uint8_t*)cm->dall.ensure(cm->ctx, rec * n);
-        HIPX(hipMemcpyAsync(dmine, hmine, rec, hipMemcpyHostToDevice, cm->stream));
-        NCCLX(ncclAllGather(dmine, dall, rec, ncclUint8, cm->comm, cm->stream));
-        uint8_t* all = (uint8_t*)cm->hall.ensure(rec * n);
-        HIPX(hipMemcpyAsync(all, dall, rec * n, hipMemcpyDeviceToHost, cm->stream));
-        HIPX(hipStreamSynchronize(cm->stream));
-        std::vector<std::vector<Block>> shards(cm->nranks);
-        std::vector<const std::vector<Block>*> lists;
-        for (int r = 0; r < cm->nranks; ++r) {
-            require(deserialize(all + rec * r, sizes[r], shards[r]), ESGPU_ERR_DEVICE, "corrupt shard record");
-            lists.push_back(&shards[r]);
-        }
-        std::unique_ptr<ResultHolder> h(new ResultHolder());
-        h->aggs = reduce_lists(lists);
-        h->export_view();
-        *out = &h.release()->pub;
-    });
-}

@@ -188,6 +188,12 @@ class Plan:
         N.check(N.lib().esgpu_plan_last_collect_stats(self._ptr, ctypes.byref(ms), ctypes.byref(nbytes), ctypes.byref(path)))
         return ms.value, nbytes.value, path.value
 
+    def shard_mergeable(self):
+        """True if several shards may be collected into this one plan (no terms aggregation, see include/esgpu.h)."""
+        v = ctypes.c_int32()
+        N.check(N.lib().esgpu_plan_shard_mergeable(self._ptr, ctypes.byref(v)))
+        return bool(v.value)
+
     def close(self):
         if self._ptr:
             N.check(N.lib().esgpu_plan_destroy(self._ptr))
@@ -354,13 +360,15 @@ def precision_from_threshold(t):
 
 
 class Communicator:
-    """RCCL communicator over xGMI for the shard-level reduce (one process per GPU)."""
+    """The shard reduce across ranks (include/esgpu.h "Shard reduce across ranks"): RCCL over xGMI between the GPUs of a
+    node, or the same reduce over a torch.distributed process group on the host (gloo: cross-node, CPU tests)."""
 
     def __init__(self, engine, nranks, rank, unique_id):
         ptr = ctypes.c_void_p()
         idbuf = (ctypes.c_uint8 * N.COMM_ID_BYTES).from_buffer_copy(unique_id)
         N.check(N.lib().esgpu_comm_init(engine.ptr, nranks, rank, idbuf, ctypes.byref(ptr)))
         self._ptr = ptr
+        self._keep = None
 
     @staticmethod
     def unique_id():
@@ -368,10 +376,74 @@ class Communicator:
         N.check(N.lib().esgpu_comm_unique_id(buf))
         return bytes(buf)
 
+    @classmethod
+    def over_process_group(cls, group=None):
+        """The reduce's collectives over torch.distributed (the default group, or `group`) in host memory."""
+        import numpy as _np
+        import torch
+        import torch.distributed as dist
+        nranks, rank = dist.get_world_size(group), dist.get_rank(group)
+        np_types = {N.DT_U8: _np.uint8, N.DT_I64: _np.int64, N.DT_U64: _np.uint64, N.DT_F64: _np.float64}
+        ops = {N.RED_SUM: dist.ReduceOp.SUM, N.RED_MIN: dist.ReduceOp.MIN, N.RED_MAX: dist.ReduceOp.MAX}
+
+        def allreduce(_user, buf, count, dt, op):
+            try:
+                a = _np.ctypeslib.as_array(ctypes.cast(buf, ctypes.POINTER(_np.ctypeslib.as_ctypes_type(np_types[dt]))),
+                                           shape=(count,))
+                if dt == N.DT_U64:  # unsigned order through signed int64: flip the sign bit around min / max
+                    x = a.view(_np.int64).copy()
+                    if op != N.RED_SUM:
+                        x ^= _np.int64(-(1 << 63))
+                    t = torch.from_numpy(x)
+                    dist.all_reduce(t, op=ops[op], group=group)
+                    y = t.numpy()
+                    if op != N.RED_SUM:
+                        y ^= _np.int64(-(1 << 63))
+                    a.view(_np.int64)[:] = y
+                else:
+                    t = torch.from_numpy(a.copy())
+                    dist.all_reduce(t, op=ops[op], group=group)
+                    a[:] = t.numpy()
+                return 0
+            except Exception:  # noqa: BLE001 -- a C caller cannot take a Python exception
+                return 1
+
+        def allgather(_user, src, dst, nbytes):
+            try:
+                x = torch.from_numpy(_np.frombuffer(ctypes.string_at(src, nbytes), dtype=_np.uint8).copy())
+                outs = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(nranks)]
+                dist.all_gather(outs, x, group=group)
+                joined = torch.cat(outs).numpy()  # keep a reference while copying out of it
+                ctypes.memmove(dst, joined.ctypes.data, nbytes * nranks)
+                return 0
+            except Exception:  # noqa: BLE001
+                return 1
+
+        t = N.HostTransport(None, N.ALLREDUCE_FN(allreduce), N.ALLGATHER_FN(allgather))
+        ptr = ctypes.c_void_p()
+        N.check(N.lib().esgpu_comm_init_host(nranks, rank, ctypes.byref(t), ctypes.byref(ptr)))
+        self = cls.__new__(cls)
+        self._ptr = ptr
+        self._keep = t  # the callbacks must outlive the communicator
+        return self
+
+    def reduce(self, shard_results):
+        """InternalAggregations.reduce over every rank's shard results (this rank's in its shard order)."""
+        arr = (ctypes.POINTER(N.Result) * len(shard_results))(*[r.ptr for r in shard_results])
+        out = ctypes.POINTER(N.Result)()
+        N.check(N.lib().esgpu_comm_reduce(self._ptr, arr, len(shard_results), ctypes.byref(out)))
+        return ShardResult(out)
+
     def gather_reduce(self, shard_result):
         out = ctypes.POINTER(N.Result)()
         N.check(N.lib().esgpu_comm_gather_reduce(self._ptr, shard_result.ptr, ctypes.byref(out)))
         return ShardResult(out)
+
+    def last_exchange(self):
+        """(all-reduce bytes, all-gather bytes, collectives) of the last reduce."""
+        ar, ag, n = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int32()
+        N.check(N.lib().esgpu_comm_last_exchange(self._ptr, ctypes.byref(ar), ctypes.byref(ag), ctypes.byref(n)))
+        return ar.value, ag.value, n.value
 
     def close(self):
         if self._ptr:

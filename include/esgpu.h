@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define ESGPU_ABI_VERSION 3
+#define ESGPU_ABI_VERSION 4
 
 /* ---------------------------------------------------------------------------------------------------------
  * Status codes.  Mapping used by the JNI shim (SURVEY §8(b) "Errors"):
@@ -311,6 +311,11 @@ int esgpu_plan_destroy(esgpu_plan* plan);
  * and the algorithmic bytes it read (SURVEY §8(d) formula). */
 int esgpu_plan_last_collect_stats(const esgpu_plan* plan, double* kernel_ms, uint64_t* algorithmic_bytes,
                                   int32_t* path);
+/* 1 if the plan's shard results are fixed-shape (no terms aggregation at any level): several shards of one GPU may
+ * then be collected into one plan -- their doc counts, sums, extrema and sketches add up exactly as the reduce of their
+ * separate results would (HistogramAggregator / metrics / HyperLogLogPlusPlus.merge; min_doc_count and empty buckets
+ * apply at reduce) -- while terms need one build per shard (per-shard top-k, InternalTerms.doReduce). */
+int esgpu_plan_shard_mergeable(const esgpu_plan* plan, int32_t* mergeable);
 
 /* ---------------------------------------------------------------------------------------------------------
  * Results: columnar InternalAggregations, owned by the library.
@@ -389,17 +394,46 @@ int esgpu_result_serialize(const esgpu_result* r, uint8_t* buf, size_t cap, size
 int esgpu_result_deserialize(const uint8_t* buf, size_t len, esgpu_result** out);
 
 /* ---------------------------------------------------------------------------------------------------------
- * Multi-GPU shard reduce over RCCL (one process per GPU; shards map one-per-GPU).
- * The unique id (ESGPU_COMM_ID_BYTES bytes) is created on rank 0 and broadcast by the caller.
- * esgpu_comm_gather_reduce: ncclAllGather of every rank's serialized shard result (fixed-size padded
- * records, xGMI), then InternalAggregations.reduce in rank (= shard) order on every rank.
+ * Shard reduce across ranks (one process per GPU; S shards per job, S / nranks per GPU); the
+ * coordinating reduce of SearchPhaseController.merge (C/search/controller/SearchPhaseController.java:401-411) done by
+ * every rank over a collective instead of a gather to one node.
+ *   esgpu_comm_init:      RCCL communicator over xGMI; the unique id (ESGPU_COMM_ID_BYTES bytes) is created on rank 0
+ *                         (esgpu_comm_unique_id) and broadcast by the caller.
+ *   esgpu_comm_init_host: the same reduce over a caller-supplied host transport (cross-node: the node's own transport,
+ *                         TransportService in the reference; tests: gloo).  Callbacks run on the calling thread and
+ *                         return 0 on success.
+ *   esgpu_comm_reduce:    InternalAggregations.reduce over every rank's shard results, the shards in rank-major order
+ *                         (rank r passes its n_local results in its shard order).  Fixed-shape partials are combined by
+ *                         all-reduce: top-level histograms with numeric metric sub-aggregations (bucket keys all-gathered,
+ *                         then ncclAllReduce sum of doc counts / value counts / sums / sums of squares, min / max of the
+ *                         order-preserving u64 image of the doubles), top-level stats / extended_stats / avg, and
+ *                         top-level cardinality (ncclAllReduce max over the 2^p u8 registers, or the union of the
+ *                         linear-counting sets while every rank is still in LINEAR_COUNTING).  Everything else --
+ *                         terms at any level, whose reduce is per-shard top-k then merge (InternalTerms.doReduce) -- is
+ *                         all-gathered as shard records and reduced in shard order.  Integer-valued sums are bit-exact;
+ *                         non-integer floating sums differ from the shard-order sum in the last bits only.
+ *   esgpu_comm_gather_reduce: every aggregation through the all-gather path (one local shard).
+ *   esgpu_comm_last_exchange: bytes moved by the last reduce on this communicator.
  * ------------------------------------------------------------------------------------------------------- */
 #define ESGPU_COMM_ID_BYTES 128
 typedef struct esgpu_comm esgpu_comm;
+enum { ESGPU_DT_U8 = 0, ESGPU_DT_I64 = 1, ESGPU_DT_U64 = 2, ESGPU_DT_F64 = 3 };
+enum { ESGPU_RED_SUM = 0, ESGPU_RED_MIN = 1, ESGPU_RED_MAX = 2 };
+typedef struct esgpu_host_transport {
+    void* user;
+    /* in place over `count` elements of dtype ESGPU_DT_*, op ESGPU_RED_* */
+    int (*allreduce)(void* user, void* buf, uint64_t count, int32_t dtype, int32_t op);
+    /* every rank contributes `bytes` bytes; `out` receives nranks * bytes in rank order */
+    int (*allgather)(void* user, const void* in, void* out, uint64_t bytes);
+} esgpu_host_transport;
 int esgpu_comm_unique_id(uint8_t* id_out);
 int esgpu_comm_init(esgpu_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t* id, esgpu_comm** out);
+int esgpu_comm_init_host(int32_t nranks, int32_t rank, const esgpu_host_transport* transport, esgpu_comm** out);
 int esgpu_comm_destroy(esgpu_comm* comm);
+int esgpu_comm_reduce(esgpu_comm* comm, const esgpu_result* const* locals, int32_t n_local, esgpu_result** out);
 int esgpu_comm_gather_reduce(esgpu_comm* comm, const esgpu_result* local, esgpu_result** out);
+int esgpu_comm_last_exchange(const esgpu_comm* comm, uint64_t* allreduce_bytes, uint64_t* allgather_bytes,
+                             int32_t* collectives);
 
 #ifdef __cplusplus
 }

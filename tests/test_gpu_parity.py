@@ -383,6 +383,24 @@ def test_rccl_gather_reduce_single_rank(engine):  # the bench's N > 1 exchange (
         assert_same(got, want["reduced"], "rccl reduced")
     plan.close()
     seg.close()
+    # esgpu_comm_reduce over RCCL with two local shards: all-reduce for the fixed-shape aggregations (histogram with
+    # metrics, top-level stats, cardinality), all-gather for terms; == the oracle's two-shard coordinator reduce
+    aggs2 = aggs + [AB.dateHistogram("days").field("@timestamp").interval("1d").minDocCount(0).subAggregation(
+        AB.extendedStats("rt").field("response_time_ms")), AB.stats("all").field("response_time_ms")]
+    want2 = O.run([(synthetic_columns(fields, n, shard=s), n) for s in range(2)], aggs2, number_of_shards=2)
+    plan = engine.plan(aggs2, number_of_shards=2)
+    locals_ = []
+    for s in range(2):
+        seg = engine.synthetic_segment(n, fields=fields, shard=s)
+        plan.reset()
+        plan.collect(seg)
+        locals_.append(plan.build())
+        seg.close()
+    got = comm.reduce(locals_).to_dict()
+    assert_same(got, want2["reduced"], "rccl comm reduce")
+    ar_bytes, _, _ = comm.last_exchange()
+    assert ar_bytes >= (1 << 10)  # the registers went through ncclAllReduce(max)
+    plan.close()
     comm.close()
 
 
@@ -398,3 +416,27 @@ def test_filter_aggregation(engine):  # FilterAggregator: top-level filter{...} 
             AB.terms("all_hosts").field("host").size(3)]
     run_both(engine, aggs, fields, n, filters=[QB.rangeQuery("response_time_ms").lt(900)])
     run_both(engine, aggs, fields, n)  # no query clauses: only the filters' own
+
+
+def test_fixed_shape_shards_collected_into_one_plan(engine):
+    """esgpu_plan_shard_mergeable: a request without terms may collect several shards into one plan (bench.py
+    --shards S on fewer GPUs); its one shard result reduces to what the reduce of the separate shard results gives."""
+    n = 300_000
+    fields = ("@timestamp", "response_time_ms", "client_ip.hash")
+    aggs = [AB.dateHistogram("h").field("@timestamp").interval("1h").minDocCount(3).subAggregation(
+                AB.extendedStats("rt").field("response_time_ms")).subAggregation(
+                AB.cardinality("ips").field("client_ip.hash").precisionThreshold(200)),
+            AB.cardinality("all_ips").field("client_ip.hash").precisionThreshold(40000),
+            AB.avg("rt").field("response_time_ms")]
+    shards = [(synthetic_columns(fields, n, shard=s), n) for s in range(3)]
+    want = O.run(shards, aggs, number_of_shards=3)
+    plan = engine.plan(aggs, number_of_shards=3)
+    assert plan.shard_mergeable()
+    assert not engine.plan([AB.terms("t").field("host")]).shard_mergeable()
+    segs = [engine.synthetic_segment(n, fields=fields, shard=s) for s in range(3)]
+    for s in segs:
+        plan.collect(s)
+    assert_same(reduce([plan.build()]).to_dict(), want["reduced"], "merged shards")
+    plan.close()
+    for s in segs:
+        s.close()
