@@ -26,6 +26,12 @@ for s in $STEPS; do
         tests) run pytest_gpu 1100 python3 -u -m pytest "$R/tests" -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         kbench) run kbench 600 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 ${KBENCH_ONLY:+--only $KBENCH_ONLY} ;;
         bench) run bench 600 python3 "$R/bench.py" ;;
+        configs) # every BASELINE config at its own shape (1 GPU: the 8 shards of configs 3-5 collected in turn)
+              run bench_config2 300 python3 "$R/bench.py" --workload config2 --docs 100000000 --cpu-docs 160000000 &&
+              run bench_config3 300 python3 "$R/bench.py" --workload config3 --shards 8 --docs 125000000 --cpu-docs 320000000 &&
+              run bench_config4 300 python3 "$R/bench.py" --workload config4 --shards 8 --docs 125000000 --cpu-docs 320000000 &&
+              run bench_config5 300 python3 "$R/bench.py" --workload config5 --shards 8 --docs 125000000 --cpu-docs 320000000 &&
+              run bench_ns_shards8 300 python3 "$R/bench.py" --shards 8 --docs 125000000 --cpu-docs 0 ;;
         prof) cd /tmp && run rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
                   python3 "$R/bench.py" --steps 10 --warmup 3 --cpu-docs 0 --inflight 1 ;;
         profk) cd /tmp && run rocprof_kbench 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profk" -o kbench -- \
