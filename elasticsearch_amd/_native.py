@@ -28,6 +28,7 @@ AGG_TERMS, AGG_HISTOGRAM, AGG_DATE_HISTOGRAM, AGG_STATS, AGG_EXTENDED_STATS, AGG
 AGG_SUM, AGG_MIN, AGG_MAX, AGG_VALUE_COUNT, AGG_FILTER = 8, 9, 10, 11, 12
 ORDER_COUNT_DESC, ORDER_COUNT_ASC, ORDER_TERM_ASC, ORDER_TERM_DESC = 0, 1, 2, 3
 ORDER_KEY_ASC, ORDER_KEY_DESC, ORDER_HCOUNT_ASC, ORDER_HCOUNT_DESC = 4, 5, 6, 7
+ORDER_AGG_ASC, ORDER_AGG_DESC = 8, 9
 UNIT_NONE, UNIT_WEEK, UNIT_YEAR, UNIT_QUARTER, UNIT_MONTH, UNIT_DAY, UNIT_HOUR, UNIT_MINUTE, UNIT_SECOND = range(9)
 FILTER_TERM, FILTER_RANGE = 1, 2
 COMM_ID_BYTES = 128
@@ -53,7 +54,7 @@ class AggSpec(ctypes.Structure):
         ("extended_bounds_min", ctypes.c_int64), ("extended_bounds_max", ctypes.c_int64),
         ("sigma", ctypes.c_double), ("precision_threshold", ctypes.c_int64),
         ("tz_starts", ctypes.POINTER(ctypes.c_int64)), ("tz_offsets_ms", ctypes.POINTER(ctypes.c_int64)),
-        ("tz_count", ctypes.c_int32), ("reserved_tz", ctypes.c_int32),
+        ("tz_count", ctypes.c_int32), ("reserved_tz", ctypes.c_int32), ("order_path", ctypes.c_char_p),
     ]
 
 
@@ -91,6 +92,7 @@ AggBlock._fields_ = [
     ("hll_present", ctypes.POINTER(_I32)), ("hll_mode", ctypes.POINTER(_I32)),
     ("registers", ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8))),
     ("lc_hashes", ctypes.POINTER(ctypes.POINTER(ctypes.c_uint32))), ("lc_sizes", ctypes.POINTER(_I64)),
+    ("order_path", ctypes.c_char_p),
 ]
 
 

@@ -109,6 +109,18 @@ def tz_history(name, first_year=1900, last_year=2100):
     return tuple(starts), tuple(offs)
 
 
+class AggOrder:
+    def __init__(self, path, asc):
+        self.path, self.asc = path, bool(asc)
+
+
+def order_code(o):
+    """-> (ESGPU_ORDER_*, order path or None)"""
+    if isinstance(o, AggOrder):
+        return (N.ORDER_AGG_ASC if o.asc else N.ORDER_AGG_DESC), o.path
+    return o, None
+
+
 class Order:
     """Terms.Order (InternalOrder.java) and Histogram.Order."""
 
@@ -119,6 +131,11 @@ class Order:
     @staticmethod
     def term(asc):
         return N.ORDER_TERM_ASC if asc else N.ORDER_TERM_DESC
+
+    @staticmethod
+    def aggregation(path, asc):
+        """Terms.Order.aggregation: order by a metric sub-aggregation, "avg_rt" or "rt.max" (InternalOrder.Aggregation)."""
+        return AggOrder(path, asc)
 
     KEY_ASC = N.ORDER_KEY_ASC
     KEY_DESC = N.ORDER_KEY_DESC
@@ -417,9 +434,12 @@ def flatten(aggs, number_of_shards=1):
         sp.sigma = 2.0
         sp.precision_threshold = -1
         if b.type == N.AGG_TERMS:
-            size, ssize, mn, smn = thresholds(b._size, b._shard_size, b._min, b._shard_min, b._order, number_of_shards)
+            code, path = order_code(b._order)
+            size, ssize, mn, smn = thresholds(b._size, b._shard_size, b._min, b._shard_min, code, number_of_shards)
             sp.size, sp.shard_size, sp.min_doc_count, sp.shard_min_doc_count = size, ssize, mn, smn
-            sp.order = b._order
+            sp.order = code
+            if path is not None:
+                sp.order_path = enc(path)
             sp.show_term_doc_count_error = int(b._show_err)
         elif b.type in (N.AGG_HISTOGRAM, N.AGG_DATE_HISTOGRAM):
             unit, interval, off, zone = _rounding_params(b)

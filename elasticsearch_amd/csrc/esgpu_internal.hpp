@@ -115,6 +115,15 @@ struct PinnedBuf {
     PinnedBuf() = default;
     PinnedBuf(const PinnedBuf&) = delete;
     PinnedBuf& operator=(const PinnedBuf&) = delete;
+    PinnedBuf(PinnedBuf&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+    PinnedBuf& operator=(PinnedBuf&& o) noexcept {
+        if (this != &o) {
+            if (p) (void)hipHostFree(p);
+            p = o.p; bytes = o.bytes;
+            o.p = nullptr; o.bytes = 0;
+        }
+        return *this;
+    }
     ~PinnedBuf() { if (p) (void)hipHostFree(p); }
     void* ensure(size_t n) {
         if (n <= bytes) return p;

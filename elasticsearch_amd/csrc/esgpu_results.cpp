@@ -47,6 +47,50 @@ static inline int64_t jround(double a) {
 }
 static inline int64_t fdiv(int64_t a, int64_t b) { return a < 0 ? (a - b + 1) / b : a / b; }
 
+bool parse_order_path(const std::string& path, std::string* name, std::string* key) {  // AggregationPath.java:68-113
+    if (path.empty() || path.find('>') != std::string::npos) return false;
+    const size_t br = path.rfind('[');
+    if (br != std::string::npos) {
+        if (br == 0 || br > path.size() - 3 || path.back() != ']') return false;
+        *name = path.substr(0, br);
+        *key = path.substr(br + 1, path.size() - br - 2);
+        return true;
+    }
+    const size_t dot = path.rfind('.');
+    if (dot == std::string::npos) { *name = path; key->clear(); return true; }
+    if (dot == 0 || dot > path.size() - 2) return false;
+    *name = path.substr(0, dot);
+    *key = path.substr(dot + 1);
+    return true;
+}
+
+bool metric_value(int type, const std::string& key, int64_t count, double sum, double min, double max, double sumsq,
+                  double sigma, double* out) {
+    const double avg = sum / (double)count;
+    if (type == ESGPU_AGG_AVG) {
+        if (!key.empty() && key != "value") return false;
+        *out = avg;
+        return true;
+    }
+    if (key == "count") *out = (double)count;
+    else if (key == "sum") *out = sum;
+    else if (key == "min") *out = min;
+    else if (key == "max") *out = max;
+    else if (key == "avg") *out = avg;
+    else if (type == ESGPU_AGG_EXTENDED_STATS) {  // InternalExtendedStats.value / ExtendedStatsAggregator.metric
+        const double variance = (sumsq - ((sum * sum) / (double)count)) / (double)count;
+        if (key == "sum_of_squares") *out = sumsq;
+        else if (key == "variance") *out = variance;
+        else if (key == "std_deviation") *out = std::sqrt(variance);
+        else if (key == "std_upper") *out = avg + (std::sqrt(variance) * sigma);
+        else if (key == "std_lower") *out = avg - (std::sqrt(variance) * sigma);
+        else return false;
+    } else {
+        return false;
+    }
+    return true;
+}
+
 // EmptyBucketInfo.rounding (InternalHistogram.java:395-449): the spec's Rounding, time zone included
 Rounding Block::rounding() const {
     esgpu_agg_spec sp{};
@@ -187,7 +231,7 @@ Block Block::like() const {
     b.has_empty_info = has_empty_info; b.date_unit = date_unit; b.interval = interval; b.offset = offset;
     b.tz_starts = tz_starts; b.tz_offs = tz_offs;
     b.has_bmin = has_bmin; b.has_bmax = has_bmax; b.bmin = bmin; b.bmax = bmax;
-    b.sigma = sigma; b.precision = precision;
+    b.sigma = sigma; b.precision = precision; b.order_path = order_path;
     b.n = 0;
     if (is_bucket()) {
         b.boff.assign(1, 0);
@@ -306,9 +350,11 @@ struct OutBucket {
     int64_t err;
     uint32_t c0, c1;
     bool empty;
+    uint32_t val = 0;  // terms ordered by a sub-aggregation: index of the bucket's value
 };
 
 struct Scratch {
+    std::vector<double> vals;
     std::vector<Ref> contrib;
     std::vector<OutBucket> buckets, filled;
     std::vector<uint32_t> ids, start;
@@ -394,7 +440,41 @@ void reduce_terms(const Ref* refs, size_t nrefs, Block& out, Scratch& sc, std::v
     }
     sc.buckets.resize(m);
     const size_t size = std::min<size_t>((size_t)std::max(out.required_size, 0), nb);
+    // InternalOrder.Aggregation: the reduced sub-aggregation's value (AggregationPath.resolveValue on the reduced
+    // bucket), from the metric partials of the bucket's contributions reduced in shard order
+    const bool agg_order = out.order == ESGPU_ORDER_AGG_ASC || out.order == ESGPU_ORDER_AGG_DESC;
+    std::vector<double>& vals = sc.vals;
+    if (agg_order) {
+        std::string name, key;
+        int j = -1;
+        if (parse_order_path(out.order_path, &name, &key))
+            for (size_t x = 0; x < out.subs.size(); ++x) if (out.subs[x].name == name) j = (int)x;
+        if (j < 0) throw std::invalid_argument("Invalid order path [" + out.order_path + "]");
+        vals.resize(sc.buckets.size());
+        for (size_t b = 0; b < sc.buckets.size(); ++b) {
+            const OutBucket& ob = sc.buckets[b];
+            int64_t cnt = 0;
+            double sum = 0, mn = INFINITY, mx = -INFINITY, sq = 0;
+            for (uint32_t c = ob.c0; c < ob.c1; ++c) {
+                const Block& m = sc.contrib[c].b->subs[j];
+                const uint64_t i = sc.contrib[c].i;
+                cnt += m.count[i];
+                sum += m.sum[i];
+                mn = jmin(mn, m.min[i]);
+                mx = jmax(mx, m.max[i]);
+                sq += m.sumsq[i];
+            }
+            if (!metric_value(out.subs[j].type, key, cnt, sum, mn, mx, sq, out.subs[j].sigma, &vals[b]))
+                throw std::invalid_argument("Invalid order path [" + out.order_path + "]");
+            sc.buckets[b].val = (uint32_t)b;
+        }
+    }
     auto less = [&](const OutBucket& a, const OutBucket& b) {
+        if (agg_order) {
+            const int c = compare_discard_nan(vals[a.val], vals[b.val], out.order == ESGPU_ORDER_AGG_ASC);
+            if (c != 0) return c < 0;
+            return term_of(*a.tb, a.tk).compare(term_of(*b.tb, b.tk)) < 0;
+        }
         return cmp_terms(out.order, a.count, b.count, term_of(*a.tb, a.tk), term_of(*b.tb, b.tk)) < 0;
     };
     if (sc.buckets.size() > size) {
@@ -815,7 +895,7 @@ void w_block(W& w, const Block& a) {
     w.pod<uint8_t>(a.has_empty_info); w.pod(a.date_unit); w.pod(a.interval); w.pod(a.offset);
     w.vec(a.tz_starts); w.vec(a.tz_offs);
     w.pod<uint8_t>(a.has_bmin); w.pod<uint8_t>(a.has_bmax); w.pod(a.bmin); w.pod(a.bmax);
-    w.pod(a.sigma); w.pod(a.precision); w.pod(a.n);
+    w.pod(a.sigma); w.pod(a.precision); w.str(a.order_path); w.pod(a.n);
     w.vec(a.doc_count_error); w.vec(a.other_doc_count); w.vec(a.boff); w.vec(a.key); w.vec(a.term_off);
     w.str(a.term_pool); w.vec(a.bcount); w.vec(a.berr);
     w_blocks(w, a.subs);
@@ -842,7 +922,7 @@ void r_block(R& r, Block& a, int depth) {
     r.vec(a.tz_starts); r.vec(a.tz_offs);
     if (a.tz_starts.size() != a.tz_offs.size()) throw std::runtime_error("bad time zone table");
     a.has_bmin = r.pod<uint8_t>(); a.has_bmax = r.pod<uint8_t>(); a.bmin = r.pod<int64_t>(); a.bmax = r.pod<int64_t>();
-    a.sigma = r.pod<double>(); a.precision = r.pod<int32_t>(); a.n = r.pod<uint64_t>();
+    a.sigma = r.pod<double>(); a.precision = r.pod<int32_t>(); a.order_path = r.str(); a.n = r.pod<uint64_t>();
     r.vec(a.doc_count_error); r.vec(a.other_doc_count); r.vec(a.boff); r.vec(a.key); r.vec(a.term_off);
     a.term_pool = r.str(); r.vec(a.bcount); r.vec(a.berr);
     r_blocks(r, a.subs, depth + 1);
@@ -898,7 +978,7 @@ void r_blocks(R& r, std::vector<Block>& l, int depth) {
     for (Block& a : l) r_block(r, a, depth);
 }
 const uint32_t kStreamMagic = 0x45534750;  // "ESGP"
-const uint32_t kStreamVersion = 3;
+const uint32_t kStreamVersion = 4;
 }  // namespace
 
 void serialize(const std::vector<Block>& aggs, std::string& out) {
@@ -948,6 +1028,7 @@ void export_block(ResultHolder& h, const Block& a, esgpu_agg_block& o) {
     o.extended_bounds_max = a.bmax;
     o.sigma = a.sigma;
     o.precision = a.precision;
+    o.order_path = a.order_path.c_str();
     o.nsubs = (int32_t)a.subs.size();
     o.n_instances = a.n;
     o.doc_count_error = ptr(a.doc_count_error);

@@ -38,6 +38,7 @@ struct Block {
     int64_t bmin = 0, bmax = 0;
     double sigma = 2.0;
     int32_t precision = 14;
+    std::string order_path;  // terms ordered by a metric sub-aggregation (ESGPU_ORDER_AGG_*)
 
     uint64_t n = 0;  // instances
 
@@ -76,6 +77,28 @@ struct Block {
     void append_empty();
 };
 
+
+// ---- terms ordered by a metric sub-aggregation (InternalOrder.Aggregation) ----
+// AggregationPath.parse of a one-element path: "name", "name.key" or "name[key]" (key empty when absent)
+bool parse_order_path(const std::string& path, std::string* name, std::string* key);
+// the metric the path's key names, with Java double arithmetic: InternalAvg.value / InternalStats.value(name) /
+// InternalExtendedStats.value(name), equal to the shard-level AvgAggregator.metric / StatsAggegator.metric /
+// ExtendedStatsAggregator.metric(name, bucket); returns false for a key the metric does not have
+bool metric_value(int type, const std::string& key, int64_t count, double sum, double min, double max, double sumsq,
+                  double sigma, double* out);
+// Comparators.compareDiscardNaN: NaN sorts last in both directions
+inline int compare_discard_nan(double a, double b, bool asc) {
+    if (a != a) return b != b ? 0 : 1;
+    if (b != b) return -1;
+    const int c = a < b ? -1 : a > b ? 1 : 0;  // Double.compare on non-NaN values, except -0.0 vs 0.0 below
+    if (c != 0) return asc ? c : -c;
+    if (a == 0.0 && b == 0.0) {  // Double.compare orders -0.0 before 0.0
+        const bool na = __builtin_signbit(a), nb = __builtin_signbit(b);
+        const int z = na == nb ? 0 : (na ? -1 : 1);
+        return asc ? z : -z;
+    }
+    return 0;
+}
 
 // HyperLogLogPlusPlus
 int hll_precision_from_threshold(int64_t count);

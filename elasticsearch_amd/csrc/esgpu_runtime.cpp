@@ -713,6 +713,9 @@ static bool is_metric(int t) { return t == ESGPU_AGG_STATS || t == ESGPU_AGG_EXT
 struct SpecNode {
     esgpu_agg_spec s;
     std::string name, field;
+    std::string order_path;            // terms ordered by a sub-aggregation: the path, its child spec and metric key
+    int order_child = -1;
+    std::string order_key;
     std::vector<int> children;
     int precision = 14;
     std::vector<int64_t> tz_starts, tz_offs;  // owned copy of the spec's time zone table
@@ -737,7 +740,17 @@ struct CardState {
     std::vector<uint32_t> h_sets, h_cnt, h_nz;
 };
 
-// One top-level aggregation subtree compiled to one kernel pipeline.
+// host views of one pipeline's cells (its pinned staging buffers), gathered rows or the whole grid
+struct HostCells {
+    const unsigned long long* cnt = nullptr;
+    const unsigned long long* vcnt = nullptr;
+    const unsigned long long* mn = nullptr;
+    const unsigned long long* mx = nullptr;
+    const double* sum = nullptr;
+    const double* sq = nullptr;
+};
+
+// One cell grid ([H][T]: outer / inner bucket dimensions) with its leaf metrics, collected by one kernel launch.
 struct Pipeline {
     int root = -1;             // spec index of the top-level aggregation (for a filter's children: the child)
     int kind = 0;              // 0 = cell grid (bucket / metric), 1 = cardinality
@@ -783,6 +796,30 @@ struct Pipeline {
     bool timed = false;
     uint64_t occ_key = ~0ull;   // cached occupancy of the last launch configuration
     int occ = 1;
+    // build: the pipeline's cells on the host (gathered winner rows or the whole grid) and their staging buffers
+    HostCells hc;
+    PinnedBuf h_cells[6], h_ocnt;
+    Scratch d_rows[6];
+};
+
+// One aggregation subtree (a top-level aggregation, or a child of a top-level filter aggregation) compiled to one or
+// more pipelines.  A bucket aggregation's children are split over pipelines so that each pipeline's grid has at most
+// one inner bucket dimension and one metric field: its metric children grouped by field, each bucket child (with its
+// own metric children grouped by field) in pipelines of its own -- the way AggregatorFactories.createSubAggregators
+// (A/AggregatorFactories.java:68-79) gives every child its own aggregator behind BucketCollector.wrap
+// (A/BucketCollector.java:59).  Every pipeline counts the outer buckets alike; pipes[0]'s counts pick the buckets.
+struct LeafRef { int pipe = -1, leaf = -1; };  // a metric / cardinality spec: its pipeline and index in pl.metrics
+struct ChildSrc {
+    int spec = -1;
+    bool bucket = false;
+    LeafRef leaf;                    // metric / cardinality child
+    std::vector<int> pipes;          // bucket child: pipelines carrying it (pipes[0]'s counts define its buckets)
+    std::vector<LeafRef> grand;      // bucket child: its children in request order
+};
+struct Group {
+    int root = -1, fspec = -1;
+    std::vector<int> pipes;          // pipes[0] holds the outer doc counts
+    std::vector<ChildSrc> kids;      // bucket root: its children in request order
 };
 
 struct esgpu_plan {
@@ -796,6 +833,7 @@ struct esgpu_plan {
     std::vector<std::string> filter_lo, filter_hi;  // owned copies of keyword range bounds (the caller's may not outlive create)
     std::vector<int> tops;                     // top-level spec indices in request order
     std::vector<Pipeline> pipes;
+    std::vector<Group> groups;                 // top-level subtrees (and filter aggregations' children) in request order
     bool collected = false, posted = false;
     double last_ms = 0;
     uint64_t last_bytes = 0;
@@ -804,6 +842,7 @@ struct esgpu_plan {
     Scratch s_accept, s_tcnt, s_rows, s_dst[6];
     Scratch s_wgc, s_pbeg, s_pbuf, s_tiles, s_cand, s_keys, s_hist;  // partitioned counting + GPU top-k
     Scratch s_fbits, s_vbits;  // doc bitset of multi-valued filters, per-value bitset of a multi-valued HLL field
+    Scratch s_cells;           // cell list of a cardinality gather
     PinnedBuf h_keys;
     hipEvent_t ev_mid = nullptr;
     PinnedBuf h_tcnt, h_rows, h_dst[6];
@@ -813,6 +852,137 @@ static int metric_level(int t) { return t == ESGPU_AGG_AVG ? 1 : t == ESGPU_AGG_
 
 static int64_t key_value(const Pipeline& pl, uint32_t slot) {
     return pl.ktable ? pl.kt_key[slot] : (pl.key0 + (int64_t)slot) * pl.interval + pl.offset;
+}
+
+// a pipeline over the outer (and optional inner) bucket spec with the given leaves (metric specs of one field and/or
+// cardinality specs), appended to p->pipes; returns its index
+static int add_pipeline(esgpu_plan* p, int root, int fspec, int outer, int inner, const std::vector<int>& leaves) {
+    Pipeline pl;
+    pl.root = root;
+    pl.fspec = fspec;
+    pl.outer = outer;
+    pl.inner = inner;
+    pl.metrics = leaves;
+    for (int b : {outer, inner}) {
+        if (b < 0) continue;
+        const SpecNode& n = p->specs[b];
+        if (n.s.type == ESGPU_AGG_TERMS) { pl.term_spec = b; pl.ord_field = n.field; }
+        else {
+            pl.hist_spec = b;
+            pl.hist_field = n.field;
+            try {
+                pl.rnd = n.rounding();
+            } catch (const std::invalid_argument& e) {
+                throw EsError(ESGPU_ERR_INVALID, std::string(e.what()) + " for histogram aggregation [" + n.name + "]");
+            }
+            pl.ktable = !pl.rnd.affine(&pl.interval, &pl.offset);
+        }
+    }
+    for (int m : leaves) {
+        const SpecNode& n = p->specs[m];
+        if (n.s.type == ESGPU_AGG_CARDINALITY) {
+            CardState cs;
+            cs.spec = m;
+            cs.p = n.precision;
+            cs.field = n.field;
+            cs.m = 1u << cs.p;
+            cs.thr = (uint32_t)((float)(cs.m / 4) * 0.75f);  // Hashset threshold (HyperLogLogPlusPlus.java:437-440)
+            cs.cap = 16;
+            while (cs.cap < 4 * (cs.thr + 1)) cs.cap <<= 1;
+            pl.cards.push_back(std::move(cs));
+            continue;
+        }
+        if (pl.metric_field.empty()) pl.metric_field = n.field;
+        pl.met = std::max(pl.met, metric_level(n.s.type));
+    }
+    p->pipes.push_back(std::move(pl));
+    return (int)p->pipes.size() - 1;
+}
+
+// leaves grouped into pipelines: one per metric field (first-appearance order), cardinality leaves with the first;
+// `refs` gets each leaf's (pipeline, index); a bucket with no leaves still gets one pipeline for its counts
+static std::vector<int> add_leaf_pipelines(esgpu_plan* p, int root, int fspec, int outer, int inner, const std::vector<int>& leaves,
+                                           std::vector<LeafRef>* refs) {
+    std::vector<std::string> fields;
+    std::vector<std::vector<int>> by;
+    std::vector<int> cards;
+    for (int m : leaves) {
+        if (p->specs[m].s.type == ESGPU_AGG_CARDINALITY) { cards.push_back(m); continue; }
+        const std::string& f = p->specs[m].field;
+        size_t k = std::find(fields.begin(), fields.end(), f) - fields.begin();
+        if (k == fields.size()) { fields.push_back(f); by.emplace_back(); }
+        by[k].push_back(m);
+    }
+    if (by.empty()) by.emplace_back();
+    by[0].insert(by[0].end(), cards.begin(), cards.end());
+    std::vector<int> idx;
+    for (const auto& g : by) idx.push_back(add_pipeline(p, root, fspec, outer, inner, g));
+    refs->assign(leaves.size(), LeafRef{});
+    for (size_t j = 0; j < leaves.size(); ++j)
+        for (int pi : idx) {
+            const auto& ms = p->pipes[pi].metrics;
+            const auto it = std::find(ms.begin(), ms.end(), leaves[j]);
+            if (it != ms.end()) (*refs)[j] = LeafRef{pi, (int)(it - ms.begin())};
+        }
+    return idx;
+}
+
+static Group compile_group(esgpu_plan* p, int r, int fspec) {
+    Group g;
+    g.root = r;
+    g.fspec = fspec;
+    const SpecNode& root = p->specs[r];
+    if (root.s.type == ESGPU_AGG_CARDINALITY) {
+        Pipeline pl;
+        pl.root = r;
+        pl.fspec = fspec;
+        pl.kind = 1;
+        pl.p = root.precision;
+        pl.metric_field = root.field;
+        p->pipes.push_back(std::move(pl));
+        g.pipes.push_back((int)p->pipes.size() - 1);
+        return g;
+    }
+    if (is_metric(root.s.type)) {
+        g.pipes.push_back(add_pipeline(p, r, fspec, -1, -1, {r}));
+        return g;
+    }
+    require(is_bucket(root.s.type), ESGPU_ERR_UNSUPPORTED, "aggregation type not on the GPU path");
+    std::vector<int> leaves;
+    for (int ch : root.children) {
+        const int t = p->specs[ch].s.type;
+        if (is_metric(t) || t == ESGPU_AGG_CARDINALITY) leaves.push_back(ch);
+        else if (!is_bucket(t)) throw EsError(ESGPU_ERR_UNSUPPORTED, "aggregation type not on the GPU path");
+    }
+    std::vector<LeafRef> leaf_refs;
+    bool have_bucket_child = false;
+    for (int ch : root.children) have_bucket_child |= is_bucket(p->specs[ch].s.type);
+    if (!leaves.empty() || !have_bucket_child)  // the outer level's own pipelines (also: a bucket with no children)
+        for (int pi : add_leaf_pipelines(p, r, fspec, r, -1, leaves, &leaf_refs)) g.pipes.push_back(pi);
+    size_t li = 0;
+    for (int ch : root.children) {
+        ChildSrc cs;
+        cs.spec = ch;
+        if (!is_bucket(p->specs[ch].s.type)) {
+            cs.leaf = leaf_refs[li++];
+        } else {
+            cs.bucket = true;
+            const bool ot = root.s.type == ESGPU_AGG_TERMS, it = p->specs[ch].s.type == ESGPU_AGG_TERMS;
+            require(ot != it, ESGPU_ERR_UNSUPPORTED, "terms-under-terms and histogram-under-histogram");
+            std::vector<int> inner_leaves;
+            for (int gc : p->specs[ch].children) {
+                const int t = p->specs[gc].s.type;
+                require(is_metric(t) || t == ESGPU_AGG_CARDINALITY, ESGPU_ERR_UNSUPPORTED, "bucket aggregations nested three levels deep");
+                inner_leaves.push_back(gc);
+            }
+            cs.pipes = add_leaf_pipelines(p, r, fspec, r, ch, inner_leaves, &cs.grand);
+            for (int pi : cs.pipes) g.pipes.push_back(pi);
+        }
+        g.kids.push_back(std::move(cs));
+    }
+    // a terms aggregation ordered by a metric child: that child's pipeline must hold the selection (it is a direct
+    // child, so its pipeline is an outer-level one)
+    return g;
 }
 
 extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int32_t nspecs, const esgpu_filter* filters,
@@ -854,9 +1024,15 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
             if (n.s.type == ESGPU_AGG_TERMS) {
                 require(n.s.size >= 0 && n.s.min_doc_count >= 0, ESGPU_ERR_INVALID,
                         "parameters [requiredSize] and [minDocCount] must be >=0 in terms aggregation.");
-                require(n.s.order >= ESGPU_ORDER_COUNT_DESC && n.s.order <= ESGPU_ORDER_TERM_DESC, ESGPU_ERR_UNSUPPORTED,
-                        "terms order by sub-aggregation runs on the CPU path");
+                require((n.s.order >= ESGPU_ORDER_COUNT_DESC && n.s.order <= ESGPU_ORDER_TERM_DESC) ||
+                            n.s.order == ESGPU_ORDER_AGG_ASC || n.s.order == ESGPU_ORDER_AGG_DESC,
+                        ESGPU_ERR_INVALID, "unknown terms order");
+                if (n.s.order == ESGPU_ORDER_AGG_ASC || n.s.order == ESGPU_ORDER_AGG_DESC) {
+                    require(specs[i].order_path != nullptr, ESGPU_ERR_INVALID, "terms order by sub-aggregation without a path");
+                    n.order_path = specs[i].order_path;
+                }
             }
+            n.s.order_path = nullptr;
             if (n.s.type == ESGPU_AGG_CARDINALITY) {
                 if (n.s.precision_threshold >= 0) n.precision = hll_precision_from_threshold(n.s.precision_threshold);
                 else {
@@ -895,90 +1071,43 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
                 require(p->specs[ch].s.type != ESGPU_AGG_FILTER, ESGPU_ERR_UNSUPPORTED, "nested filter aggregations");
         }
         p->tops = tops;
-        // compile each top-level subtree into a pipeline; a filter aggregation (FilterAggregator) becomes one
-        // counting pipeline for its doc_count plus one pipeline per sub-aggregation, all under its clauses
-        auto compile = [&](int r, int fspec) {
-            Pipeline pl;
-            pl.root = r;
-            pl.fspec = fspec;
-            const SpecNode& root = p->specs[r];
-            if (root.s.type == ESGPU_AGG_CARDINALITY) {
-                pl.kind = 1;
-                pl.p = root.precision;
-                pl.metric_field = root.field;
-                p->pipes.push_back(std::move(pl));
-                return;
-            }
-            if (is_metric(root.s.type)) {
-                pl.metrics.push_back(r);
+        // terms ordered by a sub-aggregation: AggregationPath.validate (A/support/AggregationPath.java:289-347)
+        for (SpecNode& n : p->specs) {
+            if (n.s.type != ESGPU_AGG_TERMS || (n.s.order != ESGPU_ORDER_AGG_ASC && n.s.order != ESGPU_ORDER_AGG_DESC)) continue;
+            std::string name, key;
+            require(parse_order_path(n.order_path, &name, &key), ESGPU_ERR_INVALID,
+                    "Invalid path element in path [" + n.order_path + "]");
+            for (int ch : n.children) if (p->specs[ch].name == name) n.order_child = ch;
+            require(n.order_child >= 0, ESGPU_ERR_INVALID, "Invalid term-aggregator order path [" + n.order_path +
+                    "]. Unknown aggregation [" + name + "]");
+            const int t = p->specs[n.order_child].s.type;
+            require(t != ESGPU_AGG_CARDINALITY, ESGPU_ERR_UNSUPPORTED, "terms ordered by a cardinality runs on the CPU path");
+            require(is_metric(t), ESGPU_ERR_INVALID, "Invalid terms aggregation order path [" + n.order_path +
+                    "]. Terms buckets can only be sorted on a sub-aggregator path that is built out of zero or more "
+                    "single-bucket aggregations within the path and a final single-bucket or a metrics aggregation at the path end.");
+            double probe;
+            if (t == ESGPU_AGG_AVG) {
+                require(key.empty() || key == "value", ESGPU_ERR_INVALID, "Invalid terms aggregation order path [" + n.order_path +
+                        "]. Ordering on a single-value metrics aggregation can only be done on its value.");
             } else {
-                pl.outer = r;
-                std::vector<int> mets, buckets;
-                for (int ch : root.children) {
-                    const int t = p->specs[ch].s.type;
-                    if (is_metric(t) || t == ESGPU_AGG_CARDINALITY) mets.push_back(ch);
-                    else if (is_bucket(t)) buckets.push_back(ch);
-                    else throw EsError(ESGPU_ERR_UNSUPPORTED, "aggregation type not on the GPU path");
-                }
-                require(buckets.size() <= 1, ESGPU_ERR_UNSUPPORTED, "more than one bucket sub-aggregation");
-                if (!buckets.empty()) {
-                    require(mets.empty(), ESGPU_ERR_UNSUPPORTED, "metrics beside a bucket sub-aggregation");
-                    pl.inner = buckets[0];
-                    for (int ch : p->specs[pl.inner].children) {
-                        const int t = p->specs[ch].s.type;
-                        require(is_metric(t) || t == ESGPU_AGG_CARDINALITY, ESGPU_ERR_UNSUPPORTED,
-                                "bucket aggregations nested three levels deep");
-                        mets.push_back(ch);
-                    }
-                    const bool ot = p->specs[pl.outer].s.type == ESGPU_AGG_TERMS;
-                    const bool it = p->specs[pl.inner].s.type == ESGPU_AGG_TERMS;
-                    require(ot != it, ESGPU_ERR_UNSUPPORTED, "terms-under-terms and histogram-under-histogram");
-                }
-                pl.metrics = mets;
+                require(!key.empty(), ESGPU_ERR_INVALID, "Invalid terms aggregation order path [" + n.order_path +
+                        "]. When ordering on a multi-value metrics aggregation a metric name must be specified");
+                require(metric_value(t, key, 1, 0, 0, 0, 0, 2.0, &probe), ESGPU_ERR_INVALID, "Invalid terms aggregation order path [" +
+                        n.order_path + "]. Unknown metric name [" + key + "] on multi-value metrics aggregation [" + name + "]");
             }
-            for (int b : {pl.outer, pl.inner}) {
-                if (b < 0) continue;
-                const SpecNode& n = p->specs[b];
-                if (n.s.type == ESGPU_AGG_TERMS) { pl.term_spec = b; pl.ord_field = n.field; }
-                else {
-                    pl.hist_spec = b;
-                    pl.hist_field = n.field;
-                    try {
-                        pl.rnd = n.rounding();
-                    } catch (const std::invalid_argument& e) {
-                        throw EsError(ESGPU_ERR_INVALID, std::string(e.what()) + " for histogram aggregation [" + n.name + "]");
-                    }
-                    pl.ktable = !pl.rnd.affine(&pl.interval, &pl.offset);
-                }
-            }
-            for (int m : pl.metrics) {
-                const SpecNode& n = p->specs[m];
-                if (n.s.type == ESGPU_AGG_CARDINALITY) {
-                    CardState cs;
-                    cs.spec = m;
-                    cs.p = n.precision;
-                    cs.field = n.field;
-                    cs.m = 1u << cs.p;
-                    cs.thr = (uint32_t)((float)(cs.m / 4) * 0.75f);  // Hashset threshold (HyperLogLogPlusPlus.java:437-440)
-                    cs.cap = 16;
-                    while (cs.cap < 4 * (cs.thr + 1)) cs.cap <<= 1;
-                    pl.cards.push_back(std::move(cs));
-                    continue;
-                }
-                if (pl.metric_field.empty()) pl.metric_field = n.field;
-                require(pl.metric_field == n.field, ESGPU_ERR_UNSUPPORTED, "metrics on different fields at one level");
-                pl.met = std::max(pl.met, metric_level(n.s.type));
-            }
-            p->pipes.push_back(std::move(pl));
-        };
+            n.order_key = key;
+        }
+        // compile each top-level subtree into a group of pipelines (one cell grid each, one kernel launch each);
+        // a filter aggregation (FilterAggregator) becomes one counting pipeline for its doc_count plus one group per
+        // sub-aggregation, all under its clauses
         for (int r : tops) {
-            if (p->specs[r].s.type != ESGPU_AGG_FILTER) { compile(r, -1); continue; }
+            if (p->specs[r].s.type != ESGPU_AGG_FILTER) { p->groups.push_back(compile_group(p.get(), r, -1)); continue; }
             Pipeline cnt;
             cnt.root = r;
             cnt.fspec = r;
             cnt.count_only = true;
             p->pipes.push_back(std::move(cnt));
-            for (int ch : p->specs[r].children) compile(ch, r);
+            for (int ch : p->specs[r].children) p->groups.push_back(compile_group(p.get(), ch, r));
         }
         HIPX(hipSetDevice(c->device));
         HIPX(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
@@ -1279,9 +1408,9 @@ static bool collect_multi(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, C
     P.hv_off = (hc && hc->multi) ? hc->offsets.as<uint64_t>() : nullptr;
     P.mv_off = (mc && mc->multi) ? mc->offsets.as<uint64_t>() : nullptr;
     if (P.ocnt_mode == OCNT_TERMS_DERIVED) P.ocnt_mode = OCNT_TERMS;  // outer counts per doc, never from the cells
-    P.W = pl.H;
+    P.W = P.H;
     P.windowed = 0;
-    size_t lds = collect_lds_bytes(pl.T, pl.H, met_launch, pl.vcnt_mode, P.ocnt_mode);
+    size_t lds = collect_lds_bytes(P.T, P.H, met_launch, P.vcnt_mode, P.ocnt_mode);
     P.lds_mode = lds <= 64 * 1024 ? 1 : 0;
     if (!P.lds_mode) lds = 0;
     const uint32_t want = (s->max_doc + 511) / 512;
@@ -1363,12 +1492,13 @@ static void collect_cards(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, c
     HIPX(hipEventRecord(pl.e1, p->stream));
 }
 
-static bool collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept);
+// 0 = nothing collected, 1 = the grid, 2 = only the outer doc counts (the segment lacks the inner dimension's field)
+static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept);
 
 static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
-    const bool done = collect_grid_cells(p, pl, s, d_accept);
-    if (done && !pl.cards.empty()) collect_cards(p, pl, s, d_accept);
-    return done;
+    const int done = collect_grid_cells(p, pl, s, d_accept);
+    if (done == 1 && !pl.cards.empty()) collect_cards(p, pl, s, d_accept);
+    return done != 0;
 }
 
 #ifndef ESGPU_TERMS_COPIES
@@ -1379,13 +1509,17 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
 #endif
 static constexpr uint32_t kTermsCopies = ESGPU_TERMS_COPIES;
 
-static bool collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
+static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
     const bool ORD = pl.term_spec >= 0, HIST = pl.hist_spec >= 0;
     const DevColumn* oc = ORD ? s->col(pl.ord_field.c_str()) : nullptr;
     const DevColumn* hc = HIST ? s->col(pl.hist_field.c_str()) : nullptr;
     const DevColumn* mc = pl.met > 0 ? s->col(pl.metric_field.c_str()) : nullptr;
-    // unmapped fields: a bucket aggregation over a missing field collects nothing (ValuesSource null)
-    if ((ORD && !oc) || (HIST && !hc)) return false;
+    const bool terms_outer = pl.outer == pl.term_spec;
+    // unmapped fields: a bucket aggregation over a missing field collects nothing (ValuesSource null); when only the
+    // inner bucket aggregation's field is missing, the outer buckets still count the segment's docs and the inner
+    // aggregation of those docs is empty
+    const bool inner_missing = ORD && HIST && (terms_outer ? (oc && !hc) : (hc && !oc));
+    if (((ORD && !oc) || (HIST && !hc)) && !inner_missing) return 0;
     if (oc) require(oc->type == ESGPU_COL_ORD_U32, ESGPU_ERR_UNSUPPORTED, "terms on numeric fields run on the CPU path");
     if (hc) require(hc->type == ESGPU_COL_I64 || hc->type == ESGPU_COL_F64, ESGPU_ERR_UNSUPPORTED,
                     "histogram over a keyword field runs on the CPU path");
@@ -1422,11 +1556,10 @@ static bool collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment*
         has_keys = true;
     }
     const bool sparse_metric = pl.met > 0 && (!mc || mc->present.p || mc->multi);
-    const bool terms_outer = pl.outer == pl.term_spec;
     // ords may be missing; a doc may have several keys: then the outer counts cannot be summed from the cells
-    const bool inner_sparse = ORD && HIST && (terms_outer ? (hc->present.p != nullptr || hc->multi) : true);
+    const bool inner_sparse = ORD && HIST && (inner_missing || (terms_outer ? (hc->present.p != nullptr || hc->multi) : true));
     if (!pl.allocated || pl.fresh) {
-        const uint32_t T = ORD ? (uint32_t)std::max<uint64_t>(oc->ord_count(), 1) : 1;
+        const uint32_t T = oc ? (uint32_t)std::max<uint64_t>(oc->ord_count(), 1) : 1;
         const int64_t key0 = has_keys ? kmin : 0;
         require(!HIST || !has_keys || kmax - kmin + 1 <= 64 * 1024 * 1024, ESGPU_ERR_UNSUPPORTED,
                 "histogram key range too large for a dense grid");
@@ -1444,12 +1577,14 @@ static bool collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment*
         pl.vcnt_mode = vcnt;
         pl.ocnt_mode = ocnt;
         pl.keyed = has_keys;
-        pl.value_count = ORD ? oc->ord_count() : 1;
-        pl.tdict = ORD ? oc->ord_dict() : nullptr;
+        pl.value_count = oc ? oc->ord_count() : (ORD ? 0 : 1);
+        pl.tdict = oc ? oc->ord_dict() : nullptr;
         if (!same) alloc_grid(p, pl);
         pl.fresh = false;
     } else {
-        if (ORD) require(same_dict(oc->ord_dict(), pl.tdict), ESGPU_ERR_INVALID,
+        if (oc && !pl.tdict)
+            throw EsError(ESGPU_ERR_UNSUPPORTED, "terms field [" + pl.ord_field + "] unmapped in the first segment under a histogram");
+        if (oc) require(same_dict(oc->ord_dict(), pl.tdict), ESGPU_ERR_INVALID,
                          "segments number the terms of [" + pl.ord_field + "] differently: build an ordinal map "
                          "(esgpu_ordinal_map_build) over the reader's segments first");
         if (HIST && has_keys && !pl.keyed) {
@@ -1475,13 +1610,19 @@ static bool collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment*
         if (inner_sparse && pl.ocnt_mode == OCNT_TERMS_DERIVED) pl.ocnt_mode = OCNT_TERMS;
     }
     // ---- launch configuration ----
+    // what this launch collects: the grid, or -- the segment lacking the inner dimension's field -- only the outer doc
+    // counts, as a one-dimensional grid over g_ocnt
+    const bool L_ORD = ORD && (!inner_missing || terms_outer), L_HIST = HIST && (!inner_missing || !terms_outer);
+    const uint32_t LT = L_ORD ? pl.T : 1, LH = L_HIST ? pl.H : 1;
+    const int L_met = inner_missing ? 0 : met_launch;
+    const int L_vcnt = inner_missing ? 0 : pl.vcnt_mode, L_ocnt = inner_missing ? (int)OCNT_NONE : pl.ocnt_mode;
     CollectParams P{};
     P.n_docs = s->max_doc;
     P.n_blocks = s->n_pad / kBlockDocs;
-    if (P.n_blocks == 0) return false;
+    if (P.n_blocks == 0) return 0;
     P.ord = oc ? oc->ords().as<uint32_t>() : nullptr;
-    P.T = pl.T;
-    P.H = pl.H;
+    P.T = LT;
+    P.H = LH;
     P.hv = hc ? hc->values.as<int64_t>() : nullptr;
     P.hv_present = hc ? hc->present.as<uint64_t>() : nullptr;
     P.hv_f64 = hc && hc->type == ESGPU_COL_F64;
@@ -1496,56 +1637,59 @@ static bool collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment*
     P.mv = mc ? mc->values.p : nullptr;
     P.mv_present = mc ? mc->present.as<uint64_t>() : nullptr;
     P.mv_f64 = mc && mc->type == ESGPU_COL_F64;
-    P.vcnt_mode = pl.vcnt_mode;
-    P.ocnt_mode = pl.ocnt_mode;
+    P.vcnt_mode = L_vcnt;
+    P.ocnt_mode = L_ocnt;
     P.accept = d_accept;
-    uint64_t bytes_per_doc = (oc ? 4 : 0) + (hc ? 8 : 0) + (mc ? 8 : 0);
+    if (inner_missing) { P.mv = nullptr; P.mv_present = nullptr; P.mv_f64 = 0; }
+    uint64_t bytes_per_doc = (oc ? 4 : 0) + (hc ? 8 : 0) + (mc && !inner_missing ? 8 : 0);
     set_preds(p, pl, s, P.pred, &P.npred, &bytes_per_doc);
-    P.g_cnt = pl.g_cnt.as<unsigned long long>();
+    P.g_cnt = inner_missing ? pl.g_ocnt.as<unsigned long long>() : pl.g_cnt.as<unsigned long long>();
     P.g_ocnt = pl.g_ocnt.as<unsigned long long>();
     P.g_vcnt = pl.g_vcnt.as<unsigned long long>();
     P.g_sum = pl.g_sum.as<double>();
     P.g_min = pl.g_min.as<unsigned long long>();
     P.g_max = pl.g_max.as<unsigned long long>();
     P.g_sq = pl.g_sq.as<double>();
-    if (multi) return collect_multi(p, pl, s, P, oc, hc, mc, met_launch, d_accept);
+    const int ret = inner_missing ? 2 : 1;
+    if (multi) return collect_multi(p, pl, s, P, L_ORD ? oc : nullptr, L_HIST ? hc : nullptr, inner_missing ? nullptr : mc, L_met,
+                                    d_accept) ? ret : 0;
 
     // LDS sizing: the whole grid if it fits, else a sliding window over the key dimension (time-sorted data)
     const size_t kLdsPair = 64 * 1024, kLdsMax = 150 * 1024;
-    uint32_t W = pl.H;
-    size_t lds = collect_lds_bytes(pl.T, W, met_launch, pl.vcnt_mode, pl.ocnt_mode);
+    uint32_t W = LH;
+    size_t lds = collect_lds_bytes(LT, W, L_met, L_vcnt, L_ocnt);
     P.lds_mode = 1;
     P.windowed = 0;
     if (lds > kLdsPair) {
-        if (HIST && !P.kslot) {  // the key window needs buckets that rise with the value (zone-map ranges)
-            uint32_t w = pl.H;
-            while (w > 1 && collect_lds_bytes(pl.T, w, met_launch, pl.vcnt_mode, pl.ocnt_mode) > kLdsPair) w = (w + 1) / 2;
-            if (collect_lds_bytes(pl.T, w, met_launch, pl.vcnt_mode, pl.ocnt_mode) > kLdsPair) w = 1;
+        if (L_HIST && !P.kslot) {  // the key window needs buckets that rise with the value (zone-map ranges)
+            uint32_t w = LH;
+            while (w > 1 && collect_lds_bytes(LT, w, L_met, L_vcnt, L_ocnt) > kLdsPair) w = (w + 1) / 2;
+            if (collect_lds_bytes(LT, w, L_met, L_vcnt, L_ocnt) > kLdsPair) w = 1;
             W = w;
             P.windowed = 1;
-            lds = collect_lds_bytes(pl.T, W, met_launch, pl.vcnt_mode, pl.ocnt_mode);
+            lds = collect_lds_bytes(LT, W, L_met, L_vcnt, L_ocnt);
         }
         if (lds > kLdsMax) {
             P.lds_mode = 0;
             P.windowed = 0;
             lds = 0;
-            W = pl.H;
+            W = LH;
         }
     }
     P.W = W;
     // grids with a terms dimension: lane-rotated copies of the additive cells while they still fit two workgroups per
     // CU (the Zipf-head terms otherwise serialise a wave's LDS atomics on one address)
     P.ncopies = 1;
-    if (P.lds_mode && ORD && (!HIST || ESGPU_COPIES_HIST)) {
+    if (P.lds_mode && L_ORD && (!L_HIST || ESGPU_COPIES_HIST)) {
         for (uint32_t nc = kTermsCopies; nc > 1; nc /= 2) {
-            const size_t b = collect_lds_bytes(pl.T, W, met_launch, pl.vcnt_mode, pl.ocnt_mode, nc);
+            const size_t b = collect_lds_bytes(LT, W, L_met, L_vcnt, L_ocnt, nc);
             if (b <= kLdsPair) { P.ncopies = nc; lds = b; break; }
         }
     }
-    if (!P.lds_mode && ORD && !HIST && met_launch == 0 && !pl.vcnt_mode && pl.ocnt_mode == OCNT_NONE &&
+    if (!P.lds_mode && L_ORD && !L_HIST && L_met == 0 && !L_vcnt && L_ocnt == OCNT_NONE && !inner_missing &&
         (((uint64_t)pl.T + (1u << kPartShift) - 1) >> kPartShift) <= kPartMaxStaged) {
         p->last_bytes += bytes_per_doc * (uint64_t)s->max_doc + (d_accept ? ((uint64_t)s->max_doc + 7) / 8 : 0);
-        return collect_partitioned(p, pl, s, oc, d_accept, P.pred, P.npred);
+        return collect_partitioned(p, pl, s, oc, d_accept, P.pred, P.npred) ? 1 : 0;
     }
     const uint64_t span = (uint64_t)pl.interval * (uint64_t)W;
     P.fast32 = !P.kstart && pl.interval < (1ll << 32) && span < (1ull << 32);
@@ -1553,12 +1697,12 @@ static bool collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment*
         const MagicU32 mg = make_magic((uint32_t)pl.interval);
         P.mg_m = mg.m; P.mg_s1 = mg.s1; P.mg_s2 = mg.s2;
     }
-    const int hk = HIST ? (P.kstart ? 2 : 1) : 0;
+    const int hk = L_HIST ? (P.kstart ? 2 : 1) : 0;
     const int vk = (P.hv_f64 ? 1 : 0) | (P.mv_f64 ? 2 : 0);
-    const uint64_t occ_key = ((uint64_t)lds << 10) | ((uint64_t)vk << 8) | ((uint64_t)met_launch << 4) | ((uint64_t)hk << 1) |
-                             (ORD ? 1 : 0);
+    const uint64_t occ_key = ((uint64_t)lds << 10) | ((uint64_t)vk << 8) | ((uint64_t)L_met << 4) | ((uint64_t)hk << 1) |
+                             (L_ORD ? 1 : 0);
     if (pl.occ_key != occ_key) {
-        pl.occ = std::max(1, collect_occupancy(ORD, hk, met_launch, lds, vk));
+        pl.occ = std::max(1, collect_occupancy(L_ORD, hk, L_met, lds, vk));
         pl.occ_key = occ_key;
     }
     const uint32_t wg_per_cu = (uint32_t)pl.occ;
@@ -1571,12 +1715,12 @@ static bool collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment*
     P.blocks_per_wg = std::max(1u, bpw);
     const uint32_t grid = (P.n_blocks + P.blocks_per_wg - 1) / P.blocks_per_wg;
     HIPX(hipEventRecord(pl.e0, p->stream));
-    launch_collect(P, ORD, HIST, met_launch, grid, lds, p->stream);
+    launch_collect(P, L_ORD, L_HIST, L_met, grid, lds, p->stream);
     HIPX(hipGetLastError());
     HIPX(hipEventRecord(pl.e1, p->stream));
     p->last_bytes += bytes_per_doc * (uint64_t)s->max_doc + (d_accept ? ((uint64_t)s->max_doc + 7) / 8 : 0);
     p->last_path = P.lds_mode ? (P.windowed ? 2 : 1) : 0;
-    return true;
+    return ret;
 }
 
 static void ensure_ord_hash(esgpu_ctx* c, const DevColumn* col, hipStream_t st) {
@@ -1821,6 +1965,7 @@ static Block terms_shell(const esgpu_plan* p, int spec, const std::vector<Block>
     r.required_size = n.s.size;
     r.shard_size = n.s.shard_size;
     r.min_doc_count = n.s.min_doc_count;
+    r.order_path = n.order_path;
     r.show_err = n.s.show_term_doc_count_error;
     r.boff.assign(1, 0);
     r.term_off.assign(1, 0);
@@ -1842,16 +1987,6 @@ static void push_bucket(Block& b, int64_t key, const std::string* term, int64_t 
     b.berr.push_back(0);
 }
 
-// host views (pinned staging buffers of the plan) of one grid row set
-struct HostCells {
-    const unsigned long long* cnt = nullptr;
-    const unsigned long long* vcnt = nullptr;
-    const unsigned long long* mn = nullptr;
-    const unsigned long long* mx = nullptr;
-    const double* sum = nullptr;
-    const double* sq = nullptr;
-};
-
 // the cardinality sketches of the given bucket cells, gathered to the host in that order (rows index like HostCells)
 static void gather_cards(esgpu_plan* p, Pipeline& pl, const std::vector<uint32_t>& cells) {
     if (pl.cards.empty()) return;
@@ -1859,7 +1994,7 @@ static void gather_cards(esgpu_plan* p, Pipeline& pl, const std::vector<uint32_t
     const uint32_t n = (uint32_t)cells.size();
     uint32_t* dcells = nullptr;
     if (n) {
-        dcells = (uint32_t*)p->s_rows.ensure(p->ctx, (size_t)n * 4);
+        dcells = (uint32_t*)p->s_cells.ensure(p->ctx, (size_t)n * 4);
         HIPX(hipMemcpyAsync(dcells, cells.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
     }
     for (CardState& cs : pl.cards) {
@@ -1904,70 +2039,107 @@ static void append_card(const CardState& cs, size_t c, Block& r) {
     }
 }
 
-// one instance of every leaf metric of the pipeline, from grid cell c, appended to blocks[0..]
-static void append_metrics(const esgpu_plan* p, const Pipeline& pl, const HostCells& h, size_t c, std::vector<Block>& blocks) {
-    size_t card = 0;
-    for (size_t j = 0; j < pl.metrics.size(); ++j) {
-        const int32_t type = p->specs[pl.metrics[j]].s.type;
-        Block& r = blocks[j];
-        if (type == ESGPU_AGG_CARDINALITY) {
-            append_card(pl.cards[card++], c, r);
-            continue;
+// the numeric partials of leaf j of a pipeline at host cell c: (count, sum, min, max, sum of squares)
+struct MetricCell { int64_t count; double sum, min, max, sq; };
+static MetricCell metric_cell(const esgpu_plan* p, const Pipeline& pl, int j, size_t c) {
+    const int32_t type = p->specs[pl.metrics[j]].s.type;
+    const HostCells& h = pl.hc;
+    const uint64_t vc = pl.vcnt_mode ? h.vcnt[c] : h.cnt[c];
+    MetricCell m{(int64_t)vc, 0.0, INFINITY, -INFINITY, 0.0};
+    if (vc > 0) {
+        m.sum = h.sum[c];
+        if (pl.met >= 2 && type != ESGPU_AGG_AVG) {
+            const uint64_t emn = h.mn[c], emx = h.mx[c];
+            if (emn < kEncNegInf || emx > kEncPosInf) { m.min = NAN; m.max = NAN; }  // a NaN value was collected
+            else { m.min = unsortable(emn); m.max = unsortable(emx); }
         }
-        const uint64_t vc = pl.vcnt_mode ? h.vcnt[c] : h.cnt[c];
-        double sum = 0.0, mn = INFINITY, mx = -INFINITY, sq = 0.0;
-        if (vc > 0) {
-            sum = h.sum[c];
-            if (pl.met >= 2 && type != ESGPU_AGG_AVG) {
-                const uint64_t emn = h.mn[c], emx = h.mx[c];
-                if (emn < kEncNegInf || emx > kEncPosInf) { mn = NAN; mx = NAN; }  // a NaN value was collected
-                else { mn = unsortable(emn); mx = unsortable(emx); }
-            }
-            if (pl.met >= 3 && type == ESGPU_AGG_EXTENDED_STATS) sq = h.sq[c];
-        }
-        ++r.n;
-        r.count.push_back((int64_t)vc);
-        r.sum.push_back(sum);
-        r.min.push_back(mn);
-        r.max.push_back(mx);
-        r.sumsq.push_back(sq);
+        if (pl.met >= 3 && type == ESGPU_AGG_EXTENDED_STATS) m.sq = h.sq[c];
     }
+    return m;
 }
 
-static std::vector<Block> metric_protos(const esgpu_plan* p, const Pipeline& pl) {
-    std::vector<Block> out;
-    for (int m : pl.metrics) {
-        out.push_back(metric_shell(p->specs[m]));
-        if (p->specs[m].s.type == ESGPU_AGG_CARDINALITY) out.back().precision = p->specs[m].precision;
-        out.back().append_empty();
+// one instance of leaf j (metric or cardinality) of a pipeline, from its host cell c
+static void append_leaf(const esgpu_plan* p, const Pipeline& pl, int j, size_t c, Block& r) {
+    if (p->specs[pl.metrics[j]].s.type == ESGPU_AGG_CARDINALITY) {
+        size_t card = 0;
+        for (int q = 0; q < j; ++q) card += p->specs[pl.metrics[q]].s.type == ESGPU_AGG_CARDINALITY;
+        append_card(pl.cards[card], c, r);
+        return;
     }
-    return out;
+    const MetricCell m = metric_cell(p, pl, j, c);
+    ++r.n;
+    r.count.push_back(m.count);
+    r.sum.push_back(m.sum);
+    r.min.push_back(m.min);
+    r.max.push_back(m.max);
+    r.sumsq.push_back(m.sq);
 }
 
-// device cell arrays -> the plan's pinned staging buffers (one stream sync)
-static void d2h(esgpu_plan* p, HostCells& h, const Pipeline& pl, size_t n, const void* cnt, const void* vcnt, const void* sum,
-                const void* mn, const void* mx, const void* sq) {
-    hipStream_t st = p->stream;
-    const void* src[6] = {cnt, pl.vcnt_mode ? vcnt : nullptr, pl.met > 0 ? sum : nullptr, pl.met >= 2 ? mn : nullptr,
-                          pl.met >= 2 ? mx : nullptr, pl.met >= 3 ? sq : nullptr};
-    void* dst[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+static Block leaf_proto(const esgpu_plan* p, int spec) {
+    Block b = metric_shell(p->specs[spec]);
+    if (p->specs[spec].s.type == ESGPU_AGG_CARDINALITY) b.precision = p->specs[spec].precision;
+    b.append_empty();
+    return b;
+}
+
+// device arrays of a pipeline's grid, in HostCells order (null: absent in its metric level)
+static void grid_arrays(const Pipeline& pl, const void* src[6]) {
+    src[0] = pl.g_cnt.p;
+    src[1] = pl.vcnt_mode ? pl.g_vcnt.p : nullptr;
+    src[2] = pl.met > 0 ? pl.g_sum.p : nullptr;
+    src[3] = pl.met >= 2 ? pl.g_min.p : nullptr;
+    src[4] = pl.met >= 2 ? pl.g_max.p : nullptr;
+    src[5] = pl.met >= 3 ? pl.g_sq.p : nullptr;
+}
+static void point_cells(Pipeline& pl, const void* const src[6]) {
+    auto h = [&](int a) { return src[a] ? pl.h_cells[a].p : nullptr; };
+    pl.hc.cnt = (const unsigned long long*)h(0);
+    pl.hc.vcnt = (const unsigned long long*)h(1);
+    pl.hc.sum = (const double*)h(2);
+    pl.hc.mn = (const unsigned long long*)h(3);
+    pl.hc.mx = (const unsigned long long*)h(4);
+    pl.hc.sq = (const double*)h(5);
+}
+// the rows [k][H] of the given ordinals, gathered on the GPU, copied (asynchronously) into the pipeline's pinned cells
+static void fetch_rows(esgpu_plan* p, Pipeline& pl, const uint32_t* drows, uint32_t k) {
+    const void* src[6];
+    grid_arrays(pl, src);
+    GatherParams G{};
+    G.rows = drows;
+    G.k = k; G.H = pl.H; G.T = pl.T;
+    void* dst[6] = {};
+    const size_t bytes = std::max<size_t>((size_t)k * pl.H, 1) * 8;
     for (int a = 0; a < 6; ++a) {
         if (!src[a]) continue;
-        dst[a] = p->h_dst[a].ensure(std::max<size_t>(n, 1) * 8);
-        HIPX(hipMemcpyAsync(dst[a], src[a], n * 8, hipMemcpyDeviceToHost, st));
+        dst[a] = pl.d_rows[a].ensure(p->ctx, bytes);
+        G.src[G.narrays] = (const unsigned long long*)src[a];
+        G.dst[G.narrays] = (unsigned long long*)dst[a];
+        G.narrays++;
     }
-    HIPX(hipStreamSynchronize(st));
-    h.cnt = (const unsigned long long*)dst[0];
-    h.vcnt = (const unsigned long long*)dst[1];
-    h.sum = (const double*)dst[2];
-    h.mn = (const unsigned long long*)dst[3];
-    h.mx = (const unsigned long long*)dst[4];
-    h.sq = (const double*)dst[5];
+    if (k) {
+        launch_gather_rows(G, p->stream);
+        HIPX(hipGetLastError());
+    }
+    for (int a = 0; a < 6; ++a)
+        if (src[a]) HIPX(hipMemcpyAsync(pl.h_cells[a].ensure(bytes), dst[a], (size_t)k * pl.H * 8, hipMemcpyDeviceToHost, p->stream));
+    point_cells(pl, src);
+}
+// the whole grid into the pipeline's pinned cells (asynchronous)
+static void fetch_grid(esgpu_plan* p, Pipeline& pl) {
+    const void* src[6];
+    grid_arrays(pl, src);
+    const size_t cells = (size_t)pl.T * pl.H;
+    for (int a = 0; a < 6; ++a)
+        if (src[a]) HIPX(hipMemcpyAsync(pl.h_cells[a].ensure(cells * 8), src[a], cells * 8, hipMemcpyDeviceToHost, p->stream));
+    point_cells(pl, src);
 }
 
-// GlobalOrdinalsStringTermsAggregator.buildAggregation candidate selection + PQ (:146-208)
+// GlobalOrdinalsStringTermsAggregator.buildAggregation candidate selection + PQ (:146-208); `value` is the
+// InternalOrder.Aggregation metric of an ordinal (terms ordered by a sub-aggregation)
 struct TermPick { uint32_t ord; int64_t count; };
-static std::vector<TermPick> select_terms(const esgpu_agg_spec& s, const unsigned long long* counts, uint32_t T, int64_t* other) {
+template <class Value>
+static std::vector<TermPick> select_terms(const esgpu_agg_spec& s, const unsigned long long* counts, uint32_t T, int64_t* other,
+                                          Value&& value) {
     std::vector<TermPick> cands;
     int64_t oth = 0;
     for (uint32_t g = 0; g < T; ++g) {
@@ -1977,11 +2149,23 @@ static std::vector<TermPick> select_terms(const esgpu_agg_spec& s, const unsigne
         if (s.shard_min_doc_count <= c) cands.push_back({g, c});
     }
     const size_t size = (size_t)std::min<int64_t>((int64_t)T, (int64_t)s.shard_size);
+    std::vector<double> vals;
+    const bool agg = s.order == ESGPU_ORDER_AGG_ASC || s.order == ESGPU_ORDER_AGG_DESC;
+    if (agg) {
+        vals.resize(T);
+        for (const TermPick& t : cands) vals[t.ord] = value(t.ord);
+    }
     auto cmp = [&](const TermPick& a, const TermPick& b) {
         switch (s.order) {
             case ESGPU_ORDER_COUNT_DESC: if (a.count != b.count) return a.count > b.count; return a.ord < b.ord;
             case ESGPU_ORDER_COUNT_ASC: if (a.count != b.count) return a.count < b.count; return a.ord < b.ord;
             case ESGPU_ORDER_TERM_DESC: return a.ord > b.ord;
+            case ESGPU_ORDER_AGG_ASC:
+            case ESGPU_ORDER_AGG_DESC: {  // CompoundOrder(Aggregation, TERM_ASC) over the sub-aggregator's metric(bucketOrd)
+                const int c = compare_discard_nan(vals[a.ord], vals[b.ord], s.order == ESGPU_ORDER_AGG_ASC);
+                if (c != 0) return c < 0;
+                return a.ord < b.ord;
+            }
             default: return a.ord < b.ord;
         }
     };
@@ -1996,196 +2180,246 @@ static std::vector<TermPick> select_terms(const esgpu_agg_spec& s, const unsigne
     return cands;
 }
 
-static Block build_grid(esgpu_plan* p, Pipeline& pl) {
-    hipStream_t st = p->stream;
-    const bool ORD = pl.term_spec >= 0;
-    const std::vector<Block> leaf = metric_protos(p, pl);  // empty metric instances (n == 1)
-    // ---- top-level metric ----
-    if (pl.outer < 0) {
-        Block r = leaf[0].like();
-        if (!pl.allocated) { r.append_empty(); return r; }
-        HostCells h;
-        d2h(p, h, pl, 1, pl.g_cnt.p, pl.g_vcnt.p, pl.g_sum.p, pl.g_min.p, pl.g_max.p, pl.g_sq.p);
-        std::vector<Block> one{std::move(r)};
-        append_metrics(p, pl, h, 0, one);
-        return std::move(one[0]);
-    }
-    const bool terms_outer = pl.outer == pl.term_spec;
-    // what an outer bucket carries as sub-aggregations (prototypes = bucketEmptyAggregations)
-    std::vector<Block> inner_protos;
-    if (pl.inner >= 0) {
-        Block in = p->specs[pl.inner].s.type == ESGPU_AGG_TERMS ? terms_shell(p, pl.inner, leaf) : hist_shell(p, pl.inner, leaf);
+// prototypes (n == 1 empty instances) of a bucket aggregation's children, in request order
+static std::vector<Block> child_protos(const esgpu_plan* p, const Group& g) {
+    std::vector<Block> out;
+    for (const ChildSrc& k : g.kids) {
+        if (!k.bucket) { out.push_back(leaf_proto(p, k.spec)); continue; }
+        std::vector<Block> grand;
+        for (int gc : p->specs[k.spec].children) grand.push_back(leaf_proto(p, gc));
+        Block in = p->specs[k.spec].s.type == ESGPU_AGG_TERMS ? terms_shell(p, k.spec, grand) : hist_shell(p, k.spec, grand);
         in.append_empty();
-        inner_protos.push_back(std::move(in));
-    } else {
-        inner_protos = leaf;
+        out.push_back(std::move(in));
     }
-    if (terms_outer) {
-        const SpecNode& tn = p->specs[pl.outer];
-        Block r = terms_shell(p, pl.outer, inner_protos);
-        if (!pl.allocated) { r.append_empty(); return r; }  // unmapped: buildEmptyAggregation
-        const uint32_t T = pl.T, H = pl.H;
-        // outer doc counts per ordinal (term_totals over the [H][T] grid unless counted separately)
-        const unsigned long long* dcnt = pl.g_cnt.as<unsigned long long>();
-        if (pl.ocnt_mode == OCNT_TERMS || pl.ocnt_mode == OCNT_TERMS_DERIVED) dcnt = pl.g_ocnt.as<unsigned long long>();
-        else if (H > 1) {
-            unsigned long long* tmp = (unsigned long long*)p->s_tcnt.ensure(p->ctx, (size_t)T * 8);
-            launch_term_totals(pl.g_cnt.as<unsigned long long>(), H, T, tmp, st);
-            HIPX(hipGetLastError());
-            dcnt = tmp;
-        }
-        int64_t other = 0;
-        std::vector<TermPick> top;
-        const uint64_t k_req = std::min<uint64_t>(pl.value_count, (uint64_t)std::max(tn.s.shard_size, 0));
-        const bool count_order = tn.s.order == ESGPU_ORDER_COUNT_DESC || tn.s.order == ESGPU_ORDER_COUNT_ASC;
-        const bool gpu_topk = pl.value_count > 65536 && k_req <= kTopkMax && (H == 1 || count_order);
-        if (gpu_topk) {
-            // K3 on the GPU: only the k winners (and the count total) cross PCIe
-            const uint32_t kk = (uint32_t)std::max<uint64_t>(k_req, 1);
-            TopkParams K{};
-            K.counts = dcnt;
-            K.T = (uint32_t)pl.value_count;
-            K.order = tn.s.order;
-            K.min_doc_count = tn.s.min_doc_count;
-            K.shard_min_doc_count = tn.s.shard_min_doc_count;
-            K.k = kk;
-            K.n_wg = std::min<uint32_t>(512, (K.T + 4095) / 4096);
-            const bool select = K.order == ESGPU_ORDER_COUNT_DESC || K.order == ESGPU_ORDER_COUNT_ASC;
-            K.cand = (unsigned long long*)p->s_cand.ensure(p->ctx, (select ? (size_t)K.T : (size_t)K.n_wg * kk) * 8);
-            uint32_t* hs = (uint32_t*)p->s_hist.ensure(p->ctx, (2048 + 2) * 4);
-            K.hist = hs;
-            K.sel = hs + 2048;
-            unsigned long long* dk = (unsigned long long*)p->s_keys.ensure(p->ctx, ((size_t)kk + 1) * 8);
-            K.out_keys = dk;
-            K.out_sum = dk + kk;
-            HIPX(hipMemsetAsync(K.out_sum, 0, 8, st));
-            launch_topk(K, st);
-            HIPX(hipGetLastError());
-            unsigned long long* hk = (unsigned long long*)p->h_keys.ensure(((size_t)kk + 1) * 8);
-            HIPX(hipMemcpyAsync(hk, dk, ((size_t)kk + 1) * 8, hipMemcpyDeviceToHost, st));
-            HIPX(hipStreamSynchronize(st));
-            other = (int64_t)hk[kk];
-            for (uint32_t i = 0; i < (uint32_t)k_req; ++i) {
-                const unsigned long long key = hk[i];
-                if (key == 0) break;
-                TermPick tp;
-                const uint32_t lo = (uint32_t)key;
-                tp.ord = (tn.s.order == ESGPU_ORDER_TERM_DESC) ? lo : 0xFFFFFFFFu - lo;
-                const uint64_t hi = (key >> 32) & 0x7FFFFFFFull;
-                tp.count = tn.s.order == ESGPU_ORDER_COUNT_DESC ? (int64_t)hi
-                         : tn.s.order == ESGPU_ORDER_COUNT_ASC ? (int64_t)(0x7FFFFFFFull - hi) : -1;  // term orders: gathered below
-                top.push_back(tp);
-            }
-        } else {
-            unsigned long long* tcnt = (unsigned long long*)p->h_tcnt.ensure((size_t)T * 8);
-            HIPX(hipMemcpyAsync(tcnt, dcnt, (size_t)T * 8, hipMemcpyDeviceToHost, st));
-            HIPX(hipStreamSynchronize(st));
-            top = select_terms(tn.s, tcnt, (uint32_t)pl.value_count, &other);
-        }
-        const uint32_t k = (uint32_t)top.size();
-        // gather the winners' rows [k][H] on the GPU and bring back only those
-        HostCells h;
-        if (k > 0) {
-            uint32_t* rows = (uint32_t*)p->h_rows.ensure((size_t)k * 4);
-            for (uint32_t i = 0; i < k; ++i) rows[i] = top[i].ord;
-            void* drows = p->s_rows.ensure(p->ctx, (size_t)k * 4);
-            HIPX(hipMemcpyAsync(drows, rows, (size_t)k * 4, hipMemcpyHostToDevice, st));
-            GatherParams G{};
-            G.rows = (const uint32_t*)drows;
-            G.k = k; G.H = H; G.T = T;
-            const void* srcs[6] = {pl.g_cnt.p, pl.vcnt_mode ? pl.g_vcnt.p : nullptr, pl.met > 0 ? pl.g_sum.p : nullptr,
-                                   pl.met >= 2 ? pl.g_min.p : nullptr, pl.met >= 2 ? pl.g_max.p : nullptr,
-                                   pl.met >= 3 ? pl.g_sq.p : nullptr};
-            void* dsts[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-            for (int a = 0; a < 6; ++a) {
-                if (!srcs[a]) continue;
-                dsts[a] = p->s_dst[a].ensure(p->ctx, (size_t)k * H * 8);
-                G.src[G.narrays] = (const unsigned long long*)srcs[a];
-                G.dst[G.narrays] = (unsigned long long*)dsts[a];
-                G.narrays++;
-            }
-            launch_gather_rows(G, st);
-            HIPX(hipGetLastError());
-            d2h(p, h, pl, (size_t)k * H, dsts[0], dsts[1], dsts[2], dsts[3], dsts[4], dsts[5]);
-        }
-        if (!pl.cards.empty()) {
-            std::vector<uint32_t> cells((size_t)k * H);
-            for (uint32_t i = 0; i < k; ++i)
-                for (uint32_t s2 = 0; s2 < H; ++s2) cells[(size_t)i * H + s2] = s2 * T + top[i].ord;
-            gather_cards(p, pl, cells);
-        }
-        if (gpu_topk) {  // otherDocCount = (sum of all counts) - (sum of the winners' counts)
-            for (uint32_t i = 0; i < k; ++i) {
-                if (top[i].count < 0) top[i].count = (int64_t)h.cnt[i];  // term orders (H == 1): count from the row
-                other -= top[i].count;
-            }
-        }
-        begin_instance(r, other);
-        for (uint32_t i = 0; i < k; ++i) {
-            const std::string term = plan_term(p, pl, top[i].ord);
-            push_bucket(r, top[i].ord, &term, top[i].count);
-            if (top[i].count == 0) {  // bucketEmptyAggregations
-                for (Block& sb : r.subs) sb.append_empty();
-            } else if (pl.inner < 0) {
-                append_metrics(p, pl, h, i, r.subs);
-            } else {
-                Block& hr = r.subs[0];
-                begin_instance(hr, 0);
-                for (uint32_t s = 0; s < H; ++s) {
-                    const size_t c = (size_t)i * H + s;
-                    if (h.cnt[c] == 0) continue;
-                    push_bucket(hr, key_value(pl, s), nullptr, (int64_t)h.cnt[c]);
-                    append_metrics(p, pl, h, c, hr.subs);
-                }
-                end_instance(hr);
-            }
-        }
-        end_instance(r);
-        return r;
-    }
-    // ---- histogram outer (optionally terms inner) ----
-    Block r = hist_shell(p, pl.outer, inner_protos);
+    return out;
+}
+
+// the InternalOrder.Aggregation value of terms spec `t` for ordinal cell c of the pipeline holding its order child
+static double order_value(const esgpu_plan* p, const SpecNode& t, const Pipeline& pl, int leaf, size_t c) {
+    const MetricCell m = metric_cell(p, pl, leaf, c);
+    const SpecNode& mn = p->specs[t.order_child];
+    double v = NAN;
+    metric_value(mn.s.type, t.order_key, m.count, m.sum, m.min, m.max, m.sq, mn.s.sigma, &v);
+    return v;
+}
+
+static Block build_metric_root(esgpu_plan* p, const Group& g) {
+    Pipeline& pl = p->pipes[g.pipes[0]];
+    Block r = leaf_proto(p, g.root).like();
     if (!pl.allocated) { r.append_empty(); return r; }
-    const uint32_t T = pl.T, H = pl.H;
-    HostCells h;
-    d2h(p, h, pl, (size_t)T * H, pl.g_cnt.p, pl.g_vcnt.p, pl.g_sum.p, pl.g_min.p, pl.g_max.p, pl.g_sq.p);
-    if (!pl.cards.empty()) {
-        std::vector<uint32_t> cells((size_t)T * H);
-        for (size_t i = 0; i < cells.size(); ++i) cells[i] = (uint32_t)i;
+    fetch_grid(p, pl);
+    HIPX(hipStreamSynchronize(p->stream));
+    append_leaf(p, pl, 0, 0, r);
+    return r;
+}
+
+static Block build_terms_root(esgpu_plan* p, const Group& g) {
+    hipStream_t st = p->stream;
+    const SpecNode& tn = p->specs[g.root];
+    Block r = terms_shell(p, g.root, child_protos(p, g));
+    Pipeline& P0 = p->pipes[g.pipes[0]];
+    if (!P0.allocated) { r.append_empty(); return r; }  // unmapped: buildEmptyAggregation
+    const uint32_t T = P0.T;
+    // the pipeline of the child the terms are ordered by (an outer-level pipeline: one cell per ordinal)
+    const bool agg_order = tn.s.order == ESGPU_ORDER_AGG_ASC || tn.s.order == ESGPU_ORDER_AGG_DESC;
+    LeafRef ord_ref;
+    if (agg_order)
+        for (const ChildSrc& k : g.kids) if (k.spec == tn.order_child) ord_ref = k.leaf;
+    // outer doc counts per ordinal (term_totals over the [H][T] grid unless counted separately)
+    const unsigned long long* dcnt = P0.g_cnt.as<unsigned long long>();
+    if (P0.ocnt_mode == OCNT_TERMS || P0.ocnt_mode == OCNT_TERMS_DERIVED) dcnt = P0.g_ocnt.as<unsigned long long>();
+    else if (P0.H > 1) {
+        unsigned long long* tmp = (unsigned long long*)p->s_tcnt.ensure(p->ctx, (size_t)T * 8);
+        launch_term_totals(P0.g_cnt.as<unsigned long long>(), P0.H, T, tmp, st);
+        HIPX(hipGetLastError());
+        dcnt = tmp;
+    }
+    int64_t other = 0;
+    std::vector<TermPick> top;
+    const uint64_t k_req = std::min<uint64_t>(P0.value_count, (uint64_t)std::max(tn.s.shard_size, 0));
+    const bool count_order = tn.s.order == ESGPU_ORDER_COUNT_DESC || tn.s.order == ESGPU_ORDER_COUNT_ASC;
+    const bool gpu_topk = !agg_order && P0.value_count > 65536 && k_req <= kTopkMax && (P0.H == 1 || count_order);
+    if (gpu_topk) {
+        // K3 on the GPU: only the k winners (and the count total) cross PCIe
+        const uint32_t kk = (uint32_t)std::max<uint64_t>(k_req, 1);
+        TopkParams K{};
+        K.counts = dcnt;
+        K.T = (uint32_t)P0.value_count;
+        K.order = tn.s.order;
+        K.min_doc_count = tn.s.min_doc_count;
+        K.shard_min_doc_count = tn.s.shard_min_doc_count;
+        K.k = kk;
+        K.n_wg = std::min<uint32_t>(512, (K.T + 4095) / 4096);
+        K.cand = (unsigned long long*)p->s_cand.ensure(p->ctx, (count_order ? (size_t)K.T : (size_t)K.n_wg * kk) * 8);
+        uint32_t* hs = (uint32_t*)p->s_hist.ensure(p->ctx, (2048 + 2) * 4);
+        K.hist = hs;
+        K.sel = hs + 2048;
+        unsigned long long* dk = (unsigned long long*)p->s_keys.ensure(p->ctx, ((size_t)kk + 1) * 8);
+        K.out_keys = dk;
+        K.out_sum = dk + kk;
+        HIPX(hipMemsetAsync(K.out_sum, 0, 8, st));
+        launch_topk(K, st);
+        HIPX(hipGetLastError());
+        unsigned long long* hk = (unsigned long long*)p->h_keys.ensure(((size_t)kk + 1) * 8);
+        HIPX(hipMemcpyAsync(hk, dk, ((size_t)kk + 1) * 8, hipMemcpyDeviceToHost, st));
+        HIPX(hipStreamSynchronize(st));
+        other = (int64_t)hk[kk];
+        for (uint32_t i = 0; i < (uint32_t)k_req; ++i) {
+            const unsigned long long key = hk[i];
+            if (key == 0) break;
+            TermPick tp;
+            const uint32_t lo = (uint32_t)key;
+            tp.ord = (tn.s.order == ESGPU_ORDER_TERM_DESC) ? lo : 0xFFFFFFFFu - lo;
+            const uint64_t hi = (key >> 32) & 0x7FFFFFFFull;
+            tp.count = tn.s.order == ESGPU_ORDER_COUNT_DESC ? (int64_t)hi
+                     : tn.s.order == ESGPU_ORDER_COUNT_ASC ? (int64_t)(0x7FFFFFFFull - hi) : -1;  // term orders: gathered below
+            top.push_back(tp);
+        }
+    } else {
+        unsigned long long* tcnt = (unsigned long long*)p->h_tcnt.ensure((size_t)T * 8);
+        HIPX(hipMemcpyAsync(tcnt, dcnt, (size_t)T * 8, hipMemcpyDeviceToHost, st));
+        if (agg_order) fetch_grid(p, p->pipes[ord_ref.pipe]);  // every ordinal's metric partials
+        HIPX(hipStreamSynchronize(st));
+        const Pipeline* OP = agg_order ? &p->pipes[ord_ref.pipe] : nullptr;
+        top = select_terms(tn.s, tcnt, (uint32_t)P0.value_count, &other,
+                           [&](uint32_t ord) { return order_value(p, tn, *OP, ord_ref.leaf, ord); });
+    }
+    const uint32_t k = (uint32_t)top.size();
+    // gather the winners' rows [k][H] of every pipeline on the GPU and bring back only those
+    uint32_t* rows = (uint32_t*)p->h_rows.ensure(std::max<size_t>(k, 1) * 4);
+    for (uint32_t i = 0; i < k; ++i) rows[i] = top[i].ord;
+    uint32_t* drows = (uint32_t*)p->s_rows.ensure(p->ctx, std::max<size_t>(k, 1) * 4);
+    if (k) HIPX(hipMemcpyAsync(drows, rows, (size_t)k * 4, hipMemcpyHostToDevice, st));
+    for (int pi : g.pipes) {
+        Pipeline& pl = p->pipes[pi];
+        if (pl.allocated) fetch_rows(p, pl, drows, k);
+    }
+    HIPX(hipStreamSynchronize(st));
+    for (int pi : g.pipes) {
+        Pipeline& pl = p->pipes[pi];
+        if (!pl.allocated || pl.cards.empty()) continue;
+        std::vector<uint32_t> cells((size_t)k * pl.H);
+        for (uint32_t i = 0; i < k; ++i)
+            for (uint32_t s2 = 0; s2 < pl.H; ++s2) cells[(size_t)i * pl.H + s2] = s2 * pl.T + top[i].ord;
         gather_cards(p, pl, cells);
     }
-    std::vector<unsigned long long> ocnt;
-    if (pl.ocnt_mode == OCNT_HIST) {
-        ocnt.resize(H);
-        HIPX(hipMemcpy(ocnt.data(), pl.g_ocnt.p, (size_t)H * 8, hipMemcpyDeviceToHost));
+    if (gpu_topk) {  // otherDocCount = (sum of all counts) - (sum of the winners' counts)
+        for (uint32_t i = 0; i < k; ++i) {
+            if (top[i].count < 0) top[i].count = (int64_t)P0.hc.cnt[i];  // term orders (H == 1): count from the row
+            other -= top[i].count;
+        }
     }
-    begin_instance(r, 0);
-    for (uint32_t s = 0; s < H; ++s) {
-        uint64_t dc = 0;
-        if (!ORD) dc = h.cnt[s];
-        else if (pl.ocnt_mode == OCNT_HIST) dc = ocnt[s];
-        else for (uint32_t t = 0; t < T; ++t) dc += h.cnt[(size_t)s * T + t];
-        if (dc == 0) continue;
-        push_bucket(r, key_value(pl, s), nullptr, (int64_t)dc);
-        if (!ORD) {
-            append_metrics(p, pl, h, s, r.subs);
+    begin_instance(r, other);
+    for (uint32_t i = 0; i < k; ++i) {
+        const std::string term = plan_term(p, P0, top[i].ord);
+        push_bucket(r, top[i].ord, &term, top[i].count);
+        if (top[i].count == 0) {  // bucketEmptyAggregations
+            for (Block& sb : r.subs) sb.append_empty();
             continue;
         }
-        const SpecNode& tn = p->specs[pl.inner];
-        Block& tr = r.subs[0];
-        int64_t other = 0;
-        std::vector<TermPick> top = select_terms(tn.s, h.cnt + (size_t)s * T, (uint32_t)pl.value_count, &other);
-        begin_instance(tr, other);
-        for (auto& tp : top) {
-            const std::string term = plan_term(p, pl, tp.ord);
-            push_bucket(tr, tp.ord, &term, tp.count);
-            if (tp.count == 0) for (Block& sb : tr.subs) sb.append_empty();
-            else append_metrics(p, pl, h, (size_t)s * T + tp.ord, tr.subs);
+        for (size_t ki = 0; ki < g.kids.size(); ++ki) {
+            const ChildSrc& kid = g.kids[ki];
+            Block& sub = r.subs[ki];
+            if (!kid.bucket) {
+                const Pipeline& L = p->pipes[kid.leaf.pipe];
+                if (!L.allocated) sub.append_empty(); else append_leaf(p, L, kid.leaf.leaf, i, sub);
+                continue;
+            }
+            const Pipeline& B0 = p->pipes[kid.pipes[0]];
+            if (!B0.allocated) { sub.append_empty(); continue; }
+            begin_instance(sub, 0);
+            for (uint32_t s = 0; s < B0.H; ++s) {
+                const size_t c = (size_t)i * B0.H + s;
+                if (B0.hc.cnt[c] == 0) continue;
+                push_bucket(sub, key_value(B0, s), nullptr, (int64_t)B0.hc.cnt[c]);
+                for (size_t gj = 0; gj < kid.grand.size(); ++gj) {
+                    const Pipeline& L = p->pipes[kid.grand[gj].pipe];
+                    require(L.H == B0.H && L.key0 == B0.key0, ESGPU_ERR_DEVICE, "sibling pipelines disagree on the key grid");
+                    append_leaf(p, L, kid.grand[gj].leaf, c, sub.subs[gj]);
+                }
+            }
+            end_instance(sub);
         }
-        end_instance(tr);
     }
     end_instance(r);
     return r;
+}
+
+static Block build_hist_root(esgpu_plan* p, const Group& g) {
+    hipStream_t st = p->stream;
+    Block r = hist_shell(p, g.root, child_protos(p, g));
+    Pipeline& P0 = p->pipes[g.pipes[0]];
+    if (!P0.allocated) { r.append_empty(); return r; }
+    for (int pi : g.pipes) {
+        Pipeline& pl = p->pipes[pi];
+        if (pl.allocated) fetch_grid(p, pl);
+    }
+    const bool p0_terms = P0.term_spec >= 0;
+    unsigned long long* ocnt = nullptr;
+    if (p0_terms) {  // histogram doc counts counted per doc beside the [H][T] cells (OCNT_HIST)
+        ocnt = (unsigned long long*)P0.h_ocnt.ensure((size_t)P0.H * 8);
+        HIPX(hipMemcpyAsync(ocnt, P0.g_ocnt.p, (size_t)P0.H * 8, hipMemcpyDeviceToHost, st));
+    }
+    HIPX(hipStreamSynchronize(st));
+    for (int pi : g.pipes) {
+        Pipeline& pl = p->pipes[pi];
+        if (!pl.allocated || pl.cards.empty()) continue;
+        std::vector<uint32_t> cells((size_t)pl.T * pl.H);
+        for (size_t i = 0; i < cells.size(); ++i) cells[i] = (uint32_t)i;
+        gather_cards(p, pl, cells);
+    }
+    begin_instance(r, 0);
+    for (uint32_t s = 0; s < P0.H; ++s) {
+        const uint64_t dc = p0_terms ? ocnt[s] : P0.hc.cnt[s];
+        if (dc == 0) continue;
+        push_bucket(r, key_value(P0, s), nullptr, (int64_t)dc);
+        for (size_t ki = 0; ki < g.kids.size(); ++ki) {
+            const ChildSrc& kid = g.kids[ki];
+            Block& sub = r.subs[ki];
+            if (!kid.bucket) {
+                const Pipeline& L = p->pipes[kid.leaf.pipe];
+                require(L.H == P0.H && L.key0 == P0.key0, ESGPU_ERR_DEVICE, "sibling pipelines disagree on the key grid");
+                append_leaf(p, L, kid.leaf.leaf, s, sub);
+                continue;
+            }
+            const Pipeline& B0 = p->pipes[kid.pipes[0]];
+            if (!B0.allocated || B0.tdict == nullptr) { sub.append_empty(); continue; }
+            require(B0.H == P0.H && B0.key0 == P0.key0, ESGPU_ERR_DEVICE, "sibling pipelines disagree on the key grid");
+            const SpecNode& tn = p->specs[kid.spec];
+            LeafRef ord_ref;
+            if (tn.s.order == ESGPU_ORDER_AGG_ASC || tn.s.order == ESGPU_ORDER_AGG_DESC) {
+                const auto& ch = tn.children;
+                for (size_t gj = 0; gj < ch.size(); ++gj) if (ch[gj] == tn.order_child) ord_ref = kid.grand[gj];
+            }
+            int64_t other = 0;
+            const size_t row = (size_t)s * B0.T;
+            std::vector<TermPick> top = select_terms(tn.s, B0.hc.cnt + row, (uint32_t)B0.value_count, &other, [&](uint32_t ord) {
+                return order_value(p, tn, p->pipes[ord_ref.pipe], ord_ref.leaf, row + ord);
+            });
+            begin_instance(sub, other);
+            for (auto& tp : top) {
+                const std::string term = plan_term(p, B0, tp.ord);
+                push_bucket(sub, tp.ord, &term, tp.count);
+                if (tp.count == 0) { for (Block& sb : sub.subs) sb.append_empty(); continue; }
+                for (size_t gj = 0; gj < kid.grand.size(); ++gj)
+                    append_leaf(p, p->pipes[kid.grand[gj].pipe], kid.grand[gj].leaf, row + tp.ord, sub.subs[gj]);
+            }
+            end_instance(sub);
+        }
+    }
+    end_instance(r);
+    return r;
+}
+
+static Block build_cardinality(esgpu_plan* p, Pipeline& pl);
+
+static Block build_group(esgpu_plan* p, const Group& g) {
+    Pipeline& P0 = p->pipes[g.pipes[0]];
+    if (P0.kind == 1) return build_cardinality(p, P0);
+    const int t = p->specs[g.root].s.type;
+    if (is_metric(t)) return build_metric_root(p, g);
+    if (t == ESGPU_AGG_TERMS) return build_terms_root(p, g);
+    return build_hist_root(p, g);
 }
 
 static Block build_cardinality(esgpu_plan* p, Pipeline& pl) {
@@ -2217,24 +2451,26 @@ extern "C" int esgpu_plan_build(esgpu_plan* p, esgpu_result** out) {
         std::unique_ptr<ResultHolder> h(new ResultHolder());
         // top-level aggregations in request order; a filter aggregation (InternalFilter, FilterAggregator.java:72-80)
         // is its counting pipeline's doc_count plus its sub-aggregations' pipelines, in the order compile() made them
-        size_t k = 0;
-        auto build_one = [&](Pipeline& pl) { return pl.kind == 1 ? build_cardinality(p, pl) : build_grid(p, pl); };
+        // top-level aggregations in request order; a filter aggregation (InternalFilter, FilterAggregator.java:72-80)
+        // is its counting pipeline's doc_count plus its sub-aggregations' groups, in the order create made them
+        size_t gi = 0;
         for (int r : p->tops) {
-            if (p->specs[r].s.type != ESGPU_AGG_FILTER) { h->aggs.push_back(build_one(p->pipes[k++])); continue; }
-            Pipeline& cnt = p->pipes[k++];
+            if (p->specs[r].s.type != ESGPU_AGG_FILTER) { h->aggs.push_back(build_group(p, p->groups[gi++])); continue; }
+            Pipeline* cnt = nullptr;
+            for (Pipeline& pl : p->pipes) if (pl.count_only && pl.root == r) cnt = &pl;
             Block fb;
             fb.type = ESGPU_AGG_FILTER;
             fb.name = p->specs[r].name;
             fb.n = 1;
             uint64_t dc = 0;
-            if (cnt.allocated) {
+            if (cnt && cnt->allocated) {
                 uint64_t* hc = (uint64_t*)p->h_tcnt.ensure(16);
-                HIPX(hipMemcpyAsync(hc, cnt.g_cnt.p, 8, hipMemcpyDeviceToHost, p->stream));
+                HIPX(hipMemcpyAsync(hc, cnt->g_cnt.p, 8, hipMemcpyDeviceToHost, p->stream));
                 HIPX(hipStreamSynchronize(p->stream));
                 dc = hc[0];
             }
             fb.count.push_back((int64_t)dc);
-            for (size_t j = 0; j < p->specs[r].children.size(); ++j) fb.subs.push_back(build_one(p->pipes[k++]));
+            for (size_t j = 0; j < p->specs[r].children.size(); ++j) fb.subs.push_back(build_group(p, p->groups[gi++]));
             h->aggs.push_back(std::move(fb));
         }
         h->export_view();

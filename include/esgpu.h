@@ -185,7 +185,14 @@ enum {
     ESGPU_ORDER_KEY_ASC = 4,
     ESGPU_ORDER_KEY_DESC = 5,
     ESGPU_ORDER_HCOUNT_ASC = 6,
-    ESGPU_ORDER_HCOUNT_DESC = 7
+    ESGPU_ORDER_HCOUNT_DESC = 7,
+    /* terms ordered by a metric sub-aggregation (InternalOrder.Aggregation, A/bucket/terms/InternalOrder.java:149-225;
+     * compound with _term asc tie-break; NaN values last, Comparators.compareDiscardNaN): esgpu_agg_spec.order_path
+     * names a direct stats / extended_stats / avg child, "<name>" or "<name>.value" for avg, "<name>.<metric>" for
+     * stats (count, sum, min, max, avg) and extended_stats (+ sum_of_squares, variance, std_deviation, std_upper,
+     * std_lower) -- AggregationPath.parse / validate (A/support/AggregationPath.java:68-113, 289-347) */
+    ESGPU_ORDER_AGG_ASC = 8,
+    ESGPU_ORDER_AGG_DESC = 9
 };
 
 /* date_histogram calendar units (DateTimeUnit.java:36-43); ESGPU_UNIT_NONE = fixed interval in ms */
@@ -236,6 +243,8 @@ typedef struct esgpu_agg_spec {
     const int64_t* tz_offsets_ms;
     int32_t tz_count;
     int32_t reserved_tz;
+    /* terms order ESGPU_ORDER_AGG_*: the sub-aggregation path (NUL-terminated) */
+    const char* order_path;
 } esgpu_agg_spec;
 
 /* Query filters: bool{filter:[...]} conjunction of term / range clauses. */
@@ -373,6 +382,7 @@ struct esgpu_agg_block {
     const uint8_t* const* registers;        /* 2^precision run lengths (hll_mode 1) */
     const uint32_t* const* lc_hashes;       /* encoded hashes, ascending (hll_mode 0) */
     const int64_t* lc_sizes;
+    const char* order_path;                 /* terms ordered by ESGPU_ORDER_AGG_*: the sub-aggregation path, else "" */
 };
 
 struct esgpu_result {

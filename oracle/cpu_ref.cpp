@@ -546,6 +546,7 @@ struct Internal {
     std::string name;
     // terms
     int order = ESGPU_ORDER_COUNT_DESC;
+    std::string order_path;  // InternalOrder.Aggregation path
     int required_size = 10, shard_size = 10;
     int64_t min_doc_count = 1;
     bool show_err = false;
@@ -582,6 +583,49 @@ static int terms_compare(int order, int64_t ca, int64_t cb, KeyCmp keycmp) {
         case ESGPU_ORDER_TERM_DESC: return -keycmp();
     }
     throw std::invalid_argument("order");
+}
+
+// ---- InternalOrder.Aggregation (A/bucket/terms/InternalOrder.java:149-225) ----
+// AggregationPath.parse of a one-element path (A/support/AggregationPath.java:68-113): "name", "name.key", "name[key]"
+static void split_path(const std::string& path, std::string* name, std::string* key) {
+    const size_t br = path.rfind('[');
+    if (br != std::string::npos && path.back() == ']') { *name = path.substr(0, br); *key = path.substr(br + 1, path.size() - br - 2); return; }
+    const size_t dot = path.rfind('.');
+    if (dot == std::string::npos) { *name = path; key->clear(); return; }
+    *name = path.substr(0, dot);
+    *key = path.substr(dot + 1);
+}
+// InternalAvg.value / InternalStats.value(name) / InternalExtendedStats.value(name) (and the aggregators' metric(name,
+// bucket), the same formulas)
+static double metric_of(int type, const std::string& key, int64_t count, double sum, double mn, double mx, double sq, double sigma) {
+    const double avg = sum / (double)count;
+    if (type == ESGPU_AGG_AVG) return avg;
+    if (key == "count") return (double)count;
+    if (key == "sum") return sum;
+    if (key == "min") return mn;
+    if (key == "max") return mx;
+    if (key == "avg") return avg;
+    const double variance = (sq - ((sum * sum) / (double)count)) / (double)count;  // InternalExtendedStats.getVariance
+    if (key == "sum_of_squares") return sq;
+    if (key == "variance") return variance;
+    if (key == "std_deviation") return std::sqrt(variance);
+    if (key == "std_upper") return avg + (std::sqrt(variance) * sigma);
+    if (key == "std_lower") return avg - (std::sqrt(variance) * sigma);
+    throw std::invalid_argument("Unknown value [" + key + "] in common stats aggregation");
+}
+// Comparators.compareDiscardNaN (common/util/Comparators.java): NaN last, Double.compare otherwise
+static int compare_discard_nan(double a, double b, bool asc) {
+    if (a != a) return b != b ? 0 : 1;
+    if (b != b) return -1;
+    auto dcmp = [](double x, double y) {  // Double.compare
+        if (x < y) return -1;
+        if (x > y) return 1;
+        uint64_t bx, by;
+        std::memcpy(&bx, &x, 8);
+        std::memcpy(&by, &y, 8);
+        return bx == by ? 0 : ((int64_t)bx < (int64_t)by ? -1 : 1);
+    };
+    return asc ? dcmp(a, b) : dcmp(b, a);
 }
 
 // Lucene PriorityQueue.insertWithOverflow + pop-into-array, with lessThan(a,b) = cmp(a,b) > 0
@@ -668,6 +712,9 @@ struct MultiBucketWrapper : Aggregator {
     }
 };
 
+// the shard-level metric(name, bucketOrd) of a metrics sub-aggregator (defined after StatsAgg)
+static double sub_metric(Aggregator* a, const std::string& key, int64_t bucket);
+
 // GlobalOrdinalsStringTermsAggregator (A/bucket/terms/GlobalOrdinalsStringTermsAggregator.java:90-224)
 struct TermsAgg : Aggregator {
     const Column* ords = nullptr;
@@ -697,6 +744,7 @@ struct TermsAgg : Aggregator {
         r->type = ESGPU_AGG_TERMS;
         r->name = f->name;
         r->order = f->spec.order;
+        if (f->spec.order_path) r->order_path = f->spec.order_path;
         r->required_size = f->spec.size;
         r->shard_size = f->spec.shard_size;
         r->min_doc_count = f->spec.min_doc_count;
@@ -722,9 +770,25 @@ struct TermsAgg : Aggregator {
         size_t size = s.min_doc_count == 0 ? (size_t)std::min<uint64_t>(valueCount, (uint64_t)s.shard_size)
                                            : (size_t)std::min<uint64_t>(std::max<uint64_t>(valueCount, docCounts.size()),
                                                                         (uint64_t)s.shard_size);
-        auto top = top_k(cands, size, [&](const OB& a, const OB& b) {
-            return terms_compare(s.order, a.count, b.count, [&] { return a.ord < b.ord ? -1 : a.ord > b.ord ? 1 : 0; });
-        }, (std::vector<OB>*)nullptr);
+        std::vector<OB> top;
+        if (s.order == ESGPU_ORDER_AGG_ASC || s.order == ESGPU_ORDER_AGG_DESC) {
+            // CompoundOrder(Aggregation(path), TERM_ASC) with the sub-aggregator's metric(key, bucketOrd)
+            std::string name, key;
+            split_path(s.order_path ? s.order_path : "", &name, &key);
+            Aggregator* sub = nullptr;
+            for (auto& a : subs) if (a->f->name == name) sub = a.get();
+            if (!sub) throw std::invalid_argument("Invalid term-aggregator order path [" + std::string(s.order_path) + "]");
+            std::unordered_map<uint64_t, double> v;
+            for (const OB& c : cands) v[c.ord] = sub_metric(sub, key, (int64_t)c.ord);
+            top = top_k(cands, size, [&](const OB& a, const OB& b) {
+                const int c = compare_discard_nan(v[a.ord], v[b.ord], s.order == ESGPU_ORDER_AGG_ASC);
+                return c != 0 ? c : (a.ord < b.ord ? -1 : a.ord > b.ord ? 1 : 0);
+            }, (std::vector<OB>*)nullptr);
+        } else {
+            top = top_k(cands, size, [&](const OB& a, const OB& b) {
+                return terms_compare(s.order, a.count, b.count, [&] { return a.ord < b.ord ? -1 : a.ord > b.ord ? 1 : 0; });
+            }, (std::vector<OB>*)nullptr);
+        }
         std::vector<Bucket> list;
         for (auto& ob : top) {
             Bucket b;
@@ -854,6 +918,15 @@ struct StatsAgg : Aggregator {
     }
     InternalPtr build_empty() override { return make(0, 0.0, INFINITY, -INFINITY, 0.0); }
 };
+
+static double sub_metric(Aggregator* a, const std::string& key, int64_t b) {  // StatsAggegator / AvgAggregator .metric
+    StatsAgg* sa = dynamic_cast<StatsAgg*>(a);
+    if (!sa) throw std::invalid_argument("terms order path must name a metrics aggregation");
+    const bool have = sa->values && b < (int64_t)sa->counts.size();
+    const int64_t cnt = have ? sa->counts[b] : 0;
+    return metric_of(sa->f->spec.type, key, cnt, have ? sa->sums[b] : 0.0, have ? sa->mins[b] : INFINITY,
+                     have ? sa->maxes[b] : -INFINITY, have ? sa->sumsqs[b] : 0.0, sa->f->spec.sigma);
+}
 
 // CardinalityAggregator (A/metrics/cardinality/CardinalityAggregator.java:80-150,186-294)
 struct CardinalityAgg : Aggregator {
@@ -1069,9 +1142,27 @@ static InternalPtr reduce_one(const InternalList& aggs) {
             }
             const size_t size = std::min<size_t>((size_t)first.required_size, key_order.size());
             std::vector<Bucket> overflow;
-            auto top = top_k(std::move(reduced), size, [&](const Bucket& a, const Bucket& b) {
-                return terms_compare(first.order, a.doc_count, b.doc_count, [&] { return term_compare(a.term, b.term); });
-            }, &overflow);
+            std::vector<Bucket> top;
+            if (first.order == ESGPU_ORDER_AGG_ASC || first.order == ESGPU_ORDER_AGG_DESC) {
+                // SubAggregationComparator: AggregationPath.resolveValue on the reduced bucket, then _term asc
+                std::string name, key;
+                split_path(first.order_path, &name, &key);
+                auto value = [&](const Bucket& b) {
+                    for (const InternalPtr& a : b.aggs)
+                        if (a->name == name) return metric_of(a->type, key, a->count, a->sum, a->min, a->max, a->sumsq, a->sigma);
+                    throw std::invalid_argument("Invalid order path [" + first.order_path + "]");
+                };
+                std::vector<double> vals(reduced.size());
+                for (size_t i = 0; i < reduced.size(); ++i) { vals[i] = value(reduced[i]); reduced[i].key = (int64_t)i; }
+                top = top_k(std::move(reduced), size, [&](const Bucket& a, const Bucket& b) {
+                    const int c = compare_discard_nan(vals[a.key], vals[b.key], first.order == ESGPU_ORDER_AGG_ASC);
+                    return c != 0 ? c : term_compare(a.term, b.term);
+                }, &overflow);
+            } else {
+                top = top_k(std::move(reduced), size, [&](const Bucket& a, const Bucket& b) {
+                    return terms_compare(first.order, a.doc_count, b.doc_count, [&] { return term_compare(a.term, b.term); });
+                }, &overflow);
+            }
             for (auto& o : overflow) otherDocCount += o.doc_count;
             r->buckets = std::move(top);
             r->doc_count_error = sumDocCountError == -1 ? -1 : (aggs.size() == 1 ? 0 : sumDocCountError);

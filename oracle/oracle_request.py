@@ -230,9 +230,14 @@ def lower(lib, aggs, number_of_shards=1):
         sp.sigma = 2.0
         sp.precision_threshold = -1
         if b.type == N.AGG_TERMS:
+            order = b._order
+            if hasattr(order, "path"):  # Terms.Order.aggregation(path, asc)
+                sp.order = N.ORDER_AGG_ASC if order.asc else N.ORDER_AGG_DESC
+                sp.order_path = enc(order.path)
+            else:
+                sp.order = order
             sp.size, sp.shard_size, sp.min_doc_count, sp.shard_min_doc_count = terms_thresholds(
-                b._size, b._shard_size, b._min, b._shard_min, b._order, number_of_shards)
-            sp.order = b._order
+                b._size, b._shard_size, b._min, b._shard_min, sp.order, number_of_shards)
             sp.show_term_doc_count_error = int(b._show_err)
         elif b.type == N.AGG_HISTOGRAM:
             if b._interval is None or int(b._interval) < 1:

@@ -1,4 +1,4 @@
-"""Test-side encoder of the libesgpu shard-result stream (esgpu_result_serialize format, version 3, esgpu_results.cpp).
+"""Test-side encoder of the libesgpu shard-result stream (esgpu_result_serialize format, version 4, esgpu_results.cpp).
 
 Lets CPU tests hand-build shard-level InternalAggregations (the way the reference's unit tests construct
 StringTerms / InternalHistogram / InternalCardinality objects) and push them through esgpu_result_deserialize +
@@ -10,7 +10,7 @@ import struct
 from elasticsearch_amd import _native as N
 
 MAGIC = 0x45534750
-VERSION = 3
+VERSION = 4
 BUCKET_TYPES = (N.AGG_TERMS, N.AGG_HISTOGRAM, N.AGG_DATE_HISTOGRAM)
 
 
@@ -36,7 +36,9 @@ def _block(b, insts):
     _vec(b, "q", a.get("tz_starts", []))
     _vec(b, "q", a.get("tz_offs", []))
     b += struct.pack("<BBqq", a.get("has_bmin", 0), a.get("has_bmax", 0), a.get("bmin", 0), a.get("bmax", 0))
-    b += struct.pack("<diQ", a.get("sigma", 2.0), a.get("precision", 14), len(insts))
+    b += struct.pack("<di", a.get("sigma", 2.0), a.get("precision", 14))
+    _str(b, a.get("order_path", ""))
+    b += struct.pack("<Q", len(insts))
     bucket = t in BUCKET_TYPES
     buckets = [bk for x in insts for bk in x.get("buckets", [])] if bucket else []
     _vec(b, "q", [x.get("doc_count_error", 0) for x in insts] if bucket else [])
@@ -94,7 +96,9 @@ def _empty_block(b, spec):
     _vec(b, "q", s.get("tz_starts", []))
     _vec(b, "q", s.get("tz_offs", []))
     b += struct.pack("<BBqq", s.get("has_bmin", 0), s.get("has_bmax", 0), s.get("bmin", 0), s.get("bmax", 0))
-    b += struct.pack("<diQ", s.get("sigma", 2.0), s.get("precision", 14), 0)
+    b += struct.pack("<di", s.get("sigma", 2.0), s.get("precision", 14))
+    _str(b, s.get("order_path", ""))
+    b += struct.pack("<Q", 0)
     bucket = t in BUCKET_TYPES
     _vec(b, "q", [])
     _vec(b, "q", [])
@@ -160,7 +164,7 @@ def from_shard_json(aggs, shard_json, number_of_shards=1):
         p = {"type": s.type, "name": s.name.decode(), "order": s.order, "sigma": s.sigma}
         if s.type == N.AGG_TERMS:
             p.update(required_size=s.size, shard_size=s.shard_size, min_doc_count=s.min_doc_count,
-                     show_err=s.show_term_doc_count_error)
+                     show_err=s.show_term_doc_count_error, order_path=(s.order_path or b"").decode())
         if hist:
             p.update(min_doc_count=s.min_doc_count, keyed=s.keyed, interval=s.interval, offset=s.offset,
                      date_unit=s.date_unit if s.type == N.AGG_DATE_HISTOGRAM else 0)

@@ -1,0 +1,155 @@
+"""GPU parity for general aggregator trees: a bucket aggregation with several children of mixed
+kinds -- metrics beside a bucket sub-aggregation, metrics on different fields, sibling bucket sub-aggregations --
+compiled to one pipeline per (inner bucket, metric field) and assembled into one result tree, the way
+AggregatorFactories.createSubAggregators (A/AggregatorFactories.java:68-79) gives every child its own aggregator;
+and terms ordered by a metric sub-aggregation (InternalOrder.Aggregation, A/bucket/terms/InternalOrder.java:149-225;
+the doc_count_error -1 rule of InternalTerms.doReduce, :195-196)."""
+import numpy as np
+import pytest
+
+import oracle as O
+from elasticsearch_amd import AggregationBuilders as AB
+from elasticsearch_amd import Order, QueryBuilders as QB
+from elasticsearch_amd import _native as N
+from elasticsearch_amd import reduce
+from helpers import assert_same, bits_from_mask, synthetic_columns
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("host", "@timestamp", "response_time_ms", "bytes", "status", "price", "client_ip.hash")
+
+
+def _both(engine, aggs, n=600_000, filters=None, shards=1, exact=True, fields=FIELDS):
+    want = O.run([(synthetic_columns(fields, n, shard=s), n) for s in range(shards)], aggs, filters=filters,
+                 number_of_shards=shards)
+    results = []
+    plan = engine.plan(aggs, filters=filters, number_of_shards=shards)
+    for s in range(shards):
+        seg = engine.synthetic_segment(n, fields=fields, shard=s)
+        plan.reset()
+        plan.collect(seg)
+        r = plan.build()
+        assert_same(r.to_dict(), want["shards"][s], f"shard{s}", exact)
+        results.append(r)
+        seg.close()
+    red = reduce(results).to_dict()
+    assert_same(red, want["reduced"], "reduced", exact)
+    plan.close()
+    return red
+
+
+def test_metrics_beside_a_bucket_sub_aggregation(engine):
+    aggs = [AB.terms("hosts").field("host").size(8).subAggregation(
+        AB.dateHistogram("h").field("@timestamp").interval("6h").subAggregation(AB.stats("rt").field("response_time_ms")))
+        .subAggregation(AB.stats("rt_all").field("response_time_ms")).subAggregation(AB.avg("b").field("bytes"))]
+    _both(engine, aggs)
+
+
+def test_metrics_on_different_fields_at_one_level(engine):
+    aggs = [AB.terms("hosts").field("host").size(12).subAggregation(AB.stats("rt").field("response_time_ms"))
+            .subAggregation(AB.avg("b").field("bytes")).subAggregation(AB.extendedStats("rt_x").field("response_time_ms"))
+            .subAggregation(AB.cardinality("ips").field("client_ip.hash").precisionThreshold(100)),
+            AB.dateHistogram("d").field("@timestamp").interval("1d").subAggregation(AB.avg("s").field("status"))
+            .subAggregation(AB.extendedStats("b").field("bytes"))]
+    _both(engine, aggs, shards=2)
+
+
+def test_sibling_bucket_sub_aggregations(engine):
+    aggs = [AB.terms("hosts").field("host").size(5).subAggregation(
+                AB.dateHistogram("h").field("@timestamp").interval("1d").subAggregation(AB.avg("rt").field("response_time_ms"))
+                .subAggregation(AB.stats("b").field("bytes")))
+            .subAggregation(AB.histogram("rt_h").field("response_time_ms").interval(100).subAggregation(AB.avg("s").field("status")))
+            .subAggregation(AB.avg("all").field("bytes")),
+            AB.dateHistogram("days").field("@timestamp").interval("1d").subAggregation(
+                AB.terms("top").field("host").size(3).subAggregation(AB.avg("rt").field("response_time_ms")))
+            .subAggregation(AB.terms("bottom").field("host").size(2).order(Order.count(True)))
+            .subAggregation(AB.stats("rt").field("response_time_ms"))]
+    _both(engine, aggs, shards=3)
+
+
+@pytest.mark.parametrize("order", [Order.aggregation("rt.avg", False), Order.aggregation("a", True),
+                                   Order.aggregation("x.max", False), Order.aggregation("x.std_upper", True),
+                                   Order.aggregation("x.count", True), Order.aggregation("a.value", False)])
+def test_terms_ordered_by_a_metric(engine, order):
+    aggs = [AB.terms("hosts").field("host").size(6).order(order).subAggregation(AB.stats("rt").field("response_time_ms"))
+            .subAggregation(AB.avg("a").field("bytes")).subAggregation(AB.extendedStats("x").field("response_time_ms"))
+            .subAggregation(AB.dateHistogram("h").field("@timestamp").interval("1d"))]
+    red = _both(engine, aggs, shards=3)
+    assert red["hosts"]["doc_count_error_upper_bound"] == -1  # InternalTerms.doReduce: not a count-desc order
+
+
+def test_terms_ordered_by_a_metric_min_doc_count_zero_and_nan(engine):
+    """Zero-count terms (min_doc_count 0) have a NaN average: Comparators.compareDiscardNaN puts them last in both
+    directions; the rt field is missing on 40 % of the docs."""
+    n = 400_000
+    rng = np.random.default_rng(3)
+    cols = synthetic_columns(("host", "response_time_ms"), n)
+    host = cols["host"]["values"].copy()
+    host[host >= 900] = 5  # hosts 900..999 never occur
+    cols["host"]["values"] = host
+    cols["response_time_ms"]["present"] = bits_from_mask(rng.random(n) >= 0.4)
+    for asc in (True, False):
+        aggs = [AB.terms("hosts").field("host").size(1000).minDocCount(0).order(Order.aggregation("a", asc))
+                .subAggregation(AB.avg("a").field("response_time_ms"))]
+        want = O.run([(cols, n)], aggs)
+        seg = engine.upload_segment(cols, n)
+        plan = engine.plan(aggs)
+        plan.collect(seg)
+        res = plan.build()
+        assert_same(res.to_dict(), want["shards"][0], "shard")
+        assert_same(reduce([res]).to_dict(), want["reduced"], "reduced")
+        plan.close()
+        seg.close()
+
+
+def test_nested_terms_ordered_by_a_metric_under_a_histogram(engine):
+    aggs = [AB.dateHistogram("days").field("@timestamp").interval("1d").subAggregation(
+        AB.terms("hosts").field("host").size(4).order(Order.aggregation("rt.max", True))
+        .subAggregation(AB.stats("rt").field("response_time_ms")))]
+    _both(engine, aggs, shards=2)
+
+
+def test_high_cardinality_terms_ordered_by_a_metric(engine):
+    aggs = [AB.terms("urls").field("url").size(10).order(Order.aggregation("rt", False))
+            .subAggregation(AB.avg("rt").field("response_time_ms"))]
+    _both(engine, aggs, n=1_000_000, fields=("url", "response_time_ms"))
+
+
+def test_inner_bucket_field_unmapped(engine):
+    """terms{date_histogram(missing)} still counts the terms; histogram{terms(missing)} still counts the keys."""
+    aggs = [AB.terms("hosts").field("host").size(5).subAggregation(
+                AB.dateHistogram("h").field("no_such_date").interval("1h").subAggregation(AB.avg("rt").field("response_time_ms"))),
+            AB.histogram("rt_h").field("response_time_ms").interval(250).subAggregation(
+                AB.terms("t").field("no_such_keyword").subAggregation(AB.stats("b").field("bytes")))]
+    _both(engine, aggs, fields=("host", "response_time_ms", "bytes"))
+
+
+def test_inner_field_missing_in_one_segment(engine):
+    """A later segment lacks the inner histogram's field: its docs count for the terms only."""
+    n = 200_000
+    a = synthetic_columns(("host", "@timestamp", "response_time_ms"), n)
+    b = {"host": synthetic_columns(("host",), n, shard=1)["host"],
+         "response_time_ms": synthetic_columns(("response_time_ms",), n, shard=1)["response_time_ms"]}
+    aggs = [AB.terms("hosts").field("host").size(7).subAggregation(
+        AB.dateHistogram("h").field("@timestamp").interval("12h").subAggregation(AB.avg("rt").field("response_time_ms")))
+        .subAggregation(AB.stats("rt").field("response_time_ms"))]
+    one = {"host": dict(a["host"], values=np.concatenate([a["host"]["values"], b["host"]["values"]])),
+           "response_time_ms": dict(a["response_time_ms"], values=np.concatenate([a["response_time_ms"]["values"],
+                                                                                    b["response_time_ms"]["values"]])),
+           "@timestamp": {"type": N.COL_I64, "values": np.concatenate([a["@timestamp"]["values"], np.zeros(n, np.int64)]),
+                          "present": bits_from_mask(np.arange(2 * n) < n)}}
+    want = O.run([(one, 2 * n)], aggs)
+    segs = [engine.upload_segment(a, n), engine.upload_segment(b, n)]
+    plan = engine.plan(aggs)
+    for s in segs:
+        plan.collect(s)
+    assert_same(plan.build().to_dict(), want["shards"][0], "shard")
+    plan.close()
+
+
+def test_filter_aggregation_with_mixed_children(engine):
+    aggs = [AB.filter("ok", QB.termQuery("status", 200)).subAggregation(
+        AB.terms("hosts").field("host").size(4).subAggregation(AB.avg("rt").field("response_time_ms"))
+        .subAggregation(AB.dateHistogram("d").field("@timestamp").interval("1d"))
+        .order(Order.aggregation("rt", False))).subAggregation(AB.stats("b").field("bytes"))]
+    _both(engine, aggs, shards=2, filters=[QB.rangeQuery("bytes").gte(512)])

@@ -74,3 +74,24 @@ def test_reduce_rejects_mismatched_trees():
     from elasticsearch_amd import _native as N
     with pytest.raises(N.EsGpuError):
         reduce([ShardResult.deserialize(a), ShardResult.deserialize(b)])
+
+
+@pytest.mark.parametrize("path,asc", [("rt.avg", False), ("a", True), ("x.std_upper", True), ("x.count", False),
+                                      ("rt.min", True)])
+def test_reduce_terms_ordered_by_a_metric(path, asc):
+    """InternalTerms.doReduce with InternalOrder.Aggregation: the reduced sub-aggregation's value orders the merged
+    buckets (NaN last), ties by term; doc_count_error is -1 (not a count-desc order).  Shard results come from the
+    oracle (its shard-level GlobalOrdinalsStringTermsAggregator selection by metric(name, bucketOrd))."""
+    from elasticsearch_amd import Order
+    from helpers import synthetic_columns
+    from result_stream import from_shard_json
+    aggs = [AB.terms("hosts").field("host").size(6).order(Order.aggregation(path, asc))
+            .subAggregation(AB.stats("rt").field("response_time_ms")).subAggregation(AB.avg("a").field("bytes"))
+            .subAggregation(AB.extendedStats("x").field("response_time_ms"))]
+    fields = ("host", "response_time_ms", "bytes")
+    shards = [(synthetic_columns(fields, 100_000, shard=s), 100_000) for s in range(3)]
+    want = O.run(shards, aggs, number_of_shards=3)
+    blobs = [encode(from_shard_json(aggs, want["shards"][s], 3)) for s in range(3)]
+    got = reduce([ShardResult.deserialize(b) for b in blobs]).to_dict()
+    assert_same(got, want["reduced"], "reduced")
+    assert got["hosts"]["doc_count_error_upper_bound"] == -1
