@@ -1544,7 +1544,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     bool has_keys = false;
     int64_t table_shift = 0;
     const uint32_t H_before = pl.H;
-    if (HIST && hc->vmin <= hc->vmax) {
+    if (HIST && hc && hc->vmin <= hc->vmax) {
         if (pl.ktable) {
             table_shift = build_key_table(p, pl, hc->vmin, hc->vmax);
             kmin = 0;
