@@ -6,7 +6,7 @@ without the built library or without a GPU the calls raise.
 """
 from ._native import (CircuitBreakingError, EsGpuError, NoDeviceError, UnsupportedOnGpu)  # noqa: F401
 from .aggs import AggregationBuilders, Order, QueryBuilders  # noqa: F401
-from .engine import (Communicator, Engine, Plan, Segment, ShardResult, device_count, precision_from_threshold,  # noqa: F401
+from .engine import (Communicator, Engine, Plan, Segment, ShardResult, device_count, pinned_empty, precision_from_threshold,  # noqa: F401
                      reduce, routing_hash, synthetic_host_column, synthetic_terms)
 
 __all__ = [

@@ -120,12 +120,15 @@ SIGNATURES = [
     ("esgpu_ctx_destroy", ctypes.c_int, [_VP]),
     ("esgpu_ctx_hbm_used", ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_uint64)]),
     ("esgpu_device_count", ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    ("esgpu_host_alloc", ctypes.c_int, [ctypes.c_size_t, _PP]),
+    ("esgpu_host_free", ctypes.c_int, [_VP]),
     ("esgpu_segment_upload", ctypes.c_int, [_VP, ctypes.POINTER(ColumnDesc), ctypes.c_int32, ctypes.c_uint32, _PP]),
     ("esgpu_segment_destroy", ctypes.c_int, [_VP]),
     ("esgpu_segment_max_doc", ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_uint32)]),
-    ("esgpu_segment_synthetic", ctypes.c_int, [_VP, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _PP]),
+    ("esgpu_segment_synthetic", ctypes.c_int, [_VP, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                               ctypes.c_int64, _PP]),
     ("esgpu_synthetic_fill_host", ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
-                                                 ctypes.c_uint64, ctypes.c_uint64, _VP]),
+                                                 ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint64, _VP]),
     ("esgpu_synthetic_term", ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_size_t]),
     ("esgpu_segment_read_column", ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64, _VP]),
     ("esgpu_ordinal_map_build", ctypes.c_int, [_VP, ctypes.POINTER(_VP), ctypes.c_int32, ctypes.c_char_p,

@@ -245,14 +245,19 @@ ES_HD uint32_t cdf_search(const double* cdf, uint32_t n, double u) {
     return lo;
 }
 
-enum SynthField : uint32_t { F_TS = 0, F_HOST = 1, F_URL = 2, F_STATUS = 3, F_RT = 4, F_BYTES = 5, F_IP = 6, F_PRICE = 7 };
+enum SynthField : uint32_t { F_TS = 0, F_HOST = 1, F_URL = 2, F_STATUS = 3, F_RT = 4, F_BYTES = 5, F_IP = 6, F_PRICE = 7,
+                              F_TS_JITTER = 8 };
 
-ES_HD int64_t synth_timestamp(uint64_t sseed, uint64_t doc, uint64_t n) {
+// non-decreasing in doc order; jitter_ms > 0 displaces each doc by a uniform offset in [-jitter_ms, +jitter_ms] (docs
+// roughly time-ordered, as merged segments are, instead of sorted)
+ES_HD int64_t synth_timestamp(uint64_t sseed, uint64_t doc, uint64_t n, int64_t jitter_ms = 0) {
     const uint64_t base = (doc * (uint64_t)kSynthSpan) / n;
     const uint64_t next = ((doc + 1) * (uint64_t)kSynthSpan) / n;
     const uint64_t gap = next - base;
     const uint64_t r = synth_rand(sseed, doc, F_TS);
-    return kSynthT0 + (int64_t)(base + (gap ? r % gap : 0));
+    int64_t t = kSynthT0 + (int64_t)(base + (gap ? r % gap : 0));
+    if (jitter_ms > 0) t += (int64_t)(synth_rand(sseed, doc, F_TS_JITTER) % (uint64_t)(2 * jitter_ms + 1)) - jitter_ms;
+    return t;
 }
 ES_HD uint32_t synth_host(uint64_t sseed, uint64_t doc, const double* cdf) {
     const uint32_t rank = cdf_search(cdf, kHostTerms, unit_double(synth_rand(sseed, doc, F_HOST)));

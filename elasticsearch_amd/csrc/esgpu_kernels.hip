@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void synth_kernel(SynthParams P) {
     const uint64_t sseed = shard_seed(P.seed, P.shard);
     for (uint64_t d = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; d < P.n_pad; d += (uint64_t)gridDim.x * blockDim.x) {
         const bool live = d < P.n;
-        if (P.ts) P.ts[d] = live ? synth_timestamp(sseed, d, P.n) : 0;
+        if (P.ts) P.ts[d] = live ? synth_timestamp(sseed, d, P.n, P.ts_jitter) : 0;
         if (P.host) P.host[d] = live ? synth_host(sseed, d, P.host_cdf) : kMissingOrd;
         if (P.url) P.url[d] = live ? synth_url(sseed, d, P.url_cdf) : kMissingOrd;
         if (P.status) P.status[d] = live ? synth_status(sseed, d) : 0;

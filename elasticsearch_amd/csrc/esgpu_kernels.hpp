@@ -13,6 +13,7 @@ struct SynthParams {
     uint32_t pad0;
     uint64_t n;       // live docs
     uint64_t n_pad;   // allocated (multiple of kBlockDocs)
+    int64_t ts_jitter;  // @timestamp displacement bound in ms (0 = sorted)
     int64_t* ts;
     uint32_t* host;
     uint32_t* url;

@@ -148,7 +148,7 @@ extern "C" int esgpu_synthetic_term(uint32_t field_bit, uint64_t ord, char* buf,
 }
 
 extern "C" int esgpu_synthetic_fill_host(uint64_t seed, uint32_t shard, uint32_t num_docs, uint32_t field_bit,
-                                         uint64_t start, uint64_t count, void* out) {
+                                         int64_t ts_jitter_ms, uint64_t start, uint64_t count, void* out) {
     return guarded([&] {
         ensure_tables();
         if (field_bit == ESGPU_SYNTH_URL) ensure_url_table();
@@ -156,7 +156,7 @@ extern "C" int esgpu_synthetic_fill_host(uint64_t seed, uint32_t shard, uint32_t
         for (uint64_t i = 0; i < count; ++i) {
             const uint64_t d = start + i;
             switch (field_bit) {
-                case ESGPU_SYNTH_TIMESTAMP: ((int64_t*)out)[i] = synth_timestamp(ss, d, num_docs); break;
+                case ESGPU_SYNTH_TIMESTAMP: ((int64_t*)out)[i] = synth_timestamp(ss, d, num_docs, ts_jitter_ms); break;
                 case ESGPU_SYNTH_HOST: ((uint32_t*)out)[i] = synth_host(ss, d, g_host_cdf.data()); break;
                 case ESGPU_SYNTH_URL: ((uint32_t*)out)[i] = synth_url(ss, d, g_url_cdf.data()); break;
                 case ESGPU_SYNTH_STATUS: ((int64_t*)out)[i] = synth_status(ss, d); break;
@@ -296,6 +296,19 @@ static void build_zone_map(esgpu_ctx* c, DevColumn& col, uint32_t n) {
     }
 }
 
+extern "C" int esgpu_host_alloc(size_t bytes, void** out) {
+    return guarded([&] {
+        require(out != nullptr, ESGPU_ERR_INVALID, "null argument");
+        *out = nullptr;
+        if (!bytes) return;
+        HIPX(hipHostMalloc(out, bytes, hipHostMallocDefault));
+    });
+}
+
+extern "C" int esgpu_host_free(void* p) {
+    return guarded([&] { if (p) HIPX(hipHostFree(p)); });
+}
+
 extern "C" int esgpu_segment_upload(esgpu_ctx* c, const esgpu_column_desc* cols, int32_t ncols, uint32_t max_doc,
                                     esgpu_segment** out) {
     return guarded([&] {
@@ -384,7 +397,7 @@ extern "C" int esgpu_segment_upload(esgpu_ctx* c, const esgpu_column_desc* cols,
 }
 
 extern "C" int esgpu_segment_synthetic(esgpu_ctx* c, uint64_t seed, uint32_t shard, uint32_t num_docs, uint32_t mask,
-                                       esgpu_segment** out) {
+                                       int64_t ts_jitter_ms, esgpu_segment** out) {
     return guarded([&] {
         require(c && out, ESGPU_ERR_INVALID, "null argument");
         require(num_docs <= 0x7FFFFFFFu, ESGPU_ERR_INVALID, "num_docs exceeds Lucene's int doc id space");
@@ -411,6 +424,8 @@ extern "C" int esgpu_segment_synthetic(esgpu_ctx* c, uint64_t seed, uint32_t sha
         p.shard = shard;
         p.n = num_docs;
         p.n_pad = s->n_pad;
+        require(ts_jitter_ms >= 0, ESGPU_ERR_INVALID, "negative timestamp jitter");
+        p.ts_jitter = ts_jitter_ms;
         p.host_cdf = c->d_host_cdf;
         p.rt_cdf = c->d_rt_cdf;
         p.url_cdf = c->d_url_cdf;

@@ -225,12 +225,12 @@ class Engine:
         return v.value
 
     def synthetic_segment(self, num_docs, fields=("host", "@timestamp", "response_time_ms"), shard=0,
-                          seed=0x5EEDE1A5):
+                          seed=0x5EEDE1A5, ts_jitter_ms=0):
         mask = 0
         for f in fields:
             mask |= N.SYNTH_FIELDS[f]
         ptr = ctypes.c_void_p()
-        N.check(N.lib().esgpu_segment_synthetic(self._ptr, seed, shard, num_docs, mask, ctypes.byref(ptr)))
+        N.check(N.lib().esgpu_segment_synthetic(self._ptr, seed, shard, num_docs, mask, ts_jitter_ms, ctypes.byref(ptr)))
         return Segment(self, ptr)
 
     def ordinal_map(self, segments, field):
@@ -321,18 +321,42 @@ class Engine:
             self._ptr = None
 
 
+class PinnedArray(np.ndarray):
+    """A numpy array over page-locked host memory (esgpu_host_alloc); freed with the array."""
+
+    def __array_finalize__(self, obj):
+        pass
+
+
+def pinned_empty(count, dtype):
+    """numpy array of `count` elements in page-locked host memory, for K11 exports (esgpu_segment_upload)."""
+    dtype = np.dtype(dtype)
+    nbytes = max(int(count) * dtype.itemsize, 1)
+    ptr = ctypes.c_void_p()
+    N.check(N.lib().esgpu_host_alloc(nbytes, ctypes.byref(ptr)))
+    buf = (ctypes.c_uint8 * nbytes).from_address(ptr.value)
+    arr = np.frombuffer(buf, dtype=np.uint8, count=int(count) * dtype.itemsize).view(dtype)
+    import weakref
+    holder = arr.view(PinnedArray)
+    weakref.finalize(holder, N.lib().esgpu_host_free, ptr.value)
+    holder._pin_buf = buf  # noqa: SLF001 -- keeps the ctypes view alive with the array
+    return holder
+
+
 def device_count():
     n = ctypes.c_int()
     N.check(N.lib().esgpu_device_count(ctypes.byref(n)))
     return n.value
 
 
-def synthetic_host_column(field, num_docs, start=0, count=None, shard=0, seed=0x5EEDE1A5):
+def synthetic_host_column(field, num_docs, start=0, count=None, shard=0, seed=0x5EEDE1A5, ts_jitter_ms=0, out=None):
     """The same synthetic values the device generator writes, computed on the CPU (oracle / CPU baseline input)."""
     count = num_docs - start if count is None else count
     dtype = {N.COL_ORD_U32: np.uint32, N.COL_I64: np.int64, N.COL_F64: np.float64, N.COL_U64: np.uint64}[N.SYNTH_TYPES[field]]
-    out = np.empty(count, dtype=dtype)
-    N.check(N.lib().esgpu_synthetic_fill_host(seed, shard, num_docs, N.SYNTH_FIELDS[field], start, count, out.ctypes.data))
+    if out is None:
+        out = np.empty(count, dtype=dtype)
+    N.check(N.lib().esgpu_synthetic_fill_host(seed, shard, num_docs, N.SYNTH_FIELDS[field], ts_jitter_ms, start, count,
+                                              out.ctypes.data))
     return out
 
 

@@ -104,6 +104,12 @@ typedef struct esgpu_column_desc {
 
 typedef struct esgpu_segment esgpu_segment;
 
+/* Page-locked host memory for the export side of K11 (ValuesSource doc values decoded into flat arrays by the JNI
+ * shim, A/support/ValuesSource.java:148-152, 391-398): esgpu_segment_upload copies from such buffers by DMA at the
+ * host link's rate; from pageable memory the HIP runtime stages every copy through a bounce buffer. */
+int esgpu_host_alloc(size_t bytes, void** out);
+int esgpu_host_free(void* p);
+
 /* K11: copies each column once into HBM (hipMemcpyAsync from the caller's buffers), builds per-block
  * min/max zone maps for numeric columns, keeps the term dictionaries host-side for lookupOrd. */
 int esgpu_segment_upload(esgpu_ctx* ctx, const esgpu_column_desc* cols, int32_t ncols, uint32_t max_doc,
@@ -123,12 +129,14 @@ enum {
     ESGPU_SYNTH_CLIENT_IP = 1 << 6,   /* "client_ip.hash"   U64  murmur3 h1 of a dotted quad */
     ESGPU_SYNTH_PRICE = 1 << 7        /* "price"            F64  non-integer doubles (float-stress) */
 };
+/* ts_jitter_ms: 0 = "@timestamp" non-decreasing in doc order; > 0 = each doc displaced by up to +-ts_jitter_ms
+ * (roughly time-ordered docs, as merged segments hold them). */
 int esgpu_segment_synthetic(esgpu_ctx* ctx, uint64_t seed, uint32_t shard, uint32_t num_docs, uint32_t fields_mask,
-                            esgpu_segment** out);
+                            int64_t ts_jitter_ms, esgpu_segment** out);
 /* Host-side generation of the same values (doc range [start, start+count)), for the CPU oracle/baseline.
  * out must hold count entries of the column's natural width (u32 for ORD columns, 8 bytes otherwise). */
-int esgpu_synthetic_fill_host(uint64_t seed, uint32_t shard, uint32_t num_docs, uint32_t field_bit, uint64_t start,
-                              uint64_t count, void* out);
+int esgpu_synthetic_fill_host(uint64_t seed, uint32_t shard, uint32_t num_docs, uint32_t field_bit, int64_t ts_jitter_ms,
+                              uint64_t start, uint64_t count, void* out);
 /* Term bytes of a synthetic dictionary term (host / url).  Returns length, writes at most cap bytes. */
 int esgpu_synthetic_term(uint32_t field_bit, uint64_t ord, char* buf, size_t cap);
 /* Copy a device column range back to host (tests compare device vs host generator). */

@@ -40,16 +40,19 @@ def synthetic_dict(field):
     raise KeyError(field)
 
 
-def _host_column(field, num_docs, shard, seed, threads):
+def _host_column(field, num_docs, shard, seed, threads, ts_jitter_ms=0):
     """synthetic_host_column in `threads` concurrent chunks (the C generator releases the GIL)."""
     if threads <= 1 or num_docs < (1 << 22):
-        return synthetic_host_column(field, num_docs, shard=shard, seed=seed)
+        return synthetic_host_column(field, num_docs, shard=shard, seed=seed, ts_jitter_ms=ts_jitter_ms)
     from concurrent.futures import ThreadPoolExecutor
     bounds = [num_docs * i // threads for i in range(threads + 1)]
+    first = synthetic_host_column(field, num_docs, start=0, count=1, shard=shard, seed=seed)
+    out = np.empty(num_docs, dtype=first.dtype)
     with ThreadPoolExecutor(threads) as ex:
-        parts = list(ex.map(lambda i: synthetic_host_column(field, num_docs, start=bounds[i], count=bounds[i + 1] - bounds[i],
-                                                            shard=shard, seed=seed), range(threads)))
-    return np.concatenate(parts)
+        list(ex.map(lambda i: synthetic_host_column(field, num_docs, start=bounds[i], count=bounds[i + 1] - bounds[i],
+                                                    shard=shard, seed=seed, ts_jitter_ms=ts_jitter_ms,
+                                                    out=out[bounds[i]:bounds[i + 1]]), range(threads)))
+    return out
 
 
 def host_threads():
@@ -60,12 +63,12 @@ def host_threads():
     return max(1, min(n, omp) if omp > 0 else n)
 
 
-def synthetic_columns(fields, num_docs, shard=0, seed=0x5EEDE1A5, threads=None):
+def synthetic_columns(fields, num_docs, shard=0, seed=0x5EEDE1A5, threads=None, ts_jitter_ms=0):
     """Host copies of a synthetic shard, in the column-dict format of Engine.upload_segment / oracle.run."""
     threads = host_threads() if threads is None else threads
     cols = {}
     for f in fields:
-        c = {"type": N.SYNTH_TYPES[f], "values": _host_column(f, num_docs, shard, seed, threads)}
+        c = {"type": N.SYNTH_TYPES[f], "values": _host_column(f, num_docs, shard, seed, threads, ts_jitter_ms)}
         if f in ("host", "url"):
             c["terms_blob"] = synthetic_dict(f)
         cols[f] = c

@@ -115,3 +115,29 @@ def test_table_grows_across_segments(engine):
     plan.close()
     for s in segs:
         s.close()
+
+
+@pytest.mark.parametrize("jitter", [60_000, 3_600_000])
+def test_roughly_sorted_timestamps(engine, jitter):
+    """Docs displaced by up to +-1 min / +-1 h (merged segments are only roughly time-ordered): blocks span more hour
+    keys than the LDS window, the rest go through the global-atomic path; results stay bit-exact."""
+    from elasticsearch_amd import reduce
+    import oracle as O
+    from helpers import assert_same, synthetic_columns
+    n = 2_000_000
+    fields = ("host", "@timestamp", "response_time_ms")
+    aggs = [AB.terms("hosts").field("host").size(10).subAggregation(
+                AB.dateHistogram("h").field("@timestamp").interval("1h").subAggregation(AB.stats("rt").field("response_time_ms"))),
+            AB.dateHistogram("m").field("@timestamp").interval("1m").subAggregation(AB.extendedStats("rt").field("response_time_ms"))]
+    want = O.run([(synthetic_columns(fields, n, ts_jitter_ms=jitter), n)], aggs)
+    seg = engine.synthetic_segment(n, fields=fields, ts_jitter_ms=jitter)
+    host_ts = synthetic_columns(("@timestamp",), n, ts_jitter_ms=jitter)["@timestamp"]["values"]
+    assert np.array_equal(seg.read_column("@timestamp", 0, n, np.int64), host_ts)  # device generator == host generator
+    assert np.any(np.diff(host_ts) < 0)
+    plan = engine.plan(aggs)
+    plan.collect(seg)
+    res = plan.build()
+    assert_same(res.to_dict(), want["shards"][0], "shard")
+    assert_same(reduce([res]).to_dict(), want["reduced"], "reduced")
+    plan.close()
+    seg.close()

@@ -26,6 +26,12 @@ for s in $STEPS; do
         tests) run pytest_gpu 1100 python3 -u -m pytest "$R/tests" -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         kbench) run kbench 600 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 ${KBENCH_ONLY:+--only $KBENCH_ONLY} ;;
         bench) run bench 600 python3 "$R/bench.py" ;;
+        jitter) for j in 0 60000 3600000; do
+                    run "kbench_jitter_$j" 300 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 --ts-jitter $j \
+                        --only north_star,config2_dh_ext,date_hist,terms_dh || exit 1
+                done ;;
+        export) run export_bench 300 python3 "$R/tools/export_bench.py" --docs 250000000 --reps 3 ;;
+        shape125) run kbench_125m 300 python3 "$R/tools/kbench.py" --docs 125000000 --reps 5 --shards 8 ;;
         configs) # every BASELINE config at its own shape (1 GPU: the 8 shards of configs 3-5 collected in turn)
               run bench_config2 300 python3 "$R/bench.py" --workload config2 --docs 100000000 --cpu-docs 160000000 &&
               run bench_config3 300 python3 "$R/bench.py" --workload config3 --shards 8 --docs 125000000 --cpu-docs 320000000 &&

@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--docs", type=int, default=1_000_000_000)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--only", default="")
+    ap.add_argument("--ts-jitter", type=int, default=0,
+                    help="@timestamp displacement bound in ms (0 = time-sorted docs; 60000 / 3600000 = roughly sorted)")
+    ap.add_argument("--shards", type=int, default=1, help="number_of_shards of the request (terms shard_size heuristic)")
     args = ap.parse_args()
     only = set(filter(None, args.only.split(",")))
     e = ea.Engine(0)
@@ -51,10 +54,11 @@ def main():
     if "config3_url" in vs:
         fields.add("url")
     t = time.time()
-    seg = e.synthetic_segment(args.docs, fields=tuple(sorted(fields)))
-    print(json.dumps({"generated_s": time.time() - t, "hbm_gb": e.hbm_used() / 1e9}), flush=True)
+    seg = e.synthetic_segment(args.docs, fields=tuple(sorted(fields)), ts_jitter_ms=args.ts_jitter)
+    print(json.dumps({"generated_s": time.time() - t, "hbm_gb": e.hbm_used() / 1e9, "ts_jitter_ms": args.ts_jitter,
+                      "shards": args.shards}), flush=True)
     for name, (aggs, flt) in vs.items():
-        plan = e.plan(aggs, filters=flt)
+        plan = e.plan(aggs, filters=flt, number_of_shards=args.shards)
         ms = []
         steps = []
         parts = {"reset": [], "collect_call": [], "kernel_wait": [], "build": [], "reduce": []}
@@ -79,7 +83,7 @@ def main():
                     parts[key].append((b - a) * 1e3)
         kms = sorted(ms)[len(ms) // 2]
         gbs = nbytes / (kms / 1e3) / 1e9
-        print(json.dumps({"name": name, "kernel_ms": round(kms, 4), "bytes": nbytes, "gbs": round(gbs, 1),
+        print(json.dumps({"name": name, "ts_jitter_ms": args.ts_jitter, "kernel_ms": round(kms, 4), "bytes": nbytes, "gbs": round(gbs, 1),
                           "frac": round(gbs / 8000, 4), "path": path, "step_ms": round(sorted(steps)[len(steps) // 2], 3),
                           "docs_per_s": args.docs / (kms / 1e3),
                           "parts_ms": {k: round(sorted(v)[len(v) // 2], 3) for k, v in parts.items()}}), flush=True)
