@@ -155,6 +155,7 @@ SIGNATURES = [
     ("esgpu_plan_destroy", ctypes.c_int, [_VP]),
     ("esgpu_plan_last_collect_stats", ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64),
                                                      ctypes.POINTER(ctypes.c_int32)]),
+    ("esgpu_plan_last_build_stats", ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     ("esgpu_plan_shard_mergeable", ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_int32)]),
     ("esgpu_result_free", ctypes.c_int, [ctypes.POINTER(Result)]),
     ("esgpu_reduce", ctypes.c_int, [ctypes.POINTER(ctypes.POINTER(Result)), ctypes.c_int32,

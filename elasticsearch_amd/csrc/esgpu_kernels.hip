@@ -91,6 +91,14 @@ constexpr int kWG = 512;                         // threads per workgroup (8 wav
 constexpr int kVec = 4;                          // consecutive docs per thread per iteration
 constexpr int kIterDocs = kWG * kVec;            // 2048
 constexpr int kItersPerBlock = kBlockDocs / kIterDocs;  // 4
+#ifndef ESGPU_MAX_PASSES  // passes over a block whose keys span more than the LDS window, before global atomics
+#define ESGPU_MAX_PASSES 8
+#endif
+constexpr int kMaxPasses = ESGPU_MAX_PASSES;
+#ifndef ESGPU_GROUP_BLOCKS  // blocks per multi-pass group
+#define ESGPU_GROUP_BLOCKS 4
+#endif
+constexpr uint32_t kGroup = ESGPU_GROUP_BLOCKS;
 #ifndef ESGPU_NBUF_NARROW  // load buffers in flight per thread for shapes reading one narrow column
 #define ESGPU_NBUF_NARROW 2  // measured: 4 no faster for terms(host), 4 % slower for date_histogram
 #endif
@@ -234,11 +242,14 @@ __device__ __forceinline__ void add_value(const Acc& a, uint32_t c, double x, bo
 }
 
 // Per-doc update.  `slot` is the key index relative to the accumulator's first slot (window or grid).
+// `outer` = false in the extra passes over a multi-pass block (its docs' terms were counted in the first pass).
 template <bool ORD, bool HIST, int MET, bool LDS, int MS>
 __device__ __forceinline__ void update_doc(const CollectParams& P, const Acc& a, uint32_t T, bool has_t, uint32_t t,
-                                           bool has_h, uint32_t slot, bool mpres, double x) {
-    if (P.ocnt_mode == OCNT_TERMS && has_t) {
-        if (LDS) atomicAdd(&a.ocnt32[t], 1u); else atomicAdd(&a.ocnt64[t], 1ull);
+                                           bool has_h, uint32_t slot, bool mpres, double x, bool outer) {
+    if (P.ocnt_mode == OCNT_TERMS) {
+        if (has_t && outer) {
+            if (LDS) atomicAdd(&a.ocnt32[t], 1u); else atomicAdd(&a.ocnt64[t], 1ull);
+        }
     } else if (!LDS && P.ocnt_mode == OCNT_TERMS_DERIVED && has_t && has_h) {
         atomicAdd(&a.ocnt64[t], 1ull);
     } else if (P.ocnt_mode == OCNT_HIST && has_h) {
@@ -343,9 +354,68 @@ __device__ __forceinline__ void run_flush(const CollectParams& P, const Acc& a, 
     run_reset(r);
 }
 
+// Several run accumulators per thread (runs_for<MET>): roughly time-ordered data (a doc displaced by up to an hour) alternates between
+// neighbouring keys, which a single run would flush to LDS on almost every doc (conflicting LDS atomics on ~3
+// addresses per wave).  A miss replaces the runs round-robin.
+#ifndef ESGPU_RUNS  // run accumulators with a metric (measured: 3 takes config 2 at +-1 h jitter from 4.6 to 3.0 ms)
+#define ESGPU_RUNS 3
+#endif
+// counting only (MET 0): one run -- a count flush is a single LDS add, and the run array would go to scratch
+template <int MET> constexpr int runs_for() { return MET == 0 ? 1 : ESGPU_RUNS; }
+template <int NR>
+struct Runs {
+    Run r[NR];
+    uint32_t victim;
+};
+template <int NR>
+__device__ __forceinline__ void runs_reset(Runs<NR>& R) {
+#pragma unroll
+    for (int k = 0; k < NR; ++k) run_reset(R.r[k]);
+    R.victim = 0;
+}
+template <int MET, int MS, int NR>
+__device__ __forceinline__ void runs_flush(const CollectParams& P, const Acc& a, Runs<NR>& R) {
+#pragma unroll
+    for (int k = 0; k < NR; ++k) run_flush<MET, MS>(P, a, R.r[k]);
+}
+template <int MET, int MS, int NR>
+__device__ __forceinline__ void runs_add(const CollectParams& P, const Acc& a, Runs<NR>& R, uint32_t slot, bool mpres, double x) {
+    int hit = -1;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) hit = R.r[k].slot == slot ? k : hit;
+    if (hit < 0) {
+        hit = NR == 1 ? 0 : (int)R.victim;
+#pragma unroll
+        for (int k = 0; k < NR; ++k)
+            if (k == hit) {
+                run_flush<MET, MS>(P, a, R.r[k]);
+                R.r[k].slot = slot;
+            }
+        if (NR > 1) R.victim = R.victim + 1 == (uint32_t)NR ? 0u : R.victim + 1;
+    }
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+        if (k != hit) continue;
+        Run& run = R.r[k];
+        ++run.cnt;
+        if (MET > 0 && mpres) {
+            ++run.vc;
+            run.sum += x;
+            if (MET >= 3) run.sq += x * x;
+            if (MET >= 2) {
+                const bool nan = x != x;
+                const unsigned long long e = sortable(x);
+                const unsigned long long emn = nan ? 0ull : e, emx = nan ? ~0ull : e;
+                run.mn = emn < run.mn ? emn : run.mn;
+                run.mx = emx > run.mx ? emx : run.mx;
+            }
+        }
+    }
+}
+
 template <bool ORD, bool HIST, int MET, bool LDS, bool KT, int MS>
 __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, const Doc4& d, uint32_t T, int64_t base,
-                                         uint32_t win0, Run& run) {
+                                         uint32_t win0, Runs<runs_for<MET>()>& run, uint32_t mw = 0, bool outer = true) {
     uint32_t slot[kVec];
     bool hv_ok[kVec];
 #pragma unroll
@@ -355,7 +425,15 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
         if (HIST) {
             hv_ok[j] = (d.hpres >> j) & 1;
             if (LDS) {
-                slot[j] = KT ? (uint32_t)(key_index<KT>(P, d.hv[j]) - (int64_t)win0) : slot_of(P, d.hv[j], base);
+                if (KT) {
+                    const int64_t k = key_index<KT>(P, d.hv[j]) - (int64_t)win0;
+                    slot[j] = (uint32_t)k;
+                    if (mw) hv_ok[j] = hv_ok[j] && k >= 0 && k < (int64_t)mw;
+                } else {
+                    slot[j] = slot_of(P, d.hv[j], base);
+                    // 64-bit range test: slot_of's 32-bit fast path wraps for values 2^32 past the window
+                    if (mw) hv_ok[j] = hv_ok[j] && (uint64_t)d.hv[j] - (uint64_t)base < (uint64_t)mw * (uint64_t)P.interval;
+                }
             } else {
                 const int64_t k = key_index<KT>(P, d.hv[j]);
                 hv_ok[j] = hv_ok[j] && k >= 0 && k < (int64_t)P.H;
@@ -367,24 +445,7 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
 #pragma unroll
         for (int j = 0; j < kVec; ++j) {
             if (!((d.ok >> j) & 1) || !hv_ok[j]) continue;
-            if (slot[j] != run.slot) {
-                run_flush<MET, MS>(P, a, run);
-                run.slot = slot[j];
-            }
-            ++run.cnt;
-            if (MET > 0 && ((d.mpres >> j) & 1)) {
-                const double x = d.mv[j];
-                ++run.vc;
-                run.sum += x;
-                if (MET >= 3) run.sq += x * x;
-                if (MET >= 2) {
-                    const bool nan = x != x;
-                    const unsigned long long e = sortable(x);
-                    const unsigned long long emn = nan ? 0ull : e, emx = nan ? ~0ull : e;
-                    run.mn = emn < run.mn ? emn : run.mn;
-                    run.mx = emx > run.mx ? emx : run.mx;
-                }
-            }
+            runs_add<MET, MS>(P, a, run, slot[j], MET > 0 && ((d.mpres >> j) & 1), MET > 0 ? d.mv[j] : 0.0);
         }
         return;
     }
@@ -394,7 +455,7 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
         const uint32_t t = ORD ? d.ord[j] : 0u;
         const bool has_t = ORD ? (t != kMissingOrd && t < T) : true;
         update_doc<ORD, HIST, MET, LDS, MS>(P, a, T, has_t, t, hv_ok[j], slot[j], MET > 0 && ((d.mpres >> j) & 1),
-                                        MET > 0 ? d.mv[j] : 0.0);
+                                        MET > 0 ? d.mv[j] : 0.0, outer);
     }
 }
 
@@ -525,68 +586,119 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
     bool dirty = false;
     int64_t base = HIST ? P.key0 * P.interval + P.offset : 0;  // value of the first LDS slot
 
-    Run run;
-    run_reset(run);
+    Runs<runs_for<MET>()> run;
+    runs_reset(run);
     // software pipeline over two buffers: each is reloaded (iteration i + 2) right after it is processed, so one
     // buffer's loads are in flight while the other is processed.  Loads are unconditional (past the end: the last
-    // iteration's docs again, never processed) and no loaded register is copied: a conditional load or a register
+    // block's docs again, never processed) and no loaded register is copied: a conditional load or a register
     // copy of a load's result makes the compiler wait vmcnt(0), which drains the other buffer's loads as well.
+    //
+    // Multi-pass groups (roughly time-ordered data whose blocks span more keys than the window): the blocks are taken
+    // in groups of kGroup; a group holding a block that spans more than W keys is replayed once per W keys of the
+    // group's key range, each pass accumulating only the docs whose key falls in its window (replays re-read the
+    // group from L2 / MALL).  One window flush per pass of a group instead of one per pass of every block: with
+    // +-1 h jitter the flushes (T x W cells of global atomics) cost 4x the column read when taken per block.  The
+    // replay is part of the schedule the prefetches follow -- the pass count is known at the group's first
+    // iteration, before any replayed iteration is prefetched -- so it costs no extra load buffers.  Groups whose
+    // blocks each fit the window are taken block by block, the window sliding as before.
     const uint32_t tid4 = threadIdx.x * kVec;
-    const uint32_t n_it = (b_end - b_begin) * kItersPerBlock;  // a multiple of kItersPerBlock (even)
-    auto doc_of = [&](uint32_t i) {
-        i = min(i, n_it - 1);
-        return (b_begin + i / kItersPerBlock) * kBlockDocs + (i % kItersPerBlock) * kIterDocs + tid4;
-    };
     // shapes that read few bytes per doc (one ordinal or one key column) keep 4 buffers in flight, the rest 2 (their
     // buffers are 5x larger; 4 would cost occupancy).  kItersPerBlock (4) is a multiple of either.
     constexpr int kBuf = (MET == 0 && !(ORD && HIST)) ? ESGPU_NBUF_NARROW : 2;
     static_assert(kItersPerBlock % kBuf == 0, "buffers per block");
     Doc4 q[kBuf];
 #pragma unroll
-    for (int k = 0; k < kBuf; ++k) load_docs<ORD, HIST, MET, VK>(P, doc_of(k), q[k]);
+    for (int k = 0; k < kBuf; ++k) load_docs<ORD, HIST, MET, VK>(P, b_begin * kBlockDocs + k * kIterDocs + tid4, q[k]);
 
     bool use_lds = P.lds_mode != 0;
-    auto step = [&](uint32_t i, Doc4& q) {
-        if (i % kItersPerBlock == 0) {
-            // ---- per-block decision (wave-uniform: every lane reads the same zone-map words) ----
+    uint32_t cb = b_begin;                               // block being processed
+    uint32_t gb = b_begin, ge = min(b_begin + kGroup, b_end);  // its group
+    uint32_t pass = 0, npass = 1;                        // npass > 1: a multi-pass group
+    auto slide_to = [&](uint32_t k0) {
+        if (dirty) {
+            if (!ORD) runs_flush<MET, kMS>(P, s, run);
+            flush_window<MET, kMS>(P, s, T, W, win0, ncp);
+        }
+        dirty = false;
+        win0 = k0;
+        win_set = true;
+        base = (P.key0 + (int64_t)win0) * P.interval + P.offset;
+    };
+    auto step = [&](uint32_t it, Doc4& q) {
+        if (it == 0) {
+            // ---- per-group / per-block decisions (wave-uniform: every lane reads the same zone-map words) ----
             // readfirstlane: the zone-map words become scalar loads (lgkmcnt), not vector loads whose vmcnt wait
             // would drain the prefetched buffers
-            const uint32_t b = __builtin_amdgcn_readfirstlane(b_begin + i / kItersPerBlock);
-            use_lds = P.lds_mode != 0;
-            if (use_lds && HIST && P.windowed) {
-                const int64_t zmn = P.zmin[b], zmx = P.zmax[b];
-                if (zmn <= zmx) {  // block has at least one timestamp
-                    const int64_t kmn = key_index<KT>(P, zmn);
-                    const int64_t kmx = key_index<KT>(P, zmx);
-                    if (kmx - kmn + 1 > (int64_t)W) {
-                        use_lds = false;  // block spans more keys than the window: global atomics for this block
-                    } else if (!win_set || kmn < (int64_t)win0 || kmx >= (int64_t)win0 + (int64_t)W) {
-                        if (dirty) {
-                            if (!ORD) run_flush<MET, kMS>(P, s, run);
-                            flush_window<MET, kMS>(P, s, T, W, win0, ncp);
-                        }
-                        dirty = false;
-                        win0 = (uint32_t)kmn;
-                        win_set = true;
-                        base = (P.key0 + (int64_t)win0) * P.interval + P.offset;
+            const uint32_t b = __builtin_amdgcn_readfirstlane(cb);
+            if (cb == gb && pass == 0) {
+                use_lds = P.lds_mode != 0;
+                npass = 1;
+                if (use_lds && HIST && P.windowed) {
+                    int64_t gmn = INT64_MAX, gmx = INT64_MIN, maxspan = 0;
+                    for (uint32_t x = b; x < ge; ++x) {
+                        const int64_t zmn = P.zmin[x], zmx = P.zmax[x];
+                        if (zmn > zmx) continue;  // no timestamp in the block
+                        const int64_t kmn = key_index<KT>(P, zmn), kmx = key_index<KT>(P, zmx);
+                        gmn = kmn < gmn ? kmn : gmn;
+                        gmx = kmx > gmx ? kmx : gmx;
+                        maxspan = kmx - kmn + 1 > maxspan ? kmx - kmn + 1 : maxspan;
                     }
+                    if (maxspan > (int64_t)W) {
+                        const int64_t span = gmx - gmn + 1;
+                        if (span > (int64_t)W * kMaxPasses) {
+                            use_lds = false;  // the group spans too many keys: global atomics for it
+                        } else {
+                            npass = (uint32_t)((span + W - 1) / W);
+                            if (!win_set || (uint32_t)gmn != win0) slide_to((uint32_t)gmn);
+                        }
+                    }
+                }
+            } else if (HIST && npass > 1 && cb == gb) {  // next pass over a multi-pass group: the window moves up W keys
+                slide_to(win0 + W);
+            }
+            if (HIST && use_lds && P.windowed && npass == 1) {  // block by block: slide the window when it must
+                const int64_t zmn = P.zmin[b], zmx = P.zmax[b];
+                if (zmn <= zmx) {
+                    const int64_t kmn = key_index<KT>(P, zmn), kmx = key_index<KT>(P, zmx);
+                    if (!win_set || kmn < (int64_t)win0 || kmx >= (int64_t)win0 + (int64_t)W) slide_to((uint32_t)kmn);
                 }
             }
         }
         if (use_lds) {
-            process4<ORD, HIST, MET, true, KT, kMS>(P, s, q, T, base, win0, run);
+            process4<ORD, HIST, MET, true, KT, kMS>(P, s, q, T, base, win0, run, npass > 1 ? W : 0u, pass == 0);
             dirty = true;
         } else {
             process4<ORD, HIST, MET, false, KT, kMS>(P, g, q, T, base, win0, run);
         }
-        load_docs<ORD, HIST, MET, VK>(P, doc_of(i + kBuf), q);
+        // prefetch kBuf iterations ahead along the schedule (next block of the group, the group's next pass, or the
+        // next group)
+        uint32_t nit = it + kBuf, nb = cb;
+        if (nit >= (uint32_t)kItersPerBlock) {
+            nit -= kItersPerBlock;
+            nb = cb + 1;
+            if (nb == ge && pass + 1 < npass) nb = gb;
+            nb = min(nb, b_end - 1);
+        }
+        load_docs<ORD, HIST, MET, VK>(P, nb * kBlockDocs + nit * kIterDocs + tid4, q);
     };
-    for (uint32_t i = 0; i < n_it; i += kBuf) {
+    while (cb < b_end) {
+        for (uint32_t it = 0; it < (uint32_t)kItersPerBlock; it += kBuf) {
 #pragma unroll
-        for (int k = 0; k < kBuf; ++k) step(i + k, q[k]);
+            for (int k = 0; k < kBuf; ++k) step(it + k, q[k]);
+        }
+        if (++cb == ge) {
+            if (++pass < npass) {
+                cb = gb;
+            } else {
+                pass = 0;
+                npass = 1;
+                gb = ge;
+                ge = min(gb + kGroup, b_end);
+            }
+        }
     }
     if (P.lds_mode && (dirty || !(HIST && P.windowed))) {
-        if (!ORD) run_flush<MET, kMS>(P, s, run);
+        if (!ORD) runs_flush<MET, kMS>(P, s, run);
         flush_window<MET, kMS>(P, s, T, W, win0, ncp);
     }
 }
@@ -1004,8 +1116,11 @@ __global__ __launch_bounds__(256) void hll_lc_kernel(HllParams P) {
 void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
     const uint32_t n = p.n_docs;
     const uint32_t m = 1u << p.p;
-    // phases [0, 16m), then x4 each: every register has seen ~16 hashes after the first cut, so the floor (min
-    // register) starts to rise, and each later phase reads registers only for hashes longer than the floor
+    // phases [0, 4m), then x4 each: every register has seen ~4 hashes after the first cut, so the floor (min
+    // register) starts to rise, and each later phase reads registers only for hashes longer than the floor.  The cuts
+    // are positions in the request's whole value stream: a later segment (p.seen values already in the registers)
+    // continues the sequence -- its first phase refreshes the floor and snapshot and runs the LDS pass at once,
+    // instead of restarting with a floor-0 phase that reads a register for every hash.
     std::vector<uint32_t> cuts{0};
 #ifndef ESGPU_HLL_GROW
 #define ESGPU_HLL_GROW 4
@@ -1014,8 +1129,9 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
 #define ESGPU_HLL_CUT0 4  // measured: 4 beats 16 by 3-4 % (phase 0 reads and raises registers for every hash)
 #endif
     uint64_t c = (uint64_t)m * ESGPU_HLL_CUT0;
-    while (c < n) {
-        cuts.push_back((uint32_t)c & ~3u);
+    while (c <= p.seen) c *= ESGPU_HLL_GROW;
+    while (c < p.seen + n) {
+        cuts.push_back((uint32_t)(c - p.seen) & ~3u);
         c *= ESGPU_HLL_GROW;
     }
     cuts.push_back(n);
@@ -1026,16 +1142,33 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
 #endif
     const bool lds = ESGPU_HLL_LDS && fast && p.snap && (p.kind == HLL_I64 || p.kind == HLL_F64) && p.p >= 4;
     const uint32_t floor_grid = std::max(1u, std::min(64u, m / 4096));
+    // floor (and group floors + LDS snapshot) of the registers as they stand
+    auto refresh = [&]() {
+        (void)hipMemsetAsync(p.floor, 0xFF, 4, st);
+        if (fast) {
+            const uint32_t ng = m >= kHllGroup ? m / kHllGroup : 1u;
+            hipLaunchKernelGGL(hll_group_floor_kernel, dim3((ng + 15) / 16), dim3(1024), 0, st, (const unsigned int*)p.regs, m,
+                               p.gfloor, p.floor);
+            if (lds)
+                hipLaunchKernelGGL(hll_snapshot_kernel, dim3((hll_snap_bytes(m) + 255) / 256), dim3(256), 0, st, (const unsigned int*)p.regs, m,
+                                   (const unsigned int*)p.floor, p.snap);
+        } else {
+            hipLaunchKernelGGL(hll_floor_kernel, dim3(floor_grid), dim3(1024), 0, st, (const unsigned int*)p.regs, m, p.floor);
+        }
+    };
+    const bool warm = p.seen >= (uint64_t)m * ESGPU_HLL_CUT0;  // the registers already passed the first cut
+    if (warm) refresh();
     for (size_t ph = 0; ph + 1 < cuts.size(); ++ph) {
         const uint32_t span = cuts[ph + 1] - cuts[ph];
         if (span == 0) continue;
+        const bool floored = warm || ph > 0;
         // contiguous range per workgroup, a multiple of 4 docs, at least 4 iterations of 1024 docs (the first phase is
         // small and latency-bound: every hash reads a register there, so it needs the whole chip)
         uint32_t wgs = std::max(1u, std::min(wgs_max, span / (kHllIter * 4)));
         const uint32_t per = ((span + wgs - 1) / wgs + 3) & ~3u;
         wgs = (span + per - 1) / per;
-        const unsigned int* fl = ph == 0 ? (const unsigned int*)nullptr : (const unsigned int*)p.floor;
-        if (lds && ph > 0) {
+        const unsigned int* fl = floored ? (const unsigned int*)p.floor : (const unsigned int*)nullptr;
+        if (lds && floored) {
             // one 1024-thread workgroup per CU (128 KB of nibbles at p = 18), more for smaller p
             const uint32_t per_cu = std::max(1u, std::min(4u, (uint32_t)(160u * 1024u / (hll_snap_bytes(m) + 1024u))));
             uint32_t lw = std::max(1u, std::min(cus * per_cu, span / (kHllLdsIter * 4)));
@@ -1053,19 +1186,7 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
             hipLaunchKernelGGL(hll_registers_fast_kernel<HLL_ORD>, dim3(wgs), dim3(kHllWG), 0, st, p, cuts[ph], cuts[ph + 1], per, fl);
         else
             hipLaunchKernelGGL(hll_registers_kernel, dim3(wgs), dim3(kHllWG), 0, st, p, cuts[ph], cuts[ph + 1], per, fl);
-        if (ph + 2 < cuts.size()) {
-            (void)hipMemsetAsync(p.floor, 0xFF, 4, st);
-            if (fast) {
-                const uint32_t ng = m >= kHllGroup ? m / kHllGroup : 1u;
-                hipLaunchKernelGGL(hll_group_floor_kernel, dim3((ng + 15) / 16), dim3(1024), 0, st, (const unsigned int*)p.regs, m,
-                                   p.gfloor, p.floor);
-                if (lds)
-                    hipLaunchKernelGGL(hll_snapshot_kernel, dim3((hll_snap_bytes(m) + 255) / 256), dim3(256), 0, st, (const unsigned int*)p.regs, m,
-                                       (const unsigned int*)p.floor, p.snap);
-            } else {
-                hipLaunchKernelGGL(hll_floor_kernel, dim3(floor_grid), dim3(1024), 0, st, (const unsigned int*)p.regs, m, p.floor);
-            }
-        }
+        if (ph + 2 < cuts.size()) refresh();
     }
     (void)hipMemsetAsync(p.nonzero, 0, 4, st);  // recount over the registers (they accumulate across segments)
     hipLaunchKernelGGL(hll_nonzero_kernel, dim3(floor_grid), dim3(1024), 0, st, (const unsigned int*)p.regs, m, p.nonzero);

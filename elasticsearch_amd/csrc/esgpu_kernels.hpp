@@ -111,6 +111,7 @@ struct HllParams {
     unsigned char* snap;        // scratch: registers as 4-bit lower bounds over the floor ([2^p / 2], 16-byte aligned)
     uint32_t lc_mask;
     uint32_t lc_threshold;
+    uint64_t seen;              // values the registers already hold from earlier segments of this request
 };
 
 struct GatherParams {

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -797,6 +798,7 @@ struct Pipeline {
     int p = 14;
     DevBuf regs, lc_set, lc_count;
     uint32_t lc_mask = 0, lc_threshold = 0;
+    uint64_t hll_seen = 0;           // values hashed into the registers by earlier segments of this request
     // post_collection products
     std::vector<uint8_t> h_regs;
     std::vector<uint32_t> h_lc;
@@ -852,6 +854,7 @@ struct esgpu_plan {
     bool collected = false, posted = false;
     double last_ms = 0;
     uint64_t last_bytes = 0;
+    double b_wait = 0, b_total = 0;  // last build: stream waits / whole call (ms)
     int32_t last_path = 0;
     // per-request scratch, reused across requests
     Scratch s_accept, s_tcnt, s_rows, s_dst[6];
@@ -1670,7 +1673,10 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
                                     d_accept) ? ret : 0;
 
     // LDS sizing: the whole grid if it fits, else a sliding window over the key dimension (time-sorted data)
-    const size_t kLdsPair = 64 * 1024, kLdsMax = 150 * 1024;
+#ifndef ESGPU_LDS_PAIR  // LDS budget of a window that keeps two workgroups per CU
+#define ESGPU_LDS_PAIR (64 * 1024)
+#endif
+    const size_t kLdsPair = ESGPU_LDS_PAIR, kLdsMax = 150 * 1024;
     uint32_t W = LH;
     size_t lds = collect_lds_bytes(LT, W, L_met, L_vcnt, L_ocnt);
     P.lds_mode = 1;
@@ -1827,7 +1833,9 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
     H.snap = pl.lc_count.as<unsigned char>() + hll_snap_offset(1u << pl.p);
     H.lc_mask = pl.lc_mask;
     H.lc_threshold = pl.lc_threshold;
+    H.seen = pl.hll_seen;
     if (H.n_docs == 0) return false;
+    pl.hll_seen += H.n_docs;
     HIPX(hipEventRecord(pl.e0, p->stream));
     launch_hll(H, (uint32_t)p->ctx->cus, p->stream);
     HIPX(hipGetLastError());
@@ -1891,17 +1899,35 @@ extern "C" int esgpu_plan_last_collect_stats(const esgpu_plan* cp, double* kerne
     });
 }
 
+// build-phase stream waits, timed (esgpu_plan_last_build_stats: device wait vs host assembly)
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static void bsync(esgpu_plan* p) {
+    const double t0 = now_ms();
+    HIPX(hipStreamSynchronize(p->stream));
+    p->b_wait += now_ms() - t0;
+}
+
+extern "C" int esgpu_plan_last_build_stats(const esgpu_plan* p, double* total_ms, double* wait_ms) {
+    return guarded([&] {
+        require(p && total_ms && wait_ms, ESGPU_ERR_INVALID, "null argument");
+        *total_ms = p->b_total;
+        *wait_ms = p->b_wait;
+    });
+}
+
 extern "C" int esgpu_plan_post_collection(esgpu_plan* p) {
     return guarded([&] {
         require(p != nullptr, ESGPU_ERR_INVALID, "null plan");
         HIPX(hipSetDevice(p->ctx->device));
-        HIPX(hipStreamSynchronize(p->stream));
+        bsync(p);
         for (Pipeline& pl : p->pipes) {
             if (pl.kind != 1 || !pl.allocated) continue;
             // [0] = distinct encoded hashes inserted (LC pass), [1] = non-zero registers (register pass)
             uint32_t* cnt = (uint32_t*)p->h_tcnt.ensure(16);
             HIPX(hipMemcpyAsync(cnt, pl.lc_count.p, 8, hipMemcpyDeviceToHost, p->stream));
-            HIPX(hipStreamSynchronize(p->stream));
+            bsync(p);
             const uint32_t m = 1u << pl.p;
             pl.any_value = cnt[0] > 0 || cnt[1] > 0;
             if (cnt[1] <= pl.lc_threshold && cnt[0] <= pl.lc_threshold) {  // LINEAR_COUNTING: the distinct encoded hashes
@@ -1909,7 +1935,7 @@ extern "C" int esgpu_plan_post_collection(esgpu_plan* p) {
                 const size_t cap = (size_t)pl.lc_mask + 1;
                 uint32_t* set = (uint32_t*)p->h_dst[0].ensure(cap * 4);
                 HIPX(hipMemcpyAsync(set, pl.lc_set.p, cap * 4, hipMemcpyDeviceToHost, p->stream));
-                HIPX(hipStreamSynchronize(p->stream));
+                bsync(p);
                 pl.h_lc.clear();
                 for (size_t i = 0; i < cap; ++i) if (set[i]) pl.h_lc.push_back(set[i]);
                 std::sort(pl.h_lc.begin(), pl.h_lc.end());
@@ -1921,7 +1947,7 @@ extern "C" int esgpu_plan_post_collection(esgpu_plan* p) {
                 HIPX(hipGetLastError());
                 uint8_t* r = (uint8_t*)p->h_dst[0].ensure(m);
                 HIPX(hipMemcpyAsync(r, d8, m, hipMemcpyDeviceToHost, p->stream));
-                HIPX(hipStreamSynchronize(p->stream));
+                bsync(p);
                 pl.h_regs.assign(r, r + m);
             }
         }
@@ -2026,7 +2052,7 @@ static void gather_cards(esgpu_plan* p, Pipeline& pl, const std::vector<uint32_t
             launch_gather_bytes(dcells, n, pt.row, pt.src->as<uint8_t>(), d, st);
             HIPX(hipGetLastError());
             HIPX(hipMemcpyAsync(pt.host, d, (size_t)n * pt.row, hipMemcpyDeviceToHost, st));
-            HIPX(hipStreamSynchronize(st));  // s_dst[5] is reused by the next part
+            bsync(p);  // s_dst[5] is reused by the next part
         }
     }
 }
@@ -2088,6 +2114,44 @@ static void append_leaf(const esgpu_plan* p, const Pipeline& pl, int j, size_t c
     r.min.push_back(m.min);
     r.max.push_back(m.max);
     r.sumsq.push_back(m.sq);
+}
+
+// instances of leaf j of a pipeline for the given host cells, appended in order (columnar: one resize per array)
+static void append_leaves(const esgpu_plan* p, const Pipeline& pl, int j, const std::vector<uint32_t>& cells, Block& r) {
+    const int32_t type = p->specs[pl.metrics[j]].s.type;
+    if (type == ESGPU_AGG_CARDINALITY) {
+        for (uint32_t c : cells) append_leaf(p, pl, j, c, r);
+        return;
+    }
+    const size_t n0 = r.count.size(), m = cells.size();
+    r.n += m;
+    r.count.resize(n0 + m);
+    r.sum.resize(n0 + m);
+    r.min.resize(n0 + m);
+    r.max.resize(n0 + m);
+    r.sumsq.resize(n0 + m);
+    for (size_t i = 0; i < m; ++i) {
+        const MetricCell mc = metric_cell(p, pl, j, cells[i]);
+        r.count[n0 + i] = mc.count;
+        r.sum[n0 + i] = mc.sum;
+        r.min[n0 + i] = mc.min;
+        r.max[n0 + i] = mc.max;
+        r.sumsq[n0 + i] = mc.sq;
+    }
+}
+
+// histogram buckets of the given key slots (host cells `cells`, counts `counts[i]`), appended to the open instance
+static void append_hist_buckets(const Pipeline& B, const std::vector<uint32_t>& slots, const std::vector<int64_t>& counts,
+                                Block& r) {
+    const size_t n0 = r.key.size(), m = slots.size();
+    r.key.resize(n0 + m);
+    r.bcount.resize(n0 + m);
+    r.berr.resize(n0 + m, 0);
+    r.term_off.resize(r.term_off.size() + m, r.term_pool.size());
+    for (size_t i = 0; i < m; ++i) {
+        r.key[n0 + i] = key_value(B, slots[i]);
+        r.bcount[n0 + i] = counts[i];
+    }
 }
 
 static Block leaf_proto(const esgpu_plan* p, int spec) {
@@ -2223,7 +2287,7 @@ static Block build_metric_root(esgpu_plan* p, const Group& g) {
     Block r = leaf_proto(p, g.root).like();
     if (!pl.allocated) { r.append_empty(); return r; }
     fetch_grid(p, pl);
-    HIPX(hipStreamSynchronize(p->stream));
+    bsync(p);
     append_leaf(p, pl, 0, 0, r);
     return r;
 }
@@ -2277,7 +2341,7 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
         HIPX(hipGetLastError());
         unsigned long long* hk = (unsigned long long*)p->h_keys.ensure(((size_t)kk + 1) * 8);
         HIPX(hipMemcpyAsync(hk, dk, ((size_t)kk + 1) * 8, hipMemcpyDeviceToHost, st));
-        HIPX(hipStreamSynchronize(st));
+        bsync(p);
         other = (int64_t)hk[kk];
         for (uint32_t i = 0; i < (uint32_t)k_req; ++i) {
             const unsigned long long key = hk[i];
@@ -2294,7 +2358,7 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
         unsigned long long* tcnt = (unsigned long long*)p->h_tcnt.ensure((size_t)T * 8);
         HIPX(hipMemcpyAsync(tcnt, dcnt, (size_t)T * 8, hipMemcpyDeviceToHost, st));
         if (agg_order) fetch_grid(p, p->pipes[ord_ref.pipe]);  // every ordinal's metric partials
-        HIPX(hipStreamSynchronize(st));
+        bsync(p);
         const Pipeline* OP = agg_order ? &p->pipes[ord_ref.pipe] : nullptr;
         top = select_terms(tn.s, tcnt, (uint32_t)P0.value_count, &other,
                            [&](uint32_t ord) { return order_value(p, tn, *OP, ord_ref.leaf, ord); });
@@ -2309,7 +2373,7 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
         Pipeline& pl = p->pipes[pi];
         if (pl.allocated) fetch_rows(p, pl, drows, k);
     }
-    HIPX(hipStreamSynchronize(st));
+    bsync(p);
     for (int pi : g.pipes) {
         Pipeline& pl = p->pipes[pi];
         if (!pl.allocated || pl.cards.empty()) continue;
@@ -2324,6 +2388,17 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
             other -= top[i].count;
         }
     }
+    for (const ChildSrc& kid : g.kids) {  // every pipeline of a bucket child shares its key grid
+        if (!kid.bucket) continue;
+        const Pipeline& B0 = p->pipes[kid.pipes[0]];
+        for (const LeafRef& l : kid.grand) {
+            const Pipeline& L = p->pipes[l.pipe];
+            require(!B0.allocated || (L.H == B0.H && L.key0 == B0.key0), ESGPU_ERR_DEVICE,
+                    "sibling pipelines disagree on the key grid");
+        }
+    }
+    std::vector<uint32_t> slots, cells;
+    std::vector<int64_t> counts;
     begin_instance(r, other);
     for (uint32_t i = 0; i < k; ++i) {
         const std::string term = plan_term(p, P0, top[i].ord);
@@ -2343,16 +2418,19 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
             const Pipeline& B0 = p->pipes[kid.pipes[0]];
             if (!B0.allocated) { sub.append_empty(); continue; }
             begin_instance(sub, 0);
+            const unsigned long long* crow = B0.hc.cnt + (size_t)i * B0.H;
+            slots.clear();
+            cells.clear();
+            counts.clear();
             for (uint32_t s = 0; s < B0.H; ++s) {
-                const size_t c = (size_t)i * B0.H + s;
-                if (B0.hc.cnt[c] == 0) continue;
-                push_bucket(sub, key_value(B0, s), nullptr, (int64_t)B0.hc.cnt[c]);
-                for (size_t gj = 0; gj < kid.grand.size(); ++gj) {
-                    const Pipeline& L = p->pipes[kid.grand[gj].pipe];
-                    require(L.H == B0.H && L.key0 == B0.key0, ESGPU_ERR_DEVICE, "sibling pipelines disagree on the key grid");
-                    append_leaf(p, L, kid.grand[gj].leaf, c, sub.subs[gj]);
-                }
+                if (crow[s] == 0) continue;
+                slots.push_back(s);
+                cells.push_back(i * B0.H + s);
+                counts.push_back((int64_t)crow[s]);
             }
+            append_hist_buckets(B0, slots, counts, sub);
+            for (size_t gj = 0; gj < kid.grand.size(); ++gj)
+                append_leaves(p, p->pipes[kid.grand[gj].pipe], kid.grand[gj].leaf, cells, sub.subs[gj]);
             end_instance(sub);
         }
     }
@@ -2375,7 +2453,7 @@ static Block build_hist_root(esgpu_plan* p, const Group& g) {
         ocnt = (unsigned long long*)P0.h_ocnt.ensure((size_t)P0.H * 8);
         HIPX(hipMemcpyAsync(ocnt, P0.g_ocnt.p, (size_t)P0.H * 8, hipMemcpyDeviceToHost, st));
     }
-    HIPX(hipStreamSynchronize(st));
+    bsync(p);
     for (int pi : g.pipes) {
         Pipeline& pl = p->pipes[pi];
         if (!pl.allocated || pl.cards.empty()) continue;
@@ -2383,23 +2461,31 @@ static Block build_hist_root(esgpu_plan* p, const Group& g) {
         for (size_t i = 0; i < cells.size(); ++i) cells[i] = (uint32_t)i;
         gather_cards(p, pl, cells);
     }
-    begin_instance(r, 0);
+    // the buckets: key slots with a doc count (columnar fill), then each child over those slots
+    std::vector<uint32_t> slots;
+    std::vector<int64_t> counts;
     for (uint32_t s = 0; s < P0.H; ++s) {
         const uint64_t dc = p0_terms ? ocnt[s] : P0.hc.cnt[s];
         if (dc == 0) continue;
-        push_bucket(r, key_value(P0, s), nullptr, (int64_t)dc);
-        for (size_t ki = 0; ki < g.kids.size(); ++ki) {
-            const ChildSrc& kid = g.kids[ki];
-            Block& sub = r.subs[ki];
-            if (!kid.bucket) {
-                const Pipeline& L = p->pipes[kid.leaf.pipe];
-                require(L.H == P0.H && L.key0 == P0.key0, ESGPU_ERR_DEVICE, "sibling pipelines disagree on the key grid");
-                append_leaf(p, L, kid.leaf.leaf, s, sub);
-                continue;
-            }
-            const Pipeline& B0 = p->pipes[kid.pipes[0]];
+        slots.push_back(s);
+        counts.push_back((int64_t)dc);
+    }
+    begin_instance(r, 0);
+    append_hist_buckets(P0, slots, counts, r);
+    for (size_t ki = 0; ki < g.kids.size(); ++ki) {
+        const ChildSrc& kid = g.kids[ki];
+        Block& sub = r.subs[ki];
+        if (!kid.bucket) {
+            const Pipeline& L = p->pipes[kid.leaf.pipe];
+            require(L.H == P0.H && L.key0 == P0.key0, ESGPU_ERR_DEVICE, "sibling pipelines disagree on the key grid");
+            append_leaves(p, L, kid.leaf.leaf, slots, sub);  // one cell per key (T == 1): cell == slot
+            continue;
+        }
+        const Pipeline& B0 = p->pipes[kid.pipes[0]];
+        require(!B0.allocated || B0.tdict == nullptr || (B0.H == P0.H && B0.key0 == P0.key0), ESGPU_ERR_DEVICE,
+                "sibling pipelines disagree on the key grid");
+        for (uint32_t s : slots) {
             if (!B0.allocated || B0.tdict == nullptr) { sub.append_empty(); continue; }
-            require(B0.H == P0.H && B0.key0 == P0.key0, ESGPU_ERR_DEVICE, "sibling pipelines disagree on the key grid");
             const SpecNode& tn = p->specs[kid.spec];
             LeafRef ord_ref;
             if (tn.s.order == ESGPU_ORDER_AGG_ASC || tn.s.order == ESGPU_ORDER_AGG_DESC) {
@@ -2458,6 +2544,8 @@ static Block build_cardinality(esgpu_plan* p, Pipeline& pl) {
 extern "C" int esgpu_plan_build(esgpu_plan* p, esgpu_result** out) {
     return guarded([&] {
         require(p && out, ESGPU_ERR_INVALID, "null argument");
+        const double t0 = now_ms();
+        p->b_wait = 0;
         if (!p->posted) {
             int rc = esgpu_plan_post_collection(p);
             if (rc != ESGPU_OK) throw EsError(rc, g_err);
@@ -2481,7 +2569,7 @@ extern "C" int esgpu_plan_build(esgpu_plan* p, esgpu_result** out) {
             if (cnt && cnt->allocated) {
                 uint64_t* hc = (uint64_t*)p->h_tcnt.ensure(16);
                 HIPX(hipMemcpyAsync(hc, cnt->g_cnt.p, 8, hipMemcpyDeviceToHost, p->stream));
-                HIPX(hipStreamSynchronize(p->stream));
+                bsync(p);
                 dc = hc[0];
             }
             fb.count.push_back((int64_t)dc);
@@ -2490,6 +2578,7 @@ extern "C" int esgpu_plan_build(esgpu_plan* p, esgpu_result** out) {
         }
         h->export_view();
         *out = &h.release()->pub;
+        p->b_total = now_ms() - t0;
     });
 }
 
@@ -2509,6 +2598,7 @@ extern "C" int esgpu_plan_reset(esgpu_plan* p) {
                 pl.h_lc.clear();
                 pl.h_regs.clear();
                 pl.any_value = false;
+                pl.hll_seen = 0;
                 continue;
             }
             const size_t cells = (size_t)pl.T * pl.H;

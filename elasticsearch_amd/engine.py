@@ -188,6 +188,12 @@ class Plan:
         N.check(N.lib().esgpu_plan_last_collect_stats(self._ptr, ctypes.byref(ms), ctypes.byref(nbytes), ctypes.byref(path)))
         return ms.value, nbytes.value, path.value
 
+    def last_build_stats(self):
+        """(total_ms, stream_wait_ms) of the last build()"""
+        tot, wait = ctypes.c_double(), ctypes.c_double()
+        N.check(N.lib().esgpu_plan_last_build_stats(self._ptr, ctypes.byref(tot), ctypes.byref(wait)))
+        return tot.value, wait.value
+
     def shard_mergeable(self):
         """True if several shards may be collected into this one plan (no terms aggregation, see include/esgpu.h)."""
         v = ctypes.c_int32()

@@ -328,6 +328,9 @@ int esgpu_plan_destroy(esgpu_plan* plan);
  * and the algorithmic bytes it read (SURVEY §8(d) formula). */
 int esgpu_plan_last_collect_stats(const esgpu_plan* plan, double* kernel_ms, uint64_t* algorithmic_bytes,
                                   int32_t* path);
+/* Wall time of the last esgpu_plan_build and the part of it spent waiting on the plan's stream (gathers and copies of
+ * the winners' cells); the rest is host assembly of the result blocks.  Milliseconds. */
+int esgpu_plan_last_build_stats(const esgpu_plan* plan, double* total_ms, double* wait_ms);
 /* 1 if the plan's shard results are fixed-shape (no terms aggregation at any level): several shards of one GPU may
  * then be collected into one plan -- their doc counts, sums, extrema and sketches add up exactly as the reduce of their
  * separate results would (HistogramAggregator / metrics / HyperLogLogPlusPlus.merge; min_doc_count and empty buckets

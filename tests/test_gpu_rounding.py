@@ -128,12 +128,43 @@ def test_roughly_sorted_timestamps(engine, jitter):
     fields = ("host", "@timestamp", "response_time_ms")
     aggs = [AB.terms("hosts").field("host").size(10).subAggregation(
                 AB.dateHistogram("h").field("@timestamp").interval("1h").subAggregation(AB.stats("rt").field("response_time_ms"))),
-            AB.dateHistogram("m").field("@timestamp").interval("1m").subAggregation(AB.extendedStats("rt").field("response_time_ms"))]
+            AB.dateHistogram("m").field("@timestamp").interval("1m").subAggregation(AB.extendedStats("rt").field("response_time_ms")),
+            # a bucket table (DST zone) under terms: multi-pass windows over table keys
+            AB.terms("ny").field("host").size(5).subAggregation(
+                AB.dateHistogram("h").field("@timestamp").interval("hour").timeZone("America/New_York")
+                .subAggregation(AB.avg("rt").field("response_time_ms"))),
+            # minute keys under terms: a block spans more than kMaxPasses windows -> the global-atomic path
+            AB.terms("mm").field("host").size(3).subAggregation(AB.dateHistogram("m").field("@timestamp").interval("1m"))]
     want = O.run([(synthetic_columns(fields, n, ts_jitter_ms=jitter), n)], aggs)
     seg = engine.synthetic_segment(n, fields=fields, ts_jitter_ms=jitter)
     host_ts = synthetic_columns(("@timestamp",), n, ts_jitter_ms=jitter)["@timestamp"]["values"]
     assert np.array_equal(seg.read_column("@timestamp", 0, n, np.int64), host_ts)  # device generator == host generator
     assert np.any(np.diff(host_ts) < 0)
+    plan = engine.plan(aggs)
+    plan.collect(seg)
+    res = plan.build()
+    assert_same(res.to_dict(), want["shards"][0], "shard")
+    assert_same(reduce([res]).to_dict(), want["reduced"], "reduced")
+    plan.close()
+    seg.close()
+
+
+def test_multi_pass_blocks_with_missing_timestamps(engine):
+    """Multi-pass blocks (+-1 h jitter, hour keys under / over terms) with 15 % of the timestamps missing: the terms'
+    doc counts (docs without a timestamp included) are taken in the first pass only, the histogram's per-key counts
+    (date_histogram over terms) in the pass whose window holds the key."""
+    from elasticsearch_amd import reduce
+    import oracle as O
+    from helpers import assert_same, bits_from_mask, synthetic_columns
+    n = 3_000_000
+    cols = synthetic_columns(("host", "@timestamp", "bytes"), n, ts_jitter_ms=3_600_000)
+    cols["@timestamp"]["present"] = bits_from_mask(np.random.default_rng(11).random(n) >= 0.15)
+    aggs = [AB.terms("hosts").field("host").size(20).subAggregation(
+                AB.dateHistogram("h").field("@timestamp").interval("1h").subAggregation(AB.avg("b").field("bytes"))),
+            AB.dateHistogram("d").field("@timestamp").interval("1h").subAggregation(
+                AB.terms("t").field("host").size(4).subAggregation(AB.stats("b").field("bytes")))]
+    want = O.run([(cols, n)], aggs)
+    seg = engine.upload_segment(cols, n)
     plan = engine.plan(aggs)
     plan.collect(seg)
     res = plan.build()

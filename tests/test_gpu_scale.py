@@ -60,3 +60,24 @@ def test_config5_120m(engine):
     filters = [QB.termQuery("status", 200), QB.rangeQuery("bytes").gte(1024).lte(65536)]
     _compare(engine, aggs, ("status", "bytes", "host", "@timestamp", "response_time_ms"), 120_000_000, filters=filters,
              number_of_shards=8)
+
+
+def test_config4_shards_merged_into_one_plan(engine):
+    """Config 4 as bench.py --shards runs it on one GPU: 4 shards of 40M docs collected into one plan.  From the second
+    segment on the register kernel continues the phase sequence with the floor the earlier segments left (no floor-0
+    phase); the merged registers must equal the reduce of the per-shard sketches."""
+    n, shards = 40_000_000, 4
+    fields = ("client_ip.hash",)
+    aggs = [AB.cardinality("ips").field("client_ip.hash").precisionThreshold(40000)]
+    want = O.run([(synthetic_columns(fields, n, shard=s), n) for s in range(shards)], aggs, number_of_shards=shards)
+    plan = engine.plan(aggs, number_of_shards=shards)
+    assert plan.shard_mergeable()
+    segs = [engine.synthetic_segment(n, fields=fields, shard=s) for s in range(shards)]
+    for seg in segs:
+        plan.collect(seg)
+    got = reduce([plan.build()]).to_dict()
+    assert_same(got, want["reduced"], "merged shards")
+    assert got["ips"]["_internal"]["mode"] == "hll"
+    plan.close()
+    for seg in segs:
+        seg.close()

@@ -2,7 +2,7 @@
 # One gpurun session: GPU parity tests, kernel sweep, bench, rocprofv3 kernel-trace stats and PMC HBM-traffic passes.
 #   gpurun --timeout 1200 -- bash tools/gpu_check.sh <tag> [steps...]
 # steps: tests kbench bench prof profk pmc pmck variants (default: tests kbench bench prof pmc)
-# KBENCH_ONLY=name,name restricts the kbench sweeps; variants = every build/variants/libesgpu_*.so via ESGPU_LIBRARY.  Every GPU step has its own time limit; the first failure ends it.
+# KBENCH_ONLY=name,name restricts the kbench sweeps (KBENCH_ARGS: extra kbench flags for variants, KBENCH_TAG: log suffix); variants = every build/variants/libesgpu_*.so via ESGPU_LIBRARY.  Every GPU step has its own time limit; the first failure ends it.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r1}
@@ -56,8 +56,8 @@ for s in $STEPS; do
               done ;;
         variants) for so in "$R"/build/variants/libesgpu_*.so; do
                       v=$(basename "$so" .so)
-                      ESGPU_LIBRARY=$so run "kbench_$v" 600 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 \
-                          ${KBENCH_ONLY:+--only $KBENCH_ONLY}
+                      ESGPU_LIBRARY=$so run "kbench_$v${KBENCH_TAG:-}" 600 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 \
+                          ${KBENCH_ONLY:+--only $KBENCH_ONLY} ${KBENCH_ARGS:-}
                   done ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac

@@ -61,7 +61,7 @@ def main():
         plan = e.plan(aggs, filters=flt, number_of_shards=args.shards)
         ms = []
         steps = []
-        parts = {"reset": [], "collect_call": [], "kernel_wait": [], "build": [], "reduce": []}
+        parts = {"reset": [], "collect_call": [], "kernel_wait": [], "build": [], "build_wait": [], "reduce": []}
         for r in range(args.reps + 1):
             t0 = time.perf_counter()
             plan.reset()
@@ -72,6 +72,7 @@ def main():
             t3 = time.perf_counter()
             res = plan.build()
             t4 = time.perf_counter()
+            bwait = plan.last_build_stats()[1]
             ea.reduce([res])
             t5 = time.perf_counter()
             dt = (t5 - t0) * 1e3
@@ -81,6 +82,7 @@ def main():
                 for key, a, b in (("reset", t0, t1), ("collect_call", t1, t2), ("kernel_wait", t2, t3),
                                   ("build", t3, t4), ("reduce", t4, t5)):
                     parts[key].append((b - a) * 1e3)
+                parts["build_wait"].append(bwait)
         kms = sorted(ms)[len(ms) // 2]
         gbs = nbytes / (kms / 1e3) / 1e9
         print(json.dumps({"name": name, "ts_jitter_ms": args.ts_jitter, "kernel_ms": round(kms, 4), "bytes": nbytes, "gbs": round(gbs, 1),
