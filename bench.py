@@ -226,12 +226,19 @@ def main():
                 kernel_ms[0] += ms
                 kernel_bytes[0] += nbytes
 
+    host_ms = {"build": 0.0, "reduce": 0.0}
+
     def finish(p, unit):
         nonlocal final, partial
+        t0 = time.perf_counter()
         partial.append(p.build())
+        t1 = time.perf_counter()
         if unit == units_per_request - 1:
             final = comm.reduce(partial) if comm else ea.reduce(partial)
             partial = []
+        t2 = time.perf_counter()
+        host_ms["build"] += (t1 - t0) * 1e3
+        host_ms["reduce"] += (t2 - t1) * 1e3
 
     # one unit = one collect (+ build) of a shard, or of all this GPU's shards of a fixed-shape request; with two plans
     # the host build + reduce of one unit overlaps the collect kernel of the next -- how a node serves a stream of
@@ -270,7 +277,10 @@ def main():
     elapsed = timed(len(plans), len(plans) == 1)
     # one unit at a time: the sequential rate, reported alongside, and the collect kernels' HIP-event time (measured
     # here, where no two collects overlap on the GPU)
+    for k in host_ms:
+        host_ms[k] = 0.0
     elapsed_seq = timed(1, True) if len(plans) > 1 else elapsed
+    host_ms = {k: round(v / args.steps, 4) for k, v in host_ms.items()}  # per request, sequential phase
     exchange = None
     if comm:
         ar, ag, ncoll = comm.last_exchange()
@@ -340,6 +350,7 @@ def main():
                          "kernel": "collect_kernel", "kernel_ms": avg_kernel_ms * args.steps / launches,
                          "algorithmic_bytes_per_launch": kernel_bytes[0] // launches},
             "exchange": exchange,
+            "host_ms_per_request": host_ms,
             "cpu_baseline": cpu,
             "checked": checked,
             "check_errors": check_errors[:5],

@@ -111,16 +111,17 @@ struct DevBuf {
 // pinned host staging buffer (D2H of build results without a pageable bounce)
 struct PinnedBuf {
     void* p = nullptr;
+    void* dp = nullptr;  // the same memory as the device addresses it (kernels write build results straight into it)
     size_t bytes = 0;
     PinnedBuf() = default;
     PinnedBuf(const PinnedBuf&) = delete;
     PinnedBuf& operator=(const PinnedBuf&) = delete;
-    PinnedBuf(PinnedBuf&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+    PinnedBuf(PinnedBuf&& o) noexcept : p(o.p), dp(o.dp), bytes(o.bytes) { o.p = nullptr; o.dp = nullptr; o.bytes = 0; }
     PinnedBuf& operator=(PinnedBuf&& o) noexcept {
         if (this != &o) {
             if (p) (void)hipHostFree(p);
-            p = o.p; bytes = o.bytes;
-            o.p = nullptr; o.bytes = 0;
+            p = o.p; dp = o.dp; bytes = o.bytes;
+            o.p = nullptr; o.dp = nullptr; o.bytes = 0;
         }
         return *this;
     }
@@ -129,10 +130,15 @@ struct PinnedBuf {
         if (n <= bytes) return p;
         if (p) (void)hipHostFree(p);
         p = nullptr;
+        dp = nullptr;
         bytes = 0;
         HIPX(hipHostMalloc(&p, n, hipHostMallocDefault));
         bytes = n;
         return p;
+    }
+    void* dev() {
+        if (!dp && p) HIPX(hipHostGetDevicePointer(&dp, p, 0));
+        return dp;
     }
     template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };

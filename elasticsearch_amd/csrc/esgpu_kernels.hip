@@ -459,12 +459,12 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
     }
 }
 
-template <int MET, int MS>
+template <int MET, int MS, int WGS>
 __device__ void flush_window(const CollectParams& P, const Acc& s, uint32_t T, uint32_t W, uint32_t win0, uint32_t ncp = 1) {
     __syncthreads();
     const uint32_t C = T * W;
     if (P.ocnt_mode == OCNT_TERMS_DERIVED) {  // per-term totals of this window (one atomic per term)
-        for (uint32_t t = threadIdx.x; t < T; t += kWG) {
+        for (uint32_t t = threadIdx.x; t < T; t += WGS) {
             uint32_t tot = 0;
             for (uint32_t k = 0; k < ncp; ++k)
                 for (uint32_t l = 0; l < W; ++l) tot += s.cnt32[k * C + l * T + t];
@@ -472,7 +472,7 @@ __device__ void flush_window(const CollectParams& P, const Acc& s, uint32_t T, u
         }
         __syncthreads();
     }
-    for (uint32_t c = threadIdx.x; c < C; c += kWG) {
+    for (uint32_t c = threadIdx.x; c < C; c += WGS) {
         uint32_t n = 0;
         for (uint32_t k = 0; k < ncp; ++k) n += s.cnt32[k * C + c];
         if (n == 0) continue;
@@ -507,12 +507,12 @@ __device__ void flush_window(const CollectParams& P, const Acc& s, uint32_t T, u
         }
     }
     if (P.ocnt_mode == OCNT_TERMS) {
-        for (uint32_t t = threadIdx.x; t < T; t += kWG) {
+        for (uint32_t t = threadIdx.x; t < T; t += WGS) {
             const uint32_t n = s.ocnt32[t];
             if (n) { atomicAdd(&P.g_ocnt[t], (unsigned long long)n); s.ocnt32[t] = 0; }
         }
     } else if (P.ocnt_mode == OCNT_HIST) {
-        for (uint32_t l = threadIdx.x; l < W; l += kWG) {
+        for (uint32_t l = threadIdx.x; l < W; l += WGS) {
             const uint32_t n = s.ocnt32[l];
             if (n && win0 + l < P.H) { atomicAdd(&P.g_ocnt[win0 + l], (unsigned long long)n); }
             s.ocnt32[l] = 0;
@@ -522,8 +522,13 @@ __device__ void flush_window(const CollectParams& P, const Acc& s, uint32_t T, u
 }
 
 // HK: 0 = no histogram dimension, 1 = affine rounding, 2 = bucket table (calendar units / DST zones)
-template <bool ORD, int HK, int MET, int VK>
-__global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
+// WGS: threads per workgroup -- 512 (two resident per CU, each with an LDS window of <= 64 KB), or 1024 for
+// histogram grids whose data needs a wider window than 64 KB holds (one workgroup per CU with up to 150 KB of LDS,
+// the same 16 waves per CU)
+template <bool ORD, int HK, int MET, int VK, int WGS>
+__global__ __launch_bounds__(WGS) void collect_kernel(CollectParams P) {
+    constexpr int kIterDocsW = WGS * kVec;
+    constexpr int kItersPerBlockW = kBlockDocs / kIterDocsW;
     constexpr bool HIST = HK != 0;
     constexpr bool KT = HK == 2;
     // min/max LDS layout: interleaved (one paired read per check) with a key dimension, two arrays without one
@@ -562,16 +567,16 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
                                     : P.ocnt_mode == OCNT_HIST ? sizeof(uint32_t) * W : 0);
     }
     if (P.lds_mode) {
-        for (uint32_t c = threadIdx.x; c < C * ncp; c += kWG) {
+        for (uint32_t c = threadIdx.x; c < C * ncp; c += WGS) {
             s.cnt32[c] = 0;
             if (P.vcnt_mode) s.vcnt32[c] = 0;
             if (MET > 0) s.sum[c] = 0.0;
             if (MET >= 3) s.sq[c] = 0.0;
         }
-        for (uint32_t c = threadIdx.x; c < C; c += kWG)
+        for (uint32_t c = threadIdx.x; c < C; c += WGS)
             if (MET >= 2) { s.mn[kMS * c] = kMinInit; s.mx[kMS * c] = kMaxInit; }
         if (P.ocnt_mode == OCNT_TERMS || P.ocnt_mode == OCNT_HIST)
-            for (uint32_t c = threadIdx.x; c < (P.ocnt_mode == OCNT_TERMS ? T : W); c += kWG) s.ocnt32[c] = 0;
+            for (uint32_t c = threadIdx.x; c < (P.ocnt_mode == OCNT_TERMS ? T : W); c += WGS) s.ocnt32[c] = 0;
         __syncthreads();
     }
 
@@ -603,12 +608,12 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
     // blocks each fit the window are taken block by block, the window sliding as before.
     const uint32_t tid4 = threadIdx.x * kVec;
     // shapes that read few bytes per doc (one ordinal or one key column) keep 4 buffers in flight, the rest 2 (their
-    // buffers are 5x larger; 4 would cost occupancy).  kItersPerBlock (4) is a multiple of either.
+    // buffers are 5x larger; 4 would cost occupancy).  kItersPerBlockW (4) is a multiple of either.
     constexpr int kBuf = (MET == 0 && !(ORD && HIST)) ? ESGPU_NBUF_NARROW : 2;
-    static_assert(kItersPerBlock % kBuf == 0, "buffers per block");
+    static_assert(kItersPerBlockW % kBuf == 0, "buffers per block");
     Doc4 q[kBuf];
 #pragma unroll
-    for (int k = 0; k < kBuf; ++k) load_docs<ORD, HIST, MET, VK>(P, b_begin * kBlockDocs + k * kIterDocs + tid4, q[k]);
+    for (int k = 0; k < kBuf; ++k) load_docs<ORD, HIST, MET, VK>(P, b_begin * kBlockDocs + k * kIterDocsW + tid4, q[k]);
 
     bool use_lds = P.lds_mode != 0;
     uint32_t cb = b_begin;                               // block being processed
@@ -617,7 +622,7 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
     auto slide_to = [&](uint32_t k0) {
         if (dirty) {
             if (!ORD) runs_flush<MET, kMS>(P, s, run);
-            flush_window<MET, kMS>(P, s, T, W, win0, ncp);
+            flush_window<MET, kMS, WGS>(P, s, T, W, win0, ncp);
         }
         dirty = false;
         win0 = k0;
@@ -673,16 +678,16 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
         // prefetch kBuf iterations ahead along the schedule (next block of the group, the group's next pass, or the
         // next group)
         uint32_t nit = it + kBuf, nb = cb;
-        if (nit >= (uint32_t)kItersPerBlock) {
-            nit -= kItersPerBlock;
+        if (nit >= (uint32_t)kItersPerBlockW) {
+            nit -= kItersPerBlockW;
             nb = cb + 1;
             if (nb == ge && pass + 1 < npass) nb = gb;
             nb = min(nb, b_end - 1);
         }
-        load_docs<ORD, HIST, MET, VK>(P, nb * kBlockDocs + nit * kIterDocs + tid4, q);
+        load_docs<ORD, HIST, MET, VK>(P, nb * kBlockDocs + nit * kIterDocsW + tid4, q);
     };
     while (cb < b_end) {
-        for (uint32_t it = 0; it < (uint32_t)kItersPerBlock; it += kBuf) {
+        for (uint32_t it = 0; it < (uint32_t)kItersPerBlockW; it += kBuf) {
 #pragma unroll
             for (int k = 0; k < kBuf; ++k) step(it + k, q[k]);
         }
@@ -699,7 +704,7 @@ __global__ __launch_bounds__(kWG) void collect_kernel(CollectParams P) {
     }
     if (P.lds_mode && (dirty || !(HIST && P.windowed))) {
         if (!ORD) runs_flush<MET, kMS>(P, s, run);
-        flush_window<MET, kMS>(P, s, T, W, win0, ncp);
+        flush_window<MET, kMS, WGS>(P, s, T, W, win0, ncp);
     }
 }
 
@@ -724,59 +729,75 @@ static auto with_vk(bool hv_f64, bool mv_f64, F f) {
     }
 }
 
+// wide = 1024-thread workgroups (instantiated for histogram grids only)
+template <bool ORD, int HK, int MET, class F>
+static auto with_wg(bool wide, F f) {
+    if constexpr (HK != 0) {
+        if (wide) return f(std::integral_constant<int, 1024>{});
+    }
+    return f(std::integral_constant<int, kWG>{});
+}
+
 template <bool ORD, int HK, int MET>
-static void launch_t(const CollectParams& p, uint32_t grid, size_t lds, hipStream_t st) {
+static void launch_t(const CollectParams& p, bool wide, uint32_t grid, size_t lds, hipStream_t st) {
     with_vk<HK, MET>(p.hv_f64 != 0, p.mv_f64 != 0, [&](auto vk) {
-        hipLaunchKernelGGL((collect_kernel<ORD, HK, MET, decltype(vk)::value>), dim3(grid), dim3(kWG), lds, st, p);
-        return 0;
+        return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
+            hipLaunchKernelGGL((collect_kernel<ORD, HK, MET, decltype(vk)::value, decltype(wg)::value>), dim3(grid),
+                               dim3(decltype(wg)::value), lds, st, p);
+            return 0;
+        });
     });
 }
 
 template <bool ORD, int HK>
-static void launch_m(const CollectParams& p, int met, uint32_t grid, size_t lds, hipStream_t st) {
+static void launch_m(const CollectParams& p, int met, bool wide, uint32_t grid, size_t lds, hipStream_t st) {
     switch (met) {
-        case 0: launch_t<ORD, HK, 0>(p, grid, lds, st); break;
-        case 1: launch_t<ORD, HK, 1>(p, grid, lds, st); break;
-        case 2: launch_t<ORD, HK, 2>(p, grid, lds, st); break;
-        default: launch_t<ORD, HK, 3>(p, grid, lds, st); break;
+        case 0: launch_t<ORD, HK, 0>(p, wide, grid, lds, st); break;
+        case 1: launch_t<ORD, HK, 1>(p, wide, grid, lds, st); break;
+        case 2: launch_t<ORD, HK, 2>(p, wide, grid, lds, st); break;
+        default: launch_t<ORD, HK, 3>(p, wide, grid, lds, st); break;
     }
 }
 
-void launch_collect(const CollectParams& p, bool ord, bool hist, int met, uint32_t grid, size_t lds, hipStream_t st) {
+void launch_collect(const CollectParams& p, bool ord, bool hist, int met, bool wide, uint32_t grid, size_t lds, hipStream_t st) {
     const int hk = hist ? (p.kstart ? 2 : 1) : 0;
     if (ord) {
-        if (hk == 2) launch_m<true, 2>(p, met, grid, lds, st);
-        else if (hk == 1) launch_m<true, 1>(p, met, grid, lds, st);
-        else launch_m<true, 0>(p, met, grid, lds, st);
+        if (hk == 2) launch_m<true, 2>(p, met, wide, grid, lds, st);
+        else if (hk == 1) launch_m<true, 1>(p, met, wide, grid, lds, st);
+        else launch_m<true, 0>(p, met, false, grid, lds, st);
     } else {
-        if (hk == 2) launch_m<false, 2>(p, met, grid, lds, st);
-        else if (hk == 1) launch_m<false, 1>(p, met, grid, lds, st);
-        else launch_m<false, 0>(p, met, grid, lds, st);
+        if (hk == 2) launch_m<false, 2>(p, met, wide, grid, lds, st);
+        else if (hk == 1) launch_m<false, 1>(p, met, wide, grid, lds, st);
+        else launch_m<false, 0>(p, met, false, grid, lds, st);
     }
 }
 
 template <bool ORD, int HK, int MET>
-static int occ_t(size_t lds, int vkbits) {
+static int occ_t(size_t lds, int vkbits, bool wide) {
     return with_vk<HK, MET>((vkbits & 1) != 0, (vkbits & 2) != 0, [&](auto vk) {
-        int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, collect_kernel<ORD, HK, MET, decltype(vk)::value>, kWG, lds) !=
-            hipSuccess)
-            n = 1;
-        return n;
+        return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
+            int n = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                    &n, collect_kernel<ORD, HK, MET, decltype(vk)::value, decltype(wg)::value>, decltype(wg)::value, lds) !=
+                hipSuccess)
+                n = 1;
+            return n;
+        });
     });
 }
 template <bool ORD, int HK>
-static int occ_m(int met, size_t lds, int vk) {
+static int occ_m(int met, size_t lds, int vk, bool wide) {
     switch (met) {
-        case 0: return occ_t<ORD, HK, 0>(lds, vk);
-        case 1: return occ_t<ORD, HK, 1>(lds, vk);
-        case 2: return occ_t<ORD, HK, 2>(lds, vk);
-        default: return occ_t<ORD, HK, 3>(lds, vk);
+        case 0: return occ_t<ORD, HK, 0>(lds, vk, wide);
+        case 1: return occ_t<ORD, HK, 1>(lds, vk, wide);
+        case 2: return occ_t<ORD, HK, 2>(lds, vk, wide);
+        default: return occ_t<ORD, HK, 3>(lds, vk, wide);
     }
 }
-int collect_occupancy(bool ord, int hk, int met, size_t lds, int vk) {
-    if (ord) return hk == 2 ? occ_m<true, 2>(met, lds, vk) : hk == 1 ? occ_m<true, 1>(met, lds, vk) : occ_m<true, 0>(met, lds, vk);
-    return hk == 2 ? occ_m<false, 2>(met, lds, vk) : hk == 1 ? occ_m<false, 1>(met, lds, vk) : occ_m<false, 0>(met, lds, vk);
+int collect_occupancy(bool ord, int hk, int met, size_t lds, int vk, bool wide) {
+    if (ord)
+        return hk == 2 ? occ_m<true, 2>(met, lds, vk, wide) : hk == 1 ? occ_m<true, 1>(met, lds, vk, wide) : occ_m<true, 0>(met, lds, vk, false);
+    return hk == 2 ? occ_m<false, 2>(met, lds, vk, wide) : hk == 1 ? occ_m<false, 1>(met, lds, vk, wide) : occ_m<false, 0>(met, lds, vk, false);
 }
 
 size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode, uint32_t ncopies) {
@@ -1219,6 +1240,19 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(GatherParams P) {
     const uint32_t r = i / P.H, h = i - r * P.H;
     const size_t src = (size_t)h * P.T + P.rows[r];
     for (int a = 0; a < P.narrays; ++a) P.dst[a][i] = P.src[a][src];
+}
+
+// device -> pinned host memory for the build's small transfers: a kernel writing over the link beats a DMA copy,
+// whose setup measured ~130 us per 144 KB transfer
+__global__ __launch_bounds__(256) void copy_u64_kernel(const unsigned long long* __restrict__ src,
+                                                       unsigned long long* __restrict__ dst, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) dst[i] = src[i];
+}
+
+void launch_copy_u64(const unsigned long long* src, unsigned long long* dst, size_t n, hipStream_t st) {
+    if (n == 0) return;
+    const size_t g = std::min<size_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(copy_u64_kernel, dim3((uint32_t)g), dim3(256), 0, st, src, dst, n);
 }
 
 void launch_gather_rows(const GatherParams& p, hipStream_t st) {
@@ -1991,7 +2025,7 @@ __global__ __launch_bounds__(kWG) void collect_multi_kernel(CollectParams P) {
             }
         }
     }
-    if (P.lds_mode) flush_window<MET, 2>(P, s, T, H, 0);
+    if (P.lds_mode) flush_window<MET, 2, kWG>(P, s, T, H, 0);
 }
 
 template <bool ORD, int HK, int MET>

@@ -126,10 +126,11 @@ struct GatherParams {
 void launch_zone_map(const int64_t* v, const uint64_t* present, uint32_t n, int64_t* zmin, int64_t* zmax, bool f64,
                      hipStream_t s);
 void launch_synth(const SynthParams& p, hipStream_t s);
-void launch_collect(const CollectParams& p, bool ord, bool hist, int met, uint32_t grid, size_t lds, hipStream_t s);
+// wide: 1024-thread workgroups (histogram grids whose LDS window exceeds the two-per-CU budget), else 512
+void launch_collect(const CollectParams& p, bool ord, bool hist, int met, bool wide, uint32_t grid, size_t lds, hipStream_t s);
 size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode, uint32_t ncopies = 1);
 // resident workgroups per CU (hk: 0 none, 1 affine, 2 table; vk: bit 0 double histogram column, bit 1 double metric)
-int collect_occupancy(bool ord, int hk, int met, size_t lds, int vk);
+int collect_occupancy(bool ord, int hk, int met, size_t lds, int vk, bool wide = false);
 void launch_hll(const HllParams& p, uint32_t cus, hipStream_t s);
 
 // ---- multi-valued (CSR) columns, esgpu_kernels_multi.hip ----
@@ -178,6 +179,8 @@ void launch_minmax_i64(const int64_t* v, uint64_t n, int64_t* out, bool f64, hip
 void launch_remap_ords(const uint32_t* in, uint32_t n, const uint32_t* map, uint32_t map_n, uint32_t* out, hipStream_t s);
 void launch_pack_u8(const unsigned int* src, uint32_t n, uint8_t* dst, hipStream_t s);
 void launch_term_totals(const unsigned long long* cnt, uint32_t H, uint32_t T, unsigned long long* out, hipStream_t s);
+// n u64 words device -> device-visible pinned host memory
+void launch_copy_u64(const unsigned long long* src, unsigned long long* dst, size_t n, hipStream_t s);
 void launch_gather_rows(const GatherParams& p, hipStream_t s);
 void launch_fill_u64(unsigned long long* p, size_t n, unsigned long long v, hipStream_t s);
 

@@ -504,12 +504,48 @@ void reduce_histogram(const Ref* refs, size_t nrefs, Block& out, Scratch& sc, st
             list.push_back(OutBucket{h.key[k], nullptr, 0, h.bcount[k], 0, c, c + 1, false});
         }
     } else {
-        std::vector<Ref>& all = sc.child;
+        // InternalHistogram.reduceBuckets: every shard's buckets are key-ascending, so a k-way merge by (key, shard)
+        // orders them (equal keys in shard order); inputs not in key order (a reduced result with another order)
+        // take a stable sort instead
+        std::vector<Ref>& all = sc.contrib;
         all.clear();
-        for (size_t x = 0; x < nrefs; ++x)
-            for (uint64_t k = refs[x].b->boff[refs[x].i]; k < refs[x].b->boff[refs[x].i + 1]; ++k) all.push_back({refs[x].b, k});
-        std::stable_sort(all.begin(), all.end(), [](const Ref& a, const Ref& b) { return a.b->key[a.i] < b.b->key[b.i]; });
-        sc.contrib = all;
+        bool sorted = true;
+        size_t total = 0;
+        for (size_t x = 0; x < nrefs; ++x) {
+            const Block& h = *refs[x].b;
+            const uint64_t b0 = h.boff[refs[x].i], b1 = h.boff[refs[x].i + 1];
+            total += b1 - b0;
+            for (uint64_t k = b0 + 1; k < b1 && sorted; ++k) sorted = h.key[k - 1] < h.key[k];
+        }
+        all.reserve(total);
+        if (sorted) {
+            struct Head { int64_t key; uint32_t x; uint64_t k, end; };
+            std::vector<Head> heap;
+            heap.reserve(nrefs);
+            auto later = [](const Head& a, const Head& b) { return a.key != b.key ? a.key > b.key : a.x > b.x; };
+            for (size_t x = 0; x < nrefs; ++x) {
+                const Block& h = *refs[x].b;
+                const uint64_t b0 = h.boff[refs[x].i], b1 = h.boff[refs[x].i + 1];
+                if (b0 < b1) heap.push_back({h.key[b0], (uint32_t)x, b0, b1});
+            }
+            std::make_heap(heap.begin(), heap.end(), later);
+            while (!heap.empty()) {
+                std::pop_heap(heap.begin(), heap.end(), later);
+                Head& t = heap.back();
+                const Block* b = refs[t.x].b;
+                all.push_back({b, t.k});
+                if (++t.k < t.end) {
+                    t.key = b->key[t.k];
+                    std::push_heap(heap.begin(), heap.end(), later);
+                } else {
+                    heap.pop_back();
+                }
+            }
+        } else {
+            for (size_t x = 0; x < nrefs; ++x)
+                for (uint64_t k = refs[x].b->boff[refs[x].i]; k < refs[x].b->boff[refs[x].i + 1]; ++k) all.push_back({refs[x].b, k});
+            std::stable_sort(all.begin(), all.end(), [](const Ref& a, const Ref& b) { return a.b->key[a.i] < b.b->key[b.i]; });
+        }
         for (size_t x = 0; x < all.size();) {
             const int64_t key = all[x].b->key[all[x].i];
             OutBucket ob{key, nullptr, 0, 0, 0, (uint32_t)x, 0, false};

@@ -17,6 +17,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <queue>
@@ -233,6 +234,7 @@ struct DevColumn {
     uint64_t n_values = 0;
     DevBuf zmin, zmax;
     int64_t vmin = INT64_MAX, vmax = INT64_MIN;  // over present values (I64 columns)
+    int64_t zspan = 0;  // 90th percentile of a block's value range (zmax - zmin): how far the data is from sorted
     uint64_t value_count = 0;
     std::shared_ptr<const TermDict> dict;   // ORD: the segment's own dictionary (value_count terms)
     DevBuf ord_hash;  // murmur3 h1 per term (built lazily for cardinality on keyword fields)
@@ -291,9 +293,17 @@ static void build_zone_map(esgpu_ctx* c, DevColumn& col, uint32_t n) {
         HIPX(hipMemcpyAsync(mx.data(), col.zmax.p, nb * 8, hipMemcpyDeviceToHost, c->stream));
     }
     HIPX(hipStreamSynchronize(c->stream));
+    std::vector<int64_t> range;
+    range.reserve(nb);
     for (uint32_t b = 0; b < nb; ++b) {
         col.vmin = std::min(col.vmin, mn[b]);
         col.vmax = std::max(col.vmax, mx[b]);
+        if (mn[b] <= mx[b]) range.push_back((int64_t)std::min<uint64_t>((uint64_t)mx[b] - (uint64_t)mn[b], INT64_MAX));
+    }
+    if (!range.empty()) {
+        const size_t q = range.size() * 9 / 10;
+        std::nth_element(range.begin(), range.begin() + q, range.end());
+        col.zspan = range[q];
     }
 }
 
@@ -816,7 +826,6 @@ struct Pipeline {
     // build: the pipeline's cells on the host (gathered winner rows or the whole grid) and their staging buffers
     HostCells hc;
     PinnedBuf h_cells[6], h_ocnt;
-    Scratch d_rows[6];
 };
 
 // One aggregation subtree (a top-level aggregation, or a child of a top-level filter aggregation) compiled to one or
@@ -855,6 +864,8 @@ struct esgpu_plan {
     double last_ms = 0;
     uint64_t last_bytes = 0;
     double b_wait = 0, b_total = 0;  // last build: stream waits / whole call (ms)
+    bool b_trace = false;
+    std::vector<std::pair<const char*, double>> b_marks;
     int32_t last_path = 0;
     // per-request scratch, reused across requests
     Scratch s_accept, s_tcnt, s_rows, s_dst[6];
@@ -1697,6 +1708,27 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
             W = LH;
         }
     }
+    // Roughly time-ordered data (merged segments: docs displaced by up to an hour or so) has blocks spanning more keys
+    // than a two-per-CU window holds; each such block is then read once per W keys (multi-pass groups).  When the
+    // segment's blocks typically span more keys (90th percentile of the zone-map ranges), widen the window instead:
+    // one 1024-thread workgroup per CU with up to kLdsMax of LDS (the same 16 waves per CU).
+    bool wide = false;
+#ifndef ESGPU_WIDE_WINDOW
+#define ESGPU_WIDE_WINDOW 1
+#endif
+    if (ESGPU_WIDE_WINDOW && P.lds_mode && P.windowed && !P.kstart && hc && pl.interval > 0) {
+        const int64_t need = std::min<int64_t>(hc->zspan / pl.interval + 2, (int64_t)LH);
+        if (need > (int64_t)W) {
+            uint32_t w2 = W;
+            while ((int64_t)w2 < need && collect_lds_bytes(LT, w2 + 1, L_met, L_vcnt, L_ocnt) <= kLdsMax) ++w2;
+            if (w2 > W) {
+                W = w2;
+                wide = true;
+                if (W >= LH) { W = LH; P.windowed = 0; }
+                lds = collect_lds_bytes(LT, W, L_met, L_vcnt, L_ocnt);
+            }
+        }
+    }
     P.W = W;
     // grids with a terms dimension: lane-rotated copies of the additive cells while they still fit two workgroups per
     // CU (the Zipf-head terms otherwise serialise a wave's LDS atomics on one address)
@@ -1720,10 +1752,10 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     }
     const int hk = L_HIST ? (P.kstart ? 2 : 1) : 0;
     const int vk = (P.hv_f64 ? 1 : 0) | (P.mv_f64 ? 2 : 0);
-    const uint64_t occ_key = ((uint64_t)lds << 10) | ((uint64_t)vk << 8) | ((uint64_t)L_met << 4) | ((uint64_t)hk << 1) |
-                             (L_ORD ? 1 : 0);
+    const uint64_t occ_key = ((uint64_t)lds << 11) | ((uint64_t)wide << 10) | ((uint64_t)vk << 8) | ((uint64_t)L_met << 4) |
+                             ((uint64_t)hk << 1) | (L_ORD ? 1 : 0);
     if (pl.occ_key != occ_key) {
-        pl.occ = std::max(1, collect_occupancy(L_ORD, hk, L_met, lds, vk));
+        pl.occ = std::max(1, collect_occupancy(L_ORD, hk, L_met, lds, vk, wide));
         pl.occ_key = occ_key;
     }
     const uint32_t wg_per_cu = (uint32_t)pl.occ;
@@ -1733,10 +1765,18 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     // ESGPU_WG_WAVES > 1: more, shorter workgroup ranges than resident slots (tail balancing vs per-workgroup setup)
     const uint32_t target = (uint32_t)p->ctx->cus * wg_per_cu * ESGPU_WG_WAVES;
     const uint32_t bpw = (P.n_blocks + target - 1) / target;
-    P.blocks_per_wg = std::max(1u, bpw);
+#ifndef ESGPU_MIN_BPW
+#define ESGPU_MIN_BPW 32  // measured at 125M docs: terms(host) 0.19 -> 0.10 ms, terms{stats} -16 %, config 5 -8 %
+#endif
+    // a workgroup flushes its LDS cells once; with a terms dimension that is ~T x W global atomics, so keep at least
+    // ESGPU_MIN_BPW blocks per workgroup (fewer, longer ranges than the tail-balancing target) -- small segments
+    // otherwise pay about one global atomic per 30 docs.  Histogram-only grids flush only the keys they touched.
+    const uint32_t slots = (uint32_t)p->ctx->cus * wg_per_cu;
+    const uint32_t min_bpw = L_ORD ? std::min<uint32_t>(ESGPU_MIN_BPW, (P.n_blocks + slots - 1) / slots) : 1u;
+    P.blocks_per_wg = std::max(std::max(1u, bpw), min_bpw);
     const uint32_t grid = (P.n_blocks + P.blocks_per_wg - 1) / P.blocks_per_wg;
     HIPX(hipEventRecord(pl.e0, p->stream));
-    launch_collect(P, L_ORD, L_HIST, L_met, grid, lds, p->stream);
+    launch_collect(P, L_ORD, L_HIST, L_met, wide, grid, lds, p->stream);
     HIPX(hipGetLastError());
     HIPX(hipEventRecord(pl.e1, p->stream));
     p->last_bytes += bytes_per_doc * (uint64_t)s->max_doc + (d_accept ? ((uint64_t)s->max_doc + 7) / 8 : 0);
@@ -1899,6 +1939,18 @@ extern "C" int esgpu_plan_last_collect_stats(const esgpu_plan* cp, double* kerne
     });
 }
 
+// n u64 words from the device into pinned host memory (asynchronous): small transfers by a kernel writing through
+// the buffer's device mapping, large ones by DMA
+static void d2h_u64(esgpu_plan* p, PinnedBuf& dst, const void* src, size_t n) {
+    dst.ensure(std::max<size_t>(n, 1) * 8);
+    if (n == 0) return;
+    if (n * 8 <= (4u << 20)) {
+        launch_copy_u64((const unsigned long long*)src, (unsigned long long*)dst.dev(), n, p->stream);
+        HIPX(hipGetLastError());
+    } else {
+        HIPX(hipMemcpyAsync(dst.p, src, n * 8, hipMemcpyDeviceToHost, p->stream));
+    }
+}
 // build-phase stream waits, timed (esgpu_plan_last_build_stats: device wait vs host assembly)
 static double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -1907,6 +1959,10 @@ static void bsync(esgpu_plan* p) {
     const double t0 = now_ms();
     HIPX(hipStreamSynchronize(p->stream));
     p->b_wait += now_ms() - t0;
+}
+// ESGPU_TRACE_BUILD=1: per-phase marks of each build on stderr (diagnostics only)
+static void bmark(esgpu_plan* p, const char* what) {
+    if (p->b_trace) p->b_marks.emplace_back(what, now_ms());
 }
 
 extern "C" int esgpu_plan_last_build_stats(const esgpu_plan* p, double* total_ms, double* wait_ms) {
@@ -1925,16 +1981,16 @@ extern "C" int esgpu_plan_post_collection(esgpu_plan* p) {
         for (Pipeline& pl : p->pipes) {
             if (pl.kind != 1 || !pl.allocated) continue;
             // [0] = distinct encoded hashes inserted (LC pass), [1] = non-zero registers (register pass)
-            uint32_t* cnt = (uint32_t*)p->h_tcnt.ensure(16);
-            HIPX(hipMemcpyAsync(cnt, pl.lc_count.p, 8, hipMemcpyDeviceToHost, p->stream));
+            d2h_u64(p, p->h_tcnt, pl.lc_count.p, 1);
+            const uint32_t* cnt = p->h_tcnt.as<uint32_t>();
             bsync(p);
             const uint32_t m = 1u << pl.p;
             pl.any_value = cnt[0] > 0 || cnt[1] > 0;
             if (cnt[1] <= pl.lc_threshold && cnt[0] <= pl.lc_threshold) {  // LINEAR_COUNTING: the distinct encoded hashes
                 pl.hll_mode = 0;
                 const size_t cap = (size_t)pl.lc_mask + 1;
-                uint32_t* set = (uint32_t*)p->h_dst[0].ensure(cap * 4);
-                HIPX(hipMemcpyAsync(set, pl.lc_set.p, cap * 4, hipMemcpyDeviceToHost, p->stream));
+                d2h_u64(p, p->h_dst[0], pl.lc_set.p, cap / 2);  // cap is a power of two >= 1024
+                const uint32_t* set = p->h_dst[0].as<uint32_t>();
                 bsync(p);
                 pl.h_lc.clear();
                 for (size_t i = 0; i < cap; ++i) if (set[i]) pl.h_lc.push_back(set[i]);
@@ -1945,8 +2001,8 @@ extern "C" int esgpu_plan_post_collection(esgpu_plan* p) {
                 uint8_t* d8 = (uint8_t*)p->s_dst[0].ensure(p->ctx, m);
                 launch_pack_u8(pl.regs.as<unsigned int>(), m, d8, p->stream);
                 HIPX(hipGetLastError());
-                uint8_t* r = (uint8_t*)p->h_dst[0].ensure(m);
-                HIPX(hipMemcpyAsync(r, d8, m, hipMemcpyDeviceToHost, p->stream));
+                d2h_u64(p, p->h_dst[0], d8, std::max<size_t>(m / 8, 1));  // m = 2^p >= 16
+                const uint8_t* r = p->h_dst[0].as<uint8_t>();
                 bsync(p);
                 pl.h_regs.assign(r, r + m);
             }
@@ -2140,6 +2196,21 @@ static void append_leaves(const esgpu_plan* p, const Pipeline& pl, int j, const 
     }
 }
 
+static void reserve_buckets(Block& b, size_t buckets, size_t instances) {
+    b.key.reserve(b.key.size() + buckets);
+    b.bcount.reserve(b.bcount.size() + buckets);
+    b.berr.reserve(b.berr.size() + buckets);
+    b.term_off.reserve(b.term_off.size() + buckets);
+    b.boff.reserve(b.boff.size() + instances);
+    b.doc_count_error.reserve(b.doc_count_error.size() + instances);
+    b.other_doc_count.reserve(b.other_doc_count.size() + instances);
+}
+static void reserve_leaves(Block& b, size_t n) {
+    if (b.type == ESGPU_AGG_CARDINALITY) return;
+    for (auto* v : {&b.sum, &b.min, &b.max, &b.sumsq}) v->reserve(v->size() + n);
+    b.count.reserve(b.count.size() + n);
+}
+
 // histogram buckets of the given key slots (host cells `cells`, counts `counts[i]`), appended to the open instance
 static void append_hist_buckets(const Pipeline& B, const std::vector<uint32_t>& slots, const std::vector<int64_t>& counts,
                                 Block& r) {
@@ -2179,28 +2250,25 @@ static void point_cells(Pipeline& pl, const void* const src[6]) {
     pl.hc.mx = (const unsigned long long*)h(4);
     pl.hc.sq = (const double*)h(5);
 }
-// the rows [k][H] of the given ordinals, gathered on the GPU, copied (asynchronously) into the pipeline's pinned cells
+// the rows [k][H] of the given ordinals, gathered on the GPU straight into the pipeline's pinned cells (asynchronous)
 static void fetch_rows(esgpu_plan* p, Pipeline& pl, const uint32_t* drows, uint32_t k) {
     const void* src[6];
     grid_arrays(pl, src);
     GatherParams G{};
     G.rows = drows;
     G.k = k; G.H = pl.H; G.T = pl.T;
-    void* dst[6] = {};
     const size_t bytes = std::max<size_t>((size_t)k * pl.H, 1) * 8;
     for (int a = 0; a < 6; ++a) {
         if (!src[a]) continue;
-        dst[a] = pl.d_rows[a].ensure(p->ctx, bytes);
+        pl.h_cells[a].ensure(bytes);
         G.src[G.narrays] = (const unsigned long long*)src[a];
-        G.dst[G.narrays] = (unsigned long long*)dst[a];
+        G.dst[G.narrays] = (unsigned long long*)pl.h_cells[a].dev();
         G.narrays++;
     }
     if (k) {
         launch_gather_rows(G, p->stream);
         HIPX(hipGetLastError());
     }
-    for (int a = 0; a < 6; ++a)
-        if (src[a]) HIPX(hipMemcpyAsync(pl.h_cells[a].ensure(bytes), dst[a], (size_t)k * pl.H * 8, hipMemcpyDeviceToHost, p->stream));
     point_cells(pl, src);
 }
 // the whole grid into the pipeline's pinned cells (asynchronous)
@@ -2209,7 +2277,7 @@ static void fetch_grid(esgpu_plan* p, Pipeline& pl) {
     grid_arrays(pl, src);
     const size_t cells = (size_t)pl.T * pl.H;
     for (int a = 0; a < 6; ++a)
-        if (src[a]) HIPX(hipMemcpyAsync(pl.h_cells[a].ensure(cells * 8), src[a], cells * 8, hipMemcpyDeviceToHost, p->stream));
+        if (src[a]) d2h_u64(p, pl.h_cells[a], src[a], cells);
     point_cells(pl, src);
 }
 
@@ -2339,8 +2407,8 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
         HIPX(hipMemsetAsync(K.out_sum, 0, 8, st));
         launch_topk(K, st);
         HIPX(hipGetLastError());
-        unsigned long long* hk = (unsigned long long*)p->h_keys.ensure(((size_t)kk + 1) * 8);
-        HIPX(hipMemcpyAsync(hk, dk, ((size_t)kk + 1) * 8, hipMemcpyDeviceToHost, st));
+        d2h_u64(p, p->h_keys, dk, (size_t)kk + 1);
+        const unsigned long long* hk = p->h_keys.as<unsigned long long>();
         bsync(p);
         other = (int64_t)hk[kk];
         for (uint32_t i = 0; i < (uint32_t)k_req; ++i) {
@@ -2355,14 +2423,15 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
             top.push_back(tp);
         }
     } else {
-        unsigned long long* tcnt = (unsigned long long*)p->h_tcnt.ensure((size_t)T * 8);
-        HIPX(hipMemcpyAsync(tcnt, dcnt, (size_t)T * 8, hipMemcpyDeviceToHost, st));
+        d2h_u64(p, p->h_tcnt, dcnt, T);
+        const unsigned long long* tcnt = p->h_tcnt.as<unsigned long long>();
         if (agg_order) fetch_grid(p, p->pipes[ord_ref.pipe]);  // every ordinal's metric partials
         bsync(p);
         const Pipeline* OP = agg_order ? &p->pipes[ord_ref.pipe] : nullptr;
         top = select_terms(tn.s, tcnt, (uint32_t)P0.value_count, &other,
                            [&](uint32_t ord) { return order_value(p, tn, *OP, ord_ref.leaf, ord); });
     }
+    bmark(p, "selected");
     const uint32_t k = (uint32_t)top.size();
     // gather the winners' rows [k][H] of every pipeline on the GPU and bring back only those
     uint32_t* rows = (uint32_t*)p->h_rows.ensure(std::max<size_t>(k, 1) * 4);
@@ -2373,7 +2442,9 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
         Pipeline& pl = p->pipes[pi];
         if (pl.allocated) fetch_rows(p, pl, drows, k);
     }
+    bmark(p, "fetch_issued");
     bsync(p);
+    bmark(p, "fetched");
     for (int pi : g.pipes) {
         Pipeline& pl = p->pipes[pi];
         if (!pl.allocated || pl.cards.empty()) continue;
@@ -2395,6 +2466,21 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
             const Pipeline& L = p->pipes[l.pipe];
             require(!B0.allocated || (L.H == B0.H && L.key0 == B0.key0), ESGPU_ERR_DEVICE,
                     "sibling pipelines disagree on the key grid");
+        }
+    }
+    // one allocation per array: the bucket children's total bucket count over the winners, reserved up front
+    for (size_t ki = 0; ki < g.kids.size(); ++ki) {
+        const ChildSrc& kid = g.kids[ki];
+        const Pipeline& B0 = kid.bucket ? p->pipes[kid.pipes[0]] : p->pipes[kid.leaf.pipe];
+        if (!B0.allocated) continue;
+        size_t nb = k;
+        if (kid.bucket) {
+            nb = 0;
+            for (size_t c = 0; c < (size_t)k * B0.H; ++c) nb += B0.hc.cnt[c] != 0;
+            reserve_buckets(r.subs[ki], nb, k);
+            for (Block& gb : r.subs[ki].subs) reserve_leaves(gb, nb);
+        } else {
+            reserve_leaves(r.subs[ki], nb);
         }
     }
     std::vector<uint32_t> slots, cells;
@@ -2450,8 +2536,8 @@ static Block build_hist_root(esgpu_plan* p, const Group& g) {
     const bool p0_terms = P0.term_spec >= 0;
     unsigned long long* ocnt = nullptr;
     if (p0_terms) {  // histogram doc counts counted per doc beside the [H][T] cells (OCNT_HIST)
-        ocnt = (unsigned long long*)P0.h_ocnt.ensure((size_t)P0.H * 8);
-        HIPX(hipMemcpyAsync(ocnt, P0.g_ocnt.p, (size_t)P0.H * 8, hipMemcpyDeviceToHost, st));
+        d2h_u64(p, P0.h_ocnt, P0.g_ocnt.p, P0.H);
+        ocnt = P0.h_ocnt.as<unsigned long long>();
     }
     bsync(p);
     for (int pi : g.pipes) {
@@ -2546,10 +2632,14 @@ extern "C" int esgpu_plan_build(esgpu_plan* p, esgpu_result** out) {
         require(p && out, ESGPU_ERR_INVALID, "null argument");
         const double t0 = now_ms();
         p->b_wait = 0;
+        p->b_trace = std::getenv("ESGPU_TRACE_BUILD") != nullptr;
+        p->b_marks.clear();
+        bmark(p, "start");
         if (!p->posted) {
             int rc = esgpu_plan_post_collection(p);
             if (rc != ESGPU_OK) throw EsError(rc, g_err);
         }
+        bmark(p, "posted");
         HIPX(hipSetDevice(p->ctx->device));
         std::unique_ptr<ResultHolder> h(new ResultHolder());
         // top-level aggregations in request order; a filter aggregation (InternalFilter, FilterAggregator.java:72-80)
@@ -2567,8 +2657,8 @@ extern "C" int esgpu_plan_build(esgpu_plan* p, esgpu_result** out) {
             fb.n = 1;
             uint64_t dc = 0;
             if (cnt && cnt->allocated) {
-                uint64_t* hc = (uint64_t*)p->h_tcnt.ensure(16);
-                HIPX(hipMemcpyAsync(hc, cnt->g_cnt.p, 8, hipMemcpyDeviceToHost, p->stream));
+                d2h_u64(p, p->h_tcnt, cnt->g_cnt.p, 1);
+                const uint64_t* hc = p->h_tcnt.as<uint64_t>();
                 bsync(p);
                 dc = hc[0];
             }
@@ -2576,9 +2666,22 @@ extern "C" int esgpu_plan_build(esgpu_plan* p, esgpu_result** out) {
             for (size_t j = 0; j < p->specs[r].children.size(); ++j) fb.subs.push_back(build_group(p, p->groups[gi++]));
             h->aggs.push_back(std::move(fb));
         }
+        bmark(p, "assembled");
         h->export_view();
         *out = &h.release()->pub;
         p->b_total = now_ms() - t0;
+        bmark(p, "exported");
+        if (p->b_trace) {
+            std::string line = "esgpu build:";
+            char buf[64];
+            for (size_t i = 1; i < p->b_marks.size(); ++i) {
+                std::snprintf(buf, sizeof buf, " %s +%.3f", p->b_marks[i].first, p->b_marks[i].second - p->b_marks[i - 1].second);
+                line += buf;
+            }
+            std::snprintf(buf, sizeof buf, " (wait %.3f ms)\n", p->b_wait);
+            line += buf;
+            std::fputs(line.c_str(), stderr);
+        }
     });
 }
 

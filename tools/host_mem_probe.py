@@ -1,11 +1,14 @@
 """Host-side read cost of the plan's pinned staging buffers (esgpu_host_alloc = hipHostMalloc) vs pageable memory:
 the build step reads the gathered winner cells from pinned memory on the host."""
 import json
+import os
+import sys
 import time
 
 import numpy as np
 
-from elasticsearch_amd import Engine, pinned_empty
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from elasticsearch_amd import Engine, pinned_empty  # noqa: E402
 
 
 def _time(f, reps=20):
