@@ -227,18 +227,35 @@ def main():
                 kernel_bytes[0] += nbytes
 
     host_ms = {"build": 0.0, "reduce": 0.0}
+    # the coordinating reduce of a request runs on a worker thread (the C call releases the GIL), the way a
+    # coordinating node merges one request's shard results while the data nodes collect the next; requests are
+    # reduced in order, and every one is finished inside the timed region (drain() below)
+    from concurrent.futures import ThreadPoolExecutor
+    reducer = ThreadPoolExecutor(1)
+    pending = []
+
+    def reduce_request(parts):
+        t = time.perf_counter()
+        out = comm.reduce(parts) if comm else ea.reduce(parts)
+        host_ms["reduce"] += (time.perf_counter() - t) * 1e3
+        return out
+
+    def drain():
+        nonlocal final
+        while pending:
+            final = pending.pop(0).result()
 
     def finish(p, unit):
-        nonlocal final, partial
+        nonlocal partial
         t0 = time.perf_counter()
         partial.append(p.build())
-        t1 = time.perf_counter()
+        host_ms["build"] += (time.perf_counter() - t0) * 1e3
         if unit == units_per_request - 1:
-            final = comm.reduce(partial) if comm else ea.reduce(partial)
+            pending.append(reducer.submit(reduce_request, partial))
             partial = []
-        t2 = time.perf_counter()
-        host_ms["build"] += (t1 - t0) * 1e3
-        host_ms["reduce"] += (t2 - t1) * 1e3
+            while len(pending) > 1 and pending[0].done():
+                drain_one = pending.pop(0)
+                drain_one.result()
 
     # one unit = one collect (+ build) of a shard, or of all this GPU's shards of a fixed-shape request; with two plans
     # the host build + reduce of one unit overlaps the collect kernel of the next -- how a node serves a stream of
@@ -256,6 +273,7 @@ def main():
                     finish(*pend.pop(0))
         while pend:
             finish(*pend.pop(0))
+        drain()
 
     def timed(depth, record):
         if dist:

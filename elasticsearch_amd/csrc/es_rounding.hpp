@@ -59,6 +59,7 @@ struct TimeZone {
 
     bool fixed() const { return starts.size() <= 1; }
     int64_t offset(int64_t t) const {  // getOffset(instant)
+        if (starts.size() == 1) return offs[0];
         const size_t i = (size_t)(std::upper_bound(starts.begin(), starts.end(), t) - starts.begin());
         return offs[i ? i - 1 : 0];
     }
@@ -68,6 +69,7 @@ struct TimeZone {
     }
     int64_t utc_to_local(int64_t t) const { return t + offset(t); }  // convertUTCToLocal
     int64_t local_to_utc(int64_t local) const {  // convertLocalToUTC(instantLocal, strict = false)
+        if (starts.size() == 1) return local - offs[0];
         const int64_t offset_local = offset(local);
         int64_t off = offset(local - offset_local);
         if (offset_local != off && offset_local < 0) {  // Western hemisphere: is instantLocal in a DST gap?

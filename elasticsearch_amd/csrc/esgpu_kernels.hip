@@ -84,721 +84,42 @@ void launch_synth(const SynthParams& p, hipStream_t stream) {
     hipLaunchKernelGGL(synth_kernel, dim3(4096), dim3(256), 0, stream, p);
 }
 
-// ------------------------------------------------------------------------------------------------------------
-// collect
-// ------------------------------------------------------------------------------------------------------------
-constexpr int kWG = 512;                         // threads per workgroup (8 waves)
-constexpr int kVec = 4;                          // consecutive docs per thread per iteration
-constexpr int kIterDocs = kWG * kVec;            // 2048
-constexpr int kItersPerBlock = kBlockDocs / kIterDocs;  // 4
-#ifndef ESGPU_MAX_PASSES  // passes over a block whose keys span more than the LDS window, before global atomics
-#define ESGPU_MAX_PASSES 8
-#endif
-constexpr int kMaxPasses = ESGPU_MAX_PASSES;
-#ifndef ESGPU_GROUP_BLOCKS  // blocks per multi-pass group
-#define ESGPU_GROUP_BLOCKS 4
-#endif
-constexpr uint32_t kGroup = ESGPU_GROUP_BLOCKS;
-#ifndef ESGPU_NBUF_NARROW  // load buffers in flight per thread for shapes reading one narrow column
-#define ESGPU_NBUF_NARROW 2  // measured: 4 no faster for terms(host), 4 % slower for date_histogram
-#endif
+}  // namespace esgpu
 
-struct Doc4 {
-    uint32_t ord[kVec];
-    int64_t hv[kVec];
-    double mv[kVec];
-    uint32_t ok;      // bit j: doc j passes filters / accept / bounds
-    uint32_t hpres;   // bit j: hist value present
-    uint32_t mpres;   // bit j: metric value present
-};
+#include "esgpu_collect.hpp"
 
-__device__ __forceinline__ uint32_t bits4(const uint64_t* bm, uint32_t doc0) {
-    return (uint32_t)(bm[doc0 >> 6] >> (doc0 & 63)) & 0xFu;
+namespace esgpu {
+
+void launch_zone_keys(const CollectParams& p, int64_t* out, hipStream_t st) {
+    if (p.n_blocks == 0) return;
+    const uint32_t g = (p.n_blocks + 255) / 256;
+    if (p.kstart) hipLaunchKernelGGL(zone_keys_kernel<true>, dim3(g), dim3(256), 0, st, p, out);
+    else hipLaunchKernelGGL(zone_keys_kernel<false>, dim3(g), dim3(256), 0, st, p, out);
 }
 
-// Column streams are read once per request: ESGPU_NT=1 marks them non-temporal (nt) so they do not displace the
-// cell grid and the zone maps in L2 / MALL.
-#ifndef ESGPU_NT
-#define ESGPU_NT 0
-#endif
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ u32x4_t load16(const void* p) {
-#if ESGPU_NT
-    return __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
-#else
-    return *reinterpret_cast<const u32x4_t*>(p);
-#endif
-}
-__device__ __forceinline__ uint64_t join64(uint32_t lo, uint32_t hi) { return (uint64_t)lo | ((uint64_t)hi << 32); }
-__device__ __forceinline__ void load_i64x4(const int64_t* p, uint32_t doc0, int64_t out[4]) {
-    const u32x4_t a = load16(p + doc0), b = load16(p + doc0 + 2);
-    out[0] = (int64_t)join64(a.x, a.y); out[1] = (int64_t)join64(a.z, a.w);
-    out[2] = (int64_t)join64(b.x, b.y); out[3] = (int64_t)join64(b.z, b.w);
-}
-__device__ __forceinline__ void load_f64x4(const double* p, uint32_t doc0, double out[4]) {
-    const u32x4_t a = load16(p + doc0), b = load16(p + doc0 + 2);
-    out[0] = bits_dbl(join64(a.x, a.y)); out[1] = bits_dbl(join64(a.z, a.w));
-    out[2] = bits_dbl(join64(b.x, b.y)); out[3] = bits_dbl(join64(b.z, b.w));
-}
-__device__ __forceinline__ void load_u32x4(const uint32_t* p, uint32_t doc0, uint32_t out[4]) {
-    const u32x4_t a = load16(p + doc0);
-    out[0] = a.x; out[1] = a.y; out[2] = a.z; out[3] = a.w;
-}
-
-__device__ __forceinline__ uint32_t eval_pred(const PredDev& q, uint32_t doc0) {
-    uint32_t m = 0;
-    if (q.kind == PRED_ORD_EQ || q.kind == PRED_ORD_RANGE) {  // a term is the range [ord, ord]
-        uint32_t o[4];
-        load_u32x4((const uint32_t*)q.col, doc0, o);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) m |= (uint32_t)((int64_t)o[j] >= q.lo && (int64_t)o[j] <= q.hi && o[j] != kMissingOrd) << j;
-    } else if (q.kind == PRED_F64_RANGE) {
-        double v[4];
-        load_f64x4((const double*)q.col, doc0, v);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const bool lo = q.lo_incl ? v[j] >= q.dlo : v[j] > q.dlo;
-            const bool hi = q.hi_incl ? v[j] <= q.dhi : v[j] < q.dhi;
-            m |= (uint32_t)(lo && hi) << j;
-        }
-    } else {  // PRED_I64_RANGE (term on a long is the degenerate range [t, t])
-        int64_t v[4];
-        load_i64x4((const int64_t*)q.col, doc0, v);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) m |= (uint32_t)(v[j] >= q.lo && v[j] <= q.hi) << j;
-    }
-    if (q.present) m &= bits4(q.present, doc0);
-    return m;
-}
-
-// VK (value kinds, compile time): bit 0 = the histogram column holds doubles (keys are (long) casts), bit 1 = the
-// metric column holds doubles (else longs cast to double).  A runtime branch on these cost the north-star kernel ~6 %.
-template <bool ORD, bool HIST, int MET, int VK>
-__device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0, Doc4& d) {
-    uint32_t ok = 0xF;
-    if (doc0 + 4 > P.n_docs) ok = doc0 >= P.n_docs ? 0u : ((1u << (P.n_docs - doc0)) - 1u);
-    if (P.accept) ok &= bits4(P.accept, doc0);
-    for (int k = 0; k < P.npred; ++k) ok &= eval_pred(P.pred[k], doc0);
-    d.ok = ok;
-    if (ORD) load_u32x4(P.ord, doc0, d.ord);
-    if (HIST) {
-        load_i64x4(P.hv, doc0, d.hv);
-        if (VK & 1) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) d.hv[j] = java_long(bits_dbl((uint64_t)d.hv[j]));
-        }
-        d.hpres = P.hv_present ? bits4(P.hv_present, doc0) : 0xFu;
-    }
-    if (MET > 0) {
-        if (VK & 2) {
-            load_f64x4((const double*)P.mv, doc0, d.mv);
-        } else {
-            int64_t t[4];
-            load_i64x4((const int64_t*)P.mv, doc0, t);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) d.mv[j] = (double)t[j];  // FieldData.castToDouble
-        }
-        d.mpres = P.mv_present ? bits4(P.mv_present, doc0) : 0xFu;
-    }
-}
-
-// Accumulator views: either the workgroup's LDS window or the global cell grid.
-struct Acc {
-    uint32_t* cnt32;                // LDS
-    unsigned long long* cnt64;      // global
-    uint32_t* vcnt32;
-    unsigned long long* vcnt64;
-    double* sum;
-    unsigned long long* mn;         // LDS min / max: interleaved (mx == mn + 1, stride 2) or two arrays (stride 1)
-    unsigned long long* mx;
-    double* sq;
-    uint32_t* ocnt32;
-    unsigned long long* ocnt64;
-    uint32_t mstride;               // LDS min/max stride; 1 in the global grid
-    uint32_t coff;                  // this lane's copy of the additive LDS cells (CollectParams.ncopies); 0 in the grid
-};
-
-template <int MET, bool LDS, int MS>
-__device__ __forceinline__ void add_value(const Acc& a, uint32_t c, double x, bool has_vcnt) {
-    const uint32_t ca = LDS ? c + a.coff : c;  // additive cell (lane copy)
-    if (LDS) {
-        if (has_vcnt) atomicAdd(&a.vcnt32[ca], 1u);
-    } else {
-        if (has_vcnt) atomicAdd(&a.vcnt64[c], 1ull);
-    }
-    atomicAdd(&a.sum[ca], x);
-    if (MET >= 2) {
-        const bool nan = x != x;
-        const unsigned long long e = sortable(x);
-        const unsigned long long emn = nan ? 0ull : e;
-        const unsigned long long emx = nan ? ~0ull : e;
-        // read-check before the atomic: reads of one address broadcast, and min/max converge quickly
-        constexpr uint32_t st = LDS ? MS : 1;
-        const unsigned long long cmn = a.mn[c * st], cmx = a.mx[c * st];
-        if (emn < cmn) atomicMin(&a.mn[c * st], emn);
-        if (emx > cmx) atomicMax(&a.mx[c * st], emx);
-    }
-    if (MET >= 3) atomicAdd(&a.sq[ca], x * x);  // ExtendedStatsAggregator: sumOfSqr += value * value (no FMA)
-}
-
-// Per-doc update.  `slot` is the key index relative to the accumulator's first slot (window or grid).
-// `outer` = false in the extra passes over a multi-pass block (its docs' terms were counted in the first pass).
-template <bool ORD, bool HIST, int MET, bool LDS, int MS>
-__device__ __forceinline__ void update_doc(const CollectParams& P, const Acc& a, uint32_t T, bool has_t, uint32_t t,
-                                           bool has_h, uint32_t slot, bool mpres, double x, bool outer) {
-    if (P.ocnt_mode == OCNT_TERMS) {
-        if (has_t && outer) {
-            if (LDS) atomicAdd(&a.ocnt32[t], 1u); else atomicAdd(&a.ocnt64[t], 1ull);
-        }
-    } else if (!LDS && P.ocnt_mode == OCNT_TERMS_DERIVED && has_t && has_h) {
-        atomicAdd(&a.ocnt64[t], 1ull);
-    } else if (P.ocnt_mode == OCNT_HIST && has_h) {
-        if (LDS) atomicAdd(&a.ocnt32[slot], 1u); else atomicAdd(&a.ocnt64[slot], 1ull);
-    }
-    if (!(has_t && has_h)) return;
-    const uint32_t c = slot * T + t;
-    if (LDS) atomicAdd(&a.cnt32[c + a.coff], 1u); else atomicAdd(&a.cnt64[c], 1ull);
-    if (MET > 0 && mpres) add_value<MET, LDS, MS>(a, c, x, P.vcnt_mode != 0);
-}
-
-// Wave-level pre-aggregation for a cell shared by the whole wave (time-sorted data without a terms dimension):
-// one LDS atomic per quantity per wave instead of 256 conflicting ones.
-__device__ __forceinline__ double wave_sum_f64(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long w = __shfl_xor(v, o, 64);
-        v = w < v ? w : v;
-    }
-    return v;
-}
-__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long w = __shfl_xor(v, o, 64);
-        v = w > v ? w : v;
-    }
-    return v;
-}
-
-// grid key index of a value: affine roundings divide, table roundings (calendar units, DST zones) search the bucket
-// start instants; values outside the grid give an index outside [0, H)
-template <bool KT>
-__device__ __forceinline__ int64_t key_index(const CollectParams& P, int64_t v) {
-    if (!KT) return floor_div64(v - P.offset, P.interval) - P.key0;
-    if (v < P.kstart[0]) return -1;
-    uint32_t lo = 0, hi = P.nsteps;  // kstart[lo] <= v < kstart[hi] (kstart[nsteps] = +inf)
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (P.kstart[mid] <= v) lo = mid; else hi = mid;
-    }
-    return P.kslot ? P.kslot[lo] : lo;
-}
-
-// key slot of a value relative to `base` (= value of the first slot); 32-bit magic division fast path
-__device__ __forceinline__ uint32_t slot_of(const CollectParams& P, int64_t v, int64_t base) {
-    if (P.fast32) return magic_div((uint32_t)((uint64_t)v - (uint64_t)base), P.mg_m, P.mg_s1, P.mg_s2, (uint32_t)P.interval);
-    return (uint32_t)(floor_div64(v - P.offset, P.interval) - floor_div64(base - P.offset, P.interval));
-}
-
-// Per-thread run accumulator for histogram-only plans over time-sorted data: a thread's consecutive docs share a
-// key slot, so their count / sum / min / max / sum-of-squares are combined in registers and reach LDS only when
-// the slot changes (an hour boundary) or at a window flush -- no per-doc LDS traffic.
-struct Run {
-    uint32_t slot;  // 0xFFFFFFFF = empty
-    uint32_t cnt, vc;
-    double sum, sq;
-    unsigned long long mn, mx;
-};
-
-__device__ __forceinline__ void run_reset(Run& r) {
-    r.slot = 0xFFFFFFFFu;
-    r.cnt = 0;
-    r.vc = 0;
-    r.sum = 0.0;
-    r.sq = 0.0;
-    r.mn = kMinInit;
-    r.mx = kMaxInit;
-}
-
-template <int MET, int MS>
-__device__ __forceinline__ void run_flush(const CollectParams& P, const Acc& a, Run& r) {
-    if (r.slot != 0xFFFFFFFFu) {
-        const uint32_t c = r.slot;  // T == 1: cell == slot
-        atomicAdd(&a.cnt32[c], r.cnt);
-        if (MET > 0 && r.vc) {
-            if (P.vcnt_mode) atomicAdd(&a.vcnt32[c], r.vc);
-            atomicAdd(&a.sum[c], r.sum);
-            if (MET >= 2) {
-                const unsigned long long cmn = a.mn[MS * c], cmx = a.mx[MS * c];  // LDS
-                if (r.mn < cmn) atomicMin(&a.mn[MS * c], r.mn);
-                if (r.mx > cmx) atomicMax(&a.mx[MS * c], r.mx);
-            }
-            if (MET >= 3) atomicAdd(&a.sq[c], r.sq);
-        }
-    }
-    run_reset(r);
-}
-
-// Several run accumulators per thread (runs_for<MET>): roughly time-ordered data (a doc displaced by up to an hour) alternates between
-// neighbouring keys, which a single run would flush to LDS on almost every doc (conflicting LDS atomics on ~3
-// addresses per wave).  A miss replaces the runs round-robin.
-#ifndef ESGPU_RUNS  // run accumulators with a metric (measured: 3 takes config 2 at +-1 h jitter from 4.6 to 3.0 ms)
-#define ESGPU_RUNS 3
-#endif
-// counting only (MET 0): one run -- a count flush is a single LDS add, and the run array would go to scratch
-template <int MET> constexpr int runs_for() { return MET == 0 ? 1 : ESGPU_RUNS; }
-template <int NR>
-struct Runs {
-    Run r[NR];
-    uint32_t victim;
-};
-template <int NR>
-__device__ __forceinline__ void runs_reset(Runs<NR>& R) {
-#pragma unroll
-    for (int k = 0; k < NR; ++k) run_reset(R.r[k]);
-    R.victim = 0;
-}
-template <int MET, int MS, int NR>
-__device__ __forceinline__ void runs_flush(const CollectParams& P, const Acc& a, Runs<NR>& R) {
-#pragma unroll
-    for (int k = 0; k < NR; ++k) run_flush<MET, MS>(P, a, R.r[k]);
-}
-template <int MET, int MS, int NR>
-__device__ __forceinline__ void runs_add(const CollectParams& P, const Acc& a, Runs<NR>& R, uint32_t slot, bool mpres, double x) {
-    int hit = -1;
-#pragma unroll
-    for (int k = 0; k < NR; ++k) hit = R.r[k].slot == slot ? k : hit;
-    if (hit < 0) {
-        hit = NR == 1 ? 0 : (int)R.victim;
-#pragma unroll
-        for (int k = 0; k < NR; ++k)
-            if (k == hit) {
-                run_flush<MET, MS>(P, a, R.r[k]);
-                R.r[k].slot = slot;
-            }
-        if (NR > 1) R.victim = R.victim + 1 == (uint32_t)NR ? 0u : R.victim + 1;
-    }
-#pragma unroll
-    for (int k = 0; k < NR; ++k) {
-        if (k != hit) continue;
-        Run& run = R.r[k];
-        ++run.cnt;
-        if (MET > 0 && mpres) {
-            ++run.vc;
-            run.sum += x;
-            if (MET >= 3) run.sq += x * x;
-            if (MET >= 2) {
-                const bool nan = x != x;
-                const unsigned long long e = sortable(x);
-                const unsigned long long emn = nan ? 0ull : e, emx = nan ? ~0ull : e;
-                run.mn = emn < run.mn ? emn : run.mn;
-                run.mx = emx > run.mx ? emx : run.mx;
-            }
-        }
-    }
-}
-
-template <bool ORD, bool HIST, int MET, bool LDS, bool KT, int MS>
-__device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, const Doc4& d, uint32_t T, int64_t base,
-                                         uint32_t win0, Runs<runs_for<MET>()>& run, uint32_t mw = 0, bool outer = true) {
-    uint32_t slot[kVec];
-    bool hv_ok[kVec];
-#pragma unroll
-    for (int j = 0; j < kVec; ++j) {
-        hv_ok[j] = true;
-        slot[j] = 0;
-        if (HIST) {
-            hv_ok[j] = (d.hpres >> j) & 1;
-            if (LDS) {
-                if (KT) {
-                    const int64_t k = key_index<KT>(P, d.hv[j]) - (int64_t)win0;
-                    slot[j] = (uint32_t)k;
-                    if (mw) hv_ok[j] = hv_ok[j] && k >= 0 && k < (int64_t)mw;
-                } else {
-                    slot[j] = slot_of(P, d.hv[j], base);
-                    // 64-bit range test: slot_of's 32-bit fast path wraps for values 2^32 past the window
-                    if (mw) hv_ok[j] = hv_ok[j] && (uint64_t)d.hv[j] - (uint64_t)base < (uint64_t)mw * (uint64_t)P.interval;
-                }
-            } else {
-                const int64_t k = key_index<KT>(P, d.hv[j]);
-                hv_ok[j] = hv_ok[j] && k >= 0 && k < (int64_t)P.H;
-                slot[j] = (uint32_t)k;
-            }
-        }
-    }
-    if (LDS && !ORD) {  // ocnt_mode is OCNT_NONE without a terms dimension; without HIST the slot is always 0
-#pragma unroll
-        for (int j = 0; j < kVec; ++j) {
-            if (!((d.ok >> j) & 1) || !hv_ok[j]) continue;
-            runs_add<MET, MS>(P, a, run, slot[j], MET > 0 && ((d.mpres >> j) & 1), MET > 0 ? d.mv[j] : 0.0);
-        }
-        return;
-    }
-#pragma unroll
-    for (int j = 0; j < kVec; ++j) {
-        if (!((d.ok >> j) & 1)) continue;
-        const uint32_t t = ORD ? d.ord[j] : 0u;
-        const bool has_t = ORD ? (t != kMissingOrd && t < T) : true;
-        update_doc<ORD, HIST, MET, LDS, MS>(P, a, T, has_t, t, hv_ok[j], slot[j], MET > 0 && ((d.mpres >> j) & 1),
-                                        MET > 0 ? d.mv[j] : 0.0, outer);
-    }
-}
-
-template <int MET, int MS, int WGS>
-__device__ void flush_window(const CollectParams& P, const Acc& s, uint32_t T, uint32_t W, uint32_t win0, uint32_t ncp = 1) {
-    __syncthreads();
-    const uint32_t C = T * W;
-    if (P.ocnt_mode == OCNT_TERMS_DERIVED) {  // per-term totals of this window (one atomic per term)
-        for (uint32_t t = threadIdx.x; t < T; t += WGS) {
-            uint32_t tot = 0;
-            for (uint32_t k = 0; k < ncp; ++k)
-                for (uint32_t l = 0; l < W; ++l) tot += s.cnt32[k * C + l * T + t];
-            if (tot) atomicAdd(&P.g_ocnt[t], (unsigned long long)tot);
-        }
-        __syncthreads();
-    }
-    for (uint32_t c = threadIdx.x; c < C; c += WGS) {
-        uint32_t n = 0;
-        for (uint32_t k = 0; k < ncp; ++k) n += s.cnt32[k * C + c];
-        if (n == 0) continue;
-        const uint32_t local = c / T;
-        const uint32_t t = c - local * T;
-        const uint32_t slot = win0 + local;
-        if (slot >= P.H) continue;
-        const size_t g = (size_t)slot * T + t;
-        atomicAdd(&P.g_cnt[g], (unsigned long long)n);
-        for (uint32_t k = 0; k < ncp; ++k) s.cnt32[k * C + c] = 0;
-        if (MET > 0) {
-            if (P.vcnt_mode) {
-                uint32_t vc = 0;
-                for (uint32_t k = 0; k < ncp; ++k) { vc += s.vcnt32[k * C + c]; s.vcnt32[k * C + c] = 0; }
-                atomicAdd(&P.g_vcnt[g], (unsigned long long)vc);
-            }
-            double sum = 0.0;
-            for (uint32_t k = 0; k < ncp; ++k) { sum += s.sum[k * C + c]; s.sum[k * C + c] = 0.0; }
-            atomicAdd(&P.g_sum[g], sum);
-            if (MET >= 2) {
-                const unsigned long long mn = s.mn[MS * c], mx = s.mx[MS * c];
-                if (mn != kMinInit) atomicMin(&P.g_min[g], mn);
-                if (mx != kMaxInit) atomicMax(&P.g_max[g], mx);
-                s.mn[MS * c] = kMinInit;
-                s.mx[MS * c] = kMaxInit;
-            }
-            if (MET >= 3) {
-                double sq = 0.0;
-                for (uint32_t k = 0; k < ncp; ++k) { sq += s.sq[k * C + c]; s.sq[k * C + c] = 0.0; }
-                atomicAdd(&P.g_sq[g], sq);
-            }
-        }
-    }
-    if (P.ocnt_mode == OCNT_TERMS) {
-        for (uint32_t t = threadIdx.x; t < T; t += WGS) {
-            const uint32_t n = s.ocnt32[t];
-            if (n) { atomicAdd(&P.g_ocnt[t], (unsigned long long)n); s.ocnt32[t] = 0; }
-        }
-    } else if (P.ocnt_mode == OCNT_HIST) {
-        for (uint32_t l = threadIdx.x; l < W; l += WGS) {
-            const uint32_t n = s.ocnt32[l];
-            if (n && win0 + l < P.H) { atomicAdd(&P.g_ocnt[win0 + l], (unsigned long long)n); }
-            s.ocnt32[l] = 0;
-        }
-    }
-    __syncthreads();
-}
-
-// HK: 0 = no histogram dimension, 1 = affine rounding, 2 = bucket table (calendar units / DST zones)
-// WGS: threads per workgroup -- 512 (two resident per CU, each with an LDS window of <= 64 KB), or 1024 for
-// histogram grids whose data needs a wider window than 64 KB holds (one workgroup per CU with up to 150 KB of LDS,
-// the same 16 waves per CU)
-template <bool ORD, int HK, int MET, int VK, int WGS>
-__global__ __launch_bounds__(WGS) void collect_kernel(CollectParams P) {
-    constexpr int kIterDocsW = WGS * kVec;
-    constexpr int kItersPerBlockW = kBlockDocs / kIterDocsW;
-    constexpr bool HIST = HK != 0;
-    constexpr bool KT = HK == 2;
-    // min/max LDS layout: interleaved (one paired read per check) with a key dimension, two arrays without one
-    // (terms{stats}: measured 11 % faster with separate arrays, the interleaved pairs conflict on fewer banks)
-    constexpr int kMS = HIST ? 2 : 1;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t T = ORD ? P.T : 1u;
-    const uint32_t W = HIST ? P.W : 1u;
-    const uint32_t C = T * W;
-
-    Acc g;  // global grid view
-    g.cnt32 = nullptr; g.vcnt32 = nullptr; g.ocnt32 = nullptr;
-    g.cnt64 = P.g_cnt; g.vcnt64 = P.g_vcnt; g.sum = P.g_sum; g.mn = P.g_min; g.mx = P.g_max; g.sq = P.g_sq;
-    g.mstride = 1;
-    g.coff = 0;
-    g.ocnt64 = P.g_ocnt;
-    const uint32_t ncp = ORD ? max(P.ncopies, 1u) : 1u;  // additive cell copies (grids with a terms dimension)
-
-    // LDS window view.  Every pointer is derived from `smem` alone -- never merged with a global pointer -- so the
-    // compiler keeps them in the LDS address space (ds_* instructions).  A generic pointer would compile to flat_*
-    // accesses, and each flat load waits for vmcnt(0): the prefetched loads of the next iteration.
-    Acc s;
-    {
-        size_t off = 0;
-        auto carve = [&](size_t bytes) { unsigned char* p = smem + off; off += (bytes + 15) & ~(size_t)15; return p; };
-        s.cnt64 = nullptr; s.vcnt64 = nullptr; s.ocnt64 = nullptr;
-        s.cnt32 = (uint32_t*)carve(sizeof(uint32_t) * C * ncp);
-        s.vcnt32 = (uint32_t*)carve(P.vcnt_mode ? sizeof(uint32_t) * C * ncp : 0);
-        s.sum = (double*)carve(MET > 0 ? sizeof(double) * C * ncp : 0);
-        s.mn = (unsigned long long*)carve(MET >= 2 ? 16 * C : 0);
-        s.mx = s.mn + (kMS == 2 ? 1 : C);
-        s.mstride = kMS;
-        s.sq = (double*)carve(MET >= 3 ? sizeof(double) * C * ncp : 0);
-        s.coff = ((threadIdx.x & 63) % ncp) * C;
-        s.ocnt32 = (uint32_t*)carve(P.ocnt_mode == OCNT_TERMS ? sizeof(uint32_t) * T
-                                    : P.ocnt_mode == OCNT_HIST ? sizeof(uint32_t) * W : 0);
-    }
-    if (P.lds_mode) {
-        for (uint32_t c = threadIdx.x; c < C * ncp; c += WGS) {
-            s.cnt32[c] = 0;
-            if (P.vcnt_mode) s.vcnt32[c] = 0;
-            if (MET > 0) s.sum[c] = 0.0;
-            if (MET >= 3) s.sq[c] = 0.0;
-        }
-        for (uint32_t c = threadIdx.x; c < C; c += WGS)
-            if (MET >= 2) { s.mn[kMS * c] = kMinInit; s.mx[kMS * c] = kMaxInit; }
-        if (P.ocnt_mode == OCNT_TERMS || P.ocnt_mode == OCNT_HIST)
-            for (uint32_t c = threadIdx.x; c < (P.ocnt_mode == OCNT_TERMS ? T : W); c += WGS) s.ocnt32[c] = 0;
-        __syncthreads();
-    }
-
-    const uint32_t b_begin = blockIdx.x * P.blocks_per_wg;
-    uint32_t b_end = b_begin + P.blocks_per_wg;
-    if (b_end > P.n_blocks) b_end = P.n_blocks;
-    if (b_begin >= b_end) return;
-
-    // window state (only meaningful with HIST && lds_mode)
-    uint32_t win0 = 0;
-    bool win_set = !(HIST && P.windowed);   // un-windowed: slot 0 of LDS == grid slot 0
-    bool dirty = false;
-    int64_t base = HIST ? P.key0 * P.interval + P.offset : 0;  // value of the first LDS slot
-
-    Runs<runs_for<MET>()> run;
-    runs_reset(run);
-    // software pipeline over two buffers: each is reloaded (iteration i + 2) right after it is processed, so one
-    // buffer's loads are in flight while the other is processed.  Loads are unconditional (past the end: the last
-    // block's docs again, never processed) and no loaded register is copied: a conditional load or a register
-    // copy of a load's result makes the compiler wait vmcnt(0), which drains the other buffer's loads as well.
-    //
-    // Multi-pass groups (roughly time-ordered data whose blocks span more keys than the window): the blocks are taken
-    // in groups of kGroup; a group holding a block that spans more than W keys is replayed once per W keys of the
-    // group's key range, each pass accumulating only the docs whose key falls in its window (replays re-read the
-    // group from L2 / MALL).  One window flush per pass of a group instead of one per pass of every block: with
-    // +-1 h jitter the flushes (T x W cells of global atomics) cost 4x the column read when taken per block.  The
-    // replay is part of the schedule the prefetches follow -- the pass count is known at the group's first
-    // iteration, before any replayed iteration is prefetched -- so it costs no extra load buffers.  Groups whose
-    // blocks each fit the window are taken block by block, the window sliding as before.
-    const uint32_t tid4 = threadIdx.x * kVec;
-    // shapes that read few bytes per doc (one ordinal or one key column) keep 4 buffers in flight, the rest 2 (their
-    // buffers are 5x larger; 4 would cost occupancy).  kItersPerBlockW (4) is a multiple of either.
-    constexpr int kBuf = (MET == 0 && !(ORD && HIST)) ? ESGPU_NBUF_NARROW : 2;
-    static_assert(kItersPerBlockW % kBuf == 0, "buffers per block");
-    Doc4 q[kBuf];
-#pragma unroll
-    for (int k = 0; k < kBuf; ++k) load_docs<ORD, HIST, MET, VK>(P, b_begin * kBlockDocs + k * kIterDocsW + tid4, q[k]);
-
-    bool use_lds = P.lds_mode != 0;
-    uint32_t cb = b_begin;                               // block being processed
-    uint32_t gb = b_begin, ge = min(b_begin + kGroup, b_end);  // its group
-    uint32_t pass = 0, npass = 1;                        // npass > 1: a multi-pass group
-    auto slide_to = [&](uint32_t k0) {
-        if (dirty) {
-            if (!ORD) runs_flush<MET, kMS>(P, s, run);
-            flush_window<MET, kMS, WGS>(P, s, T, W, win0, ncp);
-        }
-        dirty = false;
-        win0 = k0;
-        win_set = true;
-        base = (P.key0 + (int64_t)win0) * P.interval + P.offset;
-    };
-    auto step = [&](uint32_t it, Doc4& q) {
-        if (it == 0) {
-            // ---- per-group / per-block decisions (wave-uniform: every lane reads the same zone-map words) ----
-            // readfirstlane: the zone-map words become scalar loads (lgkmcnt), not vector loads whose vmcnt wait
-            // would drain the prefetched buffers
-            const uint32_t b = __builtin_amdgcn_readfirstlane(cb);
-            if (cb == gb && pass == 0) {
-                use_lds = P.lds_mode != 0;
-                npass = 1;
-                if (use_lds && HIST && P.windowed) {
-                    int64_t gmn = INT64_MAX, gmx = INT64_MIN, maxspan = 0;
-                    for (uint32_t x = b; x < ge; ++x) {
-                        const int64_t zmn = P.zmin[x], zmx = P.zmax[x];
-                        if (zmn > zmx) continue;  // no timestamp in the block
-                        const int64_t kmn = key_index<KT>(P, zmn), kmx = key_index<KT>(P, zmx);
-                        gmn = kmn < gmn ? kmn : gmn;
-                        gmx = kmx > gmx ? kmx : gmx;
-                        maxspan = kmx - kmn + 1 > maxspan ? kmx - kmn + 1 : maxspan;
-                    }
-                    if (maxspan > (int64_t)W) {
-                        const int64_t span = gmx - gmn + 1;
-                        if (span > (int64_t)W * kMaxPasses) {
-                            use_lds = false;  // the group spans too many keys: global atomics for it
-                        } else {
-                            npass = (uint32_t)((span + W - 1) / W);
-                            if (!win_set || (uint32_t)gmn != win0) slide_to((uint32_t)gmn);
-                        }
-                    }
-                }
-            } else if (HIST && npass > 1 && cb == gb) {  // next pass over a multi-pass group: the window moves up W keys
-                slide_to(win0 + W);
-            }
-            if (HIST && use_lds && P.windowed && npass == 1) {  // block by block: slide the window when it must
-                const int64_t zmn = P.zmin[b], zmx = P.zmax[b];
-                if (zmn <= zmx) {
-                    const int64_t kmn = key_index<KT>(P, zmn), kmx = key_index<KT>(P, zmx);
-                    if (!win_set || kmn < (int64_t)win0 || kmx >= (int64_t)win0 + (int64_t)W) slide_to((uint32_t)kmn);
-                }
-            }
-        }
-        if (use_lds) {
-            process4<ORD, HIST, MET, true, KT, kMS>(P, s, q, T, base, win0, run, npass > 1 ? W : 0u, pass == 0);
-            dirty = true;
-        } else {
-            process4<ORD, HIST, MET, false, KT, kMS>(P, g, q, T, base, win0, run);
-        }
-        // prefetch kBuf iterations ahead along the schedule (next block of the group, the group's next pass, or the
-        // next group)
-        uint32_t nit = it + kBuf, nb = cb;
-        if (nit >= (uint32_t)kItersPerBlockW) {
-            nit -= kItersPerBlockW;
-            nb = cb + 1;
-            if (nb == ge && pass + 1 < npass) nb = gb;
-            nb = min(nb, b_end - 1);
-        }
-        load_docs<ORD, HIST, MET, VK>(P, nb * kBlockDocs + nit * kIterDocsW + tid4, q);
-    };
-    while (cb < b_end) {
-        for (uint32_t it = 0; it < (uint32_t)kItersPerBlockW; it += kBuf) {
-#pragma unroll
-            for (int k = 0; k < kBuf; ++k) step(it + k, q[k]);
-        }
-        if (++cb == ge) {
-            if (++pass < npass) {
-                cb = gb;
-            } else {
-                pass = 0;
-                npass = 1;
-                gb = ge;
-                ge = min(gb + kGroup, b_end);
-            }
-        }
-    }
-    if (P.lds_mode && (dirty || !(HIST && P.windowed))) {
-        if (!ORD) runs_flush<MET, kMS>(P, s, run);
-        flush_window<MET, kMS, WGS>(P, s, T, W, win0, ncp);
-    }
-}
-
-// calls f(std::integral_constant<int, VK>) for the value kinds the plan uses; bits that cannot matter (no histogram
-// dimension, no metric) are never instantiated
-template <int HK, int MET, class F>
-static auto with_vk(bool hv_f64, bool mv_f64, F f) {
-    const bool hf = HK != 0 && hv_f64, mf = MET > 0 && mv_f64;
-    if constexpr (HK != 0 && MET > 0) {
-        if (hf && mf) return f(std::integral_constant<int, 3>{});
-        if (hf) return f(std::integral_constant<int, 1>{});
-        if (mf) return f(std::integral_constant<int, 2>{});
-        return f(std::integral_constant<int, 0>{});
-    } else if constexpr (HK != 0) {
-        if (hf) return f(std::integral_constant<int, 1>{});
-        return f(std::integral_constant<int, 0>{});
-    } else if constexpr (MET > 0) {
-        if (mf) return f(std::integral_constant<int, 2>{});
-        return f(std::integral_constant<int, 0>{});
-    } else {
-        return f(std::integral_constant<int, 0>{});
-    }
-}
-
-// wide = 1024-thread workgroups (instantiated for histogram grids only)
-template <bool ORD, int HK, int MET, class F>
-static auto with_wg(bool wide, F f) {
-    if constexpr (HK != 0) {
-        if (wide) return f(std::integral_constant<int, 1024>{});
-    }
-    return f(std::integral_constant<int, kWG>{});
-}
-
-template <bool ORD, int HK, int MET>
-static void launch_t(const CollectParams& p, bool wide, uint32_t grid, size_t lds, hipStream_t st) {
-    with_vk<HK, MET>(p.hv_f64 != 0, p.mv_f64 != 0, [&](auto vk) {
-        return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
-            hipLaunchKernelGGL((collect_kernel<ORD, HK, MET, decltype(vk)::value, decltype(wg)::value>), dim3(grid),
-                               dim3(decltype(wg)::value), lds, st, p);
-            return 0;
-        });
-    });
-}
-
-template <bool ORD, int HK>
-static void launch_m(const CollectParams& p, int met, bool wide, uint32_t grid, size_t lds, hipStream_t st) {
-    switch (met) {
-        case 0: launch_t<ORD, HK, 0>(p, wide, grid, lds, st); break;
-        case 1: launch_t<ORD, HK, 1>(p, wide, grid, lds, st); break;
-        case 2: launch_t<ORD, HK, 2>(p, wide, grid, lds, st); break;
-        default: launch_t<ORD, HK, 3>(p, wide, grid, lds, st); break;
-    }
-}
-
+// the collect kernels are instantiated in esgpu_collect_inst.hip, compiled once per (ORD, HK) so the variants build
+// in parallel
 void launch_collect(const CollectParams& p, bool ord, bool hist, int met, bool wide, uint32_t grid, size_t lds, hipStream_t st) {
     const int hk = hist ? (p.kstart ? 2 : 1) : 0;
     if (ord) {
-        if (hk == 2) launch_m<true, 2>(p, met, wide, grid, lds, st);
-        else if (hk == 1) launch_m<true, 1>(p, met, wide, grid, lds, st);
-        else launch_m<true, 0>(p, met, false, grid, lds, st);
+        if (hk == 2) launch_collect_inst<true, 2>(p, met, wide, grid, lds, st);
+        else if (hk == 1) launch_collect_inst<true, 1>(p, met, wide, grid, lds, st);
+        else launch_collect_inst<true, 0>(p, met, false, grid, lds, st);
     } else {
-        if (hk == 2) launch_m<false, 2>(p, met, wide, grid, lds, st);
-        else if (hk == 1) launch_m<false, 1>(p, met, wide, grid, lds, st);
-        else launch_m<false, 0>(p, met, false, grid, lds, st);
+        if (hk == 2) launch_collect_inst<false, 2>(p, met, wide, grid, lds, st);
+        else if (hk == 1) launch_collect_inst<false, 1>(p, met, wide, grid, lds, st);
+        else launch_collect_inst<false, 0>(p, met, false, grid, lds, st);
     }
 }
 
-template <bool ORD, int HK, int MET>
-static int occ_t(size_t lds, int vkbits, bool wide) {
-    return with_vk<HK, MET>((vkbits & 1) != 0, (vkbits & 2) != 0, [&](auto vk) {
-        return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
-            int n = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                    &n, collect_kernel<ORD, HK, MET, decltype(vk)::value, decltype(wg)::value>, decltype(wg)::value, lds) !=
-                hipSuccess)
-                n = 1;
-            return n;
-        });
-    });
-}
-template <bool ORD, int HK>
-static int occ_m(int met, size_t lds, int vk, bool wide) {
-    switch (met) {
-        case 0: return occ_t<ORD, HK, 0>(lds, vk, wide);
-        case 1: return occ_t<ORD, HK, 1>(lds, vk, wide);
-        case 2: return occ_t<ORD, HK, 2>(lds, vk, wide);
-        default: return occ_t<ORD, HK, 3>(lds, vk, wide);
-    }
-}
 int collect_occupancy(bool ord, int hk, int met, size_t lds, int vk, bool wide) {
     if (ord)
-        return hk == 2 ? occ_m<true, 2>(met, lds, vk, wide) : hk == 1 ? occ_m<true, 1>(met, lds, vk, wide) : occ_m<true, 0>(met, lds, vk, false);
-    return hk == 2 ? occ_m<false, 2>(met, lds, vk, wide) : hk == 1 ? occ_m<false, 1>(met, lds, vk, wide) : occ_m<false, 0>(met, lds, vk, false);
+        return hk == 2 ? collect_occ_inst<true, 2>(met, lds, vk, wide) : hk == 1 ? collect_occ_inst<true, 1>(met, lds, vk, wide)
+                                                                                : collect_occ_inst<true, 0>(met, lds, vk, false);
+    return hk == 2 ? collect_occ_inst<false, 2>(met, lds, vk, wide) : hk == 1 ? collect_occ_inst<false, 1>(met, lds, vk, wide)
+                                                                             : collect_occ_inst<false, 0>(met, lds, vk, false);
 }
+
 
 size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode, uint32_t ncopies) {
     const size_t C = (size_t)T * W;

@@ -62,6 +62,7 @@ struct CollectParams {
     uint32_t nsteps;
     const int64_t* zmin;
     const int64_t* zmax;
+    const int64_t* zkey;             // windowed collects: per-block key range [kmn, kmx] (launch_zone_keys)
     uint32_t mg_m, mg_s1, mg_s2;
     int32_t fast32;
     // metric
@@ -128,6 +129,8 @@ void launch_zone_map(const int64_t* v, const uint64_t* present, uint32_t n, int6
 void launch_synth(const SynthParams& p, hipStream_t s);
 // wide: 1024-thread workgroups (histogram grids whose LDS window exceeds the two-per-CU budget), else 512
 void launch_collect(const CollectParams& p, bool ord, bool hist, int met, bool wide, uint32_t grid, size_t lds, hipStream_t s);
+// per-block key ranges of the zone maps under the request's rounding (out: 2 x n_blocks)
+void launch_zone_keys(const CollectParams& p, int64_t* out, hipStream_t s);
 size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode, uint32_t ncopies = 1);
 // resident workgroups per CU (hk: 0 none, 1 affine, 2 table; vk: bit 0 double histogram column, bit 1 double metric)
 int collect_occupancy(bool ord, int hk, int met, size_t lds, int vk, bool wide = false);

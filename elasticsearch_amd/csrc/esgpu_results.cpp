@@ -518,7 +518,28 @@ void reduce_histogram(const Ref* refs, size_t nrefs, Block& out, Scratch& sc, st
             for (uint64_t k = b0 + 1; k < b1 && sorted; ++k) sorted = h.key[k - 1] < h.key[k];
         }
         all.reserve(total);
-        if (sorted) {
+        if (sorted && nrefs <= 16) {
+            // few shards: the next key is the minimum of the heads; every head at that key contributes, in shard
+            // order -- one scan of the heads per output key, the buckets of a key landing together
+            uint64_t pos[16], end[16];
+            for (size_t x = 0; x < nrefs; ++x) {
+                pos[x] = refs[x].b->boff[refs[x].i];
+                end[x] = refs[x].b->boff[refs[x].i + 1];
+            }
+            for (;;) {
+                int64_t key = INT64_MAX;
+                bool any = false;
+                for (size_t x = 0; x < nrefs; ++x)
+                    if (pos[x] < end[x]) {
+                        const int64_t k = refs[x].b->key[pos[x]];
+                        if (!any || k < key) key = k;
+                        any = true;
+                    }
+                if (!any) break;
+                for (size_t x = 0; x < nrefs; ++x)
+                    if (pos[x] < end[x] && refs[x].b->key[pos[x]] == key) all.push_back({refs[x].b, pos[x]++});
+            }
+        } else if (sorted) {
             struct Head { int64_t key; uint32_t x; uint64_t k, end; };
             std::vector<Head> heap;
             heap.reserve(nrefs);

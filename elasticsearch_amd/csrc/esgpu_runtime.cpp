@@ -872,6 +872,7 @@ struct esgpu_plan {
     Scratch s_wgc, s_pbeg, s_pbuf, s_tiles, s_cand, s_keys, s_hist;  // partitioned counting + GPU top-k
     Scratch s_fbits, s_vbits;  // doc bitset of multi-valued filters, per-value bitset of a multi-valued HLL field
     Scratch s_cells;           // cell list of a cardinality gather
+    Scratch s_zkey;            // per-block key ranges of a windowed collect
     PinnedBuf h_keys;
     hipEvent_t ev_mid = nullptr;
     PinnedBuf h_tcnt, h_rows, h_dst[6];
@@ -1154,38 +1155,37 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
 static void alloc_grid(esgpu_plan* p, Pipeline& pl) {
     esgpu_ctx* c = p->ctx;
     const size_t cells = (size_t)pl.T * pl.H;
-    pl.g_ocnt.release();  // arrays the (new) shape does not use
-    pl.g_vcnt.release();
-    pl.g_sum.release();
-    pl.g_min.release();
-    pl.g_max.release();
-    pl.g_sq.release();
-    pl.g_cnt.alloc(c, cells * 8);
+    // arrays the shape uses keep their allocation when it is large enough (a reset plan whose next request's first
+    // segment spans a slightly different key range: no hipFree, which would synchronise the whole device and stall
+    // the other plan's collect), grown with 25 % headroom otherwise; arrays it does not use are released
+    auto need = [&](DevBuf& b, bool used, size_t n) {
+        if (!used) { b.release(); return; }
+        if (!b.p || b.bytes < n) b.alloc(c, n + n / 4);
+    };
+    need(pl.g_cnt, true, cells * 8);
     HIPX(hipMemsetAsync(pl.g_cnt.p, 0, cells * 8, p->stream));
-    if (pl.ocnt_mode != OCNT_NONE) {
-        const size_t n = pl.ocnt_mode == OCNT_HIST ? pl.H : pl.T;
-        pl.g_ocnt.alloc(c, n * 8);
-        HIPX(hipMemsetAsync(pl.g_ocnt.p, 0, n * 8, p->stream));
-    }
-    if (pl.met > 0) {
-        if (pl.vcnt_mode) { pl.g_vcnt.alloc(c, cells * 8); HIPX(hipMemsetAsync(pl.g_vcnt.p, 0, cells * 8, p->stream)); }
-        pl.g_sum.alloc(c, cells * 8);
-        HIPX(hipMemsetAsync(pl.g_sum.p, 0, cells * 8, p->stream));
-    }
+    const size_t no = pl.ocnt_mode == OCNT_HIST ? pl.H : pl.T;
+    need(pl.g_ocnt, pl.ocnt_mode != OCNT_NONE, no * 8);
+    if (pl.ocnt_mode != OCNT_NONE) HIPX(hipMemsetAsync(pl.g_ocnt.p, 0, pl.g_ocnt.bytes, p->stream));
+    need(pl.g_vcnt, pl.met > 0 && pl.vcnt_mode, cells * 8);
+    if (pl.g_vcnt.p) HIPX(hipMemsetAsync(pl.g_vcnt.p, 0, cells * 8, p->stream));
+    need(pl.g_sum, pl.met > 0, cells * 8);
+    if (pl.g_sum.p) HIPX(hipMemsetAsync(pl.g_sum.p, 0, cells * 8, p->stream));
+    need(pl.g_min, pl.met >= 2, cells * 8);
+    need(pl.g_max, pl.met >= 2, cells * 8);
     if (pl.met >= 2) {
-        pl.g_min.alloc(c, cells * 8);
-        pl.g_max.alloc(c, cells * 8);
         launch_fill_u64(pl.g_min.as<unsigned long long>(), cells, kMinInit, p->stream);
         launch_fill_u64(pl.g_max.as<unsigned long long>(), cells, kMaxInit, p->stream);
     }
-    if (pl.met >= 3) { pl.g_sq.alloc(c, cells * 8); HIPX(hipMemsetAsync(pl.g_sq.p, 0, cells * 8, p->stream)); }
+    need(pl.g_sq, pl.met >= 3, cells * 8);
+    if (pl.g_sq.p) HIPX(hipMemsetAsync(pl.g_sq.p, 0, cells * 8, p->stream));
     for (CardState& cs : pl.cards) {
         require((double)cells * (cs.m + 4.0 * cs.cap) <= 4.0 * (1ull << 30), ESGPU_ERR_UNSUPPORTED,
                 "cardinality sketches for every bucket exceed the 4 GiB per-request budget");
-        cs.regs.alloc(c, cells * cs.m);
-        cs.sets.alloc(c, cells * cs.cap * 4);
-        cs.cnt.alloc(c, cells * 4);
-        cs.nonzero.alloc(c, cells * 4);
+        need(cs.regs, true, cells * cs.m);
+        need(cs.sets, true, cells * cs.cap * 4);
+        need(cs.cnt, true, cells * 4);
+        need(cs.nonzero, true, cells * 4);
         HIPX(hipMemsetAsync(cs.regs.p, 0, cs.regs.bytes, p->stream));
         HIPX(hipMemsetAsync(cs.sets.p, 0, cs.sets.bytes, p->stream));
         HIPX(hipMemsetAsync(cs.cnt.p, 0, cs.cnt.bytes, p->stream));
@@ -1775,6 +1775,11 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     const uint32_t min_bpw = L_ORD ? std::min<uint32_t>(ESGPU_MIN_BPW, (P.n_blocks + slots - 1) / slots) : 1u;
     P.blocks_per_wg = std::max(std::max(1u, bpw), min_bpw);
     const uint32_t grid = (P.n_blocks + P.blocks_per_wg - 1) / P.blocks_per_wg;
+    if (P.lds_mode && P.windowed) {
+        P.zkey = (const int64_t*)p->s_zkey.ensure(p->ctx, (size_t)std::max(P.n_blocks, 1u) * 16);
+        launch_zone_keys(P, const_cast<int64_t*>(P.zkey), p->stream);
+        HIPX(hipGetLastError());
+    }
     HIPX(hipEventRecord(pl.e0, p->stream));
     launch_collect(P, L_ORD, L_HIST, L_met, wide, grid, lds, p->stream);
     HIPX(hipGetLastError());

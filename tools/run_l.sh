@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU session L: full GPU suite + bench lines after the build/reduce host work (one-off; every step time-limited)
 set -u
-O=gpurun_out/r2l
+O=gpurun_out/${RUN_TAG:-r2l}
 mkdir -p $O
 step() { local name=$1 secs=$2; shift 2; echo "== $name"; timeout -k 10 $secs "$@" > $O/$name.log 2>&1; local rc=$?; echo "== $name rc=$rc"; tail -2 $O/$name.log; [ $rc -eq 0 ] || exit $rc; }
 step tests 1000 python3 -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread
