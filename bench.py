@@ -295,8 +295,9 @@ def main():
     elapsed = timed(len(plans), len(plans) == 1)
     # one unit at a time: the sequential rate, reported alongside, and the collect kernels' HIP-event time (measured
     # here, where no two collects overlap on the GPU)
-    for k in host_ms:
-        host_ms[k] = 0.0
+    if len(plans) > 1:  # host times of the sequential phase (with one plan: of the only timed phase)
+        for k in host_ms:
+            host_ms[k] = 0.0
     elapsed_seq = timed(1, True) if len(plans) > 1 else elapsed
     host_ms = {k: round(v / args.steps, 4) for k, v in host_ms.items()}  # per request, sequential phase
     exchange = None

@@ -100,9 +100,10 @@ void launch_zone_keys(const CollectParams& p, int64_t* out, hipStream_t st) {
 // the collect kernels are instantiated in esgpu_collect_inst.hip, compiled once per (ORD, HK) so the variants build
 // in parallel
 void launch_collect(const CollectParams& p, bool ord, bool hist, int met, bool wide, uint32_t grid, size_t lds, hipStream_t st) {
-    const int hk = hist ? (p.kstart ? 2 : 1) : 0;
+    const int hk = hist ? (p.hord ? 3 : p.kstart ? 2 : 1) : 0;
     if (ord) {
-        if (hk == 2) launch_collect_inst<true, 2>(p, met, wide, grid, lds, st);
+        if (hk == 3) launch_collect_inst<true, 3>(p, met, false, grid, lds, st);
+        else if (hk == 2) launch_collect_inst<true, 2>(p, met, wide, grid, lds, st);
         else if (hk == 1) launch_collect_inst<true, 1>(p, met, wide, grid, lds, st);
         else launch_collect_inst<true, 0>(p, met, false, grid, lds, st);
     } else {
@@ -113,6 +114,7 @@ void launch_collect(const CollectParams& p, bool ord, bool hist, int met, bool w
 }
 
 int collect_occupancy(bool ord, int hk, int met, size_t lds, int vk, bool wide) {
+    if (ord && hk == 3) return collect_occ_inst<true, 3>(met, lds, vk, false);
     if (ord)
         return hk == 2 ? collect_occ_inst<true, 2>(met, lds, vk, wide) : hk == 1 ? collect_occ_inst<true, 1>(met, lds, vk, wide)
                                                                                 : collect_occ_inst<true, 0>(met, lds, vk, false);

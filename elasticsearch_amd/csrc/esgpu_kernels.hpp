@@ -63,6 +63,7 @@ struct CollectParams {
     const int64_t* zmin;
     const int64_t* zmax;
     const int64_t* zkey;             // windowed collects: per-block key range [kmn, kmx] (launch_zone_keys)
+    int32_t hord;                    // the key dimension is a second terms aggregation: hv holds u32 ordinals, H of them
     uint32_t mg_m, mg_s1, mg_s2;
     int32_t fast32;
     // metric

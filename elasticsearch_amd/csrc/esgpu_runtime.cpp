@@ -802,6 +802,9 @@ struct Pipeline {
     uint64_t value_count = 1;        // terms: the global ordinal count (T is max(value_count, 1))
     int64_t key0 = 0;
     bool keyed = false;              // the key range has been taken from a segment's values (else H == 1, key0 == 0)
+    bool inner_terms = false;        // terms under terms: the key dimension is the inner terms field's ordinals
+    std::shared_ptr<const TermDict> tdict2;  // inner terms: the dictionary its keys resolve through
+    uint64_t value_count2 = 0;       // inner terms: its global ordinal count (H is max(value_count2, 1))
     int vcnt_mode = 0, ocnt_mode = OCNT_NONE;
     DevBuf g_cnt, g_ocnt, g_vcnt, g_sum, g_min, g_max, g_sq;
     // cardinality state
@@ -896,7 +899,14 @@ static int add_pipeline(esgpu_plan* p, int root, int fspec, int outer, int inner
     for (int b : {outer, inner}) {
         if (b < 0) continue;
         const SpecNode& n = p->specs[b];
-        if (n.s.type == ESGPU_AGG_TERMS) { pl.term_spec = b; pl.ord_field = n.field; }
+        if (n.s.type == ESGPU_AGG_TERMS && b == inner && outer >= 0 && p->specs[outer].s.type == ESGPU_AGG_TERMS) {
+            // terms under terms: the inner field's ordinals are the key dimension (key = ordinal)
+            pl.hist_spec = b;
+            pl.hist_field = n.field;
+            pl.inner_terms = true;
+            pl.interval = 1;
+            pl.offset = 0;
+        } else if (n.s.type == ESGPU_AGG_TERMS) { pl.term_spec = b; pl.ord_field = n.field; }
         else {
             pl.hist_spec = b;
             pl.hist_field = n.field;
@@ -998,11 +1008,13 @@ static Group compile_group(esgpu_plan* p, int r, int fspec) {
         } else {
             cs.bucket = true;
             const bool ot = root.s.type == ESGPU_AGG_TERMS, it = p->specs[ch].s.type == ESGPU_AGG_TERMS;
-            require(ot != it, ESGPU_ERR_UNSUPPORTED, "terms-under-terms and histogram-under-histogram");
+            require(ot || it, ESGPU_ERR_UNSUPPORTED, "histogram-under-histogram runs on the CPU path");
             std::vector<int> inner_leaves;
             for (int gc : p->specs[ch].children) {
                 const int t = p->specs[gc].s.type;
                 require(is_metric(t) || t == ESGPU_AGG_CARDINALITY, ESGPU_ERR_UNSUPPORTED, "bucket aggregations nested three levels deep");
+                require(!(ot && it && t == ESGPU_AGG_CARDINALITY), ESGPU_ERR_UNSUPPORTED,
+                        "cardinality under terms under terms runs on the CPU path");
                 inner_leaves.push_back(gc);
             }
             cs.pipes = add_leaf_pipelines(p, r, fspec, r, ch, inner_leaves, &cs.grand);
@@ -1550,8 +1562,14 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     const bool inner_missing = ORD && HIST && (terms_outer ? (oc && !hc) : (hc && !oc));
     if (((ORD && !oc) || (HIST && !hc)) && !inner_missing) return 0;
     if (oc) require(oc->type == ESGPU_COL_ORD_U32, ESGPU_ERR_UNSUPPORTED, "terms on numeric fields run on the CPU path");
-    if (hc) require(hc->type == ESGPU_COL_I64 || hc->type == ESGPU_COL_F64, ESGPU_ERR_UNSUPPORTED,
-                    "histogram over a keyword field runs on the CPU path");
+    if (hc && pl.inner_terms) {
+        require(hc->type == ESGPU_COL_ORD_U32, ESGPU_ERR_UNSUPPORTED, "terms on numeric fields run on the CPU path");
+        require(!hc->multi && !(oc && oc->multi), ESGPU_ERR_UNSUPPORTED,
+                "terms under terms over multi-valued fields runs on the CPU path");
+    } else if (hc) {
+        require(hc->type == ESGPU_COL_I64 || hc->type == ESGPU_COL_F64, ESGPU_ERR_UNSUPPORTED,
+                "histogram over a keyword field runs on the CPU path");
+    }
     if (mc) require(mc->type == ESGPU_COL_I64 || mc->type == ESGPU_COL_F64, ESGPU_ERR_UNSUPPORTED, "metric over non-numeric field");
     // any multi-valued column (aggregated field or filter field) takes the CSR kernel
     bool multi = (oc && oc->multi) || (hc && hc->multi) || (mc && mc->multi);
@@ -1573,7 +1591,11 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     bool has_keys = false;
     int64_t table_shift = 0;
     const uint32_t H_before = pl.H;
-    if (HIST && hc && hc->vmin <= hc->vmax) {
+    if (HIST && hc && pl.inner_terms) {  // one key per inner ordinal
+        kmin = 0;
+        kmax = (int64_t)std::max<uint64_t>(hc->ord_count(), 1) - 1;
+        has_keys = true;
+    } else if (HIST && hc && hc->vmin <= hc->vmax) {
         if (pl.ktable) {
             table_shift = build_key_table(p, pl, hc->vmin, hc->vmax);
             kmin = 0;
@@ -1586,7 +1608,9 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     }
     const bool sparse_metric = pl.met > 0 && (!mc || mc->present.p || mc->multi);
     // ords may be missing; a doc may have several keys: then the outer counts cannot be summed from the cells
-    const bool inner_sparse = ORD && HIST && (inner_missing || (terms_outer ? (hc->present.p != nullptr || hc->multi) : true));
+    const bool inner_sparse = ORD && HIST && (inner_missing || pl.inner_terms ||
+                                              (terms_outer ? (hc->present.p != nullptr || hc->multi) : true));
+    require(!(pl.inner_terms && multi), ESGPU_ERR_UNSUPPORTED, "terms under terms with multi-valued filter fields runs on the CPU path");
     if (!pl.allocated || pl.fresh) {
         const uint32_t T = oc ? (uint32_t)std::max<uint64_t>(oc->ord_count(), 1) : 1;
         const int64_t key0 = has_keys ? kmin : 0;
@@ -1608,6 +1632,8 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         pl.keyed = has_keys;
         pl.value_count = oc ? oc->ord_count() : (ORD ? 0 : 1);
         pl.tdict = oc ? oc->ord_dict() : nullptr;
+        pl.tdict2 = pl.inner_terms && hc ? hc->ord_dict() : nullptr;
+        pl.value_count2 = pl.inner_terms && hc ? hc->ord_count() : 0;
         if (!same) alloc_grid(p, pl);
         pl.fresh = false;
     } else {
@@ -1616,6 +1642,12 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         if (oc) require(same_dict(oc->ord_dict(), pl.tdict), ESGPU_ERR_INVALID,
                          "segments number the terms of [" + pl.ord_field + "] differently: build an ordinal map "
                          "(esgpu_ordinal_map_build) over the reader's segments first");
+        if (pl.inner_terms && hc) {
+            if (!pl.tdict2) { pl.tdict2 = hc->ord_dict(); pl.value_count2 = hc->ord_count(); }
+            require(same_dict(hc->ord_dict(), pl.tdict2), ESGPU_ERR_INVALID,
+                    "segments number the terms of [" + pl.hist_field + "] differently: build an ordinal map "
+                    "(esgpu_ordinal_map_build) over the reader's segments first");
+        }
         if (HIST && has_keys && !pl.keyed) {
             // the earlier segments had no histogram values: their single placeholder row is empty
             require(kmax - kmin + 1 <= 64 * 1024 * 1024, ESGPU_ERR_UNSUPPORTED, "histogram key range too large for a dense grid");
@@ -1655,6 +1687,12 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     P.hv = hc ? hc->values.as<int64_t>() : nullptr;
     P.hv_present = hc ? hc->present.as<uint64_t>() : nullptr;
     P.hv_f64 = hc && hc->type == ESGPU_COL_F64;
+    if (hc && pl.inner_terms) {  // u32 (global) ordinals of the inner terms field
+        P.hv = (const int64_t*)hc->ords().p;
+        P.hv_present = nullptr;
+        P.hv_f64 = 0;
+        P.hord = L_HIST ? 1 : 0;
+    }
     P.interval = pl.interval;
     P.offset = pl.offset;
     P.key0 = pl.key0;
@@ -1670,7 +1708,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     P.ocnt_mode = L_ocnt;
     P.accept = d_accept;
     if (inner_missing) { P.mv = nullptr; P.mv_present = nullptr; P.mv_f64 = 0; }
-    uint64_t bytes_per_doc = (oc ? 4 : 0) + (hc ? 8 : 0) + (mc && !inner_missing ? 8 : 0);
+    uint64_t bytes_per_doc = (oc ? 4 : 0) + (hc ? (pl.inner_terms ? 4 : 8) : 0) + (mc && !inner_missing ? 8 : 0);
     set_preds(p, pl, s, P.pred, &P.npred, &bytes_per_doc);
     P.g_cnt = inner_missing ? pl.g_ocnt.as<unsigned long long>() : pl.g_cnt.as<unsigned long long>();
     P.g_ocnt = pl.g_ocnt.as<unsigned long long>();
@@ -1693,7 +1731,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     P.lds_mode = 1;
     P.windowed = 0;
     if (lds > kLdsPair) {
-        if (L_HIST && !P.kslot) {  // the key window needs buckets that rise with the value (zone-map ranges)
+        if (L_HIST && !P.kslot && !P.hord) {  // the key window needs buckets that rise with the value (zone-map ranges)
             uint32_t w = LH;
             while (w > 1 && collect_lds_bytes(LT, w, L_met, L_vcnt, L_ocnt) > kLdsPair) w = (w + 1) / 2;
             if (collect_lds_bytes(LT, w, L_met, L_vcnt, L_ocnt) > kLdsPair) w = 1;
@@ -1745,12 +1783,12 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         return collect_partitioned(p, pl, s, oc, d_accept, P.pred, P.npred) ? 1 : 0;
     }
     const uint64_t span = (uint64_t)pl.interval * (uint64_t)W;
-    P.fast32 = !P.kstart && pl.interval < (1ll << 32) && span < (1ull << 32);
+    P.fast32 = !P.kstart && !P.hord && pl.interval < (1ll << 32) && span < (1ull << 32);
     if (P.fast32) {
         const MagicU32 mg = make_magic((uint32_t)pl.interval);
         P.mg_m = mg.m; P.mg_s1 = mg.s1; P.mg_s2 = mg.s2;
     }
-    const int hk = L_HIST ? (P.kstart ? 2 : 1) : 0;
+    const int hk = L_HIST ? (P.hord ? 3 : P.kstart ? 2 : 1) : 0;
     const int vk = (P.hv_f64 ? 1 : 0) | (P.mv_f64 ? 2 : 0);
     const uint64_t occ_key = ((uint64_t)lds << 11) | ((uint64_t)wide << 10) | ((uint64_t)vk << 8) | ((uint64_t)L_met << 4) |
                              ((uint64_t)hk << 1) | (L_ORD ? 1 : 0);
@@ -2508,6 +2546,27 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
             }
             const Pipeline& B0 = p->pipes[kid.pipes[0]];
             if (!B0.allocated) { sub.append_empty(); continue; }
+            if (B0.inner_terms) {  // terms under terms: the inner buckets are the top terms of the winner's row
+                if (!B0.tdict2) { sub.append_empty(); continue; }
+                const SpecNode& tn2 = p->specs[kid.spec];
+                LeafRef ord2;
+                if (tn2.s.order == ESGPU_ORDER_AGG_ASC || tn2.s.order == ESGPU_ORDER_AGG_DESC)
+                    for (size_t gj = 0; gj < tn2.children.size(); ++gj) if (tn2.children[gj] == tn2.order_child) ord2 = kid.grand[gj];
+                const size_t row = (size_t)i * B0.H;
+                int64_t other2 = 0;
+                const std::vector<TermPick> top2 = select_terms(tn2.s, B0.hc.cnt + row, (uint32_t)B0.value_count2, &other2,
+                    [&](uint32_t ord) { return order_value(p, tn2, p->pipes[ord2.pipe], ord2.leaf, row + ord); });
+                begin_instance(sub, other2);
+                for (const TermPick& tp : top2) {
+                    const std::string term2 = B0.tdict2->term(tp.ord);
+                    push_bucket(sub, tp.ord, &term2, tp.count);
+                    if (tp.count == 0) { for (Block& sb : sub.subs) sb.append_empty(); continue; }
+                    for (size_t gj = 0; gj < kid.grand.size(); ++gj)
+                        append_leaf(p, p->pipes[kid.grand[gj].pipe], kid.grand[gj].leaf, row + tp.ord, sub.subs[gj]);
+                }
+                end_instance(sub);
+                continue;
+            }
             begin_instance(sub, 0);
             const unsigned long long* crow = B0.hc.cnt + (size_t)i * B0.H;
             slots.clear();
@@ -2698,6 +2757,7 @@ extern "C" int esgpu_plan_reset(esgpu_plan* p) {
             // the next request takes its grid shape and term dictionary from its own first segment
             pl.fresh = true;
             pl.tdict.reset();
+            pl.tdict2.reset();
             if (!pl.allocated) continue;
             if (pl.kind == 1) {
                 HIPX(hipMemsetAsync(pl.regs.p, 0, pl.regs.bytes, p->stream));

@@ -27,11 +27,15 @@ def _plan_and_collect(engine, aggs, fields, n=100_000):
         seg.close()
 
 
-@pytest.mark.parametrize("case", ["terms_under_terms", "three_bucket_levels"])
+@pytest.mark.parametrize("case", ["terms_under_high_cardinality_terms", "histogram_under_histogram", "three_bucket_levels"])
 def test_unsupported_shapes_raise(engine, case):
-    if case == "terms_under_terms":
+    if case == "terms_under_high_cardinality_terms":  # 1,000 x 10M cells: no dense grid
         aggs = [AB.terms("hosts").field("host").subAggregation(AB.terms("urls").field("url"))]
         fields = ("host", "url")
+    elif case == "histogram_under_histogram":
+        aggs = [AB.dateHistogram("d").field("@timestamp").interval("1d").subAggregation(
+            AB.histogram("b").field("bytes").interval(1024))]
+        fields = ("@timestamp", "bytes")
     else:
         aggs = [AB.terms("hosts").field("host").subAggregation(
             AB.dateHistogram("h").field("@timestamp").interval("1h").subAggregation(

@@ -1,0 +1,105 @@
+"""GPU parity for terms under terms (a5): a terms aggregation whose child is another terms aggregation over a keyword
+field of modest cardinality.  The inner field's ordinals are the key dimension of the cell grid ([T_inner][T_outer]
+cells, key = ordinal), and each outer winner's inner buckets are the inner terms' own top shard_size
+(GlobalOrdinalsStringTermsAggregator under asMultiBucketAggregator, A/AggregatorFactory.java:107-200;
+buildAggregation :146-208 per owning bucket), reduced by InternalTerms.doReduce at both levels."""
+import numpy as np
+import pytest
+
+import oracle as O
+from elasticsearch_amd import AggregationBuilders as AB
+from elasticsearch_amd import Order, QueryBuilders as QB
+from elasticsearch_amd import _native as N
+from elasticsearch_amd import reduce
+from helpers import assert_same, synthetic_columns
+
+pytestmark = pytest.mark.gpu
+
+STATUS_TERMS = ["200", "301", "302", "304", "401", "403", "404", "500", "502", "503"]  # sorted: ordinal = rank
+REGIONS = ["ap-south", "eu-central", "eu-west", "us-east", "us-west"]
+
+
+def _columns(n, shard, missing_region=0.1):
+    """host / response_time_ms / bytes / @timestamp from the synthetic generator, plus two keyword fields: the status
+    code as a keyword (its ordinal is the code's rank) and a region with `missing_region` of the docs missing."""
+    cols = synthetic_columns(("host", "status", "response_time_ms", "bytes", "@timestamp"), n, shard=shard)
+    status = cols.pop("status")["values"]
+    codes = np.array([int(t) for t in STATUS_TERMS])
+    cols["status_kw"] = {"type": N.COL_ORD_U32, "values": np.searchsorted(codes, status).astype(np.uint32),
+                         "terms": STATUS_TERMS}
+    rng = np.random.default_rng(100 + shard)
+    region = rng.integers(0, len(REGIONS), n).astype(np.uint32)
+    region[rng.random(n) < missing_region] = 0xFFFFFFFF
+    cols["region"] = {"type": N.COL_ORD_U32, "values": region, "terms": REGIONS}
+    return cols
+
+
+def _both(engine, aggs, n=400_000, shards=2, filters=None, exact=True):
+    data = [(_columns(n, s), n) for s in range(shards)]
+    want = O.run(data, aggs, filters=filters, number_of_shards=shards)
+    plan = engine.plan(aggs, filters=filters, number_of_shards=shards)
+    results = []
+    for s, (cols, _) in enumerate(data):
+        seg = engine.upload_segment(cols, n)
+        plan.reset()
+        plan.collect(seg)
+        r = plan.build()
+        assert_same(r.to_dict(), want["shards"][s], f"shard{s}", exact)
+        results.append(r)
+        seg.close()
+    red = reduce(results).to_dict()
+    assert_same(red, want["reduced"], "reduced", exact)
+    plan.close()
+    return red
+
+
+def test_terms_under_terms_with_metrics(engine):
+    aggs = [AB.terms("hosts").field("host").size(5).subAggregation(
+        AB.terms("codes").field("status_kw").size(3).subAggregation(AB.avg("rt").field("response_time_ms"))
+        .subAggregation(AB.stats("b").field("bytes")))]
+    red = _both(engine, aggs)
+    assert all(len(h["codes"]["buckets"]) == 3 for h in red["hosts"]["buckets"])
+
+
+def test_inner_terms_with_missing_values_and_orders(engine):
+    """region is missing on 10 % of the docs: the outer doc counts still count them (counted per doc, not summed
+    from the cells); inner orders by term, count asc and min_doc_count 0 (every region listed)."""
+    aggs = [AB.terms("hosts").field("host").size(4).subAggregation(
+                AB.terms("r").field("region").size(5).minDocCount(0).order(Order.term(True))),
+            AB.terms("hosts2").field("host").size(3).order(Order.term(False)).subAggregation(
+                AB.terms("r").field("region").size(2).order(Order.count(True)))]
+    _both(engine, aggs, shards=3)
+
+
+def test_inner_terms_ordered_by_a_metric(engine):
+    aggs = [AB.terms("hosts").field("host").size(4).subAggregation(
+        AB.terms("codes").field("status_kw").size(4).order(Order.aggregation("rt", False))
+        .subAggregation(AB.avg("rt").field("response_time_ms")))]
+    red = _both(engine, aggs)
+    assert red["hosts"]["buckets"][0]["codes"]["doc_count_error_upper_bound"] == -1
+
+
+def test_terms_under_terms_beside_other_children_and_filtered(engine):
+    aggs = [AB.terms("hosts").field("host").size(6).subAggregation(AB.terms("r").field("region").size(2))
+            .subAggregation(AB.dateHistogram("d").field("@timestamp").interval("1d"))
+            .subAggregation(AB.avg("rt").field("response_time_ms"))]
+    _both(engine, aggs, filters=[QB.rangeQuery("bytes").gte(1024)])
+
+
+def test_inner_terms_field_missing_in_a_segment(engine):
+    """The second segment has no region field: its docs count for the hosts only."""
+    n = 200_000
+    a = _columns(n, 0)
+    b = {k: v for k, v in _columns(n, 1).items() if k != "region"}
+    aggs = [AB.terms("hosts").field("host").size(5).subAggregation(AB.terms("r").field("region").size(3))]
+    one = {k: dict(a[k], values=np.concatenate([a[k]["values"], b[k]["values"]])) for k in b}
+    one["region"] = dict(a["region"], values=np.concatenate([a["region"]["values"], np.full(n, 0xFFFFFFFF, np.uint32)]))
+    want = O.run([(one, 2 * n)], aggs)
+    segs = [engine.upload_segment(a, n), engine.upload_segment(b, n)]
+    plan = engine.plan(aggs)
+    for s in segs:
+        plan.collect(s)
+    assert_same(plan.build().to_dict(), want["shards"][0], "shard")
+    plan.close()
+    for s in segs:
+        s.close()
