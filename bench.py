@@ -173,8 +173,9 @@ def main():
                     help="host threads of the CPU baseline, one shard each (0 = every CPU this job is allotted: its "
                          "affinity, capped by OMP_NUM_THREADS)")
     ap.add_argument("--cpu-single-docs", type=int, default=20_000_000, help="docs of the single-thread CPU shard")
-    ap.add_argument("--inflight", type=int, default=2, choices=(1, 2),
-                    help="plans in flight (2: the host build of one shard result overlaps the next collect)")
+    ap.add_argument("--inflight", type=int, default=0, choices=(0, 1, 2, 3, 4),
+                    help="plans in flight (0 = 2); with one unit per shard the shard builds run on len-1 worker threads "
+                         "beside the collects")
     ap.add_argument("--traffic", default=os.path.join(HERE, "profiles", "hbm_traffic.json"),
                     help="PMC-derived HBM bytes per collect launch (profiles/), if measured for this workload")
     args = ap.parse_args()
@@ -202,11 +203,13 @@ def main():
     aggs, filters = build_request(args.workload, shards)
     # this rank's shards: global shards rank * per_gpu ... (rank-major = the reduce's shard order)
     segs = [engine.synthetic_segment(args.docs, fields=fields, shard=rank * per_gpu + i) for i in range(per_gpu)]
-    plans = [engine.plan(aggs, filters=filters, number_of_shards=shards) for _ in range(args.inflight)]
+    plans = [engine.plan(aggs, filters=filters, number_of_shards=shards)]
     # fixed-shape requests (no terms): this GPU's shards are collected into one plan, one build per request; terms
     # requests build one shard result per shard (per-shard top-k) and reduce them with the other ranks'
     merged = plans[0].shard_mergeable() and per_gpu > 1
     units_per_request = 1 if merged or per_gpu == 1 else per_gpu
+    inflight = args.inflight or 2  # measured for 8 shards per GPU: 2 plans 4.67 ms/step, 4 plans 4.89
+    plans += [engine.plan(aggs, filters=filters, number_of_shards=shards) for _ in range(inflight - 1)]
     comm = None
     if world > 1:
         uid = [ea.Communicator.unique_id() if rank == 0 else None]
@@ -227,12 +230,20 @@ def main():
                 kernel_bytes[0] += nbytes
 
     host_ms = {"build": 0.0, "reduce": 0.0}
-    # the coordinating reduce of a request runs on a worker thread (the C call releases the GIL), the way a
-    # coordinating node merges one request's shard results while the data nodes collect the next; requests are
-    # reduced in order, and every one is finished inside the timed region (drain() below)
+    # Shard builds run on worker threads (one SEARCH thread per shard in ES: distinct plans are independent), the
+    # coordinating reduce of a request on its own worker (a coordinating node merges one request while the data nodes
+    # collect the next).  Requests are reduced in order; every one is finished inside the timed region (drain()).
+    from collections import deque
     from concurrent.futures import ThreadPoolExecutor
+    builders = ThreadPoolExecutor(max(1, len(plans) - 1))
     reducer = ThreadPoolExecutor(1)
     pending = []
+
+    def build_unit(p):
+        t = time.perf_counter()
+        r = p.build()
+        host_ms["build"] += (time.perf_counter() - t) * 1e3
+        return r
 
     def reduce_request(parts):
         t = time.perf_counter()
@@ -245,34 +256,35 @@ def main():
         while pending:
             final = pending.pop(0).result()
 
-    def finish(p, unit):
+    def take(pend):  # the oldest unit in flight: its shard result, in shard order
         nonlocal partial
-        t0 = time.perf_counter()
-        partial.append(p.build())
-        host_ms["build"] += (time.perf_counter() - t0) * 1e3
+        p, unit, fut = pend.popleft()
+        partial.append(fut.result() if fut is not None else build_unit(p))
         if unit == units_per_request - 1:
             pending.append(reducer.submit(reduce_request, partial))
             partial = []
             while len(pending) > 1 and pending[0].done():
-                drain_one = pending.pop(0)
-                drain_one.result()
+                pending.pop(0).result()
 
-    # one unit = one collect (+ build) of a shard, or of all this GPU's shards of a fixed-shape request; with two plans
-    # the host build + reduce of one unit overlaps the collect kernel of the next -- how a node serves a stream of
-    # search requests.  Every request still runs reset -> collect -> build -> reduce in full.
+    # one unit = one collect (+ build) of a shard, or of all this GPU's shards of a fixed-shape request; `depth` plans
+    # rotate, so a plan's build overlaps the next units' collect kernels.  Every request still runs reset -> collect
+    # -> build -> reduce in full.
     def run(n_requests, record, depth):
-        pend = []
+        pend = deque()
         k = 0
         for _ in range(n_requests):
             for unit in range(units_per_request):
                 p = plans[k % depth]
                 k += 1
+                while pend and (len(pend) >= depth or any(q is p for q, _, _ in pend)):
+                    take(pend)  # the plan's previous unit is built before its buffers are reset
                 launch(p, unit, record)
-                pend.append((p, unit))
-                if len(pend) == depth:
-                    finish(*pend.pop(0))
+                # one shard per request: the build runs here, between launches (a builder thread measured 9 % slower
+                # there); one unit per shard: on the builder threads, several shards' host builds beside the kernels
+                threaded = depth > 1 and units_per_request > 1
+                pend.append((p, unit, builders.submit(build_unit, p) if threaded else None))
         while pend:
-            finish(*pend.pop(0))
+            take(pend)
         drain()
 
     def timed(depth, record):

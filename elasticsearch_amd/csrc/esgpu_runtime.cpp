@@ -1406,8 +1406,13 @@ static bool collect_partitioned(esgpu_plan* p, Pipeline& pl, const esgpu_segment
     Q.tile_sums = (uint32_t*)p->s_tiles.ensure(c, (size_t)ntiles * 4);
     Q.pbuf = (uint16_t*)p->s_pbuf.ensure(c, (std::max<size_t>(s->max_doc, 1) + 8) * 2);
     Q.counts = pl.g_cnt.as<unsigned long long>();
-    // ~4 counting workgroups per CU; each covers `chunk` partitioned elements (a multiple of 8: 16-byte loads)
-    const uint64_t want = (uint64_t)c->cus * 4;
+    // counting workgroups (one resident per CU at 128 KB of LDS counters); each covers `chunk` partitioned elements
+    // (a multiple of 8: 16-byte loads).  Every partition piece a workgroup counts ends in a flush of its 32768
+    // counters (256 KB of global adds), so the workgroup count is capped at one per 512K elements -- the flushes stay
+    // within a quarter of the 2-byte reads -- between 1 and 4 per CU.  Measured: 4 per CU is best at 1B docs (3.16 vs
+    // 3.47 ms for 1 per CU), 1 per CU at 125M (0.55 vs 0.62 ms).
+    const uint64_t want = std::min<uint64_t>((uint64_t)c->cus * 4,
+                                             std::max<uint64_t>((uint64_t)c->cus, (uint64_t)s->max_doc >> 19));
     Q.chunk = (uint32_t)std::max<uint64_t>(1u << 16, (((uint64_t)s->max_doc + want - 1) / want + 7) & ~7ull);
     HIPX(hipEventRecord(pl.e0, st));
     launch_part_hist(Q, st);
@@ -1829,6 +1834,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
 
 static void ensure_ord_hash(esgpu_ctx* c, const DevColumn* col, hipStream_t st) {
     DevColumn* mcol = const_cast<DevColumn*>(col);
+    std::lock_guard<std::mutex> lk(c->mu);  // plans on different threads may share the segment
     if (mcol->ord_hash.p) return;
     std::vector<uint64_t> h(std::max<uint64_t>(col->value_count, 1));
     for (uint64_t o = 0; o < col->value_count; ++o) {

@@ -56,8 +56,9 @@ int esgpu_abi_version(void);
 
 /* ---------------------------------------------------------------------------------------------------------
  * Device context: one per GPU, owns the HBM budget (REQUEST/FIELDDATA breaker analogue) and the streams.
- * Thread-safe for segment upload; plans created from it are single-threaded (one SEARCH thread per shard
- * request, SURVEY §8(b) "Threading").
+ * Thread-safe for segment upload.  A plan is used by one thread at a time (one SEARCH thread per shard request,
+ * SURVEY §8(b) "Threading"); distinct plans -- each with its own stream -- may run on different threads at once,
+ * over the same segments.
  * ------------------------------------------------------------------------------------------------------- */
 typedef struct esgpu_ctx esgpu_ctx;
 

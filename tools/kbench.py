@@ -11,6 +11,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 
@@ -38,6 +40,39 @@ def variants():
     }
 
 
+def _dict_blob(field):
+    """term bytes + offsets of the synthetic keyword fields (host-%04d / /p/%08x), built as an uploaded dictionary"""
+    n = 1000 if field == "host" else 10_000_000
+    width, prefix = (4, b"host-") if field == "host" else (8, b"/p/")
+    ids = np.arange(n, dtype=np.uint64)
+    if field == "host":
+        digits = (ids[:, None] // (10 ** np.arange(width - 1, -1, -1, dtype=np.uint64))) % 10
+        chars = np.frombuffer(b"0123456789", dtype=np.uint8)[digits.astype(np.int64)]
+    else:
+        digits = (ids[:, None] >> (np.arange(width - 1, -1, -1, dtype=np.uint64) * 4)) & 15
+        chars = np.frombuffer(b"0123456789abcdef", dtype=np.uint8)[digits.astype(np.int64)]
+    L = len(prefix) + width
+    out = np.empty((n, L), dtype=np.uint8)
+    out[:, :len(prefix)] = np.frombuffer(prefix, dtype=np.uint8)
+    out[:, len(prefix):] = chars
+    return out.reshape(-1), np.arange(0, L * (n + 1), L, dtype=np.uint64)
+
+
+def _with_real_dicts(e, seg, n, fields):
+    """the same columns, uploaded through esgpu_segment_upload (keyword fields with their dictionaries)"""
+    cols = {}
+    for f in fields:
+        t = ea._native.SYNTH_TYPES[f]
+        dt = {ea._native.COL_ORD_U32: np.uint32, ea._native.COL_I64: np.int64, ea._native.COL_F64: np.float64,
+              ea._native.COL_U64: np.uint64}[t]
+        c = {"type": t, "values": seg.read_column(f, 0, n, dt)}
+        if f in ("host", "url"):
+            c["terms_blob"] = _dict_blob(f)
+        cols[f] = c
+    seg.close()
+    return e.upload_segment(cols, n)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--docs", type=int, default=1_000_000_000)
@@ -46,6 +81,9 @@ def main():
     ap.add_argument("--ts-jitter", type=int, default=0,
                     help="@timestamp displacement bound in ms (0 = time-sorted docs; 60000 / 3600000 = roughly sorted)")
     ap.add_argument("--shards", type=int, default=1, help="number_of_shards of the request (terms shard_size heuristic)")
+    ap.add_argument("--real-dict", action="store_true",
+                    help="re-upload host/url as ordinary keyword columns with their term bytes (esgpu_segment_upload with a "
+                         "dictionary), so the build resolves winners through a real 10M-term dictionary")
     args = ap.parse_args()
     only = set(filter(None, args.only.split(",")))
     e = ea.Engine(0)
@@ -55,6 +93,8 @@ def main():
         fields.add("url")
     t = time.time()
     seg = e.synthetic_segment(args.docs, fields=tuple(sorted(fields)), ts_jitter_ms=args.ts_jitter)
+    if args.real_dict:
+        seg = _with_real_dicts(e, seg, args.docs, sorted(fields))
     print(json.dumps({"generated_s": time.time() - t, "hbm_gb": e.hbm_used() / 1e9, "ts_jitter_ms": args.ts_jitter,
                       "shards": args.shards}), flush=True)
     for name, (aggs, flt) in vs.items():
