@@ -163,6 +163,8 @@ SIGNATURES = [
     ("esgpu_cardinality_value", ctypes.c_int, [ctypes.POINTER(AggBlock), ctypes.c_uint64, ctypes.POINTER(ctypes.c_int64)]),
     ("esgpu_result_to_json", ctypes.c_int, [ctypes.POINTER(Result), ctypes.c_char_p, ctypes.c_size_t,
                                             ctypes.POINTER(ctypes.c_size_t)]),
+    ("esgpu_result_to_xcontent", ctypes.c_int, [ctypes.POINTER(Result), ctypes.c_char_p, ctypes.c_size_t,
+                                                ctypes.POINTER(ctypes.c_size_t)]),
     ("esgpu_result_serialize", ctypes.c_int, [ctypes.POINTER(Result), _VP, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
     ("esgpu_result_deserialize", ctypes.c_int, [_VP, ctypes.c_size_t, ctypes.POINTER(ctypes.POINTER(Result))]),
     ("esgpu_comm_unique_id", ctypes.c_int, [_VP]),

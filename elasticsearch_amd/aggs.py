@@ -391,8 +391,8 @@ def _rounding_params(b):
     zone = None
     if isinstance(tz, tuple):
         zone = tz
-    else:
-        off -= tz
+    elif tz != 0:  # a fixed zone as a one-entry table: Rounding.from_spec folds it into the offset, and the result
+        zone = ((0,), (tz,))  # keeps it for printing the keys (key_as_string "...+01:00")
     unit = DATE_FIELD_UNITS.get(str(b._interval))
     if unit is not None:
         return unit, 0, off, zone

@@ -908,6 +908,214 @@ std::string to_json(const std::vector<Block>& aggs) {
 }
 
 // ------------------------------------------------------------------------------------------------------------
+// XContent: the REST response body of the aggregations as Elasticsearch renders it (Jackson, compact), field by
+// field after each class's doXContentBody -- InternalTerms/StringTerms (A/bucket/terms/InternalTerms.java:220-229,
+// StringTerms.java:138-148), InternalHistogram (A/bucket/histogram/InternalHistogram.java:152-173,526-541),
+// InternalStats (A/metrics/stats/InternalStats.java:206-221), InternalExtendedStats (:192-213), InternalAvg (:109-115),
+// InternalCardinality (:129-136), InternalSingleBucketAggregation (filter).  Numeric fields use the RAW value
+// formatter (no *_as_string); date_histogram keys print with the date field's default printer
+// (strict_date_optional_time: yyyy-MM-dd'T'HH:mm:ss.SSSZZ) in the request's time zone.
+// ------------------------------------------------------------------------------------------------------------
+namespace {
+// Double.toString: the shortest digit string (at least two digits) that reads back as the same double, laid out as Java does -- plain
+// decimal for 1e-3 <= |v| < 1e7 (at least one fractional digit), else d.dddE<exp>.  JDK 19+ prints exactly this;
+// JDK 8's FloatingDecimal agrees except for rare values where it emits one digit more.
+std::string java_double(double v) {
+    if (v != v) return "NaN";
+    if (std::isinf(v)) return v > 0 ? "Infinity" : "-Infinity";
+    if (v == 0) return std::signbit(v) ? "-0.0" : "0.0";
+    char b[40];
+    int p = 1;
+    for (; p < 17; ++p) {
+        snprintf(b, sizeof b, "%.*e", p - 1, v);
+        if (std::strtod(b, nullptr) == v) break;
+    }
+    // Double.toString shows at least two digits: a one-digit shortest form becomes the closest two-digit decimal
+    // (Double.MIN_VALUE prints 4.9E-324, not 5.0E-324)
+    if (p < 2) p = 2;
+    snprintf(b, sizeof b, "%.*e", p - 1, v);
+    // b = [-]d[.ddd]e[+-]XX
+    std::string digits;
+    const char* q = b;
+    const bool neg = *q == '-';
+    if (neg) ++q;
+    for (; *q && *q != 'e'; ++q) if (*q != '.') digits += *q;
+    const int e10 = std::atoi(q + 1);
+    while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
+    std::string out = neg ? "-" : "";
+    const double a = std::fabs(v);
+    if (a >= 1e-3 && a < 1e7) {
+        if (e10 >= 0) {
+            const size_t ip = (size_t)e10 + 1;
+            std::string d = digits;
+            if (d.size() < ip) d.append(ip - d.size(), '0');
+            out += d.substr(0, ip);
+            out += '.';
+            out += d.size() > ip ? d.substr(ip) : "0";
+        } else {
+            out += "0.";
+            out.append((size_t)(-e10 - 1), '0');
+            out += digits;
+        }
+    } else {
+        out += digits[0];
+        out += '.';
+        out += digits.size() > 1 ? digits.substr(1) : "0";
+        out += 'E';
+        out += std::to_string(e10);
+    }
+    return out;
+}
+
+// strict_date_optional_time printer in the zone of the table (offset offs[i] from UTC instant starts[i]; empty = UTC)
+std::string es_date(int64_t ms, const std::vector<int64_t>& starts, const std::vector<int64_t>& offs) {
+    int64_t off = 0;
+    if (!offs.empty()) {
+        size_t i = (size_t)(std::upper_bound(starts.begin() + 1, starts.end(), ms) - starts.begin());
+        off = offs[i - 1];
+    }
+    const int64_t local = ms + off;
+    const int64_t days = fdiv(local, kMsDay);
+    const int64_t rem = local - days * kMsDay;
+    int64_t y; int m, d;
+    r_civil_from_days(days, &y, &m, &d);
+    char b[64];
+    int n = snprintf(b, sizeof b, "%04lld-%02d-%02dT%02d:%02d:%02d.%03d", (long long)y, m, d, (int)(rem / 3600000),
+                     (int)(rem / 60000 % 60), (int)(rem / 1000 % 60), (int)(rem % 1000));
+    if (off == 0) {
+        snprintf(b + n, sizeof b - n, "Z");
+    } else {
+        const int64_t a = off < 0 ? -off : off;
+        snprintf(b + n, sizeof b - n, "%c%02d:%02d", off < 0 ? '-' : '+', (int)(a / 3600000), (int)(a / 60000 % 60));
+    }
+    return b;
+}
+
+struct X {
+    std::string s;
+    void raw(const char* t) { s += t; }
+    void str(const char* p, size_t n) {  // Jackson: short escapes for \b \t \n \f \r, \uXXXX for other controls
+        s += '"';
+        for (size_t i = 0; i < n; ++i) {
+            const unsigned char c = (unsigned char)p[i];
+            switch (c) {
+                case '"': s += "\\\""; break;
+                case '\\': s += "\\\\"; break;
+                case '\b': s += "\\b"; break;
+                case '\t': s += "\\t"; break;
+                case '\n': s += "\\n"; break;
+                case '\f': s += "\\f"; break;
+                case '\r': s += "\\r"; break;
+                default:
+                    if (c < 0x20) { char b[8]; snprintf(b, sizeof b, "\\u%04X", c); s += b; }
+                    else s += (char)c;
+            }
+        }
+        s += '"';
+    }
+    void str(const std::string& v) { str(v.data(), v.size()); }
+    void key(const std::string& k) { str(k); s += ':'; }
+    void i64(int64_t v) { s += std::to_string(v); }
+    void dbl(double v) { s += java_double(v); }
+    void opt(bool c, double v) { if (c) dbl(v); else raw("null"); }
+};
+
+void x_instance(X& x, const Block& a, uint64_t i);
+
+void x_subs(X& x, const Block& a, uint64_t k) {
+    for (const Block& sb : a.subs) {
+        x.raw(",");
+        x.key(sb.name);
+        x_instance(x, sb, k);
+    }
+}
+
+void x_instance(X& x, const Block& a, uint64_t i) {
+    x.raw("{");
+    switch (a.type) {
+        case ESGPU_AGG_TERMS:
+            x.key("doc_count_error_upper_bound"); x.i64(a.doc_count_error[i]); x.raw(",");
+            x.key("sum_other_doc_count"); x.i64(a.other_doc_count[i]); x.raw(",");
+            x.key("buckets"); x.raw("[");
+            for (uint64_t k = a.boff[i]; k < a.boff[i + 1]; ++k) {
+                if (k != a.boff[i]) x.raw(",");
+                x.raw("{"); x.key("key"); x.str(a.term_pool.data() + a.term_off[k], a.term_off[k + 1] - a.term_off[k]); x.raw(",");
+                x.key("doc_count"); x.i64(a.bcount[k]);
+                if (a.show_err) { x.raw(","); x.key("doc_count_error_upper_bound"); x.i64(a.berr[k]); }
+                x_subs(x, a, k);
+                x.raw("}");
+            }
+            x.raw("]");
+            break;
+        case ESGPU_AGG_HISTOGRAM:
+        case ESGPU_AGG_DATE_HISTOGRAM: {
+            const bool date = a.type == ESGPU_AGG_DATE_HISTOGRAM;
+            x.key("buckets"); x.raw(a.keyed ? "{" : "[");
+            for (uint64_t k = a.boff[i]; k < a.boff[i + 1]; ++k) {
+                if (k != a.boff[i]) x.raw(",");
+                const std::string ks = date ? es_date(a.key[k], a.tz_starts, a.tz_offs) : std::string();
+                if (a.keyed) x.key(date ? ks : std::to_string(a.key[k]));
+                x.raw("{");
+                if (date) { x.key("key_as_string"); x.str(ks); x.raw(","); }
+                x.key("key"); x.i64(a.key[k]); x.raw(",");
+                x.key("doc_count"); x.i64(a.bcount[k]);
+                x_subs(x, a, k);
+                x.raw("}");
+            }
+            x.raw(a.keyed ? "}" : "]");
+            break;
+        }
+        case ESGPU_AGG_FILTER:
+            x.key("doc_count"); x.i64(a.count[i]);
+            x_subs(x, a, i);
+            break;
+        case ESGPU_AGG_AVG:
+            x.key("value"); x.opt(a.count[i] != 0, a.sum[i] / (double)a.count[i]);
+            break;
+        case ESGPU_AGG_STATS:
+        case ESGPU_AGG_EXTENDED_STATS: {
+            const int64_t cnt = a.count[i];
+            const double sum = a.sum[i], sq = a.sumsq[i];
+            const bool c = cnt != 0;
+            const double avg = sum / (double)cnt;
+            x.key("count"); x.i64(cnt); x.raw(",");
+            x.key("min"); x.opt(c, a.min[i]); x.raw(",");
+            x.key("max"); x.opt(c, a.max[i]); x.raw(",");
+            x.key("avg"); x.opt(c, avg); x.raw(",");
+            x.key("sum"); x.opt(c, sum);
+            if (a.type == ESGPU_AGG_EXTENDED_STATS) {
+                const double var = (sq - ((sum * sum) / (double)cnt)) / (double)cnt;
+                const double sd = std::sqrt(var);
+                x.raw(","); x.key("sum_of_squares"); x.opt(c, sq);
+                x.raw(","); x.key("variance"); x.opt(c, var);
+                x.raw(","); x.key("std_deviation"); x.opt(c, sd);
+                x.raw(","); x.key("std_deviation_bounds"); x.raw("{");
+                x.key("upper"); x.opt(c, avg + (sd * a.sigma)); x.raw(",");
+                x.key("lower"); x.opt(c, avg - (sd * a.sigma)); x.raw("}");
+            }
+            break;
+        }
+        case ESGPU_AGG_CARDINALITY:
+            x.key("value"); x.i64(hll_cardinality(a.precision, a.hll_present[i], a.hll_mode[i], a.regs[i].data(), a.lc[i].size()));
+            break;
+    }
+    x.raw("}");
+}
+}  // namespace
+
+std::string to_xcontent(const std::vector<Block>& aggs) {
+    X x;
+    x.raw("{");
+    for (size_t i = 0; i < aggs.size(); ++i) {
+        if (i) x.raw(",");
+        x.key(aggs[i].name);
+        x_instance(x, aggs[i], 0);
+    }
+    x.raw("}");
+    return x.s;
+}
+
+// ------------------------------------------------------------------------------------------------------------
 // stream format (AggregationStreams analogue): little-endian, versioned, one record per block
 // ------------------------------------------------------------------------------------------------------------
 namespace {

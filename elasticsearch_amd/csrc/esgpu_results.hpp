@@ -129,6 +129,8 @@ std::vector<Block> reduce_across(Collective& c, const std::vector<const std::vec
 bool same_shape(const Block& a, const Block& b);
 
 std::string to_json(const std::vector<Block>& aggs);
+// the aggregations object of an Elasticsearch search response, byte for byte as its XContent renders it
+std::string to_xcontent(const std::vector<Block>& aggs);
 void serialize(const std::vector<Block>& aggs, std::string& out);
 bool deserialize(const uint8_t* p, size_t n, std::vector<Block>& out);
 

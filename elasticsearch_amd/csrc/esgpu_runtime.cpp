@@ -2846,6 +2846,19 @@ extern "C" int esgpu_cardinality_value(const esgpu_agg_block* b, uint64_t instan
     });
 }
 
+extern "C" int esgpu_result_to_xcontent(const esgpu_result* r, char* buf, size_t cap, size_t* needed) {
+    return guarded([&] {
+        require(r != nullptr, ESGPU_ERR_INVALID, "null result");
+        const std::string s = to_xcontent(holder_of(r)->aggs);
+        if (needed) *needed = s.size() + 1;
+        if (buf && cap) {
+            const size_t c = std::min(cap - 1, s.size());
+            std::memcpy(buf, s.data(), c);
+            buf[c] = 0;
+        }
+    });
+}
+
 extern "C" int esgpu_result_to_json(const esgpu_result* r, char* buf, size_t cap, size_t* needed) {
     return guarded([&] {
         require(r != nullptr, ESGPU_ERR_INVALID, "null result");

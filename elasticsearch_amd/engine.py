@@ -48,6 +48,14 @@ class ShardResult:
         N.check(N.lib().esgpu_result_to_json(self._ptr, buf, len(buf), ctypes.byref(needed)))
         return buf.value.decode("utf-8")
 
+    def to_xcontent(self):
+        """the search response's "aggregations" object, as Elasticsearch renders it (esgpu_result_to_xcontent)"""
+        needed = ctypes.c_size_t()
+        N.check(N.lib().esgpu_result_to_xcontent(self._ptr, None, 0, ctypes.byref(needed)))
+        buf = ctypes.create_string_buffer(needed.value + 1)
+        N.check(N.lib().esgpu_result_to_xcontent(self._ptr, buf, len(buf), ctypes.byref(needed)))
+        return buf.value.decode("utf-8")
+
     def to_dict(self):
         return json.loads(self.to_json())
 

@@ -411,6 +411,10 @@ int esgpu_cardinality_value(const esgpu_agg_block* block, uint64_t instance, int
 /* XContent-style JSON ({"<name>": {...}}), full double precision, Infinity/NaN as JSON tokens.
  * Writes at most cap bytes (NUL-terminated) and returns the full length in *needed. */
 int esgpu_result_to_json(const esgpu_result* r, char* buf, size_t cap, size_t* needed);
+/* The "aggregations" object of the REST response as Elasticsearch's XContent writes it (compact Jackson JSON, field
+ * order of each class's doXContentBody, Double.toString numbers, null metrics for empty buckets, date keys printed
+ * with strict_date_optional_time in the request's time zone).  Same buffer contract as esgpu_result_to_json. */
+int esgpu_result_to_xcontent(const esgpu_result* r, char* buf, size_t cap, size_t* needed);
 /* Stream (AggregationStreams writeTo / readFrom analogue) for moving shard results between processes. */
 int esgpu_result_serialize(const esgpu_result* r, uint8_t* buf, size_t cap, size_t* needed);
 int esgpu_result_deserialize(const uint8_t* buf, size_t len, esgpu_result** out);
