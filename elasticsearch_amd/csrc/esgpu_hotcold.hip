@@ -1,0 +1,446 @@
+// esgpu_hotcold.hip — K1 for high-cardinality terms (valueCount >> LDS, e.g. 10M url ordinals), hot/cold partitioned
+// counting.  Replaces GlobalOrdinalsStringTermsAggregator.collect's `docCounts.increment(globalOrd)` over a BigArrays
+// LongArray of valueCount counters (A/bucket/terms/GlobalOrdinalsStringTermsAggregator.java:107-135) for the request
+// shapes whose counters cannot be privatised in LDS.
+//
+// Three facts of the segment, gathered once per ordinal column and cached beside it the way Elasticsearch caches a
+// field's global ordinals (HcStats in esgpu_runtime.cpp, built on first use):
+//   * the hot set: the most frequent ordinals (Zipf-like term distributions put most docs on a few thousand), numbered
+//     by frequency (hot slots);
+//   * a recoded copy of the ordinal column in which a hot ordinal reads kHcHotBit | its slot: telling hot from cold is
+//     one bit test, and a hot doc is one LDS add at its slot (no lookup);
+//   * per partition (32768 ordinals) the number of docs whose ordinal is not hot, which bounds what any request over
+//     the segment (any filter, any accept bitset) can write into that partition: the capacities of the partitioned
+//     buffer are therefore known before the request runs, and no histogram pass over the docs is needed.
+// Request passes:
+//   hc_init      reset the overflow cursors and the capacity flag
+//   hc_scatter   ONE read of the recoded column (4 B/doc): hot slots counted in LDS, cold ordinals through per-partition
+//                LDS rings out to the workgroup's static region of the partition as whole 64-byte segments of 16-bit
+//                partition-local offsets (overflow: 64-element-aligned chunks from the partition's overflow pool, one
+//                global atomic per chunk)
+//   hc_count     one workgroup per piece of a partition (one piece unless the partition is far above the average): the
+//                static regions (holes masked by the per-workgroup fill) and the overflow pool counted into LDS (two
+//                16-bit counters per word when the segment's cold counts fit), then one coalesced pass over the counters
+//   hc_hot_reduce  the per-workgroup hot counters summed per slot and added to their ordinals
+// Scatter workgroups: 512 threads, two per CU when the LDS layout fits, so one workgroup's barrier phases overlap the
+// other's loads.
+// Traffic: 4 B/doc + 2 x 2 B per cold doc (~43 % of docs on the Zipf(1) url field) + 8-16 B per ordinal (counters).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "es_common.hpp"
+#include "esgpu_collect.hpp"
+#include "esgpu_kernels.hpp"
+
+namespace esgpu {
+
+constexpr int kHcWG = 512;                           // scatter: 8 waves, two workgroups per CU (P <= 512)
+constexpr int kHcIt = 4;                             // 16-byte loads per thread per tile
+constexpr uint32_t kHcTileDocs = kHcWG * kHcIt * 4;  // 8192 docs per tile (<= kHcTile, the spare elements of pbuf)
+constexpr uint32_t kHcNone = 0xFFFFFFFFu;
+constexpr int kHcCountWG = 1024;                     // counting: 16 waves, 4 vectors in flight per thread
+
+__device__ __forceinline__ uint32_t hc_hash(uint32_t o, uint32_t log2) { return (o * 0x9E3779B1u) >> (32 - log2); }
+
+__global__ void hc_recode_kernel(const uint32_t* ord, uint32_t n, const uint32_t* keys, const uint32_t* vals,
+                                 uint32_t log2, uint32_t* out) {
+    const uint32_t mask = (1u << log2) - 1u;
+    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < n; d += gridDim.x * blockDim.x) {
+        const uint32_t o = ord[d];
+        uint32_t r = o;
+        if (o != kMissingOrd)
+            for (uint32_t h = hc_hash(o, log2);; h = (h + 1) & mask) {
+                const uint32_t k = keys[h];
+                if (k == o) { r = kHcHotBit | vals[h]; break; }
+                if (k == kMissingOrd) break;
+            }
+        out[d] = r;
+    }
+}
+void launch_hc_recode(const uint32_t* ord, uint32_t n, const uint32_t* keys, const uint32_t* vals, uint32_t log2,
+                      uint32_t* out, hipStream_t s) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(hc_recode_kernel, dim3(std::min<uint32_t>(8192, (n + 255) / 256)), dim3(256), 0, s, ord, n, keys,
+                       vals, log2, out);
+}
+
+__global__ void hc_init_kernel(HcParams P) {
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < P.P; p += gridDim.x * blockDim.x)
+        P.ovf_cur[p] = P.part[p].ovf_base;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *P.err = 0u;
+}
+
+// Cold ordinals leave the workgroup only as whole, aligned 64-byte segments (32 offsets; every region and chunk is a
+// multiple of 64 elements).  Each partition owns a 64-slot ring in LDS: a cold doc's single LDS atomic on the
+// partition's word returns its sequence number c since the last flush and the ring half in use, so the doc is written
+// straight into its ring slot; after the tile every full 32-offset half goes out as one 64-byte store from four lanes.
+// A partition that receives more than 64 - pending offsets in one tile (clustered data) writes the excess straight to
+// memory from registers.  (Appending each tile's few offsets per partition to memory left lines partly written in L2:
+// WRITE_SIZE 3x the cold bytes; an LDS counting sort of the tile cost twice the LDS instructions of the ring.)
+#ifndef ESGPU_HC_NT
+#define ESGPU_HC_NT 1
+#endif
+#ifndef ESGPU_HC_EXP  // timing experiments only: 1 = classify alone (steps 2-5 and the flush skipped), 2 = loads alone
+#define ESGPU_HC_EXP 0
+#endif
+constexpr uint32_t kSeg = 32;
+constexpr uint32_t kRing = 2 * kSeg;
+constexpr uint32_t kCnt = (1u << 26) - 1u;  // word: ring base (0 or 32) << 26 | offsets since the last flush
+// ring slot k of partition p in LDS (u16 units): the 16-byte granules of a partition's ring are XOR-swizzled by p, so the
+// same slot of different partitions falls on different banks (rows are 128 B = exactly the 32 banks of a dword store;
+// slots advance in step across partitions, so an unswizzled ring write is a many-way bank conflict)
+__device__ __forceinline__ uint32_t ring_idx(uint32_t p, uint32_t k) {
+    return p * kRing + ((((k >> 3) ^ p) & 7u) << 3) + (k & 7u);
+}
+
+size_t hc_scatter_lds_bytes(uint32_t n_parts, uint32_t hot_n) {
+    // hot counters | rings (u16 x 64) | stp (16 B) + word, cpos, cend
+    return (((size_t)hc_hot_counters(hot_n) * 4 + 15) & ~(size_t)15) + (size_t)n_parts * (kRing * 2 + 16 + 3 * 4);
+}
+
+template <bool HOT>
+__global__ __launch_bounds__(kHcWG) void hc_scatter_kernel(HcParams P) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t NH = HOT ? hc_hot_counters(P.hot_n) : 0u;
+    uint32_t* hot = (uint32_t*)smem;                        // [NH] hot counters (slot s < 64: 4 s + lane % 4)
+    uint16_t* ring = (uint16_t*)(smem + ((NH * 4 + 15) & ~15u));  // [P][64] (16-byte aligned: read as uint4)
+    uint4* stp = (uint4*)(ring + (size_t)P.P * kRing);      // [P] this tile: {split, base A, base B, ring base | L << 8}
+    uint32_t* word = (uint32_t*)(stp + P.P);                // [P] ring base << 26 | offsets since the last flush
+    uint32_t* cpos = word + P.P;                            // [P] next element of the workgroup's current chunk
+    uint32_t* cend = cpos + P.P;                            // [P] end of that chunk
+    const uint32_t word_off = (uint32_t)((unsigned char*)word - smem);
+    const uint32_t w = blockIdx.x;
+    constexpr uint32_t kMask = (1u << kPartShift) - 1u;
+    for (uint32_t i = threadIdx.x; i < NH; i += kHcWG) hot[i] = 0u;
+    for (uint32_t p = threadIdx.x; p < P.P; p += kHcWG) {
+        const HcPart q = P.part[p];
+        word[p] = 0u;
+        cpos[p] = q.sbase + w * q.chunk;
+        cend[p] = cpos[p] + q.chunk;
+    }
+    __syncthreads();
+    // destination of `len` more elements of partition p: the rest of the current chunk, then a fresh overflow chunk
+    // (a returning global atomic; 64-element aligned); returns {split, base A, base B}: element i -> i < split ? A + i
+    // : B + i.  `avail` and every length reserved during the tiles are multiples of 32, so a segment never straddles.
+    auto reserve = [&](uint32_t p, uint32_t len) -> uint3 {
+        const uint32_t a = cpos[p], avail = cend[p] - a;
+        if (len <= avail) {
+            cpos[p] = a + len;
+            return make_uint3(len, a, a);
+        }
+        const HcPart q = P.part[p];
+        const uint32_t need = len - avail;
+        const uint32_t sz = max(q.ovf_chunk, (need + 63u) & ~63u);
+        uint32_t nb = atomicAdd(&P.ovf_cur[p], sz);
+        uint32_t end = nb + sz;
+        if (end > q.cap_end || end < nb) {  // cannot happen by construction of the capacities
+            *P.err = 1u;
+            nb = P.trash;                   // keep every write inside pbuf (kHcTile spare elements)
+            end = nb + need;
+        }
+        cpos[p] = nb + need;
+        cend[p] = end;
+        return make_uint3(avail, a, nb - avail);
+    };
+    const uint32_t b_begin = min(w * P.blocks_per_wg, P.n_blocks);
+    const uint32_t b_end = min(b_begin + P.blocks_per_wg, P.n_blocks);
+    const uint32_t d_begin = b_begin * kBlockDocs;
+    const uint32_t d_end = min(b_end * kBlockDocs, P.n_docs);
+    const uint32_t d_last = P.n_blocks * kBlockDocs - 4;  // loads past the range re-read the segment's last quad
+    const uint32_t tid4 = threadIdx.x * 4;
+    auto load = [&](uint32_t t0, uint32_t o[kHcIt][4]) {
+#pragma unroll
+        for (int k = 0; k < kHcIt; ++k) {
+            const uint32_t d = min(t0 + k * (kHcWG * 4) + tid4, d_last);
+#if ESGPU_HC_NT  // the column is read once: non-temporal loads keep L2 for the partitions' open segments (5 % faster)
+            const u32x4_t a = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(P.rc + d));
+            o[k][0] = a.x; o[k][1] = a.y; o[k][2] = a.z; o[k][3] = a.w;
+#else
+            load_u32x4(P.rc, d, o[k]);
+#endif
+        }
+    };
+    auto process = [&](uint32_t t0, const uint32_t o[kHcIt][4]) {
+        // 1. classify: hot -> LDS counter; cold -> sequence number in the partition's ring (written when it fits).
+        //    Straight-line phases over the thread's 16 docs, so each phase's LDS operations issue back to back and
+        //    their latencies overlap (hot adds + returning adds on the partition words; ring writes).
+        constexpr int kD = kHcIt * 4;
+        uint32_t rk[kHcIt][4];
+        uint32_t okm = 0;  // bit d: doc d counts
+#pragma unroll
+        for (int k = 0; k < kHcIt; ++k) {
+            const uint32_t doc0 = t0 + k * (kHcWG * 4) + tid4;
+            uint32_t ok = 0u;
+            if (doc0 < d_end) ok = doc0 + 4 <= d_end ? 0xFu : ((1u << (d_end - doc0)) - 1u);
+            if (ok && P.accept) ok &= bits4(P.accept, doc0);
+            for (int q = 0; q < P.npred && ok; ++q) ok &= eval_pred(P.pred[q], doc0);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t v = o[k][j];
+                const bool c = (v & kHcHotBit) ? v != kMissingOrd : v < P.T;
+                okm |= (((ok >> j) & 1u) && c ? 1u : 0u) << (k * 4 + j);
+            }
+        }
+#if ESGPU_HC_EXP == 2
+        {
+            uint32_t acc = 0;
+#pragma unroll
+            for (int d = 0; d < kD; ++d) acc += ((okm >> d) & 1u) ? o[d / 4][d % 4] : 0u;
+            if (acc == 0x12345678u) hot[0] = acc;
+            return;
+        }
+#endif
+        // one LDS atomic per doc: a hot doc adds at its slot's counter (the 64 most frequent slots spread over 4 lane-
+        // rotated copies), a cold doc at its partition's word and keeps the returned sequence number; one
+        // ds_add_rtn_u32 with per-lane addresses serves both (two instructions cost twice: LDS atomics are issue-bound)
+        uint32_t old[kD];
+#pragma unroll
+        for (int d = 0; d < kD; ++d) {
+            const uint32_t v = o[d / 4][d % 4];
+            const bool hb = (v & kHcHotBit) != 0u;
+            const uint32_t sl = v & ~kHcHotBit;
+            // one LDS address (a byte offset from smem: a select between two pointers compiles to flat atomics)
+            const uint32_t off = hb ? (sl < kHcHotCopies ? 4 * sl + (threadIdx.x & 3) : 3 * kHcHotCopies + sl) * 4u
+                                    : word_off + (v >> kPartShift) * 4u;
+            old[d] = ((okm >> d) & 1u) ? atomicAdd((uint32_t*)(smem + off), 1u) : kHcNone;
+            if (hb) old[d] = kHcNone;
+        }
+        bool burst = false;
+#pragma unroll
+        for (int d = 0; d < kD; ++d) {
+            const uint32_t v = o[d / 4][d % 4];
+            const uint32_t r = old[d] == kHcNone ? kHcNone : (old[d] & kCnt);
+            if (r < kRing) ring[ring_idx(v >> kPartShift, ((old[d] >> 26) + r) & (kRing - 1))] = (uint16_t)(v & kMask);
+            burst |= r != kHcNone && r >= kRing;
+            rk[d / 4][d % 4] = r;
+        }
+        const bool any_burst = __syncthreads_or(burst);
+#if ESGPU_HC_EXP == 1
+        return;
+#endif
+        // 2. per partition: whole segments to flush (L), their destination, the ring state after the flush
+        for (uint32_t p = threadIdx.x; p < P.P; p += kHcWG) {
+            const uint32_t wd = word[p], C = wd & kCnt, rb = wd >> 26;
+            const uint32_t L = C & ~(kSeg - 1);
+            if (L) {
+                const uint3 d = reserve(p, L);
+                stp[p] = make_uint4(d.x, d.y, d.z, rb | (L << 8));
+                word[p] = (((rb + L) & (kRing - 1)) << 26) | (C - L);
+            } else {
+                stp[p].w = rb;  // bursts need the ring base only when L > 0; keep w coherent for step 5
+            }
+        }
+        __syncthreads();
+        // 3. offsets beyond the ring that are flushed this tile: straight to memory (clustered data only)
+        if (any_burst) {
+#pragma unroll
+            for (int k = 0; k < kHcIt; ++k)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t r = rk[k][j];
+                    if (r != kHcNone && r >= kRing) {
+                        const uint32_t p = o[k][j] >> kPartShift;
+                        const uint4 st = stp[p];
+                        if (r < (st.w >> 8)) P.pbuf[r < st.x ? st.y + r : st.z + r] = (uint16_t)(o[k][j] & kMask);
+                    }
+                }
+        }
+        // 4. ring halves out: four lanes per 64-byte segment, 16 bytes each (partition p -> lane group p % (WG / 4))
+        {
+            const uint32_t grp = threadIdx.x >> 2, qt = threadIdx.x & 3;
+            for (uint32_t p = grp; p < P.P; p += kHcWG / 4) {
+                const uint4 st = stp[p];
+                const uint32_t L = st.w >> 8, rb = st.w & 0xFFu;
+                const uint32_t nseg = min(L, kRing) / kSeg;
+                for (uint32_t sgi = 0; sgi < nseg; ++sgi) {
+                    const uint32_t i0 = sgi * kSeg;  // sequence index of the segment's first offset
+                    const uint32_t half = (rb + i0) & (kRing - 1);
+                    const uint4 v = *reinterpret_cast<const uint4*>(ring + ring_idx(p, half + qt * 8));
+                    *reinterpret_cast<uint4*>(P.pbuf + (i0 < st.x ? st.y + i0 : st.z + i0) + qt * 8) = v;
+                }
+            }
+        }
+        __syncthreads();
+        // 5. burst offsets that stay pending: into the ring slots the flush freed
+        if (any_burst) {
+#pragma unroll
+            for (int k = 0; k < kHcIt; ++k)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t r = rk[k][j];
+                    if (r != kHcNone && r >= kRing) {
+                        const uint32_t p = o[k][j] >> kPartShift;
+                        const uint4 st = stp[p];
+                        if (r >= (st.w >> 8)) ring[ring_idx(p, ((st.w & 0xFFu) + r) & (kRing - 1))] = (uint16_t)(o[k][j] & kMask);
+                    }
+                }
+        }
+        // the next tile's classify writes ring slots past the pending ones (step 2 set the words before two barriers);
+        // step 5's slots are the pending ones, so no barrier is needed here
+    };
+    const uint32_t span = b_end > b_begin ? (b_end - b_begin) * kBlockDocs : 0u;
+    if (span) {
+        uint32_t A[kHcIt][4], B[kHcIt][4];
+        load(d_begin, A);
+        load(d_begin + kHcTileDocs, B);
+        for (uint32_t t0 = d_begin; t0 < d_begin + span; t0 += 2 * kHcTileDocs) {
+            process(t0, A);
+            load(t0 + 2 * kHcTileDocs, A);
+            if (t0 + kHcTileDocs < d_begin + span) process(t0 + kHcTileDocs, B);
+            load(t0 + 3 * kHcTileDocs, B);
+        }
+    }
+    __syncthreads();
+    // the partitions' pending offsets (one partial segment); static-region fill; sentinel tail of an overflow chunk
+    for (uint32_t p = threadIdx.x; p < P.P && ESGPU_HC_EXP == 0; p += kHcWG) {
+        const HcPart q = P.part[p];
+        const uint32_t wd = word[p], f = wd & kCnt, rb = wd >> 26;
+        if (f) {
+            const uint3 d = reserve(p, f);
+            for (uint32_t i = 0; i < f; ++i) P.pbuf[i < d.x ? d.y + i : d.z + i] = ring[ring_idx(p, (rb + i) & (kRing - 1))];
+        }
+        const uint32_t s0 = q.sbase + w * q.chunk;
+        uint32_t used = q.chunk;
+        if (cend[p] == s0 + q.chunk) {
+            used = cpos[p] - s0;
+        } else if (cpos[p] < cend[p] && cend[p] <= q.cap_end) {
+            for (uint32_t e = cpos[p]; e < cend[p]; ++e) P.pbuf[e] = 0xFFFFu;
+        }
+        P.used[(size_t)p * P.G + w] = used;
+    }
+    if (HOT)
+        for (uint32_t i = threadIdx.x; i < NH; i += kHcWG) P.hot_slab[(size_t)w * NH + i] = hot[i];
+}
+
+// one workgroup per piece: region elements [lo, hi) of partition p, where the region is the G static regions
+// (element g * chunk + i, valid while i < used[g]) followed by the overflow pool (0xFFFF = unused)
+template <bool U16>
+__global__ __launch_bounds__(kHcCountWG) void hc_count_kernel(HcParams P) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t* cnt = (uint32_t*)smem;  // U16: [16384] two 16-bit counters per word, else [32768]
+    uint32_t* used = cnt + (U16 ? (1u << kPartShift) / 2 : (1u << kPartShift));  // [G]
+    const HcPiece pc = P.piece[blockIdx.x];
+    const uint32_t p = pc.p;
+    const HcPart q = P.part[p];
+    const uint32_t nwords = U16 ? (1u << kPartShift) / 2 : (1u << kPartShift);
+    for (uint32_t i = threadIdx.x; i < nwords; i += kHcCountWG) cnt[i] = 0u;
+    for (uint32_t i = threadIdx.x; i < P.G; i += kHcCountWG) used[i] = P.used[(size_t)p * P.G + i];
+    __syncthreads();
+    auto add = [&](uint32_t v) {
+        if (U16) atomicAdd(&cnt[v >> 1], 1u << ((v & 1u) * 16));
+        else atomicAdd(&cnt[v], 1u);
+    };
+    // static regions: 8 elements per 16-byte vector (chunk is a multiple of 64: a vector never straddles two regions)
+    const uint32_t cv = q.chunk / 8;  // vectors per region
+    const uint32_t nstat = cv * P.G;  // vectors of the static part
+    {
+        const uint32_t k0 = pc.lo / 8, k1 = min(pc.hi / 8, nstat);
+        if (k1 > k0) {
+            const uint4* src = reinterpret_cast<const uint4*>(P.pbuf + q.sbase);
+            auto count_vec = [&](uint32_t k, const uint4 v) {
+                const uint32_t g = k / cv;
+                const uint32_t r0 = (k - g * cv) * 8;
+                const uint32_t u = used[g];
+                const uint32_t m = u > r0 ? min(u - r0, 8u) : 0u;
+                const uint32_t wds[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    if (2 * t < (int)m) add(wds[t] & 0xFFFFu);
+                    if (2 * t + 1 < (int)m) add(wds[t] >> 16);
+                }
+            };
+            // four vectors in flight per thread, each reloaded right after it is counted (loads unconditional, clamped)
+            constexpr uint32_t S = kHcCountWG;
+            const uint32_t t = k0 + threadIdx.x, last = k1 - 1;
+            uint4 v0 = src[min(t, last)], v1 = src[min(t + S, last)];
+            uint4 v2 = src[min(t + 2 * S, last)], v3 = src[min(t + 3 * S, last)];
+            for (uint32_t k = t; k < k1; k += 4 * S) {
+                count_vec(k, v0);
+                v0 = src[min(k + 4 * S, last)];
+                if (k + S < k1) count_vec(k + S, v1);
+                v1 = src[min(k + 5 * S, last)];
+                if (k + 2 * S < k1) count_vec(k + 2 * S, v2);
+                v2 = src[min(k + 6 * S, last)];
+                if (k + 3 * S < k1) count_vec(k + 3 * S, v3);
+                v3 = src[min(k + 7 * S, last)];
+            }
+        }
+    }
+    // overflow pool (chunks of 64-element multiples; unused tails hold the 0xFFFF sentinel)
+    {
+        const uint32_t sn = nstat * 8;  // region index of the pool's first element
+        const uint32_t fill = min(P.ovf_cur[p], q.cap_end) - q.ovf_base;
+        const uint32_t e0 = max(pc.lo, sn) - sn, e1 = min(pc.hi, sn + fill);
+        if (e1 > sn + e0) {
+            const uint4* src = reinterpret_cast<const uint4*>(P.pbuf + q.ovf_base);
+            for (uint32_t k = e0 / 8 + threadIdx.x; k < (e1 - sn) / 8; k += kHcCountWG) {
+                const uint4 v = src[k];
+                const uint32_t wds[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const uint32_t lo = wds[t] & 0xFFFFu, hi = wds[t] >> 16;
+                    if (lo != 0xFFFFu) add(lo);
+                    if (hi != 0xFFFFu) add(hi);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t base = p << kPartShift;
+    const uint32_t S = min(1u << kPartShift, P.T - base);
+    auto get = [&](uint32_t j) { return U16 ? (cnt[j >> 1] >> ((j & 1u) * 16)) & 0xFFFFu : cnt[j]; };
+    if (!pc.whole) {  // one of several pieces of a heavy partition: add the non-zero counters
+        for (uint32_t j = threadIdx.x; j < S; j += kHcCountWG) {
+            const uint32_t c = get(j);
+            if (c) atomicAdd(&P.counts[base + j], (unsigned long long)c);
+        }
+    } else if (P.overwrite) {
+        for (uint32_t j = threadIdx.x; j < S; j += kHcCountWG) P.counts[base + j] = get(j);
+    } else {  // later segments: read-modify-write, four counters in flight per thread
+        for (uint32_t j = threadIdx.x; j < S; j += 4 * kHcCountWG) {
+            unsigned long long g[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) g[u] = j + u * kHcCountWG < S ? P.counts[base + j + u * kHcCountWG] : 0ull;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (j + u * kHcCountWG < S) P.counts[base + j + u * kHcCountWG] = g[u] + get(j + u * kHcCountWG);
+        }
+    }
+}
+
+// hot slot totals: block (b, r) sums slots [64 b, 64 b + 64) over the slabs g = r (mod kHotSplit) (4 waves split those);
+// a slot's lane-rotated copies are summed too
+constexpr uint32_t kHotSplit = 8;
+__global__ __launch_bounds__(256) void hc_hot_reduce_kernel(HcParams P) {
+    __shared__ uint32_t part[4][64];
+    const uint32_t NH = hc_hot_counters(P.hot_n);
+    const uint32_t s = blockIdx.x * 64 + (threadIdx.x & 63);
+    const uint32_t wv = threadIdx.x >> 6;
+    uint32_t sum = 0;
+    if (s < P.hot_n) {
+        const uint32_t i0 = s < kHcHotCopies ? 4 * s : 3 * kHcHotCopies + s;
+        const uint32_t nc = s < kHcHotCopies ? 4 : 1;
+        for (uint32_t g = blockIdx.y + wv * kHotSplit; g < P.G; g += 4 * kHotSplit)
+            for (uint32_t c = 0; c < nc; ++c) sum += P.hot_slab[(size_t)g * NH + i0 + c];
+    }
+    part[wv][threadIdx.x & 63] = sum;
+    __syncthreads();
+    if (wv == 0 && s < P.hot_n) {
+        const uint32_t t = part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] + part[3][threadIdx.x];
+        const uint32_t o = P.hot_ord[s];
+        if (o < P.T && t) atomicAdd(&P.counts[o], (unsigned long long)t);
+    }
+}
+
+void launch_hotcold(const HcParams& p, hipStream_t s) {
+    hipLaunchKernelGGL(hc_init_kernel, dim3((p.P + 255) / 256), dim3(256), 0, s, p);
+    const size_t lds = hc_scatter_lds_bytes(p.P, p.hot_n);
+    if (p.hot_n) hipLaunchKernelGGL(hc_scatter_kernel<true>, dim3(p.G), dim3(kHcWG), lds, s, p);
+    else hipLaunchKernelGGL(hc_scatter_kernel<false>, dim3(p.G), dim3(kHcWG), lds, s, p);
+    const size_t clds = (p.u16_counters ? (1u << kPartShift) / 2 : (1u << kPartShift)) * 4 + (size_t)p.G * 4;
+    if (p.u16_counters) hipLaunchKernelGGL(hc_count_kernel<true>, dim3(p.n_pieces), dim3(kHcCountWG), clds, s, p);
+    else hipLaunchKernelGGL(hc_count_kernel<false>, dim3(p.n_pieces), dim3(kHcCountWG), clds, s, p);
+    if (p.hot_n) hipLaunchKernelGGL(hc_hot_reduce_kernel, dim3((p.hot_n + 63) / 64, kHotSplit), dim3(256), 0, s, p);
+}
+
+}  // namespace esgpu

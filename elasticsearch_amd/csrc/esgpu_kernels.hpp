@@ -222,6 +222,53 @@ size_t part_scatter_lds_bytes(uint32_t n_parts);
 uint32_t part_wg_per_cu();  // workgroups per CU of the histogram / scatter passes
 uint32_t part_scan_tiles(uint32_t n);
 
+// ---- high-cardinality terms, hot/cold partitioned counting (esgpu_hotcold.hip) ----
+constexpr uint32_t kHcTile = 16384;     // upper bound of the docs of one scatter tile (spare elements of pbuf)
+constexpr uint32_t kHcMaxParts = 1024;  // partitions the scatter handles: T <= 2^25 ordinals
+constexpr uint32_t kHcHotBit = 0x80000000u;  // recoded column: kHcHotBit | hot slot
+constexpr uint32_t kHcHotCopies = 64;   // the 64 most frequent hot slots keep 4 lane-rotated LDS counters each
+struct HcPart {            // one partition's layout in pbuf (elements), fixed per segment by its HcStats
+    uint32_t sbase;        // static regions: workgroup g owns [sbase + g * chunk, sbase + (g + 1) * chunk)
+    uint32_t chunk;        // multiple of 64
+    uint32_t ovf_base;     // overflow pool [ovf_base, cap_end): chunks of >= ovf_chunk elements
+    uint32_t cap_end;
+    uint32_t ovf_chunk;
+    uint32_t pad[3];
+};
+struct HcPiece {           // a counting workgroup's share: region elements [lo, hi) of partition p (static ++ overflow)
+    uint32_t p, lo, hi, whole;  // whole: the piece is the partition's only one (stores its counters, no atomics)
+};
+struct HcParams {
+    uint32_t n_docs, n_blocks, blocks_per_wg, G;   // G = scatter workgroups (the segment statistics' layout)
+    const uint32_t* rc;                // recoded ordinal column: cold ordinal | kHcHotBit | hot slot | 0xFFFFFFFF missing
+    uint32_t T, P;
+    int32_t npred;
+    PredDev pred[4];
+    const uint64_t* accept;
+    uint32_t hot_n;                    // hot slots (0 = none), most frequent first
+    const uint32_t* hot_ord;           // [hot_n] ordinal of each hot slot
+    const HcPart* part;                // [P]
+    const HcPiece* piece;              // [n_pieces]
+    uint32_t n_pieces;
+    uint32_t* ovf_cur;                 // [P] next free element of each overflow pool
+    uint32_t* used;                    // [P][G] elements written into each workgroup's static region
+    uint32_t* hot_slab;                // [G][hc_hot_counters(hot_n)] per-workgroup hot counters
+    uint16_t* pbuf;                    // partition-local offsets (ord & 32767); 0xFFFF = unused overflow element
+    uint32_t trash;                    // kHcTile spare elements at the end of pbuf (capacity violation sink)
+    unsigned long long* counts;        // [T]
+    uint32_t* err;                     // set to 1 on a capacity violation (device-visible host word)
+    int32_t u16_counters;              // every cold ordinal's count in the segment < 65536: packed LDS counters
+    int32_t overwrite;                 // store the counts instead of adding (the plan's first segment)
+};
+__host__ __device__ inline uint32_t hc_hot_counters(uint32_t hot_n) { return hot_n + 3 * (hot_n < kHcHotCopies ? hot_n : kHcHotCopies); }
+size_t hc_scatter_lds_bytes(uint32_t n_parts, uint32_t hot_n);
+constexpr uint32_t kHcScatterWG = 512;  // threads of a scatter workgroup (esgpu_hotcold.hip kHcWG)
+void launch_hotcold(const HcParams& p, hipStream_t s);
+// stats time: out[d] = kHcHotBit | slot for the hot ordinals (open-addressing table keys -> vals, 2^log2 entries,
+// 0xFFFFFFFF = empty key), the ordinal itself otherwise
+void launch_hc_recode(const uint32_t* ord, uint32_t n, const uint32_t* keys, const uint32_t* vals, uint32_t log2,
+                      uint32_t* out, hipStream_t s);
+
 // ---- GPU top-k over a count vector (BucketPriorityQueue replacement for large T) ----
 struct TopkParams {
     const unsigned long long* counts;

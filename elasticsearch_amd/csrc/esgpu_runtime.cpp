@@ -224,6 +224,8 @@ static bool same_dict(const std::shared_ptr<const TermDict>& a, const std::share
     return a == b || (a && b && a->n == b->n && a->identity == b->identity);
 }
 
+struct HcStats;  // hot set + partition capacities of a high-cardinality ordinal column (collect_hotcold)
+
 struct DevColumn {
     std::string name;
     int32_t type = 0;
@@ -241,6 +243,9 @@ struct DevColumn {
     // global ordinals (esgpu_ordinal_map_build): the segment's ordinals remapped into the reader-wide dictionary
     std::shared_ptr<const TermDict> gdict;
     DevBuf gvalues;
+    // statistics of ords() for high-cardinality terms, built on first use (ensure_hc_stats); rebuilt when ords() is
+    // replaced by a remap into another global dictionary
+    std::shared_ptr<const HcStats> hc;
 
     const DevBuf& ords() const { return gdict ? gvalues : values; }       // what terms aggregations count by
     uint64_t ord_count() const { return gdict ? gdict->count() : value_count; }
@@ -876,6 +881,9 @@ struct esgpu_plan {
     Scratch s_fbits, s_vbits;  // doc bitset of multi-valued filters, per-value bitset of a multi-valued HLL field
     Scratch s_cells;           // cell list of a cardinality gather
     Scratch s_zkey;            // per-block key ranges of a windowed collect
+    Scratch s_hcur, s_hused, s_hslab;  // hot/cold counting: overflow cursors, static-region fills, hot slabs
+    PinnedBuf h_hcerr;         // hot/cold counting: capacity-violation word (written by the scatter kernel)
+    bool hc_check = false;     // a hot/cold collect ran since the last post_collection
     PinnedBuf h_keys;
     hipEvent_t ev_mid = nullptr;
     PinnedBuf h_tcnt, h_rows, h_dst[6];
@@ -1425,6 +1433,255 @@ static bool collect_partitioned(esgpu_plan* p, Pipeline& pl, const esgpu_segment
     return true;
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// K1 for valueCount >> LDS, hot/cold form (esgpu_hotcold.hip): one read of the ordinal column instead of two, the
+// most frequent ordinals counted in LDS and never written out, the rest appended to partitions whose capacities come
+// from the segment's statistics (no histogram pass).  The statistics are the segment's, built on the first request
+// over the column and kept beside it, the way Elasticsearch builds a field's global ordinals on first use and caches
+// them (GlobalOrdinalsBuilder.build via IndexFieldDataService's cache, C/index/fielddata/ordinals/
+// GlobalOrdinalsBuilder.java:46-70).
+// ------------------------------------------------------------------------------------------------------------
+#ifndef ESGPU_HOTCOLD
+#define ESGPU_HOTCOLD 1
+#endif
+#ifndef ESGPU_HOT_MAX
+#define ESGPU_HOT_MAX 16384  // hot slots at most (LDS counters of the scatter)
+#endif
+#ifndef ESGPU_NO_HOT
+#define ESGPU_NO_HOT 0  // timing experiments: no hot set
+#endif
+
+struct HcStats {
+    const void* src = nullptr;   // the ordinal buffer described (DevColumn::ords())
+    uint64_t T = 0;
+    uint32_t G = 0, P = 0, hot_n = 0, trash = 0, n_pieces = 0;
+    bool u16 = false;            // every cold ordinal's count < 65536: packed 16-bit counters in the counting pass
+    uint64_t pbuf_elems = 0;     // partition regions + kHcTile spare elements
+    uint64_t hot_docs = 0, docs = 0;
+    DevBuf d_rc;                 // recoded ordinal column (hot ordinals as kHcHotBit | slot); empty: no hot set
+    DevBuf d_hot_ord, d_part, d_piece;
+};
+
+static uint32_t hc_hash_host(uint32_t o, uint32_t log2) { return (uint32_t)(o * 0x9E3779B1u) >> (32 - log2); }
+
+// doc count of every ordinal of a column (no filters), by the radix-partitioned passes (collect_partitioned's kernels)
+static void count_all_ordinals(esgpu_ctx* c, const uint32_t* ord, uint32_t max_doc, uint32_t n_pad, uint32_t T,
+                               DevBuf& counts, hipStream_t st) {
+    counts.alloc(c, (size_t)std::max<uint32_t>(T, 1) * 8);
+    HIPX(hipMemsetAsync(counts.p, 0, counts.bytes, st));
+    if (max_doc == 0) return;
+    PartParams Q{};
+    Q.n_docs = max_doc;
+    Q.n_blocks = n_pad / kBlockDocs;
+    const uint32_t target = (uint32_t)c->cus * part_wg_per_cu();
+    Q.blocks_per_wg = std::max(1u, (Q.n_blocks + target - 1) / target);
+    Q.G = (Q.n_blocks + Q.blocks_per_wg - 1) / Q.blocks_per_wg;
+    Q.ord = ord;
+    Q.T = T;
+    Q.shift = kPartShift;
+    Q.P = (uint32_t)(((uint64_t)T + (1u << Q.shift) - 1) >> Q.shift);
+    DevBuf wgc, pbeg, tiles, pbuf;
+    wgc.alloc(c, (size_t)Q.P * Q.G * 4);
+    pbeg.alloc(c, (size_t)(Q.P + 1) * 4);
+    const uint32_t ntiles = part_scan_tiles(Q.P * Q.G);
+    require(ntiles <= 4096, ESGPU_ERR_INVALID, "partition scan too large");
+    tiles.alloc(c, (size_t)ntiles * 4);
+    pbuf.alloc(c, ((size_t)max_doc + 8) * 2);
+    Q.wg_counts = wgc.as<uint32_t>();
+    Q.part_begin = pbeg.as<uint32_t>();
+    Q.tile_sums = tiles.as<uint32_t>();
+    Q.pbuf = pbuf.as<uint16_t>();
+    Q.counts = counts.as<unsigned long long>();
+    const uint64_t want = std::min<uint64_t>((uint64_t)c->cus * 4, std::max<uint64_t>((uint64_t)c->cus, (uint64_t)max_doc >> 19));
+    Q.chunk = (uint32_t)std::max<uint64_t>(1u << 16, (((uint64_t)max_doc + want - 1) / want + 7) & ~7ull);
+    launch_part_hist(Q, st);
+    launch_part_scan(Q, st);
+    launch_part_scatter(Q, st);
+    launch_part_count(Q, st);
+    HIPX(hipGetLastError());
+    HIPX(hipStreamSynchronize(st));  // the scratch buffers are released on return
+}
+
+// The column's hot set and partition capacities (built once per ordinal buffer, under the context lock).  Returns null
+// when the column is outside what the hot/cold kernels handle (more than kHcMaxParts partitions, or a buffer beyond
+// 32-bit element offsets): the caller keeps the histogram-pass form.
+static std::shared_ptr<const HcStats> ensure_hc_stats(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s,
+                                                     uint32_t T, hipStream_t st) {
+    DevColumn* mcol = const_cast<DevColumn*>(col);
+    std::lock_guard<std::mutex> lk(c->mu);  // plans on different threads may share the segment
+    const void* src = col->ords().p;
+    if (mcol->hc && mcol->hc->src == src && mcol->hc->T == T) return mcol->hc;
+    const uint32_t P = (uint32_t)(((uint64_t)T + (1u << kPartShift) - 1) >> kPartShift);
+    if (P == 0 || P > kHcMaxParts || c->cus <= 0) return nullptr;
+    auto hs = std::make_shared<HcStats>();
+    hs->src = src;
+    hs->T = T;
+    hs->P = P;
+    std::vector<uint64_t> cnt(T, 0);
+    {
+        DevBuf d;
+        count_all_ordinals(c, (const uint32_t*)src, s->max_doc, s->n_pad, T, d, st);
+        HIPX(hipMemcpy(cnt.data(), d.p, (size_t)T * 8, hipMemcpyDeviceToHost));
+    }
+    uint64_t total = 0;
+    for (uint64_t v : cnt) total += v;
+    hs->docs = total;
+    // scatter workgroups and hot slots: two workgroups per CU while their LDS layouts fit with >= 2048 hot counters
+    const size_t kLdsCu = 160 * 1024 - 512;
+    auto hot_fit = [&](size_t budget) -> int64_t {
+        const int64_t room = ((int64_t)budget - (int64_t)hc_scatter_lds_bytes(P, 0)) / 4 - 3 * (int64_t)kHcHotCopies - 4;
+        return std::min<int64_t>(ESGPU_HOT_MAX, room) & ~63ll;
+    };
+    uint32_t H;
+    if (hot_fit(kLdsCu / 2) >= 2048) {
+        hs->G = (uint32_t)c->cus * 2;
+        H = (uint32_t)hot_fit(kLdsCu / 2);
+    } else {
+        hs->G = (uint32_t)c->cus;
+        H = (uint32_t)std::max<int64_t>(0, hot_fit(kLdsCu));
+    }
+    // hot set: the H most frequent ordinals (ties by ordinal), slot 0 the most frequent
+    std::vector<uint32_t> hot;
+    uint64_t hot_total = 0;
+    if (H && !ESGPU_NO_HOT) {
+        const uint32_t ncand = (uint32_t)std::min<uint64_t>(T, H);
+        std::vector<uint32_t> idx(T);
+        for (uint32_t o = 0; o < T; ++o) idx[o] = o;
+        auto better = [&](uint32_t a, uint32_t b) { return cnt[a] != cnt[b] ? cnt[a] > cnt[b] : a < b; };
+        if (ncand < T) std::nth_element(idx.begin(), idx.begin() + ncand, idx.end(), better);
+        idx.resize(ncand);
+        std::sort(idx.begin(), idx.end(), better);
+        for (uint32_t o : idx) {
+            if (cnt[o] == 0) break;
+            hot.push_back(o);
+            hot_total += cnt[o];
+        }
+        if (hot_total * 20 < total) {  // under 5 % of the docs: the recoded copy would not pay for itself
+            hot.clear();
+            hot_total = 0;
+        }
+    }
+    hs->hot_n = (uint32_t)hot.size();
+    hs->hot_docs = hot_total;
+    std::vector<uint8_t> is_hot(T, 0);
+    for (uint32_t o : hot) is_hot[o] = 1;
+    std::vector<uint64_t> cold(P, 0);
+    uint64_t max_cold = 0;
+    for (uint32_t o = 0; o < T; ++o) {
+        if (!cnt[o] || is_hot[o]) continue;
+        cold[o >> kPartShift] += cnt[o];
+        max_cold = std::max(max_cold, cnt[o]);
+    }
+    hs->u16 = max_cold < 65536;
+    // layout: per partition, G static regions of `chunk` (its expected share per workgroup) then an overflow pool that
+    // covers every way the docs can be spread over the workgroups: a workgroup allocates a new overflow chunk only when
+    // its current one is full, so what it leaves unused is under one chunk (sizes: DESIGN.md §5)
+    std::vector<HcPart> parts(P);
+    std::vector<uint64_t> cap(P);
+    uint64_t acc = 0;
+    const uint64_t G = hs->G;
+    for (uint32_t p = 0; p < P; ++p) {
+        HcPart& q = parts[p];
+        // static region: the expected share x 1.125 (+64): overflow allocations (a returning global atomic that the
+        // whole workgroup waits for) stay rare on evenly spread data
+        const uint64_t share = (cold[p] + G - 1) / G;
+        const uint64_t chunk = cold[p] ? ((share + share / 8 + 64 + 63) & ~63ull) : 0;
+        const uint64_t ovf = std::max<uint64_t>(64, ((chunk / 4) + 63) & ~63ull);
+        q.sbase = (uint32_t)acc;
+        q.chunk = (uint32_t)chunk;
+        q.ovf_base = (uint32_t)(acc + G * chunk);
+        acc += G * chunk + cold[p] + G * ovf;
+        q.cap_end = (uint32_t)acc;
+        q.ovf_chunk = (uint32_t)ovf;
+        cap[p] = acc - q.sbase;
+        if (acc + kHcTile + 64 >= 0xFFFFFFFFull) return nullptr;
+    }
+    hs->trash = (uint32_t)acc;
+    hs->pbuf_elems = acc + kHcTile;
+    // counting pieces: a partition far above the average region (a heavy cold ordinal) is split so that no counting
+    // workgroup serialises the pass; the pieces of a split partition add their counters atomically
+    const uint64_t piece_len = std::max<uint64_t>(1ull << 20, (4 * acc / P + 63) & ~63ull);
+    std::vector<HcPiece> pieces;
+    for (uint32_t p = 0; p < P; ++p) {
+        const uint32_t n = (uint32_t)std::max<uint64_t>(1, (cap[p] + piece_len - 1) / piece_len);
+        for (uint32_t k = 0; k < n; ++k)
+            pieces.push_back(HcPiece{p, (uint32_t)(k * piece_len), (uint32_t)std::min<uint64_t>((k + 1) * piece_len, cap[p]),
+                                     n == 1 ? 1u : 0u});
+    }
+    hs->n_pieces = (uint32_t)pieces.size();
+    hs->d_part.alloc(c, parts.size() * sizeof(HcPart));
+    hs->d_piece.alloc(c, pieces.size() * sizeof(HcPiece));
+    HIPX(hipMemcpy(hs->d_part.p, parts.data(), parts.size() * sizeof(HcPart), hipMemcpyHostToDevice));
+    HIPX(hipMemcpy(hs->d_piece.p, pieces.data(), pieces.size() * sizeof(HcPiece), hipMemcpyHostToDevice));
+    if (!hot.empty()) {
+        // the recoded column: an open-addressing table (load <= 1/4) of the hot ordinals, probed once per doc here
+        uint32_t log2 = 2;
+        while ((1u << log2) < 4 * hot.size()) ++log2;
+        std::vector<uint32_t> keys(1u << log2, kMissingOrd), vals(1u << log2, 0);
+        for (uint32_t sl = 0; sl < hot.size(); ++sl) {
+            uint32_t h = hc_hash_host(hot[sl], log2);
+            while (keys[h] != kMissingOrd) h = (h + 1) & ((1u << log2) - 1);
+            keys[h] = hot[sl];
+            vals[h] = sl;
+        }
+        DevBuf dk, dv;
+        dk.alloc(c, keys.size() * 4);
+        dv.alloc(c, vals.size() * 4);
+        HIPX(hipMemcpy(dk.p, keys.data(), keys.size() * 4, hipMemcpyHostToDevice));
+        HIPX(hipMemcpy(dv.p, vals.data(), vals.size() * 4, hipMemcpyHostToDevice));
+        hs->d_rc.alloc(c, (size_t)s->n_pad * 4);
+        launch_hc_recode((const uint32_t*)src, s->n_pad, dk.as<uint32_t>(), dv.as<uint32_t>(), log2, hs->d_rc.as<uint32_t>(), st);
+        HIPX(hipGetLastError());
+        hs->d_hot_ord.alloc(c, hot.size() * 4);
+        HIPX(hipMemcpy(hs->d_hot_ord.p, hot.data(), hot.size() * 4, hipMemcpyHostToDevice));
+        HIPX(hipStreamSynchronize(st));  // the table buffers are released on return
+    }
+    mcol->hc = hs;
+    return hs;
+}
+
+static bool collect_hotcold(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const DevColumn* oc,
+                            const uint64_t* d_accept, const PredDev* pred, int npred, bool first_segment) {
+    esgpu_ctx* c = p->ctx;
+    hipStream_t st = p->stream;
+    std::shared_ptr<const HcStats> hs = ensure_hc_stats(c, oc, s, pl.T, st);
+    if (!hs) return false;
+    HcParams H{};
+    H.n_docs = s->max_doc;
+    H.n_blocks = s->n_pad / kBlockDocs;
+    H.G = hs->G;
+    H.blocks_per_wg = std::max(1u, (H.n_blocks + H.G - 1) / H.G);
+    H.rc = hs->hot_n ? hs->d_rc.as<uint32_t>() : oc->ords().as<uint32_t>();
+    H.T = pl.T;
+    H.P = hs->P;
+    H.npred = npred;
+    for (int k = 0; k < npred; ++k) H.pred[k] = pred[k];
+    H.accept = d_accept;
+    H.hot_n = hs->hot_n;
+    H.hot_ord = hs->d_hot_ord.as<uint32_t>();
+    H.part = hs->d_part.as<HcPart>();
+    H.piece = hs->d_piece.as<HcPiece>();
+    H.n_pieces = hs->n_pieces;
+    H.ovf_cur = (uint32_t*)p->s_hcur.ensure(c, (size_t)H.P * 4);
+    H.used = (uint32_t*)p->s_hused.ensure(c, (size_t)H.P * H.G * 4);
+    H.hot_slab = H.hot_n ? (uint32_t*)p->s_hslab.ensure(c, (size_t)hc_hot_counters(H.hot_n) * H.G * 4) : nullptr;
+    H.pbuf = (uint16_t*)p->s_pbuf.ensure(c, hs->pbuf_elems * 2);
+    H.trash = hs->trash;
+    H.counts = pl.g_cnt.as<unsigned long long>();
+    p->h_hcerr.ensure(8);
+    H.err = (uint32_t*)p->h_hcerr.dev();
+    p->hc_check = true;
+    H.u16_counters = hs->u16 ? 1 : 0;
+    H.overwrite = first_segment ? 1 : 0;  // every counter is stored by the counting pass: no read of the zeroed grid
+    require(hc_scatter_lds_bytes(H.P, H.hot_n) <= 160 * 1024 - 256, ESGPU_ERR_STATE, "hot/cold LDS layout");
+    HIPX(hipEventRecord(pl.e0, st));
+    launch_hotcold(H, st);
+    HIPX(hipGetLastError());
+    HIPX(hipEventRecord(pl.e1, st));
+    p->last_path = 6;
+    return true;
+}
+
 // algorithmic bytes of one referenced column over a segment: natural width per value, plus the CSR
 // offsets (8 B per doc) of a multi-valued column
 static uint64_t column_bytes(const DevColumn* c, uint32_t max_doc) {
@@ -1584,6 +1841,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     }
     // an unmapped metric field collects nothing (ValuesSource null => NO_OP collector); counts stay separate
     const int met_launch = mc ? pl.met : 0;
+    const bool first_segment = pl.fresh;
     // ---- shape the grid ----
     if (pl.fresh) {  // first segment since create / reset: the grid shape and the dictionary are taken from it
         pl.kt_lo = 0;
@@ -1785,6 +2043,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     if (!P.lds_mode && L_ORD && !L_HIST && L_met == 0 && !L_vcnt && L_ocnt == OCNT_NONE && !inner_missing &&
         (((uint64_t)pl.T + (1u << kPartShift) - 1) >> kPartShift) <= kPartMaxStaged) {
         p->last_bytes += bytes_per_doc * (uint64_t)s->max_doc + (d_accept ? ((uint64_t)s->max_doc + 7) / 8 : 0);
+        if (ESGPU_HOTCOLD && collect_hotcold(p, pl, s, oc, d_accept, P.pred, P.npred, first_segment)) return 1;
         return collect_partitioned(p, pl, s, oc, d_accept, P.pred, P.npred) ? 1 : 0;
     }
     const uint64_t span = (uint64_t)pl.interval * (uint64_t)W;
@@ -2027,6 +2286,10 @@ extern "C" int esgpu_plan_post_collection(esgpu_plan* p) {
         require(p != nullptr, ESGPU_ERR_INVALID, "null plan");
         HIPX(hipSetDevice(p->ctx->device));
         bsync(p);
+        if (p->hc_check) {  // a partition overran the capacity the segment statistics promised (a bug, never data)
+            p->hc_check = false;
+            require(*p->h_hcerr.as<volatile uint32_t>() == 0, ESGPU_ERR_DEVICE, "hot/cold counting: partition capacity exceeded");
+        }
         for (Pipeline& pl : p->pipes) {
             if (pl.kind != 1 || !pl.allocated) continue;
             // [0] = distinct encoded hashes inserted (LC pass), [1] = non-zero registers (register pass)

@@ -1,0 +1,118 @@
+"""GPU parity of the hot/cold partitioned terms counting (esgpu_hotcold.hip) against the oracle.
+
+valueCount > 65536 ordinals takes the high-cardinality path (GlobalOrdinalsStringTermsAggregator.java:107-135 with a
+LongArray of valueCount counters): the segment's statistics (hot set, partition capacities) are built on the first
+request and reused.  Each case stresses one part of that design: ordinals clustered by doc id (every workgroup's
+share of a partition is far from its static region: overflow chunks), a flat distribution (no hot table), a cold
+ordinal with more than 65535 docs (32-bit counters in the counting pass), filters and accept bitsets (requests that
+use a fraction of the capacities), several segments into one plan, and reuse of the statistics across requests.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from elasticsearch_amd import AggregationBuilders as AB
+from elasticsearch_amd import Order, QueryBuilders as QB
+from elasticsearch_amd import _native as N
+from elasticsearch_amd import reduce
+from helpers import assert_same, bits_from_mask
+
+pytestmark = pytest.mark.gpu
+
+def _cols(ords, T, rng):
+    n = len(ords)
+    return {"kw": {"type": N.COL_ORD_U32, "values": ords.astype(np.uint32), "terms": ["u%07d" % i for i in range(T)]},
+            "status": {"type": N.COL_I64, "values": rng.integers(0, 4, size=n).astype(np.int64)}}
+
+
+def _check(engine, cols, n, aggs, filters=None, accept=None, reps=1):
+    want = O.run([(cols, n)], aggs, filters=filters, accept=[accept] if accept is not None else None)
+    seg = engine.upload_segment(cols, n)
+    plan = engine.plan(aggs, filters=filters)
+    for rep in range(reps):  # the second request reuses the segment statistics built by the first
+        plan.collect(seg, accept_bits=accept)
+        _, _, path = plan.last_collect_stats()
+        assert path == 6, path
+        res = plan.build()
+        assert_same(res.to_dict(), want["shards"][0], f"shard rep{rep}")
+        assert_same(reduce([res]).to_dict(), want["reduced"], f"reduced rep{rep}")
+        plan.reset()
+    plan.close()
+    seg.close()
+
+
+def test_zipf_terms_orders_reused_stats(engine):
+    """Zipf(1.1) over 300,000 ordinals (hot table on), every terms order, two requests over one segment."""
+    rng = np.random.default_rng(101)
+    n, T = 2_000_000, 300_000
+    ranks = np.minimum(rng.zipf(1.1, size=n) - 1, T - 1)
+    ords = (ranks * 7919 + 17) % T
+    ords[rng.random(n) < 0.02] = 0xFFFFFFFF
+    cols = _cols(ords, T, rng)
+    aggs = [AB.terms("c").field("kw").size(20),
+            AB.terms("a").field("kw").size(9).order(Order.count(True)),
+            AB.terms("t").field("kw").size(11).order(Order.term(False)).minDocCount(0)]
+    _check(engine, cols, n, aggs, reps=2)
+
+
+def test_clustered_ordinals_overflow(engine):
+    """Ordinals sorted by doc id: each partition's docs sit in a few workgroups' ranges, so almost every append goes
+    through overflow chunks; a term range filter keeps about half of them."""
+    rng = np.random.default_rng(102)
+    n, T = 3_000_000, 250_000
+    ords = np.sort(rng.integers(0, T, size=n))
+    ords[rng.random(n) < 0.01] = 0xFFFFFFFF
+    cols = _cols(ords, T, rng)
+    aggs = [AB.terms("c").field("kw").size(30), AB.terms("t").field("kw").size(5).order(Order.term(True))]
+    _check(engine, cols, n, aggs)
+    _check(engine, cols, n, aggs, filters=[QB.rangeQuery("status").gte(2)])
+
+
+def test_flat_distribution_accept_bits(engine):
+    """Uniform over 200,000 ordinals with an accept bitset (the top 16,384 hold ~15 % of the docs: a hot set)."""
+    rng = np.random.default_rng(103)
+    n, T = 1_500_000, 200_000
+    ords = rng.integers(0, T, size=n)
+    cols = _cols(ords, T, rng)
+    accept = rng.random(n) < 0.7
+    _check(engine, cols, n, [AB.terms("c").field("kw").size(40)], accept=bits_from_mask(accept))
+
+
+def test_cold_ordinal_over_16_bits(engine):
+    """4M ordinals, one doc each on average, plus one ordinal with 70,000 docs: the 16,384 most frequent hold under
+    5 % of the docs, so there is no hot set and the heavy ordinal is cold -- the counting pass keeps 32-bit counters and
+    splits the heavy partition over several workgroups."""
+    rng = np.random.default_rng(104)
+    T = 4_000_000
+    n = 4_000_000
+    ords = rng.integers(0, T, size=n)
+    ords[rng.choice(n, size=70_000, replace=False)] = 777
+    cols = _cols(ords, T, rng)
+    _check(engine, cols, n, [AB.terms("c").field("kw").size(10)], filters=[QB.rangeQuery("status").lte(2)])
+
+
+def test_two_segments_one_plan(engine):
+    """Two segments with their own statistics counted into one plan (same dictionary, no ordinal map)."""
+    rng = np.random.default_rng(105)
+    T = 180_000
+    sizes = [700_001, 1_100_000]
+    parts = []
+    for k, n in enumerate(sizes):
+        ranks = np.minimum(rng.zipf(1.05 + 0.2 * k, size=n) - 1, T - 1)
+        parts.append(((ranks * 104729 + 11 * k) % T).astype(np.uint32))
+    cols = [_cols(o, T, rng) for o in parts]
+    allc = {"kw": dict(cols[0]["kw"], values=np.concatenate(parts)),
+            "status": {"type": N.COL_I64, "values": np.concatenate([c["status"]["values"] for c in cols])}}
+    aggs = [AB.terms("c").field("kw").size(25), AB.terms("t").field("kw").size(6).order(Order.term(False))]
+    flt = [QB.rangeQuery("status").gte(1)]
+    want = O.run([(allc, sum(sizes))], aggs, filters=flt)
+    segs = [engine.upload_segment(c, n) for c, n in zip(cols, sizes)]
+    plan = engine.plan(aggs, filters=flt)
+    for s in segs:
+        plan.collect(s)
+        assert plan.last_collect_stats()[2] == 6
+    res = plan.build()
+    assert_same(res.to_dict(), want["shards"][0], "shard")
+    plan.close()
+    for s in segs:
+        s.close()
