@@ -29,6 +29,7 @@ AGG_SUM, AGG_MIN, AGG_MAX, AGG_VALUE_COUNT, AGG_FILTER = 8, 9, 10, 11, 12
 ORDER_COUNT_DESC, ORDER_COUNT_ASC, ORDER_TERM_ASC, ORDER_TERM_DESC = 0, 1, 2, 3
 ORDER_KEY_ASC, ORDER_KEY_DESC, ORDER_HCOUNT_ASC, ORDER_HCOUNT_DESC = 4, 5, 6, 7
 ORDER_AGG_ASC, ORDER_AGG_DESC = 8, 9
+FORMAT_RAW, FORMAT_DATE_TIME, FORMAT_NUMBER = 0, 1, 2
 UNIT_NONE, UNIT_WEEK, UNIT_YEAR, UNIT_QUARTER, UNIT_MONTH, UNIT_DAY, UNIT_HOUR, UNIT_MINUTE, UNIT_SECOND = range(9)
 FILTER_TERM, FILTER_RANGE = 1, 2
 COMM_ID_BYTES = 128
@@ -55,6 +56,8 @@ class AggSpec(ctypes.Structure):
         ("sigma", ctypes.c_double), ("precision_threshold", ctypes.c_int64),
         ("tz_starts", ctypes.POINTER(ctypes.c_int64)), ("tz_offsets_ms", ctypes.POINTER(ctypes.c_int64)),
         ("tz_count", ctypes.c_int32), ("reserved_tz", ctypes.c_int32), ("order_path", ctypes.c_char_p),
+        ("time_zone", ctypes.c_char_p), ("value_format", ctypes.c_int32), ("reserved_fmt", ctypes.c_int32),
+        ("format", ctypes.c_char_p),
     ]
 
 
@@ -93,6 +96,7 @@ AggBlock._fields_ = [
     ("registers", ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8))),
     ("lc_hashes", ctypes.POINTER(ctypes.POINTER(ctypes.c_uint32))), ("lc_sizes", ctypes.POINTER(_I64)),
     ("order_path", ctypes.c_char_p),
+    ("time_zone", ctypes.c_char_p), ("value_format", _I32), ("reserved_fmt", _I32), ("format", ctypes.c_char_p),
 ]
 
 
@@ -165,6 +169,7 @@ SIGNATURES = [
                                             ctypes.POINTER(ctypes.c_size_t)]),
     ("esgpu_result_to_xcontent", ctypes.c_int, [ctypes.POINTER(Result), ctypes.c_char_p, ctypes.c_size_t,
                                                 ctypes.POINTER(ctypes.c_size_t)]),
+    ("esgpu_result_to_stream", ctypes.c_int, [ctypes.POINTER(Result), _VP, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
     ("esgpu_result_serialize", ctypes.c_int, [ctypes.POINTER(Result), _VP, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
     ("esgpu_result_deserialize", ctypes.c_int, [_VP, ctypes.c_size_t, ctypes.POINTER(ctypes.POINTER(Result))]),
     ("esgpu_comm_unique_id", ctypes.c_int, [_VP]),

@@ -149,10 +149,17 @@ class _Builder:
     def __init__(self, name):
         self.name = name
         self._field = None
+        self._format = None
         self.subs = []
 
     def field(self, f):
         self._field = f
+        return self
+
+    def format(self, pattern):
+        """the request's "format" (ValuesSourceParser formattable aggregations): a date pattern on a date field, a
+        DecimalFormat pattern on a numeric one"""
+        self._format = pattern
         return self
 
     def subAggregation(self, sub):  # noqa: N802 - mirrors the Java API
@@ -399,6 +406,35 @@ def _rounding_params(b):
     return N.UNIT_NONE, parse_time_value(b._interval), off, zone
 
 
+# The index mapping behind the synthetic log documents: "@timestamp" is a date field with the
+# default date format; every other numeric field is a long / double / murmur3 (NumberFieldType).  A JNI caller reads
+# both from the field's MappedFieldType instead.
+DATE_FIELDS = {"@timestamp": "strict_date_optional_time||epoch_millis"}  # DateFieldMapper.Defaults.DATE_TIME_FORMATTER
+
+
+def time_zone_id(tz):
+    """DateTimeZone.forID(tz).getID(): "UTC" for a zero offset, "+hh:mm" / "-hh:mm" for a fixed one, a region id as
+    given.  None = UTC (ValuesSourceParser's default)."""
+    if tz is None:
+        return "UTC"
+    off = parse_time_zone(tz)
+    if isinstance(off, tuple):
+        return str(tz)
+    if off == 0:
+        return "UTC"
+    a = abs(off)
+    return "%s%02d:%02d" % ("-" if off < 0 else "+", a // 3600000, a // 60000 % 60)
+
+
+def _value_format(b):
+    """ValuesSourceParser.resolveFormat (ValuesSourceParser.java:244-257): (ESGPU_FORMAT_*, pattern)"""
+    if b._field in DATE_FIELDS:
+        return N.FORMAT_DATE_TIME, b._format or DATE_FIELDS[b._field]
+    if b._format is not None:
+        return N.FORMAT_NUMBER, b._format
+    return N.FORMAT_RAW, None
+
+
 def _round_bound(spec, v):
     """ExtendedBounds.round: the bound is rounded with the aggregation's own Rounding (esgpu_date_rounding)."""
     if v is None:
@@ -433,6 +469,12 @@ def flatten(aggs, number_of_shards=1):
         sp.field = enc(b._field)
         sp.sigma = 2.0
         sp.precision_threshold = -1
+        if b.type != N.AGG_FILTER:
+            fmt, pattern = _value_format(b)
+            sp.value_format = fmt
+            sp.format = enc(pattern)
+            # the request time zone reaches the formatter through ValuesSourceParser.Input.timezone: date_histogram only
+            sp.time_zone = enc(time_zone_id(b._tz) if b.type == N.AGG_DATE_HISTOGRAM else "UTC")
         if b.type == N.AGG_TERMS:
             code, path = order_code(b._order)
             size, ssize, mn, smn = thresholds(b._size, b._shard_size, b._min, b._shard_min, code, number_of_shards)

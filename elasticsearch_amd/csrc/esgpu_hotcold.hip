@@ -80,6 +80,9 @@ __global__ void hc_init_kernel(HcParams P) {
 #ifndef ESGPU_HC_NT
 #define ESGPU_HC_NT 1
 #endif
+#ifndef ESGPU_HC_MERGE  // 1: tiles without bursts decide and write their flushes in one pass (two barriers per tile)
+#define ESGPU_HC_MERGE 1
+#endif
 #ifndef ESGPU_HC_EXP  // timing experiments only: 1 = classify alone (steps 2-5 and the flush skipped), 2 = loads alone
 #define ESGPU_HC_EXP 0
 #endif
@@ -218,6 +221,26 @@ __global__ __launch_bounds__(kHcWG) void hc_scatter_kernel(HcParams P) {
 #if ESGPU_HC_EXP == 1
         return;
 #endif
+#if ESGPU_HC_MERGE
+        if (!any_burst) {  // (uniform) 2 + 4 in one pass: the partition's owner thread flushes its whole segments itself
+            for (uint32_t p = threadIdx.x; p < P.P; p += kHcWG) {
+                const uint32_t wd = word[p], C = wd & kCnt, rb = wd >> 26;
+                const uint32_t L = C & ~(kSeg - 1);
+                if (!L) continue;
+                const uint3 d = reserve(p, L);
+                word[p] = (((rb + L) & (kRing - 1)) << 26) | (C - L);
+                for (uint32_t i0 = 0; i0 < L; i0 += kSeg) {  // L <= kRing without bursts
+                    const uint32_t half = (rb + i0) & (kRing - 1);
+                    uint16_t* dst = P.pbuf + (i0 < d.x ? d.y + i0 : d.z + i0);
+#pragma unroll
+                    for (uint32_t qt = 0; qt < 4; ++qt)
+                        reinterpret_cast<uint4*>(dst)[qt] = *reinterpret_cast<const uint4*>(ring + ring_idx(p, half + qt * 8));
+                }
+            }
+            __syncthreads();  // the next tile's classify reuses the flushed ring halves
+            return;
+        }
+#endif
         // 2. per partition: whole segments to flush (L), their destination, the ring state after the flush
         for (uint32_t p = threadIdx.x; p < P.P; p += kHcWG) {
             const uint32_t wd = word[p], C = wd & kCnt, rb = wd >> 26;
@@ -281,7 +304,10 @@ __global__ __launch_bounds__(kHcWG) void hc_scatter_kernel(HcParams P) {
     const uint32_t span = b_end > b_begin ? (b_end - b_begin) * kBlockDocs : 0u;
     if (span) {
         uint32_t A[kHcIt][4], B[kHcIt][4];
+        // A's loads must issue before B's, as they do on the loop's back edge: the wait counts at the loop head are
+        // merged over both paths, and with B issued first the head waited vmcnt(0), draining the prefetch every tile
         load(d_begin, A);
+        __builtin_amdgcn_sched_barrier(0);
         load(d_begin + kHcTileDocs, B);
         for (uint32_t t0 = d_begin; t0 < d_begin + span; t0 += 2 * kHcTileDocs) {
             process(t0, A);

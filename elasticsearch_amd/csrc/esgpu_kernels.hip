@@ -295,6 +295,9 @@ __global__ __launch_bounds__(kHllWG) void hll_registers_fast_kernel(HllParams P,
 // prefetch).  Nibble writes are plain read-modify-writes of a byte: a lost update leaves an older nibble, which is
 // still a lower bound (registers only grow, and every nibble written came with an atomicMax of at least its value).
 constexpr uint32_t kHllLdsWG = 1024;
+#ifndef ESGPU_HLL_NBUF
+#define ESGPU_HLL_NBUF 2  // load buffers in flight per thread (2 or 3)
+#endif
 constexpr uint32_t kHllLdsIter = kHllLdsWG * 4;
 #ifndef ESGPU_HLL_BITS
 #define ESGPU_HLL_BITS 4
@@ -345,16 +348,32 @@ __global__ __launch_bounds__(kHllLdsWG) void hll_registers_lds_kernel(HllParams 
             }
         }
     };
-    // two buffers, each reloaded right after it is hashed: no register copies (which would wait for the loads)
+    // ESGPU_HLL_NBUF buffers, each reloaded right after it is hashed: no register copies (which would wait for the
+    // loads); the prologue issues them in the loop's order (the loop head's wait counts merge both paths)
     uint64_t a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
     load(w0 + t4, a);
+    __builtin_amdgcn_sched_barrier(0);
     load(w0 + kHllLdsIter + t4, b);
+#if ESGPU_HLL_NBUF == 3
+    uint64_t c[4] = {0, 0, 0, 0};
+    __builtin_amdgcn_sched_barrier(0);
+    load(w0 + 2 * kHllLdsIter + t4, c);
+    for (uint32_t base = w0; base < w1; base += 3 * kHllLdsIter) {
+        hash4(base + t4, a);
+        load(base + 3 * kHllLdsIter + t4, a);
+        hash4(base + kHllLdsIter + t4, b);
+        load(base + 4 * kHllLdsIter + t4, b);
+        hash4(base + 2 * kHllLdsIter + t4, c);
+        load(base + 5 * kHllLdsIter + t4, c);
+    }
+#else
     for (uint32_t base = w0; base < w1; base += 2 * kHllLdsIter) {
         hash4(base + t4, a);
         load(base + 2 * kHllLdsIter + t4, a);
         hash4(base + kHllLdsIter + t4, b);
         load(base + 3 * kHllLdsIter + t4, b);
     }
+#endif
 }
 
 // packed 4-bit lower bounds of the registers relative to the floor: nibble = min(reg - floor, 15)

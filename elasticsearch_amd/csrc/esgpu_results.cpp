@@ -232,6 +232,7 @@ Block Block::like() const {
     b.tz_starts = tz_starts; b.tz_offs = tz_offs;
     b.has_bmin = has_bmin; b.has_bmax = has_bmax; b.bmin = bmin; b.bmax = bmax;
     b.sigma = sigma; b.precision = precision; b.order_path = order_path;
+    b.time_zone = time_zone; b.value_format = value_format; b.format = format;
     b.n = 0;
     if (is_bucket()) {
         b.boff.assign(1, 0);
@@ -1116,6 +1117,253 @@ std::string to_xcontent(const std::vector<Block>& aggs) {
 }
 
 // ------------------------------------------------------------------------------------------------------------
+// Elasticsearch's transport bytes: InternalAggregations.writeTo(StreamOutput) (A/InternalAggregations.java:215-222)
+// ------------------------------------------------------------------------------------------------------------
+namespace {
+struct JavaOut {  // org.elasticsearch.common.io.stream.StreamOutput encodings (C/common/io/stream/StreamOutput.java)
+    std::string& o;
+    void byte(uint8_t b) { o.push_back((char)b); }
+    void boolean(bool b) { byte(b ? 1 : 0); }                        // :263-265
+    void vint(int32_t i) {                                           // :157-163 (i >>>= 7)
+        uint32_t u = (uint32_t)i;
+        while (u & ~0x7Fu) { byte((uint8_t)((u & 0x7F) | 0x80)); u >>= 7; }
+        byte((uint8_t)u);
+    }
+    void vlong(int64_t i) {                                          // :178-185
+        uint64_t u = (uint64_t)i;
+        while (u & ~0x7Full) { byte((uint8_t)((u & 0x7F) | 0x80)); u >>= 7; }
+        byte((uint8_t)u);
+    }
+    void i32(int32_t i) { for (int s = 24; s >= 0; s -= 8) byte((uint8_t)((uint32_t)i >> s)); }  // :144-149
+    void i64(int64_t i) { i32((int32_t)(i >> 32)); i32((int32_t)i); }                           // :168-171
+    void f64(double v) {                                             // :251-253, Double.doubleToLongBits
+        uint64_t b;
+        std::memcpy(&b, &v, 8);
+        if (v != v) b = 0x7ff8000000000000ULL;
+        i64((int64_t)b);
+    }
+    void bytes_ref(const char* p, size_t n) { vint((int32_t)n); o.append(p, n); }  // writeBytesRef / writeBytesReference
+    // writeString (:228-245): the String's UTF-16 code units, each in 1-3 bytes (modified UTF-8; surrogates separately)
+    void str(const std::string& utf8) {
+        std::vector<uint16_t> u;
+        for (size_t i = 0; i < utf8.size();) {
+            const uint8_t c = (uint8_t)utf8[i];
+            uint32_t cp = c, len = 1;
+            if (c >= 0xF0) { cp = c & 0x07; len = 4; }
+            else if (c >= 0xE0) { cp = c & 0x0F; len = 3; }
+            else if (c >= 0xC0) { cp = c & 0x1F; len = 2; }
+            if (i + len > utf8.size()) { len = 1; cp = c; }
+            for (uint32_t k = 1; k < len; ++k) cp = (cp << 6) | ((uint8_t)utf8[i + k] & 0x3F);
+            i += len;
+            if (cp >= 0x10000) {
+                cp -= 0x10000;
+                u.push_back((uint16_t)(0xD800 + (cp >> 10)));
+                u.push_back((uint16_t)(0xDC00 + (cp & 0x3FF)));
+            } else {
+                u.push_back((uint16_t)cp);
+            }
+        }
+        vint((int32_t)u.size());
+        for (uint16_t c : u) {
+            if (c <= 0x007F) byte((uint8_t)c);
+            else if (c > 0x07FF) { byte((uint8_t)(0xE0 | ((c >> 12) & 0x0F))); byte((uint8_t)(0x80 | ((c >> 6) & 0x3F))); byte((uint8_t)(0x80 | (c & 0x3F))); }
+            else { byte((uint8_t)(0xC0 | ((c >> 6) & 0x1F))); byte((uint8_t)(0x80 | (c & 0x3F))); }
+        }
+    }
+    void size(int32_t s) { vint(s == INT32_MAX ? 0 : s); }  // InternalAggregation.writeSize (A/InternalAggregation.java:181-186)
+};
+
+const char* stream_type(int32_t type) {  // InternalAggregation.Type stream names (each class's TYPE)
+    switch (type) {
+        case ESGPU_AGG_TERMS: return "sterms";               // StringTerms.java:43
+        case ESGPU_AGG_HISTOGRAM: return "histo";            // InternalHistogram.java:55
+        case ESGPU_AGG_DATE_HISTOGRAM: return "dhisto";      // InternalDateHistogram.java:33
+        case ESGPU_AGG_STATS: return "stats";                // InternalStats.java:41
+        case ESGPU_AGG_EXTENDED_STATS: return "estats";      // InternalExtendedStats.java:41
+        case ESGPU_AGG_AVG: return "avg";                    // InternalAvg.java:40
+        case ESGPU_AGG_CARDINALITY: return "cardinality";    // InternalCardinality.java:39
+        case ESGPU_AGG_FILTER: return "filter";              // InternalFilter.java:36
+    }
+    throw std::invalid_argument("aggregation type without a stream");
+}
+
+// ValueFormatterStreams.writeOptional (A/support/format/ValueFormatterStreams.java:54-64) of the field's formatter;
+// ValuesSourceParser.resolveFormat never leaves it null for a field (RAW at worst, ValuesSourceParser.java:233-257)
+void write_formatter(JavaOut& w, const Block& a) {
+    w.boolean(true);
+    switch (a.value_format) {
+        case ESGPU_FORMAT_DATE_TIME: w.byte(2); w.str(a.format); w.str(a.time_zone); break;  // ValueFormatter.java:155-158
+        case ESGPU_FORMAT_NUMBER: w.byte(4); w.str(a.format); break;                       // ValueFormatter.java:208-211
+        default: w.byte(1); break;                                                         // Raw: no payload (:93-94)
+    }
+}
+
+// Rounding.Streams.write (C/common/rounding/Rounding.java:229-234) of the histogram's rounding:
+// HistogramParser.java:128-131 (Interval, OffsetRounding) and TimeZoneRounding.Builder.build (TimeZoneRounding.java:84-98)
+void write_rounding(JavaOut& w, const Block& a) {
+    if (a.offset != 0) { w.byte(8); }  // OffsetRounding: the wrapped rounding, then the offset (Rounding.java:223-226)
+    if (a.type == ESGPU_AGG_HISTOGRAM) {
+        w.byte(0);                     // Rounding.Interval (:126-128)
+        w.vlong(a.interval);
+    } else if (a.date_unit != ESGPU_UNIT_NONE) {
+        w.byte(1);                     // TimeUnitRounding: DateTimeUnit id (DateTimeUnit.java:30-37) + zone id (:156-159)
+        w.byte((uint8_t)a.date_unit);
+        w.str(a.time_zone);
+    } else {
+        w.byte(2);                     // TimeIntervalRounding: vLong interval + zone id (:213-216)
+        w.vlong(a.interval);
+        w.str(a.time_zone);
+    }
+    if (a.offset != 0) w.i64(a.offset);
+}
+
+// InternalOrder.Streams.writeOrder (A/bucket/terms/InternalOrder.java:289-306) of the order TermsParser builds: a single
+// term order as itself, every other order as CompoundOrder(order, _term asc) (TermsParser.java:57-67, :233-241)
+void write_terms_order(JavaOut& w, const Block& a) {
+    switch (a.order) {
+        case ESGPU_ORDER_TERM_ASC: w.byte(4); return;
+        case ESGPU_ORDER_TERM_DESC: w.byte(3); return;
+    }
+    w.byte(0xFF);  // CompoundOrder.ID = -1
+    w.vint(2);
+    switch (a.order) {
+        case ESGPU_ORDER_COUNT_DESC: w.byte(1); break;
+        case ESGPU_ORDER_COUNT_ASC: w.byte(2); break;
+        case ESGPU_ORDER_AGG_ASC:
+        case ESGPU_ORDER_AGG_DESC:  // InternalOrder.Aggregation: id 0, asc, AggregationPath.toString
+            w.byte(0);
+            w.boolean(a.order == ESGPU_ORDER_AGG_ASC);
+            w.str(a.order_path);
+            break;
+        default: throw std::invalid_argument("unknown terms order");
+    }
+    w.byte(4);  // _term asc tie-break
+}
+
+uint8_t hist_order_id(int32_t order) {  // Histogram.Order ids (A/bucket/histogram/Histogram.java:51-77)
+    switch (order) {
+        case ESGPU_ORDER_KEY_ASC: return 1;
+        case ESGPU_ORDER_KEY_DESC: return 2;
+        case ESGPU_ORDER_HCOUNT_ASC: return 3;
+        case ESGPU_ORDER_HCOUNT_DESC: return 4;
+    }
+    throw std::invalid_argument("unknown histogram order");
+}
+
+void es_list(JavaOut& w, const std::vector<Block>& l, uint64_t i);
+
+// InternalAggregation.writeTo (A/InternalAggregation.java:212-221) of instance i, then the class's doWriteTo
+void es_instance(JavaOut& w, const Block& a, uint64_t i) {
+    w.str(a.name);
+    w.byte(0xFF);  // writeGenericValue(null metaData)
+    w.vint(0);     // no pipeline aggregators
+    switch (a.type) {
+        case ESGPU_AGG_TERMS: {  // StringTerms.doWriteTo (:205-217), Bucket.writeTo (:128-136)
+            w.i64(a.doc_count_error[i]);
+            write_terms_order(w, a);
+            w.size(a.required_size);
+            w.size(a.shard_size);
+            w.boolean(a.show_err != 0);
+            w.vlong(a.min_doc_count);
+            w.vlong(a.other_doc_count[i]);
+            const uint64_t b0 = a.boff[i], b1 = a.boff[i + 1];
+            w.vint((int32_t)(b1 - b0));
+            for (uint64_t b = b0; b < b1; ++b) {
+                w.bytes_ref(a.term_pool.data() + a.term_off[b], a.term_off[b + 1] - a.term_off[b]);
+                w.vlong(a.bcount[b]);
+                if (a.show_err) w.i64(a.berr[b]);
+                es_list(w, a.subs, b);
+            }
+            break;
+        }
+        case ESGPU_AGG_HISTOGRAM:
+        case ESGPU_AGG_DATE_HISTOGRAM: {  // InternalHistogram.doWriteTo (:510-523), Bucket.writeTo (:183-187)
+            w.str(a.type == ESGPU_AGG_DATE_HISTOGRAM ? "date_histogram" : "histogram");  // factory.type()
+            w.byte(hist_order_id(a.order));
+            w.vlong(a.min_doc_count);
+            if (a.min_doc_count == 0) {  // EmptyBucketInfo.writeTo (:223-230)
+                write_rounding(w, a);
+                es_list(w, a.empty_subs, 0);
+                const bool bounds = a.has_bmin || a.has_bmax;
+                w.boolean(bounds);
+                if (bounds) {  // ExtendedBounds.writeTo (A/bucket/histogram/ExtendedBounds.java:67-80)
+                    w.boolean(a.has_bmin);
+                    if (a.has_bmin) w.i64(a.bmin);
+                    w.boolean(a.has_bmax);
+                    if (a.has_bmax) w.i64(a.bmax);
+                }
+            }
+            write_formatter(w, a);
+            w.boolean(a.keyed != 0);
+            const uint64_t b0 = a.boff[i], b1 = a.boff[i + 1];
+            w.vint((int32_t)(b1 - b0));
+            for (uint64_t b = b0; b < b1; ++b) {
+                w.i64(a.key[b]);
+                w.vlong(a.bcount[b]);
+                es_list(w, a.subs, b);
+            }
+            break;
+        }
+        case ESGPU_AGG_STATS:
+        case ESGPU_AGG_EXTENDED_STATS:  // InternalStats.doWriteTo (:182-189) + InternalExtendedStats.writeOtherStatsTo (:169-174)
+            write_formatter(w, a);
+            w.vlong(a.count[i]);
+            w.f64(a.min[i]);
+            w.f64(a.max[i]);
+            w.f64(a.sum[i]);
+            if (a.type == ESGPU_AGG_EXTENDED_STATS) {
+                w.f64(a.sumsq[i]);
+                w.f64(a.sigma);
+            }
+            break;
+        case ESGPU_AGG_AVG:  // InternalAvg.doWriteTo (:102-106)
+            write_formatter(w, a);
+            w.f64(a.sum[i]);
+            w.vlong(a.count[i]);
+            break;
+        case ESGPU_AGG_CARDINALITY:  // InternalCardinality.doWriteTo (:92-100), HyperLogLogPlusPlus.writeTo (:519-535)
+            write_formatter(w, a);
+            w.boolean(a.hll_present[i] != 0);
+            if (a.hll_present[i]) {
+                w.vint(a.precision);
+                if (a.hll_mode[i] == 0) {  // LINEAR_COUNTING = false
+                    w.boolean(false);
+                    w.vlong((int64_t)a.lc[i].size());
+                    for (uint32_t e : a.lc[i]) w.i32((int32_t)e);
+                } else {
+                    w.boolean(true);
+                    const std::vector<uint8_t>& r = a.regs[i];
+                    if (r.size() != ((size_t)1 << a.precision)) throw std::runtime_error("register array size");
+                    w.o.append((const char*)r.data(), r.size());
+                }
+            }
+            break;
+        case ESGPU_AGG_FILTER:  // InternalSingleBucketAggregation.doWriteTo (:124-127)
+            w.vlong(a.count[i]);
+            es_list(w, a.subs, i);
+            break;
+        default: throw std::invalid_argument("aggregation type without a stream");
+    }
+}
+
+// InternalAggregations.writeTo: count, then per aggregation its stream type and writeTo
+void es_list(JavaOut& w, const std::vector<Block>& l, uint64_t i) {
+    w.vint((int32_t)l.size());
+    for (const Block& a : l) {
+        const char* t = stream_type(a.type);
+        w.bytes_ref(t, std::strlen(t));
+        es_instance(w, a, i);
+    }
+}
+}  // namespace
+
+void to_es_stream(const std::vector<Block>& aggs, std::string& out) {
+    out.clear();
+    JavaOut w{out};
+    es_list(w, aggs, 0);
+}
+
+// ------------------------------------------------------------------------------------------------------------
 // stream format (AggregationStreams analogue): little-endian, versioned, one record per block
 // ------------------------------------------------------------------------------------------------------------
 namespace {
@@ -1160,7 +1408,8 @@ void w_block(W& w, const Block& a) {
     w.pod<uint8_t>(a.has_empty_info); w.pod(a.date_unit); w.pod(a.interval); w.pod(a.offset);
     w.vec(a.tz_starts); w.vec(a.tz_offs);
     w.pod<uint8_t>(a.has_bmin); w.pod<uint8_t>(a.has_bmax); w.pod(a.bmin); w.pod(a.bmax);
-    w.pod(a.sigma); w.pod(a.precision); w.str(a.order_path); w.pod(a.n);
+    w.pod(a.sigma); w.pod(a.precision); w.str(a.order_path);
+    w.str(a.time_zone); w.pod(a.value_format); w.str(a.format); w.pod(a.n);
     w.vec(a.doc_count_error); w.vec(a.other_doc_count); w.vec(a.boff); w.vec(a.key); w.vec(a.term_off);
     w.str(a.term_pool); w.vec(a.bcount); w.vec(a.berr);
     w_blocks(w, a.subs);
@@ -1187,7 +1436,8 @@ void r_block(R& r, Block& a, int depth) {
     r.vec(a.tz_starts); r.vec(a.tz_offs);
     if (a.tz_starts.size() != a.tz_offs.size()) throw std::runtime_error("bad time zone table");
     a.has_bmin = r.pod<uint8_t>(); a.has_bmax = r.pod<uint8_t>(); a.bmin = r.pod<int64_t>(); a.bmax = r.pod<int64_t>();
-    a.sigma = r.pod<double>(); a.precision = r.pod<int32_t>(); a.order_path = r.str(); a.n = r.pod<uint64_t>();
+    a.sigma = r.pod<double>(); a.precision = r.pod<int32_t>(); a.order_path = r.str();
+    a.time_zone = r.str(); a.value_format = r.pod<int32_t>(); a.format = r.str(); a.n = r.pod<uint64_t>();
     r.vec(a.doc_count_error); r.vec(a.other_doc_count); r.vec(a.boff); r.vec(a.key); r.vec(a.term_off);
     a.term_pool = r.str(); r.vec(a.bcount); r.vec(a.berr);
     r_blocks(r, a.subs, depth + 1);
@@ -1243,7 +1493,7 @@ void r_blocks(R& r, std::vector<Block>& l, int depth) {
     for (Block& a : l) r_block(r, a, depth);
 }
 const uint32_t kStreamMagic = 0x45534750;  // "ESGP"
-const uint32_t kStreamVersion = 4;
+const uint32_t kStreamVersion = 5;
 }  // namespace
 
 void serialize(const std::vector<Block>& aggs, std::string& out) {
@@ -1294,6 +1544,9 @@ void export_block(ResultHolder& h, const Block& a, esgpu_agg_block& o) {
     o.sigma = a.sigma;
     o.precision = a.precision;
     o.order_path = a.order_path.c_str();
+    o.time_zone = a.time_zone.c_str();
+    o.value_format = a.value_format;
+    o.format = a.format.c_str();
     o.nsubs = (int32_t)a.subs.size();
     o.n_instances = a.n;
     o.doc_count_error = ptr(a.doc_count_error);

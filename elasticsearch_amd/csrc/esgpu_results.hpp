@@ -39,6 +39,9 @@ struct Block {
     double sigma = 2.0;
     int32_t precision = 14;
     std::string order_path;  // terms ordered by a metric sub-aggregation (ESGPU_ORDER_AGG_*)
+    std::string time_zone = "UTC";  // request time zone id (wire stream: TimeZoneRounding, ValueFormatter.DateTime)
+    int32_t value_format = 0;       // ESGPU_FORMAT_* of the field (ValuesSourceParser.resolveFormat)
+    std::string format;             // its pattern
 
     uint64_t n = 0;  // instances
 
@@ -132,6 +135,8 @@ std::string to_json(const std::vector<Block>& aggs);
 // the aggregations object of an Elasticsearch search response, byte for byte as its XContent renders it
 std::string to_xcontent(const std::vector<Block>& aggs);
 void serialize(const std::vector<Block>& aggs, std::string& out);
+// InternalAggregations.writeTo(StreamOutput): Elasticsearch's transport bytes of these aggregations
+void to_es_stream(const std::vector<Block>& aggs, std::string& out);
 bool deserialize(const uint8_t* p, size_t n, std::vector<Block>& out);
 
 // owning wrapper behind the public esgpu_result (pub must stay the first member)

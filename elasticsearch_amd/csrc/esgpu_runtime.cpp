@@ -750,6 +750,7 @@ struct SpecNode {
     std::vector<int> children;
     int precision = 14;
     std::vector<int64_t> tz_starts, tz_offs;  // owned copy of the spec's time zone table
+    std::string time_zone = "UTC", format;    // wire-stream parameters (esgpu_agg_spec.time_zone / format)
     Rounding rounding() const {               // histogram specs (Rounding.java / TimeZoneRounding.java)
         esgpu_agg_spec sp = s;
         sp.tz_count = (int32_t)tz_starts.size();
@@ -1059,6 +1060,15 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
             n.s.tz_starts = nullptr;
             n.s.tz_offsets_ms = nullptr;
             n.s.tz_count = 0;
+            if (specs[i].time_zone && *specs[i].time_zone) n.time_zone = specs[i].time_zone;
+            require(n.s.value_format >= ESGPU_FORMAT_RAW && n.s.value_format <= ESGPU_FORMAT_NUMBER, ESGPU_ERR_INVALID,
+                    "unknown value format");
+            if (n.s.value_format != ESGPU_FORMAT_RAW) {
+                require(specs[i].format != nullptr, ESGPU_ERR_INVALID, "value format without a pattern");
+                n.format = specs[i].format;
+            }
+            n.s.time_zone = nullptr;
+            n.s.format = nullptr;
             require(n.s.type >= ESGPU_AGG_TERMS && n.s.type <= ESGPU_AGG_FILTER, ESGPU_ERR_INVALID, "unknown aggregation type");
             if (n.s.type == ESGPU_AGG_FILTER)
                 require(n.s.parent < 0, ESGPU_ERR_UNSUPPORTED, "filter aggregation under another aggregation runs on the CPU path");
@@ -2329,11 +2339,18 @@ static std::string plan_term(const esgpu_plan*, const Pipeline& pl, uint64_t ord
 }
 
 // ---- result blocks (columnar InternalAggregations, see esgpu_results.hpp) ----
+static void set_format(Block& r, const SpecNode& n) {
+    r.time_zone = n.time_zone;
+    r.value_format = n.s.value_format;
+    r.format = n.format;
+}
+
 static Block metric_shell(const SpecNode& n) {
     Block r;
     r.type = n.s.type;
     r.name = n.name;
     r.sigma = n.s.sigma;
+    set_format(r, n);
     return r;
 }
 
@@ -2351,6 +2368,7 @@ static Block hist_shell(const esgpu_plan* p, int spec, const std::vector<Block>&
     r.offset = n.s.offset;
     r.tz_starts = n.tz_starts;
     r.tz_offs = n.tz_offs;
+    set_format(r, n);
     r.boff.assign(1, 0);
     r.term_off.assign(1, 0);
     for (const Block& b : protos) r.subs.push_back(b.like());
@@ -2947,6 +2965,7 @@ static Block build_cardinality(esgpu_plan* p, Pipeline& pl) {
     Block r;
     r.type = ESGPU_AGG_CARDINALITY;
     r.name = n.name;
+    set_format(r, n);
     r.precision = pl.p;
     r.append_empty();  // counts == null
     if (!pl.allocated || !pl.any_value) return r;
@@ -3118,6 +3137,19 @@ extern "C" int esgpu_result_to_xcontent(const esgpu_result* r, char* buf, size_t
             const size_t c = std::min(cap - 1, s.size());
             std::memcpy(buf, s.data(), c);
             buf[c] = 0;
+        }
+    });
+}
+
+extern "C" int esgpu_result_to_stream(const esgpu_result* r, uint8_t* buf, size_t cap, size_t* needed) {
+    return guarded([&] {
+        require(r != nullptr, ESGPU_ERR_INVALID, "null result");
+        std::string s;
+        to_es_stream(holder_of(r)->aggs, s);
+        if (needed) *needed = s.size();
+        if (buf) {
+            require(cap >= s.size(), ESGPU_ERR_INVALID, "buffer too small");
+            std::memcpy(buf, s.data(), s.size());
         }
     });
 }

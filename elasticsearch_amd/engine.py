@@ -59,6 +59,15 @@ class ShardResult:
     def to_dict(self):
         return json.loads(self.to_json())
 
+    def to_stream(self):
+        """the bytes InternalAggregations.writeTo(StreamOutput) sends over Elasticsearch's transport
+        (esgpu_result_to_stream)"""
+        needed = ctypes.c_size_t()
+        N.check(N.lib().esgpu_result_to_stream(self._ptr, None, 0, ctypes.byref(needed)))
+        buf = (ctypes.c_uint8 * max(needed.value, 1))()
+        N.check(N.lib().esgpu_result_to_stream(self._ptr, buf, needed.value, ctypes.byref(needed)))
+        return bytes(buf[: needed.value])
+
     def serialize(self):
         needed = ctypes.c_size_t()
         N.check(N.lib().esgpu_result_serialize(self._ptr, None, 0, ctypes.byref(needed)))

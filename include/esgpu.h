@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define ESGPU_ABI_VERSION 4
+#define ESGPU_ABI_VERSION 5
 
 /* ---------------------------------------------------------------------------------------------------------
  * Status codes.  Mapping used by the JNI shim (SURVEY §8(b) "Errors"):
@@ -254,7 +254,25 @@ typedef struct esgpu_agg_spec {
     int32_t reserved_tz;
     /* terms order ESGPU_ORDER_AGG_*: the sub-aggregation path (NUL-terminated) */
     const char* order_path;
+    /* What the shard result's wire stream (esgpu_result_to_stream) carries besides the numbers:
+     *   time_zone:    DateTimeZone.getID() of the request's time_zone ("UTC", "+01:00", "Europe/Berlin"); NULL = "UTC".
+     *                 Written by TimeZoneRounding.TimeUnitRounding/TimeIntervalRounding.writeTo (TimeZoneRounding.java:
+     *                 156-159, 213-216) and by the date formatter.
+     *   value_format: the ValueFormatter ValuesSourceParser.resolveFormat picks for the field (ValuesSourceParser.java:
+     *                 233-257): ESGPU_FORMAT_RAW (numeric field, no "format"), ESGPU_FORMAT_DATE_TIME (date field: the
+     *                 mapping's date format, or the request's "format", with the request time zone), ESGPU_FORMAT_NUMBER
+     *                 (numeric field with a "format" pattern); `format` holds the pattern. */
+    const char* time_zone;
+    int32_t value_format;
+    int32_t reserved_fmt;
+    const char* format;
 } esgpu_agg_spec;
+
+enum {
+    ESGPU_FORMAT_RAW = 0,         /* ValueFormatter.Raw, stream id 1 */
+    ESGPU_FORMAT_DATE_TIME = 1,   /* ValueFormatter.DateTime, stream id 2 (pattern, time zone id) */
+    ESGPU_FORMAT_NUMBER = 2       /* ValueFormatter.Number.Pattern, stream id 4 (pattern) */
+};
 
 /* Query filters: bool{filter:[...]} conjunction of term / range clauses. */
 enum {
@@ -395,6 +413,10 @@ struct esgpu_agg_block {
     const uint32_t* const* lc_hashes;       /* encoded hashes, ascending (hll_mode 0) */
     const int64_t* lc_sizes;
     const char* order_path;                 /* terms ordered by ESGPU_ORDER_AGG_*: the sub-aggregation path, else "" */
+    const char* time_zone;                  /* the spec's time_zone id ("UTC" when none) */
+    int32_t value_format;                   /* ESGPU_FORMAT_* */
+    int32_t reserved_fmt;
+    const char* format;                     /* pattern of DATE_TIME / NUMBER formats, else "" */
 };
 
 struct esgpu_result {
@@ -415,6 +437,19 @@ int esgpu_result_to_json(const esgpu_result* r, char* buf, size_t cap, size_t* n
  * order of each class's doXContentBody, Double.toString numbers, null metrics for empty buckets, date keys printed
  * with strict_date_optional_time in the request's time zone).  Same buffer contract as esgpu_result_to_json. */
 int esgpu_result_to_xcontent(const esgpu_result* r, char* buf, size_t cap, size_t* needed);
+/* Elasticsearch's transport wire format of a shard result: the bytes InternalAggregations.writeTo(StreamOutput) writes
+ * (InternalAggregations.java:215-222) -- per aggregation its AggregationStreams type ("sterms", "dhisto", "histo",
+ * "stats", "estats", "avg", "cardinality", "filter"), InternalAggregation.writeTo (name, null metadata, no pipeline
+ * aggregators, InternalAggregation.java:212-221) and the class's doWriteTo (StringTerms.java:205-217 + Bucket.writeTo
+ * :128-136, InternalHistogram.java:510-523 + Bucket.writeTo :183-187 + EmptyBucketInfo :223-230, InternalStats.java:
+ * 182-189, InternalExtendedStats.java:169-174, InternalAvg.java:102-106, InternalCardinality.java:92-100 +
+ * HyperLogLogPlusPlus.writeTo :519-535, InternalSingleBucketAggregation.java:124-127), with StreamOutput's encodings
+ * (vInt/vLong, big-endian long/int, writeString as Java chars in modified UTF-8, StreamOutput.java:118-270).
+ * A JNI shim hands these bytes to StreamInput and InternalAggregations.readAggregations to get the Java objects.
+ * Exception: a LINEAR_COUNTING cardinality writes its hashes in ascending order; the reference writes them in its
+ * hash-table slot order, a permutation -- readFrom re-adds them to a set, so the state read back is the same.
+ * Same buffer contract as esgpu_result_to_json. */
+int esgpu_result_to_stream(const esgpu_result* r, uint8_t* buf, size_t cap, size_t* needed);
 /* Stream (AggregationStreams writeTo / readFrom analogue) for moving shard results between processes. */
 int esgpu_result_serialize(const esgpu_result* r, uint8_t* buf, size_t cap, size_t* needed);
 int esgpu_result_deserialize(const uint8_t* buf, size_t len, esgpu_result** out);

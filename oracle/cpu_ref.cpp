@@ -566,6 +566,14 @@ struct Internal {
     std::shared_ptr<HLLPP> hll;
     // filter (InternalSingleBucketAggregation): doc_count in `count`, sub-aggregations here
     InternalList subs;
+    // the ValueFormatter of the aggregation's ValuesSourceConfig and the request time zone (wire stream only)
+    int value_format = ESGPU_FORMAT_RAW;
+    std::string format, tz_id = "UTC";
+    void set_format(const esgpu_agg_spec& sp) {
+        value_format = sp.value_format;
+        format = sp.format ? sp.format : "";
+        tz_id = sp.time_zone && *sp.time_zone ? sp.time_zone : "UTC";
+    }
 };
 
 // ---- comparators (A/bucket/terms/InternalOrder.java:47-76, CompoundOrder with _term asc tie-break) ----
@@ -844,6 +852,7 @@ struct HistogramAgg : Aggregator {
         r->type = f->spec.type;
         r->name = f->name;
         r->date = f->spec.type == ESGPU_AGG_DATE_HISTOGRAM;
+        r->set_format(f->spec);
         r->order = f->spec.order;
         r->keyed = f->spec.keyed != 0;
         r->min_doc_count = f->spec.min_doc_count;
@@ -910,6 +919,7 @@ struct StatsAgg : Aggregator {
         r->name = f->name;
         r->count = c; r->sum = s; r->min = mn; r->max = mx; r->sumsq = sq;
         r->sigma = f->spec.sigma;
+        r->set_format(f->spec);
         return r;
     }
     InternalPtr build(int64_t b) override {
@@ -1004,6 +1014,7 @@ struct CardinalityAgg : Aggregator {
         auto r = std::make_shared<Internal>();
         r->type = ESGPU_AGG_CARDINALITY;
         r->name = f->name;
+        r->set_format(f->spec);
         r->hll = std::move(h);
         return r;
     }
@@ -1420,6 +1431,192 @@ static void write_list(Json& j, const InternalList& aggs) {
 }
 
 // ------------------------------------------------------------------------------------------------------------
+// Transport bytes of a shard result: InternalAggregations.writeTo (A/InternalAggregations.java:215-222), restated
+// from each class's writeTo / doWriteTo over org.elasticsearch.common.io.stream.StreamOutput (C/common/io/stream/
+// StreamOutput.java).  The LINEAR_COUNTING hashes come out in the hash table's slot order, as HyperLogLogPlusPlus
+// .writeTo iterates hashSet.values(bucket) (HyperLogLogPlusPlus.java:519-528).
+// ------------------------------------------------------------------------------------------------------------
+struct StreamOutput {
+    std::string b;
+    void writeByte(int v) { b.push_back((char)(uint8_t)v); }
+    void writeBoolean(bool v) { writeByte(v ? 1 : 0); }
+    void writeInt(int32_t i) { writeByte(i >> 24); writeByte(i >> 16); writeByte(i >> 8); writeByte(i); }
+    void writeLong(int64_t i) { writeInt((int32_t)(i >> 32)); writeInt((int32_t)i); }
+    void writeVInt(int32_t i) {
+        while ((i & ~0x7F) != 0) { writeByte((i & 0x7F) | 0x80); i = (int32_t)((uint32_t)i >> 7); }
+        writeByte(i);
+    }
+    void writeVLong(int64_t i) {
+        while ((i & ~0x7FLL) != 0) { writeByte((int)((i & 0x7F) | 0x80)); i = (int64_t)((uint64_t)i >> 7); }
+        writeByte((int)i);
+    }
+    void writeDouble(double v) {  // Double.doubleToLongBits: NaN canonical
+        int64_t bits;
+        if (v != v) bits = 0x7ff8000000000000LL; else std::memcpy(&bits, &v, 8);
+        writeLong(bits);
+    }
+    void writeString(const std::string& utf8) {  // String.length() chars, then each char as 1-3 bytes
+        std::vector<uint32_t> chars;
+        size_t i = 0;
+        while (i < utf8.size()) {
+            uint32_t c = (uint8_t)utf8[i], n = c < 0x80 ? 1 : c < 0xE0 ? 2 : c < 0xF0 ? 3 : 4;
+            if (i + n > utf8.size()) n = 1;
+            uint32_t cp = n == 1 ? c : n == 2 ? (c & 0x1F) : n == 3 ? (c & 0x0F) : (c & 0x07);
+            for (uint32_t k = 1; k < n; ++k) cp = (cp << 6) | ((uint8_t)utf8[i + k] & 0x3F);
+            i += n;
+            if (cp > 0xFFFF) { chars.push_back(0xD800 + ((cp - 0x10000) >> 10)); chars.push_back(0xDC00 + ((cp - 0x10000) & 0x3FF)); }
+            else chars.push_back(cp);
+        }
+        writeVInt((int32_t)chars.size());
+        for (uint32_t c : chars) {
+            if (c <= 0x007F) writeByte((int)c);
+            else if (c > 0x07FF) { writeByte(0xE0 | ((c >> 12) & 0x0F)); writeByte(0x80 | ((c >> 6) & 0x3F)); writeByte(0x80 | (c & 0x3F)); }
+            else { writeByte(0xC0 | ((c >> 6) & 0x1F)); writeByte(0x80 | (c & 0x3F)); }
+        }
+    }
+    void writeBytes(const std::string& bytes) { writeVInt((int32_t)bytes.size()); b += bytes; }  // writeBytesRef / Reference
+};
+
+static void writeSize(int size, StreamOutput& out) { out.writeVInt(size == INT32_MAX ? 0 : size); }  // InternalAggregation.java:181-186
+
+static void writeFormatter(const Internal& a, StreamOutput& out) {  // ValueFormatterStreams.writeOptional / write
+    out.writeBoolean(true);  // ValuesSourceParser.resolveFormat never yields null for a field
+    if (a.value_format == ESGPU_FORMAT_DATE_TIME) { out.writeByte(2); out.writeString(a.format); out.writeString(a.tz_id); }
+    else if (a.value_format == ESGPU_FORMAT_NUMBER) { out.writeByte(4); out.writeString(a.format); }
+    else out.writeByte(1);  // ValueFormatter.Raw: writeTo writes nothing
+}
+
+static void writeRounding(const Internal& a, StreamOutput& out) {  // Rounding.Streams.write: id, then writeTo
+    const Rounding& r = a.rounding;
+    if (r.offset != 0) out.writeByte(8);  // OffsetRounding.writeTo: the inner rounding, then writeLong(offset)
+    if (r.kind == 0) { out.writeByte(0); out.writeVLong(r.interval); }                            // Rounding.Interval
+    else if (r.kind == 1) { out.writeByte(1); out.writeByte(r.unit); out.writeString(a.tz_id); }  // TimeUnitRounding
+    else { out.writeByte(2); out.writeVLong(r.interval); out.writeString(a.tz_id); }              // TimeIntervalRounding
+    if (r.offset != 0) out.writeLong(r.offset);
+}
+
+static void writeTermsOrder(const Internal& a, StreamOutput& out) {  // InternalOrder.Streams.writeOrder
+    if (a.order == ESGPU_ORDER_TERM_ASC) { out.writeByte(4); return; }   // TermsParser: a lone term order stays itself
+    if (a.order == ESGPU_ORDER_TERM_DESC) { out.writeByte(3); return; }
+    out.writeByte(-1);  // CompoundOrder(user order, _term asc)
+    out.writeVInt(2);
+    if (a.order == ESGPU_ORDER_COUNT_DESC) out.writeByte(1);
+    else if (a.order == ESGPU_ORDER_COUNT_ASC) out.writeByte(2);
+    else { out.writeByte(0); out.writeBoolean(a.order == ESGPU_ORDER_AGG_ASC); out.writeString(a.order_path); }
+    out.writeByte(4);
+}
+
+static void writeAggregations(const InternalList& aggs, StreamOutput& out);
+
+static const char* streamType(int type) {
+    switch (type) {
+        case ESGPU_AGG_TERMS: return "sterms";
+        case ESGPU_AGG_HISTOGRAM: return "histo";
+        case ESGPU_AGG_DATE_HISTOGRAM: return "dhisto";
+        case ESGPU_AGG_STATS: return "stats";
+        case ESGPU_AGG_EXTENDED_STATS: return "estats";
+        case ESGPU_AGG_AVG: return "avg";
+        case ESGPU_AGG_CARDINALITY: return "cardinality";
+        default: return "filter";
+    }
+}
+
+static void writeAggregation(const Internal& a, StreamOutput& out) {  // InternalAggregation.writeTo (:212-221)
+    out.writeString(a.name);
+    out.writeByte(-1);  // writeGenericValue(null)
+    out.writeVInt(0);   // pipelineAggregators.size()
+    switch (a.type) {
+        case ESGPU_AGG_TERMS:  // StringTerms.doWriteTo (:205-217)
+            out.writeLong(a.doc_count_error);
+            writeTermsOrder(a, out);
+            writeSize(a.required_size, out);
+            writeSize(a.shard_size, out);
+            out.writeBoolean(a.show_err);
+            out.writeVLong(a.min_doc_count);
+            out.writeVLong(a.other_doc_count);
+            out.writeVInt((int32_t)a.buckets.size());
+            for (const Bucket& bk : a.buckets) {  // StringTerms.Bucket.writeTo (:128-136)
+                out.writeBytes(bk.term);
+                out.writeVLong(bk.doc_count);
+                if (a.show_err) out.writeLong(bk.doc_count_error);
+                writeAggregations(bk.aggs, out);
+            }
+            break;
+        case ESGPU_AGG_HISTOGRAM:
+        case ESGPU_AGG_DATE_HISTOGRAM:  // InternalHistogram.doWriteTo (:510-523)
+            out.writeString(a.date ? "date_histogram" : "histogram");
+            out.writeByte(a.order == ESGPU_ORDER_KEY_ASC ? 1 : a.order == ESGPU_ORDER_KEY_DESC ? 2 :
+                          a.order == ESGPU_ORDER_HCOUNT_ASC ? 3 : 4);
+            out.writeVLong(a.min_doc_count);
+            if (a.min_doc_count == 0) {  // EmptyBucketInfo.writeTo (:223-230)
+                writeRounding(a, out);
+                writeAggregations(a.empty_subs, out);
+                out.writeBoolean(a.has_bmin || a.has_bmax);
+                if (a.has_bmin || a.has_bmax) {  // ExtendedBounds.writeTo
+                    out.writeBoolean(a.has_bmin);
+                    if (a.has_bmin) out.writeLong(a.bmin);
+                    out.writeBoolean(a.has_bmax);
+                    if (a.has_bmax) out.writeLong(a.bmax);
+                }
+            }
+            writeFormatter(a, out);
+            out.writeBoolean(a.keyed);
+            out.writeVInt((int32_t)a.buckets.size());
+            for (const Bucket& bk : a.buckets) {  // InternalHistogram.Bucket.writeTo (:183-187)
+                out.writeLong(bk.key);
+                out.writeVLong(bk.doc_count);
+                writeAggregations(bk.aggs, out);
+            }
+            break;
+        case ESGPU_AGG_STATS:
+        case ESGPU_AGG_EXTENDED_STATS:  // InternalStats.doWriteTo (:182-189), InternalExtendedStats.writeOtherStatsTo
+            writeFormatter(a, out);
+            out.writeVLong(a.count);
+            out.writeDouble(a.min);
+            out.writeDouble(a.max);
+            out.writeDouble(a.sum);
+            if (a.type == ESGPU_AGG_EXTENDED_STATS) { out.writeDouble(a.sumsq); out.writeDouble(a.sigma); }
+            break;
+        case ESGPU_AGG_AVG:  // InternalAvg.doWriteTo (:102-106)
+            writeFormatter(a, out);
+            out.writeDouble(a.sum);
+            out.writeVLong(a.count);
+            break;
+        case ESGPU_AGG_CARDINALITY:  // InternalCardinality.doWriteTo (:92-100), HyperLogLogPlusPlus.writeTo(0, out)
+            writeFormatter(a, out);
+            out.writeBoolean(a.hll != nullptr);
+            if (a.hll) {
+                const HLLPP& h = *a.hll;
+                out.writeVInt(h.p);
+                if (!h.algo(0)) {
+                    out.writeBoolean(false);
+                    const std::vector<int> v = h.hs_values(0);
+                    out.writeVLong((int64_t)v.size());
+                    for (int e : v) out.writeInt(e);
+                } else {
+                    out.writeBoolean(true);
+                    for (int i = 0; i < h.m; ++i) out.writeByte(h.runLens[(size_t)i]);
+                }
+            }
+            break;
+        case ESGPU_AGG_FILTER:  // InternalSingleBucketAggregation.doWriteTo (:124-127)
+            out.writeVLong(a.count);
+            writeAggregations(a.subs, out);
+            break;
+    }
+}
+
+static void writeAggregations(const InternalList& aggs, StreamOutput& out) {  // InternalAggregations.writeTo
+    out.writeVInt((int32_t)aggs.size());
+    for (const InternalPtr& a : aggs) {
+        out.writeBytes(streamType(a->type));
+        writeAggregation(*a, out);
+    }
+}
+
+static int g_emit_streams = 0;
+
+// ------------------------------------------------------------------------------------------------------------
 // Driver: AggregationPhase.preProcess -> QueryPhase collection loop -> postCollection -> buildAggregation(0)
 // (A/AggregationPhase.java:69-168; C/search/query/QueryPhase.java:254-258,312-314) and the coordinator reduce
 // (C/search/controller/SearchPhaseController.java:401-411).
@@ -1556,7 +1753,22 @@ int oracle_run(const oracle_shard* shards, int32_t nshards, const esgpu_agg_spec
         }
         j.raw("],\"reduced\":{");
         if (!shard_results.empty()) write_list(j, reduce_list(shard_results));
-        j.raw("}}");
+        j.raw("}");
+        if (g_emit_streams) {  // per shard, hex of InternalAggregations.writeTo
+            j.raw(",\"streams\":[");
+            for (size_t s = 0; s < shard_results.size(); ++s) {
+                StreamOutput out;
+                writeAggregations(shard_results[s], out);
+                static const char* hx = "0123456789abcdef";
+                std::string h;
+                h.reserve(out.b.size() * 2);
+                for (unsigned char c : out.b) { h.push_back(hx[c >> 4]); h.push_back(hx[c & 15]); }
+                if (s) j.raw(",");
+                j.raw("\""); j.raw(h.c_str()); j.raw("\"");
+            }
+            j.raw("]");
+        }
+        j.raw("}");
         *json_out = strdup(j.s.c_str());
         if (collect_seconds) *collect_seconds = secs;
         return 0;
@@ -1567,6 +1779,8 @@ int oracle_run(const oracle_shard* shards, int32_t nshards, const esgpu_agg_spec
 }
 
 void oracle_free(char* p) { free(p); }
+/* 1: oracle_run's JSON also carries "streams": per shard, the hex of InternalAggregations.writeTo */
+void oracle_set_emit_streams(int32_t on) { oracle::g_emit_streams = on; }
 
 /* known-answer helpers */
 void oracle_murmur3_128(const uint8_t* key, int32_t len, int64_t seed, uint64_t* h1, uint64_t* h2) {

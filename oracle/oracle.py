@@ -45,6 +45,7 @@ def lib():
                                  ctypes.POINTER(N.Filter), ctypes.c_int32, ctypes.POINTER(ctypes.c_char_p),
                                  ctypes.POINTER(ctypes.c_double)]
         L.oracle_free.argtypes = [ctypes.c_char_p]
+        L.oracle_set_emit_streams.argtypes = [ctypes.c_int32]
         L.oracle_last_error.restype = ctypes.c_char_p
         L.oracle_murmur3_128.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int64, ctypes.POINTER(ctypes.c_uint64),
                                          ctypes.POINTER(ctypes.c_uint64)]
@@ -123,9 +124,12 @@ def _columns(columns):
     return arr, len(descs), keep
 
 
-def run(shards, aggs, filters=None, number_of_shards=None, accept=None, ord_lookup=None, return_seconds=False):
-    """shards: list of (columns_dict, max_doc).  Returns {"shards": [...], "reduced": {...}} (parsed JSON)."""
+def run(shards, aggs, filters=None, number_of_shards=None, accept=None, ord_lookup=None, return_seconds=False,
+        streams=False):
+    """shards: list of (columns_dict, max_doc).  Returns {"shards": [...], "reduced": {...}} (parsed JSON); with
+    streams=True also "streams": per shard the bytes of InternalAggregations.writeTo."""
     L = lib()
+    L.oracle_set_emit_streams(1 if streams else 0)
     number_of_shards = number_of_shards or len(shards)
     specs, nspecs, k1 = oracle_request.lower(L, aggs, number_of_shards)
     flt, nf, k2 = oracle_request.lower_filters(filters, ord_lookup, aggs)
@@ -150,6 +154,9 @@ def run(shards, aggs, filters=None, number_of_shards=None, accept=None, ord_look
         raise RuntimeError("oracle: " + L.oracle_last_error().decode())
     res = json.loads(out.value.decode("utf-8"))
     L.oracle_free(out)
+    L.oracle_set_emit_streams(0)
+    if streams:
+        res["streams"] = [bytes.fromhex(h) for h in res["streams"]]
     if return_seconds:
         return res, secs.value
     return res

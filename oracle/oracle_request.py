@@ -198,6 +198,36 @@ def zone_table(tz):
     return tuple(starts), tuple(offs)
 
 
+# ---- value formatter and time zone id (wire stream) ----
+# The test index mapping (SURVEY §8(d) synthetic log documents): "@timestamp" is a date field with the mapper's default
+# format, DateFieldMapper.Defaults.DATE_TIME_FORMATTER (C/index/mapper/core/DateFieldMapper.java:75); every other field
+# is a NumberFieldType (long / double / murmur3) or a string.
+_DATE_FIELD_FORMATS = {"@timestamp": "strict_date_optional_time||epoch_millis"}
+
+
+def _resolve_format(field, fmt):
+    """ValuesSourceParser.resolveFormat(format, timezone, fieldType) (ValuesSourceParser.java:244-257)"""
+    if field in _DATE_FIELD_FORMATS:  # ValueFormat.DateTime.format(format, tz) / .mapper(fieldType, tz)
+        return N.FORMAT_DATE_TIME, fmt if fmt is not None else _DATE_FIELD_FORMATS[field]
+    if fmt is not None:               # NumberFieldType with a pattern: ValueFormat.Number.format(format)
+        return N.FORMAT_NUMBER, fmt
+    return N.FORMAT_RAW, None         # ValueFormat.RAW
+
+
+def zone_id(tz):
+    """joda DateTimeZone.forID(tz).getID(): UTC for "UTC" and for a zero offset (forOffsetMillis(0) == UTC), the offset
+    printed as [+-]hh:mm for a fixed zone (DateTimeZone.printOffset), a region id as named."""
+    if tz is None or tz in ("UTC", "utc", "Z", "Etc/UTC"):
+        return "UTC"
+    m = re.fullmatch(r"([+-])?(\d{1,2})(?::?(\d{2}))?", tz)
+    if not m:
+        return tz
+    ms = int(m.group(2)) * 3_600_000 + int(m.group(3) or 0) * 60_000
+    if ms == 0:
+        return "UTC"
+    return "%s%02d:%02d" % ("-" if m.group(1) == "-" else "+", ms // 3_600_000, ms // 60_000 % 60)
+
+
 # ---- lowering ----
 def _zone_arrays(zone, keep):
     starts = (ctypes.c_int64 * len(zone[0]))(*zone[0])
@@ -229,6 +259,11 @@ def lower(lib, aggs, number_of_shards=1):
         sp.field = enc(b._field)
         sp.sigma = 2.0
         sp.precision_threshold = -1
+        if b.type != N.AGG_FILTER:
+            fmt, pattern = _resolve_format(b._field, getattr(b, "_format", None))
+            sp.value_format = fmt
+            sp.format = enc(pattern)
+            sp.time_zone = enc(zone_id(b._tz) if b.type == N.AGG_DATE_HISTOGRAM else "UTC")
         if b.type == N.AGG_TERMS:
             order = b._order
             if hasattr(order, "path"):  # Terms.Order.aggregation(path, asc)

@@ -1,4 +1,4 @@
-"""Test-side encoder of the libesgpu shard-result stream (esgpu_result_serialize format, version 4, esgpu_results.cpp).
+"""Test-side encoder of the libesgpu shard-result stream (esgpu_result_serialize format, version 5, esgpu_results.cpp).
 
 Lets CPU tests hand-build shard-level InternalAggregations (the way the reference's unit tests construct
 StringTerms / InternalHistogram / InternalCardinality objects) and push them through esgpu_result_deserialize +
@@ -10,7 +10,7 @@ import struct
 from elasticsearch_amd import _native as N
 
 MAGIC = 0x45534750
-VERSION = 4
+VERSION = 5
 BUCKET_TYPES = (N.AGG_TERMS, N.AGG_HISTOGRAM, N.AGG_DATE_HISTOGRAM)
 
 
@@ -22,6 +22,13 @@ def _str(b, s):
 def _vec(b, fmt, xs):
     xs = list(xs)
     b += struct.pack("<Q", len(xs)) + (struct.pack("<%d%s" % (len(xs), fmt), *xs) if xs else b"")
+
+
+def _fmt(b, a):
+    """time zone id, ESGPU_FORMAT_* and pattern (version 5)"""
+    _str(b, a.get("time_zone", "UTC"))
+    b += struct.pack("<i", a.get("value_format", N.FORMAT_RAW))
+    _str(b, a.get("format", ""))
 
 
 def _block(b, insts):
@@ -38,6 +45,7 @@ def _block(b, insts):
     b += struct.pack("<BBqq", a.get("has_bmin", 0), a.get("has_bmax", 0), a.get("bmin", 0), a.get("bmax", 0))
     b += struct.pack("<di", a.get("sigma", 2.0), a.get("precision", 14))
     _str(b, a.get("order_path", ""))
+    _fmt(b, a)
     b += struct.pack("<Q", len(insts))
     bucket = t in BUCKET_TYPES
     buckets = [bk for x in insts for bk in x.get("buckets", [])] if bucket else []
@@ -98,6 +106,7 @@ def _empty_block(b, spec):
     b += struct.pack("<BBqq", s.get("has_bmin", 0), s.get("has_bmax", 0), s.get("bmin", 0), s.get("bmax", 0))
     b += struct.pack("<di", s.get("sigma", 2.0), s.get("precision", 14))
     _str(b, s.get("order_path", ""))
+    _fmt(b, s)
     b += struct.pack("<Q", 0)
     bucket = t in BUCKET_TYPES
     _vec(b, "q", [])
@@ -161,7 +170,9 @@ def from_shard_json(aggs, shard_json, number_of_shards=1):
     def params(i):
         s = specs[i]
         hist = s.type in (N.AGG_HISTOGRAM, N.AGG_DATE_HISTOGRAM)
-        p = {"type": s.type, "name": s.name.decode(), "order": s.order, "sigma": s.sigma}
+        p = {"type": s.type, "name": s.name.decode(), "order": s.order, "sigma": s.sigma,
+             "time_zone": (s.time_zone or b"UTC").decode(), "value_format": s.value_format,
+             "format": (s.format or b"").decode()}
         if s.type == N.AGG_TERMS:
             p.update(required_size=s.size, shard_size=s.shard_size, min_doc_count=s.min_doc_count,
                      show_err=s.show_term_doc_count_error, order_path=(s.order_path or b"").decode())
