@@ -261,9 +261,19 @@ struct HcParams {
     int32_t overwrite;                 // store the counts instead of adding (the plan's first segment)
 };
 __host__ __device__ inline uint32_t hc_hot_counters(uint32_t hot_n) { return hot_n + 3 * (hot_n < kHcHotCopies ? hot_n : kHcHotCopies); }
+// per-workgroup hot slab row: the counters padded to 16 bytes (the reduce reads them as uint4)
+__host__ __device__ inline uint32_t hc_slab_stride(uint32_t hot_n) { return (hc_hot_counters(hot_n) + 3u) & ~3u; }
 size_t hc_scatter_lds_bytes(uint32_t n_parts, uint32_t hot_n);
 constexpr uint32_t kHcScatterWG = 512;  // threads of a scatter workgroup (esgpu_hotcold.hip kHcWG)
 void launch_hotcold(const HcParams& p, hipStream_t s);
+// Requests without predicates or accept bits over a segment whose cold docs are also stored in partition order
+// (HcStats' cold lists): `hot` streams the recoded column and counts only the hot slots (G = hot.G workgroups), `cold`
+// counts the cold lists (one static region per partition, G = 1) with the scatter path's counting pass.
+void launch_hotcold_postings(const HcParams& hot, const HcParams& cold, hipStream_t s);
+// stats time: the dense partition-ordered cold offsets -> one list per partition starting at pad_begin[p] (a multiple
+// of 64 elements), 0xFFFF between lists
+void launch_hc_pad(const uint16_t* dense, const uint32_t* dense_begin, const uint32_t* pad_begin, uint32_t P,
+                   uint16_t* out, hipStream_t s);
 // stats time: out[d] = kHcHotBit | slot for the hot ordinals (open-addressing table keys -> vals, 2^log2 entries,
 // 0xFFFFFFFF = empty key), the ordinal itself otherwise
 void launch_hc_recode(const uint32_t* ord, uint32_t n, const uint32_t* keys, const uint32_t* vals, uint32_t log2,

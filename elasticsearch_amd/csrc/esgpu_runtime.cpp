@@ -1457,6 +1457,12 @@ static bool collect_partitioned(esgpu_plan* p, Pipeline& pl, const esgpu_segment
 #ifndef ESGPU_HOT_MAX
 #define ESGPU_HOT_MAX 16384  // hot slots at most (LDS counters of the scatter)
 #endif
+#ifndef ESGPU_HOT_PER_CU
+#define ESGPU_HOT_PER_CU 2  // hot-pass workgroups per CU (postings path; 4 measured 13 % slower)
+#endif
+#ifndef ESGPU_HC_POSTINGS
+#define ESGPU_HC_POSTINGS 1  // cold lists for requests without predicates / accept bits (0: always the scatter path)
+#endif
 #ifndef ESGPU_NO_HOT
 #define ESGPU_NO_HOT 0  // timing experiments: no hot set
 #endif
@@ -1470,6 +1476,11 @@ struct HcStats {
     uint64_t hot_docs = 0, docs = 0;
     DevBuf d_rc;                 // recoded ordinal column (hot ordinals as kHcHotBit | slot); empty: no hot set
     DevBuf d_hot_ord, d_part, d_piece;
+    // cold lists: the cold docs' partition-local offsets grouped by partition (postings of the cold ordinals, 64-element
+    // aligned per partition), read by requests without predicates or accept bits instead of scattering the cold docs
+    bool cold_lists = false;
+    uint32_t cold_pieces = 0;
+    DevBuf d_cold, d_cold_part, d_cold_piece, d_cold_used, d_cold_ovf;
 };
 
 static uint32_t hc_hash_host(uint32_t o, uint32_t log2) { return (uint32_t)(o * 0x9E3779B1u) >> (32 - log2); }
@@ -1646,6 +1657,77 @@ static std::shared_ptr<const HcStats> ensure_hc_stats(esgpu_ctx* c, const DevCol
         HIPX(hipMemcpy(hs->d_hot_ord.p, hot.data(), hot.size() * 4, hipMemcpyHostToDevice));
         HIPX(hipStreamSynchronize(st));  // the table buffers are released on return
     }
+    if (ESGPU_HC_POSTINGS) {
+        // cold lists: the radix-partition passes over the recoded column (hot and missing values are >= T and skipped)
+        // give the cold docs' offsets partition by partition; each partition's list is then copied to a 64-aligned start
+        const uint32_t* col = hot.empty() ? (const uint32_t*)src : hs->d_rc.as<uint32_t>();
+        std::vector<uint32_t> pad(P + 1, 0);
+        for (uint32_t p = 0; p < P; ++p) pad[p + 1] = pad[p] + (uint32_t)((cold[p] + 63) & ~63ull);
+        if ((uint64_t)pad[P] + (uint64_t)64 * P < 0xFFFFFFF0ull) {
+            DevBuf dense, wgc, pbeg, tiles, dpad;
+            PartParams Q{};
+            Q.n_docs = s->max_doc;
+            Q.n_blocks = s->n_pad / kBlockDocs;
+            const uint32_t target = (uint32_t)c->cus * part_wg_per_cu();
+            Q.blocks_per_wg = std::max(1u, (Q.n_blocks + target - 1) / target);
+            Q.G = (Q.n_blocks + Q.blocks_per_wg - 1) / Q.blocks_per_wg;
+            Q.ord = col;
+            Q.T = T;
+            Q.shift = kPartShift;
+            Q.P = P;
+            wgc.alloc(c, (size_t)Q.P * Q.G * 4);
+            pbeg.alloc(c, (size_t)(Q.P + 1) * 4);
+            const uint32_t ntiles = part_scan_tiles(Q.P * Q.G);
+            require(ntiles <= 4096, ESGPU_ERR_INVALID, "partition scan too large");
+            tiles.alloc(c, (size_t)ntiles * 4);
+            dense.alloc(c, ((size_t)total + 8) * 2);
+            Q.wg_counts = wgc.as<uint32_t>();
+            Q.part_begin = pbeg.as<uint32_t>();
+            Q.tile_sums = tiles.as<uint32_t>();
+            Q.pbuf = dense.as<uint16_t>();
+            if (s->max_doc) {
+                launch_part_hist(Q, st);
+                launch_part_scan(Q, st);
+                launch_part_scatter(Q, st);
+            } else {
+                HIPX(hipMemsetAsync(pbeg.p, 0, pbeg.bytes, st));
+            }
+            dpad.alloc(c, pad.size() * 4);
+            HIPX(hipMemcpyAsync(dpad.p, pad.data(), pad.size() * 4, hipMemcpyHostToDevice, st));
+            hs->d_cold.alloc(c, ((size_t)pad[P] + 8) * 2);
+            launch_hc_pad(dense.as<uint16_t>(), pbeg.as<uint32_t>(), dpad.as<uint32_t>(), P, hs->d_cold.as<uint16_t>(), st);
+            HIPX(hipGetLastError());
+            std::vector<HcPart> cparts(P);
+            std::vector<uint32_t> used(P);
+            std::vector<HcPiece> cpieces;
+            const uint64_t cpiece_len = std::max<uint64_t>(1ull << 20, (4 * (uint64_t)pad[P] / P + 63) & ~63ull);
+            for (uint32_t p = 0; p < P; ++p) {
+                HcPart& q = cparts[p];
+                q.sbase = pad[p];
+                q.chunk = pad[p + 1] - pad[p];
+                q.ovf_base = q.cap_end = pad[p + 1];
+                q.ovf_chunk = 64;
+                used[p] = (uint32_t)cold[p];
+                const uint32_t n = (uint32_t)std::max<uint64_t>(1, (q.chunk + cpiece_len - 1) / cpiece_len);
+                for (uint32_t k = 0; k < n; ++k)  // at least one piece per partition: the first segment's counts are stored
+                    cpieces.push_back(HcPiece{p, (uint32_t)(k * cpiece_len),
+                                              (uint32_t)std::min<uint64_t>((k + 1) * cpiece_len, q.chunk), n == 1 ? 1u : 0u});
+            }
+            hs->cold_pieces = (uint32_t)cpieces.size();
+            hs->d_cold_part.alloc(c, cparts.size() * sizeof(HcPart));
+            hs->d_cold_piece.alloc(c, cpieces.size() * sizeof(HcPiece));
+            hs->d_cold_used.alloc(c, used.size() * 4);
+            std::vector<uint32_t> ovf(P);
+            for (uint32_t p = 0; p < P; ++p) ovf[p] = cparts[p].ovf_base;  // no overflow pool: fill 0 for every request
+            hs->d_cold_ovf.alloc(c, ovf.size() * 4);
+            HIPX(hipMemcpyAsync(hs->d_cold_ovf.p, ovf.data(), ovf.size() * 4, hipMemcpyHostToDevice, st));
+            HIPX(hipMemcpyAsync(hs->d_cold_part.p, cparts.data(), cparts.size() * sizeof(HcPart), hipMemcpyHostToDevice, st));
+            HIPX(hipMemcpyAsync(hs->d_cold_piece.p, cpieces.data(), cpieces.size() * sizeof(HcPiece), hipMemcpyHostToDevice, st));
+            HIPX(hipMemcpyAsync(hs->d_cold_used.p, used.data(), used.size() * 4, hipMemcpyHostToDevice, st));
+            HIPX(hipStreamSynchronize(st));  // the scratch buffers and host vectors are released on return
+            hs->cold_lists = true;
+        }
+    }
     mcol->hc = hs;
     return hs;
 }
@@ -1674,7 +1756,7 @@ static bool collect_hotcold(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s,
     H.n_pieces = hs->n_pieces;
     H.ovf_cur = (uint32_t*)p->s_hcur.ensure(c, (size_t)H.P * 4);
     H.used = (uint32_t*)p->s_hused.ensure(c, (size_t)H.P * H.G * 4);
-    H.hot_slab = H.hot_n ? (uint32_t*)p->s_hslab.ensure(c, (size_t)hc_hot_counters(H.hot_n) * H.G * 4) : nullptr;
+    H.hot_slab = H.hot_n ? (uint32_t*)p->s_hslab.ensure(c, (size_t)hc_slab_stride(H.hot_n) * H.G * 4) : nullptr;
     H.pbuf = (uint16_t*)p->s_pbuf.ensure(c, hs->pbuf_elems * 2);
     H.trash = hs->trash;
     H.counts = pl.g_cnt.as<unsigned long long>();
@@ -1683,6 +1765,30 @@ static bool collect_hotcold(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s,
     p->hc_check = true;
     H.u16_counters = hs->u16 ? 1 : 0;
     H.overwrite = first_segment ? 1 : 0;  // every counter is stored by the counting pass: no read of the zeroed grid
+    if (hs->cold_lists && npred == 0 && !d_accept) {  // every doc counts: hot slots from the column, cold lists
+        HcParams K = H;                                 // the cold lists: one static region per partition
+        K.G = 1;
+        K.part = hs->d_cold_part.as<HcPart>();
+        K.piece = hs->d_cold_piece.as<HcPiece>();
+        K.n_pieces = hs->cold_pieces;
+        K.used = hs->d_cold_used.as<uint32_t>();
+        K.pbuf = hs->d_cold.as<uint16_t>();
+        K.ovf_cur = hs->d_cold_ovf.as<uint32_t>();
+        K.hot_n = 0;
+        HcParams Hh = H;                                // hot pass: ESGPU_HOT_PER_CU 512-thread workgroups per CU
+        const size_t hot_lds = (size_t)hc_hot_counters(Hh.hot_n) * 4;
+        require(hot_lds <= 160 * 1024, ESGPU_ERR_STATE, "hot counters beyond LDS");
+        Hh.G = (uint32_t)c->cus * (uint32_t)std::max<size_t>(1, std::min<size_t>(ESGPU_HOT_PER_CU, 160 * 1024 / (hot_lds + 1024)));
+        Hh.blocks_per_wg = std::max(1u, (Hh.n_blocks + Hh.G - 1) / Hh.G);
+        Hh.G = std::max(1u, (Hh.n_blocks + Hh.blocks_per_wg - 1) / Hh.blocks_per_wg);
+        Hh.hot_slab = Hh.hot_n ? (uint32_t*)p->s_hslab.ensure(c, (size_t)hc_slab_stride(Hh.hot_n) * Hh.G * 4) : nullptr;
+        HIPX(hipEventRecord(pl.e0, st));
+        launch_hotcold_postings(Hh, K, st);
+        HIPX(hipGetLastError());
+        HIPX(hipEventRecord(pl.e1, st));
+        p->last_path = 7;
+        return true;
+    }
     require(hc_scatter_lds_bytes(H.P, H.hot_n) <= 160 * 1024 - 256, ESGPU_ERR_STATE, "hot/cold LDS layout");
     HIPX(hipEventRecord(pl.e0, st));
     launch_hotcold(H, st);

@@ -6,6 +6,8 @@ request and reused.  Each case stresses one part of that design: ordinals cluste
 share of a partition is far from its static region: overflow chunks), a flat distribution (no hot table), a cold
 ordinal with more than 65535 docs (32-bit counters in the counting pass), filters and accept bitsets (requests that
 use a fraction of the capacities), several segments into one plan, and reuse of the statistics across requests.
+Requests without predicates or accept bits take the postings form (path 7: hot slots from the recoded column, the cold
+docs counted from the segment's partition-ordered cold lists); the others scatter the cold docs per request (path 6).
 """
 import numpy as np
 import pytest
@@ -32,7 +34,7 @@ def _check(engine, cols, n, aggs, filters=None, accept=None, reps=1):
     for rep in range(reps):  # the second request reuses the segment statistics built by the first
         plan.collect(seg, accept_bits=accept)
         _, _, path = plan.last_collect_stats()
-        assert path == 6, path
+        assert path == (7 if not filters and accept is None else 6), path
         res = plan.build()
         assert_same(res.to_dict(), want["shards"][0], f"shard rep{rep}")
         assert_same(reduce([res]).to_dict(), want["reduced"], f"reduced rep{rep}")
@@ -89,10 +91,13 @@ def test_cold_ordinal_over_16_bits(engine):
     ords[rng.choice(n, size=70_000, replace=False)] = 777
     cols = _cols(ords, T, rng)
     _check(engine, cols, n, [AB.terms("c").field("kw").size(10)], filters=[QB.rangeQuery("status").lte(2)])
+    _check(engine, cols, n, [AB.terms("c").field("kw").size(10)], reps=2)
 
 
-def test_two_segments_one_plan(engine):
-    """Two segments with their own statistics counted into one plan (same dictionary, no ordinal map)."""
+@pytest.mark.parametrize("filtered", [True, False])
+def test_two_segments_one_plan(engine, filtered):
+    """Two segments with their own statistics counted into one plan (same dictionary, no ordinal map); unfiltered, the
+    second segment's cold lists add to the first's counts."""
     rng = np.random.default_rng(105)
     T = 180_000
     sizes = [700_001, 1_100_000]
@@ -104,13 +109,13 @@ def test_two_segments_one_plan(engine):
     allc = {"kw": dict(cols[0]["kw"], values=np.concatenate(parts)),
             "status": {"type": N.COL_I64, "values": np.concatenate([c["status"]["values"] for c in cols])}}
     aggs = [AB.terms("c").field("kw").size(25), AB.terms("t").field("kw").size(6).order(Order.term(False))]
-    flt = [QB.rangeQuery("status").gte(1)]
+    flt = [QB.rangeQuery("status").gte(1)] if filtered else None
     want = O.run([(allc, sum(sizes))], aggs, filters=flt)
     segs = [engine.upload_segment(c, n) for c, n in zip(cols, sizes)]
     plan = engine.plan(aggs, filters=flt)
     for s in segs:
         plan.collect(s)
-        assert plan.last_collect_stats()[2] == 6
+        assert plan.last_collect_stats()[2] == (6 if filtered else 7)
     res = plan.build()
     assert_same(res.to_dict(), want["shards"][0], "shard")
     plan.close()
