@@ -376,10 +376,20 @@ __global__ __launch_bounds__(kHllLdsWG) void hll_registers_lds_kernel(HllParams 
 #endif
 }
 
-// packed 4-bit lower bounds of the registers relative to the floor: nibble = min(reg - floor, 15)
-__global__ __launch_bounds__(256) void hll_snapshot_kernel(const unsigned int* regs, uint32_t m, const unsigned int* floor_ptr,
-                                                           unsigned char* snap) {
-    const uint32_t F = *floor_ptr;
+// packed 4-bit lower bounds of the registers relative to the floor: nibble = min(reg - floor, 15).  The floor F is the
+// min of the group floors (4 KB, read by every block); block 0 also stores it for the phase kernel, so no memset and
+// no atomic are needed between phases.
+__global__ __launch_bounds__(256) void hll_snapshot_kernel(const unsigned int* regs, uint32_t m, const unsigned char* gfloor,
+                                                           uint32_t ngroups, unsigned int* floor_out, unsigned char* snap) {
+    __shared__ uint32_t wmin[4];
+    uint32_t f = 0xFFFFFFFFu;
+    for (uint32_t g = threadIdx.x; g < ngroups; g += 256) f = min(f, (uint32_t)gfloor[g]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) f = min(f, (uint32_t)__shfl_xor((int)f, o, 64));
+    if ((threadIdx.x & 63) == 0) wmin[threadIdx.x >> 6] = f;
+    __syncthreads();
+    const uint32_t F = min(min(wmin[0], wmin[1]), min(wmin[2], wmin[3]));
+    if (blockIdx.x == 0 && threadIdx.x == 0) *floor_out = F;
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (kHllPerByte * i >= m) return;
     uint32_t b = 0;
@@ -388,8 +398,8 @@ __global__ __launch_bounds__(256) void hll_snapshot_kernel(const unsigned int* r
     snap[i] = (unsigned char)b;
 }
 
-// group floors: one wave per group of 64 registers; the global floor is their min (*out initialised to ~0), one
-// atomic per workgroup of 16 groups
+// group floors: one wave per group of 64 registers; with `out`, the global floor is their min (*out initialised to ~0),
+// one atomic per workgroup of 16 groups
 __global__ __launch_bounds__(1024) void hll_group_floor_kernel(const unsigned int* regs, uint32_t m, unsigned char* gfloor,
                                                                unsigned int* out) {
     __shared__ uint32_t wmin[16];
@@ -403,6 +413,7 @@ __global__ __launch_bounds__(1024) void hll_group_floor_kernel(const unsigned in
         if (g * gsz < m) gfloor[g] = (unsigned char)min(v, 255u);
         wmin[threadIdx.x >> 6] = v;
     }
+    if (!out) return;
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t t = wmin[0];
@@ -507,17 +518,20 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
     const uint32_t floor_grid = std::max(1u, std::min(64u, m / 4096));
     // floor (and group floors + LDS snapshot) of the registers as they stand
     auto refresh = [&]() {
+        const uint32_t ng = m >= kHllGroup ? m / kHllGroup : 1u;
+        if (lds) {  // group floors, then the snapshot kernel derives and stores the floor itself
+            hipLaunchKernelGGL(hll_group_floor_kernel, dim3((ng + 15) / 16), dim3(1024), 0, st, (const unsigned int*)p.regs, m,
+                               p.gfloor, (unsigned int*)nullptr);
+            hipLaunchKernelGGL(hll_snapshot_kernel, dim3((hll_snap_bytes(m) + 255) / 256), dim3(256), 0, st,
+                               (const unsigned int*)p.regs, m, (const unsigned char*)p.gfloor, ng, p.floor, p.snap);
+            return;
+        }
         (void)hipMemsetAsync(p.floor, 0xFF, 4, st);
-        if (fast) {
-            const uint32_t ng = m >= kHllGroup ? m / kHllGroup : 1u;
+        if (fast)
             hipLaunchKernelGGL(hll_group_floor_kernel, dim3((ng + 15) / 16), dim3(1024), 0, st, (const unsigned int*)p.regs, m,
                                p.gfloor, p.floor);
-            if (lds)
-                hipLaunchKernelGGL(hll_snapshot_kernel, dim3((hll_snap_bytes(m) + 255) / 256), dim3(256), 0, st, (const unsigned int*)p.regs, m,
-                                   (const unsigned int*)p.floor, p.snap);
-        } else {
+        else
             hipLaunchKernelGGL(hll_floor_kernel, dim3(floor_grid), dim3(1024), 0, st, (const unsigned int*)p.regs, m, p.floor);
-        }
     };
     const bool warm = p.seen >= (uint64_t)m * ESGPU_HLL_CUT0;  // the registers already passed the first cut
     if (warm) refresh();
