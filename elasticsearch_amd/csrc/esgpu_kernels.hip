@@ -1235,6 +1235,14 @@ __device__ __forceinline__ int64_t hv_at(const CollectParams& P, uint64_t i) {
     return P.hv_f64 ? java_long(bits_dbl((uint64_t)x)) : x;
 }
 
+// key slot of histogram value i: a rounded / table-looked-up key, or (HK 3, terms under terms) the inner field's ordinal
+// itself (u32 column; missing = 0xFFFFFFFF lands outside [0, H) and is skipped)
+template <int HK>
+__device__ __forceinline__ int64_t multi_key(const CollectParams& P, uint64_t i) {
+    if constexpr (HK == 3) return (int64_t)((const uint32_t*)P.hv)[i];
+    else return key_index<HK == 2>(P, hv_at(P, i));
+}
+
 // values [b, e) of doc d in a column (single valued: [d, d+1) when present)
 __device__ __forceinline__ void value_range(const uint64_t* off, const uint64_t* present, uint32_t d, uint64_t& b,
                                             uint64_t& e) {
@@ -1338,7 +1346,7 @@ __global__ __launch_bounds__(kWG) void collect_multi_kernel(CollectParams P) {
             bool first = true;
             int64_t prev = 0;
             for (uint64_t h = hb; h < he; ++h) {
-                const int64_t k = key_index<KT>(P, hv_at(P, h));
+                const int64_t k = multi_key<HK>(P, h);
                 if (!first && k == prev) continue;
                 first = false;
                 prev = k;
@@ -1357,7 +1365,7 @@ __global__ __launch_bounds__(kWG) void collect_multi_kernel(CollectParams P) {
             for (uint64_t h = hb; h < he; ++h) {
                 uint32_t slot = 0;
                 if (HIST) {
-                    const int64_t k = key_index<KT>(P, hv_at(P, h));
+                    const int64_t k = multi_key<HK>(P, h);
                     if (!first && k == prev) continue;
                     first = false;
                     prev = k;
@@ -1398,9 +1406,10 @@ static void launch_multi_m(const CollectParams& p, int met, uint32_t grid, size_
     }
 }
 void launch_collect_multi(const CollectParams& p, bool ord, bool hist, int met, uint32_t grid, size_t lds, hipStream_t st) {
-    const int hk = hist ? (p.kstart ? 2 : 1) : 0;
+    const int hk = hist ? (p.hord ? 3 : p.kstart ? 2 : 1) : 0;
     if (ord) {
-        if (hk == 2) launch_multi_m<true, 2>(p, met, grid, lds, st);
+        if (hk == 3) launch_multi_m<true, 3>(p, met, grid, lds, st);
+        else if (hk == 2) launch_multi_m<true, 2>(p, met, grid, lds, st);
         else if (hk == 1) launch_multi_m<true, 1>(p, met, grid, lds, st);
         else launch_multi_m<true, 0>(p, met, grid, lds, st);
     } else {

@@ -1940,10 +1940,8 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     const bool inner_missing = ORD && HIST && (terms_outer ? (oc && !hc) : (hc && !oc));
     if (((ORD && !oc) || (HIST && !hc)) && !inner_missing) return 0;
     if (oc) require(oc->type == ESGPU_COL_ORD_U32, ESGPU_ERR_UNSUPPORTED, "terms on numeric fields run on the CPU path");
-    if (hc && pl.inner_terms) {
+    if (hc && pl.inner_terms) {  // multi-valued outer / inner fields take the CSR kernel (inner ordinals as keys)
         require(hc->type == ESGPU_COL_ORD_U32, ESGPU_ERR_UNSUPPORTED, "terms on numeric fields run on the CPU path");
-        require(!hc->multi && !(oc && oc->multi), ESGPU_ERR_UNSUPPORTED,
-                "terms under terms over multi-valued fields runs on the CPU path");
     } else if (hc) {
         require(hc->type == ESGPU_COL_I64 || hc->type == ESGPU_COL_F64, ESGPU_ERR_UNSUPPORTED,
                 "histogram over a keyword field runs on the CPU path");
@@ -1989,7 +1987,6 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     // ords may be missing; a doc may have several keys: then the outer counts cannot be summed from the cells
     const bool inner_sparse = ORD && HIST && (inner_missing || pl.inner_terms ||
                                               (terms_outer ? (hc->present.p != nullptr || hc->multi) : true));
-    require(!(pl.inner_terms && multi), ESGPU_ERR_UNSUPPORTED, "terms under terms with multi-valued filter fields runs on the CPU path");
     if (!pl.allocated || pl.fresh) {
         const uint32_t T = oc ? (uint32_t)std::max<uint64_t>(oc->ord_count(), 1) : 1;
         const int64_t key0 = has_keys ? kmin : 0;

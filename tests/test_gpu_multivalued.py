@@ -171,3 +171,15 @@ def test_filter_aggregation_over_multi_valued_fields(engine):  # FilterAggregato
             AB.stats("all_prices").field("prices")]
     got = check(engine, aggs, cols, N_DOCS, filters=[QB.rangeQuery("response_time_ms").lt(700)])
     assert got["tagged"]["doc_count"] > 0
+
+
+def test_multi_valued_terms_under_terms(engine):
+    """terms under terms with a multi-valued outer or inner keyword field (the CSR kernel with the inner field's
+    ordinals as the key dimension): every (outer ordinal, inner ordinal) pair of a doc is one cell."""
+    aggs = [AB.terms("tags").field("tags").size(8).subAggregation(
+                AB.terms("hosts").field("host").size(5).subAggregation(AB.stats("rt").field("response_time_ms"))),
+            AB.terms("hosts").field("host").size(6).order(Order.term(True)).subAggregation(
+                AB.terms("tags").field("tags").size(4).order(Order.count(True))),
+            AB.terms("pairs").field("tags").size(5).subAggregation(AB.terms("co").field("tags").size(3).minDocCount(0))]
+    check(engine, aggs, segment(N_DOCS, 11), N_DOCS, exact=True)
+    check(engine, aggs[:1], segment(N_DOCS, 12), N_DOCS, filters=[QB.rangeQuery("codes").gte(100).lte(300)], exact=True)
