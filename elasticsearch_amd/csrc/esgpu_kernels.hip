@@ -1522,7 +1522,7 @@ __global__ __launch_bounds__(256) void card_kernel(CardParams C, int pass) {
             for (uint64_t hh = hb; hh < he; ++hh) {
                 uint32_t slot = 0;
                 if (HIST) {
-                    const int64_t k = key_index<KT>(P, hv_at(P, hh));
+                    const int64_t k = multi_key<HK>(P, hh);
                     if (!first && k == prev) continue;
                     first = false;
                     prev = k;
@@ -1562,9 +1562,10 @@ __global__ __launch_bounds__(256) void card_kernel(CardParams C, int pass) {
 }
 
 void launch_card(const CardParams& c, bool ord, bool hist, int pass, uint32_t grid, hipStream_t st) {
-    const int hk = hist ? (c.G.kstart ? 2 : 1) : 0;
+    const int hk = hist ? (c.G.hord ? 3 : c.G.kstart ? 2 : 1) : 0;
     if (ord) {
-        if (hk == 2) hipLaunchKernelGGL((card_kernel<true, 2>), dim3(grid), dim3(256), 0, st, c, pass);
+        if (hk == 3) hipLaunchKernelGGL((card_kernel<true, 3>), dim3(grid), dim3(256), 0, st, c, pass);
+        else if (hk == 2) hipLaunchKernelGGL((card_kernel<true, 2>), dim3(grid), dim3(256), 0, st, c, pass);
         else if (hk == 1) hipLaunchKernelGGL((card_kernel<true, 1>), dim3(grid), dim3(256), 0, st, c, pass);
         else hipLaunchKernelGGL((card_kernel<true, 0>), dim3(grid), dim3(256), 0, st, c, pass);
     } else {

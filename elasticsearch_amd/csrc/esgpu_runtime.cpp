@@ -1022,8 +1022,6 @@ static Group compile_group(esgpu_plan* p, int r, int fspec) {
             for (int gc : p->specs[ch].children) {
                 const int t = p->specs[gc].s.type;
                 require(is_metric(t) || t == ESGPU_AGG_CARDINALITY, ESGPU_ERR_UNSUPPORTED, "bucket aggregations nested three levels deep");
-                require(!(ot && it && t == ESGPU_AGG_CARDINALITY), ESGPU_ERR_UNSUPPORTED,
-                        "cardinality under terms under terms runs on the CPU path");
                 inner_leaves.push_back(gc);
             }
             cs.pipes = add_leaf_pipelines(p, r, fspec, r, ch, inner_leaves, &cs.grand);
@@ -1866,6 +1864,12 @@ static void collect_cards(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, c
     G.kstart = (HIST && pl.ktable) ? pl.d_kstart.as<int64_t>() : nullptr;
     G.kslot = G.kstart ? pl.d_kslot.as<uint32_t>() : nullptr;
     G.nsteps = (uint32_t)pl.kt_start.size();
+    if (hc && pl.inner_terms) {  // terms under terms: the inner field's (global) ordinals are the keys
+        G.hv = (const int64_t*)hc->ords().p;
+        G.hv_present = nullptr;
+        G.hv_f64 = 0;
+        G.hord = 1;
+    }
     G.accept = d_accept;
     PredDev pred[4];
     int npred = 0;

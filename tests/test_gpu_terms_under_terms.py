@@ -103,3 +103,15 @@ def test_inner_terms_field_missing_in_a_segment(engine):
     plan.close()
     for s in segs:
         s.close()
+
+
+def test_cardinality_under_terms_under_terms(engine):
+    """cardinality leaves of the inner terms buckets: one HyperLogLogPlusPlus per (outer ordinal, inner ordinal) cell,
+    keyed by the inner field's ordinals like the counts; default precision (14 - 5 - 5 = 4) and an explicit one"""
+    aggs = [AB.terms("hosts").field("host").size(4).subAggregation(
+                AB.terms("codes").field("status_kw").size(3)
+                .subAggregation(AB.cardinality("rts").field("response_time_ms"))
+                .subAggregation(AB.cardinality("sizes").field("bytes").precisionThreshold(3000))),
+            AB.terms("regions").field("region").subAggregation(
+                AB.terms("hosts").field("host").size(2).subAggregation(AB.cardinality("c").field("bytes")))]
+    _both(engine, aggs, n=300_000)
