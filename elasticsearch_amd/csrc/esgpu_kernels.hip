@@ -1645,6 +1645,28 @@ __global__ __launch_bounds__(256) void minmax_i64_kernel(const int64_t* v, uint6
     atomicMin((long long*)&out[0], (long long)mn);
     atomicMax((long long*)&out[1], (long long)mx);
 }
+// histogram under histogram: the inner histogram's key index of every doc as a u32 "ordinal" (affine rounding;
+// 0xFFFFFFFF = no value, or a key outside [key0, key0 + nkeys)), padded docs included
+__global__ __launch_bounds__(256) void hist_ords_kernel(const int64_t* v, const uint64_t* present, uint32_t n_docs,
+                                                        uint32_t n_pad, int f64, int64_t interval, int64_t offset,
+                                                        int64_t key0, uint32_t nkeys, uint32_t* out) {
+    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < n_pad; d += gridDim.x * blockDim.x) {
+        uint32_t o = 0xFFFFFFFFu;
+        if (d < n_docs && (!present || ((present[d >> 6] >> (d & 63)) & 1))) {
+            const int64_t x = f64 ? java_long(bits_dbl((uint64_t)v[d])) : v[d];  // ValuesSource.Numeric.longValues
+            const int64_t k = floor_div64(x - offset, interval) - key0;         // Rounding.Interval.roundKey
+            if (k >= 0 && k < (int64_t)nkeys) o = (uint32_t)k;
+        }
+        out[d] = o;
+    }
+}
+void launch_hist_ords(const int64_t* v, const uint64_t* present, uint32_t n_docs, uint32_t n_pad, bool f64, int64_t interval,
+                      int64_t offset, int64_t key0, uint32_t nkeys, uint32_t* out, hipStream_t st) {
+    if (n_pad == 0) return;
+    hipLaunchKernelGGL(hist_ords_kernel, dim3(std::min<uint32_t>(8192, (n_pad + 255) / 256)), dim3(256), 0, st, v, present, n_docs,
+                       n_pad, f64 ? 1 : 0, interval, offset, key0, nkeys, out);
+}
+
 void launch_minmax_i64(const int64_t* v, uint64_t n, int64_t* out, bool f64, hipStream_t st) {
     if (n == 0) return;
     hipLaunchKernelGGL(minmax_i64_kernel, dim3((uint32_t)std::min<uint64_t>(1024, (n + 255) / 256)), dim3(256), 0, st, v, n, out,

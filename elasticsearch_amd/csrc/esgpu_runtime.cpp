@@ -794,6 +794,13 @@ struct Pipeline {
     std::vector<int> metrics;        // leaf specs at the deepest level, in request order (numeric metrics + cardinality)
     std::vector<CardState> cards;    // cardinality leaves (spec order)
     std::string ord_field, hist_field, metric_field;
+    // histogram under histogram: the inner histogram's key indices are the ordinal dimension (ord_field = its field),
+    // derived per segment into ord_col (affine rounding ord_interval / ord_offset; keys ord_key0 .. + ord_keys - 1, fixed
+    // by the request's first segment)
+    bool ord_hist = false;
+    int64_t ord_interval = 1, ord_offset = 0, ord_key0 = 0;
+    uint32_t ord_keys = 0;
+    std::shared_ptr<DevColumn> ord_col;
     int met = 0;                     // 0 none, 1 avg, 2 stats, 3 extended
     int64_t interval = 1, offset = 0;  // affine roundings: key = floor((v - offset) / interval) * interval + offset
     Rounding rnd;                    // the histogram spec's rounding
@@ -916,7 +923,20 @@ static int add_pipeline(esgpu_plan* p, int root, int fspec, int outer, int inner
             pl.interval = 1;
             pl.offset = 0;
         } else if (n.s.type == ESGPU_AGG_TERMS) { pl.term_spec = b; pl.ord_field = n.field; }
-        else {
+        else if (b == inner && outer >= 0 && p->specs[outer].s.type != ESGPU_AGG_TERMS) {
+            // histogram under histogram: the inner histogram's key indices take the ordinal dimension of the grid
+            pl.term_spec = b;
+            pl.ord_field = n.field;
+            pl.ord_hist = true;
+            Rounding r;
+            try {
+                r = n.rounding();
+            } catch (const std::invalid_argument& e) {
+                throw EsError(ESGPU_ERR_INVALID, std::string(e.what()) + " for histogram aggregation [" + n.name + "]");
+            }
+            require(r.affine(&pl.ord_interval, &pl.ord_offset), ESGPU_ERR_UNSUPPORTED,
+                    "a calendar or DST rounding of an inner histogram runs on the CPU path");
+        } else {
             pl.hist_spec = b;
             pl.hist_field = n.field;
             try {
@@ -1017,7 +1037,6 @@ static Group compile_group(esgpu_plan* p, int r, int fspec) {
         } else {
             cs.bucket = true;
             const bool ot = root.s.type == ESGPU_AGG_TERMS, it = p->specs[ch].s.type == ESGPU_AGG_TERMS;
-            require(ot || it, ESGPU_ERR_UNSUPPORTED, "histogram-under-histogram runs on the CPU path");
             std::vector<int> inner_leaves;
             for (int gc : p->specs[ch].children) {
                 const int t = p->specs[gc].s.type;
@@ -1842,11 +1861,49 @@ static bool collect_multi(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, C
 
 static void ensure_ord_hash(esgpu_ctx* c, const DevColumn* col, hipStream_t st);
 
+// histogram under histogram: this segment's inner key indices as a u32 ordinal column (pl.ord_col), or null when the
+// segment lacks the inner field.  The key range is taken from the request's first segment that has values; a later
+// segment whose values fall outside it is refused (the ordinal dimension of a dense grid cannot grow).
+static const DevColumn* derive_hist_ords(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s) {
+    const DevColumn* src = s->col(pl.ord_field.c_str());
+    if (!src) return nullptr;
+    require(src->type == ESGPU_COL_I64 || src->type == ESGPU_COL_F64, ESGPU_ERR_UNSUPPORTED,
+            "histogram over a keyword field runs on the CPU path");
+    require(!src->multi, ESGPU_ERR_UNSUPPORTED, "a multi-valued inner histogram field runs on the CPU path");
+    const bool has = src->vmin <= src->vmax;
+    const int64_t kmin = has ? floor_div64(src->vmin - pl.ord_offset, pl.ord_interval) : 0;
+    const int64_t kmax = has ? floor_div64(src->vmax - pl.ord_offset, pl.ord_interval) : -1;
+    if (pl.fresh || pl.ord_keys == 0) {
+        if (has) {
+            require(kmax - kmin + 1 <= 65536, ESGPU_ERR_UNSUPPORTED, "an inner histogram over 65536 keys runs on the CPU path");
+            pl.ord_key0 = kmin;
+            pl.ord_keys = (uint32_t)(kmax - kmin + 1);
+        } else if (pl.fresh) {
+            pl.ord_key0 = 0;
+            pl.ord_keys = 0;
+        }
+    } else if (has) {
+        require(kmin >= pl.ord_key0 && kmax < pl.ord_key0 + (int64_t)pl.ord_keys, ESGPU_ERR_UNSUPPORTED,
+                "a later segment extends the inner histogram's key range: runs on the CPU path");
+    }
+    if (!pl.ord_col) pl.ord_col = std::make_shared<DevColumn>();
+    DevColumn& d = *pl.ord_col;
+    d.name = pl.ord_field;
+    d.type = ESGPU_COL_ORD_U32;
+    d.multi = false;
+    d.value_count = std::max<uint32_t>(pl.ord_keys, 1);
+    if (d.values.bytes < (size_t)s->n_pad * 4) d.values.alloc(p->ctx, (size_t)s->n_pad * 4);
+    launch_hist_ords(src->values.as<int64_t>(), src->present.as<uint64_t>(), s->max_doc, s->n_pad, src->type == ESGPU_COL_F64,
+                     pl.ord_interval, pl.ord_offset, pl.ord_key0, pl.ord_keys, d.values.as<uint32_t>(), p->stream);
+    HIPX(hipGetLastError());
+    return &d;
+}
+
 // cardinality leaves of a bucket pipeline: register pass, nonzero recount, linear-counting pass (per segment, in
 // order, so a bucket's set holds every encoded hash of every segment while it can still end in LINEAR_COUNTING)
 static void collect_cards(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
     const bool ORD = pl.term_spec >= 0, HIST = pl.hist_spec >= 0;
-    const DevColumn* oc = ORD ? s->col(pl.ord_field.c_str()) : nullptr;
+    const DevColumn* oc = ORD ? (pl.ord_hist ? pl.ord_col.get() : s->col(pl.ord_field.c_str())) : nullptr;
     const DevColumn* hc = HIST ? s->col(pl.hist_field.c_str()) : nullptr;
     CollectParams G{};
     G.n_docs = s->max_doc;
@@ -1934,7 +1991,7 @@ static constexpr uint32_t kTermsCopies = ESGPU_TERMS_COPIES;
 
 static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
     const bool ORD = pl.term_spec >= 0, HIST = pl.hist_spec >= 0;
-    const DevColumn* oc = ORD ? s->col(pl.ord_field.c_str()) : nullptr;
+    const DevColumn* oc = ORD ? (pl.ord_hist ? derive_hist_ords(p, pl, s) : s->col(pl.ord_field.c_str())) : nullptr;
     const DevColumn* hc = HIST ? s->col(pl.hist_field.c_str()) : nullptr;
     const DevColumn* mc = pl.met > 0 ? s->col(pl.metric_field.c_str()) : nullptr;
     const bool terms_outer = pl.outer == pl.term_spec;
@@ -2017,9 +2074,12 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         if (!same) alloc_grid(p, pl);
         pl.fresh = false;
     } else {
-        if (oc && !pl.tdict)
+        if (oc && !pl.tdict && !pl.ord_hist)
             throw EsError(ESGPU_ERR_UNSUPPORTED, "terms field [" + pl.ord_field + "] unmapped in the first segment under a histogram");
-        if (oc) require(same_dict(oc->ord_dict(), pl.tdict), ESGPU_ERR_INVALID,
+        if (oc && pl.ord_hist)
+            require(pl.T == std::max<uint32_t>(pl.ord_keys, 1), ESGPU_ERR_UNSUPPORTED,
+                    "the inner histogram had no values in the request's first segment: runs on the CPU path");
+        if (oc && !pl.ord_hist) require(same_dict(oc->ord_dict(), pl.tdict), ESGPU_ERR_INVALID,
                          "segments number the terms of [" + pl.ord_field + "] differently: build an ordinal map "
                          "(esgpu_ordinal_map_build) over the reader's segments first");
         if (pl.inner_terms && hc) {
@@ -2088,7 +2148,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     P.ocnt_mode = L_ocnt;
     P.accept = d_accept;
     if (inner_missing) { P.mv = nullptr; P.mv_present = nullptr; P.mv_f64 = 0; }
-    uint64_t bytes_per_doc = (oc ? 4 : 0) + (hc ? (pl.inner_terms ? 4 : 8) : 0) + (mc && !inner_missing ? 8 : 0);
+    uint64_t bytes_per_doc = (oc ? (pl.ord_hist ? 8 : 4) : 0) + (hc ? (pl.inner_terms ? 4 : 8) : 0) + (mc && !inner_missing ? 8 : 0);
     set_preds(p, pl, s, P.pred, &P.npred, &bytes_per_doc);
     P.g_cnt = inner_missing ? pl.g_ocnt.as<unsigned long long>() : pl.g_cnt.as<unsigned long long>();
     P.g_ocnt = pl.g_ocnt.as<unsigned long long>();
@@ -3026,6 +3086,24 @@ static Block build_hist_root(esgpu_plan* p, const Group& g) {
             continue;
         }
         const Pipeline& B0 = p->pipes[kid.pipes[0]];
+        if (B0.ord_hist) {  // histogram under histogram: each outer key's row holds the inner histogram's key cells
+            require(!B0.allocated || (B0.H == P0.H && B0.key0 == P0.key0), ESGPU_ERR_DEVICE, "sibling pipelines disagree on the key grid");
+            for (uint32_t s : slots) {
+                begin_instance(sub, 0);
+                if (B0.allocated && B0.ord_keys) {
+                    const size_t row = (size_t)s * B0.T;
+                    for (uint32_t t = 0; t < B0.T; ++t) {  // HistogramAggregator.buildAggregation: keys ascending
+                        const int64_t c = (int64_t)B0.hc.cnt[row + t];
+                        if (c == 0) continue;
+                        push_bucket(sub, (B0.ord_key0 + (int64_t)t) * B0.ord_interval + B0.ord_offset, nullptr, c);
+                        for (size_t gj = 0; gj < kid.grand.size(); ++gj)
+                            append_leaf(p, p->pipes[kid.grand[gj].pipe], kid.grand[gj].leaf, row + t, sub.subs[gj]);
+                    }
+                }
+                end_instance(sub);
+            }
+            continue;
+        }
         require(!B0.allocated || B0.tdict == nullptr || (B0.H == P0.H && B0.key0 == P0.key0), ESGPU_ERR_DEVICE,
                 "sibling pipelines disagree on the key grid");
         for (uint32_t s : slots) {

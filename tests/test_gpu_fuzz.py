@@ -2,7 +2,7 @@
 mid- / high-cardinality and multi-valued keyword fields, histogram, date_histogram with calendar and fixed intervals,
 offsets, fixed and DST time zones, min_doc_count 0 with extended bounds, every terms order including metric-path
 orders, stats / extended_stats / avg / cardinality leaves, terms under terms, filter aggregations, query term / range
-clauses) over random columns (missing values, unsorted timestamps, ragged sizes).  Each case compares the shard-level
+clauses, histogram under histogram) over random columns (missing values, unsorted timestamps, ragged sizes).  Each case compares the shard-level
 and the reduced results with the oracle (tests/helpers.assert_same) and, when every metric is integer-valued, the
 transport bytes of the shard result with the oracle's writer.
 
@@ -116,11 +116,11 @@ class Gen:
             t.showTermDocCountError(True)
         return t
 
-    def date_histogram(self):
+    def date_histogram(self, affine=False):
         r = self.r
-        interval = str(r.choice(["1h", "1h", "30m", "3h", "1d", "day", "week", "month"]))
+        interval = str(r.choice(["1h", "30m", "3h", "1d"] if affine else ["1h", "1h", "30m", "3h", "1d", "day", "week", "month"]))
         d = AB.dateHistogram(self.name("d")).field("@timestamp").interval(interval)
-        tz = r.choice([None, None, "+01:00", "-05:30", "Europe/Berlin", "America/New_York"])
+        tz = r.choice([None, "+01:00", "-05:30"] if affine else [None, None, "+01:00", "-05:30", "Europe/Berlin", "America/New_York"])
         if tz is not None:
             d.timeZone(str(tz))
         if r.random() < 0.3:
@@ -159,8 +159,8 @@ class Gen:
         if depth == 0 and r.random() < 0.5:
             inner = self.terms(True) if kind == "terms" and r.random() < 0.5 else (
                 self.date_histogram() if kind == "terms" else self.terms(True))
-            if kind != "terms" and inner.type == N.AGG_TERMS:
-                inner = self.terms(True)
+            if kind != "terms" and r.random() < 0.4:  # histogram under histogram (affine inner rounding)
+                inner = self.histogram() if kind == "date_histogram" or r.random() < 0.5 else self.date_histogram(affine=True)
             for _ in range(int(r.integers(0, 2))):
                 inner.subAggregation(self.metric()[0])
             b.subAggregation(inner)

@@ -1,0 +1,96 @@
+"""GPU parity for histogram under histogram (a5; e.g. the latency heat map date_histogram{histogram}): the outer
+histogram is the key dimension of the cell grid, the inner histogram's key indices -- derived per segment from its field
+with its affine rounding -- are the ordinal dimension (HistogramAggregator under asMultiBucketAggregator,
+A/AggregatorFactory.java:107-200; buckets per owning bucket in key order, HistogramAggregator.java:110-133), reduced by
+InternalHistogram.doReduce at both levels (empty-bucket fill included)."""
+import numpy as np
+import pytest
+
+import oracle as O
+from elasticsearch_amd import AggregationBuilders as AB
+from elasticsearch_amd import _native as N
+from elasticsearch_amd import reduce
+from helpers import assert_same, synthetic_columns
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("@timestamp", "response_time_ms", "bytes", "price", "client_ip.hash")
+
+
+def _both(engine, aggs, n=300_000, shards=2, exact=True):
+    data = [(synthetic_columns(FIELDS, n, shard=s), n) for s in range(shards)]
+    want = O.run(data, aggs, number_of_shards=shards)
+    plan = engine.plan(aggs, number_of_shards=shards)
+    results = []
+    for s, (cols, _) in enumerate(data):
+        seg = engine.upload_segment(cols, n)
+        plan.reset()
+        plan.collect(seg)
+        r = plan.build()
+        assert_same(r.to_dict(), want["shards"][s], f"shard{s}", exact)
+        results.append(r)
+        seg.close()
+    red = reduce(results).to_dict()
+    assert_same(red, want["reduced"], "reduced", exact)
+    plan.close()
+    return red
+
+
+def test_latency_heat_map(engine):
+    aggs = [AB.dateHistogram("per_hour").field("@timestamp").interval("1h").minDocCount(1).subAggregation(
+        AB.histogram("latency").field("response_time_ms").interval(100).minDocCount(1)
+        .subAggregation(AB.avg("b").field("bytes")))]
+    red = _both(engine, aggs)
+    assert len(red["per_hour"]["buckets"]) > 10 and len(red["per_hour"]["buckets"][0]["latency"]["buckets"]) > 3
+
+
+def test_inner_empty_buckets_bounds_and_stats(engine):
+    """inner min_doc_count 0 with extended bounds (EmptyBucketInfo at both levels), an offset, extended_stats leaves"""
+    aggs = [AB.dateHistogram("d").field("@timestamp").interval("1d").subAggregation(
+        AB.histogram("rt").field("response_time_ms").interval(250).offset(10).extendedBounds(-500, 1500)
+        .subAggregation(AB.extendedStats("x").field("response_time_ms")))]
+    _both(engine, aggs)
+
+
+def test_inner_date_histogram_fixed_zone_and_double_field(engine):
+    """outer histogram over a double field, inner date_histogram with a fixed time zone (affine) and cardinality"""
+    aggs = [AB.histogram("p").field("price").interval(50).minDocCount(1).subAggregation(
+        AB.dateHistogram("days").field("@timestamp").interval("1d").timeZone("+02:00").minDocCount(1)
+        .subAggregation(AB.cardinality("ips").field("client_ip.hash"))
+        .subAggregation(AB.stats("s").field("bytes")))]
+    _both(engine, aggs, exact=False)
+
+
+def test_inner_calendar_rounding_refused(engine):
+    """a DST zone or a calendar unit is not affine: the plan refuses it (the plugin keeps the stock aggregator)"""
+    aggs = [AB.histogram("b").field("bytes").interval(100000).subAggregation(
+        AB.dateHistogram("m").field("@timestamp").interval("month"))]
+    with pytest.raises(N.UnsupportedOnGpu):
+        engine.plan(aggs)
+
+
+def test_inner_field_missing_in_a_segment(engine):
+    """the second segment lacks the inner field: its docs count in the outer buckets only"""
+    n = 200_000
+    c0 = synthetic_columns(FIELDS, n, shard=0)
+    c1 = synthetic_columns(FIELDS, n, shard=1)
+    del c1["response_time_ms"]
+    aggs = [AB.dateHistogram("d").field("@timestamp").interval("6h").subAggregation(
+        AB.histogram("rt").field("response_time_ms").interval(200))]
+    both = {k: v for k, v in c0.items()}
+    for k in c0:
+        if k != "response_time_ms":
+            both[k] = {"type": c0[k]["type"], "values": np.concatenate([c0[k]["values"], c1[k]["values"]])}
+    both["response_time_ms"] = {"type": c0["response_time_ms"]["type"],
+                                "values": np.concatenate([c0["response_time_ms"]["values"], np.zeros(n, np.int64)]),
+                                "present": np.concatenate([np.full(n // 64, ~np.uint64(0), np.uint64),
+                                                           np.zeros(n // 64, np.uint64)])}
+    want = O.run([(both, 2 * n)], aggs)
+    plan = engine.plan(aggs)
+    segs = [engine.upload_segment(c0, n), engine.upload_segment(c1, n)]
+    for s in segs:
+        plan.collect(s)
+    assert_same(plan.build().to_dict(), want["shards"][0], "shard")
+    plan.close()
+    for s in segs:
+        s.close()
