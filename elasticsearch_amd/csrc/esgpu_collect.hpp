@@ -110,7 +110,20 @@ __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0,
     if (P.accept) ok &= bits4(P.accept, doc0);
     for (int k = 0; k < P.npred; ++k) ok &= eval_pred(P.pred[k], doc0);
     d.ok = ok;
-    if (ORD) load_u32x4(P.ord, doc0, d.ord);
+    if (ORD && (VK & 8)) {  // inner histogram key index, derived in registers (HistogramAggregator under a histogram)
+        int64_t v[4];
+        load_i64x4(P.ord_src, doc0, v);
+        const uint32_t pres = P.ord_src_present ? bits4(P.ord_src_present, doc0) : 0xFu;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t x = P.ord_src_f64 ? java_long(bits_dbl((uint64_t)v[j])) : v[j];  // longValues of a double
+            const uint64_t u = (uint64_t)x - (uint64_t)P.ord_base;
+            d.ord[j] = ((pres >> j) & 1) && u < P.ord_span ? magic_div((uint32_t)u, P.omg_m, P.omg_s1, P.omg_s2, P.ord_div)
+                                                           : kMissingOrd;
+        }
+    } else if (ORD) {
+        load_u32x4(P.ord, doc0, d.ord);
+    }
     if (HIST && (VK & 4)) {  // the key dimension is a second terms aggregation: u32 ordinals, missing = kMissingOrd
         uint32_t o[4];
         load_u32x4((const uint32_t*)P.hv, doc0, o);
@@ -353,6 +366,23 @@ __device__ __forceinline__ void runs_add(const CollectParams& P, const Acc& a, R
     }
 }
 
+#ifndef ESGPU_COMBINE4  // counting ORD x histogram grids: combine a thread's equal keys before the LDS atomics
+#define ESGPU_COMBINE4 1
+#endif
+// calls emit(key, multiplicity) once per distinct key of k[0..3] (~0u = none)
+template <class F>
+__device__ __forceinline__ void combine4(uint32_t (&k)[kVec], F emit) {
+#pragma unroll
+    for (int j = 0; j < kVec; ++j) {
+        if (k[j] == ~0u) continue;
+        uint32_t n = 1;
+#pragma unroll
+        for (int i = j + 1; i < kVec; ++i)
+            if (k[i] == k[j]) { ++n; k[i] = ~0u; }
+        emit(k[j], n);
+    }
+}
+
 template <bool ORD, bool HIST, int MET, bool LDS, bool KT, int MS, bool HORD = false>
 __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, const Doc4& d, uint32_t T, int64_t base,
                                          uint32_t win0, Runs<runs_for<MET>()>& run, uint32_t mw = 0, bool outer = true) {
@@ -390,6 +420,43 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
             if (!((d.ok >> j) & 1) || !hv_ok[j]) continue;
             runs_add<MET, MS>(P, a, run, slot[j], MET > 0 && ((d.mpres >> j) & 1), MET > 0 ? d.mv[j] : 0.0);
         }
+        return;
+    }
+    if constexpr (LDS && ORD && HIST && MET == 0 && ESGPU_COMBINE4) if (P.ocnt_mode != OCNT_TERMS) {
+        // counting grids: a thread's 4 docs usually share the outer key (time-sorted data) and often the cell (skewed
+        // inner keys): equal keys are combined in registers, and an outer key shared by the whole wave takes one LDS
+        // atomic for the wave instead of 64 on one address
+        uint32_t hk[kVec], cell[kVec];
+#pragma unroll
+        for (int j = 0; j < kVec; ++j) {
+            const bool hit = ((d.ok >> j) & 1) && hv_ok[j];
+            const uint32_t t = d.ord[j];
+            hk[j] = hit ? slot[j] : ~0u;
+            cell[j] = hit && t != kMissingOrd && t < T ? slot[j] * T + t : ~0u;
+        }
+        if (P.ocnt_mode == OCNT_HIST) {
+            uint32_t key = ~0u, n = 0;
+            bool single = true;
+#pragma unroll
+            for (int j = 0; j < kVec; ++j) {
+                if (hk[j] == ~0u) continue;
+                if (n == 0) key = hk[j];
+                single = single && hk[j] == key;
+                ++n;
+            }
+            const uint64_t live = __ballot(n > 0);
+            if (live) {
+                const int src = __ffsll((unsigned long long)live) - 1;
+                const uint32_t k0 = __shfl(key, src, 64);
+                if (__all(n == 0 || (single && key == k0))) {
+                    const uint32_t tot = wave_sum_u32(n);
+                    if ((int)(threadIdx.x & 63) == src) atomicAdd(&a.ocnt32[k0], tot);
+                } else {
+                    combine4(hk, [&](uint32_t k, uint32_t m) { atomicAdd(&a.ocnt32[k], m); });
+                }
+            }
+        }
+        combine4(cell, [&](uint32_t c, uint32_t m) { atomicAdd(&a.cnt32[c + a.coff], m); });
         return;
     }
 #pragma unroll
@@ -671,7 +738,7 @@ __global__ __launch_bounds__(256) void zone_keys_kernel(CollectParams P, int64_t
 // calls f(std::integral_constant<int, VK>) for the value kinds the plan uses; bits that cannot matter (no histogram
 // dimension, no metric) are never instantiated
 template <int HK, int MET, class F>
-static auto with_vk(bool hv_f64, bool mv_f64, F f) {
+static auto with_vk0(bool hv_f64, bool mv_f64, F f) {
     const bool hf = HK != 0 && hv_f64, mf = MET > 0 && mv_f64;
     if constexpr (HK == 3) {  // ordinal keys: only the metric's kind varies
         if constexpr (MET > 0) {
@@ -693,6 +760,15 @@ static auto with_vk(bool hv_f64, bool mv_f64, F f) {
         return f(std::integral_constant<int, 0>{});
     }
 }
+// VK bit 8: the terms dimension is a derived histogram key index (CollectParams.ord_src); only for ORD x histogram grids
+template <bool ORD, int HK, int MET, class F>
+static auto with_vk(bool hv_f64, bool mv_f64, bool dord, F f) {
+    if constexpr (ORD && (HK == 1 || HK == 2)) {
+        if (dord)
+            return with_vk0<HK, MET>(hv_f64, mv_f64, [&](auto vk) { return f(std::integral_constant<int, decltype(vk)::value | 8>{}); });
+    }
+    return with_vk0<HK, MET>(hv_f64, mv_f64, f);
+}
 
 // wide = 1024-thread workgroups (instantiated for histogram grids only)
 template <bool ORD, int HK, int MET, class F>
@@ -705,7 +781,7 @@ static auto with_wg(bool wide, F f) {
 
 template <bool ORD, int HK, int MET>
 static void launch_t(const CollectParams& p, bool wide, uint32_t grid, size_t lds, hipStream_t st) {
-    with_vk<HK, MET>(p.hv_f64 != 0, p.mv_f64 != 0, [&](auto vk) {
+    with_vk<ORD, HK, MET>(p.hv_f64 != 0, p.mv_f64 != 0, p.ord_src != nullptr, [&](auto vk) {
         return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
             hipLaunchKernelGGL((collect_kernel<ORD, HK, MET, decltype(vk)::value, decltype(wg)::value>), dim3(grid),
                                dim3(decltype(wg)::value), lds, st, p);
@@ -726,7 +802,7 @@ static void launch_m(const CollectParams& p, int met, bool wide, uint32_t grid, 
 
 template <bool ORD, int HK, int MET>
 static int occ_t(size_t lds, int vkbits, bool wide) {
-    return with_vk<HK, MET>((vkbits & 1) != 0, (vkbits & 2) != 0, [&](auto vk) {
+    return with_vk<ORD, HK, MET>((vkbits & 1) != 0, (vkbits & 2) != 0, (vkbits & 8) != 0, [&](auto vk) {
         return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
             int n = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(

@@ -50,6 +50,14 @@ struct CollectParams {
     // terms dimension
     const uint32_t* ord;
     uint32_t T;
+    // histogram under histogram, fused (loader VK bit 8): the terms dimension is the inner histogram's key index,
+    // derived from its i64 / f64 column as t = (v - ord_base) / ord_div when 0 <= v - ord_base < ord_span (a 32-bit
+    // magic division; ord_span = keys x interval < 2^32), else missing -- no materialised ordinal column
+    const int64_t* ord_src;
+    const uint64_t* ord_src_present;
+    int32_t ord_src_f64;
+    int64_t ord_base;
+    uint32_t ord_span, ord_div, omg_m, omg_s1, omg_s2;
     // histogram dimension
     uint32_t H, W;
     int32_t windowed;    // 1: W < H, slide a W-slot window using the zone maps

@@ -1864,7 +1864,10 @@ static void ensure_ord_hash(esgpu_ctx* c, const DevColumn* col, hipStream_t st);
 // histogram under histogram: this segment's inner key indices as a u32 ordinal column (pl.ord_col), or null when the
 // segment lacks the inner field.  The key range is taken from the request's first segment that has values; a later
 // segment whose values fall outside it is refused (the ordinal dimension of a dense grid cannot grow).
-static const DevColumn* derive_hist_ords(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s) {
+// materialize = false: only the key range is checked / taken; pl.ord_col describes the dimension (T) and its values
+// are written later by materialize_hist_ords when the launch cannot derive the keys in its loader.
+static void materialize_hist_ords(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s);
+static const DevColumn* derive_hist_ords(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, bool materialize = true) {
     const DevColumn* src = s->col(pl.ord_field.c_str());
     if (!src) return nullptr;
     require(src->type == ESGPU_COL_I64 || src->type == ESGPU_COL_F64, ESGPU_ERR_UNSUPPORTED,
@@ -1892,11 +1895,16 @@ static const DevColumn* derive_hist_ords(esgpu_plan* p, Pipeline& pl, const esgp
     d.type = ESGPU_COL_ORD_U32;
     d.multi = false;
     d.value_count = std::max<uint32_t>(pl.ord_keys, 1);
+    if (materialize) materialize_hist_ords(p, pl, s);
+    return &d;
+}
+static void materialize_hist_ords(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s) {
+    const DevColumn* src = s->col(pl.ord_field.c_str());
+    DevColumn& d = *pl.ord_col;
     if (d.values.bytes < (size_t)s->n_pad * 4) d.values.alloc(p->ctx, (size_t)s->n_pad * 4);
     launch_hist_ords(src->values.as<int64_t>(), src->present.as<uint64_t>(), s->max_doc, s->n_pad, src->type == ESGPU_COL_F64,
                      pl.ord_interval, pl.ord_offset, pl.ord_key0, pl.ord_keys, d.values.as<uint32_t>(), p->stream);
     HIPX(hipGetLastError());
-    return &d;
 }
 
 // cardinality leaves of a bucket pipeline: register pass, nonzero recount, linear-counting pass (per segment, in
@@ -1987,11 +1995,14 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
 #ifndef ESGPU_COPIES_HIST
 #define ESGPU_COPIES_HIST 0  // terms x histogram grids: copies measured within noise
 #endif
+#ifndef ESGPU_FUSE_HIST_ORDS
+#define ESGPU_FUSE_HIST_ORDS 1  // histogram under histogram: inner key index derived in the collect kernel's loader
+#endif
 static constexpr uint32_t kTermsCopies = ESGPU_TERMS_COPIES;
 
 static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
     const bool ORD = pl.term_spec >= 0, HIST = pl.hist_spec >= 0;
-    const DevColumn* oc = ORD ? (pl.ord_hist ? derive_hist_ords(p, pl, s) : s->col(pl.ord_field.c_str())) : nullptr;
+    const DevColumn* oc = ORD ? (pl.ord_hist ? derive_hist_ords(p, pl, s, false) : s->col(pl.ord_field.c_str())) : nullptr;
     const DevColumn* hc = HIST ? s->col(pl.hist_field.c_str()) : nullptr;
     const DevColumn* mc = pl.met > 0 ? s->col(pl.metric_field.c_str()) : nullptr;
     const bool terms_outer = pl.outer == pl.term_spec;
@@ -2014,6 +2025,16 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         const DevColumn* fc = applies(p, pl, k) ? s->col(p->filter_fields[k].c_str()) : nullptr;
         if (fc && fc->multi) multi = true;
     }
+    // histogram under histogram: the collect kernel's loader derives the inner key index from the field (no ordinal
+    // column written and re-read) unless a kernel that reads the materialised column runs on this segment (the CSR
+    // kernel, cardinality leaves) or the key span does not fit the loader's 32-bit division
+    const DevColumn* osrc = pl.ord_hist && oc ? s->col(pl.ord_field.c_str()) : nullptr;
+    int64_t ord_base = 0;
+    const bool fuse_ords = osrc && ESGPU_FUSE_HIST_ORDS && !multi && pl.cards.empty() && pl.ord_interval > 0 &&
+                           pl.ord_interval < (1ll << 32) && (uint64_t)pl.ord_keys * (uint64_t)pl.ord_interval < (1ull << 32) &&
+                           !__builtin_mul_overflow(pl.ord_key0, pl.ord_interval, &ord_base) &&
+                           !__builtin_add_overflow(ord_base, pl.ord_offset, &ord_base);
+    if (osrc && !fuse_ords) materialize_hist_ords(p, pl, s);
     // an unmapped metric field collects nothing (ValuesSource null => NO_OP collector); counts stay separate
     const int met_launch = mc ? pl.met : 0;
     const bool first_segment = pl.fresh;
@@ -2122,6 +2143,17 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     P.n_blocks = s->n_pad / kBlockDocs;
     if (P.n_blocks == 0) return 0;
     P.ord = oc ? oc->ords().as<uint32_t>() : nullptr;
+    if (fuse_ords && L_ORD) {
+        P.ord = nullptr;
+        P.ord_src = osrc->values.as<int64_t>();
+        P.ord_src_present = osrc->present.as<uint64_t>();
+        P.ord_src_f64 = osrc->type == ESGPU_COL_F64;
+        P.ord_base = ord_base;
+        P.ord_span = (uint32_t)((uint64_t)pl.ord_keys * (uint64_t)pl.ord_interval);
+        P.ord_div = (uint32_t)pl.ord_interval;
+        const MagicU32 mg = make_magic(P.ord_div);
+        P.omg_m = mg.m; P.omg_s1 = mg.s1; P.omg_s2 = mg.s2;
+    }
     P.T = LT;
     P.H = LH;
     P.hv = hc ? hc->values.as<int64_t>() : nullptr;
@@ -2230,8 +2262,8 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         P.mg_m = mg.m; P.mg_s1 = mg.s1; P.mg_s2 = mg.s2;
     }
     const int hk = L_HIST ? (P.hord ? 3 : P.kstart ? 2 : 1) : 0;
-    const int vk = (P.hv_f64 ? 1 : 0) | (P.mv_f64 ? 2 : 0);
-    const uint64_t occ_key = ((uint64_t)lds << 11) | ((uint64_t)wide << 10) | ((uint64_t)vk << 8) | ((uint64_t)L_met << 4) |
+    const int vk = (P.hv_f64 ? 1 : 0) | (P.mv_f64 ? 2 : 0) | (P.ord_src ? 8 : 0);
+    const uint64_t occ_key = ((uint64_t)lds << 16) | ((uint64_t)wide << 15) | ((uint64_t)vk << 8) | ((uint64_t)L_met << 4) |
                              ((uint64_t)hk << 1) | (L_ORD ? 1 : 0);
     if (pl.occ_key != occ_key) {
         pl.occ = std::max(1, collect_occupancy(L_ORD, hk, L_met, lds, vk, wide));

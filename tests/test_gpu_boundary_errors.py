@@ -27,14 +27,14 @@ def _plan_and_collect(engine, aggs, fields, n=100_000):
         seg.close()
 
 
-@pytest.mark.parametrize("case", ["terms_under_high_cardinality_terms", "histogram_under_histogram", "three_bucket_levels"])
+@pytest.mark.parametrize("case", ["terms_under_high_cardinality_terms", "calendar_histogram_under_histogram", "three_bucket_levels"])
 def test_unsupported_shapes_raise(engine, case):
     if case == "terms_under_high_cardinality_terms":  # 1,000 x 10M cells: no dense grid
         aggs = [AB.terms("hosts").field("host").subAggregation(AB.terms("urls").field("url"))]
         fields = ("host", "url")
-    elif case == "histogram_under_histogram":
-        aggs = [AB.dateHistogram("d").field("@timestamp").interval("1d").subAggregation(
-            AB.histogram("b").field("bytes").interval(1024))]
+    elif case == "calendar_histogram_under_histogram":  # the inner key index needs an affine rounding
+        aggs = [AB.histogram("b").field("bytes").interval(4096).subAggregation(
+            AB.dateHistogram("m").field("@timestamp").interval("month"))]
         fields = ("@timestamp", "bytes")
     else:
         aggs = [AB.terms("hosts").field("host").subAggregation(

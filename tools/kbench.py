@@ -37,6 +37,10 @@ def variants():
                     [QB.termQuery("status", 200), QB.rangeQuery("bytes").gte(1024).lte(65536)]),
         "config4_card": ([AB.cardinality("ips").field("client_ip.hash").precisionThreshold(40000)], None),
         "config3_url": ([AB.terms("urls").field("url").size(10)], None),
+        "dh_terms": ([AB.dateHistogram("h").field("@timestamp").interval("1h").subAggregation(
+            AB.terms("hosts").field("host").size(10))], None),
+        "heatmap": ([AB.dateHistogram("h").field("@timestamp").interval("1h").subAggregation(
+            AB.histogram("lat").field("response_time_ms").interval(100))], None),
     }
 
 
