@@ -1215,6 +1215,52 @@ void launch_topk(const TopkParams& p, hipStream_t s) {
                        p.out_keys);
 }
 
+// K3 per owning bucket for terms under a histogram (GlobalOrdinalsStringTermsAggregator.buildAggregation :146-208 once
+// per outer key, count orders): one wave per row.  Each lane keeps the best key of its strided share of the row; the
+// wave's maximum is a pick, and only the lane that held it rescans its share for the best key below it -- S picks cost
+// S wave reductions plus S rescans of T / 64 cells, where the host spent a pass over all T cells and a partial sort.
+__device__ __forceinline__ unsigned long long row_key(unsigned long long c, uint32_t t, bool asc, int64_t min_count) {
+    if ((int64_t)c < min_count) return 0ull;
+    const unsigned long long hi = asc ? (0xFFFFFFFFull - c) : c;  // counts < 2^32 (docs per shard)
+    return (hi << 32) | (unsigned long long)(0xFFFFFFFFu - t);   // never 0: t < 2^32 - 1
+}
+__global__ __launch_bounds__(64) void row_topk_kernel(const unsigned long long* cnt, uint32_t T, uint32_t S, int asc,
+                                                      int64_t min_count, unsigned long long* out,
+                                                      unsigned long long* total) {
+    const uint32_t row = blockIdx.x;
+    const unsigned long long* r = cnt + (size_t)row * T;
+    const uint32_t lane = threadIdx.x;
+    unsigned long long tot = 0, best = 0;
+    for (uint32_t t = lane; t < T; t += 64) {
+        const unsigned long long c = r[t];
+        tot += c;
+        const unsigned long long k = row_key(c, t, asc != 0, min_count);
+        best = k > best ? k : best;
+    }
+    tot = wave_sum_u64(tot);
+    uint32_t n = 0;
+    for (; n < S; ++n) {
+        const unsigned long long m = wave_max_u64(best);
+        if (m == 0ull) break;
+        if (lane == 0) out[(size_t)row * S + n] = m;
+        if (best == m) {
+            unsigned long long nb = 0;
+            for (uint32_t t = lane; t < T; t += 64) {
+                const unsigned long long k = row_key(r[t], t, asc != 0, min_count);
+                nb = (k < m && k > nb) ? k : nb;
+            }
+            best = nb;
+        }
+    }
+    for (uint32_t i = n + lane; i < S; i += 64) out[(size_t)row * S + i] = 0ull;
+    if (lane == 0) total[row] = tot;
+}
+void launch_row_topk(const unsigned long long* cnt, uint32_t T, uint32_t H, uint32_t S, bool asc, int64_t min_count,
+                     unsigned long long* out, unsigned long long* total, hipStream_t st) {
+    if (H == 0) return;
+    hipLaunchKernelGGL(row_topk_kernel, dim3(H), dim3(64), 0, st, cnt, T, S, asc ? 1 : 0, min_count, out, total);
+}
+
 }  // namespace esgpu
 
 // ------------------------------------------------------------------------------------------------------------

@@ -305,6 +305,12 @@ struct TopkParams {
 };
 constexpr uint32_t kTopkMax = 1024;
 void launch_topk(const TopkParams& p, hipStream_t s);
+// terms under a histogram, count orders: per row r of the [H][T] count grid, the row's total (total[r]) and its top S
+// candidates (count >= min_count) as u64 keys in selection order, count-major (asc: complemented), ties by ascending
+// ordinal -- out[r * S + i], 0 past the last candidate.  S <= kRowTopkMax.
+constexpr uint32_t kRowTopkMax = 1024;
+void launch_row_topk(const unsigned long long* cnt, uint32_t T, uint32_t H, uint32_t S, bool asc, int64_t min_count,
+                     unsigned long long* out, unsigned long long* total, hipStream_t st);
 uint64_t topk_key(int order, uint64_t count, uint32_t ord);   // host mirror of the device key (for tests)
 
 }  // namespace esgpu

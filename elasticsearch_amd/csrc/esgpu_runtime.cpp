@@ -842,6 +842,7 @@ struct Pipeline {
     // build: the pipeline's cells on the host (gathered winner rows or the whole grid) and their staging buffers
     HostCells hc;
     PinnedBuf h_cells[6], h_ocnt;
+    PinnedBuf h_picks, h_rowtot;     // terms under a histogram: per-row picks and totals (row_topk_kernel)
 };
 
 // One aggregation subtree (a top-level aggregation, or a child of a top-level filter aggregation) compiled to one or
@@ -1995,6 +1996,9 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
 #ifndef ESGPU_COPIES_HIST
 #define ESGPU_COPIES_HIST 0  // terms x histogram grids: copies measured within noise
 #endif
+#ifndef ESGPU_ROW_TOPK
+#define ESGPU_ROW_TOPK 1  // terms under a histogram, count orders: per-row selection on the GPU at build
+#endif
 #ifndef ESGPU_FUSE_HIST_ORDS
 #define ESGPU_FUSE_HIST_ORDS 1  // histogram under histogram: inner key index derived in the collect kernel's loader
 #endif
@@ -3079,11 +3083,37 @@ static Block build_hist_root(esgpu_plan* p, const Group& g) {
     Block r = hist_shell(p, g.root, child_protos(p, g));
     Pipeline& P0 = p->pipes[g.pipes[0]];
     if (!P0.allocated) { r.append_empty(); return r; }
+    const bool p0_terms = P0.term_spec >= 0;
+    // terms children in a count order select each outer key's terms on the GPU (row_topk_kernel, picks written into
+    // pinned memory); the whole grid reaches the host only for pipelines whose cells the build still reads
+    std::vector<uint32_t> pick_s(g.kids.size(), 0);
+    std::vector<char> need(p->pipes.size(), 0);
+    if (!p0_terms) need[g.pipes[0]] = 1;
+    for (size_t ki = 0; ki < g.kids.size(); ++ki) {
+        const ChildSrc& kid = g.kids[ki];
+        if (!kid.bucket) { need[kid.leaf.pipe] = 1; continue; }
+        for (const LeafRef& gr : kid.grand) need[gr.pipe] = 1;
+        Pipeline& B0 = p->pipes[kid.pipes[0]];
+        const SpecNode& tn = p->specs[kid.spec];
+        const bool count_order = tn.s.order == ESGPU_ORDER_COUNT_DESC || tn.s.order == ESGPU_ORDER_COUNT_ASC;
+        const uint64_t S = std::min<uint64_t>(B0.value_count, (uint64_t)std::max<int64_t>(tn.s.shard_size, 0));
+        if (ESGPU_ROW_TOPK && !B0.ord_hist && B0.allocated && B0.tdict && count_order && B0.value_count == B0.T && S > 0 &&
+            S <= kRowTopkMax) {
+            pick_s[ki] = (uint32_t)S;
+            B0.h_picks.ensure((size_t)B0.H * S * 8);
+            B0.h_rowtot.ensure((size_t)B0.H * 8);
+            const int64_t min_count = std::max<int64_t>(tn.s.shard_min_doc_count, tn.s.min_doc_count > 0 ? 1 : 0);
+            launch_row_topk(B0.g_cnt.as<unsigned long long>(), B0.T, B0.H, (uint32_t)S, tn.s.order == ESGPU_ORDER_COUNT_ASC,
+                            min_count, (unsigned long long*)B0.h_picks.dev(), (unsigned long long*)B0.h_rowtot.dev(), st);
+            HIPX(hipGetLastError());
+        } else {
+            need[kid.pipes[0]] = 1;
+        }
+    }
     for (int pi : g.pipes) {
         Pipeline& pl = p->pipes[pi];
-        if (pl.allocated) fetch_grid(p, pl);
+        if (pl.allocated && (need[pi] || !pl.cards.empty() || !ESGPU_ROW_TOPK)) fetch_grid(p, pl);
     }
-    const bool p0_terms = P0.term_spec >= 0;
     unsigned long long* ocnt = nullptr;
     if (p0_terms) {  // histogram doc counts counted per doc beside the [H][T] cells (OCNT_HIST)
         d2h_u64(p, P0.h_ocnt, P0.g_ocnt.p, P0.H);
@@ -3148,9 +3178,22 @@ static Block build_hist_root(esgpu_plan* p, const Group& g) {
             }
             int64_t other = 0;
             const size_t row = (size_t)s * B0.T;
-            std::vector<TermPick> top = select_terms(tn.s, B0.hc.cnt + row, (uint32_t)B0.value_count, &other, [&](uint32_t ord) {
-                return order_value(p, tn, p->pipes[ord_ref.pipe], ord_ref.leaf, row + ord);
-            });
+            std::vector<TermPick> top;
+            if (const uint32_t S = pick_s[ki]) {  // the GPU's picks: count-major keys in the order's sequence
+                const unsigned long long* pk = B0.h_picks.as<unsigned long long>() + (size_t)s * S;
+                const bool asc = tn.s.order == ESGPU_ORDER_COUNT_ASC;
+                other = (int64_t)B0.h_rowtot.as<unsigned long long>()[s];
+                for (uint32_t i = 0; i < S && pk[i]; ++i) {
+                    const uint64_t hi = pk[i] >> 32;
+                    const int64_t c = (int64_t)(asc ? 0xFFFFFFFFull - hi : hi);
+                    top.push_back({0xFFFFFFFFu - (uint32_t)pk[i], c});
+                    other -= c;
+                }
+            } else {
+                top = select_terms(tn.s, B0.hc.cnt + row, (uint32_t)B0.value_count, &other, [&](uint32_t ord) {
+                    return order_value(p, tn, p->pipes[ord_ref.pipe], ord_ref.leaf, row + ord);
+                });
+            }
             begin_instance(sub, other);
             for (auto& tp : top) {
                 const std::string term = plan_term(p, B0, tp.ord);
