@@ -1224,9 +1224,15 @@ __device__ __forceinline__ unsigned long long row_key(unsigned long long c, uint
     const unsigned long long hi = asc ? (0xFFFFFFFFull - c) : c;  // counts < 2^32 (docs per shard)
     return (hi << 32) | (unsigned long long)(0xFFFFFFFFu - t);   // never 0: t < 2^32 - 1
 }
+// the row's keys are staged in LDS when they fit (the rescans then read LDS, not L2 at ~1 us a dependent round), and the
+// picks are staged in LDS and written out coalesced at the end
+constexpr uint32_t kRowTopkLdsKeys = 4096;  // 32 KB of keys
+template <bool LROW>
 __global__ __launch_bounds__(64) void row_topk_kernel(const unsigned long long* cnt, uint32_t T, uint32_t S, int asc,
                                                       int64_t min_count, unsigned long long* out,
                                                       unsigned long long* total) {
+    __shared__ unsigned long long picks[kRowTopkMax];
+    extern __shared__ unsigned long long rowk[];
     const uint32_t row = blockIdx.x;
     const unsigned long long* r = cnt + (size_t)row * T;
     const uint32_t lane = threadIdx.x;
@@ -1235,6 +1241,7 @@ __global__ __launch_bounds__(64) void row_topk_kernel(const unsigned long long* 
         const unsigned long long c = r[t];
         tot += c;
         const unsigned long long k = row_key(c, t, asc != 0, min_count);
+        if (LROW) rowk[t] = k;
         best = k > best ? k : best;
     }
     tot = wave_sum_u64(tot);
@@ -1242,23 +1249,27 @@ __global__ __launch_bounds__(64) void row_topk_kernel(const unsigned long long* 
     for (; n < S; ++n) {
         const unsigned long long m = wave_max_u64(best);
         if (m == 0ull) break;
-        if (lane == 0) out[(size_t)row * S + n] = m;
+        if (lane == 0) picks[n] = m;
         if (best == m) {
             unsigned long long nb = 0;
             for (uint32_t t = lane; t < T; t += 64) {
-                const unsigned long long k = row_key(r[t], t, asc != 0, min_count);
+                const unsigned long long k = LROW ? rowk[t] : row_key(r[t], t, asc != 0, min_count);
                 nb = (k < m && k > nb) ? k : nb;
             }
             best = nb;
         }
     }
-    for (uint32_t i = n + lane; i < S; i += 64) out[(size_t)row * S + i] = 0ull;
+    __syncthreads();
+    for (uint32_t i = lane; i < S; i += 64) out[(size_t)row * S + i] = i < n ? picks[i] : 0ull;
     if (lane == 0) total[row] = tot;
 }
 void launch_row_topk(const unsigned long long* cnt, uint32_t T, uint32_t H, uint32_t S, bool asc, int64_t min_count,
                      unsigned long long* out, unsigned long long* total, hipStream_t st) {
     if (H == 0) return;
-    hipLaunchKernelGGL(row_topk_kernel, dim3(H), dim3(64), 0, st, cnt, T, S, asc ? 1 : 0, min_count, out, total);
+    if (T <= kRowTopkLdsKeys)
+        hipLaunchKernelGGL(row_topk_kernel<true>, dim3(H), dim3(64), (size_t)T * 8, st, cnt, T, S, asc ? 1 : 0, min_count, out, total);
+    else
+        hipLaunchKernelGGL(row_topk_kernel<false>, dim3(H), dim3(64), 0, st, cnt, T, S, asc ? 1 : 0, min_count, out, total);
 }
 
 }  // namespace esgpu

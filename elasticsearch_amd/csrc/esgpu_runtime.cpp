@@ -136,11 +136,25 @@ static const char* synth_name(uint32_t bit) {
 }
 
 extern "C" int esgpu_synthetic_term(uint32_t field_bit, uint64_t ord, char* buf, size_t cap) {
+    // formatted by hand ("host-%04u" / "/p/%08x"): builds resolve every winning ordinal of a synthetic field here
     char tmp[32];
     int n = 0;
-    if (field_bit == ESGPU_SYNTH_HOST) n = snprintf(tmp, sizeof tmp, "host-%04u", (unsigned)ord);
-    else if (field_bit == ESGPU_SYNTH_URL) n = snprintf(tmp, sizeof tmp, "/p/%08x", (unsigned)ord);
-    else return -1;
+    const uint32_t o = (uint32_t)ord;
+    if (field_bit == ESGPU_SYNTH_HOST) {
+        char d[10];
+        int k = 0;
+        for (uint32_t v = o; v || k < 4; v /= 10) d[k++] = (char)('0' + v % 10);
+        std::memcpy(tmp, "host-", 5);
+        n = 5;
+        while (k) tmp[n++] = d[--k];
+    } else if (field_bit == ESGPU_SYNTH_URL) {
+        std::memcpy(tmp, "/p/", 3);
+        for (int i = 0; i < 8; ++i) tmp[3 + i] = "0123456789abcdef"[(o >> (28 - 4 * i)) & 15];
+        n = 11;
+    } else {
+        return -1;
+    }
+    tmp[n] = 0;
     if (buf && cap) {
         const size_t c = std::min((size_t)n, cap - 1);
         std::memcpy(buf, tmp, c);
@@ -2609,6 +2623,13 @@ static void begin_instance(Block& b, int64_t other) {
     b.other_doc_count.push_back(other);
 }
 static void end_instance(Block& b) { b.boff.push_back(b.key.size()); }
+static void push_bucket(Block& b, int64_t key, std::string_view term, int64_t count) {
+    b.key.push_back(key);
+    b.term_pool += term;
+    b.term_off.push_back(b.term_pool.size());
+    b.bcount.push_back(count);
+    b.berr.push_back(0);
+}
 static void push_bucket(Block& b, int64_t key, const std::string* term, int64_t count) {
     b.key.push_back(key);
     if (term) b.term_pool += *term;
@@ -3114,12 +3135,14 @@ static Block build_hist_root(esgpu_plan* p, const Group& g) {
         Pipeline& pl = p->pipes[pi];
         if (pl.allocated && (need[pi] || !pl.cards.empty() || !ESGPU_ROW_TOPK)) fetch_grid(p, pl);
     }
+    bmark(p, "hist_issued");
     unsigned long long* ocnt = nullptr;
     if (p0_terms) {  // histogram doc counts counted per doc beside the [H][T] cells (OCNT_HIST)
         d2h_u64(p, P0.h_ocnt, P0.g_ocnt.p, P0.H);
         ocnt = P0.h_ocnt.as<unsigned long long>();
     }
     bsync(p);
+    bmark(p, "hist_synced");
     for (int pi : g.pipes) {
         Pipeline& pl = p->pipes[pi];
         if (!pl.allocated || pl.cards.empty()) continue;
@@ -3168,6 +3191,7 @@ static Block build_hist_root(esgpu_plan* p, const Group& g) {
         }
         require(!B0.allocated || B0.tdict == nullptr || (B0.H == P0.H && B0.key0 == P0.key0), ESGPU_ERR_DEVICE,
                 "sibling pipelines disagree on the key grid");
+        std::string term_scratch;
         for (uint32_t s : slots) {
             if (!B0.allocated || B0.tdict == nullptr) { sub.append_empty(); continue; }
             const SpecNode& tn = p->specs[kid.spec];
@@ -3196,8 +3220,7 @@ static Block build_hist_root(esgpu_plan* p, const Group& g) {
             }
             begin_instance(sub, other);
             for (auto& tp : top) {
-                const std::string term = plan_term(p, B0, tp.ord);
-                push_bucket(sub, tp.ord, &term, tp.count);
+                push_bucket(sub, tp.ord, B0.tdict->view(tp.ord, term_scratch), tp.count);
                 if (tp.count == 0) { for (Block& sb : sub.subs) sb.append_empty(); continue; }
                 for (size_t gj = 0; gj < kid.grand.size(); ++gj)
                     append_leaf(p, p->pipes[kid.grand[gj].pipe], kid.grand[gj].leaf, row + tp.ord, sub.subs[gj]);

@@ -80,6 +80,13 @@ def test_synthetic_generator_host_properties():
     assert rt.min() >= 0 and rt.max() <= 999
     assert np.array_equal(synthetic_host_column("host", n, start=1000, count=50), host[1000:1050])
     assert synthetic_terms("host", 3) == ["host-0000", "host-0001", "host-0002"]
+    import ctypes
+    buf = ctypes.create_string_buffer(64)
+    for o in (0, 7, 999, 9999, 10000, 123456, 2**32 - 1):  # the hand formatter against printf's "%04u" / "%08x"
+        assert N.lib().esgpu_synthetic_term(N.SYNTH_FIELDS["host"], o, buf, 64) == len("host-%04u" % o)
+        assert buf.value.decode() == "host-%04u" % o
+        N.lib().esgpu_synthetic_term(N.SYNTH_FIELDS["url"], o, buf, 64)
+        assert buf.value.decode() == "/p/%08x" % o
     ip = synthetic_host_column("client_ip.hash", 1000)
     assert len(np.unique(ip)) > 990
 
