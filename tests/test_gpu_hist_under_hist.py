@@ -10,7 +10,7 @@ import oracle as O
 from elasticsearch_amd import AggregationBuilders as AB
 from elasticsearch_amd import _native as N
 from elasticsearch_amd import reduce
-from helpers import assert_same, synthetic_columns
+from helpers import assert_same, bits_from_mask, synthetic_columns
 
 pytestmark = pytest.mark.gpu
 
@@ -94,3 +94,35 @@ def test_inner_field_missing_in_a_segment(engine):
     plan.close()
     for s in segs:
         s.close()
+
+
+def test_fused_inner_key_double_sparse_and_negative(engine):
+    """the collect loader derives the inner key index (no cardinality leaf, single-valued): a sparse double inner field,
+    and a long inner field with negative values and an offset (keys below zero, floor division)"""
+    n = 250_000
+    rng = np.random.default_rng(5)
+    data = []
+    for s in range(2):
+        cols = synthetic_columns(FIELDS, n, shard=s)
+        keep = rng.random(n) >= 0.2
+        cols["price"]["values"] = np.where(keep, cols["price"]["values"], 0.0)
+        cols["price"]["present"] = bits_from_mask(keep)
+        cols["delta"] = {"type": N.COL_I64, "values": rng.integers(-5000, 5000, size=n).astype(np.int64)}
+        data.append((cols, n))
+    aggs = [AB.dateHistogram("d").field("@timestamp").interval("12h").subAggregation(
+                AB.histogram("p").field("price").interval(25).minDocCount(1).subAggregation(AB.avg("b").field("bytes"))),
+            AB.histogram("r").field("response_time_ms").interval(200).subAggregation(
+                AB.histogram("dl").field("delta").interval(700).offset(-33).minDocCount(1))]
+    want = O.run(data, aggs, number_of_shards=2)
+    plan = engine.plan(aggs, number_of_shards=2)
+    results = []
+    for s, (cols, _) in enumerate(data):
+        seg = engine.upload_segment(cols, n)
+        plan.reset()
+        plan.collect(seg)
+        r = plan.build()
+        assert_same(r.to_dict(), want["shards"][s], f"shard{s}", False)
+        results.append(r)
+        seg.close()
+    assert_same(reduce(results).to_dict(), want["reduced"], "reduced", False)
+    plan.close()
