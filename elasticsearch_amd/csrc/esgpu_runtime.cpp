@@ -2244,8 +2244,11 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
 #ifndef ESGPU_WIDE_WINDOW
 #define ESGPU_WIDE_WINDOW 1
 #endif
+#ifndef ESGPU_WIDE_MIN  // widen to at least this many keys whenever the two-per-CU window is narrower (A/B knob)
+#define ESGPU_WIDE_MIN 0
+#endif
     if (ESGPU_WIDE_WINDOW && P.lds_mode && P.windowed && !P.kstart && hc && pl.interval > 0) {
-        const int64_t need = std::min<int64_t>(hc->zspan / pl.interval + 2, (int64_t)LH);
+        const int64_t need = std::min<int64_t>(std::max<int64_t>(hc->zspan / pl.interval + 2, ESGPU_WIDE_MIN), (int64_t)LH);
         if (need > (int64_t)W) {
             uint32_t w2 = W;
             while ((int64_t)w2 < need && collect_lds_bytes(LT, w2 + 1, L_met, L_vcnt, L_ocnt) <= kLdsMax) ++w2;
