@@ -17,6 +17,7 @@ import es_stream as ES
 from elasticsearch_amd import AggregationBuilders as AB
 from elasticsearch_amd import Order, QueryBuilders as QB
 from elasticsearch_amd import _native as N
+from elasticsearch_amd.aggs import TermsBuilder
 from elasticsearch_amd import reduce
 from helpers import assert_same, bits_from_mask
 
@@ -163,6 +164,9 @@ class Gen:
                 inner = self.histogram() if kind == "date_histogram" or r.random() < 0.5 else self.date_histogram(affine=True)
             for _ in range(int(r.integers(0, 2))):
                 inner.subAggregation(self.metric()[0])
+            if kind != "terms" and isinstance(inner, TermsBuilder) and r.random() < 0.4:
+                # terms under a histogram: count orders select per row on the GPU, term orders on the host
+                inner.order(Order.count(bool(r.random() < 0.5)) if r.random() < 0.7 else Order.term(bool(r.random() < 0.5)))
             b.subAggregation(inner)
         if kind == "terms":
             c = r.random()
