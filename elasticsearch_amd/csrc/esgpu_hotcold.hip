@@ -67,8 +67,7 @@ void launch_hc_recode(const uint32_t* ord, uint32_t n, const uint32_t* keys, con
 __global__ void hc_init_kernel(HcParams P) {
     for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < P.P; p += gridDim.x * blockDim.x)
         P.ovf_cur[p] = P.part[p].ovf_base;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *P.err = 0u;
-}
+}  // P.err is zeroed by the host (after each check), so overruns of every segment of a request accumulate
 
 // Cold ordinals leave the workgroup only as whole, aligned 64-byte segments (32 offsets; every region and chunk is a
 // multiple of 64 elements).  Each partition owns a 64-slot ring in LDS: a cold doc's single LDS atomic on the

@@ -1506,6 +1506,7 @@ struct HcStats {
     bool u16 = false;            // every cold ordinal's count < 65536: packed 16-bit counters in the counting pass
     uint64_t pbuf_elems = 0;     // partition regions + kHcTile spare elements
     uint64_t hot_docs = 0, docs = 0;
+    bool refused = false;        // outside what the hot/cold kernels handle (cached: the check counts the column)
     DevBuf d_rc;                 // recoded ordinal column (hot ordinals as kHcHotBit | slot); empty: no hot set
     DevBuf d_hot_ord, d_part, d_piece;
     // cold lists: the cold docs' partition-local offsets grouped by partition (postings of the cold ordinals, 64-element
@@ -1563,13 +1564,21 @@ static std::shared_ptr<const HcStats> ensure_hc_stats(esgpu_ctx* c, const DevCol
     DevColumn* mcol = const_cast<DevColumn*>(col);
     std::lock_guard<std::mutex> lk(c->mu);  // plans on different threads may share the segment
     const void* src = col->ords().p;
-    if (mcol->hc && mcol->hc->src == src && mcol->hc->T == T) return mcol->hc;
+    if (mcol->hc && mcol->hc->src == src && mcol->hc->T == T) return mcol->hc->refused ? nullptr : mcol->hc;
     const uint32_t P = (uint32_t)(((uint64_t)T + (1u << kPartShift) - 1) >> kPartShift);
     if (P == 0 || P > kHcMaxParts || c->cus <= 0) return nullptr;
     auto hs = std::make_shared<HcStats>();
     hs->src = src;
     hs->T = T;
     hs->P = P;
+    auto refuse = [&]() -> std::shared_ptr<const HcStats> {  // remembered for this (buffer, T): not counted again
+        auto r = std::make_shared<HcStats>();
+        r->src = src;
+        r->T = T;
+        r->refused = true;
+        mcol->hc = r;
+        return nullptr;
+    };
     std::vector<uint64_t> cnt(T, 0);
     {
         DevBuf d;
@@ -1647,8 +1656,10 @@ static std::shared_ptr<const HcStats> ensure_hc_stats(esgpu_ctx* c, const DevCol
         q.cap_end = (uint32_t)acc;
         q.ovf_chunk = (uint32_t)ovf;
         cap[p] = acc - q.sbase;
-        if (acc + kHcTile + 64 >= 0xFFFFFFFFull) return nullptr;
+        if (acc + kHcTile + 64 >= 0xFFFFFFFFull) return refuse();
     }
+    if (const char* e = std::getenv("ESGPU_DEBUG_HC_NO_OVERFLOW"); e && *e == '1')  // tests only: no overflow pools,
+        for (HcPart& q : parts) q.cap_end = q.ovf_base;                          // so an uneven spread overruns
     hs->trash = (uint32_t)acc;
     hs->pbuf_elems = acc + kHcTile;
     // counting pieces: a partition far above the average region (a heavy cold ordinal) is split so that no counting
@@ -1792,7 +1803,10 @@ static bool collect_hotcold(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s,
     H.pbuf = (uint16_t*)p->s_pbuf.ensure(c, hs->pbuf_elems * 2);
     H.trash = hs->trash;
     H.counts = pl.g_cnt.as<unsigned long long>();
-    p->h_hcerr.ensure(8);
+    if (!p->h_hcerr.bytes) {  // zeroed once here and after each check: overruns of every segment accumulate
+        p->h_hcerr.ensure(8);
+        *p->h_hcerr.as<volatile uint32_t>() = 0;
+    }
     H.err = (uint32_t*)p->h_hcerr.dev();
     p->hc_check = true;
     H.u16_counters = hs->u16 ? 1 : 0;
@@ -2518,7 +2532,10 @@ extern "C" int esgpu_plan_post_collection(esgpu_plan* p) {
         bsync(p);
         if (p->hc_check) {  // a partition overran the capacity the segment statistics promised (a bug, never data)
             p->hc_check = false;
-            require(*p->h_hcerr.as<volatile uint32_t>() == 0, ESGPU_ERR_DEVICE, "hot/cold counting: partition capacity exceeded");
+            volatile uint32_t* err = p->h_hcerr.as<volatile uint32_t>();
+            const uint32_t e = *err;
+            *err = 0;
+            require(e == 0, ESGPU_ERR_DEVICE, "hot/cold counting: partition capacity exceeded");
         }
         for (Pipeline& pl : p->pipes) {
             if (pl.kind != 1 || !pl.allocated) continue;

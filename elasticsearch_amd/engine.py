@@ -237,6 +237,7 @@ class Engine:
         N.check(N.lib().esgpu_ctx_create(device, hbm_budget_bytes, ctypes.byref(ptr)))
         self._ptr = ptr
         self.device = device
+        self._comms = []  # communicators over this context: destroyed before it (they use its device and budget)
 
     @property
     def ptr(self):
@@ -340,6 +341,9 @@ class Engine:
 
     def close(self):
         if self._ptr:
+            for c in self._comms:
+                c.close()
+            self._comms = []
             N.check(N.lib().esgpu_ctx_destroy(self._ptr))
             self._ptr = None
 
@@ -415,7 +419,8 @@ class Communicator:
         idbuf = (ctypes.c_uint8 * N.COMM_ID_BYTES).from_buffer_copy(unique_id)
         N.check(N.lib().esgpu_comm_init(engine.ptr, nranks, rank, idbuf, ctypes.byref(ptr)))
         self._ptr = ptr
-        self._keep = None
+        self._keep = engine  # the context outlives the communicator (esgpu_comm_destroy frees device buffers in it)
+        engine._comms.append(self)
 
     @staticmethod
     def unique_id():

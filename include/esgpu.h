@@ -475,6 +475,7 @@ int esgpu_result_deserialize(const uint8_t* buf, size_t len, esgpu_result** out)
  *                         non-integer floating sums differ from the shard-order sum in the last bits only.
  *   esgpu_comm_gather_reduce: every aggregation through the all-gather path (one local shard).
  *   esgpu_comm_last_exchange: bytes moved by the last reduce on this communicator.
+ *   esgpu_comm_destroy:   an RCCL communicator holds device buffers of its context: destroy it before esgpu_ctx_destroy.
  * ------------------------------------------------------------------------------------------------------- */
 #define ESGPU_COMM_ID_BYTES 128
 typedef struct esgpu_comm esgpu_comm;

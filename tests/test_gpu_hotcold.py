@@ -121,3 +121,37 @@ def test_two_segments_one_plan(engine, filtered):
     plan.close()
     for s in segs:
         s.close()
+
+
+def test_capacity_overrun_in_first_segment_is_reported(engine, monkeypatch):
+    """A partition overrun in segment 1 of a two-segment plan must survive segment 2's collect and fail the request
+    with ESGPU_ERR_DEVICE (the flag accumulates over the request's segments and is cleared after each check).  The test
+    knob ESGPU_DEBUG_HC_NO_OVERFLOW removes the overflow pools while a segment's statistics are built, so clustered
+    ordinals (each partition's docs in a few workgroups' ranges) overrun their static regions; the evenly spread second
+    segment does not.  The same plan then serves a clean request."""
+    rng = np.random.default_rng(106)
+    T = 150_000
+    clustered = np.sort(rng.integers(0, T, size=2_000_000)).astype(np.uint32)
+    spread = rng.integers(0, T, size=1_000_000).astype(np.uint32)
+    c1, c2 = _cols(clustered, T, rng), _cols(spread, T, rng)
+    aggs = [AB.terms("c").field("kw").size(10)]
+    flt = [QB.rangeQuery("status").gte(0)]  # predicates: the scatter form (path 6), which allocates overflow chunks
+    monkeypatch.setenv("ESGPU_DEBUG_HC_NO_OVERFLOW", "1")
+    s1 = engine.upload_segment(c1, len(clustered))
+    s2 = engine.upload_segment(c2, len(spread))
+    plan = engine.plan(aggs, filters=flt)
+    try:
+        plan.collect(s1)
+        monkeypatch.delenv("ESGPU_DEBUG_HC_NO_OVERFLOW")
+        plan.collect(s2)
+        with pytest.raises(N.EsGpuError) as ei:
+            plan.build()
+        assert ei.value.code == N.ERR_DEVICE, ei.value
+        plan.reset()
+        plan.collect(s2)  # the error word was cleared by the check
+        want = O.run([(c2, len(spread))], aggs, filters=flt)
+        assert_same(plan.build().to_dict(), want["shards"][0], "clean request")
+    finally:
+        plan.close()
+        s1.close()
+        s2.close()
