@@ -126,6 +126,7 @@ extern "C" int esgpu_comm_init(esgpu_ctx* c, int32_t nranks, int32_t rank, const
 }
 
 extern "C" int esgpu_comm_init_host(int32_t nranks, int32_t rank, const esgpu_host_transport* t, esgpu_comm** out) {
+    tune_host_heap();
     return guarded([&] {
         require(t && t->allreduce && t->allgather && out && nranks >= 1 && rank >= 0 && rank < nranks, ESGPU_ERR_INVALID,
                 "bad communicator arguments");

@@ -51,6 +51,14 @@ inline void require(bool c, int code, const std::string& msg) {
     if (!c) throw EsError(code, msg);
 }
 
+// Shard results and reduces allocate multi-MB columnar arrays per request (57,700 buckets x 9 arrays for a north-star
+// shard at 8 shards).  glibc serves those from fresh mmap'd pages (above its mmap threshold) or returns them to the OS
+// by heap trimming, so every request paid a page fault per 4 KB touched: 2.1 ms to copy one shard's arrays into new
+// vectors against 0.37 ms into recycled heap memory (measured on this build host).  The first context / reduce raises
+// M_MMAP_THRESHOLD (32 MB, glibc's maximum) and M_TRIM_THRESHOLD (256 MB) once for the process, so freed result
+// memory is reused; ESGPU_MALLOC_TUNE=0 leaves the host process's allocator settings alone.
+void tune_host_heap();
+
 // ------------------------------------------------------------------------------------------------------------
 // context + HBM accounting (the REQUEST/FIELDDATA circuit breakers' analogue, BigArrays.java:393-395)
 // ------------------------------------------------------------------------------------------------------------

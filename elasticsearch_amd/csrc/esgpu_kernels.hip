@@ -598,6 +598,77 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(GatherParams P) {
     for (int a = 0; a < P.narrays; ++a) P.dst[a][i] = P.src[a][src];
 }
 
+// compact_rows, pass 1: non-empty key slots of each winner's row (one workgroup per row)
+__global__ __launch_bounds__(256) void row_nnz_kernel(CompactParams P) {
+    __shared__ uint32_t part[4];
+    const uint32_t r = blockIdx.x, ord = P.rows[r];
+    uint32_t n = 0;
+    for (uint32_t s = threadIdx.x; s < P.H; s += 256) n += P.cnt[(size_t)s * P.T + ord] != 0ull;
+    for (int o = 32; o > 0; o >>= 1) n += (uint32_t)__shfl_xor((int)n, o, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = n;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t t = part[0] + part[1] + part[2] + part[3];
+        P.nnz[r] = t;
+        P.o_nnz[r] = t;
+    }
+}
+
+// compact_rows, pass 2: row r's non-empty slots written from position sum(nnz[0..r)), key-ascending, with every leaf's
+// partials decoded (vc == 0: sum 0, min +inf, max -inf, sum of squares 0; a NaN collected: min = max = NaN)
+__global__ __launch_bounds__(256) void compact_rows_kernel(CompactParams P) {
+    __shared__ uint32_t part[4];
+    __shared__ uint32_t wsum[4];
+    const uint32_t r = blockIdx.x, ord = P.rows[r];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t b = 0;
+    for (uint32_t j = threadIdx.x; j < r; j += 256) b += P.nnz[j];
+    for (int o = 32; o > 0; o >>= 1) b += (uint32_t)__shfl_xor((int)b, o, 64);
+    if (lane == 0) part[wave] = b;
+    __syncthreads();
+    uint64_t pos = (uint64_t)part[0] + part[1] + part[2] + part[3];
+    for (uint32_t s0 = 0; s0 < P.H; s0 += 256) {
+        const uint32_t s = s0 + threadIdx.x;
+        const size_t cell = (size_t)s * P.T + ord;
+        const unsigned long long c = s < P.H ? P.cnt[cell] : 0ull;
+        const unsigned long long m = __ballot(c != 0ull);
+        __syncthreads();  // wsum of the previous chunk consumed
+        if (lane == 0) wsum[wave] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint64_t at = pos + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        for (uint32_t w = 0; w < wave; ++w) at += wsum[w];
+        pos += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        if (c == 0ull) continue;
+        P.o_key[at] = P.affine ? (long long)((P.key0 + (int64_t)s) * P.interval + P.offset) : (long long)s;
+        P.o_count[at] = (long long)c;
+        for (int l = 0; l < P.nleaves; ++l) {
+            const CompactLeaf& L = P.leaf[l];
+            const unsigned long long vc = L.cnt[cell];
+            double sum = 0.0, mn = __builtin_inf(), mx = -__builtin_inf(), sq = 0.0;
+            if (vc) {
+                sum = L.sum[cell];
+                if (L.mn) {
+                    const uint64_t emn = L.mn[cell], emx = L.mx[cell];
+                    if (emn < kEncNegInf || emx > kEncPosInf) { mn = __builtin_nan(""); mx = __builtin_nan(""); }
+                    else { mn = unsortable(emn); mx = unsortable(emx); }
+                }
+                if (L.sq) sq = L.sq[cell];
+            }
+            L.o_count[at] = (long long)vc;
+            L.o_sum[at] = sum;
+            L.o_min[at] = mn;
+            L.o_max[at] = mx;
+            L.o_sq[at] = sq;
+        }
+    }
+}
+
+void launch_compact_rows(const CompactParams& p, hipStream_t st) {
+    if (p.k == 0) return;
+    hipLaunchKernelGGL(row_nnz_kernel, dim3(p.k), dim3(256), 0, st, p);
+    hipLaunchKernelGGL(compact_rows_kernel, dim3(p.k), dim3(256), 0, st, p);
+}
+
 // device -> pinned host memory for the build's small transfers: a kernel writing over the link beats a DMA copy,
 // whose setup measured ~130 us per 144 KB transfer
 __global__ __launch_bounds__(256) void copy_u64_kernel(const unsigned long long* __restrict__ src,

@@ -132,6 +132,35 @@ struct GatherParams {
     unsigned long long* dst[6];
 };
 
+// build: the winners' histogram rows compacted on the GPU into the result's columnar arrays (HistogramAggregator
+// .buildAggregation per winner: the non-empty key slots ascending, each with its metric leaves decoded the way the
+// host's metric_cell does), written straight into pinned host memory -- the host copies whole arrays instead of
+// visiting k x H cells
+struct CompactLeaf {
+    const unsigned long long* cnt;   // the leaf's value counts ([H][T]: the value-count grid, or the doc-count grid)
+    const double* sum;               // null: avg-less leaves never happen (every numeric metric keeps a sum)
+    const unsigned long long* mn;    // order-preserving encodings; null: no min / max (avg)
+    const unsigned long long* mx;
+    const double* sq;                // null: no sum of squares (avg, stats)
+    long long* o_count;              // [cap] outputs (pinned, device-mapped)
+    double *o_sum, *o_min, *o_max, *o_sq;
+};
+constexpr int kCompactLeaves = 4;
+struct CompactParams {
+    const uint32_t* rows;            // [k] winners' ordinals
+    uint32_t k, H, T;
+    const unsigned long long* cnt;   // bucket doc counts [H][T]
+    int32_t affine;                  // 1: key = (key0 + slot) * interval + offset; 0: o_key receives the slot
+    int64_t key0, interval, offset;
+    uint32_t* nnz;                   // [k] non-empty slots per row (device scratch)
+    uint32_t* o_nnz;                 // [k] the same, pinned
+    long long* o_key;                // [cap] bucket keys (or slots)
+    long long* o_count;              // [cap] bucket doc counts
+    int32_t nleaves;
+    CompactLeaf leaf[kCompactLeaves];
+};
+void launch_compact_rows(const CompactParams& p, hipStream_t s);
+
 // per-8192-doc-block min / max; f64 = the column holds doubles, taken as (long) casts (FieldData.castToLong)
 void launch_zone_map(const int64_t* v, const uint64_t* present, uint32_t n, int64_t* zmin, int64_t* zmax, bool f64,
                      hipStream_t s);

@@ -19,6 +19,7 @@
 #include <map>
 #include <stdexcept>
 #include <string_view>
+#include <numeric>
 #include <unordered_map>
 
 namespace esgpu {
@@ -351,7 +352,21 @@ struct OutBucket {
     int64_t err;
     uint32_t c0, c1;
     bool empty;
-    uint32_t val = 0;  // terms ordered by a sub-aggregation: index of the bucket's value
+    uint32_t val = 0;   // terms ordered by a sub-aggregation: index of the bucket's value
+    uint32_t slot = 0;  // histogram keys on a lattice: the key's slot (DenseKeys)
+};
+
+// a histogram reduce whose keys lie on one lattice kmin + j * step: every contribution's slot j, in input order
+struct DenseKeys {
+    const Ref* refs = nullptr;
+    size_t nrefs = 0;
+    int64_t kmin = 0;
+    uint64_t step = 1;
+    uint32_t span = 0;
+    std::vector<uint32_t> slot;      // [contributions] in input (shard, bucket) order
+    std::vector<int64_t> count;      // [span] summed doc counts
+    std::vector<uint32_t> n;         // [span] contributions
+    std::vector<int32_t> out;        // [span] position of the slot's bucket among the emitted ones, -1: none
 };
 
 struct Scratch {
@@ -361,9 +376,88 @@ struct Scratch {
     std::vector<uint32_t> ids, start;
     std::unordered_map<std::string_view, uint32_t> index;
     std::vector<Ref> child;
+    DenseKeys dense;
 };
 
-void emit_buckets(Block& out, const std::vector<OutBucket>& buckets, const Scratch& sc, std::vector<Level>& child) {
+// numeric metric sub-aggregations of a bucket reduce are reduced as their bucket is emitted (no child level): their
+// reduce reads nothing but the contributions' partials, and instances are appended in emission order either way
+inline bool fused_leaf(const Block& b) {
+    return b.type == ESGPU_AGG_STATS || b.type == ESGPU_AGG_EXTENDED_STATS || b.type == ESGPU_AGG_AVG;
+}
+
+// InternalStats / InternalExtendedStats / InternalAvg .doReduce of sub-aggregation j over contributions [c0, c1) (shard
+// order): sums in that order from 0, Math.min / Math.max
+void reduce_leaf(Block& m, const Scratch& sc, size_t j, uint32_t c0, uint32_t c1) {
+    int64_t count = 0;
+    double mn = INFINITY, mx = -INFINITY, sum = 0, sq = 0;
+    for (uint32_t c = c0; c < c1; ++c) {
+        const Block& b = sc.contrib[c].b->subs[j];
+        const uint64_t i = sc.contrib[c].i;
+        count += b.count[i];
+        mn = jmin(mn, b.min[i]);
+        mx = jmax(mx, b.max[i]);
+        sum += b.sum[i];
+        sq += b.sumsq[i];
+    }
+    ++m.n;
+    m.count.push_back(count);
+    m.min.push_back(mn);
+    m.max.push_back(mx);
+    m.sum.push_back(sum);
+    m.sumsq.push_back(sq);
+}
+
+// fused metric sub-aggregation j of a lattice histogram reduce: the emitted buckets' instances initialised (an empty
+// bucket's from its prototype), then every shard's partials streamed in shard order into their bucket's instance --
+// the same additions in the same order as reduce_leaf, without a contribution list
+void stream_leaf(Block& m, const Block* proto, const std::vector<OutBucket>& buckets, const DenseKeys& dk, size_t j) {
+    const size_t base = m.count.size(), nb = buckets.size();
+    m.n += nb;
+    m.count.resize(base + nb, 0);
+    m.sum.resize(base + nb, 0.0);
+    m.min.resize(base + nb, INFINITY);
+    m.max.resize(base + nb, -INFINITY);
+    m.sumsq.resize(base + nb, 0.0);
+    for (size_t q = 0; q < nb; ++q)
+        if (buckets[q].empty) {  // only with EmptyBucketInfo: proto = its prototype
+            m.count[base + q] = proto->count[0];
+            m.sum[base + q] = proto->sum[0];
+            m.min[base + q] = proto->min[0];
+            m.max[base + q] = proto->max[0];
+            m.sumsq[base + q] = proto->sumsq[0];
+        }
+    int64_t* cnt = m.count.data() + base;
+    double *sum = m.sum.data() + base, *mn = m.min.data() + base, *mx = m.max.data() + base, *sq = m.sumsq.data() + base;
+    size_t e = 0;
+    for (size_t x = 0; x < dk.nrefs; ++x) {
+        const Block& h = *dk.refs[x].b;
+        const Block& L = h.subs[j];
+        const uint64_t b0 = h.boff[dk.refs[x].i], b1 = h.boff[dk.refs[x].i + 1];
+        for (uint64_t k = b0; k < b1; ++k) {
+            const int32_t o = dk.out[dk.slot[e++]];
+            if (o < 0) continue;
+            cnt[o] += L.count[k];
+            mn[o] = jmin(mn[o], L.min[k]);
+            mx[o] = jmax(mx[o], L.max[k]);
+            sum[o] += L.sum[k];
+            sq[o] += L.sumsq[k];
+        }
+    }
+}
+
+void emit_buckets(Block& out, const std::vector<OutBucket>& buckets, const Scratch& sc, std::vector<Level>& child,
+                  DenseKeys* dk = nullptr) {
+    const size_t nb = buckets.size();
+    out.key.reserve(out.key.size() + nb);
+    out.term_off.reserve(out.term_off.size() + nb);
+    out.bcount.reserve(out.bcount.size() + nb);
+    out.berr.reserve(out.berr.size() + nb);
+    for (size_t j = 0; j < out.subs.size(); ++j) {
+        Block& m = out.subs[j];
+        if (!fused_leaf(m) || dk) continue;
+        for (auto* v : {&m.sum, &m.min, &m.max, &m.sumsq}) v->reserve(v->size() + nb);
+        m.count.reserve(m.count.size() + nb);
+    }
     for (const OutBucket& ob : buckets) {
         out.key.push_back(ob.key);
         if (ob.tb) {
@@ -374,6 +468,12 @@ void emit_buckets(Block& out, const std::vector<OutBucket>& buckets, const Scrat
         out.bcount.push_back(ob.count);
         out.berr.push_back(ob.err);
         for (size_t j = 0; j < out.subs.size(); ++j) {
+            if (fused_leaf(out.subs[j])) {
+                if (dk) continue;  // streamed below
+                if (ob.empty) out.subs[j].append_instance(out.empty_subs[j], 0);
+                else reduce_leaf(out.subs[j], sc, j, ob.c0, ob.c1);
+                continue;
+            }
             Level& lv = child[j];
             if (ob.empty) {
                 const Ref r{&out.empty_subs[j], 0};
@@ -387,6 +487,18 @@ void emit_buckets(Block& out, const std::vector<OutBucket>& buckets, const Scrat
         }
     }
     out.boff.push_back(out.boff.back() + buckets.size());
+    if (dk) {
+        bool any = false;
+        for (const Block& m : out.subs) any |= fused_leaf(m);
+        if (any) {
+            dk->out.assign(dk->span, -1);
+            for (size_t q = 0; q < nb; ++q)
+                if (!buckets[q].empty) dk->out[buckets[q].slot] = (int32_t)q;
+            for (size_t j = 0; j < out.subs.size(); ++j)
+                if (fused_leaf(out.subs[j]))
+                    stream_leaf(out.subs[j], j < out.empty_subs.size() ? &out.empty_subs[j] : nullptr, buckets, *dk, j);
+        }
+    }
 }
 
 void reduce_terms(const Ref* refs, size_t nrefs, Block& out, Scratch& sc, std::vector<Level>& child) {  // InternalTerms.doReduce
@@ -491,10 +603,63 @@ void reduce_terms(const Ref* refs, size_t nrefs, Block& out, Scratch& sc, std::v
     emit_buckets(out, sc.buckets, sc, child);
 }
 
+// InternalHistogram.reduceBuckets' merge when every key lies on one lattice kmin + j * step (step = the gcd of the key
+// gaps: a fixed interval or a fixed-length date unit): a contribution's slot is its key's position on the lattice, so the
+// merged buckets are the non-empty slots in slot order -- exactly the k-way merge by (key, shard) -- and their doc
+// counts are summed by streaming each shard.  Returns false (nothing usable) when the keys are off one lattice or span
+// more than ~4 slots per contribution.
+bool dense_slots(const Ref* refs, size_t nrefs, size_t total, DenseKeys& dk) {
+    int64_t kmin = INT64_MAX, kmax = INT64_MIN;
+    uint64_t step = 0;
+    for (size_t x = 0; x < nrefs; ++x) {
+        const Block& h = *refs[x].b;
+        const uint64_t b0 = h.boff[refs[x].i], b1 = h.boff[refs[x].i + 1];
+        if (b0 == b1) continue;
+        kmin = std::min(kmin, h.key[b0]);
+        kmax = std::max(kmax, h.key[b1 - 1]);
+        for (uint64_t k = b0 + 1; k < b1; ++k) {
+            const uint64_t d = (uint64_t)h.key[k] - (uint64_t)h.key[k - 1];
+            if (d != step) step = std::gcd(step, d);  // consecutive keys one step apart: nothing to do
+        }
+    }
+    if (kmin > kmax) return false;
+    const uint64_t range = (uint64_t)kmax - (uint64_t)kmin;  // kmin <= kmax: exact in two's complement
+    if (step == 0) step = range ? range : 1;
+    if (range / step + 1 > 4 * (uint64_t)total + 64) return false;
+    dk.refs = refs;
+    dk.nrefs = nrefs;
+    dk.kmin = kmin;
+    dk.step = step;
+    dk.span = (uint32_t)(range / step + 1);
+    dk.slot.resize(total);
+    dk.count.assign(dk.span, 0);
+    dk.n.assign(dk.span, 0);
+    size_t e = 0;
+    for (size_t x = 0; x < nrefs; ++x) {
+        const Block& h = *refs[x].b;
+        const uint64_t b0 = h.boff[refs[x].i], b1 = h.boff[refs[x].i + 1];
+        if (b0 == b1) continue;
+        const uint64_t off0 = (uint64_t)h.key[b0] - (uint64_t)kmin;
+        if (off0 % step) return false;  // this shard's keys are off the lattice (its gaps are multiples of step)
+        uint32_t j = (uint32_t)(off0 / step);
+        for (uint64_t k = b0; k < b1; ++k) {
+            if (k > b0) {  // one division per gap longer than a step
+                const uint64_t d = (uint64_t)h.key[k] - (uint64_t)h.key[k - 1];
+                j += d == step ? 1u : (uint32_t)(d / step);
+            }
+            dk.slot[e++] = j;
+            dk.count[j] += h.bcount[k];
+            ++dk.n[j];
+        }
+    }
+    return true;
+}
+
 void reduce_histogram(const Ref* refs, size_t nrefs, Block& out, Scratch& sc, std::vector<Level>& child) {  // InternalHistogram.doReduce
     std::vector<OutBucket>& list = sc.buckets;
     list.clear();
     sc.contrib.clear();
+    DenseKeys* dense = nullptr;
     if (nrefs == 1) {  // one shard: already key-sorted, nothing to merge
         const Block& h = *refs[0].b;
         const uint64_t i = refs[0].i;
@@ -518,8 +683,32 @@ void reduce_histogram(const Ref* refs, size_t nrefs, Block& out, Scratch& sc, st
             total += b1 - b0;
             for (uint64_t k = b0 + 1; k < b1 && sorted; ++k) sorted = h.key[k - 1] < h.key[k];
         }
-        all.reserve(total);
-        if (sorted && nrefs <= 16) {
+        DenseKeys& dk = sc.dense;
+        if (sorted && total && dense_slots(refs, nrefs, total, dk)) {
+            bool need_contrib = false;  // contributions grouped by slot only for sub-aggregations that are not streamed
+            for (const Block& m : out.subs) need_contrib |= !fused_leaf(m);
+            std::vector<uint32_t>& start = sc.start;
+            if (need_contrib) {
+                start.assign((size_t)dk.span + 1, 0);
+                for (uint32_t j = 0; j < dk.span; ++j) start[j + 1] = start[j] + dk.n[j];
+            }
+            for (uint32_t j = 0; j < dk.span; ++j) {
+                if (!dk.n[j] || dk.count[j] < out.min_doc_count) continue;
+                OutBucket ob{dk.kmin + (int64_t)((uint64_t)j * dk.step), nullptr, 0, dk.count[j], 0, 0, 0, false};
+                if (need_contrib) { ob.c0 = start[j]; ob.c1 = start[j + 1]; }
+                ob.slot = j;
+                list.push_back(ob);
+            }
+            if (need_contrib) {  // counting sort by slot, shard order kept within a slot
+                all.resize(total);
+                size_t e = 0;
+                for (size_t x = 0; x < nrefs; ++x) {
+                    const Block& h = *refs[x].b;
+                    for (uint64_t k = h.boff[refs[x].i]; k < h.boff[refs[x].i + 1]; ++k) all[start[dk.slot[e++]]++] = Ref{&h, k};
+                }
+            }
+            dense = &dk;
+        } else if (sorted && nrefs <= 16) {
             // few shards: the next key is the minimum of the heads; every head at that key contributes, in shard
             // order -- one scan of the heads per output key, the buckets of a key landing together
             uint64_t pos[16], end[16];
@@ -568,7 +757,7 @@ void reduce_histogram(const Ref* refs, size_t nrefs, Block& out, Scratch& sc, st
                 for (uint64_t k = refs[x].b->boff[refs[x].i]; k < refs[x].b->boff[refs[x].i + 1]; ++k) all.push_back({refs[x].b, k});
             std::stable_sort(all.begin(), all.end(), [](const Ref& a, const Ref& b) { return a.b->key[a.i] < b.b->key[b.i]; });
         }
-        for (size_t x = 0; x < all.size();) {
+        for (size_t x = 0; !dense && x < all.size();) {
             const int64_t key = all[x].b->key[all[x].i];
             OutBucket ob{key, nullptr, 0, 0, 0, (uint32_t)x, 0, false};
             size_t y = x;
@@ -612,7 +801,7 @@ void reduce_histogram(const Ref* refs, size_t nrefs, Block& out, Scratch& sc, st
     ++out.n;
     out.doc_count_error.push_back(0);
     out.other_doc_count.push_back(0);
-    emit_buckets(out, list, sc, child);
+    emit_buckets(out, list, sc, child, dense);
 }
 
 // copy a prototype instance; its sub-aggregations stay verbatim too (queued in bucket order)
@@ -630,6 +819,7 @@ void copy_verbatim(const Ref& r, Block& out, std::vector<Level>& child) {
         out.bcount.push_back(src.bcount[k]);
         out.berr.push_back(src.berr[k]);
         for (size_t j = 0; j < out.subs.size(); ++j) {
+            if (fused_leaf(out.subs[j])) { out.subs[j].append_instance(src.subs[j], k); continue; }
             const Ref c{&src.subs[j], k};
             child[j].add(&c, 1, true);
         }
@@ -648,7 +838,8 @@ void reduce_level(const Level& lv, Block& out) {
             else if (out.type == ESGPU_AGG_TERMS) reduce_terms(refs, n, out, sc, child);
             else reduce_histogram(refs, n, out, sc, child);
         }
-        for (size_t j = 0; j < out.subs.size(); ++j) reduce_level(child[j], out.subs[j]);
+        for (size_t j = 0; j < out.subs.size(); ++j)
+            if (!fused_leaf(out.subs[j])) reduce_level(child[j], out.subs[j]);
         return;
     }
     if (out.type == ESGPU_AGG_FILTER) {  // InternalFilter (InternalSingleBucketAggregation.doReduce): Σ doc_count, subs

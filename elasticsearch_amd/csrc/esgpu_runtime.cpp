@@ -11,6 +11,7 @@
 //   esgpu_plan_build            buildAggregation(0) (GlobalOrdinalsStringTermsAggregator.java:146-208,
 //                               HistogramAggregator.java:120-133, StatsAggegator.java:140-152, ...)
 #include <hip/hip_runtime.h>
+#include <malloc.h>
 
 #include <algorithm>
 #include <atomic>
@@ -56,7 +57,18 @@ extern "C" int esgpu_device_count(int* count) {
     });
 }
 
+void tune_host_heap() {
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const char* e = std::getenv("ESGPU_MALLOC_TUNE");
+        if (e && *e == '0') return;
+        mallopt(M_MMAP_THRESHOLD, 32 << 20);
+        mallopt(M_TRIM_THRESHOLD, 256 << 20);
+    });
+}
+
 extern "C" int esgpu_ctx_create(int device, uint64_t budget, esgpu_ctx** out) {
+    tune_host_heap();
     return guarded([&] {
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
@@ -910,6 +922,8 @@ struct esgpu_plan {
     PinnedBuf h_keys;
     hipEvent_t ev_mid = nullptr;
     PinnedBuf h_tcnt, h_rows, h_dst[6];
+    Scratch s_nnz;                     // build: non-empty slots per winner row (compact_rows)
+    std::vector<PinnedBuf> h_compact;  // build: per bucket child, its GPU-compacted buckets and leaves (pinned)
 };
 
 static int metric_level(int t) { return t == ESGPU_AGG_AVG ? 1 : t == ESGPU_AGG_STATS ? 2 : 3; }
@@ -2031,6 +2045,9 @@ static bool collect_grid(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, co
 #define ESGPU_FUSE_HIST_ORDS 1  // histogram under histogram: inner key index derived in the collect kernel's loader
 #endif
 static constexpr uint32_t kTermsCopies = ESGPU_TERMS_COPIES;
+#ifndef ESGPU_COMPACT_ROWS
+#define ESGPU_COMPACT_ROWS 1  // build: histogram children of terms compacted on the GPU (0: host assembly, for A/B)
+#endif
 
 static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
     const bool ORD = pl.term_spec >= 0, HIST = pl.hist_spec >= 0;
@@ -3007,14 +3024,74 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
     }
     bmark(p, "selected");
     const uint32_t k = (uint32_t)top.size();
-    // gather the winners' rows [k][H] of every pipeline on the GPU and bring back only those
     uint32_t* rows = (uint32_t*)p->h_rows.ensure(std::max<size_t>(k, 1) * 4);
     for (uint32_t i = 0; i < k; ++i) rows[i] = top[i].ord;
     uint32_t* drows = (uint32_t*)p->s_rows.ensure(p->ctx, std::max<size_t>(k, 1) * 4);
     if (k) HIPX(hipMemcpyAsync(drows, rows, (size_t)k * 4, hipMemcpyHostToDevice, st));
+    // histogram children whose own children are numeric metrics are compacted on the GPU (compact_rows): the host
+    // receives their buckets as whole columnar arrays; every other child reads the winners' rows [k][H] on the host
+    std::vector<char> fast(g.kids.size(), 0), need_rows(p->pipes.size(), 0);
+    need_rows[g.pipes[0]] = gpu_topk;  // term orders read the winners' counts from P0's rows
+    p->h_compact.resize(g.kids.size());
+    for (size_t ki = 0; ki < g.kids.size(); ++ki) {
+        const ChildSrc& kid = g.kids[ki];
+        if (!kid.bucket) { need_rows[kid.leaf.pipe] = 1; continue; }
+        const Pipeline& B0 = p->pipes[kid.pipes[0]];
+        bool ok = ESGPU_COMPACT_ROWS && B0.allocated && !B0.inner_terms && !B0.ord_hist && B0.cards.empty() &&
+                  kid.grand.size() <= (size_t)kCompactLeaves;
+        for (const LeafRef& l : kid.grand) {  // the leaves' grids index like B0's (the kernel reads one cell of each)
+            const Pipeline& L = p->pipes[l.pipe];
+            ok = ok && L.allocated && L.H == B0.H && L.T == B0.T && L.key0 == B0.key0 &&
+                 is_metric(p->specs[L.metrics[l.leaf]].s.type);
+        }
+        fast[ki] = ok;
+        if (ok) continue;
+        for (int pi : kid.pipes) need_rows[pi] = 1;
+        for (const LeafRef& l : kid.grand) need_rows[l.pipe] = 1;
+    }
     for (int pi : g.pipes) {
         Pipeline& pl = p->pipes[pi];
-        if (pl.allocated) fetch_rows(p, pl, drows, k);
+        if (pl.allocated && (need_rows[pi] || !pl.cards.empty())) fetch_rows(p, pl, drows, k);
+    }
+    for (size_t ki = 0; ki < g.kids.size(); ++ki) {
+        if (!fast[ki] || !k) continue;
+        const ChildSrc& kid = g.kids[ki];
+        const Pipeline& B0 = p->pipes[kid.pipes[0]];
+        const size_t cap = (size_t)k * B0.H, nl = kid.grand.size();
+        PinnedBuf& hb = p->h_compact[ki];
+        const size_t nnz_bytes = ((size_t)k * 4 + 63) & ~(size_t)63;
+        char* base = (char*)hb.ensure(nnz_bytes + cap * 8 * (2 + 5 * nl));
+        char* dbase = (char*)hb.dev();
+        auto dev_at = [&](size_t a) { return dbase + nnz_bytes + a * cap * 8; };
+        CompactParams C{};
+        C.rows = drows;
+        C.k = k; C.H = B0.H; C.T = B0.T;
+        C.cnt = B0.g_cnt.as<unsigned long long>();
+        C.affine = B0.ktable ? 0 : 1;
+        C.key0 = B0.key0; C.interval = B0.interval; C.offset = B0.offset;
+        C.nnz = (uint32_t*)p->s_nnz.ensure(p->ctx, (size_t)k * 4);
+        C.o_nnz = (uint32_t*)dbase;
+        C.o_key = (long long*)dev_at(0);
+        C.o_count = (long long*)dev_at(1);
+        C.nleaves = (int32_t)nl;
+        for (size_t gj = 0; gj < nl; ++gj) {
+            const Pipeline& L = p->pipes[kid.grand[gj].pipe];
+            const int32_t type = p->specs[L.metrics[kid.grand[gj].leaf]].s.type;
+            CompactLeaf& o = C.leaf[gj];
+            o.cnt = (L.vcnt_mode ? L.g_vcnt : L.g_cnt).as<unsigned long long>();
+            o.sum = L.g_sum.as<double>();
+            o.mn = L.met >= 2 && type != ESGPU_AGG_AVG ? L.g_min.as<unsigned long long>() : nullptr;
+            o.mx = o.mn ? L.g_max.as<unsigned long long>() : nullptr;
+            o.sq = L.met >= 3 && type == ESGPU_AGG_EXTENDED_STATS ? L.g_sq.as<double>() : nullptr;
+            o.o_count = (long long*)dev_at(2 + 5 * gj);
+            o.o_sum = (double*)dev_at(3 + 5 * gj);
+            o.o_min = (double*)dev_at(4 + 5 * gj);
+            o.o_max = (double*)dev_at(5 + 5 * gj);
+            o.o_sq = (double*)dev_at(6 + 5 * gj);
+        }
+        launch_compact_rows(C, st);
+        HIPX(hipGetLastError());
+        (void)base;
     }
     bmark(p, "fetch_issued");
     bsync(p);
@@ -3033,6 +3110,50 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
             other -= top[i].count;
         }
     }
+    for (size_t ki = 0; ki < g.kids.size(); ++ki) {  // compacted children: k instances appended as whole arrays
+        if (!fast[ki]) continue;
+        const ChildSrc& kid = g.kids[ki];
+        const Pipeline& B0 = p->pipes[kid.pipes[0]];
+        Block& sub = r.subs[ki];
+        if (!k) continue;
+        const size_t cap = (size_t)k * B0.H, nl = kid.grand.size();
+        const char* hb = (const char*)p->h_compact[ki].p;
+        const size_t nnz_bytes = ((size_t)k * 4 + 63) & ~(size_t)63;
+        auto host_at = [&](size_t a) { return hb + nnz_bytes + a * cap * 8; };
+        const uint32_t* nnz = (const uint32_t*)hb;
+        size_t total = 0;
+        sub.n += k;
+        sub.doc_count_error.insert(sub.doc_count_error.end(), k, 0);
+        sub.other_doc_count.insert(sub.other_doc_count.end(), k, 0);
+        sub.boff.reserve(sub.boff.size() + k);
+        for (uint32_t i = 0; i < k; ++i) {
+            total += nnz[i];
+            sub.boff.push_back(sub.boff.back() + nnz[i]);
+        }
+        const int64_t* keys = (const int64_t*)host_at(0);
+        if (B0.ktable) {  // slots: the bucket-start table's keys
+            const size_t n0 = sub.key.size();
+            sub.key.resize(n0 + total);
+            for (size_t q = 0; q < total; ++q) sub.key[n0 + q] = key_value(B0, (uint32_t)keys[q]);
+        } else {
+            sub.key.insert(sub.key.end(), keys, keys + total);
+        }
+        const int64_t* cnts = (const int64_t*)host_at(1);
+        sub.bcount.insert(sub.bcount.end(), cnts, cnts + total);
+        sub.berr.insert(sub.berr.end(), total, 0);
+        sub.term_off.insert(sub.term_off.end(), total, sub.term_pool.size());
+        for (size_t gj = 0; gj < nl; ++gj) {
+            Block& gb = sub.subs[gj];
+            gb.n += total;
+            const int64_t* c = (const int64_t*)host_at(2 + 5 * gj);
+            gb.count.insert(gb.count.end(), c, c + total);
+            std::vector<double>* dst[4] = {&gb.sum, &gb.min, &gb.max, &gb.sumsq};
+            for (int a = 0; a < 4; ++a) {
+                const double* v = (const double*)host_at(3 + a + 5 * gj);
+                dst[a]->insert(dst[a]->end(), v, v + total);
+            }
+        }
+    }
     for (const ChildSrc& kid : g.kids) {  // every pipeline of a bucket child shares its key grid
         if (!kid.bucket) continue;
         const Pipeline& B0 = p->pipes[kid.pipes[0]];
@@ -3046,7 +3167,7 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
     for (size_t ki = 0; ki < g.kids.size(); ++ki) {
         const ChildSrc& kid = g.kids[ki];
         const Pipeline& B0 = kid.bucket ? p->pipes[kid.pipes[0]] : p->pipes[kid.leaf.pipe];
-        if (!B0.allocated) continue;
+        if (!B0.allocated || fast[ki]) continue;
         size_t nb = k;
         if (kid.bucket) {
             nb = 0;
@@ -3063,13 +3184,14 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
     for (uint32_t i = 0; i < k; ++i) {
         const std::string term = plan_term(p, P0, top[i].ord);
         push_bucket(r, top[i].ord, &term, top[i].count);
-        if (top[i].count == 0) {  // bucketEmptyAggregations
-            for (Block& sb : r.subs) sb.append_empty();
+        if (top[i].count == 0) {  // bucketEmptyAggregations (a compacted child's row is empty too: appended above)
+            for (size_t ki = 0; ki < g.kids.size(); ++ki) if (!fast[ki]) r.subs[ki].append_empty();
             continue;
         }
         for (size_t ki = 0; ki < g.kids.size(); ++ki) {
             const ChildSrc& kid = g.kids[ki];
             Block& sub = r.subs[ki];
+            if (fast[ki]) continue;
             if (!kid.bucket) {
                 const Pipeline& L = p->pipes[kid.leaf.pipe];
                 if (!L.allocated) sub.append_empty(); else append_leaf(p, L, kid.leaf.leaf, i, sub);
@@ -3406,6 +3528,7 @@ extern "C" int esgpu_result_free(esgpu_result* r) {
 }
 
 extern "C" int esgpu_reduce(const esgpu_result* const* shards, int32_t n, esgpu_result** out) {
+    tune_host_heap();
     return guarded([&] {
         require(out && n >= 1 && shards, ESGPU_ERR_INVALID, "reduce needs at least one shard result");
         std::vector<const std::vector<Block>*> lists;

@@ -46,6 +46,14 @@ CASES = {
                        ("response_time_ms",)),
     "day_hist_terms": ([AB.dateHistogram("d").field("@timestamp").interval("1d")
                         .subAggregation(AB.terms("hosts").field("host").size(4))], ("@timestamp", "host")),
+    # lattice merge (dense slots) vs k-way merge fallbacks: calendar months (gaps of 28-31 days: a 1-day lattice too
+    # sparse for the slot array), a sparse wide histogram, and an offset histogram with a non-integer-valued metric
+    "month_hist_stats": ([AB.dateHistogram("m").field("@timestamp").interval("month")
+                          .subAggregation(AB.stats("rt").field("response_time_ms"))], ("@timestamp", "response_time_ms")),
+    "sparse_wide_hist": ([AB.histogram("b").field("bytes").interval(7).minDocCount(1)
+                          .subAggregation(AB.avg("rt").field("response_time_ms"))], ("bytes", "response_time_ms")),
+    "offset_hist_price": ([AB.histogram("p").field("price").interval(10).offset(3)
+                           .subAggregation(AB.extendedStats("x").field("price"))], ("price",)),
     "top_metrics": ([AB.stats("s").field("response_time_ms"), AB.extendedStats("e").field("bytes"),
                      AB.avg("a").field("response_time_ms")], ("response_time_ms", "bytes")),
 }
