@@ -21,6 +21,7 @@
 #include <string_view>
 #include <numeric>
 #include <unordered_map>
+#include <unordered_set>
 
 namespace esgpu {
 
@@ -1884,6 +1885,37 @@ void unpack_lists(const std::string& msg, std::vector<std::vector<Block>>& out) 
     }
 }
 
+// a one-instance terms result with its buckets' sub-aggregations as empty instances (the two-phase terms exchange)
+Block terms_skeleton(const Block& t) {
+    Block s = t.like();
+    s.n = t.n;
+    s.doc_count_error = t.doc_count_error;
+    s.other_doc_count = t.other_doc_count;
+    s.boff = t.boff;
+    s.key = t.key;
+    s.term_off = t.term_off;
+    s.term_pool = t.term_pool;
+    s.bcount = t.bcount;
+    s.berr = t.berr;
+    for (Block& sub : s.subs)
+        for (uint64_t k = 0; k < t.nbuckets(); ++k) sub.append_empty();
+    return s;
+}
+
+// the shard's terms result with the sub-aggregations of the buckets whose term is not in `keep` emptied
+Block terms_pruned(const Block& t, const std::unordered_set<std::string>& keep) {
+    Block s = terms_skeleton(t);
+    for (Block& sub : s.subs) sub = sub.like();
+    for (uint64_t k = 0; k < t.nbuckets(); ++k) {
+        const bool kept = keep.count(t.term(k)) != 0;
+        for (size_t j = 0; j < s.subs.size(); ++j) {
+            if (kept) s.subs[j].append_instance(t.subs[j], k);
+            else s.subs[j].append_empty();
+        }
+    }
+    return s;
+}
+
 }  // namespace
 
 std::vector<Block> reduce_across(Collective& c, const std::vector<const std::vector<Block>*>& locals, bool gather_only) {
@@ -1903,10 +1935,44 @@ std::vector<Block> reduce_across(Collective& c, const std::vector<const std::vec
 
     // ---- all-gather path: every rank's shard records, reduced in global shard order (rank-major) ----
     if (!gathered.empty()) {
+        // Top-level terms in a count or term order reduce their sub-aggregations only for the buckets that survive the
+        // reduce (InternalTerms.doReduce: the top `size` merged buckets), and which survive depends on the terms-level
+        // records alone.  So the records travel first without sub-aggregations (skeletons), every rank reduces them to
+        // the same winners, and the shard records then carry the sub-aggregations of the winners' buckets only -- the
+        // other buckets' sub-aggregations are empty instances the reduce never reads.  Same result, the sub-trees of
+        // shard_size - size buckets per shard (70 of the north star's 80 at 8 shards) off the wire.
+        std::vector<std::unordered_set<std::string>> winners(naggs);
+        std::vector<char> two(naggs, 0);
+        bool any_two = false;
+        for (int a : gathered) {
+            const Block& b = first[a];
+            two[a] = c.nranks > 1 && b.type == ESGPU_AGG_TERMS && !b.subs.empty() && b.order != ESGPU_ORDER_AGG_ASC &&
+                     b.order != ESGPU_ORDER_AGG_DESC;
+            any_two |= two[a] != 0;
+        }
+        if (any_two) {
+            std::vector<std::vector<Block>> skel;
+            for (auto* l : locals) {
+                skel.emplace_back();
+                for (int a : gathered) if (two[a]) skel.back().push_back(terms_skeleton((*l)[a]));
+            }
+            std::vector<std::string> msgs = gather_messages(c, pack_lists(skel));
+            std::vector<std::vector<Block>> all;
+            for (const std::string& m : msgs) unpack_lists(m, all);
+            std::vector<const std::vector<Block>*> lists;
+            for (auto& s : all) lists.push_back(&s);
+            const std::vector<Block> red = reduce_lists(lists);
+            size_t q = 0;
+            for (int a : gathered) {
+                if (!two[a]) continue;
+                const Block& r = red[q++];
+                for (uint64_t b = 0; b < r.nbuckets(); ++b) winners[a].insert(r.term(b));
+            }
+        }
         std::vector<std::vector<Block>> mine;
         for (auto* l : locals) {
             mine.emplace_back();
-            for (int a : gathered) mine.back().push_back((*l)[a]);
+            for (int a : gathered) mine.back().push_back(two[a] ? terms_pruned((*l)[a], winners[a]) : (*l)[a]);
         }
         std::vector<std::string> msgs = gather_messages(c, pack_lists(mine));
         std::vector<std::vector<Block>> shards;
@@ -1975,13 +2041,17 @@ std::vector<Block> reduce_across(Collective& c, const std::vector<const std::vec
         lay.push_back(L);
     }
     if (!lay.empty()) {
+        // integer counts and the order-preserving extrema are exact under any combination order: all-reduced.  The f64
+        // sums are not: each shard's (sum, sum of squares) partials are all-gathered and added in global shard order,
+        // the order of the shard-order reduce (InternalStats.doReduce), so the result is bit-identical to it.
         std::vector<uint64_t> U(nu, 0), MN(nmn, ~0ULL), MX(nmx, 0);
-        std::vector<double> F(nf, 0.0);
+        std::vector<double> FS(nf * locals.size(), 0.0);  // [local shard][nf]
         for (const Layout& L : lay) {
             const bool hist = first[L.agg].is_bucket();
             const size_t du = hist ? 1 : 0;
-            for (auto* l : locals) {  // local shards in shard order
-                const Block& b = (*l)[L.agg];
+            for (size_t li = 0; li < locals.size(); ++li) {  // local shards in shard order
+                const Block& b = (*locals[li])[L.agg];
+                double* F = FS.data() + li * nf;
                 const uint64_t k0 = hist ? b.boff[0] : 0, k1 = hist ? b.boff[1] : 1;
                 for (uint64_t k = k0; k < k1; ++k) {
                     size_t slot = 0;
@@ -2004,7 +2074,16 @@ std::vector<Block> reduce_across(Collective& c, const std::vector<const std::vec
             }
         }
         if (nu) c.allreduce(U.data(), nu, ESGPU_DT_U64, ESGPU_RED_SUM);
-        if (nf) c.allreduce(F.data(), nf, ESGPU_DT_F64, ESGPU_RED_SUM);
+        std::vector<double> F(nf, 0.0);
+        if (nf) {
+            const std::vector<std::string> msgs = gather_messages(c, std::string((const char*)FS.data(), FS.size() * 8));
+            for (const std::string& m : msgs) {  // ranks in order, each rank's shards in order
+                if (m.size() % (nf * 8)) throw std::runtime_error("corrupt partial-sum message");
+                const double* v = (const double*)m.data();
+                for (size_t sh = 0; sh < m.size() / (nf * 8); ++sh)
+                    for (size_t i = 0; i < nf; ++i) F[i] += v[sh * nf + i];
+            }
+        }
         if (nmn) c.allreduce(MN.data(), nmn, ESGPU_DT_U64, ESGPU_RED_MIN);
         if (nmx) c.allreduce(MX.data(), nmx, ESGPU_DT_U64, ESGPU_RED_MAX);
         // (3) one merged shard result per aggregation, then the reference's own single-shard reduce on it (min_doc_count,

@@ -469,10 +469,12 @@ int esgpu_result_deserialize(const uint8_t* buf, size_t len, esgpu_result** out)
  *                         then ncclAllReduce sum of doc counts / value counts / sums / sums of squares, min / max of the
  *                         order-preserving u64 image of the doubles), top-level stats / extended_stats / avg, and
  *                         top-level cardinality (ncclAllReduce max over the 2^p u8 registers, or the union of the
- *                         linear-counting sets while every rank is still in LINEAR_COUNTING).  Everything else --
- *                         terms at any level, whose reduce is per-shard top-k then merge (InternalTerms.doReduce) -- is
- *                         all-gathered as shard records and reduced in shard order.  Integer-valued sums are bit-exact;
- *                         non-integer floating sums differ from the shard-order sum in the last bits only.
+ *                         linear-counting sets while every rank is still in LINEAR_COUNTING); their f64 sums are
+ *                         all-gathered per shard and added in global shard order.  Everything else -- terms at any
+ *                         level, whose reduce is per-shard top-k then merge (InternalTerms.doReduce) -- is all-gathered
+ *                         as shard records and reduced in shard order; top-level terms in a count or term order in two
+ *                         phases (terms-level records first, then only the surviving buckets' sub-aggregations).  The
+ *                         result is bit-identical to esgpu_reduce over every shard in shard order.
  *   esgpu_comm_gather_reduce: every aggregation through the all-gather path (one local shard).
  *   esgpu_comm_last_exchange: bytes moved by the last reduce on this communicator.
  *   esgpu_comm_destroy:   an RCCL communicator holds device buffers of its context: destroy it before esgpu_ctx_destroy.

@@ -3,8 +3,9 @@ esgpu_comm_init_host), several shards per rank, against esgpu_reduce over every 
 oracle's coordinator reduce.
 
 Fixed-shape partials (top-level histograms with metric subs, top-level metrics, top-level cardinality) take the
-all-reduce path; terms take the all-gather path.  With integer-valued metrics the two reduces must produce identical
-JSON; with non-integer doubles the sums agree within the parity bar (1e-12 relative)."""
+all-reduce path (their f64 sums all-gathered per shard and added in shard order); terms take the all-gather path, in
+two phases when their order is a count or term order (terms-level skeletons first, then only the surviving buckets'
+sub-aggregations).  Both reduces must produce identical JSON, for integer-valued and non-integer doubles alike."""
 import json
 import socket
 
@@ -13,7 +14,7 @@ import pytest
 
 import oracle as O
 from elasticsearch_amd import AggregationBuilders as AB
-from elasticsearch_amd import ShardResult, reduce
+from elasticsearch_amd import Order, ShardResult, reduce
 from helpers import assert_same, synthetic_columns
 from result_stream import cardinality, encode, from_shard_json
 
@@ -27,7 +28,11 @@ def _request(metric_field):
             AB.histogram("rt_hist").field("response_time_ms").interval(100).minDocCount(0).extendedBounds(-300, 1500)
               .subAggregation(AB.stats("s").field(metric_field)),
             AB.dateHistogram("busy").field("@timestamp").interval("6h").minDocCount(2000),
-            AB.extendedStats("all").field(metric_field)]
+            AB.extendedStats("all").field(metric_field),
+            AB.terms("ns").field("host").size(3).subAggregation(AB.dateHistogram("h").field("@timestamp").interval("1h")
+                                                                 .subAggregation(AB.stats("s").field(metric_field))),
+            AB.terms("by_term").field("host").size(4).order(Order.term(False)).subAggregation(
+                AB.terms("inner").field("host").size(2).order(Order.count(True)))]
 
 
 def _cards(shard, rng):
@@ -111,16 +116,34 @@ def test_comm_reduce_matches_shard_order_reduce(world):
         assert again == got
         assert ar_bytes > (1 << 13)  # the HYPERLOGLOG registers and the dense histogram partials were all-reduced
         assert ag_bytes > 0 and ncoll >= 6
-    for name in ("hosts", "per_hour", "rt_hist", "busy", "all"):  # the oracle's coordinator reduce
+    for name in ("hosts", "per_hour", "rt_hist", "busy", "all", "ns", "by_term"):  # the oracle's coordinator reduce
         assert_same(out[0][0][name], want["reduced"][name], name)
     modes = {k: out[0][0][k]["_internal"]["mode"] for k in ("small", "union", "hll")}
     assert modes == {"small": "lc", "union": "hll", "hll": "hll"}
 
 
-def test_comm_reduce_float_sums_within_parity_bar():
+def test_comm_reduce_float_sums_bit_identical():
+    """Non-integer doubles: the cross-rank sums are added in global shard order, so they are bit-identical to the
+    shard-order reduce (the oracle's reduce is compared at the parity bar: its shard sums are its own collect's)."""
     blobs, want = _shard_blobs("price")
     ref = reduce([ShardResult.deserialize(b) for b in blobs]).to_dict()
     out = _run(2, blobs)
-    assert_same(out[1][0], ref, "vs shard-order reduce", exact_floats=False)
-    for name in ("hosts", "per_hour", "rt_hist", "all"):
+    assert json.dumps(out[1][0], sort_keys=True) == json.dumps(ref, sort_keys=True)
+    for name in ("hosts", "per_hour", "rt_hist", "all", "ns"):
         assert_same(out[1][0][name], want["reduced"][name], name, exact_floats=False)
+
+
+def test_two_phase_terms_exchange_moves_fewer_bytes():
+    """The terms-level skeletons + surviving sub-trees move fewer all-gather bytes than whole shard records would
+    (esgpu_comm_gather_reduce on the same shards sends whole records for every aggregation) -- same JSON."""
+    aggs = [AB.terms("ns").field("host").size(2).subAggregation(AB.dateHistogram("h").field("@timestamp").interval("1h")
+                                                                .subAggregation(AB.stats("s").field("response_time_ms")))]
+    fields = ("host", "@timestamp", "response_time_ms")
+    shards = [(synthetic_columns(fields, 200_000, shard=s), 200_000) for s in range(2)]
+    want = O.run(shards, aggs, number_of_shards=2)
+    blobs = [encode(from_shard_json(aggs, want["shards"][s], 2)) for s in range(2)]
+    out = _run(2, blobs)
+    full = sum(len(b) for b in blobs)
+    got, _, (_, ag_bytes, _) = out[0]
+    assert_same(got, want["reduced"], "reduced")
+    assert ag_bytes < full / 2, (ag_bytes, full)
