@@ -149,6 +149,7 @@ SIGNATURES = [
     ("esgpu_routing_hash", ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int32)]),
     ("esgpu_route_shards", ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint64, ctypes.c_int32, _VP, _VP]),
     ("esgpu_murmur3_field", ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint64, _VP]),
+    ("esgpu_java_double", ctypes.c_int, [ctypes.c_double, ctypes.c_char_p, ctypes.c_size_t]),
     ("esgpu_murmur3_x64_128", ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int64, ctypes.POINTER(ctypes.c_uint64)]),
     ("esgpu_plan_create", ctypes.c_int, [_VP, ctypes.POINTER(AggSpec), ctypes.c_int32, ctypes.POINTER(Filter),
                                          ctypes.c_int32, _PP]),

@@ -10,6 +10,7 @@
 //   InternalCardinality.doReduce / HLL++ merge .. metrics/cardinality/InternalCardinality.java:103-126,
 //                                                 metrics/cardinality/HyperLogLogPlusPlus.java:201-307
 #include "esgpu_results.hpp"
+#include "java_double.hpp"
 
 #include <algorithm>
 #include <iterator>
@@ -1110,55 +1111,7 @@ std::string to_json(const std::vector<Block>& aggs) {
 // (strict_date_optional_time: yyyy-MM-dd'T'HH:mm:ss.SSSZZ) in the request's time zone.
 // ------------------------------------------------------------------------------------------------------------
 namespace {
-// Double.toString: the shortest digit string (at least two digits) that reads back as the same double, laid out as Java does -- plain
-// decimal for 1e-3 <= |v| < 1e7 (at least one fractional digit), else d.dddE<exp>.  JDK 19+ prints exactly this;
-// JDK 8's FloatingDecimal agrees except for rare values where it emits one digit more.
-std::string java_double(double v) {
-    if (v != v) return "NaN";
-    if (std::isinf(v)) return v > 0 ? "Infinity" : "-Infinity";
-    if (v == 0) return std::signbit(v) ? "-0.0" : "0.0";
-    char b[40];
-    int p = 1;
-    for (; p < 17; ++p) {
-        snprintf(b, sizeof b, "%.*e", p - 1, v);
-        if (std::strtod(b, nullptr) == v) break;
-    }
-    // Double.toString shows at least two digits: a one-digit shortest form becomes the closest two-digit decimal
-    // (Double.MIN_VALUE prints 4.9E-324, not 5.0E-324)
-    if (p < 2) p = 2;
-    snprintf(b, sizeof b, "%.*e", p - 1, v);
-    // b = [-]d[.ddd]e[+-]XX
-    std::string digits;
-    const char* q = b;
-    const bool neg = *q == '-';
-    if (neg) ++q;
-    for (; *q && *q != 'e'; ++q) if (*q != '.') digits += *q;
-    const int e10 = std::atoi(q + 1);
-    while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
-    std::string out = neg ? "-" : "";
-    const double a = std::fabs(v);
-    if (a >= 1e-3 && a < 1e7) {
-        if (e10 >= 0) {
-            const size_t ip = (size_t)e10 + 1;
-            std::string d = digits;
-            if (d.size() < ip) d.append(ip - d.size(), '0');
-            out += d.substr(0, ip);
-            out += '.';
-            out += d.size() > ip ? d.substr(ip) : "0";
-        } else {
-            out += "0.";
-            out.append((size_t)(-e10 - 1), '0');
-            out += digits;
-        }
-    } else {
-        out += digits[0];
-        out += '.';
-        out += digits.size() > 1 ? digits.substr(1) : "0";
-        out += 'E';
-        out += std::to_string(e10);
-    }
-    return out;
-}
+// Double.toString: java_double.hpp (JDK 8 FloatingDecimal)
 
 // strict_date_optional_time printer in the zone of the table (offset offs[i] from UTC instant starts[i]; empty = UTC)
 std::string es_date(int64_t ms, const std::vector<int64_t>& starts, const std::vector<int64_t>& offs) {

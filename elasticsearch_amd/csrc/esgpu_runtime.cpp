@@ -35,6 +35,7 @@
 #include "esgpu_kernels.hpp"
 #include "esgpu_results.hpp"
 #include "esgpu_internal.hpp"
+#include "java_double.hpp"
 
 using namespace esgpu;
 
@@ -679,6 +680,14 @@ extern "C" int esgpu_murmur3_x64_128(const uint8_t* bytes, size_t len, int64_t s
     return guarded([&] {
         require(out2 && (bytes || len == 0), ESGPU_ERR_INVALID, "null argument");
         murmur3_x64_128(bytes, (int)len, (uint64_t)seed, &out2[0], &out2[1]);
+    });
+}
+
+extern "C" int esgpu_java_double(double v, char* buf, size_t cap) {
+    return guarded([&] {
+        require(buf && cap >= 26, ESGPU_ERR_INVALID, "buffer under 26 bytes");
+        const std::string s = java_double(v);
+        std::memcpy(buf, s.c_str(), s.size() + 1);
     });
 }
 

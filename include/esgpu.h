@@ -309,6 +309,10 @@ int esgpu_date_rounding(const esgpu_agg_spec* spec, int32_t op, int64_t value, i
 /* MurmurHash3_x64_128 (common/hash/MurmurHash3.java:62-157): the murmur3 field's index-time hash is out[0] (h1)
  * (plugins/mapper-murmur3/.../Murmur3FieldMapper.java:152-165). */
 int esgpu_murmur3_x64_128(const uint8_t* bytes, size_t len, int64_t seed, uint64_t* out2);
+/* Double.toString(v) as the reference's JVM (Java 8, sun.misc.FloatingDecimal) prints it -- the digits every double of
+ * esgpu_result_to_xcontent carries (XContentBuilder.value(double) -> Jackson -> Double.toString).  NUL-terminated into
+ * buf (at most cap bytes incl. the NUL); returns ESGPU_ERR_INVALID when cap < 26. */
+int esgpu_java_double(double v, char* buf, size_t cap);
 
 /* ---------------------------------------------------------------------------------------------------------
  * Index-time hashing for bulk ingest: the shard a document routes to, and the murmur3 field value
