@@ -470,14 +470,19 @@ __global__ __launch_bounds__(256) void hll_lc_kernel(HllParams P) {
         for (int j = 0; j < 4; ++j) {
             if (!((ok >> j) & 1)) continue;
             const uint32_t enc = hll_encode(hv[j], P.p);
+            const unsigned long long pos = P.pos_base + (P.pos_ord ? raw[j] : (uint64_t)(i0 + j));
             uint32_t slot = (uint32_t)(mix64(enc) & P.lc_mask);
             for (uint32_t probe = 0; probe <= P.lc_threshold + 1; ++probe) {
                 const uint32_t cur = __hip_atomic_load(&P.lc_set[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (cur == enc) break;
-                if (cur == 0) {
+                bool found = cur == enc;
+                if (!found && cur == 0) {
                     const uint32_t prev = atomicCAS(&P.lc_set[slot], 0u, enc);
-                    if (prev == 0) { ++added; break; }
-                    if (prev == enc) break;
+                    if (prev == 0) ++added;
+                    found = prev == 0 || prev == enc;
+                }
+                if (found) {
+                    atomicMin(&P.lc_first[slot], pos);
+                    break;
                 }
                 if (probe == P.lc_threshold + 1) { added = P.lc_threshold + 1; break; }  // run longer than the set
                 slot = (slot + 1) & P.lc_mask;
@@ -1669,16 +1674,21 @@ __global__ __launch_bounds__(256) void card_kernel(CardParams C, int pass) {
                         continue;
                     }
                     const uint32_t enc = hll_encode(h, C.p);
+                    const unsigned long long pos = C.pos_base + (C.pos_ord ? (uint64_t)((const uint32_t*)C.col)[i] : i);
                     uint32_t* set = C.sets + b * C.cap;
                     uint32_t sl = (uint32_t)(mix64(enc) & (C.cap - 1));
                     uint32_t probe = 0;
                     for (; probe < C.cap; ++probe) {
                         const uint32_t cur = __hip_atomic_load(&set[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (cur == enc) break;
-                        if (cur == 0) {
+                        bool found = cur == enc;
+                        if (!found && cur == 0) {
                             const uint32_t was = atomicCAS(&set[sl], 0u, enc);
-                            if (was == 0) { atomicAdd(&C.set_cnt[b], 1u); break; }
-                            if (was == enc) break;
+                            if (was == 0) atomicAdd(&C.set_cnt[b], 1u);
+                            found = was == 0 || was == enc;
+                        }
+                        if (found) {
+                            atomicMin(&C.first[b * C.cap + sl], pos);
+                            break;
                         }
                         sl = (sl + 1) & (C.cap - 1);
                     }

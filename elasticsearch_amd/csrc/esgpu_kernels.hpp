@@ -122,6 +122,12 @@ struct HllParams {
     uint32_t lc_mask;
     uint32_t lc_threshold;
     uint64_t seen;              // values the registers already hold from earlier segments of this request
+    // LINEAR_COUNTING insertion order: lc_first[slot] = min over the slot's hash occurrences of pos_base + (pos_ord ?
+    // the ordinal : the value index) -- the order the reference's collector adds the hash to its Hashset (DirectCollector:
+    // doc / value order; OrdinalsCollector.postCollect: ordinal order), pos_base = the segment's sequence << 40
+    unsigned long long* lc_first;
+    uint64_t pos_base;
+    int32_t pos_ord;
 };
 
 struct GatherParams {
@@ -202,6 +208,9 @@ struct CardParams {
     uint32_t* set_cnt;           // [B]
     uint32_t* nonzero;           // [B]
     uint32_t cap, thr;
+    unsigned long long* first;   // [B][cap] insertion order of each set entry (HllParams.lc_first)
+    uint64_t pos_base;
+    int32_t pos_ord;
 };
 void launch_card(const CardParams& c, bool ord, bool hist, int pass, uint32_t grid, hipStream_t s);
 void launch_card_nonzero(const uint8_t* regs, uint64_t n_buckets, int p, uint32_t* nonzero, hipStream_t s);

@@ -173,51 +173,54 @@ static uint32_t dec_index(uint32_t enc, int p) {
     const uint32_t idx = (enc & 1) ? (enc >> 7) : (enc >> 1);
     return idx >> (kP2 - p);
 }
-// HyperLogLogPlusPlus.merge (:201-230) on one instance's state: (mode, registers, lc)
+// HyperLogLogPlusPlus (:161-330) for one bucket: LINEAR_COUNTING keeps the Hashset (:428-498) -- m / 4 int slots, linear
+// probing from (k & mask), 0 = empty -- so its values come out in the reference's slot order (writeTo :519-528 and
+// merge :201-230 iterate hashSet.values(bucket) in slot order, and the layout depends on the insertion order).
 struct HllState {
     int p = 14;
     bool present = false;
     int mode = 0;
     std::vector<uint8_t> regs;
-    std::vector<uint32_t> lc;
+    std::vector<uint32_t> table;  // LINEAR_COUNTING: the Hashset slots
+    size_t size = 0;
+    size_t threshold() const { return (size_t)((float)((1u << p) / 4) * 0.75f); }  // (int) (capacity * MAX_LOAD_FACTOR)
+    void collect_hll(uint32_t e) {  // collectHllEncoded
+        uint8_t& r = regs[dec_index(e, p)];
+        r = (uint8_t)std::max<uint32_t>(r, dec_run_len(e, p));
+    }
+    std::vector<uint32_t> lc() const {  // hashSet.values(bucket): slot order
+        std::vector<uint32_t> v;
+        v.reserve(size);
+        for (uint32_t k : table) if (k) v.push_back(k);
+        return v;
+    }
     void upgrade() {  // upgradeToHll (:309-322)
         regs.assign((size_t)1 << p, 0);
-        for (uint32_t e : lc) {
-            uint8_t& r = regs[dec_index(e, p)];
-            r = (uint8_t)std::max<uint32_t>(r, dec_run_len(e, p));
-        }
-        lc.clear();
+        for (uint32_t k : table) if (k) collect_hll(k);
+        table.clear();
+        size = 0;
         mode = 1;
+    }
+    void add(uint32_t k) {  // collectLcEncoded: Hashset.add, upgrade once the size passes the threshold
+        if (mode) { collect_hll(k); return; }
+        const uint32_t cap = (1u << p) / 4, mask = cap - 1;
+        if (table.empty()) table.assign(cap, 0);
+        for (uint32_t i = k & mask;; i = (i + 1) & mask) {
+            if (table[i] == 0) {
+                table[i] = k;
+                if (++size > threshold()) upgrade();
+                return;
+            }
+            if (table[i] == k) return;
+        }
     }
     void merge(int op, int omode, const std::vector<uint8_t>& oregs, const std::vector<uint32_t>& olc) {
         if (p != op) throw std::invalid_argument("cardinality precision mismatch");
-        const int m = 1 << p;
-        const size_t threshold = (size_t)((float)(m / 4) * 0.75f);
         if (omode == 0) {
-            if (mode == 0) {
-                // Hashset adds with an upgrade once the set exceeds the threshold: the upgraded registers are the
-                // maxima over the union, so the sorted union (then one upgrade if it is too large) is the same state
-                std::vector<uint32_t> sorted_olc;
-                const std::vector<uint32_t>* o = &olc;
-                if (!std::is_sorted(olc.begin(), olc.end())) {
-                    sorted_olc = olc;
-                    std::sort(sorted_olc.begin(), sorted_olc.end());
-                    o = &sorted_olc;
-                }
-                std::vector<uint32_t> u;
-                u.reserve(lc.size() + o->size());
-                std::set_union(lc.begin(), lc.end(), o->begin(), o->end(), std::back_inserter(u));
-                u.erase(std::unique(u.begin(), u.end()), u.end());
-                lc.swap(u);
-                if (lc.size() > threshold) upgrade();
-            } else {
-                for (uint32_t e : olc) {
-                    uint8_t& r = regs[dec_index(e, p)];
-                    r = (uint8_t)std::max<uint32_t>(r, dec_run_len(e, p));
-                }
-            }
+            for (uint32_t e : olc) add(e);  // the other sketch's values in its slot order
         } else {
             if (mode == 0) upgrade();
+            const int m = 1 << p;
             for (int i = 0; i < m; ++i) regs[i] = std::max(regs[i], oregs[i]);
         }
     }
@@ -884,7 +887,7 @@ void reduce_level(const Level& lv, Block& out) {
             out.hll_present.push_back(1);
             out.hll_mode.push_back(st.mode);
             out.regs.push_back(std::move(st.regs));
-            out.lc.push_back(std::move(st.lc));
+            out.lc.push_back(st.mode ? std::vector<uint32_t>() : st.lc());
             continue;
         }
         // InternalStats / InternalExtendedStats / InternalAvg .doReduce: sums in shard order, Math.min / Math.max
@@ -1077,7 +1080,9 @@ void write_instance(J& j, const Block& a, uint64_t i) {
                     j.raw(","); j.key("registers_fnv1a64"); j.str(b);
                 } else {
                     j.raw(","); j.key("lc_size"); j.i64((int64_t)a.lc[i].size());
-                    snprintf(b, sizeof b, "%016llx", (unsigned long long)fnv1a((const uint8_t*)a.lc[i].data(), a.lc[i].size() * 4));
+                    std::vector<uint32_t> u(a.lc[i].begin(), a.lc[i].end());  // fingerprint of the set (order-free)
+                    std::sort(u.begin(), u.end());
+                    snprintf(b, sizeof b, "%016llx", (unsigned long long)fnv1a((const uint8_t*)u.data(), u.size() * 4));
                     j.raw(","); j.key("lc_fnv1a64"); j.str(b);
                 }
             }
@@ -2116,43 +2121,54 @@ std::vector<Block> reduce_across(Collective& c, const std::vector<const std::vec
             m.lc.emplace_back();
             out[cards[k]] = std::move(m);
         }
-        if (!to_union.empty()) {  // every rank in LINEAR_COUNTING: all-gather the sets, union, upgrade past threshold
+        if (!to_union.empty()) {
+            // every rank in LINEAR_COUNTING: the shards' hash lists are all-gathered and merged in global shard order
+            // into one Hashset -- the insertion order of the shard-order reduce, so the slots (and the hashes' order on
+            // the wire) come out as the reference's coordinator lays them out
             std::string msg;
             for (int k : to_union) {
-                const uint64_t n = st[k].lc.size();
-                msg.append((const char*)&n, 8);
-                msg.append((const char*)st[k].lc.data(), n * 4);
-            }
-            const std::vector<std::string> msgs = gather_messages(c, msg);
-            for (size_t u = 0; u < to_union.size(); ++u) {
-                const int k = to_union[u];
-                const Block& proto = first[cards[k]];
-                HllState s;
-                s.p = proto.precision;
-                s.present = true;
-                for (const std::string& mm : msgs) {  // rank order; the result only depends on the union
-                    size_t pos = 0;
-                    for (size_t v = 0; v <= u; ++v) {
-                        if (pos + 8 > mm.size()) throw std::runtime_error("corrupt set message");
-                        uint64_t n;
-                        std::memcpy(&n, mm.data() + pos, 8);
-                        pos += 8;
-                        if (pos + n * 4 > mm.size()) throw std::runtime_error("corrupt set message");
-                        if (v == u) {
-                            std::vector<uint32_t> lc(n);
-                            std::memcpy(lc.data(), mm.data() + pos, n * 4);
-                            s.merge(s.p, 0, {}, lc);
-                        }
-                        pos += n * 4;
-                    }
+                for (auto* l : locals) {
+                    const Block& b = (*l)[cards[k]];
+                    const uint64_t n = b.hll_present[0] && !b.hll_mode[0] ? b.lc[0].size() : 0;
+                    msg.append((const char*)&n, 8);
+                    if (n) msg.append((const char*)b.lc[0].data(), n * 4);
                 }
-                Block m = proto.like();
+            }
+            const uint64_t nl = locals.size();
+            const std::vector<std::string> msgs = gather_messages(c, std::string((const char*)&nl, 8) + msg);
+            std::vector<HllState> merged(to_union.size());
+            for (size_t u = 0; u < to_union.size(); ++u) {
+                merged[u].p = first[cards[to_union[u]]].precision;
+                merged[u].present = true;
+            }
+            for (const std::string& mm : msgs) {  // ranks in order, each rank's shards in order
+                size_t pos = 0;
+                auto take = [&](size_t n) {
+                    if (pos + n > mm.size()) throw std::runtime_error("corrupt set message");
+                    const char* q = mm.data() + pos;
+                    pos += n;
+                    return q;
+                };
+                uint64_t nsh;
+                std::memcpy(&nsh, take(8), 8);
+                for (size_t u = 0; u < to_union.size(); ++u)
+                    for (uint64_t sh = 0; sh < nsh; ++sh) {
+                        uint64_t n;
+                        std::memcpy(&n, take(8), 8);
+                        std::vector<uint32_t> lc(n);
+                        if (n) std::memcpy(lc.data(), take(n * 4), n * 4);
+                        merged[u].merge(merged[u].p, 0, {}, lc);
+                    }
+            }
+            for (size_t u = 0; u < to_union.size(); ++u) {
+                HllState& s = merged[u];
+                Block m = first[cards[to_union[u]]].like();
                 ++m.n;
                 m.hll_present.push_back(1);
                 m.hll_mode.push_back(s.mode);
+                m.lc.push_back(s.mode ? std::vector<uint32_t>() : s.lc());
                 m.regs.push_back(std::move(s.regs));
-                m.lc.push_back(std::move(s.lc));
-                out[cards[k]] = std::move(m);
+                out[cards[to_union[u]]] = std::move(m);
             }
         }
     }

@@ -65,7 +65,7 @@ struct Block {
     std::vector<uint8_t> hll_present;
     std::vector<int32_t> hll_mode;
     std::vector<std::vector<uint8_t>> regs;
-    std::vector<std::vector<uint32_t>> lc;  // ascending encoded hashes
+    std::vector<std::vector<uint32_t>> lc;  // encoded hashes in the Hashset's slot order (HyperLogLogPlusPlus.java:428-498)
 
     Rounding rounding() const;  // histogram specs: the request's Rounding (EmptyBucketInfo)
     bool is_bucket() const { return type == ESGPU_AGG_TERMS || type == ESGPU_AGG_HISTOGRAM || type == ESGPU_AGG_DATE_HISTOGRAM; }

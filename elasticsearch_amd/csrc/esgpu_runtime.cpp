@@ -802,9 +802,11 @@ struct CardState {
     std::string field;
     uint32_t m = 0, cap = 0, thr = 0;
     DevBuf regs, sets, cnt, nonzero;  // [B][m] u8, [B][cap] u32, [B], [B]
+    DevBuf first;                     // [B][cap] u64: insertion order of each set entry (CardParams.first)
     // gathered rows of the emitted buckets (build)
     std::vector<uint8_t> h_regs;
     std::vector<uint32_t> h_sets, h_cnt, h_nz;
+    std::vector<uint64_t> h_first;
 };
 
 // host views of one pipeline's cells (its pinned staging buffers), gathered rows or the whole grid
@@ -858,6 +860,7 @@ struct Pipeline {
     // cardinality state
     int p = 14;
     DevBuf regs, lc_set, lc_count;
+    DevBuf lc_first;                 // [lc_mask + 1] u64: insertion order of each LC set entry (HllParams.lc_first)
     uint32_t lc_mask = 0, lc_threshold = 0;
     uint64_t hll_seen = 0;           // values hashed into the registers by earlier segments of this request
     // post_collection products
@@ -932,6 +935,7 @@ struct esgpu_plan {
     hipEvent_t ev_mid = nullptr;
     PinnedBuf h_tcnt, h_rows, h_dst[6];
     Scratch s_nnz;                     // build: non-empty slots per winner row (compact_rows)
+    uint32_t seg_seq = 0;              // segments collected since create / reset (cardinality insertion order)
     std::vector<PinnedBuf> h_compact;  // build: per bucket child, its GPU-compacted buckets and leaves (pinned)
 };
 
@@ -1265,10 +1269,12 @@ static void alloc_grid(esgpu_plan* p, Pipeline& pl) {
     need(pl.g_sq, pl.met >= 3, cells * 8);
     if (pl.g_sq.p) HIPX(hipMemsetAsync(pl.g_sq.p, 0, cells * 8, p->stream));
     for (CardState& cs : pl.cards) {
-        require((double)cells * (cs.m + 4.0 * cs.cap) <= 4.0 * (1ull << 30), ESGPU_ERR_UNSUPPORTED,
+        require((double)cells * (cs.m + 12.0 * cs.cap) <= 4.0 * (1ull << 30), ESGPU_ERR_UNSUPPORTED,
                 "cardinality sketches for every bucket exceed the 4 GiB per-request budget");
         need(cs.regs, true, cells * cs.m);
         need(cs.sets, true, cells * cs.cap * 4);
+        need(cs.first, true, cells * cs.cap * 8);
+        HIPX(hipMemsetAsync(cs.first.p, 0xFF, cs.first.bytes, p->stream));
         need(cs.cnt, true, cells * 4);
         need(cs.nonzero, true, cells * 4);
         HIPX(hipMemsetAsync(cs.regs.p, 0, cs.regs.bytes, p->stream));
@@ -1287,6 +1293,7 @@ static void regrid(esgpu_plan* p, Pipeline& pl, uint32_t newH, int64_t shift) {
     for (size_t i = 0; i < pl.cards.size(); ++i) {
         old_cards[i].regs = std::move(pl.cards[i].regs);
         old_cards[i].sets = std::move(pl.cards[i].sets);
+        old_cards[i].first = std::move(pl.cards[i].first);
         old_cards[i].cnt = std::move(pl.cards[i].cnt);
         old_cards[i].nonzero = std::move(pl.cards[i].nonzero);
     }
@@ -1317,6 +1324,7 @@ static void regrid(esgpu_plan* p, Pipeline& pl, uint32_t newH, int64_t shift) {
         CardState& cs = pl.cards[i];
         cp(cs.regs, old_cards[i].regs, (size_t)pl.T * cs.m);
         cp(cs.sets, old_cards[i].sets, (size_t)pl.T * cs.cap * 4);
+        cp(cs.first, old_cards[i].first, (size_t)pl.T * cs.cap * 8);
         cp(cs.cnt, old_cards[i].cnt, (size_t)pl.T * 4);
         cp(cs.nonzero, old_cards[i].nonzero, (size_t)pl.T * 4);
     }
@@ -1961,6 +1969,36 @@ static void materialize_hist_ords(esgpu_plan* p, Pipeline& pl, const esgpu_segme
 
 // cardinality leaves of a bucket pipeline: register pass, nonzero recount, linear-counting pass (per segment, in
 // order, so a bucket's set holds every encoded hash of every segment while it can still end in LINEAR_COUNTING)
+// CardinalityAggregator.pickCollector (:86-108): a keyword field whose segment has few ordinals takes the
+// OrdinalsCollector (hashes added per segment in ordinal order at postCollect), every other field the DirectCollector
+// (hashes added in doc / value order).  memoryOverhead = object reference + FixedBitSet shell (8 + 32 bytes, the
+// oracle's figures for a 64-bit JVM) + one bit per ordinal, against HyperLogLogPlusPlus.memoryUsage = 2^p.
+static int ordinals_collector(uint64_t max_ord, int p) {
+    return max_ord > 0 && (int64_t)(8 + 32 + (max_ord + 7) / 8) < ((int64_t)1 << p) / 4 ? 1 : 0;
+}
+
+// HyperLogLogPlusPlus.Hashset (:428-498) as the reference fills it: the distinct encoded hashes, each with the position
+// at which its collector first added it, added in that order into m / 4 slots by linear probing from (k & mask).
+// CardinalityAggregator.buildAggregation (:145-149) then copies the bucket's sketch into a fresh one by merge, which
+// re-adds the values in slot order (a wrapped probe run lands elsewhere the second time); returns the copy's
+// hashSet.values() -- the slot order writeTo and the coordinator's merge iterate (:519-528, :201-230)
+static std::vector<uint32_t> hashset_values(std::vector<std::pair<uint64_t, uint32_t>>& added, int p) {
+    std::sort(added.begin(), added.end());
+    const uint32_t cap = (1u << p) / 4, mask = cap - 1;
+    std::vector<uint32_t> t(cap, 0), copy(cap, 0);
+    auto put = [&](std::vector<uint32_t>& tab, uint32_t k) {
+        uint32_t i = k & mask;
+        while (tab[i] != 0 && tab[i] != k) i = (i + 1) & mask;
+        tab[i] = k;
+    };
+    for (const auto& e : added) put(t, e.second);
+    for (uint32_t k : t) if (k) put(copy, k);
+    std::vector<uint32_t> out;
+    out.reserve(added.size());
+    for (uint32_t k : copy) if (k) out.push_back(k);
+    return out;
+}
+
 static void collect_cards(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
     const bool ORD = pl.term_spec >= 0, HIST = pl.hist_spec >= 0;
     const DevColumn* oc = ORD ? (pl.ord_hist ? pl.ord_col.get() : s->col(pl.ord_field.c_str())) : nullptr;
@@ -2014,6 +2052,7 @@ static void collect_cards(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, c
             ensure_ord_hash(p->ctx, col, p->stream);
             C.ord_hash = col->ord_hash.as<uint64_t>();
             C.n_ords = col->value_count;
+            C.pos_ord = ordinals_collector(col->value_count, cs.p);
         } else {
             C.kind = col->type == ESGPU_COL_F64 ? HLL_F64 : HLL_I64;
         }
@@ -2023,6 +2062,8 @@ static void collect_cards(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, c
         C.nonzero = cs.nonzero.as<uint32_t>();
         C.cap = cs.cap;
         C.thr = cs.thr;
+        C.first = cs.first.as<unsigned long long>();
+        C.pos_base = (uint64_t)p->seg_seq << 40;
         launch_card(C, ORD, HIST, 0, grid, p->stream);
         launch_card_nonzero(C.regs, B, cs.p, C.nonzero, p->stream);
         launch_card(C, ORD, HIST, 1, grid, p->stream);
@@ -2392,6 +2433,8 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
         pl.lc_mask = cap - 1;
         pl.lc_set.alloc(p->ctx, (size_t)cap * 4);
         HIPX(hipMemsetAsync(pl.lc_set.p, 0, (size_t)cap * 4, p->stream));
+        pl.lc_first.alloc(p->ctx, (size_t)cap * 8);
+        HIPX(hipMemsetAsync(pl.lc_first.p, 0xFF, (size_t)cap * 8, p->stream));
         // counters, then the group floors, then the packed register snapshot (16-byte aligned)
         pl.lc_count.alloc(p->ctx, hll_snap_offset(m) + std::max<size_t>(m / 2, 16));
         HIPX(hipMemsetAsync(pl.lc_count.p, 0, 16, p->stream));
@@ -2409,6 +2452,7 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
         ensure_ord_hash(p->ctx, col, p->stream);
         H.ord_hash = col->ord_hash.as<uint64_t>();
         H.n_ords = col->value_count;
+        H.pos_ord = ordinals_collector(col->value_count, pl.p);
     } else {
         H.kind = col->type == ESGPU_COL_F64 ? HLL_F64 : HLL_I64;
     }
@@ -2451,6 +2495,8 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
     H.snap = pl.lc_count.as<unsigned char>() + hll_snap_offset(1u << pl.p);
     H.lc_mask = pl.lc_mask;
     H.lc_threshold = pl.lc_threshold;
+    H.lc_first = pl.lc_first.as<unsigned long long>();
+    H.pos_base = (uint64_t)p->seg_seq << 40;
     H.seen = pl.hll_seen;
     if (H.n_docs == 0) return false;
     pl.hll_seen += H.n_docs;
@@ -2485,6 +2531,7 @@ extern "C" int esgpu_plan_collect_segment(esgpu_plan* p, const esgpu_segment* s,
             pl.timed = pl.kind == 1 ? collect_hll(p, pl, s, d_accept) : collect_grid(p, pl, s, d_accept);
         }
         p->collected = true;
+        ++p->seg_seq;
     });
 }
 
@@ -2575,11 +2622,13 @@ extern "C" int esgpu_plan_post_collection(esgpu_plan* p) {
                 pl.hll_mode = 0;
                 const size_t cap = (size_t)pl.lc_mask + 1;
                 d2h_u64(p, p->h_dst[0], pl.lc_set.p, cap / 2);  // cap is a power of two >= 1024
+                d2h_u64(p, p->h_dst[1], pl.lc_first.p, cap);
                 const uint32_t* set = p->h_dst[0].as<uint32_t>();
+                const uint64_t* first = p->h_dst[1].as<uint64_t>();
                 bsync(p);
-                pl.h_lc.clear();
-                for (size_t i = 0; i < cap; ++i) if (set[i]) pl.h_lc.push_back(set[i]);
-                std::sort(pl.h_lc.begin(), pl.h_lc.end());
+                std::vector<std::pair<uint64_t, uint32_t>> added;
+                for (size_t i = 0; i < cap; ++i) if (set[i]) added.emplace_back(first[i], set[i]);
+                pl.h_lc = hashset_values(added, pl.p);
             } else {  // HYPERLOGLOG
                 pl.hll_mode = 1;
                 // registers are u32 on the device (atomicMax); pack to the reference's byte array before the copy
@@ -2699,10 +2748,11 @@ static void gather_cards(esgpu_plan* p, Pipeline& pl, const std::vector<uint32_t
         cs.h_sets.resize((size_t)n * cs.cap);
         cs.h_cnt.resize(n);
         cs.h_nz.resize(n);
+        cs.h_first.resize((size_t)n * cs.cap);
         if (!n) continue;
-        struct { const DevBuf* src; uint32_t row; void* host; } parts[4] = {
+        struct { const DevBuf* src; uint32_t row; void* host; } parts[5] = {
             {&cs.regs, cs.m, cs.h_regs.data()}, {&cs.sets, cs.cap * 4, cs.h_sets.data()},
-            {&cs.cnt, 4, cs.h_cnt.data()}, {&cs.nonzero, 4, cs.h_nz.data()}};
+            {&cs.cnt, 4, cs.h_cnt.data()}, {&cs.nonzero, 4, cs.h_nz.data()}, {&cs.first, cs.cap * 8, cs.h_first.data()}};
         for (auto& pt : parts) {
             uint8_t* d = (uint8_t*)p->s_dst[5].ensure(p->ctx, (size_t)n * pt.row);
             launch_gather_bytes(dcells, n, pt.row, pt.src->as<uint8_t>(), d, st);
@@ -2726,13 +2776,13 @@ static void append_card(const CardState& cs, size_t c, Block& r) {
         r.regs[i].assign(cs.h_regs.begin() + c * cs.m, cs.h_regs.begin() + (c + 1) * cs.m);
     } else {
         r.hll_mode[i] = 0;
-        std::vector<uint32_t>& lc = r.lc[i];
+        std::vector<std::pair<uint64_t, uint32_t>> added;
         for (size_t k = 0; k < cs.cap; ++k) {
             const uint32_t e = cs.h_sets[c * cs.cap + k];
-            if (e) lc.push_back(e);
+            if (e) added.emplace_back(cs.h_first[c * cs.cap + k], e);
         }
-        std::sort(lc.begin(), lc.end());
-        if (lc.empty()) r.hll_present[i] = 0;
+        r.lc[i] = hashset_values(added, cs.p);
+        if (r.lc[i].empty()) r.hll_present[i] = 0;
     }
 }
 
@@ -3484,6 +3534,7 @@ extern "C" int esgpu_plan_reset(esgpu_plan* p) {
             if (pl.kind == 1) {
                 HIPX(hipMemsetAsync(pl.regs.p, 0, pl.regs.bytes, p->stream));
                 HIPX(hipMemsetAsync(pl.lc_set.p, 0, pl.lc_set.bytes, p->stream));
+                HIPX(hipMemsetAsync(pl.lc_first.p, 0xFF, pl.lc_first.bytes, p->stream));
                 HIPX(hipMemsetAsync(pl.lc_count.p, 0, pl.lc_count.bytes, p->stream));
                 pl.h_lc.clear();
                 pl.h_regs.clear();
@@ -3495,6 +3546,7 @@ extern "C" int esgpu_plan_reset(esgpu_plan* p) {
             for (CardState& cs : pl.cards) {
                 HIPX(hipMemsetAsync(cs.regs.p, 0, cs.regs.bytes, p->stream));
                 HIPX(hipMemsetAsync(cs.sets.p, 0, cs.sets.bytes, p->stream));
+                HIPX(hipMemsetAsync(cs.first.p, 0xFF, cs.first.bytes, p->stream));
                 HIPX(hipMemsetAsync(cs.cnt.p, 0, cs.cnt.bytes, p->stream));
                 HIPX(hipMemsetAsync(cs.nonzero.p, 0, cs.nonzero.bytes, p->stream));
             }
@@ -3508,6 +3560,7 @@ extern "C" int esgpu_plan_reset(esgpu_plan* p) {
         }
         p->posted = false;
         p->collected = false;
+        p->seg_seq = 0;
     });
 }
 

@@ -414,7 +414,7 @@ struct esgpu_agg_block {
     const int32_t* hll_present;             /* 0 = InternalCardinality with counts == null */
     const int32_t* hll_mode;                /* 0 = linear counting, 1 = hyperloglog */
     const uint8_t* const* registers;        /* 2^precision run lengths (hll_mode 1) */
-    const uint32_t* const* lc_hashes;       /* encoded hashes, ascending (hll_mode 0) */
+    const uint32_t* const* lc_hashes;       /* encoded hashes in Hashset slot order (hll_mode 0) */
     const int64_t* lc_sizes;
     const char* order_path;                 /* terms ordered by ESGPU_ORDER_AGG_*: the sub-aggregation path, else "" */
     const char* time_zone;                  /* the spec's time_zone id ("UTC" when none) */
@@ -450,8 +450,9 @@ int esgpu_result_to_xcontent(const esgpu_result* r, char* buf, size_t cap, size_
  * HyperLogLogPlusPlus.writeTo :519-535, InternalSingleBucketAggregation.java:124-127), with StreamOutput's encodings
  * (vInt/vLong, big-endian long/int, writeString as Java chars in modified UTF-8, StreamOutput.java:118-270).
  * A JNI shim hands these bytes to StreamInput and InternalAggregations.readAggregations to get the Java objects.
- * Exception: a LINEAR_COUNTING cardinality writes its hashes in ascending order; the reference writes them in its
- * hash-table slot order, a permutation -- readFrom re-adds them to a set, so the state read back is the same.
+ * A LINEAR_COUNTING cardinality writes its hashes in the slot order of the reference's Hashset (HyperLogLogPlusPlus
+ * .java:428-528): the collect records where each hash first occurred (the order its collector -- DirectCollector or
+ * OrdinalsCollector -- adds it) and the build re-adds them in that order into a restated Hashset.
  * Same buffer contract as esgpu_result_to_json. */
 int esgpu_result_to_stream(const esgpu_result* r, uint8_t* buf, size_t cap, size_t* needed);
 /* Stream (AggregationStreams writeTo / readFrom analogue) for moving shard results between processes. */

@@ -4,7 +4,7 @@ StreamInput's encodings (C/common/io/stream/StreamInput.java).  A = core/src/mai
 aggregations, C = core/src/main/java/org/elasticsearch.
 
 decode(bytes) -> list of dicts, one per aggregation, in stream order; raises on trailing or missing bytes.
-normalized(aggs) -> the same with every LINEAR_COUNTING hash list sorted (the reference writes them in hash-table slot
+normalized(aggs) -> the same with every LINEAR_COUNTING hash list sorted (diagnostics: the set regardless of slot
 order, a permutation; HyperLogLogPlusPlus.readFrom re-adds them to a set, HyperLogLogPlusPlus.java:537-547).
 """
 import struct
@@ -229,3 +229,24 @@ def _walk(aggs):
             yield from _walk(bk["aggs"])
         yield from _walk(a.get("aggs", []))
         yield from _walk(a.get("empty_aggs", []))
+
+
+def first_diff(a, b, path="aggs"):
+    """Path and values of the first difference between two decoded trees (diagnostics)."""
+    if isinstance(a, dict) and isinstance(b, dict):
+        for k in sorted(set(a) | set(b), key=str):
+            if k not in a or k not in b:
+                return f"{path}.{k}", a.get(k), b.get(k)
+            d = first_diff(a[k], b[k], f"{path}.{k}")
+            if d:
+                return d
+        return None
+    if isinstance(a, (list, tuple)) and isinstance(b, (list, tuple)):
+        if len(a) != len(b):
+            return f"{path}[len]", len(a), len(b)
+        for i, (x, y) in enumerate(zip(a, b)):
+            d = first_diff(x, y, f"{path}[{i}]")
+            if d:
+                return d
+        return None
+    return None if a == b else (path, a, b)

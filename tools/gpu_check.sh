@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun session: GPU parity tests, kernel sweep, bench, rocprofv3 kernel-trace stats and PMC HBM-traffic passes.
 #   gpurun --timeout 1200 -- bash tools/gpu_check.sh <tag> [steps...]
-# steps: tests kbench bench prof profk pmc pmck variants (default: tests kbench bench prof pmc)
+# steps: tests kbench bench jitter export shape125 configs buildtrace prof profk pmc pmck variants (default: tests kbench bench prof pmc)
 # KBENCH_ONLY=name,name restricts the kbench sweeps (KBENCH_ARGS: extra kbench flags for variants, KBENCH_TAG: log suffix); variants = every build/variants/libesgpu_*.so via ESGPU_LIBRARY.  Every GPU step has its own time limit; the first failure ends it.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -38,6 +38,9 @@ for s in $STEPS; do
               run bench_config4 300 python3 "$R/bench.py" --workload config4 --shards 8 --docs 125000000 --cpu-docs 320000000 &&
               run bench_config5 300 python3 "$R/bench.py" --workload config5 --shards 8 --docs 125000000 --cpu-docs 320000000 &&
               run bench_ns_shards8 300 python3 "$R/bench.py" --shards 8 --docs 125000000 --cpu-docs 0 ;;
+        buildtrace) # per-phase host marks of every shard build (ESGPU_TRACE_BUILD) in the 8-shard north star
+              ESGPU_TRACE_BUILD=1 run bench_ns8_trace 300 python3 "$R/bench.py" --shards 8 --docs 125000000 --cpu-docs 0 \
+                  --steps 4 --warmup 2 ;;
         prof) cd /tmp && run rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
                   python3 "$R/bench.py" --steps 10 --warmup 3 --cpu-docs 0 --inflight 1 ;;
         profk) cd /tmp && run rocprof_kbench 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profk" -o kbench -- \
