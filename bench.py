@@ -3,17 +3,21 @@
 
 Workload (default, `north_star`): terms(host){date_histogram(@timestamp,1h){stats(response_time_ms)}} over a
 1,000,000,000-doc synthetic log shard per GPU (BASELINE.md "north star": 1B docs / 1 shard / 1 GPU), columns
-HBM-resident before timing.  One step = one shard request: reset accumulators, collect the segment (fused gfx950
-kernel), postCollection + buildAggregation (top-k on the host, winners' rows gathered on the GPU), and the
-coordinator reduce (RCCL all-gather of the shard results across ranks when N > 1).
+HBM-resident before timing.  One step = one request: for each of the GPU's shards reset accumulators, collect the
+segment (fused gfx950 kernel), postCollection + buildAggregation (top-k on the host or GPU, winners' rows compacted on
+the GPU), then the coordinator reduce (RCCL across ranks when N > 1).
 
     python bench.py --gpus N --steps K --warmup W
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-Rank 0 prints ONE JSON line.  value = docs aggregated per second for the whole job (every rank owns one 1B-doc
-shard: weak scaling).  roofline = algorithmic HBM bytes of the collect kernel per launch / its HIP-event time.
-cpu_baseline = the oracle (line-by-line restatement of the reference Java collect loop, oracle/cpu_ref.cpp) on one
-host core over a bounded synthetic shard of the same workload.
+Rank 0 prints ONE JSON line.  value = docs aggregated per second for the whole job, with `--inflight` requests in
+flight (default 2: one request's builds and reduce overlap the next one's collects).  ms_per_request_latency: one request
+at a time, its shards collected back to back (one plan and HIP stream per shard) and built on worker threads, as
+Elasticsearch runs one SEARCH thread per shard.  ms_per_step_sequential: nothing overlapping at all (one plan, collect
+-> build per shard, then the reduce); the collect kernels' HIP-event times come from that phase.
+roofline = algorithmic HBM bytes of the collect kernel per launch / its HIP-event time.  cpu_baseline = the oracle
+(line-by-line restatement of the reference Java collect loop, oracle/cpu_ref.cpp) on the host cores over a bounded
+synthetic sample of the same workload.
 """
 import argparse
 import json
@@ -174,8 +178,7 @@ def main():
                          "affinity, capped by OMP_NUM_THREADS)")
     ap.add_argument("--cpu-single-docs", type=int, default=20_000_000, help="docs of the single-thread CPU shard")
     ap.add_argument("--inflight", type=int, default=0, choices=(0, 1, 2, 3, 4),
-                    help="plans in flight (0 = 2); with one unit per shard the shard builds run on len-1 worker threads "
-                         "beside the collects")
+                    help="requests in flight (0 = 2): plan sets that alternate, one plan per shard of a request")
     ap.add_argument("--traffic", default=os.path.join(HERE, "profiles", "hbm_traffic.json"),
                     help="PMC-derived HBM bytes per collect launch (profiles/), if measured for this workload")
     args = ap.parse_args()
@@ -203,13 +206,17 @@ def main():
     aggs, filters = build_request(args.workload, shards)
     # this rank's shards: global shards rank * per_gpu ... (rank-major = the reduce's shard order)
     segs = [engine.synthetic_segment(args.docs, fields=fields, shard=rank * per_gpu + i) for i in range(per_gpu)]
-    plans = [engine.plan(aggs, filters=filters, number_of_shards=shards)]
+    probe = engine.plan(aggs, filters=filters, number_of_shards=shards)
     # fixed-shape requests (no terms): this GPU's shards are collected into one plan, one build per request; terms
     # requests build one shard result per shard (per-shard top-k) and reduce them with the other ranks'
-    merged = plans[0].shard_mergeable() and per_gpu > 1
+    merged = probe.shard_mergeable() and per_gpu > 1
+    probe.close()
     units_per_request = 1 if merged or per_gpu == 1 else per_gpu
-    inflight = args.inflight or 2  # measured for 8 shards per GPU: 2 plans 4.67 ms/step, 4 plans 4.89
-    plans += [engine.plan(aggs, filters=filters, number_of_shards=shards) for _ in range(inflight - 1)]
+    # plan sets: one plan per unit (a shard, or all of a fixed-shape request's shards); `inflight` sets alternate, so
+    # one request's builds and reduce run while the next request's collects are on the GPU
+    inflight = args.inflight or 2
+    sets = [[engine.plan(aggs, filters=filters, number_of_shards=shards) for _ in range(units_per_request)]
+            for _ in range(inflight)]
     comm = None
     if world > 1:
         uid = [ea.Communicator.unique_id() if rank == 0 else None]
@@ -218,26 +225,26 @@ def main():
 
     kernel_ms, kernel_bytes = [0.0], [0]
     final = None
-    partial = []
 
     def launch(p, unit, record):
         p.reset()
         for seg in (segs if merged or per_gpu == 1 else [segs[unit]]):
             p.collect(seg)
-            if record:  # HIP-event time of this collect (synchronises: sequential phase only)
+            if record:  # HIP-event time of this collect (synchronises: serial phase only)
                 ms, nbytes, _ = p.last_collect_stats()
                 kernel_ms[0] += ms
                 kernel_bytes[0] += nbytes
 
     host_ms = {"build": 0.0, "reduce": 0.0}
-    # Shard builds run on worker threads (one SEARCH thread per shard in ES: distinct plans are independent), the
-    # coordinating reduce of a request on its own worker (a coordinating node merges one request while the data nodes
-    # collect the next).  Requests are reduced in order; every one is finished inside the timed region (drain()).
+    # A request's shard builds run on worker threads -- Elasticsearch runs one SEARCH thread per shard of a request --
+    # and the coordinating reduce of a request on its own worker (a coordinating node merges one request while the
+    # data nodes collect the next).  Requests are reduced in order; every one finishes inside the timed region.
     from collections import deque
     from concurrent.futures import ThreadPoolExecutor
-    builders = ThreadPoolExecutor(max(1, len(plans) - 1))
+    sys.path.insert(0, os.path.join(HERE, "tests"))
+    from helpers import host_threads
+    builders = ThreadPoolExecutor(max(1, min(units_per_request, host_threads() - 2)))
     reducer = ThreadPoolExecutor(1)
-    pending = []
 
     def build_unit(p):
         t = time.perf_counter()
@@ -245,54 +252,50 @@ def main():
         host_ms["build"] += (time.perf_counter() - t) * 1e3
         return r
 
-    def reduce_request(parts):
+    def reduce_request(futs):
+        parts = [f.result() for f in futs]
         t = time.perf_counter()
         out = comm.reduce(parts) if comm else ea.reduce(parts)
         host_ms["reduce"] += (time.perf_counter() - t) * 1e3
         return out
 
-    def drain():
+    def run(n_requests, depth):
+        """n requests on `depth` plan sets: a request's collects are issued back to back (each plan has its own HIP
+        stream), its builds go to the builder threads, its reduce to the reducer; a set is reused once its previous
+        request is reduced.  depth 1: one request at a time (its shards still in parallel), the request latency."""
         nonlocal final
-        while pending:
-            final = pending.pop(0).result()
-
-    def take(pend):  # the oldest unit in flight: its shard result, in shard order
-        nonlocal partial
-        p, unit, fut = pend.popleft()
-        partial.append(fut.result() if fut is not None else build_unit(p))
-        if unit == units_per_request - 1:
-            pending.append(reducer.submit(reduce_request, partial))
-            partial = []
-            while len(pending) > 1 and pending[0].done():
-                pending.pop(0).result()
-
-    # one unit = one collect (+ build) of a shard, or of all this GPU's shards of a fixed-shape request; `depth` plans
-    # rotate, so a plan's build overlaps the next units' collect kernels.  Every request still runs reset -> collect
-    # -> build -> reduce in full.
-    def run(n_requests, record, depth):
         pend = deque()
-        k = 0
-        for _ in range(n_requests):
-            for unit in range(units_per_request):
-                p = plans[k % depth]
-                k += 1
-                while pend and (len(pend) >= depth or any(q is p for q, _, _ in pend)):
-                    take(pend)  # the plan's previous unit is built before its buffers are reset
-                launch(p, unit, record)
-                # one shard per request: the build runs here, between launches (a builder thread measured 9 % slower
-                # there); one unit per shard: on the builder threads, several shards' host builds beside the kernels
-                threaded = depth > 1 and units_per_request > 1
-                pend.append((p, unit, builders.submit(build_unit, p) if threaded else None))
+        for r in range(n_requests):
+            while len(pend) >= depth:
+                final = pend.popleft().result()
+            futs = []
+            for unit, p in enumerate(sets[r % depth]):
+                launch(p, unit, False)
+                futs.append(builders.submit(build_unit, p))
+            pend.append(reducer.submit(reduce_request, futs))
         while pend:
-            take(pend)
-        drain()
+            final = pend.popleft().result()
 
-    def timed(depth, record):
+    def run_serial(n_requests):
+        """one unit at a time on one plan: collect, build, and finally reduce, nothing overlapping -- the collect
+        kernels' HIP-event times are taken here, where no two kernels run at once"""
+        nonlocal final
+        p = sets[0][0]
+        for _ in range(n_requests):
+            parts = []
+            for unit in range(units_per_request):
+                launch(p, unit, True)
+                parts.append(build_unit(p))
+            t = time.perf_counter()
+            final = comm.reduce(parts) if comm else ea.reduce(parts)
+            host_ms["reduce"] += (time.perf_counter() - t) * 1e3
+
+    def timed(fn, *a):
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        run(args.steps, record, depth)
+        fn(*a)
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
@@ -303,15 +306,13 @@ def main():
             el = float(t.item())
         return el
 
-    run(args.warmup, False, len(plans))
-    elapsed = timed(len(plans), len(plans) == 1)
-    # one unit at a time: the sequential rate, reported alongside, and the collect kernels' HIP-event time (measured
-    # here, where no two collects overlap on the GPU)
-    if len(plans) > 1:  # host times of the sequential phase (with one plan: of the only timed phase)
-        for k in host_ms:
-            host_ms[k] = 0.0
-    elapsed_seq = timed(1, True) if len(plans) > 1 else elapsed
-    host_ms = {k: round(v / args.steps, 4) for k, v in host_ms.items()}  # per request, sequential phase
+    run(args.warmup, inflight)
+    elapsed = timed(run, args.steps, inflight)
+    elapsed_latency = timed(run, args.steps, 1) if inflight > 1 else elapsed
+    for k in host_ms:  # host times per request, from the serial phase
+        host_ms[k] = 0.0
+    elapsed_seq = timed(run_serial, args.steps)
+    host_ms = {k: round(v / args.steps, 4) for k, v in host_ms.items()}
     exchange = None
     if comm:
         ar, ag, ncoll = comm.last_exchange()
@@ -353,8 +354,6 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and args.cpu_docs > 0:
-            sys.path.insert(0, os.path.join(HERE, "tests"))
-            from helpers import host_threads
             threads = args.cpu_threads if args.cpu_threads > 0 else host_threads()
             cpu = cpu_baseline(args.workload, shards, args.cpu_docs, threads, args.cpu_single_docs)
         out = {
@@ -365,7 +364,8 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
-            "inflight_requests": len(plans),
+            "inflight_requests": inflight,
+            "ms_per_request_latency": elapsed_latency * 1000.0 / args.steps,
             "ms_per_step_sequential": elapsed_seq * 1000.0 / args.steps,
             "higher_is_better": True,
             "scaling": "strong" if args.shards > 0 else "weak",
@@ -387,8 +387,11 @@ def main():
             "check_errors": check_errors[:5],
         }
         print(json.dumps(out), flush=True)
-    for p in plans:
-        p.close()
+    builders.shutdown()
+    reducer.shutdown()
+    for st in sets:
+        for p in st:
+            p.close()
     for seg in segs:
         seg.close()
     if comm:
