@@ -179,6 +179,9 @@ def main():
     ap.add_argument("--cpu-single-docs", type=int, default=20_000_000, help="docs of the single-thread CPU shard")
     ap.add_argument("--inflight", type=int, default=0, choices=(0, 1, 2, 3, 4),
                     help="requests in flight (0 = 2): plan sets that alternate, one plan per shard of a request")
+    ap.add_argument("--scheme", default="rotate", choices=("rotate", "sets"),
+                    help="pipelined phase: rotate = `inflight` plans taken in turn by the shards of consecutive requests; "
+                         "sets = one plan per shard, `inflight` sets of them alternating between requests")
     ap.add_argument("--traffic", default=os.path.join(HERE, "profiles", "hbm_traffic.json"),
                     help="PMC-derived HBM bytes per collect launch (profiles/), if measured for this workload")
     args = ap.parse_args()
@@ -276,6 +279,30 @@ def main():
         while pend:
             final = pend.popleft().result()
 
+    def run_rotate(n_requests, depth):
+        """`depth` plans taken in turn by the units of consecutive requests (one plan's unit is built on a worker
+        thread while the next plans' collects run); a plan is reset only once its previous unit is built"""
+        nonlocal final
+        plans = [st[0] for st in sets[:depth]]
+        owner = [None] * depth
+        pend = deque()
+        k = 0
+        for _ in range(n_requests):
+            futs = []
+            for unit in range(units_per_request):
+                i = k % depth
+                k += 1
+                if owner[i] is not None:
+                    owner[i].result()
+                launch(plans[i], unit, False)
+                owner[i] = builders.submit(build_unit, plans[i])
+                futs.append(owner[i])
+            while len(pend) >= 2:
+                final = pend.popleft().result()
+            pend.append(reducer.submit(reduce_request, futs))
+        while pend:
+            final = pend.popleft().result()
+
     def run_serial(n_requests):
         """one unit at a time on one plan: collect, build, and finally reduce, nothing overlapping -- the collect
         kernels' HIP-event times are taken here, where no two kernels run at once"""
@@ -306,8 +333,9 @@ def main():
             el = float(t.item())
         return el
 
-    run(args.warmup, inflight)
-    elapsed = timed(run, args.steps, inflight)
+    pipelined = run_rotate if args.scheme == "rotate" else run
+    pipelined(args.warmup, inflight)
+    elapsed = timed(pipelined, args.steps, inflight)
     elapsed_latency = timed(run, args.steps, 1) if inflight > 1 else elapsed
     for k in host_ms:  # host times per request, from the serial phase
         host_ms[k] = 0.0
@@ -365,6 +393,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "inflight_requests": inflight,
+            "scheme": args.scheme,
             "ms_per_request_latency": elapsed_latency * 1000.0 / args.steps,
             "ms_per_step_sequential": elapsed_seq * 1000.0 / args.steps,
             "higher_is_better": True,

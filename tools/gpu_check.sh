@@ -38,6 +38,11 @@ for s in $STEPS; do
               run bench_config4 300 python3 "$R/bench.py" --workload config4 --shards 8 --docs 125000000 --cpu-docs 320000000 &&
               run bench_config5 300 python3 "$R/bench.py" --workload config5 --shards 8 --docs 125000000 --cpu-docs 320000000 &&
               run bench_ns_shards8 300 python3 "$R/bench.py" --shards 8 --docs 125000000 --cpu-docs 0 ;;
+        schemes) # pipelined-phase A/B on one box: rotating plans vs one plan per shard
+              for i in 1 2; do for sc in rotate sets; do
+                  run "bench_ns8_${sc}_$i" 300 python3 "$R/bench.py" --shards 8 --docs 125000000 --cpu-docs 0 --scheme $sc || exit 1
+                  run "bench_c5_${sc}_$i" 300 python3 "$R/bench.py" --workload config5 --shards 8 --docs 125000000 --cpu-docs 0 --scheme $sc || exit 1
+              done; done ;;
         buildtrace) # per-phase host marks of every shard build (ESGPU_TRACE_BUILD) in the 8-shard north star
               ESGPU_TRACE_BUILD=1 run bench_ns8_trace 300 python3 "$R/bench.py" --shards 8 --docs 125000000 --cpu-docs 0 \
                   --steps 4 --warmup 2 ;;
