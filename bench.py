@@ -344,7 +344,7 @@ def main():
     exchange = None
     if comm:
         ar, ag, ncoll = comm.last_exchange()
-        exchange = {"allreduce_bytes": ar, "allgather_bytes": ag, "collectives": ncoll}
+        exchange = {"allreduce_bytes": ar, "allgather_bytes": ag, "collectives": ncoll, "ms": comm.last_exchange_ms()}
 
     # self-check of the last timed request's final result (outside the timed region)
     matching = None

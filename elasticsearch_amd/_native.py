@@ -180,6 +180,7 @@ SIGNATURES = [
     ("esgpu_comm_reduce", ctypes.c_int, [_VP, ctypes.POINTER(ctypes.POINTER(Result)), ctypes.c_int32,
                                          ctypes.POINTER(ctypes.POINTER(Result))]),
     ("esgpu_comm_gather_reduce", ctypes.c_int, [_VP, ctypes.POINTER(Result), ctypes.POINTER(ctypes.POINTER(Result))]),
+    ("esgpu_comm_last_exchange_ms", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]),
     ("esgpu_comm_last_exchange", ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                                 ctypes.POINTER(ctypes.c_int32)]),
 ]

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -27,6 +28,14 @@ namespace {
 
 size_t dt_size(int dt) { return dt == ESGPU_DT_U8 ? 1 : 8; }
 
+// adds the lifetime of the scope to a collective's exchange time
+struct Clock {
+    Collective& c;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    explicit Clock(Collective& col) : c(col) {}
+    ~Clock() { c.exchange_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
+};
+
 // RCCL over xGMI: host operands staged through pinned memory into a device buffer, reduced in place on the
 // communicator's stream.  The operands are small (KB for histograms, 2^p bytes of registers, shard records).
 struct RcclCollective : Collective {
@@ -42,6 +51,7 @@ struct RcclCollective : Collective {
     }
     void allreduce(void* buf, uint64_t count, int dt, int op) override {
         if (!count) return;
+        Clock clk(*this);
         const size_t bytes = count * dt_size(dt);
         HIPX(hipSetDevice(ctx->device));
         void* h = h_in.ensure(bytes);
@@ -58,6 +68,7 @@ struct RcclCollective : Collective {
         ++collectives;
     }
     void allgather(const void* in, void* out, uint64_t bytes) override {
+        Clock clk(*this);
         HIPX(hipSetDevice(ctx->device));
         const size_t total = (size_t)bytes * nranks;
         void* hi = h_in.ensure(std::max<size_t>(bytes, 1));
@@ -80,11 +91,13 @@ struct HostCollective : Collective {
     esgpu_host_transport t{};
     void allreduce(void* buf, uint64_t count, int dt, int op) override {
         if (!count) return;
+        Clock clk(*this);
         require(t.allreduce(t.user, buf, count, dt, op) == 0, ESGPU_ERR_DEVICE, "host transport all-reduce failed");
         allreduce_bytes += count * dt_size(dt);
         ++collectives;
     }
     void allgather(const void* in, void* out, uint64_t bytes) override {
+        Clock clk(*this);
         require(t.allgather(t.user, in, out, bytes) == 0, ESGPU_ERR_DEVICE, "host transport all-gather failed");
         allgather_bytes += bytes * nranks;
         ++collectives;
@@ -165,6 +178,13 @@ extern "C" int esgpu_comm_reduce(esgpu_comm* cm, const esgpu_result* const* loca
 
 extern "C" int esgpu_comm_gather_reduce(esgpu_comm* cm, const esgpu_result* local, esgpu_result** out) {
     return comm_reduce(cm, &local, 1, out, true);
+}
+
+extern "C" int esgpu_comm_last_exchange_ms(const esgpu_comm* cm, double* ms) {
+    return guarded([&] {
+        require(cm && ms, ESGPU_ERR_INVALID, "null argument");
+        *ms = cm->coll->exchange_ms;
+    });
 }
 
 extern "C" int esgpu_comm_last_exchange(const esgpu_comm* cm, uint64_t* ar, uint64_t* ag, int32_t* n) {

@@ -1880,6 +1880,7 @@ std::vector<Block> reduce_across(Collective& c, const std::vector<const std::vec
     if (locals.empty()) throw std::invalid_argument("every rank reduces at least one local shard result");
     c.allreduce_bytes = c.allgather_bytes = 0;
     c.collectives = 0;
+    c.exchange_ms = 0;
     const std::vector<Block>& first = *locals[0];
     const size_t naggs = first.size();
     for (auto* l : locals) {

@@ -117,6 +117,7 @@ struct Collective {
     int nranks = 1, rank = 0;
     uint64_t allreduce_bytes = 0, allgather_bytes = 0;  // per reduce call (statistics)
     int32_t collectives = 0;
+    double exchange_ms = 0;                             // wall time inside the collectives of the last reduce
     virtual ~Collective() {}
     virtual void allreduce(void* buf, uint64_t count, int dtype, int op) = 0;  // in place
     virtual void allgather(const void* in, void* out, uint64_t bytes) = 0;     // out: nranks * bytes, rank order

@@ -497,6 +497,12 @@ class Communicator:
         N.check(N.lib().esgpu_comm_last_exchange(self._ptr, ctypes.byref(ar), ctypes.byref(ag), ctypes.byref(n)))
         return ar.value, ag.value, n.value
 
+    def last_exchange_ms(self):
+        """wall-clock ms the last reduce spent inside its collectives"""
+        v = ctypes.c_double()
+        N.check(N.lib().esgpu_comm_last_exchange_ms(self._ptr, ctypes.byref(v)))
+        return v.value
+
     def close(self):
         if self._ptr:
             N.check(N.lib().esgpu_comm_destroy(self._ptr))

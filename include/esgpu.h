@@ -503,6 +503,8 @@ int esgpu_comm_reduce(esgpu_comm* comm, const esgpu_result* const* locals, int32
 int esgpu_comm_gather_reduce(esgpu_comm* comm, const esgpu_result* local, esgpu_result** out);
 int esgpu_comm_last_exchange(const esgpu_comm* comm, uint64_t* allreduce_bytes, uint64_t* allgather_bytes,
                              int32_t* collectives);
+/* wall-clock milliseconds the last reduce spent inside its collectives (staging copies included) */
+int esgpu_comm_last_exchange_ms(const esgpu_comm* comm, double* ms);
 
 #ifdef __cplusplus
 }

@@ -78,7 +78,7 @@ def _worker(rank, world, port, blobs, q):
     per = len(blobs) // world
     local = [ShardResult.deserialize(b) for b in blobs[rank * per:(rank + 1) * per]]
     red = comm.reduce(local)
-    ex = comm.last_exchange()
+    ex = comm.last_exchange() + (comm.last_exchange_ms(),)
     again = comm.reduce(local)  # communicator state is reused across requests
     q.put((rank, red.to_json(), again.to_json(), ex))
     comm.close()
@@ -111,11 +111,11 @@ def test_comm_reduce_matches_shard_order_reduce(world):
     ref = reduce([ShardResult.deserialize(b) for b in blobs]).to_dict()
     out = _run(world, blobs)
     for r in range(world):
-        got, again, (ar_bytes, ag_bytes, ncoll) = out[r]
+        got, again, (ar_bytes, ag_bytes, ncoll, ex_ms) = out[r]
         assert json.dumps(got, sort_keys=True) == json.dumps(ref, sort_keys=True), f"rank {r}"
         assert again == got
         assert ar_bytes > (1 << 13)  # the HYPERLOGLOG registers and the dense histogram partials were all-reduced
-        assert ag_bytes > 0 and ncoll >= 6
+        assert ag_bytes > 0 and ncoll >= 6 and ex_ms > 0
     for name in ("hosts", "per_hour", "rt_hist", "busy", "all", "ns", "by_term"):  # the oracle's coordinator reduce
         assert_same(out[0][0][name], want["reduced"][name], name)
     modes = {k: out[0][0][k]["_internal"]["mode"] for k in ("small", "union", "hll")}
@@ -144,6 +144,6 @@ def test_two_phase_terms_exchange_moves_fewer_bytes():
     blobs = [encode(from_shard_json(aggs, want["shards"][s], 2)) for s in range(2)]
     out = _run(2, blobs)
     full = sum(len(b) for b in blobs)
-    got, _, (_, ag_bytes, _) = out[0]
+    got, _, (_, ag_bytes, _, _) = out[0]
     assert_same(got, want["reduced"], "reduced")
     assert ag_bytes < full / 2, (ag_bytes, full)
