@@ -27,6 +27,7 @@ struct SynthParams {
     const double* rt_cdf;
 };
 
+constexpr int kMaxPreds = 4;  // clauses a collect kernel evaluates itself (more: folded into a doc bitset first)
 enum PredKind : int32_t { PRED_ORD_EQ = 0, PRED_I64_RANGE = 1, PRED_F64_RANGE = 2, PRED_ORD_RANGE = 3 };
 
 struct PredDev {

@@ -935,6 +935,7 @@ struct esgpu_plan {
     hipEvent_t ev_mid = nullptr;
     PinnedBuf h_tcnt, h_rows, h_dst[6];
     Scratch s_nnz;                     // build: non-empty slots per winner row (compact_rows)
+    Scratch s_xbits;                   // doc bitset of a pipeline with more than kMaxPreds clauses
     uint32_t seg_seq = 0;              // segments collected since create / reset (cardinality insertion order)
     std::vector<PinnedBuf> h_compact;  // build: per bucket child, its GPU-compacted buckets and leaves (pinned)
 };
@@ -1176,16 +1177,13 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
             if (f.hi_term) { p->filter_hi[k].assign((const char*)f.hi_term, (size_t)f.hi_term_len); f.hi_term = (const uint8_t*)p->filter_hi[k].data(); }
             f.field = nullptr;  // filter_fields[k] holds it
         }
-        // every pipeline evaluates the query clauses plus those of its filter aggregation: at most 4 predicates
-        int nquery = 0;
-        for (int o : p->filter_owner) nquery += o < 0;
-        require(nquery <= 4, ESGPU_ERR_UNSUPPORTED, "at most 4 filter clauses run on the GPU path");
+        // every pipeline evaluates the query clauses plus those of its filter aggregation (set_preds folds more than
+        // kMaxPreds of them into a doc bitset)
         for (int r : tops) {
             if (p->specs[r].s.type != ESGPU_AGG_FILTER) continue;
             int own = 0;
             for (int o : p->filter_owner) own += o == r;
             require(own >= 1, ESGPU_ERR_INVALID, "filter aggregation without a filter clause");
-            require(nquery + own <= 4, ESGPU_ERR_UNSUPPORTED, "at most 4 filter clauses run on the GPU path");
             for (int ch : p->specs[r].children)
                 require(p->specs[ch].s.type != ESGPU_AGG_FILTER, ESGPU_ERR_UNSUPPORTED, "nested filter aggregations");
         }
@@ -1382,8 +1380,12 @@ static bool applies(const esgpu_plan* p, const Pipeline& pl, size_t k) {
     return p->filter_owner[k] < 0 || p->filter_owner[k] == pl.fspec;
 }
 
+// The pipeline's clauses as device predicates: up to kMaxPreds of them are evaluated inside the collect kernels; with
+// more, all of them (and the accept bitset) are folded first into one doc bitset -- chained filter_bits passes of four
+// clauses each -- which replaces *accept, and no predicate is left for the kernel.
 static void set_preds(esgpu_plan* p, const Pipeline& pl, const esgpu_segment* s, PredDev* out, int32_t* npred,
-                      uint64_t* bytes_per_doc) {
+                      uint64_t* bytes_per_doc, const uint64_t** accept) {
+    std::vector<PredDev> all;
     *npred = 0;
     for (size_t k = 0; k < p->filters.size(); ++k) {
         if (!applies(p, pl, k)) continue;
@@ -1455,8 +1457,21 @@ static void set_preds(esgpu_plan* p, const Pipeline& pl, const esgpu_segment* s,
             }
             *bytes_per_doc += 8;
         }
-        out[(*npred)++] = q;
+        all.push_back(q);
     }
+    if (all.size() <= (size_t)kMaxPreds) {
+        for (const PredDev& q : all) out[(*npred)++] = q;
+        return;
+    }
+    uint64_t* bits = (uint64_t*)p->s_xbits.ensure(p->ctx, std::max<size_t>(s->n_pad / 64, 1) * 8);
+    const uint64_t* in = *accept;
+    for (size_t k = 0; k < all.size(); k += kMaxPreds) {
+        launch_filter_bits(s->max_doc, in, all.data() + k, (int)std::min<size_t>(kMaxPreds, all.size() - k), bits, p->stream);
+        HIPX(hipGetLastError());
+        in = bits;  // in place: each thread reads and rewrites its own word
+    }
+    *accept = bits;
+    *bytes_per_doc += 0;  // the clause columns were counted above; the bitset the kernel then reads is 1 bit per doc
 }
 
 // K1 for valueCount >> LDS (e.g. 10M url ordinals): radix-partitioned counting instead of global atomics, which
@@ -2029,10 +2044,10 @@ static void collect_cards(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, c
     PredDev pred[4];
     int npred = 0;
     uint64_t fbytes = 0;
-    set_preds(p, pl, s, pred, &npred, &fbytes);
+    set_preds(p, pl, s, pred, &npred, &fbytes, &G.accept);
     if (npred > 0) {
         uint64_t* bits = (uint64_t*)p->s_fbits.ensure(p->ctx, std::max<size_t>(s->n_pad / 64, 1) * 8);
-        launch_filter_bits(s->max_doc, d_accept, pred, npred, bits, p->stream);
+        launch_filter_bits(s->max_doc, G.accept, pred, npred, bits, p->stream);
         HIPX(hipGetLastError());
         G.accept = bits;
     }
@@ -2280,7 +2295,8 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     P.accept = d_accept;
     if (inner_missing) { P.mv = nullptr; P.mv_present = nullptr; P.mv_f64 = 0; }
     uint64_t bytes_per_doc = (oc ? (pl.ord_hist ? 8 : 4) : 0) + (hc ? (pl.inner_terms ? 4 : 8) : 0) + (mc && !inner_missing ? 8 : 0);
-    set_preds(p, pl, s, P.pred, &P.npred, &bytes_per_doc);
+    set_preds(p, pl, s, P.pred, &P.npred, &bytes_per_doc, &P.accept);
+    d_accept = P.accept;  // the clauses folded into a bitset when there are more than kMaxPreds
     P.g_cnt = inner_missing ? pl.g_ocnt.as<unsigned long long>() : pl.g_cnt.as<unsigned long long>();
     P.g_ocnt = pl.g_ocnt.as<unsigned long long>();
     P.g_vcnt = pl.g_vcnt.as<unsigned long long>();
@@ -2456,7 +2472,8 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
     } else {
         H.kind = col->type == ESGPU_COL_F64 ? HLL_F64 : HLL_I64;
     }
-    set_preds(p, pl, s, H.pred, &H.npred, &bytes_per_doc);
+    set_preds(p, pl, s, H.pred, &H.npred, &bytes_per_doc, &H.accept);
+    d_accept = H.accept;
     bool multi_pred = false;
     for (int k = 0; k < H.npred; ++k) multi_pred |= H.pred[k].offsets != nullptr;
     uint64_t bytes = bytes_per_doc * (uint64_t)s->max_doc;

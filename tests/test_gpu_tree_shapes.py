@@ -153,3 +153,20 @@ def test_filter_aggregation_with_mixed_children(engine):
         .subAggregation(AB.dateHistogram("d").field("@timestamp").interval("1d"))
         .order(Order.aggregation("rt", False))).subAggregation(AB.stats("b").field("bytes"))]
     _both(engine, aggs, shards=2, filters=[QB.rangeQuery("bytes").gte(512)])
+
+
+def test_more_than_four_clauses(engine):
+    """Six query clauses (bool.filter) plus three of a filter aggregation: more than the four a collect kernel evaluates
+    itself, so each pipeline folds its clauses (and the accept bits) into one doc bitset first (set_preds); terms,
+    histograms, metrics and a cardinality leaf all read that bitset."""
+    q = [QB.rangeQuery("bytes").gte(100), QB.rangeQuery("bytes").lt(900_000), QB.rangeQuery("response_time_ms").gte(5),
+         QB.rangeQuery("response_time_ms").lte(990), QB.rangeQuery("price").gt(1.0), QB.termQuery("status", 200)]
+    aggs = [AB.terms("hosts").field("host").size(6).subAggregation(AB.stats("rt").field("response_time_ms"))
+            .subAggregation(AB.cardinality("ips").field("client_ip.hash")),
+            AB.filter("f", [QB.rangeQuery("bytes").gte(5000), QB.rangeQuery("response_time_ms").lt(500),
+                            QB.rangeQuery("price").lt(400.0)])
+            .subAggregation(AB.dateHistogram("d").field("@timestamp").interval("1d")
+                            .subAggregation(AB.avg("b").field("bytes"))),
+            AB.extendedStats("all").field("bytes")]
+    red = _both(engine, aggs, shards=2, filters=q, exact=False)
+    assert red["f"]["doc_count"] > 0
