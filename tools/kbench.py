@@ -85,6 +85,9 @@ def main():
     ap.add_argument("--ts-jitter", type=int, default=0,
                     help="@timestamp displacement bound in ms (0 = time-sorted docs; 60000 / 3600000 = roughly sorted)")
     ap.add_argument("--shards", type=int, default=1, help="number_of_shards of the request (terms shard_size heuristic)")
+    ap.add_argument("--deletes", type=float, default=0.0,
+                    help="fraction of deleted docs: every request passes a live-docs accept bitset with that many random "
+                         "docs cleared (Lucene liveDocs; the high-cardinality terms path then takes its scatter form)")
     ap.add_argument("--real-dict", action="store_true",
                     help="re-upload host/url as ordinary keyword columns with their term bytes (esgpu_segment_upload with a "
                          "dictionary), so the build resolves winners through a real 10M-term dictionary")
@@ -99,8 +102,17 @@ def main():
     seg = e.synthetic_segment(args.docs, fields=tuple(sorted(fields)), ts_jitter_ms=args.ts_jitter)
     if args.real_dict:
         seg = _with_real_dicts(e, seg, args.docs, sorted(fields))
+    accept = None
+    if args.deletes > 0:  # live docs: a random `deletes` fraction cleared, as u64 words (include/esgpu.h layout)
+        rng = np.random.default_rng(7)
+        words = np.full((args.docs + 63) // 64, np.uint64(0xFFFFFFFFFFFFFFFF), dtype=np.uint64)
+        dead = rng.choice(args.docs, size=int(args.docs * args.deletes), replace=False)
+        np.bitwise_and.at(words, dead // 64, ~(np.uint64(1) << (dead % 64).astype(np.uint64)))
+        if args.docs % 64:
+            words[-1] &= np.uint64((1 << (args.docs % 64)) - 1)
+        accept = words
     print(json.dumps({"generated_s": time.time() - t, "hbm_gb": e.hbm_used() / 1e9, "ts_jitter_ms": args.ts_jitter,
-                      "shards": args.shards}), flush=True)
+                      "shards": args.shards, "deletes": args.deletes}), flush=True)
     for name, (aggs, flt) in vs.items():
         plan = e.plan(aggs, filters=flt, number_of_shards=args.shards)
         ms = []
@@ -110,7 +122,7 @@ def main():
             t0 = time.perf_counter()
             plan.reset()
             t1 = time.perf_counter()
-            plan.collect(seg)
+            plan.collect(seg, accept_bits=accept)
             t2 = time.perf_counter()
             k, nbytes, path = plan.last_collect_stats()
             t3 = time.perf_counter()
@@ -129,7 +141,7 @@ def main():
                 parts["build_wait"].append(bwait)
         kms = sorted(ms)[len(ms) // 2]
         gbs = nbytes / (kms / 1e3) / 1e9
-        print(json.dumps({"name": name, "ts_jitter_ms": args.ts_jitter, "kernel_ms": round(kms, 4), "bytes": nbytes, "gbs": round(gbs, 1),
+        print(json.dumps({"name": name, "ts_jitter_ms": args.ts_jitter, "deletes": args.deletes, "kernel_ms": round(kms, 4), "bytes": nbytes, "gbs": round(gbs, 1),
                           "frac": round(gbs / 8000, 4), "path": path, "step_ms": round(sorted(steps)[len(steps) // 2], 3),
                           "docs_per_s": args.docs / (kms / 1e3),
                           "parts_ms": {k: round(sorted(v)[len(v) // 2], 3) for k, v in parts.items()}}), flush=True)
