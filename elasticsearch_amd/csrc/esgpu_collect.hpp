@@ -25,10 +25,7 @@ constexpr int kItersPerBlock = kBlockDocs / kIterDocs;  // 4
 #define ESGPU_MAX_PASSES 8
 #endif
 constexpr int kMaxPasses = ESGPU_MAX_PASSES;
-#ifndef ESGPU_GROUP_BLOCKS  // blocks per multi-pass group
-#define ESGPU_GROUP_BLOCKS 4
-#endif
-constexpr uint32_t kGroup = ESGPU_GROUP_BLOCKS;
+constexpr uint32_t kGroup = kGroupBlocks;  // blocks per multi-pass group (esgpu_kernels.hpp)
 #ifndef ESGPU_NBUF_NARROW  // load buffers in flight per thread for shapes reading one narrow column
 #define ESGPU_NBUF_NARROW 2  // measured: 4 no faster for terms(host), 4 % slower for date_histogram
 #endif
@@ -531,6 +528,16 @@ __device__ void flush_window(const CollectParams& P, const Acc& s, uint32_t T, u
     __syncthreads();
 }
 
+// next chunk of a dynamically claimed collect (thread 0 only).  The counter address goes through an opaque VGPR zero:
+// with a provably uniform address the atomic optimizer broadcasts the returned value at once (v_readfirstlane right
+// after the atomic, i.e. a vmcnt(0) wait that drains the wave's prefetched loads); this way the value is first used a
+// chunk later, when the claim is published.
+__device__ __forceinline__ uint32_t claim_chunk(unsigned int* claim) {
+    uint32_t zero;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
+    return atomicAdd(claim + zero, 1u);  // chunks claimed past the grid's first gridDim.x
+}
+
 // HK: 0 = no histogram dimension, 1 = affine rounding, 2 = bucket table (calendar units / DST zones)
 // WGS: threads per workgroup -- 512 (two resident per CU, each with an LDS window of <= 64 KB), or 1024 for
 // histogram grids whose data needs a wider window than 64 KB holds (one workgroup per CU with up to 150 KB of LDS,
@@ -592,10 +599,25 @@ __global__ __launch_bounds__(WGS) void collect_kernel(CollectParams P) {
         __syncthreads();
     }
 
-    const uint32_t b_begin = blockIdx.x * P.blocks_per_wg;
-    uint32_t b_end = b_begin + P.blocks_per_wg;
-    if (b_end > P.n_blocks) b_end = P.n_blocks;
-    if (b_begin >= b_end) return;
+    // dynamic claiming: a workgroup's blocks are chunks of kGroup blocks (= the multi-pass groups) taken from a
+    // counter while they last, so the workgroups that run faster (a CU holding one workgroup, an idle XCD) take more
+    // and the single wave of resident workgroups ends together.  Thread 0 claims one chunk ahead: the claim issued
+    // at the start of chunk k is published (LDS + the barrier) at the start of chunk k + 1, and names chunk k + 2,
+    // so its latency hides behind a chunk of loads and the prefetch into the next chunk knows where to go.
+    const bool dyn = P.claim != nullptr;
+    __shared__ uint32_t claim_lds[2];
+    uint32_t claim_pend = 0, claim_k = 0, nxt_c = ~0u;
+    uint32_t b_begin, b_end;
+    if (dyn) {
+        b_begin = blockIdx.x * kGroup;
+        b_end = P.n_blocks;
+        if (threadIdx.x == 0) claim_pend = claim_chunk(P.claim);
+    } else {
+        b_begin = blockIdx.x * P.blocks_per_wg;
+        b_end = b_begin + P.blocks_per_wg;
+        if (b_end > P.n_blocks) b_end = P.n_blocks;
+        if (b_begin >= b_end) return;
+    }
 
     // window state (only meaningful with HIST && lds_mode)
     uint32_t win0 = 0;
@@ -648,6 +670,13 @@ __global__ __launch_bounds__(WGS) void collect_kernel(CollectParams P) {
             // would drain the prefetched buffers
             const uint32_t b = __builtin_amdgcn_readfirstlane(cb);
             if (cb == gb && pass == 0) {
+                if (dyn) {  // publish the pending claim (the chunk after this one), then claim the one after that
+                    if (threadIdx.x == 0) claim_lds[claim_k & 1] = gridDim.x + claim_pend;
+                    __syncthreads();
+                    nxt_c = __builtin_amdgcn_readfirstlane(claim_lds[claim_k & 1]);
+                    if (threadIdx.x == 0 && nxt_c < P.n_chunks) claim_pend = claim_chunk(P.claim);
+                    ++claim_k;
+                }
                 use_lds = P.lds_mode != 0;
                 npass = 1;
                 if (use_lds && HIST && P.windowed) {
@@ -692,6 +721,7 @@ __global__ __launch_bounds__(WGS) void collect_kernel(CollectParams P) {
             nit -= kItersPerBlockW;
             nb = cb + 1;
             if (nb == ge && pass + 1 < npass) nb = gb;
+            else if (dyn && nb == ge) nb = nxt_c < P.n_chunks ? nxt_c * kGroup : cb;
             nb = min(nb, b_end - 1);
         }
         load_docs<ORD, HIST, MET, VKL>(P, nb * kBlockDocs + nit * kIterDocsW + tid4, q);
@@ -707,7 +737,12 @@ __global__ __launch_bounds__(WGS) void collect_kernel(CollectParams P) {
             } else {
                 pass = 0;
                 npass = 1;
-                gb = ge;
+                if (dyn) {
+                    if (nxt_c >= P.n_chunks) break;
+                    gb = cb = nxt_c * kGroup;
+                } else {
+                    gb = ge;
+                }
                 ge = min(gb + kGroup, b_end);
             }
         }
@@ -715,6 +750,13 @@ __global__ __launch_bounds__(WGS) void collect_kernel(CollectParams P) {
     if (P.lds_mode && (dirty || !(HIST && P.windowed))) {
         if (!ORD) runs_flush<MET, kMS>(P, s, run);
         flush_window<MET, kMS, WGS>(P, s, T, W, win0, ncp);
+    }
+    if (dyn && threadIdx.x == 0) {  // the last workgroup to finish re-arms the counter pair (vector atomics only)
+        __threadfence();
+        if (atomicAdd(&P.claim[1], 1u) == gridDim.x - 1) {
+            atomicExch(&P.claim[0], 0u);
+            atomicExch(&P.claim[1], 0u);
+        }
     }
 }
 

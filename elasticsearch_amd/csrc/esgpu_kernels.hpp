@@ -27,6 +27,13 @@ struct SynthParams {
     const double* rt_cdf;
 };
 
+#ifndef ESGPU_GROUP_BLOCKS  // collect: blocks per multi-pass group (and per dynamically claimed chunk)
+#define ESGPU_GROUP_BLOCKS 4
+#endif
+constexpr uint32_t kGroupBlocks = ESGPU_GROUP_BLOCKS;
+#ifndef ESGPU_DYN_CLAIM  // collect: claim chunks dynamically (1) or split the blocks statically (0); env ESGPU_DYN overrides
+#define ESGPU_DYN_CLAIM 0
+#endif
 constexpr int kMaxPreds = 4;  // clauses a collect kernel evaluates itself (more: folded into a doc bitset first)
 enum PredKind : int32_t { PRED_ORD_EQ = 0, PRED_I64_RANGE = 1, PRED_F64_RANGE = 2, PRED_ORD_RANGE = 3 };
 
@@ -98,6 +105,11 @@ struct CollectParams {
     unsigned long long* g_min;
     unsigned long long* g_max;
     double* g_sq;
+    // dynamic chunk claiming (null: static ranges of blocks_per_wg blocks): the grid is the resident workgroup slots,
+    // workgroup g starts on chunk g (kGroup blocks) and claims later chunks from claim[0]; claim[1] counts finished
+    // workgroups, and the last one resets both, so the pair is zero again for the next launch on the plan's stream
+    unsigned int* claim;
+    uint32_t n_chunks;
 };
 
 enum HllKind : int32_t { HLL_I64 = 0, HLL_F64 = 1, HLL_ORD = 2 };

@@ -571,6 +571,20 @@ void reduce_terms(const Ref* refs, size_t nrefs, Block& out, Scratch& sc, std::v
         vals.resize(sc.buckets.size());
         for (size_t b = 0; b < sc.buckets.size(); ++b) {
             const OutBucket& ob = sc.buckets[b];
+            sc.buckets[b].val = (uint32_t)b;
+            if (out.subs[j].type == ESGPU_AGG_CARDINALITY) {  // InternalCardinality.doReduce, then .value()
+                if (!key.empty() && key != "value") throw std::invalid_argument("Invalid order path [" + out.order_path + "]");
+                HllState st;
+                for (uint32_t c = ob.c0; c < ob.c1; ++c) {
+                    const Block& m = sc.contrib[c].b->subs[j];
+                    const uint64_t i = sc.contrib[c].i;
+                    if (!m.hll_present[i]) continue;
+                    if (!st.present) { st.present = true; st.p = m.precision; st.mode = 0; }
+                    st.merge(m.precision, m.hll_mode[i], m.regs[i], m.lc[i]);
+                }
+                vals[b] = (double)(st.present ? hll_cardinality(st.p, true, st.mode, st.regs.data(), st.mode ? 0 : st.lc().size()) : 0);
+                continue;
+            }
             int64_t cnt = 0;
             double sum = 0, mn = INFINITY, mx = -INFINITY, sq = 0;
             for (uint32_t c = ob.c0; c < ob.c1; ++c) {

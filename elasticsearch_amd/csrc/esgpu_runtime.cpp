@@ -928,6 +928,7 @@ struct esgpu_plan {
     Scratch s_fbits, s_vbits;  // doc bitset of multi-valued filters, per-value bitset of a multi-valued HLL field
     Scratch s_cells;           // cell list of a cardinality gather
     Scratch s_zkey;            // per-block key ranges of a windowed collect
+    DevBuf d_claim;            // collect kernel's chunk-claim counter pair (zeroed once; every launch leaves it zero)
     Scratch s_hcur, s_hused, s_hslab;  // hot/cold counting: overflow cursors, static-region fills, hot slabs
     PinnedBuf h_hcerr;         // hot/cold counting: capacity-violation word (written by the scatter kernel)
     bool hc_check = false;     // a hot/cold collect ran since the last post_collection
@@ -1198,7 +1199,18 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
             require(n.order_child >= 0, ESGPU_ERR_INVALID, "Invalid term-aggregator order path [" + n.order_path +
                     "]. Unknown aggregation [" + name + "]");
             const int t = p->specs[n.order_child].s.type;
-            require(t != ESGPU_AGG_CARDINALITY, ESGPU_ERR_UNSUPPORTED, "terms ordered by a cardinality runs on the CPU path");
+            if (t == ESGPU_AGG_CARDINALITY) {
+                // CardinalityAggregator.metric(bucketOrd) = counts.cardinality(bucketOrd) (a single-value metric): every
+                // candidate ordinal's sketch estimate, derived at build for a top-level terms (or one under a top-level
+                // filter); under another bucket level the per-row sketches are not gathered for selection
+                const int par = n.s.parent;
+                require(par < 0 || (p->specs[par].s.type == ESGPU_AGG_FILTER && p->specs[par].s.parent < 0), ESGPU_ERR_UNSUPPORTED,
+                        "terms under another bucket aggregation ordered by a cardinality runs on the CPU path");
+                require(key.empty() || key == "value", ESGPU_ERR_INVALID, "Invalid terms aggregation order path [" + n.order_path +
+                        "]. Ordering on a single-value metrics aggregation can only be done on its value.");
+                n.order_key = key;
+                continue;
+            }
             require(is_metric(t), ESGPU_ERR_INVALID, "Invalid terms aggregation order path [" + n.order_path +
                     "]. Terms buckets can only be sorted on a sub-aggregator path that is built out of zero or more "
                     "single-bucket aggregations within the path and a final single-bucket or a metrics aggregation at the path end.");
@@ -2403,7 +2415,23 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     const uint32_t slots = (uint32_t)p->ctx->cus * wg_per_cu;
     const uint32_t min_bpw = L_ORD ? std::min<uint32_t>(ESGPU_MIN_BPW, (P.n_blocks + slots - 1) / slots) : 1u;
     P.blocks_per_wg = std::max(std::max(1u, bpw), min_bpw);
-    const uint32_t grid = (P.n_blocks + P.blocks_per_wg - 1) / P.blocks_per_wg;
+    uint32_t grid = (P.n_blocks + P.blocks_per_wg - 1) / P.blocks_per_wg;
+    // dynamic chunk claiming: one resident wave of workgroups, each flushing its LDS cells once, taking chunks of
+    // kGroup blocks until none are left (ESGPU_DYN=0/1 overrides the build default for A/B runs)
+    static const int dyn_claim = [] {
+        const char* e = std::getenv("ESGPU_DYN");
+        return e && *e ? (*e == '1' ? 1 : 0) : ESGPU_DYN_CLAIM;
+    }();
+    P.claim = nullptr;
+    P.n_chunks = (P.n_blocks + kGroupBlocks - 1) / kGroupBlocks;
+    if (dyn_claim && P.n_chunks > slots) {
+        if (!p->d_claim.p) {
+            p->d_claim.alloc(p->ctx, 16);
+            HIPX(hipMemsetAsync(p->d_claim.p, 0, 16, p->stream));
+        }
+        P.claim = (unsigned int*)p->d_claim.p;
+        grid = slots;
+    }
     if (P.lds_mode && P.windowed) {
         P.zkey = (const int64_t*)p->s_zkey.ensure(p->ctx, (size_t)std::max(P.n_blocks, 1u) * 16);
         launch_zone_keys(P, const_cast<int64_t*>(P.zkey), p->stream);
@@ -2803,6 +2831,17 @@ static void append_card(const CardState& cs, size_t c, Block& r) {
     }
 }
 
+// the estimate of gathered row c's sketch (CardinalityAggregator.metric -> HyperLogLogPlusPlus.cardinality :270-282:
+// LINEAR_COUNTING over the set's size, else the HLL++ estimate; a sketch that saw no value counts 0)
+static int64_t card_estimate(const CardState& cs, size_t c) {
+    const uint32_t nz = cs.h_nz[c], cnt = cs.h_cnt[c];
+    if (nz == 0 && cnt == 0) return 0;
+    if (nz > cs.thr || cnt > cs.thr) return hll_cardinality(cs.p, true, 1, cs.h_regs.data() + c * cs.m, 0);
+    size_t n = 0;
+    for (size_t k = 0; k < cs.cap; ++k) n += cs.h_sets[c * cs.cap + k] != 0;
+    return n ? hll_cardinality(cs.p, true, 0, nullptr, n) : 0;
+}
+
 // the numeric partials of leaf j of a pipeline at host cell c: (count, sum, min, max, sum of squares)
 struct MetricCell { int64_t count; double sum, min, max, sq; };
 static MetricCell metric_cell(const esgpu_plan* p, const Pipeline& pl, int j, size_t c) {
@@ -3092,11 +3131,25 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
     } else {
         d2h_u64(p, p->h_tcnt, dcnt, T);
         const unsigned long long* tcnt = p->h_tcnt.as<unsigned long long>();
-        if (agg_order) fetch_grid(p, p->pipes[ord_ref.pipe]);  // every ordinal's metric partials
+        const bool card_order = agg_order && p->specs[tn.order_child].s.type == ESGPU_AGG_CARDINALITY;
+        std::vector<double> card_vals;
+        if (card_order) {  // every ordinal's sketch, gathered, and its estimate (HyperLogLogPlusPlus.cardinality)
+            Pipeline& OPc = p->pipes[ord_ref.pipe];
+            std::vector<uint32_t> all(T);
+            for (uint32_t o = 0; o < T; ++o) all[o] = o;
+            gather_cards(p, OPc, all);
+            card_vals.assign(T, 0.0);
+            for (const CardState& cs : OPc.cards)
+                if (cs.spec == tn.order_child)
+                    for (uint32_t o = 0; o < T; ++o) card_vals[o] = (double)card_estimate(cs, o);
+        } else if (agg_order) {
+            fetch_grid(p, p->pipes[ord_ref.pipe]);  // every ordinal's metric partials
+        }
         bsync(p);
         const Pipeline* OP = agg_order ? &p->pipes[ord_ref.pipe] : nullptr;
-        top = select_terms(tn.s, tcnt, (uint32_t)P0.value_count, &other,
-                           [&](uint32_t ord) { return order_value(p, tn, *OP, ord_ref.leaf, ord); });
+        top = select_terms(tn.s, tcnt, (uint32_t)P0.value_count, &other, [&](uint32_t ord) {
+            return card_order ? card_vals[ord] : order_value(p, tn, *OP, ord_ref.leaf, ord);
+        });
     }
     bmark(p, "selected");
     const uint32_t k = (uint32_t)top.size();

@@ -929,7 +929,9 @@ struct StatsAgg : Aggregator {
     InternalPtr build_empty() override { return make(0, 0.0, INFINITY, -INFINITY, 0.0); }
 };
 
+static double card_metric(Aggregator* a, const std::string& key, int64_t b);
 static double sub_metric(Aggregator* a, const std::string& key, int64_t b) {  // StatsAggegator / AvgAggregator .metric
+    if (a->f->spec.type == ESGPU_AGG_CARDINALITY) return card_metric(a, key, b);
     StatsAgg* sa = dynamic_cast<StatsAgg*>(a);
     if (!sa) throw std::invalid_argument("terms order path must name a metrics aggregation");
     const bool have = sa->values && b < (int64_t)sa->counts.size();
@@ -1026,6 +1028,16 @@ struct CardinalityAgg : Aggregator {
     }
     InternalPtr build_empty() override { return make(nullptr); }
 };
+
+// CardinalityAggregator.metric (:136-138): counts.cardinality(bucketOrd), a single-value metric (InternalOrder.Aggregation
+// accepts no other key than "value"); the collectors have posted their hashes before buildAggregation asks
+static double card_metric(Aggregator* a, const std::string& key, int64_t b) {
+    if (!key.empty() && key != "value")
+        throw std::invalid_argument("Ordering on a single-value metrics aggregation can only be done on its value.");
+    CardinalityAgg* ca = dynamic_cast<CardinalityAgg*>(a);
+    if (!ca || !ca->counts || b >= ca->counts->max_bucket()) return 0.0;
+    return (double)ca->counts->cardinality(b);
+}
 
 // FilterAggregator (A/bucket/filter/FilterAggregator.java:57-81): a SingleBucketAggregator; collect(doc, bucket) counts
 // the doc into docCounts[bucket] and collects the sub-aggregators iff the doc matches the filter's query.  Not wrapped
@@ -1159,8 +1171,11 @@ static InternalPtr reduce_one(const InternalList& aggs) {
                 std::string name, key;
                 split_path(first.order_path, &name, &key);
                 auto value = [&](const Bucket& b) {
-                    for (const InternalPtr& a : b.aggs)
-                        if (a->name == name) return metric_of(a->type, key, a->count, a->sum, a->min, a->max, a->sumsq, a->sigma);
+                    for (const InternalPtr& a : b.aggs) {
+                        if (a->name != name) continue;
+                        if (a->type == ESGPU_AGG_CARDINALITY) return (double)(a->hll ? a->hll->cardinality(0) : 0);  // .value()
+                        return metric_of(a->type, key, a->count, a->sum, a->min, a->max, a->sumsq, a->sigma);
+                    }
                     throw std::invalid_argument("Invalid order path [" + first.order_path + "]");
                 };
                 std::vector<double> vals(reduced.size());

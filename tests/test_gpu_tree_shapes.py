@@ -170,3 +170,17 @@ def test_more_than_four_clauses(engine):
             AB.extendedStats("all").field("bytes")]
     red = _both(engine, aggs, shards=2, filters=q, exact=False)
     assert red["f"]["doc_count"] > 0
+
+
+@pytest.mark.parametrize("asc,thr", [(False, 50), (True, 50), (False, 3000)])
+def test_terms_ordered_by_cardinality(engine, asc, thr):
+    """InternalOrder.Aggregation over a cardinality child (CardinalityAggregator.metric = counts.cardinality(bucketOrd)):
+    shard selection by every ordinal's sketch estimate (LINEAR_COUNTING sizes at threshold 3000, HLL++ estimates at
+    50), the reduce by the merged sketches' values; under a top-level filter too."""
+    card = AB.cardinality("ips").field("client_ip.hash").precisionThreshold(thr)
+    aggs = [AB.terms("hosts").field("host").size(6).order(Order.aggregation("ips", asc)).subAggregation(card)
+            .subAggregation(AB.avg("rt").field("response_time_ms")),
+            AB.filter("f", [QB.rangeQuery("bytes").gte(5000)]).subAggregation(
+                AB.terms("h2").field("host").size(4).order(Order.aggregation("ips2.value", not asc))
+                .subAggregation(AB.cardinality("ips2").field("client_ip.hash").precisionThreshold(thr)))]
+    _both(engine, aggs, n=300_000, shards=2)

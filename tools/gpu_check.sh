@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun session: GPU parity tests, kernel sweep, bench, rocprofv3 kernel-trace stats and PMC HBM-traffic passes.
 #   gpurun --timeout 1200 -- bash tools/gpu_check.sh <tag> [steps...]
-# steps: tests kbench bench jitter export shape125 configs buildtrace prof profk pmc pmck variants (default: tests kbench bench prof pmc)
+# steps: tests testsdyn kbench bench jitter export shape125 configs dynab buildtrace prof profk pmc pmck variants (default: tests kbench bench prof pmc)
 # KBENCH_ONLY=name,name restricts the kbench sweeps (KBENCH_ARGS: extra kbench flags for variants, KBENCH_TAG: log suffix); variants = every build/variants/libesgpu_*.so via ESGPU_LIBRARY.  Every GPU step has its own time limit; the first failure ends it.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -43,6 +43,17 @@ for s in $STEPS; do
                   run "bench_ns8_${sc}_$i" 300 python3 "$R/bench.py" --shards 8 --docs 125000000 --cpu-docs 0 --scheme $sc || exit 1
                   run "bench_c5_${sc}_$i" 300 python3 "$R/bench.py" --workload config5 --shards 8 --docs 125000000 --cpu-docs 0 --scheme $sc || exit 1
               done; done ;;
+        dynab) # collect kernel: static block ranges vs dynamic chunk claiming (ESGPU_DYN), 125M- and 1B-doc shards
+              for i in 1 2; do for d in 0 1; do
+                  ESGPU_DYN=$d run "kbench_125m_dyn${d}_$i" 300 python3 "$R/tools/kbench.py" --docs 125000000 --reps 5 \
+                      ${KBENCH_ONLY:+--only $KBENCH_ONLY} || exit 1
+              done; done
+              for d in 0 1; do
+                  ESGPU_DYN=$d run "kbench_1b_dyn$d" 300 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 \
+                      ${KBENCH_ONLY:+--only $KBENCH_ONLY} || exit 1
+              done ;;
+        testsdyn) ESGPU_DYN=1 run pytest_gpu_dyn 1100 python3 -u -m pytest "$R/tests" -m gpu -x -v -p no:cacheprovider \
+                      --timeout 300 --timeout-method thread ;;
         buildtrace) # per-phase host marks of every shard build (ESGPU_TRACE_BUILD) in the 8-shard north star
               ESGPU_TRACE_BUILD=1 run bench_ns8_trace 300 python3 "$R/bench.py" --shards 8 --docs 125000000 --cpu-docs 0 \
                   --steps 4 --warmup 2 ;;
