@@ -306,21 +306,45 @@ constexpr uint32_t kHllBits = ESGPU_HLL_BITS;            // bits per register bo
 constexpr uint32_t kHllPerByte = 8 / kHllBits;
 constexpr uint32_t kHllMaxDelta = (1u << kHllBits) - 1;
 __host__ __device__ constexpr uint32_t hll_snap_bytes(uint32_t m) { return m / kHllPerByte; }
+// the phase kernel's LDS: the nibbles, then one group floor byte per group of kHllGroup registers (16-byte multiple)
+__host__ __device__ constexpr uint32_t hll_lds_bytes(uint32_t m) {
+    return hll_snap_bytes(m) + (((m >= 64u ? m / 64u : 1u) + 15u) & ~15u);
+}
 
 template <int KIND>
 __global__ __launch_bounds__(kHllLdsWG) void hll_registers_lds_kernel(HllParams P, uint32_t d_begin, uint32_t d_end,
                                                                        uint32_t per_wg, const unsigned int* floor_ptr) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char nib[];  // [2^p / 2] packed nibbles
-    const uint32_t F = min(*floor_ptr, 64u - (uint32_t)P.p);
-    const uint64_t zmask = F == 0 ? 0ull : (((1ull << F) - 1ull) << (64 - P.p - F));  // rl > F <=> these bits are 0
-    const uint32_t nbytes = hll_snap_bytes(1u << P.p);
+    // LDS: [2^p / 2] packed nibbles, then the group floors [ngroups] (one byte per group of 64 registers)
+    extern __shared__ __attribute__((aligned(16))) unsigned char nib[];
+    const uint32_t m = 1u << P.p;
+    const uint32_t nbytes = hll_snap_bytes(m);
+    const uint32_t ngroups = m >= kHllGroup ? m / kHllGroup : 1u;
+    const uint32_t gshift = m >= kHllGroup ? 6u : (uint32_t)P.p;
+    unsigned char* gfl = nib + nbytes;
     if ((nbytes & 15u) == 0) {
         for (uint32_t i = threadIdx.x * 16; i < nbytes; i += kHllLdsWG * 16)
             *reinterpret_cast<u32x4_t*>(nib + i) = load16(P.snap + i);
     } else {
         for (uint32_t i = threadIdx.x; i < nbytes; i += kHllLdsWG) nib[i] = P.snap[i];
     }
+    // the floor F (min register) is the min of the group floors, derived here rather than by a separate kernel
+    __shared__ uint32_t wmin[kHllLdsWG / 64];
+    uint32_t f = 0xFFFFFFFFu;
+    for (uint32_t i = threadIdx.x; i < ngroups; i += kHllLdsWG) {
+        const uint32_t g = P.gfloor[i];
+        gfl[i] = (unsigned char)g;
+        f = min(f, g);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) f = min(f, (uint32_t)__shfl_xor((int)f, o, 64));
+    if ((threadIdx.x & 63) == 0) wmin[threadIdx.x >> 6] = f;
     __syncthreads();
+    f = wmin[0];
+#pragma unroll
+    for (uint32_t w = 1; w < kHllLdsWG / 64; ++w) f = min(f, wmin[w]);
+    const uint32_t F = min(f, 64u - (uint32_t)P.p);
+    (void)floor_ptr;
+    const uint64_t zmask = F == 0 ? 0ull : (((1ull << F) - 1ull) << (64 - P.p - F));  // rl > F <=> these bits are 0
     const uint32_t w0 = d_begin + blockIdx.x * per_wg;
     const uint32_t w1 = min(d_end, w0 + per_wg);
     if (w0 >= w1) return;
@@ -341,9 +365,10 @@ __global__ __launch_bounds__(kHllLdsWG) void hll_registers_lds_kernel(HllParams 
                 const uint32_t bi = idx / kHllPerByte;
                 const uint32_t byte = nib[bi];
                 const uint32_t sh = (idx % kHllPerByte) * kHllBits;
-                if (rl > F + ((byte >> sh) & kHllMaxDelta)) {
+                const uint32_t gf = gfl[idx >> gshift];
+                if (rl > gf + ((byte >> sh) & kHllMaxDelta)) {
                     atomicMax(&P.regs[idx], rl);
-                    nib[bi] = (unsigned char)((byte & ~(kHllMaxDelta << sh)) | (min(rl - F, kHllMaxDelta) << sh));
+                    nib[bi] = (unsigned char)((byte & ~(kHllMaxDelta << sh)) | (min(rl - gf, kHllMaxDelta) << sh));
                 }
             }
         }
@@ -376,26 +401,98 @@ __global__ __launch_bounds__(kHllLdsWG) void hll_registers_lds_kernel(HllParams 
 #endif
 }
 
-// packed 4-bit lower bounds of the registers relative to the floor: nibble = min(reg - floor, 15).  The floor F is the
-// min of the group floors (4 KB, read by every block); block 0 also stores it for the phase kernel, so no memset and
-// no atomic are needed between phases.
-__global__ __launch_bounds__(256) void hll_snapshot_kernel(const unsigned int* regs, uint32_t m, const unsigned char* gfloor,
-                                                           uint32_t ngroups, unsigned int* floor_out, unsigned char* snap) {
-    __shared__ uint32_t wmin[4];
-    uint32_t f = 0xFFFFFFFFu;
-    for (uint32_t g = threadIdx.x; g < ngroups; g += 256) f = min(f, (uint32_t)gfloor[g]);
+// one refresh between register phases: per group of 64 registers (one wave) its floor (min register) and each
+// register's 4-bit lower bound over that floor, nibble = min(reg - group floor, 15), packed two per byte.  The phase
+// kernel derives the global floor from the group floors itself, so no second kernel, memset or atomic is needed.
+__global__ __launch_bounds__(1024) void hll_refresh_kernel(const unsigned int* regs, uint32_t m, unsigned char* gfloor,
+                                                           unsigned char* snap) {
+    static_assert(kHllBits == 4, "two nibbles per snapshot byte");
+    const uint32_t gsz = m >= kHllGroup ? kHllGroup : m;
+    const uint32_t g = blockIdx.x * 16 + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    const bool live = g * gsz < m && lane < gsz;
+    const uint32_t r = live ? regs[g * gsz + lane] : 0xFFFFFFFFu;
+    uint32_t v = r;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) f = min(f, (uint32_t)__shfl_xor((int)f, o, 64));
-    if ((threadIdx.x & 63) == 0) wmin[threadIdx.x >> 6] = f;
+    for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    if (g * gsz >= m) return;
+    if (lane == 0) gfloor[g] = (unsigned char)min(v, 255u);
+    const uint32_t d = live ? min(r - v, kHllMaxDelta) : 0u;
+    const uint32_t hi = (uint32_t)__shfl_down((int)d, 1, 64);  // the odd neighbour's nibble
+    if (live && (lane & 1) == 0) snap[(g * gsz + lane) / 2] = (unsigned char)(d | (lane + 1 < gsz ? hi << 4 : 0u));
+}
+
+// Phase 0 by register range (a fresh request's first cut0 * m values, when every hash finds an empty or low
+// register): instead of one scattered global atomicMax per hash (~4 per register, the atomic rate bounds it), the
+// entries are partitioned by register range and each range's owner maxes them in LDS and stores its registers once.
+// hll_p0_scatter: 16 docs per thread, a slot per entry reserved in LDS per range, one global reservation per (workgroup,
+// range); an entry past its range's capacity raises its register with an atomicMax directly (never expected: the
+// capacity is ~8 sigma above the mean).
+constexpr uint32_t kP0WG = 256, kP0Docs = 16;
+template <int KIND>
+__global__ __launch_bounds__(kP0WG) void hll_p0_scatter_kernel(HllParams P, uint32_t d_end) {
+    __shared__ uint32_t lcnt[256], lbase[256];
+    const uint32_t m = 1u << P.p, R = hll_p0_ranges(m);
+    const uint32_t rshift = (uint32_t)P.p - (31u - (uint32_t)__builtin_clz(R));  // log2(m / R)
+    for (uint32_t i = threadIdx.x; i < R; i += kP0WG) lcnt[i] = 0;
     __syncthreads();
-    const uint32_t F = min(min(wmin[0], wmin[1]), min(wmin[2], wmin[3]));
-    if (blockIdx.x == 0 && threadIdx.x == 0) *floor_out = F;
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (kHllPerByte * i >= m) return;
-    uint32_t b = 0;
+    const uint32_t base = blockIdx.x * kP0WG * kP0Docs;
+    const uint32_t last4 = (d_end - 1) & ~3u;
+    uint64_t raw[kP0Docs];
 #pragma unroll
-    for (uint32_t k = 0; k < kHllPerByte; ++k) b |= min(regs[kHllPerByte * i + k] - F, kHllMaxDelta) << (k * kHllBits);
-    snap[i] = (unsigned char)b;
+    for (uint32_t k = 0; k < kP0Docs / 4; ++k)
+        load_i64x4((const int64_t*)P.col, min(base + (k * kP0WG + threadIdx.x) * 4, last4), (int64_t*)&raw[4 * k]);
+    uint32_t ent[kP0Docs], pos[kP0Docs];
+#pragma unroll
+    for (uint32_t k = 0; k < kP0Docs; ++k) {
+        const uint32_t d = base + ((k / 4) * kP0WG + threadIdx.x) * 4 + (k & 3);
+        const uint64_t h = hll_fast_hash<KIND>(P, raw[k]);
+        const uint32_t idx = hll_index(h, P.p);
+        ent[k] = (hll_run_len(h, P.p) << 24) | idx;
+        pos[k] = d < d_end ? atomicAdd(&lcnt[idx >> rshift], 1u) : ~0u;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < R; i += kP0WG) lbase[i] = lcnt[i] ? atomicAdd(&P.p0_cnt[i], lcnt[i]) : 0u;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kP0Docs; ++k) {
+        if (pos[k] == ~0u) continue;
+        const uint32_t idx = ent[k] & 0xFFFFFFu, r = idx >> rshift;
+        const uint32_t slot = lbase[r] + pos[k];
+        if (slot < P.p0_cap) P.p0_buf[(size_t)r * P.p0_cap + slot] = ent[k];
+        else atomicMax(&P.regs[idx], ent[k] >> 24);
+    }
+}
+// hll_p0_gather: one workgroup per range: its registers maxed with its entries in LDS, stored once, and the range's
+// group floors and nibble snapshot written as hll_refresh_kernel would (the first LDS phase needs no refresh launch);
+// the range's fill counter is re-armed for the next request
+__global__ __launch_bounds__(1024) void hll_p0_gather_kernel(HllParams P) {
+    static_assert(kHllBits == 4, "two nibbles per snapshot byte");
+    __shared__ uint32_t reg[1024];
+    const uint32_t m = 1u << P.p, per = m / hll_p0_ranges(m);  // 64 .. 1024 registers (p <= 18)
+    const uint32_t b = blockIdx.x, r0 = b * per;
+    for (uint32_t i = threadIdx.x; i < per; i += 1024) reg[i] = P.regs[r0 + i];
+    __syncthreads();
+    const uint32_t n = min(P.p0_cnt[b], P.p0_cap);
+    const uint32_t* src = P.p0_buf + (size_t)b * P.p0_cap;
+    for (uint32_t i = threadIdx.x; i < n; i += 1024) {
+        const uint32_t e = src[i];
+        atomicMax(&reg[(e & 0xFFFFFFu) - r0], e >> 24);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < per; i += 1024) P.regs[r0 + i] = reg[i];
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t gl = threadIdx.x >> 6; gl < per / kHllGroup; gl += 16) {
+        const uint32_t v0 = reg[gl * kHllGroup + lane];
+        uint32_t v = v0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+        if (lane == 0) P.gfloor[r0 / kHllGroup + gl] = (unsigned char)min(v, 255u);
+        const uint32_t d = min(v0 - v, kHllMaxDelta);
+        const uint32_t hi = (uint32_t)__shfl_down((int)d, 1, 64);
+        if ((lane & 1) == 0) P.snap[(r0 + gl * kHllGroup + lane) / 2] = (unsigned char)(d | (hi << 4));
+    }
+    if (threadIdx.x == 0) atomicExch(&P.p0_cnt[b], 0u);
 }
 
 // group floors: one wave per group of 64 registers; with `out`, the global floor is their min (*out initialised to ~0),
@@ -504,9 +601,6 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
 #ifndef ESGPU_HLL_GROW
 #define ESGPU_HLL_GROW 4
 #endif
-#ifndef ESGPU_HLL_CUT0
-#define ESGPU_HLL_CUT0 4  // measured: 4 beats 16 by 3-4 % (phase 0 reads and raises registers for every hash)
-#endif
     uint64_t c = (uint64_t)m * ESGPU_HLL_CUT0;
     while (c <= p.seen) c *= ESGPU_HLL_GROW;
     while (c < p.seen + n) {
@@ -524,11 +618,9 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
     // floor (and group floors + LDS snapshot) of the registers as they stand
     auto refresh = [&]() {
         const uint32_t ng = m >= kHllGroup ? m / kHllGroup : 1u;
-        if (lds) {  // group floors, then the snapshot kernel derives and stores the floor itself
-            hipLaunchKernelGGL(hll_group_floor_kernel, dim3((ng + 15) / 16), dim3(1024), 0, st, (const unsigned int*)p.regs, m,
-                               p.gfloor, (unsigned int*)nullptr);
-            hipLaunchKernelGGL(hll_snapshot_kernel, dim3((hll_snap_bytes(m) + 255) / 256), dim3(256), 0, st,
-                               (const unsigned int*)p.regs, m, (const unsigned char*)p.gfloor, ng, p.floor, p.snap);
+        if (lds) {  // group floors and the nibble snapshot in one pass
+            hipLaunchKernelGGL(hll_refresh_kernel, dim3((ng + 15) / 16), dim3(1024), 0, st, (const unsigned int*)p.regs, m,
+                               p.gfloor, p.snap);
             return;
         }
         (void)hipMemsetAsync(p.floor, 0xFF, 4, st);
@@ -540,9 +632,21 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
     };
     const bool warm = p.seen >= (uint64_t)m * ESGPU_HLL_CUT0;  // the registers already passed the first cut
     if (warm) refresh();
+#ifndef ESGPU_HLL_P0
+#define ESGPU_HLL_P0 1
+#endif
+    // phase 0 partitioned by register range (the LDS phases' kinds, p >= 12: at least 64 ranges of whole groups)
+    const bool p0 = ESGPU_HLL_P0 && lds && !warm && p.p >= 12 && p.p0_cnt && cuts.size() > 1 && cuts[1] > 0;
     for (size_t ph = 0; ph + 1 < cuts.size(); ++ph) {
         const uint32_t span = cuts[ph + 1] - cuts[ph];
         if (span == 0) continue;
+        if (ph == 0 && p0) {
+            const dim3 g1((span + kP0WG * kP0Docs - 1) / (kP0WG * kP0Docs));
+            if (p.kind == HLL_I64) hipLaunchKernelGGL(hll_p0_scatter_kernel<HLL_I64>, g1, dim3(kP0WG), 0, st, p, span);
+            else hipLaunchKernelGGL(hll_p0_scatter_kernel<HLL_F64>, g1, dim3(kP0WG), 0, st, p, span);
+            hipLaunchKernelGGL(hll_p0_gather_kernel, dim3(hll_p0_ranges(m)), dim3(1024), 0, st, p);
+            continue;  // the gather left the registers' group floors and snapshot behind: no refresh
+        }
         const bool floored = warm || ph > 0;
         // contiguous range per workgroup, a multiple of 4 docs, at least 4 iterations of 1024 docs (the first phase is
         // small and latency-bound: every hash reads a register there, so it needs the whole chip)
@@ -552,14 +656,14 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
         const unsigned int* fl = floored ? (const unsigned int*)p.floor : (const unsigned int*)nullptr;
         if (lds && floored) {
             // one 1024-thread workgroup per CU (128 KB of nibbles at p = 18), more for smaller p
-            const uint32_t per_cu = std::max(1u, std::min(4u, (uint32_t)(160u * 1024u / (hll_snap_bytes(m) + 1024u))));
+            const uint32_t per_cu = std::max(1u, std::min(4u, (uint32_t)(160u * 1024u / (hll_lds_bytes(m) + 1024u))));
             uint32_t lw = std::max(1u, std::min(cus * per_cu, span / (kHllLdsIter * 4)));
             const uint32_t lper = ((span + lw - 1) / lw + 3) & ~3u;
             lw = (span + lper - 1) / lper;
             if (p.kind == HLL_I64)
-                hipLaunchKernelGGL(hll_registers_lds_kernel<HLL_I64>, dim3(lw), dim3(kHllLdsWG), hll_snap_bytes(m), st, p, cuts[ph], cuts[ph + 1], lper, fl);
+                hipLaunchKernelGGL(hll_registers_lds_kernel<HLL_I64>, dim3(lw), dim3(kHllLdsWG), hll_lds_bytes(m), st, p, cuts[ph], cuts[ph + 1], lper, fl);
             else
-                hipLaunchKernelGGL(hll_registers_lds_kernel<HLL_F64>, dim3(lw), dim3(kHllLdsWG), hll_snap_bytes(m), st, p, cuts[ph], cuts[ph + 1], lper, fl);
+                hipLaunchKernelGGL(hll_registers_lds_kernel<HLL_F64>, dim3(lw), dim3(kHllLdsWG), hll_lds_bytes(m), st, p, cuts[ph], cuts[ph + 1], lper, fl);
         } else if (fast && p.kind == HLL_I64)
             hipLaunchKernelGGL(hll_registers_fast_kernel<HLL_I64>, dim3(wgs), dim3(kHllWG), 0, st, p, cuts[ph], cuts[ph + 1], per, fl);
         else if (fast && p.kind == HLL_F64)

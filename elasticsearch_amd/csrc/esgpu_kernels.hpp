@@ -141,7 +141,20 @@ struct HllParams {
     unsigned long long* lc_first;
     uint64_t pos_base;
     int32_t pos_ord;
+    // phase 0 by register range (hll_p0_*): per-range fill counters [p0_ranges] (zero between requests) and the
+    // entries (run length << 24 | register index) of each range, p0_cap per range; null: no partitioned phase 0
+    unsigned int* p0_cnt;
+    unsigned int* p0_buf;
+    uint32_t p0_cap;
 };
+#ifndef ESGPU_HLL_CUT0  // HLL phase 0 spans the request's first ESGPU_HLL_CUT0 * 2^p values
+#define ESGPU_HLL_CUT0 4  // measured: 4 beats 16 by 3-4 % (phase 0 reads and raises registers for every hash)
+#endif
+// partitioned phase 0: ranges of registers (each whole groups of 64) and the entries a range holds
+__host__ __device__ constexpr uint32_t hll_p0_ranges(uint32_t m) { return m >= 256u * 64u ? 256u : m / 64u; }
+__host__ __device__ constexpr uint32_t hll_p0_cap(uint32_t m, uint32_t cut0) {  // mean + mean / 8 + 256 (> 8 sigma)
+    return (cut0 * (m / hll_p0_ranges(m)) * 9u / 8u + 256u + 3u) & ~3u;
+}
 
 struct GatherParams {
     const uint32_t* rows;

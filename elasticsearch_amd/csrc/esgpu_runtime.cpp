@@ -2463,6 +2463,7 @@ static void ensure_ord_hash(esgpu_ctx* c, const DevColumn* col, hipStream_t st) 
 }
 
 static size_t hll_snap_offset(uint32_t m) { return (16 + std::max<size_t>(m / 64, 1) + 15) & ~(size_t)15; }
+static size_t hll_p0_offset(uint32_t m) { return (hll_snap_offset(m) + std::max<size_t>(m / 2, 16) + 15) & ~(size_t)15; }
 
 static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
     const DevColumn* col = s->col(pl.metric_field.c_str());
@@ -2479,9 +2480,14 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
         HIPX(hipMemsetAsync(pl.lc_set.p, 0, (size_t)cap * 4, p->stream));
         pl.lc_first.alloc(p->ctx, (size_t)cap * 8);
         HIPX(hipMemsetAsync(pl.lc_first.p, 0xFF, (size_t)cap * 8, p->stream));
-        // counters, then the group floors, then the packed register snapshot (16-byte aligned)
-        pl.lc_count.alloc(p->ctx, hll_snap_offset(m) + std::max<size_t>(m / 2, 16));
+        // counters, then the group floors, then the packed register snapshot (16-byte aligned), then (p >= 12) the
+        // partitioned phase 0's range counters (zero between requests) and entries
+        const size_t p0_off = hll_p0_offset(m);
+        const size_t p0_bytes = pl.p >= 12 ? 16 * (((size_t)hll_p0_ranges(m) * 4 + 15) / 16) +
+                                                 (size_t)hll_p0_ranges(m) * hll_p0_cap(m, ESGPU_HLL_CUT0) * 4 : 0;
+        pl.lc_count.alloc(p->ctx, p0_off + p0_bytes);
         HIPX(hipMemsetAsync(pl.lc_count.p, 0, 16, p->stream));
+        if (p0_bytes) HIPX(hipMemsetAsync(pl.lc_count.as<unsigned char>() + p0_off, 0, (size_t)hll_p0_ranges(m) * 4, p->stream));
         pl.allocated = true;
     }
     HllParams H{};
@@ -2538,6 +2544,12 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
     H.floor = pl.lc_count.as<unsigned int>() + 2;
     H.gfloor = pl.lc_count.as<unsigned char>() + 16;
     H.snap = pl.lc_count.as<unsigned char>() + hll_snap_offset(1u << pl.p);
+    if (pl.p >= 12) {
+        const uint32_t m = 1u << pl.p;
+        H.p0_cnt = (unsigned int*)(pl.lc_count.as<unsigned char>() + hll_p0_offset(m));
+        H.p0_buf = H.p0_cnt + 4 * (((size_t)hll_p0_ranges(m) * 4 + 15) / 16);
+        H.p0_cap = hll_p0_cap(m, ESGPU_HLL_CUT0);
+    }
     H.lc_mask = pl.lc_mask;
     H.lc_threshold = pl.lc_threshold;
     H.lc_first = pl.lc_first.as<unsigned long long>();
