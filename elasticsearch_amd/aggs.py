@@ -302,7 +302,8 @@ class CardinalityBuilder(_MetricBuilder):
 
 class FilterBuilder(_Builder):
     """filter aggregation (FilterAggregator / InternalFilter): one bucket of the docs matching `query` -- a TermQuery,
-    a RangeQuery or a list of them (bool.filter conjunction) -- with sub-aggregations.  Top level on the GPU path."""
+    a RangeQuery or a list of them (bool.filter conjunction) -- with sub-aggregations.  On the GPU path at the top level
+    (any sub-aggregations) or directly under a top-level bucket aggregation (metric sub-aggregations)."""
     type = N.AGG_FILTER
 
     def __init__(self, name, query=None):

@@ -893,6 +893,8 @@ struct LeafRef { int pipe = -1, leaf = -1; };  // a metric / cardinality spec: i
 struct ChildSrc {
     int spec = -1;
     bool bucket = false;
+    bool filter = false;             // a filter aggregation (FilterAggregator): pipes = its doc counts per outer bucket
+                                     // (pipes[0]) and its metric children (grand), all under its clauses
     LeafRef leaf;                    // metric / cardinality child
     std::vector<int> pipes;          // bucket child: pipelines carrying it (pipes[0]'s counts define its buckets)
     std::vector<LeafRef> grand;      // bucket child: its children in request order
@@ -1065,18 +1067,38 @@ static Group compile_group(esgpu_plan* p, int r, int fspec) {
     for (int ch : root.children) {
         const int t = p->specs[ch].s.type;
         if (is_metric(t) || t == ESGPU_AGG_CARDINALITY) leaves.push_back(ch);
+        else if (t == ESGPU_AGG_FILTER) require(fspec < 0, ESGPU_ERR_UNSUPPORTED, "nested filter aggregations");
         else if (!is_bucket(t)) throw EsError(ESGPU_ERR_UNSUPPORTED, "aggregation type not on the GPU path");
     }
     std::vector<LeafRef> leaf_refs;
-    bool have_bucket_child = false;
-    for (int ch : root.children) have_bucket_child |= is_bucket(p->specs[ch].s.type);
-    if (!leaves.empty() || !have_bucket_child)  // the outer level's own pipelines (also: a bucket with no children)
+    bool have_bucket_child = false, have_filter_child = false;
+    for (int ch : root.children) {
+        have_bucket_child |= is_bucket(p->specs[ch].s.type);
+        have_filter_child |= p->specs[ch].s.type == ESGPU_AGG_FILTER;
+    }
+    // the outer level's own pipelines (also: a bucket with no children, and one with a filter child, whose pipelines
+    // count only the filter's docs -- pipes[0] must count every doc of the outer buckets)
+    if (!leaves.empty() || !have_bucket_child || have_filter_child)
         for (int pi : add_leaf_pipelines(p, r, fspec, r, -1, leaves, &leaf_refs)) g.pipes.push_back(pi);
     size_t li = 0;
     for (int ch : root.children) {
         ChildSrc cs;
         cs.spec = ch;
-        if (!is_bucket(p->specs[ch].s.type)) {
+        if (p->specs[ch].s.type == ESGPU_AGG_FILTER) {
+            // FilterAggregator under a bucket aggregation (A/bucket/filter/FilterAggregator.java:57-70): per outer bucket,
+            // the docs matching its clauses counted, and its metric children collected over them -- outer-level pipelines
+            // carrying the filter's clauses (a filter with no children still gets one for its doc counts)
+            cs.filter = true;
+            std::vector<int> fl;
+            for (int gc : p->specs[ch].children) {
+                const int t = p->specs[gc].s.type;
+                require(is_metric(t) || t == ESGPU_AGG_CARDINALITY, ESGPU_ERR_UNSUPPORTED,
+                        "bucket aggregations under a filter aggregation under a bucket aggregation run on the CPU path");
+                fl.push_back(gc);
+            }
+            cs.pipes = add_leaf_pipelines(p, r, ch, r, -1, fl, &cs.grand);
+            for (int pi : cs.pipes) g.pipes.push_back(pi);
+        } else if (!is_bucket(p->specs[ch].s.type)) {
             cs.leaf = leaf_refs[li++];
         } else {
             cs.bucket = true;
@@ -1131,8 +1153,11 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
             n.s.time_zone = nullptr;
             n.s.format = nullptr;
             require(n.s.type >= ESGPU_AGG_TERMS && n.s.type <= ESGPU_AGG_FILTER, ESGPU_ERR_INVALID, "unknown aggregation type");
-            if (n.s.type == ESGPU_AGG_FILTER)
-                require(n.s.parent < 0, ESGPU_ERR_UNSUPPORTED, "filter aggregation under another aggregation runs on the CPU path");
+            if (n.s.type == ESGPU_AGG_FILTER && n.s.parent >= 0) {  // one bucket level above it (compile_group)
+                const SpecNode& par = p->specs[n.s.parent];
+                require(is_bucket(par.s.type) && par.s.parent < 0, ESGPU_ERR_UNSUPPORTED,
+                        "a filter aggregation below the first bucket level runs on the CPU path");
+            }
             if (n.s.parent < 0) tops.push_back(i);
             else {
                 require(n.s.parent < i, ESGPU_ERR_INVALID, "parent must precede child");
@@ -1180,7 +1205,7 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
         }
         // every pipeline evaluates the query clauses plus those of its filter aggregation (set_preds folds more than
         // kMaxPreds of them into a doc bitset)
-        for (int r : tops) {
+        for (int r = 0; r < nspecs; ++r) {
             if (p->specs[r].s.type != ESGPU_AGG_FILTER) continue;
             int own = 0;
             for (int o : p->filter_owner) own += o == r;
@@ -3045,10 +3070,32 @@ static std::vector<TermPick> select_terms(const esgpu_agg_spec& s, const unsigne
     return cands;
 }
 
+// one InternalFilter instance of filter child `kid` at host cell c of its outer-level pipelines
+// (FilterAggregator.buildAggregation: bucketDocCount(owningBucketOrdinal), bucketAggregations(owningBucketOrdinal))
+static void append_filter(const esgpu_plan* p, const ChildSrc& kid, size_t c, Block& sub) {
+    const Pipeline& F0 = p->pipes[kid.pipes[0]];
+    ++sub.n;
+    sub.count.push_back(F0.allocated ? (int64_t)F0.hc.cnt[c] : 0);
+    for (size_t gj = 0; gj < kid.grand.size(); ++gj) {
+        const Pipeline& L = p->pipes[kid.grand[gj].pipe];
+        if (!L.allocated) sub.subs[gj].append_empty();
+        else append_leaf(p, L, kid.grand[gj].leaf, c, sub.subs[gj]);
+    }
+}
+
 // prototypes (n == 1 empty instances) of a bucket aggregation's children, in request order
 static std::vector<Block> child_protos(const esgpu_plan* p, const Group& g) {
     std::vector<Block> out;
     for (const ChildSrc& k : g.kids) {
+        if (k.filter) {  // InternalFilter: doc_count + its metric children
+            Block f;
+            f.type = ESGPU_AGG_FILTER;
+            f.name = p->specs[k.spec].name;
+            for (int gc : p->specs[k.spec].children) f.subs.push_back(leaf_proto(p, gc));
+            f.append_empty();
+            out.push_back(std::move(f));
+            continue;
+        }
         if (!k.bucket) { out.push_back(leaf_proto(p, k.spec)); continue; }
         std::vector<Block> grand;
         for (int gc : p->specs[k.spec].children) grand.push_back(leaf_proto(p, gc));
@@ -3176,6 +3223,7 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
     p->h_compact.resize(g.kids.size());
     for (size_t ki = 0; ki < g.kids.size(); ++ki) {
         const ChildSrc& kid = g.kids[ki];
+        if (kid.filter) { for (int pi : kid.pipes) need_rows[pi] = 1; continue; }
         if (!kid.bucket) { need_rows[kid.leaf.pipe] = 1; continue; }
         const Pipeline& B0 = p->pipes[kid.pipes[0]];
         bool ok = ESGPU_COMPACT_ROWS && B0.allocated && !B0.inner_terms && !B0.ord_hist && B0.cards.empty() &&
@@ -3307,6 +3355,7 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
     // one allocation per array: the bucket children's total bucket count over the winners, reserved up front
     for (size_t ki = 0; ki < g.kids.size(); ++ki) {
         const ChildSrc& kid = g.kids[ki];
+        if (kid.filter) continue;
         const Pipeline& B0 = kid.bucket ? p->pipes[kid.pipes[0]] : p->pipes[kid.leaf.pipe];
         if (!B0.allocated || fast[ki]) continue;
         size_t nb = k;
@@ -3333,6 +3382,10 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
             const ChildSrc& kid = g.kids[ki];
             Block& sub = r.subs[ki];
             if (fast[ki]) continue;
+            if (kid.filter) {
+                append_filter(p, kid, i, sub);
+                continue;
+            }
             if (!kid.bucket) {
                 const Pipeline& L = p->pipes[kid.leaf.pipe];
                 if (!L.allocated) sub.append_empty(); else append_leaf(p, L, kid.leaf.leaf, i, sub);
@@ -3395,6 +3448,7 @@ static Block build_hist_root(esgpu_plan* p, const Group& g) {
     if (!p0_terms) need[g.pipes[0]] = 1;
     for (size_t ki = 0; ki < g.kids.size(); ++ki) {
         const ChildSrc& kid = g.kids[ki];
+        if (kid.filter) { for (int pi : kid.pipes) need[pi] = 1; continue; }
         if (!kid.bucket) { need[kid.leaf.pipe] = 1; continue; }
         for (const LeafRef& gr : kid.grand) need[gr.pipe] = 1;
         Pipeline& B0 = p->pipes[kid.pipes[0]];
@@ -3447,6 +3501,14 @@ static Block build_hist_root(esgpu_plan* p, const Group& g) {
     for (size_t ki = 0; ki < g.kids.size(); ++ki) {
         const ChildSrc& kid = g.kids[ki];
         Block& sub = r.subs[ki];
+        if (kid.filter) {
+            for (int pi : kid.pipes) {
+                const Pipeline& L = p->pipes[pi];
+                require(!L.allocated || (L.H == P0.H && L.key0 == P0.key0), ESGPU_ERR_DEVICE, "sibling pipelines disagree on the key grid");
+            }
+            for (uint32_t s : slots) append_filter(p, kid, s, sub);  // one cell per key (T == 1): cell == slot
+            continue;
+        }
         if (!kid.bucket) {
             const Pipeline& L = p->pipes[kid.leaf.pipe];
             require(L.H == P0.H && L.key0 == P0.key0, ESGPU_ERR_DEVICE, "sibling pipelines disagree on the key grid");

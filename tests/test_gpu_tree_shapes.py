@@ -184,3 +184,33 @@ def test_terms_ordered_by_cardinality(engine, asc, thr):
                 AB.terms("h2").field("host").size(4).order(Order.aggregation("ips2.value", not asc))
                 .subAggregation(AB.cardinality("ips2").field("client_ip.hash").precisionThreshold(thr)))]
     _both(engine, aggs, n=300_000, shards=2)
+
+
+def test_filter_under_terms(engine):
+    """FilterAggregator below the top level (A/bucket/filter/FilterAggregator.java:57-70): per term bucket the docs
+    matching its clauses and its metric children over them; beside an unfiltered metric and a histogram child, and a
+    filter with no children (doc_count only), under query clauses."""
+    aggs = [AB.terms("hosts").field("host").size(7)
+            .subAggregation(AB.filter("ok", QB.termQuery("status", 200))
+                            .subAggregation(AB.avg("rt").field("response_time_ms"))
+                            .subAggregation(AB.stats("b").field("bytes"))
+                            .subAggregation(AB.cardinality("ips").field("client_ip.hash").precisionThreshold(100)))
+            .subAggregation(AB.filter("big", [QB.rangeQuery("bytes").gte(500_000), QB.rangeQuery("price").lt(300.0)]))
+            .subAggregation(AB.extendedStats("all_rt").field("response_time_ms"))
+            .subAggregation(AB.dateHistogram("d").field("@timestamp").interval("1d"))]
+    _both(engine, aggs, n=400_000, shards=2, filters=[QB.rangeQuery("response_time_ms").gte(3)])
+
+
+@pytest.mark.parametrize("first", [True, False])
+def test_filter_under_histogram(engine, first):
+    """Filter children of a (date_)histogram, with min_doc_count 0 (empty buckets carry the filter's prototype); the
+    filter as the first child (the outer counts then come from the histogram's own pipeline)."""
+    f = AB.filter("slow", QB.rangeQuery("response_time_ms").gte(900)).subAggregation(AB.avg("b").field("bytes"))
+    h = AB.histogram("rt").field("response_time_ms").interval(100).minDocCount(0).extendedBounds(-200, 1200)
+    if first:
+        h.subAggregation(f).subAggregation(AB.stats("p").field("price"))
+    else:
+        h.subAggregation(AB.stats("p").field("price")).subAggregation(f)
+    aggs = [h, AB.dateHistogram("day").field("@timestamp").interval("1d").subAggregation(
+        AB.filter("s200", QB.termQuery("status", 200)))]
+    _both(engine, aggs, n=300_000, shards=2, exact=False)
