@@ -71,8 +71,10 @@ def make_segment(rng, n):
 
 
 class Gen:
-    def __init__(self, rng, T_kw):
+    def __init__(self, rng, T_kw, rng2=None):
         self.r = rng
+        # shapes added later draw from their own stream, so the earlier shapes of every seed stay what they were
+        self.r2 = rng2 if rng2 is not None else np.random.default_rng(0)
         self.T_kw = T_kw
         self.k = 0
         self.inexact = False
@@ -157,6 +159,16 @@ class Gen:
             b.subAggregation(m)
             if key is not None:
                 order_targets.append(m.name + key)
+            elif self.r2.random() < 0.5:  # a cardinality child as the terms order (its single value)
+                order_targets.append(m.name)
+        if depth == 0 and self.r2.random() < 0.25:  # a filter aggregation under the bucket, with metric children
+            r_main, self.r = self.r, self.r2
+            f = AB.filter(self.name("g"), QB.termQuery("status", int(self.r2.choice([200, 404]))) if self.r2.random() < 0.6
+                          else QB.rangeQuery("num").gte(int(self.r2.integers(0, 600))))
+            for _ in range(int(self.r2.integers(0, 3))):
+                f.subAggregation(self.metric()[0])
+            self.r = r_main
+            b.subAggregation(f)
         if depth == 0 and r.random() < 0.5:
             inner = self.terms(True) if kind == "terms" and r.random() < 0.5 else (
                 self.date_histogram() if kind == "terms" else self.terms(True))
@@ -206,7 +218,7 @@ def test_random_request(engine, seed):
     rng = np.random.default_rng(1000 + seed)
     n = int(rng.integers(30_000, 300_000))
     cols, T_kw = make_segment(rng, n)
-    gen = Gen(rng, T_kw)
+    gen = Gen(rng, T_kw, np.random.default_rng(50_000 + seed))
     aggs, filters = gen.request()
     lookups = {f: {t: i for i, t in enumerate(cols[f]["terms"])} for f in ("kw", "kw2", "tags")}
     ord_lookup = lambda f, t: lookups.get(f, {}).get(t, -1)  # noqa: E731
