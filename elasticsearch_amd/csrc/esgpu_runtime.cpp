@@ -1973,9 +1973,57 @@ static bool collect_multi(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, C
 
 static void ensure_ord_hash(esgpu_ctx* c, const DevColumn* col, hipStream_t st);
 
+// re-shape an allocated grid to newT ordinal columns, the old columns landing at column `shift` (histogram under
+// histogram: a later segment widens the inner key range).  Rows are [T] cells, so every array moves as a strided 2D
+// copy; the new cells start from the arrays' initial values (alloc_grid).
+static void regrid_cols(esgpu_plan* p, Pipeline& pl, uint32_t newT, int64_t shift) {
+    const uint32_t oldT = pl.T;
+    std::vector<CardState> old_cards(pl.cards.size());
+    for (size_t i = 0; i < pl.cards.size(); ++i) {
+        old_cards[i].regs = std::move(pl.cards[i].regs);
+        old_cards[i].sets = std::move(pl.cards[i].sets);
+        old_cards[i].first = std::move(pl.cards[i].first);
+        old_cards[i].cnt = std::move(pl.cards[i].cnt);
+        old_cards[i].nonzero = std::move(pl.cards[i].nonzero);
+    }
+    struct { DevBuf g_cnt, g_ocnt, g_vcnt, g_sum, g_min, g_max, g_sq; } old;
+    old.g_cnt = std::move(pl.g_cnt);
+    old.g_ocnt = std::move(pl.g_ocnt);
+    old.g_vcnt = std::move(pl.g_vcnt);
+    old.g_sum = std::move(pl.g_sum);
+    old.g_min = std::move(pl.g_min);
+    old.g_max = std::move(pl.g_max);
+    old.g_sq = std::move(pl.g_sq);
+    pl.T = newT;
+    alloc_grid(p, pl);
+    auto cp = [&](DevBuf& dst, DevBuf& src, size_t esz) {  // [H][oldT] cells of esz bytes -> [H][newT] at column shift
+        if (!src.p) return;
+        HIPX(hipMemcpy2DAsync(dst.as<uint8_t>() + (size_t)shift * esz, (size_t)newT * esz, src.p, (size_t)oldT * esz,
+                              (size_t)oldT * esz, pl.H, hipMemcpyDeviceToDevice, p->stream));
+    };
+    cp(pl.g_cnt, old.g_cnt, 8);
+    cp(pl.g_vcnt, old.g_vcnt, 8);
+    cp(pl.g_sum, old.g_sum, 8);
+    cp(pl.g_min, old.g_min, 8);
+    cp(pl.g_max, old.g_max, 8);
+    cp(pl.g_sq, old.g_sq, 8);
+    if (pl.ocnt_mode == OCNT_HIST && old.g_ocnt.p)
+        HIPX(hipMemcpyAsync(pl.g_ocnt.p, old.g_ocnt.p, (size_t)pl.H * 8, hipMemcpyDeviceToDevice, p->stream));
+    require(pl.ocnt_mode == OCNT_HIST || pl.ocnt_mode == OCNT_NONE, ESGPU_ERR_DEVICE, "ordinal regrid of per-term counts");
+    for (size_t i = 0; i < pl.cards.size(); ++i) {
+        CardState& cs = pl.cards[i];
+        cp(cs.regs, old_cards[i].regs, cs.m);
+        cp(cs.sets, old_cards[i].sets, (size_t)cs.cap * 4);
+        cp(cs.first, old_cards[i].first, (size_t)cs.cap * 8);
+        cp(cs.cnt, old_cards[i].cnt, 4);
+        cp(cs.nonzero, old_cards[i].nonzero, 4);
+    }
+    HIPX(hipStreamSynchronize(p->stream));
+}
+
 // histogram under histogram: this segment's inner key indices as a u32 ordinal column (pl.ord_col), or null when the
 // segment lacks the inner field.  The key range is taken from the request's first segment that has values; a later
-// segment whose values fall outside it is refused (the ordinal dimension of a dense grid cannot grow).
+// segment whose values fall outside it widens the range (up to 65536 keys): the grid's ordinal columns move over.
 // materialize = false: only the key range is checked / taken; pl.ord_col describes the dimension (T) and its values
 // are written later by materialize_hist_ords when the launch cannot derive the keys in its loader.
 static void materialize_hist_ords(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s);
@@ -1993,13 +2041,19 @@ static const DevColumn* derive_hist_ords(esgpu_plan* p, Pipeline& pl, const esgp
             require(kmax - kmin + 1 <= 65536, ESGPU_ERR_UNSUPPORTED, "an inner histogram over 65536 keys runs on the CPU path");
             pl.ord_key0 = kmin;
             pl.ord_keys = (uint32_t)(kmax - kmin + 1);
+            // earlier segments of the request had no inner values: their grid has one empty ordinal column
+            if (!pl.fresh && pl.allocated && pl.T != pl.ord_keys) regrid_cols(p, pl, pl.ord_keys, 0);
         } else if (pl.fresh) {
             pl.ord_key0 = 0;
             pl.ord_keys = 0;
         }
-    } else if (has) {
-        require(kmin >= pl.ord_key0 && kmax < pl.ord_key0 + (int64_t)pl.ord_keys, ESGPU_ERR_UNSUPPORTED,
-                "a later segment extends the inner histogram's key range: runs on the CPU path");
+    } else if (has && (kmin < pl.ord_key0 || kmax >= pl.ord_key0 + (int64_t)pl.ord_keys)) {
+        const int64_t nk0 = std::min(kmin, pl.ord_key0), nk1 = std::max(kmax, pl.ord_key0 + (int64_t)pl.ord_keys - 1);
+        require(nk1 - nk0 + 1 <= 65536, ESGPU_ERR_UNSUPPORTED, "an inner histogram over 65536 keys runs on the CPU path");
+        const int64_t shift = pl.ord_key0 - nk0;
+        pl.ord_key0 = nk0;
+        pl.ord_keys = (uint32_t)(nk1 - nk0 + 1);
+        if (pl.allocated) regrid_cols(p, pl, pl.ord_keys, shift);
     }
     if (!pl.ord_col) pl.ord_col = std::make_shared<DevColumn>();
     DevColumn& d = *pl.ord_col;

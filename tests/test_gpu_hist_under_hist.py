@@ -126,3 +126,38 @@ def test_fused_inner_key_double_sparse_and_negative(engine):
         seg.close()
     assert_same(reduce(results).to_dict(), want["reduced"], "reduced", False)
     plan.close()
+
+
+@pytest.mark.parametrize("first", ["narrow", "missing"])
+def test_later_segment_widens_inner_keys(engine, first):
+    """a later segment's inner values fall outside the key range the first segment fixed (or the first segment has no
+    inner values at all): the grid's ordinal columns move over to the wider range (strided copies of every cell array,
+    cardinality sketches included) and the request stays on the GPU"""
+    n = 200_000
+    c0 = synthetic_columns(FIELDS, n, shard=0)
+    c1 = synthetic_columns(FIELDS, n, shard=1)
+    rt0 = c0["response_time_ms"]["values"]
+    if first == "narrow":
+        c0["response_time_ms"]["values"] = np.clip(rt0, 300, 599)
+    else:
+        c0["response_time_ms"]["values"] = np.zeros_like(rt0)
+        c0["response_time_ms"]["present"] = np.zeros(n // 64, np.uint64)
+    aggs = [AB.dateHistogram("d").field("@timestamp").interval("6h").subAggregation(
+        AB.histogram("rt").field("response_time_ms").interval(100)
+        .subAggregation(AB.stats("b").field("bytes"))
+        .subAggregation(AB.cardinality("ips").field("client_ip.hash").precisionThreshold(50)))]
+    both = {}
+    for k in c0:
+        both[k] = {"type": c0[k]["type"], "values": np.concatenate([c0[k]["values"], c1[k]["values"]])}
+        if "present" in c0[k] or "present" in c1[k]:
+            full = np.full(n // 64, ~np.uint64(0), np.uint64)
+            both[k]["present"] = np.concatenate([c0[k].get("present", full), c1[k].get("present", full)])
+    want = O.run([(both, 2 * n)], aggs)
+    plan = engine.plan(aggs)
+    segs = [engine.upload_segment(c0, n), engine.upload_segment(c1, n)]
+    for s in segs:
+        plan.collect(s)
+    assert_same(plan.build().to_dict(), want["shards"][0], "shard")
+    plan.close()
+    for s in segs:
+        s.close()

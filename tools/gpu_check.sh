@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun session: GPU parity tests, kernel sweep, bench, rocprofv3 kernel-trace stats and PMC HBM-traffic passes.
 #   gpurun --timeout 1200 -- bash tools/gpu_check.sh <tag> [steps...]
-# steps: tests testsdyn kbench bench jitter export shape125 configs dynab buildtrace prof profk pmc pmck variants (default: tests kbench bench prof pmc)
+# steps: tests testsdyn testfile kbench bench jitter export shape125 configs dynab buildtrace profk125 prof profk pmc pmck variants (default: tests kbench bench prof pmc)
 # KBENCH_ONLY=name,name restricts the kbench sweeps (KBENCH_ARGS: extra kbench flags for variants, KBENCH_TAG: log suffix); variants = every build/variants/libesgpu_*.so via ESGPU_LIBRARY.  Every GPU step has its own time limit; the first failure ends it.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -61,6 +61,10 @@ for s in $STEPS; do
                   python3 "$R/bench.py" --steps 10 --warmup 3 --cpu-docs 0 --inflight 1 ;;
         profk) cd /tmp && run rocprof_kbench 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profk" -o kbench -- \
                    python3 "$R/tools/kbench.py" --docs 1000000000 --reps 3 ;;
+        profk125) cd /tmp && run rocprof_kbench125 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profk125" -o kb125 -- \
+                   python3 "$R/tools/kbench.py" --docs 125000000 --reps 3 ${KBENCH_ONLY:+--only $KBENCH_ONLY} ;;
+        testfile) run "pytest_${TESTFILE:-x}" 600 python3 -u -m pytest "$R/tests/${TESTFILE:-test_gpu_parity}.py" -m gpu -x -v \
+                      -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         pmc) cd /tmp && run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o bench -- \
                  python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-docs 0 --inflight 1 &&
              run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o bench -- \
