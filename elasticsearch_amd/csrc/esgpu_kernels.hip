@@ -306,9 +306,13 @@ constexpr uint32_t kHllBits = ESGPU_HLL_BITS;            // bits per register bo
 constexpr uint32_t kHllPerByte = 8 / kHllBits;
 constexpr uint32_t kHllMaxDelta = (1u << kHllBits) - 1;
 __host__ __device__ constexpr uint32_t hll_snap_bytes(uint32_t m) { return m / kHllPerByte; }
-// the phase kernel's LDS: the nibbles, then one group floor byte per group of kHllGroup registers (16-byte multiple)
-__host__ __device__ constexpr uint32_t hll_lds_bytes(uint32_t m) {
-    return hll_snap_bytes(m) + (((m >= 64u ? m / 64u : 1u) + 15u) & ~15u);
+// raises a phase workgroup logs in LDS (more: straight to the registers with an atomicMax); expected about
+// (growth - 1) * m / workgroups = 3,072 per workgroup and phase at p = 18
+constexpr uint32_t kHllLog = 4096;
+// the phase kernel's LDS: the nibbles, then one group floor byte per group of kHllGroup registers (16-byte multiple),
+// then (logging) the raise log, per-range counters and cursors, bases, and the log length
+__host__ __device__ constexpr uint32_t hll_lds_bytes(uint32_t m, bool logm = false) {
+    return hll_snap_bytes(m) + (((m >= 64u ? m / 64u : 1u) + 15u) & ~15u) + (logm ? kHllLog * 4u + 3u * 256u * 4u + 16u : 0u);
 }
 
 template <int KIND>
@@ -321,6 +325,13 @@ __global__ __launch_bounds__(kHllLdsWG) void hll_registers_lds_kernel(HllParams 
     const uint32_t ngroups = m >= kHllGroup ? m / kHllGroup : 1u;
     const uint32_t gshift = m >= kHllGroup ? 6u : (uint32_t)P.p;
     unsigned char* gfl = nib + nbytes;
+    const bool logm = P.log_raises != 0;
+    uint32_t* rlog = (uint32_t*)(gfl + ((ngroups + 15u) & ~15u));  // [kHllLog] (rl << 24 | idx)
+    uint32_t* lcnt = rlog + kHllLog;                                 // [256] entries per register range
+    uint32_t* lcur = lcnt + 256;                                     // [256] their write cursors
+    uint32_t* lbase = lcur + 256;                                    // [256] reserved base in the range's slots
+    uint32_t* nlog = lbase + 256;                                    // [1]
+    if (logm && threadIdx.x == 0) *nlog = 0;
     if ((nbytes & 15u) == 0) {
         for (uint32_t i = threadIdx.x * 16; i < nbytes; i += kHllLdsWG * 16)
             *reinterpret_cast<u32x4_t*>(nib + i) = load16(P.snap + i);
@@ -347,7 +358,7 @@ __global__ __launch_bounds__(kHllLdsWG) void hll_registers_lds_kernel(HllParams 
     const uint64_t zmask = F == 0 ? 0ull : (((1ull << F) - 1ull) << (64 - P.p - F));  // rl > F <=> these bits are 0
     const uint32_t w0 = d_begin + blockIdx.x * per_wg;
     const uint32_t w1 = min(d_end, w0 + per_wg);
-    if (w0 >= w1) return;
+    if (w0 >= w1) return;  // workgroup-uniform: no docs, nothing logged
     const uint32_t t4 = threadIdx.x * 4;
     // unconditional loads (past the range: the range's last 4 docs again, never hashed), so the compiler can count
     // them: a conditional load makes every later wait a vmcnt(0), which drains the other buffer's prefetch too
@@ -367,7 +378,11 @@ __global__ __launch_bounds__(kHllLdsWG) void hll_registers_lds_kernel(HllParams 
                 const uint32_t sh = (idx % kHllPerByte) * kHllBits;
                 const uint32_t gf = gfl[idx >> gshift];
                 if (rl > gf + ((byte >> sh) & kHllMaxDelta)) {
-                    atomicMax(&P.regs[idx], rl);
+                    // logged (a lost nibble write only repeats a log entry: the log holds the values, the nibbles
+                    // only filter), or past the log's end an atomicMax straight on the register
+                    const uint32_t k = logm ? atomicAdd(nlog, 1u) : kHllLog;
+                    if (k < kHllLog) rlog[k] = (rl << 24) | idx;
+                    else atomicMax(&P.regs[idx], rl);
                     nib[bi] = (unsigned char)((byte & ~(kHllMaxDelta << sh)) | (min(rl - gf, kHllMaxDelta) << sh));
                 }
             }
@@ -399,27 +414,69 @@ __global__ __launch_bounds__(kHllLdsWG) void hll_registers_lds_kernel(HllParams 
         load(base + 3 * kHllLdsIter + t4, b);
     }
 #endif
+    if (!logm) return;
+    // the log out, partitioned by register range like hll_p0_scatter: per range a count, one global reservation, then
+    // each entry at its range's base + its cursor (past the range's capacity: an atomicMax straight on the register)
+    __syncthreads();
+    const uint32_t n = min(*nlog, kHllLog);
+    const uint32_t R = hll_p0_ranges(m);
+    const uint32_t rshift = (uint32_t)P.p - (31u - (uint32_t)__builtin_clz(R));
+    for (uint32_t i = threadIdx.x; i < R; i += kHllLdsWG) { lcnt[i] = 0; lcur[i] = 0; }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += kHllLdsWG) atomicAdd(&lcnt[(rlog[i] & 0xFFFFFFu) >> rshift], 1u);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < R; i += kHllLdsWG) lbase[i] = lcnt[i] ? atomicAdd(&P.p0_cnt[i], lcnt[i]) : 0u;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += kHllLdsWG) {
+        const uint32_t e = rlog[i], idx = e & 0xFFFFFFu, r = idx >> rshift;
+        const uint32_t slot = lbase[r] + atomicAdd(&lcur[r], 1u);
+        if (slot < P.p0_cap) P.p0_buf[(size_t)r * P.p0_cap + slot] = e;
+        else atomicMax(&P.regs[idx], e >> 24);
+    }
+}
+
+// the refresh (or the phase-0 gather) counts the non-zero registers as it reads them: each block adds its count to
+// nz_part[0]; the last block to finish raises *nonzero to the total and re-arms the pair.  Registers only grow, so
+// the count is a lower bound on the registers at the end of the segment, which is all the LINEAR_COUNTING decision
+// needs (a lower bound above the threshold proves HYPERLOGLOG; otherwise the LC pass counts exactly)
+__device__ __forceinline__ void hll_count_nonzero(const HllParams& P, uint32_t nz, uint32_t* wsum) {
+    nz = wave_sum_u32(nz);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = nz;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (uint32_t w = 0; w < blockDim.x / 64; ++w) t += wsum[w];
+        if (t) atomicAdd(&P.nz_part[0], t);
+        __threadfence();
+        if (atomicAdd(&P.nz_part[1], 1u) == gridDim.x - 1) {
+            atomicMax(P.nonzero, atomicExch(&P.nz_part[0], 0u));
+            atomicExch(&P.nz_part[1], 0u);
+        }
+    }
 }
 
 // one refresh between register phases: per group of 64 registers (one wave) its floor (min register) and each
 // register's 4-bit lower bound over that floor, nibble = min(reg - group floor, 15), packed two per byte.  The phase
 // kernel derives the global floor from the group floors itself, so no second kernel, memset or atomic is needed.
-__global__ __launch_bounds__(1024) void hll_refresh_kernel(const unsigned int* regs, uint32_t m, unsigned char* gfloor,
-                                                           unsigned char* snap) {
+__global__ __launch_bounds__(1024) void hll_refresh_kernel(HllParams P) {
     static_assert(kHllBits == 4, "two nibbles per snapshot byte");
+    __shared__ uint32_t wsum[16];
+    const uint32_t m = 1u << P.p;
     const uint32_t gsz = m >= kHllGroup ? kHllGroup : m;
     const uint32_t g = blockIdx.x * 16 + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     const bool live = g * gsz < m && lane < gsz;
-    const uint32_t r = live ? regs[g * gsz + lane] : 0xFFFFFFFFu;
+    const uint32_t r = live ? P.regs[g * gsz + lane] : 0xFFFFFFFFu;
     uint32_t v = r;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
-    if (g * gsz >= m) return;
-    if (lane == 0) gfloor[g] = (unsigned char)min(v, 255u);
     const uint32_t d = live ? min(r - v, kHllMaxDelta) : 0u;
     const uint32_t hi = (uint32_t)__shfl_down((int)d, 1, 64);  // the odd neighbour's nibble
-    if (live && (lane & 1) == 0) snap[(g * gsz + lane) / 2] = (unsigned char)(d | (lane + 1 < gsz ? hi << 4 : 0u));
+    if (g * gsz < m) {
+        if (lane == 0) P.gfloor[g] = (unsigned char)min(v, 255u);
+        if (live && (lane & 1) == 0) P.snap[(g * gsz + lane) / 2] = (unsigned char)(d | (lane + 1 < gsz ? hi << 4 : 0u));
+    }
+    hll_count_nonzero(P, live && r != 0 ? 1u : 0u, wsum);
 }
 
 // Phase 0 by register range (a fresh request's first cut0 * m values, when every hash finds an empty or low
@@ -493,6 +550,10 @@ __global__ __launch_bounds__(1024) void hll_p0_gather_kernel(HllParams P) {
         if ((lane & 1) == 0) P.snap[(r0 + gl * kHllGroup + lane) / 2] = (unsigned char)(d | (hi << 4));
     }
     if (threadIdx.x == 0) atomicExch(&P.p0_cnt[b], 0u);
+    uint32_t nz = 0;
+    for (uint32_t i = threadIdx.x; i < per; i += 1024) nz += reg[i] != 0;
+    __shared__ uint32_t wsum[16];
+    hll_count_nonzero(P, nz, wsum);
 }
 
 // group floors: one wave per group of 64 registers; with `out`, the global floor is their min (*out initialised to ~0),
@@ -619,8 +680,7 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
     auto refresh = [&]() {
         const uint32_t ng = m >= kHllGroup ? m / kHllGroup : 1u;
         if (lds) {  // group floors and the nibble snapshot in one pass
-            hipLaunchKernelGGL(hll_refresh_kernel, dim3((ng + 15) / 16), dim3(1024), 0, st, (const unsigned int*)p.regs, m,
-                               p.gfloor, p.snap);
+            hipLaunchKernelGGL(hll_refresh_kernel, dim3((ng + 15) / 16), dim3(1024), 0, st, p);
             return;
         }
         (void)hipMemsetAsync(p.floor, 0xFF, 4, st);
@@ -637,6 +697,9 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
 #endif
     // phase 0 partitioned by register range (the LDS phases' kinds, p >= 12: at least 64 ranges of whole groups)
     const bool p0 = ESGPU_HLL_P0 && lds && !warm && p.p >= 12 && p.p0_cnt && cuts.size() > 1 && cuts[1] > 0;
+    // LDS phases log their raises and a gather applies them (p.log_raises, set by the host when p0_cnt is there)
+    const bool logr = lds && p.log_raises && p.p0_cnt && p.p >= 12;
+    bool counted = false;  // the last launch that touched the registers was a gather: *nonzero is exact
     for (size_t ph = 0; ph + 1 < cuts.size(); ++ph) {
         const uint32_t span = cuts[ph + 1] - cuts[ph];
         if (span == 0) continue;
@@ -645,6 +708,7 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
             if (p.kind == HLL_I64) hipLaunchKernelGGL(hll_p0_scatter_kernel<HLL_I64>, g1, dim3(kP0WG), 0, st, p, span);
             else hipLaunchKernelGGL(hll_p0_scatter_kernel<HLL_F64>, g1, dim3(kP0WG), 0, st, p, span);
             hipLaunchKernelGGL(hll_p0_gather_kernel, dim3(hll_p0_ranges(m)), dim3(1024), 0, st, p);
+            counted = true;
             continue;  // the gather left the registers' group floors and snapshot behind: no refresh
         }
         const bool floored = warm || ph > 0;
@@ -656,14 +720,14 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
         const unsigned int* fl = floored ? (const unsigned int*)p.floor : (const unsigned int*)nullptr;
         if (lds && floored) {
             // one 1024-thread workgroup per CU (128 KB of nibbles at p = 18), more for smaller p
-            const uint32_t per_cu = std::max(1u, std::min(4u, (uint32_t)(160u * 1024u / (hll_lds_bytes(m) + 1024u))));
+            const uint32_t per_cu = std::max(1u, std::min(4u, (uint32_t)(160u * 1024u / (hll_lds_bytes(m, logr) + 1024u))));
             uint32_t lw = std::max(1u, std::min(cus * per_cu, span / (kHllLdsIter * 4)));
             const uint32_t lper = ((span + lw - 1) / lw + 3) & ~3u;
             lw = (span + lper - 1) / lper;
             if (p.kind == HLL_I64)
-                hipLaunchKernelGGL(hll_registers_lds_kernel<HLL_I64>, dim3(lw), dim3(kHllLdsWG), hll_lds_bytes(m), st, p, cuts[ph], cuts[ph + 1], lper, fl);
+                hipLaunchKernelGGL(hll_registers_lds_kernel<HLL_I64>, dim3(lw), dim3(kHllLdsWG), hll_lds_bytes(m, logr), st, p, cuts[ph], cuts[ph + 1], lper, fl);
             else
-                hipLaunchKernelGGL(hll_registers_lds_kernel<HLL_F64>, dim3(lw), dim3(kHllLdsWG), hll_lds_bytes(m), st, p, cuts[ph], cuts[ph + 1], lper, fl);
+                hipLaunchKernelGGL(hll_registers_lds_kernel<HLL_F64>, dim3(lw), dim3(kHllLdsWG), hll_lds_bytes(m, logr), st, p, cuts[ph], cuts[ph + 1], lper, fl);
         } else if (fast && p.kind == HLL_I64)
             hipLaunchKernelGGL(hll_registers_fast_kernel<HLL_I64>, dim3(wgs), dim3(kHllWG), 0, st, p, cuts[ph], cuts[ph + 1], per, fl);
         else if (fast && p.kind == HLL_F64)
@@ -672,12 +736,22 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
             hipLaunchKernelGGL(hll_registers_fast_kernel<HLL_ORD>, dim3(wgs), dim3(kHllWG), 0, st, p, cuts[ph], cuts[ph + 1], per, fl);
         else
             hipLaunchKernelGGL(hll_registers_kernel, dim3(wgs), dim3(kHllWG), 0, st, p, cuts[ph], cuts[ph + 1], per, fl);
+        if (lds && floored && logr) {  // the phase's logged raises applied; floors, snapshot and count refreshed
+            hipLaunchKernelGGL(hll_p0_gather_kernel, dim3(hll_p0_ranges(m)), dim3(1024), 0, st, p);
+            counted = true;
+            continue;
+        }
+        counted = false;
         if (ph + 2 < cuts.size()) refresh();
     }
-    (void)hipMemsetAsync(p.nonzero, 0, 4, st);  // recount over the registers (they accumulate across segments)
-    hipLaunchKernelGGL(hll_nonzero_kernel, dim3(floor_grid), dim3(1024), 0, st, (const unsigned int*)p.regs, m, p.nonzero);
+    if (!counted) {  // after a gather *nonzero is already the count of the final registers (hll_count_nonzero)
+        (void)hipMemsetAsync(p.nonzero, 0, 4, st);  // recount over the registers (they accumulate across segments)
+        hipLaunchKernelGGL(hll_nonzero_kernel, dim3(floor_grid), dim3(1024), 0, st, (const unsigned int*)p.regs, m, p.nonzero);
+    }
+    // the LC pass: mostly a launch whose blocks see *nonzero above the threshold and return at once; 2048 blocks
+    // loop over the docs when it does run
     uint32_t grid = (n + 1023) / 1024;
-    if (grid > 8192) grid = 8192;
+    if (grid > 2048) grid = 2048;
     if (grid == 0) grid = 1;
     hipLaunchKernelGGL(hll_lc_kernel, dim3(grid), dim3(256), 0, st, p);
 }

@@ -132,6 +132,7 @@ struct HllParams {
     unsigned int* floor;        // scratch: min register after a phase
     unsigned char* gfloor;      // scratch: min register of each group of 64 registers after a phase ([max(m / 64, 1)])
     unsigned char* snap;        // scratch: registers as 4-bit lower bounds over the floor ([2^p / 2], 16-byte aligned)
+    unsigned int* nz_part;      // [2] refresh / phase-0 gather: partial non-zero count and finished blocks (self-resetting)
     uint32_t lc_mask;
     uint32_t lc_threshold;
     uint64_t seen;              // values the registers already hold from earlier segments of this request
@@ -146,6 +147,8 @@ struct HllParams {
     unsigned int* p0_cnt;
     unsigned int* p0_buf;
     uint32_t p0_cap;
+    int32_t log_raises;         // LDS phases log their register raises and leave them, partitioned by range, in p0_buf
+                                // for the gather kernel (instead of one global atomicMax per raise); needs p0_cnt
 };
 #ifndef ESGPU_HLL_CUT0  // HLL phase 0 spans the request's first ESGPU_HLL_CUT0 * 2^p values
 #define ESGPU_HLL_CUT0 4  // measured: 4 beats 16 by 3-4 % (phase 0 reads and raises registers for every hash)

@@ -863,6 +863,7 @@ struct Pipeline {
     DevBuf lc_first;                 // [lc_mask + 1] u64: insertion order of each LC set entry (HllParams.lc_first)
     uint32_t lc_mask = 0, lc_threshold = 0;
     uint64_t hll_seen = 0;           // values hashed into the registers by earlier segments of this request
+    bool lc_dirty = true;            // lc_set / lc_first may hold entries (cleared at reset only then)
     // post_collection products
     std::vector<uint8_t> h_regs;
     std::vector<uint32_t> h_lc;
@@ -2541,7 +2542,7 @@ static void ensure_ord_hash(esgpu_ctx* c, const DevColumn* col, hipStream_t st) 
     HIPX(hipStreamSynchronize(st));
 }
 
-static size_t hll_snap_offset(uint32_t m) { return (16 + std::max<size_t>(m / 64, 1) + 15) & ~(size_t)15; }
+static size_t hll_snap_offset(uint32_t m) { return (32 + std::max<size_t>(m / 64, 1) + 15) & ~(size_t)15; }
 static size_t hll_p0_offset(uint32_t m) { return (hll_snap_offset(m) + std::max<size_t>(m / 2, 16) + 15) & ~(size_t)15; }
 
 static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
@@ -2559,13 +2560,13 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
         HIPX(hipMemsetAsync(pl.lc_set.p, 0, (size_t)cap * 4, p->stream));
         pl.lc_first.alloc(p->ctx, (size_t)cap * 8);
         HIPX(hipMemsetAsync(pl.lc_first.p, 0xFF, (size_t)cap * 8, p->stream));
-        // counters, then the group floors, then the packed register snapshot (16-byte aligned), then (p >= 12) the
+        // counters (32 bytes), then the group floors, then the packed register snapshot (16-byte aligned), then (p >= 12) the
         // partitioned phase 0's range counters (zero between requests) and entries
         const size_t p0_off = hll_p0_offset(m);
         const size_t p0_bytes = pl.p >= 12 ? 16 * (((size_t)hll_p0_ranges(m) * 4 + 15) / 16) +
                                                  (size_t)hll_p0_ranges(m) * hll_p0_cap(m, ESGPU_HLL_CUT0) * 4 : 0;
         pl.lc_count.alloc(p->ctx, p0_off + p0_bytes);
-        HIPX(hipMemsetAsync(pl.lc_count.p, 0, 16, p->stream));
+        HIPX(hipMemsetAsync(pl.lc_count.p, 0, 32, p->stream));
         if (p0_bytes) HIPX(hipMemsetAsync(pl.lc_count.as<unsigned char>() + p0_off, 0, (size_t)hll_p0_ranges(m) * 4, p->stream));
         pl.allocated = true;
     }
@@ -2621,13 +2622,18 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
     H.lc_count = pl.lc_count.as<unsigned int>();
     H.nonzero = pl.lc_count.as<unsigned int>() + 1;
     H.floor = pl.lc_count.as<unsigned int>() + 2;
-    H.gfloor = pl.lc_count.as<unsigned char>() + 16;
+    H.nz_part = pl.lc_count.as<unsigned int>() + 4;
+    H.gfloor = pl.lc_count.as<unsigned char>() + 32;
     H.snap = pl.lc_count.as<unsigned char>() + hll_snap_offset(1u << pl.p);
     if (pl.p >= 12) {
         const uint32_t m = 1u << pl.p;
         H.p0_cnt = (unsigned int*)(pl.lc_count.as<unsigned char>() + hll_p0_offset(m));
         H.p0_buf = H.p0_cnt + 4 * (((size_t)hll_p0_ranges(m) * 4 + 15) / 16);
         H.p0_cap = hll_p0_cap(m, ESGPU_HLL_CUT0);
+        // the register phases log their raises for a gather instead of raising each with a scattered global atomic
+        // (which run at the memory side at ~20 G/s); ESGPU_HLL_LOG=0 keeps the atomics (A/B runs)
+        static const int log_raises = [] { const char* e = std::getenv("ESGPU_HLL_LOG"); return e && *e == '0' ? 0 : 1; }();
+        H.log_raises = log_raises;
     }
     H.lc_mask = pl.lc_mask;
     H.lc_threshold = pl.lc_threshold;
@@ -2636,6 +2642,7 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
     H.seen = pl.hll_seen;
     if (H.n_docs == 0) return false;
     pl.hll_seen += H.n_docs;
+    pl.lc_dirty = true;
     HIPX(hipEventRecord(pl.e0, p->stream));
     launch_hll(H, (uint32_t)p->ctx->cus, p->stream);
     HIPX(hipGetLastError());
@@ -2754,6 +2761,7 @@ extern "C" int esgpu_plan_post_collection(esgpu_plan* p) {
             bsync(p);
             const uint32_t m = 1u << pl.p;
             pl.any_value = cnt[0] > 0 || cnt[1] > 0;
+            pl.lc_dirty = cnt[0] > 0;  // the LC pass inserted nothing: its set is still clear
             if (cnt[1] <= pl.lc_threshold && cnt[0] <= pl.lc_threshold) {  // LINEAR_COUNTING: the distinct encoded hashes
                 pl.hll_mode = 0;
                 const size_t cap = (size_t)pl.lc_mask + 1;
@@ -3731,9 +3739,16 @@ extern "C" int esgpu_plan_reset(esgpu_plan* p) {
             if (!pl.allocated) continue;
             if (pl.kind == 1) {
                 HIPX(hipMemsetAsync(pl.regs.p, 0, pl.regs.bytes, p->stream));
-                HIPX(hipMemsetAsync(pl.lc_set.p, 0, pl.lc_set.bytes, p->stream));
-                HIPX(hipMemsetAsync(pl.lc_first.p, 0xFF, pl.lc_first.bytes, p->stream));
-                HIPX(hipMemsetAsync(pl.lc_count.p, 0, pl.lc_count.bytes, p->stream));
+                if (pl.lc_dirty) {  // the LC pass inserted hashes in the last request (12 MB at p = 18 otherwise skipped)
+                    HIPX(hipMemsetAsync(pl.lc_set.p, 0, pl.lc_set.bytes, p->stream));
+                    HIPX(hipMemsetAsync(pl.lc_first.p, 0xFF, pl.lc_first.bytes, p->stream));
+                    pl.lc_dirty = false;
+                }
+                // the counters (the group floors, snapshot and phase-0 entries are rewritten before they are read)
+                HIPX(hipMemsetAsync(pl.lc_count.p, 0, 32, p->stream));
+                if (pl.p >= 12)
+                    HIPX(hipMemsetAsync(pl.lc_count.as<unsigned char>() + hll_p0_offset(1u << pl.p), 0,
+                                        (size_t)hll_p0_ranges(1u << pl.p) * 4, p->stream));
                 pl.h_lc.clear();
                 pl.h_regs.clear();
                 pl.any_value = false;
