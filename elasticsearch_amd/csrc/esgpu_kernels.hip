@@ -523,7 +523,7 @@ __global__ __launch_bounds__(kP0WG) void hll_p0_scatter_kernel(HllParams P, uint
 // hll_p0_gather: one workgroup per range: its registers maxed with its entries in LDS, stored once, and the range's
 // group floors and nibble snapshot written as hll_refresh_kernel would (the first LDS phase needs no refresh launch);
 // the range's fill counter is re-armed for the next request
-__global__ __launch_bounds__(1024) void hll_p0_gather_kernel(HllParams P) {
+__global__ __launch_bounds__(1024) void hll_p0_gather_kernel(HllParams P, int count) {
     static_assert(kHllBits == 4, "two nibbles per snapshot byte");
     __shared__ uint32_t reg[1024];
     const uint32_t m = 1u << P.p, per = m / hll_p0_ranges(m);  // 64 .. 1024 registers (p <= 18)
@@ -550,6 +550,7 @@ __global__ __launch_bounds__(1024) void hll_p0_gather_kernel(HllParams P) {
         if ((lane & 1) == 0) P.snap[(r0 + gl * kHllGroup + lane) / 2] = (unsigned char)(d | (hi << 4));
     }
     if (threadIdx.x == 0) atomicExch(&P.p0_cnt[b], 0u);
+    if (!count) return;  // only the segment's last gather counts (the LC decision reads the final registers)
     uint32_t nz = 0;
     for (uint32_t i = threadIdx.x; i < per; i += 1024) nz += reg[i] != 0;
     __shared__ uint32_t wsum[16];
@@ -662,7 +663,8 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
 #ifndef ESGPU_HLL_GROW
 #define ESGPU_HLL_GROW 4
 #endif
-    uint64_t c = (uint64_t)m * ESGPU_HLL_CUT0;
+    const uint32_t cut0 = p.cut0 ? p.cut0 : ESGPU_HLL_CUT0;
+    uint64_t c = (uint64_t)m * cut0;
     while (c <= p.seen) c *= ESGPU_HLL_GROW;
     while (c < p.seen + n) {
         cuts.push_back((uint32_t)(c - p.seen) & ~3u);
@@ -690,7 +692,7 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
         else
             hipLaunchKernelGGL(hll_floor_kernel, dim3(floor_grid), dim3(1024), 0, st, (const unsigned int*)p.regs, m, p.floor);
     };
-    const bool warm = p.seen >= (uint64_t)m * ESGPU_HLL_CUT0;  // the registers already passed the first cut
+    const bool warm = p.seen >= (uint64_t)m * cut0;  // the registers already passed the first cut
     if (warm) refresh();
 #ifndef ESGPU_HLL_P0
 #define ESGPU_HLL_P0 1
@@ -707,8 +709,8 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
             const dim3 g1((span + kP0WG * kP0Docs - 1) / (kP0WG * kP0Docs));
             if (p.kind == HLL_I64) hipLaunchKernelGGL(hll_p0_scatter_kernel<HLL_I64>, g1, dim3(kP0WG), 0, st, p, span);
             else hipLaunchKernelGGL(hll_p0_scatter_kernel<HLL_F64>, g1, dim3(kP0WG), 0, st, p, span);
-            hipLaunchKernelGGL(hll_p0_gather_kernel, dim3(hll_p0_ranges(m)), dim3(1024), 0, st, p);
-            counted = true;
+            hipLaunchKernelGGL(hll_p0_gather_kernel, dim3(hll_p0_ranges(m)), dim3(1024), 0, st, p, ph + 2 >= cuts.size() ? 1 : 0);
+            counted = ph + 2 >= cuts.size();
             continue;  // the gather left the registers' group floors and snapshot behind: no refresh
         }
         const bool floored = warm || ph > 0;
@@ -737,8 +739,8 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
         else
             hipLaunchKernelGGL(hll_registers_kernel, dim3(wgs), dim3(kHllWG), 0, st, p, cuts[ph], cuts[ph + 1], per, fl);
         if (lds && floored && logr) {  // the phase's logged raises applied; floors, snapshot and count refreshed
-            hipLaunchKernelGGL(hll_p0_gather_kernel, dim3(hll_p0_ranges(m)), dim3(1024), 0, st, p);
-            counted = true;
+            hipLaunchKernelGGL(hll_p0_gather_kernel, dim3(hll_p0_ranges(m)), dim3(1024), 0, st, p, ph + 2 >= cuts.size() ? 1 : 0);
+            counted = ph + 2 >= cuts.size();
             continue;
         }
         counted = false;

@@ -147,6 +147,7 @@ struct HllParams {
     unsigned int* p0_cnt;
     unsigned int* p0_buf;
     uint32_t p0_cap;
+    uint32_t cut0;              // phase 0 spans the request's first cut0 * 2^p values (ESGPU_HLL_CUT0)
     int32_t log_raises;         // LDS phases log their register raises and leave them, partitioned by range, in p0_buf
                                 // for the gather kernel (instead of one global atomicMax per raise); needs p0_cnt
 };

@@ -2543,6 +2543,15 @@ static void ensure_ord_hash(esgpu_ctx* c, const DevColumn* col, hipStream_t st) 
 }
 
 static size_t hll_snap_offset(uint32_t m) { return (32 + std::max<size_t>(m / 64, 1) + 15) & ~(size_t)15; }
+// HLL phase 0 length in registers' worth of values (ESGPU_HLL_CUT0 env overrides the build default for A/B runs)
+static uint32_t hll_cut0() {
+    static const uint32_t c = [] {
+        const char* e = std::getenv("ESGPU_HLL_CUT0");
+        const int v = e && *e ? std::atoi(e) : 0;
+        return v >= 1 && v <= 256 ? (uint32_t)v : (uint32_t)ESGPU_HLL_CUT0;
+    }();
+    return c;
+}
 static size_t hll_p0_offset(uint32_t m) { return (hll_snap_offset(m) + std::max<size_t>(m / 2, 16) + 15) & ~(size_t)15; }
 
 static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
@@ -2564,7 +2573,7 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
         // partitioned phase 0's range counters (zero between requests) and entries
         const size_t p0_off = hll_p0_offset(m);
         const size_t p0_bytes = pl.p >= 12 ? 16 * (((size_t)hll_p0_ranges(m) * 4 + 15) / 16) +
-                                                 (size_t)hll_p0_ranges(m) * hll_p0_cap(m, ESGPU_HLL_CUT0) * 4 : 0;
+                                                 (size_t)hll_p0_ranges(m) * hll_p0_cap(m, hll_cut0()) * 4 : 0;
         pl.lc_count.alloc(p->ctx, p0_off + p0_bytes);
         HIPX(hipMemsetAsync(pl.lc_count.p, 0, 32, p->stream));
         if (p0_bytes) HIPX(hipMemsetAsync(pl.lc_count.as<unsigned char>() + p0_off, 0, (size_t)hll_p0_ranges(m) * 4, p->stream));
@@ -2623,13 +2632,14 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
     H.nonzero = pl.lc_count.as<unsigned int>() + 1;
     H.floor = pl.lc_count.as<unsigned int>() + 2;
     H.nz_part = pl.lc_count.as<unsigned int>() + 4;
+    H.cut0 = hll_cut0();
     H.gfloor = pl.lc_count.as<unsigned char>() + 32;
     H.snap = pl.lc_count.as<unsigned char>() + hll_snap_offset(1u << pl.p);
     if (pl.p >= 12) {
         const uint32_t m = 1u << pl.p;
         H.p0_cnt = (unsigned int*)(pl.lc_count.as<unsigned char>() + hll_p0_offset(m));
         H.p0_buf = H.p0_cnt + 4 * (((size_t)hll_p0_ranges(m) * 4 + 15) / 16);
-        H.p0_cap = hll_p0_cap(m, ESGPU_HLL_CUT0);
+        H.p0_cap = hll_p0_cap(m, hll_cut0());
         // the register phases log their raises for a gather instead of raising each with a scattered global atomic
         // (which run at the memory side at ~20 G/s); ESGPU_HLL_LOG=0 keeps the atomics (A/B runs)
         static const int log_raises = [] { const char* e = std::getenv("ESGPU_HLL_LOG"); return e && *e == '0' ? 0 : 1; }();
