@@ -1985,6 +1985,28 @@ void launch_hist_ords(const int64_t* v, const uint64_t* present, uint32_t n_docs
                        n_pad, f64 ? 1 : 0, interval, offset, key0, nkeys, out);
 }
 
+// three bucket levels: the pair of two single-valued ordinal columns as one composite ordinal a * nb + b (missing when
+// either is missing or out of its dictionary); 16-byte loads and stores, n_pad is a multiple of kBlockDocs
+__global__ __launch_bounds__(256) void comp_ords_kernel(const uint32_t* a, const uint32_t* b, uint32_t n_pad, uint32_t na,
+                                                        uint32_t nb, uint32_t* out) {
+    for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n_pad; i += gridDim.x * blockDim.x * 4) {
+        uint32_t x[4], y[4];
+        load_u32x4(a, i, x);
+        load_u32x4(b, i, y);
+        u32x4_t o;
+        o.x = x[0] < na && y[0] < nb ? x[0] * nb + y[0] : kMissingOrd;
+        o.y = x[1] < na && y[1] < nb ? x[1] * nb + y[1] : kMissingOrd;
+        o.z = x[2] < na && y[2] < nb ? x[2] * nb + y[2] : kMissingOrd;
+        o.w = x[3] < na && y[3] < nb ? x[3] * nb + y[3] : kMissingOrd;
+        *reinterpret_cast<u32x4_t*>(out + i) = o;
+    }
+}
+void launch_comp_ords(const uint32_t* a, const uint32_t* b, uint32_t n_pad, uint32_t na, uint32_t nb, uint32_t* out, hipStream_t st) {
+    if (n_pad == 0) return;
+    hipLaunchKernelGGL(comp_ords_kernel, dim3(std::min<uint32_t>(8192, (n_pad / 4 + 255) / 256)), dim3(256), 0, st, a, b, n_pad,
+                       na, nb, out);
+}
+
 void launch_minmax_i64(const int64_t* v, uint64_t n, int64_t* out, bool f64, hipStream_t st) {
     if (n == 0) return;
     hipLaunchKernelGGL(minmax_i64_kernel, dim3((uint32_t)std::min<uint64_t>(1024, (n + 255) / 256)), dim3(256), 0, st, v, n, out,

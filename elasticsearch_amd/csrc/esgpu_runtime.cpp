@@ -854,6 +854,13 @@ struct Pipeline {
     bool keyed = false;              // the key range has been taken from a segment's values (else H == 1, key0 == 0)
     bool inner_terms = false;        // terms under terms: the key dimension is the inner terms field's ordinals
     std::shared_ptr<const TermDict> tdict2;  // inner terms: the dictionary its keys resolve through
+    // three bucket levels (two terms and one histogram): the ordinal dimension is the pair of the two terms fields,
+    // ord = a * vcB + b (ord_field = a's field, ord_field2 = b's), derived per segment into ord_col
+    bool comp = false;
+    int comp_spec2 = -1;
+    std::string ord_field2;
+    std::shared_ptr<const TermDict> tdictB;
+    uint64_t vcA = 0, vcB = 0;
     uint64_t value_count2 = 0;       // inner terms: its global ordinal count (H is max(value_count2, 1))
     int vcnt_mode = 0, ocnt_mode = OCNT_NONE;
     DevBuf g_cnt, g_ocnt, g_vcnt, g_sum, g_min, g_max, g_sq;
@@ -898,7 +905,12 @@ struct ChildSrc {
                                      // (pipes[0]) and its metric children (grand), all under its clauses
     LeafRef leaf;                    // metric / cardinality child
     std::vector<int> pipes;          // bucket child: pipelines carrying it (pipes[0]'s counts define its buckets)
-    std::vector<LeafRef> grand;      // bucket child: its children in request order
+    std::vector<LeafRef> grand;      // bucket child: its children in request order (a deep child excluded)
+    // a bucket child X whose last child is a bucket aggregation Y (three levels): Y's spec, the shape (1: terms{terms{
+    // histogram}}, 2: terms{histogram{terms}}, 3: histogram{terms{terms}}), Y's composite pipelines and leaf refs
+    int deep = -1, deep_shape = 0;
+    std::vector<int> dpipes;
+    std::vector<LeafRef> dgrand;
 };
 struct Group {
     int root = -1, fspec = -1;
@@ -939,6 +951,7 @@ struct esgpu_plan {
     hipEvent_t ev_mid = nullptr;
     PinnedBuf h_tcnt, h_rows, h_dst[6];
     Scratch s_nnz;                     // build: non-empty slots per winner row (compact_rows)
+    Scratch s_drows;                   // build: composite ordinals a three-level child reads (fetch_rows)
     Scratch s_xbits;                   // doc bitset of a pipeline with more than kMaxPreds clauses
     uint32_t seg_seq = 0;              // segments collected since create / reset (cardinality insertion order)
     std::vector<PinnedBuf> h_compact;  // build: per bucket child, its GPU-compacted buckets and leaves (pinned)
@@ -1103,15 +1116,41 @@ static Group compile_group(esgpu_plan* p, int r, int fspec) {
             cs.leaf = leaf_refs[li++];
         } else {
             cs.bucket = true;
-            const bool ot = root.s.type == ESGPU_AGG_TERMS, it = p->specs[ch].s.type == ESGPU_AGG_TERMS;
             std::vector<int> inner_leaves;
-            for (int gc : p->specs[ch].children) {
-                const int t = p->specs[gc].s.type;
-                require(is_metric(t) || t == ESGPU_AGG_CARDINALITY, ESGPU_ERR_UNSUPPORTED, "bucket aggregations nested three levels deep");
-                inner_leaves.push_back(gc);
+            const std::vector<int>& xc = p->specs[ch].children;
+            for (size_t q = 0; q < xc.size(); ++q) {
+                const int t = p->specs[xc[q]].s.type;
+                if (is_bucket(t) && q + 1 == xc.size()) { cs.deep = xc[q]; continue; }
+                require(is_metric(t) || t == ESGPU_AGG_CARDINALITY, ESGPU_ERR_UNSUPPORTED,
+                        "a bucket aggregation three levels deep other than the last sub-aggregation runs on the CPU path");
+                inner_leaves.push_back(xc[q]);
             }
             cs.pipes = add_leaf_pipelines(p, r, fspec, r, ch, inner_leaves, &cs.grand);
             for (int pi : cs.pipes) g.pipes.push_back(pi);
+            if (cs.deep >= 0) {  // three levels: two terms and one histogram (the histogram at any level)
+                const SpecNode& Y = p->specs[cs.deep];
+                std::vector<int> yl;
+                for (int gc : Y.children) {
+                    const int t = p->specs[gc].s.type;
+                    require(is_metric(t) || t == ESGPU_AGG_CARDINALITY, ESGPU_ERR_UNSUPPORTED, "bucket aggregations nested four levels deep");
+                    yl.push_back(gc);
+                }
+                const bool rt = root.s.type == ESGPU_AGG_TERMS, xt = p->specs[ch].s.type == ESGPU_AGG_TERMS,
+                           yt = Y.s.type == ESGPU_AGG_TERMS;
+                require((int)rt + (int)xt + (int)yt == 2, ESGPU_ERR_UNSUPPORTED,
+                        "three bucket levels other than two terms and one histogram run on the CPU path");
+                cs.deep_shape = rt && xt ? 1 : rt ? 2 : 3;
+                // the composite pipelines: shape 1 [Y keys][R x X], shape 2 [X keys][R x Y], shape 3 [R keys][X x Y]
+                const int outer_b = cs.deep_shape == 1 ? cs.deep : ch;
+                cs.dpipes = add_leaf_pipelines(p, r, fspec, r, outer_b, yl, &cs.dgrand);
+                for (int pi : cs.dpipes) {
+                    Pipeline& D = p->pipes[pi];
+                    D.comp = true;
+                    D.comp_spec2 = cs.deep_shape == 1 ? ch : cs.deep;
+                    D.ord_field2 = p->specs[D.comp_spec2].field;
+                    g.pipes.push_back(pi);
+                }
+            }
         }
         g.kids.push_back(std::move(cs));
     }
@@ -2065,6 +2104,41 @@ static const DevColumn* derive_hist_ords(esgpu_plan* p, Pipeline& pl, const esgp
     if (materialize) materialize_hist_ords(p, pl, s);
     return &d;
 }
+// three bucket levels: this segment's composite ordinals of the two terms fields (a * vcB + b) as pl.ord_col, or null
+// when the segment lacks either field (its docs then fall in no bucket of the deepest level; the levels above count them
+// through their own pipelines).  Both fields single-valued keyword fields numbered by the request's dictionaries.
+static const DevColumn* derive_comp_ords(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s) {
+    const DevColumn* a = s->col(pl.ord_field.c_str());
+    const DevColumn* b = s->col(pl.ord_field2.c_str());
+    if (!a || !b) return nullptr;
+    require(a->type == ESGPU_COL_ORD_U32 && b->type == ESGPU_COL_ORD_U32, ESGPU_ERR_UNSUPPORTED,
+            "terms on numeric fields run on the CPU path");
+    require(!a->multi && !b->multi, ESGPU_ERR_UNSUPPORTED, "multi-valued terms fields three bucket levels deep run on the CPU path");
+    if (pl.fresh || !pl.tdict) {
+        pl.tdict = a->ord_dict();
+        pl.tdictB = b->ord_dict();
+        pl.vcA = a->ord_count();
+        pl.vcB = b->ord_count();
+    } else {
+        require(same_dict(a->ord_dict(), pl.tdict) && same_dict(b->ord_dict(), pl.tdictB), ESGPU_ERR_INVALID,
+                "segments number the terms of [" + pl.ord_field + "] or [" + pl.ord_field2 + "] differently: build an "
+                "ordinal map (esgpu_ordinal_map_build) over the reader's segments first");
+    }
+    const uint64_t na = std::max<uint64_t>(pl.vcA, 1), nb = std::max<uint64_t>(pl.vcB, 1);
+    require(na * nb < 0xFFFFFFFFull, ESGPU_ERR_UNSUPPORTED, "three bucket levels over more than 2^32 term pairs");
+    if (!pl.ord_col) pl.ord_col = std::make_shared<DevColumn>();
+    DevColumn& d = *pl.ord_col;
+    d.name = pl.ord_field;
+    d.type = ESGPU_COL_ORD_U32;
+    d.multi = false;
+    d.value_count = na * nb;
+    if (d.values.bytes < (size_t)s->n_pad * 4) d.values.alloc(p->ctx, (size_t)s->n_pad * 4);
+    launch_comp_ords(a->ords().as<uint32_t>(), b->ords().as<uint32_t>(), (uint32_t)s->n_pad, (uint32_t)pl.vcA,
+                     (uint32_t)pl.vcB, d.values.as<uint32_t>(), p->stream);
+    HIPX(hipGetLastError());
+    return &d;
+}
+
 static void materialize_hist_ords(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s) {
     const DevColumn* src = s->col(pl.ord_field.c_str());
     DevColumn& d = *pl.ord_col;
@@ -2108,7 +2182,7 @@ static std::vector<uint32_t> hashset_values(std::vector<std::pair<uint64_t, uint
 
 static void collect_cards(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
     const bool ORD = pl.term_spec >= 0, HIST = pl.hist_spec >= 0;
-    const DevColumn* oc = ORD ? (pl.ord_hist ? pl.ord_col.get() : s->col(pl.ord_field.c_str())) : nullptr;
+    const DevColumn* oc = ORD ? (pl.ord_hist || pl.comp ? pl.ord_col.get() : s->col(pl.ord_field.c_str())) : nullptr;
     const DevColumn* hc = HIST ? s->col(pl.hist_field.c_str()) : nullptr;
     CollectParams G{};
     G.n_docs = s->max_doc;
@@ -2208,7 +2282,9 @@ static constexpr uint32_t kTermsCopies = ESGPU_TERMS_COPIES;
 
 static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
     const bool ORD = pl.term_spec >= 0, HIST = pl.hist_spec >= 0;
-    const DevColumn* oc = ORD ? (pl.ord_hist ? derive_hist_ords(p, pl, s, false) : s->col(pl.ord_field.c_str())) : nullptr;
+    const DevColumn* oc = !ORD ? nullptr : pl.ord_hist ? derive_hist_ords(p, pl, s, false)
+                        : pl.comp ? derive_comp_ords(p, pl, s) : s->col(pl.ord_field.c_str());
+    if (pl.comp && !oc) return 0;
     const DevColumn* hc = HIST ? s->col(pl.hist_field.c_str()) : nullptr;
     const DevColumn* mc = pl.met > 0 ? s->col(pl.metric_field.c_str()) : nullptr;
     const bool terms_outer = pl.outer == pl.term_spec;
@@ -2295,18 +2371,18 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         pl.ocnt_mode = ocnt;
         pl.keyed = has_keys;
         pl.value_count = oc ? oc->ord_count() : (ORD ? 0 : 1);
-        pl.tdict = oc ? oc->ord_dict() : nullptr;
+        if (!pl.comp) pl.tdict = oc ? oc->ord_dict() : nullptr;
         pl.tdict2 = pl.inner_terms && hc ? hc->ord_dict() : nullptr;
         pl.value_count2 = pl.inner_terms && hc ? hc->ord_count() : 0;
         if (!same) alloc_grid(p, pl);
         pl.fresh = false;
     } else {
-        if (oc && !pl.tdict && !pl.ord_hist)
+        if (oc && !pl.tdict && !pl.ord_hist && !pl.comp)
             throw EsError(ESGPU_ERR_UNSUPPORTED, "terms field [" + pl.ord_field + "] unmapped in the first segment under a histogram");
         if (oc && pl.ord_hist)
             require(pl.T == std::max<uint32_t>(pl.ord_keys, 1), ESGPU_ERR_UNSUPPORTED,
                     "the inner histogram had no values in the request's first segment: runs on the CPU path");
-        if (oc && !pl.ord_hist) require(same_dict(oc->ord_dict(), pl.tdict), ESGPU_ERR_INVALID,
+        if (oc && !pl.ord_hist && !pl.comp) require(same_dict(oc->ord_dict(), pl.tdict), ESGPU_ERR_INVALID,
                          "segments number the terms of [" + pl.ord_field + "] differently: build an ordinal map "
                          "(esgpu_ordinal_map_build) over the reader's segments first");
         if (pl.inner_terms && hc) {
@@ -3142,6 +3218,53 @@ static std::vector<TermPick> select_terms(const esgpu_agg_spec& s, const unsigne
     return cands;
 }
 
+// Three bucket levels: one instance of the deepest aggregation Y of bucket child `kid` from its composite pipelines'
+// host cells.  Terms: its candidates are the cells base + y * stride for every Y ordinal y (the same selection and
+// comparators as a two-level terms, GlobalOrdinalsStringTermsAggregator.buildAggregation); histogram: the cells base + s
+// for every key slot s, non-empty ones ascending (HistogramAggregator.buildAggregation).
+static double order_value(const esgpu_plan* p, const SpecNode& t, const Pipeline& pl, int leaf, size_t c);
+static void emit_deep(const esgpu_plan* p, const ChildSrc& kid, size_t base, size_t stride, Block& yb) {
+    const Pipeline& C0 = p->pipes[kid.dpipes[0]];
+    if (!C0.allocated) { yb.append_empty(); return; }
+    const SpecNode& tn = p->specs[kid.deep];
+    if (tn.s.type != ESGPU_AGG_TERMS) {
+        begin_instance(yb, 0);
+        std::vector<uint32_t> slots, cells;
+        std::vector<int64_t> counts;
+        for (uint32_t s2 = 0; s2 < C0.H; ++s2) {
+            const unsigned long long c = C0.hc.cnt[base + s2];
+            if (c == 0) continue;
+            slots.push_back(s2);
+            cells.push_back((uint32_t)(base + s2));
+            counts.push_back((int64_t)c);
+        }
+        append_hist_buckets(C0, slots, counts, yb);
+        for (size_t gj = 0; gj < kid.dgrand.size(); ++gj)
+            append_leaves(p, p->pipes[kid.dgrand[gj].pipe], kid.dgrand[gj].leaf, cells, yb.subs[gj]);
+        end_instance(yb);
+        return;
+    }
+    const uint32_t Ty = (uint32_t)C0.vcB;
+    std::vector<unsigned long long> cnt(std::max<uint32_t>(Ty, 1), 0);
+    for (uint32_t y = 0; y < Ty; ++y) cnt[y] = C0.hc.cnt[base + (size_t)y * stride];
+    LeafRef ordr;
+    if (tn.s.order == ESGPU_ORDER_AGG_ASC || tn.s.order == ESGPU_ORDER_AGG_DESC)
+        for (size_t gj = 0; gj < tn.children.size(); ++gj) if (tn.children[gj] == tn.order_child) ordr = kid.dgrand[gj];
+    int64_t other = 0;
+    const std::vector<TermPick> top = select_terms(tn.s, cnt.data(), Ty, &other, [&](uint32_t ord) {
+        return order_value(p, tn, p->pipes[ordr.pipe], ordr.leaf, base + (size_t)ord * stride);
+    });
+    begin_instance(yb, other);
+    std::string scratch;
+    for (const TermPick& tp : top) {
+        push_bucket(yb, tp.ord, C0.tdictB->view(tp.ord, scratch), tp.count);
+        if (tp.count == 0) { for (Block& sb : yb.subs) sb.append_empty(); continue; }
+        for (size_t gj = 0; gj < kid.dgrand.size(); ++gj)
+            append_leaf(p, p->pipes[kid.dgrand[gj].pipe], kid.dgrand[gj].leaf, base + (size_t)tp.ord * stride, yb.subs[gj]);
+    }
+    end_instance(yb);
+}
+
 // one InternalFilter instance of filter child `kid` at host cell c of its outer-level pipelines
 // (FilterAggregator.buildAggregation: bucketDocCount(owningBucketOrdinal), bucketAggregations(owningBucketOrdinal))
 static void append_filter(const esgpu_plan* p, const ChildSrc& kid, size_t c, Block& sub) {
@@ -3170,7 +3293,14 @@ static std::vector<Block> child_protos(const esgpu_plan* p, const Group& g) {
         }
         if (!k.bucket) { out.push_back(leaf_proto(p, k.spec)); continue; }
         std::vector<Block> grand;
-        for (int gc : p->specs[k.spec].children) grand.push_back(leaf_proto(p, gc));
+        for (int gc : p->specs[k.spec].children) {
+            if (gc != k.deep) { grand.push_back(leaf_proto(p, gc)); continue; }
+            std::vector<Block> yl;  // the third level's prototype: its (empty) instance over its own leaf prototypes
+            for (int gy : p->specs[gc].children) yl.push_back(leaf_proto(p, gy));
+            Block yb = p->specs[gc].s.type == ESGPU_AGG_TERMS ? terms_shell(p, gc, yl) : hist_shell(p, gc, yl);
+            yb.append_empty();
+            grand.push_back(std::move(yb));
+        }
         Block in = p->specs[k.spec].s.type == ESGPU_AGG_TERMS ? terms_shell(p, k.spec, grand) : hist_shell(p, k.spec, grand);
         in.append_empty();
         out.push_back(std::move(in));
@@ -3299,7 +3429,7 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
         if (!kid.bucket) { need_rows[kid.leaf.pipe] = 1; continue; }
         const Pipeline& B0 = p->pipes[kid.pipes[0]];
         bool ok = ESGPU_COMPACT_ROWS && B0.allocated && !B0.inner_terms && !B0.ord_hist && B0.cards.empty() &&
-                  kid.grand.size() <= (size_t)kCompactLeaves;
+                  kid.grand.size() <= (size_t)kCompactLeaves && kid.deep < 0;
         for (const LeafRef& l : kid.grand) {  // the leaves' grids index like B0's (the kernel reads one cell of each)
             const Pipeline& L = p->pipes[l.pipe];
             ok = ok && L.allocated && L.H == B0.H && L.T == B0.T && L.key0 == B0.key0 &&
@@ -3312,7 +3442,7 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
     }
     for (int pi : g.pipes) {
         Pipeline& pl = p->pipes[pi];
-        if (pl.allocated && (need_rows[pi] || !pl.cards.empty())) fetch_rows(p, pl, drows, k);
+        if (pl.allocated && !pl.comp && (need_rows[pi] || !pl.cards.empty())) fetch_rows(p, pl, drows, k);
     }
     for (size_t ki = 0; ki < g.kids.size(); ++ki) {
         if (!fast[ki] || !k) continue;
@@ -3359,11 +3489,59 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
     bmark(p, "fetched");
     for (int pi : g.pipes) {
         Pipeline& pl = p->pipes[pi];
-        if (!pl.allocated || pl.cards.empty()) continue;
+        if (!pl.allocated || pl.cards.empty() || pl.comp) continue;
         std::vector<uint32_t> cells((size_t)k * pl.H);
         for (uint32_t i = 0; i < k; ++i)
             for (uint32_t s2 = 0; s2 < pl.H; ++s2) cells[(size_t)i * pl.H + s2] = s2 * pl.T + top[i].ord;
         gather_cards(p, pl, cells);
+    }
+    // three-level children: the composite ordinals their emission reads, gathered as rows [r][H] -- shape 1 (terms{terms
+    // {histogram}}): (winner, each X term it selects), shape 2 (terms{histogram{terms}}): (winner, every Y term)
+    std::vector<std::vector<uint32_t>> deep_off(g.kids.size());
+    for (size_t ki = 0; ki < g.kids.size(); ++ki) {
+        const ChildSrc& kid = g.kids[ki];
+        if (kid.deep < 0) continue;
+        const Pipeline& B0 = p->pipes[kid.pipes[0]];
+        Pipeline& C0 = p->pipes[kid.dpipes[0]];
+        if (!C0.allocated || !B0.allocated) continue;
+        const uint64_t nb = C0.vcB;
+        std::vector<uint32_t> rows;
+        deep_off[ki].assign(k + 1, 0);
+        for (uint32_t i = 0; i < k; ++i) {
+            deep_off[ki][i] = (uint32_t)rows.size();
+            if (top[i].count == 0) continue;
+            if (kid.deep_shape == 1) {
+                if (!B0.tdict2) continue;
+                const SpecNode& tn2 = p->specs[kid.spec];
+                LeafRef ord2;
+                if (tn2.s.order == ESGPU_ORDER_AGG_ASC || tn2.s.order == ESGPU_ORDER_AGG_DESC)
+                    for (size_t gj = 0; gj < tn2.children.size(); ++gj) if (tn2.children[gj] == tn2.order_child) ord2 = kid.grand[gj];
+                const size_t row = (size_t)i * B0.H;
+                int64_t other2 = 0;
+                for (const TermPick& tp : select_terms(tn2.s, B0.hc.cnt + row, (uint32_t)B0.value_count2, &other2,
+                         [&](uint32_t ord) { return order_value(p, tn2, p->pipes[ord2.pipe], ord2.leaf, row + ord); }))
+                    rows.push_back((uint32_t)(top[i].ord * nb + tp.ord));
+            } else {
+                for (uint64_t y = 0; y < nb; ++y) rows.push_back((uint32_t)(top[i].ord * nb + y));
+            }
+        }
+        deep_off[ki][k] = (uint32_t)rows.size();
+        const uint32_t nr = (uint32_t)rows.size();
+        uint32_t* dr = (uint32_t*)p->s_drows.ensure(p->ctx, std::max<size_t>(nr, 1) * 4);
+        if (nr) HIPX(hipMemcpyAsync(dr, rows.data(), (size_t)nr * 4, hipMemcpyHostToDevice, st));
+        for (int pi : kid.dpipes) {
+            Pipeline& D = p->pipes[pi];
+            if (!D.allocated) continue;
+            require(D.H == C0.H && D.T == C0.T && D.key0 == C0.key0, ESGPU_ERR_DEVICE, "sibling pipelines disagree on the key grid");
+            fetch_rows(p, D, dr, nr);
+            if (!D.cards.empty()) {
+                std::vector<uint32_t> cells((size_t)nr * D.H);
+                for (uint32_t r2 = 0; r2 < nr; ++r2)
+                    for (uint32_t s2 = 0; s2 < D.H; ++s2) cells[(size_t)r2 * D.H + s2] = s2 * D.T + rows[r2];
+                gather_cards(p, D, cells);
+            }
+        }
+        bsync(p);  // s_drows is reused by the next three-level child
     }
     if (gpu_topk) {  // otherDocCount = (sum of all counts) - (sum of the winners' counts)
         for (uint32_t i = 0; i < k; ++i) {
@@ -3476,12 +3654,18 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
                 const std::vector<TermPick> top2 = select_terms(tn2.s, B0.hc.cnt + row, (uint32_t)B0.value_count2, &other2,
                     [&](uint32_t ord) { return order_value(p, tn2, p->pipes[ord2.pipe], ord2.leaf, row + ord); });
                 begin_instance(sub, other2);
+                uint32_t dj = kid.deep >= 0 && !deep_off[ki].empty() ? deep_off[ki][i] : 0;
                 for (const TermPick& tp : top2) {
                     const std::string term2 = B0.tdict2->term(tp.ord);
                     push_bucket(sub, tp.ord, &term2, tp.count);
-                    if (tp.count == 0) { for (Block& sb : sub.subs) sb.append_empty(); continue; }
+                    if (tp.count == 0) { for (Block& sb : sub.subs) sb.append_empty(); ++dj; continue; }
                     for (size_t gj = 0; gj < kid.grand.size(); ++gj)
                         append_leaf(p, p->pipes[kid.grand[gj].pipe], kid.grand[gj].leaf, row + tp.ord, sub.subs[gj]);
+                    if (kid.deep >= 0) {  // terms{terms{histogram}}: the histogram of composite row dj
+                        if (deep_off[ki].empty()) sub.subs.back().append_empty();
+                        else emit_deep(p, kid, (size_t)dj * p->pipes[kid.dpipes[0]].H, 1, sub.subs.back());
+                        ++dj;
+                    }
                 }
                 end_instance(sub);
                 continue;
@@ -3500,6 +3684,13 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
             append_hist_buckets(B0, slots, counts, sub);
             for (size_t gj = 0; gj < kid.grand.size(); ++gj)
                 append_leaves(p, p->pipes[kid.grand[gj].pipe], kid.grand[gj].leaf, cells, sub.subs[gj]);
+            if (kid.deep >= 0) {  // terms{histogram{terms}}: per key slot, Y's candidates in the winner's composite rows
+                const Pipeline& C0 = p->pipes[kid.dpipes[0]];
+                for (uint32_t s2 : slots) {
+                    if (deep_off[ki].empty()) { sub.subs.back().append_empty(); continue; }
+                    emit_deep(p, kid, (size_t)deep_off[ki][i] * C0.H + s2, C0.H, sub.subs.back());
+                }
+            }
             end_instance(sub);
         }
     }
@@ -3523,6 +3714,7 @@ static Block build_hist_root(esgpu_plan* p, const Group& g) {
         if (kid.filter) { for (int pi : kid.pipes) need[pi] = 1; continue; }
         if (!kid.bucket) { need[kid.leaf.pipe] = 1; continue; }
         for (const LeafRef& gr : kid.grand) need[gr.pipe] = 1;
+        for (int pi : kid.dpipes) need[pi] = 1;  // histogram{terms{terms}}: the whole composite grid
         Pipeline& B0 = p->pipes[kid.pipes[0]];
         const SpecNode& tn = p->specs[kid.spec];
         const bool count_order = tn.s.order == ESGPU_ORDER_COUNT_DESC || tn.s.order == ESGPU_ORDER_COUNT_ASC;
@@ -3641,6 +3833,12 @@ static Block build_hist_root(esgpu_plan* p, const Group& g) {
                 if (tp.count == 0) { for (Block& sb : sub.subs) sb.append_empty(); continue; }
                 for (size_t gj = 0; gj < kid.grand.size(); ++gj)
                     append_leaf(p, p->pipes[kid.grand[gj].pipe], kid.grand[gj].leaf, row + tp.ord, sub.subs[gj]);
+                if (kid.deep >= 0) {  // histogram{terms{terms}}: Y's candidates at (slot, X term) in the composite grid
+                    const Pipeline& C0 = p->pipes[kid.dpipes[0]];
+                    if (!C0.allocated) { sub.subs.back().append_empty(); continue; }
+                    require(C0.H == P0.H && C0.key0 == P0.key0, ESGPU_ERR_DEVICE, "sibling pipelines disagree on the key grid");
+                    emit_deep(p, kid, (size_t)s * C0.T + (size_t)tp.ord * C0.vcB, 1, sub.subs.back());
+                }
             }
             end_instance(sub);
         }
