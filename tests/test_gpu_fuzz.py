@@ -176,6 +176,15 @@ class Gen:
                 inner = self.histogram() if kind == "date_histogram" or r.random() < 0.5 else self.date_histogram(affine=True)
             for _ in range(int(r.integers(0, 2))):
                 inner.subAggregation(self.metric()[0])
+            root_t, inner_t = kind == "terms", isinstance(inner, TermsBuilder)
+            if (root_t or inner_t) and self.r2.random() < 0.3:  # a third level: two terms and one histogram
+                r_main, self.r = self.r, self.r2
+                third = self.terms(True) if not (root_t and inner_t) else (
+                    self.date_histogram(affine=True) if self.r2.random() < 0.6 else self.histogram())
+                for _ in range(int(self.r2.integers(0, 2))):
+                    third.subAggregation(self.metric()[0])
+                self.r = r_main
+                inner.subAggregation(third)
             if kind != "terms" and isinstance(inner, TermsBuilder) and r.random() < 0.4:
                 # terms under a histogram: count orders select per row on the GPU, term orders on the host
                 inner.order(Order.count(bool(r.random() < 0.5)) if r.random() < 0.7 else Order.term(bool(r.random() < 0.5)))
