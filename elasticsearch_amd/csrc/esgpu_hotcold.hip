@@ -395,15 +395,15 @@ __global__ __launch_bounds__(kHcCountWG) void hc_count_kernel(HcParams P) {
     if (!pc.whole) {  // one of several pieces of a heavy partition: add the non-zero counters
         for (uint32_t j = threadIdx.x; j < S; j += kHcCountWG) {
             const uint32_t c = get(j);
-            if (c) atomicAdd(&P.counts[base + j], (unsigned long long)c);
+            if (c) atomicAdd(&P.counts[base + j], c);
         }
     } else if (P.overwrite) {
         for (uint32_t j = threadIdx.x; j < S; j += kHcCountWG) P.counts[base + j] = get(j);
     } else {  // later segments: read-modify-write, four counters in flight per thread
         for (uint32_t j = threadIdx.x; j < S; j += 4 * kHcCountWG) {
-            unsigned long long g[4];
+            uint32_t g[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) g[u] = j + u * kHcCountWG < S ? P.counts[base + j + u * kHcCountWG] : 0ull;
+            for (int u = 0; u < 4; ++u) g[u] = j + u * kHcCountWG < S ? P.counts[base + j + u * kHcCountWG] : 0u;
 #pragma unroll
             for (int u = 0; u < 4; ++u)
                 if (j + u * kHcCountWG < S) P.counts[base + j + u * kHcCountWG] = g[u] + get(j + u * kHcCountWG);
@@ -460,7 +460,7 @@ __global__ __launch_bounds__(256) void hc_hot_final_kernel(HcParams P, uint32_t 
     auto add = [&](uint32_t slot, uint32_t t) {
         if (!t || slot >= P.hot_n) return;
         const uint32_t o = P.hot_ord[slot];
-        if (o < P.T) atomicAdd(&P.counts[o], (unsigned long long)t);
+        if (o < P.T) atomicAdd(&P.counts[o], t);
     };
     if (base < 4 * kHcHotCopies) {
         add(base / 4, acc.x + acc.y + acc.z + acc.w);

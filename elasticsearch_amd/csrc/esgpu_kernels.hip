@@ -780,7 +780,8 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(GatherParams P) {
     if (i >= P.k * P.H) return;
     const uint32_t r = i / P.H, h = i - r * P.H;
     const size_t src = (size_t)h * P.T + P.rows[r];
-    for (int a = 0; a < P.narrays; ++a) P.dst[a][i] = P.src[a][src];
+    for (int a = 0; a < P.narrays; ++a)
+        P.dst[a][i] = (a == 0 && P.cnt32) ? (unsigned long long)((const unsigned int*)P.src[0])[src] : P.src[a][src];
 }
 
 // compact_rows, pass 1: non-empty key slots of each winner's row (one workgroup per row)
@@ -875,6 +876,12 @@ void launch_gather_rows(const GatherParams& p, hipStream_t st) {
 
 __global__ void fill_u64_kernel(unsigned long long* p, size_t n, unsigned long long v) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
+}
+__global__ void widen_u32_kernel(const unsigned int* src, size_t n, unsigned long long* dst) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) dst[i] = src[i];
+}
+void launch_widen_u32(const unsigned int* src, size_t n, unsigned long long* dst, hipStream_t st) {
+    if (n) hipLaunchKernelGGL(widen_u32_kernel, dim3((uint32_t)std::min<size_t>(4096, (n + 255) / 256)), dim3(256), 0, st, src, n, dst);
 }
 // global ordinals: out[d] = map[in[d]] (ordinals outside the segment dictionary, incl. missing, stay missing)
 __global__ void remap_ords_kernel(const uint32_t* in, uint32_t n, const uint32_t* map, uint32_t map_n, uint32_t* out) {
@@ -1222,7 +1229,7 @@ __global__ __launch_bounds__(kCountWG) void part_count_kernel(PartParams P) {
             const uint32_t c = cnt[j];
             if (c == 0 || base + j >= P.T) continue;
             if (whole) P.counts[base + j] += c;
-            else atomicAdd(&P.counts[base + j], (unsigned long long)c);
+            else atomicAdd(&P.counts[base + j], c);
         }
         __syncthreads();
     }
@@ -1313,7 +1320,7 @@ __global__ __launch_bounds__(1024) void topk_kernel(TopkParams P, const unsigned
             unsigned long long key = 0;
             if (i < e) {
                 if (FROM_COUNTS) {
-                    const unsigned long long c = src[i];
+                    const unsigned long long c = P.counts32 ? (unsigned long long)P.counts32[i] : src[i];
                     sum += c;
                     const bool eligible = !(P.min_doc_count > 0 && c == 0) && (long long)c >= P.shard_min_doc_count;
                     key = eligible ? make_topk_key(P.order, c, i) : 0ull;
@@ -1371,6 +1378,17 @@ __device__ __forceinline__ void load_counts4(const unsigned long long* c, uint32
     }
 }
 
+__device__ __forceinline__ void load_counts4(const TopkParams& P, uint32_t i, unsigned long long v[4]) {
+    if (!P.counts32) { load_counts4(P.counts, P.T, i, v); return; }
+    if (i + 4 <= P.T) {  // u32 counts: one 16-byte load per 4 ordinals
+        const u32x4_t a = load16(P.counts32 + i);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = i + j < P.T ? P.counts32[i + j] : 0ull;
+    }
+}
+
 __global__ __launch_bounds__(1024) void topk_hist_kernel(TopkParams P) {
     __shared__ uint32_t hist[kTopkBins];
     for (uint32_t i = threadIdx.x; i < kTopkBins; i += 1024) hist[i] = 0;
@@ -1378,7 +1396,7 @@ __global__ __launch_bounds__(1024) void topk_hist_kernel(TopkParams P) {
     unsigned long long sum = 0;
     for (uint32_t i = (blockIdx.x * 1024 + threadIdx.x) * 4; i < P.T; i += gridDim.x * 1024 * 4) {
         unsigned long long c[4];
-        load_counts4(P.counts, P.T, i, c);
+        load_counts4(P, i, c);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             sum += c[j];
@@ -1417,7 +1435,7 @@ __global__ __launch_bounds__(1024) void topk_compact_kernel(TopkParams P) {
     for (uint32_t i0 = blockIdx.x * 1024 * 4; i0 < P.T; i0 += gridDim.x * 1024 * 4) {
         const uint32_t i = i0 + threadIdx.x * 4;
         unsigned long long c[4] = {0, 0, 0, 0};
-        if (i < P.T) load_counts4(P.counts, P.T, i, c);
+        if (i < P.T) load_counts4(P, i, c);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const bool take = i + j < P.T && topk_eligible(P, c[j]) && count_bin(P.order, c[j]) >= tb;

@@ -166,6 +166,7 @@ struct GatherParams {
     int32_t narrays;
     const unsigned long long* src[6];
     unsigned long long* dst[6];
+    int32_t cnt32;   // src[0] holds u32 counts (widened to u64 in dst[0])
 };
 
 // build: the winners' histogram rows compacted on the GPU into the result's columnar arrays (HistogramAggregator
@@ -256,6 +257,7 @@ void launch_murmur3_field(const uint8_t* bytes, const uint64_t* offsets, uint64_
 
 // min / max over a value array (multi-valued i64 columns: key range of a histogram), out[0] = min, out[1] = max
 void launch_minmax_i64(const int64_t* v, uint64_t n, int64_t* out, bool f64, hipStream_t s);
+void launch_widen_u32(const unsigned int* src, size_t n, unsigned long long* dst, hipStream_t st);
 void launch_comp_ords(const uint32_t* a, const uint32_t* b, uint32_t n_pad, uint32_t na, uint32_t nb, uint32_t* out, hipStream_t st);
 void launch_hist_ords(const int64_t* v, const uint64_t* present, uint32_t n_docs, uint32_t n_pad, bool f64, int64_t interval,
                       int64_t offset, int64_t key0, uint32_t nkeys, uint32_t* out, hipStream_t s);
@@ -284,7 +286,7 @@ struct PartParams {
     uint32_t* wg_counts;     // [P][G] docs of partition p seen by workgroup g (pass 1), exclusive offsets after the scan
     uint32_t* part_begin;    // [P + 1] start of each partition in pbuf
     uint16_t* pbuf;          // partitioned ordinals as partition-local offsets (ord & (2^shift - 1))
-    unsigned long long* counts;  // [T] output doc counts
+    unsigned int* counts;    // [T] output doc counts, u32 (BucketsAggregator's IntArray; max_doc < 2^31)
     uint32_t chunk;          // partitioned elements per counting workgroup
     uint32_t* tile_sums;     // scratch of the scan: part_scan_tiles(P * G) entries
 };
@@ -334,7 +336,7 @@ struct HcParams {
     uint32_t* hot_slab;                // [G][hc_hot_counters(hot_n)] per-workgroup hot counters
     uint16_t* pbuf;                    // partition-local offsets (ord & 32767); 0xFFFF = unused overflow element
     uint32_t trash;                    // kHcTile spare elements at the end of pbuf (capacity violation sink)
-    unsigned long long* counts;        // [T]
+    unsigned int* counts;              // [T] u32 doc counts (IntArray: a shard's max_doc is below 2^31)
     uint32_t* err;                     // set to 1 on a capacity violation (device-visible host word)
     int32_t u16_counters;              // every cold ordinal's count in the segment < 65536: packed LDS counters
     int32_t overwrite;                 // store the counts instead of adding (the plan's first segment)
@@ -361,6 +363,7 @@ void launch_hc_recode(const uint32_t* ord, uint32_t n, const uint32_t* keys, con
 // ---- GPU top-k over a count vector (BucketPriorityQueue replacement for large T) ----
 struct TopkParams {
     const unsigned long long* counts;
+    const unsigned int* counts32;  // non-null: u32 counts (the partitioned / hot-cold paths), read instead of counts
     uint32_t T;
     int32_t order;           // ESGPU_ORDER_COUNT_DESC / COUNT_ASC / TERM_ASC / TERM_DESC
     int64_t min_doc_count, shard_min_doc_count;

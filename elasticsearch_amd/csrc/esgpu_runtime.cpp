@@ -856,6 +856,7 @@ struct Pipeline {
     std::shared_ptr<const TermDict> tdict2;  // inner terms: the dictionary its keys resolve through
     // three bucket levels (two terms and one histogram): the ordinal dimension is the pair of the two terms fields,
     // ord = a * vcB + b (ord_field = a's field, ord_field2 = b's), derived per segment into ord_col
+    bool cnt32 = false;              // g_cnt holds u32 counts (written by the partitioned / hot-cold terms paths)
     bool comp = false;
     int comp_spec2 = -1;
     std::string ord_field2;
@@ -1578,7 +1579,8 @@ static bool collect_partitioned(esgpu_plan* p, Pipeline& pl, const esgpu_segment
     require(ntiles <= 4096, ESGPU_ERR_INVALID, "partition scan too large");
     Q.tile_sums = (uint32_t*)p->s_tiles.ensure(c, (size_t)ntiles * 4);
     Q.pbuf = (uint16_t*)p->s_pbuf.ensure(c, (std::max<size_t>(s->max_doc, 1) + 8) * 2);
-    Q.counts = pl.g_cnt.as<unsigned long long>();
+    Q.counts = pl.g_cnt.as<unsigned int>();
+    pl.cnt32 = true;
     // counting workgroups (one resident per CU at 128 KB of LDS counters); each covers `chunk` partitioned elements
     // (a multiple of 8: 16-byte loads).  Every partition piece a workgroup counts ends in a flush of its 32768
     // counters (256 KB of global adds), so the workgroup count is capped at one per 512K elements -- the flushes stay
@@ -1644,7 +1646,7 @@ static uint32_t hc_hash_host(uint32_t o, uint32_t log2) { return (uint32_t)(o * 
 // doc count of every ordinal of a column (no filters), by the radix-partitioned passes (collect_partitioned's kernels)
 static void count_all_ordinals(esgpu_ctx* c, const uint32_t* ord, uint32_t max_doc, uint32_t n_pad, uint32_t T,
                                DevBuf& counts, hipStream_t st) {
-    counts.alloc(c, (size_t)std::max<uint32_t>(T, 1) * 8);
+    counts.alloc(c, (size_t)std::max<uint32_t>(T, 1) * 4);
     HIPX(hipMemsetAsync(counts.p, 0, counts.bytes, st));
     if (max_doc == 0) return;
     PartParams Q{};
@@ -1668,7 +1670,7 @@ static void count_all_ordinals(esgpu_ctx* c, const uint32_t* ord, uint32_t max_d
     Q.part_begin = pbeg.as<uint32_t>();
     Q.tile_sums = tiles.as<uint32_t>();
     Q.pbuf = pbuf.as<uint16_t>();
-    Q.counts = counts.as<unsigned long long>();
+    Q.counts = counts.as<unsigned int>();
     const uint64_t want = std::min<uint64_t>((uint64_t)c->cus * 4, std::max<uint64_t>((uint64_t)c->cus, (uint64_t)max_doc >> 19));
     Q.chunk = (uint32_t)std::max<uint64_t>(1u << 16, (((uint64_t)max_doc + want - 1) / want + 7) & ~7ull);
     launch_part_hist(Q, st);
@@ -1706,7 +1708,9 @@ static std::shared_ptr<const HcStats> ensure_hc_stats(esgpu_ctx* c, const DevCol
     {
         DevBuf d;
         count_all_ordinals(c, (const uint32_t*)src, s->max_doc, s->n_pad, T, d, st);
-        HIPX(hipMemcpy(cnt.data(), d.p, (size_t)T * 8, hipMemcpyDeviceToHost));
+        std::vector<uint32_t> c32(T);
+        HIPX(hipMemcpy(c32.data(), d.p, (size_t)T * 4, hipMemcpyDeviceToHost));
+        for (uint32_t o = 0; o < T; ++o) cnt[o] = c32[o];
     }
     uint64_t total = 0;
     for (uint64_t v : cnt) total += v;
@@ -1925,7 +1929,8 @@ static bool collect_hotcold(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s,
     H.hot_slab = H.hot_n ? (uint32_t*)p->s_hslab.ensure(c, (size_t)hc_slab_stride(H.hot_n) * H.G * 4) : nullptr;
     H.pbuf = (uint16_t*)p->s_pbuf.ensure(c, hs->pbuf_elems * 2);
     H.trash = hs->trash;
-    H.counts = pl.g_cnt.as<unsigned long long>();
+    H.counts = pl.g_cnt.as<unsigned int>();
+    pl.cnt32 = true;
     if (!p->h_hcerr.bytes) {  // zeroed once here and after each check: overruns of every segment accumulate
         p->h_hcerr.ensure(8);
         *p->h_hcerr.as<volatile uint32_t>() = 0;
@@ -3148,6 +3153,7 @@ static void fetch_rows(esgpu_plan* p, Pipeline& pl, const uint32_t* drows, uint3
     GatherParams G{};
     G.rows = drows;
     G.k = k; G.H = pl.H; G.T = pl.T;
+    G.cnt32 = pl.cnt32 ? 1 : 0;
     const size_t bytes = std::max<size_t>((size_t)k * pl.H, 1) * 8;
     for (int a = 0; a < 6; ++a) {
         if (!src[a]) continue;
@@ -3167,6 +3173,12 @@ static void fetch_grid(esgpu_plan* p, Pipeline& pl) {
     const void* src[6];
     grid_arrays(pl, src);
     const size_t cells = (size_t)pl.T * pl.H;
+    if (pl.cnt32) {  // u32 counts widened on the device first
+        unsigned long long* w = (unsigned long long*)p->s_tcnt.ensure(p->ctx, std::max<size_t>(cells, 1) * 8);
+        launch_widen_u32(pl.g_cnt.as<unsigned int>(), cells, w, p->stream);
+        HIPX(hipGetLastError());
+        src[0] = w;
+    }
     for (int a = 0; a < 6; ++a)
         if (src[a]) d2h_u64(p, pl.h_cells[a], src[a], cells);
     point_cells(pl, src);
@@ -3353,11 +3365,18 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
     const uint64_t k_req = std::min<uint64_t>(P0.value_count, (uint64_t)std::max(tn.s.shard_size, 0));
     const bool count_order = tn.s.order == ESGPU_ORDER_COUNT_DESC || tn.s.order == ESGPU_ORDER_COUNT_ASC;
     const bool gpu_topk = !agg_order && P0.value_count > 65536 && k_req <= kTopkMax && (P0.H == 1 || count_order);
+    if (P0.cnt32 && !gpu_topk) {  // u32 counts (partitioned / hot-cold paths) widened for the host selection
+        unsigned long long* w = (unsigned long long*)p->s_tcnt.ensure(p->ctx, (size_t)T * 8);
+        launch_widen_u32(P0.g_cnt.as<unsigned int>(), T, w, st);
+        HIPX(hipGetLastError());
+        dcnt = w;
+    }
     if (gpu_topk) {
         // K3 on the GPU: only the k winners (and the count total) cross PCIe
         const uint32_t kk = (uint32_t)std::max<uint64_t>(k_req, 1);
         TopkParams K{};
         K.counts = dcnt;
+        K.counts32 = P0.cnt32 ? P0.g_cnt.as<unsigned int>() : nullptr;  // the top-k reads 4 B per ordinal
         K.T = (uint32_t)P0.value_count;
         K.order = tn.s.order;
         K.min_doc_count = tn.s.min_doc_count;

@@ -69,6 +69,18 @@ for s in $STEPS; do
                   --steps 4 --warmup 2 ;;
         prof) cd /tmp && run rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
                   python3 "$R/bench.py" --steps 10 --warmup 3 --cpu-docs 0 --inflight 1 ;;
+        c3) # config 3 at 125M docs: clean (postings form) and with 1 % deletions (scatter form), kernel and bench line
+              run kbench_c3_125m 300 python3 "$R/tools/kbench.py" --docs 125000000 --reps 5 --only config3_url &&
+              run kbench_c3_125m_del 300 python3 "$R/tools/kbench.py" --docs 125000000 --reps 5 --only config3_url --deletes 0.01 &&
+              run bench_config3 300 python3 "$R/bench.py" --workload config3 --shards 8 --docs 125000000 --cpu-docs 0 ;;
+        inflightab) # requests in flight: 2 / 3 / 4 (north star 1 x 1B and 8 x 125M)
+              for d in 2 3 4; do
+                  run "bench_if$d" 300 python3 "$R/bench.py" --inflight $d --cpu-docs 0 || exit 1
+                  run "bench_ns8_if$d" 300 python3 "$R/bench.py" --inflight $d --shards 8 --docs 125000000 --cpu-docs 0 || exit 1
+              done ;;
+        proftl) # kernel timeline of the default bench (2 requests in flight): GPU idle gaps between collect launches
+              cd /tmp && run rocprof_timeline 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/proftl" -o bench -- \
+                  python3 "$R/bench.py" --steps 10 --warmup 3 --cpu-docs 0 ;;
         profk) cd /tmp && run rocprof_kbench 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profk" -o kbench -- \
                    python3 "$R/tools/kbench.py" --docs 1000000000 --reps 3 ;;
         profk125) cd /tmp && run rocprof_kbench125 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profk125" -o kb125 -- \
