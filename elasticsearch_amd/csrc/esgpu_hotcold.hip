@@ -495,6 +495,8 @@ void launch_hotcold(const HcParams& p, hipStream_t s) {
 // more in the reduce than the extra waves gain).
 constexpr int kHotWG = 512;
 constexpr uint32_t kHotTileDocs = kHotWG * kHcIt * 4;
+// ACC: an accept bitset (live docs) -- its word loaded beside each 16-byte column load and tested at counting time
+template <bool ACC>
 __global__ __launch_bounds__(kHotWG) void hc_hot_kernel(HcParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t* hot = (uint32_t*)smem;
@@ -509,23 +511,25 @@ __global__ __launch_bounds__(kHotWG) void hc_hot_kernel(HcParams P) {
     const uint32_t span = b_end > b_begin ? (b_end - b_begin) * kBlockDocs : 0u;
     const uint32_t d_last = P.n_blocks * kBlockDocs - 4;
     const uint32_t tid4 = threadIdx.x * 4;
-    auto load = [&](uint32_t t0, uint32_t o[kHcIt][4]) {
+    auto load = [&](uint32_t t0, uint32_t o[kHcIt][4], uint64_t aw[kHcIt]) {
 #pragma unroll
         for (int k = 0; k < kHcIt; ++k) {
             const uint32_t d = min(t0 + k * (kHotWG * 4) + tid4, d_last);
             const u32x4_t a = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(P.rc + d));
             o[k][0] = a.x; o[k][1] = a.y; o[k][2] = a.z; o[k][3] = a.w;
+            if (ACC) aw[k] = P.accept[d >> 6];  // the raw word: shifted only when counted (no early wait on it)
         }
     };
-    auto count = [&](uint32_t t0, const uint32_t o[kHcIt][4]) {
+    auto count = [&](uint32_t t0, const uint32_t o[kHcIt][4], const uint64_t aw[kHcIt]) {
         if (t0 >= d_begin + span) return;
 #pragma unroll
         for (int k = 0; k < kHcIt; ++k) {
             const uint32_t doc0 = t0 + k * (kHotWG * 4) + tid4;
+            const uint32_t live = ACC ? (uint32_t)(aw[k] >> (doc0 & 63)) & 0xFu : 0xFu;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const uint32_t v = o[k][j];
-                if ((v & kHcHotBit) && v != kMissingOrd && doc0 + j < d_end) {
+                if ((v & kHcHotBit) && v != kMissingOrd && doc0 + j < d_end && ((live >> j) & 1u)) {
                     const uint32_t sl = v & ~kHcHotBit;
                     atomicAdd(&hot[sl < kHcHotCopies ? 4 * sl + (threadIdx.x & 3) : 3 * kHcHotCopies + sl], 1u);
                 }
@@ -534,18 +538,19 @@ __global__ __launch_bounds__(kHotWG) void hc_hot_kernel(HcParams P) {
     };
     if (span) {
         uint32_t A[kHcIt][4], B[kHcIt][4], C[kHcIt][4];
-        load(d_begin, A);
+        uint64_t Aw[kHcIt], Bw[kHcIt], Cw[kHcIt];
+        load(d_begin, A, Aw);
         __builtin_amdgcn_sched_barrier(0);
-        load(d_begin + kHotTileDocs, B);
+        load(d_begin + kHotTileDocs, B, Bw);
         __builtin_amdgcn_sched_barrier(0);
-        load(d_begin + 2 * kHotTileDocs, C);
+        load(d_begin + 2 * kHotTileDocs, C, Cw);
         for (uint32_t t0 = d_begin; t0 < d_begin + span; t0 += 3 * kHotTileDocs) {
-            count(t0, A);
-            load(t0 + 3 * kHotTileDocs, A);
-            count(t0 + kHotTileDocs, B);
-            load(t0 + 4 * kHotTileDocs, B);
-            count(t0 + 2 * kHotTileDocs, C);
-            load(t0 + 5 * kHotTileDocs, C);
+            count(t0, A, Aw);
+            load(t0 + 3 * kHotTileDocs, A, Aw);
+            count(t0 + kHotTileDocs, B, Bw);
+            load(t0 + 4 * kHotTileDocs, B, Bw);
+            count(t0 + 2 * kHotTileDocs, C, Cw);
+            load(t0 + 5 * kHotTileDocs, C, Cw);
         }
     }
     __syncthreads();
@@ -564,15 +569,40 @@ void launch_hc_pad(const uint16_t* dense, const uint32_t* dense_begin, const uin
     if (P) hipLaunchKernelGGL(hc_pad_kernel, dim3(P), dim3(256), 0, s, dense, dense_begin, pad_begin, out);
 }
 
+// live docs under the postings form: the cold lists hold every doc of the segment, so the cold docs the accept bitset
+// clears are taken back out -- each dead doc's recoded value read, a cold one's counter decremented (one scattered
+// atomic per dead cold doc: cheap while deletions are few, the hot ones were never counted)
+__global__ __launch_bounds__(256) void hc_cold_sub_kernel(const uint32_t* rc, const uint64_t* accept, uint32_t n_docs, uint32_t T,
+                                                          unsigned int* counts) {
+    const uint32_t nw = (n_docs + 63) / 64;
+    for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += gridDim.x * blockDim.x) {
+        uint64_t dead = ~accept[w];
+        if (w == nw - 1 && (n_docs & 63)) dead &= (1ull << (n_docs & 63)) - 1ull;
+        while (dead) {
+            const uint32_t d = w * 64 + (uint32_t)__builtin_ctzll(dead);
+            dead &= dead - 1ull;
+            const uint32_t v = rc[d];
+            if (!(v & kHcHotBit) && v < T) atomicSub(&counts[v], 1u);
+        }
+    }
+}
+
 void launch_hotcold_postings(const HcParams& hot, const HcParams& cold, hipStream_t s) {
-    if (hot.hot_n)
-        hipLaunchKernelGGL(hc_hot_kernel, dim3(hot.G), dim3(kHotWG), (size_t)hc_hot_counters(hot.hot_n) * 4, s, hot);
+    if (hot.hot_n && hot.accept)
+        hipLaunchKernelGGL(hc_hot_kernel<true>, dim3(hot.G), dim3(kHotWG), (size_t)hc_hot_counters(hot.hot_n) * 4, s, hot);
+    else if (hot.hot_n)
+        hipLaunchKernelGGL(hc_hot_kernel<false>, dim3(hot.G), dim3(kHotWG), (size_t)hc_hot_counters(hot.hot_n) * 4, s, hot);
     if (cold.n_pieces) {  // the cold lists never use overflow chunks: their cursors were set once (HcStats)
         const size_t clds = (cold.u16_counters ? (1u << kPartShift) / 2 : (1u << kPartShift)) * 4 + (size_t)cold.G * 4;
         if (cold.u16_counters) hipLaunchKernelGGL(hc_count_kernel<true>, dim3(cold.n_pieces), dim3(kHcCountWG), clds, s, cold);
         else hipLaunchKernelGGL(hc_count_kernel<false>, dim3(cold.n_pieces), dim3(kHcCountWG), clds, s, cold);
     }
     if (hot.hot_n) launch_hot_reduce(hot, s);
+    if (hot.accept) {
+        const uint32_t nw = (hot.n_docs + 63) / 64;
+        hipLaunchKernelGGL(hc_cold_sub_kernel, dim3(std::max(1u, std::min(4096u, (nw + 255) / 256))), dim3(256), 0, s, hot.rc,
+                           hot.accept, hot.n_docs, hot.T, hot.counts);
+    }
 }
 
 }  // namespace esgpu

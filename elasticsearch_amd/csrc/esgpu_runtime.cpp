@@ -953,6 +953,7 @@ struct esgpu_plan {
     PinnedBuf h_tcnt, h_rows, h_dst[6];
     Scratch s_nnz;                     // build: non-empty slots per winner row (compact_rows)
     Scratch s_drows;                   // build: composite ordinals a three-level child reads (fetch_rows)
+    bool sparse_dead = false;          // the current segment's accept bitset clears few docs (host sample, <= 10 %)
     Scratch s_xbits;                   // doc bitset of a pipeline with more than kMaxPreds clauses
     uint32_t seg_seq = 0;              // segments collected since create / reset (cardinality insertion order)
     std::vector<PinnedBuf> h_compact;  // build: per bucket child, its GPU-compacted buckets and leaves (pinned)
@@ -1939,8 +1940,12 @@ static bool collect_hotcold(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s,
     p->hc_check = true;
     H.u16_counters = hs->u16 ? 1 : 0;
     H.overwrite = first_segment ? 1 : 0;  // every counter is stored by the counting pass: no read of the zeroed grid
-    if (hs->cold_lists && npred == 0 && !d_accept) {  // every doc counts: hot slots from the column, cold lists
+    // every doc counts (or all but a few: a live-docs bitset with few deletions, sampled on the host at collect) -- hot
+    // slots from the column (testing the accept bits), the cold lists, then the dead cold docs taken back out
+    const bool live_docs_only = d_accept && d_accept == (const uint64_t*)p->s_accept.buf.p && p->sparse_dead;
+    if (hs->cold_lists && npred == 0 && (!d_accept || live_docs_only)) {
         HcParams K = H;                                 // the cold lists: one static region per partition
+        K.accept = nullptr;
         K.G = 1;
         K.part = hs->d_cold_part.as<HcPart>();
         K.piece = hs->d_cold_piece.as<HcPiece>();
@@ -2750,8 +2755,15 @@ extern "C" int esgpu_plan_collect_segment(esgpu_plan* p, const esgpu_segment* s,
         require(s->ctx == p->ctx, ESGPU_ERR_INVALID, "segment belongs to another device context");
         HIPX(hipSetDevice(p->ctx->device));
         const uint64_t* d_accept = nullptr;
+        p->sparse_dead = false;
         if (accept_bits) {
             const size_t words = std::max<size_t>(s->n_pad / 64, 1);
+            {  // how many docs the bitset clears, from up to 1,024 evenly spaced words (picks the hot/cold form)
+                const size_t nw = ((size_t)s->max_doc + 63) / 64, step = std::max<size_t>(1, nw / 1024);
+                uint64_t dead = 0, seen = 0;
+                for (size_t w = 0; w + 1 < nw; w += step, seen += 64) dead += 64 - __builtin_popcountll(accept_bits[w]);
+                p->sparse_dead = seen == 0 || dead * 10 <= seen;
+            }
             void* a = p->s_accept.ensure(p->ctx, words * 8);
             HIPX(hipMemsetAsync(a, 0, words * 8, p->stream));
             HIPX(hipMemcpyAsync(a, accept_bits, ((size_t)s->max_doc + 63) / 64 * 8, hipMemcpyHostToDevice, p->stream));
