@@ -162,6 +162,7 @@ SIGNATURES = [
                                                      ctypes.POINTER(ctypes.c_int32)]),
     ("esgpu_plan_last_build_stats", ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     ("esgpu_plan_shard_mergeable", ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_int32)]),
+    ("esgpu_plan_deferred_segments", ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_int32)]),
     ("esgpu_result_free", ctypes.c_int, [ctypes.POINTER(Result)]),
     ("esgpu_reduce", ctypes.c_int, [ctypes.POINTER(ctypes.POINTER(Result)), ctypes.c_int32,
                                     ctypes.POINTER(ctypes.POINTER(Result))]),

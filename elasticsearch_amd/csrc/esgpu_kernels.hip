@@ -2005,12 +2005,18 @@ void launch_hist_ords(const int64_t* v, const uint64_t* present, uint32_t n_docs
 
 // three bucket levels: the pair of two single-valued ordinal columns as one composite ordinal a * nb + b (missing when
 // either is missing or out of its dictionary); 16-byte loads and stores, n_pad is a multiple of kBlockDocs
+// composite ordinals a * nb + b (missing when either is); with `amap`, a is first mapped through it (breadth-first
+// replay: the outer ordinal's winner slot, kMissingOrd for the ordinals that did not survive)
 __global__ __launch_bounds__(256) void comp_ords_kernel(const uint32_t* a, const uint32_t* b, uint32_t n_pad, uint32_t na,
-                                                        uint32_t nb, uint32_t* out) {
+                                                        uint32_t nb, const uint32_t* amap, uint32_t amap_n, uint32_t* out) {
     for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n_pad; i += gridDim.x * blockDim.x * 4) {
         uint32_t x[4], y[4];
         load_u32x4(a, i, x);
         load_u32x4(b, i, y);
+        if (amap) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x[j] = x[j] < amap_n ? amap[x[j]] : kMissingOrd;
+        }
         u32x4_t o;
         o.x = x[0] < na && y[0] < nb ? x[0] * nb + y[0] : kMissingOrd;
         o.y = x[1] < na && y[1] < nb ? x[1] * nb + y[1] : kMissingOrd;
@@ -2019,10 +2025,11 @@ __global__ __launch_bounds__(256) void comp_ords_kernel(const uint32_t* a, const
         *reinterpret_cast<u32x4_t*>(out + i) = o;
     }
 }
-void launch_comp_ords(const uint32_t* a, const uint32_t* b, uint32_t n_pad, uint32_t na, uint32_t nb, uint32_t* out, hipStream_t st) {
+void launch_comp_ords(const uint32_t* a, const uint32_t* b, uint32_t n_pad, uint32_t na, uint32_t nb, const uint32_t* amap,
+                      uint32_t amap_n, uint32_t* out, hipStream_t st) {
     if (n_pad == 0) return;
     hipLaunchKernelGGL(comp_ords_kernel, dim3(std::min<uint32_t>(8192, (n_pad / 4 + 255) / 256)), dim3(256), 0, st, a, b, n_pad,
-                       na, nb, out);
+                       na, nb, amap, amap_n, out);
 }
 
 void launch_minmax_i64(const int64_t* v, uint64_t n, int64_t* out, bool f64, hipStream_t st) {

@@ -258,7 +258,8 @@ void launch_murmur3_field(const uint8_t* bytes, const uint64_t* offsets, uint64_
 // min / max over a value array (multi-valued i64 columns: key range of a histogram), out[0] = min, out[1] = max
 void launch_minmax_i64(const int64_t* v, uint64_t n, int64_t* out, bool f64, hipStream_t s);
 void launch_widen_u32(const unsigned int* src, size_t n, unsigned long long* dst, hipStream_t st);
-void launch_comp_ords(const uint32_t* a, const uint32_t* b, uint32_t n_pad, uint32_t na, uint32_t nb, uint32_t* out, hipStream_t st);
+void launch_comp_ords(const uint32_t* a, const uint32_t* b, uint32_t n_pad, uint32_t na, uint32_t nb, const uint32_t* amap,
+                      uint32_t amap_n, uint32_t* out, hipStream_t st);
 void launch_hist_ords(const int64_t* v, const uint64_t* present, uint32_t n_docs, uint32_t n_pad, bool f64, int64_t interval,
                       int64_t offset, int64_t key0, uint32_t nkeys, uint32_t* out, hipStream_t s);
 void launch_remap_ords(const uint32_t* in, uint32_t n, const uint32_t* map, uint32_t map_n, uint32_t* out, hipStream_t s);

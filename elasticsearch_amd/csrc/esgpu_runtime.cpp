@@ -285,6 +285,10 @@ struct esgpu_segment {
     esgpu_ctx* ctx = nullptr;
     uint32_t max_doc = 0;
     uint32_t n_pad = 0;
+    // plans that will read the segment again at build (breadth-first replay, the way BestBucketsDeferringCollector keeps
+    // each LeafReaderContext until prepareSelectedBuckets): a destroy while pinned is carried out at the last unpin
+    int pins = 0;
+    bool doomed = false;
     std::map<std::string, std::unique_ptr<DevColumn>> cols;
     const DevColumn* col(const char* name) const {
         if (!name) return nullptr;
@@ -505,8 +509,30 @@ extern "C" int esgpu_segment_synthetic(esgpu_ctx* c, uint64_t seed, uint32_t sha
     });
 }
 
+static std::mutex g_pin_mu;
+static void pin_segment(const esgpu_segment* cs) {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    ++const_cast<esgpu_segment*>(cs)->pins;
+}
+static void unpin_segment(const esgpu_segment* cs) {
+    esgpu_segment* s = const_cast<esgpu_segment*>(cs);
+    bool drop = false;
+    {
+        std::lock_guard<std::mutex> lk(g_pin_mu);
+        drop = --s->pins == 0 && s->doomed;
+    }
+    if (drop) delete s;
+}
+
 extern "C" int esgpu_segment_destroy(esgpu_segment* s) {
-    return guarded([&] { delete s; });
+    return guarded([&] {
+        if (!s) return;
+        {
+            std::lock_guard<std::mutex> lk(g_pin_mu);
+            if (s->pins > 0) { s->doomed = true; return; }
+        }
+        delete s;
+    });
 }
 
 extern "C" int esgpu_segment_max_doc(const esgpu_segment* s, uint32_t* max_doc) {
@@ -859,6 +885,12 @@ struct Pipeline {
     bool cnt32 = false;              // g_cnt holds u32 counts (written by the partitioned / hot-cold terms paths)
     bool comp = false;
     int comp_spec2 = -1;
+    // terms under terms whose [outer x inner] grid is over the dense budget (ESGPU_DEFER_CELLS, default 2^31 cells):
+    // `deferred` -- this inner-terms pipeline counts only the outer doc counts while collecting, and its bucket child is
+    // collected again at build over the surviving outer buckets (TermsAggregator's breadth_first mode,
+    // BestBucketsDeferringCollector.prepareSelectedBuckets) by the companion `replay` pipelines: a composite grid over
+    // (winner slot, inner ordinal), ord = slot * vcB + b, derived per retained segment through `slot_map`
+    bool can_defer = false, deferred = false, replay = false;
     std::string ord_field2;
     std::shared_ptr<const TermDict> tdictB;
     uint64_t vcA = 0, vcB = 0;
@@ -912,6 +944,9 @@ struct ChildSrc {
     int deep = -1, deep_shape = 0;
     std::vector<int> dpipes;
     std::vector<LeafRef> dgrand;
+    // terms under terms: the breadth-first replay pipelines (parallel to pipes) and the leaves' refs into them
+    std::vector<int> rpipes;
+    std::vector<LeafRef> rgrand;
 };
 struct Group {
     int root = -1, fspec = -1;
@@ -957,6 +992,20 @@ struct esgpu_plan {
     Scratch s_xbits;                   // doc bitset of a pipeline with more than kMaxPreds clauses
     uint32_t seg_seq = 0;              // segments collected since create / reset (cardinality insertion order)
     std::vector<PinnedBuf> h_compact;  // build: per bucket child, its GPU-compacted buckets and leaves (pinned)
+    // breadth-first replay: the segments collected while a pipeline was deferred (pinned until reset / destroy) with a
+    // device copy of each one's accept bits, and the outer ordinal -> winner slot map of the replay being run
+    struct DeferredSeg { const esgpu_segment* s; int accept; };
+    std::vector<DeferredSeg> dsegs;
+    std::vector<DevBuf> d_daccept;
+    Scratch s_slotmap;
+    const uint32_t* slot_map = nullptr;
+    uint32_t slot_map_n = 0, slot_k = 0;
+    Scratch s_rkeys;                   // replay: per winner, the GPU top-k's keys and row total
+    PinnedBuf h_rkeys;
+    void unpin_all() {
+        for (const DeferredSeg& d : dsegs) unpin_segment(d.s);
+        dsegs.clear();
+    }
 };
 
 static int metric_level(int t) { return t == ESGPU_AGG_AVG ? 1 : t == ESGPU_AGG_STATS ? 2 : 3; }
@@ -1152,6 +1201,22 @@ static Group compile_group(esgpu_plan* p, int r, int fspec) {
                     D.ord_field2 = p->specs[D.comp_spec2].field;
                     g.pipes.push_back(pi);
                 }
+            }
+            // terms under terms with numeric-metric leaves: replay pipelines for a grid over the dense budget
+            // (collected at build over the surviving outer buckets only; not in g.pipes, so never collected per segment)
+            bool defer_ok = root.s.type == ESGPU_AGG_TERMS && p->specs[ch].s.type == ESGPU_AGG_TERMS && cs.deep < 0;
+            for (int m : inner_leaves) defer_ok = defer_ok && is_metric(p->specs[m].s.type);
+            if (defer_ok) {
+                cs.rpipes = add_leaf_pipelines(p, r, fspec, ch, -1, inner_leaves, &cs.rgrand);
+                for (int pi : cs.rpipes) {
+                    Pipeline& R = p->pipes[pi];
+                    R.comp = true;
+                    R.replay = true;
+                    R.comp_spec2 = ch;
+                    R.ord_field = p->specs[r].field;
+                    R.ord_field2 = p->specs[ch].field;
+                }
+                for (int pi : cs.pipes) p->pipes[pi].can_defer = true;
             }
         }
         g.kids.push_back(std::move(cs));
@@ -2117,6 +2182,10 @@ static const DevColumn* derive_hist_ords(esgpu_plan* p, Pipeline& pl, const esgp
 // three bucket levels: this segment's composite ordinals of the two terms fields (a * vcB + b) as pl.ord_col, or null
 // when the segment lacks either field (its docs then fall in no bucket of the deepest level; the levels above count them
 // through their own pipelines).  Both fields single-valued keyword fields numbered by the request's dictionaries.
+// replay grids: each winner's row of inner ordinals padded to a multiple of 4 cells (16-byte aligned row starts for the
+// top-k's vector loads)
+static uint64_t replay_stride(uint64_t vcB) { return (std::max<uint64_t>(vcB, 1) + 3) & ~3ull; }
+
 static const DevColumn* derive_comp_ords(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s) {
     const DevColumn* a = s->col(pl.ord_field.c_str());
     const DevColumn* b = s->col(pl.ord_field2.c_str());
@@ -2127,14 +2196,14 @@ static const DevColumn* derive_comp_ords(esgpu_plan* p, Pipeline& pl, const esgp
     if (pl.fresh || !pl.tdict) {
         pl.tdict = a->ord_dict();
         pl.tdictB = b->ord_dict();
-        pl.vcA = a->ord_count();
+        pl.vcA = pl.replay ? p->slot_k : a->ord_count();  // replay: the surviving outer buckets' slots
         pl.vcB = b->ord_count();
     } else {
         require(same_dict(a->ord_dict(), pl.tdict) && same_dict(b->ord_dict(), pl.tdictB), ESGPU_ERR_INVALID,
                 "segments number the terms of [" + pl.ord_field + "] or [" + pl.ord_field2 + "] differently: build an "
                 "ordinal map (esgpu_ordinal_map_build) over the reader's segments first");
     }
-    const uint64_t na = std::max<uint64_t>(pl.vcA, 1), nb = std::max<uint64_t>(pl.vcB, 1);
+    const uint64_t na = std::max<uint64_t>(pl.vcA, 1), nb = pl.replay ? replay_stride(pl.vcB) : std::max<uint64_t>(pl.vcB, 1);
     require(na * nb < 0xFFFFFFFFull, ESGPU_ERR_UNSUPPORTED, "three bucket levels over more than 2^32 term pairs");
     if (!pl.ord_col) pl.ord_col = std::make_shared<DevColumn>();
     DevColumn& d = *pl.ord_col;
@@ -2143,8 +2212,9 @@ static const DevColumn* derive_comp_ords(esgpu_plan* p, Pipeline& pl, const esgp
     d.multi = false;
     d.value_count = na * nb;
     if (d.values.bytes < (size_t)s->n_pad * 4) d.values.alloc(p->ctx, (size_t)s->n_pad * 4);
-    launch_comp_ords(a->ords().as<uint32_t>(), b->ords().as<uint32_t>(), (uint32_t)s->n_pad, (uint32_t)pl.vcA,
-                     (uint32_t)pl.vcB, d.values.as<uint32_t>(), p->stream);
+    require(!pl.replay || p->slot_map, ESGPU_ERR_STATE, "replay outside a build");
+    launch_comp_ords(a->ords().as<uint32_t>(), b->ords().as<uint32_t>(), (uint32_t)s->n_pad, (uint32_t)pl.vcA, (uint32_t)nb,
+                     pl.replay ? p->slot_map : nullptr, p->slot_map_n, d.values.as<uint32_t>(), p->stream);
     HIPX(hipGetLastError());
     return &d;
 }
@@ -2290,6 +2360,14 @@ static constexpr uint32_t kTermsCopies = ESGPU_TERMS_COPIES;
 #define ESGPU_COMPACT_ROWS 1  // build: histogram children of terms compacted on the GPU (0: host assembly, for A/B)
 #endif
 
+// cells of a terms-under-terms grid above which the inner buckets are collected breadth-first (ESGPU_DEFER_CELLS
+// overrides: tests force the replay on small grids)
+static uint64_t defer_cells() {
+    const char* e = std::getenv("ESGPU_DEFER_CELLS");
+    if (e && *e) return std::strtoull(e, nullptr, 10);
+    return 1ull << 31;
+}
+
 static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const uint64_t* d_accept) {
     const bool ORD = pl.term_spec >= 0, HIST = pl.hist_spec >= 0;
     const DevColumn* oc = !ORD ? nullptr : pl.ord_hist ? derive_hist_ords(p, pl, s, false)
@@ -2298,10 +2376,28 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     const DevColumn* hc = HIST ? s->col(pl.hist_field.c_str()) : nullptr;
     const DevColumn* mc = pl.met > 0 ? s->col(pl.metric_field.c_str()) : nullptr;
     const bool terms_outer = pl.outer == pl.term_spec;
+    if (pl.inner_terms && pl.fresh) pl.deferred = false;
+    if (pl.inner_terms && pl.can_defer && pl.fresh && oc && hc && oc->type == ESGPU_COL_ORD_U32 && hc->type == ESGPU_COL_ORD_U32 &&
+        !oc->multi && !hc->multi) {
+        // terms under terms over the dense budget: breadth-first (TermsAggregator.shouldDefer / BestBucketsDeferringCollector)
+        // -- the outer doc counts now, the inner buckets replayed at build for the outer winners; the replay grid (winners x
+        // inner ordinals) must fit, and an inner order by a metric selects on the host (rows of at most 65,536 terms)
+        const uint64_t T = std::max<uint64_t>(oc->ord_count(), 1), H = std::max<uint64_t>(hc->ord_count(), 1);
+        const SpecNode& to = p->specs[pl.outer];
+        const SpecNode& ti = p->specs[pl.hist_spec];
+        const uint64_t W = std::max<uint64_t>(1, std::min<uint64_t>(T, (uint64_t)std::max<int64_t>(to.s.shard_size, 0)));
+        const bool agg2 = ti.s.order == ESGPU_ORDER_AGG_ASC || ti.s.order == ESGPU_ORDER_AGG_DESC;
+        pl.deferred = T * H > defer_cells() && W * replay_stride(H) <= (1ull << 31) && (!agg2 || H <= 65536) &&
+                      (agg2 || H <= 65536 || (uint64_t)std::max<int64_t>(ti.s.shard_size, 1) <= kTopkMax);
+    }
+    if (pl.deferred && oc) {
+        require(!oc->multi && !(hc && hc->multi), ESGPU_ERR_UNSUPPORTED,
+                "a breadth-first replay over multi-valued terms fields runs on the CPU path");
+    }
     // unmapped fields: a bucket aggregation over a missing field collects nothing (ValuesSource null); when only the
     // inner bucket aggregation's field is missing, the outer buckets still count the segment's docs and the inner
-    // aggregation of those docs is empty
-    const bool inner_missing = ORD && HIST && (terms_outer ? (oc && !hc) : (hc && !oc));
+    // aggregation of those docs is empty.  A deferred pipeline collects the same way: only the outer doc counts.
+    const bool inner_missing = ORD && HIST && ((pl.deferred && oc) || (terms_outer ? (oc && !hc) : (hc && !oc)));
     if (((ORD && !oc) || (HIST && !hc)) && !inner_missing) return 0;
     if (oc) require(oc->type == ESGPU_COL_ORD_U32, ESGPU_ERR_UNSUPPORTED, "terms on numeric fields run on the CPU path");
     if (hc && pl.inner_terms) {  // multi-valued outer / inner fields take the CSR kernel (inner ordinals as keys)
@@ -2342,10 +2438,12 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     bool has_keys = false;
     int64_t table_shift = 0;
     const uint32_t H_before = pl.H;
-    if (HIST && hc && pl.inner_terms) {  // one key per inner ordinal
-        kmin = 0;
-        kmax = (int64_t)std::max<uint64_t>(hc->ord_count(), 1) - 1;
-        has_keys = true;
+    if (HIST && hc && pl.inner_terms) {  // one key per inner ordinal (deferred: none, the grid is the outer counts)
+        if (!pl.deferred) {
+            kmin = 0;
+            kmax = (int64_t)std::max<uint64_t>(hc->ord_count(), 1) - 1;
+            has_keys = true;
+        }
     } else if (HIST && hc && hc->vmin <= hc->vmax) {
         if (pl.ktable) {
             table_shift = build_key_table(p, pl, hc->vmin, hc->vmax);
@@ -2548,7 +2646,8 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     if (!P.lds_mode && L_ORD && !L_HIST && L_met == 0 && !L_vcnt && L_ocnt == OCNT_NONE && !inner_missing &&
         (((uint64_t)pl.T + (1u << kPartShift) - 1) >> kPartShift) <= kPartMaxStaged) {
         p->last_bytes += bytes_per_doc * (uint64_t)s->max_doc + (d_accept ? ((uint64_t)s->max_doc + 7) / 8 : 0);
-        if (ESGPU_HOTCOLD && collect_hotcold(p, pl, s, oc, d_accept, P.pred, P.npred, first_segment)) return 1;
+        // (the hot/cold form keeps statistics per ordinal column: not for a column derived per request)
+        if (ESGPU_HOTCOLD && !pl.comp && collect_hotcold(p, pl, s, oc, d_accept, P.pred, P.npred, first_segment)) return 1;
         return collect_partitioned(p, pl, s, oc, d_accept, P.pred, P.npred) ? 1 : 0;
     }
     const uint64_t span = (uint64_t)pl.interval * (uint64_t)W;
@@ -2773,8 +2872,28 @@ extern "C" int esgpu_plan_collect_segment(esgpu_plan* p, const esgpu_segment* s,
         }
         p->last_bytes = 0;
         p->last_ms = -1;
+        bool deferred = false;
         for (Pipeline& pl : p->pipes) {
+            if (pl.replay) { pl.timed = false; continue; }
             pl.timed = pl.kind == 1 ? collect_hll(p, pl, s, d_accept) : collect_grid(p, pl, s, d_accept);
+            deferred |= pl.timed && pl.deferred;
+        }
+        if (deferred) {  // BestBucketsDeferringCollector: the segment (and its accept bits) kept for the replay at build
+            esgpu_plan::DeferredSeg d{s, -1};
+            if (d_accept) {
+                const size_t bytes = std::max<size_t>(s->n_pad / 64, 1) * 8;
+                size_t slot = 0;
+                while (slot < p->d_daccept.size() && std::any_of(p->dsegs.begin(), p->dsegs.end(),
+                                                                 [&](const esgpu_plan::DeferredSeg& x) { return x.accept == (int)slot; }))
+                    ++slot;
+                if (slot == p->d_daccept.size()) p->d_daccept.emplace_back();
+                DevBuf& b = p->d_daccept[slot];
+                if (b.bytes < bytes) b.alloc(p->ctx, bytes);
+                HIPX(hipMemcpyAsync(b.p, d_accept, bytes, hipMemcpyDeviceToDevice, p->stream));
+                d.accept = (int)slot;
+            }
+            pin_segment(s);
+            p->dsegs.push_back(d);
         }
         p->collected = true;
         ++p->seg_seq;
@@ -2787,6 +2906,13 @@ extern "C" int esgpu_plan_shard_mergeable(const esgpu_plan* p, int32_t* mergeabl
         int32_t m = 1;
         for (const SpecNode& n : p->specs) if (n.s.type == ESGPU_AGG_TERMS) m = 0;
         *mergeable = m;
+    });
+}
+
+extern "C" int esgpu_plan_deferred_segments(const esgpu_plan* p, int32_t* n) {
+    return guarded([&] {
+        require(p && n, ESGPU_ERR_INVALID, "null argument");
+        *n = (int32_t)p->dsegs.size();
     });
 }
 
@@ -3351,6 +3477,145 @@ static Block build_metric_root(esgpu_plan* p, const Group& g) {
     return r;
 }
 
+// The replayed inner terms of a deferred terms-under-terms child: per outer winner i, the selected inner terms, the
+// instance's other-doc count, and each pick's host cell in the replay pipelines (append_leaf / order_value index)
+struct ReplaySel {
+    std::vector<std::vector<TermPick>> picks;
+    std::vector<int64_t> other;
+    std::vector<std::vector<size_t>> cell;
+};
+
+// TermsAggregator breadth_first (A/bucket/terms/TermsAggregator.java:161 shouldDefer; BestBucketsDeferringCollector
+// .prepareSelectedBuckets :127-166, replayed from GlobalOrdinalsStringTermsAggregator.buildAggregation :195-196): the
+// child's collectors run again over the retained segments, each doc counted in its outer bucket's winner slot when that
+// bucket survived (the replay grid [slot][inner ordinal], rows padded to replay_stride); then the inner terms of every
+// winner are selected -- on the GPU per row (count / term orders) or from the fetched rows on the host (metric orders,
+// rows of at most 65,536 terms), with the same comparators as the dense grid's select_terms
+static ReplaySel replay_child(esgpu_plan* p, const ChildSrc& kid, const std::vector<TermPick>& top, uint64_t T_outer) {
+    ReplaySel rs;
+    const uint32_t k = (uint32_t)top.size();
+    rs.picks.resize(k);
+    rs.other.assign(k, 0);
+    rs.cell.resize(k);
+    if (!k || kid.rpipes.empty()) return rs;
+    hipStream_t st = p->stream;
+    const SpecNode& tn2 = p->specs[kid.spec];
+    std::vector<uint32_t> map(std::max<uint64_t>(T_outer, 1), kMissingOrd);
+    for (uint32_t i = 0; i < k; ++i) if (top[i].ord < map.size()) map[top[i].ord] = i;
+    uint32_t* dmap = (uint32_t*)p->s_slotmap.ensure(p->ctx, map.size() * 4);
+    HIPX(hipMemcpyAsync(dmap, map.data(), map.size() * 4, hipMemcpyHostToDevice, st));
+    p->slot_map = dmap;
+    p->slot_map_n = (uint32_t)map.size();
+    p->slot_k = k;
+    bool any = false;
+    try {
+        for (int pi : kid.rpipes) p->pipes[pi].fresh = true;
+        for (const esgpu_plan::DeferredSeg& d : p->dsegs) {
+            const uint64_t* acc = d.accept >= 0 ? p->d_daccept[d.accept].as<uint64_t>() : nullptr;
+            for (size_t j = 0; j < kid.rpipes.size(); ++j) {
+                const bool done = collect_grid(p, p->pipes[kid.rpipes[j]], d.s, acc);
+                if (j == 0) any |= done;
+            }
+        }
+        HIPX(hipStreamSynchronize(st));  // `map` is read by the copy above
+    } catch (...) {
+        p->slot_map = nullptr;
+        throw;
+    }
+    p->slot_map = nullptr;
+    Pipeline& R0 = p->pipes[kid.rpipes[0]];
+    const Pipeline& B0 = p->pipes[kid.pipes[0]];
+    const uint64_t nb = any ? R0.vcB : B0.value_count2;
+    const uint64_t stride = replay_stride(nb);
+    const bool agg2 = tn2.s.order == ESGPU_ORDER_AGG_ASC || tn2.s.order == ESGPU_ORDER_AGG_DESC;
+    LeafRef ord2;
+    if (agg2)
+        for (size_t gj = 0; gj < tn2.children.size(); ++gj) if (tn2.children[gj] == tn2.order_child) ord2 = kid.rgrand[gj];
+    if (!any) {  // no doc of a winner has an inner term: every row is empty (min_doc_count 0 still lists the terms)
+        std::vector<unsigned long long> zero(std::max<uint64_t>(nb, 1), 0ull);
+        for (uint32_t i = 0; i < k; ++i) {
+            rs.picks[i] = select_terms(tn2.s, zero.data(), (uint32_t)nb, &rs.other[i], [](uint32_t) { return NAN; });
+            rs.cell[i].assign(rs.picks[i].size(), 0);
+        }
+        return rs;
+    }
+    if (agg2 || nb <= 65536) {  // the winners' rows on the host
+        for (int pi : kid.rpipes) fetch_grid(p, p->pipes[pi]);
+        bsync(p);
+        for (uint32_t i = 0; i < k; ++i) {
+            const size_t row = (size_t)i * stride;
+            rs.picks[i] = select_terms(tn2.s, R0.hc.cnt + row, (uint32_t)nb, &rs.other[i], [&](uint32_t ord) {
+                return order_value(p, tn2, p->pipes[ord2.pipe], ord2.leaf, row + ord);
+            });
+            for (const TermPick& tp : rs.picks[i]) rs.cell[i].push_back(row + tp.ord);
+        }
+        return rs;
+    }
+    // per winner row: the GPU top-k (K3) over its inner ordinals, then one gather of the picked cells of every array
+    const bool count_order = tn2.s.order == ESGPU_ORDER_COUNT_DESC || tn2.s.order == ESGPU_ORDER_COUNT_ASC;
+    const uint32_t kk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nb, (uint64_t)std::max<int64_t>(tn2.s.shard_size, 0)));
+    require(kk <= kTopkMax, ESGPU_ERR_UNSUPPORTED, "inner shard_size beyond the GPU top-k");
+    unsigned long long* dk = (unsigned long long*)p->s_rkeys.ensure(p->ctx, (size_t)k * (kk + 1) * 8);
+    HIPX(hipMemsetAsync(dk, 0, (size_t)k * (kk + 1) * 8, st));
+    const uint32_t n_wg = std::min<uint32_t>(512, (uint32_t)((nb + 4095) / 4096));
+    unsigned long long* cand = (unsigned long long*)p->s_cand.ensure(p->ctx, (count_order ? (size_t)nb : (size_t)n_wg * kk) * 8);
+    uint32_t* hs = (uint32_t*)p->s_hist.ensure(p->ctx, (2048 + 2) * 4);
+    for (uint32_t i = 0; i < k; ++i) {
+        TopkParams K{};
+        if (R0.cnt32) K.counts32 = R0.g_cnt.as<unsigned int>() + (size_t)i * stride;
+        else K.counts = R0.g_cnt.as<unsigned long long>() + (size_t)i * stride;
+        K.T = (uint32_t)nb;
+        K.order = tn2.s.order;
+        K.min_doc_count = tn2.s.min_doc_count;
+        K.shard_min_doc_count = tn2.s.shard_min_doc_count;
+        K.k = kk;
+        K.n_wg = n_wg;
+        K.cand = cand;
+        K.hist = hs;
+        K.sel = hs + 2048;
+        K.out_keys = dk + (size_t)i * (kk + 1);
+        K.out_sum = K.out_keys + kk;
+        launch_topk(K, st);
+        HIPX(hipGetLastError());
+    }
+    d2h_u64(p, p->h_rkeys, dk, (size_t)k * (kk + 1));
+    bsync(p);
+    const unsigned long long* hk = p->h_rkeys.as<unsigned long long>();
+    std::vector<uint32_t> cells;
+    for (uint32_t i = 0; i < k; ++i) {
+        const unsigned long long* ki = hk + (size_t)i * (kk + 1);
+        rs.other[i] = (int64_t)ki[kk];
+        for (uint32_t j = 0; j < kk; ++j) {
+            const unsigned long long key = ki[j];
+            if (key == 0) break;
+            TermPick tp;
+            const uint32_t lo = (uint32_t)key;
+            tp.ord = tn2.s.order == ESGPU_ORDER_TERM_DESC ? lo : 0xFFFFFFFFu - lo;
+            const uint64_t hi = (key >> 32) & 0x7FFFFFFFull;
+            tp.count = tn2.s.order == ESGPU_ORDER_COUNT_DESC ? (int64_t)hi
+                     : tn2.s.order == ESGPU_ORDER_COUNT_ASC ? (int64_t)(0x7FFFFFFFull - hi) : -1;
+            rs.cell[i].push_back(cells.size());
+            cells.push_back((uint32_t)((size_t)i * stride + tp.ord));
+            rs.picks[i].push_back(tp);
+        }
+    }
+    uint32_t* dc = (uint32_t*)p->s_cells.ensure(p->ctx, std::max<size_t>(cells.size(), 1) * 4);
+    if (!cells.empty()) HIPX(hipMemcpyAsync(dc, cells.data(), cells.size() * 4, hipMemcpyHostToDevice, st));
+    for (int pi : kid.rpipes) {  // H == 1: the gather of rows is a gather of cells
+        Pipeline& R = p->pipes[pi];
+        require(R.H == 1, ESGPU_ERR_DEVICE, "replay grid with a key dimension");
+        fetch_rows(p, R, dc, (uint32_t)cells.size());
+    }
+    bsync(p);  // also keeps `cells` alive for the copy
+    for (uint32_t i = 0; i < k; ++i)
+        for (size_t j = 0; j < rs.picks[i].size(); ++j) {
+            TermPick& tp = rs.picks[i][j];
+            if (tp.count < 0) tp.count = (int64_t)R0.hc.cnt[rs.cell[i][j]];  // term orders: the count from the gather
+            rs.other[i] -= tp.count;
+        }
+    return rs;
+}
+
 static Block build_terms_root(esgpu_plan* p, const Group& g) {
     hipStream_t st = p->stream;
     const SpecNode& tn = p->specs[g.root];
@@ -3526,6 +3791,14 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
             for (uint32_t s2 = 0; s2 < pl.H; ++s2) cells[(size_t)i * pl.H + s2] = s2 * pl.T + top[i].ord;
         gather_cards(p, pl, cells);
     }
+    // deferred terms-under-terms children: their breadth-first replay over the surviving outer buckets
+    std::vector<ReplaySel> replays(g.kids.size());
+    for (size_t ki = 0; ki < g.kids.size(); ++ki) {
+        const ChildSrc& kid = g.kids[ki];
+        if (!kid.bucket || kid.rpipes.empty() || !p->pipes[kid.pipes[0]].deferred || !p->pipes[kid.pipes[0]].allocated) continue;
+        replays[ki] = replay_child(p, kid, top, P0.value_count);
+    }
+    bmark(p, "replayed");
     // three-level children: the composite ordinals their emission reads, gathered as rows [r][H] -- shape 1 (terms{terms
     // {histogram}}): (winner, each X term it selects), shape 2 (terms{histogram{terms}}): (winner, every Y term)
     std::vector<std::vector<uint32_t>> deep_off(g.kids.size());
@@ -3674,6 +3947,21 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
             }
             const Pipeline& B0 = p->pipes[kid.pipes[0]];
             if (!B0.allocated) { sub.append_empty(); continue; }
+            if (B0.inner_terms && B0.deferred) {  // replayed breadth-first: the picks of replay_child
+                if (!B0.tdict2) { sub.append_empty(); continue; }
+                const ReplaySel& rs = replays[ki];
+                begin_instance(sub, rs.other[i]);
+                for (size_t j = 0; j < rs.picks[i].size(); ++j) {
+                    const TermPick& tp = rs.picks[i][j];
+                    const std::string term2 = B0.tdict2->term(tp.ord);
+                    push_bucket(sub, tp.ord, &term2, tp.count);
+                    if (tp.count == 0) { for (Block& sb : sub.subs) sb.append_empty(); continue; }
+                    for (size_t gj = 0; gj < kid.rgrand.size(); ++gj)
+                        append_leaf(p, p->pipes[kid.rgrand[gj].pipe], kid.rgrand[gj].leaf, rs.cell[i][j], sub.subs[gj]);
+                }
+                end_instance(sub);
+                continue;
+            }
             if (B0.inner_terms) {  // terms under terms: the inner buckets are the top terms of the winner's row
                 if (!B0.tdict2) { sub.append_empty(); continue; }
                 const SpecNode& tn2 = p->specs[kid.spec];
@@ -4013,6 +4301,7 @@ extern "C" int esgpu_plan_reset(esgpu_plan* p) {
         p->posted = false;
         p->collected = false;
         p->seg_seq = 0;
+        p->unpin_all();
     });
 }
 
@@ -4021,6 +4310,7 @@ extern "C" int esgpu_plan_destroy(esgpu_plan* p) {
         if (!p) return;
         (void)hipSetDevice(p->ctx->device);
         (void)hipStreamSynchronize(p->stream);
+        p->unpin_all();
         for (Pipeline& pl : p->pipes) {
             if (pl.e0) (void)hipEventDestroy(pl.e0);
             if (pl.e1) (void)hipEventDestroy(pl.e1);

@@ -217,6 +217,12 @@ class Plan:
         N.check(N.lib().esgpu_plan_shard_mergeable(self._ptr, ctypes.byref(v)))
         return bool(v.value)
 
+    def deferred_segments(self):
+        """Segments retained for a breadth-first replay at build (terms under terms over the dense budget)."""
+        v = ctypes.c_int32()
+        N.check(N.lib().esgpu_plan_deferred_segments(self._ptr, ctypes.byref(v)))
+        return v.value
+
     def close(self):
         if self._ptr:
             N.check(N.lib().esgpu_plan_destroy(self._ptr))

@@ -359,6 +359,12 @@ int esgpu_plan_last_build_stats(const esgpu_plan* plan, double* total_ms, double
  * separate results would (HistogramAggregator / metrics / HyperLogLogPlusPlus.merge; min_doc_count and empty buckets
  * apply at reduce) -- while terms need one build per shard (per-shard top-k, InternalTerms.doReduce). */
 int esgpu_plan_shard_mergeable(const esgpu_plan* plan, int32_t* mergeable);
+/* Segments the plan retains for a breadth-first replay at build (TermsAggregator breadth_first collect mode,
+ * BestBucketsDeferringCollector.java:96-166): a terms-under-terms child whose [outer x inner] grid is over the dense
+ * budget counts only the outer buckets while collecting and is collected again at build over the retained segments for
+ * the surviving outer buckets.  A retained segment stays valid until the plan's reset / destroy even if
+ * esgpu_segment_destroy is called on it first (its destroy is then carried out at that point). */
+int esgpu_plan_deferred_segments(const esgpu_plan* plan, int32_t* segments);
 
 /* ---------------------------------------------------------------------------------------------------------
  * Results: columnar InternalAggregations, owned by the library.

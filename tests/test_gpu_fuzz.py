@@ -223,7 +223,9 @@ _stats = {"ran": 0, "refused": 0}
 
 
 @pytest.mark.parametrize("seed", SEEDS)
-def test_random_request(engine, seed):
+def test_random_request(engine, seed, monkeypatch):
+    if seed % 3 == 0:  # terms under terms collected breadth-first (replayed at build) whatever the grid size
+        monkeypatch.setenv("ESGPU_DEFER_CELLS", "1")
     rng = np.random.default_rng(1000 + seed)
     n = int(rng.integers(30_000, 300_000))
     cols, T_kw = make_segment(rng, n)
