@@ -2570,7 +2570,8 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     P.ocnt_mode = L_ocnt;
     P.accept = d_accept;
     if (inner_missing) { P.mv = nullptr; P.mv_present = nullptr; P.mv_f64 = 0; }
-    uint64_t bytes_per_doc = (oc ? (pl.ord_hist ? 8 : 4) : 0) + (hc ? (pl.inner_terms ? 4 : 8) : 0) + (mc && !inner_missing ? 8 : 0);
+    uint64_t bytes_per_doc = (oc ? (pl.ord_hist ? 8 : 4) : 0) + (hc && !pl.deferred ? (pl.inner_terms ? 4 : 8) : 0) +
+                             (mc && !inner_missing ? 8 : 0);
     set_preds(p, pl, s, P.pred, &P.npred, &bytes_per_doc, &P.accept);
     d_accept = P.accept;  // the clauses folded into a bitset when there are more than kMaxPreds
     P.g_cnt = inner_missing ? pl.g_ocnt.as<unsigned long long>() : pl.g_cnt.as<unsigned long long>();
@@ -3491,25 +3492,28 @@ struct ReplaySel {
 // bucket survived (the replay grid [slot][inner ordinal], rows padded to replay_stride); then the inner terms of every
 // winner are selected -- on the GPU per row (count / term orders) or from the fetched rows on the host (metric orders,
 // rows of at most 65,536 terms), with the same comparators as the dense grid's select_terms
-static ReplaySel replay_child(esgpu_plan* p, const ChildSrc& kid, const std::vector<TermPick>& top, uint64_t T_outer) {
-    ReplaySel rs;
-    const uint32_t k = (uint32_t)top.size();
-    rs.picks.resize(k);
-    rs.other.assign(k, 0);
-    rs.cell.resize(k);
-    if (!k || kid.rpipes.empty()) return rs;
+// One replay pass: outer winners [b0, b0 + kb) take slots 0 .. kb - 1 and the replay pipelines collect every retained
+// segment into their [slot][inner ordinal] grid; false when no retained segment had both fields
+static bool replay_pass(esgpu_plan* p, const ChildSrc& kid, const std::vector<TermPick>& top, uint32_t b0, uint32_t kb,
+                        uint64_t T_outer) {
     hipStream_t st = p->stream;
-    const SpecNode& tn2 = p->specs[kid.spec];
     std::vector<uint32_t> map(std::max<uint64_t>(T_outer, 1), kMissingOrd);
-    for (uint32_t i = 0; i < k; ++i) if (top[i].ord < map.size()) map[top[i].ord] = i;
+    for (uint32_t i = 0; i < kb; ++i) if (top[b0 + i].ord < map.size()) map[top[b0 + i].ord] = i;
     uint32_t* dmap = (uint32_t*)p->s_slotmap.ensure(p->ctx, map.size() * 4);
     HIPX(hipMemcpyAsync(dmap, map.data(), map.size() * 4, hipMemcpyHostToDevice, st));
     p->slot_map = dmap;
     p->slot_map_n = (uint32_t)map.size();
-    p->slot_k = k;
+    p->slot_k = kb;
     bool any = false;
     try {
-        for (int pi : kid.rpipes) p->pipes[pi].fresh = true;
+        for (int pi : kid.rpipes) {
+            Pipeline& R = p->pipes[pi];
+            if (b0 > 0 && R.allocated) {  // a later pass over the same buffers: the grid starts from zero again
+                R.fresh = true;
+                HIPX(hipMemsetAsync(R.g_cnt.p, 0, R.g_cnt.bytes, st));
+            }
+            R.fresh = true;
+        }
         for (const esgpu_plan::DeferredSeg& d : p->dsegs) {
             const uint64_t* acc = d.accept >= 0 ? p->d_daccept[d.accept].as<uint64_t>() : nullptr;
             for (size_t j = 0; j < kid.rpipes.size(); ++j) {
@@ -3523,96 +3527,126 @@ static ReplaySel replay_child(esgpu_plan* p, const ChildSrc& kid, const std::vec
         throw;
     }
     p->slot_map = nullptr;
-    Pipeline& R0 = p->pipes[kid.rpipes[0]];
+    return any;
+}
+
+// TermsAggregator breadth_first (A/bucket/terms/TermsAggregator.java:161 shouldDefer; BestBucketsDeferringCollector
+// .prepareSelectedBuckets :127-166, replayed from GlobalOrdinalsStringTermsAggregator.buildAggregation :195-196): the
+// child's collectors run again over the retained segments, each doc counted in its outer bucket's winner slot when that
+// bucket survived (the replay grid [slot][inner ordinal], rows padded to replay_stride); then the inner terms of every
+// winner are selected -- on the GPU per row (count / term orders) or from the fetched rows on the host (metric orders,
+// rows of at most 65,536 terms), with the same comparators as the dense grid's select_terms.  A count-only child whose
+// grid is over what the partitioned counting path stages (kPartMaxStaged partitions) replays the winners in batches, so
+// every pass counts in LDS partitions instead of one global atomic per doc (hot inner terms serialise those).
+static ReplaySel replay_child(esgpu_plan* p, const ChildSrc& kid, const std::vector<TermPick>& top, uint64_t T_outer) {
+    ReplaySel rs;
+    const uint32_t k = (uint32_t)top.size();
+    rs.picks.resize(k);
+    rs.other.assign(k, 0);
+    rs.cell.resize(k);
+    if (!k || kid.rpipes.empty()) return rs;
+    hipStream_t st = p->stream;
+    const SpecNode& tn2 = p->specs[kid.spec];
     const Pipeline& B0 = p->pipes[kid.pipes[0]];
-    const uint64_t nb = any ? R0.vcB : B0.value_count2;
-    const uint64_t stride = replay_stride(nb);
+    Pipeline& R0 = p->pipes[kid.rpipes[0]];
     const bool agg2 = tn2.s.order == ESGPU_ORDER_AGG_ASC || tn2.s.order == ESGPU_ORDER_AGG_DESC;
+    const bool host_sel = agg2 || B0.value_count2 <= 65536;
+    uint32_t wb = k;
+    if (!host_sel && kid.rpipes.size() == 1 && R0.met == 0 && R0.cards.empty()) {
+        const uint64_t part_cells = (uint64_t)kPartMaxStaged << kPartShift;
+        wb = (uint32_t)std::min<uint64_t>(k, std::max<uint64_t>(1, part_cells / replay_stride(B0.value_count2)));
+    }
     LeafRef ord2;
     if (agg2)
         for (size_t gj = 0; gj < tn2.children.size(); ++gj) if (tn2.children[gj] == tn2.order_child) ord2 = kid.rgrand[gj];
-    if (!any) {  // no doc of a winner has an inner term: every row is empty (min_doc_count 0 still lists the terms)
-        std::vector<unsigned long long> zero(std::max<uint64_t>(nb, 1), 0ull);
-        for (uint32_t i = 0; i < k; ++i) {
-            rs.picks[i] = select_terms(tn2.s, zero.data(), (uint32_t)nb, &rs.other[i], [](uint32_t) { return NAN; });
-            rs.cell[i].assign(rs.picks[i].size(), 0);
+    for (uint32_t b0 = 0; b0 < k; b0 += wb) {
+        const uint32_t kb = std::min(wb, k - b0);
+        const bool any = replay_pass(p, kid, top, b0, kb, T_outer);
+        const uint64_t nb = any ? R0.vcB : B0.value_count2;
+        const uint64_t stride = replay_stride(nb);
+        if (!any) {  // no doc of these winners has an inner term: every row is empty (min_doc_count 0 still lists terms)
+            std::vector<unsigned long long> zero(std::max<uint64_t>(nb, 1), 0ull);
+            for (uint32_t i = b0; i < b0 + kb; ++i) {
+                rs.picks[i] = select_terms(tn2.s, zero.data(), (uint32_t)nb, &rs.other[i], [](uint32_t) { return NAN; });
+                rs.cell[i].assign(rs.picks[i].size(), 0);
+            }
+            continue;
         }
-        return rs;
-    }
-    if (agg2 || nb <= 65536) {  // the winners' rows on the host
-        for (int pi : kid.rpipes) fetch_grid(p, p->pipes[pi]);
+        if (host_sel) {  // the winners' rows on the host (one pass: wb == k)
+            for (int pi : kid.rpipes) fetch_grid(p, p->pipes[pi]);
+            bsync(p);
+            for (uint32_t r = 0; r < kb; ++r) {
+                const size_t row = (size_t)r * stride;
+                rs.picks[b0 + r] = select_terms(tn2.s, R0.hc.cnt + row, (uint32_t)nb, &rs.other[b0 + r], [&](uint32_t ord) {
+                    return order_value(p, tn2, p->pipes[ord2.pipe], ord2.leaf, row + ord);
+                });
+                for (const TermPick& tp : rs.picks[b0 + r]) rs.cell[b0 + r].push_back(row + tp.ord);
+            }
+            continue;
+        }
+        // per winner row: the GPU top-k (K3) over its inner ordinals, then one gather of the picked cells of every array
+        const bool count_order = tn2.s.order == ESGPU_ORDER_COUNT_DESC || tn2.s.order == ESGPU_ORDER_COUNT_ASC;
+        const uint32_t kk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nb, (uint64_t)std::max<int64_t>(tn2.s.shard_size, 0)));
+        require(kk <= kTopkMax, ESGPU_ERR_UNSUPPORTED, "inner shard_size beyond the GPU top-k");
+        unsigned long long* dk = (unsigned long long*)p->s_rkeys.ensure(p->ctx, (size_t)kb * (kk + 1) * 8);
+        HIPX(hipMemsetAsync(dk, 0, (size_t)kb * (kk + 1) * 8, st));
+        const uint32_t n_wg = std::min<uint32_t>(512, (uint32_t)((nb + 4095) / 4096));
+        unsigned long long* cand = (unsigned long long*)p->s_cand.ensure(p->ctx, (count_order ? (size_t)nb : (size_t)n_wg * kk) * 8);
+        uint32_t* hs = (uint32_t*)p->s_hist.ensure(p->ctx, (2048 + 2) * 4);
+        for (uint32_t r = 0; r < kb; ++r) {
+            TopkParams K{};
+            if (R0.cnt32) K.counts32 = R0.g_cnt.as<unsigned int>() + (size_t)r * stride;
+            else K.counts = R0.g_cnt.as<unsigned long long>() + (size_t)r * stride;
+            K.T = (uint32_t)nb;
+            K.order = tn2.s.order;
+            K.min_doc_count = tn2.s.min_doc_count;
+            K.shard_min_doc_count = tn2.s.shard_min_doc_count;
+            K.k = kk;
+            K.n_wg = n_wg;
+            K.cand = cand;
+            K.hist = hs;
+            K.sel = hs + 2048;
+            K.out_keys = dk + (size_t)r * (kk + 1);
+            K.out_sum = K.out_keys + kk;
+            launch_topk(K, st);
+            HIPX(hipGetLastError());
+        }
+        d2h_u64(p, p->h_rkeys, dk, (size_t)kb * (kk + 1));
         bsync(p);
-        for (uint32_t i = 0; i < k; ++i) {
-            const size_t row = (size_t)i * stride;
-            rs.picks[i] = select_terms(tn2.s, R0.hc.cnt + row, (uint32_t)nb, &rs.other[i], [&](uint32_t ord) {
-                return order_value(p, tn2, p->pipes[ord2.pipe], ord2.leaf, row + ord);
-            });
-            for (const TermPick& tp : rs.picks[i]) rs.cell[i].push_back(row + tp.ord);
+        const unsigned long long* hk = p->h_rkeys.as<unsigned long long>();
+        std::vector<uint32_t> cells;
+        for (uint32_t r = 0; r < kb; ++r) {
+            const unsigned long long* ki = hk + (size_t)r * (kk + 1);
+            rs.other[b0 + r] = (int64_t)ki[kk];
+            for (uint32_t j = 0; j < kk; ++j) {
+                const unsigned long long key = ki[j];
+                if (key == 0) break;
+                TermPick tp;
+                const uint32_t lo = (uint32_t)key;
+                tp.ord = tn2.s.order == ESGPU_ORDER_TERM_DESC ? lo : 0xFFFFFFFFu - lo;
+                const uint64_t hi = (key >> 32) & 0x7FFFFFFFull;
+                tp.count = tn2.s.order == ESGPU_ORDER_COUNT_DESC ? (int64_t)hi
+                         : tn2.s.order == ESGPU_ORDER_COUNT_ASC ? (int64_t)(0x7FFFFFFFull - hi) : -1;
+                rs.cell[b0 + r].push_back(cells.size());
+                cells.push_back((uint32_t)((size_t)r * stride + tp.ord));
+                rs.picks[b0 + r].push_back(tp);
+            }
         }
-        return rs;
-    }
-    // per winner row: the GPU top-k (K3) over its inner ordinals, then one gather of the picked cells of every array
-    const bool count_order = tn2.s.order == ESGPU_ORDER_COUNT_DESC || tn2.s.order == ESGPU_ORDER_COUNT_ASC;
-    const uint32_t kk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nb, (uint64_t)std::max<int64_t>(tn2.s.shard_size, 0)));
-    require(kk <= kTopkMax, ESGPU_ERR_UNSUPPORTED, "inner shard_size beyond the GPU top-k");
-    unsigned long long* dk = (unsigned long long*)p->s_rkeys.ensure(p->ctx, (size_t)k * (kk + 1) * 8);
-    HIPX(hipMemsetAsync(dk, 0, (size_t)k * (kk + 1) * 8, st));
-    const uint32_t n_wg = std::min<uint32_t>(512, (uint32_t)((nb + 4095) / 4096));
-    unsigned long long* cand = (unsigned long long*)p->s_cand.ensure(p->ctx, (count_order ? (size_t)nb : (size_t)n_wg * kk) * 8);
-    uint32_t* hs = (uint32_t*)p->s_hist.ensure(p->ctx, (2048 + 2) * 4);
-    for (uint32_t i = 0; i < k; ++i) {
-        TopkParams K{};
-        if (R0.cnt32) K.counts32 = R0.g_cnt.as<unsigned int>() + (size_t)i * stride;
-        else K.counts = R0.g_cnt.as<unsigned long long>() + (size_t)i * stride;
-        K.T = (uint32_t)nb;
-        K.order = tn2.s.order;
-        K.min_doc_count = tn2.s.min_doc_count;
-        K.shard_min_doc_count = tn2.s.shard_min_doc_count;
-        K.k = kk;
-        K.n_wg = n_wg;
-        K.cand = cand;
-        K.hist = hs;
-        K.sel = hs + 2048;
-        K.out_keys = dk + (size_t)i * (kk + 1);
-        K.out_sum = K.out_keys + kk;
-        launch_topk(K, st);
-        HIPX(hipGetLastError());
-    }
-    d2h_u64(p, p->h_rkeys, dk, (size_t)k * (kk + 1));
-    bsync(p);
-    const unsigned long long* hk = p->h_rkeys.as<unsigned long long>();
-    std::vector<uint32_t> cells;
-    for (uint32_t i = 0; i < k; ++i) {
-        const unsigned long long* ki = hk + (size_t)i * (kk + 1);
-        rs.other[i] = (int64_t)ki[kk];
-        for (uint32_t j = 0; j < kk; ++j) {
-            const unsigned long long key = ki[j];
-            if (key == 0) break;
-            TermPick tp;
-            const uint32_t lo = (uint32_t)key;
-            tp.ord = tn2.s.order == ESGPU_ORDER_TERM_DESC ? lo : 0xFFFFFFFFu - lo;
-            const uint64_t hi = (key >> 32) & 0x7FFFFFFFull;
-            tp.count = tn2.s.order == ESGPU_ORDER_COUNT_DESC ? (int64_t)hi
-                     : tn2.s.order == ESGPU_ORDER_COUNT_ASC ? (int64_t)(0x7FFFFFFFull - hi) : -1;
-            rs.cell[i].push_back(cells.size());
-            cells.push_back((uint32_t)((size_t)i * stride + tp.ord));
-            rs.picks[i].push_back(tp);
+        uint32_t* dc = (uint32_t*)p->s_cells.ensure(p->ctx, std::max<size_t>(cells.size(), 1) * 4);
+        if (!cells.empty()) HIPX(hipMemcpyAsync(dc, cells.data(), cells.size() * 4, hipMemcpyHostToDevice, st));
+        for (int pi : kid.rpipes) {  // H == 1: the gather of rows is a gather of cells
+            Pipeline& R = p->pipes[pi];
+            require(R.H == 1, ESGPU_ERR_DEVICE, "replay grid with a key dimension");
+            fetch_rows(p, R, dc, (uint32_t)cells.size());
         }
+        bsync(p);  // also keeps `cells` alive for the copy
+        for (uint32_t r = 0; r < kb; ++r)
+            for (size_t j = 0; j < rs.picks[b0 + r].size(); ++j) {
+                TermPick& tp = rs.picks[b0 + r][j];
+                if (tp.count < 0) tp.count = (int64_t)R0.hc.cnt[rs.cell[b0 + r][j]];  // term orders: count from the gather
+                rs.other[b0 + r] -= tp.count;
+            }
     }
-    uint32_t* dc = (uint32_t*)p->s_cells.ensure(p->ctx, std::max<size_t>(cells.size(), 1) * 4);
-    if (!cells.empty()) HIPX(hipMemcpyAsync(dc, cells.data(), cells.size() * 4, hipMemcpyHostToDevice, st));
-    for (int pi : kid.rpipes) {  // H == 1: the gather of rows is a gather of cells
-        Pipeline& R = p->pipes[pi];
-        require(R.H == 1, ESGPU_ERR_DEVICE, "replay grid with a key dimension");
-        fetch_rows(p, R, dc, (uint32_t)cells.size());
-    }
-    bsync(p);  // also keeps `cells` alive for the copy
-    for (uint32_t i = 0; i < k; ++i)
-        for (size_t j = 0; j < rs.picks[i].size(); ++j) {
-            TermPick& tp = rs.picks[i][j];
-            if (tp.count < 0) tp.count = (int64_t)R0.hc.cnt[rs.cell[i][j]];  // term orders: the count from the gather
-            rs.other[i] -= tp.count;
-        }
     return rs;
 }
 
