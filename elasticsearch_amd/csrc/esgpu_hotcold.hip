@@ -64,6 +64,17 @@ void launch_hc_recode(const uint32_t* ord, uint32_t n, const uint32_t* keys, con
                        vals, log2, out);
 }
 
+__global__ void hc_hot16_kernel(const uint32_t* rc, uint32_t n, uint16_t* out) {
+    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < n; d += gridDim.x * blockDim.x) {
+        const uint32_t v = rc[d];
+        out[d] = (v & kHcHotBit) && v != kMissingOrd ? (uint16_t)(v & ~kHcHotBit) : (uint16_t)0xFFFFu;
+    }
+}
+void launch_hc_hot16(const uint32_t* rc, uint32_t n, uint16_t* out, hipStream_t s) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(hc_hot16_kernel, dim3(std::min<uint32_t>(8192, (n + 255) / 256)), dim3(256), 0, s, rc, n, out);
+}
+
 __global__ void hc_init_kernel(HcParams P) {
     for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < P.P; p += gridDim.x * blockDim.x)
         P.ovf_cur[p] = P.part[p].ovf_base;
@@ -558,6 +569,69 @@ __global__ __launch_bounds__(kHotWG) void hc_hot_kernel(HcParams P) {
     for (uint32_t i = threadIdx.x; i < stride; i += kHotWG) P.hot_slab[(size_t)w * stride + i] = i < NH ? hot[i] : 0u;
 }
 
+// The same pass over the 16-bit hot-slot column (the segment statistics' compressed copy, like Lucene's bit-packed
+// ordinals): 8 docs per 16-byte load, half the bytes of the recoded column
+constexpr uint32_t kHot16TileDocs = kHotWG * kHcIt * 8;
+template <bool ACC>
+__global__ __launch_bounds__(kHotWG) void hc_hot16_count_kernel(HcParams P) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t* hot = (uint32_t*)smem;
+    const uint32_t NH = hc_hot_counters(P.hot_n);
+    for (uint32_t i = threadIdx.x; i < NH; i += kHotWG) hot[i] = 0u;
+    __syncthreads();
+    const uint32_t w = blockIdx.x;
+    const uint32_t b_begin = min(w * P.blocks_per_wg, P.n_blocks);
+    const uint32_t b_end = min(b_begin + P.blocks_per_wg, P.n_blocks);
+    const uint32_t d_begin = b_begin * kBlockDocs;
+    const uint32_t d_end = min(b_end * kBlockDocs, P.n_docs);
+    const uint32_t span = b_end > b_begin ? (b_end - b_begin) * kBlockDocs : 0u;
+    const uint32_t d_last = P.n_blocks * kBlockDocs - 8;
+    const uint32_t tid8 = threadIdx.x * 8;
+    auto load = [&](uint32_t t0, uint32_t o[kHcIt][4], uint64_t aw[kHcIt]) {
+#pragma unroll
+        for (int k = 0; k < kHcIt; ++k) {
+            const uint32_t d = min(t0 + k * (kHotWG * 8) + tid8, d_last);
+            const u32x4_t a = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(P.rc16 + d));
+            o[k][0] = a.x; o[k][1] = a.y; o[k][2] = a.z; o[k][3] = a.w;
+            if (ACC) aw[k] = P.accept[d >> 6];
+        }
+    };
+    auto count = [&](uint32_t t0, const uint32_t o[kHcIt][4], const uint64_t aw[kHcIt]) {
+        if (t0 >= d_begin + span) return;
+#pragma unroll
+        for (int k = 0; k < kHcIt; ++k) {
+            const uint32_t doc0 = t0 + k * (kHotWG * 8) + tid8;
+            const uint32_t live = ACC ? (uint32_t)(aw[k] >> (doc0 & 63)) & 0xFFu : 0xFFu;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t sl = (o[k][j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                if (sl != 0xFFFFu && doc0 + j < d_end && ((live >> j) & 1u))
+                    atomicAdd(&hot[sl < kHcHotCopies ? 4 * sl + (threadIdx.x & 3) : 3 * kHcHotCopies + sl], 1u);
+            }
+        }
+    };
+    if (span) {
+        uint32_t A[kHcIt][4], B[kHcIt][4], C[kHcIt][4];
+        uint64_t Aw[kHcIt], Bw[kHcIt], Cw[kHcIt];
+        load(d_begin, A, Aw);
+        __builtin_amdgcn_sched_barrier(0);
+        load(d_begin + kHot16TileDocs, B, Bw);
+        __builtin_amdgcn_sched_barrier(0);
+        load(d_begin + 2 * kHot16TileDocs, C, Cw);
+        for (uint32_t t0 = d_begin; t0 < d_begin + span; t0 += 3 * kHot16TileDocs) {
+            count(t0, A, Aw);
+            load(t0 + 3 * kHot16TileDocs, A, Aw);
+            count(t0 + kHot16TileDocs, B, Bw);
+            load(t0 + 4 * kHot16TileDocs, B, Bw);
+            count(t0 + 2 * kHot16TileDocs, C, Cw);
+            load(t0 + 5 * kHot16TileDocs, C, Cw);
+        }
+    }
+    __syncthreads();
+    const uint32_t stride = hc_slab_stride(P.hot_n);
+    for (uint32_t i = threadIdx.x; i < stride; i += kHotWG) P.hot_slab[(size_t)w * stride + i] = i < NH ? hot[i] : 0u;
+}
+
 __global__ __launch_bounds__(256) void hc_pad_kernel(const uint16_t* dense, const uint32_t* dense_begin,
                                                      const uint32_t* pad_begin, uint16_t* out) {
     const uint32_t p = blockIdx.x;
@@ -588,7 +662,12 @@ __global__ __launch_bounds__(256) void hc_cold_sub_kernel(const uint32_t* rc, co
 }
 
 void launch_hotcold_postings(const HcParams& hot, const HcParams& cold, hipStream_t s) {
-    if (hot.hot_n && hot.accept)
+    const size_t hlds = (size_t)hc_hot_counters(hot.hot_n) * 4;
+    if (hot.hot_n && hot.rc16 && hot.accept)
+        hipLaunchKernelGGL(hc_hot16_count_kernel<true>, dim3(hot.G), dim3(kHotWG), hlds, s, hot);
+    else if (hot.hot_n && hot.rc16)
+        hipLaunchKernelGGL(hc_hot16_count_kernel<false>, dim3(hot.G), dim3(kHotWG), hlds, s, hot);
+    else if (hot.hot_n && hot.accept)
         hipLaunchKernelGGL(hc_hot_kernel<true>, dim3(hot.G), dim3(kHotWG), (size_t)hc_hot_counters(hot.hot_n) * 4, s, hot);
     else if (hot.hot_n)
         hipLaunchKernelGGL(hc_hot_kernel<false>, dim3(hot.G), dim3(kHotWG), (size_t)hc_hot_counters(hot.hot_n) * 4, s, hot);

@@ -323,6 +323,7 @@ struct HcPiece {           // a counting workgroup's share: region elements [lo,
 struct HcParams {
     uint32_t n_docs, n_blocks, blocks_per_wg, G;   // G = scatter workgroups (the segment statistics' layout)
     const uint32_t* rc;                // recoded ordinal column: cold ordinal | kHcHotBit | hot slot | 0xFFFFFFFF missing
+    const uint16_t* rc16;              // postings hot pass: the hot slot of each doc, 0xFFFF for a cold / missing one
     uint32_t T, P;
     int32_t npred;
     PredDev pred[4];
@@ -360,6 +361,8 @@ void launch_hc_pad(const uint16_t* dense, const uint32_t* dense_begin, const uin
 // 0xFFFFFFFF = empty key), the ordinal itself otherwise
 void launch_hc_recode(const uint32_t* ord, uint32_t n, const uint32_t* keys, const uint32_t* vals, uint32_t log2,
                       uint32_t* out, hipStream_t s);
+// stats time: the 16-bit hot-slot column of the postings hot pass from the recoded column (0xFFFF: cold or missing)
+void launch_hc_hot16(const uint32_t* rc, uint32_t n, uint16_t* out, hipStream_t s);
 
 // ---- GPU top-k over a count vector (BucketPriorityQueue replacement for large T) ----
 struct TopkParams {

@@ -1690,6 +1690,13 @@ static bool collect_partitioned(esgpu_plan* p, Pipeline& pl, const esgpu_segment
 #define ESGPU_NO_HOT 0  // timing experiments: no hot set
 #endif
 
+// the postings hot pass reads the 16-bit hot-slot column (ESGPU_HOT16=0: the 32-bit recoded column, for A/B runs)
+static bool hc_hot16() {
+    static const bool on = [] { const char* e = std::getenv("ESGPU_HOT16"); return !(e && *e == '0'); }();
+    return on;
+}
+static_assert(ESGPU_HOT_MAX <= 0xFFFF, "hot slots must fit the 16-bit column");
+
 struct HcStats {
     const void* src = nullptr;   // the ordinal buffer described (DevColumn::ords())
     uint64_t T = 0;
@@ -1699,6 +1706,7 @@ struct HcStats {
     uint64_t hot_docs = 0, docs = 0;
     bool refused = false;        // outside what the hot/cold kernels handle (cached: the check counts the column)
     DevBuf d_rc;                 // recoded ordinal column (hot ordinals as kHcHotBit | slot); empty: no hot set
+    DevBuf d_hot16;              // the hot slot of each doc in 16 bits (0xFFFF: cold / missing) for the postings hot pass
     DevBuf d_hot_ord, d_part, d_piece;
     // cold lists: the cold docs' partition-local offsets grouped by partition (postings of the cold ordinals, 64-element
     // aligned per partition), read by requests without predicates or accept bits instead of scattering the cold docs
@@ -1889,6 +1897,11 @@ static std::shared_ptr<const HcStats> ensure_hc_stats(esgpu_ctx* c, const DevCol
         hs->d_rc.alloc(c, (size_t)s->n_pad * 4);
         launch_hc_recode((const uint32_t*)src, s->n_pad, dk.as<uint32_t>(), dv.as<uint32_t>(), log2, hs->d_rc.as<uint32_t>(), st);
         HIPX(hipGetLastError());
+        if (ESGPU_HC_POSTINGS && hc_hot16()) {  // slots < ESGPU_HOT_MAX (16,384) fit 16 bits beside the 0xFFFF sentinel
+            hs->d_hot16.alloc(c, (size_t)s->n_pad * 2);
+            launch_hc_hot16(hs->d_rc.as<uint32_t>(), s->n_pad, hs->d_hot16.as<uint16_t>(), st);
+            HIPX(hipGetLastError());
+        }
         hs->d_hot_ord.alloc(c, hot.size() * 4);
         HIPX(hipMemcpy(hs->d_hot_ord.p, hot.data(), hot.size() * 4, hipMemcpyHostToDevice));
         HIPX(hipStreamSynchronize(st));  // the table buffers are released on return
@@ -2026,6 +2039,7 @@ static bool collect_hotcold(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s,
         Hh.blocks_per_wg = std::max(1u, (Hh.n_blocks + Hh.G - 1) / Hh.G);
         Hh.G = std::max(1u, (Hh.n_blocks + Hh.blocks_per_wg - 1) / Hh.blocks_per_wg);
         Hh.hot_slab = Hh.hot_n ? (uint32_t*)p->s_hslab.ensure(c, (size_t)hc_slab_stride(Hh.hot_n) * Hh.G * 4) : nullptr;
+        Hh.rc16 = hs->d_hot16.p ? hs->d_hot16.as<uint16_t>() : nullptr;
         HIPX(hipEventRecord(pl.e0, st));
         launch_hotcold_postings(Hh, K, st);
         HIPX(hipGetLastError());

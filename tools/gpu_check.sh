@@ -73,6 +73,11 @@ for s in $STEPS; do
               run kbench_c3_125m 300 python3 "$R/tools/kbench.py" --docs 125000000 --reps 5 --only config3_url &&
               run kbench_c3_125m_del 300 python3 "$R/tools/kbench.py" --docs 125000000 --reps 5 --only config3_url --deletes 0.01 &&
               run bench_config3 300 python3 "$R/bench.py" --workload config3 --shards 8 --docs 125000000 --cpu-docs 0 ;;
+        hot16ab) # config 3 postings hot pass: 32-bit recoded column vs the 16-bit hot-slot column, clean and 1 % deleted
+              for h in 0 1; do for d in 0 0.01; do
+                  ESGPU_HOT16=$h run "kbench_c3_hot16_${h}_del$d" 300 python3 "$R/tools/kbench.py" --docs 125000000 --reps 7 \
+                      --only config3_url --deletes $d || exit 1
+              done; done ;;
         smoke) run smoke 300 python3 -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke()" ;;
         inflightab) # requests in flight: 2 / 3 / 4 (north star 1 x 1B and 8 x 125M)
               for d in 2 3 4; do
