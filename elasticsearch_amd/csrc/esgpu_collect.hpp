@@ -29,6 +29,9 @@ constexpr uint32_t kGroup = kGroupBlocks;  // blocks per multi-pass group (esgpu
 #ifndef ESGPU_NBUF_NARROW  // load buffers in flight per thread for shapes reading one narrow column
 #define ESGPU_NBUF_NARROW 2  // measured: 4 no faster for terms(host), 4 % slower for date_histogram
 #endif
+#ifndef ESGPU_NBUF_COMPACT  // load buffers of the metric / two-dimension shapes over compact columns
+#define ESGPU_NBUF_COMPACT 2
+#endif
 
 struct Doc4 {
     uint32_t ord[kVec];
@@ -54,6 +57,14 @@ __device__ __forceinline__ u32x4_t load16(const void* p) {
     return __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
 #else
     return *reinterpret_cast<const u32x4_t*>(p);
+#endif
+}
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u32x2_t load8(const void* p) {
+#if ESGPU_NT
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(p));
+#else
+    return *reinterpret_cast<const u32x2_t*>(p);
 #endif
 }
 __device__ __forceinline__ uint64_t join64(uint32_t lo, uint32_t hi) { return (uint64_t)lo | ((uint64_t)hi << 32); }
@@ -100,6 +111,8 @@ __device__ __forceinline__ uint32_t eval_pred(const PredDev& q, uint32_t doc0) {
 
 // VK (value kinds, compile time): bit 0 = the histogram column holds doubles (keys are (long) casts), bit 1 = the
 // metric column holds doubles (else longs cast to double).  A runtime branch on these cost the north-star kernel ~6 %.
+// Compact columns (segment products built on first use): bit 16 = the terms dimension is read from the
+// 16-bit ordinal column (0xFFFF missing), bit 32 = the histogram column from its 32-bit deltas over hv_base.
 template <bool ORD, bool HIST, int MET, int VK>
 __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0, Doc4& d) {
     uint32_t ok = 0xF;
@@ -118,6 +131,11 @@ __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0,
             d.ord[j] = ((pres >> j) & 1) && u < P.ord_span ? magic_div((uint32_t)u, P.omg_m, P.omg_s1, P.omg_s2, P.ord_div)
                                                            : kMissingOrd;
         }
+    } else if (ORD && (VK & 16)) {
+        const u32x2_t w = load8(P.ord16 + doc0);
+        const uint32_t x[4] = {w.x & 0xFFFFu, w.x >> 16, w.y & 0xFFFFu, w.y >> 16};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d.ord[j] = x[j] == 0xFFFFu ? kMissingOrd : x[j];
     } else if (ORD) {
         load_u32x4(P.ord, doc0, d.ord);
     }
@@ -131,6 +149,12 @@ __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0,
             pres |= (uint32_t)(o[j] < P.H) << j;
         }
         d.hpres = pres;
+    } else if (HIST && (VK & 32)) {
+        uint32_t o[4];
+        load_u32x4(P.hv32, doc0, o);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d.hv[j] = P.hv_base + (int64_t)o[j];
+        d.hpres = P.hv_present ? bits4(P.hv_present, doc0) : 0xFu;
     } else if (HIST) {
         load_i64x4(P.hv, doc0, d.hv);
         if (VK & 1) {
@@ -643,7 +667,7 @@ __global__ __launch_bounds__(WGS) void collect_kernel(CollectParams P) {
     const uint32_t tid4 = threadIdx.x * kVec;
     // shapes that read few bytes per doc (one ordinal or one key column) keep 4 buffers in flight, the rest 2 (their
     // buffers are 5x larger; 4 would cost occupancy).  kItersPerBlockW (4) is a multiple of either.
-    constexpr int kBuf = (MET == 0 && !(ORD && HIST)) ? ESGPU_NBUF_NARROW : 2;
+    constexpr int kBuf = (MET == 0 && !(ORD && HIST)) ? ESGPU_NBUF_NARROW : ((VK & 48) ? (ESGPU_NBUF_COMPACT <= kItersPerBlockW ? ESGPU_NBUF_COMPACT : kItersPerBlockW) : 2);
     static_assert(kItersPerBlockW % kBuf == 0, "buffers per block");
     Doc4 q[kBuf];
 #pragma unroll
@@ -802,12 +826,27 @@ static auto with_vk0(bool hv_f64, bool mv_f64, F f) {
         return f(std::integral_constant<int, 0>{});
     }
 }
-// VK bit 8: the terms dimension is a derived histogram key index (CollectParams.ord_src); only for ORD x histogram grids
+// VK bit 8: the terms dimension is a derived histogram key index (CollectParams.ord_src); only for ORD x histogram grids.
+// Bits 16 / 32 (compact ordinal / histogram columns): terms dimensions without a derived key index, affine histograms
+// over a long column.
 template <bool ORD, int HK, int MET, class F>
-static auto with_vk(bool hv_f64, bool mv_f64, bool dord, F f) {
+static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, F f) {
     if constexpr (ORD && (HK == 1 || HK == 2)) {
         if (dord)
             return with_vk0<HK, MET>(hv_f64, mv_f64, [&](auto vk) { return f(std::integral_constant<int, decltype(vk)::value | 8>{}); });
+    }
+    if constexpr (HK == 1) {
+        if (t32 && !hv_f64) {
+            if constexpr (ORD) {
+                if (c16)
+                    return with_vk0<HK, MET>(false, mv_f64, [&](auto vk) { return f(std::integral_constant<int, decltype(vk)::value | 48>{}); });
+            }
+            return with_vk0<HK, MET>(false, mv_f64, [&](auto vk) { return f(std::integral_constant<int, decltype(vk)::value | 32>{}); });
+        }
+    }
+    if constexpr (ORD && (HK == 0 || HK == 1)) {
+        if (c16)
+            return with_vk0<HK, MET>(hv_f64, mv_f64, [&](auto vk) { return f(std::integral_constant<int, decltype(vk)::value | 16>{}); });
     }
     return with_vk0<HK, MET>(hv_f64, mv_f64, f);
 }
@@ -823,7 +862,7 @@ static auto with_wg(bool wide, F f) {
 
 template <bool ORD, int HK, int MET>
 static void launch_t(const CollectParams& p, bool wide, uint32_t grid, size_t lds, hipStream_t st) {
-    with_vk<ORD, HK, MET>(p.hv_f64 != 0, p.mv_f64 != 0, p.ord_src != nullptr, [&](auto vk) {
+    with_vk<ORD, HK, MET>(p.hv_f64 != 0, p.mv_f64 != 0, p.ord_src != nullptr, p.ord16 != nullptr, p.hv32 != nullptr, [&](auto vk) {
         return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
             hipLaunchKernelGGL((collect_kernel<ORD, HK, MET, decltype(vk)::value, decltype(wg)::value>), dim3(grid),
                                dim3(decltype(wg)::value), lds, st, p);
@@ -844,7 +883,8 @@ static void launch_m(const CollectParams& p, int met, bool wide, uint32_t grid, 
 
 template <bool ORD, int HK, int MET>
 static int occ_t(size_t lds, int vkbits, bool wide) {
-    return with_vk<ORD, HK, MET>((vkbits & 1) != 0, (vkbits & 2) != 0, (vkbits & 8) != 0, [&](auto vk) {
+    return with_vk<ORD, HK, MET>((vkbits & 1) != 0, (vkbits & 2) != 0, (vkbits & 8) != 0, (vkbits & 16) != 0,
+                                 (vkbits & 32) != 0, [&](auto vk) {
         return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
             int n = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(

@@ -902,6 +902,25 @@ void launch_remap_ords(const uint32_t* in, uint32_t n, const uint32_t* map, uint
     hipLaunchKernelGGL(remap_ords_kernel, dim3(grid), dim3(256), 0, st, in, n, map, map_n, out);
 }
 
+// compact columns: ordinals in 16 bits (kMissingOrd -> 0xFFFF; only for dictionaries under 65,535 terms) and long
+// values as 32-bit deltas over the column's minimum (a missing value's delta is never read: the present bits decide)
+__global__ void pack_ord16_kernel(const uint32_t* src, uint32_t n, uint16_t* out) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t o = src[i];
+        out[i] = o == kMissingOrd ? (uint16_t)0xFFFFu : (uint16_t)o;
+    }
+}
+void launch_pack_ord16(const uint32_t* src, uint32_t n, uint16_t* out, hipStream_t st) {
+    if (n) hipLaunchKernelGGL(pack_ord16_kernel, dim3(std::min<uint32_t>(8192, (n + 255) / 256)), dim3(256), 0, st, src, n, out);
+}
+__global__ void delta32_kernel(const int64_t* v, uint32_t n, int64_t base, uint32_t* out) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        out[i] = (uint32_t)((uint64_t)v[i] - (uint64_t)base);
+}
+void launch_delta32(const int64_t* v, uint32_t n, int64_t base, uint32_t* out, hipStream_t st) {
+    if (n) hipLaunchKernelGGL(delta32_kernel, dim3(std::min<uint32_t>(8192, (n + 255) / 256)), dim3(256), 0, st, v, n, base, out);
+}
+
 __global__ void pack_u8_kernel(const unsigned int* src, uint32_t n, uint8_t* dst) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) dst[i] = (uint8_t)src[i];
 }

@@ -58,6 +58,11 @@ struct CollectParams {
     // terms dimension
     const uint32_t* ord;
     uint32_t T;
+    // compact columns (loader VK bits 16 / 32): the ordinals as u16 (0xFFFF missing), the histogram column's long values
+    // as u32 deltas over hv_base (a missing value's delta is 0; hv_present still decides)
+    const uint16_t* ord16;
+    const uint32_t* hv32;
+    int64_t hv_base;
     // histogram under histogram, fused (loader VK bit 8): the terms dimension is the inner histogram's key index,
     // derived from its i64 / f64 column as t = (v - ord_base) / ord_div when 0 <= v - ord_base < ord_span (a 32-bit
     // magic division; ord_span = keys x interval < 2^32), else missing -- no materialised ordinal column
@@ -258,6 +263,8 @@ void launch_murmur3_field(const uint8_t* bytes, const uint64_t* offsets, uint64_
 // min / max over a value array (multi-valued i64 columns: key range of a histogram), out[0] = min, out[1] = max
 void launch_minmax_i64(const int64_t* v, uint64_t n, int64_t* out, bool f64, hipStream_t s);
 void launch_widen_u32(const unsigned int* src, size_t n, unsigned long long* dst, hipStream_t st);
+void launch_pack_ord16(const uint32_t* src, uint32_t n, uint16_t* out, hipStream_t st);
+void launch_delta32(const int64_t* v, uint32_t n, int64_t base, uint32_t* out, hipStream_t st);
 void launch_comp_ords(const uint32_t* a, const uint32_t* b, uint32_t n_pad, uint32_t na, uint32_t nb, const uint32_t* amap,
                       uint32_t amap_n, uint32_t* out, hipStream_t st);
 void launch_hist_ords(const int64_t* v, const uint64_t* present, uint32_t n_docs, uint32_t n_pad, bool f64, int64_t interval,

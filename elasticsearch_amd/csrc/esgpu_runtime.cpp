@@ -273,6 +273,12 @@ struct DevColumn {
     // statistics of ords() for high-cardinality terms, built on first use (ensure_hc_stats); rebuilt when ords() is
     // replaced by a remap into another global dictionary
     std::shared_ptr<const HcStats> hc;
+    // compact copies the collect kernel's loader reads instead (ensure_ord16 / ensure_d32, built on first use and cached
+    // with the column): ords() in 16 bits (0xFFFF missing) while the dictionary has fewer than 65,535 terms -- keyed by
+    // the ords() buffer it was made from -- and a long column's values as 32-bit deltas over vmin while vmax - vmin < 2^32
+    DevBuf ord16, d32;
+    const void* ord16_src = nullptr;
+    bool d32_done = false;
 
     const DevBuf& ords() const { return gdict ? gvalues : values; }       // what terms aggregations count by
     uint64_t ord_count() const { return gdict ? gdict->count() : value_count; }
@@ -2101,6 +2107,9 @@ static bool collect_multi(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, C
 }
 
 static void ensure_ord_hash(esgpu_ctx* c, const DevColumn* col, hipStream_t st);
+static bool compact_cols();
+static const uint16_t* ensure_ord16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
+static const uint32_t* ensure_d32(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
 
 // re-shape an allocated grid to newT ordinal columns, the old columns landing at column `shift` (histogram under
 // histogram: a later segment widens the inner key range).  Rows are [T] cells, so every array moves as a strided 2D
@@ -2598,6 +2607,19 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     const int ret = inner_missing ? 2 : 1;
     if (multi) return collect_multi(p, pl, s, P, L_ORD ? oc : nullptr, L_HIST ? hc : nullptr, inner_missing ? nullptr : mc, L_met,
                                     d_accept) ? ret : 0;
+    // compact columns: 2 B per ordinal instead of 4, 4 B per timestamp instead of 8 -- the bytes the layout moves; the
+    // reported (algorithmic) bytes stay SURVEY §8(d)'s per-doc figure of the upload-width columns
+    if (compact_cols()) {
+        const bool plain_ord = oc && !pl.comp && !pl.ord_hist && oc == s->col(pl.ord_field.c_str());
+        if (L_ORD && P.ord && plain_ord && !oc->multi && oc->ord_count() < 0xFFFFu) {
+            P.ord16 = ensure_ord16(p->ctx, oc, s, p->stream);
+        }
+        if (L_HIST && hc && !pl.inner_terms && !P.kstart && hc->type == ESGPU_COL_I64 && !hc->multi && hc->vmin <= hc->vmax &&
+            (uint64_t)hc->vmax - (uint64_t)hc->vmin < (1ull << 32)) {
+            P.hv32 = ensure_d32(p->ctx, hc, s, p->stream);
+            if (P.hv32) P.hv_base = hc->vmin;
+        }
+    }
 
     // LDS sizing: the whole grid if it fits, else a sliding window over the key dimension (time-sorted data)
 #ifndef ESGPU_LDS_PAIR  // LDS budget of a window that keeps two workgroups per CU
@@ -2672,7 +2694,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         P.mg_m = mg.m; P.mg_s1 = mg.s1; P.mg_s2 = mg.s2;
     }
     const int hk = L_HIST ? (P.hord ? 3 : P.kstart ? 2 : 1) : 0;
-    const int vk = (P.hv_f64 ? 1 : 0) | (P.mv_f64 ? 2 : 0) | (P.ord_src ? 8 : 0);
+    const int vk = (P.hv_f64 ? 1 : 0) | (P.mv_f64 ? 2 : 0) | (P.ord_src ? 8 : 0) | (P.ord16 ? 16 : 0) | (P.hv32 ? 32 : 0);
     const uint64_t occ_key = ((uint64_t)lds << 16) | ((uint64_t)wide << 15) | ((uint64_t)vk << 8) | ((uint64_t)L_met << 4) |
                              ((uint64_t)hk << 1) | (L_ORD ? 1 : 0);
     if (pl.occ_key != occ_key) {
@@ -2724,6 +2746,49 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     p->last_bytes += bytes_per_doc * (uint64_t)s->max_doc + (d_accept ? ((uint64_t)s->max_doc + 7) / 8 : 0);
     p->last_path = P.lds_mode ? (P.windowed ? 2 : 1) : 0;
     return ret;
+}
+
+// Compact columns: a segment's ordinals and timestamps need fewer bits than their upload width -- Lucene
+// stores them bit-packed / delta-coded for the same reason -- and the collect loop is HBM-bound, so the single-valued
+// collect kernel reads 16-bit ordinals and 32-bit timestamp deltas when the segment's values fit (ESGPU_COMPACT=0: the
+// upload-width columns, for A/B runs).  Built once per column under the context lock (plans on other threads may share
+// the segment); an allocation over the HBM budget leaves the column as it is.
+static bool compact_cols() {
+    static const bool on = [] { const char* e = std::getenv("ESGPU_COMPACT"); return !(e && *e == '0'); }();
+    return on;
+}
+static const uint16_t* ensure_ord16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st) {
+    DevColumn* m = const_cast<DevColumn*>(col);
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (m->ord16.p && m->ord16_src == col->ords().p) return m->ord16.as<uint16_t>();
+    if (m->ord16_src == col->ords().p) return nullptr;  // tried: over the budget
+    m->ord16_src = col->ords().p;
+    try {
+        m->ord16.alloc(c, (size_t)s->n_pad * 2);
+    } catch (const EsError&) {
+        m->ord16.release();
+        return nullptr;
+    }
+    launch_pack_ord16(col->ords().as<uint32_t>(), s->n_pad, m->ord16.as<uint16_t>(), st);
+    HIPX(hipGetLastError());
+    HIPX(hipStreamSynchronize(st));
+    return m->ord16.as<uint16_t>();
+}
+static const uint32_t* ensure_d32(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st) {
+    DevColumn* m = const_cast<DevColumn*>(col);
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (m->d32_done) return m->d32.as<uint32_t>();
+    m->d32_done = true;
+    try {
+        m->d32.alloc(c, (size_t)s->n_pad * 4);
+    } catch (const EsError&) {
+        m->d32.release();
+        return nullptr;
+    }
+    launch_delta32(col->values.as<int64_t>(), s->n_pad, col->vmin, m->d32.as<uint32_t>(), st);
+    HIPX(hipGetLastError());
+    HIPX(hipStreamSynchronize(st));
+    return m->d32.as<uint32_t>();
 }
 
 static void ensure_ord_hash(esgpu_ctx* c, const DevColumn* col, hipStream_t st) {

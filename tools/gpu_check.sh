@@ -78,6 +78,11 @@ for s in $STEPS; do
                   ESGPU_HOT16=$h run "kbench_c3_hot16_${h}_del$d" 300 python3 "$R/tools/kbench.py" --docs 125000000 --reps 7 \
                       --only config3_url --deletes $d || exit 1
               done; done ;;
+        compactab) # compact columns (16-bit ordinals, 32-bit timestamp deltas) vs the upload-width columns
+              for c in 1 0; do for docs in 1000000000 125000000; do
+                  ESGPU_COMPACT=$c run "kbench_compact${c}_$docs" 400 python3 "$R/tools/kbench.py" --docs $docs --reps 5 \
+                      --only terms_host,date_hist,config2_dh_ext,terms_dh,config1_terms_stats,north_star,config5,dh_terms,heatmap || exit 1
+              done; done ;;
         smoke) run smoke 300 python3 -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke()" ;;
         inflightab) # requests in flight: 2 / 3 / 4 (north star 1 x 1B and 8 x 125M)
               for d in 2 3 4; do
