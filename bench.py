@@ -370,7 +370,7 @@ def main():
             first.append((time.perf_counter() - t0) * 1e3 - k_ms)
             hbm.append(engine.hbm_used() - h0)
         p.build()
-        if sum(hbm) > 0:
+        if sum(hbm) >= 2 * args.docs * len(segs):  # at least 2 B per doc: compact columns were built
             precomputed = {"what": "compact columns of the segment (u16 ordinals / u32 timestamp deltas, cached with it; "
                                    "the first segment's figure includes the plan's grid)",
                            "build_ms_per_segment": round(sum(first) / len(first), 3),
