@@ -29,6 +29,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+# bytes per doc of the request's columns at their upload width
+UPLOAD_BYTES = {"north_star": 20, "config2": 16, "config3": 4, "config4": 8, "config5": 36}
 
 WORKLOADS = {
     # name: (fields, builder fn, filters fn, description, number_of_docs default)
@@ -449,6 +451,12 @@ def main():
                        "parallelism": f"{per_gpu} shard(s) per GPU x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+                         # bytes per doc of the GPU layout (compact columns) against the upload-width figure of
+                         # SURVEY §8(d); effective = the upload-width bytes over the kernel time
+                         "bytes_per_doc": round(bytes_per_step / max(args.docs * per_gpu, 1), 3),
+                         "upload_width_bytes_per_doc": UPLOAD_BYTES.get(args.workload),
+                         "effective_gbs": UPLOAD_BYTES[args.workload] * args.docs * per_gpu / (avg_kernel_ms / 1000.0) / 1e9
+                                          if args.workload in UPLOAD_BYTES else None,
                          "kernel": "collect_kernel", "kernel_ms": avg_kernel_ms * args.steps / launches,
                          "algorithmic_bytes_per_launch": kernel_bytes[0] // launches},
             "exchange": exchange,

@@ -99,6 +99,14 @@ __device__ __forceinline__ uint32_t eval_pred(const PredDev& q, uint32_t doc0) {
             const bool hi = q.hi_incl ? v[j] <= q.dhi : v[j] < q.dhi;
             m |= (uint32_t)(lo && hi) << j;
         }
+    } else if (q.kind == PRED_D32_RANGE) {
+        uint32_t o[4];
+        load_u32x4((const uint32_t*)q.col, doc0, o);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t v = q.base + (int64_t)o[j];
+            m |= (uint32_t)(v >= q.lo && v <= q.hi) << j;
+        }
     } else {  // PRED_I64_RANGE (term on a long is the degenerate range [t, t])
         int64_t v[4];
         load_i64x4((const int64_t*)q.col, doc0, v);

@@ -1616,6 +1616,9 @@ __device__ bool pred_doc(const PredDev& q, uint32_t d) {
         } else if (q.kind == PRED_F64_RANGE) {
             const double v = ((const double*)q.col)[i];
             m = (q.lo_incl ? v >= q.dlo : v > q.dlo) && (q.hi_incl ? v <= q.dhi : v < q.dhi);
+        } else if (q.kind == PRED_D32_RANGE) {
+            const int64_t v = q.base + (int64_t)((const uint32_t*)q.col)[i];
+            m = v >= q.lo && v <= q.hi;
         } else {
             const int64_t v = ((const int64_t*)q.col)[i];
             m = v >= q.lo && v <= q.hi;

@@ -35,7 +35,8 @@ constexpr uint32_t kGroupBlocks = ESGPU_GROUP_BLOCKS;
 #define ESGPU_DYN_CLAIM 0
 #endif
 constexpr int kMaxPreds = 4;  // clauses a collect kernel evaluates itself (more: folded into a doc bitset first)
-enum PredKind : int32_t { PRED_ORD_EQ = 0, PRED_I64_RANGE = 1, PRED_F64_RANGE = 2, PRED_ORD_RANGE = 3 };
+// PRED_D32_RANGE: an I64 range over the column's compact copy (u32 deltas over `base`)
+enum PredKind : int32_t { PRED_ORD_EQ = 0, PRED_I64_RANGE = 1, PRED_F64_RANGE = 2, PRED_ORD_RANGE = 3, PRED_D32_RANGE = 4 };
 
 struct PredDev {
     const void* col;
@@ -45,6 +46,7 @@ struct PredDev {
     int32_t lo_incl, hi_incl, pad;
     int64_t lo, hi;    // ORD_EQ: lo = ordinal; I64_RANGE / ORD_RANGE: inclusive [lo, hi]
     double dlo, dhi;   // F64_RANGE with include flags
+    int64_t base;      // D32_RANGE: value = base + delta
 };
 
 // separate outer-level doc counts: TERMS / HIST = counted per doc (the inner column has missing values);

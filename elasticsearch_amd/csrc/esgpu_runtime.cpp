@@ -1530,6 +1530,10 @@ static bool applies(const esgpu_plan* p, const Pipeline& pl, size_t k) {
     return p->filter_owner[k] < 0 || p->filter_owner[k] == pl.fspec;
 }
 
+static bool compact_cols();
+static const uint16_t* ensure_ord16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
+static const uint32_t* ensure_d32(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
+
 // The pipeline's clauses as device predicates: up to kMaxPreds of them are evaluated inside the collect kernels; with
 // more, all of them (and the accept bitset) are folded first into one doc bitset -- chained filter_bits passes of four
 // clauses each -- which replaces *accept, and no predicate is left for the kernel.
@@ -1605,7 +1609,16 @@ static void set_preds(esgpu_plan* p, const Pipeline& pl, const esgpu_segment* s,
                 q.lo = lo;
                 q.hi = hi;
             }
-            *bytes_per_doc += 8;
+            // single-valued: the compact copy of the column (u32 deltas) when its values span < 2^32
+            if (compact_cols() && !col->multi && col->vmin <= col->vmax &&
+                (uint64_t)col->vmax - (uint64_t)col->vmin < (1ull << 32)) {
+                if (const uint32_t* d = ensure_d32(p->ctx, col, s, p->stream)) {
+                    q.col = d;
+                    q.kind = PRED_D32_RANGE;
+                    q.base = col->vmin;
+                }
+            }
+            *bytes_per_doc += q.kind == PRED_D32_RANGE ? 4 : 8;
         }
         all.push_back(q);
     }
@@ -2046,6 +2059,8 @@ static bool collect_hotcold(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s,
         Hh.G = std::max(1u, (Hh.n_blocks + Hh.blocks_per_wg - 1) / Hh.blocks_per_wg);
         Hh.hot_slab = Hh.hot_n ? (uint32_t*)p->s_hslab.ensure(c, (size_t)hc_slab_stride(Hh.hot_n) * Hh.G * 4) : nullptr;
         Hh.rc16 = hs->d_hot16.p ? hs->d_hot16.as<uint16_t>() : nullptr;
+        if (Hh.rc16)  // the bytes this form moves: 2 B per doc of hot slots plus 2 B per listed cold doc (not 4 B per doc)
+            p->last_bytes = p->last_bytes - 2ull * s->max_doc + 2ull * (hs->docs - hs->hot_docs);
         HIPX(hipEventRecord(pl.e0, st));
         launch_hotcold_postings(Hh, K, st);
         HIPX(hipGetLastError());
@@ -2107,9 +2122,6 @@ static bool collect_multi(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, C
 }
 
 static void ensure_ord_hash(esgpu_ctx* c, const DevColumn* col, hipStream_t st);
-static bool compact_cols();
-static const uint16_t* ensure_ord16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
-static const uint32_t* ensure_d32(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
 
 // re-shape an allocated grid to newT ordinal columns, the old columns landing at column `shift` (histogram under
 // histogram: a later segment widens the inner key range).  Rows are [T] cells, so every array moves as a strided 2D
@@ -2607,17 +2619,21 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     const int ret = inner_missing ? 2 : 1;
     if (multi) return collect_multi(p, pl, s, P, L_ORD ? oc : nullptr, L_HIST ? hc : nullptr, inner_missing ? nullptr : mc, L_met,
                                     d_accept) ? ret : 0;
-    // compact columns: 2 B per ordinal instead of 4, 4 B per timestamp instead of 8 -- the bytes the layout moves; the
-    // reported (algorithmic) bytes stay SURVEY §8(d)'s per-doc figure of the upload-width columns
+    // compact columns: 2 B per ordinal instead of 4, 4 B per timestamp instead of 8 -- the reported (algorithmic) bytes
+    // are the bytes this layout must move (SURVEY §8(d)'s upload-width figure would put config 5 above the HBM peak)
     if (compact_cols()) {
         const bool plain_ord = oc && !pl.comp && !pl.ord_hist && oc == s->col(pl.ord_field.c_str());
         if (L_ORD && P.ord && plain_ord && !oc->multi && oc->ord_count() < 0xFFFFu) {
             P.ord16 = ensure_ord16(p->ctx, oc, s, p->stream);
+            if (P.ord16) bytes_per_doc -= 2;
         }
         if (L_HIST && hc && !pl.inner_terms && !P.kstart && hc->type == ESGPU_COL_I64 && !hc->multi && hc->vmin <= hc->vmax &&
             (uint64_t)hc->vmax - (uint64_t)hc->vmin < (1ull << 32)) {
             P.hv32 = ensure_d32(p->ctx, hc, s, p->stream);
-            if (P.hv32) P.hv_base = hc->vmin;
+            if (P.hv32) {
+                P.hv_base = hc->vmin;
+                bytes_per_doc -= 4;
+            }
         }
     }
 
