@@ -29,6 +29,9 @@ constexpr uint32_t kGroup = kGroupBlocks;  // blocks per multi-pass group (esgpu
 #ifndef ESGPU_NBUF_NARROW  // load buffers in flight per thread for shapes reading one narrow column
 #define ESGPU_NBUF_NARROW 2  // measured: 4 no faster for terms(host), 4 % slower for date_histogram
 #endif
+#ifndef ESGPU_MINMAX_CHECK
+#define ESGPU_MINMAX_CHECK 1
+#endif
 #ifndef ESGPU_NBUF_COMPACT  // load buffers of the metric / two-dimension shapes over compact columns
 #define ESGPU_NBUF_COMPACT 2
 #endif
@@ -215,10 +218,16 @@ __device__ __forceinline__ void add_value(const Acc& a, uint32_t c, double x, bo
         const unsigned long long emn = nan ? 0ull : e;
         const unsigned long long emx = nan ? ~0ull : e;
         // read-check before the atomic: reads of one address broadcast, and min/max converge quickly
+        // (ESGPU_MINMAX_CHECK=0: unconditional no-return atomics -- no LDS read to wait on -- for A/B runs)
         constexpr uint32_t st = LDS ? MS : 1;
+#if ESGPU_MINMAX_CHECK
         const unsigned long long cmn = a.mn[c * st], cmx = a.mx[c * st];
         if (emn < cmn) atomicMin(&a.mn[c * st], emn);
         if (emx > cmx) atomicMax(&a.mx[c * st], emx);
+#else
+        atomicMin(&a.mn[c * st], emn);
+        atomicMax(&a.mx[c * st], emx);
+#endif
     }
     if (MET >= 3) atomicAdd(&a.sq[ca], x * x);  // ExtendedStatsAggregator: sumOfSqr += value * value (no FMA)
 }
