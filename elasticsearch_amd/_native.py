@@ -123,6 +123,8 @@ SIGNATURES = [
     ("esgpu_ctx_create", ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, _PP]),
     ("esgpu_ctx_destroy", ctypes.c_int, [_VP]),
     ("esgpu_ctx_hbm_used", ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_uint64)]),
+    ("esgpu_ctx_set_option", ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_int64]),
+    ("esgpu_ctx_get_option", ctypes.c_int, [_VP, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]),
     ("esgpu_device_count", ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     ("esgpu_host_alloc", ctypes.c_int, [ctypes.c_size_t, _PP]),
     ("esgpu_host_free", ctypes.c_int, [_VP]),

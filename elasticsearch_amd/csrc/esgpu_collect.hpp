@@ -35,11 +35,15 @@ constexpr uint32_t kGroup = kGroupBlocks;  // blocks per multi-pass group (esgpu
 #ifndef ESGPU_NBUF_COMPACT  // load buffers of the metric / two-dimension shapes over compact columns
 #define ESGPU_NBUF_COMPACT 2
 #endif
+#ifndef ESGPU_NBUF_PI  // load buffers with packed integer metric cells (all columns compact)
+#define ESGPU_NBUF_PI 2
+#endif
 
 struct Doc4 {
     uint32_t ord[kVec];
     int64_t hv[kVec];
     double mv[kVec];
+    uint32_t mvd[kVec];  // VK bit 64: the metric's u32 deltas over P.mv_base
     uint32_t ok;      // bit j: doc j passes filters / accept / bounds
     uint32_t hpres;   // bit j: hist value present
     uint32_t mpres;   // bit j: metric value present
@@ -174,7 +178,10 @@ __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0,
         }
         d.hpres = P.hv_present ? bits4(P.hv_present, doc0) : 0xFu;
     }
-    if (MET > 0) {
+    if (MET > 0 && (VK & 64)) {  // packed integer cells: a dense long metric as its compact u32 deltas
+        load_u32x4(P.mv32, doc0, d.mvd);
+        d.mpres = 0xFu;
+    } else if (MET > 0) {
         if (VK & 2) {
             load_f64x4((const double*)P.mv, doc0, d.mv);
         } else {
@@ -201,6 +208,8 @@ struct Acc {
     unsigned long long* ocnt64;
     uint32_t mstride;               // LDS min/max stride; 1 in the global grid
     uint32_t coff;                  // this lane's copy of the additive LDS cells (CollectParams.ncopies); 0 in the grid
+    unsigned long long* pk;         // LDS, packed integer cells (VK bit 64): count << pk_shift | sum of deltas [C][ncopies]
+    uint32_t* mm;                   // LDS, packed integer cells: (min, max) delta pair per cell [C][2]
 };
 
 template <int MET, bool LDS, int MS>
@@ -421,7 +430,7 @@ __device__ __forceinline__ void combine4(uint32_t (&k)[kVec], F emit) {
     }
 }
 
-template <bool ORD, bool HIST, int MET, bool LDS, bool KT, int MS, bool HORD = false>
+template <bool ORD, bool HIST, int MET, bool LDS, bool KT, int MS, bool HORD = false, int VK = 0>
 __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, const Doc4& d, uint32_t T, int64_t base,
                                          uint32_t win0, Runs<runs_for<MET>()>& run, uint32_t mw = 0, bool outer = true) {
     uint32_t slot[kVec];
@@ -457,6 +466,50 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
         for (int j = 0; j < kVec; ++j) {
             if (!((d.ok >> j) & 1) || !hv_ok[j]) continue;
             runs_add<MET, MS>(P, a, run, slot[j], MET > 0 && ((d.mpres >> j) & 1), MET > 0 ? d.mv[j] : 0.0);
+        }
+        return;
+    }
+    if constexpr (LDS && ORD && MET > 0 && (VK & 64)) {
+        // packed integer cells: one ds_add_u64 per doc carries count and sum; the 4 docs' (min, max) pairs are read
+        // first with one wait for all four (the read-check is only a filter: a stale pair costs an extra atomic), so the
+        // thread waits once per 4 docs instead of once per doc behind the queued atomics
+        uint32_t cell[kVec], hit = 0;
+#pragma unroll
+        for (int j = 0; j < kVec; ++j) {
+            const uint32_t t = d.ord[j];
+            const bool ok = (d.ok >> j) & 1, has_t = t != kMissingOrd && t < T;
+            if (P.ocnt_mode == OCNT_TERMS) {
+                if (ok && has_t && outer) atomicAdd(&a.ocnt32[t], 1u);
+            } else if (P.ocnt_mode == OCNT_HIST) {
+                if (ok && hv_ok[j]) atomicAdd(&a.ocnt32[slot[j]], 1u);
+            }
+            hit |= (uint32_t)(ok && hv_ok[j] && has_t) << j;
+            cell[j] = slot[j] * T + t;
+        }
+        uint32_t mlo[kVec], mhi[kVec];
+        if (MET >= 2) {
+#pragma unroll
+            for (int j = 0; j < kVec; ++j) {
+                mlo[j] = 0u;
+                mhi[j] = ~0u;
+                if ((hit >> j) & 1) {
+                    const u32x2_t m = *reinterpret_cast<const u32x2_t*>(a.mm + 2 * cell[j]);
+                    mlo[j] = m.x;
+                    mhi[j] = m.y;
+                }
+            }
+        }
+        const unsigned long long one = 1ull << P.pk_shift;
+#pragma unroll
+        for (int j = 0; j < kVec; ++j)
+            if ((hit >> j) & 1) atomicAdd(&a.pk[cell[j] + a.coff], one + d.mvd[j]);
+        if (MET >= 2) {
+#pragma unroll
+            for (int j = 0; j < kVec; ++j) {
+                if (!((hit >> j) & 1)) continue;
+                if (d.mvd[j] < mlo[j]) atomicMin(&a.mm[2 * cell[j]], d.mvd[j]);
+                if (d.mvd[j] > mhi[j]) atomicMax(&a.mm[2 * cell[j] + 1], d.mvd[j]);
+            }
         }
         return;
     }
@@ -502,9 +555,64 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
         if (!((d.ok >> j) & 1)) continue;
         const uint32_t t = ORD ? d.ord[j] : 0u;
         const bool has_t = ORD ? (t != kMissingOrd && t < T) : true;
-        update_doc<ORD, HIST, MET, LDS, MS>(P, a, T, has_t, t, hv_ok[j], slot[j], MET > 0 && ((d.mpres >> j) & 1),
-                                        MET > 0 ? d.mv[j] : 0.0, outer);
+        const double x = MET > 0 ? ((VK & 64) ? (double)(P.mv_base + (int64_t)d.mvd[j]) : d.mv[j]) : 0.0;
+        update_doc<ORD, HIST, MET, LDS, MS>(P, a, T, has_t, t, hv_ok[j], slot[j], MET > 0 && ((d.mpres >> j) & 1), x, outer);
     }
+}
+
+// packed integer cells (VK bit 64): decoded into the grid's u64 counts, f64 sums (the exact integer sum of the cell's
+// values, count * base + sum of deltas) and order-preserving extrema of (double) values -- (double) is monotonic on
+// longs, so the min / max of the casts are the casts of the min / max
+template <int MET, int WGS>
+__device__ void flush_window_pi(const CollectParams& P, const Acc& s, uint32_t T, uint32_t W, uint32_t win0, uint32_t ncp) {
+    __syncthreads();
+    const uint32_t C = T * W;
+    const uint32_t sh = P.pk_shift;
+    const unsigned long long mask = (1ull << sh) - 1ull;
+    if (P.ocnt_mode == OCNT_TERMS_DERIVED) {
+        for (uint32_t t = threadIdx.x; t < T; t += WGS) {
+            unsigned long long tot = 0;
+            for (uint32_t k = 0; k < ncp; ++k)
+                for (uint32_t l = 0; l < W; ++l) tot += s.pk[k * C + l * T + t];
+            tot >>= sh;
+            if (tot) atomicAdd(&P.g_ocnt[t], tot);
+        }
+        __syncthreads();
+    }
+    for (uint32_t c = threadIdx.x; c < C; c += WGS) {
+        unsigned long long n = 0;
+        for (uint32_t k = 0; k < ncp; ++k) n += s.pk[k * C + c];
+        if (n == 0) continue;
+        const uint32_t local = c / T;
+        const uint32_t t = c - local * T;
+        const uint32_t slot = win0 + local;
+        if (slot >= P.H) continue;
+        const size_t g = (size_t)slot * T + t;
+        const unsigned long long cnt = n >> sh;
+        atomicAdd(&P.g_cnt[g], cnt);
+        for (uint32_t k = 0; k < ncp; ++k) s.pk[k * C + c] = 0;
+        atomicAdd(&P.g_sum[g], (double)((long long)(n & mask) + (long long)cnt * P.mv_base));
+        if (MET >= 2) {
+            const uint32_t lo = s.mm[2 * c], hi = s.mm[2 * c + 1];
+            atomicMin(&P.g_min[g], sortable((double)(P.mv_base + (int64_t)lo)));
+            atomicMax(&P.g_max[g], sortable((double)(P.mv_base + (int64_t)hi)));
+            s.mm[2 * c] = ~0u;
+            s.mm[2 * c + 1] = 0u;
+        }
+    }
+    if (P.ocnt_mode == OCNT_TERMS) {
+        for (uint32_t t = threadIdx.x; t < T; t += WGS) {
+            const uint32_t n = s.ocnt32[t];
+            if (n) { atomicAdd(&P.g_ocnt[t], (unsigned long long)n); s.ocnt32[t] = 0; }
+        }
+    } else if (P.ocnt_mode == OCNT_HIST) {
+        for (uint32_t l = threadIdx.x; l < W; l += WGS) {
+            const uint32_t n = s.ocnt32[l];
+            if (n && win0 + l < P.H) { atomicAdd(&P.g_ocnt[win0 + l], (unsigned long long)n); }
+            s.ocnt32[l] = 0;
+        }
+    }
+    __syncthreads();
 }
 
 template <int MET, int MS, int WGS>
@@ -610,10 +718,23 @@ __global__ __launch_bounds__(WGS) void collect_kernel(CollectParams P) {
     // LDS window view.  Every pointer is derived from `smem` alone -- never merged with a global pointer -- so the
     // compiler keeps them in the LDS address space (ds_* instructions).  A generic pointer would compile to flat_*
     // accesses, and each flat load waits for vmcnt(0): the prefetched loads of the next iteration.
+    constexpr bool PI = MET > 0 && (VK & 64) != 0;  // packed integer cells
     Acc s;
-    {
+    if constexpr (PI) {  // collect_lds_bytes(pi = true) mirrors this carve
         size_t off = 0;
         auto carve = [&](size_t bytes) { unsigned char* p = smem + off; off += (bytes + 15) & ~(size_t)15; return p; };
+        s.cnt64 = nullptr; s.vcnt64 = nullptr; s.ocnt64 = nullptr;
+        s.cnt32 = nullptr; s.vcnt32 = nullptr; s.sum = nullptr; s.sq = nullptr; s.mn = nullptr; s.mx = nullptr;
+        s.mstride = 1;
+        s.pk = (unsigned long long*)carve(8 * C * ncp);
+        s.mm = (uint32_t*)carve(MET >= 2 ? 8 * C : 0);
+        s.coff = ((threadIdx.x & 63) % ncp) * C;
+        s.ocnt32 = (uint32_t*)carve(P.ocnt_mode == OCNT_TERMS ? sizeof(uint32_t) * T
+                                    : P.ocnt_mode == OCNT_HIST ? sizeof(uint32_t) * W : 0);
+    } else {
+        size_t off = 0;
+        auto carve = [&](size_t bytes) { unsigned char* p = smem + off; off += (bytes + 15) & ~(size_t)15; return p; };
+        s.pk = nullptr; s.mm = nullptr;
         s.cnt64 = nullptr; s.vcnt64 = nullptr; s.ocnt64 = nullptr;
         s.cnt32 = (uint32_t*)carve(sizeof(uint32_t) * C * ncp);
         s.vcnt32 = (uint32_t*)carve(P.vcnt_mode ? sizeof(uint32_t) * C * ncp : 0);
@@ -626,7 +747,14 @@ __global__ __launch_bounds__(WGS) void collect_kernel(CollectParams P) {
         s.ocnt32 = (uint32_t*)carve(P.ocnt_mode == OCNT_TERMS ? sizeof(uint32_t) * T
                                     : P.ocnt_mode == OCNT_HIST ? sizeof(uint32_t) * W : 0);
     }
-    if (P.lds_mode) {
+    if (PI && P.lds_mode) {
+        for (uint32_t c = threadIdx.x; c < C * ncp; c += WGS) s.pk[c] = 0;
+        if (MET >= 2)
+            for (uint32_t c = threadIdx.x; c < C; c += WGS) { s.mm[2 * c] = ~0u; s.mm[2 * c + 1] = 0u; }
+        if (P.ocnt_mode == OCNT_TERMS || P.ocnt_mode == OCNT_HIST)
+            for (uint32_t c = threadIdx.x; c < (P.ocnt_mode == OCNT_TERMS ? T : W); c += WGS) s.ocnt32[c] = 0;
+        __syncthreads();
+    } else if (P.lds_mode) {
         for (uint32_t c = threadIdx.x; c < C * ncp; c += WGS) {
             s.cnt32[c] = 0;
             if (P.vcnt_mode) s.vcnt32[c] = 0;
@@ -684,7 +812,9 @@ __global__ __launch_bounds__(WGS) void collect_kernel(CollectParams P) {
     const uint32_t tid4 = threadIdx.x * kVec;
     // shapes that read few bytes per doc (one ordinal or one key column) keep 4 buffers in flight, the rest 2 (their
     // buffers are 5x larger; 4 would cost occupancy).  kItersPerBlockW (4) is a multiple of either.
-    constexpr int kBuf = (MET == 0 && !(ORD && HIST)) ? ESGPU_NBUF_NARROW : ((VK & 48) ? (ESGPU_NBUF_COMPACT <= kItersPerBlockW ? ESGPU_NBUF_COMPACT : kItersPerBlockW) : 2);
+    constexpr int kBuf = (MET == 0 && !(ORD && HIST)) ? ESGPU_NBUF_NARROW
+                         : (VK & 64) ? (ESGPU_NBUF_PI <= kItersPerBlockW ? ESGPU_NBUF_PI : kItersPerBlockW)
+                         : ((VK & 48) ? (ESGPU_NBUF_COMPACT <= kItersPerBlockW ? ESGPU_NBUF_COMPACT : kItersPerBlockW) : 2);
     static_assert(kItersPerBlockW % kBuf == 0, "buffers per block");
     Doc4 q[kBuf];
 #pragma unroll
@@ -697,7 +827,8 @@ __global__ __launch_bounds__(WGS) void collect_kernel(CollectParams P) {
     auto slide_to = [&](uint32_t k0) {
         if (dirty) {
             if (!ORD) runs_flush<MET, kMS>(P, s, run);
-            flush_window<MET, kMS, WGS>(P, s, T, W, win0, ncp);
+            if constexpr (PI) flush_window_pi<MET, WGS>(P, s, T, W, win0, ncp);
+            else flush_window<MET, kMS, WGS>(P, s, T, W, win0, ncp);
         }
         dirty = false;
         win0 = k0;
@@ -750,10 +881,10 @@ __global__ __launch_bounds__(WGS) void collect_kernel(CollectParams P) {
             }
         }
         if (use_lds) {
-            process4<ORD, HIST, MET, true, KT, kMS, HORD>(P, s, q, T, base, win0, run, npass > 1 ? W : 0u, pass == 0);
+            process4<ORD, HIST, MET, true, KT, kMS, HORD, VKL>(P, s, q, T, base, win0, run, npass > 1 ? W : 0u, pass == 0);
             dirty = true;
         } else {
-            process4<ORD, HIST, MET, false, KT, kMS, HORD>(P, g, q, T, base, win0, run);
+            process4<ORD, HIST, MET, false, KT, kMS, HORD, VKL>(P, g, q, T, base, win0, run);
         }
         // prefetch kBuf iterations ahead along the schedule (next block of the group, the group's next pass, or the
         // next group)
@@ -790,7 +921,8 @@ __global__ __launch_bounds__(WGS) void collect_kernel(CollectParams P) {
     }
     if (P.lds_mode && (dirty || !(HIST && P.windowed))) {
         if (!ORD) runs_flush<MET, kMS>(P, s, run);
-        flush_window<MET, kMS, WGS>(P, s, T, W, win0, ncp);
+        if constexpr (PI) flush_window_pi<MET, WGS>(P, s, T, W, win0, ncp);
+        else flush_window<MET, kMS, WGS>(P, s, T, W, win0, ncp);
     }
     if (dyn && threadIdx.x == 0) {  // the last workgroup to finish re-arms the counter pair (vector atomics only)
         __threadfence();
@@ -847,7 +979,22 @@ static auto with_vk0(bool hv_f64, bool mv_f64, F f) {
 // Bits 16 / 32 (compact ordinal / histogram columns): terms dimensions without a derived key index, affine histograms
 // over a long column.
 template <bool ORD, int HK, int MET, class F>
-static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, F f) {
+static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, bool pi, F f) {
+    // VK bit 64, packed integer metric cells: terms grids (no key, or an affine key over the compact timestamps) with
+    // avg / stats over a dense long metric
+    if constexpr (ORD && (HK == 0 || HK == 1) && (MET == 1 || MET == 2)) {
+        if (pi && !mv_f64 && !dord) {
+            if constexpr (HK == 1) {
+                if (t32 && !hv_f64) {
+                    if (c16) return f(std::integral_constant<int, 48 | 64>{});
+                    return f(std::integral_constant<int, 32 | 64>{});
+                }
+            } else {
+                if (c16) return f(std::integral_constant<int, 16 | 64>{});
+                return f(std::integral_constant<int, 64>{});
+            }
+        }
+    }
     if constexpr (ORD && (HK == 1 || HK == 2)) {
         if (dord)
             return with_vk0<HK, MET>(hv_f64, mv_f64, [&](auto vk) { return f(std::integral_constant<int, decltype(vk)::value | 8>{}); });
@@ -879,7 +1026,8 @@ static auto with_wg(bool wide, F f) {
 
 template <bool ORD, int HK, int MET>
 static void launch_t(const CollectParams& p, bool wide, uint32_t grid, size_t lds, hipStream_t st) {
-    with_vk<ORD, HK, MET>(p.hv_f64 != 0, p.mv_f64 != 0, p.ord_src != nullptr, p.ord16 != nullptr, p.hv32 != nullptr, [&](auto vk) {
+    with_vk<ORD, HK, MET>(p.hv_f64 != 0, p.mv_f64 != 0, p.ord_src != nullptr, p.ord16 != nullptr, p.hv32 != nullptr, p.mv32 != nullptr,
+                          [&](auto vk) {
         return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
             hipLaunchKernelGGL((collect_kernel<ORD, HK, MET, decltype(vk)::value, decltype(wg)::value>), dim3(grid),
                                dim3(decltype(wg)::value), lds, st, p);
@@ -901,7 +1049,7 @@ static void launch_m(const CollectParams& p, int met, bool wide, uint32_t grid, 
 template <bool ORD, int HK, int MET>
 static int occ_t(size_t lds, int vkbits, bool wide) {
     return with_vk<ORD, HK, MET>((vkbits & 1) != 0, (vkbits & 2) != 0, (vkbits & 8) != 0, (vkbits & 16) != 0,
-                                 (vkbits & 32) != 0, [&](auto vk) {
+                                 (vkbits & 32) != 0, (vkbits & 64) != 0, [&](auto vk) {
         return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
             int n = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -921,10 +1069,28 @@ static int occ_m(int met, size_t lds, int vk, bool wide) {
         default: return occ_t<ORD, HK, 3>(lds, vk, wide);
     }
 }
-// explicit instantiations live in esgpu_collect_inst.hip (one object per ORD x HK)
+// explicit instantiations live in esgpu_collect_inst.hip (one object per ORD x HK x MET)
+template <bool ORD, int HK, int MET>
+void launch_collect_met(const CollectParams& p, bool wide, uint32_t grid, size_t lds, hipStream_t st);
+template <bool ORD, int HK, int MET>
+int collect_occ_met(size_t lds, int vk, bool wide);
 template <bool ORD, int HK>
-void launch_collect_inst(const CollectParams& p, int met, bool wide, uint32_t grid, size_t lds, hipStream_t st);
+void launch_collect_inst(const CollectParams& p, int met, bool wide, uint32_t grid, size_t lds, hipStream_t st) {
+    switch (met) {
+        case 0: launch_collect_met<ORD, HK, 0>(p, wide, grid, lds, st); break;
+        case 1: launch_collect_met<ORD, HK, 1>(p, wide, grid, lds, st); break;
+        case 2: launch_collect_met<ORD, HK, 2>(p, wide, grid, lds, st); break;
+        default: launch_collect_met<ORD, HK, 3>(p, wide, grid, lds, st); break;
+    }
+}
 template <bool ORD, int HK>
-int collect_occ_inst(int met, size_t lds, int vk, bool wide);
+int collect_occ_inst(int met, size_t lds, int vk, bool wide) {
+    switch (met) {
+        case 0: return collect_occ_met<ORD, HK, 0>(lds, vk, wide);
+        case 1: return collect_occ_met<ORD, HK, 1>(lds, vk, wide);
+        case 2: return collect_occ_met<ORD, HK, 2>(lds, vk, wide);
+        default: return collect_occ_met<ORD, HK, 3>(lds, vk, wide);
+    }
+}
 
 }  // namespace esgpu

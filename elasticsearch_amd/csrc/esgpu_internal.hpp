@@ -69,6 +69,8 @@ struct esgpu_ctx {
     std::atomic<uint64_t> used{0};
     hipStream_t stream = nullptr;  // upload / generation stream
     std::mutex mu;
+    // layout options (esgpu_ctx_set_option): compact columns, packed integer metric cells
+    std::atomic<int> opt_compact{1}, opt_pi{1};
     // synthetic tables (device copies)
     double* d_host_cdf = nullptr;
     double* d_rt_cdf = nullptr;

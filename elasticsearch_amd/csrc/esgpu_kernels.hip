@@ -123,10 +123,16 @@ int collect_occupancy(bool ord, int hk, int met, size_t lds, int vk, bool wide) 
 }
 
 
-size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode, uint32_t ncopies) {
+size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode, uint32_t ncopies, bool pi) {
     const size_t C = (size_t)T * W;
     const size_t n = std::max(ncopies, 1u);
     auto r = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    if (pi) {  // must match collect_kernel's carve order
+        size_t bytes = r(8 * C * n) + (met >= 2 ? r(8 * C) : 0);
+        if (ocnt_mode == OCNT_TERMS) bytes += r(4 * (size_t)T);
+        if (ocnt_mode == OCNT_HIST) bytes += r(4 * (size_t)W);
+        return bytes;
+    }
     size_t bytes = r(4 * C * n);
     if (vcnt_mode) bytes += r(4 * C * n);
     if (met > 0) bytes += r(8 * C * n);
@@ -882,6 +888,12 @@ __global__ void widen_u32_kernel(const unsigned int* src, size_t n, unsigned lon
 }
 void launch_widen_u32(const unsigned int* src, size_t n, unsigned long long* dst, hipStream_t st) {
     if (n) hipLaunchKernelGGL(widen_u32_kernel, dim3((uint32_t)std::min<size_t>(4096, (n + 255) / 256)), dim3(256), 0, st, src, n, dst);
+}
+__global__ void narrow_u64_kernel(const unsigned long long* src, size_t n, unsigned int* dst) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) dst[i] = (unsigned int)src[i];
+}
+void launch_narrow_u64(const unsigned long long* src, size_t n, unsigned int* dst, hipStream_t st) {
+    if (n) hipLaunchKernelGGL(narrow_u64_kernel, dim3((uint32_t)std::min<size_t>(4096, (n + 255) / 256)), dim3(256), 0, st, src, n, dst);
 }
 // global ordinals: out[d] = map[in[d]] (ordinals outside the segment dictionary, incl. missing, stay missing)
 __global__ void remap_ords_kernel(const uint32_t* in, uint32_t n, const uint32_t* map, uint32_t map_n, uint32_t* out) {

@@ -93,6 +93,13 @@ struct CollectParams {
     const void* mv;
     const uint64_t* mv_present;
     int32_t mv_f64;
+    // packed integer metric cells (loader VK bit 64): a dense single-valued long metric read as u32 deltas over mv_base
+    // (the column's compact copy); an LDS cell is one u64 word, count << pk_shift | sum of deltas, plus a u32 (min, max)
+    // delta pair -- one LDS atomic per doc for count + sum instead of two.  The host picks pk_shift so that neither field
+    // can overflow within one workgroup's range of docs.
+    const uint32_t* mv32;
+    int64_t mv_base;
+    uint32_t pk_shift;
     int32_t vcnt_mode;   // separate value counts (metric column has missing values)
     int32_t ocnt_mode;   // separate outer-level doc counts (inner dimension column has missing values)
     uint32_t ncopies;    // terms-only LDS grids: copies of the additive cells (count, value count, sum, sum of squares);
@@ -213,7 +220,8 @@ void launch_synth(const SynthParams& p, hipStream_t s);
 void launch_collect(const CollectParams& p, bool ord, bool hist, int met, bool wide, uint32_t grid, size_t lds, hipStream_t s);
 // per-block key ranges of the zone maps under the request's rounding (out: 2 x n_blocks)
 void launch_zone_keys(const CollectParams& p, int64_t* out, hipStream_t s);
-size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode, uint32_t ncopies = 1);
+// pi: packed integer metric cells (CollectParams.pk_shift): 8 B per cell copy + an 8 B (min, max) pair per cell
+size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode, uint32_t ncopies = 1, bool pi = false);
 // resident workgroups per CU (hk: 0 none, 1 affine, 2 table; vk: bit 0 double histogram column, bit 1 double metric)
 int collect_occupancy(bool ord, int hk, int met, size_t lds, int vk, bool wide = false);
 void launch_hll(const HllParams& p, uint32_t cus, hipStream_t s);
@@ -265,6 +273,7 @@ void launch_murmur3_field(const uint8_t* bytes, const uint64_t* offsets, uint64_
 // min / max over a value array (multi-valued i64 columns: key range of a histogram), out[0] = min, out[1] = max
 void launch_minmax_i64(const int64_t* v, uint64_t n, int64_t* out, bool f64, hipStream_t s);
 void launch_widen_u32(const unsigned int* src, size_t n, unsigned long long* dst, hipStream_t st);
+void launch_narrow_u64(const unsigned long long* src, size_t n, unsigned int* dst, hipStream_t st);
 void launch_pack_ord16(const uint32_t* src, uint32_t n, uint16_t* out, hipStream_t st);
 void launch_delta32(const int64_t* v, uint32_t n, int64_t base, uint32_t* out, hipStream_t st);
 void launch_comp_ords(const uint32_t* a, const uint32_t* b, uint32_t n_pad, uint32_t na, uint32_t nb, const uint32_t* amap,

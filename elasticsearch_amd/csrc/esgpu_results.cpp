@@ -41,6 +41,30 @@ static inline double jmax(double a, double b) {
     if (a == 0.0 && b == 0.0 && std::signbit(a)) return b;
     return a >= b ? a : b;
 }
+// the same as jmin / jmax without branches (the reduce's contiguous runs vectorise): a NaN operand wins, and of two
+// zeros min takes -0.0 / max +0.0 if either operand is one
+static inline double jmin_v(double a, double b) {
+    uint64_t ua, ub, uz;
+    std::memcpy(&ua, &a, 8);
+    std::memcpy(&ub, &b, 8);
+    uz = ua | ub;
+    double z;
+    std::memcpy(&z, &uz, 8);
+    double r = a <= b ? a : b;
+    r = (a == 0.0 && b == 0.0) ? z : r;
+    return a != a ? a : r;
+}
+static inline double jmax_v(double a, double b) {
+    uint64_t ua, ub, uz;
+    std::memcpy(&ua, &a, 8);
+    std::memcpy(&ub, &b, 8);
+    uz = ua & ub;
+    double z;
+    std::memcpy(&z, &uz, 8);
+    double r = a >= b ? a : b;
+    r = (a == 0.0 && b == 0.0) ? z : r;
+    return a != a ? a : r;
+}
 static inline int64_t jround(double a) {
     if (a != a) return 0;
     if (a >= 9.2233720368547758e18) return INT64_MAX;
@@ -438,6 +462,40 @@ void stream_leaf(Block& m, const Block* proto, const std::vector<OutBucket>& buc
         const Block& h = *dk.refs[x].b;
         const Block& L = h.subs[j];
         const uint64_t b0 = h.boff[dk.refs[x].i], b1 = h.boff[dk.refs[x].i + 1];
+        const uint64_t len = b1 - b0;
+        if (len > 1) {  // the shard's run lands on consecutive emitted buckets (a complete time series): one vector pass
+            const int32_t o0 = dk.out[dk.slot[e]], o1 = dk.out[dk.slot[e + len - 1]];
+            if (o0 >= 0 && o1 >= 0 && (uint64_t)(o1 - o0) == len - 1) {
+                // one loop per array (two streams each, no aliasing between output arrays to disprove): each vectorises
+                {
+                    int64_t* __restrict__ o = cnt + o0;
+                    const int64_t* __restrict__ in = L.count.data() + b0;
+                    for (uint64_t t = 0; t < len; ++t) o[t] += in[t];
+                }
+                {
+                    double* __restrict__ o = mn + o0;
+                    const double* __restrict__ in = L.min.data() + b0;
+                    for (uint64_t t = 0; t < len; ++t) o[t] = jmin_v(o[t], in[t]);
+                }
+                {
+                    double* __restrict__ o = mx + o0;
+                    const double* __restrict__ in = L.max.data() + b0;
+                    for (uint64_t t = 0; t < len; ++t) o[t] = jmax_v(o[t], in[t]);
+                }
+                {
+                    double* __restrict__ o = sum + o0;
+                    const double* __restrict__ in = L.sum.data() + b0;
+                    for (uint64_t t = 0; t < len; ++t) o[t] += in[t];
+                }
+                {
+                    double* __restrict__ o = sq + o0;
+                    const double* __restrict__ in = L.sumsq.data() + b0;
+                    for (uint64_t t = 0; t < len; ++t) o[t] += in[t];
+                }
+                e += len;
+                continue;
+            }
+        }
         for (uint64_t k = b0; k < b1; ++k) {
             const int32_t o = dk.out[dk.slot[e++]];
             if (o < 0) continue;
@@ -661,6 +719,21 @@ bool dense_slots(const Ref* refs, size_t nrefs, size_t total, DenseKeys& dk) {
         const uint64_t off0 = (uint64_t)h.key[b0] - (uint64_t)kmin;
         if (off0 % step) return false;  // this shard's keys are off the lattice (its gaps are multiples of step)
         uint32_t j = (uint32_t)(off0 / step);
+        if ((uint64_t)h.key[b1 - 1] - (uint64_t)h.key[b0] == (b1 - b0 - 1) * step) {
+            // strictly increasing keys whose gaps (multiples of step) sum to (n - 1) steps: every gap is one step
+            const int64_t* bc = h.bcount.data() + b0;
+            uint32_t* sl = dk.slot.data() + e;
+            int64_t* dc = dk.count.data() + j;
+            uint32_t* dn = dk.n.data() + j;
+            const uint64_t len = b1 - b0;
+            for (uint64_t t = 0; t < len; ++t) {
+                sl[t] = j + (uint32_t)t;
+                dc[t] += bc[t];
+                dn[t] += 1;
+            }
+            e += len;
+            continue;
+        }
         for (uint64_t k = b0; k < b1; ++k) {
             if (k > b0) {  // one division per gap longer than a step
                 const uint64_t d = (uint64_t)h.key[k] - (uint64_t)h.key[k - 1];

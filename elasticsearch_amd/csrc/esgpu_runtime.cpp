@@ -61,10 +61,31 @@ extern "C" int esgpu_device_count(int* count) {
 void tune_host_heap() {
     static std::once_flag once;
     std::call_once(once, [] {
+        // opt-in: the settings are the whole host process's (a JVM embedding the library keeps its own allocator
+        // behaviour unless the operator asks for this)
         const char* e = std::getenv("ESGPU_MALLOC_TUNE");
-        if (e && *e == '0') return;
+        if (!(e && *e == '1')) return;
         mallopt(M_MMAP_THRESHOLD, 32 << 20);
         mallopt(M_TRIM_THRESHOLD, 256 << 20);
+    });
+}
+
+extern "C" int esgpu_ctx_set_option(esgpu_ctx* c, int32_t option, int64_t value) {
+    return guarded([&] {
+        require(c, ESGPU_ERR_INVALID, "null context");
+        require(value == 0 || value == 1, ESGPU_ERR_INVALID, "option value must be 0 or 1");
+        if (option == ESGPU_OPT_COMPACT_COLUMNS) c->opt_compact = (int)value;
+        else if (option == ESGPU_OPT_PACKED_METRIC) c->opt_pi = (int)value;
+        else throw EsError(ESGPU_ERR_INVALID, "unknown context option");
+    });
+}
+
+extern "C" int esgpu_ctx_get_option(const esgpu_ctx* c, int32_t option, int64_t* value) {
+    return guarded([&] {
+        require(c && value, ESGPU_ERR_INVALID, "null argument");
+        if (option == ESGPU_OPT_COMPACT_COLUMNS) *value = c->opt_compact;
+        else if (option == ESGPU_OPT_PACKED_METRIC) *value = c->opt_pi;
+        else throw EsError(ESGPU_ERR_INVALID, "unknown context option");
     });
 }
 
@@ -82,6 +103,9 @@ extern "C" int esgpu_ctx_create(int device, uint64_t budget, esgpu_ctx** out) {
         c->device = device;
         c->budget = budget ? budget : (uint64_t)(prop.totalGlobalMem * 0.9);
         c->cus = prop.multiProcessorCount;
+        auto env_on = [](const char* name) { const char* e = std::getenv(name); return !(e && *e == '0'); };
+        c->opt_compact = env_on("ESGPU_COMPACT") ? 1 : 0;
+        c->opt_pi = env_on("ESGPU_PI") ? 1 : 0;
         HIPX(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         *out = c.release();
     });
@@ -632,6 +656,11 @@ extern "C" int esgpu_ordinal_map_build(esgpu_ctx* ctx, esgpu_segment* const* seg
                               (uint32_t)maps[k].size(), gv.as<uint32_t>(), nullptr);
             HIPX(hipGetLastError());
             HIPX(hipDeviceSynchronize());
+            {  // the 16-bit copy of the old ords() goes with it (a new buffer may reuse the old address)
+                std::lock_guard<std::mutex> lk(ctx->mu);
+                c->ord16.release();
+                c->ord16_src = nullptr;
+            }
             c->gvalues = std::move(gv);
             c->gdict = g;
         }
@@ -997,6 +1026,7 @@ struct esgpu_plan {
     bool sparse_dead = false;          // the current segment's accept bitset clears few docs (host sample, <= 10 %)
     Scratch s_xbits;                   // doc bitset of a pipeline with more than kMaxPreds clauses
     uint32_t seg_seq = 0;              // segments collected since create / reset (cardinality insertion order)
+    uint64_t docs_seen = 0;            // max_doc summed over those segments (u32 terms counts need it below 2^32)
     std::vector<PinnedBuf> h_compact;  // build: per bucket child, its GPU-compacted buckets and leaves (pinned)
     // breadth-first replay: the segments collected while a pipeline was deferred (pinned until reset / destroy) with a
     // device copy of each one's accept bits, and the outer ordinal -> winner slot map of the replay being run
@@ -1530,7 +1560,10 @@ static bool applies(const esgpu_plan* p, const Pipeline& pl, size_t k) {
     return p->filter_owner[k] < 0 || p->filter_owner[k] == pl.fspec;
 }
 
-static bool compact_cols();
+static bool compact_cols(const esgpu_ctx* c);
+static bool dyn_claim_on();
+static bool pi_cells(const esgpu_ctx* c);
+static uint32_t pi_copies();
 static const uint16_t* ensure_ord16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
 static const uint32_t* ensure_d32(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
 
@@ -1610,7 +1643,7 @@ static void set_preds(esgpu_plan* p, const Pipeline& pl, const esgpu_segment* s,
                 q.hi = hi;
             }
             // single-valued: the compact copy of the column (u32 deltas) when its values span < 2^32
-            if (compact_cols() && !col->multi && col->vmin <= col->vmax &&
+            if (compact_cols(p->ctx) && !col->multi && col->vmin <= col->vmax &&
                 (uint64_t)col->vmax - (uint64_t)col->vmin < (1ull << 32)) {
                 if (const uint32_t* d = ensure_d32(p->ctx, col, s, p->stream)) {
                     q.col = d;
@@ -1635,6 +1668,34 @@ static void set_preds(esgpu_plan* p, const Pipeline& pl, const esgpu_segment* s,
     }
     *accept = bits;
     *bytes_per_doc += 0;  // the clause columns were counted above; the bitset the kernel then reads is 1 bit per doc
+}
+
+// The terms doc counts in g_cnt are u32 on the partitioned / hot-cold paths (BucketsAggregator's IntArray,
+// A/bucket/BucketsAggregator.java:44-50) and u64 for every other kernel (LDS flushes, the CSR kernel, global atomics).
+// Which kernel runs can change from one segment of a request to the next (a field multi-valued in only some segments),
+// so the width is settled per segment before the launch: the grid is zero at a request's first segment (either width),
+// later ones convert the counts in place through a scratch copy.  u32 counts need the request's docs below 2^32 --
+// a shard holds at most IndexWriter.MAX_DOCS = 2^31 - 128 docs over all its segments, so only a caller collecting more
+// than a shard into one plan can reach that.
+static void count_width(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, bool want32, bool first_segment) {
+    if (want32)
+        require(p->docs_seen + (uint64_t)s->max_doc <= 0xFFFFFFFFull, ESGPU_ERR_UNSUPPORTED,
+                "a terms request over more than 2^32 docs (a shard holds at most 2^31 - 128): runs on the CPU path");
+    if (first_segment || want32 == pl.cnt32) { pl.cnt32 = want32; return; }
+    const size_t cells = (size_t)pl.T * pl.H;
+    if (cells) {
+        void* tmp = p->s_tcnt.ensure(p->ctx, cells * 8);
+        if (want32) {  // u64 -> u32: the scratch takes the narrow copy, then it goes back over the grid's head
+            launch_narrow_u64(pl.g_cnt.as<unsigned long long>(), cells, (unsigned int*)tmp, p->stream);
+            HIPX(hipGetLastError());
+            HIPX(hipMemcpyAsync(pl.g_cnt.p, tmp, cells * 4, hipMemcpyDeviceToDevice, p->stream));
+        } else {
+            launch_widen_u32(pl.g_cnt.as<unsigned int>(), cells, (unsigned long long*)tmp, p->stream);
+            HIPX(hipGetLastError());
+            HIPX(hipMemcpyAsync(pl.g_cnt.p, tmp, cells * 8, hipMemcpyDeviceToDevice, p->stream));
+        }
+    }
+    pl.cnt32 = want32;
 }
 
 // K1 for valueCount >> LDS (e.g. 10M url ordinals): radix-partitioned counting instead of global atomics, which
@@ -1665,7 +1726,6 @@ static bool collect_partitioned(esgpu_plan* p, Pipeline& pl, const esgpu_segment
     Q.tile_sums = (uint32_t*)p->s_tiles.ensure(c, (size_t)ntiles * 4);
     Q.pbuf = (uint16_t*)p->s_pbuf.ensure(c, (std::max<size_t>(s->max_doc, 1) + 8) * 2);
     Q.counts = pl.g_cnt.as<unsigned int>();
-    pl.cnt32 = true;
     // counting workgroups (one resident per CU at 128 KB of LDS counters); each covers `chunk` partitioned elements
     // (a multiple of 8: 16-byte loads).  Every partition piece a workgroup counts ends in a flush of its 32768
     // counters (256 KB of global adds), so the workgroup count is capped at one per 512K elements -- the flushes stay
@@ -2028,7 +2088,6 @@ static bool collect_hotcold(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s,
     H.pbuf = (uint16_t*)p->s_pbuf.ensure(c, hs->pbuf_elems * 2);
     H.trash = hs->trash;
     H.counts = pl.g_cnt.as<unsigned int>();
-    pl.cnt32 = true;
     if (!p->h_hcerr.bytes) {  // zeroed once here and after each check: overruns of every segment accumulate
         p->h_hcerr.ensure(8);
         *p->h_hcerr.as<volatile uint32_t>() = 0;
@@ -2617,11 +2676,12 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     P.g_max = pl.g_max.as<unsigned long long>();
     P.g_sq = pl.g_sq.as<double>();
     const int ret = inner_missing ? 2 : 1;
+    if (multi && !inner_missing) count_width(p, pl, s, false, first_segment);
     if (multi) return collect_multi(p, pl, s, P, L_ORD ? oc : nullptr, L_HIST ? hc : nullptr, inner_missing ? nullptr : mc, L_met,
                                     d_accept) ? ret : 0;
     // compact columns: 2 B per ordinal instead of 4, 4 B per timestamp instead of 8 -- the reported (algorithmic) bytes
     // are the bytes this layout must move (SURVEY §8(d)'s upload-width figure would put config 5 above the HBM peak)
-    if (compact_cols()) {
+    if (compact_cols(p->ctx)) {
         const bool plain_ord = oc && !pl.comp && !pl.ord_hist && oc == s->col(pl.ord_field.c_str());
         if (L_ORD && P.ord && plain_ord && !oc->multi && oc->ord_count() < 0xFFFFu) {
             P.ord16 = ensure_ord16(p->ctx, oc, s, p->stream);
@@ -2636,6 +2696,33 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
             }
         }
     }
+    // packed integer metric cells (CollectParams.pk_shift): terms grids with avg / stats over a dense
+    // single-valued long metric whose values span < 2^32, read as the column's u32 deltas -- the kernel instantiations
+    // exist for no key and for an affine key over the compact timestamps (with_vk); confirmed below once the workgroup
+    // ranges are known (neither packed field may overflow)
+    bool pi = false;
+    const int hk_launch = L_HIST ? (P.hord ? 3 : P.kstart ? 2 : 1) : 0;
+    if (pi_cells(p->ctx) && compact_cols(p->ctx) && L_ORD && !P.ord_src && (L_met == 1 || L_met == 2) && mc && mc->type == ESGPU_COL_I64 &&
+        !mc->multi && !mc->present.p && !L_vcnt && mc->vmin <= mc->vmax && (uint64_t)mc->vmax - (uint64_t)mc->vmin < (1ull << 32) &&
+        (hk_launch == 0 || (hk_launch == 1 && P.hv32 && !P.hv_f64)) && !dyn_claim_on()) {
+        if (const uint32_t* d = ensure_d32(p->ctx, mc, s, p->stream)) {
+            P.mv32 = d;
+            P.mv_base = mc->vmin;
+            pi = true;
+        }
+    }
+    auto pi_fits = [&](uint32_t bpw) {  // docs of one workgroup range: count field and sum-of-deltas field both fit
+        const uint64_t docs = std::min<uint64_t>((uint64_t)bpw * kBlockDocs, (uint64_t)s->max_doc);
+        const uint32_t cbits = 64 - __builtin_clzll(docs | 1);
+        const uint32_t sh = 64 - cbits;
+        const unsigned __int128 maxsum = (unsigned __int128)docs * (uint64_t)((uint64_t)mc->vmax - (uint64_t)mc->vmin);
+        // the decoded sum count * base + deltas must stay a long as well
+        const unsigned __int128 mag = (unsigned __int128)docs *
+                                      (uint64_t)std::max<int64_t>(mc->vmax < 0 ? -(mc->vmax + 1) : mc->vmax, mc->vmin < 0 ? -(mc->vmin + 1) : mc->vmin);
+        P.pk_shift = sh;
+        return sh < 64 && (maxsum >> sh) == 0 && (mag >> 62) == 0;
+    };
+  relaunch:
 
     // LDS sizing: the whole grid if it fits, else a sliding window over the key dimension (time-sorted data)
 #ifndef ESGPU_LDS_PAIR  // LDS budget of a window that keeps two workgroups per CU
@@ -2643,17 +2730,17 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
 #endif
     const size_t kLdsPair = ESGPU_LDS_PAIR, kLdsMax = 150 * 1024;
     uint32_t W = LH;
-    size_t lds = collect_lds_bytes(LT, W, L_met, L_vcnt, L_ocnt);
+    size_t lds = collect_lds_bytes(LT, W, L_met, L_vcnt, L_ocnt, 1, pi);
     P.lds_mode = 1;
     P.windowed = 0;
     if (lds > kLdsPair) {
         if (L_HIST && !P.kslot && !P.hord) {  // the key window needs buckets that rise with the value (zone-map ranges)
             uint32_t w = LH;
-            while (w > 1 && collect_lds_bytes(LT, w, L_met, L_vcnt, L_ocnt) > kLdsPair) w = (w + 1) / 2;
-            if (collect_lds_bytes(LT, w, L_met, L_vcnt, L_ocnt) > kLdsPair) w = 1;
+            while (w > 1 && collect_lds_bytes(LT, w, L_met, L_vcnt, L_ocnt, 1, pi) > kLdsPair) w = (w + 1) / 2;
+            if (collect_lds_bytes(LT, w, L_met, L_vcnt, L_ocnt, 1, pi) > kLdsPair) w = 1;
             W = w;
             P.windowed = 1;
-            lds = collect_lds_bytes(LT, W, L_met, L_vcnt, L_ocnt);
+            lds = collect_lds_bytes(LT, W, L_met, L_vcnt, L_ocnt, 1, pi);
         }
         if (lds > kLdsMax) {
             P.lds_mode = 0;
@@ -2677,12 +2764,12 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         const int64_t need = std::min<int64_t>(std::max<int64_t>(hc->zspan / pl.interval + 2, ESGPU_WIDE_MIN), (int64_t)LH);
         if (need > (int64_t)W) {
             uint32_t w2 = W;
-            while ((int64_t)w2 < need && collect_lds_bytes(LT, w2 + 1, L_met, L_vcnt, L_ocnt) <= kLdsMax) ++w2;
+            while ((int64_t)w2 < need && collect_lds_bytes(LT, w2 + 1, L_met, L_vcnt, L_ocnt, 1, pi) <= kLdsMax) ++w2;
             if (w2 > W) {
                 W = w2;
                 wide = true;
                 if (W >= LH) { W = LH; P.windowed = 0; }
-                lds = collect_lds_bytes(LT, W, L_met, L_vcnt, L_ocnt);
+                lds = collect_lds_bytes(LT, W, L_met, L_vcnt, L_ocnt, 1, pi);
             }
         }
     }
@@ -2692,25 +2779,40 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     P.ncopies = 1;
     if (P.lds_mode && L_ORD && (!L_HIST || ESGPU_COPIES_HIST)) {
         for (uint32_t nc = kTermsCopies; nc > 1; nc /= 2) {
-            const size_t b = collect_lds_bytes(LT, W, L_met, L_vcnt, L_ocnt, nc);
+            const size_t b = collect_lds_bytes(LT, W, L_met, L_vcnt, L_ocnt, nc, pi);
+            if (b <= kLdsPair) { P.ncopies = nc; lds = b; break; }
+        }
+    } else if (pi && P.lds_mode && L_HIST && pi_copies() > 1 && !wide) {
+        // packed cells are 16 B instead of 28: a time-sorted window of 2 keys leaves room for lane-rotated copies of the
+        // count + sum words (the Zipf-head terms of a wave otherwise queue on one LDS address)
+        if (P.windowed && W > 2) {
+            W = 2;
+            P.W = W;
+            lds = collect_lds_bytes(LT, W, L_met, L_vcnt, L_ocnt, 1, pi);
+        }
+        for (uint32_t nc = pi_copies(); nc > 1; --nc) {
+            const size_t b = collect_lds_bytes(LT, W, L_met, L_vcnt, L_ocnt, nc, pi);
             if (b <= kLdsPair) { P.ncopies = nc; lds = b; break; }
         }
     }
     if (!P.lds_mode && L_ORD && !L_HIST && L_met == 0 && !L_vcnt && L_ocnt == OCNT_NONE && !inner_missing &&
         (((uint64_t)pl.T + (1u << kPartShift) - 1) >> kPartShift) <= kPartMaxStaged) {
         p->last_bytes += bytes_per_doc * (uint64_t)s->max_doc + (d_accept ? ((uint64_t)s->max_doc + 7) / 8 : 0);
+        count_width(p, pl, s, true, first_segment);
         // (the hot/cold form keeps statistics per ordinal column: not for a column derived per request)
         if (ESGPU_HOTCOLD && !pl.comp && collect_hotcold(p, pl, s, oc, d_accept, P.pred, P.npred, first_segment)) return 1;
         return collect_partitioned(p, pl, s, oc, d_accept, P.pred, P.npred) ? 1 : 0;
     }
+    if (!inner_missing) count_width(p, pl, s, false, first_segment);
     const uint64_t span = (uint64_t)pl.interval * (uint64_t)W;
-    P.fast32 = !P.kstart && !P.hord && pl.interval < (1ll << 32) && span < (1ull << 32);
+    P.fast32 =!P.kstart && !P.hord && pl.interval < (1ll << 32) && span < (1ull << 32);
     if (P.fast32) {
         const MagicU32 mg = make_magic((uint32_t)pl.interval);
         P.mg_m = mg.m; P.mg_s1 = mg.s1; P.mg_s2 = mg.s2;
     }
     const int hk = L_HIST ? (P.hord ? 3 : P.kstart ? 2 : 1) : 0;
-    const int vk = (P.hv_f64 ? 1 : 0) | (P.mv_f64 ? 2 : 0) | (P.ord_src ? 8 : 0) | (P.ord16 ? 16 : 0) | (P.hv32 ? 32 : 0);
+    const int vk = (P.hv_f64 ? 1 : 0) | (P.mv_f64 ? 2 : 0) | (P.ord_src ? 8 : 0) | (P.ord16 ? 16 : 0) | (P.hv32 ? 32 : 0) |
+                   (P.mv32 ? 64 : 0);
     const uint64_t occ_key = ((uint64_t)lds << 16) | ((uint64_t)wide << 15) | ((uint64_t)vk << 8) | ((uint64_t)L_met << 4) |
                              ((uint64_t)hk << 1) | (L_ORD ? 1 : 0);
     if (pl.occ_key != occ_key) {
@@ -2733,16 +2835,19 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     const uint32_t slots = (uint32_t)p->ctx->cus * wg_per_cu;
     const uint32_t min_bpw = L_ORD ? std::min<uint32_t>(ESGPU_MIN_BPW, (P.n_blocks + slots - 1) / slots) : 1u;
     P.blocks_per_wg = std::max(std::max(1u, bpw), min_bpw);
+    if (pi && P.lds_mode && !pi_fits(P.blocks_per_wg)) {  // a packed field could overflow: the f64 cells instead
+        pi = false;
+        P.mv32 = nullptr;
+        P.ncopies = 1;
+        goto relaunch;
+    }
+    if (pi) bytes_per_doc -= 4;
     uint32_t grid = (P.n_blocks + P.blocks_per_wg - 1) / P.blocks_per_wg;
     // dynamic chunk claiming: one resident wave of workgroups, each flushing its LDS cells once, taking chunks of
     // kGroup blocks until none are left (ESGPU_DYN=0/1 overrides the build default for A/B runs)
-    static const int dyn_claim = [] {
-        const char* e = std::getenv("ESGPU_DYN");
-        return e && *e ? (*e == '1' ? 1 : 0) : ESGPU_DYN_CLAIM;
-    }();
     P.claim = nullptr;
     P.n_chunks = (P.n_blocks + kGroupBlocks - 1) / kGroupBlocks;
-    if (dyn_claim && P.n_chunks > slots) {
+    if (dyn_claim_on() && P.n_chunks > slots) {
         if (!p->d_claim.p) {
             p->d_claim.alloc(p->ctx, 16);
             HIPX(hipMemsetAsync(p->d_claim.p, 0, 16, p->stream));
@@ -2764,15 +2869,34 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     return ret;
 }
 
+static bool dyn_claim_on() {
+    static const int dyn_claim = [] {
+        const char* e = std::getenv("ESGPU_DYN");
+        return e && *e ? (*e == '1' ? 1 : 0) : ESGPU_DYN_CLAIM;
+    }();
+    return dyn_claim != 0;
+}
+// packed integer metric cells (CollectParams.pk_shift; ESGPU_PI=0: the f64 cells, for A/B runs) and the lane-rotated
+// copies of their count + sum words under a time window (ESGPU_PI_COPIES, 1 = none)
+#ifndef ESGPU_PI_COPIES
+#define ESGPU_PI_COPIES 1
+#endif
+static bool pi_cells(const esgpu_ctx* c) { return c->opt_pi.load() != 0; }
+static uint32_t pi_copies() {
+    static const uint32_t n = [] {
+        const char* e = std::getenv("ESGPU_PI_COPIES");
+        const int v = e && *e ? std::atoi(e) : ESGPU_PI_COPIES;
+        return (uint32_t)std::min(std::max(v, 1), 4);
+    }();
+    return n;
+}
+
 // Compact columns: a segment's ordinals and timestamps need fewer bits than their upload width -- Lucene
 // stores them bit-packed / delta-coded for the same reason -- and the collect loop is HBM-bound, so the single-valued
 // collect kernel reads 16-bit ordinals and 32-bit timestamp deltas when the segment's values fit (ESGPU_COMPACT=0: the
 // upload-width columns, for A/B runs).  Built once per column under the context lock (plans on other threads may share
 // the segment); an allocation over the HBM budget leaves the column as it is.
-static bool compact_cols() {
-    static const bool on = [] { const char* e = std::getenv("ESGPU_COMPACT"); return !(e && *e == '0'); }();
-    return on;
-}
+static bool compact_cols(const esgpu_ctx* c) { return c->opt_compact.load() != 0; }
 static const uint16_t* ensure_ord16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st) {
     DevColumn* m = const_cast<DevColumn*>(col);
     std::lock_guard<std::mutex> lk(c->mu);
@@ -2993,6 +3117,7 @@ extern "C" int esgpu_plan_collect_segment(esgpu_plan* p, const esgpu_segment* s,
         }
         p->collected = true;
         ++p->seg_seq;
+        p->docs_seen += s->max_doc;
     });
 }
 
@@ -4430,6 +4555,7 @@ extern "C" int esgpu_plan_reset(esgpu_plan* p) {
         p->posted = false;
         p->collected = false;
         p->seg_seq = 0;
+        p->docs_seen = 0;
         p->unpin_all();
     });
 }

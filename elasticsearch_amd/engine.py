@@ -254,6 +254,17 @@ class Engine:
         N.check(N.lib().esgpu_ctx_hbm_used(self._ptr, ctypes.byref(v)))
         return v.value
 
+    OPTIONS = {"compact_columns": 1, "packed_metric": 2}  # include/esgpu.h ESGPU_OPT_*
+
+    def set_option(self, name, value):
+        """Layout option of this context (esgpu_ctx_set_option): 'compact_columns' / 'packed_metric', 0 or 1."""
+        N.check(N.lib().esgpu_ctx_set_option(self._ptr, self.OPTIONS[name], int(value)))
+
+    def get_option(self, name):
+        v = ctypes.c_int64()
+        N.check(N.lib().esgpu_ctx_get_option(self._ptr, self.OPTIONS[name], ctypes.byref(v)))
+        return v.value
+
     def synthetic_segment(self, num_docs, fields=("host", "@timestamp", "response_time_ms"), shard=0,
                           seed=0x5EEDE1A5, ts_jitter_ms=0):
         mask = 0

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define ESGPU_ABI_VERSION 5
+#define ESGPU_ABI_VERSION 6
 
 /* ---------------------------------------------------------------------------------------------------------
  * Status codes.  Mapping used by the JNI shim (SURVEY §8(b) "Errors"):
@@ -67,6 +67,18 @@ int esgpu_ctx_create(int device, uint64_t hbm_budget_bytes, esgpu_ctx** out);
 int esgpu_ctx_destroy(esgpu_ctx* ctx);
 int esgpu_ctx_hbm_used(const esgpu_ctx* ctx, uint64_t* bytes);
 int esgpu_device_count(int* count);
+
+/* Per-context layout options (no reference counterpart: they choose between equivalent GPU layouts, the results are
+ * identical).  Defaults come from the environment (ESGPU_COMPACT / ESGPU_PI = 0 turn them off), else on; a change
+ * applies from the next collect of any plan of the context.
+ *   ESGPU_OPT_COMPACT_COLUMNS: the single-valued collect kernels read the segments' compact copies -- u16 ordinals
+ *                              (dictionaries under 65,535 terms) and u32 deltas of long columns spanning < 2^32 --
+ *                              instead of the upload-width columns
+ *   ESGPU_OPT_PACKED_METRIC:   avg / stats under terms over a dense long metric accumulate in packed integer LDS cells
+ *                              (count and sum of deltas in one u64 word; needs compact columns) */
+enum { ESGPU_OPT_COMPACT_COLUMNS = 1, ESGPU_OPT_PACKED_METRIC = 2 };
+int esgpu_ctx_set_option(esgpu_ctx* ctx, int32_t option, int64_t value);
+int esgpu_ctx_get_option(const esgpu_ctx* ctx, int32_t option, int64_t* value);
 
 /* ---------------------------------------------------------------------------------------------------------
  * Segment = one Lucene LeafReaderContext exported from doc values (K11).

@@ -199,3 +199,84 @@ def test_live_docs_two_segments_postings(engine):
     plan.close()
     for seg in segs:
         seg.close()
+
+
+def _csr(counts, values):
+    offs = np.zeros(len(counts) + 1, dtype=np.uint64)
+    np.cumsum(counts, out=offs[1:])
+    return values, offs
+
+
+@pytest.mark.parametrize("multi_field", ["kw", "status"])
+@pytest.mark.parametrize("multi_first", [False, True])
+def test_count_width_across_single_and_multi_segments(engine, multi_field, multi_first):
+    """One request over two segments of a 200,000-term field, the terms field (or the filter field) multi-valued in only
+    one of them: the single-valued segment counts into u32 counters (hot/cold path), the multi-valued one through the
+    CSR kernel's u64 atomics, so the grid's count width changes between the two collects -- in both orders."""
+    rng = np.random.default_rng(108 + multi_first)
+    T = 200_000
+    n1, n2 = 800_000, 600_000
+    # single-valued segment
+    ranks = np.minimum(rng.zipf(1.1, size=n1) - 1, T - 1)
+    o1 = ((ranks * 7919 + 5) % T).astype(np.uint32)
+    o1[rng.random(n1) < 0.02] = 0xFFFFFFFF
+    st1 = rng.integers(0, 4, size=n1).astype(np.int64)
+    terms = ["u%07d" % i for i in range(T)]
+    single = {"kw": {"type": N.COL_ORD_U32, "values": o1, "terms": terms},
+              "status": {"type": N.COL_I64, "values": st1}}
+    # the other segment: `multi_field` multi-valued (CSR, values sorted and unique per doc for the keyword field)
+    if multi_field == "kw":
+        cnt = rng.integers(0, 4, size=n2)
+        vals = np.minimum(rng.zipf(1.1, size=int(cnt.sum())) - 1, T - 1)
+        vals = ((vals * 7919 + 5) % T).astype(np.uint32)
+        doc = np.repeat(np.arange(n2), cnt)
+        order = np.lexsort((vals, doc))
+        doc, vals = doc[order], vals[order]
+        keep = np.ones(len(vals), dtype=bool)
+        keep[1:] = (doc[1:] != doc[:-1]) | (vals[1:] != vals[:-1])
+        doc, vals = doc[keep], vals[keep]
+        cnt = np.bincount(doc, minlength=n2)
+        v, offs = _csr(cnt, vals)
+        other = {"kw": {"type": N.COL_ORD_U32, "values": v, "offsets": offs, "terms": terms},
+                 "status": {"type": N.COL_I64, "values": rng.integers(0, 4, size=n2).astype(np.int64)}}
+        # the whole shard in CSR form for the oracle: the single-valued docs have 0 or 1 value
+        c1 = (o1 != 0xFFFFFFFF).astype(np.int64)
+        v1 = o1[o1 != 0xFFFFFFFF]
+        seqs = [(c1, v1), (cnt, v)] if not multi_first else [(cnt, v), (c1, v1)]
+        allv, alloffs = _csr(np.concatenate([s[0] for s in seqs]), np.concatenate([s[1] for s in seqs]))
+        st = [st1, other["status"]["values"]] if not multi_first else [other["status"]["values"], st1]
+        allc = {"kw": {"type": N.COL_ORD_U32, "values": allv, "offsets": alloffs, "terms": terms},
+                "status": {"type": N.COL_I64, "values": np.concatenate(st)}}
+    else:
+        ranks2 = np.minimum(rng.zipf(1.1, size=n2) - 1, T - 1)
+        o2 = ((ranks2 * 7919 + 5) % T).astype(np.uint32)
+        cnt = rng.integers(0, 3, size=n2)
+        sv = np.sort(rng.integers(0, 4, size=(n2, 2)), axis=1)
+        # values of doc d: the first cnt[d] of its two sorted draws (SortedNumeric order)
+        vals = sv[np.arange(2)[None, :] < cnt[:, None]].astype(np.int64)
+        v, offs = _csr(cnt, vals)
+        other = {"kw": {"type": N.COL_ORD_U32, "values": o2, "terms": terms},
+                 "status": {"type": N.COL_I64, "values": v, "offsets": offs}}
+        parts = [(o1, np.ones(n1, dtype=np.int64), st1), (o2, cnt, vals)]
+        if multi_first:
+            parts = parts[::-1]
+        allv, alloffs = _csr(np.concatenate([p[1] for p in parts]), np.concatenate([p[2] for p in parts]))
+        allc = {"kw": {"type": N.COL_ORD_U32, "values": np.concatenate([p[0] for p in parts]), "terms": terms},
+                "status": {"type": N.COL_I64, "values": allv, "offsets": alloffs}}
+    aggs = [AB.terms("c").field("kw").size(25), AB.terms("t").field("kw").size(7).order(Order.term(False))]
+    flt = [QB.rangeQuery("status").gte(1)] if multi_field == "status" else None
+    want = O.run([(allc, n1 + n2)], aggs, filters=flt)
+    segs = [engine.upload_segment(single, n1), engine.upload_segment(other, n2)]
+    if multi_first:
+        segs = segs[::-1]
+    plan = engine.plan(aggs, filters=flt)
+    try:
+        for rep in range(2):  # the second request starts from the width the first one ended with
+            for s in segs:
+                plan.collect(s)
+            assert_same(plan.build().to_dict(), want["shards"][0], f"shard rep{rep}")
+            plan.reset()
+    finally:
+        plan.close()
+        for s in segs:
+            s.close()

@@ -1,0 +1,182 @@
+"""GPU parity of every collect-kernel column layout ("parity leg for the upload-width kernels").
+
+The single-valued collect kernel reads, per segment, the narrowest layout the data allows:
+  * upload width: u32 ordinals, i64 timestamps / filter values / metric (compact columns off);
+  * compact: u16 ordinals (dictionaries under 65,535 terms), u32 deltas of long columns spanning < 2^32;
+  * compact + packed integer metric cells: a dense long metric under terms read as its u32 deltas and accumulated as
+    count << shift | sum of deltas in one u64 LDS word.
+Real indices take each of them: timestamps over more than 2^32 ms (49.7 days) keep i64 keys, sparse or double metrics
+keep f64 cells.  The layout is a per-context option (Engine.set_option), so one session runs them all against the same
+oracle result; the algorithmic bytes the plan reports name the layout that ran (north star: 20 / 14 / 10 B per doc).
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from elasticsearch_amd import AggregationBuilders as AB
+from elasticsearch_amd import Order, QueryBuilders as QB
+from elasticsearch_amd import _native as N
+from elasticsearch_amd import reduce
+from helpers import assert_same, bits_from_mask, synthetic_columns
+
+pytestmark = pytest.mark.gpu
+
+# (compact columns, packed metric) -> name
+LAYOUTS = {"upload": (0, 0), "compact": (1, 0), "packed": (1, 1)}
+
+
+class layout:
+    """Context options for the duration of a block (the session's engine is shared by every GPU test)."""
+
+    def __init__(self, engine, name):
+        self.e, self.v = engine, LAYOUTS[name]
+
+    def __enter__(self):
+        self.e.set_option("compact_columns", self.v[0])
+        self.e.set_option("packed_metric", self.v[1])
+
+    def __exit__(self, *a):
+        self.e.set_option("compact_columns", 1)
+        self.e.set_option("packed_metric", 1)
+
+
+def _run(engine, seg, aggs, filters=None, number_of_shards=1, segs=None):
+    plan = engine.plan(aggs, filters=filters, number_of_shards=number_of_shards)
+    nbytes = 0
+    for s in (segs or [seg]):
+        plan.collect(s)
+        nbytes += plan.last_collect_stats()[1]
+    res = plan.build()
+    plan.close()
+    return res, nbytes
+
+
+NS_FIELDS = ("host", "@timestamp", "response_time_ms")
+NS_AGGS = [AB.terms("hosts").field("host").size(10).subAggregation(
+    AB.dateHistogram("per_hour").field("@timestamp").interval("1h").subAggregation(AB.stats("rt").field("response_time_ms")))]
+C5_FIELDS = ("status", "bytes", "host", "@timestamp", "response_time_ms")
+C5_AGGS = [AB.terms("hosts").field("host").size(10).subAggregation(
+    AB.dateHistogram("per_hour").field("@timestamp").interval("1h").subAggregation(AB.avg("rt").field("response_time_ms")))]
+C5_FILTERS = [QB.termQuery("status", 200), QB.rangeQuery("bytes").gte(1024).lte(65536)]
+
+
+@pytest.fixture(scope="module")
+def ns_100m():
+    n = 100_000_000
+    cols = synthetic_columns(NS_FIELDS, n)
+    want = O.run([(cols, n)], NS_AGGS)
+    return n, want
+
+
+@pytest.fixture(scope="module")
+def c5_100m():
+    n = 100_000_000
+    cols = synthetic_columns(C5_FIELDS, n, shard=2)
+    want = O.run([(cols, n)], C5_AGGS, filters=C5_FILTERS, number_of_shards=8)
+    return n, want
+
+
+@pytest.mark.parametrize("name,bpd", [("upload", 20), ("compact", 14), ("packed", 10)])
+def test_north_star_100m_every_layout(engine, ns_100m, name, bpd):
+    n, want = ns_100m
+    with layout(engine, name):
+        seg = engine.synthetic_segment(n, fields=NS_FIELDS)  # a fresh segment: its compact copies are built by this layout
+        res, nbytes = _run(engine, seg, NS_AGGS)
+        seg.close()
+    assert nbytes == bpd * n, (name, nbytes / n)
+    assert_same(res.to_dict(), want["shards"][0], f"{name} shard")
+    assert_same(reduce([res]).to_dict(), want["reduced"], f"{name} reduced")
+
+
+@pytest.mark.parametrize("name,bpd", [("upload", 36), ("compact", 22), ("packed", 18)])
+def test_config5_100m_every_layout(engine, c5_100m, name, bpd):
+    n, want = c5_100m
+    with layout(engine, name):
+        seg = engine.synthetic_segment(n, fields=C5_FIELDS, shard=2)
+        res, nbytes = _run(engine, seg, C5_AGGS, filters=C5_FILTERS, number_of_shards=8)
+        seg.close()
+    assert nbytes == bpd * n, (name, nbytes / n)
+    assert_same(res.to_dict(), want["shards"][0], f"{name} shard")
+
+
+def _log_segment(rng, n, t0, span_ms, nterms=300, metric=None):
+    ranks = np.minimum(rng.zipf(1.2, size=n) - 1, nterms - 1)
+    cols = {
+        "host": {"type": N.COL_ORD_U32, "values": ((ranks * 37 + 11) % nterms).astype(np.uint32),
+                 "terms": ["h%04d" % i for i in range(nterms)]},
+        "@timestamp": {"type": N.COL_I64, "values": np.sort(rng.integers(t0, t0 + span_ms, size=n)).astype(np.int64)},
+        "rt": {"type": N.COL_I64, "values": (rng.integers(0, 1000, size=n) if metric is None else metric).astype(np.int64)},
+    }
+    return cols
+
+
+@pytest.mark.parametrize("name", ["upload", "compact", "packed"])
+def test_timestamps_over_2_32_ms(engine, name):
+    """Timestamps spanning 60 days (5.2e9 ms > 2^32): the key column stays i64 on every layout (u16 ordinals and the
+    packed metric still apply where they can: terms{stats} without a key takes packed cells, the daily and hourly
+    histograms i64 keys)."""
+    rng = np.random.default_rng(41)
+    n = 3_000_000
+    cols = _log_segment(rng, n, 1_420_070_400_000, 60 * 86_400_000)
+    aggs = [AB.terms("h").field("host").size(8).subAggregation(
+                AB.dateHistogram("d").field("@timestamp").interval("1h").subAggregation(AB.stats("s").field("rt"))),
+            AB.terms("hs").field("host").size(12).order(Order.aggregation("s.max", False)).subAggregation(AB.stats("s").field("rt")),
+            AB.dateHistogram("days").field("@timestamp").interval("1d").subAggregation(
+                AB.terms("t").field("host").size(3).subAggregation(AB.avg("a").field("rt")))]
+    want = O.run([(cols, n)], aggs)
+    with layout(engine, name):
+        seg = engine.upload_segment(cols, n)
+        res, _ = _run(engine, seg, aggs)
+        seg.close()
+    assert_same(res.to_dict(), want["shards"][0], f"{name} shard")
+
+
+@pytest.mark.parametrize("name", ["compact", "packed"])
+def test_packed_metric_edge_values(engine, name):
+    """Packed cells decode count * base + sum of deltas: negative metrics, a base far from zero (sums beyond 2^53,
+    compared at the big-sum tolerance), deltas near 2^32, and two segments whose metric bases differ -- each decoded with
+    its own base; stats, avg and extended_stats (the latter never packed) side by side."""
+    rng = np.random.default_rng(42)
+    t0 = 1_441_065_600_000
+    segs_cols = []
+    for k, (lo, hi) in enumerate([(-500_000, 500_000), (1_000_000_000_000, 1_000_000_000_999), (0, (1 << 32) - 1)]):
+        n = 700_000 + 100_000 * k
+        cols = _log_segment(rng, n, t0 + k * 86_400_000, 86_400_000, metric=rng.integers(lo, hi + 1, size=n))
+        segs_cols.append((cols, n))
+    allc = {f: dict(segs_cols[0][0][f], values=np.concatenate([c[f]["values"] for c, _ in segs_cols])) for f in segs_cols[0][0]}
+    ntot = sum(n for _, n in segs_cols)
+    aggs = [AB.terms("h").field("host").size(6).subAggregation(
+                AB.dateHistogram("d").field("@timestamp").interval("1h").minDocCount(0).subAggregation(AB.stats("s").field("rt"))),
+            AB.terms("a").field("host").size(9).subAggregation(AB.avg("m").field("rt")),
+            AB.terms("x").field("host").size(4).subAggregation(AB.extendedStats("e").field("rt"))]
+    want = O.run([(allc, ntot)], aggs)
+    with layout(engine, name):
+        segs = [engine.upload_segment(c, n) for c, n in segs_cols]
+        res, _ = _run(engine, None, aggs, segs=segs)
+        for s in segs:
+            s.close()
+    assert_same(res.to_dict(), want["shards"][0], f"{name} shard", exact_floats=False)
+
+
+def test_packed_then_sparse_metric_segment(engine):
+    """The first segment's metric is dense (packed cells), the second's sparse (a present bitset: value counts split
+    from doc counts mid-request, f64 cells for that segment)."""
+    rng = np.random.default_rng(43)
+    t0 = 1_441_065_600_000
+    c1 = _log_segment(rng, 900_000, t0, 86_400_000)
+    c2 = _log_segment(rng, 600_000, t0 + 86_400_000, 86_400_000)
+    pres = rng.random(600_000) < 0.8
+    c2["rt"]["present"] = bits_from_mask(pres)
+    aggs = [AB.terms("h").field("host").size(7).subAggregation(
+        AB.dateHistogram("d").field("@timestamp").interval("1h").subAggregation(AB.stats("s").field("rt")))]
+    vals2 = c2["rt"]["values"].copy()
+    vals2[~pres] = 0
+    c2["rt"]["values"] = vals2
+    allc = {f: dict(c1[f], values=np.concatenate([c1[f]["values"], c2[f]["values"]])) for f in c1}
+    allc["rt"]["present"] = bits_from_mask(np.concatenate([np.ones(900_000, dtype=bool), pres]))
+    want = O.run([(allc, 1_500_000)], aggs)
+    segs = [engine.upload_segment(c1, 900_000), engine.upload_segment(c2, 600_000)]
+    res, _ = _run(engine, None, aggs, segs=segs)
+    for s in segs:
+        s.close()
+    assert_same(res.to_dict(), want["shards"][0], "shard")

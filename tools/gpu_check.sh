@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun session: GPU parity tests, kernel sweep, bench, rocprofv3 kernel-trace stats and PMC HBM-traffic passes.
 #   gpurun --timeout 1200 -- bash tools/gpu_check.sh <tag> [steps...]
-# steps: tests testsdyn testfile kbench bench jitter export shape125 configs dynab hllab cut0ab buildtrace profk125 prof profk pmc pmck variants (default: tests kbench bench prof pmc)
+# steps: tests testsdyn testfile testfiles piab kbench bench jitter export shape125 configs dynab hllab cut0ab buildtrace profk125 prof profk pmc pmck variants (default: tests kbench bench prof pmc)
 # KBENCH_ONLY=name,name restricts the kbench sweeps (KBENCH_ARGS: extra kbench flags for variants, KBENCH_TAG: log suffix); variants = every build/variants/libesgpu_*.so via ESGPU_LIBRARY.  Every GPU step has its own time limit; the first failure ends it.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -96,6 +96,18 @@ for s in $STEPS; do
                    python3 "$R/tools/kbench.py" --docs 1000000000 --reps 3 ;;
         profk125) cd /tmp && run rocprof_kbench125 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profk125" -o kb125 -- \
                    python3 "$R/tools/kbench.py" --docs 125000000 --reps 3 ${KBENCH_ONLY:+--only $KBENCH_ONLY} ;;
+        testfiles) # several test files in one pytest process: TESTFILES="test_gpu_layouts test_gpu_hotcold"
+              args=""; for f in ${TESTFILES:-test_gpu_parity}; do args="$args $R/tests/$f.py"; done
+              run pytest_files 900 python3 -u -m pytest $args -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+        piab) # packed integer metric cells (ESGPU_PI) and lane-rotated copies of their count + sum words (ESGPU_PI_COPIES)
+              for pi in 1 0; do
+                  ESGPU_PI=$pi run "kbench_pi$pi" 400 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 \
+                      --only ${KBENCH_ONLY:-north_star,ns_avg,config5,config1_terms_stats} || exit 1
+              done
+              for c in 2 3; do
+                  ESGPU_PI_COPIES=$c run "kbench_picp$c" 400 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 \
+                      --only ${KBENCH_ONLY:-north_star,ns_avg,config5,config1_terms_stats} || exit 1
+              done ;;
         testfile) run "pytest_${TESTFILE:-x}" 600 python3 -u -m pytest "$R/tests/${TESTFILE:-test_gpu_parity}.py" -m gpu -x -v \
                       -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         pmc) cd /tmp && run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o bench -- \
@@ -104,7 +116,7 @@ for s in $STEPS; do
                  python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-docs 0 --inflight 1 ;;
         pmck) # counters for the kbench shapes in KBENCH_ONLY (default config3_url), one counter group per pass
               for grp in FETCH_SIZE WRITE_SIZE "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
-                         "SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT"; do
+                         "SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"; do
                   tag=$(echo "$grp" | cut -d' ' -f1)
                   cd /tmp && run "pmck_$tag" 600 rocprofv3 --pmc $grp --kernel-trace --output-format csv \
                       -d "$OUT/pmck_$tag" -o kb -- python3 "$R/tools/kbench.py" --docs 1000000000 --reps 1 \

@@ -15,6 +15,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
+os.environ.setdefault("ESGPU_MALLOC_TUNE", "1")  # as bench.py: the host process opts into the library's malloc settings
 
 import elasticsearch_amd as ea  # noqa: E402
 from elasticsearch_amd import AggregationBuilders as AB  # noqa: E402
