@@ -2066,6 +2066,72 @@ void launch_comp_ords(const uint32_t* a, const uint32_t* b, uint32_t n_pad, uint
                        na, nb, amap, amap_n, out);
 }
 
+// one 8192-doc block per workgroup: each doc's batch and replay ordinal, a position inside the workgroup's share of
+// its batch (the wave's lanes of one batch take consecutive positions with one LDS atomic: the Zipf-head winners put
+// most of a wave in one batch), one global reservation per (workgroup, batch), then the appends
+__global__ __launch_bounds__(kWG) void replay_compact_kernel(ReplayCompactParams P) {
+    __shared__ uint32_t cnt[kReplayMaxBatches], base[kReplayMaxBatches];
+    for (uint32_t i = threadIdx.x; i < P.nbatch; i += kWG) cnt[i] = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t val[kItersPerBlock][4], bid[kItersPerBlock][4], pos[kItersPerBlock][4];
+#pragma unroll
+    for (int it = 0; it < kItersPerBlock; ++it) {
+        const uint32_t doc0 = blockIdx.x * kBlockDocs + it * kIterDocs + threadIdx.x * kVec;
+        uint32_t x[4], y[4];
+        load_u32x4(P.a, doc0, x);
+        load_u32x4(P.b, doc0, y);
+        uint32_t ok = 0xF;
+        if (doc0 + 4 > P.n_docs) ok = doc0 >= P.n_docs ? 0u : ((1u << (P.n_docs - doc0)) - 1u);
+        if (P.accept) ok &= bits4(P.accept, doc0);
+        for (int k = 0; k < P.npred; ++k) ok &= eval_pred(P.pred[k], doc0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t w = ((ok >> j) & 1) && x[j] < P.slot_map_n ? P.slot_map[x[j]] : kMissingOrd;
+            const bool live = w != kMissingOrd && y[j] < P.vcB;
+            bid[it][j] = live ? w / P.wb : kMissingOrd;
+            val[it][j] = live ? (w % P.wb) * P.stride + y[j] : 0u;
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < kItersPerBlock; ++it)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t mine = bid[it][j];
+            uint64_t todo = __ballot(mine != kMissingOrd);
+            uint32_t p = 0;
+            while (todo) {  // one round per distinct batch among the wave's live lanes
+                const int leader = __ffsll((unsigned long long)todo) - 1;
+                const uint32_t bl = __shfl(mine, leader, 64);
+                const uint64_t same = __ballot(mine == bl);
+                uint32_t b0 = 0;
+                if ((int)lane == leader) b0 = atomicAdd(&cnt[bl], (uint32_t)__popcll(same));
+                b0 = __shfl(b0, leader, 64);
+                if (mine == bl) p = b0 + (uint32_t)__popcll(same & lt);
+                todo &= ~same;
+            }
+            pos[it][j] = p;
+        }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < P.nbatch; i += kWG) base[i] = cnt[i] ? atomicAdd(&P.fill[i], cnt[i]) : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kItersPerBlock; ++it)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t bb = bid[it][j];
+            if (bb == kMissingOrd) continue;
+            const uint32_t q = base[bb] + pos[it][j];
+            if (q < P.cap[bb]) P.out[P.region[bb] + q] = val[it][j];
+            else *P.overflow = 1u;
+        }
+}
+void launch_replay_compact(const ReplayCompactParams& p, hipStream_t st) {
+    const uint32_t blocks = (p.n_docs + kBlockDocs - 1) / kBlockDocs;
+    if (blocks) hipLaunchKernelGGL(replay_compact_kernel, dim3(blocks), dim3(kWG), 0, st, p);
+}
+
 void launch_minmax_i64(const int64_t* v, uint64_t n, int64_t* out, bool f64, hipStream_t st) {
     if (n == 0) return;
     hipLaunchKernelGGL(minmax_i64_kernel, dim3((uint32_t)std::min<uint64_t>(1024, (n + 255) / 256)), dim3(256), 0, st, v, n, out,

@@ -276,6 +276,29 @@ void launch_widen_u32(const unsigned int* src, size_t n, unsigned long long* dst
 void launch_narrow_u64(const unsigned long long* src, size_t n, unsigned int* dst, hipStream_t st);
 void launch_pack_ord16(const uint32_t* src, uint32_t n, uint16_t* out, hipStream_t st);
 void launch_delta32(const int64_t* v, uint32_t n, int64_t base, uint32_t* out, hipStream_t st);
+// breadth-first replay, compacted: one pass over a retained segment appends, for every doc whose outer bucket survived
+// (slot_map) and that has an inner term, its replay-grid ordinal (winner w % wb) * stride + inner into the region of
+// its batch of wb winners; the batches are then counted from their regions alone (the ordinal columns are read once for
+// all batches instead of once per batch).  An append past a region's capacity is dropped and sets *overflow.
+struct ReplayCompactParams {
+    uint32_t n_docs;
+    const uint32_t* a;           // outer (global) ordinals
+    const uint32_t* b;           // inner (global) ordinals
+    const uint32_t* slot_map;    // outer ordinal -> winner index (kMissingOrd: the bucket did not survive)
+    uint32_t slot_map_n;
+    uint32_t vcB;                // inner ordinals (b >= vcB: missing)
+    uint32_t wb, stride, nbatch;
+    int32_t npred;
+    PredDev pred[4];
+    const uint64_t* accept;
+    uint32_t* out;
+    const uint64_t* region;      // [nbatch] first element of each batch's region in out
+    const uint32_t* cap;         // [nbatch] its capacity (elements)
+    uint32_t* fill;              // [nbatch] elements appended so far (zeroed before the first segment)
+    uint32_t* overflow;          // set to 1 when an append did not fit
+};
+constexpr uint32_t kReplayMaxBatches = 1024;
+void launch_replay_compact(const ReplayCompactParams& p, hipStream_t s);
 void launch_comp_ords(const uint32_t* a, const uint32_t* b, uint32_t n_pad, uint32_t na, uint32_t nb, const uint32_t* amap,
                       uint32_t amap_n, uint32_t* out, hipStream_t st);
 void launch_hist_ords(const int64_t* v, const uint64_t* present, uint32_t n_docs, uint32_t n_pad, bool f64, int64_t interval,

@@ -14,6 +14,7 @@
 #include <malloc.h>
 
 #include <algorithm>
+#include <functional>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -1038,6 +1039,8 @@ struct esgpu_plan {
     uint32_t slot_map_n = 0, slot_k = 0;
     Scratch s_rkeys;                   // replay: per winner, the GPU top-k's keys and row total
     PinnedBuf h_rkeys;
+    Scratch s_rregion, s_rmeta;        // compacted replay: the batches' regions; region offsets, capacities, fills
+    PinnedBuf h_rfill;
     void unpin_all() {
         for (const DeferredSeg& d : dsegs) unpin_segment(d.s);
         dsegs.clear();
@@ -1143,6 +1146,13 @@ static std::vector<int> add_leaf_pipelines(esgpu_plan* p, int root, int fspec, i
     return idx;
 }
 
+// x is -1 or a filter aggregation whose ancestors are all filter aggregations (a chain of filters from the top)
+static bool filter_chain_to_top(const esgpu_plan* p, int x) {
+    for (; x >= 0; x = p->specs[x].s.parent)
+        if (p->specs[x].s.type != ESGPU_AGG_FILTER) return false;
+    return true;
+}
+
 static Group compile_group(esgpu_plan* p, int r, int fspec) {
     Group g;
     g.root = r;
@@ -1168,7 +1178,7 @@ static Group compile_group(esgpu_plan* p, int r, int fspec) {
     for (int ch : root.children) {
         const int t = p->specs[ch].s.type;
         if (is_metric(t) || t == ESGPU_AGG_CARDINALITY) leaves.push_back(ch);
-        else if (t == ESGPU_AGG_FILTER) require(fspec < 0, ESGPU_ERR_UNSUPPORTED, "nested filter aggregations");
+        else if (t == ESGPU_AGG_FILTER) continue;  // its own pipelines below (under the enclosing filters' clauses too)
         else if (!is_bucket(t)) throw EsError(ESGPU_ERR_UNSUPPORTED, "aggregation type not on the GPU path");
     }
     std::vector<LeafRef> leaf_refs;
@@ -1296,10 +1306,14 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
             n.s.time_zone = nullptr;
             n.s.format = nullptr;
             require(n.s.type >= ESGPU_AGG_TERMS && n.s.type <= ESGPU_AGG_FILTER, ESGPU_ERR_INVALID, "unknown aggregation type");
-            if (n.s.type == ESGPU_AGG_FILTER && n.s.parent >= 0) {  // one bucket level above it (compile_group)
+            if (n.s.type == ESGPU_AGG_FILTER && n.s.parent >= 0) {
+                // a chain of filter aggregations from the top (each one's docs: its clauses and its ancestors'), or a
+                // filter directly under a bucket aggregation of the first bucket level (compile_group)
+                require(n.s.parent < i, ESGPU_ERR_INVALID, "parent must precede child");
                 const SpecNode& par = p->specs[n.s.parent];
-                require(is_bucket(par.s.type) && par.s.parent < 0, ESGPU_ERR_UNSUPPORTED,
-                        "a filter aggregation below the first bucket level runs on the CPU path");
+                require((par.s.type == ESGPU_AGG_FILTER && filter_chain_to_top(p.get(), n.s.parent)) ||
+                            (is_bucket(par.s.type) && filter_chain_to_top(p.get(), par.s.parent)),
+                        ESGPU_ERR_UNSUPPORTED, "a filter aggregation below the first bucket level runs on the CPU path");
             }
             if (n.s.parent < 0) tops.push_back(i);
             else {
@@ -1353,8 +1367,9 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
             int own = 0;
             for (int o : p->filter_owner) own += o == r;
             require(own >= 1, ESGPU_ERR_INVALID, "filter aggregation without a filter clause");
-            for (int ch : p->specs[r].children)
-                require(p->specs[ch].s.type != ESGPU_AGG_FILTER, ESGPU_ERR_UNSUPPORTED, "nested filter aggregations");
+            for (int ch : p->specs[r].children)  // filters under a filter: only on a chain of filters from the top
+                require(p->specs[ch].s.type != ESGPU_AGG_FILTER || filter_chain_to_top(p.get(), r), ESGPU_ERR_UNSUPPORTED,
+                        "a filter aggregation below the first bucket level runs on the CPU path");
         }
         p->tops = tops;
         // terms ordered by a sub-aggregation: AggregationPath.validate (A/support/AggregationPath.java:289-347)
@@ -1372,7 +1387,7 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
                 // candidate ordinal's sketch estimate, derived at build for a top-level terms (or one under a top-level
                 // filter); under another bucket level the per-row sketches are not gathered for selection
                 const int par = n.s.parent;
-                require(par < 0 || (p->specs[par].s.type == ESGPU_AGG_FILTER && p->specs[par].s.parent < 0), ESGPU_ERR_UNSUPPORTED,
+                require(filter_chain_to_top(p.get(), par), ESGPU_ERR_UNSUPPORTED,
                         "terms under another bucket aggregation ordered by a cardinality runs on the CPU path");
                 require(key.empty() || key == "value", ESGPU_ERR_INVALID, "Invalid terms aggregation order path [" + n.order_path +
                         "]. Ordering on a single-value metrics aggregation can only be done on its value.");
@@ -1397,14 +1412,20 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
         // compile each top-level subtree into a group of pipelines (one cell grid each, one kernel launch each);
         // a filter aggregation (FilterAggregator) becomes one counting pipeline for its doc_count plus one group per
         // sub-aggregation, all under its clauses
-        for (int r : tops) {
-            if (p->specs[r].s.type != ESGPU_AGG_FILTER) { p->groups.push_back(compile_group(p.get(), r, -1)); continue; }
+        std::function<void(int)> compile_filter = [&](int r) {  // a filter, its children (nested filters: recursively)
             Pipeline cnt;
             cnt.root = r;
             cnt.fspec = r;
             cnt.count_only = true;
             p->pipes.push_back(std::move(cnt));
-            for (int ch : p->specs[r].children) p->groups.push_back(compile_group(p.get(), ch, r));
+            for (int ch : p->specs[r].children) {
+                if (p->specs[ch].s.type == ESGPU_AGG_FILTER) compile_filter(ch);
+                else p->groups.push_back(compile_group(p.get(), ch, r));
+            }
+        };
+        for (int r : tops) {
+            if (p->specs[r].s.type != ESGPU_AGG_FILTER) { p->groups.push_back(compile_group(p.get(), r, -1)); continue; }
+            compile_filter(r);
         }
         HIPX(hipSetDevice(c->device));
         HIPX(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
@@ -1556,12 +1577,19 @@ static int64_t build_key_table(esgpu_plan* p, Pipeline& pl, int64_t lo, int64_t 
 }
 
 // the query clauses and those of the pipeline's filter aggregation
+// a clause applies to a pipeline when it is a query clause or belongs to a filter aggregation enclosing the pipeline's
+// (its own filter, and every filter aggregation above it: nested filters intersect, FilterAggregator.java:57-70 per level)
 static bool applies(const esgpu_plan* p, const Pipeline& pl, size_t k) {
-    return p->filter_owner[k] < 0 || p->filter_owner[k] == pl.fspec;
+    const int owner = p->filter_owner[k];
+    if (owner < 0) return true;
+    for (int x = pl.fspec; x >= 0; x = p->specs[x].s.parent)
+        if (x == owner) return true;
+    return false;
 }
 
 static bool compact_cols(const esgpu_ctx* c);
 static bool dyn_claim_on();
+static bool replay_compaction();
 static bool pi_cells(const esgpu_ctx* c);
 static uint32_t pi_copies();
 static const uint16_t* ensure_ord16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
@@ -1701,17 +1729,25 @@ static void count_width(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, boo
 // K1 for valueCount >> LDS (e.g. 10M url ordinals): radix-partitioned counting instead of global atomics, which
 // serialise on the Zipf head terms.  Reads the ordinal column twice (4 + 4 B/doc), writes and re-reads a 2 B/doc
 // partition-local copy: 12 B/doc of traffic for the 4 B/doc algorithmic stream.  Fully asynchronous.
+static bool count_partitioned(esgpu_plan* p, Pipeline& pl, const uint32_t* ords, uint32_t n_docs, uint32_t n_blocks,
+                              const uint64_t* d_accept, const PredDev* pred, int npred);
 static bool collect_partitioned(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const DevColumn* oc,
                                 const uint64_t* d_accept, const PredDev* pred, int npred) {
+    return count_partitioned(p, pl, oc->ords().as<uint32_t>(), s->max_doc, s->n_pad / kBlockDocs, d_accept, pred, npred);
+}
+// the counting core over any u32 ordinal list of n_docs entries, readable up to n_blocks * kBlockDocs (a segment's
+// column, or a compacted replay region)
+static bool count_partitioned(esgpu_plan* p, Pipeline& pl, const uint32_t* ords, uint32_t n_docs, uint32_t n_blocks,
+                              const uint64_t* d_accept, const PredDev* pred, int npred) {
     esgpu_ctx* c = p->ctx;
     hipStream_t st = p->stream;
     PartParams Q{};
-    Q.n_docs = s->max_doc;
-    Q.n_blocks = s->n_pad / kBlockDocs;
+    Q.n_docs = n_docs;
+    Q.n_blocks = n_blocks;
     const uint32_t target = (uint32_t)c->cus * part_wg_per_cu();
     Q.blocks_per_wg = std::max(1u, (Q.n_blocks + target - 1) / target);
     Q.G = (Q.n_blocks + Q.blocks_per_wg - 1) / Q.blocks_per_wg;
-    Q.ord = oc->ords().as<uint32_t>();
+    Q.ord = ords;
     Q.T = pl.T;
     Q.shift = kPartShift;  // 32768 ordinals per partition: 128 KB of LDS counters in the counting pass
     Q.P = (uint32_t)(((uint64_t)pl.T + (1u << Q.shift) - 1) >> Q.shift);
@@ -1724,7 +1760,7 @@ static bool collect_partitioned(esgpu_plan* p, Pipeline& pl, const esgpu_segment
     const uint32_t ntiles = part_scan_tiles(Q.P * Q.G);
     require(ntiles <= 4096, ESGPU_ERR_INVALID, "partition scan too large");
     Q.tile_sums = (uint32_t*)p->s_tiles.ensure(c, (size_t)ntiles * 4);
-    Q.pbuf = (uint16_t*)p->s_pbuf.ensure(c, (std::max<size_t>(s->max_doc, 1) + 8) * 2);
+    Q.pbuf = (uint16_t*)p->s_pbuf.ensure(c, (std::max<size_t>(n_docs, 1) + 8) * 2);
     Q.counts = pl.g_cnt.as<unsigned int>();
     // counting workgroups (one resident per CU at 128 KB of LDS counters); each covers `chunk` partitioned elements
     // (a multiple of 8: 16-byte loads).  Every partition piece a workgroup counts ends in a flush of its 32768
@@ -1732,8 +1768,8 @@ static bool collect_partitioned(esgpu_plan* p, Pipeline& pl, const esgpu_segment
     // within a quarter of the 2-byte reads -- between 1 and 4 per CU.  Measured: 4 per CU is best at 1B docs (3.16 vs
     // 3.47 ms for 1 per CU), 1 per CU at 125M (0.55 vs 0.62 ms).
     const uint64_t want = std::min<uint64_t>((uint64_t)c->cus * 4,
-                                             std::max<uint64_t>((uint64_t)c->cus, (uint64_t)s->max_doc >> 19));
-    Q.chunk = (uint32_t)std::max<uint64_t>(1u << 16, (((uint64_t)s->max_doc + want - 1) / want + 7) & ~7ull);
+                                             std::max<uint64_t>((uint64_t)c->cus, (uint64_t)n_docs >> 19));
+    Q.chunk = (uint32_t)std::max<uint64_t>(1u << 16, (((uint64_t)n_docs + want - 1) / want + 7) & ~7ull);
     HIPX(hipEventRecord(pl.e0, st));
     launch_part_hist(Q, st);
     launch_part_scan(Q, st);
@@ -2869,6 +2905,11 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     return ret;
 }
 
+// the compacted replay (ESGPU_REPLAY_COMPACT=0: one pass over the segments per batch of winners, for A/B runs)
+static bool replay_compaction() {
+    static const bool on = [] { const char* e = std::getenv("ESGPU_REPLAY_COMPACT"); return !(e && *e == '0'); }();
+    return on;
+}
 static bool dyn_claim_on() {
     static const int dyn_claim = [] {
         const char* e = std::getenv("ESGPU_DYN");
@@ -3750,6 +3791,103 @@ static bool replay_pass(esgpu_plan* p, const ChildSrc& kid, const std::vector<Te
     return any;
 }
 
+// The compacted replay of a count-only child in batches of wb winners (ReplayCompactParams): one pass over every retained
+// segment writes each surviving doc's replay ordinal into its batch's region -- capacity from the winners' outer doc
+// counts, which bound the docs that can land there -- so each batch is counted from its region alone instead of
+// re-reading both ordinal columns of every segment per batch.  False (nothing changed) when it does not apply: more
+// batches than the kernel stages, a region budget over the context's HBM, or an append that did not fit.
+struct ReplayRegions {
+    std::vector<uint32_t> n;      // elements per batch
+    std::vector<uint64_t> off;    // first element of each batch's region
+    uint64_t vcB = 0;
+    bool any = false;             // some retained segment had both fields
+    std::shared_ptr<const TermDict> da, db;
+};
+static bool replay_compact(esgpu_plan* p, const ChildSrc& kid, const std::vector<TermPick>& top, uint32_t wb, uint64_t T_outer,
+                           ReplayRegions& rr) {
+    hipStream_t st = p->stream;
+    Pipeline& R0 = p->pipes[kid.rpipes[0]];
+    const uint32_t k = (uint32_t)top.size();
+    const uint32_t nbatch = (k + wb - 1) / wb;
+    if (nbatch > kReplayMaxBatches || dyn_claim_on()) return false;
+    // the inner dictionary: the first retained segment with both fields (every later one must number alike)
+    for (const esgpu_plan::DeferredSeg& d : p->dsegs) {
+        const DevColumn* a = d.s->col(R0.ord_field.c_str());
+        const DevColumn* b = d.s->col(R0.ord_field2.c_str());
+        if (!a || !b) continue;
+        if (!rr.db) { rr.da = a->ord_dict(); rr.db = b->ord_dict(); rr.vcB = b->ord_count(); }
+        else require(same_dict(a->ord_dict(), rr.da) && same_dict(b->ord_dict(), rr.db), ESGPU_ERR_INVALID,
+                     "segments number the terms of [" + R0.ord_field + "] or [" + R0.ord_field2 + "] differently: build an "
+                     "ordinal map (esgpu_ordinal_map_build) over the reader's segments first");
+        require(!a->multi && !b->multi, ESGPU_ERR_UNSUPPORTED, "a breadth-first replay over multi-valued terms fields runs on the CPU path");
+        rr.any = true;
+    }
+    rr.n.assign(nbatch, 0);
+    rr.off.assign(nbatch + 1, 0);
+    if (!rr.any) return true;
+    const uint64_t stride = replay_stride(rr.vcB);
+    if ((uint64_t)wb * stride >= 0xFFFFFFFFull) return false;
+    std::vector<uint32_t> cap(nbatch);
+    for (uint32_t bi = 0; bi < nbatch; ++bi) {
+        uint64_t c = 0;
+        for (uint32_t w = bi * wb; w < std::min(k, (bi + 1) * wb); ++w) {
+            if (top[w].count < 0) return false;  // a count not gathered yet (GPU top-k in a term order): no capacity known
+            c += (uint64_t)top[w].count;
+        }
+        if (c >= 0x7FFFFFFFull) return false;
+        cap[bi] = (uint32_t)c;
+        rr.off[bi + 1] = rr.off[bi] + ((c + kBlockDocs - 1) / kBlockDocs + 1) * kBlockDocs;  // + one block: the loads past n
+    }
+    uint32_t* region;
+    try {
+        region = (uint32_t*)p->s_rregion.ensure(p->ctx, rr.off[nbatch] * 4);
+    } catch (const EsError& e) {
+        if (e.code != ESGPU_ERR_OOM) throw;
+        return false;
+    }
+    std::vector<uint32_t> map(std::max<uint64_t>(T_outer, 1), kMissingOrd);
+    for (uint32_t w = 0; w < k; ++w) if (top[w].ord < map.size()) map[top[w].ord] = w;
+    // device metadata: [slot map][region offsets (u64)][capacities][fills][overflow]
+    const size_t moff = ((map.size() * 4 + 15) & ~(size_t)15), coff = moff + (size_t)nbatch * 8, foff = coff + (size_t)nbatch * 4;
+    unsigned char* meta = (unsigned char*)p->s_rmeta.ensure(p->ctx, foff + (size_t)nbatch * 4 + 16);
+    HIPX(hipMemcpyAsync(meta, map.data(), map.size() * 4, hipMemcpyHostToDevice, st));
+    HIPX(hipMemcpyAsync(meta + moff, rr.off.data(), (size_t)nbatch * 8, hipMemcpyHostToDevice, st));
+    HIPX(hipMemcpyAsync(meta + coff, cap.data(), (size_t)nbatch * 4, hipMemcpyHostToDevice, st));
+    HIPX(hipMemsetAsync(meta + foff, 0, (size_t)nbatch * 4 + 16, st));
+    for (const esgpu_plan::DeferredSeg& d : p->dsegs) {
+        const DevColumn* a = d.s->col(R0.ord_field.c_str());
+        const DevColumn* b = d.s->col(R0.ord_field2.c_str());
+        if (!a || !b) continue;
+        ReplayCompactParams C{};
+        C.n_docs = d.s->max_doc;
+        C.a = a->ords().as<uint32_t>();
+        C.b = b->ords().as<uint32_t>();
+        C.slot_map = (const uint32_t*)meta;
+        C.slot_map_n = (uint32_t)map.size();
+        C.vcB = (uint32_t)std::min<uint64_t>(rr.vcB, 0xFFFFFFFFull);
+        C.wb = wb;
+        C.stride = (uint32_t)stride;
+        C.nbatch = nbatch;
+        const uint64_t* acc = d.accept >= 0 ? p->d_daccept[d.accept].as<uint64_t>() : nullptr;
+        uint64_t bytes = 0;
+        set_preds(p, R0, d.s, C.pred, &C.npred, &bytes, &acc);
+        C.accept = acc;
+        C.out = region;
+        C.region = (const uint64_t*)(meta + moff);
+        C.cap = (const uint32_t*)(meta + coff);
+        C.fill = (uint32_t*)(meta + foff);
+        C.overflow = (uint32_t*)(meta + foff + (size_t)nbatch * 4);
+        launch_replay_compact(C, st);
+        HIPX(hipGetLastError());
+    }
+    uint32_t* hf = (uint32_t*)p->h_rfill.ensure((size_t)nbatch * 4 + 16);
+    HIPX(hipMemcpyAsync(hf, meta + foff, (size_t)nbatch * 4 + 16, hipMemcpyDeviceToHost, st));
+    HIPX(hipStreamSynchronize(st));  // also keeps `map` / `cap` alive for the copies
+    if (hf[nbatch] != 0) return false;  // an append past its capacity: the per-pass replay instead
+    for (uint32_t bi = 0; bi < nbatch; ++bi) rr.n[bi] = hf[bi];
+    return true;
+}
+
 // TermsAggregator breadth_first (A/bucket/terms/TermsAggregator.java:161 shouldDefer; BestBucketsDeferringCollector
 // .prepareSelectedBuckets :127-166, replayed from GlobalOrdinalsStringTermsAggregator.buildAggregation :195-196): the
 // child's collectors run again over the retained segments, each doc counted in its outer bucket's winner slot when that
@@ -3779,9 +3917,38 @@ static ReplaySel replay_child(esgpu_plan* p, const ChildSrc& kid, const std::vec
     LeafRef ord2;
     if (agg2)
         for (size_t gj = 0; gj < tn2.children.size(); ++gj) if (tn2.children[gj] == tn2.order_child) ord2 = kid.rgrand[gj];
+    // count-only children in batches: compact the winners' docs once, then count each batch from its region
+    ReplayRegions rr;
+    const bool compact = wb < k && replay_compaction() && replay_compact(p, kid, top, wb, T_outer, rr);
     for (uint32_t b0 = 0; b0 < k; b0 += wb) {
         const uint32_t kb = std::min(wb, k - b0);
-        const bool any = replay_pass(p, kid, top, b0, kb, T_outer);
+        bool any;
+        if (compact) {
+            const uint32_t bi = b0 / wb;
+            any = rr.any && rr.n[bi] > 0;
+            if (any) {  // the batch's replay grid, counted from its region (the partitioned path's u32 counters)
+                Pipeline& R = R0;
+                R.vcA = kb;
+                R.vcB = rr.vcB;
+                R.tdict = rr.da;
+                R.tdictB = rr.db;
+                R.T = (uint32_t)(kb * replay_stride(rr.vcB));
+                R.H = 1;
+                R.key0 = 0;
+                R.keyed = false;
+                R.value_count = R.T;
+                R.vcnt_mode = 0;
+                R.ocnt_mode = OCNT_NONE;
+                alloc_grid(p, R);
+                R.allocated = true;
+                R.fresh = false;
+                R.cnt32 = true;  // the grid was just zeroed: either width
+                const uint32_t* reg = p->s_rregion.as<uint32_t>() + rr.off[bi];
+                count_partitioned(p, R, reg, rr.n[bi], (rr.n[bi] + kBlockDocs - 1) / kBlockDocs, nullptr, nullptr, 0);
+            }
+        } else {
+            any = replay_pass(p, kid, top, b0, kb, T_outer);
+        }
         const uint64_t nb = any ? R0.vcB : B0.value_count2;
         const uint64_t stride = replay_stride(nb);
         if (!any) {  // no doc of these winners has an inner term: every row is empty (min_doc_count 0 still lists terms)
@@ -4470,8 +4637,7 @@ extern "C" int esgpu_plan_build(esgpu_plan* p, esgpu_result** out) {
         // top-level aggregations in request order; a filter aggregation (InternalFilter, FilterAggregator.java:72-80)
         // is its counting pipeline's doc_count plus its sub-aggregations' groups, in the order create made them
         size_t gi = 0;
-        for (int r : p->tops) {
-            if (p->specs[r].s.type != ESGPU_AGG_FILTER) { h->aggs.push_back(build_group(p, p->groups[gi++])); continue; }
+        std::function<Block(int)> build_filter = [&](int r) {  // InternalFilter: doc_count, then its sub-aggregations
             Pipeline* cnt = nullptr;
             for (Pipeline& pl : p->pipes) if (pl.count_only && pl.root == r) cnt = &pl;
             Block fb;
@@ -4486,8 +4652,13 @@ extern "C" int esgpu_plan_build(esgpu_plan* p, esgpu_result** out) {
                 dc = hc[0];
             }
             fb.count.push_back((int64_t)dc);
-            for (size_t j = 0; j < p->specs[r].children.size(); ++j) fb.subs.push_back(build_group(p, p->groups[gi++]));
-            h->aggs.push_back(std::move(fb));
+            for (int ch : p->specs[r].children)
+                fb.subs.push_back(p->specs[ch].s.type == ESGPU_AGG_FILTER ? build_filter(ch) : build_group(p, p->groups[gi++]));
+            return fb;
+        };
+        for (int r : p->tops) {
+            if (p->specs[r].s.type != ESGPU_AGG_FILTER) { h->aggs.push_back(build_group(p, p->groups[gi++])); continue; }
+            h->aggs.push_back(build_filter(r));
         }
         bmark(p, "assembled");
         h->export_view();

@@ -71,10 +71,11 @@ def make_segment(rng, n):
 
 
 class Gen:
-    def __init__(self, rng, T_kw, rng2=None):
+    def __init__(self, rng, T_kw, rng2=None, rng3=None):
         self.r = rng
         # shapes added later draw from their own stream, so the earlier shapes of every seed stay what they were
         self.r2 = rng2 if rng2 is not None else np.random.default_rng(0)
+        self.r3 = rng3 if rng3 is not None else np.random.default_rng(1)  # round 4: nested filter aggregations
         self.T_kw = T_kw
         self.k = 0
         self.inexact = False
@@ -161,7 +162,8 @@ class Gen:
                 order_targets.append(m.name + key)
             elif self.r2.random() < 0.5:  # a cardinality child as the terms order (its single value)
                 order_targets.append(m.name)
-        if depth == 0 and self.r2.random() < 0.25:  # a filter aggregation under the bucket, with metric children
+        if (depth == 0 and self.r2.random() < 0.25) or (depth == 1 and self.r3.random() < 0.3):
+            # a filter aggregation under the bucket (a first-level bucket: at the top, or inside a top-level filter)
             r_main, self.r = self.r, self.r2
             f = AB.filter(self.name("g"), QB.termQuery("status", int(self.r2.choice([200, 404]))) if self.r2.random() < 0.6
                           else QB.rangeQuery("num").gte(int(self.r2.integers(0, 600))))
@@ -207,6 +209,12 @@ class Gen:
             elif c < 0.85:
                 f = AB.filter(self.name("f"), QB.termQuery("status", int(r.choice([200, 404]))))
                 f.subAggregation(self.metric()[0] if r.random() < 0.5 else self.bucket(1))
+                if self.r3.random() < 0.4:  # a filter inside the filter (nested FilterAggregators intersect)
+                    g = AB.filter(self.name("n"), QB.rangeQuery("num").gte(int(self.r3.integers(0, 700))))
+                    r_main, self.r = self.r, self.r3
+                    g.subAggregation(self.metric()[0] if self.r3.random() < 0.5 else self.bucket(1))
+                    self.r = r_main
+                    f.subAggregation(g)
                 aggs.append(f)
             else:
                 aggs.append(self.metric()[0])
@@ -229,7 +237,7 @@ def test_random_request(engine, seed, monkeypatch):
     rng = np.random.default_rng(1000 + seed)
     n = int(rng.integers(30_000, 300_000))
     cols, T_kw = make_segment(rng, n)
-    gen = Gen(rng, T_kw, np.random.default_rng(50_000 + seed))
+    gen = Gen(rng, T_kw, np.random.default_rng(50_000 + seed), np.random.default_rng(90_000 + seed))
     aggs, filters = gen.request()
     lookups = {f: {t: i for i, t in enumerate(cols[f]["terms"])} for f in ("kw", "kw2", "tags")}
     ord_lookup = lambda f, t: lookups.get(f, {}).get(t, -1)  # noqa: E731

@@ -214,3 +214,29 @@ def test_filter_under_histogram(engine, first):
     aggs = [h, AB.dateHistogram("day").field("@timestamp").interval("1d").subAggregation(
         AB.filter("s200", QB.termQuery("status", 200)))]
     _both(engine, aggs, n=300_000, shards=2, exact=False)
+
+
+def test_nested_filter_aggregations(engine):
+    """Filter aggregations inside filter aggregations (FilterAggregator.java:57-70 at every level: a doc reaches the
+    inner filter's sub-aggregations only if it matches every enclosing filter's clauses), three deep; a filter under a
+    terms aggregation that is itself inside a filter; terms ordered by a cardinality child inside two filters; beside
+    query clauses."""
+    card = AB.cardinality("ips").field("client_ip.hash").precisionThreshold(200)
+    aggs = [AB.filter("ok", QB.termQuery("status", 200))
+            .subAggregation(AB.filter("big", QB.rangeQuery("bytes").gte(5000))
+                            .subAggregation(AB.terms("hosts").field("host").size(5).subAggregation(AB.avg("rt").field("response_time_ms")))
+                            .subAggregation(AB.filter("cheap", [QB.rangeQuery("price").lt(300.0), QB.rangeQuery("response_time_ms").lt(700)])
+                                            .subAggregation(AB.stats("b").field("bytes"))
+                                            .subAggregation(AB.dateHistogram("d").field("@timestamp").interval("1d")))
+                            .subAggregation(AB.filter("empty", QB.rangeQuery("bytes").lt(0))))
+            .subAggregation(AB.extendedStats("p").field("price")),
+            AB.filter("any", QB.rangeQuery("response_time_ms").gte(10))
+            .subAggregation(AB.terms("h2").field("host").size(4)
+                            .subAggregation(AB.filter("slow", QB.rangeQuery("response_time_ms").gte(800))
+                                            .subAggregation(AB.avg("b2").field("bytes"))))
+            .subAggregation(AB.filter("f2", QB.rangeQuery("bytes").gte(1000))
+                            .subAggregation(AB.terms("h3").field("host").size(3).order(Order.aggregation("ips", False))
+                                            .subAggregation(card)))]
+    red = _both(engine, aggs, n=300_000, shards=2, filters=[QB.rangeQuery("price").gte(2.0)], exact=False)
+    assert red["ok"]["big"]["empty"]["doc_count"] == 0
+    assert 0 < red["ok"]["big"]["cheap"]["doc_count"] < red["ok"]["big"]["doc_count"] < red["ok"]["doc_count"]

@@ -108,6 +108,11 @@ for s in $STEPS; do
                   ESGPU_PI_COPIES=$c run "kbench_picp$c" 400 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 \
                       --only ${KBENCH_ONLY:-north_star,ns_avg,config5,config1_terms_stats} || exit 1
               done ;;
+        replayab) # breadth-first replay of terms(host){terms(url)}: compacted winners' docs vs one pass per batch
+              for c in 1 0; do for docs in 125000000 1000000000; do
+                  ESGPU_REPLAY_COMPACT=$c run "kbench_replay${c}_$docs" 400 python3 "$R/tools/kbench.py" --docs $docs --reps 3 \
+                      --only hosts_urls || exit 1
+              done; done ;;
         testfile) run "pytest_${TESTFILE:-x}" 600 python3 -u -m pytest "$R/tests/${TESTFILE:-test_gpu_parity}.py" -m gpu -x -v \
                       -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         pmc) cd /tmp && run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o bench -- \
