@@ -1503,6 +1503,51 @@ __global__ __launch_bounds__(1024) void topk_final_kernel(TopkParams P) {
     for (uint32_t i = threadIdx.x; i < P.k; i += 1024) P.out_keys[i] = best[i];
 }
 
+// segment statistics of a high-cardinality column: per partition of 2^shift ordinals, the docs of its cold (not hot)
+// ordinals and their largest count -- one workgroup per partition, the hot ordinals as a bitset
+__global__ __launch_bounds__(1024) void hc_part_stats_kernel(const unsigned int* counts, uint32_t T, uint32_t shift,
+                                                             const uint64_t* hot_bits, unsigned long long* part_sum,
+                                                             unsigned int* part_max) {
+    const uint32_t p = blockIdx.x;
+    const uint32_t o0 = p << shift, o1 = min(T, (p + 1) << shift);
+    unsigned long long sum = 0;
+    uint32_t mx = 0;
+    for (uint32_t o = o0 + threadIdx.x; o < o1; o += 1024) {
+        const uint32_t c = counts[o];
+        if ((hot_bits[o >> 6] >> (o & 63)) & 1) continue;
+        sum += c;
+        mx = max(mx, c);
+    }
+    sum = wave_sum_u64(sum);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+    __shared__ unsigned long long ws[16];
+    __shared__ uint32_t wm[16];
+    if ((threadIdx.x & 63) == 0) { ws[threadIdx.x >> 6] = sum; wm[threadIdx.x >> 6] = mx; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        uint32_t m = 0;
+        for (int w = 0; w < 16; ++w) { t += ws[w]; m = max(m, wm[w]); }
+        part_sum[p] = t;
+        part_max[p] = m;
+    }
+}
+void launch_hc_part_stats(const unsigned int* counts, uint32_t T, uint32_t shift, uint32_t P, const uint64_t* hot_bits,
+                          unsigned long long* part_sum, unsigned int* part_max, hipStream_t st) {
+    if (P) hipLaunchKernelGGL(hc_part_stats_kernel, dim3(P), dim3(1024), 0, st, counts, T, shift, hot_bits, part_sum, part_max);
+}
+
+// count orders, k beyond the final sort: the count histogram, its threshold and the candidates at or above it (sel[1]
+// of them in cand, in no order; the caller sorts them)
+void launch_topk_candidates(const TopkParams& p, hipStream_t s) {
+    const uint32_t g = std::max(1u, std::min(p.n_wg, (p.T + 4095) / 4096));
+    (void)hipMemsetAsync(p.hist, 0, kTopkBins * 4, s);
+    hipLaunchKernelGGL(topk_hist_kernel, dim3(g), dim3(1024), 0, s, p);
+    hipLaunchKernelGGL(topk_thresh_kernel, dim3(1), dim3(kWG), 0, s, p);
+    hipLaunchKernelGGL(topk_compact_kernel, dim3(g), dim3(1024), 0, s, p);
+}
+
 void launch_topk(const TopkParams& p, hipStream_t s) {
     if (p.order == 0 || p.order == 1) {  // count orders: select, then sort the few candidates
         const uint32_t g = std::max(1u, std::min(p.n_wg, (p.T + 4095) / 4096));

@@ -404,6 +404,9 @@ void launch_hc_recode(const uint32_t* ord, uint32_t n, const uint32_t* keys, con
                       uint32_t* out, hipStream_t s);
 // stats time: the 16-bit hot-slot column of the postings hot pass from the recoded column (0xFFFF: cold or missing)
 void launch_hc_hot16(const uint32_t* rc, uint32_t n, uint16_t* out, hipStream_t s);
+// stats time: per partition of 2^shift ordinals the summed counts of its cold ordinals and the largest one
+void launch_hc_part_stats(const unsigned int* counts, uint32_t T, uint32_t shift, uint32_t P, const uint64_t* hot_bits,
+                          unsigned long long* part_sum, unsigned int* part_max, hipStream_t st);
 
 // ---- GPU top-k over a count vector (BucketPriorityQueue replacement for large T) ----
 struct TopkParams {
@@ -422,6 +425,7 @@ struct TopkParams {
 };
 constexpr uint32_t kTopkMax = 1024;
 void launch_topk(const TopkParams& p, hipStream_t s);
+void launch_topk_candidates(const TopkParams& p, hipStream_t s);  // count orders: cand[0, sel[1]) unsorted, out_sum
 // terms under a histogram, count orders: per row r of the [H][T] count grid, the row's total (total[r]) and its top S
 // candidates (count >= min_count) as u64 keys in selection order, count-major (asc: complemented), ties by ascending
 // ordinal -- out[r * S + i], 0 past the last candidate.  S <= kRowTopkMax.

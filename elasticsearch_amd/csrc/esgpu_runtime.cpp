@@ -1040,7 +1040,7 @@ struct esgpu_plan {
     Scratch s_rkeys;                   // replay: per winner, the GPU top-k's keys and row total
     PinnedBuf h_rkeys;
     Scratch s_rregion, s_rmeta;        // compacted replay: the batches' regions; region offsets, capacities, fills
-    PinnedBuf h_rfill;
+    PinnedBuf h_rfill, h_rcand;        // compacted replay fills; large inner top-k: row sum + candidates
     void unpin_all() {
         for (const DeferredSeg& d : dsegs) unpin_segment(d.s);
         dsegs.clear();
@@ -1893,17 +1893,11 @@ static std::shared_ptr<const HcStats> ensure_hc_stats(esgpu_ctx* c, const DevCol
         mcol->hc = r;
         return nullptr;
     };
-    std::vector<uint64_t> cnt(T, 0);
-    {
-        DevBuf d;
-        count_all_ordinals(c, (const uint32_t*)src, s->max_doc, s->n_pad, T, d, st);
-        std::vector<uint32_t> c32(T);
-        HIPX(hipMemcpy(c32.data(), d.p, (size_t)T * 4, hipMemcpyDeviceToHost));
-        for (uint32_t o = 0; o < T; ++o) cnt[o] = c32[o];
-    }
-    uint64_t total = 0;
-    for (uint64_t v : cnt) total += v;
-    hs->docs = total;
+    // the segment's counts per ordinal on the GPU; the hot set from the GPU top-k's threshold candidates (sorted on the
+    // host: a few times H keys), the cold totals per partition from one more pass over the counts -- the T counts never
+    // leave the device (a 10M-ordinal column: 40 MB of counts, an nth_element over 10M on the host before)
+    DevBuf dcnt;
+    count_all_ordinals(c, (const uint32_t*)src, s->max_doc, s->n_pad, T, dcnt, st);
     // scatter workgroups and hot slots: two workgroups per CU while their LDS layouts fit with >= 2048 hot counters
     const size_t kLdsCu = 160 * 1024 - 512;
     auto hot_fit = [&](size_t budget) -> int64_t {
@@ -1920,35 +1914,69 @@ static std::shared_ptr<const HcStats> ensure_hc_stats(esgpu_ctx* c, const DevCol
     }
     // hot set: the H most frequent ordinals (ties by ordinal), slot 0 the most frequent
     std::vector<uint32_t> hot;
-    uint64_t hot_total = 0;
-    if (H && !ESGPU_NO_HOT) {
-        const uint32_t ncand = (uint32_t)std::min<uint64_t>(T, H);
-        std::vector<uint32_t> idx(T);
-        for (uint32_t o = 0; o < T; ++o) idx[o] = o;
-        auto better = [&](uint32_t a, uint32_t b) { return cnt[a] != cnt[b] ? cnt[a] > cnt[b] : a < b; };
-        if (ncand < T) std::nth_element(idx.begin(), idx.begin() + ncand, idx.end(), better);
-        idx.resize(ncand);
-        std::sort(idx.begin(), idx.end(), better);
-        for (uint32_t o : idx) {
-            if (cnt[o] == 0) break;
-            hot.push_back(o);
-            hot_total += cnt[o];
+    uint64_t hot_total = 0, total = 0;
+    {
+        DevBuf dcand, dmeta;
+        dcand.alloc(c, (size_t)std::max<uint32_t>(T, 1) * 8);
+        dmeta.alloc(c, (2048 + 2) * 4 + 16);
+        HIPX(hipMemsetAsync(dmeta.p, 0, dmeta.bytes, st));
+        TopkParams K{};
+        K.counts32 = dcnt.as<unsigned int>();
+        K.T = T;
+        K.order = ESGPU_ORDER_COUNT_DESC;
+        K.min_doc_count = 1;
+        K.shard_min_doc_count = 0;
+        K.k = std::max<uint32_t>(std::min<uint32_t>(H, T), 1);
+        K.n_wg = std::min<uint32_t>(512, (T + 4095) / 4096);
+        K.cand = dcand.as<unsigned long long>();
+        K.hist = dmeta.as<uint32_t>();
+        K.sel = K.hist + 2048;
+        K.out_sum = (unsigned long long*)(dmeta.as<unsigned char>() + (2048 + 2) * 4);  // 8,200: 8-byte aligned
+        launch_topk_candidates(K, st);
+        HIPX(hipGetLastError());
+        uint32_t sel[2];
+        HIPX(hipMemcpyAsync(sel, K.sel, 8, hipMemcpyDeviceToHost, st));
+        HIPX(hipMemcpyAsync(&total, K.out_sum, 8, hipMemcpyDeviceToHost, st));
+        HIPX(hipStreamSynchronize(st));
+        if (H && !ESGPU_NO_HOT && sel[1]) {
+            std::vector<unsigned long long> keys(sel[1]);
+            HIPX(hipMemcpyAsync(keys.data(), dcand.p, keys.size() * 8, hipMemcpyDeviceToHost, st));
+            HIPX(hipStreamSynchronize(st));
+            const size_t take = std::min<size_t>(keys.size(), H);
+            std::partial_sort(keys.begin(), keys.begin() + take, keys.end(), std::greater<unsigned long long>());
+            for (size_t i = 0; i < take; ++i) {  // key: flag | count << 32 | ~ordinal (make_topk_key, _count desc)
+                const uint64_t cntv = (keys[i] >> 32) & 0x7FFFFFFFull;
+                if (cntv == 0) break;
+                hot.push_back(0xFFFFFFFFu - (uint32_t)keys[i]);
+                hot_total += cntv;
+            }
         }
         if (hot_total * 20 < total) {  // under 5 % of the docs: the recoded copy would not pay for itself
             hot.clear();
             hot_total = 0;
         }
     }
+    hs->docs = total;
     hs->hot_n = (uint32_t)hot.size();
     hs->hot_docs = hot_total;
-    std::vector<uint8_t> is_hot(T, 0);
-    for (uint32_t o : hot) is_hot[o] = 1;
     std::vector<uint64_t> cold(P, 0);
     uint64_t max_cold = 0;
-    for (uint32_t o = 0; o < T; ++o) {
-        if (!cnt[o] || is_hot[o]) continue;
-        cold[o >> kPartShift] += cnt[o];
-        max_cold = std::max(max_cold, cnt[o]);
+    {
+        std::vector<uint64_t> bits(((size_t)T + 63) / 64, 0);
+        for (uint32_t o : hot) bits[o >> 6] |= 1ull << (o & 63);
+        DevBuf dbits, dsum, dmax;
+        dbits.alloc(c, std::max<size_t>(bits.size(), 1) * 8);
+        dsum.alloc(c, (size_t)P * 8);
+        dmax.alloc(c, (size_t)P * 4);
+        HIPX(hipMemcpyAsync(dbits.p, bits.data(), bits.size() * 8, hipMemcpyHostToDevice, st));
+        launch_hc_part_stats(dcnt.as<unsigned int>(), T, kPartShift, P, dbits.as<uint64_t>(), dsum.as<unsigned long long>(),
+                             dmax.as<unsigned int>(), st);
+        HIPX(hipGetLastError());
+        std::vector<uint32_t> pmax(P);
+        HIPX(hipMemcpyAsync(cold.data(), dsum.p, (size_t)P * 8, hipMemcpyDeviceToHost, st));
+        HIPX(hipMemcpyAsync(pmax.data(), dmax.p, (size_t)P * 4, hipMemcpyDeviceToHost, st));
+        HIPX(hipStreamSynchronize(st));  // `bits` is read by the copy above
+        for (uint32_t m : pmax) max_cold = std::max<uint64_t>(max_cold, m);
     }
     hs->u16 = max_cold < 65536;
     // layout: per partition, G static regions of `chunk` (its expected share per workgroup) then an overflow pool that
@@ -2517,8 +2545,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         const SpecNode& ti = p->specs[pl.hist_spec];
         const uint64_t W = std::max<uint64_t>(1, std::min<uint64_t>(T, (uint64_t)std::max<int64_t>(to.s.shard_size, 0)));
         const bool agg2 = ti.s.order == ESGPU_ORDER_AGG_ASC || ti.s.order == ESGPU_ORDER_AGG_DESC;
-        pl.deferred = T * H > defer_cells() && W * replay_stride(H) <= (1ull << 31) && (!agg2 || H <= 65536) &&
-                      (agg2 || H <= 65536 || (uint64_t)std::max<int64_t>(ti.s.shard_size, 1) <= kTopkMax);
+        pl.deferred = T * H > defer_cells() && W * replay_stride(H) <= (1ull << 31) && (!agg2 || H <= 65536);
     }
     if (pl.deferred && oc) {
         require(!oc->multi && !(hc && hc->multi), ESGPU_ERR_UNSUPPORTED,
@@ -3913,6 +3940,10 @@ static ReplaySel replay_child(esgpu_plan* p, const ChildSrc& kid, const std::vec
     if (!host_sel && kid.rpipes.size() == 1 && R0.met == 0 && R0.cards.empty()) {
         const uint64_t part_cells = (uint64_t)kPartMaxStaged << kPartShift;
         wb = (uint32_t)std::min<uint64_t>(k, std::max<uint64_t>(1, part_cells / replay_stride(B0.value_count2)));
+        if (const char* e = std::getenv("ESGPU_REPLAY_BATCH")) {  // tests: smaller batches on small grids
+            const int v = std::atoi(e);
+            if (v >= 1) wb = std::min<uint32_t>(wb, (uint32_t)v);
+        }
     }
     LeafRef ord2;
     if (agg2)
@@ -3959,7 +3990,11 @@ static ReplaySel replay_child(esgpu_plan* p, const ChildSrc& kid, const std::vec
             }
             continue;
         }
-        if (host_sel) {  // the winners' rows on the host (one pass: wb == k)
+        const bool count_order = tn2.s.order == ESGPU_ORDER_COUNT_DESC || tn2.s.order == ESGPU_ORDER_COUNT_ASC;
+        const uint32_t kk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nb, (uint64_t)std::max<int64_t>(tn2.s.shard_size, 0)));
+        // an inner shard_size beyond the GPU top-k's final sort: count orders select their candidates on the GPU and
+        // sort them on the host (below); term orders select from the batch's rows on the host
+        if (host_sel || (kk > kTopkMax && !count_order)) {  // the winners' rows on the host
             for (int pi : kid.rpipes) fetch_grid(p, p->pipes[pi]);
             bsync(p);
             for (uint32_t r = 0; r < kb; ++r) {
@@ -3972,11 +4007,10 @@ static ReplaySel replay_child(esgpu_plan* p, const ChildSrc& kid, const std::vec
             continue;
         }
         // per winner row: the GPU top-k (K3) over its inner ordinals, then one gather of the picked cells of every array
-        const bool count_order = tn2.s.order == ESGPU_ORDER_COUNT_DESC || tn2.s.order == ESGPU_ORDER_COUNT_ASC;
-        const uint32_t kk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nb, (uint64_t)std::max<int64_t>(tn2.s.shard_size, 0)));
-        require(kk <= kTopkMax, ESGPU_ERR_UNSUPPORTED, "inner shard_size beyond the GPU top-k");
+        const bool big = kk > kTopkMax;
         unsigned long long* dk = (unsigned long long*)p->s_rkeys.ensure(p->ctx, (size_t)kb * (kk + 1) * 8);
         HIPX(hipMemsetAsync(dk, 0, (size_t)kb * (kk + 1) * 8, st));
+        std::vector<unsigned long long> big_keys;
         const uint32_t n_wg = std::min<uint32_t>(512, (uint32_t)((nb + 4095) / 4096));
         unsigned long long* cand = (unsigned long long*)p->s_cand.ensure(p->ctx, (count_order ? (size_t)nb : (size_t)n_wg * kk) * 8);
         uint32_t* hs = (uint32_t*)p->s_hist.ensure(p->ctx, (2048 + 2) * 4);
@@ -3995,12 +4029,38 @@ static ReplaySel replay_child(esgpu_plan* p, const ChildSrc& kid, const std::vec
             K.sel = hs + 2048;
             K.out_keys = dk + (size_t)r * (kk + 1);
             K.out_sum = K.out_keys + kk;
-            launch_topk(K, st);
+            if (!big) {
+                launch_topk(K, st);
+                HIPX(hipGetLastError());
+                continue;
+            }
+            // the histogram threshold and the candidates at or above it on the GPU; their sort on the host
+            launch_topk_candidates(K, st);
             HIPX(hipGetLastError());
+            uint32_t* hsel = (uint32_t*)p->h_rfill.ensure(16);
+            HIPX(hipMemcpyAsync(hsel, K.sel, 8, hipMemcpyDeviceToHost, st));
+            HIPX(hipMemcpyAsync(hsel + 2, K.out_sum, 8, hipMemcpyDeviceToHost, st));
+            bsync(p);
+            const uint32_t nc = hsel[1];
+            uint64_t row_sum;
+            std::memcpy(&row_sum, hsel + 2, 8);
+            d2h_u64(p, p->h_rcand, cand, nc);
+            bsync(p);
+            std::vector<unsigned long long> ck(p->h_rcand.as<unsigned long long>(), p->h_rcand.as<unsigned long long>() + nc);
+            const size_t take = std::min<size_t>(kk, ck.size());
+            std::partial_sort(ck.begin(), ck.begin() + take, ck.end(), std::greater<unsigned long long>());
+            big_keys.resize((size_t)kb * (kk + 1), 0ull);
+            std::copy(ck.begin(), ck.begin() + take, big_keys.begin() + (size_t)r * (kk + 1));
+            big_keys[(size_t)r * (kk + 1) + kk] = row_sum;
         }
-        d2h_u64(p, p->h_rkeys, dk, (size_t)kb * (kk + 1));
-        bsync(p);
-        const unsigned long long* hk = p->h_rkeys.as<unsigned long long>();
+        const unsigned long long* hk;
+        if (big) {
+            hk = big_keys.data();
+        } else {
+            d2h_u64(p, p->h_rkeys, dk, (size_t)kb * (kk + 1));
+            bsync(p);
+            hk = p->h_rkeys.as<unsigned long long>();
+        }
         std::vector<uint32_t> cells;
         for (uint32_t r = 0; r < kb; ++r) {
             const unsigned long long* ki = hk + (size_t)r * (kk + 1);

@@ -159,3 +159,26 @@ def test_hosts_by_urls_10m(engine):
     assert got["hosts"]["buckets"][0]["urls"]["buckets"]
     plan.close()
     seg.close()
+
+
+@pytest.mark.parametrize("order", ["count", "term", "count_asc"])
+def test_replayed_batches_compacted(engine, forced, monkeypatch, order):
+    """Count-only inner terms over 100,000 ordinals replayed in batches of 2 winners (ESGPU_REPLAY_BATCH): the winners'
+    docs are compacted once per retained segment into per-batch regions -- under a query filter and live docs, over two
+    segments -- and each batch is counted from its region (ReplayCompactParams)."""
+    monkeypatch.setenv("ESGPU_REPLAY_BATCH", "2")
+    inner = AB.terms("B").field("b").size(4)
+    inner.order(Order.count(False) if order == "count" else Order.term(True) if order == "term" else Order.count(True))
+    aggs = [AB.terms("A").field("a").size(5).subAggregation(inner)]
+    _run(engine, aggs, t_b=100_000, n=150_000, shards=1, segs_per_shard=2, filters=[QB.termQuery("status", 200)],
+         deletes=0.03)
+
+
+@pytest.mark.parametrize("order", ["count", "term", "count_asc"])
+def test_replayed_inner_shard_size_over_1024(engine, forced, order):
+    """An inner shard_size above the GPU top-k's final sort (1,100 of 100,000 inner terms): count orders take the GPU's
+    threshold candidates and sort them on the host, term orders select from the fetched rows (refused before round 4)."""
+    inner = AB.terms("B").field("b").size(1100)
+    inner.order(Order.count(False) if order == "count" else Order.term(True) if order == "term" else Order.count(True))
+    aggs = [AB.terms("A").field("a").size(3).subAggregation(inner)]
+    _run(engine, aggs, t_b=100_000, n=200_000, shards=1)
