@@ -511,33 +511,38 @@ void stream_leaf(Block& m, const Block* proto, const std::vector<OutBucket>& buc
 void emit_buckets(Block& out, const std::vector<OutBucket>& buckets, const Scratch& sc, std::vector<Level>& child,
                   DenseKeys* dk = nullptr) {
     const size_t nb = buckets.size();
-    out.key.reserve(out.key.size() + nb);
-    out.term_off.reserve(out.term_off.size() + nb);
-    out.bcount.reserve(out.bcount.size() + nb);
-    out.berr.reserve(out.berr.size() + nb);
-    for (size_t j = 0; j < out.subs.size(); ++j) {
-        Block& m = out.subs[j];
-        if (!fused_leaf(m) || dk) continue;
-        for (auto* v : {&m.sum, &m.min, &m.max, &m.sumsq}) v->reserve(v->size() + nb);
-        m.count.reserve(m.count.size() + nb);
-    }
-    for (const OutBucket& ob : buckets) {
-        out.key.push_back(ob.key);
+    // the bucket arrays sized once and written by index; then each sub-aggregation's instances in bucket order (every
+    // sub-block is independent of the others, so per-sub passes append exactly what the per-bucket loop did)
+    const size_t k0 = out.key.size(), t0 = out.term_off.size();
+    out.key.resize(k0 + nb);
+    out.bcount.resize(k0 + nb);
+    out.berr.resize(k0 + nb);
+    out.term_off.resize(t0 + nb);
+    for (size_t q = 0; q < nb; ++q) {
+        const OutBucket& ob = buckets[q];
+        out.key[k0 + q] = ob.key;
         if (ob.tb) {
             const std::string_view t = term_of(*ob.tb, ob.tk);
             out.term_pool.append(t.data(), t.size());
         }
-        out.term_off.push_back(out.term_pool.size());
-        out.bcount.push_back(ob.count);
-        out.berr.push_back(ob.err);
-        for (size_t j = 0; j < out.subs.size(); ++j) {
-            if (fused_leaf(out.subs[j])) {
-                if (dk) continue;  // streamed below
-                if (ob.empty) out.subs[j].append_instance(out.empty_subs[j], 0);
-                else reduce_leaf(out.subs[j], sc, j, ob.c0, ob.c1);
-                continue;
+        out.term_off[t0 + q] = out.term_pool.size();
+        out.bcount[k0 + q] = ob.count;
+        out.berr[k0 + q] = ob.err;
+    }
+    for (size_t j = 0; j < out.subs.size(); ++j) {
+        Block& m = out.subs[j];
+        if (fused_leaf(m)) {
+            if (dk) continue;  // streamed below
+            for (auto* v : {&m.sum, &m.min, &m.max, &m.sumsq}) v->reserve(v->size() + nb);
+            m.count.reserve(m.count.size() + nb);
+            for (const OutBucket& ob : buckets) {
+                if (ob.empty) m.append_instance(out.empty_subs[j], 0);
+                else reduce_leaf(m, sc, j, ob.c0, ob.c1);
             }
-            Level& lv = child[j];
+            continue;
+        }
+        Level& lv = child[j];
+        for (const OutBucket& ob : buckets) {
             if (ob.empty) {
                 const Ref r{&out.empty_subs[j], 0};
                 lv.add(&r, 1, true);
@@ -861,7 +866,14 @@ void reduce_histogram(const Ref* refs, size_t nrefs, Block& out, Scratch& sc, st
     }
     if (out.min_doc_count == 0 && out.has_empty_info) {  // addEmptyBuckets (InternalHistogram.java:395-449)
         const Rounding rnd = out.rounding();
-        auto next = [&](int64_t k) { return rnd.next_rounding_value(k); };
+        // an affine rounding's next bucket key is the key plus its interval (no time-zone arithmetic per bucket)
+        int64_t ai = 0, ao = 0;
+        const bool aff = rnd.affine(&ai, &ao);
+        auto next = [&](int64_t k) {
+            int64_t n;
+            if (aff && !__builtin_add_overflow(k, ai, &n)) return n;
+            return rnd.next_rounding_value(k);
+        };
         auto empty = [](int64_t k) { return OutBucket{k, nullptr, 0, 0, 0, 0, 0, true}; };
         std::vector<OutBucket>& filled = sc.filled;
         filled.clear();
