@@ -1384,11 +1384,8 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
             const int t = p->specs[n.order_child].s.type;
             if (t == ESGPU_AGG_CARDINALITY) {
                 // CardinalityAggregator.metric(bucketOrd) = counts.cardinality(bucketOrd) (a single-value metric): every
-                // candidate ordinal's sketch estimate, derived at build for a top-level terms (or one under a top-level
-                // filter); under another bucket level the per-row sketches are not gathered for selection
-                const int par = n.s.parent;
-                require(filter_chain_to_top(p.get(), par), ESGPU_ERR_UNSUPPORTED,
-                        "terms under another bucket aggregation ordered by a cardinality runs on the CPU path");
+                // candidate ordinal's sketch estimate, derived at build from the sketches gathered beside the cells
+                // (order_value), at the top level or under other bucket levels
                 require(key.empty() || key == "value", ESGPU_ERR_INVALID, "Invalid terms aggregation order path [" + n.order_path +
                         "]. Ordering on a single-value metrics aggregation can only be done on its value.");
                 n.order_key = key;
@@ -3749,8 +3746,15 @@ static std::vector<Block> child_protos(const esgpu_plan* p, const Group& g) {
 
 // the InternalOrder.Aggregation value of terms spec `t` for ordinal cell c of the pipeline holding its order child
 static double order_value(const esgpu_plan* p, const SpecNode& t, const Pipeline& pl, int leaf, size_t c) {
-    const MetricCell m = metric_cell(p, pl, leaf, c);
     const SpecNode& mn = p->specs[t.order_child];
+    if (mn.s.type == ESGPU_AGG_CARDINALITY) {
+        // CardinalityAggregator.metric(bucketOrd) = counts.cardinality(bucketOrd): the estimate of the cell's sketch,
+        // gathered to the host beside the cells (the same host-cell layout at every nesting level)
+        for (const CardState& cs : pl.cards)
+            if (cs.spec == t.order_child) return (double)card_estimate(cs, c);
+        return 0.0;
+    }
+    const MetricCell m = metric_cell(p, pl, leaf, c);
     double v = NAN;
     metric_value(mn.s.type, t.order_key, m.count, m.sum, m.min, m.max, m.sq, mn.s.sigma, &v);
     return v;

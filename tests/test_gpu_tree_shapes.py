@@ -240,3 +240,42 @@ def test_nested_filter_aggregations(engine):
     red = _both(engine, aggs, n=300_000, shards=2, filters=[QB.rangeQuery("price").gte(2.0)], exact=False)
     assert red["ok"]["big"]["empty"]["doc_count"] == 0
     assert 0 < red["ok"]["big"]["cheap"]["doc_count"] < red["ok"]["big"]["doc_count"] < red["ok"]["doc_count"]
+
+
+@pytest.mark.parametrize("asc", [False, True])
+def test_terms_ordered_by_cardinality_below_the_top(engine, asc):
+    """InternalOrder.Aggregation over a cardinality child of terms nested in another bucket aggregation: terms under a
+    date_histogram, terms under terms, and the middle terms of terms{terms{date_histogram}} -- each candidate cell's
+    sketch estimate (CardinalityAggregator.metric(bucketOrd)) from the sketches gathered beside the cells (refused
+    before round 4)."""
+    rng = np.random.default_rng(77)
+    n = 250_000
+    cols = {
+        "g": {"type": N.COL_ORD_U32, "values": rng.integers(0, 3, size=n).astype(np.uint32), "terms": ["g0", "g1", "g2"]},
+        "k": {"type": N.COL_ORD_U32, "values": np.minimum(rng.zipf(1.3, size=n) - 1, 59).astype(np.uint32),
+              "terms": ["k%02d" % i for i in range(60)]},
+        "ip": {"type": N.COL_I64, "values": (rng.integers(0, 400, size=n) * rng.integers(1, 5, size=n)).astype(np.int64)},
+        "@timestamp": {"type": N.COL_I64, "values": np.sort(rng.integers(1441065600000, 1441065600000 + 3 * 86_400_000,
+                                                                         size=n)).astype(np.int64)},
+        "rt": {"type": N.COL_I64, "values": rng.integers(0, 1000, size=n).astype(np.int64)},
+    }
+    card = lambda nm: AB.cardinality(nm).field("ip").precisionThreshold(100)  # noqa: E731
+    aggs = [AB.dateHistogram("d").field("@timestamp").interval("1d").subAggregation(
+                AB.terms("h").field("k").size(3).order(Order.aggregation("ips", asc)).subAggregation(card("ips"))),
+            AB.terms("o").field("g").size(2).subAggregation(
+                AB.terms("i").field("k").size(4).order(Order.aggregation("c2.value", asc)).subAggregation(card("c2"))
+                .subAggregation(AB.avg("a").field("rt"))),
+            AB.terms("t1").field("g").size(2).subAggregation(
+                AB.terms("t2").field("k").size(3).order(Order.aggregation("c3", not asc)).subAggregation(card("c3"))
+                .subAggregation(AB.dateHistogram("d3").field("@timestamp").interval("1d")))]
+    lookups = {f: {t: i for i, t in enumerate(cols[f]["terms"])} for f in ("g", "k")}
+    ord_lookup = lambda f, t: lookups.get(f, {}).get(t, -1)  # noqa: E731
+    want = O.run([(cols, n)], aggs, ord_lookup=ord_lookup)
+    seg = engine.upload_segment(cols, n)
+    plan = engine.plan(aggs, ord_lookup=ord_lookup)
+    plan.collect(seg)
+    res = plan.build()
+    assert_same(res.to_dict(), want["shards"][0], "shard")
+    assert_same(reduce([res]).to_dict(), want["reduced"], "reduced")
+    plan.close()
+    seg.close()
