@@ -181,6 +181,12 @@ __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0,
     if (MET > 0 && (VK & 64)) {  // packed integer cells: a dense long metric as its compact u32 deltas
         load_u32x4(P.mv32, doc0, d.mvd);
         d.mpres = 0xFu;
+    } else if (MET > 0 && (VK & 128)) {  // a long metric read as its compact u32 deltas, the values restored exactly
+        uint32_t t[4];
+        load_u32x4(P.mv32, doc0, t);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d.mv[j] = (double)(P.mv_base + (int64_t)t[j]);  // FieldData.castToDouble of the long
+        d.mpres = P.mv_present ? bits4(P.mv_present, doc0) : 0xFu;
     } else if (MET > 0) {
         if (VK & 2) {
             load_f64x4((const double*)P.mv, doc0, d.mv);
@@ -366,12 +372,40 @@ template <int NR>
 struct Runs {
     Run r[NR];
     uint32_t victim;
+    // packed integer cells (VK bit 64) with ESGPU_PI_HOT: the segment's most frequent ordinal (CollectParams.hot_t)
+    // accumulated in registers for its current key slot -- the Zipf head's docs leave the LDS atomics, whose same-address
+    // conflicts they caused
+    uint32_t hslot, hlo, hhi;
+    unsigned long long hpk;
 };
 template <int NR>
 __device__ __forceinline__ void runs_reset(Runs<NR>& R) {
 #pragma unroll
     for (int k = 0; k < NR; ++k) run_reset(R.r[k]);
     R.victim = 0;
+    R.hslot = ~0u;
+    R.hlo = ~0u;
+    R.hhi = 0u;
+    R.hpk = 0ull;
+}
+#ifndef ESGPU_PI_HOT
+#define ESGPU_PI_HOT 0
+#endif
+// the hot ordinal's run into its LDS cell (before a window moves, and at the end)
+template <int MET, int NR>
+__device__ __forceinline__ void pi_hot_flush(const CollectParams& P, const Acc& a, Runs<NR>& R, uint32_t T) {
+    if (R.hslot != ~0u) {
+        const uint32_t c = R.hslot * T + P.hot_t;
+        atomicAdd(&a.pk[c + a.coff], R.hpk);
+        if (MET >= 2) {
+            if (R.hlo < a.mm[2 * c]) atomicMin(&a.mm[2 * c], R.hlo);
+            if (R.hhi > a.mm[2 * c + 1]) atomicMax(&a.mm[2 * c + 1], R.hhi);
+        }
+    }
+    R.hslot = ~0u;
+    R.hlo = ~0u;
+    R.hhi = 0u;
+    R.hpk = 0ull;
 }
 template <int MET, int MS, int NR>
 __device__ __forceinline__ void runs_flush(const CollectParams& P, const Acc& a, Runs<NR>& R) {
@@ -486,6 +520,21 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
             hit |= (uint32_t)(ok && hv_ok[j] && has_t) << j;
             cell[j] = slot[j] * T + t;
         }
+        const unsigned long long one = 1ull << P.pk_shift;
+#if ESGPU_PI_HOT
+#pragma unroll
+        for (int j = 0; j < kVec; ++j) {
+            if (!((hit >> j) & 1) || d.ord[j] != P.hot_t) continue;
+            if (slot[j] != run.hslot) {
+                pi_hot_flush<MET>(P, a, run, T);
+                run.hslot = slot[j];
+            }
+            run.hpk += one + d.mvd[j];
+            run.hlo = min(run.hlo, d.mvd[j]);
+            run.hhi = max(run.hhi, d.mvd[j]);
+            hit &= ~(1u << j);
+        }
+#endif
         uint32_t mlo[kVec], mhi[kVec];
         if (MET >= 2) {
 #pragma unroll
@@ -499,7 +548,6 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
                 }
             }
         }
-        const unsigned long long one = 1ull << P.pk_shift;
 #pragma unroll
         for (int j = 0; j < kVec; ++j)
             if ((hit >> j) & 1) atomicAdd(&a.pk[cell[j] + a.coff], one + d.mvd[j]);
@@ -814,7 +862,7 @@ __global__ __launch_bounds__(WGS) void collect_kernel(CollectParams P) {
     // buffers are 5x larger; 4 would cost occupancy).  kItersPerBlockW (4) is a multiple of either.
     constexpr int kBuf = (MET == 0 && !(ORD && HIST)) ? ESGPU_NBUF_NARROW
                          : (VK & 64) ? (ESGPU_NBUF_PI <= kItersPerBlockW ? ESGPU_NBUF_PI : kItersPerBlockW)
-                         : ((VK & 48) ? (ESGPU_NBUF_COMPACT <= kItersPerBlockW ? ESGPU_NBUF_COMPACT : kItersPerBlockW) : 2);
+                         : ((VK & 176) ? (ESGPU_NBUF_COMPACT <= kItersPerBlockW ? ESGPU_NBUF_COMPACT : kItersPerBlockW) : 2);
     static_assert(kItersPerBlockW % kBuf == 0, "buffers per block");
     Doc4 q[kBuf];
 #pragma unroll
@@ -827,6 +875,7 @@ __global__ __launch_bounds__(WGS) void collect_kernel(CollectParams P) {
     auto slide_to = [&](uint32_t k0) {
         if (dirty) {
             if (!ORD) runs_flush<MET, kMS>(P, s, run);
+            if constexpr (PI && ESGPU_PI_HOT) pi_hot_flush<MET>(P, s, run, T);
             if constexpr (PI) flush_window_pi<MET, WGS>(P, s, T, W, win0, ncp);
             else flush_window<MET, kMS, WGS>(P, s, T, W, win0, ncp);
         }
@@ -921,6 +970,7 @@ __global__ __launch_bounds__(WGS) void collect_kernel(CollectParams P) {
     }
     if (P.lds_mode && (dirty || !(HIST && P.windowed))) {
         if (!ORD) runs_flush<MET, kMS>(P, s, run);
+        if constexpr (PI && ESGPU_PI_HOT) pi_hot_flush<MET>(P, s, run, T);
         if constexpr (PI) flush_window_pi<MET, WGS>(P, s, T, W, win0, ncp);
         else flush_window<MET, kMS, WGS>(P, s, T, W, win0, ncp);
     }
@@ -979,7 +1029,21 @@ static auto with_vk0(bool hv_f64, bool mv_f64, F f) {
 // Bits 16 / 32 (compact ordinal / histogram columns): terms dimensions without a derived key index, affine histograms
 // over a long column.
 template <bool ORD, int HK, int MET, class F>
-static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, bool pi, F f) {
+static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, bool pi, bool m32, F f) {
+    // VK bit 128, a compact long metric (u32 deltas, values restored in the loader): histogram-only grids over compact
+    // timestamps (date_histogram{stats / extended_stats / avg}) and extended_stats under terms over compact columns
+    if constexpr (MET > 0 && !ORD && HK == 1) {
+        if (m32 && !pi && !mv_f64 && t32 && !hv_f64) return f(std::integral_constant<int, 32 | 128>{});
+    }
+    if constexpr (MET == 3 && ORD && (HK == 0 || HK == 1)) {
+        if (m32 && !pi && !mv_f64 && !dord && c16) {
+            if constexpr (HK == 1) {
+                if (t32 && !hv_f64) return f(std::integral_constant<int, 48 | 128>{});
+            } else {
+                return f(std::integral_constant<int, 16 | 128>{});
+            }
+        }
+    }
     // VK bit 64, packed integer metric cells: terms grids (no key, or an affine key over the compact timestamps) with
     // avg / stats over a dense long metric
     if constexpr (ORD && (HK == 0 || HK == 1) && (MET == 1 || MET == 2)) {
@@ -1026,8 +1090,8 @@ static auto with_wg(bool wide, F f) {
 
 template <bool ORD, int HK, int MET>
 static void launch_t(const CollectParams& p, bool wide, uint32_t grid, size_t lds, hipStream_t st) {
-    with_vk<ORD, HK, MET>(p.hv_f64 != 0, p.mv_f64 != 0, p.ord_src != nullptr, p.ord16 != nullptr, p.hv32 != nullptr, p.mv32 != nullptr,
-                          [&](auto vk) {
+    with_vk<ORD, HK, MET>(p.hv_f64 != 0, p.mv_f64 != 0, p.ord_src != nullptr, p.ord16 != nullptr, p.hv32 != nullptr,
+                          p.mv32 != nullptr && p.pk_shift != 0, p.mv32 != nullptr && p.pk_shift == 0, [&](auto vk) {
         return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
             hipLaunchKernelGGL((collect_kernel<ORD, HK, MET, decltype(vk)::value, decltype(wg)::value>), dim3(grid),
                                dim3(decltype(wg)::value), lds, st, p);
@@ -1049,7 +1113,7 @@ static void launch_m(const CollectParams& p, int met, bool wide, uint32_t grid, 
 template <bool ORD, int HK, int MET>
 static int occ_t(size_t lds, int vkbits, bool wide) {
     return with_vk<ORD, HK, MET>((vkbits & 1) != 0, (vkbits & 2) != 0, (vkbits & 8) != 0, (vkbits & 16) != 0,
-                                 (vkbits & 32) != 0, (vkbits & 64) != 0, [&](auto vk) {
+                                 (vkbits & 32) != 0, (vkbits & 64) != 0, (vkbits & 128) != 0, [&](auto vk) {
         return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
             int n = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(

@@ -304,6 +304,9 @@ struct DevColumn {
     DevBuf ord16, d32;
     const void* ord16_src = nullptr;
     bool d32_done = false;
+    // the most frequent ordinal of ords() in a sample (a hint for the packed cells' register run; any value is correct)
+    uint32_t hot_ord = 0xFFFFFFFFu;
+    const void* hot_src = nullptr;
 
     const DevBuf& ords() const { return gdict ? gvalues : values; }       // what terms aggregations count by
     uint64_t ord_count() const { return gdict ? gdict->count() : value_count; }
@@ -1591,6 +1594,7 @@ static bool pi_cells(const esgpu_ctx* c);
 static uint32_t pi_copies();
 static const uint16_t* ensure_ord16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
 static const uint32_t* ensure_d32(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
+static uint32_t sampled_hot_ord(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s);
 
 // The pipeline's clauses as device predicates: up to kMaxPreds of them are evaluated inside the collect kernels; with
 // more, all of them (and the accept bitset) are folded first into one doc bitset -- chained filter_bits passes of four
@@ -1817,7 +1821,12 @@ struct HcStats {
     uint64_t pbuf_elems = 0;     // partition regions + kHcTile spare elements
     uint64_t hot_docs = 0, docs = 0;
     bool refused = false;        // outside what the hot/cold kernels handle (cached: the check counts the column)
-    DevBuf d_rc;                 // recoded ordinal column (hot ordinals as kHcHotBit | slot); empty: no hot set
+    // recoded ordinal column (hot ordinals as kHcHotBit | slot); empty: no hot set, or released once the postings form is
+    // ready (the hot16 column and the cold lists serve unfiltered requests) and rebuilt from the hot table on the first
+    // request that needs it (predicates, live docs: ensure_rc)
+    mutable DevBuf d_rc;
+    DevBuf d_rc_keys, d_rc_vals;  // the hot ordinals' open-addressing table (hc_recode)
+    uint32_t rc_log2 = 0;
     DevBuf d_hot16;              // the hot slot of each doc in 16 bits (0xFFFF: cold / missing) for the postings hot pass
     DevBuf d_hot_ord, d_part, d_piece;
     // cold lists: the cold docs' partition-local offsets grouped by partition (postings of the cold ordinals, 64-element
@@ -2029,7 +2038,9 @@ static std::shared_ptr<const HcStats> ensure_hc_stats(esgpu_ctx* c, const DevCol
             keys[h] = hot[sl];
             vals[h] = sl;
         }
-        DevBuf dk, dv;
+        DevBuf& dk = hs->d_rc_keys;
+        DevBuf& dv = hs->d_rc_vals;
+        hs->rc_log2 = log2;
         dk.alloc(c, keys.size() * 4);
         dv.alloc(c, vals.size() * 4);
         HIPX(hipMemcpy(dk.p, keys.data(), keys.size() * 4, hipMemcpyHostToDevice));
@@ -2117,8 +2128,29 @@ static std::shared_ptr<const HcStats> ensure_hc_stats(esgpu_ctx* c, const DevCol
             hs->cold_lists = true;
         }
     }
+    // the postings form is complete: the 32-bit recoded column (2 B per doc more than the hot16 column) is released and
+    // rebuilt only for a request that scatters or subtracts dead docs (ESGPU_HC_KEEP_RC=1 keeps it)
+    if (hs->cold_lists && hs->d_hot16.p && hs->d_rc.p) {
+        static const bool keep = [] { const char* e = std::getenv("ESGPU_HC_KEEP_RC"); return e && *e == '1'; }();
+        if (!keep) hs->d_rc.release();
+    }
     mcol->hc = hs;
     return hs;
+}
+
+// the recoded column of a segment's statistics, rebuilt from the hot table when it was released (under the context
+// lock: plans on other threads may share the segment)
+static const uint32_t* ensure_rc(esgpu_ctx* c, const HcStats& hs, const DevColumn* col, const esgpu_segment* s, hipStream_t st) {
+    if (!hs.hot_n) return col->ords().as<uint32_t>();
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!hs.d_rc.p) {
+        hs.d_rc.alloc(c, (size_t)s->n_pad * 4);
+        launch_hc_recode(col->ords().as<uint32_t>(), s->n_pad, hs.d_rc_keys.as<uint32_t>(), hs.d_rc_vals.as<uint32_t>(), hs.rc_log2,
+                         hs.d_rc.as<uint32_t>(), st);
+        HIPX(hipGetLastError());
+        HIPX(hipStreamSynchronize(st));
+    }
+    return hs.d_rc.as<uint32_t>();
 }
 
 static bool collect_hotcold(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const DevColumn* oc,
@@ -2132,7 +2164,10 @@ static bool collect_hotcold(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s,
     H.n_blocks = s->n_pad / kBlockDocs;
     H.G = hs->G;
     H.blocks_per_wg = std::max(1u, (H.n_blocks + H.G - 1) / H.G);
-    H.rc = hs->hot_n ? hs->d_rc.as<uint32_t>() : oc->ords().as<uint32_t>();
+    // the recoded column: read by the scatter form and the dead-doc subtraction; an unfiltered request on the postings
+    // form reads only the hot16 column and the cold lists
+    const bool clean_postings = hs->cold_lists && npred == 0 && !d_accept && hs->d_hot16.p && hc_hot16();
+    H.rc = clean_postings ? nullptr : ensure_rc(c, *hs, oc, s, st);
     H.T = pl.T;
     H.P = hs->P;
     H.npred = npred;
@@ -2685,6 +2720,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     CollectParams P{};
     P.n_docs = s->max_doc;
     P.n_blocks = s->n_pad / kBlockDocs;
+    P.hot_t = kMissingOrd;
     if (P.n_blocks == 0) return 0;
     P.ord = oc ? oc->ords().as<uint32_t>() : nullptr;
     if (fuse_ords && L_ORD) {
@@ -2768,6 +2804,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         if (const uint32_t* d = ensure_d32(p->ctx, mc, s, p->stream)) {
             P.mv32 = d;
             P.mv_base = mc->vmin;
+            P.hot_t = sampled_hot_ord(p->ctx, oc, s);
             pi = true;
         }
     }
@@ -2783,6 +2820,21 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         return sh < 64 && (maxsum >> sh) == 0 && (mag >> 62) == 0;
     };
   relaunch:
+    // otherwise a long metric spanning < 2^32 is still read as its compact u32 deltas where a kernel instantiation reads
+    // them (VK bit 128, with_vk): date_histogram{stats / extended_stats / avg} over compact timestamps, extended_stats
+    // under terms over compact columns -- 4 B per doc instead of 8, the values restored exactly in the loader
+    bool m32 = false;
+    if (!pi && compact_cols(p->ctx) && L_met > 0 && mc && mc->type == ESGPU_COL_I64 && !mc->multi && mc->vmin <= mc->vmax &&
+        (uint64_t)mc->vmax - (uint64_t)mc->vmin < (1ull << 32) && !P.mv_f64 && !inner_missing &&
+        ((!L_ORD && hk_launch == 1 && P.hv32 && !P.hv_f64) ||
+         (L_ORD && L_met == 3 && !P.ord_src && P.ord16 && (hk_launch == 0 || (hk_launch == 1 && P.hv32 && !P.hv_f64))))) {
+        if (const uint32_t* d = ensure_d32(p->ctx, mc, s, p->stream)) {
+            P.mv32 = d;
+            P.mv_base = mc->vmin;
+            P.pk_shift = 0;
+            m32 = true;
+        }
+    }
 
     // LDS sizing: the whole grid if it fits, else a sliding window over the key dimension (time-sorted data)
 #ifndef ESGPU_LDS_PAIR  // LDS budget of a window that keeps two workgroups per CU
@@ -2872,8 +2924,8 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     }
     const int hk = L_HIST ? (P.hord ? 3 : P.kstart ? 2 : 1) : 0;
     const int vk = (P.hv_f64 ? 1 : 0) | (P.mv_f64 ? 2 : 0) | (P.ord_src ? 8 : 0) | (P.ord16 ? 16 : 0) | (P.hv32 ? 32 : 0) |
-                   (P.mv32 ? 64 : 0);
-    const uint64_t occ_key = ((uint64_t)lds << 16) | ((uint64_t)wide << 15) | ((uint64_t)vk << 8) | ((uint64_t)L_met << 4) |
+                   (pi ? 64 : 0) | (m32 ? 128 : 0);
+    const uint64_t occ_key = ((uint64_t)lds << 17) | ((uint64_t)wide << 16) | ((uint64_t)vk << 8) | ((uint64_t)L_met << 4) |
                              ((uint64_t)hk << 1) | (L_ORD ? 1 : 0);
     if (pl.occ_key != occ_key) {
         pl.occ = std::max(1, collect_occupancy(L_ORD, hk, L_met, lds, vk, wide));
@@ -2898,10 +2950,11 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     if (pi && P.lds_mode && !pi_fits(P.blocks_per_wg)) {  // a packed field could overflow: the f64 cells instead
         pi = false;
         P.mv32 = nullptr;
+        P.pk_shift = 0;
         P.ncopies = 1;
         goto relaunch;
     }
-    if (pi) bytes_per_doc -= 4;
+    if (pi || m32) bytes_per_doc -= 4;
     uint32_t grid = (P.n_blocks + P.blocks_per_wg - 1) / P.blocks_per_wg;
     // dynamic chunk claiming: one resident wave of workgroups, each flushing its LDS cells once, taking chunks of
     // kGroup blocks until none are left (ESGPU_DYN=0/1 overrides the build default for A/B runs)
@@ -2979,6 +3032,29 @@ static const uint16_t* ensure_ord16(esgpu_ctx* c, const DevColumn* col, const es
     HIPX(hipStreamSynchronize(st));
     return m->ord16.as<uint16_t>();
 }
+// the most frequent ordinal among 64 evenly spaced runs of 4,096 docs (cached with the ordinal buffer)
+static uint32_t sampled_hot_ord(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s) {
+    DevColumn* m = const_cast<DevColumn*>(col);
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (m->hot_src == col->ords().p) return m->hot_ord;
+    m->hot_src = col->ords().p;
+    m->hot_ord = kMissingOrd;
+    const uint64_t T = col->ord_count();
+    if (!T || T > (1u << 24) || s->max_doc == 0) return m->hot_ord;
+    const uint32_t run = std::min<uint32_t>(4096, s->max_doc), nrun = s->max_doc >= 64u * run ? 64u : 1u;
+    std::vector<uint32_t> buf((size_t)run * nrun), hist(T, 0);
+    for (uint32_t r = 0; r < nrun; ++r) {
+        const uint64_t at = nrun == 1 ? 0 : (uint64_t)(s->max_doc - run) * r / (nrun - 1);
+        HIPX(hipMemcpyAsync(buf.data() + (size_t)r * run, col->ords().as<uint32_t>() + at, (size_t)run * 4, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPX(hipStreamSynchronize(c->stream));
+    for (uint32_t o : buf) if (o < T) ++hist[o];
+    uint32_t best = 0;
+    for (uint64_t o = 1; o < T; ++o) if (hist[o] > hist[best]) best = (uint32_t)o;
+    if (hist[best]) m->hot_ord = best;
+    return m->hot_ord;
+}
+
 static const uint32_t* ensure_d32(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st) {
     DevColumn* m = const_cast<DevColumn*>(col);
     std::lock_guard<std::mutex> lk(c->mu);
