@@ -216,6 +216,7 @@ struct Acc {
     uint32_t coff;                  // this lane's copy of the additive LDS cells (CollectParams.ncopies); 0 in the grid
     unsigned long long* pk;         // LDS, packed integer cells (VK bit 64): count << pk_shift | sum of deltas [C][ncopies]
     uint32_t* mm;                   // LDS, packed integer cells: (min, max) delta pair per cell [C][2]
+    unsigned long long* pkd;        // LDS, packed integer cells: this thread's spare word (the adds of docs that hit nothing)
 };
 
 template <int MET, bool LDS, int MS>
@@ -391,6 +392,9 @@ __device__ __forceinline__ void runs_reset(Runs<NR>& R) {
 #ifndef ESGPU_PI_HOT
 #define ESGPU_PI_HOT 0
 #endif
+#ifndef ESGPU_PI_STRAIGHT  // packed cells: straight-line reads and adds (1), or under the hit mask (0, for A/B runs)
+#define ESGPU_PI_STRAIGHT 1
+#endif
 // the hot ordinal's run into its LDS cell (before a window moves, and at the end)
 template <int MET, int NR>
 __device__ __forceinline__ void pi_hot_flush(const CollectParams& P, const Acc& a, Runs<NR>& R, uint32_t T) {
@@ -535,7 +539,25 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
             hit &= ~(1u << j);
         }
 #endif
+        // straight-line LDS traffic, so the compiler can count the one wait below (lgkmcnt(4): the reads, not the adds
+        // queued behind them): every lane reads a (min, max) pair (a doc that hits nothing reads cell 0 and ignores it)
+        // and adds to a cell (a miss adds 0 to the lane's own spare word)
         uint32_t mlo[kVec], mhi[kVec];
+#if ESGPU_PI_STRAIGHT
+        if (MET >= 2) {
+#pragma unroll
+            for (int j = 0; j < kVec; ++j) {
+                const u32x2_t m = *reinterpret_cast<const u32x2_t*>(a.mm + 2 * (((hit >> j) & 1) ? cell[j] : 0u));
+                mlo[j] = m.x;
+                mhi[j] = m.y;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kVec; ++j) {
+            const bool h = (hit >> j) & 1;
+            atomicAdd(h ? &a.pk[cell[j] + a.coff] : a.pkd, h ? one + d.mvd[j] : 0ull);
+        }
+#else  // (A/B) reads and adds under the hit mask: the compiler then waits for every queued LDS op before the checks
         if (MET >= 2) {
 #pragma unroll
             for (int j = 0; j < kVec; ++j) {
@@ -551,6 +573,7 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
 #pragma unroll
         for (int j = 0; j < kVec; ++j)
             if ((hit >> j) & 1) atomicAdd(&a.pk[cell[j] + a.coff], one + d.mvd[j]);
+#endif
         if (MET >= 2) {
 #pragma unroll
             for (int j = 0; j < kVec; ++j) {
@@ -761,6 +784,7 @@ __global__ __launch_bounds__(WGS) void collect_kernel(CollectParams P) {
     g.mstride = 1;
     g.coff = 0;
     g.ocnt64 = P.g_ocnt;
+    g.pk = nullptr; g.mm = nullptr; g.pkd = nullptr;
     const uint32_t ncp = ORD ? max(P.ncopies, 1u) : 1u;  // additive cell copies (grids with a terms dimension)
 
     // LDS window view.  Every pointer is derived from `smem` alone -- never merged with a global pointer -- so the
@@ -779,10 +803,11 @@ __global__ __launch_bounds__(WGS) void collect_kernel(CollectParams P) {
         s.coff = ((threadIdx.x & 63) % ncp) * C;
         s.ocnt32 = (uint32_t*)carve(P.ocnt_mode == OCNT_TERMS ? sizeof(uint32_t) * T
                                     : P.ocnt_mode == OCNT_HIST ? sizeof(uint32_t) * W : 0);
+        s.pkd = (unsigned long long*)carve(8 * WGS) + threadIdx.x;
     } else {
         size_t off = 0;
         auto carve = [&](size_t bytes) { unsigned char* p = smem + off; off += (bytes + 15) & ~(size_t)15; return p; };
-        s.pk = nullptr; s.mm = nullptr;
+        s.pk = nullptr; s.mm = nullptr; s.pkd = nullptr;
         s.cnt64 = nullptr; s.vcnt64 = nullptr; s.ocnt64 = nullptr;
         s.cnt32 = (uint32_t*)carve(sizeof(uint32_t) * C * ncp);
         s.vcnt32 = (uint32_t*)carve(P.vcnt_mode ? sizeof(uint32_t) * C * ncp : 0);

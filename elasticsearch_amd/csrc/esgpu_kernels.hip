@@ -131,7 +131,7 @@ size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocn
         size_t bytes = r(8 * C * n) + (met >= 2 ? r(8 * C) : 0);
         if (ocnt_mode == OCNT_TERMS) bytes += r(4 * (size_t)T);
         if (ocnt_mode == OCNT_HIST) bytes += r(4 * (size_t)W);
-        return bytes;
+        return bytes + 8 * 1024;  // a spare word per thread (1024-thread workgroups at most)
     }
     size_t bytes = r(4 * C * n);
     if (vcnt_mode) bytes += r(4 * C * n);
@@ -2114,6 +2114,7 @@ void launch_comp_ords(const uint32_t* a, const uint32_t* b, uint32_t n_pad, uint
 // one 8192-doc block per workgroup: each doc's batch and replay ordinal, a position inside the workgroup's share of
 // its batch (the wave's lanes of one batch take consecutive positions with one LDS atomic: the Zipf-head winners put
 // most of a wave in one batch), one global reservation per (workgroup, batch), then the appends
+constexpr uint32_t kReplayFastBatches = 8;
 __global__ __launch_bounds__(kWG) void replay_compact_kernel(ReplayCompactParams P) {
     __shared__ uint32_t cnt[kReplayMaxBatches], base[kReplayMaxBatches];
     for (uint32_t i = threadIdx.x; i < P.nbatch; i += kWG) cnt[i] = 0;
@@ -2139,6 +2140,46 @@ __global__ __launch_bounds__(kWG) void replay_compact_kernel(ReplayCompactParams
             val[it][j] = live ? (w % P.wb) * P.stride + y[j] : 0u;
         }
     }
+    if (P.nbatch <= kReplayFastBatches) {
+        // few batches (the usual case: a handful of batches of winners): per batch, the lane's docs as a 16-bit mask, a
+        // wave scan of their counts and one returning LDS atomic per wave -- every batch's atomic issued before the
+        // first wait, so no round trip sits in a dependent chain per doc
+        uint32_t mb[kReplayFastBatches], wpre[kReplayFastBatches], wtot[kReplayFastBatches], wb[kReplayFastBatches];
+#pragma unroll
+        for (uint32_t b = 0; b < kReplayFastBatches; ++b) {
+            uint32_t m = 0;
+#pragma unroll
+            for (int it = 0; it < kItersPerBlock; ++it)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) m |= (uint32_t)(bid[it][j] == b) << (it * 4 + j);
+            mb[b] = m;
+            const uint32_t c = (uint32_t)__popc(m);
+            uint32_t incl = c;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(incl, off, 64);
+                if ((int)lane >= off) incl += y;
+            }
+            wtot[b] = __shfl(incl, 63, 64);
+            wpre[b] = incl - c;
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < kReplayFastBatches; ++b)
+            wb[b] = (lane == 0 && b < P.nbatch && wtot[b]) ? atomicAdd(&cnt[b], wtot[b]) : 0u;
+#pragma unroll
+        for (uint32_t b = 0; b < kReplayFastBatches; ++b) wb[b] = __shfl(wb[b], 0, 64) + wpre[b];
+#pragma unroll
+        for (int it = 0; it < kItersPerBlock; ++it)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t k = it * 4 + j;
+                uint32_t p = 0;
+#pragma unroll
+                for (uint32_t b = 0; b < kReplayFastBatches; ++b)
+                    if (bid[it][j] == b) p = wb[b] + (uint32_t)__popc(mb[b] & ((1u << k) - 1u));
+                pos[it][j] = p;
+            }
+    } else {
 #pragma unroll
     for (int it = 0; it < kItersPerBlock; ++it)
 #pragma unroll
@@ -2158,6 +2199,7 @@ __global__ __launch_bounds__(kWG) void replay_compact_kernel(ReplayCompactParams
             }
             pos[it][j] = p;
         }
+    }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < P.nbatch; i += kWG) base[i] = cnt[i] ? atomicAdd(&P.fill[i], cnt[i]) : 0u;
     __syncthreads();

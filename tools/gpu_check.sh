@@ -116,6 +116,9 @@ for s in $STEPS; do
         c3stats) # config 3: the per-segment statistics build (bench precomputed) and the filtered / deleted forms
               run bench_config3 300 python3 "$R/bench.py" --workload config3 --shards 8 --docs 125000000 --cpu-docs 0 --steps 5 &&
               run kbench_c3_125m_del 300 python3 "$R/tools/kbench.py" --docs 125000000 --reps 5 --only config3_url --deletes 0.01 ;;
+        profreplay) # kernel breakdown of the breadth-first replay (terms(host){terms(url)} at 1B docs)
+              cd /tmp && run rocprof_replay 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profreplay" -o kb -- \
+                  python3 "$R/tools/kbench.py" --docs 1000000000 --reps 2 --only hosts_urls ;;
         testfile) run "pytest_${TESTFILE:-x}" 600 python3 -u -m pytest "$R/tests/${TESTFILE:-test_gpu_parity}.py" -m gpu -x -v \
                       -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         pmc) cd /tmp && run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o bench -- \
