@@ -106,6 +106,14 @@ __device__ __forceinline__ uint32_t eval_pred(const PredDev& q, uint32_t doc0) {
             const bool hi = q.hi_incl ? v[j] <= q.dhi : v[j] < q.dhi;
             m |= (uint32_t)(lo && hi) << j;
         }
+    } else if (q.kind == PRED_D16_RANGE) {
+        const u32x2_t w = load8((const uint16_t*)q.col + doc0);
+        const uint32_t o[4] = {w.x & 0xFFFFu, w.x >> 16, w.y & 0xFFFFu, w.y >> 16};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t v = q.base + (int64_t)o[j];
+            m |= (uint32_t)(v >= q.lo && v <= q.hi) << j;
+        }
     } else if (q.kind == PRED_D32_RANGE) {
         uint32_t o[4];
         load_u32x4((const uint32_t*)q.col, doc0, o);
@@ -178,7 +186,11 @@ __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0,
         }
         d.hpres = P.hv_present ? bits4(P.hv_present, doc0) : 0xFu;
     }
-    if (MET > 0 && (VK & 64)) {  // packed integer cells: a dense long metric as its compact u32 deltas
+    if (MET > 0 && (VK & 64) && (VK & 256)) {  // packed integer cells over the 16-bit deltas (values span < 2^16)
+        const u32x2_t w = load8(P.mv16 + doc0);
+        d.mvd[0] = w.x & 0xFFFFu; d.mvd[1] = w.x >> 16; d.mvd[2] = w.y & 0xFFFFu; d.mvd[3] = w.y >> 16;
+        d.mpres = 0xFu;
+    } else if (MET > 0 && (VK & 64)) {  // packed integer cells: a dense long metric as its compact u32 deltas
         load_u32x4(P.mv32, doc0, d.mvd);
         d.mpres = 0xFu;
     } else if (MET > 0 && (VK & 128)) {  // a long metric read as its compact u32 deltas, the values restored exactly
@@ -1054,7 +1066,7 @@ static auto with_vk0(bool hv_f64, bool mv_f64, F f) {
 // Bits 16 / 32 (compact ordinal / histogram columns): terms dimensions without a derived key index, affine histograms
 // over a long column.
 template <bool ORD, int HK, int MET, class F>
-static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, bool pi, bool m32, F f) {
+static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, bool pi, bool m32, bool m16, F f) {
     // VK bit 128, a compact long metric (u32 deltas, values restored in the loader): histogram-only grids over compact
     // timestamps (date_histogram{stats / extended_stats / avg}) and extended_stats under terms over compact columns
     if constexpr (MET > 0 && !ORD && HK == 1) {
@@ -1071,14 +1083,17 @@ static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, boo
     }
     // VK bit 64, packed integer metric cells: terms grids (no key, or an affine key over the compact timestamps) with
     // avg / stats over a dense long metric
+    // (+ bit 256: the 16-bit deltas, with 16-bit ordinals only)
     if constexpr (ORD && (HK == 0 || HK == 1) && (MET == 1 || MET == 2)) {
         if (pi && !mv_f64 && !dord) {
             if constexpr (HK == 1) {
                 if (t32 && !hv_f64) {
+                    if (c16 && m16) return f(std::integral_constant<int, 48 | 64 | 256>{});
                     if (c16) return f(std::integral_constant<int, 48 | 64>{});
                     return f(std::integral_constant<int, 32 | 64>{});
                 }
             } else {
+                if (c16 && m16) return f(std::integral_constant<int, 16 | 64 | 256>{});
                 if (c16) return f(std::integral_constant<int, 16 | 64>{});
                 return f(std::integral_constant<int, 64>{});
             }
@@ -1116,7 +1131,8 @@ static auto with_wg(bool wide, F f) {
 template <bool ORD, int HK, int MET>
 static void launch_t(const CollectParams& p, bool wide, uint32_t grid, size_t lds, hipStream_t st) {
     with_vk<ORD, HK, MET>(p.hv_f64 != 0, p.mv_f64 != 0, p.ord_src != nullptr, p.ord16 != nullptr, p.hv32 != nullptr,
-                          p.mv32 != nullptr && p.pk_shift != 0, p.mv32 != nullptr && p.pk_shift == 0, [&](auto vk) {
+                          p.mv32 != nullptr && p.pk_shift != 0, p.mv32 != nullptr && p.pk_shift == 0, p.mv16 != nullptr,
+                          [&](auto vk) {
         return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
             hipLaunchKernelGGL((collect_kernel<ORD, HK, MET, decltype(vk)::value, decltype(wg)::value>), dim3(grid),
                                dim3(decltype(wg)::value), lds, st, p);
@@ -1138,7 +1154,7 @@ static void launch_m(const CollectParams& p, int met, bool wide, uint32_t grid, 
 template <bool ORD, int HK, int MET>
 static int occ_t(size_t lds, int vkbits, bool wide) {
     return with_vk<ORD, HK, MET>((vkbits & 1) != 0, (vkbits & 2) != 0, (vkbits & 8) != 0, (vkbits & 16) != 0,
-                                 (vkbits & 32) != 0, (vkbits & 64) != 0, (vkbits & 128) != 0, [&](auto vk) {
+                                 (vkbits & 32) != 0, (vkbits & 64) != 0, (vkbits & 128) != 0, (vkbits & 256) != 0, [&](auto vk) {
         return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
             int n = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(

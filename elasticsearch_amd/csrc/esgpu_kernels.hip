@@ -15,6 +15,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cmath>
 #include <type_traits>
 #include <vector>
 
@@ -441,6 +442,97 @@ __global__ __launch_bounds__(kHllLdsWG) void hll_registers_lds_kernel(HllParams 
     }
 }
 
+// Floored stream (one pass over the segment instead of phase 0 + the LDS phases, when the request's values per register
+// are many): a register that will hold at least F is decided only by hashes with run length >= F, i.e. those whose F - 1
+// bits below the index bits are zero -- one 64-bit AND per hash.  Those (a fraction 2^-(F-1)) are logged in LDS and
+// flushed, partitioned by register range, into fs_buf for one gather (hll_p0_gather_kernel); the host picks F so that
+// a register ending below F is a ~1e-3 event per request, and the tail pass (hll_lc_kernel) finishes such registers
+// from the hashes below F.  No snapshot, no phase structure: the pass streams the column at the HBM rate.
+constexpr uint32_t kHllFsWG = 1024;
+constexpr uint32_t kHllFsIter = kHllFsWG * 4;
+constexpr uint32_t kHllFsLog = 16384;  // LDS log entries; flushed once it is half full (checked every ~kHllFsLog / 4 entries)
+constexpr uint32_t hll_fs_lds_bytes() { return kHllFsLog * 4u + 3u * 256u * 4u + 16u; }
+
+// one workgroup's log out, partitioned by register range (as the LDS phase kernel's end does); the callers barrier
+// before (the log is complete) and this barriers before returning (the log may be reused)
+__device__ __forceinline__ void hll_fs_flush(const HllParams& P, uint32_t* rlog, uint32_t* lcnt, uint32_t* lcur,
+                                             uint32_t* lbase, uint32_t* nlog) {
+    const uint32_t m = 1u << P.p;
+    const uint32_t n = min(*nlog, kHllFsLog);
+    const uint32_t R = hll_p0_ranges(m);
+    const uint32_t rshift = (uint32_t)P.p - (31u - (uint32_t)__builtin_clz(R));
+    for (uint32_t i = threadIdx.x; i < R; i += kHllFsWG) { lcnt[i] = 0; lcur[i] = 0; }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += kHllFsWG) atomicAdd(&lcnt[(rlog[i] & 0xFFFFFFu) >> rshift], 1u);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < R; i += kHllFsWG) lbase[i] = lcnt[i] ? atomicAdd(&P.p0_cnt[i], lcnt[i]) : 0u;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += kHllFsWG) {
+        const uint32_t e = rlog[i], idx = e & 0xFFFFFFu, r = idx >> rshift;
+        const uint32_t slot = lbase[r] + atomicAdd(&lcur[r], 1u);
+        if (slot < P.fs_cap) P.fs_buf[(size_t)r * P.fs_cap + slot] = e;
+        else atomicMax(&P.regs[idx], e >> 24);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *nlog = 0;
+    __syncthreads();
+}
+
+template <int KIND>
+__global__ __launch_bounds__(kHllFsWG) void hll_fs_kernel(HllParams P, uint32_t per_wg, uint32_t check_iters) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t fs_lds[];
+    uint32_t* rlog = fs_lds;                // [kHllFsLog] (rl << 24 | idx)
+    uint32_t* lcnt = rlog + kHllFsLog;      // [256]
+    uint32_t* lcur = lcnt + 256;            // [256]
+    uint32_t* lbase = lcur + 256;           // [256]
+    uint32_t* nlog = lbase + 256;           // [1]
+    if (threadIdx.x == 0) *nlog = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *P.unres = 0;  // counted by the gather that follows this launch
+    const uint32_t G = P.fs_f - 1;          // kept: run length > G <=> the G bits below the index bits are zero
+    const uint64_t zmask = G == 0 ? 0ull : (((1ull << G) - 1ull) << (64 - P.p - G));
+    const uint32_t w0 = blockIdx.x * per_wg;
+    const uint32_t w1 = min(P.n_docs, w0 + per_wg);
+    __syncthreads();
+    if (w0 >= w1) return;  // workgroup-uniform
+    const uint32_t t4 = threadIdx.x * 4;
+    const uint32_t last4 = (w1 - 1) & ~3u;  // unconditional loads (see hll_registers_lds_kernel)
+    auto load = [&](uint32_t i0, uint64_t raw[4]) { load_i64x4((const int64_t*)P.col, min(i0, last4), (int64_t*)raw); };
+    auto hash4 = [&](uint32_t i0, const uint64_t raw[4]) {
+        if (i0 >= w1) return;
+        const uint32_t lim = w1 - i0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t h = hll_fast_hash<KIND>(P, raw[j]);
+            if ((uint32_t)j < lim && (h & zmask) == 0) {
+                const uint32_t e = (hll_run_len(h, P.p) << 24) | hll_index(h, P.p);
+                const uint32_t k = atomicAdd(nlog, 1u);
+                if (k < kHllFsLog) rlog[k] = e;
+                else atomicMax(&P.regs[e & 0xFFFFFFu], e >> 24);  // never expected: flushed at half full
+            }
+        }
+    };
+    uint64_t a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+    load(w0 + t4, a);
+    __builtin_amdgcn_sched_barrier(0);
+    load(w0 + kHllFsIter + t4, b);
+    uint32_t it = 0;
+    for (uint32_t base = w0; base < w1; base += 2 * kHllFsIter) {
+        hash4(base + t4, a);
+        load(base + 2 * kHllFsIter + t4, a);
+        hash4(base + kHllFsIter + t4, b);
+        load(base + 3 * kHllFsIter + t4, b);
+        if (++it == check_iters) {  // workgroup-uniform: every thread runs the same iterations
+            it = 0;
+            __syncthreads();
+            const uint32_t n = *nlog;
+            __syncthreads();
+            if (n > kHllFsLog / 2) hll_fs_flush(P, rlog, lcnt, lcur, lbase, nlog);
+        }
+    }
+    __syncthreads();
+    hll_fs_flush(P, rlog, lcnt, lcur, lbase, nlog);
+}
+
 // the refresh (or the phase-0 gather) counts the non-zero registers as it reads them: each block adds its count to
 // nz_part[0]; the last block to finish raises *nonzero to the total and re-arms the pair.  Registers only grow, so
 // the count is a lower bound on the registers at the end of the segment, which is all the LINEAR_COUNTING decision
@@ -536,8 +628,9 @@ __global__ __launch_bounds__(1024) void hll_p0_gather_kernel(HllParams P, int co
     const uint32_t b = blockIdx.x, r0 = b * per;
     for (uint32_t i = threadIdx.x; i < per; i += 1024) reg[i] = P.regs[r0 + i];
     __syncthreads();
-    const uint32_t n = min(P.p0_cnt[b], P.p0_cap);
-    const uint32_t* src = P.p0_buf + (size_t)b * P.p0_cap;
+    const uint32_t cap = P.fs_f ? P.fs_cap : P.p0_cap;
+    const uint32_t n = min(P.p0_cnt[b], cap);
+    const uint32_t* src = (P.fs_f ? P.fs_buf : P.p0_buf) + (size_t)b * cap;
     for (uint32_t i = threadIdx.x; i < n; i += 1024) {
         const uint32_t e = src[i];
         atomicMax(&reg[(e & 0xFFFFFFu) - r0], e >> 24);
@@ -556,6 +649,12 @@ __global__ __launch_bounds__(1024) void hll_p0_gather_kernel(HllParams P, int co
         if ((lane & 1) == 0) P.snap[(r0 + gl * kHllGroup + lane) / 2] = (unsigned char)(d | (hi << 4));
     }
     if (threadIdx.x == 0) atomicExch(&P.p0_cnt[b], 0u);
+    if (P.fs_f) {  // floored stream: registers below the floor are finished by the tail pass
+        uint32_t u = 0;
+        for (uint32_t i = threadIdx.x; i < per; i += 1024) u += reg[i] < P.fs_f;
+        u = wave_sum_u32(u);
+        if ((threadIdx.x & 63) == 0 && u) atomicAdd(P.unres, u);
+    }
     if (!count) return;  // only the segment's last gather counts (the LC decision reads the final registers)
     uint32_t nz = 0;
     for (uint32_t i = threadIdx.x; i < per; i += 1024) nz += reg[i] != 0;
@@ -622,14 +721,30 @@ __global__ __launch_bounds__(1024) void hll_nonzero_kernel(const unsigned int* r
 // pass 2 (only while nonzero <= threshold): the exact LINEAR_COUNTING set of encodeHash values.  Open addressing,
 // probes bounded by threshold+1 (a longer run proves > threshold distinct values), stops once the count passes
 // the threshold.  Final mode = LC iff count <= threshold, exactly as Hashset.add/upgradeToHll decide.
+// With the floored stream the same launch is its tail pass: while the gather left registers below the floor F
+// (*unres, a ~1e-3 event), every hash with run length < F raises its register if it is still below -- registers at or
+// above F are exact already and are only read.
 __global__ __launch_bounds__(256) void hll_lc_kernel(HllParams P) {
-    if (*P.nonzero > P.lc_threshold) return;  // already proven HYPERLOGLOG
+    const bool fix = P.fs_f && *P.unres != 0;
+    bool lc = *P.nonzero <= P.lc_threshold;  // else already proven HYPERLOGLOG
+    if (!lc && !fix) return;
     const uint32_t gsz = gridDim.x * blockDim.x;
     for (uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < P.n_docs; i0 += gsz * 4) {
-        if (__hip_atomic_load(P.lc_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > P.lc_threshold) return;
+        if (lc && __hip_atomic_load(P.lc_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > P.lc_threshold) {
+            if (!fix) return;
+            lc = false;
+        }
         uint64_t raw[4], hv[4];
         hll_load_raw(P, i0, raw);
         const uint32_t ok = hll_hash_raw(P, i0, raw, hv);
+        if (fix) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t rl = hll_run_len(hv[j], P.p), idx = hll_index(hv[j], P.p);
+                if (((ok >> j) & 1) && rl < P.fs_f && P.regs[idx] < rl) atomicMax(&P.regs[idx], rl);
+            }
+        }
+        if (!lc) continue;
         uint32_t added = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -655,6 +770,22 @@ __global__ __launch_bounds__(256) void hll_lc_kernel(HllParams P) {
         }
         if (added) atomicAdd(P.lc_count, added);
     }
+}
+
+uint32_t hll_fs_floor(uint64_t total, int p, uint32_t min_f) {
+    const double m = (double)(1u << p);
+    const double lam = (double)total / m, need = std::log(m) + 6.9;  // m * exp(-lam * 2^-(F-1)) <= 1e-3
+    if (lam < need * 2.0) return 0;
+    const uint32_t f = 1u + (uint32_t)std::floor(std::log2(lam / need));
+    const uint32_t fmax = 64u - (uint32_t)p;  // run lengths top out at 64 - p + 1
+    const uint32_t F = std::min(f, fmax);
+    return F >= min_f ? F : 0u;
+}
+uint32_t hll_fs_cap(uint64_t n, int p, uint32_t f) {
+    const uint32_t R = hll_p0_ranges(1u << p);
+    const double e = (double)n / std::ldexp(1.0, (int)f - 1) / R;  // mean entries per range
+    const double c = e + e / 8 + 8 * std::sqrt(e) + 256;
+    return (uint32_t)std::min(c, 4.0e9) & ~3u;
 }
 
 void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
@@ -698,6 +829,39 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
         else
             hipLaunchKernelGGL(hll_floor_kernel, dim3(floor_grid), dim3(1024), 0, st, (const unsigned int*)p.regs, m, p.floor);
     };
+    // LC / tail pass: mostly a launch whose blocks see *nonzero above the threshold and return at once; 2048 blocks
+    // loop over the docs when it does run
+    auto tail = [&](const HllParams& t) {
+        uint32_t grid = (n + 1023) / 1024;
+        if (grid > 2048) grid = 2048;
+        if (grid == 0) grid = 1;
+        hipLaunchKernelGGL(hll_lc_kernel, dim3(grid), dim3(256), 0, st, t);
+    };
+    if (p.fs_f && lds && p.p0_cnt && p.p >= 12 && n > 0) {
+        // floored stream: one resident wave of workgroups, contiguous ranges; the log is checked every ~kHllFsLog / 4
+        // expected entries (2^(F-1) docs per entry)
+        static int per_cu = 0;
+        if (!per_cu) {
+            int b = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, hll_fs_kernel<HLL_I64>, kHllFsWG, hll_fs_lds_bytes()) != hipSuccess || b < 1)
+                b = 1;
+            per_cu = b;
+        }
+        uint32_t wgs = std::max(1u, std::min(cus * (uint32_t)per_cu, n / (kHllFsIter * 2)));
+        const uint32_t per = ((n + wgs - 1) / wgs + 3) & ~3u;
+        wgs = (n + per - 1) / per;
+        const uint64_t docs_per_check = ((uint64_t)kHllFsLog / 4) << (p.fs_f - 1);
+        const uint32_t check = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, docs_per_check / (2 * kHllFsIter)));
+        if (p.kind == HLL_I64)
+            hipLaunchKernelGGL(hll_fs_kernel<HLL_I64>, dim3(wgs), dim3(kHllFsWG), hll_fs_lds_bytes(), st, p, per, check);
+        else
+            hipLaunchKernelGGL(hll_fs_kernel<HLL_F64>, dim3(wgs), dim3(kHllFsWG), hll_fs_lds_bytes(), st, p, per, check);
+        hipLaunchKernelGGL(hll_p0_gather_kernel, dim3(hll_p0_ranges(m)), dim3(1024), 0, st, p, 1);
+        tail(p);
+        return;
+    }
+    HllParams q = p;  // the phases (fs_f = 0 for their gathers)
+    q.fs_f = 0;
     const bool warm = p.seen >= (uint64_t)m * cut0;  // the registers already passed the first cut
     if (warm) refresh();
 #ifndef ESGPU_HLL_P0
@@ -713,9 +877,9 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
         if (span == 0) continue;
         if (ph == 0 && p0) {
             const dim3 g1((span + kP0WG * kP0Docs - 1) / (kP0WG * kP0Docs));
-            if (p.kind == HLL_I64) hipLaunchKernelGGL(hll_p0_scatter_kernel<HLL_I64>, g1, dim3(kP0WG), 0, st, p, span);
-            else hipLaunchKernelGGL(hll_p0_scatter_kernel<HLL_F64>, g1, dim3(kP0WG), 0, st, p, span);
-            hipLaunchKernelGGL(hll_p0_gather_kernel, dim3(hll_p0_ranges(m)), dim3(1024), 0, st, p, ph + 2 >= cuts.size() ? 1 : 0);
+            if (p.kind == HLL_I64) hipLaunchKernelGGL(hll_p0_scatter_kernel<HLL_I64>, g1, dim3(kP0WG), 0, st, q, span);
+            else hipLaunchKernelGGL(hll_p0_scatter_kernel<HLL_F64>, g1, dim3(kP0WG), 0, st, q, span);
+            hipLaunchKernelGGL(hll_p0_gather_kernel, dim3(hll_p0_ranges(m)), dim3(1024), 0, st, q, ph + 2 >= cuts.size() ? 1 : 0);
             counted = ph + 2 >= cuts.size();
             continue;  // the gather left the registers' group floors and snapshot behind: no refresh
         }
@@ -733,19 +897,19 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
             const uint32_t lper = ((span + lw - 1) / lw + 3) & ~3u;
             lw = (span + lper - 1) / lper;
             if (p.kind == HLL_I64)
-                hipLaunchKernelGGL(hll_registers_lds_kernel<HLL_I64>, dim3(lw), dim3(kHllLdsWG), hll_lds_bytes(m, logr), st, p, cuts[ph], cuts[ph + 1], lper, fl);
+                hipLaunchKernelGGL(hll_registers_lds_kernel<HLL_I64>, dim3(lw), dim3(kHllLdsWG), hll_lds_bytes(m, logr), st, q, cuts[ph], cuts[ph + 1], lper, fl);
             else
-                hipLaunchKernelGGL(hll_registers_lds_kernel<HLL_F64>, dim3(lw), dim3(kHllLdsWG), hll_lds_bytes(m, logr), st, p, cuts[ph], cuts[ph + 1], lper, fl);
+                hipLaunchKernelGGL(hll_registers_lds_kernel<HLL_F64>, dim3(lw), dim3(kHllLdsWG), hll_lds_bytes(m, logr), st, q, cuts[ph], cuts[ph + 1], lper, fl);
         } else if (fast && p.kind == HLL_I64)
-            hipLaunchKernelGGL(hll_registers_fast_kernel<HLL_I64>, dim3(wgs), dim3(kHllWG), 0, st, p, cuts[ph], cuts[ph + 1], per, fl);
+            hipLaunchKernelGGL(hll_registers_fast_kernel<HLL_I64>, dim3(wgs), dim3(kHllWG), 0, st, q, cuts[ph], cuts[ph + 1], per, fl);
         else if (fast && p.kind == HLL_F64)
-            hipLaunchKernelGGL(hll_registers_fast_kernel<HLL_F64>, dim3(wgs), dim3(kHllWG), 0, st, p, cuts[ph], cuts[ph + 1], per, fl);
+            hipLaunchKernelGGL(hll_registers_fast_kernel<HLL_F64>, dim3(wgs), dim3(kHllWG), 0, st, q, cuts[ph], cuts[ph + 1], per, fl);
         else if (fast)
-            hipLaunchKernelGGL(hll_registers_fast_kernel<HLL_ORD>, dim3(wgs), dim3(kHllWG), 0, st, p, cuts[ph], cuts[ph + 1], per, fl);
+            hipLaunchKernelGGL(hll_registers_fast_kernel<HLL_ORD>, dim3(wgs), dim3(kHllWG), 0, st, q, cuts[ph], cuts[ph + 1], per, fl);
         else
-            hipLaunchKernelGGL(hll_registers_kernel, dim3(wgs), dim3(kHllWG), 0, st, p, cuts[ph], cuts[ph + 1], per, fl);
+            hipLaunchKernelGGL(hll_registers_kernel, dim3(wgs), dim3(kHllWG), 0, st, q, cuts[ph], cuts[ph + 1], per, fl);
         if (lds && floored && logr) {  // the phase's logged raises applied; floors, snapshot and count refreshed
-            hipLaunchKernelGGL(hll_p0_gather_kernel, dim3(hll_p0_ranges(m)), dim3(1024), 0, st, p, ph + 2 >= cuts.size() ? 1 : 0);
+            hipLaunchKernelGGL(hll_p0_gather_kernel, dim3(hll_p0_ranges(m)), dim3(1024), 0, st, q, ph + 2 >= cuts.size() ? 1 : 0);
             counted = ph + 2 >= cuts.size();
             continue;
         }
@@ -756,12 +920,7 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
         (void)hipMemsetAsync(p.nonzero, 0, 4, st);  // recount over the registers (they accumulate across segments)
         hipLaunchKernelGGL(hll_nonzero_kernel, dim3(floor_grid), dim3(1024), 0, st, (const unsigned int*)p.regs, m, p.nonzero);
     }
-    // the LC pass: mostly a launch whose blocks see *nonzero above the threshold and return at once; 2048 blocks
-    // loop over the docs when it does run
-    uint32_t grid = (n + 1023) / 1024;
-    if (grid > 2048) grid = 2048;
-    if (grid == 0) grid = 1;
-    hipLaunchKernelGGL(hll_lc_kernel, dim3(grid), dim3(256), 0, st, p);
+    tail(q);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -931,6 +1090,14 @@ __global__ void delta32_kernel(const int64_t* v, uint32_t n, int64_t base, uint3
 }
 void launch_delta32(const int64_t* v, uint32_t n, int64_t base, uint32_t* out, hipStream_t st) {
     if (n) hipLaunchKernelGGL(delta32_kernel, dim3(std::min<uint32_t>(8192, (n + 255) / 256)), dim3(256), 0, st, v, n, base, out);
+}
+
+__global__ void delta16_kernel(const int64_t* v, uint32_t n, int64_t base, uint16_t* out) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        out[i] = (uint16_t)((uint64_t)v[i] - (uint64_t)base);
+}
+void launch_delta16(const int64_t* v, uint32_t n, int64_t base, uint16_t* out, hipStream_t st) {
+    if (n) hipLaunchKernelGGL(delta16_kernel, dim3(std::min<uint32_t>(8192, (n + 255) / 256)), dim3(256), 0, st, v, n, base, out);
 }
 
 __global__ void pack_u8_kernel(const unsigned int* src, uint32_t n, uint8_t* dst) {
@@ -1673,8 +1840,8 @@ __device__ bool pred_doc(const PredDev& q, uint32_t d) {
         } else if (q.kind == PRED_F64_RANGE) {
             const double v = ((const double*)q.col)[i];
             m = (q.lo_incl ? v >= q.dlo : v > q.dlo) && (q.hi_incl ? v <= q.dhi : v < q.dhi);
-        } else if (q.kind == PRED_D32_RANGE) {
-            const int64_t v = q.base + (int64_t)((const uint32_t*)q.col)[i];
+        } else if (q.kind == PRED_D32_RANGE || q.kind == PRED_D16_RANGE) {
+            const int64_t v = q.base + (q.kind == PRED_D16_RANGE ? (int64_t)((const uint16_t*)q.col)[i] : (int64_t)((const uint32_t*)q.col)[i]);
             m = v >= q.lo && v <= q.hi;
         } else {
             const int64_t v = ((const int64_t*)q.col)[i];

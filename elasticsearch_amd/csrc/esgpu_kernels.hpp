@@ -35,8 +35,10 @@ constexpr uint32_t kGroupBlocks = ESGPU_GROUP_BLOCKS;
 #define ESGPU_DYN_CLAIM 0
 #endif
 constexpr int kMaxPreds = 4;  // clauses a collect kernel evaluates itself (more: folded into a doc bitset first)
-// PRED_D32_RANGE: an I64 range over the column's compact copy (u32 deltas over `base`)
-enum PredKind : int32_t { PRED_ORD_EQ = 0, PRED_I64_RANGE = 1, PRED_F64_RANGE = 2, PRED_ORD_RANGE = 3, PRED_D32_RANGE = 4 };
+// PRED_D32_RANGE / PRED_D16_RANGE: an I64 range over the column's compact copy (u32 / u16 deltas over `base`)
+enum PredKind : int32_t {
+    PRED_ORD_EQ = 0, PRED_I64_RANGE = 1, PRED_F64_RANGE = 2, PRED_ORD_RANGE = 3, PRED_D32_RANGE = 4, PRED_D16_RANGE = 5
+};
 
 struct PredDev {
     const void* col;
@@ -46,7 +48,7 @@ struct PredDev {
     int32_t lo_incl, hi_incl, pad;
     int64_t lo, hi;    // ORD_EQ: lo = ordinal; I64_RANGE / ORD_RANGE: inclusive [lo, hi]
     double dlo, dhi;   // F64_RANGE with include flags
-    int64_t base;      // D32_RANGE: value = base + delta
+    int64_t base;      // D32_RANGE / D16_RANGE: value = base + delta
 };
 
 // separate outer-level doc counts: TERMS / HIST = counted per doc (the inner column has missing values);
@@ -98,6 +100,7 @@ struct CollectParams {
     // delta pair -- one LDS atomic per doc for count + sum instead of two.  The host picks pk_shift so that neither field
     // can overflow within one workgroup's range of docs.
     const uint32_t* mv32;
+    const uint16_t* mv16;  // the same deltas in 16 bits when the values span < 2^16 (loader VK bit 256)
     int64_t mv_base;
     uint32_t pk_shift;
     uint32_t hot_t;      // the segment's most frequent ordinal (a sampled hint; kMissingOrd: none) -- ESGPU_PI_HOT builds
@@ -165,7 +168,21 @@ struct HllParams {
     uint32_t cut0;              // phase 0 spans the request's first cut0 * 2^p values (ESGPU_HLL_CUT0)
     int32_t log_raises;         // LDS phases log their register raises and leave them, partitioned by range, in p0_buf
                                 // for the gather kernel (instead of one global atomicMax per raise); needs p0_cnt
+    // floored stream (hll_fs_*, one pass instead of the phases): only hashes with run length >= fs_f are kept, logged
+    // by register range into fs_buf (fs_cap per range) and maxed by one gather; a register still below fs_f afterwards
+    // ("unresolved", counted into *unres by the gather) is finished by the tail pass over this segment's hashes with
+    // run length < fs_f.  fs_f = 0: the phases.
+    uint32_t fs_f;
+    uint32_t fs_cap;
+    unsigned int* fs_buf;
+    unsigned int* unres;
 };
+// floored stream: the floor F (kept hashes have run length >= F, a fraction 2^-(F-1) of the stream) for a request whose
+// registers will have seen `total` values when this segment is done: the largest F for which the expected number of
+// registers ending below F, m * exp(-(total / m) * 2^-(F-1)), stays under 1e-3 (then a tail pass finishes them).
+// 0 = too few values per register for a floor worth a pass (the phases instead).
+uint32_t hll_fs_floor(uint64_t total, int p, uint32_t min_f);
+uint32_t hll_fs_cap(uint64_t n, int p, uint32_t f);  // entries per register range for n values at floor f
 #ifndef ESGPU_HLL_CUT0  // HLL phase 0 spans the request's first ESGPU_HLL_CUT0 * 2^p values
 #define ESGPU_HLL_CUT0 4  // measured: 4 beats 16 by 3-4 % (phase 0 reads and raises registers for every hash)
 #endif
@@ -276,6 +293,7 @@ void launch_minmax_i64(const int64_t* v, uint64_t n, int64_t* out, bool f64, hip
 void launch_widen_u32(const unsigned int* src, size_t n, unsigned long long* dst, hipStream_t st);
 void launch_narrow_u64(const unsigned long long* src, size_t n, unsigned int* dst, hipStream_t st);
 void launch_pack_ord16(const uint32_t* src, uint32_t n, uint16_t* out, hipStream_t st);
+void launch_delta16(const int64_t* v, uint32_t n, int64_t base, uint16_t* out, hipStream_t st);
 void launch_delta32(const int64_t* v, uint32_t n, int64_t base, uint32_t* out, hipStream_t st);
 // breadth-first replay, compacted: one pass over a retained segment appends, for every doc whose outer bucket survived
 // (slot_map) and that has an inner term, its replay-grid ordinal (winner w % wb) * stride + inner into the region of

@@ -74,6 +74,11 @@ void tune_host_heap() {
 extern "C" int esgpu_ctx_set_option(esgpu_ctx* c, int32_t option, int64_t value) {
     return guarded([&] {
         require(c, ESGPU_ERR_INVALID, "null context");
+        if (option == ESGPU_OPT_HLL_FLOOR) {
+            require(value >= 0 && value <= 8, ESGPU_ERR_INVALID, "hll floor option must be 0..8");
+            c->opt_hll_fs = (int)value;
+            return;
+        }
         require(value == 0 || value == 1, ESGPU_ERR_INVALID, "option value must be 0 or 1");
         if (option == ESGPU_OPT_COMPACT_COLUMNS) c->opt_compact = (int)value;
         else if (option == ESGPU_OPT_PACKED_METRIC) c->opt_pi = (int)value;
@@ -86,6 +91,7 @@ extern "C" int esgpu_ctx_get_option(const esgpu_ctx* c, int32_t option, int64_t*
         require(c && value, ESGPU_ERR_INVALID, "null argument");
         if (option == ESGPU_OPT_COMPACT_COLUMNS) *value = c->opt_compact;
         else if (option == ESGPU_OPT_PACKED_METRIC) *value = c->opt_pi;
+        else if (option == ESGPU_OPT_HLL_FLOOR) *value = c->opt_hll_fs;
         else throw EsError(ESGPU_ERR_INVALID, "unknown context option");
     });
 }
@@ -107,6 +113,7 @@ extern "C" int esgpu_ctx_create(int device, uint64_t budget, esgpu_ctx** out) {
         auto env_on = [](const char* name) { const char* e = std::getenv(name); return !(e && *e == '0'); };
         c->opt_compact = env_on("ESGPU_COMPACT") ? 1 : 0;
         c->opt_pi = env_on("ESGPU_PI") ? 1 : 0;
+        c->opt_hll_fs = env_on("ESGPU_HLL_FS") ? 1 : 0;
         HIPX(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         *out = c.release();
     });
@@ -301,9 +308,9 @@ struct DevColumn {
     // compact copies the collect kernel's loader reads instead (ensure_ord16 / ensure_d32, built on first use and cached
     // with the column): ords() in 16 bits (0xFFFF missing) while the dictionary has fewer than 65,535 terms -- keyed by
     // the ords() buffer it was made from -- and a long column's values as 32-bit deltas over vmin while vmax - vmin < 2^32
-    DevBuf ord16, d32;
+    DevBuf ord16, d32, d16;  // d16: the same deltas in 16 bits while vmax - vmin < 2^16 (ensure_d16)
     const void* ord16_src = nullptr;
-    bool d32_done = false;
+    bool d32_done = false, d16_done = false;
     // the most frequent ordinal of ords() in a sample (a hint for the packed cells' register run; any value is correct)
     uint32_t hot_ord = 0xFFFFFFFFu;
     const void* hot_src = nullptr;
@@ -939,6 +946,7 @@ struct Pipeline {
     // cardinality state
     int p = 14;
     DevBuf regs, lc_set, lc_count;
+    DevBuf fs_buf;                   // floored-stream HLL: entries by register range (grown on demand)
     DevBuf lc_first;                 // [lc_mask + 1] u64: insertion order of each LC set entry (HllParams.lc_first)
     uint32_t lc_mask = 0, lc_threshold = 0;
     uint64_t hll_seen = 0;           // values hashed into the registers by earlier segments of this request
@@ -1594,6 +1602,7 @@ static bool pi_cells(const esgpu_ctx* c);
 static uint32_t pi_copies();
 static const uint16_t* ensure_ord16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
 static const uint32_t* ensure_d32(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
+static const uint16_t* ensure_d16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
 static uint32_t sampled_hot_ord(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s);
 
 // The pipeline's clauses as device predicates: up to kMaxPreds of them are evaluated inside the collect kernels; with
@@ -1671,8 +1680,16 @@ static void set_preds(esgpu_plan* p, const Pipeline& pl, const esgpu_segment* s,
                 q.lo = lo;
                 q.hi = hi;
             }
-            // single-valued: the compact copy of the column (u32 deltas) when its values span < 2^32
+            // single-valued: the compact copy of the column (u16 / u32 deltas) when its values span < 2^16 / 2^32
             if (compact_cols(p->ctx) && !col->multi && col->vmin <= col->vmax &&
+                (uint64_t)col->vmax - (uint64_t)col->vmin < (1ull << 16)) {
+                if (const uint16_t* d = ensure_d16(p->ctx, col, s, p->stream)) {
+                    q.col = d;
+                    q.kind = PRED_D16_RANGE;
+                    q.base = col->vmin;
+                }
+            }
+            if (q.kind != PRED_D16_RANGE && compact_cols(p->ctx) && !col->multi && col->vmin <= col->vmax &&
                 (uint64_t)col->vmax - (uint64_t)col->vmin < (1ull << 32)) {
                 if (const uint32_t* d = ensure_d32(p->ctx, col, s, p->stream)) {
                     q.col = d;
@@ -1680,7 +1697,7 @@ static void set_preds(esgpu_plan* p, const Pipeline& pl, const esgpu_segment* s,
                     q.base = col->vmin;
                 }
             }
-            *bytes_per_doc += q.kind == PRED_D32_RANGE ? 4 : 8;
+            *bytes_per_doc += q.kind == PRED_D16_RANGE ? 2 : q.kind == PRED_D32_RANGE ? 4 : 8;
         }
         all.push_back(q);
     }
@@ -2806,6 +2823,9 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
             P.mv_base = mc->vmin;
             P.hot_t = sampled_hot_ord(p->ctx, oc, s);
             pi = true;
+            // values spanning < 2^16 (a latency in ms, a status code): the 16-bit deltas, 2 B per doc (instantiated with
+            // 16-bit ordinals)
+            if (P.ord16 && (uint64_t)mc->vmax - (uint64_t)mc->vmin < (1ull << 16)) P.mv16 = ensure_d16(p->ctx, mc, s, p->stream);
         }
     }
     auto pi_fits = [&](uint32_t bpw) {  // docs of one workgroup range: count field and sum-of-deltas field both fit
@@ -2924,8 +2944,8 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     }
     const int hk = L_HIST ? (P.hord ? 3 : P.kstart ? 2 : 1) : 0;
     const int vk = (P.hv_f64 ? 1 : 0) | (P.mv_f64 ? 2 : 0) | (P.ord_src ? 8 : 0) | (P.ord16 ? 16 : 0) | (P.hv32 ? 32 : 0) |
-                   (pi ? 64 : 0) | (m32 ? 128 : 0);
-    const uint64_t occ_key = ((uint64_t)lds << 17) | ((uint64_t)wide << 16) | ((uint64_t)vk << 8) | ((uint64_t)L_met << 4) |
+                   (pi ? 64 : 0) | (m32 ? 128 : 0) | (P.mv16 ? 256 : 0);
+    const uint64_t occ_key = ((uint64_t)lds << 18) | ((uint64_t)wide << 17) | ((uint64_t)vk << 8) | ((uint64_t)L_met << 4) |
                              ((uint64_t)hk << 1) | (L_ORD ? 1 : 0);
     if (pl.occ_key != occ_key) {
         pl.occ = std::max(1, collect_occupancy(L_ORD, hk, L_met, lds, vk, wide));
@@ -2950,11 +2970,12 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     if (pi && P.lds_mode && !pi_fits(P.blocks_per_wg)) {  // a packed field could overflow: the f64 cells instead
         pi = false;
         P.mv32 = nullptr;
+        P.mv16 = nullptr;
         P.pk_shift = 0;
         P.ncopies = 1;
         goto relaunch;
     }
-    if (pi || m32) bytes_per_doc -= 4;
+    if (pi || m32) bytes_per_doc -= P.mv16 ? 6 : 4;
     uint32_t grid = (P.n_blocks + P.blocks_per_wg - 1) / P.blocks_per_wg;
     // dynamic chunk claiming: one resident wave of workgroups, each flushing its LDS cells once, taking chunks of
     // kGroup blocks until none are left (ESGPU_DYN=0/1 overrides the build default for A/B runs)
@@ -3070,6 +3091,23 @@ static const uint32_t* ensure_d32(esgpu_ctx* c, const DevColumn* col, const esgp
     HIPX(hipGetLastError());
     HIPX(hipStreamSynchronize(st));
     return m->d32.as<uint32_t>();
+}
+
+static const uint16_t* ensure_d16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st) {
+    DevColumn* m = const_cast<DevColumn*>(col);
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (m->d16_done) return m->d16.as<uint16_t>();
+    m->d16_done = true;
+    try {
+        m->d16.alloc(c, (size_t)s->n_pad * 2);
+    } catch (const EsError&) {
+        m->d16.release();
+        return nullptr;
+    }
+    launch_delta16(col->values.as<int64_t>(), s->n_pad, col->vmin, m->d16.as<uint16_t>(), st);
+    HIPX(hipGetLastError());
+    HIPX(hipStreamSynchronize(st));
+    return m->d16.as<uint16_t>();
 }
 
 static void ensure_ord_hash(esgpu_ctx* c, const DevColumn* col, hipStream_t st) {
@@ -3190,6 +3228,26 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
         // (which run at the memory side at ~20 G/s); ESGPU_HLL_LOG=0 keeps the atomics (A/B runs)
         static const int log_raises = [] { const char* e = std::getenv("ESGPU_HLL_LOG"); return e && *e == '0' ? 0 : 1; }();
         H.log_raises = log_raises;
+        // the floored stream (one pass) when the request's values per register allow a floor F >= 4 (the
+        // pass keeps 1/8 of the hashes or fewer); ESGPU_HLL_FS_MINF overrides the minimum (A/B runs), the context
+        // option ESGPU_OPT_HLL_FLOOR turns it off or raises the floor (test leg for the tail pass)
+        static const uint32_t fs_minf = [] {
+            const char* e = std::getenv("ESGPU_HLL_FS_MINF");
+            return e && *e ? std::max(2u, (uint32_t)std::atoi(e)) : 4u;
+        }();
+        const int fs_mode = p->ctx->opt_hll_fs.load();
+        const bool dense = !H.accept && H.npred == 0 && !H.present && !col->multi && H.kind != HLL_ORD;
+        uint32_t F = fs_mode && dense ? hll_fs_floor(pl.hll_seen + H.n_docs, pl.p, fs_minf) : 0u;
+        if (F && fs_mode > 1) F = std::min<uint32_t>(F + (uint32_t)fs_mode - 1, 64u - (uint32_t)pl.p);
+        if (F) {
+            const uint32_t cap = hll_fs_cap(H.n_docs, pl.p, F);
+            const size_t need = (size_t)hll_p0_ranges(m) * cap * 4;
+            if (pl.fs_buf.bytes < need) pl.fs_buf.alloc(p->ctx, need);
+            H.fs_f = F;
+            H.fs_cap = cap;
+            H.fs_buf = pl.fs_buf.as<unsigned int>();
+            H.unres = pl.lc_count.as<unsigned int>() + 6;
+        }
     }
     H.lc_mask = pl.lc_mask;
     H.lc_threshold = pl.lc_threshold;

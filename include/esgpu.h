@@ -75,8 +75,12 @@ int esgpu_device_count(int* count);
  *                              (dictionaries under 65,535 terms) and u32 deltas of long columns spanning < 2^32 --
  *                              instead of the upload-width columns
  *   ESGPU_OPT_PACKED_METRIC:   avg / stats under terms over a dense long metric accumulate in packed integer LDS cells
- *                              (count and sum of deltas in one u64 word; needs compact columns) */
-enum { ESGPU_OPT_COMPACT_COLUMNS = 1, ESGPU_OPT_PACKED_METRIC = 2 };
+ *                              (count and sum of deltas in one u64 word; needs compact columns)
+ *   ESGPU_OPT_HLL_FLOOR:       cardinality register passes over a dense numeric column take the floored stream when
+ *                              the request's values per register allow it: 0 = the register phases
+ *                              instead, 1 = on (default), 2..8 = on with the floor raised by value - 1 (a test leg:
+ *                              registers left below the floor are finished by the tail pass) */
+enum { ESGPU_OPT_COMPACT_COLUMNS = 1, ESGPU_OPT_PACKED_METRIC = 2, ESGPU_OPT_HLL_FLOOR = 3 };
 int esgpu_ctx_set_option(esgpu_ctx* ctx, int32_t option, int64_t value);
 int esgpu_ctx_get_option(const esgpu_ctx* ctx, int32_t option, int64_t* value);
 

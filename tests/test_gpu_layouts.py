@@ -2,12 +2,13 @@
 
 The single-valued collect kernel reads, per segment, the narrowest layout the data allows:
   * upload width: u32 ordinals, i64 timestamps / filter values / metric (compact columns off);
-  * compact: u16 ordinals (dictionaries under 65,535 terms), u32 deltas of long columns spanning < 2^32;
-  * compact + packed integer metric cells: a dense long metric under terms read as its u32 deltas and accumulated as
-    count << shift | sum of deltas in one u64 LDS word.
+  * compact: u16 ordinals (dictionaries under 65,535 terms), u32 deltas of long columns spanning < 2^32 (u16 deltas
+    for filter columns spanning < 2^16);
+  * compact + packed integer metric cells: a dense long metric under terms read as its u32 deltas (u16 when its values
+    span < 2^16) and accumulated as count << shift | sum of deltas in one u64 LDS word.
 Real indices take each of them: timestamps over more than 2^32 ms (49.7 days) keep i64 keys, sparse or double metrics
 keep f64 cells.  The layout is a per-context option (Engine.set_option), so one session runs them all against the same
-oracle result; the algorithmic bytes the plan reports name the layout that ran (north star: 20 / 14 / 10 B per doc).
+oracle result; the algorithmic bytes the plan reports name the layout that ran (north star: 20 / 14 / 8 B per doc).
 """
 import numpy as np
 import pytest
@@ -76,7 +77,7 @@ def c5_100m():
     return n, want
 
 
-@pytest.mark.parametrize("name,bpd", [("upload", 20), ("compact", 14), ("packed", 10)])
+@pytest.mark.parametrize("name,bpd", [("upload", 20), ("compact", 14), ("packed", 8)])
 def test_north_star_100m_every_layout(engine, ns_100m, name, bpd):
     n, want = ns_100m
     with layout(engine, name):
@@ -88,7 +89,7 @@ def test_north_star_100m_every_layout(engine, ns_100m, name, bpd):
     assert_same(reduce([res]).to_dict(), want["reduced"], f"{name} reduced")
 
 
-@pytest.mark.parametrize("name,bpd", [("upload", 36), ("compact", 22), ("packed", 18)])
+@pytest.mark.parametrize("name,bpd", [("upload", 36), ("compact", 20), ("packed", 14)])
 def test_config5_100m_every_layout(engine, c5_100m, name, bpd):
     n, want = c5_100m
     with layout(engine, name):
@@ -134,7 +135,7 @@ def test_timestamps_over_2_32_ms(engine, name):
 @pytest.mark.parametrize("name", ["compact", "packed"])
 def test_packed_metric_edge_values(engine, name):
     """Packed cells decode count * base + sum of deltas: negative metrics, a base far from zero (sums beyond 2^53,
-    compared at the big-sum tolerance), deltas near 2^32, and two segments whose metric bases differ -- each decoded with
+    compared at the big-sum tolerance; values spanning < 2^16, read as u16 deltas), deltas near 2^32, and two segments whose metric bases differ -- each decoded with
     its own base; stats, avg and extended_stats (the latter never packed) side by side."""
     rng = np.random.default_rng(42)
     t0 = 1_441_065_600_000

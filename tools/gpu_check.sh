@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun session: GPU parity tests, kernel sweep, bench, rocprofv3 kernel-trace stats and PMC HBM-traffic passes.
 #   gpurun --timeout 1200 -- bash tools/gpu_check.sh <tag> [steps...]
-# steps: tests testsdyn testfile testfiles piab kbench bench jitter export shape125 configs dynab hllab cut0ab buildtrace profk125 prof profk pmc pmck variants (default: tests kbench bench prof pmc)
+# steps: tests testsdyn testfile testfiles piab fsab kbench bench jitter export shape125 configs dynab hllab cut0ab buildtrace profk125 prof profk pmc pmck variants (default: tests kbench bench prof pmc)
 # KBENCH_ONLY=name,name restricts the kbench sweeps (KBENCH_ARGS: extra kbench flags for variants, KBENCH_TAG: log suffix); variants = every build/variants/libesgpu_*.so via ESGPU_LIBRARY.  Every GPU step has its own time limit; the first failure ends it.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -55,6 +55,11 @@ for s in $STEPS; do
         hllab) # HLL register phases: raises logged for a gather (default) vs one global atomicMax per raise (ESGPU_HLL_LOG=0)
               for d in 1 0; do for docs in 125000000 1000000000; do
                   ESGPU_HLL_LOG=$d run "kbench_hll${d}_$docs" 300 python3 "$R/tools/kbench.py" --docs $docs --reps 5 \
+                      --only config4_card || exit 1
+              done; done ;;
+        fsab) # HLL floored stream (one pass + gather + tail) vs the register phases (ESGPU_HLL_FS=0)
+              for f in 1 0; do for docs in 125000000 1000000000; do
+                  ESGPU_HLL_FS=$f run "kbench_fs${f}_$docs" 300 python3 "$R/tools/kbench.py" --docs $docs --reps 5 \
                       --only config4_card || exit 1
               done; done ;;
         cut0ab) # HLL phase 0 length (ESGPU_HLL_CUT0 x 2^p values through the partitioned phase 0)
