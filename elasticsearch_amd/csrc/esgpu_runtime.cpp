@@ -311,6 +311,10 @@ struct DevColumn {
     DevBuf ord16, d32, d16;  // d16: the same deltas in 16 bits while vmax - vmin < 2^16 (ensure_d16)
     const void* ord16_src = nullptr;
     bool d32_done = false, d16_done = false;
+    // distinct values of the column, estimated from the HLL registers of an earlier request that collected this segment
+    // alone and unfiltered (-1: none yet) -- picks the floored stream's floor (collect_hll); any value is correct
+    // (shared: a plan that collected the segment keeps it alive for its build, whatever happens to the segment meanwhile)
+    std::shared_ptr<std::atomic<double>> hll_distinct = std::make_shared<std::atomic<double>>(-1.0);
     // the most frequent ordinal of ords() in a sample (a hint for the packed cells' register run; any value is correct)
     uint32_t hot_ord = 0xFFFFFFFFu;
     const void* hot_src = nullptr;
@@ -950,6 +954,11 @@ struct Pipeline {
     DevBuf lc_first;                 // [lc_mask + 1] u64: insertion order of each LC set entry (HllParams.lc_first)
     uint32_t lc_mask = 0, lc_threshold = 0;
     uint64_t hll_seen = 0;           // values hashed into the registers by earlier segments of this request
+    // the request's first segment, when it was collected dense (its registers alone then estimate its distinct values at
+    // build), the segments collected, and the largest distinct estimate among them
+    std::shared_ptr<std::atomic<double>> hll_d1;
+    int hll_nseg = 0;
+    double hll_dmax = 0.0;
     bool lc_dirty = true;            // lc_set / lc_first may hold entries (cleared at reset only then)
     // post_collection products
     std::vector<uint8_t> h_regs;
@@ -1598,6 +1607,7 @@ static bool applies(const esgpu_plan* p, const Pipeline& pl, size_t k) {
 static bool compact_cols(const esgpu_ctx* c);
 static bool dyn_claim_on();
 static bool replay_compaction();
+static bool d16_on();
 static bool pi_cells(const esgpu_ctx* c);
 static uint32_t pi_copies();
 static const uint16_t* ensure_ord16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
@@ -1681,7 +1691,7 @@ static void set_preds(esgpu_plan* p, const Pipeline& pl, const esgpu_segment* s,
                 q.hi = hi;
             }
             // single-valued: the compact copy of the column (u16 / u32 deltas) when its values span < 2^16 / 2^32
-            if (compact_cols(p->ctx) && !col->multi && col->vmin <= col->vmax &&
+            if (compact_cols(p->ctx) && d16_on() && !col->multi && col->vmin <= col->vmax &&
                 (uint64_t)col->vmax - (uint64_t)col->vmin < (1ull << 16)) {
                 if (const uint16_t* d = ensure_d16(p->ctx, col, s, p->stream)) {
                     q.col = d;
@@ -2825,7 +2835,8 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
             pi = true;
             // values spanning < 2^16 (a latency in ms, a status code): the 16-bit deltas, 2 B per doc (instantiated with
             // 16-bit ordinals)
-            if (P.ord16 && (uint64_t)mc->vmax - (uint64_t)mc->vmin < (1ull << 16)) P.mv16 = ensure_d16(p->ctx, mc, s, p->stream);
+            if (P.ord16 && d16_on() && (uint64_t)mc->vmax - (uint64_t)mc->vmin < (1ull << 16))
+                P.mv16 = ensure_d16(p->ctx, mc, s, p->stream);
         }
     }
     auto pi_fits = [&](uint32_t bpw) {  // docs of one workgroup range: count field and sum-of-deltas field both fit
@@ -3003,6 +3014,12 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     return ret;
 }
 
+// 16-bit deltas of long columns spanning < 2^16 (the packed cells' metric, range predicates); ESGPU_D16=0: the 32-bit
+// deltas instead (A/B runs)
+static bool d16_on() {
+    static const bool on = [] { const char* e = std::getenv("ESGPU_D16"); return !(e && *e == '0'); }();
+    return on;
+}
 // the compacted replay (ESGPU_REPLAY_COMPACT=0: one pass over the segments per batch of winners, for A/B runs)
 static bool replay_compaction() {
     static const bool on = [] { const char* e = std::getenv("ESGPU_REPLAY_COMPACT"); return !(e && *e == '0'); }();
@@ -3235,9 +3252,16 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
             const char* e = std::getenv("ESGPU_HLL_FS_MINF");
             return e && *e ? std::max(2u, (uint32_t)std::atoi(e)) : 4u;
         }();
+        // The floor is chosen from the distinct values the registers will have seen -- not the doc count: values
+        // repeat (2^27 synthetic IPs over 1B docs: ~7 docs per value), and a floor picked from the docs would leave
+        // registers below it for the tail pass.  The segment's distinct count comes from an earlier request's registers
+        // (DevColumn::hll_distinct, a cached statistic like the compact columns); the first request on a segment takes
+        // the register phases.  Over several segments the largest estimate is a lower bound of the union's.
         const int fs_mode = p->ctx->opt_hll_fs.load();
         const bool dense = !H.accept && H.npred == 0 && !H.present && !col->multi && H.kind != HLL_ORD;
-        uint32_t F = fs_mode && dense ? hll_fs_floor(pl.hll_seen + H.n_docs, pl.p, fs_minf) : 0u;
+        const double dseg = col->hll_distinct->load();
+        const double dknown = dseg >= 0 ? std::max(dseg, pl.hll_dmax) : -1.0;
+        uint32_t F = fs_mode && dense && dknown >= 0 ? hll_fs_floor((uint64_t)dknown, pl.p, fs_minf) : 0u;
         if (F && fs_mode > 1) F = std::min<uint32_t>(F + (uint32_t)fs_mode - 1, 64u - (uint32_t)pl.p);
         if (F) {
             const uint32_t cap = hll_fs_cap(H.n_docs, pl.p, F);
@@ -3255,6 +3279,14 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
     H.pos_base = (uint64_t)p->seg_seq << 40;
     H.seen = pl.hll_seen;
     if (H.n_docs == 0) return false;
+    if (pl.hll_seen == 0) {
+        const bool dense1 = !H.accept && H.npred == 0 && !H.present && !col->multi && H.kind != HLL_ORD;
+        pl.hll_d1 = dense1 ? col->hll_distinct : nullptr;
+        pl.hll_nseg = 0;
+        pl.hll_dmax = 0.0;
+    }
+    ++pl.hll_nseg;
+    if (col->hll_distinct->load() >= 0) pl.hll_dmax = std::max(pl.hll_dmax, col->hll_distinct->load());
     pl.hll_seen += H.n_docs;
     pl.lc_dirty = true;
     HIPX(hipEventRecord(pl.e0, p->stream));
@@ -3422,6 +3454,7 @@ extern "C" int esgpu_plan_post_collection(esgpu_plan* p) {
                 std::vector<std::pair<uint64_t, uint32_t>> added;
                 for (size_t i = 0; i < cap; ++i) if (set[i]) added.emplace_back(first[i], set[i]);
                 pl.h_lc = hashset_values(added, pl.p);
+                if (pl.hll_nseg == 1 && pl.hll_d1 && pl.hll_d1->load() < 0) pl.hll_d1->store((double)added.size());
             } else {  // HYPERLOGLOG
                 pl.hll_mode = 1;
                 // registers are u32 on the device (atomicMax); pack to the reference's byte array before the copy
@@ -3432,6 +3465,14 @@ extern "C" int esgpu_plan_post_collection(esgpu_plan* p) {
                 const uint8_t* r = p->h_dst[0].as<uint8_t>();
                 bsync(p);
                 pl.h_regs.assign(r, r + m);
+                if (pl.hll_nseg == 1 && pl.hll_d1 && pl.hll_d1->load() < 0) {
+                    // the raw HyperLogLog estimate of the segment's distinct values (once per segment: the floored
+                    // stream's floor on later requests)
+                    double z = 0.0;
+                    for (uint32_t i = 0; i < m; ++i) z += std::ldexp(1.0, -(int)r[i]);
+                    const double alpha = 0.7213 / (1.0 + 1.079 / m);
+                    pl.hll_d1->store(alpha * (double)m * (double)m / z);
+                }
             }
         }
         p->posted = true;
@@ -4903,6 +4944,8 @@ extern "C" int esgpu_plan_reset(esgpu_plan* p) {
                 pl.h_regs.clear();
                 pl.any_value = false;
                 pl.hll_seen = 0;
+                pl.hll_d1.reset();
+                pl.hll_nseg = 0;
                 continue;
             }
             const size_t cells = (size_t)pl.T * pl.H;

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun session: GPU parity tests, kernel sweep, bench, rocprofv3 kernel-trace stats and PMC HBM-traffic passes.
 #   gpurun --timeout 1200 -- bash tools/gpu_check.sh <tag> [steps...]
-# steps: tests testsdyn testfile testfiles piab fsab kbench bench jitter export shape125 configs dynab hllab cut0ab buildtrace profk125 prof profk pmc pmck variants (default: tests kbench bench prof pmc)
+# steps: tests testsdyn testfile testfiles piab fsab d16ab kbench bench jitter export shape125 configs dynab hllab cut0ab buildtrace profk125 prof profk pmc pmck variants (default: tests kbench bench prof pmc)
 # KBENCH_ONLY=name,name restricts the kbench sweeps (KBENCH_ARGS: extra kbench flags for variants, KBENCH_TAG: log suffix); variants = every build/variants/libesgpu_*.so via ESGPU_LIBRARY.  Every GPU step has its own time limit; the first failure ends it.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -62,6 +62,11 @@ for s in $STEPS; do
                   ESGPU_HLL_FS=$f run "kbench_fs${f}_$docs" 300 python3 "$R/tools/kbench.py" --docs $docs --reps 5 \
                       --only config4_card || exit 1
               done; done ;;
+        d16ab) # 16-bit deltas (packed cells' metric, range predicates) vs 32-bit (ESGPU_D16=0), same box
+              for d in 1 0; do
+                  ESGPU_D16=$d run "kbench_d16_$d" 400 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 \
+                      --only ${KBENCH_ONLY:-north_star,ns_avg,config5,config1_terms_stats} || exit 1
+              done ;;
         cut0ab) # HLL phase 0 length (ESGPU_HLL_CUT0 x 2^p values through the partitioned phase 0)
               for c in 4 16 64; do for docs in 125000000 1000000000; do
                   ESGPU_HLL_CUT0=$c run "kbench_cut${c}_$docs" 300 python3 "$R/tools/kbench.py" --docs $docs --reps 5 \
