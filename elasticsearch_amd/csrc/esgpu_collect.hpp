@@ -463,6 +463,66 @@ __device__ __forceinline__ void runs_add(const CollectParams& P, const Acc& a, R
     }
 }
 
+// n docs at once into the run of `slot` (a thread's 4 docs that share a key slot, combined in registers first): the run
+// lookup and its predicated per-run updates once per 4 docs instead of once per doc
+template <int MET, int MS, int NR>
+__device__ __forceinline__ void runs_add_n(const CollectParams& P, const Acc& a, Runs<NR>& R, uint32_t slot, uint32_t n,
+                                           uint32_t vc, double sum, double sq, unsigned long long mn, unsigned long long mx) {
+    int hit = -1;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) hit = R.r[k].slot == slot ? k : hit;
+    if (hit < 0) {
+        hit = NR == 1 ? 0 : (int)R.victim;
+#pragma unroll
+        for (int k = 0; k < NR; ++k)
+            if (k == hit) {
+                run_flush<MET, MS>(P, a, R.r[k]);
+                R.r[k].slot = slot;
+            }
+        if (NR > 1) R.victim = R.victim + 1 == (uint32_t)NR ? 0u : R.victim + 1;
+    }
+    // the hit run's fields selected into registers, updated once, and selected back (indexing R.r by `hit`, or
+    // updating under `k == hit`, lets the compiler turn the runs into a dynamically indexed array in scratch)
+    Run c = R.r[0];
+#pragma unroll
+    for (int k = 1; k < NR; ++k) {
+        const bool h = hit == k;
+        c.cnt = h ? R.r[k].cnt : c.cnt;
+        c.vc = h ? R.r[k].vc : c.vc;
+        c.sum = h ? R.r[k].sum : c.sum;
+        c.sq = h ? R.r[k].sq : c.sq;
+        c.mn = h ? R.r[k].mn : c.mn;
+        c.mx = h ? R.r[k].mx : c.mx;
+    }
+    c.cnt += n;
+    if (MET > 0) {
+        c.vc += vc;
+        c.sum += sum;
+        if (MET >= 3) c.sq += sq;
+        if (MET >= 2) {
+            c.mn = mn < c.mn ? mn : c.mn;
+            c.mx = mx > c.mx ? mx : c.mx;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+        const bool h = hit == k;
+        R.r[k].cnt = h ? c.cnt : R.r[k].cnt;
+        if (MET > 0) {
+            R.r[k].vc = h ? c.vc : R.r[k].vc;
+            R.r[k].sum = h ? c.sum : R.r[k].sum;
+            if (MET >= 3) R.r[k].sq = h ? c.sq : R.r[k].sq;
+            if (MET >= 2) {
+                R.r[k].mn = h ? c.mn : R.r[k].mn;
+                R.r[k].mx = h ? c.mx : R.r[k].mx;
+            }
+        }
+    }
+}
+#ifndef ESGPU_RUN4  // histogram-only grids: a thread's 4 docs with one key slot combined before the run update
+#define ESGPU_RUN4 1
+#endif
+
 #ifndef ESGPU_COMBINE4  // counting ORD x histogram grids: combine a thread's equal keys before the LDS atomics
 #define ESGPU_COMBINE4 1
 #endif
@@ -512,6 +572,53 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
         }
     }
     if (LDS && !ORD) {  // ocnt_mode is OCNT_NONE without a terms dimension; without HIST the slot is always 0
+        if (ESGPU_RUN4) {
+            uint32_t okm = 0, first = ~0u;
+#pragma unroll
+            for (int j = 0; j < kVec; ++j) okm |= (((d.ok >> j) & 1) && hv_ok[j] ? 1u : 0u) << j;
+            bool same = true;
+#pragma unroll
+            for (int j = 0; j < kVec; ++j)
+                if ((okm >> j) & 1) {
+                    if (first == ~0u) first = slot[j];
+                    same = same && slot[j] == first;
+                }
+            // groups of docs with one key slot: all of them (time-sorted data: nearly always, a thread's 4 docs are
+            // consecutive), else one doc each; one run update per group (a rolled loop: one inlined copy of the update)
+            uint32_t rest = okm;
+#pragma unroll
+            for (int it = 0; it < kVec; ++it) {
+                if (!rest) break;
+                const uint32_t g = same ? rest : (rest & (0u - rest));
+                rest &= ~g;
+                uint32_t gs = first;
+#pragma unroll
+                for (int j = kVec - 1; j >= 0; --j)
+                    if (!same && ((g >> j) & 1)) gs = slot[j];
+                uint32_t vc = 0;
+                double sum = 0.0, sq = 0.0;
+                unsigned long long mn = kMinInit, mx = kMaxInit;
+                if (MET > 0) {
+#pragma unroll
+                    for (int j = 0; j < kVec; ++j) {
+                        const bool m = ((g >> j) & 1) && ((d.mpres >> j) & 1);
+                        const double x = m ? d.mv[j] : 0.0;
+                        vc += m ? 1u : 0u;
+                        sum += x;
+                        if (MET >= 3) sq += x * x;
+                        if (MET >= 2) {
+                            const bool nan = x != x;
+                            const unsigned long long e = sortable(x);
+                            const unsigned long long emn = !m ? kMinInit : nan ? 0ull : e, emx = !m ? kMaxInit : nan ? ~0ull : e;
+                            mn = emn < mn ? emn : mn;
+                            mx = emx > mx ? emx : mx;
+                        }
+                    }
+                }
+                runs_add_n<MET, MS>(P, a, run, gs, (uint32_t)__builtin_popcount(g), vc, sum, sq, mn, mx);
+            }
+            return;
+        }
 #pragma unroll
         for (int j = 0; j < kVec; ++j) {
             if (!((d.ok >> j) & 1) || !hv_ok[j]) continue;
@@ -774,8 +881,14 @@ __device__ __forceinline__ uint32_t claim_chunk(unsigned int* claim) {
 // WGS: threads per workgroup -- 512 (two resident per CU, each with an LDS window of <= 64 KB), or 1024 for
 // histogram grids whose data needs a wider window than 64 KB holds (one workgroup per CU with up to 150 KB of LDS,
 // the same 16 waves per CU)
+#ifndef ESGPU_PI_WAVES  // packed-cell kernels: waves per SIMD the register budget must allow (6: three 512-thread workgroups per CU)
+#define ESGPU_PI_WAVES 6
+#endif
+// 4 waves per SIMD (16 per CU): <= 128 VGPRs; packed-cell kernels ESGPU_PI_WAVES (6: <= 80 VGPRs, 24 waves per CU with the
+// runtime's ESGPU_LDS_PI window budget -- the stream's bytes in flight scale with the waves)
+template <int VK, int WGS> constexpr int collect_min_waves() { return (VK & 64) && WGS == 512 ? ESGPU_PI_WAVES : 4; }
 template <bool ORD, int HK, int MET, int VK, int WGS>
-__global__ __launch_bounds__(WGS) void collect_kernel(CollectParams P) {
+__global__ __launch_bounds__(WGS, (collect_min_waves<VK, WGS>())) void collect_kernel(CollectParams P) {
     constexpr int kIterDocsW = WGS * kVec;
     constexpr int kItersPerBlockW = kBlockDocs / kIterDocsW;
     constexpr bool HIST = HK != 0;

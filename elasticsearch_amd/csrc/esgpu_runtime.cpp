@@ -2871,7 +2871,10 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
 #ifndef ESGPU_LDS_PAIR  // LDS budget of a window that keeps two workgroups per CU
 #define ESGPU_LDS_PAIR (64 * 1024)
 #endif
-    const size_t kLdsPair = ESGPU_LDS_PAIR, kLdsMax = 150 * 1024;
+#ifndef ESGPU_LDS_PI  // packed cells: a window that keeps three 512-thread workgroups per CU (24 waves: more loads in flight)
+#define ESGPU_LDS_PI (52 * 1024)
+#endif
+    const size_t kLdsPair = pi ? (size_t)ESGPU_LDS_PI : (size_t)ESGPU_LDS_PAIR, kLdsMax = 150 * 1024;
     uint32_t W = LH;
     size_t lds = collect_lds_bytes(LT, W, L_met, L_vcnt, L_ocnt, 1, pi);
     P.lds_mode = 1;
@@ -3261,7 +3264,16 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
         const bool dense = !H.accept && H.npred == 0 && !H.present && !col->multi && H.kind != HLL_ORD;
         const double dseg = col->hll_distinct->load();
         const double dknown = dseg >= 0 ? std::max(dseg, pl.hll_dmax) : -1.0;
-        uint32_t F = fs_mode && dense && dknown >= 0 ? hll_fs_floor((uint64_t)dknown, pl.p, fs_minf) : 0u;
+        // Measured at p = 18 (profiles/r4_hll_floor_ab.jsonl): the stream wins over the phases on a 125M-doc segment
+        // (0.233 vs 0.290 ms) and loses on 1B (1.77 vs 1.60 ms) -- the phases' cost beyond streaming is a fixed ~0.1 ms
+        // (their gathers and snapshot loads), the stream's grows with the entries it logs -- so it takes segments of up
+        // to 1,024 values per register
+        static const uint64_t fs_max_per_reg = [] {
+            const char* e = std::getenv("ESGPU_HLL_FS_MAXPR");
+            return e && *e ? (uint64_t)std::atoll(e) : (uint64_t)1024;
+        }();
+        const bool fs_size = (uint64_t)H.n_docs <= fs_max_per_reg * m;
+        uint32_t F = fs_mode && dense && fs_size && dknown >= 0 ? hll_fs_floor((uint64_t)dknown, pl.p, fs_minf) : 0u;
         if (F && fs_mode > 1) F = std::min<uint32_t>(F + (uint32_t)fs_mode - 1, 64u - (uint32_t)pl.p);
         if (F) {
             const uint32_t cap = hll_fs_cap(H.n_docs, pl.p, F);
@@ -4186,6 +4198,8 @@ static ReplaySel replay_child(esgpu_plan* p, const ChildSrc& kid, const std::vec
             continue;
         }
         // per winner row: the GPU top-k (K3) over its inner ordinals, then one gather of the picked cells of every array
+        require(p->docs_seen < (1ull << 31), ESGPU_ERR_UNSUPPORTED,
+                "a breadth-first terms request over more than 2^31 - 1 docs (more than one Lucene shard): runs on the CPU path");
         const bool big = kk > kTopkMax;
         unsigned long long* dk = (unsigned long long*)p->s_rkeys.ensure(p->ctx, (size_t)kb * (kk + 1) * 8);
         HIPX(hipMemsetAsync(dk, 0, (size_t)kb * (kk + 1) * 8, st));
@@ -4301,7 +4315,9 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
     std::vector<TermPick> top;
     const uint64_t k_req = std::min<uint64_t>(P0.value_count, (uint64_t)std::max(tn.s.shard_size, 0));
     const bool count_order = tn.s.order == ESGPU_ORDER_COUNT_DESC || tn.s.order == ESGPU_ORDER_COUNT_ASC;
-    const bool gpu_topk = !agg_order && P0.value_count > 65536 && k_req <= kTopkMax && (P0.H == 1 || count_order);
+    // (the GPU top-k's keys hold a count in 31 bits: a request over at most 2^31 - 1 docs, i.e. one Lucene shard)
+    const bool gpu_topk = !agg_order && P0.value_count > 65536 && k_req <= kTopkMax && (P0.H == 1 || count_order) &&
+                          p->docs_seen < (1ull << 31);
     if (P0.cnt32 && !gpu_topk) {  // u32 counts (partitioned / hot-cold paths) widened for the host selection
         unsigned long long* w = (unsigned long long*)p->s_tcnt.ensure(p->ctx, (size_t)T * 8);
         launch_widen_u32(P0.g_cnt.as<unsigned int>(), T, w, st);

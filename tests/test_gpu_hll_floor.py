@@ -71,10 +71,10 @@ def test_config4_fresh_125m_plan(engine, c4_125m, mode):
 
 @pytest.mark.parametrize("mode", MODES)
 def test_merged_shards_continue_the_floor(engine, mode):
-    """4 x 30M-doc segments into one plan after each was collected alone once (their distinct estimates; each later
-    segment's floor comes from the largest estimate so far).  At p = 18 (~27M distinct per segment) no segment reaches a
-    floor (the phases run); at p = 14 every segment takes F = 7."""
-    n, shards = 30_000_000, 4
+    """4 x 15M-doc segments into one plan after each was collected alone once (their distinct estimates; each later
+    segment's floor comes from the largest estimate so far).  At p = 18 (~14M distinct per segment) no segment reaches a
+    floor (the phases run); at p = 14 every segment takes F = 6."""
+    n, shards = 15_000_000, 4
     fields = ("client_ip.hash",)
     for thr in (40000, 2000):
         aggs = [AB.cardinality("ips").field("client_ip.hash").precisionThreshold(thr)]
@@ -96,8 +96,9 @@ def test_merged_shards_continue_the_floor(engine, mode):
 @pytest.mark.parametrize("field,thr", [("client_ip.hash", 1000), ("price", 1000), ("price", 40000)])
 def test_smaller_precision_and_double_values(engine, mode, field, thr):
     """p = 13 (128 register ranges of 64 instead of 256) and a double column (doubleToLongBits, NaN canonicalised) over
-    24M docs; at p = 18 the double column has too few values per register for a floor (the phases run in every mode)."""
-    n = 24_000_000
+    8M docs (F = 6: the stream takes segments of up to 1,024 values per register); at p = 18 the double column has too
+    few values per register for a floor (the phases run in every mode)."""
+    n = 8_000_000
     aggs = [AB.cardinality("c").field(field).precisionThreshold(thr)]
     want = O.run([(synthetic_columns((field,), n, shard=7), n)], aggs)
     seg = engine.synthetic_segment(n, fields=(field,), shard=7)

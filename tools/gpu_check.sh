@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun session: GPU parity tests, kernel sweep, bench, rocprofv3 kernel-trace stats and PMC HBM-traffic passes.
 #   gpurun --timeout 1200 -- bash tools/gpu_check.sh <tag> [steps...]
-# steps: tests testsdyn testfile testfiles piab fsab d16ab kbench bench jitter export shape125 configs dynab hllab cut0ab buildtrace profk125 prof profk pmc pmck variants (default: tests kbench bench prof pmc)
+# steps: tests testsdyn testfile testfiles piab fsab d16ab pmcall kbench bench jitter export shape125 configs dynab hllab cut0ab buildtrace profk125 prof profk pmc pmck variants (default: tests kbench bench prof pmc)
 # KBENCH_ONLY=name,name restricts the kbench sweeps (KBENCH_ARGS: extra kbench flags for variants, KBENCH_TAG: log suffix); variants = every build/variants/libesgpu_*.so via ESGPU_LIBRARY.  Every GPU step has its own time limit; the first failure ends it.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -135,6 +135,17 @@ for s in $STEPS; do
                  python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-docs 0 --inflight 1 &&
              run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o bench -- \
                  python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-docs 0 --inflight 1 ;;
+        pmcall) # FETCH_SIZE / WRITE_SIZE passes (one counter per pass) of every bench shape's collect, 4 collects each
+                # (kbench --reps 3), for tools/pmc_traffic.py -> profiles/hbm_traffic.json (bench roofline.traffic)
+              for spec in north_star:1000000000 north_star:125000000 config2_dh_ext:100000000 config3_url:125000000 \
+                          config4_card:125000000 config5:125000000; do
+                  v=${spec%%:*}; d=${spec##*:}
+                  for c in FETCH_SIZE WRITE_SIZE; do
+                      cd /tmp && run "pmcall_${v}_${d}_$c" 300 rocprofv3 --pmc $c --kernel-trace --output-format csv \
+                          -d "$OUT/pmcall_${v}_${d}_$c" -o kb -- python3 "$R/tools/kbench.py" --docs $d --reps 3 --only $v \
+                          || exit 1
+                  done
+              done ;;
         pmck) # counters for the kbench shapes in KBENCH_ONLY (default config3_url), one counter group per pass
               for grp in FETCH_SIZE WRITE_SIZE "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
                          "SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"; do
