@@ -140,8 +140,15 @@ template <bool ORD, bool HIST, int MET, int VK>
 __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0, Doc4& d) {
     uint32_t ok = 0xF;
     if (doc0 + 4 > P.n_docs) ok = doc0 >= P.n_docs ? 0u : ((1u << (P.n_docs - doc0)) - 1u);
-    if (P.accept) ok &= bits4(P.accept, doc0);
-    for (int k = 0; k < P.npred; ++k) ok &= eval_pred(P.pred[k], doc0);
+    if constexpr (MET > 0 && (VK & 64)) {
+        // packed-cell kernels read no clause and no conditional bitset: the host folds the request's clauses and live
+        // docs into one accept bitset first (VK bit 512: loaded unconditionally) -- a load under a runtime branch makes
+        // the compiler wait for every load in flight at each later use, i.e. for the other buffer's prefetch
+        if constexpr ((VK & 512) != 0) ok &= bits4(P.accept, doc0);
+    } else {
+        if (P.accept) ok &= bits4(P.accept, doc0);
+        for (int k = 0; k < P.npred; ++k) ok &= eval_pred(P.pred[k], doc0);
+    }
     d.ok = ok;
     if (ORD && (VK & 8)) {  // inner histogram key index, derived in registers (HistogramAggregator under a histogram)
         int64_t v[4];
@@ -519,8 +526,8 @@ __device__ __forceinline__ void runs_add_n(const CollectParams& P, const Acc& a,
         }
     }
 }
-#ifndef ESGPU_RUN4  // histogram-only grids: a thread's 4 docs with one key slot combined before the run update
-#define ESGPU_RUN4 1
+#ifndef ESGPU_RUN4  // histogram-only grids: a thread's 4 docs with one key slot combined before the run update; measured
+#define ESGPU_RUN4 0  // slower (config 2 at 1B docs 2.15 -> 2.62 ms, date_histogram 1.03 -> 1.14 ms): off, kept for A/B
 #endif
 
 #ifndef ESGPU_COMBINE4  // counting ORD x histogram grids: combine a thread's equal keys before the LDS atomics
@@ -1179,7 +1186,7 @@ static auto with_vk0(bool hv_f64, bool mv_f64, F f) {
 // Bits 16 / 32 (compact ordinal / histogram columns): terms dimensions without a derived key index, affine histograms
 // over a long column.
 template <bool ORD, int HK, int MET, class F>
-static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, bool pi, bool m32, bool m16, F f) {
+static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, bool pi, bool m32, bool m16, bool acc, F f) {
     // VK bit 128, a compact long metric (u32 deltas, values restored in the loader): histogram-only grids over compact
     // timestamps (date_histogram{stats / extended_stats / avg}) and extended_stats under terms over compact columns
     if constexpr (MET > 0 && !ORD && HK == 1) {
@@ -1196,16 +1203,19 @@ static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, boo
     }
     // VK bit 64, packed integer metric cells: terms grids (no key, or an affine key over the compact timestamps) with
     // avg / stats over a dense long metric
-    // (+ bit 256: the 16-bit deltas, with 16-bit ordinals only)
+    // (+ bit 256: the 16-bit deltas, with 16-bit ordinals only; + bit 512: filtered through one accept bitset, with the
+    // 16-bit deltas only -- the host keeps the f64 cells for other filtered shapes)
     if constexpr (ORD && (HK == 0 || HK == 1) && (MET == 1 || MET == 2)) {
         if (pi && !mv_f64 && !dord) {
             if constexpr (HK == 1) {
                 if (t32 && !hv_f64) {
+                    if (c16 && m16 && acc) return f(std::integral_constant<int, 48 | 64 | 256 | 512>{});
                     if (c16 && m16) return f(std::integral_constant<int, 48 | 64 | 256>{});
                     if (c16) return f(std::integral_constant<int, 48 | 64>{});
                     return f(std::integral_constant<int, 32 | 64>{});
                 }
             } else {
+                if (c16 && m16 && acc) return f(std::integral_constant<int, 16 | 64 | 256 | 512>{});
                 if (c16 && m16) return f(std::integral_constant<int, 16 | 64 | 256>{});
                 if (c16) return f(std::integral_constant<int, 16 | 64>{});
                 return f(std::integral_constant<int, 64>{});
@@ -1245,7 +1255,7 @@ template <bool ORD, int HK, int MET>
 static void launch_t(const CollectParams& p, bool wide, uint32_t grid, size_t lds, hipStream_t st) {
     with_vk<ORD, HK, MET>(p.hv_f64 != 0, p.mv_f64 != 0, p.ord_src != nullptr, p.ord16 != nullptr, p.hv32 != nullptr,
                           p.mv32 != nullptr && p.pk_shift != 0, p.mv32 != nullptr && p.pk_shift == 0, p.mv16 != nullptr,
-                          [&](auto vk) {
+                          p.accept != nullptr, [&](auto vk) {
         return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
             hipLaunchKernelGGL((collect_kernel<ORD, HK, MET, decltype(vk)::value, decltype(wg)::value>), dim3(grid),
                                dim3(decltype(wg)::value), lds, st, p);
@@ -1267,7 +1277,8 @@ static void launch_m(const CollectParams& p, int met, bool wide, uint32_t grid, 
 template <bool ORD, int HK, int MET>
 static int occ_t(size_t lds, int vkbits, bool wide) {
     return with_vk<ORD, HK, MET>((vkbits & 1) != 0, (vkbits & 2) != 0, (vkbits & 8) != 0, (vkbits & 16) != 0,
-                                 (vkbits & 32) != 0, (vkbits & 64) != 0, (vkbits & 128) != 0, (vkbits & 256) != 0, [&](auto vk) {
+                                 (vkbits & 32) != 0, (vkbits & 64) != 0, (vkbits & 128) != 0, (vkbits & 256) != 0,
+                                 (vkbits & 512) != 0, [&](auto vk) {
         return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
             int n = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(

@@ -2031,6 +2031,38 @@ void launch_filter_bits(uint32_t n_docs, const uint64_t* accept, const PredDev* 
     hipLaunchKernelGGL(filter_bits_kernel, dim3(std::min<uint32_t>(4096, (nw + 255) / 256)), dim3(256), 0, st, A);
 }
 
+// the request's clauses over single-valued columns folded into a doc bitset at the streaming rate (4 docs per thread,
+// the collect loader's quad predicates; 16 lanes' 4-bit masks OR-ed into each 64-doc word), for the collect kernels
+// that read one accept bitset instead of evaluating clauses (VK bit 512)
+__global__ __launch_bounds__(256) void filter_bits4_kernel(FilterBitsArgs A, uint32_t n_quads) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t q0 = blockIdx.x * 256; q0 < n_quads; q0 += gridDim.x * 256) {  // block-uniform trip count
+        const uint32_t q = q0 + threadIdx.x, doc0 = q * 4;
+        uint64_t m = 0;
+        if (q < n_quads) {
+            uint32_t ok = doc0 + 4 <= A.n_docs ? 0xFu : doc0 >= A.n_docs ? 0u : (1u << (A.n_docs - doc0)) - 1u;
+            if (A.accept) ok &= (uint32_t)(A.accept[doc0 >> 6] >> (doc0 & 63)) & 0xFu;
+            for (int k = 0; k < A.npred; ++k) ok &= eval_pred(A.pred[k], doc0);
+            m = (uint64_t)ok << ((lane & 15) * 4);
+        }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) m |= (uint64_t)__shfl_xor((long long)m, o, 64);
+        if ((lane & 15) == 0 && q < n_quads) A.out[doc0 >> 6] = m;
+    }
+}
+void launch_filter_bits4(uint32_t n_docs, const uint64_t* accept, const PredDev* preds, int npred, uint64_t* out,
+                         hipStream_t st) {
+    FilterBitsArgs A{};
+    A.n_docs = n_docs;
+    A.npred = npred;
+    A.accept = accept;
+    A.out = out;
+    for (int k = 0; k < npred && k < 4; ++k) A.pred[k] = preds[k];
+    const uint32_t nq = ((n_docs + 63) / 64) * 16;  // whole words
+    if (nq == 0) return;
+    hipLaunchKernelGGL(filter_bits4_kernel, dim3(std::min<uint32_t>(8192, (nq + 255) / 256)), dim3(256), 0, st, A, nq);
+}
+
 __global__ __launch_bounds__(256) void expand_bits_kernel(uint32_t n_docs, const uint64_t* doc_bits, const uint64_t* off,
                                                          uint64_t* out) {
     for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < n_docs; d += gridDim.x * blockDim.x) {

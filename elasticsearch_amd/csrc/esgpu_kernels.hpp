@@ -249,6 +249,8 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t s);
 // pair of the doc is a cell update, metrics aggregate all of the doc's values once (StatsAggegator's local sum).
 void launch_collect_multi(const CollectParams& p, bool ord, bool hist, int met, uint32_t grid, size_t lds, hipStream_t s);
 // doc bitset of (accept AND every predicate); multi-valued predicate columns match if any value matches
+void launch_filter_bits4(uint32_t n_docs, const uint64_t* accept, const PredDev* preds, int npred, uint64_t* out,
+                         hipStream_t st);  // single-valued clauses only (no offsets)
 void launch_filter_bits(uint32_t n_docs, const uint64_t* accept, const PredDev* preds, int npred, uint64_t* out,
                         hipStream_t s);
 // per-value bitset from a doc bitset over a CSR column (out zeroed by the launcher, words for n_values)

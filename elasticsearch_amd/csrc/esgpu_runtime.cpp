@@ -2837,6 +2837,13 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
             // 16-bit ordinals)
             if (P.ord16 && d16_on() && (uint64_t)mc->vmax - (uint64_t)mc->vmin < (1ull << 16))
                 P.mv16 = ensure_d16(p->ctx, mc, s, p->stream);
+            // a filtered request (clauses or live docs) takes the packed cells through one folded accept bitset, which
+            // is instantiated with the 16-bit columns only (with_vk)
+            if ((P.npred > 0 || P.accept) && !(P.ord16 && P.mv16)) {
+                pi = false;
+                P.mv32 = nullptr;
+                P.mv16 = nullptr;
+            }
         }
     }
     auto pi_fits = [&](uint32_t bpw) {  // docs of one workgroup range: count field and sum-of-deltas field both fit
@@ -2957,8 +2964,10 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         P.mg_m = mg.m; P.mg_s1 = mg.s1; P.mg_s2 = mg.s2;
     }
     const int hk = L_HIST ? (P.hord ? 3 : P.kstart ? 2 : 1) : 0;
+    // packed cells under a filter: the clauses (and live docs) folded into one accept bitset before the collect
+    const bool fold = pi && (P.npred > 0 || P.accept);
     const int vk = (P.hv_f64 ? 1 : 0) | (P.mv_f64 ? 2 : 0) | (P.ord_src ? 8 : 0) | (P.ord16 ? 16 : 0) | (P.hv32 ? 32 : 0) |
-                   (pi ? 64 : 0) | (m32 ? 128 : 0) | (P.mv16 ? 256 : 0);
+                   (pi ? 64 : 0) | (m32 ? 128 : 0) | (P.mv16 ? 256 : 0) | (fold ? 512 : 0);
     const uint64_t occ_key = ((uint64_t)lds << 18) | ((uint64_t)wide << 17) | ((uint64_t)vk << 8) | ((uint64_t)L_met << 4) |
                              ((uint64_t)hk << 1) | (L_ORD ? 1 : 0);
     if (pl.occ_key != occ_key) {
@@ -3009,6 +3018,13 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         HIPX(hipGetLastError());
     }
     HIPX(hipEventRecord(pl.e0, p->stream));
+    if (fold && P.npred > 0) {  // (inside the timed region: part of the collect)
+        uint64_t* bits = (uint64_t*)p->s_xbits.ensure(p->ctx, std::max<size_t>(s->n_pad / 64, 1) * 8);
+        launch_filter_bits4(s->max_doc, P.accept, P.pred, P.npred, bits, p->stream);
+        HIPX(hipGetLastError());
+        P.accept = bits;
+        P.npred = 0;
+    }
     launch_collect(P, L_ORD, L_HIST, L_met, wide, grid, lds, p->stream);
     HIPX(hipGetLastError());
     HIPX(hipEventRecord(pl.e1, p->stream));

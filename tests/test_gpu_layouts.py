@@ -181,3 +181,28 @@ def test_packed_then_sparse_metric_segment(engine):
     for s in segs:
         s.close()
     assert_same(res.to_dict(), want["shards"][0], "shard")
+
+
+@pytest.mark.parametrize("name", ["compact", "packed"])
+@pytest.mark.parametrize("dead", [0.0, 0.3])
+def test_packed_cells_through_folded_filters(engine, name, dead):
+    """Packed cells under a filter read one accept bitset into which the host folds the request's clauses and the live
+    docs first (VK bit 512): config 5's clauses (a 16-bit status range, a 32-bit bytes range) with and without 30 % of the
+    docs deleted, terms{date_histogram{avg}} and terms{stats}, against the oracle; the compact layout (f64 cells,
+    clauses evaluated in the loader) runs the same request."""
+    n = 6_000_000
+    cols = synthetic_columns(C5_FIELDS, n, shard=4)
+    rng = np.random.default_rng(44)
+    accept = None
+    if dead:
+        accept = bits_from_mask(rng.random(n) >= dead)
+    aggs = C5_AGGS + [AB.terms("hs").field("host").size(15).subAggregation(AB.stats("s").field("response_time_ms"))]
+    want = O.run([(cols, n)], aggs, filters=C5_FILTERS, number_of_shards=8, accept=[accept] if accept is not None else None)
+    with layout(engine, name):
+        seg = engine.synthetic_segment(n, fields=C5_FIELDS, shard=4)
+        plan = engine.plan(aggs, filters=C5_FILTERS, number_of_shards=8)
+        plan.collect(seg, accept_bits=accept)
+        res = plan.build()
+        plan.close()
+        seg.close()
+    assert_same(res.to_dict(), want["shards"][0], f"{name} dead {dead}")
