@@ -40,6 +40,11 @@ constexpr uint32_t kGroup = kGroupBlocks;  // blocks per multi-pass group (esgpu
 #endif
 
 struct Doc4 {
+    // raw-loaded packed-cell kernels (kRawPI): the loads' words as they arrive, unpacked only when the docs are processed
+    // (a conversion right after the load would wait for it there, a full memory latency per buffer reload)
+    uint32_t raw[8];
+    uint64_t racc;
+    uint32_t doc0;
     uint32_t ord[kVec];
     int64_t hv[kVec];
     double mv[kVec];
@@ -136,8 +141,26 @@ __device__ __forceinline__ uint32_t eval_pred(const PredDev& q, uint32_t doc0) {
 // metric column holds doubles (else longs cast to double).  A runtime branch on these cost the north-star kernel ~6 %.
 // Compact columns (segment products built on first use): bit 16 = the terms dimension is read from the
 // 16-bit ordinal column (0xFFFF missing), bit 32 = the histogram column from its 32-bit deltas over hv_base.
+// packed-cell kernels over the 16-bit ordinals and metric deltas (and, with a key, the 32-bit timestamp deltas of a dense
+// timestamp column): loads only, no use of a loaded word until unpack_docs
+template <int MET, int VK, bool HIST>
+constexpr bool kRawPI = MET > 0 && (VK & 64) != 0 && (VK & 16) != 0 && (VK & 256) != 0 && (!HIST || (VK & 32) != 0);
+
 template <bool ORD, bool HIST, int MET, int VK>
 __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0, Doc4& d) {
+    if constexpr (kRawPI<MET, VK, HIST>) {
+        const u32x2_t o = load8(P.ord16 + doc0);
+        d.raw[0] = o.x; d.raw[1] = o.y;
+        if constexpr (HIST) {
+            const u32x4_t t = load16(P.hv32 + doc0);
+            d.raw[2] = t.x; d.raw[3] = t.y; d.raw[4] = t.z; d.raw[5] = t.w;
+        }
+        const u32x2_t m = load8(P.mv16 + doc0);
+        d.raw[6] = m.x; d.raw[7] = m.y;
+        if constexpr ((VK & 512) != 0) d.racc = P.accept[doc0 >> 6];
+        d.doc0 = doc0;
+        return;
+    }
     uint32_t ok = 0xF;
     if (doc0 + 4 > P.n_docs) ok = doc0 >= P.n_docs ? 0u : ((1u << (P.n_docs - doc0)) - 1u);
     if constexpr (MET > 0 && (VK & 64)) {
@@ -547,9 +570,34 @@ __device__ __forceinline__ void combine4(uint32_t (&k)[kVec], F emit) {
     }
 }
 
+// kRawPI: the raw words of a buffer turned into the docs' fields (ordinals, key values, metric deltas, pass mask)
+template <bool HIST, int MET, int VK>
+__device__ __forceinline__ void unpack_docs(const CollectParams& P, Doc4& d) {
+    const uint32_t doc0 = d.doc0;
+    uint32_t ok = doc0 + 4 <= P.n_docs ? 0xFu : doc0 >= P.n_docs ? 0u : ((1u << (P.n_docs - doc0)) - 1u);
+    if constexpr ((VK & 512) != 0) ok &= (uint32_t)(d.racc >> (doc0 & 63)) & 0xFu;
+    d.ok = ok;
+    const uint32_t x[4] = {d.raw[0] & 0xFFFFu, d.raw[0] >> 16, d.raw[1] & 0xFFFFu, d.raw[1] >> 16};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) d.ord[j] = x[j] == 0xFFFFu ? kMissingOrd : x[j];
+    if constexpr (HIST) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d.hv[j] = P.hv_base + (int64_t)d.raw[2 + j];
+        d.hpres = 0xFu;
+    }
+    d.mvd[0] = d.raw[6] & 0xFFFFu; d.mvd[1] = d.raw[6] >> 16; d.mvd[2] = d.raw[7] & 0xFFFFu; d.mvd[3] = d.raw[7] >> 16;
+    d.mpres = 0xFu;
+}
+
 template <bool ORD, bool HIST, int MET, bool LDS, bool KT, int MS, bool HORD = false, int VK = 0>
-__device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, const Doc4& d, uint32_t T, int64_t base,
+__device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, const Doc4& d_in, uint32_t T, int64_t base,
                                          uint32_t win0, Runs<runs_for<MET>()>& run, uint32_t mw = 0, bool outer = true) {
+    Doc4 du;
+    if constexpr (kRawPI<MET, VK, HIST>) {
+        du = d_in;
+        unpack_docs<HIST, MET, VK>(P, du);
+    }
+    const Doc4& d = kRawPI<MET, VK, HIST> ? du : d_in;
     uint32_t slot[kVec];
     bool hv_ok[kVec];
 #pragma unroll
@@ -893,9 +941,14 @@ __device__ __forceinline__ uint32_t claim_chunk(unsigned int* claim) {
 #endif
 // 4 waves per SIMD (16 per CU): <= 128 VGPRs; packed-cell kernels ESGPU_PI_WAVES (6: <= 80 VGPRs, 24 waves per CU with the
 // runtime's ESGPU_LDS_PI window budget -- the stream's bytes in flight scale with the waves)
-template <int VK, int WGS> constexpr int collect_min_waves() { return (VK & 64) && WGS == 512 ? ESGPU_PI_WAVES : 4; }
+#ifndef ESGPU_HIST_WAVES  // histogram-only grids with a metric over compact timestamps (VK bit 128): waves per SIMD
+#define ESGPU_HIST_WAVES 4
+#endif
+template <bool ORD, int VK, int WGS> constexpr int collect_min_waves() {
+    return (VK & 64) && WGS == 512 ? ESGPU_PI_WAVES : !ORD && (VK & 128) && WGS == 512 ? ESGPU_HIST_WAVES : 4;
+}
 template <bool ORD, int HK, int MET, int VK, int WGS>
-__global__ __launch_bounds__(WGS, (collect_min_waves<VK, WGS>())) void collect_kernel(CollectParams P) {
+__global__ __launch_bounds__(WGS, (collect_min_waves<ORD, VK, WGS>())) void collect_kernel(CollectParams P) {
     constexpr int kIterDocsW = WGS * kVec;
     constexpr int kItersPerBlockW = kBlockDocs / kIterDocsW;
     constexpr bool HIST = HK != 0;

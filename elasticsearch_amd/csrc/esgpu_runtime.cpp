@@ -2835,7 +2835,8 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
             pi = true;
             // values spanning < 2^16 (a latency in ms, a status code): the 16-bit deltas, 2 B per doc (instantiated with
             // 16-bit ordinals)
-            if (P.ord16 && d16_on() && (uint64_t)mc->vmax - (uint64_t)mc->vmin < (1ull << 16))
+            // (those kernels load raw words and unpack them when the docs are processed: dense timestamps only)
+            if (P.ord16 && d16_on() && (uint64_t)mc->vmax - (uint64_t)mc->vmin < (1ull << 16) && !(hk_launch == 1 && P.hv_present))
                 P.mv16 = ensure_d16(p->ctx, mc, s, p->stream);
             // a filtered request (clauses or live docs) takes the packed cells through one folded accept bitset, which
             // is instantiated with the 16-bit columns only (with_vk)
