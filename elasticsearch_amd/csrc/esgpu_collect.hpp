@@ -145,6 +145,10 @@ __device__ __forceinline__ uint32_t eval_pred(const PredDev& q, uint32_t doc0) {
 // timestamp column): loads only, no use of a loaded word until unpack_docs
 template <int MET, int VK, bool HIST>
 constexpr bool kRawPI = MET > 0 && (VK & 64) != 0 && (VK & 16) != 0 && (VK & 256) != 0 && (!HIST || (VK & 32) != 0);
+// VK bit 1024: histogram-only grids over dense compact timestamps (and a dense compact long metric), no filter -- the
+// same raw loads (the timestamps' and the metric's u32 deltas), unpacked when processed
+template <bool ORD, int MET, int VK>
+constexpr bool kRawH = !ORD && (VK & 1024) != 0;
 
 template <bool ORD, bool HIST, int MET, int VK>
 __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0, Doc4& d) {
@@ -158,6 +162,16 @@ __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0,
         const u32x2_t m = load8(P.mv16 + doc0);
         d.raw[6] = m.x; d.raw[7] = m.y;
         if constexpr ((VK & 512) != 0) d.racc = P.accept[doc0 >> 6];
+        d.doc0 = doc0;
+        return;
+    }
+    if constexpr (kRawH<ORD, MET, VK>) {
+        const u32x4_t t = load16(P.hv32 + doc0);
+        d.raw[2] = t.x; d.raw[3] = t.y; d.raw[4] = t.z; d.raw[5] = t.w;
+        if constexpr (MET > 0) {
+            const u32x4_t m = load16(P.mv32 + doc0);
+            d.raw[0] = m.x; d.raw[1] = m.y; d.raw[6] = m.z; d.raw[7] = m.w;
+        }
         d.doc0 = doc0;
         return;
     }
@@ -596,8 +610,21 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
     if constexpr (kRawPI<MET, VK, HIST>) {
         du = d_in;
         unpack_docs<HIST, MET, VK>(P, du);
+    } else if constexpr (kRawH<ORD, MET, VK>) {
+        du = d_in;
+        const uint32_t doc0 = du.doc0;
+        du.ok = doc0 + 4 <= P.n_docs ? 0xFu : doc0 >= P.n_docs ? 0u : ((1u << (P.n_docs - doc0)) - 1u);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) du.hv[j] = P.hv_base + (int64_t)du.raw[2 + j];
+        du.hpres = 0xFu;
+        if constexpr (MET > 0) {
+            const uint32_t t[4] = {du.raw[0], du.raw[1], du.raw[6], du.raw[7]};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) du.mv[j] = (double)(P.mv_base + (int64_t)t[j]);  // FieldData.castToDouble of the long
+            du.mpres = 0xFu;
+        }
     }
-    const Doc4& d = kRawPI<MET, VK, HIST> ? du : d_in;
+    const Doc4& d = kRawPI<MET, VK, HIST> || kRawH<ORD, MET, VK> ? du : d_in;
     uint32_t slot[kVec];
     bool hv_ok[kVec];
 #pragma unroll
@@ -941,11 +968,11 @@ __device__ __forceinline__ uint32_t claim_chunk(unsigned int* claim) {
 #endif
 // 4 waves per SIMD (16 per CU): <= 128 VGPRs; packed-cell kernels ESGPU_PI_WAVES (6: <= 80 VGPRs, 24 waves per CU with the
 // runtime's ESGPU_LDS_PI window budget -- the stream's bytes in flight scale with the waves)
-#ifndef ESGPU_HIST_WAVES  // histogram-only grids with a metric over compact timestamps (VK bit 128): waves per SIMD
+#ifndef ESGPU_HIST_WAVES  // raw-load histogram-only grids (VK bit 1024): waves per SIMD
 #define ESGPU_HIST_WAVES 4
 #endif
 template <bool ORD, int VK, int WGS> constexpr int collect_min_waves() {
-    return (VK & 64) && WGS == 512 ? ESGPU_PI_WAVES : !ORD && (VK & 128) && WGS == 512 ? ESGPU_HIST_WAVES : 4;
+    return (VK & 64) && WGS == 512 ? ESGPU_PI_WAVES : !ORD && (VK & 1024) && WGS == 512 ? ESGPU_HIST_WAVES : 4;
 }
 template <bool ORD, int HK, int MET, int VK, int WGS>
 __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, VK, WGS>())) void collect_kernel(CollectParams P) {
@@ -1239,11 +1266,18 @@ static auto with_vk0(bool hv_f64, bool mv_f64, F f) {
 // Bits 16 / 32 (compact ordinal / histogram columns): terms dimensions without a derived key index, affine histograms
 // over a long column.
 template <bool ORD, int HK, int MET, class F>
-static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, bool pi, bool m32, bool m16, bool acc, F f) {
+static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, bool pi, bool m32, bool m16, bool acc, bool raw,
+                    F f) {
     // VK bit 128, a compact long metric (u32 deltas, values restored in the loader): histogram-only grids over compact
     // timestamps (date_histogram{stats / extended_stats / avg}) and extended_stats under terms over compact columns
     if constexpr (MET > 0 && !ORD && HK == 1) {
-        if (m32 && !pi && !mv_f64 && t32 && !hv_f64) return f(std::integral_constant<int, 32 | 128>{});
+        if (m32 && !pi && !mv_f64 && t32 && !hv_f64) {
+            if (raw) return f(std::integral_constant<int, 32 | 128 | 1024>{});
+            return f(std::integral_constant<int, 32 | 128>{});
+        }
+    }
+    if constexpr (MET == 0 && !ORD && HK == 1) {
+        if (raw && t32 && !hv_f64) return f(std::integral_constant<int, 32 | 1024>{});
     }
     if constexpr (MET == 3 && ORD && (HK == 0 || HK == 1)) {
         if (m32 && !pi && !mv_f64 && !dord && c16) {
@@ -1308,7 +1342,7 @@ template <bool ORD, int HK, int MET>
 static void launch_t(const CollectParams& p, bool wide, uint32_t grid, size_t lds, hipStream_t st) {
     with_vk<ORD, HK, MET>(p.hv_f64 != 0, p.mv_f64 != 0, p.ord_src != nullptr, p.ord16 != nullptr, p.hv32 != nullptr,
                           p.mv32 != nullptr && p.pk_shift != 0, p.mv32 != nullptr && p.pk_shift == 0, p.mv16 != nullptr,
-                          p.accept != nullptr, [&](auto vk) {
+                          p.accept != nullptr, p.raw_dense != 0, [&](auto vk) {
         return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
             hipLaunchKernelGGL((collect_kernel<ORD, HK, MET, decltype(vk)::value, decltype(wg)::value>), dim3(grid),
                                dim3(decltype(wg)::value), lds, st, p);
@@ -1331,7 +1365,7 @@ template <bool ORD, int HK, int MET>
 static int occ_t(size_t lds, int vkbits, bool wide) {
     return with_vk<ORD, HK, MET>((vkbits & 1) != 0, (vkbits & 2) != 0, (vkbits & 8) != 0, (vkbits & 16) != 0,
                                  (vkbits & 32) != 0, (vkbits & 64) != 0, (vkbits & 128) != 0, (vkbits & 256) != 0,
-                                 (vkbits & 512) != 0, [&](auto vk) {
+                                 (vkbits & 512) != 0, (vkbits & 1024) != 0, [&](auto vk) {
         return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
             int n = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(

@@ -1608,6 +1608,7 @@ static bool compact_cols(const esgpu_ctx* c);
 static bool dyn_claim_on();
 static bool replay_compaction();
 static bool d16_on();
+static bool raw_hist_on();
 static bool pi_cells(const esgpu_ctx* c);
 static uint32_t pi_copies();
 static const uint16_t* ensure_ord16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
@@ -2967,9 +2968,12 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     const int hk = L_HIST ? (P.hord ? 3 : P.kstart ? 2 : 1) : 0;
     // packed cells under a filter: the clauses (and live docs) folded into one accept bitset before the collect
     const bool fold = pi && (P.npred > 0 || P.accept);
+    // histogram-only grids over dense compact timestamps (and a dense compact metric), no filter: raw-load kernels
+    P.raw_dense = !L_ORD && hk_launch == 1 && P.hv32 && !P.hv_f64 && !P.hv_present && !P.accept && P.npred == 0 &&
+                  (L_met == 0 || (m32 && !P.mv_present)) && raw_hist_on() ? 1 : 0;
     const int vk = (P.hv_f64 ? 1 : 0) | (P.mv_f64 ? 2 : 0) | (P.ord_src ? 8 : 0) | (P.ord16 ? 16 : 0) | (P.hv32 ? 32 : 0) |
-                   (pi ? 64 : 0) | (m32 ? 128 : 0) | (P.mv16 ? 256 : 0) | (fold ? 512 : 0);
-    const uint64_t occ_key = ((uint64_t)lds << 18) | ((uint64_t)wide << 17) | ((uint64_t)vk << 8) | ((uint64_t)L_met << 4) |
+                   (pi ? 64 : 0) | (m32 ? 128 : 0) | (P.mv16 ? 256 : 0) | (fold ? 512 : 0) | (P.raw_dense ? 1024 : 0);
+    const uint64_t occ_key = ((uint64_t)lds << 21) | ((uint64_t)wide << 20) | ((uint64_t)vk << 8) | ((uint64_t)L_met << 4) |
                              ((uint64_t)hk << 1) | (L_ORD ? 1 : 0);
     if (pl.occ_key != occ_key) {
         pl.occ = std::max(1, collect_occupancy(L_ORD, hk, L_met, lds, vk, wide));
@@ -3034,6 +3038,11 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     return ret;
 }
 
+// raw-load histogram-only kernels (VK bit 1024; ESGPU_RAW_HIST=0: the converting loader, for A/B runs)
+static bool raw_hist_on() {
+    static const bool on = [] { const char* e = std::getenv("ESGPU_RAW_HIST"); return !(e && *e == '0'); }();
+    return on;
+}
 // 16-bit deltas of long columns spanning < 2^16 (the packed cells' metric, range predicates); ESGPU_D16=0: the 32-bit
 // deltas instead (A/B runs)
 static bool d16_on() {

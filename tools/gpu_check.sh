@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun session: GPU parity tests, kernel sweep, bench, rocprofv3 kernel-trace stats and PMC HBM-traffic passes.
 #   gpurun --timeout 1200 -- bash tools/gpu_check.sh <tag> [steps...]
-# steps: tests testsdyn testfile testfiles piab fsab d16ab pmcall kbench bench jitter export shape125 configs dynab hllab cut0ab buildtrace profk125 prof profk pmc pmck variants (default: tests kbench bench prof pmc)
+# steps: tests testsdyn testfile testfiles piab fsab d16ab rawab pmcall kbench bench jitter export shape125 configs dynab hllab cut0ab buildtrace profk125 prof profk pmc pmck variants (default: tests kbench bench prof pmc)
 # KBENCH_ONLY=name,name restricts the kbench sweeps (KBENCH_ARGS: extra kbench flags for variants, KBENCH_TAG: log suffix); variants = every build/variants/libesgpu_*.so via ESGPU_LIBRARY.  Every GPU step has its own time limit; the first failure ends it.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -66,6 +66,11 @@ for s in $STEPS; do
               for d in 1 0; do
                   ESGPU_D16=$d run "kbench_d16_$d" 400 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 \
                       --only ${KBENCH_ONLY:-north_star,ns_avg,config5,config1_terms_stats} || exit 1
+              done ;;
+        rawab) # histogram-only raw-load kernels (VK bit 1024) vs the converting loader (ESGPU_RAW_HIST=0), same box
+              for r in 1 0; do
+                  ESGPU_RAW_HIST=$r run "kbench_raw_$r" 400 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 \
+                      --only ${KBENCH_ONLY:-date_hist,config2_dh_ext} || exit 1
               done ;;
         cut0ab) # HLL phase 0 length (ESGPU_HLL_CUT0 x 2^p values through the partitioned phase 0)
               for c in 4 16 64; do for docs in 125000000 1000000000; do
