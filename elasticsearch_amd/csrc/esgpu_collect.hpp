@@ -42,7 +42,7 @@ constexpr uint32_t kGroup = kGroupBlocks;  // blocks per multi-pass group (esgpu
 struct Doc4 {
     // raw-loaded packed-cell kernels (kRawPI): the loads' words as they arrive, unpacked only when the docs are processed
     // (a conversion right after the load would wait for it there, a full memory latency per buffer reload)
-    uint32_t raw[8];
+    uint32_t raw[10];
     uint64_t racc;
     uint32_t doc0;
     uint32_t ord[kVec];
@@ -145,10 +145,10 @@ __device__ __forceinline__ uint32_t eval_pred(const PredDev& q, uint32_t doc0) {
 // timestamp column): loads only, no use of a loaded word until unpack_docs
 template <int MET, int VK, bool HIST>
 constexpr bool kRawPI = MET > 0 && (VK & 64) != 0 && (VK & 16) != 0 && (VK & 256) != 0 && (!HIST || (VK & 32) != 0);
-// VK bit 1024: histogram-only grids over dense compact timestamps (and a dense compact long metric), no filter -- the
-// same raw loads (the timestamps' and the metric's u32 deltas), unpacked when processed
+// VK bit 1024: grids over dense compact columns without a filter -- 16-bit ordinals (counting terms grids), timestamp
+// deltas, a histogram-only grid's u32 metric deltas -- the same raw loads, unpacked when processed
 template <bool ORD, int MET, int VK>
-constexpr bool kRawH = !ORD && (VK & 1024) != 0;
+constexpr bool kRawH = (VK & 1024) != 0;
 
 template <bool ORD, bool HIST, int MET, int VK>
 __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0, Doc4& d) {
@@ -166,11 +166,17 @@ __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0,
         return;
     }
     if constexpr (kRawH<ORD, MET, VK>) {
-        const u32x4_t t = load16(P.hv32 + doc0);
-        d.raw[2] = t.x; d.raw[3] = t.y; d.raw[4] = t.z; d.raw[5] = t.w;
+        if constexpr (ORD) {
+            const u32x2_t o = load8(P.ord16 + doc0);
+            d.raw[0] = o.x; d.raw[1] = o.y;
+        }
+        if constexpr (HIST) {
+            const u32x4_t t = load16(P.hv32 + doc0);
+            d.raw[2] = t.x; d.raw[3] = t.y; d.raw[4] = t.z; d.raw[5] = t.w;
+        }
         if constexpr (MET > 0) {
             const u32x4_t m = load16(P.mv32 + doc0);
-            d.raw[0] = m.x; d.raw[1] = m.y; d.raw[6] = m.z; d.raw[7] = m.w;
+            d.raw[6] = m.x; d.raw[7] = m.y; d.raw[8] = m.z; d.raw[9] = m.w;
         }
         d.doc0 = doc0;
         return;
@@ -614,13 +620,19 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
         du = d_in;
         const uint32_t doc0 = du.doc0;
         du.ok = doc0 + 4 <= P.n_docs ? 0xFu : doc0 >= P.n_docs ? 0u : ((1u << (P.n_docs - doc0)) - 1u);
+        if constexpr (ORD) {
+            const uint32_t x[4] = {du.raw[0] & 0xFFFFu, du.raw[0] >> 16, du.raw[1] & 0xFFFFu, du.raw[1] >> 16};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) du.hv[j] = P.hv_base + (int64_t)du.raw[2 + j];
-        du.hpres = 0xFu;
+            for (int j = 0; j < 4; ++j) du.ord[j] = x[j] == 0xFFFFu ? kMissingOrd : x[j];
+        }
+        if constexpr (HIST) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) du.hv[j] = P.hv_base + (int64_t)du.raw[2 + j];
+            du.hpres = 0xFu;
+        }
         if constexpr (MET > 0) {
-            const uint32_t t[4] = {du.raw[0], du.raw[1], du.raw[6], du.raw[7]};
 #pragma unroll
-            for (int j = 0; j < 4; ++j) du.mv[j] = (double)(P.mv_base + (int64_t)t[j]);  // FieldData.castToDouble of the long
+            for (int j = 0; j < 4; ++j) du.mv[j] = (double)(P.mv_base + (int64_t)du.raw[6 + j]);  // FieldData.castToDouble of the long
             du.mpres = 0xFu;
         }
     }
@@ -1278,6 +1290,15 @@ static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, boo
     }
     if constexpr (MET == 0 && !ORD && HK == 1) {
         if (raw && t32 && !hv_f64) return f(std::integral_constant<int, 32 | 1024>{});
+    }
+    if constexpr (MET == 0 && ORD && (HK == 0 || HK == 1)) {  // counting terms grids over 16-bit ordinals
+        if (raw && c16 && !dord) {
+            if constexpr (HK == 1) {
+                if (t32 && !hv_f64) return f(std::integral_constant<int, 48 | 1024>{});
+            } else {
+                return f(std::integral_constant<int, 16 | 1024>{});
+            }
+        }
     }
     if constexpr (MET == 3 && ORD && (HK == 0 || HK == 1)) {
         if (m32 && !pi && !mv_f64 && !dord && c16) {

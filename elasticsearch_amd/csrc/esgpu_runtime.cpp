@@ -2968,9 +2968,12 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     const int hk = L_HIST ? (P.hord ? 3 : P.kstart ? 2 : 1) : 0;
     // packed cells under a filter: the clauses (and live docs) folded into one accept bitset before the collect
     const bool fold = pi && (P.npred > 0 || P.accept);
-    // histogram-only grids over dense compact timestamps (and a dense compact metric), no filter: raw-load kernels
-    P.raw_dense = !L_ORD && hk_launch == 1 && P.hv32 && !P.hv_f64 && !P.hv_present && !P.accept && P.npred == 0 &&
-                  (L_met == 0 || (m32 && !P.mv_present)) && raw_hist_on() ? 1 : 0;
+    // grids over dense compact columns without a filter -- histogram-only over the timestamp deltas (and a dense compact
+    // metric), counting terms grids over 16-bit ordinals (and the timestamp deltas): raw-load kernels (VK bit 1024)
+    const bool raw_hist = hk_launch == 1 && P.hv32 && !P.hv_f64 && !P.hv_present;
+    P.raw_dense = raw_hist_on() && !pi && !P.accept && P.npred == 0 &&
+                  ((!L_ORD && raw_hist && (L_met == 0 || (m32 && !P.mv_present))) ||
+                   (L_ORD && L_met == 0 && P.ord16 && !P.ord_src && (hk_launch == 0 || raw_hist))) ? 1 : 0;
     const int vk = (P.hv_f64 ? 1 : 0) | (P.mv_f64 ? 2 : 0) | (P.ord_src ? 8 : 0) | (P.ord16 ? 16 : 0) | (P.hv32 ? 32 : 0) |
                    (pi ? 64 : 0) | (m32 ? 128 : 0) | (P.mv16 ? 256 : 0) | (fold ? 512 : 0) | (P.raw_dense ? 1024 : 0);
     const uint64_t occ_key = ((uint64_t)lds << 21) | ((uint64_t)wide << 20) | ((uint64_t)vk << 8) | ((uint64_t)L_met << 4) |
