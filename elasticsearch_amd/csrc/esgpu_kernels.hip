@@ -446,11 +446,11 @@ __global__ __launch_bounds__(kHllLdsWG) void hll_registers_lds_kernel(HllParams 
 // are many): a register that will hold at least F is decided only by hashes with run length >= F, i.e. those whose F - 1
 // bits below the index bits are zero -- one 64-bit AND per hash.  Those (a fraction 2^-(F-1)) are logged in LDS and
 // flushed, partitioned by register range, into fs_buf for one gather (hll_p0_gather_kernel); the host picks F so that
-// a register ending below F is a ~1e-3 event per request, and the tail pass (hll_lc_kernel) finishes such registers
+// a register ending below F is a ~5e-3 event per request, and the tail pass (hll_lc_kernel) finishes such registers
 // from the hashes below F.  No snapshot, no phase structure: the pass streams the column at the HBM rate.
 constexpr uint32_t kHllFsWG = 1024;
 constexpr uint32_t kHllFsIter = kHllFsWG * 4;
-constexpr uint32_t kHllFsLog = 16384;  // LDS log entries; flushed once it is half full (checked every ~kHllFsLog / 4 entries)
+constexpr uint32_t kHllFsLog = 16384;  // LDS log entries; flushed every ~kHllFsLog / 2 expected entries (a fixed schedule)
 constexpr uint32_t hll_fs_lds_bytes() { return kHllFsLog * 4u + 3u * 256u * 4u + 16u; }
 
 // one workgroup's log out, partitioned by register range (as the LDS phase kernel's end does); the callers barrier
@@ -523,10 +523,8 @@ __global__ __launch_bounds__(kHllFsWG) void hll_fs_kernel(HllParams P, uint32_t 
         load(base + 3 * kHllFsIter + t4, b);
         if (++it == check_iters) {  // workgroup-uniform: every thread runs the same iterations
             it = 0;
-            __syncthreads();
-            const uint32_t n = *nlog;
-            __syncthreads();
-            if (n > kHllFsLog / 2) hll_fs_flush(P, rlog, lcnt, lcur, lbase, nlog);
+            __syncthreads();  // the log is complete; flushed on a fixed schedule (no count check, no extra barrier)
+            hll_fs_flush(P, rlog, lcnt, lcur, lbase, nlog);
         }
     }
     __syncthreads();
@@ -722,7 +720,7 @@ __global__ __launch_bounds__(1024) void hll_nonzero_kernel(const unsigned int* r
 // probes bounded by threshold+1 (a longer run proves > threshold distinct values), stops once the count passes
 // the threshold.  Final mode = LC iff count <= threshold, exactly as Hashset.add/upgradeToHll decide.
 // With the floored stream the same launch is its tail pass: while the gather left registers below the floor F
-// (*unres, a ~1e-3 event), every hash with run length < F raises its register if it is still below -- registers at or
+// (*unres, a ~5e-3 event), every hash with run length < F raises its register if it is still below -- registers at or
 // above F are exact already and are only read.
 __global__ __launch_bounds__(256) void hll_lc_kernel(HllParams P) {
     const bool fix = P.fs_f && *P.unres != 0;
@@ -774,7 +772,7 @@ __global__ __launch_bounds__(256) void hll_lc_kernel(HllParams P) {
 
 uint32_t hll_fs_floor(uint64_t total, int p, uint32_t min_f) {
     const double m = (double)(1u << p);
-    const double lam = (double)total / m, need = std::log(m) + 6.9;  // m * exp(-lam * 2^-(F-1)) <= 1e-3
+    const double lam = (double)total / m, need = std::log(m) + 5.3;  // m * exp(-lam * 2^-(F-1)) <= 5e-3
     if (lam < need * 2.0) return 0;
     const uint32_t f = 1u + (uint32_t)std::floor(std::log2(lam / need));
     const uint32_t fmax = 64u - (uint32_t)p;  // run lengths top out at 64 - p + 1
@@ -838,8 +836,8 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
         hipLaunchKernelGGL(hll_lc_kernel, dim3(grid), dim3(256), 0, st, t);
     };
     if (p.fs_f && lds && p.p0_cnt && p.p >= 12 && n > 0) {
-        // floored stream: one resident wave of workgroups, contiguous ranges; the log is checked every ~kHllFsLog / 4
-        // expected entries (2^(F-1) docs per entry)
+        // floored stream: one resident wave of workgroups, contiguous ranges; the log is flushed every ~kHllFsLog / 2
+        // expected entries (2^(F-1) docs per entry; the count per period is binomial, far below the other half)
         static int per_cu = 0;
         if (!per_cu) {
             int b = 0;
@@ -850,7 +848,7 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
         uint32_t wgs = std::max(1u, std::min(cus * (uint32_t)per_cu, n / (kHllFsIter * 2)));
         const uint32_t per = ((n + wgs - 1) / wgs + 3) & ~3u;
         wgs = (n + per - 1) / per;
-        const uint64_t docs_per_check = ((uint64_t)kHllFsLog / 4) << (p.fs_f - 1);
+        const uint64_t docs_per_check = ((uint64_t)kHllFsLog / 2) << (p.fs_f - 1);
         const uint32_t check = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, docs_per_check / (2 * kHllFsIter)));
         if (p.kind == HLL_I64)
             hipLaunchKernelGGL(hll_fs_kernel<HLL_I64>, dim3(wgs), dim3(kHllFsWG), hll_fs_lds_bytes(), st, p, per, check);

@@ -180,7 +180,7 @@ struct HllParams {
 };
 // floored stream: the floor F (kept hashes have run length >= F, a fraction 2^-(F-1) of the stream) for a request whose
 // registers will have seen `total` values when this segment is done: the largest F for which the expected number of
-// registers ending below F, m * exp(-(total / m) * 2^-(F-1)), stays under 1e-3 (then a tail pass finishes them).
+// registers ending below F, m * exp(-(total / m) * 2^-(F-1)), stays under 5e-3 (then a tail pass finishes them).
 // 0 = too few values per register for a floor worth a pass (the phases instead).
 uint32_t hll_fs_floor(uint64_t total, int p, uint32_t min_f);
 uint32_t hll_fs_cap(uint64_t n, int p, uint32_t f);  // entries per register range for n values at floor f

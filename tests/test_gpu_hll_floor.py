@@ -58,7 +58,7 @@ def c4_125m():
 
 @pytest.mark.parametrize("mode", MODES)
 def test_config4_fresh_125m_plan(engine, c4_125m, mode):
-    """The 8-GPU per-GPU shape: one fresh plan over one 125M-doc shard (p = 18, ~81M distinct values: F = 4)."""
+    """The 8-GPU per-GPU shape: one fresh plan over one 125M-doc shard (p = 18, ~81M distinct values: F = 5)."""
     n, aggs, want = c4_125m
     seg = engine.synthetic_segment(n, fields=("client_ip.hash",), shard=5)
     for k, res in enumerate(_twice(engine, aggs, [seg], mode)):
@@ -96,7 +96,7 @@ def test_merged_shards_continue_the_floor(engine, mode):
 @pytest.mark.parametrize("field,thr", [("client_ip.hash", 1000), ("price", 1000), ("price", 40000)])
 def test_smaller_precision_and_double_values(engine, mode, field, thr):
     """p = 13 (128 register ranges of 64 instead of 256) and a double column (doubleToLongBits, NaN canonicalised) over
-    8M docs (F = 6: the stream takes segments of up to 1,024 values per register); at p = 18 the double column has too
+    8M docs (F = 7: the stream takes segments of up to 1,024 values per register); at p = 18 the double column has too
     few values per register for a floor (the phases run in every mode)."""
     n = 8_000_000
     aggs = [AB.cardinality("c").field(field).precisionThreshold(thr)]
