@@ -422,11 +422,14 @@ def main():
             with open(args.traffic) as f:
                 tr = json.load(f)
             # entries keyed by (workload, docs per shard, shards): tools/pmc_traffic.py --merge; the entry must have been
-            # measured on the layout this run reads (same algorithmic bytes per launch)
+            # measured on the layout this run reads (the same algorithmic bytes per launch within 0.1 %: config 3's
+            # postings bytes differ a little from shard to shard), scaled to this run's bytes
+            alg = kernel_bytes[0] // launches
             for e in tr.get("entries", [tr]):
+                ea_bytes = e.get("algorithmic_bytes_per_launch") or 0
                 if (e.get("workload") == args.workload and e.get("docs") == args.docs and e.get("shards", 1) == shards and
-                        e.get("algorithmic_bytes_per_launch") == kernel_bytes[0] // launches):
-                    traffic = e.get("hbm_bytes_per_launch")
+                        ea_bytes and abs(ea_bytes - alg) <= ea_bytes // 1000):
+                    traffic = int(e.get("hbm_bytes_per_launch") * alg / ea_bytes)
         except Exception:
             traffic = None
 
