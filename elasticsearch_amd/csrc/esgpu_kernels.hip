@@ -450,10 +450,10 @@ __global__ __launch_bounds__(kHllLdsWG) void hll_registers_lds_kernel(HllParams 
 // from the hashes below F.  No snapshot, no phase structure: the pass streams the column at the HBM rate.
 constexpr uint32_t kHllFsWG = 1024;
 constexpr uint32_t kHllFsIter = kHllFsWG * 4;
-// LDS log entries (two 1024-thread workgroups per CU with 79 KB each); flushed every ~0.85 x kHllFsLog expected entries (a
-// fixed schedule: the count per period is binomial, ~5 sigma below the capacity) -- at 125M docs and F = 5 a workgroup's
-// whole range fits, so the log goes out once, at the end
-constexpr uint32_t kHllFsLog = 19456;
+// LDS log entries (two 1024-thread workgroups per CU with 75 KB each; 79 KB measured slower, 16,384 entries flush once
+// mid-range at 125M docs); flushed every ~0.85 x kHllFsLog expected entries (a fixed schedule: the count per period is
+// binomial, ~5 sigma below the capacity) -- at 125M docs and F = 5 a workgroup's whole range fits: one flush, at the end
+constexpr uint32_t kHllFsLog = 18432;
 constexpr uint32_t hll_fs_lds_bytes() { return kHllFsLog * 4u + 3u * 256u * 4u + 16u; }
 
 // one workgroup's log out, partitioned by register range (as the LDS phase kernel's end does); the callers barrier
@@ -991,11 +991,11 @@ __global__ __launch_bounds__(256) void compact_rows_kernel(CompactParams P) {
         for (uint32_t w = 0; w < wave; ++w) at += wsum[w];
         pos += wsum[0] + wsum[1] + wsum[2] + wsum[3];
         if (c == 0ull) continue;
-        P.o_key[at] = P.affine ? (long long)((P.key0 + (int64_t)s) * P.interval + P.offset) : (long long)s;
-        P.o_count[at] = (long long)c;
+        P.o_slot[at] = s;
+        P.o_count[at] = (uint32_t)c;
         for (int l = 0; l < P.nleaves; ++l) {
             const CompactLeaf& L = P.leaf[l];
-            const unsigned long long vc = L.cnt[cell];
+            const unsigned long long vc = L.o_count ? L.cnt[cell] : c;
             double sum = 0.0, mn = __builtin_inf(), mx = -__builtin_inf(), sq = 0.0;
             if (vc) {
                 sum = L.sum[cell];
@@ -1006,11 +1006,13 @@ __global__ __launch_bounds__(256) void compact_rows_kernel(CompactParams P) {
                 }
                 if (L.sq) sq = L.sq[cell];
             }
-            L.o_count[at] = (long long)vc;
+            if (L.o_count) L.o_count[at] = (uint32_t)vc;
             L.o_sum[at] = sum;
-            L.o_min[at] = mn;
-            L.o_max[at] = mx;
-            L.o_sq[at] = sq;
+            if (L.o_min) {
+                L.o_min[at] = mn;
+                L.o_max[at] = mx;
+            }
+            if (L.o_sq) L.o_sq[at] = sq;
         }
     }
 }

@@ -212,7 +212,9 @@ struct CompactLeaf {
     const unsigned long long* mn;    // order-preserving encodings; null: no min / max (avg)
     const unsigned long long* mx;
     const double* sq;                // null: no sum of squares (avg, stats)
-    long long* o_count;              // [cap] outputs (pinned, device-mapped)
+    // [cap] outputs (pinned, device-mapped); o_count null: the leaf counts every doc of its bucket (the host copies the
+    // bucket counts), o_min / o_max / o_sq null: not collected (the host fills the empty-leaf values)
+    uint32_t* o_count;
     double *o_sum, *o_min, *o_max, *o_sq;
 };
 constexpr int kCompactLeaves = 4;
@@ -220,12 +222,10 @@ struct CompactParams {
     const uint32_t* rows;            // [k] winners' ordinals
     uint32_t k, H, T;
     const unsigned long long* cnt;   // bucket doc counts [H][T]
-    int32_t affine;                  // 1: key = (key0 + slot) * interval + offset; 0: o_key receives the slot
-    int64_t key0, interval, offset;
     uint32_t* nnz;                   // [k] non-empty slots per row (device scratch)
     uint32_t* o_nnz;                 // [k] the same, pinned
-    long long* o_key;                // [cap] bucket keys (or slots)
-    long long* o_count;              // [cap] bucket doc counts
+    uint32_t* o_slot;                // [cap] bucket key slots (the host maps them to keys)
+    uint32_t* o_count;               // [cap] bucket doc counts (a shard's max_doc < 2^31)
     int32_t nleaves;
     CompactLeaf leaf[kCompactLeaves];
 };

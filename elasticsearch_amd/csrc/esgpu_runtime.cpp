@@ -4424,6 +4424,7 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
     std::vector<char> fast(g.kids.size(), 0), need_rows(p->pipes.size(), 0);
     need_rows[g.pipes[0]] = gpu_topk;  // term orders read the winners' counts from P0's rows
     p->h_compact.resize(g.kids.size());
+    std::vector<std::vector<CompactLeaf>> leaf_of(g.kids.size());  // what each compacted child's transfer holds
     for (size_t ki = 0; ki < g.kids.size(); ++ki) {
         const ChildSrc& kid = g.kids[ki];
         if (kid.filter) { for (int pi : kid.pipes) need_rows[pi] = 1; continue; }
@@ -4459,12 +4460,12 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
         C.rows = drows;
         C.k = k; C.H = B0.H; C.T = B0.T;
         C.cnt = B0.g_cnt.as<unsigned long long>();
-        C.affine = B0.ktable ? 0 : 1;
-        C.key0 = B0.key0; C.interval = B0.interval; C.offset = B0.offset;
         C.nnz = (uint32_t*)p->s_nnz.ensure(p->ctx, (size_t)k * 4);
         C.o_nnz = (uint32_t*)dbase;
-        C.o_key = (long long*)dev_at(0);
-        C.o_count = (long long*)dev_at(1);
+        // the narrowest transfer the host can expand: u32 slots (keys computed on the host) and counts, leaf counts only
+        // where a leaf's value count differs from its bucket's doc count, extrema and sums of squares only where collected
+        C.o_slot = (uint32_t*)dev_at(0);
+        C.o_count = (uint32_t*)dev_at(1);
         C.nleaves = (int32_t)nl;
         for (size_t gj = 0; gj < nl; ++gj) {
             const Pipeline& L = p->pipes[kid.grand[gj].pipe];
@@ -4475,12 +4476,13 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
             o.mn = L.met >= 2 && type != ESGPU_AGG_AVG ? L.g_min.as<unsigned long long>() : nullptr;
             o.mx = o.mn ? L.g_max.as<unsigned long long>() : nullptr;
             o.sq = L.met >= 3 && type == ESGPU_AGG_EXTENDED_STATS ? L.g_sq.as<double>() : nullptr;
-            o.o_count = (long long*)dev_at(2 + 5 * gj);
+            o.o_count = o.cnt == C.cnt ? nullptr : (uint32_t*)dev_at(2 + 5 * gj);
             o.o_sum = (double*)dev_at(3 + 5 * gj);
-            o.o_min = (double*)dev_at(4 + 5 * gj);
-            o.o_max = (double*)dev_at(5 + 5 * gj);
-            o.o_sq = (double*)dev_at(6 + 5 * gj);
+            o.o_min = o.mn ? (double*)dev_at(4 + 5 * gj) : nullptr;
+            o.o_max = o.mn ? (double*)dev_at(5 + 5 * gj) : nullptr;
+            o.o_sq = o.sq ? (double*)dev_at(6 + 5 * gj) : nullptr;
         }
+        leaf_of[ki].assign(C.leaf, C.leaf + nl);
         launch_compact_rows(C, st);
         HIPX(hipGetLastError());
         (void)base;
@@ -4578,27 +4580,51 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
             total += nnz[i];
             sub.boff.push_back(sub.boff.back() + nnz[i]);
         }
-        const int64_t* keys = (const int64_t*)host_at(0);
+        const uint32_t* slots = (const uint32_t*)host_at(0);
+        const size_t n0 = sub.key.size();
+        sub.key.resize(n0 + total);
+        int64_t* kd = sub.key.data() + n0;
         if (B0.ktable) {  // slots: the bucket-start table's keys
-            const size_t n0 = sub.key.size();
-            sub.key.resize(n0 + total);
-            for (size_t q = 0; q < total; ++q) sub.key[n0 + q] = key_value(B0, (uint32_t)keys[q]);
+            for (size_t q = 0; q < total; ++q) kd[q] = B0.kt_key[slots[q]];
         } else {
-            sub.key.insert(sub.key.end(), keys, keys + total);
+            const int64_t k0 = B0.key0, iv = B0.interval, off = B0.offset;
+            for (size_t q = 0; q < total; ++q) kd[q] = (k0 + (int64_t)slots[q]) * iv + off;
         }
-        const int64_t* cnts = (const int64_t*)host_at(1);
-        sub.bcount.insert(sub.bcount.end(), cnts, cnts + total);
+        const uint32_t* cnts = (const uint32_t*)host_at(1);
+        const size_t c0 = sub.bcount.size();
+        sub.bcount.resize(c0 + total);
+        int64_t* cd = sub.bcount.data() + c0;
+        for (size_t q = 0; q < total; ++q) cd[q] = (int64_t)cnts[q];
         sub.berr.insert(sub.berr.end(), total, 0);
         sub.term_off.insert(sub.term_off.end(), total, sub.term_pool.size());
         for (size_t gj = 0; gj < nl; ++gj) {
             Block& gb = sub.subs[gj];
+            const CompactLeaf& o = leaf_of[ki][gj];
             gb.n += total;
-            const int64_t* c = (const int64_t*)host_at(2 + 5 * gj);
-            gb.count.insert(gb.count.end(), c, c + total);
-            std::vector<double>* dst[4] = {&gb.sum, &gb.min, &gb.max, &gb.sumsq};
-            for (int a = 0; a < 4; ++a) {
-                const double* v = (const double*)host_at(3 + a + 5 * gj);
-                dst[a]->insert(dst[a]->end(), v, v + total);
+            if (o.o_count) {
+                const uint32_t* c = (const uint32_t*)host_at(2 + 5 * gj);
+                const size_t g0 = gb.count.size();
+                gb.count.resize(g0 + total);
+                for (size_t q = 0; q < total; ++q) gb.count[g0 + q] = (int64_t)c[q];
+            } else {
+                gb.count.insert(gb.count.end(), cd, cd + total);
+            }
+            const double* sm = (const double*)host_at(3 + 5 * gj);
+            gb.sum.insert(gb.sum.end(), sm, sm + total);
+            if (o.o_min) {
+                const double* mn = (const double*)host_at(4 + 5 * gj);
+                const double* mx = (const double*)host_at(5 + 5 * gj);
+                gb.min.insert(gb.min.end(), mn, mn + total);
+                gb.max.insert(gb.max.end(), mx, mx + total);
+            } else {  // not collected (avg): the empty leaf's values
+                gb.min.insert(gb.min.end(), total, __builtin_inf());
+                gb.max.insert(gb.max.end(), total, -__builtin_inf());
+            }
+            if (o.o_sq) {
+                const double* sq = (const double*)host_at(6 + 5 * gj);
+                gb.sumsq.insert(gb.sumsq.end(), sq, sq + total);
+            } else {
+                gb.sumsq.insert(gb.sumsq.end(), total, 0.0);
             }
         }
     }
