@@ -450,10 +450,9 @@ __global__ __launch_bounds__(kHllLdsWG) void hll_registers_lds_kernel(HllParams 
 // from the hashes below F.  No snapshot, no phase structure: the pass streams the column at the HBM rate.
 constexpr uint32_t kHllFsWG = 1024;
 constexpr uint32_t kHllFsIter = kHllFsWG * 4;
-// LDS log entries (two 1024-thread workgroups per CU with 75 KB each; 79 KB measured slower, 16,384 entries flush once
-// mid-range at 125M docs); flushed every ~0.85 x kHllFsLog expected entries (a fixed schedule: the count per period is
-// binomial, ~5 sigma below the capacity) -- at 125M docs and F = 5 a workgroup's whole range fits: one flush, at the end
-constexpr uint32_t kHllFsLog = 18432;
+// LDS log entries; the count is checked every ~kHllFsLog / 4 expected entries and the log flushed once it is over half
+// full (measured at 125M docs: 0.231 ms; a fixed flush schedule with 18,432 / 19,456 entries 0.248 / 0.240 ms)
+constexpr uint32_t kHllFsLog = 16384;
 constexpr uint32_t hll_fs_lds_bytes() { return kHllFsLog * 4u + 3u * 256u * 4u + 16u; }
 
 // one workgroup's log out, partitioned by register range (as the LDS phase kernel's end does); the callers barrier
@@ -526,8 +525,10 @@ __global__ __launch_bounds__(kHllFsWG) void hll_fs_kernel(HllParams P, uint32_t 
         load(base + 3 * kHllFsIter + t4, b);
         if (++it == check_iters) {  // workgroup-uniform: every thread runs the same iterations
             it = 0;
-            __syncthreads();  // the log is complete; flushed on a fixed schedule (no count check, no extra barrier)
-            hll_fs_flush(P, rlog, lcnt, lcur, lbase, nlog);
+            __syncthreads();
+            const uint32_t n = *nlog;
+            __syncthreads();
+            if (n > kHllFsLog / 2) hll_fs_flush(P, rlog, lcnt, lcur, lbase, nlog);
         }
     }
     __syncthreads();
@@ -839,7 +840,7 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
         hipLaunchKernelGGL(hll_lc_kernel, dim3(grid), dim3(256), 0, st, t);
     };
     if (p.fs_f && lds && p.p0_cnt && p.p >= 12 && n > 0) {
-        // floored stream: one resident wave of workgroups, contiguous ranges; the log is flushed every ~0.85 kHllFsLog
+        // floored stream: one resident wave of workgroups, contiguous ranges; the log is checked every ~kHllFsLog / 4
         // expected entries (2^(F-1) docs per entry)
         static int per_cu = 0;
         if (!per_cu) {
@@ -851,7 +852,7 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
         uint32_t wgs = std::max(1u, std::min(cus * (uint32_t)per_cu, n / (kHllFsIter * 2)));
         const uint32_t per = ((n + wgs - 1) / wgs + 3) & ~3u;
         wgs = (n + per - 1) / per;
-        const uint64_t docs_per_check = ((uint64_t)kHllFsLog * 85 / 100) << (p.fs_f - 1);
+        const uint64_t docs_per_check = ((uint64_t)kHllFsLog / 4) << (p.fs_f - 1);
         const uint32_t check = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, docs_per_check / (2 * kHllFsIter)));
         if (p.kind == HLL_I64)
             hipLaunchKernelGGL(hll_fs_kernel<HLL_I64>, dim3(wgs), dim3(kHllFsWG), hll_fs_lds_bytes(), st, p, per, check);

@@ -4628,6 +4628,7 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
             }
         }
     }
+    bmark(p, "kids_appended");
     for (const ChildSrc& kid : g.kids) {  // every pipeline of a bucket child shares its key grid
         if (!kid.bucket) continue;
         const Pipeline& B0 = p->pipes[kid.pipes[0]];
@@ -4653,6 +4654,7 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
             reserve_leaves(r.subs[ki], nb);
         }
     }
+    bmark(p, "reserved");
     std::vector<uint32_t> slots, cells;
     std::vector<int64_t> counts;
     begin_instance(r, other);
@@ -4942,8 +4944,6 @@ extern "C" int esgpu_plan_build(esgpu_plan* p, esgpu_result** out) {
         bmark(p, "posted");
         HIPX(hipSetDevice(p->ctx->device));
         std::unique_ptr<ResultHolder> h(new ResultHolder());
-        // top-level aggregations in request order; a filter aggregation (InternalFilter, FilterAggregator.java:72-80)
-        // is its counting pipeline's doc_count plus its sub-aggregations' pipelines, in the order compile() made them
         // top-level aggregations in request order; a filter aggregation (InternalFilter, FilterAggregator.java:72-80)
         // is its counting pipeline's doc_count plus its sub-aggregations' groups, in the order create made them
         size_t gi = 0;
