@@ -448,11 +448,20 @@ __global__ __launch_bounds__(kHllLdsWG) void hll_registers_lds_kernel(HllParams 
 // flushed, partitioned by register range, into fs_buf for one gather (hll_p0_gather_kernel); the host picks F so that
 // a register ending below F is a ~5e-3 event per request, and the tail pass (hll_lc_kernel) finishes such registers
 // from the hashes below F.  No snapshot, no phase structure: the pass streams the column at the HBM rate.
-constexpr uint32_t kHllFsWG = 1024;
+#ifndef ESGPU_HLL_FS_WG
+#define ESGPU_HLL_FS_WG 1024
+#endif
+#ifndef ESGPU_HLL_FS_NBUF  // load buffers per thread (2 or 3)
+#define ESGPU_HLL_FS_NBUF 2
+#endif
+constexpr uint32_t kHllFsWG = ESGPU_HLL_FS_WG;
 constexpr uint32_t kHllFsIter = kHllFsWG * 4;
 // LDS log entries; the count is checked every ~kHllFsLog / 4 expected entries and the log flushed once it is over half
 // full (measured at 125M docs: 0.231 ms; a fixed flush schedule with 18,432 / 19,456 entries 0.248 / 0.240 ms)
-constexpr uint32_t kHllFsLog = 16384;
+#ifndef ESGPU_HLL_FS_LOG
+#define ESGPU_HLL_FS_LOG 16384
+#endif
+constexpr uint32_t kHllFsLog = ESGPU_HLL_FS_LOG;
 constexpr uint32_t hll_fs_lds_bytes() { return kHllFsLog * 4u + 3u * 256u * 4u + 16u; }
 
 // one workgroup's log out, partitioned by register range (as the LDS phase kernel's end does); the callers barrier
@@ -518,11 +527,24 @@ __global__ __launch_bounds__(kHllFsWG) void hll_fs_kernel(HllParams P, uint32_t 
     __builtin_amdgcn_sched_barrier(0);
     load(w0 + kHllFsIter + t4, b);
     uint32_t it = 0;
+#if ESGPU_HLL_FS_NBUF == 3
+    uint64_t c[4] = {0, 0, 0, 0};
+    __builtin_amdgcn_sched_barrier(0);
+    load(w0 + 2 * kHllFsIter + t4, c);
+    for (uint32_t base = w0; base < w1; base += 3 * kHllFsIter) {
+        hash4(base + t4, a);
+        load(base + 3 * kHllFsIter + t4, a);
+        hash4(base + kHllFsIter + t4, b);
+        load(base + 4 * kHllFsIter + t4, b);
+        hash4(base + 2 * kHllFsIter + t4, c);
+        load(base + 5 * kHllFsIter + t4, c);
+#else
     for (uint32_t base = w0; base < w1; base += 2 * kHllFsIter) {
         hash4(base + t4, a);
         load(base + 2 * kHllFsIter + t4, a);
         hash4(base + kHllFsIter + t4, b);
         load(base + 3 * kHllFsIter + t4, b);
+#endif
         if (++it == check_iters) {  // workgroup-uniform: every thread runs the same iterations
             it = 0;
             __syncthreads();
@@ -849,11 +871,11 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
                 b = 1;
             per_cu = b;
         }
-        uint32_t wgs = std::max(1u, std::min(cus * (uint32_t)per_cu, n / (kHllFsIter * 2)));
+        uint32_t wgs = std::max(1u, std::min(cus * (uint32_t)per_cu, n / (kHllFsIter * ESGPU_HLL_FS_NBUF)));
         const uint32_t per = ((n + wgs - 1) / wgs + 3) & ~3u;
         wgs = (n + per - 1) / per;
         const uint64_t docs_per_check = ((uint64_t)kHllFsLog / 4) << (p.fs_f - 1);
-        const uint32_t check = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, docs_per_check / (2 * kHllFsIter)));
+        const uint32_t check = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, docs_per_check / (ESGPU_HLL_FS_NBUF * kHllFsIter)));
         if (p.kind == HLL_I64)
             hipLaunchKernelGGL(hll_fs_kernel<HLL_I64>, dim3(wgs), dim3(kHllFsWG), hll_fs_lds_bytes(), st, p, per, check);
         else
