@@ -184,6 +184,9 @@ def main():
     ap.add_argument("--scheme", default="rotate", choices=("rotate", "sets"),
                     help="pipelined phase: rotate = `inflight` plans taken in turn by the shards of consecutive requests; "
                          "sets = one plan per shard, `inflight` sets of them alternating between requests")
+    ap.add_argument("--no-colo", action="store_true",
+                    help="build every shard result and reduce them on the host, instead of the co-located reduce "
+                         "(esgpu_plans_build_reduce) for a GPU's terms shards on one GPU")
     ap.add_argument("--traffic", default=os.path.join(HERE, "profiles", "hbm_traffic.json"),
                     help="PMC-derived HBM bytes per collect launch (profiles/), if measured for this workload")
     args = ap.parse_args()
@@ -220,6 +223,16 @@ def main():
     merged = probe.shard_mergeable() and per_gpu > 1
     probe.close()
     units_per_request = 1 if merged or per_gpu == 1 else per_gpu
+    # a terms request's shards on one GPU (one process): built and reduced in one call (esgpu_plans_build_reduce, the
+    # same result as reducing every shard build); with several ranks each rank's shards go to the cross-rank reduce
+    colo = units_per_request > 1 and world == 1 and not args.no_colo
+    if colo:
+        probe_plans = [engine.plan(aggs, filters=filters, number_of_shards=shards) for _ in range(units_per_request)]
+        colo = ea.colocated(probe_plans)  # a shape the device merge takes (else the builds run on worker threads)
+        for pp in probe_plans:
+            pp.close()
+    if colo:
+        args.scheme = "sets"  # one plan per shard: a request's plans are all alive at its reduce
     # plan sets: one plan per unit (a shard, or all of a fixed-shape request's shards); `inflight` sets alternate, so
     # one request's builds and reduce run while the next request's collects are on the GPU
     inflight = args.inflight or 2
@@ -244,6 +257,8 @@ def main():
                 kernel_bytes[0] += nbytes
 
     host_ms = {"build": 0.0, "reduce": 0.0}
+    if colo:
+        host_ms = {"build_reduce": 0.0}
     # A request's shard builds run on worker threads -- Elasticsearch runs one SEARCH thread per shard of a request --
     # and the coordinating reduce of a request on its own worker (a coordinating node merges one request while the
     # data nodes collect the next).  Requests are reduced in order; every one finishes inside the timed region.
@@ -267,6 +282,12 @@ def main():
         host_ms["reduce"] += (time.perf_counter() - t) * 1e3
         return out
 
+    def colo_request(plans):
+        t = time.perf_counter()
+        out = ea.build_reduce(plans)
+        host_ms["build_reduce"] += (time.perf_counter() - t) * 1e3
+        return out
+
     def run(n_requests, depth):
         """n requests on `depth` plan sets: a request's collects are issued back to back (each plan has its own HIP
         stream), its builds go to the builder threads, its reduce to the reducer; a set is reused once its previous
@@ -279,8 +300,9 @@ def main():
             futs = []
             for unit, p in enumerate(sets[r % depth]):
                 launch(p, unit, False)
-                futs.append(builders.submit(build_unit, p))
-            pend.append(reducer.submit(reduce_request, futs))
+                if not colo:
+                    futs.append(builders.submit(build_unit, p))
+            pend.append(reducer.submit(colo_request, sets[r % depth]) if colo else reducer.submit(reduce_request, futs))
         while pend:
             final = pend.popleft().result()
 
@@ -314,6 +336,11 @@ def main():
         nonlocal final
         p = sets[0][0]
         for _ in range(n_requests):
+            if colo:  # the request's shards collected one after the other, then built and reduced in one call
+                for unit, pu in enumerate(sets[0]):
+                    launch(pu, unit, True)
+                final = colo_request(sets[0])
+                continue
             parts = []
             for unit in range(units_per_request):
                 launch(p, unit, True)
@@ -457,7 +484,8 @@ def main():
             "data": "synthetic (deterministic splitmix64 log docs generated in HBM, seed 0x5EEDE1A5, shard = global shard id)",
             "config": {"workload": args.workload, "request": desc, "docs_per_shard": args.docs, "shards": shards,
                        "shards_per_gpu": per_gpu, "docs_total": docs_total,
-                       "collect": "merged (one plan per GPU)" if merged else "per shard",
+                       "collect": "merged (one plan per GPU)" if merged else
+                                  ("per shard, co-located reduce (esgpu_plans_build_reduce)" if colo else "per shard"),
                        "parallelism": f"{per_gpu} shard(s) per GPU x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,

@@ -7,10 +7,10 @@ without the built library or without a GPU the calls raise.
 from ._native import (CircuitBreakingError, EsGpuError, NoDeviceError, UnsupportedOnGpu)  # noqa: F401
 from .aggs import AggregationBuilders, Order, QueryBuilders  # noqa: F401
 from .engine import (Communicator, Engine, Plan, Segment, ShardResult, device_count, pinned_empty, precision_from_threshold,  # noqa: F401
-                     reduce, routing_hash, synthetic_host_column, synthetic_terms)
+                     build_reduce, colocated, reduce, routing_hash, synthetic_host_column, synthetic_terms)
 
 __all__ = [
     "AggregationBuilders", "QueryBuilders", "Order", "Engine", "Plan", "Segment", "ShardResult", "Communicator",
-    "reduce", "routing_hash", "device_count", "precision_from_threshold", "synthetic_host_column", "synthetic_terms",
+    "reduce", "build_reduce", "colocated", "routing_hash", "device_count", "precision_from_threshold", "synthetic_host_column", "synthetic_terms",
     "EsGpuError", "UnsupportedOnGpu", "CircuitBreakingError", "NoDeviceError",
 ]

@@ -168,6 +168,8 @@ SIGNATURES = [
     ("esgpu_result_free", ctypes.c_int, [ctypes.POINTER(Result)]),
     ("esgpu_reduce", ctypes.c_int, [ctypes.POINTER(ctypes.POINTER(Result)), ctypes.c_int32,
                                     ctypes.POINTER(ctypes.POINTER(Result))]),
+    ("esgpu_plans_build_reduce", ctypes.c_int, [ctypes.POINTER(_VP), ctypes.c_int32, ctypes.POINTER(ctypes.POINTER(Result))]),
+    ("esgpu_plans_colocated", ctypes.c_int, [ctypes.POINTER(_VP), ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
     ("esgpu_cardinality_value", ctypes.c_int, [ctypes.POINTER(AggBlock), ctypes.c_uint64, ctypes.POINTER(ctypes.c_int64)]),
     ("esgpu_result_to_json", ctypes.c_int, [ctypes.POINTER(Result), ctypes.c_char_p, ctypes.c_size_t,
                                             ctypes.POINTER(ctypes.c_size_t)]),

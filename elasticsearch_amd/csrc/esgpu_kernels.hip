@@ -1046,6 +1046,55 @@ void launch_compact_rows(const CompactParams& p, hipStream_t st) {
     hipLaunchKernelGGL(compact_rows_kernel, dim3(p.k), dim3(256), 0, st, p);
 }
 
+__global__ __launch_bounds__(256) void colo_merge_kernel(ColoParams P) {
+    const uint32_t m = blockIdx.x * 256 + threadIdx.x, r = blockIdx.y;
+    if (m >= P.Hm) return;
+    unsigned long long c = 0;
+    unsigned long long vc[kCompactLeaves] = {0, 0, 0, 0}, mn[kCompactLeaves], mx[kCompactLeaves];
+    double sum[kCompactLeaves] = {0.0, 0.0, 0.0, 0.0}, sq[kCompactLeaves] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int l = 0; l < kCompactLeaves; ++l) { mn[l] = kMinInit; mx[l] = kMaxInit; }
+    for (uint32_t sh = 0; sh < P.nsh; ++sh) {  // shard order: the reference reduce's addition order
+        const int32_t ord = P.rows[(size_t)r * P.nsh + sh];
+        if (ord < 0) continue;
+        const ColoShard& S = P.shards[sh];
+        const int64_t slot = P.kmin + (int64_t)m - S.key0;
+        if (slot < 0 || slot >= (int64_t)S.H || (uint32_t)ord >= S.T) continue;
+        const size_t cell = (size_t)slot * S.T + (uint32_t)ord;
+        const unsigned long long cs = S.cnt32 ? ((const unsigned int*)S.cnt)[cell] : S.cnt[cell];
+        if (!cs) continue;  // the shard has no bucket at this key
+        c += cs;
+        for (int l = 0; l < P.nleaves; ++l) {
+            const unsigned long long v = S.lcnt[l] ? S.lcnt[l][cell] : cs;
+            vc[l] += v;
+            sum[l] += v ? S.lsum[l][cell] : 0.0;  // an empty shard stats adds its 0.0 sum
+            if (v && S.lmn[l]) {
+                mn[l] = min(mn[l], S.lmn[l][cell]);  // order-preserving encodings: Java Math.min / max
+                mx[l] = max(mx[l], S.lmx[l][cell]);
+            }
+            if (v && S.lsq[l]) sq[l] += S.lsq[l][cell];
+        }
+    }
+    const size_t at = (size_t)r * P.Hm + m, stride = (size_t)P.R * P.Hm;
+    P.o_cnt[at] = c;
+    for (int l = 0; l < P.nleaves; ++l) {
+        double dmn = __builtin_inf(), dmx = -__builtin_inf();
+        if (vc[l]) {
+            if (mn[l] < kEncNegInf || mx[l] > kEncPosInf) { dmn = __builtin_nan(""); dmx = __builtin_nan(""); }
+            else { dmn = unsortable(mn[l]); dmx = unsortable(mx[l]); }
+        }
+        P.o_lcnt[l * stride + at] = vc[l];
+        P.o_sum[l * stride + at] = sum[l];
+        P.o_min[l * stride + at] = dmn;
+        P.o_max[l * stride + at] = dmx;
+        P.o_sq[l * stride + at] = sq[l];
+    }
+}
+void launch_colo_merge(const ColoParams& p, hipStream_t st) {
+    if (p.R == 0 || p.Hm == 0) return;
+    hipLaunchKernelGGL(colo_merge_kernel, dim3((p.Hm + 255) / 256, p.R), dim3(256), 0, st, p);
+}
+
 // device -> pinned host memory for the build's small transfers: a kernel writing over the link beats a DMA copy,
 // whose setup measured ~130 us per 144 KB transfer
 __global__ __launch_bounds__(256) void copy_u64_kernel(const unsigned long long* __restrict__ src,

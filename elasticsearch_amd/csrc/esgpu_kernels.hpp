@@ -231,6 +231,32 @@ struct CompactParams {
 };
 void launch_compact_rows(const CompactParams& p, hipStream_t s);
 
+// co-located reduce (esgpu_plans_build_reduce): the final terms buckets' histogram rows merged over the shards of one
+// device, in shard order (InternalHistogram.doReduce per key, InternalStats / InternalAvg / InternalExtendedStats.doReduce
+// per bucket), into dense [R][Hm] rows over the union of the shards' key ranges
+struct ColoShard {
+    const unsigned long long* cnt;   // bucket doc counts [H][T] (u32 when cnt32)
+    int32_t cnt32;
+    uint32_t H, T;
+    int64_t key0;
+    const unsigned long long* lcnt[kCompactLeaves];  // leaf value counts (null: the bucket counts)
+    const double* lsum[kCompactLeaves];
+    const unsigned long long* lmn[kCompactLeaves];   // null: no extrema (avg)
+    const unsigned long long* lmx[kCompactLeaves];
+    const double* lsq[kCompactLeaves];               // null: no sum of squares
+};
+struct ColoParams {
+    const ColoShard* shards;  // [nsh] (device)
+    const int32_t* rows;      // [R][nsh]: the final bucket's ordinal in each shard, -1 when the shard did not return it
+    uint32_t nsh, R, Hm;
+    int64_t kmin;
+    int32_t nleaves;
+    unsigned long long* o_cnt;  // [R][Hm] (pinned, device-mapped)
+    unsigned long long* o_lcnt; // [nleaves][R][Hm]
+    double *o_sum, *o_min, *o_max, *o_sq;  // [nleaves][R][Hm]
+};
+void launch_colo_merge(const ColoParams& p, hipStream_t s);
+
 // per-8192-doc-block min / max; f64 = the column holds doubles, taken as (long) casts (FieldData.castToLong)
 void launch_zone_map(const int64_t* v, const uint64_t* present, uint32_t n, int64_t* zmin, int64_t* zmax, bool f64,
                      hipStream_t s);

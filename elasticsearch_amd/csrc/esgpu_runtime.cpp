@@ -24,6 +24,7 @@
 #include <map>
 #include <queue>
 #include <string_view>
+#include <unordered_map>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -1028,6 +1029,12 @@ struct esgpu_plan {
     double b_wait = 0, b_total = 0;  // last build: stream waits / whole call (ms)
     bool b_trace = false;
     std::vector<std::pair<const char*, double>> b_marks;
+    // co-located reduce (esgpu_plans_build_reduce): the build stops after the terms selection (buckets with empty
+    // sub-aggregations) and keeps the winners' ordinals for the device merge of their rows
+    bool skeleton = false;
+    std::vector<uint32_t> sk_ords;
+    PinnedBuf h_colo;   // the merged rows (pinned, device-mapped)
+    Scratch s_colo;     // shard descriptors + the rows table
     int32_t last_path = 0;
     // per-request scratch, reused across requests
     Scratch s_accept, s_tcnt, s_rows, s_dst[6];
@@ -4414,6 +4421,18 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
         });
     }
     bmark(p, "selected");
+    if (p->skeleton) {  // esgpu_plans_build_reduce: the winners and their counts; the children's rows merge on the device
+        p->sk_ords.clear();
+        begin_instance(r, other);
+        for (const TermPick& tp : top) {
+            const std::string term = plan_term(p, P0, tp.ord);
+            push_bucket(r, tp.ord, &term, tp.count);
+            p->sk_ords.push_back(tp.ord);
+            for (Block& sb : r.subs) sb.append_empty();
+        }
+        end_instance(r);
+        return r;
+    }
     const uint32_t k = (uint32_t)top.size();
     uint32_t* rows = (uint32_t*)p->h_rows.ensure(std::max<size_t>(k, 1) * 4);
     for (uint32_t i = 0; i < k; ++i) rows[i] = top[i].ord;
@@ -5067,6 +5086,188 @@ extern "C" int esgpu_plan_destroy(esgpu_plan* p) {
 // ------------------------------------------------------------------------------------------------------------
 extern "C" int esgpu_result_free(esgpu_result* r) {
     return guarded([&] { delete holder_of(r); });
+}
+
+// ---- co-located reduce ----------------------------------------------------------------------------------------
+// The shards of one request that live on one device, reduced without materialising their results: each plan's build
+// stops after its terms selection (the buckets and counts of its top shard_size terms, children empty), the reference
+// reduce runs over those skeletons (InternalTerms.doReduce: the final terms, their counts, errors and other-doc count
+// are exactly the full reduce's -- a bucket's children never affect which terms survive), and the surviving terms'
+// histogram rows are merged over the shards on the device in shard order (colo_merge_kernel: the per-key
+// InternalHistogram / stats reduce) and expanded once.  Shape: a top-level terms aggregation (a count-ordered or term-
+// ordered host selection) whose only child is a histogram / date_histogram over an affine rounding with
+// min_doc_count >= 1 and numeric metric children.  Anything else builds every shard and reduces (esgpu_reduce).
+static bool colo_eligible(esgpu_plan* const* plans, int n, bool shape_only = false) {
+    if (n < 2) return false;
+    const esgpu_plan* p0 = plans[0];
+    for (int i = 0; i < n; ++i) {
+        const esgpu_plan* p = plans[i];
+        if (!p || p->ctx != p0->ctx || p->tops.size() != 1 || p->groups.size() != 1 || p->specs.size() != p0->specs.size())
+            return false;
+        const Group& g = p->groups[0];
+        const SpecNode& tn = p->specs[g.root];
+        if (tn.s.type != ESGPU_AGG_TERMS || tn.s.order == ESGPU_ORDER_AGG_ASC || tn.s.order == ESGPU_ORDER_AGG_DESC)
+            return false;
+        if (g.kids.size() != 1 || g.pipes.empty()) return false;
+        const ChildSrc& kid = g.kids[0];
+        if (!kid.bucket || kid.filter || kid.deep >= 0 || !kid.rpipes.empty() || kid.grand.empty() ||
+            kid.grand.size() > (size_t)kCompactLeaves)
+            return false;
+        const SpecNode& hn = p->specs[kid.spec];
+        if ((hn.s.type != ESGPU_AGG_HISTOGRAM && hn.s.type != ESGPU_AGG_DATE_HISTOGRAM) || hn.s.min_doc_count < 1) return false;
+        for (const LeafRef& l : kid.grand)
+            if (!is_metric(p->specs[p->pipes[l.pipe].metrics[l.leaf]].s.type)) return false;
+        if (shape_only) continue;
+        const Pipeline& P0 = p->pipes[g.pipes[0]];
+        const Pipeline& B0 = p->pipes[kid.pipes[0]];
+        if (!P0.allocated || !B0.allocated || P0.value_count > 65536 || P0.comp) return false;
+        if (B0.inner_terms || B0.ord_hist || !B0.cards.empty() || B0.ktable || B0.deferred || B0.comp) return false;
+        for (const LeafRef& l : kid.grand) {
+            const Pipeline& L = p->pipes[l.pipe];
+            if (!L.allocated || L.H != B0.H || L.T != B0.T || L.key0 != B0.key0) return false;
+        }
+        if (B0.interval != plans[0]->pipes[plans[0]->groups[0].kids[0].pipes[0]].interval ||
+            B0.offset != plans[0]->pipes[plans[0]->groups[0].kids[0].pipes[0]].offset)
+            return false;
+    }
+    return true;
+}
+
+extern "C" int esgpu_plans_colocated(esgpu_plan* const* plans, int32_t n, int32_t* merged) {
+    return guarded([&] {
+        require(plans && merged && n >= 1, ESGPU_ERR_INVALID, "null argument");
+        *merged = colo_eligible(plans, n, true) ? 1 : 0;
+    });
+}
+
+extern "C" int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esgpu_result** out) {
+    tune_host_heap();
+    return guarded([&] {
+        require(plans && out && n >= 1, ESGPU_ERR_INVALID, "build_reduce needs at least one plan");
+        std::vector<std::unique_ptr<ResultHolder, void (*)(ResultHolder*)>> parts;
+        const bool colo = colo_eligible(plans, n) && std::getenv("ESGPU_COLO") == nullptr;
+        for (int i = 0; i < n; ++i) {
+            plans[i]->skeleton = colo;
+            esgpu_result* r = nullptr;
+            const int rc = esgpu_plan_build(plans[i], &r);
+            plans[i]->skeleton = false;
+            if (rc != ESGPU_OK) throw EsError(rc, g_err);
+            parts.emplace_back(holder_of(r), +[](ResultHolder* h) { delete h; });
+        }
+        std::vector<const std::vector<Block>*> lists;
+        for (auto& h : parts) lists.push_back(&h->aggs);
+        std::unique_ptr<ResultHolder> res(new ResultHolder());
+        res->aggs = reduce_lists(lists);
+        if (colo && !res->aggs.empty() && res->aggs[0].type == ESGPU_AGG_TERMS && res->aggs[0].subs.size() == 1) {
+            Block& tb = res->aggs[0];
+            const uint64_t R = tb.nbuckets();
+            esgpu_plan* p0 = plans[0];
+            hipStream_t st = p0->stream;
+            HIPX(hipSetDevice(p0->ctx->device));
+            // rows: each final term's ordinal in each shard that returned it
+            std::vector<int32_t> rows((size_t)R * n, -1);
+            for (int i = 0; i < n; ++i) {
+                const Block& sb = parts[i]->aggs[0];
+                std::unordered_map<std::string_view, uint32_t> at;
+                for (uint64_t b = 0; b < sb.nbuckets(); ++b)
+                    at.emplace(std::string_view(sb.term_pool).substr(sb.term_off[b], sb.term_off[b + 1] - sb.term_off[b]),
+                               plans[i]->sk_ords[b]);
+                for (uint64_t b = 0; b < R; ++b) {
+                    auto it = at.find(std::string_view(tb.term_pool).substr(tb.term_off[b], tb.term_off[b + 1] - tb.term_off[b]));
+                    if (it != at.end()) rows[(size_t)b * n + i] = (int32_t)it->second;
+                }
+            }
+            // shard descriptors and the union of the key ranges
+            const ChildSrc& kid0 = p0->groups[0].kids[0];
+            const int nl = (int)kid0.grand.size();
+            std::vector<ColoShard> sh(n);
+            int64_t kmin = INT64_MAX, kmax = INT64_MIN;
+            for (int i = 0; i < n; ++i) {
+                const esgpu_plan* p = plans[i];
+                const ChildSrc& kid = p->groups[0].kids[0];
+                const Pipeline& B0 = p->pipes[kid.pipes[0]];
+                ColoShard& c = sh[i];
+                c.cnt = B0.g_cnt.as<unsigned long long>();
+                c.cnt32 = B0.cnt32 ? 1 : 0;
+                c.H = B0.H;
+                c.T = B0.T;
+                c.key0 = B0.key0;
+                kmin = std::min<int64_t>(kmin, B0.key0);
+                kmax = std::max<int64_t>(kmax, B0.key0 + (int64_t)B0.H - 1);
+                for (int l = 0; l < nl; ++l) {
+                    const Pipeline& L = p->pipes[kid.grand[l].pipe];
+                    const int32_t type = p->specs[L.metrics[kid.grand[l].leaf]].s.type;
+                    const unsigned long long* lc = (L.vcnt_mode ? L.g_vcnt : L.g_cnt).as<unsigned long long>();
+                    c.lcnt[l] = lc == c.cnt && !c.cnt32 ? nullptr : lc;
+                    c.lsum[l] = L.g_sum.as<double>();
+                    c.lmn[l] = L.met >= 2 && type != ESGPU_AGG_AVG ? L.g_min.as<unsigned long long>() : nullptr;
+                    c.lmx[l] = c.lmn[l] ? L.g_max.as<unsigned long long>() : nullptr;
+                    c.lsq[l] = L.met >= 3 && type == ESGPU_AGG_EXTENDED_STATS ? L.g_sq.as<double>() : nullptr;
+                }
+            }
+            const uint64_t Hm = R ? (uint64_t)(kmax - kmin + 1) : 0;
+            require(Hm <= (1ull << 26), ESGPU_ERR_UNSUPPORTED, "co-located reduce over a key range beyond 64M buckets");
+            const size_t cells = (size_t)R * Hm;
+            PinnedBuf& hb = p0->h_colo;
+            const size_t o_bytes = cells * 8 * (1 + 5 * (size_t)std::max(nl, 1));
+            char* hbase = (char*)hb.ensure(std::max<size_t>(o_bytes, 8));
+            char* dbase = (char*)hb.dev();
+            void* dmeta = p0->s_colo.ensure(p0->ctx, sizeof(ColoShard) * n + rows.size() * 4 + 16);
+            HIPX(hipMemcpyAsync(dmeta, sh.data(), sizeof(ColoShard) * n, hipMemcpyHostToDevice, st));
+            int32_t* drows = (int32_t*)((char*)dmeta + sizeof(ColoShard) * n);
+            if (!rows.empty()) HIPX(hipMemcpyAsync(drows, rows.data(), rows.size() * 4, hipMemcpyHostToDevice, st));
+            ColoParams C{};
+            C.shards = (const ColoShard*)dmeta;
+            C.rows = drows;
+            C.nsh = (uint32_t)n;
+            C.R = (uint32_t)R;
+            C.Hm = (uint32_t)Hm;
+            C.kmin = kmin;
+            C.nleaves = nl;
+            C.o_cnt = (unsigned long long*)dbase;
+            C.o_lcnt = (unsigned long long*)(dbase + cells * 8);
+            C.o_sum = (double*)(dbase + cells * 8 * (1 + (size_t)nl));
+            C.o_min = (double*)(dbase + cells * 8 * (1 + 2 * (size_t)nl));
+            C.o_max = (double*)(dbase + cells * 8 * (1 + 3 * (size_t)nl));
+            C.o_sq = (double*)(dbase + cells * 8 * (1 + 4 * (size_t)nl));
+            // the other plans' streams must have finished their collects (each build synchronised its own stream)
+            launch_colo_merge(C, st);
+            HIPX(hipGetLastError());
+            HIPX(hipStreamSynchronize(st));
+            // the terms block's histogram child, rebuilt from the merged rows (min_doc_count >= 1: non-empty keys only)
+            const Block proto = tb.subs[0].like();
+            Block hist = proto;
+            const Pipeline& B00 = p0->pipes[kid0.pipes[0]];
+            const int64_t iv = B00.interval, off = B00.offset;
+            const unsigned long long* oc = (const unsigned long long*)hbase;
+            const unsigned long long* olc = (const unsigned long long*)(hbase + cells * 8);
+            const double* osum = (const double*)(hbase + cells * 8 * (1 + (size_t)nl));
+            const double* omin = (const double*)(hbase + cells * 8 * (1 + 2 * (size_t)nl));
+            const double* omax = (const double*)(hbase + cells * 8 * (1 + 3 * (size_t)nl));
+            const double* osq = (const double*)(hbase + cells * 8 * (1 + 4 * (size_t)nl));
+            for (uint64_t b = 0; b < R; ++b) {
+                begin_instance(hist, 0);
+                for (uint64_t m = 0; m < Hm; ++m) {
+                    const size_t at = (size_t)b * Hm + m;
+                    if (!oc[at]) continue;
+                    push_bucket(hist, (kmin + (int64_t)m) * iv + off, nullptr, (int64_t)oc[at]);
+                    for (int l = 0; l < nl; ++l) {
+                        Block& gb = hist.subs[l];
+                        ++gb.n;
+                        gb.count.push_back((int64_t)olc[l * cells + at]);
+                        gb.sum.push_back(osum[l * cells + at]);
+                        gb.min.push_back(omin[l * cells + at]);
+                        gb.max.push_back(omax[l * cells + at]);
+                        gb.sumsq.push_back(osq[l * cells + at]);
+                    }
+                }
+                end_instance(hist);
+            }
+            tb.subs[0] = std::move(hist);
+        }
+        res->export_view();
+        *out = &res.release()->pub;
+    });
 }
 
 extern "C" int esgpu_reduce(const esgpu_result* const* shards, int32_t n, esgpu_result** out) {

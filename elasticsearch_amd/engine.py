@@ -106,6 +106,24 @@ def reduce(results):
     return ShardResult(out)
 
 
+def build_reduce(plans):
+    """The reduce of one request's shard plans that live on one device, built and reduced in one call: the same result
+    as reduce([p.build() for p in plans]); terms{histogram{metrics}} requests merge the surviving terms' rows on the
+    device instead of building every shard's result (esgpu_plans_build_reduce)."""
+    arr = (N._VP * len(plans))(*[p._ptr for p in plans])
+    out = ctypes.POINTER(N.Result)()
+    N.check(N.lib().esgpu_plans_build_reduce(arr, len(plans), ctypes.byref(out)))
+    return ShardResult(out)
+
+
+def colocated(plans):
+    """True if build_reduce merges this request's shards on the device (esgpu_plans_colocated)."""
+    arr = (N._VP * len(plans))(*[p._ptr for p in plans])
+    v = ctypes.c_int32()
+    N.check(N.lib().esgpu_plans_colocated(arr, len(plans), ctypes.byref(v)))
+    return bool(v.value)
+
+
 class OrdinalMap:
     """Global ordinals of one keyword field over a reader's segments (GlobalOrdinalsBuilder / Lucene OrdinalMap)."""
 

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define ESGPU_ABI_VERSION 6
+#define ESGPU_ABI_VERSION 7
 
 /* ---------------------------------------------------------------------------------------------------------
  * Status codes.  Mapping used by the JNI shim (SURVEY §8(b) "Errors"):
@@ -454,6 +454,15 @@ struct esgpu_result {
 int esgpu_result_free(esgpu_result* r);
 /* InternalAggregations.reduce over shard results in shard order (InternalAggregations.java:133-161). */
 int esgpu_reduce(const esgpu_result* const* shard_results, int32_t n, esgpu_result** out);
+/* The same reduce over the shards of one request whose plans live on one device, built and reduced in one call:
+ * identical to esgpu_reduce over esgpu_plan_build(plans[i]) in order.  For a top-level terms aggregation whose only
+ * child is a histogram (affine rounding, min_doc_count >= 1) with numeric metric children, each plan builds only its
+ * terms selection, the reference reduce runs over those, and the surviving terms' histogram rows are merged on the
+ * device (no shard result is materialised); any other request builds every plan and reduces. */
+int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esgpu_result** out);
+/* *merged = 1 if the request's shape is one esgpu_plans_build_reduce merges on the device (the shards' data may still
+ * send a request down the build-and-reduce path, e.g. an unmapped shard), 0 if it always builds and reduces. */
+int esgpu_plans_colocated(esgpu_plan* const* plans, int32_t n, int32_t* merged);
 /* Cardinality value of instance i of a cardinality block (HyperLogLogPlusPlus.cardinality(0)). */
 int esgpu_cardinality_value(const esgpu_agg_block* block, uint64_t instance, int64_t* value);
 /* XContent-style JSON ({"<name>": {...}}), full double precision, Infinity/NaN as JSON tokens.

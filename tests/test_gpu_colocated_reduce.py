@@ -1,0 +1,152 @@
+"""GPU parity of the co-located reduce (esgpu_plans_build_reduce): the shards of one request whose plans
+live on one device, reduced without building every shard result.  Each case compares build_reduce(plans) with the
+reduce of the shard builds (InternalAggregations.reduce, shard order) bit for bit, and with the oracle's reduce.
+
+Covered: the north star and config 5 shapes over 4-8 shards, several metric leaves (stats, avg, extended_stats on one
+histogram), shards whose key ranges differ (a timestamp span per shard), a sparse metric (value counts apart from doc
+counts), double metrics with NaN and -0.0 (Java Math.min / max over the shards), term and ascending count orders, and
+shapes outside the merge (terms{stats}, min_doc_count 0 histograms, a second child) that build and reduce instead.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from elasticsearch_amd import AggregationBuilders as AB
+from elasticsearch_amd import Order, QueryBuilders as QB
+from elasticsearch_amd import _native as N
+from elasticsearch_amd import build_reduce, colocated, reduce
+from helpers import assert_same, bits_from_mask, synthetic_columns
+
+pytestmark = pytest.mark.gpu
+
+NS_FIELDS = ("host", "@timestamp", "response_time_ms")
+C5_FIELDS = ("status", "bytes", "host", "@timestamp", "response_time_ms")
+
+
+def _both(engine, aggs, segs, filters=None):
+    """(build_reduce result, reduce-of-builds result) over one plan per segment"""
+    shards = len(segs)
+    plans = [engine.plan(aggs, filters=filters, number_of_shards=shards) for _ in segs]
+    for p, s in zip(plans, segs):
+        p.collect(s)
+    fused = build_reduce(plans).to_dict()
+    for p, s in zip(plans, segs):
+        p.reset()
+        p.collect(s)
+    plain = reduce([p.build() for p in plans]).to_dict()
+    for p in plans:
+        p.close()
+    return fused, plain
+
+
+@pytest.mark.parametrize("shards", [2, 8])
+def test_north_star_shards(engine, shards):
+    n = 1_500_000
+    aggs = [AB.terms("hosts").field("host").size(10).subAggregation(
+        AB.dateHistogram("per_hour").field("@timestamp").interval("1h").subAggregation(AB.stats("rt").field("response_time_ms")))]
+    segs = [engine.synthetic_segment(n, fields=NS_FIELDS, shard=s) for s in range(shards)]
+    probe = [engine.plan(aggs, number_of_shards=shards) for _ in segs]
+    assert colocated(probe)
+    for p in probe:
+        p.close()
+    fused, plain = _both(engine, aggs, segs)
+    assert_same(fused, plain, "fused vs builds")
+    want = O.run([(synthetic_columns(NS_FIELDS, n, shard=s), n) for s in range(shards)], aggs, number_of_shards=shards)
+    assert_same(fused, want["reduced"], "fused vs oracle")
+    for s in segs:
+        s.close()
+
+
+def test_config5_shape_several_leaves(engine):
+    n, shards = 1_200_000, 6
+    aggs = [AB.terms("hosts").field("host").size(7).subAggregation(
+        AB.dateHistogram("h").field("@timestamp").interval("3h")
+        .subAggregation(AB.avg("a").field("response_time_ms"))
+        .subAggregation(AB.stats("s").field("bytes"))
+        .subAggregation(AB.extendedStats("e").field("response_time_ms")))]
+    filters = [QB.termQuery("status", 200), QB.rangeQuery("bytes").gte(1024).lte(65536)]
+    segs = [engine.synthetic_segment(n, fields=C5_FIELDS, shard=s) for s in range(shards)]
+    fused, plain = _both(engine, aggs, segs, filters=filters)
+    assert_same(fused, plain, "fused vs builds")
+    want = O.run([(synthetic_columns(C5_FIELDS, n, shard=s), n) for s in range(shards)], aggs, filters=filters,
+                 number_of_shards=shards)
+    assert_same(fused, want["reduced"], "fused vs oracle", exact_floats=False)
+    for s in segs:
+        s.close()
+
+
+def _log_shard(rng, n, t0, span_ms, metric, present=None, nterms=200):
+    ranks = np.minimum(rng.zipf(1.3, size=n) - 1, nterms - 1)
+    cols = {
+        "host": {"type": N.COL_ORD_U32, "values": ((ranks * 17 + 3) % nterms).astype(np.uint32),
+                 "terms": ["h%03d" % i for i in range(nterms)]},
+        "@timestamp": {"type": N.COL_I64, "values": np.sort(rng.integers(t0, t0 + span_ms, size=n)).astype(np.int64)},
+        "m": metric,
+    }
+    if present is not None:
+        cols["m"] = dict(metric, present=bits_from_mask(present))
+    return cols
+
+
+def test_shards_with_different_key_ranges_sparse_and_double_metrics(engine):
+    """Shard s covers days s .. s+2 (its grid's first key differs), the metric is a double column with NaN and -0.0 in
+    some shards and missing on 20 % of the docs (value counts apart from doc counts)."""
+    rng = np.random.default_rng(91)
+    t0 = 1_441_065_600_000
+    shard_cols = []
+    for s in range(5):
+        n = 400_000 + 50_000 * s
+        vals = rng.normal(100.0, 30.0, size=n)
+        if s == 1:
+            vals[::997] = np.nan
+        if s == 3:
+            vals[::501] = -0.0
+        pres = rng.random(n) >= 0.2
+        vals[~pres] = 0.0
+        shard_cols.append((_log_shard(rng, n, t0 + s * 86_400_000, 3 * 86_400_000, {"type": N.COL_F64, "values": vals},
+                                      present=pres), n))
+    aggs = [AB.terms("t").field("host").size(12).subAggregation(
+        AB.dateHistogram("h").field("@timestamp").interval("2h")
+        .subAggregation(AB.stats("s").field("m")).subAggregation(AB.extendedStats("e").field("m")))]
+    segs = [engine.upload_segment(c, n) for c, n in shard_cols]
+    fused, plain = _both(engine, aggs, segs)
+    assert_same(fused, plain, "fused vs builds")
+    want = O.run(shard_cols, aggs, number_of_shards=len(shard_cols))
+    assert_same(fused, want["reduced"], "fused vs oracle", exact_floats=False)
+    for s in segs:
+        s.close()
+
+
+@pytest.mark.parametrize("order", [Order.term(True), Order.count(True)])
+def test_other_orders(engine, order):
+    n, shards = 800_000, 4
+    aggs = [AB.terms("hosts").field("host").size(6).order(order).subAggregation(
+        AB.dateHistogram("h").field("@timestamp").interval("1d").subAggregation(AB.avg("a").field("response_time_ms")))]
+    segs = [engine.synthetic_segment(n, fields=NS_FIELDS, shard=10 + s) for s in range(shards)]
+    fused, plain = _both(engine, aggs, segs)
+    assert_same(fused, plain, "fused vs builds")
+    for s in segs:
+        s.close()
+
+
+@pytest.mark.parametrize("shape", ["terms_stats", "min_doc_count_0", "two_children"])
+def test_shapes_outside_the_merge(engine, shape):
+    n, shards = 600_000, 3
+    if shape == "terms_stats":
+        aggs = [AB.terms("hosts").field("host").size(5).subAggregation(AB.stats("s").field("response_time_ms"))]
+    elif shape == "min_doc_count_0":
+        aggs = [AB.terms("hosts").field("host").size(5).subAggregation(
+            AB.dateHistogram("h").field("@timestamp").interval("1d").minDocCount(0).subAggregation(AB.avg("a").field("response_time_ms")))]
+    else:
+        aggs = [AB.terms("hosts").field("host").size(5)
+                .subAggregation(AB.dateHistogram("h").field("@timestamp").interval("1d"))
+                .subAggregation(AB.avg("a").field("response_time_ms"))]
+    segs = [engine.synthetic_segment(n, fields=NS_FIELDS, shard=20 + s) for s in range(shards)]
+    probe = [engine.plan(aggs, number_of_shards=shards) for _ in segs]
+    assert not colocated(probe)
+    for p in probe:
+        p.close()
+    fused, plain = _both(engine, aggs, segs)
+    assert_same(fused, plain, f"{shape}: fused vs builds")
+    for s in segs:
+        s.close()

@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
     for name in names:
         assert hasattr(lib, name), name
     assert {n for n, _, _ in N.SIGNATURES} == set(names)
-    assert lib.esgpu_abi_version() == 6
+    assert lib.esgpu_abi_version() == 7
 
 
 def test_no_silent_cpu_fallback():
