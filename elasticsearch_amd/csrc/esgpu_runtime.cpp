@@ -5114,7 +5114,9 @@ static bool colo_eligible(esgpu_plan* const* plans, int n, bool shape_only = fal
             kid.grand.size() > (size_t)kCompactLeaves)
             return false;
         const SpecNode& hn = p->specs[kid.spec];
-        if ((hn.s.type != ESGPU_AGG_HISTOGRAM && hn.s.type != ESGPU_AGG_DATE_HISTOGRAM) || hn.s.min_doc_count < 1) return false;
+        if ((hn.s.type != ESGPU_AGG_HISTOGRAM && hn.s.type != ESGPU_AGG_DATE_HISTOGRAM) || hn.s.min_doc_count < 0 ||
+            !hn.tz_starts.empty() || (hn.s.order != ESGPU_ORDER_KEY_ASC && hn.s.order != ESGPU_ORDER_KEY_DESC))
+            return false;
         for (const LeafRef& l : kid.grand)
             if (!is_metric(p->specs[p->pipes[l.pipe].metrics[l.leaf]].s.type)) return false;
         if (shape_only) continue;
@@ -5234,23 +5236,57 @@ extern "C" int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esg
             launch_colo_merge(C, st);
             HIPX(hipGetLastError());
             HIPX(hipStreamSynchronize(st));
-            // the terms block's histogram child, rebuilt from the merged rows (min_doc_count >= 1: non-empty keys only)
+            // the terms block's histogram child, rebuilt from the merged rows: keys with at least min_doc_count docs,
+            // and for min_doc_count 0 the empty buckets of addEmptyBuckets (InternalHistogram.java:395-449) -- every
+            // grid key between a row's first and last non-empty key, and the extended bounds' keys outside them
             const Block proto = tb.subs[0].like();
             Block hist = proto;
             const Pipeline& B00 = p0->pipes[kid0.pipes[0]];
             const int64_t iv = B00.interval, off = B00.offset;
+            const int64_t mdc = proto.min_doc_count;
+            const bool fill = mdc == 0 && proto.has_empty_info, desc = proto.order == ESGPU_ORDER_KEY_DESC;
             const unsigned long long* oc = (const unsigned long long*)hbase;
             const unsigned long long* olc = (const unsigned long long*)(hbase + cells * 8);
             const double* osum = (const double*)(hbase + cells * 8 * (1 + (size_t)nl));
             const double* omin = (const double*)(hbase + cells * 8 * (1 + 2 * (size_t)nl));
             const double* omax = (const double*)(hbase + cells * 8 * (1 + 3 * (size_t)nl));
             const double* osq = (const double*)(hbase + cells * 8 * (1 + 4 * (size_t)nl));
+            struct Out { int64_t key; int64_t at; };  // at < 0: an empty bucket
+            std::vector<Out> list;
             for (uint64_t b = 0; b < R; ++b) {
+                list.clear();
+                int64_t first = -1, last = -1;
+                for (uint64_t m = 0; m < Hm; ++m)
+                    if (oc[(size_t)b * Hm + m]) { if (first < 0) first = (int64_t)m; last = (int64_t)m; }
+                auto key_of = [&](int64_t m) { return (kmin + m) * iv + off; };
+                if (!fill) {
+                    for (int64_t m = first; first >= 0 && m <= last; ++m) {
+                        const size_t at = (size_t)b * Hm + (size_t)m;
+                        if (oc[at] && (int64_t)oc[at] >= mdc) list.push_back({key_of(m), (int64_t)at});
+                    }
+                } else if (first < 0) {
+                    if (proto.has_bmin && proto.has_bmax)
+                        for (int64_t k = proto.bmin; k <= proto.bmax; k += iv) list.push_back({k, -1});
+                } else {
+                    if (proto.has_bmin)
+                        for (int64_t k = proto.bmin; k < key_of(first); k += iv) list.push_back({k, -1});
+                    for (int64_t m = first; m <= last; ++m) {
+                        const size_t at = (size_t)b * Hm + (size_t)m;
+                        list.push_back({key_of(m), oc[at] ? (int64_t)at : -1});
+                    }
+                    if (proto.has_bmax && proto.bmax > key_of(last))
+                        for (int64_t k = key_of(last) + iv; k <= proto.bmax; k += iv) list.push_back({k, -1});
+                }
+                if (desc) std::reverse(list.begin(), list.end());
                 begin_instance(hist, 0);
-                for (uint64_t m = 0; m < Hm; ++m) {
-                    const size_t at = (size_t)b * Hm + m;
-                    if (!oc[at]) continue;
-                    push_bucket(hist, (kmin + (int64_t)m) * iv + off, nullptr, (int64_t)oc[at]);
+                for (const Out& o : list) {
+                    if (o.at < 0) {
+                        push_bucket(hist, o.key, nullptr, 0);
+                        for (int l = 0; l < nl; ++l) hist.subs[l].append_instance(hist.empty_subs[l], 0);
+                        continue;
+                    }
+                    const size_t at = (size_t)o.at;
+                    push_bucket(hist, o.key, nullptr, (int64_t)oc[at]);
                     for (int l = 0; l < nl; ++l) {
                         Block& gb = hist.subs[l];
                         ++gb.n;

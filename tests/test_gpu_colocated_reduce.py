@@ -4,8 +4,9 @@ reduce of the shard builds (InternalAggregations.reduce, shard order) bit for bi
 
 Covered: the north star and config 5 shapes over 4-8 shards, several metric leaves (stats, avg, extended_stats on one
 histogram), shards whose key ranges differ (a timestamp span per shard), a sparse metric (value counts apart from doc
-counts), double metrics with NaN and -0.0 (Java Math.min / max over the shards), term and ascending count orders, and
-shapes outside the merge (terms{stats}, min_doc_count 0 histograms, a second child) that build and reduce instead.
+counts), double metrics with NaN and -0.0 (Java Math.min / max over the shards), term and ascending count orders,
+histogram options (min_doc_count 3 with key-descending order, extended bounds, min_doc_count 1), and shapes outside the
+merge (terms{stats}, histograms ordered by count, a second child) that build and reduce instead.
 """
 import numpy as np
 import pytest
@@ -110,7 +111,8 @@ def test_shards_with_different_key_ranges_sparse_and_double_metrics(engine):
         .subAggregation(AB.stats("s").field("m")).subAggregation(AB.extendedStats("e").field("m")))]
     segs = [engine.upload_segment(c, n) for c, n in shard_cols]
     fused, plain = _both(engine, aggs, segs)
-    assert_same(fused, plain, "fused vs builds")
+    # double sums are accumulated by device atomics: the two collects' per-shard sums may differ in the last bits
+    assert_same(fused, plain, "fused vs builds", exact_floats=False)
     want = O.run(shard_cols, aggs, number_of_shards=len(shard_cols))
     assert_same(fused, want["reduced"], "fused vs oracle", exact_floats=False)
     for s in segs:
@@ -129,14 +131,40 @@ def test_other_orders(engine, order):
         s.close()
 
 
-@pytest.mark.parametrize("shape", ["terms_stats", "min_doc_count_0", "two_children"])
+@pytest.mark.parametrize("hist", ["mdc3_desc", "bounds", "mdc1"])
+def test_histogram_options(engine, hist):
+    """min_doc_count above 1 with key-descending order, extended bounds wider than the data (min_doc_count 0's empty
+    buckets outside the keys), min_doc_count 1 (no empty buckets)"""
+    n, shards = 700_000, 4
+    h = AB.dateHistogram("h").field("@timestamp").interval("1h")
+    if hist == "mdc3_desc":
+        h = h.minDocCount(3).order(Order.KEY_DESC)
+    elif hist == "bounds":
+        ts = [synthetic_columns(("@timestamp",), n, shard=30 + s)["@timestamp"]["values"] for s in range(shards)]
+        lo, hi = min(int(t.min()) for t in ts), max(int(t.max()) for t in ts)
+        h = h.extendedBounds(lo - 5 * 86_400_000, hi + 3 * 86_400_000)
+    else:
+        h = h.minDocCount(1)
+    aggs = [AB.terms("hosts").field("host").size(8).subAggregation(h.subAggregation(AB.stats("s").field("response_time_ms")))]
+    segs = [engine.synthetic_segment(n, fields=NS_FIELDS, shard=30 + s) for s in range(shards)]
+    probe = [engine.plan(aggs, number_of_shards=shards) for _ in segs]
+    assert colocated(probe)
+    for p in probe:
+        p.close()
+    fused, plain = _both(engine, aggs, segs)
+    assert_same(fused, plain, f"{hist}: fused vs builds")
+    for s in segs:
+        s.close()
+
+
+@pytest.mark.parametrize("shape", ["terms_stats", "count_order", "two_children"])
 def test_shapes_outside_the_merge(engine, shape):
     n, shards = 600_000, 3
     if shape == "terms_stats":
         aggs = [AB.terms("hosts").field("host").size(5).subAggregation(AB.stats("s").field("response_time_ms"))]
-    elif shape == "min_doc_count_0":
+    elif shape == "count_order":
         aggs = [AB.terms("hosts").field("host").size(5).subAggregation(
-            AB.dateHistogram("h").field("@timestamp").interval("1d").minDocCount(0).subAggregation(AB.avg("a").field("response_time_ms")))]
+            AB.dateHistogram("h").field("@timestamp").interval("1d").order(Order.COUNT_DESC).subAggregation(AB.avg("a").field("response_time_ms")))]
     else:
         aggs = [AB.terms("hosts").field("host").size(5)
                 .subAggregation(AB.dateHistogram("h").field("@timestamp").interval("1d"))

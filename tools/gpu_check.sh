@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun session: GPU parity tests, kernel sweep, bench, rocprofv3 kernel-trace stats and PMC HBM-traffic passes.
 #   gpurun --timeout 1200 -- bash tools/gpu_check.sh <tag> [steps...]
-# steps: tests testsdyn testfile testfiles piab fsab d16ab rawab pmcall kbench bench jitter export shape125 configs dynab hllab cut0ab buildtrace profk125 prof profk pmc pmck variants (default: tests kbench bench prof pmc)
+# steps: tests testsdyn testfile testfiles piab fsab d16ab rawab pmcall kbench bench jitter export shape125 configs coloab dynab hllab cut0ab buildtrace profk125 prof profk pmc pmck variants (default: tests kbench bench prof pmc)
 # KBENCH_ONLY=name,name restricts the kbench sweeps (KBENCH_ARGS: extra kbench flags for variants, KBENCH_TAG: log suffix); variants = every build/variants/libesgpu_*.so via ESGPU_LIBRARY.  Every GPU step has its own time limit; the first failure ends it.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -38,6 +38,12 @@ for s in $STEPS; do
               run bench_config4 300 python3 "$R/bench.py" --workload config4 --shards 8 --docs 125000000 --cpu-docs 320000000 &&
               run bench_config5 300 python3 "$R/bench.py" --workload config5 --shards 8 --docs 125000000 --cpu-docs 320000000 &&
               run bench_ns_shards8 300 python3 "$R/bench.py" --shards 8 --docs 125000000 --cpu-docs 0 ;;
+        coloab) # co-located reduce (one build_reduce call per request) vs one build per shard + host reduce (--no-colo)
+              for i in 1 2; do for c in "" "--no-colo"; do
+                  t=${c:+_nocolo}
+                  run "bench_ns8${t}_$i" 300 python3 "$R/bench.py" --shards 8 --docs 125000000 --cpu-docs 0 $c || exit 1
+                  run "bench_c5${t}_$i" 300 python3 "$R/bench.py" --workload config5 --shards 8 --docs 125000000 --cpu-docs 0 $c || exit 1
+              done; done ;;
         schemes) # pipelined-phase A/B on one box: rotating plans vs one plan per shard
               for i in 1 2; do for sc in rotate sets; do
                   run "bench_ns8_${sc}_$i" 300 python3 "$R/bench.py" --shards 8 --docs 125000000 --cpu-docs 0 --scheme $sc || exit 1
