@@ -1047,7 +1047,18 @@ void launch_compact_rows(const CompactParams& p, hipStream_t st) {
 }
 
 __global__ __launch_bounds__(256) void colo_merge_kernel(ColoParams P) {
+    // the descriptors live in pinned host memory: each workgroup reads them once, over the link, into LDS
+    __shared__ ColoShard shs[kColoMaxShards];
+    __shared__ int32_t srow[kColoMaxShards];
     const uint32_t m = blockIdx.x * 256 + threadIdx.x, r = blockIdx.y;
+    {
+        const uint32_t words = P.nsh * (uint32_t)(sizeof(ColoShard) / 8);
+        const unsigned long long* src = (const unsigned long long*)P.shards;
+        unsigned long long* dst = (unsigned long long*)shs;
+        for (uint32_t i = threadIdx.x; i < words; i += 256) dst[i] = src[i];
+        for (uint32_t i = threadIdx.x; i < P.nsh; i += 256) srow[i] = P.rows[(size_t)r * P.nsh + i];
+    }
+    __syncthreads();
     if (m >= P.Hm) return;
     unsigned long long c = 0;
     unsigned long long vc[kCompactLeaves] = {0, 0, 0, 0}, mn[kCompactLeaves], mx[kCompactLeaves];
@@ -1055,9 +1066,9 @@ __global__ __launch_bounds__(256) void colo_merge_kernel(ColoParams P) {
 #pragma unroll
     for (int l = 0; l < kCompactLeaves; ++l) { mn[l] = kMinInit; mx[l] = kMaxInit; }
     for (uint32_t sh = 0; sh < P.nsh; ++sh) {  // shard order: the reference reduce's addition order
-        const int32_t ord = P.rows[(size_t)r * P.nsh + sh];
+        const int32_t ord = srow[sh];
         if (ord < 0) continue;
-        const ColoShard& S = P.shards[sh];
+        const ColoShard& S = shs[sh];
         const int64_t slot = P.kmin + (int64_t)m - S.key0;
         if (slot < 0 || slot >= (int64_t)S.H || (uint32_t)ord >= S.T) continue;
         const size_t cell = (size_t)slot * S.T + (uint32_t)ord;
@@ -1090,6 +1101,26 @@ __global__ __launch_bounds__(256) void colo_merge_kernel(ColoParams P) {
         P.o_sq[l * stride + at] = sq[l];
     }
 }
+__global__ __launch_bounds__(256) void colo_totals_kernel(const ColoTotals* __restrict__ d, uint32_t Tmax,
+                                                          unsigned long long* __restrict__ out) {
+    __shared__ ColoTotals c;  // the descriptor from pinned host memory, once per workgroup
+    if (threadIdx.x < sizeof(ColoTotals) / 8)
+        ((unsigned long long*)&c)[threadIdx.x] = ((const unsigned long long*)(d + blockIdx.y))[threadIdx.x];
+    __syncthreads();
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= c.T) return;
+    unsigned long long s = 0;
+    if (c.cnt32)
+        for (uint32_t h = 0; h < c.H; ++h) s += ((const unsigned int*)c.cnt)[(size_t)h * c.T + t];
+    else
+        for (uint32_t h = 0; h < c.H; ++h) s += ((const unsigned long long*)c.cnt)[(size_t)h * c.T + t];
+    out[(size_t)blockIdx.y * Tmax + t] = s;
+}
+void launch_colo_totals(const ColoTotals* d, uint32_t n, uint32_t Tmax, unsigned long long* out, hipStream_t st) {
+    if (n == 0 || Tmax == 0) return;
+    hipLaunchKernelGGL(colo_totals_kernel, dim3((Tmax + 255) / 256, n), dim3(256), 0, st, d, Tmax, out);
+}
+
 void launch_colo_merge(const ColoParams& p, hipStream_t st) {
     if (p.R == 0 || p.Hm == 0) return;
     hipLaunchKernelGGL(colo_merge_kernel, dim3((p.Hm + 255) / 256, p.R), dim3(256), 0, st, p);

@@ -234,6 +234,7 @@ void launch_compact_rows(const CompactParams& p, hipStream_t s);
 // co-located reduce (esgpu_plans_build_reduce): the final terms buckets' histogram rows merged over the shards of one
 // device, in shard order (InternalHistogram.doReduce per key, InternalStats / InternalAvg / InternalExtendedStats.doReduce
 // per bucket), into dense [R][Hm] rows over the union of the shards' key ranges
+constexpr int kColoMaxShards = 64;  // shards one co-located reduce merges on the device (descriptors in LDS)
 struct ColoShard {
     const unsigned long long* cnt;   // bucket doc counts [H][T] (u32 when cnt32)
     int32_t cnt32;
@@ -245,8 +246,9 @@ struct ColoShard {
     const unsigned long long* lmx[kCompactLeaves];
     const double* lsq[kCompactLeaves];               // null: no sum of squares
 };
+static_assert(sizeof(ColoShard) % 8 == 0, "ColoShard is copied as 8-byte words");
 struct ColoParams {
-    const ColoShard* shards;  // [nsh] (device)
+    const ColoShard* shards;  // [nsh] (pinned, device-mapped; 8-byte multiple)
     const int32_t* rows;      // [R][nsh]: the final bucket's ordinal in each shard, -1 when the shard did not return it
     uint32_t nsh, R, Hm;
     int64_t kmin;
@@ -256,6 +258,15 @@ struct ColoParams {
     double *o_sum, *o_min, *o_max, *o_sq;  // [nleaves][R][Hm]
 };
 void launch_colo_merge(const ColoParams& p, hipStream_t s);
+// the co-located reduce's selection input: every shard's per-ordinal doc counts, summed over the [H][T] grid rows,
+// written to out[shard][Tmax] (pinned, device-mapped) by one launch over all the shards
+struct ColoTotals {
+    const void* cnt;  // [H][T] u64 counts (u32 when cnt32)
+    uint32_t H, T;
+    uint32_t cnt32, pad;
+};
+static_assert(sizeof(ColoTotals) % 8 == 0, "ColoTotals is copied as 8-byte words");
+void launch_colo_totals(const ColoTotals* d, uint32_t n, uint32_t Tmax, unsigned long long* out, hipStream_t s);
 
 // per-8192-doc-block min / max; f64 = the column holds doubles, taken as (long) casts (FieldData.castToLong)
 void launch_zone_map(const int64_t* v, const uint64_t* present, uint32_t n, int64_t* zmin, int64_t* zmax, bool f64,

@@ -27,6 +27,8 @@
 #include <unordered_map>
 #include <memory>
 #include <mutex>
+#include <condition_variable>
+#include <thread>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -1034,7 +1036,9 @@ struct esgpu_plan {
     bool skeleton = false;
     std::vector<uint32_t> sk_ords;
     PinnedBuf h_colo;   // the merged rows (pinned, device-mapped)
-    Scratch s_colo;     // shard descriptors + the rows table
+    PinnedBuf h_colo_meta;  // shard descriptors + the rows table (pinned, device-mapped: read once per workgroup)
+    PinnedBuf h_colo_tot;   // every shard's per-ordinal doc counts (pinned, device-mapped)
+    hipEvent_t ev_colo = nullptr;  // this plan's collects, waited for by the first plan's stream
     int32_t last_path = 0;
     // per-request scratch, reused across requests
     Scratch s_accept, s_tcnt, s_rows, s_dst[6];
@@ -5074,6 +5078,7 @@ extern "C" int esgpu_plan_destroy(esgpu_plan* p) {
         }
         p->pipes.clear();
         if (p->ev_mid) (void)hipEventDestroy(p->ev_mid);
+        if (p->ev_colo) (void)hipEventDestroy(p->ev_colo);
         if (p->ev0) (void)hipEventDestroy(p->ev0);
         if (p->ev1) (void)hipEventDestroy(p->ev1);
         if (p->stream) (void)hipStreamDestroy(p->stream);
@@ -5098,7 +5103,7 @@ extern "C" int esgpu_result_free(esgpu_result* r) {
 // ordered host selection) whose only child is a histogram / date_histogram over an affine rounding with
 // min_doc_count >= 1 and numeric metric children.  Anything else builds every shard and reduces (esgpu_reduce).
 static bool colo_eligible(esgpu_plan* const* plans, int n, bool shape_only = false) {
-    if (n < 2) return false;
+    if (n < 2 || n > kColoMaxShards) return false;
     const esgpu_plan* p0 = plans[0];
     for (int i = 0; i < n; ++i) {
         const esgpu_plan* p = plans[i];
@@ -5135,6 +5140,80 @@ static bool colo_eligible(esgpu_plan* const* plans, int n, bool shape_only = fal
     return true;
 }
 
+// A few host threads for esgpu_plans_build_reduce's per-shard skeleton builds: each build is mostly waits on its own
+// stream (the collect's end, one device-to-host copy of the ordinal counts), so the shards' round trips overlap instead
+// of adding up.  The caller runs jobs too; one batch at a time.
+class HostPool {
+public:
+    static HostPool& get() {
+        static HostPool pool;
+        return pool;
+    }
+    void run(int n, const std::function<void(int)>& f) {
+        std::lock_guard<std::mutex> one(run_mu_);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            if (threads_.empty())
+                for (int i = 0; i < kThreads; ++i) threads_.emplace_back([this] { loop(); });
+            job_ = &f;
+            next_ = 0;
+            n_ = n;
+            left_ = n;
+            ++gen_;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return left_ == 0; });
+        job_ = nullptr;
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (std::thread& t : threads_) t.join();
+    }
+
+private:
+    static constexpr int kThreads = 7;
+    void work() {
+        for (;;) {
+            int i;
+            const std::function<void(int)>* f;
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                if (!job_ || next_ >= n_) return;
+                i = next_++;
+                f = job_;
+            }
+            (*f)(i);
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--left_ == 0) done_.notify_all();
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+            }
+            work();
+        }
+    }
+    std::mutex run_mu_, mu_;
+    std::condition_variable cv_, done_;
+    std::vector<std::thread> threads_;
+    const std::function<void(int)>* job_ = nullptr;
+    int next_ = 0, n_ = 0, left_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
 extern "C" int esgpu_plans_colocated(esgpu_plan* const* plans, int32_t n, int32_t* merged) {
     return guarded([&] {
         require(plans && merged && n >= 1, ESGPU_ERR_INVALID, "null argument");
@@ -5148,19 +5227,102 @@ extern "C" int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esg
         require(plans && out && n >= 1, ESGPU_ERR_INVALID, "build_reduce needs at least one plan");
         std::vector<std::unique_ptr<ResultHolder, void (*)(ResultHolder*)>> parts;
         const bool colo = colo_eligible(plans, n) && std::getenv("ESGPU_COLO") == nullptr;
-        for (int i = 0; i < n; ++i) {
+        std::vector<esgpu_result*> built(n, nullptr);
+        std::vector<int> rcs(n, ESGPU_OK);
+        std::vector<std::string> errs(n);
+        auto one = [&](int i) {
             plans[i]->skeleton = colo;
-            esgpu_result* r = nullptr;
-            const int rc = esgpu_plan_build(plans[i], &r);
+            rcs[i] = esgpu_plan_build(plans[i], &built[i]);
             plans[i]->skeleton = false;
-            if (rc != ESGPU_OK) throw EsError(rc, g_err);
-            parts.emplace_back(holder_of(r), +[](ResultHolder* h) { delete h; });
+            if (rcs[i] != ESGPU_OK) errs[i] = g_err;
+        };
+        const bool trace = std::getenv("ESGPU_TRACE_BUILD") != nullptr;
+        std::vector<std::pair<const char*, double>> marks{{"start", now_ms()}};
+        auto mark = [&](const char* w) { if (trace) marks.emplace_back(w, now_ms()); };
+        // the merged shape: the skeletons' histogram instances are empty placeholders, replaced below -- the terms are
+        // reduced without them (the rebuild starts from the histogram's prototype)
+        Block hproto;
+        bool direct = colo;  // every shard's selection from one launch and one wait (no per-plan build)
+        for (int i = 0; direct && i < n; ++i) {
+            direct = !plans[i]->hc_check;
+            for (const Pipeline& pl : plans[i]->pipes) direct = direct && pl.kind != 1;
+        }
+        if (direct) {
+            esgpu_plan* p0 = plans[0];
+            hipStream_t st = p0->stream;
+            HIPX(hipSetDevice(p0->ctx->device));
+            std::vector<ColoTotals> d(n);
+            uint32_t Tmax = 0;
+            for (int i = 0; i < n; ++i) {
+                esgpu_plan* p = plans[i];
+                const Pipeline& P0 = p->pipes[p->groups[0].pipes[0]];
+                if (p != p0) {  // the first plan's stream waits for this plan's collects
+                    if (!p->ev_colo) HIPX(hipEventCreateWithFlags(&p->ev_colo, hipEventDisableTiming));
+                    HIPX(hipEventRecord(p->ev_colo, p->stream));
+                    HIPX(hipStreamWaitEvent(st, p->ev_colo, 0));
+                }
+                ColoTotals& c = d[i];
+                const bool oc = P0.ocnt_mode == OCNT_TERMS || P0.ocnt_mode == OCNT_TERMS_DERIVED;
+                c.cnt = oc ? (const void*)P0.g_ocnt.p : (const void*)P0.g_cnt.p;
+                c.H = oc ? 1u : P0.H;
+                c.T = P0.T;
+                c.cnt32 = !oc && P0.cnt32 ? 1u : 0u;
+                Tmax = std::max(Tmax, P0.T);
+            }
+            PinnedBuf& mb = p0->h_colo_meta;
+            std::memcpy(mb.ensure(sizeof(ColoTotals) * n), d.data(), sizeof(ColoTotals) * n);
+            PinnedBuf& tb = p0->h_colo_tot;
+            tb.ensure(std::max<size_t>((size_t)n * Tmax * 8, 8));
+            launch_colo_totals((const ColoTotals*)mb.dev(), (uint32_t)n, Tmax, (unsigned long long*)tb.dev(), st);
+            HIPX(hipGetLastError());
+            HIPX(hipStreamSynchronize(st));
+            const unsigned long long* tot = tb.as<unsigned long long>();
+            {
+                const Group& g0 = p0->groups[0];
+                hproto = child_protos(p0, g0)[0].like();
+            }
+            for (int i = 0; i < n; ++i) {  // build_terms_root's host selection (select_terms), its winners only
+                esgpu_plan* p = plans[i];
+                const Group& g = p->groups[0];
+                const Pipeline& P0 = p->pipes[g.pipes[0]];
+                const SpecNode& tn = p->specs[g.root];
+                int64_t other = 0;
+                const std::vector<TermPick> top = select_terms(tn.s, tot + (size_t)i * Tmax, (uint32_t)P0.value_count, &other,
+                                                               [](uint32_t) { return 0.0; });
+                Block r = terms_shell(p, g.root, {});
+                p->sk_ords.clear();
+                begin_instance(r, other);
+                for (const TermPick& tp : top) {
+                    const std::string term = plan_term(p, P0, tp.ord);
+                    push_bucket(r, tp.ord, &term, tp.count);
+                    p->sk_ords.push_back(tp.ord);
+                }
+                end_instance(r);
+                std::unique_ptr<ResultHolder> h(new ResultHolder());
+                h->aggs.push_back(std::move(r));
+                parts.emplace_back(h.release(), +[](ResultHolder* x) { delete x; });
+                p->posted = true;
+            }
+        } else {
+            if (colo) HostPool::get().run(n, one);  // skeletons: selection only, their waits overlapped
+            else for (int i = 0; i < n; ++i) one(i);
+            for (int i = 0; i < n; ++i)
+                if (built[i]) parts.emplace_back(holder_of(built[i]), +[](ResultHolder* h) { delete h; });
+            for (int i = 0; i < n; ++i)
+                if (rcs[i] != ESGPU_OK) throw EsError(rcs[i], errs[i]);
+            if (colo && !parts[0]->aggs.empty() && parts[0]->aggs[0].type == ESGPU_AGG_TERMS && parts[0]->aggs[0].subs.size() == 1) {
+                hproto = parts[0]->aggs[0].subs[0].like();
+                for (auto& h : parts) h->aggs[0].subs.clear();
+            }
         }
         std::vector<const std::vector<Block>*> lists;
         for (auto& h : parts) lists.push_back(&h->aggs);
         std::unique_ptr<ResultHolder> res(new ResultHolder());
+        mark("skeletons");
         res->aggs = reduce_lists(lists);
-        if (colo && !res->aggs.empty() && res->aggs[0].type == ESGPU_AGG_TERMS && res->aggs[0].subs.size() == 1) {
+        mark("reduced");
+        if (colo && !res->aggs.empty() && res->aggs[0].type == ESGPU_AGG_TERMS && res->aggs[0].subs.empty() &&
+            hproto.type != 0) {
             Block& tb = res->aggs[0];
             const uint64_t R = tb.nbuckets();
             esgpu_plan* p0 = plans[0];
@@ -5214,13 +5376,14 @@ extern "C" int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esg
             const size_t o_bytes = cells * 8 * (1 + 5 * (size_t)std::max(nl, 1));
             char* hbase = (char*)hb.ensure(std::max<size_t>(o_bytes, 8));
             char* dbase = (char*)hb.dev();
-            void* dmeta = p0->s_colo.ensure(p0->ctx, sizeof(ColoShard) * n + rows.size() * 4 + 16);
-            HIPX(hipMemcpyAsync(dmeta, sh.data(), sizeof(ColoShard) * n, hipMemcpyHostToDevice, st));
-            int32_t* drows = (int32_t*)((char*)dmeta + sizeof(ColoShard) * n);
-            if (!rows.empty()) HIPX(hipMemcpyAsync(drows, rows.data(), rows.size() * 4, hipMemcpyHostToDevice, st));
+            // the descriptors in pinned memory the kernel reads directly (no pageable staging copy on the stream)
+            PinnedBuf& mb = p0->h_colo_meta;
+            char* hmeta = (char*)mb.ensure(sizeof(ColoShard) * n + rows.size() * 4 + 16);
+            std::memcpy(hmeta, sh.data(), sizeof(ColoShard) * n);
+            if (!rows.empty()) std::memcpy(hmeta + sizeof(ColoShard) * n, rows.data(), rows.size() * 4);
             ColoParams C{};
-            C.shards = (const ColoShard*)dmeta;
-            C.rows = drows;
+            C.shards = (const ColoShard*)mb.dev();
+            C.rows = (const int32_t*)((const char*)mb.dev() + sizeof(ColoShard) * n);
             C.nsh = (uint32_t)n;
             C.R = (uint32_t)R;
             C.Hm = (uint32_t)Hm;
@@ -5233,14 +5396,16 @@ extern "C" int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esg
             C.o_max = (double*)(dbase + cells * 8 * (1 + 3 * (size_t)nl));
             C.o_sq = (double*)(dbase + cells * 8 * (1 + 4 * (size_t)nl));
             // the other plans' streams must have finished their collects (each build synchronised its own stream)
+            mark("rows");
             launch_colo_merge(C, st);
             HIPX(hipGetLastError());
             HIPX(hipStreamSynchronize(st));
+            mark("merged");
             // the terms block's histogram child, rebuilt from the merged rows: keys with at least min_doc_count docs,
             // and for min_doc_count 0 the empty buckets of addEmptyBuckets (InternalHistogram.java:395-449) -- every
             // grid key between a row's first and last non-empty key, and the extended bounds' keys outside them
-            const Block proto = tb.subs[0].like();
-            Block hist = proto;
+            const Block& proto = hproto;
+            Block hist = proto.like();
             const Pipeline& B00 = p0->pipes[kid0.pipes[0]];
             const int64_t iv = B00.interval, off = B00.offset;
             const int64_t mdc = proto.min_doc_count;
@@ -5253,6 +5418,18 @@ extern "C" int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esg
             const double* osq = (const double*)(hbase + cells * 8 * (1 + 4 * (size_t)nl));
             struct Out { int64_t key; int64_t at; };  // at < 0: an empty bucket
             std::vector<Out> list;
+            {
+                const size_t guess = (size_t)R * Hm;
+                hist.key.reserve(guess);
+                hist.term_off.reserve(guess + 1);
+                hist.bcount.reserve(guess);
+                hist.berr.reserve(guess);
+                for (int l = 0; l < nl; ++l) {
+                    Block& gb = hist.subs[l];
+                    gb.count.reserve(guess);
+                    for (auto* v : {&gb.sum, &gb.min, &gb.max, &gb.sumsq}) v->reserve(guess);
+                }
+            }
             for (uint64_t b = 0; b < R; ++b) {
                 list.clear();
                 int64_t first = -1, last = -1;
@@ -5299,9 +5476,20 @@ extern "C" int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esg
                 }
                 end_instance(hist);
             }
-            tb.subs[0] = std::move(hist);
+            tb.subs.push_back(std::move(hist));
+            mark("rebuilt");
         }
         res->export_view();
+        mark("exported");
+        if (trace) {
+            std::string line = "build_reduce";
+            char buf[64];
+            for (size_t i = 1; i < marks.size(); ++i) {
+                std::snprintf(buf, sizeof buf, " %s +%.3f", marks[i].first, marks[i].second - marks[i - 1].second);
+                line += buf;
+            }
+            std::fprintf(stderr, "%s\n", line.c_str());
+        }
         *out = &res.release()->pub;
     });
 }

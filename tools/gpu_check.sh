@@ -44,6 +44,11 @@ for s in $STEPS; do
                   run "bench_ns8${t}_$i" 300 python3 "$R/bench.py" --shards 8 --docs 125000000 --cpu-docs 0 $c || exit 1
                   run "bench_c5${t}_$i" 300 python3 "$R/bench.py" --workload config5 --shards 8 --docs 125000000 --cpu-docs 0 $c || exit 1
               done; done ;;
+        colotrace) # per-phase host marks of build_reduce (and each skeleton build) in the 8-shard north star / config 5
+              ESGPU_TRACE_BUILD=1 run bench_ns8_colotrace 300 python3 "$R/bench.py" --shards 8 --docs 125000000 --cpu-docs 0 \
+                  --steps 4 --warmup 2 &&
+              run bench_ns8 300 python3 "$R/bench.py" --shards 8 --docs 125000000 --cpu-docs 0 &&
+              run bench_c5 300 python3 "$R/bench.py" --workload config5 --shards 8 --docs 125000000 --cpu-docs 0 ;;
         schemes) # pipelined-phase A/B on one box: rotating plans vs one plan per shard
               for i in 1 2; do for sc in rotate sets; do
                   run "bench_ns8_${sc}_$i" 300 python3 "$R/bench.py" --shards 8 --docs 125000000 --cpu-docs 0 --scheme $sc || exit 1
