@@ -456,7 +456,8 @@ int esgpu_result_free(esgpu_result* r);
 int esgpu_reduce(const esgpu_result* const* shard_results, int32_t n, esgpu_result** out);
 /* The same reduce over the shards of one request whose plans live on one device, built and reduced in one call:
  * identical to esgpu_reduce over esgpu_plan_build(plans[i]) in order.  For a top-level terms aggregation whose only
- * child is a histogram (affine rounding, min_doc_count >= 1) with numeric metric children, each plan builds only its
+ * child is a histogram (affine rounding, key order, any min_doc_count / extended bounds) with numeric metric children
+ * (at most 4, 2 to 64 shards), each plan builds only its
  * terms selection, the reference reduce runs over those, and the surviving terms' histogram rows are merged on the
  * device (no shard result is materialised); any other request builds every plan and reduces. */
 int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esgpu_result** out);
