@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <type_traits>
 #include <vector>
 
@@ -871,10 +872,10 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
                 b = 1;
             per_cu = b;
         }
+        const uint64_t docs_per_check = ((uint64_t)kHllFsLog / 4) << (p.fs_f - 1);
         uint32_t wgs = std::max(1u, std::min(cus * (uint32_t)per_cu, n / (kHllFsIter * ESGPU_HLL_FS_NBUF)));
         const uint32_t per = ((n + wgs - 1) / wgs + 3) & ~3u;
         wgs = (n + per - 1) / per;
-        const uint64_t docs_per_check = ((uint64_t)kHllFsLog / 4) << (p.fs_f - 1);
         const uint32_t check = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, docs_per_check / (ESGPU_HLL_FS_NBUF * kHllFsIter)));
         if (p.kind == HLL_I64)
             hipLaunchKernelGGL(hll_fs_kernel<HLL_I64>, dim3(wgs), dim3(kHllFsWG), hll_fs_lds_bytes(), st, p, per, check);
@@ -1119,6 +1120,89 @@ __global__ __launch_bounds__(256) void colo_totals_kernel(const ColoTotals* __re
 void launch_colo_totals(const ColoTotals* d, uint32_t n, uint32_t Tmax, unsigned long long* out, hipStream_t st) {
     if (n == 0 || Tmax == 0) return;
     hipLaunchKernelGGL(colo_totals_kernel, dim3((Tmax + 255) / 256, n), dim3(256), 0, st, d, Tmax, out);
+}
+
+__device__ __forceinline__ unsigned long long wg_sum_u64(unsigned long long v, unsigned long long* ws) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+    __syncthreads();
+    unsigned long long t = 0;
+    for (uint32_t w = 0; w < blockDim.x / 64; ++w) t += ws[w];
+    return t;
+}
+
+// terms orders (include/esgpu.h ESGPU_ORDER_*): 0 count desc, 1 count asc, 2 term asc, 3 term desc
+constexpr int32_t kOrdCountDesc = 0, kOrdCountAsc = 1, kOrdTermDesc = 3;
+__global__ __launch_bounds__(1024) void colo_select_kernel(const unsigned long long* __restrict__ tot,
+                                                           const ColoTotals* __restrict__ d, uint32_t Tmax, ColoSelect S,
+                                                           unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long key[kColoSelMax];
+    __shared__ unsigned long long ws[16];
+    __shared__ uint32_t vcs;
+    const uint32_t i = blockIdx.x;
+    if (threadIdx.x == 0) vcs = d[i].vc;  // from pinned host memory, once
+    __syncthreads();
+    const uint32_t V = vcs;
+    uint32_t N2 = 2;
+    while (N2 < V) N2 <<= 1;
+    const unsigned long long* ti = tot + (size_t)i * Tmax;
+    // candidates (select_terms: min_doc_count drops empty terms, shard_min_doc_count bounds the candidates) as sort keys,
+    // descending = the selection order; bit 63 marks a candidate
+    unsigned long long oth = 0, nc = 0;
+    for (uint32_t t = threadIdx.x; t < N2; t += blockDim.x) {
+        unsigned long long k = 0;
+        if (t < V) {
+            const unsigned long long c = ti[t];
+            if (!(S.min_doc_count > 0 && c == 0)) {
+                oth += c;
+                if (S.shard_min_doc_count <= (long long)c) {
+                    const unsigned long long lo = S.order == kOrdTermDesc ? t : 0xFFFFFFFFull - t;
+                    const unsigned long long hi = S.order == kOrdCountDesc ? c
+                                                : S.order == kOrdCountAsc ? 0x7FFFFFFFull - c : 0ull;
+                    k = (1ull << 63) | (hi << 32) | lo;
+                    ++nc;
+                }
+            }
+        }
+        key[t] = k;
+    }
+    oth = wg_sum_u64(oth, ws);
+    nc = wg_sum_u64(nc, ws);
+    __syncthreads();
+    for (uint32_t k = 2; k <= N2; k <<= 1)  // bitonic sort, descending
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t t = threadIdx.x; t < N2; t += blockDim.x) {
+                const uint32_t u = t ^ j;
+                if (u > t) {
+                    const unsigned long long a = key[t], b = key[u];
+                    if (((t & k) == 0) ? a < b : a > b) { key[t] = b; key[u] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    const unsigned long long size = (unsigned long long)min((long long)V, max(S.shard_size, 0ll));
+    const unsigned long long np = min(size, nc);
+    unsigned long long* o = out + (size_t)i * (2 + S.K);
+    unsigned long long picked = 0;
+    for (uint32_t j = threadIdx.x; j < np; j += blockDim.x) {
+        const unsigned long long k = key[j];
+        const uint32_t lo = (uint32_t)k;
+        const uint32_t ord = S.order == kOrdTermDesc ? lo : 0xFFFFFFFFu - lo;
+        const unsigned long long c = ti[ord];
+        picked += c;
+        o[2 + j] = (c << 32) | ord;
+    }
+    picked = wg_sum_u64(picked, ws);
+    if (threadIdx.x == 0) {
+        o[0] = np;
+        o[1] = oth - picked;
+    }
+}
+void launch_colo_select(const unsigned long long* tot, const ColoTotals* d, uint32_t n, uint32_t Tmax, const ColoSelect& S,
+                        unsigned long long* out, hipStream_t st) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(colo_select_kernel, dim3(n), dim3(1024), 0, st, tot, d, Tmax, S, out);
 }
 
 void launch_colo_merge(const ColoParams& p, hipStream_t st) {

@@ -263,10 +263,22 @@ void launch_colo_merge(const ColoParams& p, hipStream_t s);
 struct ColoTotals {
     const void* cnt;  // [H][T] u64 counts (u32 when cnt32)
     uint32_t H, T;
-    uint32_t cnt32, pad;
+    uint32_t cnt32;
+    uint32_t vc;      // the terms' value count (ordinals >= vc are not terms of the field)
 };
 static_assert(sizeof(ColoTotals) % 8 == 0, "ColoTotals is copied as 8-byte words");
 void launch_colo_totals(const ColoTotals* d, uint32_t n, uint32_t Tmax, unsigned long long* out, hipStream_t s);
+// each shard's terms selection on the device (build_terms_root's select_terms, count and term orders, value count <=
+// kColoSelMax): one workgroup per shard sorts its candidates in LDS; out[shard][2 + K]: the number of picks, the
+// other-doc count, then the picks in order as count << 32 | ordinal
+constexpr uint32_t kColoSelMax = 4096;
+struct ColoSelect {
+    int32_t order;
+    uint32_t K;  // picks per shard at most (the row stride is 2 + K)
+    int64_t min_doc_count, shard_min_doc_count, shard_size;
+};
+void launch_colo_select(const unsigned long long* tot, const ColoTotals* d, uint32_t n, uint32_t Tmax, const ColoSelect& S,
+                        unsigned long long* out, hipStream_t s);
 
 // per-8192-doc-block min / max; f64 = the column holds doubles, taken as (long) casts (FieldData.castToLong)
 void launch_zone_map(const int64_t* v, const uint64_t* present, uint32_t n, int64_t* zmin, int64_t* zmax, bool f64,

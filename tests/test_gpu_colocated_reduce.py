@@ -119,7 +119,7 @@ def test_shards_with_different_key_ranges_sparse_and_double_metrics(engine):
         s.close()
 
 
-@pytest.mark.parametrize("order", [Order.term(True), Order.count(True)])
+@pytest.mark.parametrize("order", [Order.term(True), Order.term(False), Order.count(True)])
 def test_other_orders(engine, order):
     n, shards = 800_000, 4
     aggs = [AB.terms("hosts").field("host").size(6).order(order).subAggregation(
@@ -127,6 +127,28 @@ def test_other_orders(engine, order):
     segs = [engine.synthetic_segment(n, fields=NS_FIELDS, shard=10 + s) for s in range(shards)]
     fused, plain = _both(engine, aggs, segs)
     assert_same(fused, plain, "fused vs builds")
+    for s in segs:
+        s.close()
+
+
+@pytest.mark.parametrize("nterms", [3000, 6000])
+def test_many_terms_and_shard_min_doc_count(engine, nterms):
+    """Over 4,096 terms the shards' selection runs on the host (select_terms), up to 4,096 on the device; a
+    shard_min_doc_count bounds the candidates either way."""
+    rng = np.random.default_rng(nterms)
+    t0 = 1_441_065_600_000
+    shard_cols = []
+    for s in range(3):
+        n = 300_000
+        vals = rng.integers(0, 1000, size=n).astype(np.int64)
+        shard_cols.append((_log_shard(rng, n, t0, 2 * 86_400_000, {"type": N.COL_I64, "values": vals}, nterms=nterms), n))
+    aggs = [AB.terms("t").field("host").size(40).shardSize(60).shardMinDocCount(3).subAggregation(
+        AB.dateHistogram("h").field("@timestamp").interval("3h").subAggregation(AB.stats("s").field("m")))]
+    segs = [engine.upload_segment(c, n) for c, n in shard_cols]
+    fused, plain = _both(engine, aggs, segs)
+    assert_same(fused, plain, "fused vs builds")
+    want = O.run(shard_cols, aggs, number_of_shards=len(shard_cols))
+    assert_same(fused, want["reduced"], "fused vs oracle")
     for s in segs:
         s.close()
 
