@@ -1066,25 +1066,50 @@ __global__ __launch_bounds__(256) void colo_merge_kernel(ColoParams P) {
     double sum[kCompactLeaves] = {0.0, 0.0, 0.0, 0.0}, sq[kCompactLeaves] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int l = 0; l < kCompactLeaves; ++l) { mn[l] = kMinInit; mx[l] = kMaxInit; }
-    for (uint32_t sh = 0; sh < P.nsh; ++sh) {  // shard order: the reference reduce's addition order
-        const int32_t ord = srow[sh];
-        if (ord < 0) continue;
-        const ColoShard& S = shs[sh];
-        const int64_t slot = P.kmin + (int64_t)m - S.key0;
-        if (slot < 0 || slot >= (int64_t)S.H || (uint32_t)ord >= S.T) continue;
-        const size_t cell = (size_t)slot * S.T + (uint32_t)ord;
-        const unsigned long long cs = S.cnt32 ? ((const unsigned int*)S.cnt)[cell] : S.cnt[cell];
-        if (!cs) continue;  // the shard has no bucket at this key
-        c += cs;
+    // shard order: the reference reduce's addition order.  Eight shards at a time: every load of the eight is issued
+    // before the first add (an absent shard reads cell 0 and adds nothing), so their latencies overlap
+    constexpr int kC = 8;
+    for (uint32_t sh0 = 0; sh0 < P.nsh; sh0 += kC) {
+        size_t cell[kC];
+        unsigned long long cs[kC];
+#pragma unroll
+        for (int k = 0; k < kC; ++k) {
+            const uint32_t sh = sh0 + k;
+            bool ok = sh < P.nsh;
+            const ColoShard& S = shs[ok ? sh : 0];
+            const int32_t ord = ok ? srow[sh] : -1;
+            const int64_t slot = P.kmin + (int64_t)m - S.key0;
+            ok = ok && ord >= 0 && slot >= 0 && slot < (int64_t)S.H && (uint32_t)ord < S.T;
+            cell[k] = ok ? (size_t)slot * S.T + (uint32_t)ord : 0;
+            const unsigned long long x = S.cnt32 ? ((const unsigned int*)S.cnt)[cell[k]] : S.cnt[cell[k]];
+            cs[k] = ok ? x : 0ull;  // 0: the shard has no bucket at this key
+        }
+#pragma unroll
+        for (int k = 0; k < kC; ++k) c += cs[k];
         for (int l = 0; l < P.nleaves; ++l) {
-            const unsigned long long v = S.lcnt[l] ? S.lcnt[l][cell] : cs;
-            vc[l] += v;
-            sum[l] += v ? S.lsum[l][cell] : 0.0;  // an empty shard stats adds its 0.0 sum
-            if (v && S.lmn[l]) {
-                mn[l] = min(mn[l], S.lmn[l][cell]);  // order-preserving encodings: Java Math.min / max
-                mx[l] = max(mx[l], S.lmx[l][cell]);
+            unsigned long long v[kC], a[kC], b[kC];
+            double su[kC], q[kC];
+#pragma unroll
+            for (int k = 0; k < kC; ++k) {
+                const ColoShard& S = shs[sh0 + k < P.nsh ? sh0 + k : 0];
+                v[k] = S.lcnt[l] ? S.lcnt[l][cell[k]] : cs[k];
+                v[k] = cs[k] ? v[k] : 0ull;
+                su[k] = S.lsum[l][cell[k]];
+                a[k] = S.lmn[l] ? S.lmn[l][cell[k]] : kMinInit;
+                b[k] = S.lmx[l] ? S.lmx[l][cell[k]] : kMaxInit;
+                q[k] = S.lsq[l] ? S.lsq[l][cell[k]] : 0.0;
             }
-            if (v && S.lsq[l]) sq[l] += S.lsq[l][cell];
+#pragma unroll
+            for (int k = 0; k < kC; ++k) {
+                if (!cs[k]) continue;
+                vc[l] += v[k];
+                sum[l] += v[k] ? su[k] : 0.0;  // an empty shard stats adds its 0.0 sum
+                if (v[k]) {
+                    mn[l] = min(mn[l], a[k]);  // order-preserving encodings: Java Math.min / max
+                    mx[l] = max(mx[l], b[k]);
+                    sq[l] += q[k];
+                }
+            }
         }
     }
     const size_t at = (size_t)r * P.Hm + m, stride = (size_t)P.R * P.Hm;

@@ -5369,7 +5369,25 @@ extern "C" int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esg
             HIPX(hipSetDevice(p0->ctx->device));
             // rows: each final term's ordinal in each shard that returned it
             std::vector<int32_t> rows((size_t)R * n, -1);
-            for (int i = 0; i < n; ++i) {
+            // one term dictionary for every shard (global ordinals, or the same segment dictionary): a final term's
+            // ordinal is its skeleton key in any shard, so membership is a search of each shard's winners
+            bool same_dict = true;
+            {
+                const Pipeline& A = p0->pipes[p0->groups[0].pipes[0]];
+                for (int i = 0; i < n && same_dict; ++i) {
+                    const Pipeline& B = plans[i]->pipes[plans[i]->groups[0].pipes[0]];
+                    same_dict = A.tdict && B.tdict && (A.tdict == B.tdict || A.tdict->identity == B.tdict->identity);
+                }
+            }
+            for (int i = 0; same_dict && i < n; ++i) {
+                std::vector<uint32_t> won(plans[i]->sk_ords);
+                std::sort(won.begin(), won.end());
+                for (uint64_t b = 0; b < R; ++b) {
+                    const uint32_t o = (uint32_t)tb.key[b];
+                    if (std::binary_search(won.begin(), won.end(), o)) rows[(size_t)b * n + i] = (int32_t)o;
+                }
+            }
+            for (int i = 0; !same_dict && i < n; ++i) {
                 const Block& sb = parts[i]->aggs[0];
                 std::unordered_map<std::string_view, uint32_t> at;
                 for (uint64_t b = 0; b < sb.nbuckets(); ++b)
@@ -5495,22 +5513,43 @@ extern "C" int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esg
                 }
                 if (desc) std::reverse(list.begin(), list.end());
                 begin_instance(hist, 0);
-                for (const Out& o : list) {
-                    if (o.at < 0) {
-                        push_bucket(hist, o.key, nullptr, 0);
-                        for (int l = 0; l < nl; ++l) hist.subs[l].append_instance(hist.empty_subs[l], 0);
-                        continue;
-                    }
-                    const size_t at = (size_t)o.at;
-                    push_bucket(hist, o.key, nullptr, (int64_t)oc[at]);
-                    for (int l = 0; l < nl; ++l) {
-                        Block& gb = hist.subs[l];
-                        ++gb.n;
-                        gb.count.push_back((int64_t)olc[l * cells + at]);
-                        gb.sum.push_back(osum[l * cells + at]);
-                        gb.min.push_back(omin[l * cells + at]);
-                        gb.max.push_back(omax[l * cells + at]);
-                        gb.sumsq.push_back(osq[l * cells + at]);
+                // the instance's buckets written by index (no per-bucket push_back); an empty bucket's leaves are the
+                // prototypes' empty instances (addEmptyBuckets' emptyBucketInfo.subAggregations)
+                const size_t L = list.size(), k0 = hist.key.size();
+                hist.key.resize(k0 + L);
+                hist.term_off.resize(k0 + 1 + L, hist.term_pool.size());
+                hist.bcount.resize(k0 + L);
+                hist.berr.resize(k0 + L, 0);
+                for (size_t q = 0; q < L; ++q) {
+                    hist.key[k0 + q] = list[q].key;
+                    hist.bcount[k0 + q] = list[q].at < 0 ? 0 : (int64_t)oc[list[q].at];
+                }
+                for (int l = 0; l < nl; ++l) {
+                    Block& gb = hist.subs[l];
+                    const Block& eb = hist.empty_subs.empty() ? gb : hist.empty_subs[l];
+                    const size_t m0 = gb.count.size();
+                    gb.n += L;
+                    gb.count.resize(m0 + L);
+                    gb.sum.resize(m0 + L);
+                    gb.min.resize(m0 + L);
+                    gb.max.resize(m0 + L);
+                    gb.sumsq.resize(m0 + L);
+                    const size_t lo = (size_t)l * cells;
+                    for (size_t q = 0; q < L; ++q) {
+                        const int64_t at = list[q].at;
+                        if (at < 0) {
+                            gb.count[m0 + q] = eb.count[0];
+                            gb.sum[m0 + q] = eb.sum[0];
+                            gb.min[m0 + q] = eb.min[0];
+                            gb.max[m0 + q] = eb.max[0];
+                            gb.sumsq[m0 + q] = eb.sumsq[0];
+                            continue;
+                        }
+                        gb.count[m0 + q] = (int64_t)olc[lo + at];
+                        gb.sum[m0 + q] = osum[lo + at];
+                        gb.min[m0 + q] = omin[lo + at];
+                        gb.max[m0 + q] = omax[lo + at];
+                        gb.sumsq[m0 + q] = osq[lo + at];
                     }
                 }
                 end_instance(hist);

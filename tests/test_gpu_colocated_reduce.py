@@ -131,6 +131,28 @@ def test_other_orders(engine, order):
         s.close()
 
 
+def test_shards_with_their_own_dictionaries(engine):
+    """Each shard's segment has its own term dictionary (the same term has different ordinals in different shards): the
+    final terms are matched to each shard's rows by their bytes."""
+    rng = np.random.default_rng(17)
+    t0 = 1_441_065_600_000
+    shard_cols = []
+    for s in range(4):
+        n = 250_000
+        cols = _log_shard(rng, n, t0, 86_400_000, {"type": N.COL_I64, "values": rng.integers(0, 500, size=n).astype(np.int64)})
+        cols["host"]["terms"] = sorted("h%03d" % (i + 37 * s) for i in range(200))  # shifted: shared terms, other ordinals
+        shard_cols.append((cols, n))
+    aggs = [AB.terms("t").field("host").size(15).subAggregation(
+        AB.dateHistogram("h").field("@timestamp").interval("1h").subAggregation(AB.stats("s").field("m")))]
+    segs = [engine.upload_segment(c, n) for c, n in shard_cols]
+    fused, plain = _both(engine, aggs, segs)
+    assert_same(fused, plain, "fused vs builds")
+    want = O.run(shard_cols, aggs, number_of_shards=len(shard_cols))
+    assert_same(fused, want["reduced"], "fused vs oracle")
+    for s in segs:
+        s.close()
+
+
 @pytest.mark.parametrize("nterms", [3000, 6000])
 def test_many_terms_and_shard_min_doc_count(engine, nterms):
     """Over 4,096 terms the shards' selection runs on the host (select_terms), up to 4,096 on the device; a
