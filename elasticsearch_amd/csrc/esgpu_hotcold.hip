@@ -120,7 +120,6 @@ __global__ __launch_bounds__(kHcWG) void hc_scatter_kernel(HcParams P) {
     uint32_t* cend = cpos + P.P;                            // [P] end of that chunk
     const uint32_t word_off = (uint32_t)((unsigned char*)word - smem);
     const uint32_t w = blockIdx.x;
-    const bool negm = P.neg_flag ? *P.neg_flag != 0u : P.neg != 0;  // workgroup-uniform
     constexpr uint32_t kMask = (1u << kPartShift) - 1u;
     for (uint32_t i = threadIdx.x; i < NH; i += kHcWG) hot[i] = 0u;
     for (uint32_t p = threadIdx.x; p < P.P; p += kHcWG) {
@@ -187,7 +186,7 @@ __global__ __launch_bounds__(kHcWG) void hc_scatter_kernel(HcParams P) {
             if (ok && P.accept) ok &= bits4(P.accept, doc0);
             for (int q = 0; q < P.npred && ok; ++q) ok &= eval_pred(P.pred[q], doc0);
             // the dead-doc form: a cold doc goes to the rings when the accept bits clear it
-            const uint32_t cold_ok = negm ? (rng & ~ok) : ok;
+            const uint32_t cold_ok = P.neg ? (rng & ~ok) : ok;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const uint32_t v = o[k][j];
@@ -339,9 +338,6 @@ __global__ __launch_bounds__(kHcCountWG) void hc_count_kernel(HcParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t* cnt = (uint32_t*)smem;  // U16: [16384] two 16-bit counters per word, else [32768]
     uint32_t* used = cnt + (U16 ? (1u << kPartShift) / 2 : (1u << kPartShift));  // [G]
-    const bool flag = P.neg_flag ? *P.neg_flag != 0u : false;
-    if (P.cold_if_neg && !flag) return;  // the cold lists count only in the dead-doc form (whole workgroup)
-    const bool subtract = P.neg_flag ? flag && !P.cold_if_neg : P.subtract != 0;
     const HcPiece pc = P.piece[blockIdx.x];
     const uint32_t p = pc.p;
     const HcPart q = P.part[p];
@@ -412,7 +408,7 @@ __global__ __launch_bounds__(kHcCountWG) void hc_count_kernel(HcParams P) {
     const uint32_t base = p << kPartShift;
     const uint32_t S = min(1u << kPartShift, P.T - base);
     auto get = [&](uint32_t j) { return U16 ? (cnt[j >> 1] >> ((j & 1u) * 16)) & 0xFFFFu : cnt[j]; };
-    if (subtract) {  // the dead-doc form: the cleared cold docs taken back out of the cold lists' counts
+    if (P.subtract) {  // the dead-doc form: the cleared cold docs taken back out of the cold lists' counts
         for (uint32_t j = threadIdx.x; j < S; j += kHcCountWG) {
             const uint32_t c = get(j);
             if (c) {
@@ -689,44 +685,6 @@ void launch_hotcold_dead(const HcParams& neg, const HcParams& cold, hipStream_t 
     q.subtract = 1;
     q.overwrite = 0;
     launch_hotcold(q, s);
-}
-
-__global__ __launch_bounds__(1024) void hc_dead_flag_kernel(const uint64_t* __restrict__ bits, uint32_t n_docs,
-                                                              uint32_t* __restrict__ flag) {
-    __shared__ uint32_t part[2][16];
-    const uint32_t nw = (n_docs + 63) / 64;
-    const uint32_t full = nw ? nw - 1 : 0;  // whole words only (the last one is partly past max_doc)
-    const uint32_t step = max(1u, full / 8192u);
-    uint32_t dead = 0, seen = 0;
-    for (uint32_t i = threadIdx.x; i * step < full; i += 1024) {
-        dead += 64u - (uint32_t)__popcll(bits[(size_t)i * step]);
-        seen += 64u;
-    }
-    for (int o = 32; o > 0; o >>= 1) { dead += __shfl_xor(dead, o); seen += __shfl_xor(seen, o); }
-    if ((threadIdx.x & 63) == 0) { part[0][threadIdx.x >> 6] = dead; part[1][threadIdx.x >> 6] = seen; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t d = 0, t = 0;
-        for (int k = 0; k < 16; ++k) { d += part[0][k]; t += part[1][k]; }
-        *flag = (t == 0 || 2u * d <= t) ? 1u : 0u;
-    }
-}
-void launch_hc_dead_flag(const uint64_t* bits, uint32_t n_docs, uint32_t* flag, hipStream_t s) {
-    hipLaunchKernelGGL(hc_dead_flag_kernel, dim3(1), dim3(1024), 0, s, bits, n_docs, flag);
-}
-
-void launch_hotcold_flagged(const HcParams& neg, const HcParams& cold, hipStream_t s) {
-    HcParams k = cold;
-    k.neg_flag = neg.neg_flag;
-    k.cold_if_neg = 1;
-    if (k.n_pieces) {
-        const size_t clds = (k.u16_counters ? (1u << kPartShift) / 2 : (1u << kPartShift)) * 4 + (size_t)k.G * 4;
-        if (k.u16_counters) hipLaunchKernelGGL(hc_count_kernel<true>, dim3(k.n_pieces), dim3(kHcCountWG), clds, s, k);
-        else hipLaunchKernelGGL(hc_count_kernel<false>, dim3(k.n_pieces), dim3(kHcCountWG), clds, s, k);
-    }
-    HcParams q = neg;
-    q.cold_if_neg = 0;
-    launch_hotcold(q, s);  // neg / subtract from the flag; overwrite applies in the scatter form
 }
 
 void launch_hotcold_postings(const HcParams& hot, const HcParams& cold, hipStream_t s) {

@@ -458,13 +458,7 @@ struct HcParams {
     // count when accepted), and the counting pass subtracts what it counts from the cold lists' totals
     int32_t neg;
     int32_t subtract;
-    // decided on the device (a request's folded filters): *neg_flag = 1 when the accept bits clear at most half the
-    // docs (the dead-doc form), 0 for the scatter form; cold_if_neg marks the cold lists' count, which only that form runs
-    const uint32_t* neg_flag;
-    int32_t cold_if_neg;
 };
-// *flag = 1 when a sample of the doc bitset's words clears at most half of the docs
-void launch_hc_dead_flag(const uint64_t* bits, uint32_t n_docs, uint32_t* flag, hipStream_t s);
 __host__ __device__ inline uint32_t hc_hot_counters(uint32_t hot_n) { return hot_n + 3 * (hot_n < kHcHotCopies ? hot_n : kHcHotCopies); }
 // per-workgroup hot slab row: the counters padded to 16 bytes (the reduce reads them as uint4)
 __host__ __device__ inline uint32_t hc_slab_stride(uint32_t hot_n) { return (hc_hot_counters(hot_n) + 3u) & ~3u; }
@@ -479,8 +473,6 @@ void launch_hotcold_postings(const HcParams& hot, const HcParams& cold, hipStrea
 // deletions): the cold lists counted (`cold`), then one scatter pass (`neg`, its neg flag set) counting the accepted
 // hot docs and scattering the cleared cold docs, whose counts are taken back out
 void launch_hotcold_dead(const HcParams& neg, const HcParams& cold, hipStream_t s);
-// the same with the form decided on the device from neg.neg_flag (the scatter form when the flag is 0)
-void launch_hotcold_flagged(const HcParams& neg, const HcParams& cold, hipStream_t s);
 // stats time: the dense partition-ordered cold offsets -> one list per partition starting at pad_begin[p] (a multiple
 // of 64 elements), 0xFFFF between lists
 void launch_hc_pad(const uint16_t* dense, const uint32_t* dense_begin, const uint32_t* pad_begin, uint32_t P,

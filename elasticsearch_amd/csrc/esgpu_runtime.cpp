@@ -1044,7 +1044,6 @@ struct esgpu_plan {
     Scratch s_accept, s_tcnt, s_rows, s_dst[6];
     Scratch s_wgc, s_pbeg, s_pbuf, s_tiles, s_cand, s_keys, s_hist;  // partitioned counting + GPU top-k
     Scratch s_fbits, s_vbits;  // doc bitset of multi-valued filters, per-value bitset of a multi-valued HLL field
-    Scratch s_hflag;           // hot/cold: the device-decided form of a filtered request (launch_hc_dead_flag)
     Scratch s_cells;           // cell list of a cardinality gather
     Scratch s_zkey;            // per-block key ranges of a windowed collect
     DevBuf d_claim;            // collect kernel's chunk-claim counter pair (zeroed once; every launch leaves it zero)
@@ -2290,36 +2289,6 @@ static bool collect_hotcold(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s,
         HIPX(hipGetLastError());
         HIPX(hipEventRecord(pl.e1, st));
         p->last_path = 8;
-        return true;
-    }
-    // a request's filters over a segment with cold lists: folded into a doc bitset, whose sampled clear fraction
-    // picks the dead-doc form or the scatter form on the device (no host round trip)
-    if (hs->cold_lists && npred > 0 && hc_dead_form()) {
-        uint64_t* bits = (uint64_t*)p->s_fbits.ensure(c, std::max<size_t>(s->n_pad / 64, 1) * 8);
-        uint32_t* flag = (uint32_t*)p->s_hflag.ensure(c, 16);
-        HIPX(hipEventRecord(pl.e0, st));
-        launch_filter_bits(s->max_doc, d_accept, pred, npred, bits, st);
-        HIPX(hipGetLastError());
-        launch_hc_dead_flag(bits, s->max_doc, flag, st);
-        HIPX(hipGetLastError());
-        HcParams F = H;
-        F.npred = 0;
-        F.accept = bits;
-        F.neg_flag = flag;
-        HcParams K = F;
-        K.accept = nullptr;
-        K.G = 1;
-        K.part = hs->d_cold_part.as<HcPart>();
-        K.piece = hs->d_cold_piece.as<HcPiece>();
-        K.n_pieces = hs->cold_pieces;
-        K.used = hs->d_cold_used.as<uint32_t>();
-        K.pbuf = hs->d_cold.as<uint16_t>();
-        K.ovf_cur = hs->d_cold_ovf.as<uint32_t>();
-        K.hot_n = 0;
-        launch_hotcold_flagged(F, K, st);
-        HIPX(hipGetLastError());
-        HIPX(hipEventRecord(pl.e1, st));
-        p->last_path = 9;
         return true;
     }
     HIPX(hipEventRecord(pl.e0, st));

@@ -36,12 +36,7 @@ def _check(engine, cols, n, aggs, filters=None, accept=None, reps=1, path_want=N
     for rep in range(reps):  # the second request reuses the segment statistics built by the first
         plan.collect(seg, accept_bits=accept)
         _, _, path = plan.last_collect_stats()
-        if path_want:
-            assert path == path_want, path
-        elif filters:  # folded filters: the dead-doc or the scatter form, picked on the device (path 9), or path 6
-            assert path in (6, 9), path
-        else:
-            assert path == (7 if accept is None else 6), path
+        assert path == (path_want or (7 if not filters and accept is None else 6)), path
         res = plan.build()
         assert_same(res.to_dict(), want["shards"][0], f"shard rep{rep}")
         assert_same(reduce([res]).to_dict(), want["reduced"], f"reduced rep{rep}")
@@ -124,7 +119,7 @@ def test_two_segments_one_plan(engine, filtered):
     plan = engine.plan(aggs, filters=flt)
     for s in segs:
         plan.collect(s)
-        assert plan.last_collect_stats()[2] in ((6, 9) if filtered else (7,))
+        assert plan.last_collect_stats()[2] == (6 if filtered else 7)
     res = plan.build()
     assert_same(res.to_dict(), want["shards"][0], "shard")
     plan.close()
@@ -144,8 +139,7 @@ def test_capacity_overrun_in_first_segment_is_reported(engine, monkeypatch):
     spread = rng.integers(0, T, size=1_000_000).astype(np.uint32)
     c1, c2 = _cols(clustered, T, rng), _cols(spread, T, rng)
     aggs = [AB.terms("c").field("kw").size(10)]
-    # predicates keeping a quarter of the docs: the scatter form (picked on the device), which allocates overflow chunks
-    flt = [QB.rangeQuery("status").gte(3)]
+    flt = [QB.rangeQuery("status").gte(0)]  # predicates: the scatter form (path 6), which allocates overflow chunks
     monkeypatch.setenv("ESGPU_DEBUG_HC_NO_OVERFLOW", "1")
     s1 = engine.upload_segment(c1, len(clustered))
     s2 = engine.upload_segment(c2, len(spread))
@@ -258,23 +252,6 @@ def test_dead_form_clustered_and_two_segments(engine):
     plan.close()
     for seg in segs:
         seg.close()
-
-
-@pytest.mark.parametrize("keep", [0.9, 0.6, 0.3])
-def test_filtered_form_decided_on_device(engine, keep):
-    """A query filter over the high-cardinality field's segment (folded into a doc bitset, path 9): keeping 90 % / 60 %
-    of the docs takes the dead-doc form, 30 % the scatter form -- picked from a sample of the folded bits on the device;
-    with live docs as well, two requests."""
-    rng = np.random.default_rng(110)
-    n, T = 2_000_000, 300_000
-    ranks = np.minimum(rng.zipf(1.1, size=n) - 1, T - 1)
-    ords = (ranks * 7919 + 17) % T
-    cols = _cols(ords, T, rng)
-    cols["status"] = {"type": N.COL_I64, "values": (rng.random(n) * 100).astype(np.int64)}
-    flt = [QB.rangeQuery("status").lt(int(keep * 100))]
-    aggs = [AB.terms("c").field("kw").size(20), AB.terms("t").field("kw").size(8).order(Order.term(True))]
-    _check(engine, cols, n, aggs, filters=flt, reps=2, path_want=9)
-    _check(engine, cols, n, aggs, filters=flt, accept=bits_from_mask(rng.random(n) >= 0.05), path_want=9)
 
 
 def _csr(counts, values):
