@@ -180,20 +180,15 @@ __global__ __launch_bounds__(kHcWG) void hc_scatter_kernel(HcParams P) {
 #pragma unroll
         for (int k = 0; k < kHcIt; ++k) {
             const uint32_t doc0 = t0 + k * (kHcWG * 4) + tid4;
-            uint32_t rng = 0u;
-            if (doc0 < d_end) rng = doc0 + 4 <= d_end ? 0xFu : ((1u << (d_end - doc0)) - 1u);
-            uint32_t ok = rng;
+            uint32_t ok = 0u;
+            if (doc0 < d_end) ok = doc0 + 4 <= d_end ? 0xFu : ((1u << (d_end - doc0)) - 1u);
             if (ok && P.accept) ok &= bits4(P.accept, doc0);
             for (int q = 0; q < P.npred && ok; ++q) ok &= eval_pred(P.pred[q], doc0);
-            // the dead-doc form: a cold doc goes to the rings when the accept bits clear it
-            const uint32_t cold_ok = P.neg ? (rng & ~ok) : ok;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const uint32_t v = o[k][j];
-                const bool hb = (v & kHcHotBit) != 0u;
-                const bool c = hb ? v != kMissingOrd : v < P.T;
-                const uint32_t sel = hb ? ok : cold_ok;
-                okm |= (((sel >> j) & 1u) && c ? 1u : 0u) << (k * 4 + j);
+                const bool c = (v & kHcHotBit) ? v != kMissingOrd : v < P.T;
+                okm |= (((ok >> j) & 1u) && c ? 1u : 0u) << (k * 4 + j);
             }
         }
 #if ESGPU_HC_EXP == 2
@@ -408,15 +403,7 @@ __global__ __launch_bounds__(kHcCountWG) void hc_count_kernel(HcParams P) {
     const uint32_t base = p << kPartShift;
     const uint32_t S = min(1u << kPartShift, P.T - base);
     auto get = [&](uint32_t j) { return U16 ? (cnt[j >> 1] >> ((j & 1u) * 16)) & 0xFFFFu : cnt[j]; };
-    if (P.subtract) {  // the dead-doc form: the cleared cold docs taken back out of the cold lists' counts
-        for (uint32_t j = threadIdx.x; j < S; j += kHcCountWG) {
-            const uint32_t c = get(j);
-            if (c) {
-                if (pc.whole) P.counts[base + j] -= c;  // only this workgroup writes the partition's counters
-                else atomicSub(&P.counts[base + j], c);
-            }
-        }
-    } else if (!pc.whole) {  // one of several pieces of a heavy partition: add the non-zero counters
+    if (!pc.whole) {  // one of several pieces of a heavy partition: add the non-zero counters
         for (uint32_t j = threadIdx.x; j < S; j += kHcCountWG) {
             const uint32_t c = get(j);
             if (c) atomicAdd(&P.counts[base + j], c);
@@ -672,19 +659,6 @@ __global__ __launch_bounds__(256) void hc_cold_sub_kernel(const uint32_t* rc, co
             if (!(v & kHcHotBit) && v < T) atomicSub(&counts[v], 1u);
         }
     }
-}
-
-void launch_hotcold_dead(const HcParams& neg, const HcParams& cold, hipStream_t s) {
-    if (cold.n_pieces) {  // the cold lists' counts first (overwrite on the plan's first segment): the subtraction follows
-        const size_t clds = (cold.u16_counters ? (1u << kPartShift) / 2 : (1u << kPartShift)) * 4 + (size_t)cold.G * 4;
-        if (cold.u16_counters) hipLaunchKernelGGL(hc_count_kernel<true>, dim3(cold.n_pieces), dim3(kHcCountWG), clds, s, cold);
-        else hipLaunchKernelGGL(hc_count_kernel<false>, dim3(cold.n_pieces), dim3(kHcCountWG), clds, s, cold);
-    }
-    HcParams q = neg;
-    q.neg = 1;
-    q.subtract = 1;
-    q.overwrite = 0;
-    launch_hotcold(q, s);
 }
 
 void launch_hotcold_postings(const HcParams& hot, const HcParams& cold, hipStream_t s) {

@@ -454,10 +454,6 @@ struct HcParams {
     uint32_t* err;                     // set to 1 on a capacity violation (device-visible host word)
     int32_t u16_counters;              // every cold ordinal's count in the segment < 65536: packed LDS counters
     int32_t overwrite;                 // store the counts instead of adding (the plan's first segment)
-    // the dead-doc form (launch_hotcold_dead): the scatter keeps the cold docs the accept bits CLEAR (hot docs still
-    // count when accepted), and the counting pass subtracts what it counts from the cold lists' totals
-    int32_t neg;
-    int32_t subtract;
 };
 __host__ __device__ inline uint32_t hc_hot_counters(uint32_t hot_n) { return hot_n + 3 * (hot_n < kHcHotCopies ? hot_n : kHcHotCopies); }
 // per-workgroup hot slab row: the counters padded to 16 bytes (the reduce reads them as uint4)
@@ -469,10 +465,6 @@ void launch_hotcold(const HcParams& p, hipStream_t s);
 // (HcStats' cold lists): `hot` streams the recoded column and counts only the hot slots (G = hot.G workgroups), `cold`
 // counts the cold lists (one static region per partition, G = 1) with the scatter path's counting pass.
 void launch_hotcold_postings(const HcParams& hot, const HcParams& cold, hipStream_t s);
-// An accept bitset clearing more docs than the postings form's subtraction takes (a live-docs bitset with many
-// deletions): the cold lists counted (`cold`), then one scatter pass (`neg`, its neg flag set) counting the accepted
-// hot docs and scattering the cleared cold docs, whose counts are taken back out
-void launch_hotcold_dead(const HcParams& neg, const HcParams& cold, hipStream_t s);
 // stats time: the dense partition-ordered cold offsets -> one list per partition starting at pad_begin[p] (a multiple
 // of 64 elements), 0xFFFF between lists
 void launch_hc_pad(const uint16_t* dense, const uint32_t* dense_begin, const uint32_t* pad_begin, uint32_t P,

@@ -1056,7 +1056,6 @@ struct esgpu_plan {
     Scratch s_nnz;                     // build: non-empty slots per winner row (compact_rows)
     Scratch s_drows;                   // build: composite ordinals a three-level child reads (fetch_rows)
     bool sparse_dead = false;          // the current segment's accept bitset clears few docs (host sample, <= 10 %)
-    double dead_frac = 0.0;            // the fraction of docs the current segment's accept bitset clears (host sample)
     Scratch s_xbits;                   // doc bitset of a pipeline with more than kMaxPreds clauses
     uint32_t seg_seq = 0;              // segments collected since create / reset (cardinality insertion order)
     uint64_t docs_seen = 0;            // max_doc summed over those segments (u32 terms counts need it below 2^32)
@@ -2193,12 +2192,6 @@ static const uint32_t* ensure_rc(esgpu_ctx* c, const HcStats& hs, const DevColum
     return hs.d_rc.as<uint32_t>();
 }
 
-// ESGPU_HC_DEAD=0: accept bitsets clearing over 10 % of the docs take the scatter form (A/B of the dead-doc form)
-static bool hc_dead_form() {
-    static const bool on = [] { const char* e = std::getenv("ESGPU_HC_DEAD"); return !(e && *e == '0'); }();
-    return on;
-}
-
 static bool collect_hotcold(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const DevColumn* oc,
                             const uint64_t* d_accept, const PredDev* pred, int npred, bool first_segment) {
     esgpu_ctx* c = p->ctx;
@@ -2270,27 +2263,6 @@ static bool collect_hotcold(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s,
         return true;
     }
     require(hc_scatter_lds_bytes(H.P, H.hot_n) <= 160 * 1024 - 256, ESGPU_ERR_STATE, "hot/cold LDS layout");
-    // a live-docs bitset clearing more than the subtraction takes but at most half the docs: the cold lists counted,
-    // and one scatter pass sends the cleared cold docs (fewer than the kept ones) through the rings to be taken out
-    const bool caller_bits = d_accept && d_accept == (const uint64_t*)p->s_accept.buf.p;
-    if (hs->cold_lists && npred == 0 && caller_bits && !p->sparse_dead && p->dead_frac <= 0.5 && hc_dead_form()) {
-        HcParams K = H;
-        K.accept = nullptr;
-        K.G = 1;
-        K.part = hs->d_cold_part.as<HcPart>();
-        K.piece = hs->d_cold_piece.as<HcPiece>();
-        K.n_pieces = hs->cold_pieces;
-        K.used = hs->d_cold_used.as<uint32_t>();
-        K.pbuf = hs->d_cold.as<uint16_t>();
-        K.ovf_cur = hs->d_cold_ovf.as<uint32_t>();
-        K.hot_n = 0;
-        HIPX(hipEventRecord(pl.e0, st));
-        launch_hotcold_dead(H, K, st);
-        HIPX(hipGetLastError());
-        HIPX(hipEventRecord(pl.e1, st));
-        p->last_path = 8;
-        return true;
-    }
     HIPX(hipEventRecord(pl.e0, st));
     launch_hotcold(H, st);
     HIPX(hipGetLastError());
@@ -3393,7 +3365,6 @@ extern "C" int esgpu_plan_collect_segment(esgpu_plan* p, const esgpu_segment* s,
                 uint64_t dead = 0, seen = 0;
                 for (size_t w = 0; w + 1 < nw; w += step, seen += 64) dead += 64 - __builtin_popcountll(accept_bits[w]);
                 p->sparse_dead = seen == 0 || dead * 10 <= seen;
-                p->dead_frac = seen ? (double)dead / (double)seen : 0.0;
             }
             void* a = p->s_accept.ensure(p->ctx, words * 8);
             HIPX(hipMemsetAsync(a, 0, words * 8, p->stream));

@@ -7,9 +7,7 @@ share of a partition is far from its static region: overflow chunks), a flat dis
 ordinal with more than 65535 docs (32-bit counters in the counting pass), filters and accept bitsets (requests that
 use a fraction of the capacities), several segments into one plan, and reuse of the statistics across requests.
 Requests without predicates or accept bits take the postings form (path 7: hot slots from the recoded column, the cold
-docs counted from the segment's partition-ordered cold lists); a live-docs bitset clearing up to 10 % keeps it (the dead
-cold docs subtracted one by one), one clearing up to half the docs takes the dead-doc form (path 8: the cold lists
-counted, the cleared cold docs scattered and subtracted); the others scatter the kept cold docs per request (path 6).
+docs counted from the segment's partition-ordered cold lists); the others scatter the cold docs per request (path 6).
 """
 import numpy as np
 import pytest
@@ -79,9 +77,7 @@ def test_flat_distribution_accept_bits(engine):
     ords = rng.integers(0, T, size=n)
     cols = _cols(ords, T, rng)
     accept = rng.random(n) < 0.7
-    # 30 % cleared: the dead-doc form (path 8); 60 % cleared: the scatter form (path 6)
-    _check(engine, cols, n, [AB.terms("c").field("kw").size(40)], accept=bits_from_mask(accept), path_want=8)
-    _check(engine, cols, n, [AB.terms("c").field("kw").size(40)], accept=bits_from_mask(rng.random(n) < 0.4), path_want=6)
+    _check(engine, cols, n, [AB.terms("c").field("kw").size(40)], accept=bits_from_mask(accept))
 
 
 def test_cold_ordinal_over_16_bits(engine):
@@ -199,55 +195,6 @@ def test_live_docs_two_segments_postings(engine):
     for seg, m in zip(segs, masks):
         plan.collect(seg, accept_bits=bits_from_mask(m))
         assert plan.last_collect_stats()[2] == 7
-    assert_same(plan.build().to_dict(), want["shards"][0], "shard")
-    plan.close()
-    for seg in segs:
-        seg.close()
-
-
-@pytest.mark.parametrize("dead", [0.2, 0.45])
-def test_live_docs_many_deletions_dead_form(engine, dead):
-    """A live-docs bitset clearing 20 % / 45 % of the docs: the dead-doc form (path 8) -- the cold lists counted, one
-    scatter pass counting the kept hot docs and sending the cleared cold docs through the rings, their counts taken
-    back out; every terms order, two requests over one segment."""
-    rng = np.random.default_rng(108)
-    n, T = 2_000_000, 300_000
-    ranks = np.minimum(rng.zipf(1.1, size=n) - 1, T - 1)
-    ords = (ranks * 7919 + 17) % T
-    ords[rng.random(n) < 0.02] = 0xFFFFFFFF
-    cols = _cols(ords, T, rng)
-    accept = bits_from_mask(rng.random(n) >= dead)
-    aggs = [AB.terms("c").field("kw").size(20),
-            AB.terms("a").field("kw").size(9).order(Order.count(True)),
-            AB.terms("t").field("kw").size(11).order(Order.term(False)).minDocCount(0)]
-    _check(engine, cols, n, aggs, accept=accept, reps=2, path_want=8)
-
-
-def test_dead_form_clustered_and_two_segments(engine):
-    """Clustered ordinals with 30 % cleared (the cleared cold docs go through overflow chunks), then two segments with
-    25 % and 40 % cleared counted into one plan: the second segment's lists add, each subtracts its own cleared docs."""
-    rng = np.random.default_rng(109)
-    n, T = 2_500_000, 250_000
-    ords = np.sort(rng.integers(0, T, size=n))
-    cols = _cols(ords, T, rng)
-    _check(engine, cols, n, [AB.terms("c").field("kw").size(30)], accept=bits_from_mask(rng.random(n) >= 0.3), path_want=8)
-    T = 180_000
-    sizes = [900_000, 1_300_000]
-    parts, masks = [], []
-    for k, m in enumerate(sizes):
-        ranks = np.minimum(rng.zipf(1.1, size=m) - 1, T - 1)
-        parts.append(((ranks * 104729 + 7 * k) % T).astype(np.uint32))
-        masks.append(rng.random(m) >= (0.25, 0.4)[k])
-    cs = [_cols(o, T, rng) for o in parts]
-    allc = {"kw": dict(cs[0]["kw"], values=np.concatenate(parts)),
-            "status": {"type": N.COL_I64, "values": np.concatenate([c["status"]["values"] for c in cs])}}
-    aggs = [AB.terms("c").field("kw").size(25), AB.terms("t").field("kw").size(7).order(Order.term(True))]
-    want = O.run([(allc, sum(sizes))], aggs, accept=[bits_from_mask(np.concatenate(masks))])
-    segs = [engine.upload_segment(c, m) for c, m in zip(cs, sizes)]
-    plan = engine.plan(aggs)
-    for seg, m in zip(segs, masks):
-        plan.collect(seg, accept_bits=bits_from_mask(m))
-        assert plan.last_collect_stats()[2] == 8
     assert_same(plan.build().to_dict(), want["shards"][0], "shard")
     plan.close()
     for seg in segs:

@@ -139,13 +139,6 @@ for s in $STEPS; do
                   ESGPU_REPLAY_COMPACT=$c run "kbench_replay${c}_$docs" 400 python3 "$R/tools/kbench.py" --docs $docs --reps 3 \
                       --only hosts_urls || exit 1
               done; done ;;
-        c3dead) # config 3 with a live-docs bitset clearing 20 %: the dead-doc form (path 8) vs the scatter form (ESGPU_HC_DEAD=0)
-              run pytest_hotcold 600 python3 -u -m pytest "$R/tests/test_gpu_hotcold.py" -m gpu -x -v -p no:cacheprovider \
-                  --timeout 300 --timeout-method thread || exit 1
-              for i in 1 2; do for v in 1 0; do for d in 0.2 0.4; do
-                  ESGPU_HC_DEAD=$v run "kbench_c3_dead${v}_del${d}_$i" 300 python3 "$R/tools/kbench.py" --docs 125000000 \
-                      --reps 5 --only config3_url --deletes $d || exit 1
-              done; done; done ;;
         c3stats) # config 3: the per-segment statistics build (bench precomputed) and the filtered / deleted forms
               run bench_config3 300 python3 "$R/bench.py" --workload config3 --shards 8 --docs 125000000 --cpu-docs 0 --steps 5 &&
               run kbench_c3_125m_del 300 python3 "$R/tools/kbench.py" --docs 125000000 --reps 5 --only config3_url --deletes 0.01 ;;
