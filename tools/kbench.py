@@ -38,6 +38,8 @@ def variants():
                     [QB.termQuery("status", 200), QB.rangeQuery("bytes").gte(1024).lte(65536)]),
         "config4_card": ([AB.cardinality("ips").field("client_ip.hash").precisionThreshold(40000)], None),
         "config3_url": ([AB.terms("urls").field("url").size(10)], None),
+        # config 3 under a query filter keeping 80 % of the docs (bytes uniform in [0, 1e6)): the scatter form
+        "config3_url_f": ([AB.terms("urls").field("url").size(10)], [QB.rangeQuery("bytes").lt(800000)]),
         # terms under terms over 1,000 x 10M ordinals: outer counts in the collect, the inner terms replayed at build
         # (breadth-first) -- the replay's time is in parts_ms.build
         "hosts_urls": ([AB.terms("hosts").field("host").size(10).subAggregation(AB.terms("urls").field("url").size(3))], None),
@@ -100,7 +102,7 @@ def main():
     e = ea.Engine(0)
     vs = {k: v for k, v in variants().items() if not only or k in only}
     fields = {"host", "@timestamp", "response_time_ms", "status", "bytes", "client_ip.hash"}
-    if "config3_url" in vs or "hosts_urls" in vs:
+    if "config3_url" in vs or "config3_url_f" in vs or "hosts_urls" in vs:
         fields.add("url")
     t = time.time()
     seg = e.synthetic_segment(args.docs, fields=tuple(sorted(fields)), ts_jitter_ms=args.ts_jitter)
