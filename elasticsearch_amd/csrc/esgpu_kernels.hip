@@ -1323,6 +1323,24 @@ void launch_pack_u8(const unsigned int* src, uint32_t n, uint8_t* dst, hipStream
     hipLaunchKernelGGL(pack_u8_kernel, dim3(std::min<uint32_t>(1024, (n + 255) / 256)), dim3(256), 0, st, src, n, dst);
 }
 
+__global__ __launch_bounds__(256) void fill_multi_kernel(FillList L) {
+    const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
+    for (int k = 0; k < L.count; ++k) {
+        unsigned long long* p = L.p[k];
+        const unsigned long long v = L.v[k];
+        for (size_t i = g; i < L.n[k]; i += stride) p[i] = v;
+    }
+}
+void launch_fill_multi(const FillList& l, hipStream_t st) {
+    uint64_t total = 0;
+    for (int k = 0; k < l.count; ++k) total += l.n[k];
+    if (total == 0) return;
+    size_t grid = (total / (uint64_t)l.count + 255) / 256;
+    if (grid > 4096) grid = 4096;
+    if (grid == 0) grid = 1;
+    hipLaunchKernelGGL(fill_multi_kernel, dim3((uint32_t)grid), dim3(256), 0, st, l);
+}
+
 void launch_fill_u64(unsigned long long* p, size_t n, unsigned long long v, hipStream_t st) {
     if (n == 0) return;
     size_t grid = (n + 255) / 256;

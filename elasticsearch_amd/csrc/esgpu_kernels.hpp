@@ -381,6 +381,15 @@ void launch_term_totals(const unsigned long long* cnt, uint32_t H, uint32_t T, u
 void launch_copy_u64(const unsigned long long* src, unsigned long long* dst, size_t n, hipStream_t s);
 void launch_gather_rows(const GatherParams& p, hipStream_t s);
 void launch_fill_u64(unsigned long long* p, size_t n, unsigned long long v, hipStream_t s);
+// several u64 arrays filled by one launch (a plan reset: counts, sums, min / max identities)
+constexpr int kFillSpans = 8;
+struct FillList {
+    unsigned long long* p[kFillSpans];
+    uint64_t n[kFillSpans];
+    unsigned long long v[kFillSpans];
+    int32_t count;
+};
+void launch_fill_multi(const FillList& l, hipStream_t s);
 
 }  // namespace esgpu
 

@@ -5050,13 +5050,28 @@ extern "C" int esgpu_plan_reset(esgpu_plan* p) {
                 HIPX(hipMemsetAsync(cs.cnt.p, 0, cs.cnt.bytes, p->stream));
                 HIPX(hipMemsetAsync(cs.nonzero.p, 0, cs.nonzero.bytes, p->stream));
             }
-            HIPX(hipMemsetAsync(pl.g_cnt.p, 0, cells * 8, p->stream));
-            if (pl.g_ocnt.p) HIPX(hipMemsetAsync(pl.g_ocnt.p, 0, pl.g_ocnt.bytes, p->stream));
-            if (pl.g_vcnt.p) HIPX(hipMemsetAsync(pl.g_vcnt.p, 0, cells * 8, p->stream));
-            if (pl.g_sum.p) HIPX(hipMemsetAsync(pl.g_sum.p, 0, cells * 8, p->stream));
-            if (pl.g_min.p) launch_fill_u64(pl.g_min.as<unsigned long long>(), cells, kMinInit, p->stream);
-            if (pl.g_max.p) launch_fill_u64(pl.g_max.as<unsigned long long>(), cells, kMaxInit, p->stream);
-            if (pl.g_sq.p) HIPX(hipMemsetAsync(pl.g_sq.p, 0, cells * 8, p->stream));
+            // the grid's arrays in one launch (one per pipeline instead of one per array: a multi-shard request resets
+            // every shard's plan, and each launch costs host time)
+            FillList fl{};
+            auto span = [&](void* ptr, size_t n, unsigned long long v) {
+                if (!ptr || n == 0) return;
+                fl.p[fl.count] = (unsigned long long*)ptr;
+                fl.n[fl.count] = n;
+                fl.v[fl.count] = v;
+                if (++fl.count == kFillSpans) { launch_fill_multi(fl, p->stream); fl.count = 0; }
+            };
+            span(pl.g_cnt.p, cells, 0ull);
+            if (pl.g_ocnt.p) {
+                if (pl.g_ocnt.bytes % 8 == 0) span(pl.g_ocnt.p, pl.g_ocnt.bytes / 8, 0ull);
+                else HIPX(hipMemsetAsync(pl.g_ocnt.p, 0, pl.g_ocnt.bytes, p->stream));
+            }
+            span(pl.g_vcnt.p, cells, 0ull);
+            span(pl.g_sum.p, cells, 0ull);
+            span(pl.g_min.p, cells, kMinInit);
+            span(pl.g_max.p, cells, kMaxInit);
+            span(pl.g_sq.p, cells, 0ull);
+            if (fl.count) launch_fill_multi(fl, p->stream);
+            HIPX(hipGetLastError());
         }
         p->posted = false;
         p->collected = false;
