@@ -5127,7 +5127,9 @@ static bool colo_eligible(esgpu_plan* const* plans, int n, bool shape_only = fal
         const SpecNode& tn = p->specs[g.root];
         if (tn.s.type != ESGPU_AGG_TERMS || tn.s.order == ESGPU_ORDER_AGG_ASC || tn.s.order == ESGPU_ORDER_AGG_DESC)
             return false;
-        if (g.kids.size() != 1 || g.pipes.empty()) return false;
+        if (g.pipes.empty()) return false;
+        if (g.kids.empty()) continue;  // terms without sub-aggregations: the shards' builds run side by side, then reduce
+        if (g.kids.size() != 1) return false;
         const ChildSrc& kid = g.kids[0];
         if (!kid.bucket || kid.filter || kid.deep >= 0 || !kid.rpipes.empty() || kid.grand.empty() ||
             kid.grand.size() > (size_t)kCompactLeaves)
@@ -5241,11 +5243,12 @@ extern "C" int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esg
         require(plans && out && n >= 1, ESGPU_ERR_INVALID, "build_reduce needs at least one plan");
         std::vector<std::unique_ptr<ResultHolder, void (*)(ResultHolder*)>> parts;
         const bool colo = colo_eligible(plans, n) && std::getenv("ESGPU_COLO") == nullptr;
+        const bool merged_shape = colo && !plans[0]->groups[0].kids.empty();
         std::vector<esgpu_result*> built(n, nullptr);
         std::vector<int> rcs(n, ESGPU_OK);
         std::vector<std::string> errs(n);
         auto one = [&](int i) {
-            plans[i]->skeleton = colo;
+            plans[i]->skeleton = merged_shape;
             rcs[i] = esgpu_plan_build(plans[i], &built[i]);
             plans[i]->skeleton = false;
             if (rcs[i] != ESGPU_OK) errs[i] = g_err;
@@ -5256,7 +5259,10 @@ extern "C" int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esg
         // the merged shape: the skeletons' histogram instances are empty placeholders, replaced below -- the terms are
         // reduced without them (the rebuild starts from the histogram's prototype)
         Block hproto;
-        bool direct = colo;  // every shard's selection from one launch and one wait (no per-plan build)
+        // terms{histogram{metrics}}: every shard's selection from one launch and one wait (no per-plan build), the rows
+        // merged on the device; plain terms: the shards' own builds, side by side on the host pool (their top-k launches
+        // overlap on the plans' streams)
+        bool direct = merged_shape;
         for (int i = 0; direct && i < n; ++i) {
             direct = !plans[i]->hc_check;
             for (const Pipeline& pl : plans[i]->pipes) direct = direct && pl.kind != 1;
@@ -5364,7 +5370,8 @@ extern "C" int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esg
                 if (built[i]) parts.emplace_back(holder_of(built[i]), +[](ResultHolder* h) { delete h; });
             for (int i = 0; i < n; ++i)
                 if (rcs[i] != ESGPU_OK) throw EsError(rcs[i], errs[i]);
-            if (colo && !parts[0]->aggs.empty() && parts[0]->aggs[0].type == ESGPU_AGG_TERMS && parts[0]->aggs[0].subs.size() == 1) {
+            if (merged_shape && !parts[0]->aggs.empty() && parts[0]->aggs[0].type == ESGPU_AGG_TERMS &&
+                parts[0]->aggs[0].subs.size() == 1) {
                 hproto = parts[0]->aggs[0].subs[0].like();
                 for (auto& h : parts) h->aggs[0].subs.clear();
             }

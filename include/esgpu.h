@@ -459,7 +459,8 @@ int esgpu_reduce(const esgpu_result* const* shard_results, int32_t n, esgpu_resu
  * child is a histogram (affine rounding, key order, any min_doc_count / extended bounds) with numeric metric children
  * (at most 4, 2 to 64 shards), each plan builds only its
  * terms selection, the reference reduce runs over those, and the surviving terms' histogram rows are merged on the
- * device (no shard result is materialised); any other request builds every plan and reduces. */
+ * device (no shard result is materialised); a top-level terms aggregation without sub-aggregations builds its plans
+ * side by side (their device selections overlap); any other request builds every plan and reduces. */
 int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esgpu_result** out);
 /* *merged = 1 if the request's shape is one esgpu_plans_build_reduce merges on the device (the shards' data may still
  * send a request down the build-and-reduce path, e.g. an unmapped shard), 0 if it always builds and reduces. */

@@ -153,6 +153,37 @@ def test_shards_with_their_own_dictionaries(engine):
         s.close()
 
 
+@pytest.mark.parametrize("T", [1000, 150_000])
+def test_plain_terms_builds_side_by_side(engine, T):
+    """terms without sub-aggregations (config 3's shape): the shards' builds run side by side on the host pool and the
+    reference reduce follows -- 1,000 terms (host selection) and 150,000 (the high-cardinality path and its GPU top-k)."""
+    rng = np.random.default_rng(T)
+    shard_cols = []
+    for s in range(4):
+        n = 600_000
+        ranks = np.minimum(rng.zipf(1.1, size=n) - 1, T - 1)
+        cols = {"kw": {"type": N.COL_ORD_U32, "values": ((ranks * 7919 + 17 * s) % T).astype(np.uint32),
+                       "terms": ["u%07d" % i for i in range(T)]}}
+        shard_cols.append((cols, n))
+    aggs = [AB.terms("c").field("kw").size(15), AB.terms("a").field("kw").size(6).order(Order.count(True))]
+    segs = [engine.upload_segment(c, n) for c, n in shard_cols]
+    probe = [engine.plan(aggs, number_of_shards=len(segs)) for _ in segs]
+    assert not colocated(probe)  # two top-level aggregations: built and reduced
+    for p in probe:
+        p.close()
+    aggs = aggs[:1]
+    probe = [engine.plan(aggs, number_of_shards=len(segs)) for _ in segs]
+    assert colocated(probe)
+    for p in probe:
+        p.close()
+    fused, plain = _both(engine, aggs, segs)
+    assert_same(fused, plain, "fused vs builds")
+    want = O.run(shard_cols, aggs, number_of_shards=len(shard_cols))
+    assert_same(fused, want["reduced"], "fused vs oracle")
+    for s in segs:
+        s.close()
+
+
 @pytest.mark.parametrize("nterms", [3000, 6000])
 def test_many_terms_and_shard_min_doc_count(engine, nterms):
     """Over 4,096 terms the shards' selection runs on the host (select_terms), up to 4,096 on the device; a
