@@ -73,6 +73,14 @@ for s in $STEPS; do
                   ESGPU_HLL_FS=$f run "kbench_fs${f}_$docs" 300 python3 "$R/tools/kbench.py" --docs $docs --reps 5 \
                       --only config4_card || exit 1
               done; done ;;
+        gatherab) # config 4 at one fresh 125M plan: HLL tests, kbench, and the rocprof kernel trace of the request
+              run pytest_hll 600 python3 -u -m pytest "$R/tests/test_gpu_hll_floor.py" "$R/tests/test_gpu_parity.py" -k "card or hll or floor" \
+                  -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread || exit 1
+              for i in 1 2; do
+                  run "kbench_c4_125m_$i" 300 python3 "$R/tools/kbench.py" --docs 125000000 --reps 7 --only config4_card || exit 1
+              done
+              cd /tmp && run rocprof_c4 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profc4" -o kb -- \
+                  python3 "$R/tools/kbench.py" --docs 125000000 --reps 3 --only config4_card ;;
         d16ab) # 16-bit deltas (packed cells' metric, range predicates) vs 32-bit (ESGPU_D16=0), same box
               for d in 1 0; do
                   ESGPU_D16=$d run "kbench_d16_$d" 400 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 \
