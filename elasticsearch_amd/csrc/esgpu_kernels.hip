@@ -509,18 +509,35 @@ __global__ __launch_bounds__(kHllFsWG) void hll_fs_kernel(HllParams P, uint32_t 
     const uint32_t t4 = threadIdx.x * 4;
     const uint32_t last4 = (w1 - 1) & ~3u;  // unconditional loads (see hll_registers_lds_kernel)
     auto load = [&](uint32_t i0, uint64_t raw[4]) { load_i64x4((const int64_t*)P.col, min(i0, last4), (int64_t*)raw); };
+    // the thread's 4 hashes, then ONE log reservation per wave for all of the wave's entries (one returning LDS atomic
+    // and one wait per 256 docs instead of one per doc slot); called by every thread of the workgroup
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t lt = (1ull << lane) - 1ull;
     auto hash4 = [&](uint32_t i0, const uint64_t raw[4]) {
-        if (i0 >= w1) return;
-        const uint32_t lim = w1 - i0;
+        const uint32_t lim = i0 < w1 ? w1 - i0 : 0u;
+        uint32_t e[4], hit = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint64_t h = hll_fast_hash<KIND>(P, raw[j]);
-            if ((uint32_t)j < lim && (h & zmask) == 0) {
-                const uint32_t e = (hll_run_len(h, P.p) << 24) | hll_index(h, P.p);
-                const uint32_t k = atomicAdd(nlog, 1u);
-                if (k < kHllFsLog) rlog[k] = e;
-                else atomicMax(&P.regs[e & 0xFFFFFFu], e >> 24);  // never expected: flushed at half full
-            }
+            const bool t = (uint32_t)j < lim && (h & zmask) == 0;
+            e[j] = (hll_run_len(h, P.p) << 24) | hll_index(h, P.p);
+            hit |= (t ? 1u : 0u) << j;
+        }
+        const uint64_t m0 = __ballot(hit & 1u), m1 = __ballot(hit & 2u), m2 = __ballot(hit & 4u), m3 = __ballot(hit & 8u);
+        const uint32_t c0 = (uint32_t)__popcll(m0), c1 = (uint32_t)__popcll(m1), c2 = (uint32_t)__popcll(m2);
+        const uint32_t tot = c0 + c1 + c2 + (uint32_t)__popcll(m3);
+        if (tot == 0) return;  // wave-uniform
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(nlog, tot);
+        base = __shfl(base, 0, 64);
+        const uint32_t off[4] = {(uint32_t)__popcll(m0 & lt), c0 + (uint32_t)__popcll(m1 & lt),
+                                 c0 + c1 + (uint32_t)__popcll(m2 & lt), c0 + c1 + c2 + (uint32_t)__popcll(m3 & lt)};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (!((hit >> j) & 1u)) continue;
+            const uint32_t k = base + off[j];
+            if (k < kHllFsLog) rlog[k] = e[j];
+            else atomicMax(&P.regs[e[j] & 0xFFFFFFu], e[j] >> 24);  // never expected: flushed at half full
         }
     };
     uint64_t a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
