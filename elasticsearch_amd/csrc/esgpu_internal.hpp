@@ -150,6 +150,12 @@ struct PinnedBuf {
         if (!dp && p) HIPX(hipHostGetDevicePointer(&dp, p, 0));
         return dp;
     }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        dp = nullptr;
+        bytes = 0;
+    }
     template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
 

@@ -235,6 +235,8 @@ void launch_compact_rows(const CompactParams& p, hipStream_t s);
 // device, in shard order (InternalHistogram.doReduce per key, InternalStats / InternalAvg / InternalExtendedStats.doReduce
 // per bucket), into dense [R][Hm] rows over the union of the shards' key ranges
 constexpr int kColoMaxShards = 64;  // shards one co-located reduce merges on the device (descriptors in LDS)
+constexpr size_t kColoMergeBytes = 256ull << 20;  // the merge's pinned [R][Hm] rows at most (else builds + reduce)
+constexpr size_t kColoKeepBytes = 32ull << 20;    // a merge buffer above this is released after the request
 struct ColoShard {
     const unsigned long long* cnt;   // bucket doc counts [H][T] (u32 when cnt32)
     int32_t cnt32;

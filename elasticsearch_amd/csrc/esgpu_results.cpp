@@ -464,8 +464,12 @@ void stream_leaf(Block& m, const Block* proto, const std::vector<OutBucket>& buc
         const uint64_t b0 = h.boff[dk.refs[x].i], b1 = h.boff[dk.refs[x].i + 1];
         const uint64_t len = b1 - b0;
         if (len > 1) {  // the shard's run lands on consecutive emitted buckets (a complete time series): one vector pass
-            const int32_t o0 = dk.out[dk.slot[e]], o1 = dk.out[dk.slot[e + len - 1]];
-            if (o0 >= 0 && o1 >= 0 && (uint64_t)(o1 - o0) == len - 1) {
+            // every position checked, not only the ends: a count-ordered histogram permutes out[], and min_doc_count
+            // drops slots (out = -1), so a run whose ends are len - 1 apart may still map its middle elsewhere
+            const int32_t o0 = dk.out[dk.slot[e]];
+            bool run = o0 >= 0;
+            for (uint64_t t = 1; run && t < len; ++t) run = dk.out[dk.slot[e + t]] == o0 + (int32_t)t;
+            if (run) {
                 // one loop per array (two streams each, no aliasing between output arrays to disprove): each vectorises
                 {
                     int64_t* __restrict__ o = cnt + o0;

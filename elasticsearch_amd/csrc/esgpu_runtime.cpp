@@ -5153,6 +5153,20 @@ static bool colo_eligible(esgpu_plan* const* plans, int n, bool shape_only = fal
             B0.offset != plans[0]->pipes[plans[0]->groups[0].kids[0].pipes[0]].offset)
             return false;
     }
+    if (!shape_only && !p0->groups[0].kids.empty()) {
+        // the merge writes dense [R x Hm] rows into pinned host memory: R <= the terms size, Hm the union of the
+        // shards' key ranges (shards far apart in time inflate it); over the budget the shards build and reduce instead
+        int64_t kmin = INT64_MAX, kmax = INT64_MIN;
+        for (int i = 0; i < n; ++i) {
+            const Pipeline& B0 = plans[i]->pipes[plans[i]->groups[0].kids[0].pipes[0]];
+            kmin = std::min<int64_t>(kmin, B0.key0);
+            kmax = std::max<int64_t>(kmax, B0.key0 + (int64_t)B0.H - 1);
+        }
+        const SpecNode& tn = p0->specs[p0->groups[0].root];
+        const double R = (double)std::max<int64_t>(std::min<int64_t>(tn.s.size, 65536), 1);
+        const double nl = (double)p0->groups[0].kids[0].grand.size();
+        if (kmax >= kmin && R * (double)(kmax - kmin + 1) * 8.0 * (1.0 + 5.0 * nl) > (double)kColoMergeBytes) return false;
+    }
     return true;
 }
 
@@ -5179,9 +5193,16 @@ public:
         }
         cv_.notify_all();
         work();
-        std::unique_lock<std::mutex> lk(mu_);
-        done_.wait(lk, [&] { return left_ == 0; });
-        job_ = nullptr;
+        std::exception_ptr err;
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            done_.wait(lk, [&] { return left_ == 0; });
+            job_ = nullptr;
+            err = err_;
+            err_ = nullptr;
+        }
+        // every job has returned (no worker still reads f or the caller's locals): the first failure goes to the caller
+        if (err) std::rethrow_exception(err);
     }
     ~HostPool() {
         {
@@ -5204,8 +5225,14 @@ private:
                 i = next_++;
                 f = job_;
             }
-            (*f)(i);
+            std::exception_ptr e;
+            try {
+                (*f)(i);
+            } catch (...) {  // a throw must neither terminate a worker nor unwind run() while other jobs still run
+                e = std::current_exception();
+            }
             std::lock_guard<std::mutex> lk(mu_);
+            if (e && !err_) err_ = e;
             if (--left_ == 0) done_.notify_all();
         }
     }
@@ -5225,6 +5252,7 @@ private:
     std::condition_variable cv_, done_;
     std::vector<std::thread> threads_;
     const std::function<void(int)>* job_ = nullptr;
+    std::exception_ptr err_;
     int next_ = 0, n_ = 0, left_ = 0;
     uint64_t gen_ = 0;
     bool stop_ = false;
@@ -5398,7 +5426,7 @@ extern "C" int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esg
                 const Pipeline& A = p0->pipes[p0->groups[0].pipes[0]];
                 for (int i = 0; i < n && same_dict; ++i) {
                     const Pipeline& B = plans[i]->pipes[plans[i]->groups[0].pipes[0]];
-                    same_dict = A.tdict && B.tdict && (A.tdict == B.tdict || A.tdict->identity == B.tdict->identity);
+                    same_dict = A.tdict && B.tdict && ::same_dict(A.tdict, B.tdict);
                 }
             }
             for (int i = 0; same_dict && i < n; ++i) {
@@ -5577,6 +5605,8 @@ extern "C" int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esg
                 end_instance(hist);
             }
             tb.subs.push_back(std::move(hist));
+            // a large merge buffer is not kept with the plan (pinned memory outside the context's budget)
+            if (hb.bytes > kColoKeepBytes) hb.release();
             mark("rebuilt");
         }
         res->export_view();

@@ -54,6 +54,18 @@ CASES = {
                           .subAggregation(AB.avg("rt").field("response_time_ms"))], ("bytes", "response_time_ms")),
     "offset_hist_price": ([AB.histogram("p").field("price").interval(10).offset(3)
                            .subAggregation(AB.extendedStats("x").field("price"))], ("price",)),
+    # lattice reduce with metric leaves streamed per shard run: a count order permutes the emitted buckets, and
+    # min_doc_count >= 2 drops slots, so a shard's run of slots may map to non-consecutive buckets
+    "hist_count_desc_stats": ([AB.histogram("rt").field("response_time_ms").interval(50).order(Order.COUNT_DESC)
+                               .subAggregation(AB.stats("b").field("bytes"))], ("response_time_ms", "bytes")),
+    "hist_count_asc_ext": ([AB.histogram("b").field("bytes").interval(20_000).order(Order.COUNT_ASC)
+                            .subAggregation(AB.extendedStats("rt").field("response_time_ms"))],
+                           ("bytes", "response_time_ms")),
+    "sparse_hist_mdc2_stats": ([AB.histogram("b").field("bytes").interval(7).minDocCount(2)
+                                .subAggregation(AB.stats("rt").field("response_time_ms"))], ("bytes", "response_time_ms")),
+    "sparse_hist_mdc3_avg_desc": ([AB.histogram("b").field("bytes").interval(11).minDocCount(3).order(Order.KEY_DESC)
+                                   .subAggregation(AB.avg("rt").field("response_time_ms"))],
+                                  ("bytes", "response_time_ms")),
     "top_metrics": ([AB.stats("s").field("response_time_ms"), AB.extendedStats("e").field("bytes"),
                      AB.avg("a").field("response_time_ms")], ("response_time_ms", "bytes")),
 }
@@ -103,3 +115,36 @@ def test_reduce_terms_ordered_by_a_metric(path, asc):
     got = reduce([ShardResult.deserialize(b) for b in blobs]).to_dict()
     assert_same(got, want["reduced"], "reduced")
     assert got["hosts"]["doc_count_error_upper_bound"] == -1
+
+
+def _cols(b, rt):
+    from elasticsearch_amd import _native as N
+    import numpy as np
+    return {"bytes": {"type": N.COL_I64, "values": np.asarray(b, dtype=np.int64)},
+            "response_time_ms": {"type": N.COL_I64, "values": np.asarray(rt, dtype=np.int64)}}
+
+
+@pytest.mark.parametrize("shape", ["mdc2_gap", "count_desc", "count_asc_gap"])
+def test_lattice_reduce_runs_with_permuted_or_dropped_slots(shape):
+    """A shard's run of histogram slots streamed into its buckets (the lattice reduce's metric leaves) must land on the
+    right buckets when the ends of the run are len - 1 buckets apart but its middle is not: a slot dropped by
+    min_doc_count (shard A holds keys 0, 7, 21; key 7 totals 1 doc) or a count order that permutes the emitted buckets."""
+    if shape == "mdc2_gap":
+        a = _cols([0, 0, 7, 21, 21], [1, 2, 1000, 5, 6])
+        b = _cols([0, 14, 14, 21], [3, 40, 50, 7])
+        agg = AB.histogram("b").field("bytes").interval(7).minDocCount(2)
+    elif shape == "count_desc":
+        # totals: key 0 -> 6, key 7 -> 2, key 14 -> 4, key 21 -> 1: count-desc order 0, 14, 7, 21 (out = 0, 2, 1, 3)
+        a = _cols([0, 0, 0, 7, 14, 14, 21], [1, 2, 3, 1000, 9, 8, 77])
+        b = _cols([0, 0, 0, 7, 14, 14], [4, 5, 6, 2000, 10, 11])
+        agg = AB.histogram("b").field("bytes").interval(7).order(Order.COUNT_DESC)
+    else:
+        a = _cols([0, 7, 7, 7, 21, 21], [1, 500, 600, 700, 5, 6])
+        b = _cols([0, 14, 14, 21, 28, 28, 28, 28], [3, 40, 50, 7, 1, 1, 1, 1])
+        agg = AB.histogram("b").field("bytes").interval(7).order(Order.COUNT_ASC)
+    aggs = [agg.subAggregation(AB.stats("s").field("response_time_ms"))
+            .subAggregation(AB.extendedStats("x").field("response_time_ms"))]
+    shards = [(a, 5 if shape == "mdc2_gap" else len(a["bytes"]["values"])), (b, len(b["bytes"]["values"]))]
+    want = O.run(shards, aggs, number_of_shards=2)
+    blobs = [encode(from_shard_json(aggs, want["shards"][s], 2)) for s in range(2)]
+    assert_same(reduce([ShardResult.deserialize(x) for x in blobs]).to_dict(), want["reduced"], "reduced")
