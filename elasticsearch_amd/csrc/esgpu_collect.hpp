@@ -279,7 +279,33 @@ struct Acc {
     unsigned long long* pk;         // LDS, packed integer cells (VK bit 64): count << pk_shift | sum of deltas [C][ncopies]
     uint32_t* mm;                   // LDS, packed integer cells: (min, max) delta pair per cell [C][2]
     unsigned long long* pkd;        // LDS, packed integer cells: this thread's spare word (the adds of docs that hit nothing)
+    double* sum_lo;                 // global, compensated sums (CollectParams.g_sum_lo): null = plain
+    double* sq_lo;
 };
+
+// Compensated accumulation into the global grid (DESIGN §5 "Float parity"): the grid word is the high part of a
+// double-double and `lo` collects every addition's rounding error.  The returning atomic yields the value it added to,
+// so the error of that addition is TwoSum's -- exact as long as the atomic rounds like a VALU add (round to nearest
+// even, subnormals kept: tools/fpatomic_probe.hip on gfx950).  `xl` is the addend's own low part (a double-double
+// addend); a non-finite sum carries no error term (Inf / NaN propagate through the high part alone, as in Java).
+__device__ __forceinline__ void dd_atomic_add(double* hi, double* lo, double x, double xl = 0.0) {
+    if (!lo) {
+        atomicAdd(hi, x);
+        return;
+    }
+    const double old = atomicAdd(hi, x);
+    const double s = old + x;
+    const double bp = s - old;
+    const double e = ((old - (s - bp)) + (x - bp)) + xl;
+    if (e != 0.0 && __builtin_isfinite(s)) atomicAdd(lo, e);
+}
+// an exact long as a double-double (its high and low 32 bits are exact doubles; TwoSum of them)
+__device__ __forceinline__ void i64_to_dd(long long v, double& hi, double& lo) {
+    const double a = (double)(v >> 32) * 4294967296.0, b = (double)(unsigned long long)(v & 0xFFFFFFFFll);
+    hi = a + b;
+    const double bp = hi - a;
+    lo = (a - (hi - bp)) + (b - bp);
+}
 
 template <int MET, bool LDS, int MS>
 __device__ __forceinline__ void add_value(const Acc& a, uint32_t c, double x, bool has_vcnt) {
@@ -289,7 +315,8 @@ __device__ __forceinline__ void add_value(const Acc& a, uint32_t c, double x, bo
     } else {
         if (has_vcnt) atomicAdd(&a.vcnt64[c], 1ull);
     }
-    atomicAdd(&a.sum[ca], x);
+    if (LDS) atomicAdd(&a.sum[ca], x);
+    else dd_atomic_add(&a.sum[c], a.sum_lo ? a.sum_lo + c : nullptr, x);
     if (MET >= 2) {
         const bool nan = x != x;
         const unsigned long long e = sortable(x);
@@ -307,7 +334,10 @@ __device__ __forceinline__ void add_value(const Acc& a, uint32_t c, double x, bo
         atomicMax(&a.mx[c * st], emx);
 #endif
     }
-    if (MET >= 3) atomicAdd(&a.sq[ca], x * x);  // ExtendedStatsAggregator: sumOfSqr += value * value (no FMA)
+    if (MET >= 3) {  // ExtendedStatsAggregator: sumOfSqr += value * value (no FMA)
+        if (LDS) atomicAdd(&a.sq[ca], x * x);
+        else dd_atomic_add(&a.sq[c], a.sq_lo ? a.sq_lo + c : nullptr, x * x);
+    }
 }
 
 // Per-doc update.  `slot` is the key index relative to the accumulator's first slot (window or grid).
@@ -875,7 +905,15 @@ __device__ void flush_window_pi(const CollectParams& P, const Acc& s, uint32_t T
         const unsigned long long cnt = n >> sh;
         atomicAdd(&P.g_cnt[g], cnt);
         for (uint32_t k = 0; k < ncp; ++k) s.pk[k * C + c] = 0;
-        atomicAdd(&P.g_sum[g], (double)((long long)(n & mask) + (long long)cnt * P.mv_base));
+        // the cell's exact integer sum; compensated into the grid when its partial sums could pass 2^53
+        const long long isum = (long long)(n & mask) + (long long)cnt * P.mv_base;
+        if (P.g_sum_lo) {
+            double xh, xl;
+            i64_to_dd(isum, xh, xl);
+            dd_atomic_add(&P.g_sum[g], P.g_sum_lo + g, xh, xl);
+        } else {
+            atomicAdd(&P.g_sum[g], (double)isum);
+        }
         if (MET >= 2) {
             const uint32_t lo = s.mm[2 * c], hi = s.mm[2 * c + 1];
             atomicMin(&P.g_min[g], sortable((double)(P.mv_base + (int64_t)lo)));
@@ -931,7 +969,7 @@ __device__ void flush_window(const CollectParams& P, const Acc& s, uint32_t T, u
             }
             double sum = 0.0;
             for (uint32_t k = 0; k < ncp; ++k) { sum += s.sum[k * C + c]; s.sum[k * C + c] = 0.0; }
-            atomicAdd(&P.g_sum[g], sum);
+            dd_atomic_add(&P.g_sum[g], P.g_sum_lo ? P.g_sum_lo + g : nullptr, sum);
             if (MET >= 2) {
                 const unsigned long long mn = s.mn[MS * c], mx = s.mx[MS * c];
                 if (mn != kMinInit) atomicMin(&P.g_min[g], mn);
@@ -942,7 +980,7 @@ __device__ void flush_window(const CollectParams& P, const Acc& s, uint32_t T, u
             if (MET >= 3) {
                 double sq = 0.0;
                 for (uint32_t k = 0; k < ncp; ++k) { sq += s.sq[k * C + c]; s.sq[k * C + c] = 0.0; }
-                atomicAdd(&P.g_sq[g], sq);
+                dd_atomic_add(&P.g_sq[g], P.g_sq_lo ? P.g_sq_lo + g : nullptr, sq);
             }
         }
     }
@@ -1005,6 +1043,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, VK, WGS>())) void coll
     Acc g;  // global grid view
     g.cnt32 = nullptr; g.vcnt32 = nullptr; g.ocnt32 = nullptr;
     g.cnt64 = P.g_cnt; g.vcnt64 = P.g_vcnt; g.sum = P.g_sum; g.mn = P.g_min; g.mx = P.g_max; g.sq = P.g_sq;
+    g.sum_lo = P.g_sum_lo; g.sq_lo = P.g_sq_lo;
     g.mstride = 1;
     g.coff = 0;
     g.ocnt64 = P.g_ocnt;
@@ -1016,6 +1055,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, VK, WGS>())) void coll
     // accesses, and each flat load waits for vmcnt(0): the prefetched loads of the next iteration.
     constexpr bool PI = MET > 0 && (VK & 64) != 0;  // packed integer cells
     Acc s;
+    s.sum_lo = nullptr; s.sq_lo = nullptr;
     if constexpr (PI) {  // collect_lds_bytes(pi = true) mirrors this carve
         size_t off = 0;
         auto carve = [&](size_t bytes) { unsigned char* p = smem + off; off += (bytes + 15) & ~(size_t)15; return p; };

@@ -1281,6 +1281,22 @@ void launch_gather_rows(const GatherParams& p, hipStream_t st) {
     hipLaunchKernelGGL(gather_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, st, p);
 }
 
+__global__ __launch_bounds__(256) void dd_fold_kernel(double* __restrict__ hi, double* __restrict__ lo, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const double l = lo[i];
+        if (l != 0.0) {
+            const double h = hi[i];
+            if (__builtin_isfinite(h)) hi[i] = h + l;  // a non-finite sum keeps its Inf / NaN
+            lo[i] = 0.0;
+        }
+    }
+}
+void launch_dd_fold(double* hi, double* lo, size_t n, hipStream_t s) {
+    if (!n) return;
+    const uint32_t grid = (uint32_t)std::min<size_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(dd_fold_kernel, dim3(grid), dim3(256), 0, s, hi, lo, n);
+}
+
 __global__ void fill_u64_kernel(unsigned long long* p, size_t n, unsigned long long v) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
 }
@@ -2123,10 +2139,12 @@ __global__ __launch_bounds__(kWG) void collect_multi_kernel(CollectParams P) {
     Acc g;
     g.cnt32 = nullptr; g.vcnt32 = nullptr; g.ocnt32 = nullptr;
     g.cnt64 = P.g_cnt; g.vcnt64 = P.g_vcnt; g.sum = P.g_sum; g.mn = P.g_min; g.mx = P.g_max; g.sq = P.g_sq;
+    g.sum_lo = P.g_sum_lo; g.sq_lo = P.g_sq_lo;
     g.mstride = 1;
     g.coff = 0;
     g.ocnt64 = P.g_ocnt;
     Acc s;
+    s.sum_lo = nullptr; s.sq_lo = nullptr;
     {
         size_t off = 0;
         auto carve = [&](size_t bytes) { unsigned char* p = smem + off; off += (bytes + 15) & ~(size_t)15; return p; };
@@ -2216,12 +2234,16 @@ __global__ __launch_bounds__(kWG) void collect_multi_kernel(CollectParams P) {
                     if (P.vcnt_mode) {
                         if (P.lds_mode) atomicAdd(&s.vcnt32[c], nm); else atomicAdd(&g.vcnt64[c], (unsigned long long)nm);
                     }
-                    atomicAdd(&a.sum[c], msum);
+                    if (P.lds_mode) atomicAdd(&s.sum[c], msum);
+                    else dd_atomic_add(&g.sum[c], g.sum_lo ? g.sum_lo + c : nullptr, msum);
                     if (MET >= 2) {
                         if (emn < a.mn[c * a.mstride]) atomicMin(&a.mn[c * a.mstride], emn);
                         if (emx > a.mx[c * a.mstride]) atomicMax(&a.mx[c * a.mstride], emx);
                     }
-                    if (MET >= 3) atomicAdd(&a.sq[c], msq);
+                    if (MET >= 3) {
+                        if (P.lds_mode) atomicAdd(&s.sq[c], msq);
+                        else dd_atomic_add(&g.sq[c], g.sq_lo ? g.sq_lo + c : nullptr, msq);
+                    }
                 }
             }
         }

@@ -124,6 +124,10 @@ struct CollectParams {
     unsigned long long* g_min;
     unsigned long long* g_max;
     double* g_sq;
+    // compensated sums (DESIGN §5 "Float parity"; null: plain f64 adds, exact for the request's data): the low parts of
+    // g_sum / g_sq as double-doubles -- zero between collects (launch_dd_fold adds them into g_sum / g_sq and clears them)
+    double* g_sum_lo;
+    double* g_sq_lo;
     // dynamic chunk claiming (null: static ranges of blocks_per_wg blocks): the grid is the resident workgroup slots,
     // workgroup g starts on chunk g (kGroup blocks) and claims later chunks from claim[0]; claim[1] counts finished
     // workgroups, and the last one resets both, so the pair is zero again for the next launch on the plan's stream
@@ -382,6 +386,8 @@ void launch_term_totals(const unsigned long long* cnt, uint32_t H, uint32_t T, u
 // n u64 words device -> device-visible pinned host memory
 void launch_copy_u64(const unsigned long long* src, unsigned long long* dst, size_t n, hipStream_t s);
 void launch_gather_rows(const GatherParams& p, hipStream_t s);
+// g_sum / g_sq += their compensated low parts, which are cleared (after every collect launch that used them)
+void launch_dd_fold(double* hi, double* lo, size_t n, hipStream_t s);
 void launch_fill_u64(unsigned long long* p, size_t n, unsigned long long v, hipStream_t s);
 // several u64 arrays filled by one launch (a plan reset: counts, sums, min / max identities)
 constexpr int kFillSpans = 8;

@@ -950,6 +950,11 @@ struct Pipeline {
     uint64_t value_count2 = 0;       // inner terms: its global ordinal count (H is max(value_count2, 1))
     int vcnt_mode = 0, ocnt_mode = OCNT_NONE;
     DevBuf g_cnt, g_ocnt, g_vcnt, g_sum, g_min, g_max, g_sq;
+    // compensated sums (CollectParams.g_sum_lo): on once the request's metric partial sums can round -- a double metric,
+    // or |values| x values (x |values| for sums of squares) reaching 2^53 over the segments collected so far
+    DevBuf g_sum_lo, g_sq_lo;        // zero between collects
+    bool dd = false;
+    uint64_t dd_vals = 0, dd_amax = 0;
     // cardinality state
     int p = 14;
     DevBuf regs, lc_set, lc_count;
@@ -1620,6 +1625,7 @@ static bool dyn_claim_on();
 static bool replay_compaction();
 static bool d16_on();
 static bool raw_hist_on();
+static bool dd_forced();
 static bool pi_cells(const esgpu_ctx* c);
 static uint32_t pi_copies();
 static const uint16_t* ensure_ord16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
@@ -2810,10 +2816,50 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     P.g_min = pl.g_min.as<unsigned long long>();
     P.g_max = pl.g_max.as<unsigned long long>();
     P.g_sq = pl.g_sq.as<double>();
+    // compensated sums (DESIGN §5 "Float parity"): while every partial sum of the request's metric values is an integer
+    // below 2^53 the grid's f64 adds are exact in any order; otherwise (a double metric, or long values whose magnitude
+    // times their number -- squared for sums of squares -- reaches 2^53) the flushes add double-doubles, folded back into
+    // the grid after the launch (dd_fold below)
+    if (first_segment) {
+        pl.dd = false;
+        pl.dd_vals = 0;
+        pl.dd_amax = 0;
+    }
+    if (L_met > 0 && mc && !inner_missing) {
+        pl.dd_vals += mc->multi ? mc->n_values : (uint64_t)s->max_doc;
+        if (mc->type == ESGPU_COL_F64 || dd_forced()) {
+            pl.dd = true;
+        } else if (mc->vmin <= mc->vmax) {
+            auto mag = [](int64_t v) { return v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v; };
+            pl.dd_amax = std::max(pl.dd_amax, std::max(mag(mc->vmin), mag(mc->vmax)));
+            const long double n = (long double)pl.dd_vals, a = (long double)pl.dd_amax, lim = 9007199254740992.0L;
+            if (n * a >= lim || (pl.met >= 3 && n * a * a >= lim)) pl.dd = true;
+        }
+    }
+    const size_t dd_cells = (size_t)pl.T * pl.H;
+    if (pl.dd && L_met > 0 && !inner_missing) {
+        auto lo = [&](DevBuf& b) {
+            if (b.p && b.bytes >= dd_cells * 8) return b.as<double>();
+            b.alloc(p->ctx, dd_cells * 8 + dd_cells * 2);
+            HIPX(hipMemsetAsync(b.p, 0, b.bytes, p->stream));
+            return b.as<double>();
+        };
+        P.g_sum_lo = lo(pl.g_sum_lo);
+        if (pl.met >= 3 && P.g_sq) P.g_sq_lo = lo(pl.g_sq_lo);
+    }
+    auto dd_fold = [&] {
+        if (P.g_sum_lo) launch_dd_fold(P.g_sum, P.g_sum_lo, dd_cells, p->stream);
+        if (P.g_sq_lo) launch_dd_fold(P.g_sq, P.g_sq_lo, dd_cells, p->stream);
+        HIPX(hipGetLastError());
+    };
     const int ret = inner_missing ? 2 : 1;
     if (multi && !inner_missing) count_width(p, pl, s, false, first_segment);
-    if (multi) return collect_multi(p, pl, s, P, L_ORD ? oc : nullptr, L_HIST ? hc : nullptr, inner_missing ? nullptr : mc, L_met,
-                                    d_accept) ? ret : 0;
+    if (multi) {
+        const bool ok = collect_multi(p, pl, s, P, L_ORD ? oc : nullptr, L_HIST ? hc : nullptr, inner_missing ? nullptr : mc,
+                                      L_met, d_accept);
+        dd_fold();
+        return ok ? ret : 0;
+    }
     // compact columns: 2 B per ordinal instead of 4, 4 B per timestamp instead of 8 -- the reported (algorithmic) bytes
     // are the bytes this layout must move (SURVEY §8(d)'s upload-width figure would put config 5 above the HBM peak)
     if (compact_cols(p->ctx)) {
@@ -3047,6 +3093,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     launch_collect(P, L_ORD, L_HIST, L_met, wide, grid, lds, p->stream);
     HIPX(hipGetLastError());
     HIPX(hipEventRecord(pl.e1, p->stream));
+    dd_fold();
     p->last_bytes += bytes_per_doc * (uint64_t)s->max_doc + (d_accept ? ((uint64_t)s->max_doc + 7) / 8 : 0);
     p->last_path = P.lds_mode ? (P.windowed ? 2 : 1) : 0;
     return ret;
@@ -3066,6 +3113,11 @@ static bool d16_on() {
 // the compacted replay (ESGPU_REPLAY_COMPACT=0: one pass over the segments per batch of winners, for A/B runs)
 static bool replay_compaction() {
     static const bool on = [] { const char* e = std::getenv("ESGPU_REPLAY_COMPACT"); return !(e && *e == '0'); }();
+    return on;
+}
+// ESGPU_DD=1: every metric grid takes the compensated flushes, exact data or not (tests of those paths on integer data)
+static bool dd_forced() {
+    static const bool on = [] { const char* e = std::getenv("ESGPU_DD"); return e && *e == '1'; }();
     return on;
 }
 static bool dyn_claim_on() {

@@ -541,6 +541,36 @@ struct Bucket {
     InternalList aggs;
 };
 
+// Exact shadow of a floating sum (checker only, off unless oracle_set_exact_shadow(1)): the value the reference's
+// doc-order double additions approximate, so tests can tell the reference's own rounding error from the GPU's (SURVEY §7
+// "Float parity").  Double-double accumulation (Knuth TwoSum into hi, the rounding errors summed into lo; relative error
+// about n * 2^-104 of sum |v|); non-finite addends tracked apart with IEEE semantics (NaN, or +Inf with -Inf, give NaN).
+struct XSum {
+    double hi = 0.0, lo = 0.0;
+    bool pinf = false, ninf = false, nan = false;
+    void add(double v) {
+        if (!std::isfinite(v)) {
+            if (v != v) nan = true; else if (v > 0) pinf = true; else ninf = true;
+            return;
+        }
+        const double s = hi + v, bp = s - hi, e = (hi - (s - bp)) + (v - bp);
+        hi = s;
+        lo += e;
+    }
+    void merge(const XSum& o) {
+        add(o.hi);
+        lo += o.lo;
+        pinf |= o.pinf; ninf |= o.ninf; nan |= o.nan;
+    }
+    double value() const {
+        if (nan || (pinf && ninf)) return NAN;
+        if (pinf) return INFINITY;
+        if (ninf) return -INFINITY;
+        return hi + lo;
+    }
+};
+static bool g_exact_shadow = false;
+
 struct Internal {
     int type = 0;
     std::string name;
@@ -562,6 +592,7 @@ struct Internal {
     // metrics
     int64_t count = 0;
     double sum = 0, min = INFINITY, max = -INFINITY, sumsq = 0, sigma = 2.0;
+    XSum xsum, xsq;  // exact shadows of sum / sumsq (g_exact_shadow)
     // cardinality
     std::shared_ptr<HLLPP> hll;
     // filter (InternalSingleBucketAggregation): doc_count in `count`, sub-aggregations here
@@ -888,6 +919,7 @@ struct StatsAgg : Aggregator {
     const Column* values = nullptr;
     std::vector<int64_t> counts;
     std::vector<double> sums, mins, maxes, sumsqs;
+    std::vector<XSum> xsums, xsqs;  // exact shadows (g_exact_shadow only)
     bool ext = false, avg = false;
     void set_leaf(const Segment& seg) override { values = seg.col(f->field.c_str()); }
     void grow(int64_t b) {
@@ -895,6 +927,7 @@ struct StatsAgg : Aggregator {
         size_t n = (size_t)b + 1;
         counts.resize(n, 0); sums.resize(n, 0.0); sumsqs.resize(n, 0.0);
         mins.resize(n, INFINITY); maxes.resize(n, -INFINITY);
+        if (g_exact_shadow) { xsums.resize(n); xsqs.resize(n); }
     }
     void collect(uint32_t doc, int64_t bucket) override {
         if (!values) return;
@@ -908,6 +941,10 @@ struct StatsAgg : Aggregator {
             sum += v;
             if (ext) sumOfSqr += v * v;
             if (!avg) { mn = java_min(mn, v); mx = java_max(mx, v); }
+            if (g_exact_shadow) {
+                xsums[bucket].add(v);
+                if (ext) xsqs[bucket].add(v * v);  // the reference's rounded products, summed exactly
+            }
         }
         sums[bucket] += sum;
         if (ext) sumsqs[bucket] += sumOfSqr;
@@ -924,7 +961,9 @@ struct StatsAgg : Aggregator {
     }
     InternalPtr build(int64_t b) override {
         if (!values || b >= (int64_t)counts.size()) return build_empty();
-        return make(counts[b], sums[b], mins[b], maxes[b], sumsqs[b]);
+        InternalPtr r = make(counts[b], sums[b], mins[b], maxes[b], sumsqs[b]);
+        if (g_exact_shadow) { r->xsum = xsums[b]; r->xsq = xsqs[b]; }
+        return r;
     }
     InternalPtr build_empty() override { return make(0, 0.0, INFINITY, -INFINITY, 0.0); }
 };
@@ -1251,12 +1290,16 @@ static InternalPtr reduce_one(const InternalList& aggs) {
         case ESGPU_AGG_AVG: {  // InternalStats/InternalExtendedStats/InternalAvg.doReduce
             int64_t count = 0;
             double mn = INFINITY, mx = -INFINITY, sum = 0, sq = 0;
+            r->xsum = XSum();
+            r->xsq = XSum();
             for (auto& a : aggs) {
                 count += a->count;
                 mn = java_min(mn, a->min);
                 mx = java_max(mx, a->max);
                 sum += a->sum;
                 sq += a->sumsq;
+                r->xsum.merge(a->xsum);
+                r->xsq.merge(a->xsq);
             }
             r->count = count; r->min = mn; r->max = mx; r->sum = sum; r->sumsq = sq;
             return r;
@@ -1333,6 +1376,36 @@ static uint64_t fnv1a(const uint8_t* p, size_t n) {
 
 static void write_list(Json& j, const InternalList& aggs);
 
+// g_exact_shadow: ,"_exact":{...} -- the metric's rendered values recomputed from the exact sums with the same formulas
+// (InternalStats / InternalExtendedStats / InternalAvg getters), so a test can compare either value against either
+static void write_exact(Json& j, const Internal& a) {
+    const double sum = a.xsum.value(), sq = a.xsq.value();
+    j.raw(","); j.key("_exact"); j.raw("{");
+    if (a.type == ESGPU_AGG_AVG) {
+        j.key("value"); if (a.count != 0) j.dbl(sum / (double)a.count); else j.raw("null");
+        j.raw(","); j.key("_internal"); j.raw("{"); j.key("sum"); j.dbl(sum); j.raw("}");
+    } else {
+        const bool c = a.count != 0;
+        const double avg = sum / (double)a.count;
+        j.key("avg"); if (c) j.dbl(avg); else j.raw("null"); j.raw(",");
+        j.key("sum"); if (c) j.dbl(sum); else j.raw("null");
+        if (a.type == ESGPU_AGG_EXTENDED_STATS) {
+            const double var = (sq - ((sum * sum) / (double)a.count)) / (double)a.count;
+            const double sd = std::sqrt(var);
+            j.raw(","); j.key("sum_of_squares"); if (c) j.dbl(sq); else j.raw("null");
+            j.raw(","); j.key("variance"); if (c) j.dbl(var); else j.raw("null");
+            j.raw(","); j.key("std_deviation"); if (c) j.dbl(sd); else j.raw("null");
+            j.raw(","); j.key("std_deviation_bounds"); j.raw("{");
+            j.key("upper"); if (c) j.dbl(avg + (sd * a.sigma)); else j.raw("null"); j.raw(",");
+            j.key("lower"); if (c) j.dbl(avg - (sd * a.sigma)); else j.raw("null"); j.raw("}");
+        }
+        j.raw(","); j.key("_internal"); j.raw("{"); j.key("sum"); j.dbl(sum);
+        if (a.type == ESGPU_AGG_EXTENDED_STATS) { j.raw(","); j.key("sum_of_squares"); j.dbl(sq); }
+        j.raw("}");
+    }
+    j.raw("}");
+}
+
 static void write_agg(Json& j, const Internal& a) {
     j.raw("{");
     switch (a.type) {
@@ -1377,6 +1450,7 @@ static void write_agg(Json& j, const Internal& a) {
             if (a.count != 0) j.dbl(a.sum / (double)a.count); else j.raw("null");
             j.raw(","); j.key("_internal"); j.raw("{"); j.key("count"); j.i64(a.count); j.raw(",");
             j.key("sum"); j.dbl(a.sum); j.raw("}");
+            if (g_exact_shadow) write_exact(j, a);
             break;
         }
         case ESGPU_AGG_STATS:
@@ -1405,6 +1479,7 @@ static void write_agg(Json& j, const Internal& a) {
             j.key("max"); j.dbl(a.max);
             if (a.type == ESGPU_AGG_EXTENDED_STATS) { j.raw(","); j.key("sum_of_squares"); j.dbl(a.sumsq); }
             j.raw("}");
+            if (g_exact_shadow) write_exact(j, a);
             break;
         }
         case ESGPU_AGG_CARDINALITY: {
@@ -1796,6 +1871,9 @@ int oracle_run(const oracle_shard* shards, int32_t nshards, const esgpu_agg_spec
 void oracle_free(char* p) { free(p); }
 /* 1: oracle_run's JSON also carries "streams": per shard, the hex of InternalAggregations.writeTo */
 void oracle_set_emit_streams(int32_t on) { oracle::g_emit_streams = on; }
+/* 1: stats / extended_stats / avg results also carry "_exact": their values recomputed from the exact sums that the
+   reference's doc-order double additions approximate (double-double shadow accumulators) */
+void oracle_set_exact_shadow(int32_t on) { oracle::g_exact_shadow = on != 0; }
 
 /* known-answer helpers */
 void oracle_murmur3_128(const uint8_t* key, int32_t len, int64_t seed, uint64_t* h1, uint64_t* h2) {

@@ -46,6 +46,7 @@ def lib():
                                  ctypes.POINTER(ctypes.c_double)]
         L.oracle_free.argtypes = [ctypes.c_char_p]
         L.oracle_set_emit_streams.argtypes = [ctypes.c_int32]
+        L.oracle_set_exact_shadow.argtypes = [ctypes.c_int32]
         L.oracle_last_error.restype = ctypes.c_char_p
         L.oracle_murmur3_128.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int64, ctypes.POINTER(ctypes.c_uint64),
                                          ctypes.POINTER(ctypes.c_uint64)]
@@ -125,11 +126,14 @@ def _columns(columns):
 
 
 def run(shards, aggs, filters=None, number_of_shards=None, accept=None, ord_lookup=None, return_seconds=False,
-        streams=False):
+        streams=False, exact=False):
     """shards: list of (columns_dict, max_doc).  Returns {"shards": [...], "reduced": {...}} (parsed JSON); with
-    streams=True also "streams": per shard the bytes of InternalAggregations.writeTo."""
+    streams=True also "streams": per shard the bytes of InternalAggregations.writeTo; with exact=True every stats /
+    extended_stats / avg result also carries "_exact": its rendered values recomputed from the exact sums that the
+    reference's doc-order double additions approximate (tests/helpers.assert_same_exact)."""
     L = lib()
     L.oracle_set_emit_streams(1 if streams else 0)
+    L.oracle_set_exact_shadow(1 if exact else 0)
     number_of_shards = number_of_shards or len(shards)
     specs, nspecs, k1 = oracle_request.lower(L, aggs, number_of_shards)
     flt, nf, k2 = oracle_request.lower_filters(filters, ord_lookup, aggs)
@@ -150,6 +154,7 @@ def run(shards, aggs, filters=None, number_of_shards=None, accept=None, ord_look
     out = ctypes.c_char_p()
     secs = ctypes.c_double()
     rc = L.oracle_run(sarr, len(oshards), specs, nspecs, flt, nf, ctypes.byref(out), ctypes.byref(secs))
+    L.oracle_set_exact_shadow(0)
     if rc != 0:
         raise RuntimeError("oracle: " + L.oracle_last_error().decode())
     res = json.loads(out.value.decode("utf-8"))

@@ -17,10 +17,11 @@ REL_TOL = 1e-12
 # by sum_of_squares / (count * variance).  They are compared at 1e-9; the sums they come from stay at 1e-12.
 DERIVED_TOL = 1e-9
 DERIVED_KEYS = ("variance", "std_deviation", "std_deviation_bounds", "upper", "lower")
-# sums of integer values stay exact (order-independent) only below 2^53; above it (sum_of_squares of a long field such
-# as bytes, ~1e17 over 1e5 docs) every addition rounds, and the reference's doc-order sum and the GPU's partial sums
-# round differently: bounded by (n - 1) * eps relative, i.e. 1.1e-11 at 1e5 docs.  Compared at 1e-10 there.
-BIG_SUM_TOL = 1e-10
+# Sums past 2^53 (sum_of_squares of a long field such as bytes, sums of a metric with a 10^12 base) and sums of
+# non-integer doubles round on every addition, in the reference's doc order and in the GPU's partial sums alike.  Such
+# results are checked with an oracle run with exact=True (assert_same_exact): its "_exact" values are the exact sums the
+# reference approximates, and the GPU's compensated sums must lie within 1e-12 of them (as of the oracle, unless the
+# oracle's own doc-order error is the larger).
 
 
 def synthetic_dict(field):
@@ -109,14 +110,101 @@ def assert_same(got, want, path="", exact_floats=True):
     else:
         derived = any(("." + k) in path for k in DERIVED_KEYS)
         tol = DERIVED_TOL if derived else REL_TOL
-        if isinstance(want, (int, float)) and not isinstance(want, bool) and abs(float(want)) >= 2.0 ** 53:
-            tol = max(tol, BIG_SUM_TOL)
         ok = _num_equal(got, want, exact_floats, tol)
         if not ok and derived and not exact_floats and isinstance(want, float) and isinstance(got, float):
             # avg +- sigma * std_deviation near zero: the subtraction cancels, so the operands' rounding (relative to
             # their own magnitude, >= 1 here) is what the result carries -- compared against a unit scale
             ok = abs(got - want) <= tol * max(abs(got), abs(want), 1.0)
         assert ok, f"{path}: {got!r} != {want!r}"
+
+
+def _rel(a, b):
+    """Relative difference of two floats (0 when equal, NaN-equal or the same infinity; inf when only one is finite)."""
+    fa, fb = float(a), float(b)
+    if fa == fb or (math.isnan(fa) and math.isnan(fb)):
+        return 0.0
+    if not (math.isfinite(fa) and math.isfinite(fb)):
+        return math.inf
+    return abs(fa - fb) / max(abs(fa), abs(fb))
+
+
+class FloatReport:
+    """Largest relative errors against the exact sums seen by assert_same_exact, per rendered key: the oracle's
+    (the reference's doc-order rounding) and the GPU's."""
+
+    def __init__(self):
+        self.oracle, self.got, self.n = {}, {}, 0
+
+    def add(self, key, oracle_err, got_err):
+        self.n += 1
+        self.oracle[key] = max(self.oracle.get(key, 0.0), oracle_err)
+        self.got[key] = max(self.got.get(key, 0.0), got_err)
+
+    def as_dict(self):
+        return {"values_checked": self.n, "max_rel_err_oracle_vs_exact": self.oracle,
+                "max_rel_err_gpu_vs_exact": self.got}
+
+
+def _exact_leaf(got, want, exact, path, key, exact_floats, report):
+    derived = any(("." + k) in path for k in DERIVED_KEYS)
+    tol = DERIVED_TOL if derived else REL_TOL
+    if exact is None or not isinstance(want, float) or not isinstance(got, (int, float)):
+        # no exact counterpart: counts, and min / max (order-independent: always bit-exact)
+        assert _num_equal(got, want, exact_floats or key in ("min", "max"), tol), f"{path}: {got!r} != {want!r}"
+        return
+    eg, ew = _rel(got, exact), _rel(want, exact)
+    if report is not None:
+        report.add(key, ew, eg)
+    if exact_floats and ew == 0.0:
+        # the reference's sum is exact (integer data below 2^53): the GPU's must be the same double
+        assert _rel(got, want) == 0.0, f"{path}: {got!r} != {want!r} (exact {exact!r})"
+        return
+    # the GPU's compensated sums lie within the bar of the exact value; a derived statistic (its subtraction
+    # cancels) may instead match the oracle's
+    ok = eg <= tol or (derived and _num_equal(got, want, False, tol))
+    if not ok and derived and math.isfinite(float(got)) and math.isfinite(float(exact)):
+        ok = abs(float(got) - float(exact)) <= tol * max(abs(float(got)), abs(float(exact)), 1.0)
+    assert ok, f"{path}: {got!r} vs exact {exact!r} (oracle {want!r}; rel err gpu {eg:.3g}, oracle {ew:.3g})"
+
+
+def assert_same_exact(got, want, path="", exact_floats=True, report=None, _exact=None, _key=""):
+    """assert_same against an oracle run with exact=True: a metric's floating values are compared with its "_exact"
+    values (the exact sums the reference's doc-order additions approximate, and the statistics derived from them by the
+    reference's formulas).  The GPU must be within REL_TOL (DERIVED_TOL for variance / std_deviation / bounds) of the
+    exact value; with exact_floats, a value the oracle computed exactly must be bit-identical.  `report` (FloatReport)
+    collects the oracle's and the GPU's largest errors."""
+    if isinstance(want, dict):
+        if "_exact" in want:
+            want = dict(want)
+            ex = want.pop("_exact")
+            assert isinstance(got, dict), f"{path}: expected object"
+            assert set(got) == set(want), f"{path}: keys differ: {sorted(set(got) ^ set(want))}"
+            for k in want:
+                assert_same_exact(got[k], want[k], f"{path}.{k}", exact_floats, report, ex.get(k), k)
+            return
+        assert isinstance(got, dict), f"{path}: expected object, got {type(got).__name__}"
+        assert set(got) == set(want), f"{path}: keys differ: {sorted(set(got) ^ set(want))}"
+        for k in want:
+            sub = _exact.get(k) if isinstance(_exact, dict) else None
+            assert_same_exact(got[k], want[k], f"{path}.{k}", exact_floats, report, sub, k)
+    elif isinstance(want, list):
+        assert isinstance(got, list), f"{path}: expected list"
+        assert len(got) == len(want), f"{path}: length {len(got)} != {len(want)}"
+        for i, (g, w) in enumerate(zip(got, want)):
+            assert_same_exact(g, w, f"{path}[{i}]", exact_floats, report)
+    elif isinstance(want, str):
+        assert got == want, f"{path}: {got!r} != {want!r}"
+    else:
+        _exact_leaf(got, want, _exact, path, _key, exact_floats, report)
+
+
+def strip_exact(tree):
+    """An oracle result run with exact=True, without its "_exact" objects (for assert_same)."""
+    if isinstance(tree, dict):
+        return {k: strip_exact(v) for k, v in tree.items() if k != "_exact"}
+    if isinstance(tree, list):
+        return [strip_exact(v) for v in tree]
+    return tree
 
 
 def bits_from_mask(mask):

@@ -18,7 +18,7 @@ from elasticsearch_amd import AggregationBuilders as AB
 from elasticsearch_amd import Order, QueryBuilders as QB
 from elasticsearch_amd import _native as N
 from elasticsearch_amd import reduce
-from helpers import assert_same, bits_from_mask, synthetic_columns
+from helpers import assert_same, assert_same_exact, bits_from_mask, synthetic_columns
 
 pytestmark = pytest.mark.gpu
 
@@ -134,9 +134,10 @@ def test_timestamps_over_2_32_ms(engine, name):
 
 @pytest.mark.parametrize("name", ["compact", "packed"])
 def test_packed_metric_edge_values(engine, name):
-    """Packed cells decode count * base + sum of deltas: negative metrics, a base far from zero (sums beyond 2^53,
-    compared at the big-sum tolerance; values spanning < 2^16, read as u16 deltas), deltas near 2^32, and two segments whose metric bases differ -- each decoded with
-    its own base; stats, avg and extended_stats (the latter never packed) side by side."""
+    """Packed cells decode count * base + sum of deltas: negative metrics, a base far from zero (sums beyond 2^53:
+    compensated into the grid, checked against the exact sums; values spanning < 2^16, read as u16 deltas), deltas near
+    2^32, and two segments whose metric bases differ -- each decoded with its own base; stats, avg and extended_stats
+    (the latter never packed) side by side."""
     rng = np.random.default_rng(42)
     t0 = 1_441_065_600_000
     segs_cols = []
@@ -150,13 +151,13 @@ def test_packed_metric_edge_values(engine, name):
                 AB.dateHistogram("d").field("@timestamp").interval("1h").minDocCount(0).subAggregation(AB.stats("s").field("rt"))),
             AB.terms("a").field("host").size(9).subAggregation(AB.avg("m").field("rt")),
             AB.terms("x").field("host").size(4).subAggregation(AB.extendedStats("e").field("rt"))]
-    want = O.run([(allc, ntot)], aggs)
+    want = O.run([(allc, ntot)], aggs, exact=True)
     with layout(engine, name):
         segs = [engine.upload_segment(c, n) for c, n in segs_cols]
         res, _ = _run(engine, None, aggs, segs=segs)
         for s in segs:
             s.close()
-    assert_same(res.to_dict(), want["shards"][0], f"{name} shard", exact_floats=False)
+    assert_same_exact(res.to_dict(), want["shards"][0], f"{name} shard", exact_floats=True)
 
 
 def test_packed_then_sparse_metric_segment(engine):
