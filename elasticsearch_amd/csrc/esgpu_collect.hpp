@@ -35,6 +35,12 @@ constexpr uint32_t kGroup = kGroupBlocks;  // blocks per multi-pass group (esgpu
 #ifndef ESGPU_NBUF_COMPACT  // load buffers of the metric / two-dimension shapes over compact columns
 #define ESGPU_NBUF_COMPACT 2
 #endif
+#ifndef ESGPU_NBUF_HIST  // load buffers of the raw-load counting histogram grids (VK bit 1024: timestamp deltas)
+#define ESGPU_NBUF_HIST 4  // with 6 waves per SIMD: date_histogram at 1B docs 0.92 -> 0.84 ms (r5c)
+#endif
+#ifndef ESGPU_NBUF_HIST_MET  // ... and of those with a metric (their run accumulators take the registers)
+#define ESGPU_NBUF_HIST_MET 2
+#endif
 #ifndef ESGPU_NBUF_PI  // load buffers with packed integer metric cells (all columns compact)
 #define ESGPU_NBUF_PI 2
 #endif
@@ -149,6 +155,11 @@ constexpr bool kRawPI = MET > 0 && (VK & 64) != 0 && (VK & 16) != 0 && (VK & 256
 // deltas, a histogram-only grid's u32 metric deltas -- the same raw loads, unpacked when processed
 template <bool ORD, int MET, int VK>
 constexpr bool kRawH = (VK & 1024) != 0;
+// VK bit 2048 (with 1024): a histogram-only grid over a dense long metric whose values span < 2^16 and stay below 2^26 in
+// magnitude -- the metric read as its 16-bit deltas and the run accumulators kept as integers (count, sum of deltas, sum
+// of squared deltas, min / max delta): exact, and a third of the VALU work of the f64 runs; decoded at the run's flush
+template <bool ORD, int MET, int VK>
+constexpr bool kIntRuns = !ORD && MET > 0 && (VK & 2048) != 0;
 
 template <bool ORD, bool HIST, int MET, int VK>
 __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0, Doc4& d) {
@@ -174,7 +185,10 @@ __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0,
             const u32x4_t t = load16(P.hv32 + doc0);
             d.raw[2] = t.x; d.raw[3] = t.y; d.raw[4] = t.z; d.raw[5] = t.w;
         }
-        if constexpr (MET > 0) {
+        if constexpr (MET > 0 && (VK & 2048) != 0) {
+            const u32x2_t m = load8(P.mv16 + doc0);
+            d.raw[6] = m.x; d.raw[7] = m.y;
+        } else if constexpr (MET > 0) {
             const u32x4_t m = load16(P.mv32 + doc0);
             d.raw[6] = m.x; d.raw[7] = m.y; d.raw[8] = m.z; d.raw[9] = m.w;
         }
@@ -422,6 +436,10 @@ struct Run {
     uint32_t cnt, vc;
     double sum, sq;
     unsigned long long mn, mx;
+    // integer runs (kIntRuns): sum of deltas, sum of squared deltas, min / max delta (a thread's run holds at most one
+    // workgroup range of docs, < 2^19: the sums cannot overflow)
+    uint32_t isd, imn, imx;
+    unsigned long long isq;
 };
 
 __device__ __forceinline__ void run_reset(Run& r) {
@@ -432,6 +450,36 @@ __device__ __forceinline__ void run_reset(Run& r) {
     r.sq = 0.0;
     r.mn = kMinInit;
     r.mx = kMaxInit;
+    r.isd = 0;
+    r.isq = 0;
+    r.imn = ~0u;
+    r.imx = 0;
+}
+
+// an integer run into its LDS cell: the values are v = mv_base + d, so sum = cnt * base + sum d and sum of squares =
+// cnt * base^2 + 2 * base * sum d + sum d^2 -- exact in 128 bits, one rounding to double (exact while the request's sums
+// stay below 2^53, the plan's compensated flushes past it); extrema are the casts of base + the delta extrema
+template <int MET, int MS>
+__device__ __forceinline__ void run_flush_i(const CollectParams& P, const Acc& a, Run& r) {
+    if (r.slot != 0xFFFFFFFFu) {
+        const uint32_t c = r.slot;
+        atomicAdd(&a.cnt32[c], r.cnt);
+        const long long base = P.mv_base;
+        atomicAdd(&a.sum[c], (double)((long long)r.cnt * base + (long long)r.isd));
+        if (MET >= 2) {
+            const unsigned long long emn = sortable((double)(base + (long long)r.imn));
+            const unsigned long long emx = sortable((double)(base + (long long)r.imx));
+            const unsigned long long cmn = a.mn[MS * c], cmx = a.mx[MS * c];
+            if (emn < cmn) atomicMin(&a.mn[MS * c], emn);
+            if (emx > cmx) atomicMax(&a.mx[MS * c], emx);
+        }
+        if (MET >= 3) {
+            const __int128 b = base;
+            const __int128 q = (__int128)r.cnt * b * b + 2 * b * (__int128)r.isd + (__int128)r.isq;
+            atomicAdd(&a.sq[c], (double)q);
+        }
+    }
+    run_reset(r);
 }
 
 template <int MET, int MS>
@@ -460,7 +508,14 @@ __device__ __forceinline__ void run_flush(const CollectParams& P, const Acc& a, 
 #define ESGPU_RUNS 3
 #endif
 // counting only (MET 0): one run -- a count flush is a single LDS add, and the run array would go to scratch
-template <int MET> constexpr int runs_for() { return MET == 0 ? 1 : ESGPU_RUNS; }
+#ifndef ESGPU_INT_RUNS_NR  // integer run accumulators (VK bit 2048) per thread
+#define ESGPU_INT_RUNS_NR 3
+#endif
+// VK bit 4096 (with 2048): time-sorted data (a block's keys span less than one interval: CollectParams.runs1) -- one integer
+// run per thread, a third of the registers and no run lookup (config 2 at 1B docs: 1.46 -> 1.12 ms, r5d)
+template <int MET, int VK = 0> constexpr int runs_for() {
+    return MET == 0 ? 1 : (VK & 4096) != 0 ? 1 : (VK & 2048) != 0 ? ESGPU_INT_RUNS_NR : ESGPU_RUNS;
+}
 template <int NR>
 struct Runs {
     Run r[NR];
@@ -503,10 +558,43 @@ __device__ __forceinline__ void pi_hot_flush(const CollectParams& P, const Acc& 
     R.hhi = 0u;
     R.hpk = 0ull;
 }
-template <int MET, int MS, int NR>
+template <int MET, int MS, int NR, bool INT = false>
 __device__ __forceinline__ void runs_flush(const CollectParams& P, const Acc& a, Runs<NR>& R) {
 #pragma unroll
-    for (int k = 0; k < NR; ++k) run_flush<MET, MS>(P, a, R.r[k]);
+    for (int k = 0; k < NR; ++k) {
+        if constexpr (INT) run_flush_i<MET, MS>(P, a, R.r[k]);
+        else run_flush<MET, MS>(P, a, R.r[k]);
+    }
+}
+// n docs of one key slot into the integer run of `slot` (n = 1: one doc; 4: a thread's 4 docs that share the slot,
+// combined first): sd / sq / mn / mx are the docs' delta sum, squared-delta sum and extrema
+template <int MET, int MS, int NR>
+__device__ __forceinline__ void runs_add_i(const CollectParams& P, const Acc& a, Runs<NR>& R, uint32_t slot, uint32_t n,
+                                           uint32_t sd, unsigned long long sq, uint32_t mn, uint32_t mx) {
+    int hit = -1;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) hit = R.r[k].slot == slot ? k : hit;
+    if (hit < 0) {
+        hit = NR == 1 ? 0 : (int)R.victim;
+#pragma unroll
+        for (int k = 0; k < NR; ++k)
+            if (k == hit) {
+                run_flush_i<MET, MS>(P, a, R.r[k]);
+                R.r[k].slot = slot;
+            }
+        if (NR > 1) R.victim = R.victim + 1 == (uint32_t)NR ? 0u : R.victim + 1;
+    }
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+        const bool h = hit == k;
+        R.r[k].cnt += h ? n : 0u;
+        R.r[k].isd += h ? sd : 0u;
+        if (MET >= 3) R.r[k].isq += h ? sq : 0ull;
+        if (MET >= 2) {
+            R.r[k].imn = h && mn < R.r[k].imn ? mn : R.r[k].imn;
+            R.r[k].imx = h && mx > R.r[k].imx ? mx : R.r[k].imx;
+        }
+    }
 }
 template <int MET, int MS, int NR>
 __device__ __forceinline__ void runs_add(const CollectParams& P, const Acc& a, Runs<NR>& R, uint32_t slot, bool mpres, double x) {
@@ -641,7 +729,7 @@ __device__ __forceinline__ void unpack_docs(const CollectParams& P, Doc4& d) {
 
 template <bool ORD, bool HIST, int MET, bool LDS, bool KT, int MS, bool HORD = false, int VK = 0>
 __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, const Doc4& d_in, uint32_t T, int64_t base,
-                                         uint32_t win0, Runs<runs_for<MET>()>& run, uint32_t mw = 0, bool outer = true) {
+                                         uint32_t win0, Runs<runs_for<MET, VK>()>& run, uint32_t mw = 0, bool outer = true) {
     Doc4 du;
     if constexpr (kRawPI<MET, VK, HIST>) {
         du = d_in;
@@ -660,7 +748,10 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
             for (int j = 0; j < 4; ++j) du.hv[j] = P.hv_base + (int64_t)du.raw[2 + j];
             du.hpres = 0xFu;
         }
-        if constexpr (MET > 0) {
+        if constexpr (MET > 0 && (VK & 2048) != 0) {  // integer runs: the 16-bit deltas as they are
+            du.mvd[0] = du.raw[6] & 0xFFFFu; du.mvd[1] = du.raw[6] >> 16; du.mvd[2] = du.raw[7] & 0xFFFFu; du.mvd[3] = du.raw[7] >> 16;
+            du.mpres = 0xFu;
+        } else if constexpr (MET > 0) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) du.mv[j] = (double)(P.mv_base + (int64_t)du.raw[6 + j]);  // FieldData.castToDouble of the long
             du.mpres = 0xFu;
@@ -694,6 +785,28 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
                 slot[j] = (uint32_t)k;
             }
         }
+    }
+    if constexpr (LDS && kIntRuns<ORD, MET, VK>) {
+        // integer runs: a thread's 4 docs that all pass and share one slot (time-sorted data: nearly always) are combined
+        // into one run update; otherwise one update per doc
+        const bool all4 = d.ok == 0xFu && hv_ok[0] && hv_ok[1] && hv_ok[2] && hv_ok[3] && slot[0] == slot[1] &&
+                          slot[0] == slot[2] && slot[0] == slot[3];
+        if (all4) {
+            const uint32_t x0 = d.mvd[0], x1 = d.mvd[1], x2 = d.mvd[2], x3 = d.mvd[3];
+            const unsigned long long q = MET >= 3 ? (unsigned long long)(x0 * x0) + (x1 * x1) + (unsigned long long)(x2 * x2) +
+                                                        (x3 * x3)
+                                                  : 0ull;
+            runs_add_i<MET, MS>(P, a, run, slot[0], 4u, x0 + x1 + x2 + x3, q, min(min(x0, x1), min(x2, x3)),
+                                max(max(x0, x1), max(x2, x3)));
+        } else {
+#pragma unroll
+            for (int j = 0; j < kVec; ++j) {
+                if (!((d.ok >> j) & 1) || !hv_ok[j]) continue;
+                const uint32_t x = d.mvd[j];
+                runs_add_i<MET, MS>(P, a, run, slot[j], 1u, x, (unsigned long long)(x * x), x, x);
+            }
+        }
+        return;
     }
     if (LDS && !ORD) {  // ocnt_mode is OCNT_NONE without a terms dimension; without HIST the slot is always 0
         if (ESGPU_RUN4) {
@@ -1018,14 +1131,20 @@ __device__ __forceinline__ uint32_t claim_chunk(unsigned int* claim) {
 #endif
 // 4 waves per SIMD (16 per CU): <= 128 VGPRs; packed-cell kernels ESGPU_PI_WAVES (6: <= 80 VGPRs, 24 waves per CU with the
 // runtime's ESGPU_LDS_PI window budget -- the stream's bytes in flight scale with the waves)
-#ifndef ESGPU_HIST_WAVES  // raw-load histogram-only grids (VK bit 1024): waves per SIMD
-#define ESGPU_HIST_WAVES 4
+#ifndef ESGPU_HIST_WAVES  // raw-load counting histogram grids (VK bit 1024): waves per SIMD
+#define ESGPU_HIST_WAVES 6
 #endif
-template <bool ORD, int VK, int WGS> constexpr int collect_min_waves() {
-    return (VK & 64) && WGS == 512 ? ESGPU_PI_WAVES : !ORD && (VK & 1024) && WGS == 512 ? ESGPU_HIST_WAVES : 4;
+#ifndef ESGPU_HIST_MET_WAVES  // raw-load histogram-only grids with a metric: waves per SIMD
+#define ESGPU_HIST_MET_WAVES 4
+#endif
+template <bool ORD, int MET, int VK, int WGS> constexpr int collect_min_waves() {
+    return (VK & 64) && WGS == 512                    ? ESGPU_PI_WAVES
+           : !ORD && (VK & 1024) && WGS == 512 && MET == 0 ? ESGPU_HIST_WAVES
+           : !ORD && (VK & 1024) && WGS == 512        ? ESGPU_HIST_MET_WAVES
+                                                     : 4;
 }
 template <bool ORD, int HK, int MET, int VK, int WGS>
-__global__ __launch_bounds__(WGS, (collect_min_waves<ORD, VK, WGS>())) void collect_kernel(CollectParams P) {
+__global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void collect_kernel(CollectParams P) {
     constexpr int kIterDocsW = WGS * kVec;
     constexpr int kItersPerBlockW = kBlockDocs / kIterDocsW;
     constexpr bool HIST = HK != 0;
@@ -1131,7 +1250,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, VK, WGS>())) void coll
     bool dirty = false;
     int64_t base = HIST ? P.key0 * P.interval + P.offset : 0;  // value of the first LDS slot
 
-    Runs<runs_for<MET>()> run;
+    Runs<runs_for<MET, VKL>()> run;
     runs_reset(run);
     // software pipeline over two buffers: each is reloaded (iteration i + 2) right after it is processed, so one
     // buffer's loads are in flight while the other is processed.  Loads are unconditional (past the end: the last
@@ -1149,7 +1268,9 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, VK, WGS>())) void coll
     const uint32_t tid4 = threadIdx.x * kVec;
     // shapes that read few bytes per doc (one ordinal or one key column) keep 4 buffers in flight, the rest 2 (their
     // buffers are 5x larger; 4 would cost occupancy).  kItersPerBlockW (4) is a multiple of either.
-    constexpr int kBuf = (MET == 0 && !(ORD && HIST)) ? ESGPU_NBUF_NARROW
+    constexpr int kBuf = (kRawH<ORD, MET, VK> && !ORD && MET == 0) ? (ESGPU_NBUF_HIST <= kItersPerBlockW ? ESGPU_NBUF_HIST : kItersPerBlockW)
+                         : (kRawH<ORD, MET, VK> && !ORD) ? (ESGPU_NBUF_HIST_MET <= kItersPerBlockW ? ESGPU_NBUF_HIST_MET : kItersPerBlockW)
+                         : (MET == 0 && !(ORD && HIST)) ? ESGPU_NBUF_NARROW
                          : (VK & 64) ? (ESGPU_NBUF_PI <= kItersPerBlockW ? ESGPU_NBUF_PI : kItersPerBlockW)
                          : ((VK & 176) ? (ESGPU_NBUF_COMPACT <= kItersPerBlockW ? ESGPU_NBUF_COMPACT : kItersPerBlockW) : 2);
     static_assert(kItersPerBlockW % kBuf == 0, "buffers per block");
@@ -1163,7 +1284,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, VK, WGS>())) void coll
     uint32_t pass = 0, npass = 1;                        // npass > 1: a multi-pass group
     auto slide_to = [&](uint32_t k0) {
         if (dirty) {
-            if (!ORD) runs_flush<MET, kMS>(P, s, run);
+            if (!ORD) runs_flush<MET, kMS, runs_for<MET, VKL>(), kIntRuns<ORD, MET, VKL>>(P, s, run);
             if constexpr (PI && ESGPU_PI_HOT) pi_hot_flush<MET>(P, s, run, T);
             if constexpr (PI) flush_window_pi<MET, WGS>(P, s, T, W, win0, ncp);
             else flush_window<MET, kMS, WGS>(P, s, T, W, win0, ncp);
@@ -1258,7 +1379,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, VK, WGS>())) void coll
         }
     }
     if (P.lds_mode && (dirty || !(HIST && P.windowed))) {
-        if (!ORD) runs_flush<MET, kMS>(P, s, run);
+        if (!ORD) runs_flush<MET, kMS, runs_for<MET, VKL>(), kIntRuns<ORD, MET, VKL>>(P, s, run);
         if constexpr (PI && ESGPU_PI_HOT) pi_hot_flush<MET>(P, s, run, T);
         if constexpr (PI) flush_window_pi<MET, WGS>(P, s, T, W, win0, ncp);
         else flush_window<MET, kMS, WGS>(P, s, T, W, win0, ncp);
@@ -1319,11 +1440,13 @@ static auto with_vk0(bool hv_f64, bool mv_f64, F f) {
 // over a long column.
 template <bool ORD, int HK, int MET, class F>
 static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, bool pi, bool m32, bool m16, bool acc, bool raw,
-                    F f) {
+                    bool runs1, F f) {
     // VK bit 128, a compact long metric (u32 deltas, values restored in the loader): histogram-only grids over compact
     // timestamps (date_histogram{stats / extended_stats / avg}) and extended_stats under terms over compact columns
     if constexpr (MET > 0 && !ORD && HK == 1) {
         if (m32 && !pi && !mv_f64 && t32 && !hv_f64) {
+            if (raw && m16 && runs1) return f(std::integral_constant<int, 32 | 128 | 1024 | 2048 | 4096>{});
+            if (raw && m16) return f(std::integral_constant<int, 32 | 128 | 1024 | 2048>{});
             if (raw) return f(std::integral_constant<int, 32 | 128 | 1024>{});
             return f(std::integral_constant<int, 32 | 128>{});
         }
@@ -1402,8 +1525,8 @@ static auto with_wg(bool wide, F f) {
 template <bool ORD, int HK, int MET>
 static void launch_t(const CollectParams& p, bool wide, uint32_t grid, size_t lds, hipStream_t st) {
     with_vk<ORD, HK, MET>(p.hv_f64 != 0, p.mv_f64 != 0, p.ord_src != nullptr, p.ord16 != nullptr, p.hv32 != nullptr,
-                          p.mv32 != nullptr && p.pk_shift != 0, p.mv32 != nullptr && p.pk_shift == 0, p.mv16 != nullptr,
-                          p.accept != nullptr, p.raw_dense != 0, [&](auto vk) {
+                          (p.mv32 || p.mv16) && p.pk_shift != 0, (p.mv32 || p.mv16) && p.pk_shift == 0, p.mv16 != nullptr,
+                          p.accept != nullptr, p.raw_dense != 0, p.runs1 != 0, [&](auto vk) {
         return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
             hipLaunchKernelGGL((collect_kernel<ORD, HK, MET, decltype(vk)::value, decltype(wg)::value>), dim3(grid),
                                dim3(decltype(wg)::value), lds, st, p);
@@ -1426,7 +1549,7 @@ template <bool ORD, int HK, int MET>
 static int occ_t(size_t lds, int vkbits, bool wide) {
     return with_vk<ORD, HK, MET>((vkbits & 1) != 0, (vkbits & 2) != 0, (vkbits & 8) != 0, (vkbits & 16) != 0,
                                  (vkbits & 32) != 0, (vkbits & 64) != 0, (vkbits & 128) != 0, (vkbits & 256) != 0,
-                                 (vkbits & 512) != 0, (vkbits & 1024) != 0, [&](auto vk) {
+                                 (vkbits & 512) != 0, (vkbits & 1024) != 0, (vkbits & 4096) != 0, [&](auto vk) {
         return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
             int n = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(

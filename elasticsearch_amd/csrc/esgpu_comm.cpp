@@ -8,8 +8,12 @@
 #include <rccl/rccl.h>
 
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
+#include <string>
 #include <vector>
 
 #include "../../include/esgpu.h"
@@ -84,6 +88,13 @@ struct RcclCollective : Collective {
         allgather_bytes += total;
         ++collectives;
     }
+    void allgather_dev(const void* d_in, void* d_out, uint64_t bytes, void* stream) override {
+        Clock clk(*this);
+        HIPX(hipSetDevice(ctx->device));
+        NCCLX(ncclAllGather(d_in, d_out, bytes, ncclUint8, comm, (hipStream_t)stream));  // no host round trip
+        allgather_bytes += bytes * nranks;
+        ++collectives;
+    }
 };
 
 // a caller's transport (esgpu_comm_init_host)
@@ -99,6 +110,117 @@ struct HostCollective : Collective {
     void allgather(const void* in, void* out, uint64_t bytes) override {
         Clock clk(*this);
         require(t.allgather(t.user, in, out, bytes) == 0, ESGPU_ERR_DEVICE, "host transport all-gather failed");
+        allgather_bytes += bytes * nranks;
+        ++collectives;
+    }
+    PinnedBuf h_in, h_out;
+    void allgather_dev(const void* d_in, void* d_out, uint64_t bytes, void* stream) override {
+        // the caller's transport moves host memory: the operand staged through pinned buffers
+        hipStream_t st = (hipStream_t)stream;
+        void* hi = h_in.ensure(std::max<size_t>(bytes, 1));
+        void* ho = h_out.ensure(std::max<size_t>(bytes * nranks, 1));
+        HIPX(hipMemcpyAsync(hi, d_in, bytes, hipMemcpyDeviceToHost, st));
+        HIPX(hipStreamSynchronize(st));
+        allgather(hi, ho, bytes);
+        HIPX(hipMemcpyAsync(d_out, ho, bytes * nranks, hipMemcpyHostToDevice, st));
+        HIPX(hipStreamSynchronize(st));  // the staging buffer is reused by the next call
+    }
+};
+
+// in-process ranks (esgpu_comm_init_local): the threads of one process, one context each, meet at barriers; host
+// operands are copied between their buffers, device operands device to device on each rank's stream
+struct LocalGroup {
+    std::mutex mu;
+    std::condition_variable cv;
+    int n = 0, arrived = 0;
+    uint64_t gen = 0;
+    std::vector<const void*> src;
+    std::vector<hipEvent_t> ready, done;
+    bool broken = false;
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        require(!broken, ESGPU_ERR_DEVICE, "in-process communicator: a rank failed");
+        const uint64_t g = gen;
+        if (++arrived == n) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+        } else if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return gen != g || broken; }) || broken) {
+            broken = true;  // a rank that never arrives (it failed): every waiting rank fails instead of hanging
+            cv.notify_all();
+            throw EsError(ESGPU_ERR_DEVICE, "in-process communicator: a rank did not reach the collective");
+        }
+    }
+};
+std::mutex g_local_mu;
+std::map<std::string, std::weak_ptr<LocalGroup>> g_local_groups;
+
+struct LocalCollective : Collective {
+    std::shared_ptr<LocalGroup> g;
+    hipEvent_t ready = nullptr, done = nullptr;
+    std::vector<uint8_t> tmp;
+    ~LocalCollective() override {
+        if (ready) (void)hipEventDestroy(ready);
+        if (done) (void)hipEventDestroy(done);
+    }
+    void allreduce(void* buf, uint64_t count, int dt, int op) override {
+        if (!count) return;
+        Clock clk(*this);
+        const size_t bytes = count * dt_size(dt);
+        g->src[rank] = buf;
+        g->barrier();
+        tmp.assign((const uint8_t*)g->src[0], (const uint8_t*)g->src[0] + bytes);  // rank order: rank 0 first
+        for (int r = 1; r < nranks; ++r) {
+            const void* s = g->src[r];
+            for (uint64_t i = 0; i < count; ++i) {
+                switch (dt) {
+                    case ESGPU_DT_U8: red(((uint8_t*)tmp.data())[i], ((const uint8_t*)s)[i], op); break;
+                    case ESGPU_DT_I64: red(((int64_t*)tmp.data())[i], ((const int64_t*)s)[i], op); break;
+                    case ESGPU_DT_U64: red(((uint64_t*)tmp.data())[i], ((const uint64_t*)s)[i], op); break;
+                    default: red(((double*)tmp.data())[i], ((const double*)s)[i], op); break;
+                }
+            }
+        }
+        g->barrier();  // every rank has read every operand
+        std::memcpy(buf, tmp.data(), bytes);
+        allreduce_bytes += bytes;
+        ++collectives;
+    }
+    template <class T> static void red(T& a, T b, int op) {
+        if (op == ESGPU_RED_SUM) a = a + b;
+        else if (op == ESGPU_RED_MIN) a = b < a ? b : a;
+        else a = b > a ? b : a;
+    }
+    void allgather(const void* in, void* out, uint64_t bytes) override {
+        Clock clk(*this);
+        g->src[rank] = in;
+        g->barrier();
+        for (int r = 0; r < nranks; ++r) std::memcpy((uint8_t*)out + (size_t)r * bytes, g->src[r], bytes);
+        g->barrier();
+        allgather_bytes += bytes * nranks;
+        ++collectives;
+    }
+    void allgather_dev(const void* d_in, void* d_out, uint64_t bytes, void* stream) override {
+        Clock clk(*this);
+        hipStream_t st = (hipStream_t)stream;
+        if (!ready) {
+            HIPX(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+            HIPX(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+        }
+        HIPX(hipEventRecord(ready, st));  // this rank's operand is written once its stream reaches here
+        g->src[rank] = d_in;
+        g->ready[rank] = ready;
+        g->barrier();
+        for (int r = 0; r < nranks; ++r) {
+            if (r != rank) HIPX(hipStreamWaitEvent(st, g->ready[r], 0));
+            HIPX(hipMemcpyAsync((uint8_t*)d_out + (size_t)r * bytes, g->src[r], bytes, hipMemcpyDeviceToDevice, st));
+        }
+        HIPX(hipEventRecord(done, st));
+        g->done[rank] = done;
+        g->barrier();
+        // no rank's later work (the next request rewriting its operand) runs before every rank has copied it
+        for (int r = 0; r < nranks; ++r)
+            if (r != rank) HIPX(hipStreamWaitEvent(st, g->done[r], 0));
         allgather_bytes += bytes * nranks;
         ++collectives;
     }
@@ -150,6 +272,45 @@ extern "C" int esgpu_comm_init_host(int32_t nranks, int32_t rank, const esgpu_ho
         std::unique_ptr<esgpu_comm> cm(new esgpu_comm());
         cm->coll = std::move(h);
         *out = cm.release();
+    });
+}
+
+extern "C" int esgpu_comm_init_local(const char* group, int32_t nranks, int32_t rank, esgpu_comm** out) {
+    return guarded([&] {
+        require(group && out && nranks >= 1 && rank >= 0 && rank < nranks, ESGPU_ERR_INVALID, "bad communicator arguments");
+        std::shared_ptr<LocalGroup> g;
+        {
+            std::lock_guard<std::mutex> lk(g_local_mu);
+            std::weak_ptr<LocalGroup>& w = g_local_groups[group];
+            g = w.lock();
+            if (!g || g->n != nranks) {
+                g = std::make_shared<LocalGroup>();
+                g->n = nranks;
+                g->src.assign(nranks, nullptr);
+                g->ready.assign(nranks, nullptr);
+                g->done.assign(nranks, nullptr);
+                w = g;
+            }
+        }
+        std::unique_ptr<LocalCollective> c(new LocalCollective());
+        c->g = g;
+        c->nranks = nranks;
+        c->rank = rank;
+        std::unique_ptr<esgpu_comm> cm(new esgpu_comm());
+        cm->coll = std::move(c);
+        *out = cm.release();
+    });
+}
+
+namespace esgpu {
+Collective& comm_collective(esgpu_comm* c) { return *c->coll; }
+}  // namespace esgpu
+
+extern "C" int esgpu_comm_last_build_reduce(const esgpu_comm* cm, int32_t* path, double* host_ms) {
+    return guarded([&] {
+        require(cm != nullptr, ESGPU_ERR_INVALID, "null communicator");
+        if (path) *path = cm->coll->last_path;
+        if (host_ms) *host_ms = cm->coll->last_host_ms;
     });
 }
 

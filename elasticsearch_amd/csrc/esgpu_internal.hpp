@@ -169,3 +169,9 @@ struct Scratch {
     template <class T> T* as() const { return buf.as<T>(); }
 };
 
+
+// the collectives of a communicator (esgpu_comm.cpp), for the device-resident reduce across ranks in the runtime
+namespace esgpu {
+struct Collective;
+Collective& comm_collective(esgpu_comm* c);
+}  // namespace esgpu

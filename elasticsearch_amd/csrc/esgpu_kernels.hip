@@ -1257,6 +1257,41 @@ void launch_colo_select(const unsigned long long* tot, const ColoTotals* d, uint
     hipLaunchKernelGGL(colo_select_kernel, dim3(n), dim3(1024), 0, st, tot, d, Tmax, S, out);
 }
 
+// the cross-rank co-located reduce: one local shard's rows of the final terms as [F][Hmax][R] words (F = 1 + 5 leaves),
+// which colo_merge_kernel reads as a grid with T = R (the final bucket index as the ordinal); an absent row is zeros
+__global__ __launch_bounds__(256) void colo_pack_kernel(ColoPackParams P) {
+    __shared__ ColoShard S;  // the descriptor from pinned host memory, once per workgroup
+    const uint32_t i = blockIdx.y;
+    if (threadIdx.x < sizeof(ColoShard) / 8)
+        ((unsigned long long*)&S)[threadIdx.x] = ((const unsigned long long*)(P.shards + i))[threadIdx.x];
+    __syncthreads();
+    const size_t HR = (size_t)P.Hmax * P.R;
+    const size_t e = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= HR) return;
+    const uint32_t m = (uint32_t)(e / P.R), b = (uint32_t)(e - (size_t)m * P.R);
+    const int32_t ord = P.rows[(size_t)b * P.n + i];
+    const bool ok = ord >= 0 && m < S.H && (uint32_t)ord < S.T;
+    const size_t cell = ok ? (size_t)m * S.T + (uint32_t)ord : 0;
+    unsigned long long* o = P.out + (size_t)i * (1 + 5 * (size_t)P.nleaves) * HR + e;
+    const unsigned long long c = !ok ? 0ull : S.cnt32 ? ((const unsigned int*)S.cnt)[cell] : S.cnt[cell];
+    o[0] = c;
+    for (int l = 0; l < P.nleaves; ++l) {
+        unsigned long long* f = o + (size_t)(1 + 5 * l) * HR;
+        f[0] = !ok ? 0ull : S.lcnt[l] ? S.lcnt[l][cell] : c;
+        f[HR] = ok ? dbl_bits(S.lsum[l][cell]) : 0ull;
+        if (S.lmn[l]) {
+            f[2 * HR] = ok ? S.lmn[l][cell] : kMinInit;
+            f[3 * HR] = ok ? S.lmx[l][cell] : kMaxInit;
+        }
+        if (S.lsq[l]) f[4 * HR] = ok ? dbl_bits(S.lsq[l][cell]) : 0ull;
+    }
+}
+void launch_colo_pack(const ColoPackParams& p, hipStream_t st) {
+    const size_t HR = (size_t)p.Hmax * p.R;
+    if (HR == 0 || p.n == 0) return;
+    hipLaunchKernelGGL(colo_pack_kernel, dim3((uint32_t)((HR + 255) / 256), p.n), dim3(256), 0, st, p);
+}
+
 void launch_colo_merge(const ColoParams& p, hipStream_t st) {
     if (p.R == 0 || p.Hm == 0) return;
     hipLaunchKernelGGL(colo_merge_kernel, dim3((p.Hm + 255) / 256, p.R), dim3(256), 0, st, p);

@@ -105,6 +105,7 @@ struct CollectParams {
     uint32_t pk_shift;
     uint32_t hot_t;      // the segment's most frequent ordinal (a sampled hint; kMissingOrd: none) -- ESGPU_PI_HOT builds
     int32_t raw_dense;   // histogram-only grid over dense compact columns, no filter: the raw-load kernels (VK bit 1024)
+    int32_t runs1;       // integer runs over time-sorted data: one run accumulator per thread (VK bit 4096)
     int32_t vcnt_mode;   // separate value counts (metric column has missing values)
     int32_t ocnt_mode;   // separate outer-level doc counts (inner dimension column has missing values)
     uint32_t ncopies;    // terms-only LDS grids: copies of the additive cells (count, value count, sum, sum of squares);
@@ -264,6 +265,17 @@ struct ColoParams {
     double *o_sum, *o_min, *o_max, *o_sq;  // [nleaves][R][Hm]
 };
 void launch_colo_merge(const ColoParams& p, hipStream_t s);
+// the co-located reduce across ranks (esgpu_comm_build_reduce): each local shard's rows of the final terms packed as
+// [F][Hmax][R] 8-byte words (F = 1 + 5 leaves: the bucket counts, then per leaf its value counts, sums, min, max and sums
+// of squares), which colo_merge_kernel reads as a grid with T = R (the final bucket index as the ordinal)
+struct ColoPackParams {
+    const ColoShard* shards;  // [n] the local shards (pinned, device-mapped)
+    const int32_t* rows;      // [R][n]: the final bucket's ordinal in local shard i, -1 when the shard did not return it
+    uint32_t n, R, Hmax;
+    int32_t nleaves;
+    unsigned long long* out;  // [n][1 + 5 * nleaves][Hmax][R]
+};
+void launch_colo_pack(const ColoPackParams& p, hipStream_t s);
 // the co-located reduce's selection input: every shard's per-ordinal doc counts, summed over the [H][T] grid rows,
 // written to out[shard][Tmax] (pinned, device-mapped) by one launch over all the shards
 struct ColoTotals {

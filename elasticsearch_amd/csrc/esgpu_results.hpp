@@ -118,9 +118,14 @@ struct Collective {
     uint64_t allreduce_bytes = 0, allgather_bytes = 0;  // per reduce call (statistics)
     int32_t collectives = 0;
     double exchange_ms = 0;                             // wall time inside the collectives of the last reduce
+    int32_t last_path = 0;                              // esgpu_comm_build_reduce: 1 device-resident, 0 builds + reduce
+    double last_host_ms = 0;                            // ... and its host time once the local collects had finished
     virtual ~Collective() {}
     virtual void allreduce(void* buf, uint64_t count, int dtype, int op) = 0;  // in place
     virtual void allgather(const void* in, void* out, uint64_t bytes) = 0;     // out: nranks * bytes, rank order
+    // device operands, enqueued on `stream` (a hipStream_t): RCCL gathers device to device; a host transport stages
+    // through pinned memory
+    virtual void allgather_dev(const void* d_in, void* d_out, uint64_t bytes, void* stream) = 0;
 };
 // InternalAggregations.reduce over every rank's shard results, the shards in rank-major order (rank r's `locals` are
 // global shards r * n_local ...).  Fixed-shape partials are combined by all-reduce: top-level histograms with numeric

@@ -1044,6 +1044,11 @@ struct esgpu_plan {
     PinnedBuf h_colo_meta;  // shard descriptors + the rows table (pinned, device-mapped: read once per workgroup)
     PinnedBuf h_colo_tot;   // every shard's per-ordinal doc counts, or its picks (pinned, device-mapped)
     Scratch s_colo_tot;     // every shard's per-ordinal doc counts (device selection)
+    // the co-located reduce across ranks (esgpu_comm_build_reduce): local and all-gathered selection records, the packed
+    // rows sent and received, the records on the host, the pack's descriptors; the event other local plans wait on
+    Scratch s_xr_picks, s_xr_allpicks, s_xr_send, s_xr_recv;
+    PinnedBuf h_xr_picks, h_xr_meta;
+    hipEvent_t ev_xr = nullptr;
     int32_t last_path = 0;
     // per-request scratch, reused across requests
     Scratch s_accept, s_tcnt, s_rows, s_dst[6];
@@ -1626,6 +1631,8 @@ static bool replay_compaction();
 static bool d16_on();
 static bool raw_hist_on();
 static bool dd_forced();
+static bool int_runs_on();
+static bool runs1_on();
 static bool pi_cells(const esgpu_ctx* c);
 static uint32_t pi_copies();
 static const uint16_t* ensure_ord16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
@@ -2886,16 +2893,19 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     if (pi_cells(p->ctx) && compact_cols(p->ctx) && L_ORD && !P.ord_src && (L_met == 1 || L_met == 2) && mc && mc->type == ESGPU_COL_I64 &&
         !mc->multi && !mc->present.p && !L_vcnt && mc->vmin <= mc->vmax && (uint64_t)mc->vmax - (uint64_t)mc->vmin < (1ull << 32) &&
         (hk_launch == 0 || (hk_launch == 1 && P.hv32 && !P.hv_f64)) && !dyn_claim_on()) {
-        if (const uint32_t* d = ensure_d32(p->ctx, mc, s, p->stream)) {
-            P.mv32 = d;
+        // values spanning < 2^16 (a latency in ms, a status code): the 16-bit deltas, 2 B per doc (instantiated with
+        // 16-bit ordinals; those kernels load raw words and unpack them when the docs are processed: dense timestamps
+        // only).  Only the copy the kernel reads is built -- no 32-bit copy beside the 16-bit one (HBM per segment)
+        const bool span16 = P.ord16 && d16_on() && (uint64_t)mc->vmax - (uint64_t)mc->vmin < (1ull << 16) &&
+                            !(hk_launch == 1 && P.hv_present);
+        const uint16_t* d16 = span16 ? ensure_d16(p->ctx, mc, s, p->stream) : nullptr;
+        const uint32_t* d32 = d16 ? nullptr : ensure_d32(p->ctx, mc, s, p->stream);
+        if (d16 || d32) {
+            P.mv32 = d32;
+            P.mv16 = d16;
             P.mv_base = mc->vmin;
             P.hot_t = sampled_hot_ord(p->ctx, oc, s);
             pi = true;
-            // values spanning < 2^16 (a latency in ms, a status code): the 16-bit deltas, 2 B per doc (instantiated with
-            // 16-bit ordinals)
-            // (those kernels load raw words and unpack them when the docs are processed: dense timestamps only)
-            if (P.ord16 && d16_on() && (uint64_t)mc->vmax - (uint64_t)mc->vmin < (1ull << 16) && !(hk_launch == 1 && P.hv_present))
-                P.mv16 = ensure_d16(p->ctx, mc, s, p->stream);
             // a filtered request (clauses or live docs) takes the packed cells through one folded accept bitset, which
             // is instantiated with the 16-bit columns only (with_vk)
             if ((P.npred > 0 || P.accept) && !(P.ord16 && P.mv16)) {
@@ -2925,8 +2935,17 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         (uint64_t)mc->vmax - (uint64_t)mc->vmin < (1ull << 32) && !P.mv_f64 && !inner_missing &&
         ((!L_ORD && hk_launch == 1 && P.hv32 && !P.hv_f64) ||
          (L_ORD && L_met == 3 && !P.ord_src && P.ord16 && (hk_launch == 0 || (hk_launch == 1 && P.hv32 && !P.hv_f64))))) {
-        if (const uint32_t* d = ensure_d32(p->ctx, mc, s, p->stream)) {
-            P.mv32 = d;
+        // histogram-only grids over a dense metric spanning < 2^16 with |values| < 2^26 (v * v exact, as the reference's
+        // rounded products then are), read without a filter by the raw-load kernels: the 16-bit deltas and integer run
+        // accumulators (VK bit 2048), 6 B per doc -- and no 32-bit copy
+        const bool int_runs = !L_ORD && int_runs_on() && d16_on() && raw_hist_on() && !P.accept && P.npred == 0 &&
+                              !mc->present.p && !P.hv_present && (uint64_t)mc->vmax - (uint64_t)mc->vmin < (1ull << 16) &&
+                              mc->vmin > -(1ll << 26) && mc->vmax < (1ll << 26);
+        const uint16_t* d16 = int_runs ? ensure_d16(p->ctx, mc, s, p->stream) : nullptr;
+        const uint32_t* d32 = d16 ? nullptr : ensure_d32(p->ctx, mc, s, p->stream);
+        if (d16 || d32) {
+            P.mv32 = d32;
+            P.mv16 = d16;
             P.mv_base = mc->vmin;
             P.pk_shift = 0;
             m32 = true;
@@ -3031,9 +3050,15 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     P.raw_dense = raw_hist_on() && !pi && !P.accept && P.npred == 0 &&
                   ((!L_ORD && raw_hist && (L_met == 0 || (m32 && !P.mv_present))) ||
                    (L_ORD && L_met == 0 && P.ord16 && !P.ord_src && (hk_launch == 0 || raw_hist))) ? 1 : 0;
+    // the integer runs' 16-bit deltas are read only by the raw-load kernels (no 32-bit copy was built for them)
+    require(!(m32 && P.mv16 && !P.raw_dense), ESGPU_ERR_DEVICE, "internal: 16-bit metric deltas outside the raw-load kernels");
+    // integer runs over time-sorted data (90 % of the blocks span less than one interval): one run per thread; roughly
+    // time-ordered data alternates between neighbouring keys and keeps three
+    P.runs1 = m32 && P.mv16 && hc && pl.interval > 0 && hc->zspan < pl.interval && runs1_on() ? 1 : 0;
     const int vk = (P.hv_f64 ? 1 : 0) | (P.mv_f64 ? 2 : 0) | (P.ord_src ? 8 : 0) | (P.ord16 ? 16 : 0) | (P.hv32 ? 32 : 0) |
-                   (pi ? 64 : 0) | (m32 ? 128 : 0) | (P.mv16 ? 256 : 0) | (fold ? 512 : 0) | (P.raw_dense ? 1024 : 0);
-    const uint64_t occ_key = ((uint64_t)lds << 21) | ((uint64_t)wide << 20) | ((uint64_t)vk << 8) | ((uint64_t)L_met << 4) |
+                   (pi ? 64 : 0) | (m32 ? 128 : 0) | (P.mv16 ? 256 : 0) | (fold ? 512 : 0) | (P.raw_dense ? 1024 : 0) |
+                   (P.runs1 ? 4096 : 0);
+    const uint64_t occ_key = ((uint64_t)lds << 24) | ((uint64_t)wide << 23) | ((uint64_t)vk << 8) | ((uint64_t)L_met << 4) |
                              ((uint64_t)hk << 1) | (L_ORD ? 1 : 0);
     if (pl.occ_key != occ_key) {
         pl.occ = std::max(1, collect_occupancy(L_ORD, hk, L_met, lds, vk, wide));
@@ -3113,6 +3138,16 @@ static bool d16_on() {
 // the compacted replay (ESGPU_REPLAY_COMPACT=0: one pass over the segments per batch of winners, for A/B runs)
 static bool replay_compaction() {
     static const bool on = [] { const char* e = std::getenv("ESGPU_REPLAY_COMPACT"); return !(e && *e == '0'); }();
+    return on;
+}
+// integer run accumulators of histogram-only grids (VK bit 2048; ESGPU_INT_RUNS=0: the f64 runs, for A/B runs)
+static bool int_runs_on() {
+    static const bool on = [] { const char* e = std::getenv("ESGPU_INT_RUNS"); return !(e && *e == '0'); }();
+    return on;
+}
+// one integer run per thread over time-sorted data (VK bit 4096; ESGPU_RUNS1=0: three, for A/B runs)
+static bool runs1_on() {
+    static const bool on = [] { const char* e = std::getenv("ESGPU_RUNS1"); return !(e && *e == '0'); }();
     return on;
 }
 // ESGPU_DD=1: every metric grid takes the compensated flushes, exact data or not (tests of those paths on integer data)
@@ -5145,6 +5180,7 @@ extern "C" int esgpu_plan_destroy(esgpu_plan* p) {
         }
         p->pipes.clear();
         if (p->ev_mid) (void)hipEventDestroy(p->ev_mid);
+        if (p->ev_xr) (void)hipEventDestroy(p->ev_xr);
         if (p->ev0) (void)hipEventDestroy(p->ev0);
         if (p->ev1) (void)hipEventDestroy(p->ev1);
         if (p->stream) (void)hipStreamDestroy(p->stream);
@@ -5168,8 +5204,9 @@ extern "C" int esgpu_result_free(esgpu_result* r) {
 // InternalHistogram / stats reduce) and expanded once.  Shape: a top-level terms aggregation (a count-ordered or term-
 // ordered host selection) whose only child is a histogram / date_histogram over an affine rounding with
 // min_doc_count >= 1 and numeric metric children.  Anything else builds every shard and reduces (esgpu_reduce).
-static bool colo_eligible(esgpu_plan* const* plans, int n, bool shape_only = false) {
-    if (n < 2 || n > kColoMaxShards) return false;
+static bool colo_eligible(esgpu_plan* const* plans, int n, bool shape_only = false, bool cross = false) {
+    // (across ranks a rank may hold one shard of the request)
+    if (n < (cross ? 1 : 2) || n > kColoMaxShards) return false;
     const esgpu_plan* p0 = plans[0];
     for (int i = 0; i < n; ++i) {
         const esgpu_plan* p = plans[i];
@@ -5317,6 +5354,189 @@ extern "C" int esgpu_plans_colocated(esgpu_plan* const* plans, int32_t n, int32_
     });
 }
 
+// ---- co-located reduce building blocks (esgpu_plans_build_reduce, esgpu_comm_build_reduce) --------------------
+// every plan's outer doc counts as a ColoTotals descriptor, in p0's pinned h_colo_meta, after each plan's collects (a
+// query of its stream, then one wait), and whether the terms selection can run on the device (colo_select_kernel:
+// value counts <= kColoSelMax, a count or term order, doc counts below 2^31)
+struct ColoSelection {
+    std::vector<ColoTotals> d;
+    ColoSelect S{};
+    uint32_t Tmax = 0;
+    bool dev = false;
+};
+static ColoSelection colo_selection(esgpu_plan* const* plans, int n) {
+    ColoSelection r;
+    esgpu_plan* p0 = plans[0];
+    r.d.resize(n);
+    static const bool dev_sel_on = [] { const char* e = std::getenv("ESGPU_COLO_DEVSEL"); return !(e && *e == '0'); }();
+    r.dev = dev_sel_on;
+    for (int i = 0; i < n; ++i) {
+        esgpu_plan* p = plans[i];
+        const Pipeline& P0 = p->pipes[p->groups[0].pipes[0]];
+        // this plan's collects (an event wait measured slower; a query is cheaper than a wait on an idle stream)
+        if (p != p0 && hipStreamQuery(p->stream) != hipSuccess) HIPX(hipStreamSynchronize(p->stream));
+        ColoTotals& c = r.d[i];
+        const bool oc = P0.ocnt_mode == OCNT_TERMS || P0.ocnt_mode == OCNT_TERMS_DERIVED;
+        c.cnt = oc ? (const void*)P0.g_ocnt.p : (const void*)P0.g_cnt.p;
+        c.H = oc ? 1u : P0.H;
+        c.T = P0.T;
+        c.cnt32 = !oc && P0.cnt32 ? 1u : 0u;
+        c.vc = (uint32_t)P0.value_count;
+        r.Tmax = std::max(r.Tmax, P0.T);
+        r.dev = r.dev && P0.value_count <= kColoSelMax && p->docs_seen < (1ull << 31);
+    }
+    const SpecNode& tn0 = p0->specs[p0->groups[0].root];
+    r.dev = r.dev && tn0.s.order >= ESGPU_ORDER_COUNT_DESC && tn0.s.order <= ESGPU_ORDER_TERM_DESC;
+    r.S.order = tn0.s.order;
+    r.S.K = (uint32_t)std::min<int64_t>(std::max<int64_t>(tn0.s.shard_size, 0), kColoSelMax);
+    r.S.min_doc_count = tn0.s.min_doc_count;
+    r.S.shard_min_doc_count = tn0.s.shard_min_doc_count;
+    r.S.shard_size = tn0.s.shard_size;
+    std::memcpy(p0->h_colo_meta.ensure(sizeof(ColoTotals) * n), r.d.data(), sizeof(ColoTotals) * n);
+    return r;
+}
+
+// a shard's terms skeleton from its device selection record o = {picks, other-doc count, count << 32 | ordinal ...}:
+// build_terms_root's buckets and counts with empty sub-aggregations, terms resolved through plan tp's dictionary
+static Block colo_skeleton(esgpu_plan* tp, const unsigned long long* o, std::vector<uint32_t>* ords) {
+    const Group& g = tp->groups[0];
+    const Pipeline& P0 = tp->pipes[g.pipes[0]];
+    Block r = terms_shell(tp, g.root, {});
+    begin_instance(r, (int64_t)o[1]);
+    for (uint64_t j = 0; j < o[0]; ++j) {
+        const uint32_t ord = (uint32_t)o[2 + j];
+        const std::string term = plan_term(tp, P0, ord);
+        push_bucket(r, ord, &term, (int64_t)(o[2 + j] >> 32));
+        if (ords) ords->push_back(ord);
+    }
+    end_instance(r);
+    return r;
+}
+
+// the device descriptor of a plan's histogram child grid and its metric leaves (colo_merge_kernel / colo_pack_kernel)
+static ColoShard colo_shard_desc(const esgpu_plan* p, int nl) {
+    const ChildSrc& kid = p->groups[0].kids[0];
+    const Pipeline& B0 = p->pipes[kid.pipes[0]];
+    ColoShard c{};
+    c.cnt = B0.g_cnt.as<unsigned long long>();
+    c.cnt32 = B0.cnt32 ? 1 : 0;
+    c.H = B0.H;
+    c.T = B0.T;
+    c.key0 = B0.key0;
+    for (int l = 0; l < nl; ++l) {
+        const Pipeline& L = p->pipes[kid.grand[l].pipe];
+        const int32_t type = p->specs[L.metrics[kid.grand[l].leaf]].s.type;
+        const unsigned long long* lc = (L.vcnt_mode ? L.g_vcnt : L.g_cnt).as<unsigned long long>();
+        c.lcnt[l] = lc == c.cnt && !c.cnt32 ? nullptr : lc;
+        c.lsum[l] = L.g_sum.as<double>();
+        c.lmn[l] = L.met >= 2 && type != ESGPU_AGG_AVG ? L.g_min.as<unsigned long long>() : nullptr;
+        c.lmx[l] = c.lmn[l] ? L.g_max.as<unsigned long long>() : nullptr;
+        c.lsq[l] = L.met >= 3 && type == ESGPU_AGG_EXTENDED_STATS ? L.g_sq.as<double>() : nullptr;
+    }
+    return c;
+}
+
+// the terms block's histogram child, rebuilt from the merged rows [R][Hm] at hbase (count; per leaf value count, sum,
+// min, max, sum of squares): keys with at least min_doc_count docs, and for min_doc_count 0 the empty buckets of
+// addEmptyBuckets (InternalHistogram.java:395-449) -- every grid key between a row's first and last non-empty key, and the
+// extended bounds' keys outside them
+static void colo_rebuild(Block& tb, const Block& proto, int64_t iv, int64_t off, int64_t kmin, uint64_t Hm, int nl,
+                         const char* hbase) {
+    const uint64_t R = tb.nbuckets();
+    const size_t cells = (size_t)R * Hm;
+    Block hist = proto.like();
+    const int64_t mdc = proto.min_doc_count;
+    const bool fill = mdc == 0 && proto.has_empty_info, desc = proto.order == ESGPU_ORDER_KEY_DESC;
+    const unsigned long long* oc = (const unsigned long long*)hbase;
+    const unsigned long long* olc = (const unsigned long long*)(hbase + cells * 8);
+    const double* osum = (const double*)(hbase + cells * 8 * (1 + (size_t)nl));
+    const double* omin = (const double*)(hbase + cells * 8 * (1 + 2 * (size_t)nl));
+    const double* omax = (const double*)(hbase + cells * 8 * (1 + 3 * (size_t)nl));
+    const double* osq = (const double*)(hbase + cells * 8 * (1 + 4 * (size_t)nl));
+    struct Out { int64_t key; int64_t at; };  // at < 0: an empty bucket
+    std::vector<Out> list;
+    {
+        const size_t guess = (size_t)R * Hm;
+        hist.key.reserve(guess);
+        hist.term_off.reserve(guess + 1);
+        hist.bcount.reserve(guess);
+        hist.berr.reserve(guess);
+        for (int l = 0; l < nl; ++l) {
+            Block& gb = hist.subs[l];
+            gb.count.reserve(guess);
+            for (auto* v : {&gb.sum, &gb.min, &gb.max, &gb.sumsq}) v->reserve(guess);
+        }
+    }
+    for (uint64_t b = 0; b < R; ++b) {
+        list.clear();
+        int64_t first = -1, last = -1;
+        for (uint64_t m = 0; m < Hm; ++m)
+            if (oc[(size_t)b * Hm + m]) { if (first < 0) first = (int64_t)m; last = (int64_t)m; }
+        auto key_of = [&](int64_t m) { return (kmin + m) * iv + off; };
+        if (!fill) {
+            for (int64_t m = first; first >= 0 && m <= last; ++m) {
+                const size_t at = (size_t)b * Hm + (size_t)m;
+                if (oc[at] && (int64_t)oc[at] >= mdc) list.push_back({key_of(m), (int64_t)at});
+            }
+        } else if (first < 0) {
+            if (proto.has_bmin && proto.has_bmax)
+                for (int64_t k = proto.bmin; k <= proto.bmax; k += iv) list.push_back({k, -1});
+        } else {
+            if (proto.has_bmin)
+                for (int64_t k = proto.bmin; k < key_of(first); k += iv) list.push_back({k, -1});
+            for (int64_t m = first; m <= last; ++m) {
+                const size_t at = (size_t)b * Hm + (size_t)m;
+                list.push_back({key_of(m), oc[at] ? (int64_t)at : -1});
+            }
+            if (proto.has_bmax && proto.bmax > key_of(last))
+                for (int64_t k = key_of(last) + iv; k <= proto.bmax; k += iv) list.push_back({k, -1});
+        }
+        if (desc) std::reverse(list.begin(), list.end());
+        begin_instance(hist, 0);
+        // the instance's buckets written by index (no per-bucket push_back); an empty bucket's leaves are the
+        // prototypes' empty instances (addEmptyBuckets' emptyBucketInfo.subAggregations)
+        const size_t L = list.size(), k0 = hist.key.size();
+        hist.key.resize(k0 + L);
+        hist.term_off.resize(k0 + 1 + L, hist.term_pool.size());
+        hist.bcount.resize(k0 + L);
+        hist.berr.resize(k0 + L, 0);
+        for (size_t q = 0; q < L; ++q) {
+            hist.key[k0 + q] = list[q].key;
+            hist.bcount[k0 + q] = list[q].at < 0 ? 0 : (int64_t)oc[list[q].at];
+        }
+        for (int l = 0; l < nl; ++l) {
+            Block& gb = hist.subs[l];
+            const Block& eb = hist.empty_subs.empty() ? gb : hist.empty_subs[l];
+            const size_t m0 = gb.count.size();
+            gb.n += L;
+            gb.count.resize(m0 + L);
+            gb.sum.resize(m0 + L);
+            gb.min.resize(m0 + L);
+            gb.max.resize(m0 + L);
+            gb.sumsq.resize(m0 + L);
+            const size_t lo = (size_t)l * cells;
+            for (size_t q = 0; q < L; ++q) {
+                const int64_t at = list[q].at;
+                if (at < 0) {
+                    gb.count[m0 + q] = eb.count[0];
+                    gb.sum[m0 + q] = eb.sum[0];
+                    gb.min[m0 + q] = eb.min[0];
+                    gb.max[m0 + q] = eb.max[0];
+                    gb.sumsq[m0 + q] = eb.sumsq[0];
+                    continue;
+                }
+                gb.count[m0 + q] = (int64_t)olc[lo + at];
+                gb.sum[m0 + q] = osum[lo + at];
+                gb.min[m0 + q] = omin[lo + at];
+                gb.max[m0 + q] = omax[lo + at];
+                gb.sumsq[m0 + q] = osq[lo + at];
+            }
+        }
+        end_instance(hist);
+    }
+    tb.subs.push_back(std::move(hist));
+}
+
 extern "C" int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esgpu_result** out) {
     tune_host_heap();
     return guarded([&] {
@@ -5351,35 +5571,11 @@ extern "C" int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esg
             esgpu_plan* p0 = plans[0];
             hipStream_t st = p0->stream;
             HIPX(hipSetDevice(p0->ctx->device));
-            std::vector<ColoTotals> d(n);
-            uint32_t Tmax = 0;
-            static const bool dev_sel_on = [] { const char* e = std::getenv("ESGPU_COLO_DEVSEL"); return !(e && *e == '0'); }();
-            bool dev_select = dev_sel_on;
-            for (int i = 0; i < n; ++i) {
-                esgpu_plan* p = plans[i];
-                const Pipeline& P0 = p->pipes[p->groups[0].pipes[0]];
-                // this plan's collects (an event wait measured slower; a query is cheaper than a wait on an idle stream)
-                if (p != p0 && hipStreamQuery(p->stream) != hipSuccess) HIPX(hipStreamSynchronize(p->stream));
-                ColoTotals& c = d[i];
-                const bool oc = P0.ocnt_mode == OCNT_TERMS || P0.ocnt_mode == OCNT_TERMS_DERIVED;
-                c.cnt = oc ? (const void*)P0.g_ocnt.p : (const void*)P0.g_cnt.p;
-                c.H = oc ? 1u : P0.H;
-                c.T = P0.T;
-                c.cnt32 = !oc && P0.cnt32 ? 1u : 0u;
-                c.vc = (uint32_t)P0.value_count;
-                Tmax = std::max(Tmax, P0.T);
-                dev_select = dev_select && P0.value_count <= kColoSelMax && p->docs_seen < (1ull << 31);
-            }
-            const SpecNode& tn0 = p0->specs[p0->groups[0].root];
-            dev_select = dev_select && tn0.s.order >= ESGPU_ORDER_COUNT_DESC && tn0.s.order <= ESGPU_ORDER_TERM_DESC;
-            ColoSelect S{};
-            S.order = tn0.s.order;
-            S.K = (uint32_t)std::min<int64_t>(std::max<int64_t>(tn0.s.shard_size, 0), kColoSelMax);
-            S.min_doc_count = tn0.s.min_doc_count;
-            S.shard_min_doc_count = tn0.s.shard_min_doc_count;
-            S.shard_size = tn0.s.shard_size;
+            ColoSelection sel = colo_selection(plans, n);
+            const bool dev_select = sel.dev;
+            const ColoSelect& S = sel.S;
+            const uint32_t Tmax = sel.Tmax;
             PinnedBuf& mb = p0->h_colo_meta;
-            std::memcpy(mb.ensure(sizeof(ColoTotals) * n), d.data(), sizeof(ColoTotals) * n);
             PinnedBuf& tb = p0->h_colo_tot;
             if (dev_select) tb.ensure((size_t)n * (2 + S.K) * 8);
             else tb.ensure(std::max<size_t>((size_t)n * Tmax * 8, 8));
@@ -5403,38 +5599,28 @@ extern "C" int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esg
             std::vector<std::unique_ptr<ResultHolder>> sk(n);
             auto select = [&](int i) {  // build_terms_root's host selection (select_terms), its winners only
                 esgpu_plan* p = plans[i];
-                const Group& g = p->groups[0];
-                const Pipeline& P0 = p->pipes[g.pipes[0]];
-                const SpecNode& tn = p->specs[g.root];
-                int64_t other = 0;
-                std::vector<TermPick> top;
-                if (trace && i == 0) mark("sel0_start");
-                if (dev_select) {
-                    const unsigned long long* o = tot + (size_t)i * (2 + S.K);
-                    const uint64_t np = o[0];
-                    other = (int64_t)o[1];
-                    top.resize(np);
-                    for (uint64_t j = 0; j < np; ++j) top[j] = {(uint32_t)o[2 + j], (int64_t)(o[2 + j] >> 32)};
-                } else {
-                    top = select_terms(tn.s, tot + (size_t)i * Tmax, (uint32_t)P0.value_count, &other,
-                                       [](uint32_t) { return 0.0; });
-                }
-                if (trace && i == 0) mark("sel0_picks");
-                Block r = terms_shell(p, g.root, {});
-                if (trace && i == 0) mark("sel0_shell");
                 p->sk_ords.clear();
-                begin_instance(r, other);
-                for (const TermPick& tp : top) {
-                    const std::string term = plan_term(p, P0, tp.ord);
-                    push_bucket(r, tp.ord, &term, tp.count);
-                    p->sk_ords.push_back(tp.ord);
-                }
-                end_instance(r);
-                if (trace && i == 0) mark("sel0_terms");
                 sk[i].reset(new ResultHolder());
-                sk[i]->aggs.push_back(std::move(r));
+                if (dev_select) {
+                    sk[i]->aggs.push_back(colo_skeleton(p, tot + (size_t)i * (2 + S.K), &p->sk_ords));
+                } else {
+                    const Group& g = p->groups[0];
+                    const Pipeline& P0 = p->pipes[g.pipes[0]];
+                    const SpecNode& tn = p->specs[g.root];
+                    int64_t other = 0;
+                    const std::vector<TermPick> top = select_terms(tn.s, tot + (size_t)i * Tmax, (uint32_t)P0.value_count,
+                                                                   &other, [](uint32_t) { return 0.0; });
+                    Block r = terms_shell(p, g.root, {});
+                    begin_instance(r, other);
+                    for (const TermPick& tp : top) {
+                        const std::string term = plan_term(p, P0, tp.ord);
+                        push_bucket(r, tp.ord, &term, tp.count);
+                        p->sk_ords.push_back(tp.ord);
+                    }
+                    end_instance(r);
+                    sk[i]->aggs.push_back(std::move(r));
+                }
                 p->posted = true;
-                if (trace && i == 0) mark("sel0_done");
             };
             mark("protos");
             // measured at 8 x 1,000 terms: 0.05 ms on the pool, 0.10 ms one after the other (ESGPU_COLO_POOL=0)
@@ -5506,27 +5692,9 @@ extern "C" int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esg
             std::vector<ColoShard> sh(n);
             int64_t kmin = INT64_MAX, kmax = INT64_MIN;
             for (int i = 0; i < n; ++i) {
-                const esgpu_plan* p = plans[i];
-                const ChildSrc& kid = p->groups[0].kids[0];
-                const Pipeline& B0 = p->pipes[kid.pipes[0]];
-                ColoShard& c = sh[i];
-                c.cnt = B0.g_cnt.as<unsigned long long>();
-                c.cnt32 = B0.cnt32 ? 1 : 0;
-                c.H = B0.H;
-                c.T = B0.T;
-                c.key0 = B0.key0;
-                kmin = std::min<int64_t>(kmin, B0.key0);
-                kmax = std::max<int64_t>(kmax, B0.key0 + (int64_t)B0.H - 1);
-                for (int l = 0; l < nl; ++l) {
-                    const Pipeline& L = p->pipes[kid.grand[l].pipe];
-                    const int32_t type = p->specs[L.metrics[kid.grand[l].leaf]].s.type;
-                    const unsigned long long* lc = (L.vcnt_mode ? L.g_vcnt : L.g_cnt).as<unsigned long long>();
-                    c.lcnt[l] = lc == c.cnt && !c.cnt32 ? nullptr : lc;
-                    c.lsum[l] = L.g_sum.as<double>();
-                    c.lmn[l] = L.met >= 2 && type != ESGPU_AGG_AVG ? L.g_min.as<unsigned long long>() : nullptr;
-                    c.lmx[l] = c.lmn[l] ? L.g_max.as<unsigned long long>() : nullptr;
-                    c.lsq[l] = L.met >= 3 && type == ESGPU_AGG_EXTENDED_STATS ? L.g_sq.as<double>() : nullptr;
-                }
+                sh[i] = colo_shard_desc(plans[i], nl);
+                kmin = std::min<int64_t>(kmin, sh[i].key0);
+                kmax = std::max<int64_t>(kmax, sh[i].key0 + (int64_t)sh[i].H - 1);
             }
             const uint64_t Hm = R ? (uint64_t)(kmax - kmin + 1) : 0;
             require(Hm <= (1ull << 26), ESGPU_ERR_UNSUPPORTED, "co-located reduce over a key range beyond 64M buckets");
@@ -5560,103 +5728,8 @@ extern "C" int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esg
             HIPX(hipGetLastError());
             HIPX(hipStreamSynchronize(st));
             mark("merged");
-            // the terms block's histogram child, rebuilt from the merged rows: keys with at least min_doc_count docs,
-            // and for min_doc_count 0 the empty buckets of addEmptyBuckets (InternalHistogram.java:395-449) -- every
-            // grid key between a row's first and last non-empty key, and the extended bounds' keys outside them
-            const Block& proto = hproto;
-            Block hist = proto.like();
             const Pipeline& B00 = p0->pipes[kid0.pipes[0]];
-            const int64_t iv = B00.interval, off = B00.offset;
-            const int64_t mdc = proto.min_doc_count;
-            const bool fill = mdc == 0 && proto.has_empty_info, desc = proto.order == ESGPU_ORDER_KEY_DESC;
-            const unsigned long long* oc = (const unsigned long long*)hbase;
-            const unsigned long long* olc = (const unsigned long long*)(hbase + cells * 8);
-            const double* osum = (const double*)(hbase + cells * 8 * (1 + (size_t)nl));
-            const double* omin = (const double*)(hbase + cells * 8 * (1 + 2 * (size_t)nl));
-            const double* omax = (const double*)(hbase + cells * 8 * (1 + 3 * (size_t)nl));
-            const double* osq = (const double*)(hbase + cells * 8 * (1 + 4 * (size_t)nl));
-            struct Out { int64_t key; int64_t at; };  // at < 0: an empty bucket
-            std::vector<Out> list;
-            {
-                const size_t guess = (size_t)R * Hm;
-                hist.key.reserve(guess);
-                hist.term_off.reserve(guess + 1);
-                hist.bcount.reserve(guess);
-                hist.berr.reserve(guess);
-                for (int l = 0; l < nl; ++l) {
-                    Block& gb = hist.subs[l];
-                    gb.count.reserve(guess);
-                    for (auto* v : {&gb.sum, &gb.min, &gb.max, &gb.sumsq}) v->reserve(guess);
-                }
-            }
-            for (uint64_t b = 0; b < R; ++b) {
-                list.clear();
-                int64_t first = -1, last = -1;
-                for (uint64_t m = 0; m < Hm; ++m)
-                    if (oc[(size_t)b * Hm + m]) { if (first < 0) first = (int64_t)m; last = (int64_t)m; }
-                auto key_of = [&](int64_t m) { return (kmin + m) * iv + off; };
-                if (!fill) {
-                    for (int64_t m = first; first >= 0 && m <= last; ++m) {
-                        const size_t at = (size_t)b * Hm + (size_t)m;
-                        if (oc[at] && (int64_t)oc[at] >= mdc) list.push_back({key_of(m), (int64_t)at});
-                    }
-                } else if (first < 0) {
-                    if (proto.has_bmin && proto.has_bmax)
-                        for (int64_t k = proto.bmin; k <= proto.bmax; k += iv) list.push_back({k, -1});
-                } else {
-                    if (proto.has_bmin)
-                        for (int64_t k = proto.bmin; k < key_of(first); k += iv) list.push_back({k, -1});
-                    for (int64_t m = first; m <= last; ++m) {
-                        const size_t at = (size_t)b * Hm + (size_t)m;
-                        list.push_back({key_of(m), oc[at] ? (int64_t)at : -1});
-                    }
-                    if (proto.has_bmax && proto.bmax > key_of(last))
-                        for (int64_t k = key_of(last) + iv; k <= proto.bmax; k += iv) list.push_back({k, -1});
-                }
-                if (desc) std::reverse(list.begin(), list.end());
-                begin_instance(hist, 0);
-                // the instance's buckets written by index (no per-bucket push_back); an empty bucket's leaves are the
-                // prototypes' empty instances (addEmptyBuckets' emptyBucketInfo.subAggregations)
-                const size_t L = list.size(), k0 = hist.key.size();
-                hist.key.resize(k0 + L);
-                hist.term_off.resize(k0 + 1 + L, hist.term_pool.size());
-                hist.bcount.resize(k0 + L);
-                hist.berr.resize(k0 + L, 0);
-                for (size_t q = 0; q < L; ++q) {
-                    hist.key[k0 + q] = list[q].key;
-                    hist.bcount[k0 + q] = list[q].at < 0 ? 0 : (int64_t)oc[list[q].at];
-                }
-                for (int l = 0; l < nl; ++l) {
-                    Block& gb = hist.subs[l];
-                    const Block& eb = hist.empty_subs.empty() ? gb : hist.empty_subs[l];
-                    const size_t m0 = gb.count.size();
-                    gb.n += L;
-                    gb.count.resize(m0 + L);
-                    gb.sum.resize(m0 + L);
-                    gb.min.resize(m0 + L);
-                    gb.max.resize(m0 + L);
-                    gb.sumsq.resize(m0 + L);
-                    const size_t lo = (size_t)l * cells;
-                    for (size_t q = 0; q < L; ++q) {
-                        const int64_t at = list[q].at;
-                        if (at < 0) {
-                            gb.count[m0 + q] = eb.count[0];
-                            gb.sum[m0 + q] = eb.sum[0];
-                            gb.min[m0 + q] = eb.min[0];
-                            gb.max[m0 + q] = eb.max[0];
-                            gb.sumsq[m0 + q] = eb.sumsq[0];
-                            continue;
-                        }
-                        gb.count[m0 + q] = (int64_t)olc[lo + at];
-                        gb.sum[m0 + q] = osum[lo + at];
-                        gb.min[m0 + q] = omin[lo + at];
-                        gb.max[m0 + q] = omax[lo + at];
-                        gb.sumsq[m0 + q] = osq[lo + at];
-                    }
-                }
-                end_instance(hist);
-            }
-            tb.subs.push_back(std::move(hist));
+            colo_rebuild(tb, hproto, B00.interval, B00.offset, kmin, Hm, nl, hbase);
             // a large merge buffer is not kept with the plan (pinned memory outside the context's budget)
             if (hb.bytes > kColoKeepBytes) hb.release();
             mark("rebuilt");
@@ -5672,6 +5745,254 @@ extern "C" int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esg
             }
             std::fprintf(stderr, "%s\n", line.c_str());
         }
+        *out = &res.release()->pub;
+    });
+}
+
+// ---- the co-located reduce across ranks -----------------------------------------------------------------------
+// esgpu_comm_build_reduce: the co-located reduce (above) with the shards spread over the ranks of a communicator
+// (the coordinating reduce SearchPhaseController.java:401-411 over InternalTerms.doReduce,
+// InternalTerms.java:165-246, and InternalHistogram.doReduce, InternalHistogram.java:338-476).  Per request:
+//   1. every rank selects its shards' top shard_size terms on its device (colo_totals + colo_select), and the ranks
+//      all-gather a small header (shape, dictionary identity, each shard's key range) and then the selection records
+//      {picks, other-doc count, count << 32 | ordinal ...} straight from device memory;
+//   2. every rank runs InternalTerms.doReduce over the skeletons of all shards (the same answer everywhere): the final
+//      terms, their counts, errors and other-doc count;
+//   3. every rank packs its shards' rows of the final terms on its device (colo_pack_kernel: [F][Hmax][R] words per
+//      shard) and the ranks all-gather them device to device;
+//   4. the root merges every shard's rows in global shard order (colo_merge_kernel, the rows read as grids with T = R)
+//      and rebuilds the histogram child on the host, as the single-device co-located reduce does.
+// Shapes the co-located reduce does not take (or dictionaries that differ between ranks) build every local shard and
+// reduce through reduce_across (esgpu_comm_reduce) -- on every rank.
+constexpr int kXrHeader = 8 + 2 * kColoMaxShards;  // header words per rank
+
+extern "C" int esgpu_comm_build_reduce(esgpu_comm* cm, esgpu_plan* const* plans, int32_t n, int32_t root,
+                                       esgpu_result** out) {
+    tune_host_heap();
+    return guarded([&] {
+        require(cm && plans && out && n >= 1 && n <= kColoMaxShards, ESGPU_ERR_INVALID, "build_reduce needs 1..64 local plans");
+        for (int i = 0; i < n; ++i) require(plans[i] != nullptr, ESGPU_ERR_INVALID, "null plan");
+        Collective& C = comm_collective(cm);
+        const double t_start = now_ms();
+        C.allreduce_bytes = C.allgather_bytes = 0;
+        C.collectives = 0;
+        C.exchange_ms = 0;
+        const int W = C.nranks, S = W * n;
+        esgpu_plan* p0 = plans[0];
+        hipStream_t st = p0->stream;
+        HIPX(hipSetDevice(p0->ctx->device));
+        // ---- this rank's part of the header ----
+        std::vector<uint64_t> hdr(kXrHeader, 0), all((size_t)kXrHeader * W, 0);
+        bool ok = S <= kColoMaxShards && colo_eligible(plans, n, false, true) && !p0->groups[0].kids.empty();
+        for (int i = 0; ok && i < n; ++i) {
+            ok = !plans[i]->hc_check;
+            for (const Pipeline& pl : plans[i]->pipes) ok = ok && pl.kind != 1;
+        }
+        ColoSelection sel;
+        double t_host = t_start;  // the device path's host time is counted once this rank's collects have finished
+        if (ok) {
+            sel = colo_selection(plans, n);  // waits for the other local plans' collects
+            HIPX(hipStreamSynchronize(st));  // ... and p0's
+            t_host = now_ms();
+            ok = sel.dev;
+        }
+        int nl = 0;
+        if (ok) {
+            const Pipeline& A = p0->pipes[p0->groups[0].pipes[0]];
+            ok = A.tdict != nullptr;
+            for (int i = 1; ok && i < n; ++i) ok = same_dict(A.tdict, plans[i]->pipes[plans[i]->groups[0].pipes[0]].tdict);
+            if (ok) {
+                nl = (int)p0->groups[0].kids[0].grand.size();
+                hdr[2] = A.tdict->identity;
+                hdr[3] = A.tdict->n;
+                hdr[4] = sel.S.K;
+                hdr[5] = (uint64_t)nl;
+                hdr[6] = sel.Tmax;
+                for (int i = 0; i < n; ++i) {
+                    const Pipeline& B0 = plans[i]->pipes[plans[i]->groups[0].kids[0].pipes[0]];
+                    hdr[8 + 2 * i] = (uint64_t)B0.key0;
+                    hdr[9 + 2 * i] = B0.H;
+                }
+            }
+        }
+        hdr[0] = ok ? 1 : 0;
+        hdr[1] = (uint64_t)n;
+        C.allgather(hdr.data(), all.data(), hdr.size() * 8);
+        // ---- one decision on every rank: the device path, or builds + reduce_across ----
+        bool dev = true;
+        for (int r = 0; r < W && dev; ++r) {
+            const uint64_t* h = all.data() + (size_t)r * kXrHeader;
+            dev = h[0] == 1 && h[1] == (uint64_t)n && h[2] == all[2] && h[3] == all[3] && h[4] == all[4] && h[5] == all[5];
+        }
+        int64_t kmin = INT64_MAX, kmax = INT64_MIN;
+        uint32_t Hmax = 1;
+        std::vector<int64_t> skey0(S);
+        std::vector<uint32_t> sH(S);
+        if (dev) {
+            for (int s = 0; s < S; ++s) {
+                const uint64_t* h = all.data() + (size_t)(s / n) * kXrHeader + 8 + 2 * (s % n);
+                skey0[s] = (int64_t)h[0];
+                sH[s] = (uint32_t)h[1];
+                kmin = std::min<int64_t>(kmin, skey0[s]);
+                kmax = std::max<int64_t>(kmax, skey0[s] + (int64_t)sH[s] - 1);
+                Hmax = std::max(Hmax, sH[s]);
+            }
+            const SpecNode& tn = p0->specs[p0->groups[0].root];
+            const double Rb = (double)std::max<int64_t>(std::min<int64_t>(tn.s.size, 65536), 1);
+            dev = kmax >= kmin && kmax - kmin < (1ll << 26) &&
+                  Rb * (double)(kmax - kmin + 1) * 8.0 * (1.0 + 5.0 * nl) <= (double)kColoMergeBytes &&
+                  (double)S * Rb * Hmax * 8.0 * (1.0 + 5.0 * nl) <= (double)kColoMergeBytes;
+        }
+        std::unique_ptr<ResultHolder> res(new ResultHolder());
+        if (!dev) {  // every local shard built, then the reduce across ranks (its collectives on every rank)
+            std::vector<std::unique_ptr<ResultHolder, void (*)(ResultHolder*)>> parts;
+            for (int i = 0; i < n; ++i) {
+                esgpu_result* r = nullptr;
+                const int rc = esgpu_plan_build(plans[i], &r);
+                if (rc != ESGPU_OK) throw EsError(rc, g_err);
+                parts.emplace_back(holder_of(r), +[](ResultHolder* h) { delete h; });
+            }
+            std::vector<const std::vector<Block>*> lists;
+            for (auto& h : parts) lists.push_back(&h->aggs);
+            res->aggs = reduce_across(C, lists);
+            C.last_path = 0;
+            C.last_host_ms = now_ms() - t_start;
+            res->export_view();
+            *out = &res.release()->pub;
+            return;
+        }
+        // ---- 1. the local selections on the device, all-gathered device to device ----
+        const uint32_t K = sel.S.K, rec = 2 + K;
+        unsigned long long* dtot = (unsigned long long*)p0->s_colo_tot.ensure(p0->ctx, std::max<size_t>((size_t)n * sel.Tmax * 8, 8));
+        launch_colo_totals((const ColoTotals*)p0->h_colo_meta.dev(), (uint32_t)n, sel.Tmax, dtot, st);
+        HIPX(hipGetLastError());
+        unsigned long long* dpk = (unsigned long long*)p0->s_xr_picks.ensure(p0->ctx, (size_t)n * rec * 8);
+        launch_colo_select(dtot, (const ColoTotals*)p0->h_colo_meta.dev(), (uint32_t)n, sel.Tmax, sel.S, dpk, st);
+        HIPX(hipGetLastError());
+        unsigned long long* dall = (unsigned long long*)p0->s_xr_allpicks.ensure(p0->ctx, (size_t)S * rec * 8);
+        C.allgather_dev(dpk, dall, (uint64_t)n * rec * 8, st);
+        PinnedBuf& hp = p0->h_xr_picks;
+        hp.ensure((size_t)S * rec * 8);
+        launch_copy_u64(dall, (unsigned long long*)hp.dev(), (size_t)S * rec, st);
+        HIPX(hipGetLastError());
+        HIPX(hipStreamSynchronize(st));
+        // ---- 2. InternalTerms.doReduce over every shard's skeleton ----
+        const unsigned long long* picks = hp.as<unsigned long long>();
+        std::vector<std::vector<uint32_t>> won(S);
+        std::vector<std::unique_ptr<ResultHolder>> sk(S);
+        for (int s = 0; s < S; ++s) {
+            sk[s].reset(new ResultHolder());
+            sk[s]->aggs.push_back(colo_skeleton(p0, picks + (size_t)s * rec, &won[s]));
+            std::sort(won[s].begin(), won[s].end());
+        }
+        std::vector<const std::vector<Block>*> lists;
+        for (auto& h : sk) lists.push_back(&h->aggs);
+        res->aggs = reduce_lists(lists);
+        for (int i = 0; i < n; ++i) plans[i]->posted = true;
+        Block& tb = res->aggs[0];
+        const uint32_t R = (uint32_t)tb.nbuckets();
+        const bool here = root < 0 || root == C.rank;
+        // ---- 3. this rank's rows of the final terms, packed and all-gathered ----
+        const uint32_t F = 1 + 5 * (uint32_t)nl;
+        const size_t HR = (size_t)Hmax * R, blk = (size_t)F * HR;
+        std::vector<ColoShard> loc(n);
+        for (int i = 0; i < n; ++i) loc[i] = colo_shard_desc(plans[i], nl);
+        if (R > 0) {
+            std::vector<int32_t> rows((size_t)R * n, -1);
+            for (uint32_t b = 0; b < R; ++b) {
+                const uint32_t o = (uint32_t)tb.key[b];
+                for (int i = 0; i < n; ++i) {
+                    const std::vector<uint32_t>& w = won[C.rank * n + i];
+                    if (std::binary_search(w.begin(), w.end(), o)) rows[(size_t)b * n + i] = (int32_t)o;
+                }
+            }
+            PinnedBuf& pm = p0->h_xr_meta;
+            char* pmeta = (char*)pm.ensure(sizeof(ColoShard) * n + rows.size() * 4 + 16);
+            std::memcpy(pmeta, loc.data(), sizeof(ColoShard) * n);
+            std::memcpy(pmeta + sizeof(ColoShard) * n, rows.data(), rows.size() * 4);
+            ColoPackParams K2{};
+            K2.shards = (const ColoShard*)pm.dev();
+            K2.rows = (const int32_t*)((const char*)pm.dev() + sizeof(ColoShard) * n);
+            K2.n = (uint32_t)n;
+            K2.R = R;
+            K2.Hmax = Hmax;
+            K2.nleaves = nl;
+            K2.out = (unsigned long long*)p0->s_xr_send.ensure(p0->ctx, (size_t)n * blk * 8);
+            launch_colo_pack(K2, st);
+            HIPX(hipGetLastError());
+            unsigned long long* drecv = (unsigned long long*)p0->s_xr_recv.ensure(p0->ctx, (size_t)S * blk * 8);
+            C.allgather_dev(K2.out, drecv, (uint64_t)n * blk * 8, st);
+        }
+        // ---- 4. the root merges every shard's rows in global shard order ----
+        if (here) {
+            const Block hproto = child_protos(p0, p0->groups[0])[0].like();
+            const uint64_t Hm = (uint64_t)(kmax - kmin + 1);
+            const Pipeline& B00 = p0->pipes[p0->groups[0].kids[0].pipes[0]];
+            PinnedBuf& hb = p0->h_colo;
+            const char* hbase = nullptr;
+            if (R > 0) {
+                const unsigned long long* drecv = (const unsigned long long*)p0->s_xr_recv.buf.p;
+                std::vector<ColoShard> vs(S);
+                for (int s = 0; s < S; ++s) {
+                    ColoShard& c = vs[s];
+                    c = ColoShard{};
+                    const unsigned long long* base = drecv + (size_t)s * blk;
+                    c.cnt = base;
+                    c.cnt32 = 0;
+                    c.H = sH[s];
+                    c.T = R;
+                    c.key0 = skey0[s];
+                    for (int l = 0; l < nl; ++l) {
+                        const unsigned long long* f = base + (size_t)(1 + 5 * l) * HR;
+                        c.lcnt[l] = f;
+                        c.lsum[l] = (const double*)(f + HR);
+                        c.lmn[l] = loc[0].lmn[l] ? f + 2 * HR : nullptr;
+                        c.lmx[l] = loc[0].lmx[l] ? f + 3 * HR : nullptr;
+                        c.lsq[l] = loc[0].lsq[l] ? (const double*)(f + 4 * HR) : nullptr;
+                    }
+                }
+                std::vector<int32_t> vrows((size_t)R * S, -1);
+                for (uint32_t b = 0; b < R; ++b) {
+                    const uint32_t o = (uint32_t)tb.key[b];
+                    for (int s = 0; s < S; ++s)
+                        if (std::binary_search(won[s].begin(), won[s].end(), o)) vrows[(size_t)b * S + s] = (int32_t)b;
+                }
+                const size_t cells = (size_t)R * Hm;
+                PinnedBuf& vm = p0->h_colo_meta;  // (its selection descriptors are consumed)
+                char* vmeta = (char*)vm.ensure(sizeof(ColoShard) * S + vrows.size() * 4 + 16);
+                std::memcpy(vmeta, vs.data(), sizeof(ColoShard) * S);
+                std::memcpy(vmeta + sizeof(ColoShard) * S, vrows.data(), vrows.size() * 4);
+                hbase = (const char*)hb.ensure(std::max<size_t>(cells * 8 * (1 + 5 * (size_t)std::max(nl, 1)), 8));
+                char* dbase = (char*)hb.dev();
+                ColoParams M{};
+                M.shards = (const ColoShard*)vm.dev();
+                M.rows = (const int32_t*)((const char*)vm.dev() + sizeof(ColoShard) * S);
+                M.nsh = (uint32_t)S;
+                M.R = R;
+                M.Hm = (uint32_t)Hm;
+                M.kmin = kmin;
+                M.nleaves = nl;
+                M.o_cnt = (unsigned long long*)dbase;
+                M.o_lcnt = (unsigned long long*)(dbase + cells * 8);
+                M.o_sum = (double*)(dbase + cells * 8 * (1 + (size_t)nl));
+                M.o_min = (double*)(dbase + cells * 8 * (1 + 2 * (size_t)nl));
+                M.o_max = (double*)(dbase + cells * 8 * (1 + 3 * (size_t)nl));
+                M.o_sq = (double*)(dbase + cells * 8 * (1 + 4 * (size_t)nl));
+                launch_colo_merge(M, st);
+                HIPX(hipGetLastError());
+                HIPX(hipStreamSynchronize(st));
+            }
+            colo_rebuild(tb, hproto, B00.interval, B00.offset, kmin, Hm, nl, hbase);
+            if (hb.bytes > kColoKeepBytes) hb.release();
+        }
+        // the other local plans' next collects (on their own streams) must not rewrite their grids before the pack read them
+        if (!p0->ev_xr) HIPX(hipEventCreateWithFlags(&p0->ev_xr, hipEventDisableTiming));
+        HIPX(hipEventRecord(p0->ev_xr, st));
+        for (int i = 1; i < n; ++i) HIPX(hipStreamWaitEvent(plans[i]->stream, p0->ev_xr, 0));
+        if (!here) res->aggs.clear();
+        C.last_path = 1;
+        C.last_host_ms = now_ms() - t_host;
+        res->export_view();
         *out = &res.release()->pub;
     });
 }

@@ -515,6 +515,33 @@ class Communicator:
         self._keep = t  # the callbacks must outlive the communicator
         return self
 
+    @classmethod
+    def local(cls, group, nranks, rank):
+        """An in-process communicator: `nranks` ranks of this process (one thread each, each with its own Engine, on one
+        or several devices) that share the name `group`.  Collectives are barriers among the threads; device operands are
+        copied device to device.  Every rank's thread must make the same calls in the same order."""
+        ptr = ctypes.c_void_p()
+        N.check(N.lib().esgpu_comm_init_local(group.encode(), nranks, rank, ctypes.byref(ptr)))
+        self = cls.__new__(cls)
+        self._ptr = ptr
+        self._keep = None
+        return self
+
+    def build_reduce(self, plans, root=-1):
+        """The device-resident reduce across ranks (esgpu_comm_build_reduce): this rank's collected shard plans (its
+        shards in global order rank-major).  The reduced result is returned on rank `root` (every rank when root < 0;
+        an empty result elsewhere)."""
+        arr = (N._VP * len(plans))(*[p._ptr for p in plans])
+        out = ctypes.POINTER(N.Result)()
+        N.check(N.lib().esgpu_comm_build_reduce(self._ptr, arr, len(plans), root, ctypes.byref(out)))
+        return ShardResult(out)
+
+    def last_build_reduce(self):
+        """(path, host ms) of the last build_reduce: path 1 = device-resident exchange, 0 = builds + reduce."""
+        path, ms = ctypes.c_int32(), ctypes.c_double()
+        N.check(N.lib().esgpu_comm_last_build_reduce(self._ptr, ctypes.byref(path), ctypes.byref(ms)))
+        return path.value, ms.value
+
     def reduce(self, shard_results):
         """InternalAggregations.reduce over every rank's shard results (this rank's in its shard order)."""
         arr = (ctypes.POINTER(N.Result) * len(shard_results))(*[r.ptr for r in shard_results])

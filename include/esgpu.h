@@ -514,6 +514,22 @@ int esgpu_result_deserialize(const uint8_t* buf, size_t len, esgpu_result** out)
  *                         phases (terms-level records first, then only the surviving buckets' sub-aggregations).  The
  *                         result is bit-identical to esgpu_reduce over every shard in shard order.
  *   esgpu_comm_gather_reduce: every aggregation through the all-gather path (one local shard).
+ *   esgpu_comm_build_reduce: the reduce of one request straight from the ranks' collected shard plans (each rank passes
+ *                         its n_local plans, global shard order rank-major), device-resident for the co-located shape
+ *                         (esgpu_plans_colocated: terms{histogram{stats / extended_stats / avg}} in a count or term order,
+ *                         one term dictionary on every rank): each device selects its shards' top shard_size terms, the
+ *                         {count, ordinal} records are all-gathered from device memory, InternalTerms.doReduce
+ *                         (A/bucket/terms/InternalTerms.java:165-246) runs on every rank over the shards' skeletons, and
+ *                         only the surviving terms' histogram rows are all-gathered device to device and merged in global
+ *                         shard order on the device (InternalHistogram.java:338-476 and the metric reduces) -- no shard
+ *                         result is built.  The result is produced on rank `root` (an empty result elsewhere; every rank
+ *                         when root < 0).  Other shapes build every local shard and run esgpu_comm_reduce (the result
+ *                         on every rank).  Either way it equals esgpu_reduce over the shards' builds in shard order.
+ *   esgpu_comm_init_local: an in-process communicator: nranks ranks of this process (one thread each, each with its own
+ *                         context, on one or several devices) that name the same group; collectives are barriers among
+ *                         the threads, device operands copied device to device on each rank's stream.
+ *   esgpu_comm_last_build_reduce: the last build_reduce's path (1: device-resident, 0: builds + reduce) and its host
+ *                         milliseconds once the rank's collects had finished (exchanges and the root's merge included).
  *   esgpu_comm_last_exchange: bytes moved by the last reduce on this communicator.
  *   esgpu_comm_destroy:   an RCCL communicator holds device buffers of its context: destroy it before esgpu_ctx_destroy.
  * ------------------------------------------------------------------------------------------------------- */
@@ -538,6 +554,9 @@ int esgpu_comm_last_exchange(const esgpu_comm* comm, uint64_t* allreduce_bytes, 
                              int32_t* collectives);
 /* wall-clock milliseconds the last reduce spent inside its collectives (staging copies included) */
 int esgpu_comm_last_exchange_ms(const esgpu_comm* comm, double* ms);
+int esgpu_comm_build_reduce(esgpu_comm* comm, esgpu_plan* const* plans, int32_t n_local, int32_t root, esgpu_result** out);
+int esgpu_comm_init_local(const char* group, int32_t nranks, int32_t rank, esgpu_comm** out);
+int esgpu_comm_last_build_reduce(const esgpu_comm* comm, int32_t* path, double* host_ms);
 
 #ifdef __cplusplus
 }

@@ -8,6 +8,8 @@
 #include <stdio.h>
 #include <string.h>
 #include <math.h>
+#include <fenv.h>
+#include <stdlib.h>
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); return 2; } } while (0)
 
@@ -28,6 +30,7 @@ __global__ void probe(const double* __restrict__ v, int n, double* out, double* 
     if (threadIdx.x == 0) { out[0] = s[0]; out[1] = s[1]; }
 }
 
+#pragma STDC FENV_ACCESS ON
 static int run(const char* name, const double* hv, int n, int threads) {
     double *dv, *dout, *dog, *dol, *dg;
     CK(hipMalloc(&dv, n * 8)); CK(hipMalloc(&dout, 16)); CK(hipMalloc(&dog, n * 8)); CK(hipMalloc(&dol, n * 8));
@@ -59,6 +62,38 @@ static int run(const char* name, const double* hv, int n, int threads) {
     }
     printf("%-22s lds=%a lds_rtn=%a glb=%a glb_rtn=%a  rtn-sequence mismatches: lds %d, global %d\n", name, out[0],
            out[1], g[0], g[1], bad_l, bad_g);
+    // rounding mode of the atomic: the successor of each returned old value (the olds sorted by the order the atomic
+    // applied them: for positive addends, ascending) against old + v rounded each way
+    if (strcmp(name, "rounding 4096") == 0) {
+        for (int pass = 0; pass < 2; ++pass) {
+            double* o = pass ? ol : og;
+            const double fin = pass ? out[1] : g[1];
+            int* idx = (int*)malloc(n * sizeof(int));
+            for (int i = 0; i < n; ++i) idx[i] = i;
+            for (int i = 1; i < n; ++i) {  // insertion sort by old value
+                int k = idx[i], j = i - 1;
+                while (j >= 0 && o[idx[j]] > o[k]) { idx[j + 1] = idx[j]; --j; }
+                idx[j + 1] = k;
+            }
+            int rn = 0, rz = 0, ru = 0, other = 0, exact = 0;
+            for (int r = 0; r < n; ++r) {
+                const int i = idx[r];
+                const double next = r + 1 < n ? o[idx[r + 1]] : fin;
+                fesetround(FE_TONEAREST); volatile double a = o[i]; volatile double b = hv[i]; const double sn = a + b;
+                fesetround(FE_TOWARDZERO); const double sz = a + b;
+                fesetround(FE_UPWARD); const double su = a + b;
+                fesetround(FE_TONEAREST);
+                if (sn == sz && sz == su) { ++exact; if (next != sn) ++other; continue; }
+                if (next == sn) ++rn;
+                if (next == sz) ++rz;
+                if (next == su) ++ru;
+                if (next != sn && next != sz && next != su) ++other;
+            }
+            printf("  %s atomic rounding: inexact adds matching RN %d, RZ %d, RU %d; exact adds %d; unexplained %d\n",
+                   pass ? "lds" : "global", rn, rz, ru, exact, other);
+            free(idx);
+        }
+    }
     free(og); free(ol);
     (void)hipFree(dv); (void)hipFree(dout); (void)hipFree(dog); (void)hipFree(dol); (void)hipFree(dg);
     return 0;
