@@ -225,12 +225,15 @@ def main():
     units_per_request = 1 if merged or per_gpu == 1 else per_gpu
     # a terms request's shards on one GPU (one process): built and reduced in one call (esgpu_plans_build_reduce, the
     # same result as reducing every shard build); with several ranks each rank's shards go to the cross-rank reduce
-    colo = units_per_request > 1 and world == 1 and not args.no_colo
+    # with several ranks, a shape the device merge takes goes to the device-resident reduce across ranks
+    # (esgpu_comm_build_reduce: device selections and rows exchanged device to device, the merge on rank 0)
+    colo = (units_per_request > 1 or world > 1) and not merged and not args.no_colo
     if colo:
-        probe_plans = [engine.plan(aggs, filters=filters, number_of_shards=shards) for _ in range(units_per_request)]
+        probe_plans = [engine.plan(aggs, filters=filters, number_of_shards=shards) for _ in range(max(units_per_request, 2))]
         colo = ea.colocated(probe_plans)  # a shape the device merge takes (else the builds run on worker threads)
         for pp in probe_plans:
             pp.close()
+    xr = colo and world > 1
     if colo:
         args.scheme = "sets"  # one plan per shard: a request's plans are all alive at its reduce
     # plan sets: one plan per unit (a shard, or all of a fixed-shape request's shards); `inflight` sets alternate, so
@@ -284,7 +287,7 @@ def main():
 
     def colo_request(plans):
         t = time.perf_counter()
-        out = ea.build_reduce(plans)
+        out = comm.build_reduce(plans, root=0) if xr else ea.build_reduce(plans)
         host_ms["build_reduce"] += (time.perf_counter() - t) * 1e3
         return out
 
@@ -419,6 +422,9 @@ def main():
     if comm:
         ar, ag, ncoll = comm.last_exchange()
         exchange = {"allreduce_bytes": ar, "allgather_bytes": ag, "collectives": ncoll, "ms": comm.last_exchange_ms()}
+        if xr:
+            path, xms = comm.last_build_reduce()
+            exchange.update({"device_resident": path == 1, "build_reduce_host_ms": round(xms, 4)})
 
     # self-check of the last timed request's final result (outside the timed region)
     matching = None
@@ -435,7 +441,9 @@ def main():
             dist.all_reduce(t)
             matching = int(t.item())
     docs_total = args.docs * shards
-    checked, check_errors = self_check(args.workload, final.to_dict(), docs_total, matching)
+    # (the device-resident reduce across ranks leaves the result on rank 0 only: the other ranks check nothing)
+    checked, check_errors = (self_check(args.workload, final.to_dict(), docs_total, matching) if not xr or rank == 0
+                             else (True, []))
 
     ms_per_step = elapsed * 1000.0 / args.steps
     value = docs_total / (elapsed / args.steps)
@@ -485,7 +493,8 @@ def main():
             "config": {"workload": args.workload, "request": desc, "docs_per_shard": args.docs, "shards": shards,
                        "shards_per_gpu": per_gpu, "docs_total": docs_total,
                        "collect": "merged (one plan per GPU)" if merged else
-                                  ("per shard, co-located reduce (esgpu_plans_build_reduce)" if colo else "per shard"),
+                                  ("per shard, device-resident reduce across ranks (esgpu_comm_build_reduce)" if xr else
+                                   "per shard, co-located reduce (esgpu_plans_build_reduce)" if colo else "per shard"),
                        "parallelism": f"{per_gpu} shard(s) per GPU x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,

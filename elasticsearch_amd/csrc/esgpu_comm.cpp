@@ -18,6 +18,7 @@
 
 #include "../../include/esgpu.h"
 #include "esgpu_internal.hpp"
+#include "esgpu_kernels.hpp"
 #include "esgpu_results.hpp"
 
 using namespace esgpu;
@@ -135,7 +136,8 @@ struct LocalGroup {
     int n = 0, arrived = 0;
     uint64_t gen = 0;
     std::vector<const void*> src;
-    std::vector<hipEvent_t> ready, done;
+    std::vector<hipEvent_t> ready;
+    std::vector<int> dev;
     bool broken = false;
     void barrier() {
         std::unique_lock<std::mutex> lk(mu);
@@ -157,11 +159,10 @@ std::map<std::string, std::weak_ptr<LocalGroup>> g_local_groups;
 
 struct LocalCollective : Collective {
     std::shared_ptr<LocalGroup> g;
-    hipEvent_t ready = nullptr, done = nullptr;
+    hipEvent_t ready = nullptr;
     std::vector<uint8_t> tmp;
     ~LocalCollective() override {
         if (ready) (void)hipEventDestroy(ready);
-        if (done) (void)hipEventDestroy(done);
     }
     void allreduce(void* buf, uint64_t count, int dt, int op) override {
         if (!count) return;
@@ -203,24 +204,30 @@ struct LocalCollective : Collective {
     void allgather_dev(const void* d_in, void* d_out, uint64_t bytes, void* stream) override {
         Clock clk(*this);
         hipStream_t st = (hipStream_t)stream;
-        if (!ready) {
-            HIPX(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
-            HIPX(hipEventCreateWithFlags(&done, hipEventDisableTiming));
-        }
+        if (!ready) HIPX(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
         HIPX(hipEventRecord(ready, st));  // this rank's operand is written once its stream reaches here
+        int d = 0;
+        HIPX(hipGetDevice(&d));
         g->src[rank] = d_in;
         g->ready[rank] = ready;
+        g->dev[rank] = d;
         g->barrier();
+        bool one_device = bytes % 8 == 0 && nranks <= esgpu::kColoMaxShards;
         for (int r = 0; r < nranks; ++r) {
+            one_device = one_device && g->dev[r] == d;
             if (r != rank) HIPX(hipStreamWaitEvent(st, g->ready[r], 0));
-            HIPX(hipMemcpyAsync((uint8_t*)d_out + (size_t)r * bytes, g->src[r], bytes, hipMemcpyDeviceToDevice, st));
         }
-        HIPX(hipEventRecord(done, st));
-        g->done[rank] = done;
+        if (one_device) {  // every operand on this device: one gather launch instead of a DMA copy per rank
+            launch_gather_bufs(g->src.data(), nranks, bytes, d_out, st);
+            HIPX(hipGetLastError());
+        } else {
+            for (int r = 0; r < nranks; ++r)
+                HIPX(hipMemcpyAsync((uint8_t*)d_out + (size_t)r * bytes, g->src[r], bytes, hipMemcpyDeviceToDevice, st));
+        }
+        // every rank has finished reading every operand before any rank goes on: a rank may rewrite, reallocate or free
+        // its operand buffer as soon as the call returns (the next request, or the plan's destruction)
+        HIPX(hipStreamSynchronize(st));
         g->barrier();
-        // no rank's later work (the next request rewriting its operand) runs before every rank has copied it
-        for (int r = 0; r < nranks; ++r)
-            if (r != rank) HIPX(hipStreamWaitEvent(st, g->done[r], 0));
         allgather_bytes += bytes * nranks;
         ++collectives;
     }
@@ -288,7 +295,7 @@ extern "C" int esgpu_comm_init_local(const char* group, int32_t nranks, int32_t 
                 g->n = nranks;
                 g->src.assign(nranks, nullptr);
                 g->ready.assign(nranks, nullptr);
-                g->done.assign(nranks, nullptr);
+                g->dev.assign(nranks, 0);
                 w = g;
             }
         }

@@ -1292,6 +1292,31 @@ void launch_colo_pack(const ColoPackParams& p, hipStream_t st) {
     hipLaunchKernelGGL(colo_pack_kernel, dim3((uint32_t)((HR + 255) / 256), p.n), dim3(256), 0, st, p);
 }
 
+struct GatherBufs {
+    const unsigned long long* src[kColoMaxShards];
+    unsigned long long* dst;
+    uint64_t words;  // per rank
+    uint32_t n;
+};
+__global__ __launch_bounds__(256) void gather_bufs_kernel(GatherBufs G) {
+    const uint64_t total = G.words * G.n;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t r = (uint32_t)(i / G.words);
+        G.dst[i] = G.src[r][i - (uint64_t)r * G.words];
+    }
+}
+void launch_gather_bufs(const void* const* srcs, int n, size_t bytes, void* dst, hipStream_t st) {
+    if (n <= 0 || bytes == 0) return;
+    GatherBufs G{};
+    for (int r = 0; r < n && r < kColoMaxShards; ++r) G.src[r] = (const unsigned long long*)srcs[r];
+    G.dst = (unsigned long long*)dst;
+    G.words = bytes / 8;
+    G.n = (uint32_t)std::min(n, kColoMaxShards);
+    const uint64_t total = G.words * G.n;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((total + 255) / 256, 2048);
+    hipLaunchKernelGGL(gather_bufs_kernel, dim3(grid), dim3(256), 0, st, G);
+}
+
 void launch_colo_merge(const ColoParams& p, hipStream_t st) {
     if (p.R == 0 || p.Hm == 0) return;
     hipLaunchKernelGGL(colo_merge_kernel, dim3((p.Hm + 255) / 256, p.R), dim3(256), 0, st, p);

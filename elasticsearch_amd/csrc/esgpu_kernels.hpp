@@ -276,6 +276,9 @@ struct ColoPackParams {
     unsigned long long* out;  // [n][1 + 5 * nleaves][Hmax][R]
 };
 void launch_colo_pack(const ColoPackParams& p, hipStream_t s);
+// the in-process transport's all-gather on one device: rank r's `bytes` (a multiple of 8) from srcs[r] into dst + r * bytes,
+// one launch for every rank (n <= kColoMaxShards)
+void launch_gather_bufs(const void* const* srcs, int n, size_t bytes, void* dst, hipStream_t s);
 // the co-located reduce's selection input: every shard's per-ordinal doc counts, summed over the [H][T] grid rows,
 // written to out[shard][Tmax] (pinned, device-mapped) by one launch over all the shards
 struct ColoTotals {

@@ -5764,6 +5764,77 @@ extern "C" int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esg
 //      and rebuilds the histogram child on the host, as the single-device co-located reduce does.
 // Shapes the co-located reduce does not take (or dictionaries that differ between ranks) build every local shard and
 // reduce through reduce_across (esgpu_comm_reduce) -- on every rank.
+// InternalTerms.doReduce (A/bucket/terms/InternalTerms.java:165-246) over the shards' device selection records, for shards
+// that number their terms through one dictionary (an ordinal names the same term on every shard, and ordinal order is
+// the dictionary's byte order): the buckets, counts, errors and other-doc count reduce_terms computes from the shards'
+// skeletons (esgpu_results.cpp), without building them -- only the surviving terms are resolved to bytes.  won[s]: the
+// ordinals shard s returned, sorted.
+static Block xr_reduce_terms(esgpu_plan* p0, const unsigned long long* recs, int S, uint32_t rec, uint32_t T,
+                             std::vector<std::vector<uint32_t>>& won) {
+    const Group& g = p0->groups[0];
+    const Pipeline& P0 = p0->pipes[g.pipes[0]];
+    Block out = terms_shell(p0, g.root, {});
+    int64_t sumErr = 0, other = 0;
+    std::vector<int64_t> cnt(T, 0), err(T, 0);
+    std::vector<uint8_t> seen(T, 0);
+    std::vector<uint32_t> ords;
+    won.assign(S, {});
+    for (int s = 0; s < S; ++s) {
+        const unsigned long long* o = recs + (size_t)s * rec;
+        const uint64_t np = o[0];
+        other += (int64_t)o[1];
+        int64_t thisErr;  // InternalTerms: the shard's doc count error
+        if ((int64_t)np < out.shard_size || out.order == ESGPU_ORDER_TERM_ASC || out.order == ESGPU_ORDER_TERM_DESC) thisErr = 0;
+        else if (out.order == ESGPU_ORDER_COUNT_DESC) thisErr = (int64_t)(o[2 + np - 1] >> 32);  // its last bucket's count
+        else thisErr = -1;
+        if (sumErr != -1) sumErr = thisErr == -1 ? -1 : sumErr + thisErr;
+        won[s].resize(np);
+        for (uint64_t j = 0; j < np; ++j) {
+            const uint32_t ord = (uint32_t)o[2 + j];
+            require(ord < T, ESGPU_ERR_DEVICE, "internal: selection record ordinal out of range");
+            won[s][j] = ord;
+            if (!seen[ord]) { seen[ord] = 1; ords.push_back(ord); }
+            cnt[ord] += (int64_t)(o[2 + j] >> 32);
+            if (err[ord] != -1) err[ord] = thisErr == -1 ? -1 : err[ord] + thisErr;  // Bucket.reduce
+        }
+        std::sort(won[s].begin(), won[s].end());
+    }
+    const size_t nb = ords.size();
+    std::vector<uint32_t> keep;
+    keep.reserve(nb);
+    for (uint32_t o : ords) {
+        if (err[o] != -1) err[o] = sumErr == -1 ? -1 : sumErr - err[o];
+        if (cnt[o] >= out.min_doc_count) keep.push_back(o);
+    }
+    const size_t size = std::min<size_t>((size_t)std::max(out.required_size, 0), nb);
+    const int32_t order = out.order;
+    auto less = [&](uint32_t a, uint32_t b) {  // cmp_terms with the ordinal as the term
+        switch (order) {
+            case ESGPU_ORDER_COUNT_DESC: return cnt[a] != cnt[b] ? cnt[a] > cnt[b] : a < b;
+            case ESGPU_ORDER_COUNT_ASC: return cnt[a] != cnt[b] ? cnt[a] < cnt[b] : a < b;
+            case ESGPU_ORDER_TERM_DESC: return a > b;
+            default: return a < b;
+        }
+    };
+    if (keep.size() > size) {
+        std::partial_sort(keep.begin(), keep.begin() + size, keep.end(), less);
+        for (size_t i = size; i < keep.size(); ++i) other += cnt[keep[i]];
+        keep.resize(size);
+    } else {
+        std::sort(keep.begin(), keep.end(), less);
+    }
+    ++out.n;
+    out.doc_count_error.push_back(sumErr == -1 ? -1 : (S == 1 ? 0 : sumErr));
+    out.other_doc_count.push_back(other);
+    for (uint32_t o : keep) {
+        const std::string term = plan_term(p0, P0, o);
+        push_bucket(out, o, &term, cnt[o]);
+        out.berr.back() = err[o];
+    }
+    end_instance(out);
+    return out;
+}
+
 constexpr int kXrHeader = 8 + 2 * kColoMaxShards;  // header words per rank
 
 extern "C" int esgpu_comm_build_reduce(esgpu_comm* cm, esgpu_plan* const* plans, int32_t n, int32_t root,
@@ -5817,7 +5888,11 @@ extern "C" int esgpu_comm_build_reduce(esgpu_comm* cm, esgpu_plan* const* plans,
         }
         hdr[0] = ok ? 1 : 0;
         hdr[1] = (uint64_t)n;
+        static const bool trace = std::getenv("ESGPU_TRACE_XR") != nullptr;
+        std::vector<std::pair<const char*, double>> marks{{"host", t_host}};
+        auto mark = [&](const char* w) { if (trace) marks.emplace_back(w, now_ms()); };
         C.allgather(hdr.data(), all.data(), hdr.size() * 8);
+        mark("header");
         // ---- one decision on every rank: the device path, or builds + reduce_across ----
         bool dev = true;
         for (int r = 0; r < W && dev; ++r) {
@@ -5876,22 +5951,16 @@ extern "C" int esgpu_comm_build_reduce(esgpu_comm* cm, esgpu_plan* const* plans,
         launch_copy_u64(dall, (unsigned long long*)hp.dev(), (size_t)S * rec, st);
         HIPX(hipGetLastError());
         HIPX(hipStreamSynchronize(st));
+        mark("records");
         // ---- 2. InternalTerms.doReduce over every shard's skeleton ----
         const unsigned long long* picks = hp.as<unsigned long long>();
-        std::vector<std::vector<uint32_t>> won(S);
-        std::vector<std::unique_ptr<ResultHolder>> sk(S);
-        for (int s = 0; s < S; ++s) {
-            sk[s].reset(new ResultHolder());
-            sk[s]->aggs.push_back(colo_skeleton(p0, picks + (size_t)s * rec, &won[s]));
-            std::sort(won[s].begin(), won[s].end());
-        }
-        std::vector<const std::vector<Block>*> lists;
-        for (auto& h : sk) lists.push_back(&h->aggs);
-        res->aggs = reduce_lists(lists);
+        std::vector<std::vector<uint32_t>> won;
+        res->aggs.push_back(xr_reduce_terms(p0, picks, S, rec, (uint32_t)all[3], won));
         for (int i = 0; i < n; ++i) plans[i]->posted = true;
         Block& tb = res->aggs[0];
         const uint32_t R = (uint32_t)tb.nbuckets();
         const bool here = root < 0 || root == C.rank;
+        mark("skeleton_reduce");
         // ---- 3. this rank's rows of the final terms, packed and all-gathered ----
         const uint32_t F = 1 + 5 * (uint32_t)nl;
         const size_t HR = (size_t)Hmax * R, blk = (size_t)F * HR;
@@ -5923,6 +5992,7 @@ extern "C" int esgpu_comm_build_reduce(esgpu_comm* cm, esgpu_plan* const* plans,
             unsigned long long* drecv = (unsigned long long*)p0->s_xr_recv.ensure(p0->ctx, (size_t)S * blk * 8);
             C.allgather_dev(K2.out, drecv, (uint64_t)n * blk * 8, st);
         }
+        mark("rows");
         // ---- 4. the root merges every shard's rows in global shard order ----
         if (here) {
             const Block hproto = child_protos(p0, p0->groups[0])[0].like();
@@ -5981,8 +6051,10 @@ extern "C" int esgpu_comm_build_reduce(esgpu_comm* cm, esgpu_plan* const* plans,
                 launch_colo_merge(M, st);
                 HIPX(hipGetLastError());
                 HIPX(hipStreamSynchronize(st));
+                mark("merged");
             }
             colo_rebuild(tb, hproto, B00.interval, B00.offset, kmin, Hm, nl, hbase);
+            mark("rebuilt");
             if (hb.bytes > kColoKeepBytes) hb.release();
         }
         // the other local plans' next collects (on their own streams) must not rewrite their grids before the pack read them
@@ -5993,6 +6065,16 @@ extern "C" int esgpu_comm_build_reduce(esgpu_comm* cm, esgpu_plan* const* plans,
         C.last_path = 1;
         C.last_host_ms = now_ms() - t_host;
         res->export_view();
+        mark("exported");
+        if (trace && C.rank == 0) {
+            std::string line = "comm_build_reduce";
+            char buf[64];
+            for (size_t k = 1; k < marks.size(); ++k) {
+                std::snprintf(buf, sizeof buf, " %s +%.3f", marks[k].first, marks[k].second - marks[k - 1].second);
+                line += buf;
+            }
+            std::fprintf(stderr, "%s\n", line.c_str());
+        }
         *out = &res.release()->pub;
     });
 }

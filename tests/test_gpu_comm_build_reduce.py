@@ -42,6 +42,12 @@ SHAPES = {
         AB.dateHistogram("d").field("@timestamp").interval("1d").minDocCount(0).subAggregation(
             AB.extendedStats("x").field("response_time_ms")).subAggregation(AB.avg("a").field("response_time_ms")))],
         NS_FIELDS, None, True),
+    "count_asc_small_shard_size": (lambda: [AB.terms("hosts").field("host").size(5).shardSize(6).order(ea.Order.count(True))
+                                            .minDocCount(2).subAggregation(_hour(AB.avg("rt").field("response_time_ms")))],
+                                   NS_FIELDS, None, True),
+    "count_desc_errors_shown": (lambda: [AB.terms("hosts").field("host").size(3).shardSize(4).showTermDocCountError(True)
+                                         .subAggregation(_hour(AB.stats("rt").field("response_time_ms")))],
+                                NS_FIELDS, None, True),
     "terms_stats_fallback": (lambda: [AB.terms("hosts").field("host").size(5).subAggregation(AB.stats("s").field("response_time_ms"))],
                              NS_FIELDS, None, False),
 }

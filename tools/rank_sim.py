@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--docs", type=int, default=125_000_000)
     ap.add_argument("--reqs", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-align", dest="align", action="store_false",
+                    help="do not wait for every rank's collect before the reduce")
     a = ap.parse_args()
     aggs, fields, filters = request(a.workload)
     W = a.ranks
@@ -62,6 +64,11 @@ def main():
                     wall["t0"] = time.perf_counter()
                 plan.reset()
                 plan.collect(seg)
+                if a.align:
+                    # every rank's collect finished first: on one shared GPU a rank's collect otherwise ends up to
+                    # (ranks - 1) collects later than another's, and the exchange's first barrier would count that wait
+                    plan.last_collect_stats()
+                    ready.wait()
                 res = comm.build_reduce([plan], root=0)
                 path, ms = comm.last_build_reduce()
                 paths.add(path)
@@ -88,7 +95,7 @@ def main():
         sys.exit(1)
     per_rank = [statistics.median(h) for h in host_ms]
     print(json.dumps({
-        "workload": a.workload, "ranks": W, "docs_per_shard": a.docs, "requests": a.reqs, "paths": sorted(paths),
+        "workload": a.workload, "ranks": W, "aligned": a.align, "docs_per_shard": a.docs, "requests": a.reqs, "paths": sorted(paths),
         "host_ms_per_request_median_by_rank": [round(x, 4) for x in per_rank],
         "host_ms_per_request_root": round(per_rank[0], 4),
         "host_ms_per_request_max_rank": round(max(per_rank), 4),
