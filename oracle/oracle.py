@@ -125,15 +125,19 @@ def _columns(columns):
     return arr, len(descs), keep
 
 
+# oracle runs carry the exact-sum shadow unless told otherwise (tests/conftest.py turns it on for the test session)
+EXACT_DEFAULT = False
+
+
 def run(shards, aggs, filters=None, number_of_shards=None, accept=None, ord_lookup=None, return_seconds=False,
-        streams=False, exact=False):
+        streams=False, exact=None):
     """shards: list of (columns_dict, max_doc).  Returns {"shards": [...], "reduced": {...}} (parsed JSON); with
     streams=True also "streams": per shard the bytes of InternalAggregations.writeTo; with exact=True every stats /
     extended_stats / avg result also carries "_exact": its rendered values recomputed from the exact sums that the
     reference's doc-order double additions approximate (tests/helpers.assert_same_exact)."""
     L = lib()
     L.oracle_set_emit_streams(1 if streams else 0)
-    L.oracle_set_exact_shadow(1 if exact else 0)
+    L.oracle_set_exact_shadow(1 if (EXACT_DEFAULT if exact is None else exact) else 0)
     number_of_shards = number_of_shards or len(shards)
     specs, nspecs, k1 = oracle_request.lower(L, aggs, number_of_shards)
     flt, nf, k2 = oracle_request.lower_filters(filters, ord_lookup, aggs)

@@ -11,6 +11,11 @@ sys.path.insert(0, os.path.join(REPO, "oracle"))
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs the gfx950 kernels through the C-ABI)")
+    # every oracle run of the suite carries the exact sums its doc-order additions approximate ("_exact"):
+    # helpers.assert_same compares a floating value with the oracle's or, where the oracle's rounding is the larger
+    # error, with the exact one (SURVEY §7 "Float parity")
+    import oracle
+    oracle.EXACT_DEFAULT = True
 
 
 @pytest.fixture(scope="session")

@@ -94,7 +94,11 @@ def _num_equal(a, b, exact, tol=REL_TOL):
 
 
 def assert_same(got, want, path="", exact_floats=True):
-    """Deep comparison of two parsed result trees with the parity rules above."""
+    """Deep comparison of two parsed result trees with the parity rules above (a metric from an oracle run with
+    exact=True is compared through assert_same_exact)."""
+    if isinstance(want, dict) and "_exact" in want:
+        assert_same_exact(got, want, path, exact_floats)
+        return
     if isinstance(want, dict):
         assert isinstance(got, dict), f"{path}: expected object, got {type(got).__name__}"
         assert set(got) == set(want), f"{path}: keys differ: {sorted(set(got) ^ set(want))}"
@@ -145,7 +149,7 @@ class FloatReport:
                 "max_rel_err_gpu_vs_exact": self.got}
 
 
-def _exact_leaf(got, want, exact, path, key, exact_floats, report):
+def _exact_leaf(got, want, exact, path, key, exact_floats, report, strict):
     derived = any(("." + k) in path for k in DERIVED_KEYS)
     tol = DERIVED_TOL if derived else REL_TOL
     if exact is None or not isinstance(want, float) or not isinstance(got, (int, float)):
@@ -155,24 +159,26 @@ def _exact_leaf(got, want, exact, path, key, exact_floats, report):
     eg, ew = _rel(got, exact), _rel(want, exact)
     if report is not None:
         report.add(key, ew, eg)
+    if _rel(got, want) == 0.0 and not (strict and eg > tol and not derived):
+        return  # the reference's own double, bit for bit
     if exact_floats and ew == 0.0:
         # the reference's sum is exact (integer data below 2^53): the GPU's must be the same double
-        assert _rel(got, want) == 0.0, f"{path}: {got!r} != {want!r} (exact {exact!r})"
-        return
-    # the GPU's compensated sums lie within the bar of the exact value; a derived statistic (its subtraction
-    # cancels) may instead match the oracle's
-    ok = eg <= tol or (derived and _num_equal(got, want, False, tol))
+        assert False, f"{path}: {got!r} != {want!r} (exact {exact!r})"
+    # within the bar of the oracle, or -- where the oracle's doc-order rounding is the larger error -- of the exact
+    # value; strict: always within the bar of the exact value (a derived statistic, whose subtraction cancels, may
+    # instead match the oracle's)
+    ok = eg <= tol or (not strict and _num_equal(got, want, False, tol)) or (derived and _num_equal(got, want, False, tol))
     if not ok and derived and math.isfinite(float(got)) and math.isfinite(float(exact)):
         ok = abs(float(got) - float(exact)) <= tol * max(abs(float(got)), abs(float(exact)), 1.0)
     assert ok, f"{path}: {got!r} vs exact {exact!r} (oracle {want!r}; rel err gpu {eg:.3g}, oracle {ew:.3g})"
 
 
-def assert_same_exact(got, want, path="", exact_floats=True, report=None, _exact=None, _key=""):
+def assert_same_exact(got, want, path="", exact_floats=True, report=None, _exact=None, _key="", strict=False):
     """assert_same against an oracle run with exact=True: a metric's floating values are compared with its "_exact"
     values (the exact sums the reference's doc-order additions approximate, and the statistics derived from them by the
     reference's formulas).  The GPU must be within REL_TOL (DERIVED_TOL for variance / std_deviation / bounds) of the
-    exact value; with exact_floats, a value the oracle computed exactly must be bit-identical.  `report` (FloatReport)
-    collects the oracle's and the GPU's largest errors."""
+    exact value or of the oracle's (strict: of the exact value); with exact_floats, a value the oracle computed exactly
+    must be bit-identical.  `report` (FloatReport) collects the oracle's and the GPU's largest errors."""
     if isinstance(want, dict):
         if "_exact" in want:
             want = dict(want)
@@ -180,22 +186,22 @@ def assert_same_exact(got, want, path="", exact_floats=True, report=None, _exact
             assert isinstance(got, dict), f"{path}: expected object"
             assert set(got) == set(want), f"{path}: keys differ: {sorted(set(got) ^ set(want))}"
             for k in want:
-                assert_same_exact(got[k], want[k], f"{path}.{k}", exact_floats, report, ex.get(k), k)
+                assert_same_exact(got[k], want[k], f"{path}.{k}", exact_floats, report, ex.get(k), k, strict)
             return
         assert isinstance(got, dict), f"{path}: expected object, got {type(got).__name__}"
         assert set(got) == set(want), f"{path}: keys differ: {sorted(set(got) ^ set(want))}"
         for k in want:
             sub = _exact.get(k) if isinstance(_exact, dict) else None
-            assert_same_exact(got[k], want[k], f"{path}.{k}", exact_floats, report, sub, k)
+            assert_same_exact(got[k], want[k], f"{path}.{k}", exact_floats, report, sub, k, strict)
     elif isinstance(want, list):
         assert isinstance(got, list), f"{path}: expected list"
         assert len(got) == len(want), f"{path}: length {len(got)} != {len(want)}"
         for i, (g, w) in enumerate(zip(got, want)):
-            assert_same_exact(g, w, f"{path}[{i}]", exact_floats, report)
+            assert_same_exact(g, w, f"{path}[{i}]", exact_floats, report, strict=strict)
     elif isinstance(want, str):
         assert got == want, f"{path}: {got!r} != {want!r}"
     else:
-        _exact_leaf(got, want, _exact, path, _key, exact_floats, report)
+        _exact_leaf(got, want, _exact, path, _key, exact_floats, report, strict)
 
 
 def strip_exact(tree):

@@ -42,7 +42,7 @@ def _write_report():
 
 def _check(name, got, want, exact_floats=False):
     rep = FloatReport()
-    assert_same_exact(got, want, name, exact_floats=exact_floats, report=rep)
+    assert_same_exact(got, want, name, exact_floats=exact_floats, report=rep, strict=True)
     REPORT[name] = rep.as_dict()
     return rep
 
