@@ -181,6 +181,7 @@ SIGNATURES = [
     ("esgpu_comm_unique_id", ctypes.c_int, [_VP]),
     ("esgpu_comm_init", ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_int32, _VP, _PP]),
     ("esgpu_comm_init_host", ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(HostTransport), _PP]),
+    ("esgpu_segment_release_wide", ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_uint64)]),
     ("esgpu_comm_init_local", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, _PP]),
     ("esgpu_comm_build_reduce", ctypes.c_int, [_VP, ctypes.POINTER(_VP), ctypes.c_int32, ctypes.c_int32,
                                                ctypes.POINTER(ctypes.POINTER(Result))]),

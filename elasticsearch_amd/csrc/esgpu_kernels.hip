@@ -1341,6 +1341,21 @@ void launch_gather_rows(const GatherParams& p, hipStream_t st) {
     hipLaunchKernelGGL(gather_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, st, p);
 }
 
+template <class D>
+__global__ __launch_bounds__(256) void expand_delta_kernel(const D* __restrict__ d, uint32_t n, int64_t base,
+                                                           int64_t* __restrict__ out) {
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+        out[i] = (int64_t)((uint64_t)base + (uint64_t)d[i]);
+}
+void launch_expand_d32(const uint32_t* d, uint32_t n, int64_t base, int64_t* out, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(expand_delta_kernel<uint32_t>, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, s,
+                              d, n, base, out);
+}
+void launch_expand_d16(const uint16_t* d, uint32_t n, int64_t base, int64_t* out, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(expand_delta_kernel<uint16_t>, dim3(std::min<uint32_t>((n + 255) / 256, 8192)), dim3(256), 0, s,
+                              d, n, base, out);
+}
+
 __global__ __launch_bounds__(256) void dd_fold_kernel(double* __restrict__ hi, double* __restrict__ lo, size_t n) {
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
         const double l = lo[i];

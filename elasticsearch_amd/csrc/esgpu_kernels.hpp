@@ -401,6 +401,9 @@ void launch_term_totals(const unsigned long long* cnt, uint32_t H, uint32_t T, u
 // n u64 words device -> device-visible pinned host memory
 void launch_copy_u64(const unsigned long long* src, unsigned long long* dst, size_t n, hipStream_t s);
 void launch_gather_rows(const GatherParams& p, hipStream_t s);
+// a long column's upload-width values rebuilt from its compact deltas (value = base + delta)
+void launch_expand_d32(const uint32_t* d, uint32_t n, int64_t base, int64_t* out, hipStream_t s);
+void launch_expand_d16(const uint16_t* d, uint32_t n, int64_t base, int64_t* out, hipStream_t s);
 // g_sum / g_sq += their compensated low parts, which are cleared (after every collect launch that used them)
 void launch_dd_fold(double* hi, double* lo, size_t n, hipStream_t s);
 void launch_fill_u64(unsigned long long* p, size_t n, unsigned long long v, hipStream_t s);

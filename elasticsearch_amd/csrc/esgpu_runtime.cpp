@@ -312,6 +312,9 @@ struct DevColumn {
     // with the column): ords() in 16 bits (0xFFFF missing) while the dictionary has fewer than 65,535 terms -- keyed by
     // the ords() buffer it was made from -- and a long column's values as 32-bit deltas over vmin while vmax - vmin < 2^32
     DevBuf ord16, d32, d16;  // d16: the same deltas in 16 bits while vmax - vmin < 2^16 (ensure_d16)
+    // esgpu_segment_release_wide: the upload-width values of a single-valued long column with a compact copy were
+    // released; wide_i64 rebuilds them (losslessly, from the deltas) for a kernel that reads them, and keeps them
+    bool wide_released = false;
     const void* ord16_src = nullptr;
     bool d32_done = false, d16_done = false;
     // distinct values of the column, estimated from the HLL registers of an earlier request that collected this segment
@@ -344,6 +347,8 @@ struct esgpu_segment {
         return it == cols.end() ? nullptr : it->second.get();
     }
 };
+
+static const void* wide_i64(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
 
 // the synthetic dictionaries (host-%04d / /p/%08x) are formulas: one shared instance per field
 static std::shared_ptr<const TermDict> synth_dict(uint32_t bit, uint64_t n) {
@@ -587,6 +592,25 @@ extern "C" int esgpu_segment_max_doc(const esgpu_segment* s, uint32_t* max_doc) 
     return guarded([&] { *max_doc = s->max_doc; });
 }
 
+extern "C" int esgpu_segment_release_wide(esgpu_segment* s, uint64_t* released) {
+    return guarded([&] {
+        require(s != nullptr, ESGPU_ERR_INVALID, "null segment");
+        esgpu_ctx* c = s->ctx;
+        HIPX(hipSetDevice(c->device));
+        HIPX(hipDeviceSynchronize());  // no kernel still reads a buffer released below
+        std::lock_guard<std::mutex> lk(c->mu);
+        uint64_t n = 0;
+        for (auto& kv : s->cols) {
+            DevColumn& col = *kv.second;
+            if (col.type != ESGPU_COL_I64 || col.multi || !col.values.p || !(col.d32.p || col.d16.p)) continue;
+            n += col.values.bytes;
+            col.values.release();
+            col.wide_released = true;
+        }
+        if (released) *released = n;
+    });
+}
+
 extern "C" int esgpu_segment_read_column(const esgpu_segment* s, const char* field, uint64_t start, uint64_t count, void* out) {
     return guarded([&] {
         const DevColumn* col = s->col(field);
@@ -594,7 +618,8 @@ extern "C" int esgpu_segment_read_column(const esgpu_segment* s, const char* fie
         require(!col->multi && start + count <= s->max_doc, ESGPU_ERR_INVALID, "range out of bounds");
         const size_t w = col->type == ESGPU_COL_ORD_U32 ? 4 : 8;
         HIPX(hipSetDevice(s->ctx->device));
-        HIPX(hipMemcpy(out, col->values.as<uint8_t>() + start * w, count * w, hipMemcpyDeviceToHost));
+        const uint8_t* v = (const uint8_t*)(col->type == ESGPU_COL_I64 ? wide_i64(s->ctx, col, s, s->ctx->stream) : col->values.p);
+        HIPX(hipMemcpy(out, v + start * w, count * w, hipMemcpyDeviceToHost));
     });
 }
 
@@ -1638,6 +1663,7 @@ static uint32_t pi_copies();
 static const uint16_t* ensure_ord16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
 static const uint32_t* ensure_d32(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
 static const uint16_t* ensure_d16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
+static const void* wide_i64(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
 static uint32_t sampled_hot_ord(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s);
 
 // The pipeline's clauses as device predicates: up to kMaxPreds of them are evaluated inside the collect kernels; with
@@ -1653,7 +1679,7 @@ static void set_preds(esgpu_plan* p, const Pipeline& pl, const esgpu_segment* s,
         const DevColumn* col = s->col(p->filter_fields[k].c_str());
         PredDev q{};
         require(col != nullptr, ESGPU_ERR_UNSUPPORTED, "filter on a field missing from the segment");
-        q.col = col->type == ESGPU_COL_ORD_U32 ? col->ords().p : col->values.p;  // keyword terms: global ordinal
+        q.col = col->type == ESGPU_COL_ORD_U32 ? col->ords().p : col->type == ESGPU_COL_F64 ? col->values.p : nullptr;
         q.present = col->present.as<uint64_t>();
         q.offsets = col->multi ? col->offsets.as<uint64_t>() : nullptr;
         if (col->type == ESGPU_COL_ORD_U32) {
@@ -1732,6 +1758,7 @@ static void set_preds(esgpu_plan* p, const Pipeline& pl, const esgpu_segment* s,
                     q.base = col->vmin;
                 }
             }
+            if (q.kind == PRED_I64_RANGE) q.col = wide_i64(p->ctx, col, s, p->stream);  // the upload-width values
             *bytes_per_doc += q.kind == PRED_D16_RANGE ? 2 : q.kind == PRED_D32_RANGE ? 4 : 8;
         }
         all.push_back(q);
@@ -2465,7 +2492,8 @@ static void materialize_hist_ords(esgpu_plan* p, Pipeline& pl, const esgpu_segme
     const DevColumn* src = s->col(pl.ord_field.c_str());
     DevColumn& d = *pl.ord_col;
     if (d.values.bytes < (size_t)s->n_pad * 4) d.values.alloc(p->ctx, (size_t)s->n_pad * 4);
-    launch_hist_ords(src->values.as<int64_t>(), src->present.as<uint64_t>(), s->max_doc, s->n_pad, src->type == ESGPU_COL_F64,
+    launch_hist_ords((const int64_t*)wide_i64(p->ctx, src, s, p->stream), src->present.as<uint64_t>(), s->max_doc, s->n_pad,
+                     src->type == ESGPU_COL_F64,
                      pl.ord_interval, pl.ord_offset, pl.ord_key0, pl.ord_keys, d.values.as<uint32_t>(), p->stream);
     HIPX(hipGetLastError());
 }
@@ -2512,7 +2540,7 @@ static void collect_cards(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, c
     G.ord_off = (oc && oc->multi) ? oc->offsets.as<uint64_t>() : nullptr;
     G.T = pl.T;
     G.H = pl.H;
-    G.hv = hc ? hc->values.as<int64_t>() : nullptr;
+    G.hv = hc && !pl.inner_terms ? (const int64_t*)wide_i64(p->ctx, hc, s, p->stream) : nullptr;
     G.hv_present = hc ? hc->present.as<uint64_t>() : nullptr;
     G.hv_off = (hc && hc->multi) ? hc->offsets.as<uint64_t>() : nullptr;
     G.hv_f64 = hc && hc->type == ESGPU_COL_F64;
@@ -2546,7 +2574,7 @@ static void collect_cards(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, c
         if (!col || s->max_doc == 0) continue;  // unmapped in this segment: no values
         CardParams C{};
         C.G = G;
-        C.col = col->values.p;
+        C.col = wide_i64(p->ctx, col, s, p->stream);  // (any column type: only a released long is rebuilt)
         C.off = col->multi ? col->offsets.as<uint64_t>() : nullptr;
         C.present = col->present.as<uint64_t>();
         C.p = cs.p;
@@ -2854,6 +2882,14 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         P.g_sum_lo = lo(pl.g_sum_lo);
         if (pl.met >= 3 && P.g_sq) P.g_sq_lo = lo(pl.g_sq_lo);
     }
+    // upload-width values the launch reads, rebuilt if released (esgpu_segment_release_wide): the CSR kernel reads them
+    // all; the single-valued kernel the ones no compact copy replaces
+    auto need_wide = [&](bool all) {
+        if (P.ord_src && osrc && osrc->wide_released) P.ord_src = (const int64_t*)wide_i64(p->ctx, osrc, s, p->stream);
+        if (L_HIST && hc && !pl.inner_terms && hc->wide_released && (all || !P.hv32))
+            P.hv = (const int64_t*)wide_i64(p->ctx, hc, s, p->stream);
+        if (L_met > 0 && mc && mc->wide_released && (all || (!P.mv32 && !P.mv16))) P.mv = wide_i64(p->ctx, mc, s, p->stream);
+    };
     auto dd_fold = [&] {
         if (P.g_sum_lo) launch_dd_fold(P.g_sum, P.g_sum_lo, dd_cells, p->stream);
         if (P.g_sq_lo) launch_dd_fold(P.g_sq, P.g_sq_lo, dd_cells, p->stream);
@@ -2862,6 +2898,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     const int ret = inner_missing ? 2 : 1;
     if (multi && !inner_missing) count_width(p, pl, s, false, first_segment);
     if (multi) {
+        need_wide(true);
         const bool ok = collect_multi(p, pl, s, P, L_ORD ? oc : nullptr, L_HIST ? hc : nullptr, inner_missing ? nullptr : mc,
                                       L_met, d_accept);
         dd_fold();
@@ -3107,6 +3144,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         launch_zone_keys(P, const_cast<int64_t*>(P.zkey), p->stream);
         HIPX(hipGetLastError());
     }
+    need_wide(false);
     HIPX(hipEventRecord(pl.e0, p->stream));
     if (fold && P.npred > 0) {  // (inside the timed region: part of the collect)
         uint64_t* bits = (uint64_t*)p->s_xbits.ensure(p->ctx, std::max<size_t>(s->n_pad / 64, 1) * 8);
@@ -3223,6 +3261,26 @@ static uint32_t sampled_hot_ord(esgpu_ctx* c, const DevColumn* col, const esgpu_
     return m->hot_ord;
 }
 
+// the upload-width values of a long column whose wide buffer esgpu_segment_release_wide released, rebuilt from its compact
+// deltas (value = vmin + delta: lossless for every present value) on the first kernel that reads them, and kept
+// (the caller holds c->mu)
+static const void* wide_i64_locked(esgpu_ctx* c, DevColumn* m, const esgpu_segment* s, hipStream_t st) {
+    if (!m->wide_released || m->values.p) return m->values.p;
+    m->values.alloc(c, (size_t)s->n_pad * 8);
+    if (m->d32.p) launch_expand_d32(m->d32.as<uint32_t>(), s->n_pad, m->vmin, m->values.as<int64_t>(), st);
+    else launch_expand_d16(m->d16.as<uint16_t>(), s->n_pad, m->vmin, m->values.as<int64_t>(), st);
+    HIPX(hipGetLastError());
+    HIPX(hipStreamSynchronize(st));
+    m->wide_released = false;
+    return m->values.p;
+}
+static const void* wide_i64(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st) {
+    if (!col) return nullptr;
+    if (!col->wide_released) return col->values.p;
+    std::lock_guard<std::mutex> lk(c->mu);
+    return wide_i64_locked(c, const_cast<DevColumn*>(col), s, st);
+}
+
 static const uint32_t* ensure_d32(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st) {
     DevColumn* m = const_cast<DevColumn*>(col);
     std::lock_guard<std::mutex> lk(c->mu);
@@ -3234,7 +3292,7 @@ static const uint32_t* ensure_d32(esgpu_ctx* c, const DevColumn* col, const esgp
         m->d32.release();
         return nullptr;
     }
-    launch_delta32(col->values.as<int64_t>(), s->n_pad, col->vmin, m->d32.as<uint32_t>(), st);
+    launch_delta32((const int64_t*)wide_i64_locked(c, m, s, st), s->n_pad, col->vmin, m->d32.as<uint32_t>(), st);
     HIPX(hipGetLastError());
     HIPX(hipStreamSynchronize(st));
     return m->d32.as<uint32_t>();
@@ -3251,7 +3309,7 @@ static const uint16_t* ensure_d16(esgpu_ctx* c, const DevColumn* col, const esgp
         m->d16.release();
         return nullptr;
     }
-    launch_delta16(col->values.as<int64_t>(), s->n_pad, col->vmin, m->d16.as<uint16_t>(), st);
+    launch_delta16((const int64_t*)wide_i64_locked(c, m, s, st), s->n_pad, col->vmin, m->d16.as<uint16_t>(), st);
     HIPX(hipGetLastError());
     HIPX(hipStreamSynchronize(st));
     return m->d16.as<uint16_t>();
@@ -3313,7 +3371,7 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
     HllParams H{};
     H.n_docs = s->max_doc;
     H.p = pl.p;
-    H.col = col->values.p;
+    H.col = wide_i64(p->ctx, col, s, p->stream);
     H.present = col->present.as<uint64_t>();
     H.accept = d_accept;
     uint64_t bytes_per_doc = col->type == ESGPU_COL_ORD_U32 ? 4 : 8;

@@ -165,6 +165,13 @@ class Segment:
         N.check(N.lib().esgpu_segment_max_doc(self._ptr, ctypes.byref(v)))
         return v.value
 
+    def release_wide(self):
+        """Frees the upload-width values of the long columns that have compact copies (esgpu_segment_release_wide);
+        returns the bytes freed.  A later kernel that reads them rebuilds them from the deltas."""
+        v = ctypes.c_uint64()
+        N.check(N.lib().esgpu_segment_release_wide(self._ptr, ctypes.byref(v)))
+        return v.value
+
     def read_column(self, field, start, count, dtype):
         out = np.empty(count, dtype=dtype)
         N.check(N.lib().esgpu_segment_read_column(self._ptr, field.encode(), start, count, out.ctypes.data))

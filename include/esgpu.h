@@ -158,6 +158,12 @@ int esgpu_synthetic_fill_host(uint64_t seed, uint32_t shard, uint32_t num_docs, 
 int esgpu_synthetic_term(uint32_t field_bit, uint64_t ord, char* buf, size_t cap);
 /* Copy a device column range back to host (tests compare device vs host generator). */
 int esgpu_segment_read_column(const esgpu_segment* seg, const char* field, uint64_t start, uint64_t count, void* out);
+/* Frees the upload-width values of every single-valued long column that has a compact copy (its u32 / u16 deltas over
+ * the segment minimum, built by an earlier request): those kernels read only the copy.  A later request whose kernel
+ * reads the upload-width values (a calendar / DST rounding, cardinality of the field, a range filter over a wide
+ * span ...) rebuilds them from the deltas -- losslessly -- and they stay (charged to the context's budget, like every
+ * segment product).  No request may be collecting the segment during the call.  *released: the bytes freed. */
+int esgpu_segment_release_wide(esgpu_segment* seg, uint64_t* released);
 
 /* Global ordinals over the segments of one reader = GlobalOrdinalsBuilder.build / Lucene OrdinalMap
  * (core/.../index/fielddata/ordinals/GlobalOrdinalsBuilder.java:45-70, GlobalOrdinalMapping.java:51-58).

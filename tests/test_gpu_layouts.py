@@ -207,3 +207,33 @@ def test_packed_cells_through_folded_filters(engine, name, dead):
         plan.close()
         seg.close()
     assert_same(res.to_dict(), want["shards"][0], f"{name} dead {dead}")
+
+
+def test_released_wide_columns_rebuilt_on_demand(engine):
+    """esgpu_segment_release_wide (HBM footprint): after the north star built the segment's compact
+    copies, the upload-width timestamp and metric columns are freed (16 B per doc); the north star runs again from the
+    copies alone (no rebuild: the HBM in use stays down), then requests whose kernels read the upload-width values -- a
+    monthly calendar histogram (bucket-start table over the raw timestamps), cardinality of a long field, terms with
+    extended_stats (the metric's 32-bit deltas, rebuilt from the 16-bit ones through the wide column) -- rebuild them from
+    the deltas and still match the oracle."""
+    n = 3_000_000
+    fields = ("host", "@timestamp", "response_time_ms", "bytes")
+    cols = synthetic_columns(fields, n, shard=6)
+    seg = engine.synthetic_segment(n, fields=fields, shard=6)
+    res, _ = _run(engine, seg, NS_AGGS)
+    want = O.run([(cols, n)], NS_AGGS)
+    assert_same(res.to_dict(), want["shards"][0], "before release")
+    used0 = engine.hbm_used()
+    freed = seg.release_wide()
+    assert freed >= 16 * n, freed  # timestamps and response times (bytes has no compact copy yet)
+    assert engine.hbm_used() <= used0 - freed
+    res, _ = _run(engine, seg, NS_AGGS)
+    assert_same(res.to_dict(), want["shards"][0], "after release")
+    assert engine.hbm_used() <= used0 - freed  # the compact copies sufficed
+    wide_aggs = [AB.dateHistogram("m").field("@timestamp").interval("month").subAggregation(AB.stats("s").field("response_time_ms")),
+                 AB.terms("h").field("host").size(5).subAggregation(AB.extendedStats("x").field("response_time_ms")),
+                 AB.cardinality("c").field("response_time_ms"),
+                 AB.histogram("rt").field("response_time_ms").interval(100).subAggregation(AB.avg("b").field("bytes"))]
+    res, _ = _run(engine, seg, wide_aggs)
+    assert_same(res.to_dict(), O.run([(cols, n)], wide_aggs)["shards"][0], "rebuilt")
+    seg.close()
