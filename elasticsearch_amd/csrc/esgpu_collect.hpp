@@ -150,7 +150,30 @@ __device__ __forceinline__ uint32_t eval_pred(const PredDev& q, uint32_t doc0) {
 // packed-cell kernels over the 16-bit ordinals and metric deltas (and, with a key, the 32-bit timestamp deltas of a dense
 // timestamp column): loads only, no use of a loaded word until unpack_docs
 template <int MET, int VK, bool HIST>
-constexpr bool kRawPI = MET > 0 && (VK & 64) != 0 && (VK & 16) != 0 && (VK & 256) != 0 && (!HIST || (VK & 32) != 0);
+constexpr bool kRawPI = MET > 0 && (VK & 64) != 0 && (VK & 16) != 0 && (VK & 256) != 0 && (!HIST || (VK & (32 | 8192)) != 0);
+// VK bit 8192 (raw-load kernels only, instead of bit 32): the key column as block deltas -- 16 bits per doc over the
+// minimum of its run of 2^kB16Shift docs (one 8-byte word per run, the same for all 4 docs of a thread)
+template <int VK>
+__device__ __forceinline__ void load_keys_raw(const CollectParams& P, uint32_t doc0, uint32_t (&raw)[10]) {
+    if constexpr ((VK & 8192) != 0) {
+        const u32x2_t t = load8(P.hv16 + doc0), b = load8(P.hv16_base + (doc0 >> kB16Shift));
+        raw[2] = t.x; raw[3] = t.y; raw[4] = b.x; raw[5] = b.y;
+    } else {
+        const u32x4_t t = load16(P.hv32 + doc0);
+        raw[2] = t.x; raw[3] = t.y; raw[4] = t.z; raw[5] = t.w;
+    }
+}
+template <int VK>
+__device__ __forceinline__ void unpack_keys_raw(const CollectParams& P, const uint32_t (&raw)[10], int64_t (&hv)[4]) {
+    if constexpr ((VK & 8192) != 0) {
+        const int64_t b = (int64_t)join64(raw[4], raw[5]);
+        hv[0] = b + (int64_t)(raw[2] & 0xFFFFu); hv[1] = b + (int64_t)(raw[2] >> 16);
+        hv[2] = b + (int64_t)(raw[3] & 0xFFFFu); hv[3] = b + (int64_t)(raw[3] >> 16);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hv[j] = P.hv_base + (int64_t)raw[2 + j];
+    }
+}
 // VK bit 1024: grids over dense compact columns without a filter -- 16-bit ordinals (counting terms grids), timestamp
 // deltas, a histogram-only grid's u32 metric deltas -- the same raw loads, unpacked when processed
 template <bool ORD, int MET, int VK>
@@ -166,10 +189,7 @@ __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0,
     if constexpr (kRawPI<MET, VK, HIST>) {
         const u32x2_t o = load8(P.ord16 + doc0);
         d.raw[0] = o.x; d.raw[1] = o.y;
-        if constexpr (HIST) {
-            const u32x4_t t = load16(P.hv32 + doc0);
-            d.raw[2] = t.x; d.raw[3] = t.y; d.raw[4] = t.z; d.raw[5] = t.w;
-        }
+        if constexpr (HIST) load_keys_raw<VK>(P, doc0, d.raw);
         const u32x2_t m = load8(P.mv16 + doc0);
         d.raw[6] = m.x; d.raw[7] = m.y;
         if constexpr ((VK & 512) != 0) d.racc = P.accept[doc0 >> 6];
@@ -181,10 +201,7 @@ __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0,
             const u32x2_t o = load8(P.ord16 + doc0);
             d.raw[0] = o.x; d.raw[1] = o.y;
         }
-        if constexpr (HIST) {
-            const u32x4_t t = load16(P.hv32 + doc0);
-            d.raw[2] = t.x; d.raw[3] = t.y; d.raw[4] = t.z; d.raw[5] = t.w;
-        }
+        if constexpr (HIST) load_keys_raw<VK>(P, doc0, d.raw);
         if constexpr (MET > 0 && (VK & 2048) != 0) {
             const u32x2_t m = load8(P.mv16 + doc0);
             d.raw[6] = m.x; d.raw[7] = m.y;
@@ -719,8 +736,7 @@ __device__ __forceinline__ void unpack_docs(const CollectParams& P, Doc4& d) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) d.ord[j] = x[j] == 0xFFFFu ? kMissingOrd : x[j];
     if constexpr (HIST) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) d.hv[j] = P.hv_base + (int64_t)d.raw[2 + j];
+        unpack_keys_raw<VK>(P, d.raw, d.hv);
         d.hpres = 0xFu;
     }
     d.mvd[0] = d.raw[6] & 0xFFFFu; d.mvd[1] = d.raw[6] >> 16; d.mvd[2] = d.raw[7] & 0xFFFFu; d.mvd[3] = d.raw[7] >> 16;
@@ -744,8 +760,7 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
             for (int j = 0; j < 4; ++j) du.ord[j] = x[j] == 0xFFFFu ? kMissingOrd : x[j];
         }
         if constexpr (HIST) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) du.hv[j] = P.hv_base + (int64_t)du.raw[2 + j];
+            unpack_keys_raw<VK>(P, du.raw, du.hv);
             du.hpres = 0xFu;
         }
         if constexpr (MET > 0 && (VK & 2048) != 0) {  // integer runs: the 16-bit deltas as they are
@@ -1439,12 +1454,17 @@ static auto with_vk0(bool hv_f64, bool mv_f64, F f) {
 // Bits 16 / 32 (compact ordinal / histogram columns): terms dimensions without a derived key index, affine histograms
 // over a long column.
 template <bool ORD, int HK, int MET, class F>
-static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, bool pi, bool m32, bool m16, bool acc, bool raw,
-                    bool runs1, F f) {
+static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, bool t16, bool pi, bool m32, bool m16, bool acc,
+                    bool raw, bool runs1, F f) {
+    // t16: the key column is read as block deltas (VK bit 8192 in place of 32) -- by the raw-load kernels only; the host
+    // picks it only for a launch that takes one of them (t32 is then set as well)
     // VK bit 128, a compact long metric (u32 deltas, values restored in the loader): histogram-only grids over compact
     // timestamps (date_histogram{stats / extended_stats / avg}) and extended_stats under terms over compact columns
     if constexpr (MET > 0 && !ORD && HK == 1) {
         if (m32 && !pi && !mv_f64 && t32 && !hv_f64) {
+            if (raw && m16 && runs1 && t16) return f(std::integral_constant<int, 8192 | 128 | 1024 | 2048 | 4096>{});
+            if (raw && m16 && t16) return f(std::integral_constant<int, 8192 | 128 | 1024 | 2048>{});
+            if (raw && t16) return f(std::integral_constant<int, 8192 | 128 | 1024>{});
             if (raw && m16 && runs1) return f(std::integral_constant<int, 32 | 128 | 1024 | 2048 | 4096>{});
             if (raw && m16) return f(std::integral_constant<int, 32 | 128 | 1024 | 2048>{});
             if (raw) return f(std::integral_constant<int, 32 | 128 | 1024>{});
@@ -1452,11 +1472,13 @@ static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, boo
         }
     }
     if constexpr (MET == 0 && !ORD && HK == 1) {
+        if (raw && t16 && !hv_f64) return f(std::integral_constant<int, 8192 | 1024>{});
         if (raw && t32 && !hv_f64) return f(std::integral_constant<int, 32 | 1024>{});
     }
     if constexpr (MET == 0 && ORD && (HK == 0 || HK == 1)) {  // counting terms grids over 16-bit ordinals
         if (raw && c16 && !dord) {
             if constexpr (HK == 1) {
+                if (t16 && !hv_f64) return f(std::integral_constant<int, 16 | 8192 | 1024>{});
                 if (t32 && !hv_f64) return f(std::integral_constant<int, 48 | 1024>{});
             } else {
                 return f(std::integral_constant<int, 16 | 1024>{});
@@ -1480,6 +1502,8 @@ static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, boo
         if (pi && !mv_f64 && !dord) {
             if constexpr (HK == 1) {
                 if (t32 && !hv_f64) {
+                    if (c16 && m16 && acc && t16) return f(std::integral_constant<int, 16 | 8192 | 64 | 256 | 512>{});
+                    if (c16 && m16 && t16) return f(std::integral_constant<int, 16 | 8192 | 64 | 256>{});
                     if (c16 && m16 && acc) return f(std::integral_constant<int, 48 | 64 | 256 | 512>{});
                     if (c16 && m16) return f(std::integral_constant<int, 48 | 64 | 256>{});
                     if (c16) return f(std::integral_constant<int, 48 | 64>{});
@@ -1524,8 +1548,8 @@ static auto with_wg(bool wide, F f) {
 
 template <bool ORD, int HK, int MET>
 static void launch_t(const CollectParams& p, bool wide, uint32_t grid, size_t lds, hipStream_t st) {
-    with_vk<ORD, HK, MET>(p.hv_f64 != 0, p.mv_f64 != 0, p.ord_src != nullptr, p.ord16 != nullptr, p.hv32 != nullptr,
-                          (p.mv32 || p.mv16) && p.pk_shift != 0, (p.mv32 || p.mv16) && p.pk_shift == 0, p.mv16 != nullptr,
+    with_vk<ORD, HK, MET>(p.hv_f64 != 0, p.mv_f64 != 0, p.ord_src != nullptr, p.ord16 != nullptr,
+                          p.hv32 != nullptr || p.hv16 != nullptr, p.hv16 != nullptr, (p.mv32 || p.mv16) && p.pk_shift != 0, (p.mv32 || p.mv16) && p.pk_shift == 0, p.mv16 != nullptr,
                           p.accept != nullptr, p.raw_dense != 0, p.runs1 != 0, [&](auto vk) {
         return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
             hipLaunchKernelGGL((collect_kernel<ORD, HK, MET, decltype(vk)::value, decltype(wg)::value>), dim3(grid),
@@ -1548,7 +1572,7 @@ static void launch_m(const CollectParams& p, int met, bool wide, uint32_t grid, 
 template <bool ORD, int HK, int MET>
 static int occ_t(size_t lds, int vkbits, bool wide) {
     return with_vk<ORD, HK, MET>((vkbits & 1) != 0, (vkbits & 2) != 0, (vkbits & 8) != 0, (vkbits & 16) != 0,
-                                 (vkbits & 32) != 0, (vkbits & 64) != 0, (vkbits & 128) != 0, (vkbits & 256) != 0,
+                                 (vkbits & (32 | 8192)) != 0, (vkbits & 8192) != 0, (vkbits & 64) != 0, (vkbits & 128) != 0, (vkbits & 256) != 0,
                                  (vkbits & 512) != 0, (vkbits & 1024) != 0, (vkbits & 4096) != 0, [&](auto vk) {
         return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
             int n = 0;

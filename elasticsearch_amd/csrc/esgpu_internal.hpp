@@ -70,7 +70,7 @@ struct esgpu_ctx {
     hipStream_t stream = nullptr;  // upload / generation stream
     std::mutex mu;
     // layout options (esgpu_ctx_set_option): compact columns, packed integer metric cells
-    std::atomic<int> opt_compact{1}, opt_pi{1}, opt_hll_fs{1};
+    std::atomic<int> opt_compact{1}, opt_pi{1}, opt_hll_fs{1}, opt_b16{1};
     // synthetic tables (device copies)
     double* d_host_cdf = nullptr;
     double* d_rt_cdf = nullptr;

@@ -85,6 +85,7 @@ extern "C" int esgpu_ctx_set_option(esgpu_ctx* c, int32_t option, int64_t value)
         require(value == 0 || value == 1, ESGPU_ERR_INVALID, "option value must be 0 or 1");
         if (option == ESGPU_OPT_COMPACT_COLUMNS) c->opt_compact = (int)value;
         else if (option == ESGPU_OPT_PACKED_METRIC) c->opt_pi = (int)value;
+        else if (option == ESGPU_OPT_BLOCK_DELTAS) c->opt_b16 = (int)value;
         else throw EsError(ESGPU_ERR_INVALID, "unknown context option");
     });
 }
@@ -95,6 +96,7 @@ extern "C" int esgpu_ctx_get_option(const esgpu_ctx* c, int32_t option, int64_t*
         if (option == ESGPU_OPT_COMPACT_COLUMNS) *value = c->opt_compact;
         else if (option == ESGPU_OPT_PACKED_METRIC) *value = c->opt_pi;
         else if (option == ESGPU_OPT_HLL_FLOOR) *value = c->opt_hll_fs;
+        else if (option == ESGPU_OPT_BLOCK_DELTAS) *value = c->opt_b16;
         else throw EsError(ESGPU_ERR_INVALID, "unknown context option");
     });
 }
@@ -117,6 +119,7 @@ extern "C" int esgpu_ctx_create(int device, uint64_t budget, esgpu_ctx** out) {
         c->opt_compact = env_on("ESGPU_COMPACT") ? 1 : 0;
         c->opt_pi = env_on("ESGPU_PI") ? 1 : 0;
         c->opt_hll_fs = env_on("ESGPU_HLL_FS") ? 1 : 0;
+        c->opt_b16 = env_on("ESGPU_B16") ? 1 : 0;
         HIPX(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         *out = c.release();
     });
@@ -312,11 +315,14 @@ struct DevColumn {
     // with the column): ords() in 16 bits (0xFFFF missing) while the dictionary has fewer than 65,535 terms -- keyed by
     // the ords() buffer it was made from -- and a long column's values as 32-bit deltas over vmin while vmax - vmin < 2^32
     DevBuf ord16, d32, d16;  // d16: the same deltas in 16 bits while vmax - vmin < 2^16 (ensure_d16)
+    // block deltas of a dense key column (ensure_b16): per run of kB16Docs docs its minimum (b16_base) and a 16-bit delta
+    // per doc, when every run spans < 2^16 -- time-sorted timestamps at any density above ~1 doc per 32 ms
+    DevBuf b16, b16_base;
     // esgpu_segment_release_wide: the upload-width values of a single-valued long column with a compact copy were
     // released; wide_i64 rebuilds them (losslessly, from the deltas) for a kernel that reads them, and keeps them
     bool wide_released = false;
     const void* ord16_src = nullptr;
-    bool d32_done = false, d16_done = false;
+    bool d32_done = false, d16_done = false, b16_done = false;
     // distinct values of the column, estimated from the HLL registers of an earlier request that collected this segment
     // alone and unfiltered (-1: none yet) -- picks the floored stream's floor (collect_hll); any value is correct
     // (shared: a plan that collected the segment keeps it alive for its build, whatever happens to the segment meanwhile)
@@ -602,7 +608,7 @@ extern "C" int esgpu_segment_release_wide(esgpu_segment* s, uint64_t* released) 
         uint64_t n = 0;
         for (auto& kv : s->cols) {
             DevColumn& col = *kv.second;
-            if (col.type != ESGPU_COL_I64 || col.multi || !col.values.p || !(col.d32.p || col.d16.p)) continue;
+            if (col.type != ESGPU_COL_I64 || col.multi || !col.values.p || !(col.d32.p || col.d16.p || col.b16.p)) continue;
             n += col.values.bytes;
             col.values.release();
             col.wide_released = true;
@@ -1658,11 +1664,13 @@ static bool raw_hist_on();
 static bool dd_forced();
 static bool int_runs_on();
 static bool runs1_on();
+static bool b16_on(const esgpu_ctx* c);
 static bool pi_cells(const esgpu_ctx* c);
 static uint32_t pi_copies();
 static const uint16_t* ensure_ord16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
 static const uint32_t* ensure_d32(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
 static const uint16_t* ensure_d16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
+static const DevColumn* ensure_b16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
 static const void* wide_i64(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
 static uint32_t sampled_hot_ord(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s);
 
@@ -2886,7 +2894,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     // all; the single-valued kernel the ones no compact copy replaces
     auto need_wide = [&](bool all) {
         if (P.ord_src && osrc && osrc->wide_released) P.ord_src = (const int64_t*)wide_i64(p->ctx, osrc, s, p->stream);
-        if (L_HIST && hc && !pl.inner_terms && hc->wide_released && (all || !P.hv32))
+        if (L_HIST && hc && !pl.inner_terms && hc->wide_released && (all || !(P.hv32 || P.hv16)))
             P.hv = (const int64_t*)wide_i64(p->ctx, hc, s, p->stream);
         if (L_met > 0 && mc && mc->wide_released && (all || (!P.mv32 && !P.mv16))) P.mv = wide_i64(p->ctx, mc, s, p->stream);
     };
@@ -2906,6 +2914,8 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     }
     // compact columns: 2 B per ordinal instead of 4, 4 B per timestamp instead of 8 -- the reported (algorithmic) bytes
     // are the bytes this layout must move (SURVEY §8(d)'s upload-width figure would put config 5 above the HBM peak)
+    const DevColumn* t16 = nullptr;  // the key column's block deltas (ensure_b16)
+    bool tcomp = false;              // the key column is read as compact deltas (32-bit, or block deltas)
     if (compact_cols(p->ctx)) {
         const bool plain_ord = oc && !pl.comp && !pl.ord_hist && oc == s->col(pl.ord_field.c_str());
         if (L_ORD && P.ord && plain_ord && !oc->multi && oc->ord_count() < 0xFFFFu) {
@@ -2914,10 +2924,19 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         }
         if (L_HIST && hc && !pl.inner_terms && !P.kstart && hc->type == ESGPU_COL_I64 && !hc->multi && hc->vmin <= hc->vmax &&
             (uint64_t)hc->vmax - (uint64_t)hc->vmin < (1ull << 32)) {
-            P.hv32 = ensure_d32(p->ctx, hc, s, p->stream);
-            if (P.hv32) {
+            // a dense time-sorted column has block deltas (2 B per doc), which the raw-load kernels read: taken below once
+            // the launch is known to be one of them -- no 32-bit copy is built for it then
+            if (b16_on(p->ctx) && !hc->present.p) t16 = ensure_b16(p->ctx, hc, s, p->stream);
+            if (t16) {
                 P.hv_base = hc->vmin;
-                bytes_per_doc -= 4;
+                tcomp = true;
+            } else {
+                P.hv32 = ensure_d32(p->ctx, hc, s, p->stream);
+                if (P.hv32) {
+                    P.hv_base = hc->vmin;
+                    bytes_per_doc -= 4;
+                    tcomp = true;
+                }
             }
         }
     }
@@ -2929,7 +2948,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     const int hk_launch = L_HIST ? (P.hord ? 3 : P.kstart ? 2 : 1) : 0;
     if (pi_cells(p->ctx) && compact_cols(p->ctx) && L_ORD && !P.ord_src && (L_met == 1 || L_met == 2) && mc && mc->type == ESGPU_COL_I64 &&
         !mc->multi && !mc->present.p && !L_vcnt && mc->vmin <= mc->vmax && (uint64_t)mc->vmax - (uint64_t)mc->vmin < (1ull << 32) &&
-        (hk_launch == 0 || (hk_launch == 1 && P.hv32 && !P.hv_f64)) && !dyn_claim_on()) {
+        (hk_launch == 0 || (hk_launch == 1 && tcomp && !P.hv_f64)) && !dyn_claim_on()) {
         // values spanning < 2^16 (a latency in ms, a status code): the 16-bit deltas, 2 B per doc (instantiated with
         // 16-bit ordinals; those kernels load raw words and unpack them when the docs are processed: dense timestamps
         // only).  Only the copy the kernel reads is built -- no 32-bit copy beside the 16-bit one (HBM per segment)
@@ -2970,8 +2989,8 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     bool m32 = false;
     if (!pi && compact_cols(p->ctx) && L_met > 0 && mc && mc->type == ESGPU_COL_I64 && !mc->multi && mc->vmin <= mc->vmax &&
         (uint64_t)mc->vmax - (uint64_t)mc->vmin < (1ull << 32) && !P.mv_f64 && !inner_missing &&
-        ((!L_ORD && hk_launch == 1 && P.hv32 && !P.hv_f64) ||
-         (L_ORD && L_met == 3 && !P.ord_src && P.ord16 && (hk_launch == 0 || (hk_launch == 1 && P.hv32 && !P.hv_f64))))) {
+        ((!L_ORD && hk_launch == 1 && tcomp && !P.hv_f64) ||
+         (L_ORD && L_met == 3 && !P.ord_src && P.ord16 && (hk_launch == 0 || (hk_launch == 1 && tcomp && !P.hv_f64))))) {
         // histogram-only grids over a dense metric spanning < 2^16 with |values| < 2^26 (v * v exact, as the reference's
         // rounded products then are), read without a filter by the raw-load kernels: the 16-bit deltas and integer run
         // accumulators (VK bit 2048), 6 B per doc -- and no 32-bit copy
@@ -3083,18 +3102,32 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     const bool fold = pi && (P.npred > 0 || P.accept);
     // grids over dense compact columns without a filter -- histogram-only over the timestamp deltas (and a dense compact
     // metric), counting terms grids over 16-bit ordinals (and the timestamp deltas): raw-load kernels (VK bit 1024)
-    const bool raw_hist = hk_launch == 1 && P.hv32 && !P.hv_f64 && !P.hv_present;
+    const bool raw_hist = hk_launch == 1 && tcomp && !P.hv_f64 && !P.hv_present;
     P.raw_dense = raw_hist_on() && !pi && !P.accept && P.npred == 0 &&
                   ((!L_ORD && raw_hist && (L_met == 0 || (m32 && !P.mv_present))) ||
                    (L_ORD && L_met == 0 && P.ord16 && !P.ord_src && (hk_launch == 0 || raw_hist))) ? 1 : 0;
     // the integer runs' 16-bit deltas are read only by the raw-load kernels (no 32-bit copy was built for them)
     require(!(m32 && P.mv16 && !P.raw_dense), ESGPU_ERR_DEVICE, "internal: 16-bit metric deltas outside the raw-load kernels");
+    // the key column: its block deltas where the launch is a raw-load kernel (packed cells over 16-bit columns, or the
+    // dense unfiltered grids), else the 32-bit deltas
+    if (t16) {
+        P.hv16 = nullptr;
+        P.hv16_base = nullptr;
+        P.hv32 = nullptr;
+        if ((pi && P.ord16 && P.mv16) || (P.raw_dense && hk_launch == 1)) {
+            P.hv16 = t16->b16.as<uint16_t>();
+            P.hv16_base = t16->b16_base.as<int64_t>();
+        } else {
+            P.hv32 = ensure_d32(p->ctx, hc, s, p->stream);
+            require(P.hv32 != nullptr, ESGPU_ERR_DEVICE, "out of device memory for the key column's deltas");
+        }
+    }
     // integer runs over time-sorted data (90 % of the blocks span less than one interval): one run per thread; roughly
     // time-ordered data alternates between neighbouring keys and keeps three
     P.runs1 = m32 && P.mv16 && hc && pl.interval > 0 && hc->zspan < pl.interval && runs1_on() ? 1 : 0;
     const int vk = (P.hv_f64 ? 1 : 0) | (P.mv_f64 ? 2 : 0) | (P.ord_src ? 8 : 0) | (P.ord16 ? 16 : 0) | (P.hv32 ? 32 : 0) |
                    (pi ? 64 : 0) | (m32 ? 128 : 0) | (P.mv16 ? 256 : 0) | (fold ? 512 : 0) | (P.raw_dense ? 1024 : 0) |
-                   (P.runs1 ? 4096 : 0);
+                   (P.runs1 ? 4096 : 0) | (P.hv16 ? 8192 : 0);
     const uint64_t occ_key = ((uint64_t)lds << 24) | ((uint64_t)wide << 23) | ((uint64_t)vk << 8) | ((uint64_t)L_met << 4) |
                              ((uint64_t)hk << 1) | (L_ORD ? 1 : 0);
     if (pl.occ_key != occ_key) {
@@ -3126,6 +3159,8 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         goto relaunch;
     }
     if (pi || m32) bytes_per_doc -= P.mv16 ? 6 : 4;
+    if (P.hv16) bytes_per_doc -= 6;            // (+ one 8-byte base per run, below)
+    else if (t16 && P.hv32) bytes_per_doc -= 4;
     uint32_t grid = (P.n_blocks + P.blocks_per_wg - 1) / P.blocks_per_wg;
     // dynamic chunk claiming: one resident wave of workgroups, each flushing its LDS cells once, taking chunks of
     // kGroup blocks until none are left (ESGPU_DYN=0/1 overrides the build default for A/B runs)
@@ -3157,7 +3192,8 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     HIPX(hipGetLastError());
     HIPX(hipEventRecord(pl.e1, p->stream));
     dd_fold();
-    p->last_bytes += bytes_per_doc * (uint64_t)s->max_doc + (d_accept ? ((uint64_t)s->max_doc + 7) / 8 : 0);
+    p->last_bytes += bytes_per_doc * (uint64_t)s->max_doc + (d_accept ? ((uint64_t)s->max_doc + 7) / 8 : 0) +
+                     (P.hv16 ? (((uint64_t)s->max_doc + kB16Docs - 1) >> kB16Shift) * 8 : 0);
     p->last_path = P.lds_mode ? (P.windowed ? 2 : 1) : 0;
     return ret;
 }
@@ -3188,6 +3224,8 @@ static bool runs1_on() {
     static const bool on = [] { const char* e = std::getenv("ESGPU_RUNS1"); return !(e && *e == '0'); }();
     return on;
 }
+// block-delta timestamps on the raw-load kernels (ensure_b16; ESGPU_OPT_BLOCK_DELTAS)
+static bool b16_on(const esgpu_ctx* c) { return c->opt_b16.load() != 0; }
 // ESGPU_DD=1: every metric grid takes the compensated flushes, exact data or not (tests of those paths on integer data)
 static bool dd_forced() {
     static const bool on = [] { const char* e = std::getenv("ESGPU_DD"); return e && *e == '1'; }();
@@ -3268,6 +3306,7 @@ static const void* wide_i64_locked(esgpu_ctx* c, DevColumn* m, const esgpu_segme
     if (!m->wide_released || m->values.p) return m->values.p;
     m->values.alloc(c, (size_t)s->n_pad * 8);
     if (m->d32.p) launch_expand_d32(m->d32.as<uint32_t>(), s->n_pad, m->vmin, m->values.as<int64_t>(), st);
+    else if (m->b16.p) launch_expand_b16(m->b16.as<uint16_t>(), m->b16_base.as<int64_t>(), s->max_doc, s->n_pad, m->values.as<int64_t>(), st);
     else launch_expand_d16(m->d16.as<uint16_t>(), s->n_pad, m->vmin, m->values.as<int64_t>(), st);
     HIPX(hipGetLastError());
     HIPX(hipStreamSynchronize(st));
@@ -3296,6 +3335,40 @@ static const uint32_t* ensure_d32(esgpu_ctx* c, const DevColumn* col, const esgp
     HIPX(hipGetLastError());
     HIPX(hipStreamSynchronize(st));
     return m->d32.as<uint32_t>();
+}
+
+// the block deltas of a dense single-valued long column (null when some run of kB16Docs docs spans 2^16 or more: the
+// column is not sorted enough; the verdict is cached)
+static const DevColumn* ensure_b16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st) {
+    DevColumn* m = const_cast<DevColumn*>(col);
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (m->b16_done) return m->b16.p ? m : nullptr;
+    m->b16_done = true;
+    if (col->type != ESGPU_COL_I64 || col->multi || col->present.p || s->n_pad % kB16Docs) return nullptr;
+    const uint32_t runs = s->n_pad >> kB16Shift;
+    try {
+        m->b16.alloc(c, (size_t)s->n_pad * 2);
+        m->b16_base.alloc(c, (size_t)std::max<uint32_t>(runs, 1) * 8);
+    } catch (const EsError&) {
+        m->b16.release();
+        m->b16_base.release();
+        return nullptr;
+    }
+    DevBuf flag;
+    flag.alloc(c, 4);
+    HIPX(hipMemsetAsync(flag.p, 0, 4, st));
+    launch_block_delta16((const int64_t*)wide_i64_locked(c, m, s, st), s->max_doc, s->n_pad, m->b16.as<uint16_t>(),
+                         m->b16_base.as<int64_t>(), flag.as<unsigned int>(), st);
+    HIPX(hipGetLastError());
+    unsigned int bad = 0;
+    HIPX(hipMemcpyAsync(&bad, flag.p, 4, hipMemcpyDeviceToHost, st));
+    HIPX(hipStreamSynchronize(st));
+    if (bad) {
+        m->b16.release();
+        m->b16_base.release();
+        return nullptr;
+    }
+    return m;
 }
 
 static const uint16_t* ensure_d16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st) {

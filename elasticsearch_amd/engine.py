@@ -279,10 +279,10 @@ class Engine:
         N.check(N.lib().esgpu_ctx_hbm_used(self._ptr, ctypes.byref(v)))
         return v.value
 
-    OPTIONS = {"compact_columns": 1, "packed_metric": 2, "hll_floor": 3}  # include/esgpu.h ESGPU_OPT_*
+    OPTIONS = {"compact_columns": 1, "packed_metric": 2, "hll_floor": 3, "block_deltas": 4}  # include/esgpu.h ESGPU_OPT_*
 
     def set_option(self, name, value):
-        """Layout option of this context (esgpu_ctx_set_option): 'compact_columns' / 'packed_metric', 0 or 1;
+        """Layout option of this context (esgpu_ctx_set_option): 'compact_columns' / 'packed_metric' / 'block_deltas', 0 or 1;
         'hll_floor' 0..8 (include/esgpu.h ESGPU_OPT_HLL_FLOOR)."""
         N.check(N.lib().esgpu_ctx_set_option(self._ptr, self.OPTIONS[name], int(value)))
 

@@ -79,8 +79,11 @@ int esgpu_device_count(int* count);
  *   ESGPU_OPT_HLL_FLOOR:       cardinality register passes over a dense numeric column take the floored stream when
  *                              the request's values per register allow it: 0 = the register phases
  *                              instead, 1 = on (default), 2..8 = on with the floor raised by value - 1 (a test leg:
- *                              registers left below the floor are finished by the tail pass) */
-enum { ESGPU_OPT_COMPACT_COLUMNS = 1, ESGPU_OPT_PACKED_METRIC = 2, ESGPU_OPT_HLL_FLOOR = 3 };
+ *                              registers left below the floor are finished by the tail pass)
+ *   ESGPU_OPT_BLOCK_DELTAS:    a dense time-sorted key column whose every run of 2,048 docs spans < 2^16 is read by
+ *                              the raw-load collect kernels as 16-bit deltas over each run's minimum (2 B per doc
+ *                              instead of 4; needs compact columns; ESGPU_B16=0 turns the default off) */
+enum { ESGPU_OPT_COMPACT_COLUMNS = 1, ESGPU_OPT_PACKED_METRIC = 2, ESGPU_OPT_HLL_FLOOR = 3, ESGPU_OPT_BLOCK_DELTAS = 4 };
 int esgpu_ctx_set_option(esgpu_ctx* ctx, int32_t option, int64_t value);
 int esgpu_ctx_get_option(const esgpu_ctx* ctx, int32_t option, int64_t* value);
 

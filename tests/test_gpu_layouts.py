@@ -5,10 +5,12 @@ The single-valued collect kernel reads, per segment, the narrowest layout the da
   * compact: u16 ordinals (dictionaries under 65,535 terms), u32 deltas of long columns spanning < 2^32 (u16 deltas
     for filter columns spanning < 2^16);
   * compact + packed integer metric cells: a dense long metric under terms read as its u32 deltas (u16 when its values
-    span < 2^16) and accumulated as count << shift | sum of deltas in one u64 LDS word.
+    span < 2^16) and accumulated as count << shift | sum of deltas in one u64 LDS word;
+  * + block deltas: a dense time-sorted key column whose every run of 2,048 docs spans < 2^16 ms, read by the raw-load
+    kernels as 16-bit deltas over each run's minimum (2 B per timestamp, plus 8 B per run).
 Real indices take each of them: timestamps over more than 2^32 ms (49.7 days) keep i64 keys, sparse or double metrics
 keep f64 cells.  The layout is a per-context option (Engine.set_option), so one session runs them all against the same
-oracle result; the algorithmic bytes the plan reports name the layout that ran (north star: 20 / 14 / 8 B per doc).
+oracle result; the algorithmic bytes the plan reports name the layout that ran (north star: 20 / 14 / 8 / 6 B per doc).
 """
 import numpy as np
 import pytest
@@ -22,8 +24,8 @@ from helpers import assert_same, assert_same_exact, bits_from_mask, synthetic_co
 
 pytestmark = pytest.mark.gpu
 
-# (compact columns, packed metric) -> name
-LAYOUTS = {"upload": (0, 0), "compact": (1, 0), "packed": (1, 1)}
+# name -> (compact columns, packed metric, block deltas)
+LAYOUTS = {"upload": (0, 0, 0), "compact": (1, 0, 0), "packed": (1, 1, 0), "block": (1, 1, 1)}
 
 
 class layout:
@@ -35,10 +37,17 @@ class layout:
     def __enter__(self):
         self.e.set_option("compact_columns", self.v[0])
         self.e.set_option("packed_metric", self.v[1])
+        self.e.set_option("block_deltas", self.v[2])
 
     def __exit__(self, *a):
         self.e.set_option("compact_columns", 1)
         self.e.set_option("packed_metric", 1)
+        self.e.set_option("block_deltas", 1)
+
+
+def run_bytes(n):
+    """The block-delta layout's per-run words (8 B per 2,048 docs)."""
+    return (n + 2047) // 2048 * 8
 
 
 def _run(engine, seg, aggs, filters=None, number_of_shards=1, segs=None):
@@ -77,27 +86,106 @@ def c5_100m():
     return n, want
 
 
-@pytest.mark.parametrize("name,bpd", [("upload", 20), ("compact", 14), ("packed", 8)])
+@pytest.mark.parametrize("name,bpd", [("upload", 20), ("compact", 14), ("packed", 8), ("block", 6)])
 def test_north_star_100m_every_layout(engine, ns_100m, name, bpd):
     n, want = ns_100m
     with layout(engine, name):
         seg = engine.synthetic_segment(n, fields=NS_FIELDS)  # a fresh segment: its compact copies are built by this layout
         res, nbytes = _run(engine, seg, NS_AGGS)
         seg.close()
-    assert nbytes == bpd * n, (name, nbytes / n)
+    assert nbytes == bpd * n + (run_bytes(n) if name == "block" else 0), (name, nbytes / n)
     assert_same(res.to_dict(), want["shards"][0], f"{name} shard")
     assert_same(reduce([res]).to_dict(), want["reduced"], f"{name} reduced")
 
 
-@pytest.mark.parametrize("name,bpd", [("upload", 36), ("compact", 20), ("packed", 14)])
+@pytest.mark.parametrize("name,bpd", [("upload", 36), ("compact", 20), ("packed", 14), ("block", 12)])
 def test_config5_100m_every_layout(engine, c5_100m, name, bpd):
     n, want = c5_100m
     with layout(engine, name):
         seg = engine.synthetic_segment(n, fields=C5_FIELDS, shard=2)
         res, nbytes = _run(engine, seg, C5_AGGS, filters=C5_FILTERS, number_of_shards=8)
         seg.close()
-    assert nbytes == bpd * n, (name, nbytes / n)
+    assert nbytes == bpd * n + (run_bytes(n) if name == "block" else 0), (name, nbytes / n)
     assert_same(res.to_dict(), want["shards"][0], f"{name} shard")
+
+
+C2_FIELDS = ("@timestamp", "response_time_ms")
+C2_AGGS = [AB.dateHistogram("per_hour").field("@timestamp").interval("1h").subAggregation(
+    AB.extendedStats("rt").field("response_time_ms"))]
+
+
+@pytest.fixture(scope="module")
+def c2_100m():
+    n = 100_000_000
+    cols = synthetic_columns(C2_FIELDS, n, shard=3)
+    want = O.run([(cols, n)], C2_AGGS)
+    return n, want
+
+
+@pytest.mark.parametrize("name", ["upload", "compact", "packed", "block"])
+def test_config2_100m_every_layout(engine, c2_100m, name):
+    """Config 2 (date_histogram{extended_stats}) on every layout: upload-width f64 runs
+    (16 B per doc), the 32-bit timestamp deltas with the metric's 16-bit deltas in integer runs (6 B), and block deltas
+    (4 B + the run words)."""
+    n, want = c2_100m
+    with layout(engine, name):
+        seg = engine.synthetic_segment(n, fields=C2_FIELDS, shard=3)
+        res, nbytes = _run(engine, seg, C2_AGGS)
+        seg.close()
+    expect = {"upload": 16 * n, "compact": 6 * n, "packed": 6 * n, "block": 4 * n + run_bytes(n)}[name]
+    assert nbytes == expect, (name, nbytes / n)
+    assert_same(res.to_dict(), want["shards"][0], f"{name} shard")
+    assert_same(reduce([res]).to_dict(), want["reduced"], f"{name} reduced")
+
+
+def _dense_ts(rng, n, t0, per_run_span):
+    """Sorted timestamps whose runs of 2,048 docs span about per_run_span ms."""
+    step = per_run_span / 2048.0
+    return (t0 + np.floor(np.arange(n) * step) + rng.integers(0, max(int(step), 1), size=n)).astype(np.int64)
+
+
+@pytest.mark.parametrize("t0,per_run,expect_block", [
+    (1_441_065_600_000, 30_000, True),      # dense logs
+    (-3_600_000 * 5, 30_000, True),          # before the epoch: negative keys and bases
+    (1_441_065_600_000, 66_000, False),      # some run spans >= 2^16 ms: the 32-bit deltas instead
+])
+def test_block_delta_keys(engine, t0, per_run, expect_block):
+    """Block-delta timestamps on every raw-load kernel that takes them -- packed cells (terms{date_histogram{stats}},
+    unfiltered and through a folded filter), integer runs (date_histogram{extended_stats}), counting grids
+    (date_histogram, terms{date_histogram}) -- over a ragged last run (n not a multiple of 2,048), against the oracle;
+    then the upload-width timestamps released and rebuilt from the block deltas (a calendar histogram reads them)."""
+    rng = np.random.default_rng(50 + per_run)
+    n = 2_000_000 + 777
+    cols = _log_segment(rng, n, 0, 1)
+    cols["@timestamp"]["values"] = _dense_ts(rng, n, t0, per_run)
+    cols["rt"]["values"] = rng.integers(0, 5000, size=n).astype(np.int64)
+    aggs = [AB.terms("h").field("host").size(6).subAggregation(
+                AB.dateHistogram("d").field("@timestamp").interval("1h").minDocCount(0).subAggregation(AB.stats("s").field("rt"))),
+            AB.dateHistogram("x").field("@timestamp").interval("1h").subAggregation(AB.extendedStats("e").field("rt")),
+            AB.dateHistogram("c").field("@timestamp").interval("5m"),
+            AB.terms("hc").field("host").size(4).subAggregation(AB.dateHistogram("d").field("@timestamp").interval("1h"))]
+    want = O.run([(cols, n)], aggs)
+    seg = engine.upload_segment(cols, n)
+    got = {}
+    for a in aggs:
+        r, nbytes = _run(engine, seg, [a])
+        got.update(r.to_dict())
+    assert_same(got, want["shards"][0], "block deltas")
+    # the key column's bytes: 2 B per doc + the run words on the block-delta layout, else 4 B
+    r, nbytes = _run(engine, seg, [aggs[2]])
+    assert nbytes == (2 * n + run_bytes(n) if expect_block else 4 * n), nbytes
+    accept = bits_from_mask(rng.random(n) >= 0.25)
+    fw = O.run([(cols, n)], aggs[:1], accept=[accept])
+    plan = engine.plan(aggs[:1])
+    plan.collect(seg, accept_bits=accept)
+    assert_same(plan.build().to_dict(), fw["shards"][0], "folded filter")
+    plan.close()
+    freed = seg.release_wide()
+    assert freed >= 8 * n
+    month = [AB.dateHistogram("m").field("@timestamp").interval("month").subAggregation(AB.stats("s").field("rt"))]
+    r, _ = _run(engine, seg, month)
+    assert_same(r.to_dict(), O.run([(cols, n)], month)["shards"][0], "rebuilt from block deltas")
+    seg.close()
 
 
 def _log_segment(rng, n, t0, span_ms, nterms=300, metric=None):
