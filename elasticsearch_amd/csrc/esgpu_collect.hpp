@@ -51,6 +51,9 @@ struct Doc4 {
     uint32_t raw[10];
     uint64_t racc;
     uint32_t doc0;
+    // block-delta kernels (VK bit 8192): the grid key every doc of this buffer's zone block has (its zone-map range
+    // rounds to one key; kNoUKey: per-doc keys) -- the block's timestamps were then not read (zone_ukey)
+    uint32_t ukey;
     uint32_t ord[kVec];
     int64_t hv[kVec];
     double mv[kVec];
@@ -151,13 +154,28 @@ __device__ __forceinline__ uint32_t eval_pred(const PredDev& q, uint32_t doc0) {
 // timestamp column): loads only, no use of a loaded word until unpack_docs
 template <int MET, int VK, bool HIST>
 constexpr bool kRawPI = MET > 0 && (VK & 64) != 0 && (VK & 16) != 0 && (VK & 256) != 0 && (!HIST || (VK & (32 | 8192)) != 0);
+#ifndef ESGPU_B16_SCALAR  // block-delta bases as scalar loads (1) or per-lane vector loads (0)
+#define ESGPU_B16_SCALAR 0
+#endif
 // VK bit 8192 (raw-load kernels only, instead of bit 32): the key column as block deltas -- 16 bits per doc over the
 // minimum of its run of 2^kB16Shift docs (one 8-byte word per run, the same for all 4 docs of a thread)
+constexpr uint32_t kNoUKey = 0xFFFFFFFFu, kOutUKey = 0xFFFFFFFEu;  // per-doc keys / one key outside the grid
 template <int VK>
-__device__ __forceinline__ void load_keys_raw(const CollectParams& P, uint32_t doc0, uint32_t (&raw)[10]) {
+__device__ __forceinline__ void load_keys_raw(const CollectParams& P, uint32_t doc0, uint32_t (&raw)[10], uint32_t uk) {
     if constexpr ((VK & 8192) != 0) {
-        const u32x2_t t = load8(P.hv16 + doc0), b = load8(P.hv16_base + (doc0 >> kB16Shift));
-        raw[2] = t.x; raw[3] = t.y; raw[4] = b.x; raw[5] = b.y;
+        // a block whose docs all round to one key reads no timestamp: every lane loads the column's first word (one
+        // cache line per wave, in place of a branch around the load -- a load under a branch makes the compiler wait
+        // for the other buffers' loads)
+        const u32x2_t t = load8(P.hv16 + (uk == kNoUKey ? doc0 : 0u));
+        raw[2] = t.x; raw[3] = t.y;
+#if ESGPU_B16_SCALAR
+        // a wave's 256 docs lie in one run: its base is a scalar load
+        const int64_t b = P.hv16_base[__builtin_amdgcn_readfirstlane(doc0 >> kB16Shift)];
+        raw[4] = (uint32_t)b; raw[5] = (uint32_t)((uint64_t)b >> 32);
+#else
+        const u32x2_t b = load8(P.hv16_base + (doc0 >> kB16Shift));
+        raw[4] = b.x; raw[5] = b.y;
+#endif
     } else {
         const u32x4_t t = load16(P.hv32 + doc0);
         raw[2] = t.x; raw[3] = t.y; raw[4] = t.z; raw[5] = t.w;
@@ -185,11 +203,12 @@ template <bool ORD, int MET, int VK>
 constexpr bool kIntRuns = !ORD && MET > 0 && (VK & 2048) != 0;
 
 template <bool ORD, bool HIST, int MET, int VK>
-__device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0, Doc4& d) {
+__device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0, Doc4& d, uint32_t uk = kNoUKey) {
+    d.ukey = uk;
     if constexpr (kRawPI<MET, VK, HIST>) {
         const u32x2_t o = load8(P.ord16 + doc0);
         d.raw[0] = o.x; d.raw[1] = o.y;
-        if constexpr (HIST) load_keys_raw<VK>(P, doc0, d.raw);
+        if constexpr (HIST) load_keys_raw<VK>(P, doc0, d.raw, uk);
         const u32x2_t m = load8(P.mv16 + doc0);
         d.raw[6] = m.x; d.raw[7] = m.y;
         if constexpr ((VK & 512) != 0) d.racc = P.accept[doc0 >> 6];
@@ -201,7 +220,7 @@ __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0,
             const u32x2_t o = load8(P.ord16 + doc0);
             d.raw[0] = o.x; d.raw[1] = o.y;
         }
-        if constexpr (HIST) load_keys_raw<VK>(P, doc0, d.raw);
+        if constexpr (HIST) load_keys_raw<VK>(P, doc0, d.raw, uk);
         if constexpr (MET > 0 && (VK & 2048) != 0) {
             const u32x2_t m = load8(P.mv16 + doc0);
             d.raw[6] = m.x; d.raw[7] = m.y;
@@ -556,6 +575,9 @@ __device__ __forceinline__ void runs_reset(Runs<NR>& R) {
 #ifndef ESGPU_PI_HOT
 #define ESGPU_PI_HOT 0
 #endif
+#ifndef ESGPU_PI_NOATOM
+#define ESGPU_PI_NOATOM 0
+#endif
 #ifndef ESGPU_PI_STRAIGHT  // packed cells: straight-line reads and adds (1), or under the hit mask (0, for A/B runs)
 #define ESGPU_PI_STRAIGHT 1
 #endif
@@ -736,7 +758,7 @@ __device__ __forceinline__ void unpack_docs(const CollectParams& P, Doc4& d) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) d.ord[j] = x[j] == 0xFFFFu ? kMissingOrd : x[j];
     if constexpr (HIST) {
-        unpack_keys_raw<VK>(P, d.raw, d.hv);
+        if ((VK & 8192) == 0 || d.ukey == kNoUKey) unpack_keys_raw<VK>(P, d.raw, d.hv);
         d.hpres = 0xFu;
     }
     d.mvd[0] = d.raw[6] & 0xFFFFu; d.mvd[1] = d.raw[6] >> 16; d.mvd[2] = d.raw[7] & 0xFFFFu; d.mvd[3] = d.raw[7] >> 16;
@@ -760,7 +782,7 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
             for (int j = 0; j < 4; ++j) du.ord[j] = x[j] == 0xFFFFu ? kMissingOrd : x[j];
         }
         if constexpr (HIST) {
-            unpack_keys_raw<VK>(P, du.raw, du.hv);
+            if ((VK & 8192) == 0 || du.ukey == kNoUKey) unpack_keys_raw<VK>(P, du.raw, du.hv);
             du.hpres = 0xFu;
         }
         if constexpr (MET > 0 && (VK & 2048) != 0) {  // integer runs: the 16-bit deltas as they are
@@ -775,8 +797,21 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
     const Doc4& d = kRawPI<MET, VK, HIST> || kRawH<ORD, MET, VK> ? du : d_in;
     uint32_t slot[kVec];
     bool hv_ok[kVec];
+    // block-delta kernels: a zone block whose docs all share one key takes it for every doc (wave-uniform branch)
+    const bool ublock = (VK & 8192) != 0 && HIST && d.ukey != kNoUKey;
+    if (ublock) {
+        const uint32_t k = d.ukey;  // grid key index, or kOutUKey (outside the grid: no doc counts)
+        const uint32_t sl = LDS ? k - win0 : k;
+        const bool in = k < P.H && (!LDS || sl < (mw ? mw : P.W));
+#pragma unroll
+        for (int j = 0; j < kVec; ++j) {
+            slot[j] = sl;
+            hv_ok[j] = in;
+        }
+    }
 #pragma unroll
     for (int j = 0; j < kVec; ++j) {
+        if (ublock) break;
         hv_ok[j] = true;
         slot[j] = 0;
         if (HIST && HORD) {  // ordinal keys: the slot is the ordinal (never windowed)
@@ -914,6 +949,12 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
         // queued behind them): every lane reads a (min, max) pair (a doc that hits nothing reads cell 0 and ignores it)
         // and adds to a cell (a miss adds 0 to the lane's own spare word)
         uint32_t mlo[kVec], mhi[kVec];
+#if ESGPU_PI_NOATOM  // diagnostic only (A/B builds; wrong results): no LDS cell traffic, the docs folded into registers
+#pragma unroll
+        for (int j = 0; j < kVec; ++j) run.hpk += ((hit >> j) & 1) ? one + d.mvd[j] + cell[j] : 0ull;
+        *a.pkd = run.hpk;
+        return;
+#endif
 #if ESGPU_PI_STRAIGHT
         if (MET >= 2) {
 #pragma unroll
@@ -1289,9 +1330,22 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
                          : (VK & 64) ? (ESGPU_NBUF_PI <= kItersPerBlockW ? ESGPU_NBUF_PI : kItersPerBlockW)
                          : ((VK & 176) ? (ESGPU_NBUF_COMPACT <= kItersPerBlockW ? ESGPU_NBUF_COMPACT : kItersPerBlockW) : 2);
     static_assert(kItersPerBlockW % kBuf == 0, "buffers per block");
+    // block-delta kernels: the zone block's key when all its docs share one (zone_keys ranges, two scalar loads per
+    // block and wave), the block's timestamps then left unread
+    auto zone_ukey = [&](uint32_t blk) -> uint32_t {
+        if constexpr ((VKL & 8192) == 0 || !HIST) {
+            return kNoUKey;
+        } else {
+            const uint32_t b = __builtin_amdgcn_readfirstlane(blk);
+            const int64_t kmn = P.zkey[2 * b], kmx = P.zkey[2 * b + 1];
+            if (kmn != kmx) return kNoUKey;
+            return kmn >= 0 && kmn < (int64_t)P.H ? (uint32_t)kmn : kOutUKey;
+        }
+    };
+    uint32_t pf_blk = b_begin, pf_uk = zone_ukey(b_begin);  // the block the prefetches read, and its key
     Doc4 q[kBuf];
 #pragma unroll
-    for (int k = 0; k < kBuf; ++k) load_docs<ORD, HIST, MET, VKL>(P, b_begin * kBlockDocs + k * kIterDocsW + tid4, q[k]);
+    for (int k = 0; k < kBuf; ++k) load_docs<ORD, HIST, MET, VKL>(P, b_begin * kBlockDocs + k * kIterDocsW + tid4, q[k], pf_uk);
 
     bool use_lds = P.lds_mode != 0;
     uint32_t cb = b_begin;                               // block being processed
@@ -1370,7 +1424,11 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
             else if (dyn && nb == ge) nb = nxt_c < P.n_chunks ? nxt_c * kGroup : cb;
             nb = min(nb, b_end - 1);
         }
-        load_docs<ORD, HIST, MET, VKL>(P, nb * kBlockDocs + nit * kIterDocsW + tid4, q);
+        if (nb != pf_blk) {
+            pf_blk = nb;
+            pf_uk = zone_ukey(nb);
+        }
+        load_docs<ORD, HIST, MET, VKL>(P, nb * kBlockDocs + nit * kIterDocsW + tid4, q, pf_uk);
     };
     while (cb < b_end) {
         for (uint32_t it = 0; it < (uint32_t)kItersPerBlockW; it += kBuf) {
@@ -1411,18 +1469,29 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
 // per-block key range [kmn, kmx] of a windowed collect (the zone maps mapped through the request's rounding once, so
 // the collect kernel's per-block window decisions are two scalar loads instead of two 64-bit divisions or table
 // searches per block); a block without values gets (1, 0)
+// udocs (optional): the docs of the blocks whose range rounds to one key, summed -- the block-delta kernels read no
+// timestamp of those blocks (zone_ukey), and the plan's byte count leaves them out
 template <bool KT>
-__global__ __launch_bounds__(256) void zone_keys_kernel(CollectParams P, int64_t* __restrict__ out) {
+__global__ __launch_bounds__(256) void zone_keys_kernel(CollectParams P, int64_t* __restrict__ out,
+                                                        unsigned long long* __restrict__ udocs) {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= P.n_blocks) return;
-    const int64_t zmn = P.zmin[b], zmx = P.zmax[b];
-    int64_t kmn = 1, kmx = 0;
-    if (zmn <= zmx) {
-        kmn = key_index<KT>(P, zmn);
-        kmx = key_index<KT>(P, zmx);
+    unsigned long long ud = 0;
+    if (b < P.n_blocks) {
+        const int64_t zmn = P.zmin[b], zmx = P.zmax[b];
+        int64_t kmn = 1, kmx = 0;
+        if (zmn <= zmx) {
+            kmn = key_index<KT>(P, zmn);
+            kmx = key_index<KT>(P, zmx);
+        }
+        out[2 * (size_t)b] = kmn;
+        out[2 * (size_t)b + 1] = kmx;
+        const uint64_t d0 = (uint64_t)b * kBlockDocs;
+        if (kmn == kmx && d0 < P.n_docs) ud = min((uint64_t)kBlockDocs, (uint64_t)P.n_docs - d0);
     }
-    out[2 * (size_t)b] = kmn;
-    out[2 * (size_t)b + 1] = kmx;
+    if (udocs) {
+        for (int o = 32; o > 0; o >>= 1) ud += __shfl_xor(ud, o, 64);
+        if ((threadIdx.x & 63) == 0 && ud) atomicAdd(udocs, ud);
+    }
 }
 
 // calls f(std::integral_constant<int, VK>) for the value kinds the plan uses; bits that cannot matter (no histogram

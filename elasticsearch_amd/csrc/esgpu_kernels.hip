@@ -92,11 +92,11 @@ void launch_synth(const SynthParams& p, hipStream_t stream) {
 
 namespace esgpu {
 
-void launch_zone_keys(const CollectParams& p, int64_t* out, hipStream_t st) {
+void launch_zone_keys(const CollectParams& p, int64_t* out, hipStream_t st, unsigned long long* udocs) {
     if (p.n_blocks == 0) return;
     const uint32_t g = (p.n_blocks + 255) / 256;
-    if (p.kstart) hipLaunchKernelGGL(zone_keys_kernel<true>, dim3(g), dim3(256), 0, st, p, out);
-    else hipLaunchKernelGGL(zone_keys_kernel<false>, dim3(g), dim3(256), 0, st, p, out);
+    if (p.kstart) hipLaunchKernelGGL(zone_keys_kernel<true>, dim3(g), dim3(256), 0, st, p, out, udocs);
+    else hipLaunchKernelGGL(zone_keys_kernel<false>, dim3(g), dim3(256), 0, st, p, out, udocs);
 }
 
 // the collect kernels are instantiated in esgpu_collect_inst.hip, compiled once per (ORD, HK) so the variants build

@@ -91,7 +91,7 @@ struct CollectParams {
     uint32_t nsteps;
     const int64_t* zmin;
     const int64_t* zmax;
-    const int64_t* zkey;             // windowed collects: per-block key range [kmn, kmx] (launch_zone_keys)
+    const int64_t* zkey;             // windowed / block-delta collects: per-block key range [kmn, kmx] (launch_zone_keys)
     int32_t hord;                    // the key dimension is a second terms aggregation: hv holds u32 ordinals, H of them
     uint32_t mg_m, mg_s1, mg_s2;
     int32_t fast32;
@@ -312,7 +312,7 @@ void launch_synth(const SynthParams& p, hipStream_t s);
 // wide: 1024-thread workgroups (histogram grids whose LDS window exceeds the two-per-CU budget), else 512
 void launch_collect(const CollectParams& p, bool ord, bool hist, int met, bool wide, uint32_t grid, size_t lds, hipStream_t s);
 // per-block key ranges of the zone maps under the request's rounding (out: 2 x n_blocks)
-void launch_zone_keys(const CollectParams& p, int64_t* out, hipStream_t s);
+void launch_zone_keys(const CollectParams& p, int64_t* out, hipStream_t s, unsigned long long* udocs = nullptr);
 // pi: packed integer metric cells (CollectParams.pk_shift): 8 B per cell copy + an 8 B (min, max) pair per cell
 size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode, uint32_t ncopies = 1, bool pi = false);
 // resident workgroups per CU (hk: 0 none, 1 affine, 2 table; vk: bit 0 double histogram column, bit 1 double metric)

@@ -1087,6 +1087,11 @@ struct esgpu_plan {
     Scratch s_fbits, s_vbits;  // doc bitset of multi-valued filters, per-value bitset of a multi-valued HLL field
     Scratch s_cells;           // cell list of a cardinality gather
     Scratch s_zkey;            // per-block key ranges of a windowed collect
+    // block-delta collects: the docs of zone blocks whose timestamps the kernel did not read (one key per block), one
+    // device word per launch of the current collect call, copied into zu_host; taken off last_bytes by the stats call
+    Scratch s_zu;
+    PinnedBuf zu_host;
+    uint32_t zu_n = 0;
     DevBuf d_claim;            // collect kernel's chunk-claim counter pair (zeroed once; every launch leaves it zero)
     Scratch s_hcur, s_hused, s_hslab;  // hot/cold counting: overflow cursors, static-region fills, hot slabs
     PinnedBuf h_hcerr;         // hot/cold counting: capacity-violation word (written by the scatter kernel)
@@ -3174,10 +3179,21 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         P.claim = (unsigned int*)p->d_claim.p;
         grid = slots;
     }
-    if (P.lds_mode && P.windowed) {
+    if ((P.lds_mode && P.windowed) || P.hv16) {  // (block-delta kernels read the timestamps of multi-key blocks only)
         P.zkey = (const int64_t*)p->s_zkey.ensure(p->ctx, (size_t)std::max(P.n_blocks, 1u) * 16);
-        launch_zone_keys(P, const_cast<int64_t*>(P.zkey), p->stream);
+        unsigned long long* ud = nullptr;
+        constexpr uint32_t kZuSlots = 64;
+        if (P.hv16 && p->zu_n < kZuSlots) {
+            ud = (unsigned long long*)p->s_zu.ensure(p->ctx, kZuSlots * 8) + p->zu_n;
+            HIPX(hipMemsetAsync(ud, 0, 8, p->stream));
+        }
+        launch_zone_keys(P, const_cast<int64_t*>(P.zkey), p->stream, ud);
         HIPX(hipGetLastError());
+        if (ud) {
+            uint64_t* h = (uint64_t*)p->zu_host.ensure(kZuSlots * 8);
+            HIPX(hipMemcpyAsync(h + p->zu_n, ud, 8, hipMemcpyDeviceToHost, p->stream));
+            ++p->zu_n;
+        }
     }
     need_wide(false);
     HIPX(hipEventRecord(pl.e0, p->stream));
@@ -3593,6 +3609,7 @@ extern "C" int esgpu_plan_collect_segment(esgpu_plan* p, const esgpu_segment* s,
         }
         p->last_bytes = 0;
         p->last_ms = -1;
+        p->zu_n = 0;
         bool deferred = false;
         for (Pipeline& pl : p->pipes) {
             if (pl.replay) { pl.timed = false; continue; }
@@ -3651,6 +3668,13 @@ extern "C" int esgpu_plan_last_collect_stats(const esgpu_plan* cp, double* kerne
                 total += ms;
             }
             p->last_ms = total;
+            if (p->zu_n) {  // the timestamps of single-key zone blocks were not read
+                HIPX(hipStreamSynchronize(p->stream));
+                uint64_t ud = 0;
+                for (uint32_t i = 0; i < p->zu_n; ++i) ud += ((const uint64_t*)p->zu_host.p)[i];
+                p->last_bytes -= std::min<uint64_t>(p->last_bytes, 2 * ud);
+                p->zu_n = 0;
+            }
         }
         if (kernel_ms) *kernel_ms = p->last_ms;
         if (bytes) *bytes = p->last_bytes;

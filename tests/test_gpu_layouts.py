@@ -50,6 +50,17 @@ def run_bytes(n):
     return (n + 2047) // 2048 * 8
 
 
+def check_bytes(name, nbytes, bpd, n):
+    """The bytes the plan reports for its layout.  Block deltas: bpd B per doc and the run words, less the 2 B
+    timestamps of the zone blocks whose docs all round to one key (not read): at 100M docs over 30 days a block spans
+    ~212 s, so ~94 % of the blocks hold one hour."""
+    if name != "block":
+        assert nbytes == bpd * n, (name, nbytes / n)
+        return
+    full = bpd * n + run_bytes(n)
+    assert full - 2 * n <= nbytes < full - n, (name, nbytes / n)
+
+
 def _run(engine, seg, aggs, filters=None, number_of_shards=1, segs=None):
     plan = engine.plan(aggs, filters=filters, number_of_shards=number_of_shards)
     nbytes = 0
@@ -93,7 +104,7 @@ def test_north_star_100m_every_layout(engine, ns_100m, name, bpd):
         seg = engine.synthetic_segment(n, fields=NS_FIELDS)  # a fresh segment: its compact copies are built by this layout
         res, nbytes = _run(engine, seg, NS_AGGS)
         seg.close()
-    assert nbytes == bpd * n + (run_bytes(n) if name == "block" else 0), (name, nbytes / n)
+    check_bytes(name, nbytes, bpd, n)
     assert_same(res.to_dict(), want["shards"][0], f"{name} shard")
     assert_same(reduce([res]).to_dict(), want["reduced"], f"{name} reduced")
 
@@ -105,7 +116,7 @@ def test_config5_100m_every_layout(engine, c5_100m, name, bpd):
         seg = engine.synthetic_segment(n, fields=C5_FIELDS, shard=2)
         res, nbytes = _run(engine, seg, C5_AGGS, filters=C5_FILTERS, number_of_shards=8)
         seg.close()
-    assert nbytes == bpd * n + (run_bytes(n) if name == "block" else 0), (name, nbytes / n)
+    check_bytes(name, nbytes, bpd, n)
     assert_same(res.to_dict(), want["shards"][0], f"{name} shard")
 
 
@@ -132,8 +143,7 @@ def test_config2_100m_every_layout(engine, c2_100m, name):
         seg = engine.synthetic_segment(n, fields=C2_FIELDS, shard=3)
         res, nbytes = _run(engine, seg, C2_AGGS)
         seg.close()
-    expect = {"upload": 16 * n, "compact": 6 * n, "packed": 6 * n, "block": 4 * n + run_bytes(n)}[name]
-    assert nbytes == expect, (name, nbytes / n)
+    check_bytes(name, nbytes, {"upload": 16, "compact": 6, "packed": 6, "block": 4}[name], n)
     assert_same(res.to_dict(), want["shards"][0], f"{name} shard")
     assert_same(reduce([res]).to_dict(), want["reduced"], f"{name} reduced")
 
@@ -171,9 +181,13 @@ def test_block_delta_keys(engine, t0, per_run, expect_block):
         r, nbytes = _run(engine, seg, [a])
         got.update(r.to_dict())
     assert_same(got, want["shards"][0], "block deltas")
-    # the key column's bytes: 2 B per doc + the run words on the block-delta layout, else 4 B
+    # the key column's bytes: 2 B per doc + the run words on the block-delta layout (less the single-key zone blocks'
+    # timestamps: a block spans ~120 s here, 60 % of them within one 5-minute key), else 4 B
     r, nbytes = _run(engine, seg, [aggs[2]])
-    assert nbytes == (2 * n + run_bytes(n) if expect_block else 4 * n), nbytes
+    if expect_block:
+        assert run_bytes(n) + 0.4 * n < nbytes < run_bytes(n) + 1.2 * n, nbytes / n
+    else:
+        assert nbytes == 4 * n, nbytes
     accept = bits_from_mask(rng.random(n) >= 0.25)
     fw = O.run([(cols, n)], aggs[:1], accept=[accept])
     plan = engine.plan(aggs[:1])
