@@ -44,6 +44,9 @@ constexpr uint32_t kGroup = kGroupBlocks;  // blocks per multi-pass group (esgpu
 #ifndef ESGPU_NBUF_PI  // load buffers with packed integer metric cells (all columns compact)
 #define ESGPU_NBUF_PI 2
 #endif
+#ifndef ESGPU_NBUF_PI_RAW  // ... the unfiltered raw-load packed-cell kernels (north star 1.39 -> 1.34 ms at 1B, r5ab2; the
+#define ESGPU_NBUF_PI_RAW 4  // folded-accept ones spill at 4)
+#endif
 
 struct Doc4 {
     // raw-loaded packed-cell kernels (kRawPI): the loads' words as they arrive, unpacked only when the docs are processed
@@ -575,6 +578,10 @@ __device__ __forceinline__ void runs_reset(Runs<NR>& R) {
 #ifndef ESGPU_PI_HOT
 #define ESGPU_PI_HOT 0
 #endif
+#ifndef ESGPU_PI_MMCHECK  // packed cells: (min, max) pairs read first, atomics only where they change -- 2: one divergent
+                          // region per doc (NS 1.324 -> 1.29 ms, r5ab3), 1: one per bound, 0: unconditional (1.9x slower)
+#define ESGPU_PI_MMCHECK 2
+#endif
 #ifndef ESGPU_PI_NOATOM
 #define ESGPU_PI_NOATOM 0
 #endif
@@ -987,12 +994,32 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
             if ((hit >> j) & 1) atomicAdd(&a.pk[cell[j] + a.coff], one + d.mvd[j]);
 #endif
         if (MET >= 2) {
+#if ESGPU_PI_MMCHECK == 2
+            // one divergent region per doc: both atomics where either bound moves (the other is then a no-op)
+#pragma unroll
+            for (int j = 0; j < kVec; ++j) {
+                const bool mv = ((hit >> j) & 1) && (d.mvd[j] < mlo[j] || d.mvd[j] > mhi[j]);
+                if (mv) {
+                    atomicMin(&a.mm[2 * cell[j]], d.mvd[j]);
+                    atomicMax(&a.mm[2 * cell[j] + 1], d.mvd[j]);
+                }
+            }
+#elif ESGPU_PI_MMCHECK
 #pragma unroll
             for (int j = 0; j < kVec; ++j) {
                 if (!((hit >> j) & 1)) continue;
                 if (d.mvd[j] < mlo[j]) atomicMin(&a.mm[2 * cell[j]], d.mvd[j]);
                 if (d.mvd[j] > mhi[j]) atomicMax(&a.mm[2 * cell[j] + 1], d.mvd[j]);
             }
+#else  // (A/B) unconditional min / max atomics, a miss on the lane's spare word: no branches
+#pragma unroll
+            for (int j = 0; j < kVec; ++j) {
+                const bool h = (hit >> j) & 1;
+                uint32_t* w = h ? &a.mm[2 * cell[j]] : reinterpret_cast<uint32_t*>(a.pkd);
+                atomicMin(w, h ? d.mvd[j] : ~0u);
+                atomicMax(w + 1, h ? d.mvd[j] : 0u);
+            }
+#endif
         }
         return;
     }
@@ -1327,6 +1354,8 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
     constexpr int kBuf = (kRawH<ORD, MET, VK> && !ORD && MET == 0) ? (ESGPU_NBUF_HIST <= kItersPerBlockW ? ESGPU_NBUF_HIST : kItersPerBlockW)
                          : (kRawH<ORD, MET, VK> && !ORD) ? (ESGPU_NBUF_HIST_MET <= kItersPerBlockW ? ESGPU_NBUF_HIST_MET : kItersPerBlockW)
                          : (MET == 0 && !(ORD && HIST)) ? ESGPU_NBUF_NARROW
+                         : ((VK & 64) && kRawPI<MET, VK, HIST> && !(VK & 512))
+                             ? (ESGPU_NBUF_PI_RAW <= kItersPerBlockW ? ESGPU_NBUF_PI_RAW : kItersPerBlockW)
                          : (VK & 64) ? (ESGPU_NBUF_PI <= kItersPerBlockW ? ESGPU_NBUF_PI : kItersPerBlockW)
                          : ((VK & 176) ? (ESGPU_NBUF_COMPACT <= kItersPerBlockW ? ESGPU_NBUF_COMPACT : kItersPerBlockW) : 2);
     static_assert(kItersPerBlockW % kBuf == 0, "buffers per block");
