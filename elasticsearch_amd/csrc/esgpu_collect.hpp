@@ -761,9 +761,9 @@ __device__ __forceinline__ void unpack_docs(const CollectParams& P, Doc4& d) {
     uint32_t ok = doc0 + 4 <= P.n_docs ? 0xFu : doc0 >= P.n_docs ? 0u : ((1u << (P.n_docs - doc0)) - 1u);
     if constexpr ((VK & 512) != 0) ok &= (uint32_t)(d.racc >> (doc0 & 63)) & 0xFu;
     d.ok = ok;
-    const uint32_t x[4] = {d.raw[0] & 0xFFFFu, d.raw[0] >> 16, d.raw[1] & 0xFFFFu, d.raw[1] >> 16};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) d.ord[j] = x[j] == 0xFFFFu ? kMissingOrd : x[j];
+    // a missing ordinal stays 0xFFFF: the packed-cell path tests t < T, and a 16-bit ordinal column exists only while T
+    // is below 0xFFFF
+    d.ord[0] = d.raw[0] & 0xFFFFu; d.ord[1] = d.raw[0] >> 16; d.ord[2] = d.raw[1] & 0xFFFFu; d.ord[3] = d.raw[1] >> 16;
     if constexpr (HIST) {
         if ((VK & 8192) == 0 || d.ukey == kNoUKey) unpack_keys_raw<VK>(P, d.raw, d.hv);
         d.hpres = 0xFu;
@@ -928,14 +928,21 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
 #pragma unroll
         for (int j = 0; j < kVec; ++j) {
             const uint32_t t = d.ord[j];
-            const bool ok = (d.ok >> j) & 1, has_t = t != kMissingOrd && t < T;
-            if (P.ocnt_mode == OCNT_TERMS) {
-                if (ok && has_t && outer) atomicAdd(&a.ocnt32[t], 1u);
-            } else if (P.ocnt_mode == OCNT_HIST) {
-                if (ok && hv_ok[j]) atomicAdd(&a.ocnt32[slot[j]], 1u);
-            }
+            const bool ok = (d.ok >> j) & 1, has_t = t < T;  // (kMissingOrd, and a raw 16-bit 0xFFFF, are >= T)
             hit |= (uint32_t)(ok && hv_ok[j] && has_t) << j;
             cell[j] = slot[j] * T + t;
+        }
+        // separate outer counts: one wave-uniform branch per 4 docs (inside the doc loop the compiler kept each doc's
+        // masked atomic and its exec bookkeeping even when the mode counts nothing: ~10 scalar instructions per doc)
+        if (P.ocnt_mode == OCNT_TERMS) {
+            if (outer)
+#pragma unroll
+                for (int j = 0; j < kVec; ++j)
+                    if (((d.ok >> j) & 1) && d.ord[j] < T) atomicAdd(&a.ocnt32[d.ord[j]], 1u);
+        } else if (P.ocnt_mode == OCNT_HIST) {
+#pragma unroll
+            for (int j = 0; j < kVec; ++j)
+                if (((d.ok >> j) & 1) && hv_ok[j]) atomicAdd(&a.ocnt32[slot[j]], 1u);
         }
         const unsigned long long one = 1ull << P.pk_shift;
 #if ESGPU_PI_HOT
@@ -974,7 +981,7 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
 #pragma unroll
         for (int j = 0; j < kVec; ++j) {
             const bool h = (hit >> j) & 1;
-            atomicAdd(h ? &a.pk[cell[j] + a.coff] : a.pkd, h ? one + d.mvd[j] : 0ull);
+            atomicAdd(h ? &a.pk[cell[j] + a.coff] : a.pkd, one + d.mvd[j]);  // (a miss: into the lane's spare word)
         }
 #else  // (A/B) reads and adds under the hit mask: the compiler then waits for every queued LDS op before the checks
         if (MET >= 2) {

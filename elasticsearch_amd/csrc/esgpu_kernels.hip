@@ -2710,22 +2710,33 @@ void launch_comp_ords(const uint32_t* a, const uint32_t* b, uint32_t n_pad, uint
                        na, nb, amap, amap_n, out);
 }
 
-// one 8192-doc block per workgroup: each doc's batch and replay ordinal, a position inside the workgroup's share of
-// its batch (the wave's lanes of one batch take consecutive positions with one LDS atomic: the Zipf-head winners put
-// most of a wave in one batch), one global reservation per (workgroup, batch), then the appends
+// one 8192-doc block per workgroup: each doc's batch and replay ordinal (the slot map carries the batch, no per-doc
+// division), then the appends.  Up to kReplayFastBatches batches: the block's appends are sorted by batch in LDS -- a
+// thread's per-batch counts packed as 16-bit fields of two u64 words, one wave scan of each, the waves' totals combined
+// per batch -- and leave as one contiguous, coalesced run per batch after one global reservation per (workgroup, batch)
+// on its own cache line.  More batches: a position per wave round of each distinct batch, scattered appends.
 constexpr uint32_t kReplayFastBatches = 8;
-__global__ __launch_bounds__(kWG) void replay_compact_kernel(ReplayCompactParams P) {
-    __shared__ uint32_t cnt[kReplayMaxBatches], base[kReplayMaxBatches];
-    for (uint32_t i = threadIdx.x; i < P.nbatch; i += kWG) cnt[i] = 0;
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t lt = (1ull << lane) - 1ull;
-    uint32_t val[kItersPerBlock][4], bid[kItersPerBlock][4], pos[kItersPerBlock][4];
+#ifndef ESGPU_RC_EXP  // timing experiments only (wrong results): 1 = no appends, 2 = no global reservations, 3 = loads alone
+#define ESGPU_RC_EXP 0
+#endif
+// the block's docs (16 per thread): each one's batch and replay ordinal (the slot map carries the batch: no per-doc
+// division); bid = kMissingOrd when the doc does not survive
+constexpr uint32_t kReplayLdsMap = 4096;  // outer ordinals whose slot map the sort kernel stages in LDS (16 KB)
+__device__ __forceinline__ void replay_classify(const ReplayCompactParams& P, const uint32_t* __restrict__ smap,
+                                                uint32_t (&val)[kItersPerBlock][4], uint32_t (&bid)[kItersPerBlock][4]) {
+    constexpr uint32_t kRMask = (1u << kReplayBatchShift) - 1u;
 #pragma unroll
     for (int it = 0; it < kItersPerBlock; ++it) {
         const uint32_t doc0 = blockIdx.x * kBlockDocs + it * kIterDocs + threadIdx.x * kVec;
         uint32_t x[4], y[4];
-        load_u32x4(P.a, doc0, x);
+        if (P.a16) {
+            const u32x2_t w = load8(P.a16 + doc0);
+            const uint32_t h[4] = {w.x & 0xFFFFu, w.x >> 16, w.y & 0xFFFFu, w.y >> 16};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x[j] = h[j] == 0xFFFFu ? kMissingOrd : h[j];
+        } else {
+            load_u32x4(P.a, doc0, x);
+        }
         load_u32x4(P.b, doc0, y);
         uint32_t ok = 0xF;
         if (doc0 + 4 > P.n_docs) ok = doc0 >= P.n_docs ? 0u : ((1u << (P.n_docs - doc0)) - 1u);
@@ -2733,52 +2744,140 @@ __global__ __launch_bounds__(kWG) void replay_compact_kernel(ReplayCompactParams
         for (int k = 0; k < P.npred; ++k) ok &= eval_pred(P.pred[k], doc0);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint32_t w = ((ok >> j) & 1) && x[j] < P.slot_map_n ? P.slot_map[x[j]] : kMissingOrd;
-            const bool live = w != kMissingOrd && y[j] < P.vcB;
-            bid[it][j] = live ? w / P.wb : kMissingOrd;
-            val[it][j] = live ? (w % P.wb) * P.stride + y[j] : 0u;
+            const uint32_t m = ((ok >> j) & 1) && x[j] < P.slot_map_n ? smap[x[j]] : kMissingOrd;
+            const bool live = m != kMissingOrd && y[j] < P.vcB;
+            bid[it][j] = live ? m >> kReplayBatchShift : kMissingOrd;
+            val[it][j] = live ? (m & kRMask) * P.stride + y[j] : 0u;
         }
     }
-    if (P.nbatch <= kReplayFastBatches) {
-        // few batches (the usual case: a handful of batches of winners): per batch, the lane's docs as a 16-bit mask, a
-        // wave scan of their counts and one returning LDS atomic per wave -- every batch's atomic issued before the
-        // first wait, so no round trip sits in a dependent chain per doc
-        uint32_t mb[kReplayFastBatches], wpre[kReplayFastBatches], wtot[kReplayFastBatches], wb[kReplayFastBatches];
+}
+
+// up to kReplayFastBatches batches (the usual case): the block's appends are sorted by batch in LDS -- a thread's
+// per-batch counts packed as 16-bit fields of two u64 words, one wave scan of each, the waves' totals combined per
+// batch by one thread each -- and leave as one contiguous, coalesced run per batch after one global reservation per
+// (workgroup, batch) on its own cache line.  A doc's batch is kept in 4 bits and its rank among the thread's docs of
+// that batch recounted when it is staged, so the kernel holds few registers (a block's 16 docs per thread).
+__global__ __launch_bounds__(kWG, 2) void replay_compact_sort_kernel(ReplayCompactParams P) {
+    __shared__ uint32_t stage[kBlockDocs];                       // the block's appends, batch by batch
+    __shared__ uint32_t wtot[kWG / 64][kReplayFastBatches];      // per wave and batch: appends
+    __shared__ uint32_t wpos[kWG / 64][kReplayFastBatches];      // ... and their first staging position
+    __shared__ uint32_t boff[kReplayFastBatches + 1], glim[kReplayFastBatches];
+    __shared__ unsigned long long gdst[kReplayFastBatches];
+    // the slot map in LDS when it is small (the outer terms of a breadth-first request: hosts, statuses): 16 gathers per
+    // thread from a global table queue on the texture unit, tens of cycles per wave each
+    __shared__ uint32_t lmap[kReplayLdsMap];
+    const uint32_t* smap = P.slot_map;
+    if (P.slot_map_n <= kReplayLdsMap) {
+        for (uint32_t i = threadIdx.x; i < P.slot_map_n; i += kWG) lmap[i] = P.slot_map[i];
+        __syncthreads();
+        smap = lmap;
+    }
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t val[kItersPerBlock][4];
+    unsigned long long bits = 0;  // doc k's batch in bits 4k..4k+3 (15: none)
+    unsigned long long c[2] = {0ull, 0ull};
+    {
+        uint32_t bid[kItersPerBlock][4];
+        replay_classify(P, smap, val, bid);
+#if ESGPU_RC_EXP == 3
+        uint32_t acc = 0;
 #pragma unroll
-        for (uint32_t b = 0; b < kReplayFastBatches; ++b) {
-            uint32_t m = 0;
+        for (int it = 0; it < kItersPerBlock; ++it)
 #pragma unroll
-            for (int it = 0; it < kItersPerBlock; ++it)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) m |= (uint32_t)(bid[it][j] == b) << (it * 4 + j);
-            mb[b] = m;
-            const uint32_t c = (uint32_t)__popc(m);
-            uint32_t incl = c;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const uint32_t y = __shfl_up(incl, off, 64);
-                if ((int)lane >= off) incl += y;
-            }
-            wtot[b] = __shfl(incl, 63, 64);
-            wpre[b] = incl - c;
-        }
-#pragma unroll
-        for (uint32_t b = 0; b < kReplayFastBatches; ++b)
-            wb[b] = (lane == 0 && b < P.nbatch && wtot[b]) ? atomicAdd(&cnt[b], wtot[b]) : 0u;
-#pragma unroll
-        for (uint32_t b = 0; b < kReplayFastBatches; ++b) wb[b] = __shfl(wb[b], 0, 64) + wpre[b];
+            for (int j = 0; j < 4; ++j) acc += val[it][j] + bid[it][j];
+        if (acc == 0x12345u) *P.overflow = acc;
+        return;
+#endif
 #pragma unroll
         for (int it = 0; it < kItersPerBlock; ++it)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const uint32_t k = it * 4 + j;
-                uint32_t p = 0;
-#pragma unroll
-                for (uint32_t b = 0; b < kReplayFastBatches; ++b)
-                    if (bid[it][j] == b) p = wb[b] + (uint32_t)__popc(mb[b] & ((1u << k) - 1u));
-                pos[it][j] = p;
+                const uint32_t b = bid[it][j] < kReplayFastBatches ? bid[it][j] : 15u;
+                bits |= (unsigned long long)b << (4 * (it * 4 + j));
+                const unsigned long long one = b < kReplayFastBatches ? 1ull << (16u * (b & 3u)) : 0ull;
+                if (b < 4u) c[0] += one; else c[1] += one;
             }
-    } else {
+    }
+    // wave exclusive scan of both words (a wave holds at most 1,024 docs of a batch: no field overflows)
+    unsigned long long e[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        unsigned long long incl = c[h];
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const unsigned long long t = __shfl_up(incl, off, 64);
+            if ((int)lane >= off) incl += t;
+        }
+        e[h] = incl - c[h];
+        if (lane == 63)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) wtot[wave][4 * h + q] = (uint32_t)(incl >> (16 * q)) & 0xFFFFu;
+    }
+    __syncthreads();
+    if (threadIdx.x < kReplayFastBatches) {
+        // thread b: batch b's start in the staging array (the totals of the batches before it) and each wave's start
+        // inside the batch, the batch's global reservation
+        const uint32_t b = threadIdx.x;
+        uint32_t before = 0, t = 0;
+#pragma unroll 1
+        for (int w = 0; w < kWG / 64; ++w) {  // (rolled: 64 LDS words in flight would hold 64 registers)
+            wpos[w][b] = t;  // the wave's start inside the batch, made absolute below
+#pragma unroll
+            for (uint32_t q = 0; q < kReplayFastBatches; ++q) {
+                const uint32_t x = wtot[w][q];
+                before += q < b ? x : 0u;
+                t += q == b ? x : 0u;
+            }
+        }
+#if ESGPU_RC_EXP == 2
+        const uint32_t g = blockIdx.x * 2048u;
+#else
+        const uint32_t g = b < P.nbatch && t ? atomicAdd(&P.fill[(size_t)b * kReplayFillStride], t) : 0u;
+#endif
+        const uint32_t cap = b < P.nbatch ? P.cap[b] : 0u;
+        gdst[b] = (b < P.nbatch ? P.region[b] : 0ull) + g;  // where the batch's run goes, and how much of it fits
+        glim[b] = cap > g ? cap - g : 0u;
+        boff[b] = before;
+        if (b == kReplayFastBatches - 1) boff[kReplayFastBatches] = before + t;
+#pragma unroll
+        for (int w = 0; w < kWG / 64; ++w) wpos[w][b] += before;
+    }
+    __syncthreads();
+    // stage: the thread's docs in order, each at its wave's start + the lanes before it + its rank among the thread's
+    // docs of its batch (the running count, rebuilt)
+    unsigned long long r[2] = {e[0], e[1]};
+#pragma unroll
+    for (int k = 0; k < kItersPerBlock * 4; ++k) {
+        const uint32_t b = (uint32_t)(bits >> (4 * k)) & 15u;
+        if (b >= kReplayFastBatches) continue;
+        const unsigned long long rh = b < 4u ? r[0] : r[1];
+        const uint32_t sh = 16u * (b & 3u);
+        stage[wpos[wave][b] + ((uint32_t)(rh >> sh) & 0xFFFFu)] = val[k / 4][k % 4];
+        if (b < 4u) r[0] += 1ull << sh; else r[1] += 1ull << sh;
+    }
+    __syncthreads();
+    const uint32_t total = ESGPU_RC_EXP == 1 ? 0u : boff[kReplayFastBatches];
+    if (ESGPU_RC_EXP == 1 && threadIdx.x == 0 && stage[boff[1]] == 0x12345u) *P.overflow = 1u;
+    for (uint32_t i = threadIdx.x; i < total; i += kWG) {
+        uint32_t b = 0;
+#pragma unroll
+        for (uint32_t q = 1; q < kReplayFastBatches; ++q) b += i >= boff[q] ? 1u : 0u;
+        const uint32_t k = i - boff[b];
+        if (k < glim[b]) P.out[gdst[b] + k] = stage[i];
+        else *P.overflow = 1u;
+    }
+}
+
+// more batches: a position per wave round of each distinct batch, scattered appends
+__global__ __launch_bounds__(kWG) void replay_compact_kernel(ReplayCompactParams P) {
+    __shared__ uint32_t cnt[kReplayMaxBatches], base[kReplayMaxBatches];
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t val[kItersPerBlock][4], bid[kItersPerBlock][4];
+    replay_classify(P, P.slot_map, val, bid);
+    for (uint32_t i = threadIdx.x; i < P.nbatch; i += kWG) cnt[i] = 0;
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t pos[kItersPerBlock][4];
 #pragma unroll
     for (int it = 0; it < kItersPerBlock; ++it)
 #pragma unroll
@@ -2798,9 +2897,9 @@ __global__ __launch_bounds__(kWG) void replay_compact_kernel(ReplayCompactParams
             }
             pos[it][j] = p;
         }
-    }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < P.nbatch; i += kWG) base[i] = cnt[i] ? atomicAdd(&P.fill[i], cnt[i]) : 0u;
+    for (uint32_t i = threadIdx.x; i < P.nbatch; i += kWG)
+        base[i] = cnt[i] ? atomicAdd(&P.fill[(size_t)i * kReplayFillStride], cnt[i]) : 0u;
     __syncthreads();
 #pragma unroll
     for (int it = 0; it < kItersPerBlock; ++it)
@@ -2815,7 +2914,9 @@ __global__ __launch_bounds__(kWG) void replay_compact_kernel(ReplayCompactParams
 }
 void launch_replay_compact(const ReplayCompactParams& p, hipStream_t st) {
     const uint32_t blocks = (p.n_docs + kBlockDocs - 1) / kBlockDocs;
-    if (blocks) hipLaunchKernelGGL(replay_compact_kernel, dim3(blocks), dim3(kWG), 0, st, p);
+    if (!blocks) return;
+    if (p.nbatch <= kReplayFastBatches) hipLaunchKernelGGL(replay_compact_sort_kernel, dim3(blocks), dim3(kWG), 0, st, p);
+    else hipLaunchKernelGGL(replay_compact_kernel, dim3(blocks), dim3(kWG), 0, st, p);
 }
 
 void launch_minmax_i64(const int64_t* v, uint64_t n, int64_t* out, bool f64, hipStream_t st) {

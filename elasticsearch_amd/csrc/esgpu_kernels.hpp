@@ -379,8 +379,11 @@ void launch_delta32(const int64_t* v, uint32_t n, int64_t base, uint32_t* out, h
 struct ReplayCompactParams {
     uint32_t n_docs;
     const uint32_t* a;           // outer (global) ordinals
+    const uint16_t* a16;         // ... or their 16-bit copy (0xFFFF missing; null: read a)
     const uint32_t* b;           // inner (global) ordinals
-    const uint32_t* slot_map;    // outer ordinal -> winner index (kMissingOrd: the bucket did not survive)
+    // outer ordinal -> its winner's batch << kReplayBatchShift | index in the batch (kMissingOrd: the bucket did not
+    // survive) -- the per-doc batch arithmetic done once per ordinal on the host
+    const uint32_t* slot_map;
     uint32_t slot_map_n;
     uint32_t vcB;                // inner ordinals (b >= vcB: missing)
     uint32_t wb, stride, nbatch;
@@ -390,10 +393,11 @@ struct ReplayCompactParams {
     uint32_t* out;
     const uint64_t* region;      // [nbatch] first element of each batch's region in out
     const uint32_t* cap;         // [nbatch] its capacity (elements)
-    uint32_t* fill;              // [nbatch] elements appended so far (zeroed before the first segment)
+    uint32_t* fill;              // [nbatch] elements appended so far, kReplayFillStride words apart (zeroed before the
+                                 // first segment; one cache line each: the workgroups' reservations do not queue on one)
     uint32_t* overflow;          // set to 1 when an append did not fit
 };
-constexpr uint32_t kReplayMaxBatches = 1024;
+constexpr uint32_t kReplayMaxBatches = 1024, kReplayBatchShift = 20, kReplayFillStride = 64;
 void launch_replay_compact(const ReplayCompactParams& p, hipStream_t s);
 void launch_comp_ords(const uint32_t* a, const uint32_t* b, uint32_t n_pad, uint32_t na, uint32_t nb, const uint32_t* amap,
                       uint32_t amap_n, uint32_t* out, hipStream_t st);

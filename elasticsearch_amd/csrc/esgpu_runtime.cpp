@@ -1117,6 +1117,7 @@ struct esgpu_plan {
     Scratch s_rkeys;                   // replay: per winner, the GPU top-k's keys and row total
     PinnedBuf h_rkeys;
     Scratch s_rregion, s_rmeta;        // compacted replay: the batches' regions; region offsets, capacities, fills
+    Scratch s_rkeys2;                  // replay rows selected batch by batch (term orders, large shard sizes)
     PinnedBuf h_rfill, h_rcand;        // compacted replay fills; large inner top-k: row sum + candidates
     void unpin_all() {
         for (const DeferredSeg& d : dsegs) unpin_segment(d.s);
@@ -4309,7 +4310,7 @@ static bool replay_compact(esgpu_plan* p, const ChildSrc& kid, const std::vector
     Pipeline& R0 = p->pipes[kid.rpipes[0]];
     const uint32_t k = (uint32_t)top.size();
     const uint32_t nbatch = (k + wb - 1) / wb;
-    if (nbatch > kReplayMaxBatches || dyn_claim_on()) return false;
+    if (nbatch > kReplayMaxBatches || wb > (1u << kReplayBatchShift) || dyn_claim_on()) return false;
     // the inner dictionary: the first retained segment with both fields (every later one must number alike)
     for (const esgpu_plan::DeferredSeg& d : p->dsegs) {
         const DevColumn* a = d.s->col(R0.ord_field.c_str());
@@ -4345,15 +4346,18 @@ static bool replay_compact(esgpu_plan* p, const ChildSrc& kid, const std::vector
         if (e.code != ESGPU_ERR_OOM) throw;
         return false;
     }
+    // outer ordinal -> its winner's batch and index in the batch (ReplayCompactParams.slot_map)
     std::vector<uint32_t> map(std::max<uint64_t>(T_outer, 1), kMissingOrd);
-    for (uint32_t w = 0; w < k; ++w) if (top[w].ord < map.size()) map[top[w].ord] = w;
-    // device metadata: [slot map][region offsets (u64)][capacities][fills][overflow]
-    const size_t moff = ((map.size() * 4 + 15) & ~(size_t)15), coff = moff + (size_t)nbatch * 8, foff = coff + (size_t)nbatch * 4;
-    unsigned char* meta = (unsigned char*)p->s_rmeta.ensure(p->ctx, foff + (size_t)nbatch * 4 + 16);
+    for (uint32_t w = 0; w < k; ++w)
+        if (top[w].ord < map.size()) map[top[w].ord] = (w / wb) << kReplayBatchShift | (w % wb);
+    // device metadata: [slot map][region offsets (u64)][capacities][fills, one cache line each][overflow]
+    const size_t moff = ((map.size() * 4 + 15) & ~(size_t)15), coff = moff + (size_t)nbatch * 8,
+                 foff = (coff + (size_t)nbatch * 4 + 255) & ~(size_t)255, fbytes = (size_t)nbatch * kReplayFillStride * 4;
+    unsigned char* meta = (unsigned char*)p->s_rmeta.ensure(p->ctx, foff + fbytes + 16);
     HIPX(hipMemcpyAsync(meta, map.data(), map.size() * 4, hipMemcpyHostToDevice, st));
     HIPX(hipMemcpyAsync(meta + moff, rr.off.data(), (size_t)nbatch * 8, hipMemcpyHostToDevice, st));
     HIPX(hipMemcpyAsync(meta + coff, cap.data(), (size_t)nbatch * 4, hipMemcpyHostToDevice, st));
-    HIPX(hipMemsetAsync(meta + foff, 0, (size_t)nbatch * 4 + 16, st));
+    HIPX(hipMemsetAsync(meta + foff, 0, fbytes + 16, st));
     for (const esgpu_plan::DeferredSeg& d : p->dsegs) {
         const DevColumn* a = d.s->col(R0.ord_field.c_str());
         const DevColumn* b = d.s->col(R0.ord_field2.c_str());
@@ -4361,6 +4365,8 @@ static bool replay_compact(esgpu_plan* p, const ChildSrc& kid, const std::vector
         ReplayCompactParams C{};
         C.n_docs = d.s->max_doc;
         C.a = a->ords().as<uint32_t>();
+        // the outer ordinals' 16-bit copy when the request's collect built it (2 B per doc instead of 4)
+        if (a->ord16.p && a->ord16_src == a->ords().p) C.a16 = a->ord16.as<uint16_t>();
         C.b = b->ords().as<uint32_t>();
         C.slot_map = (const uint32_t*)meta;
         C.slot_map_n = (uint32_t)map.size();
@@ -4376,15 +4382,15 @@ static bool replay_compact(esgpu_plan* p, const ChildSrc& kid, const std::vector
         C.region = (const uint64_t*)(meta + moff);
         C.cap = (const uint32_t*)(meta + coff);
         C.fill = (uint32_t*)(meta + foff);
-        C.overflow = (uint32_t*)(meta + foff + (size_t)nbatch * 4);
+        C.overflow = (uint32_t*)(meta + foff + fbytes);
         launch_replay_compact(C, st);
         HIPX(hipGetLastError());
     }
-    uint32_t* hf = (uint32_t*)p->h_rfill.ensure((size_t)nbatch * 4 + 16);
-    HIPX(hipMemcpyAsync(hf, meta + foff, (size_t)nbatch * 4 + 16, hipMemcpyDeviceToHost, st));
+    uint32_t* hf = (uint32_t*)p->h_rfill.ensure(fbytes + 16);
+    HIPX(hipMemcpyAsync(hf, meta + foff, fbytes + 16, hipMemcpyDeviceToHost, st));
     HIPX(hipStreamSynchronize(st));  // also keeps `map` / `cap` alive for the copies
-    if (hf[nbatch] != 0) return false;  // an append past its capacity: the per-pass replay instead
-    for (uint32_t bi = 0; bi < nbatch; ++bi) rr.n[bi] = hf[bi];
+    if (hf[(size_t)nbatch * kReplayFillStride] != 0) return false;  // an append past its capacity: the per-pass replay instead
+    for (uint32_t bi = 0; bi < nbatch; ++bi) rr.n[bi] = hf[(size_t)bi * kReplayFillStride];
     return true;
 }
 
@@ -4424,6 +4430,11 @@ static ReplaySel replay_child(esgpu_plan* p, const ChildSrc& kid, const std::vec
     // count-only children in batches: compact the winners' docs once, then count each batch from its region
     ReplayRegions rr;
     const bool compact = wb < k && replay_compaction() && replay_compact(p, kid, top, wb, T_outer, rr);
+    // count orders selected on the GPU: every batch's rows go to one key array, fetched once after the last batch (the
+    // counts are in the keys: no gather, no wait per batch)
+    std::vector<uint8_t> deferred(k, 0);
+    unsigned long long* dk_all = nullptr;
+    uint32_t kk_all = 0;
     for (uint32_t b0 = 0; b0 < k; b0 += wb) {
         const uint32_t kb = std::min(wb, k - b0);
         bool any;
@@ -4483,8 +4494,19 @@ static ReplaySel replay_child(esgpu_plan* p, const ChildSrc& kid, const std::vec
         require(p->docs_seen < (1ull << 31), ESGPU_ERR_UNSUPPORTED,
                 "a breadth-first terms request over more than 2^31 - 1 docs (more than one Lucene shard): runs on the CPU path");
         const bool big = kk > kTopkMax;
-        unsigned long long* dk = (unsigned long long*)p->s_rkeys.ensure(p->ctx, (size_t)kb * (kk + 1) * 8);
-        HIPX(hipMemsetAsync(dk, 0, (size_t)kb * (kk + 1) * 8, st));
+        const bool defer = count_order && !big && kid.rgrand.empty();  // (grandchildren read the gathered cells)
+        unsigned long long* dk;
+        if (defer) {
+            if (!dk_all) {
+                dk_all = (unsigned long long*)p->s_rkeys.ensure(p->ctx, (size_t)k * (kk + 1) * 8);
+                HIPX(hipMemsetAsync(dk_all, 0, (size_t)k * (kk + 1) * 8, st));
+                kk_all = kk;
+            }
+            dk = dk_all + (size_t)b0 * (kk + 1);
+        } else {
+            dk = (unsigned long long*)p->s_rkeys2.ensure(p->ctx, (size_t)kb * (kk + 1) * 8);
+            HIPX(hipMemsetAsync(dk, 0, (size_t)kb * (kk + 1) * 8, st));
+        }
         std::vector<unsigned long long> big_keys;
         const uint32_t n_wg = std::min<uint32_t>(512, (uint32_t)((nb + 4095) / 4096));
         unsigned long long* cand = (unsigned long long*)p->s_cand.ensure(p->ctx, (count_order ? (size_t)nb : (size_t)n_wg * kk) * 8);
@@ -4528,6 +4550,10 @@ static ReplaySel replay_child(esgpu_plan* p, const ChildSrc& kid, const std::vec
             std::copy(ck.begin(), ck.begin() + take, big_keys.begin() + (size_t)r * (kk + 1));
             big_keys[(size_t)r * (kk + 1) + kk] = row_sum;
         }
+        if (defer) {
+            std::fill(deferred.begin() + b0, deferred.begin() + b0 + kb, 1);
+            continue;
+        }
         const unsigned long long* hk;
         if (big) {
             hk = big_keys.data();
@@ -4568,6 +4594,27 @@ static ReplaySel replay_child(esgpu_plan* p, const ChildSrc& kid, const std::vec
                 if (tp.count < 0) tp.count = (int64_t)R0.hc.cnt[rs.cell[b0 + r][j]];  // term orders: count from the gather
                 rs.other[b0 + r] -= tp.count;
             }
+    }
+    if (dk_all) {  // the deferred rows (count orders: count and ordinal in each key)
+        d2h_u64(p, p->h_rkeys, dk_all, (size_t)k * (kk_all + 1));
+        bsync(p);
+        const unsigned long long* hk = p->h_rkeys.as<unsigned long long>();
+        for (uint32_t w = 0; w < k; ++w) {
+            if (!deferred[w]) continue;
+            const unsigned long long* ki = hk + (size_t)w * (kk_all + 1);
+            rs.other[w] = (int64_t)ki[kk_all];
+            for (uint32_t j = 0; j < kk_all; ++j) {
+                const unsigned long long key = ki[j];
+                if (key == 0) break;
+                TermPick tp;
+                tp.ord = 0xFFFFFFFFu - (uint32_t)key;
+                const uint64_t hi = (key >> 32) & 0x7FFFFFFFull;
+                tp.count = tn2.s.order == ESGPU_ORDER_COUNT_DESC ? (int64_t)hi : (int64_t)(0x7FFFFFFFull - hi);
+                rs.other[w] -= tp.count;
+                rs.cell[w].push_back(0);  // (no gather: the counts came with the keys)
+                rs.picks[w].push_back(tp);
+            }
+        }
     }
     return rs;
 }

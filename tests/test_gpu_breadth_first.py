@@ -161,12 +161,14 @@ def test_hosts_by_urls_10m(engine):
     seg.close()
 
 
+@pytest.mark.parametrize("batch", ["2", "3"])
 @pytest.mark.parametrize("order", ["count", "term", "count_asc"])
-def test_replayed_batches_compacted(engine, forced, monkeypatch, order):
-    """Count-only inner terms over 100,000 ordinals replayed in batches of 2 winners (ESGPU_REPLAY_BATCH): the winners'
-    docs are compacted once per retained segment into per-batch regions -- under a query filter and live docs, over two
+def test_replayed_batches_compacted(engine, forced, monkeypatch, order, batch):
+    """Count-only inner terms over 100,000 ordinals replayed in batches of 2 or 3 winners (ESGPU_REPLAY_BATCH; 17
+    winners: 9 batches take the compaction's scattered appends, 6 its per-block sort by batch in LDS): the winners' docs
+    are compacted once per retained segment into per-batch regions -- under a query filter and live docs, over two
     segments -- and each batch is counted from its region (ReplayCompactParams)."""
-    monkeypatch.setenv("ESGPU_REPLAY_BATCH", "2")
+    monkeypatch.setenv("ESGPU_REPLAY_BATCH", batch)
     inner = AB.terms("B").field("b").size(4)
     inner.order(Order.count(False) if order == "count" else Order.term(True) if order == "term" else Order.count(True))
     aggs = [AB.terms("A").field("a").size(5).subAggregation(inner)]
