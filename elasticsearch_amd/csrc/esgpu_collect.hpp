@@ -157,6 +157,12 @@ __device__ __forceinline__ uint32_t eval_pred(const PredDev& q, uint32_t doc0) {
 // timestamp column): loads only, no use of a loaded word until unpack_docs
 template <int MET, int VK, bool HIST>
 constexpr bool kRawPI = MET > 0 && (VK & 64) != 0 && (VK & 16) != 0 && (VK & 256) != 0 && (!HIST || (VK & (32 | 8192)) != 0);
+#ifndef ESGPU_B16_NOLOAD
+#define ESGPU_B16_NOLOAD 0
+#endif
+#ifndef ESGPU_B16_BRANCH  // single-key blocks skip the timestamp and base loads (a wave-uniform branch; with ESGPU_DOCS8
+#define ESGPU_B16_BRANCH 1  // measured level with the dummy loads on the north star, 3 % better on config 5)
+#endif
 #ifndef ESGPU_B16_SCALAR  // block-delta bases as scalar loads (1) or per-lane vector loads (0)
 #define ESGPU_B16_SCALAR 0
 #endif
@@ -169,6 +175,16 @@ __device__ __forceinline__ void load_keys_raw(const CollectParams& P, uint32_t d
         // a block whose docs all round to one key reads no timestamp: every lane loads the column's first word (one
         // cache line per wave, in place of a branch around the load -- a load under a branch makes the compiler wait
         // for the other buffers' loads)
+#if ESGPU_B16_NOLOAD  // timing experiment only (wrong keys in multi-key blocks): no timestamp or base loads at all
+        raw[2] = doc0; raw[3] = doc0; raw[4] = 0; raw[5] = 0;
+        return;
+#endif
+#if ESGPU_B16_BRANCH  // (A/B) the single-key blocks' loads skipped under a wave-uniform branch
+        if (uk != kNoUKey) {
+            raw[2] = 0; raw[3] = 0; raw[4] = 0; raw[5] = 0;
+            return;
+        }
+#endif
         const u32x2_t t = load8(P.hv16 + (uk == kNoUKey ? doc0 : 0u));
         raw[2] = t.x; raw[3] = t.y;
 #if ESGPU_B16_SCALAR
@@ -313,6 +329,44 @@ __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0,
         }
         d.mpres = P.mv_present ? bits4(P.mv_present, doc0) : 0xFu;
     }
+}
+
+// Packed-cell raw-load kernels with 8 docs per thread per step (ESGPU_DOCS8): one 16-byte load per column for 8 docs
+// instead of an 8-byte load per 4, the step's loop, prefetch and zone work shared by twice the docs; processed as two
+// Doc4 halves (docs doc0 .. doc0 + 3 and doc0 + 4 .. doc0 + 7)
+#ifndef ESGPU_DOCS8  // (r5ab7, 1B docs: north star 1.21 -> 1.19 ms, terms{dh{avg}} 1.09 -> 0.96, config 5 2.36 -> 2.12)
+#define ESGPU_DOCS8 1
+#endif
+struct Doc8 {
+    Doc4 a, b;
+};
+template <bool HIST, int MET, int VK>
+__device__ __forceinline__ void load_docs8(const CollectParams& P, uint32_t doc0, Doc8& d, uint32_t uk = kNoUKey) {
+    static_assert(kRawPI<MET, VK, HIST>, "8 docs per thread: raw-load packed-cell kernels only");
+    d.a.ukey = uk;
+    d.b.ukey = uk;
+    const u32x4_t o = load16(P.ord16 + doc0);
+    d.a.raw[0] = o.x; d.a.raw[1] = o.y; d.b.raw[0] = o.z; d.b.raw[1] = o.w;
+    if constexpr (HIST) {
+        if constexpr ((VK & 8192) != 0) {
+            const u32x4_t t = load16(P.hv16 + (uk == kNoUKey ? doc0 : 0u));
+            const u32x2_t bs = load8(P.hv16_base + (doc0 >> kB16Shift));  // (8 docs never straddle a run)
+            d.a.raw[2] = t.x; d.a.raw[3] = t.y; d.b.raw[2] = t.z; d.b.raw[3] = t.w;
+            d.a.raw[4] = bs.x; d.a.raw[5] = bs.y; d.b.raw[4] = bs.x; d.b.raw[5] = bs.y;
+        } else {
+            const u32x4_t t0 = load16(P.hv32 + doc0), t1 = load16(P.hv32 + doc0 + 4);
+            d.a.raw[2] = t0.x; d.a.raw[3] = t0.y; d.a.raw[4] = t0.z; d.a.raw[5] = t0.w;
+            d.b.raw[2] = t1.x; d.b.raw[3] = t1.y; d.b.raw[4] = t1.z; d.b.raw[5] = t1.w;
+        }
+    }
+    const u32x4_t m = load16(P.mv16 + doc0);
+    d.a.raw[6] = m.x; d.a.raw[7] = m.y; d.b.raw[6] = m.z; d.b.raw[7] = m.w;
+    if constexpr ((VK & 512) != 0) {  // (both halves in one 64-doc word)
+        d.a.racc = P.accept[doc0 >> 6];
+        d.b.racc = d.a.racc;
+    }
+    d.a.doc0 = doc0;
+    d.b.doc0 = doc0 + 4;
 }
 
 // Accumulator views: either the workgroup's LDS window or the global cell grid.
@@ -1235,7 +1289,8 @@ template <bool ORD, int MET, int VK, int WGS> constexpr int collect_min_waves() 
 }
 template <bool ORD, int HK, int MET, int VK, int WGS>
 __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void collect_kernel(CollectParams P) {
-    constexpr int kIterDocsW = WGS * kVec;
+    constexpr bool WIDE8 = ESGPU_DOCS8 != 0 && kRawPI<MET, VK, (HK != 0)>;  // 8 docs per thread per step (Doc8)
+    constexpr int kIterDocsW = WGS * (WIDE8 ? 2 * kVec : kVec);
     constexpr int kItersPerBlockW = kBlockDocs / kIterDocsW;
     constexpr bool HIST = HK != 0;
     constexpr bool KT = HK == 2;
@@ -1355,7 +1410,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
     // replay is part of the schedule the prefetches follow -- the pass count is known at the group's first
     // iteration, before any replayed iteration is prefetched -- so it costs no extra load buffers.  Groups whose
     // blocks each fit the window are taken block by block, the window sliding as before.
-    const uint32_t tid4 = threadIdx.x * kVec;
+    const uint32_t tid4 = threadIdx.x * (WIDE8 ? 2 * kVec : kVec);
     // shapes that read few bytes per doc (one ordinal or one key column) keep 4 buffers in flight, the rest 2 (their
     // buffers are 5x larger; 4 would cost occupancy).  kItersPerBlockW (4) is a multiple of either.
     constexpr int kBuf = (kRawH<ORD, MET, VK> && !ORD && MET == 0) ? (ESGPU_NBUF_HIST <= kItersPerBlockW ? ESGPU_NBUF_HIST : kItersPerBlockW)
@@ -1379,9 +1434,14 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
         }
     };
     uint32_t pf_blk = b_begin, pf_uk = zone_ukey(b_begin);  // the block the prefetches read, and its key
-    Doc4 q[kBuf];
+    using Buf = std::conditional_t<WIDE8, Doc8, Doc4>;
+    auto load_buf = [&](uint32_t doc0, Buf& d, uint32_t uk) {
+        if constexpr (WIDE8) load_docs8<HIST, MET, VKL>(P, doc0, d, uk);
+        else load_docs<ORD, HIST, MET, VKL>(P, doc0, d, uk);
+    };
+    Buf q[kBuf];
 #pragma unroll
-    for (int k = 0; k < kBuf; ++k) load_docs<ORD, HIST, MET, VKL>(P, b_begin * kBlockDocs + k * kIterDocsW + tid4, q[k], pf_uk);
+    for (int k = 0; k < kBuf; ++k) load_buf(b_begin * kBlockDocs + k * kIterDocsW + tid4, q[k], pf_uk);
 
     bool use_lds = P.lds_mode != 0;
     uint32_t cb = b_begin;                               // block being processed
@@ -1399,7 +1459,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
         win_set = true;
         base = (P.key0 + (int64_t)win0) * P.interval + P.offset;
     };
-    auto step = [&](uint32_t it, Doc4& q) {
+    auto step = [&](uint32_t it, Buf& q) {
         if (it == 0) {
             // ---- per-group / per-block decisions (wave-uniform: every lane reads the same zone-map words) ----
             // readfirstlane: the zone-map words become scalar loads (lgkmcnt), not vector loads whose vmcnt wait
@@ -1445,10 +1505,20 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
             }
         }
         if (use_lds) {
-            process4<ORD, HIST, MET, true, KT, kMS, HORD, VKL>(P, s, q, T, base, win0, run, npass > 1 ? W : 0u, pass == 0);
+            if constexpr (WIDE8) {
+                process4<ORD, HIST, MET, true, KT, kMS, HORD, VKL>(P, s, q.a, T, base, win0, run, npass > 1 ? W : 0u, pass == 0);
+                process4<ORD, HIST, MET, true, KT, kMS, HORD, VKL>(P, s, q.b, T, base, win0, run, npass > 1 ? W : 0u, pass == 0);
+            } else {
+                process4<ORD, HIST, MET, true, KT, kMS, HORD, VKL>(P, s, q, T, base, win0, run, npass > 1 ? W : 0u, pass == 0);
+            }
             dirty = true;
         } else {
-            process4<ORD, HIST, MET, false, KT, kMS, HORD, VKL>(P, g, q, T, base, win0, run);
+            if constexpr (WIDE8) {
+                process4<ORD, HIST, MET, false, KT, kMS, HORD, VKL>(P, g, q.a, T, base, win0, run);
+                process4<ORD, HIST, MET, false, KT, kMS, HORD, VKL>(P, g, q.b, T, base, win0, run);
+            } else {
+                process4<ORD, HIST, MET, false, KT, kMS, HORD, VKL>(P, g, q, T, base, win0, run);
+            }
         }
         // prefetch kBuf iterations ahead along the schedule (next block of the group, the group's next pass, or the
         // next group)
@@ -1464,7 +1534,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
             pf_blk = nb;
             pf_uk = zone_ukey(nb);
         }
-        load_docs<ORD, HIST, MET, VKL>(P, nb * kBlockDocs + nit * kIterDocsW + tid4, q, pf_uk);
+        load_buf(nb * kBlockDocs + nit * kIterDocsW + tid4, q, pf_uk);
     };
     while (cb < b_end) {
         for (uint32_t it = 0; it < (uint32_t)kItersPerBlockW; it += kBuf) {
