@@ -337,31 +337,54 @@ __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0,
 #ifndef ESGPU_DOCS8  // (r5ab7, 1B docs: north star 1.21 -> 1.19 ms, terms{dh{avg}} 1.09 -> 0.96, config 5 2.36 -> 2.12)
 #define ESGPU_DOCS8 1
 #endif
+#ifndef ESGPU_DOCS8_H  // ... the raw-load counting grids with a terms dimension (VK bit 1024; r5ab8: terms{date_histogram}
+#define ESGPU_DOCS8_H 1  // 0.96 -> 0.88 ms at 1B; the histogram-only grids measured 7 % slower at 8 and keep 4)
+#endif
+#ifndef ESGPU_B16_BRANCH8  // ... single-key blocks' timestamp loads skipped under a branch, else a dummy load (r5ab8:
+#define ESGPU_B16_BRANCH8 1  // north star 1.196 -> 1.165 ms)
+#endif
 struct Doc8 {
     Doc4 a, b;
 };
-template <bool HIST, int MET, int VK>
+template <bool ORD, bool HIST, int MET, int VK>
 __device__ __forceinline__ void load_docs8(const CollectParams& P, uint32_t doc0, Doc8& d, uint32_t uk = kNoUKey) {
-    static_assert(kRawPI<MET, VK, HIST>, "8 docs per thread: raw-load packed-cell kernels only");
+    static_assert(kRawPI<MET, VK, HIST> || kRawH<ORD, MET, VK>, "8 docs per thread: raw-load kernels only");
     d.a.ukey = uk;
     d.b.ukey = uk;
-    const u32x4_t o = load16(P.ord16 + doc0);
-    d.a.raw[0] = o.x; d.a.raw[1] = o.y; d.b.raw[0] = o.z; d.b.raw[1] = o.w;
+    if constexpr (ORD) {
+        const u32x4_t o = load16(P.ord16 + doc0);
+        d.a.raw[0] = o.x; d.a.raw[1] = o.y; d.b.raw[0] = o.z; d.b.raw[1] = o.w;
+    }
     if constexpr (HIST) {
         if constexpr ((VK & 8192) != 0) {
-            const u32x4_t t = load16(P.hv16 + (uk == kNoUKey ? doc0 : 0u));
-            const u32x2_t bs = load8(P.hv16_base + (doc0 >> kB16Shift));  // (8 docs never straddle a run)
-            d.a.raw[2] = t.x; d.a.raw[3] = t.y; d.b.raw[2] = t.z; d.b.raw[3] = t.w;
-            d.a.raw[4] = bs.x; d.a.raw[5] = bs.y; d.b.raw[4] = bs.x; d.b.raw[5] = bs.y;
+            bool skip = false;
+#if ESGPU_B16_BRANCH8
+            skip = uk != kNoUKey;  // a single-key block: no timestamp is read (wave-uniform branch)
+#endif
+            if (skip) {
+                d.a.raw[2] = d.a.raw[3] = d.a.raw[4] = d.a.raw[5] = 0u;
+                d.b.raw[2] = d.b.raw[3] = d.b.raw[4] = d.b.raw[5] = 0u;
+            } else {
+                const u32x4_t t = load16(P.hv16 + (uk == kNoUKey ? doc0 : 0u));
+                const u32x2_t bs = load8(P.hv16_base + (doc0 >> kB16Shift));  // (8 docs never straddle a run)
+                d.a.raw[2] = t.x; d.a.raw[3] = t.y; d.b.raw[2] = t.z; d.b.raw[3] = t.w;
+                d.a.raw[4] = bs.x; d.a.raw[5] = bs.y; d.b.raw[4] = bs.x; d.b.raw[5] = bs.y;
+            }
         } else {
             const u32x4_t t0 = load16(P.hv32 + doc0), t1 = load16(P.hv32 + doc0 + 4);
             d.a.raw[2] = t0.x; d.a.raw[3] = t0.y; d.a.raw[4] = t0.z; d.a.raw[5] = t0.w;
             d.b.raw[2] = t1.x; d.b.raw[3] = t1.y; d.b.raw[4] = t1.z; d.b.raw[5] = t1.w;
         }
     }
-    const u32x4_t m = load16(P.mv16 + doc0);
-    d.a.raw[6] = m.x; d.a.raw[7] = m.y; d.b.raw[6] = m.z; d.b.raw[7] = m.w;
-    if constexpr ((VK & 512) != 0) {  // (both halves in one 64-doc word)
+    if constexpr (MET > 0 && (kRawPI<MET, VK, HIST> || (VK & 2048) != 0)) {  // 16-bit metric deltas
+        const u32x4_t m = load16(P.mv16 + doc0);
+        d.a.raw[6] = m.x; d.a.raw[7] = m.y; d.b.raw[6] = m.z; d.b.raw[7] = m.w;
+    } else if constexpr (MET > 0) {  // u32 metric deltas
+        const u32x4_t m0 = load16(P.mv32 + doc0), m1 = load16(P.mv32 + doc0 + 4);
+        d.a.raw[6] = m0.x; d.a.raw[7] = m0.y; d.a.raw[8] = m0.z; d.a.raw[9] = m0.w;
+        d.b.raw[6] = m1.x; d.b.raw[7] = m1.y; d.b.raw[8] = m1.z; d.b.raw[9] = m1.w;
+    }
+    if constexpr (kRawPI<MET, VK, HIST> && (VK & 512) != 0) {  // (both halves in one 64-doc word)
         d.a.racc = P.accept[doc0 >> 6];
         d.b.racc = d.a.racc;
     }
@@ -1289,7 +1312,8 @@ template <bool ORD, int MET, int VK, int WGS> constexpr int collect_min_waves() 
 }
 template <bool ORD, int HK, int MET, int VK, int WGS>
 __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void collect_kernel(CollectParams P) {
-    constexpr bool WIDE8 = ESGPU_DOCS8 != 0 && kRawPI<MET, VK, (HK != 0)>;  // 8 docs per thread per step (Doc8)
+    constexpr bool WIDE8 = (ESGPU_DOCS8 != 0 && kRawPI<MET, VK, (HK != 0)>) ||  // 8 docs per thread per step (Doc8)
+                           (ESGPU_DOCS8_H != 0 && kRawH<ORD, MET, VK> && ORD);
     constexpr int kIterDocsW = WGS * (WIDE8 ? 2 * kVec : kVec);
     constexpr int kItersPerBlockW = kBlockDocs / kIterDocsW;
     constexpr bool HIST = HK != 0;
@@ -1436,7 +1460,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
     uint32_t pf_blk = b_begin, pf_uk = zone_ukey(b_begin);  // the block the prefetches read, and its key
     using Buf = std::conditional_t<WIDE8, Doc8, Doc4>;
     auto load_buf = [&](uint32_t doc0, Buf& d, uint32_t uk) {
-        if constexpr (WIDE8) load_docs8<HIST, MET, VKL>(P, doc0, d, uk);
+        if constexpr (WIDE8) load_docs8<ORD, HIST, MET, VKL>(P, doc0, d, uk);
         else load_docs<ORD, HIST, MET, VKL>(P, doc0, d, uk);
     };
     Buf q[kBuf];
