@@ -3145,7 +3145,11 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
 #define ESGPU_WG_WAVES 8  // measured: 1-7 % faster than 1 on the collect shapes (8 and 16 alike, 32 slower)
 #endif
     // ESGPU_WG_WAVES > 1: more, shorter workgroup ranges than resident slots (tail balancing vs per-workgroup setup)
-    const uint32_t target = (uint32_t)p->ctx->cus * wg_per_cu * ESGPU_WG_WAVES;
+    static const uint32_t wg_waves = [] {  // (ESGPU_WG_WAVES_ENV: A/B runs)
+        const char* e = std::getenv("ESGPU_WG_WAVES_ENV");
+        return (uint32_t)std::max(1, e && *e ? std::atoi(e) : ESGPU_WG_WAVES);
+    }();
+    const uint32_t target = (uint32_t)p->ctx->cus * wg_per_cu * wg_waves;
     const uint32_t bpw = (P.n_blocks + target - 1) / target;
 #ifndef ESGPU_MIN_BPW
 #define ESGPU_MIN_BPW 32  // measured at 125M docs: terms(host) 0.19 -> 0.10 ms, terms{stats} -16 %, config 5 -8 %
