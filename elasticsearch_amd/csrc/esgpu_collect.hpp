@@ -1581,7 +1581,10 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
             }
         }
     }
-    if (P.lds_mode && (dirty || !(HIST && P.windowed))) {
+#ifndef ESGPU_FLUSH_DIAG  // timing experiment only (wrong results): 1 = no final window flush
+#define ESGPU_FLUSH_DIAG 0
+#endif
+    if (P.lds_mode && (dirty || !(HIST && P.windowed)) && !ESGPU_FLUSH_DIAG) {
         if (!ORD) runs_flush<MET, kMS, runs_for<MET, VKL>(), kIntRuns<ORD, MET, VKL>>(P, s, run);
         if constexpr (PI && ESGPU_PI_HOT) pi_hot_flush<MET>(P, s, run, T);
         if constexpr (PI) flush_window_pi<MET, WGS>(P, s, T, W, win0, ncp);
