@@ -181,9 +181,12 @@ def main():
     ap.add_argument("--cpu-single-docs", type=int, default=20_000_000, help="docs of the single-thread CPU shard")
     ap.add_argument("--inflight", type=int, default=0, choices=(0, 1, 2, 3, 4),
                     help="requests in flight (0 = 2): plan sets that alternate, one plan per shard of a request")
-    ap.add_argument("--scheme", default="rotate", choices=("rotate", "sets"),
-                    help="pipelined phase: rotate = `inflight` plans taken in turn by the shards of consecutive requests; "
-                         "sets = one plan per shard, `inflight` sets of them alternating between requests")
+    ap.add_argument("--scheme", default="auto", choices=("auto", "inline", "rotate", "sets"),
+                    help="pipelined phase: inline = one unit per request, the next request's collect launched before this "
+                         "one is built and reduced on the main thread (no worker threads); rotate = `inflight` plans taken "
+                         "in turn by the shards of consecutive requests, builds on worker threads; sets = one plan per "
+                         "shard, `inflight` sets of them alternating between requests; auto = inline for one-unit "
+                         "requests, else rotate")
     ap.add_argument("--no-colo", action="store_true",
                     help="build every shard result and reduce them on the host, instead of the co-located reduce "
                          "(esgpu_plans_build_reduce) for a GPU's terms shards on one GPU")
@@ -333,6 +336,21 @@ def main():
         while pend:
             final = pend.popleft().result()
 
+    def run_inline(n_requests, depth):
+        """one unit per request on `depth` plans taken in turn, no worker threads: request r + 1's collect is launched
+        (on its plan's stream) before request r is built and reduced here, so the GPU runs the next collect while the
+        host builds -- for small requests the thread handoffs of `run_rotate` cost more than the build"""
+        nonlocal final
+        plans = [st[0] for st in sets[:depth]]
+        if n_requests == 0:
+            return
+        launch(plans[0], 0, False)
+        for r in range(n_requests):
+            if r + 1 < n_requests:
+                launch(plans[(r + 1) % depth], 0, False)
+            part = plans[r % depth].build()
+            final = comm.reduce([part]) if comm else ea.reduce([part])
+
     def run_serial(n_requests):
         """one unit at a time on one plan: collect, build, and finally reduce, nothing overlapping -- the collect
         kernels' HIP-event times are taken here, where no two kernels run at once"""
@@ -406,11 +424,13 @@ def main():
             hbm.append(engine.hbm_used() - h0)
         p.build()
         if sum(hbm) >= 2 * args.docs * len(segs):  # at least 2 B per doc: compact columns were built
-            precomputed = {"what": "compact columns of the segment (u16 ordinals / u32 timestamp deltas, cached with it; "
-                                   "the first segment's figure includes the plan's grid)",
+            precomputed = {"what": "compact columns of the segment (u16 ordinals, timestamp block deltas or u32 deltas, "
+                                   "u16 / u32 metric deltas; cached with it; the first segment's figure includes the plan's grid)",
                            "build_ms_per_segment": round(sum(first) / len(first), 3),
                            "hbm_bytes_per_segment": int(sum(hbm) / len(hbm))}
-    pipelined = run_rotate if args.scheme == "rotate" else run
+    if args.scheme == "auto":
+        args.scheme = "inline" if units_per_request == 1 and not colo and inflight > 1 else "rotate"
+    pipelined = {"inline": run_inline, "rotate": run_rotate}.get(args.scheme, run)
     pipelined(args.warmup, inflight)
     elapsed = timed(pipelined, args.steps, inflight)
     elapsed_latency = timed(run, args.steps, 1) if inflight > 1 else elapsed
