@@ -5284,8 +5284,21 @@ extern "C" int esgpu_plan_build(esgpu_plan* p, esgpu_result** out) {
                 dc = hc[0];
             }
             fb.count.push_back((int64_t)dc);
-            for (int ch : p->specs[r].children)
-                fb.subs.push_back(p->specs[ch].s.type == ESGPU_AGG_FILTER ? build_filter(ch) : build_group(p, p->groups[gi++]));
+            for (int ch : p->specs[r].children) {
+                if (p->specs[ch].s.type == ESGPU_AGG_FILTER) { fb.subs.push_back(build_filter(ch)); continue; }
+                const Group& g = p->groups[gi++];
+                // sub-aggregators are wrapped by asMultiBucketAggregator (AggregatorFactories.java:75): a filter that
+                // collected no doc never created its bucket-0 aggregator, so buildAggregation(0) is
+                // first.buildEmptyAggregation() (AggregatorFactory.java:215-227) -- terms with min_doc_count 0 list
+                // no zero-count terms then
+                if (dc == 0 && p->specs[g.root].s.type == ESGPU_AGG_TERMS) {
+                    Block e = terms_shell(p, g.root, child_protos(p, g));
+                    e.append_empty();
+                    fb.subs.push_back(std::move(e));
+                    continue;
+                }
+                fb.subs.push_back(build_group(p, g));
+            }
             return fb;
         };
         for (int r : p->tops) {

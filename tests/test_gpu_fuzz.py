@@ -277,6 +277,46 @@ def test_random_request(engine, seed, monkeypatch):
     seg.close()
 
 
+DENSE_SEEDS = list(range(48))
+
+
+@pytest.mark.parametrize("seed", DENSE_SEEDS)
+def test_random_request_dense_timestamps(engine, seed, monkeypatch):
+    """The same random requests over segments whose timestamps are dense enough for the block-delta layout (every run of
+    2,048 docs spans < 2^16 ms: 30 minutes to 4 hours of docs, displaced by up to 5 s): the raw-load kernels read 16-bit
+    timestamp deltas, take single-key zone blocks' key without reading them, and step 8 docs per thread."""
+    if seed % 3 == 0:
+        monkeypatch.setenv("ESGPU_DEFER_CELLS", "1")
+    rng = np.random.default_rng(7000 + seed)
+    n = int(rng.integers(30_000, 300_000))
+    cols, T_kw = make_segment(rng, n)
+    r = np.random.default_rng(9000 + seed)
+    span = int(r.choice([1_800_000, 3_600_000, 4 * 3_600_000]))
+    span = min(span, n * 30)  # < 2^16 ms per 2,048-doc run
+    ts = T0 + np.sort(r.integers(0, span, size=n)).astype(np.int64)
+    if r.random() < 0.5:
+        ts = ts + r.integers(-5000, 5001, size=n)
+    cols["@timestamp"] = {"type": N.COL_I64, "values": ts}
+    gen = Gen(rng, T_kw, np.random.default_rng(60_000 + seed), np.random.default_rng(95_000 + seed))
+    aggs, filters = gen.request()
+    lookups = {f: {t: i for i, t in enumerate(cols[f]["terms"])} for f in ("kw", "kw2", "tags")}
+    ord_lookup = lambda f, t: lookups.get(f, {}).get(t, -1)  # noqa: E731
+    seg = engine.upload_segment(cols, n)
+    try:
+        plan = engine.plan(aggs, filters=filters, ord_lookup=ord_lookup)
+        plan.collect(seg)
+    except N.UnsupportedOnGpu as e:
+        seg.close()
+        pytest.skip("shape refused by the GPU plan: %s" % e)
+    res = plan.build()
+    want = O.run([(cols, n)], aggs, filters=filters, ord_lookup=ord_lookup)
+    exact = not gen.inexact
+    assert_same(res.to_dict(), want["shards"][0], "shard", exact)
+    assert_same(reduce([res]).to_dict(), want["reduced"], "reduced", exact)
+    plan.close()
+    seg.close()
+
+
 def test_fuzz_mostly_on_gpu():
     """runs after the cases above (file order): most random requests must have run on the GPU path"""
     total = _stats["ran"] + _stats["refused"]

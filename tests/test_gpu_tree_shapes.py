@@ -186,6 +186,23 @@ def test_terms_ordered_by_cardinality(engine, asc, thr):
     _both(engine, aggs, n=300_000, shards=2)
 
 
+def test_terms_min_doc_count_0_under_empty_filter(engine):
+    """Sub-aggregators are wrapped by asMultiBucketAggregator (AggregatorFactories.java:75): a filter that collected no
+    doc in the shard never created its bucket-0 terms aggregator, so the shard's terms is first.buildEmptyAggregation()
+    (AggregatorFactory.java:215-227) -- no zero-count terms even with min_doc_count 0 -- while a filter that matched
+    lists every term; beside a histogram with min_doc_count 0 and extended bounds, and stats, under the empty one."""
+    aggs = [AB.filter("none", QB.rangeQuery("bytes").lt(0))
+            .subAggregation(AB.terms("t0").field("host").size(20).minDocCount(0)
+                            .subAggregation(AB.avg("rt").field("response_time_ms")))
+            .subAggregation(AB.histogram("h0").field("response_time_ms").interval(250).minDocCount(0).extendedBounds(0, 1000))
+            .subAggregation(AB.stats("s0").field("bytes")),
+            AB.filter("some", QB.termQuery("status", 200))
+            .subAggregation(AB.terms("t1").field("host").size(20).minDocCount(0))]
+    red = _both(engine, aggs, n=200_000, shards=2)
+    assert red["none"]["doc_count"] == 0 and red["none"]["t0"]["buckets"] == []
+    assert red["some"]["doc_count"] > 0 and len(red["some"]["t1"]["buckets"]) > 0
+
+
 def test_filter_under_terms(engine):
     """FilterAggregator below the top level (A/bucket/filter/FilterAggregator.java:57-70): per term bucket the docs
     matching its clauses and its metric children over them; beside an unfiltered metric and a histogram child, and a
