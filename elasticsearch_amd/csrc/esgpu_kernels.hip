@@ -323,7 +323,10 @@ __host__ __device__ constexpr uint32_t hll_lds_bytes(uint32_t m, bool logm = fal
     return hll_snap_bytes(m) + (((m >= 64u ? m / 64u : 1u) + 15u) & ~15u) + (logm ? kHllLog * 4u + 3u * 256u * 4u + 16u : 0u);
 }
 
-template <int KIND>
+__device__ __forceinline__ uint32_t hll_enc32_entry(uint32_t v, int p);
+
+// E32: the enc32 words (HllParams.enc32, 4 bytes per doc) instead of the values, 8 docs per thread and buffer
+template <int KIND, bool E32>
 __global__ __launch_bounds__(kHllLdsWG) void hll_registers_lds_kernel(HllParams P, uint32_t d_begin, uint32_t d_end,
                                                                        uint32_t per_wg, const unsigned int* floor_ptr) {
     // LDS: [2^p / 2] packed nibbles, then the group floors [ngroups] (one byte per group of 64 registers)
@@ -367,20 +370,44 @@ __global__ __launch_bounds__(kHllLdsWG) void hll_registers_lds_kernel(HllParams 
     const uint32_t w0 = d_begin + blockIdx.x * per_wg;
     const uint32_t w1 = min(d_end, w0 + per_wg);
     if (w0 >= w1) return;  // workgroup-uniform: no docs, nothing logged
-    const uint32_t t4 = threadIdx.x * 4;
+    constexpr uint32_t kPer = E32 ? 8u : 4u;  // docs per thread and buffer
+    constexpr uint32_t kIt = kHllLdsWG * kPer;
+    const uint32_t t4 = threadIdx.x * kPer;
     // unconditional loads (past the range: the range's last 4 docs again, never hashed), so the compiler can count
     // them: a conditional load makes every later wait a vmcnt(0), which drains the other buffer's prefetch too
     const uint32_t last4 = (w1 - 1) & ~3u;
-    auto load = [&](uint32_t i0, uint64_t raw[4]) { load_i64x4((const int64_t*)P.col, min(i0, last4), (int64_t*)raw); };
-    auto hash4 = [&](uint32_t i0, const uint64_t raw[4]) {
+    auto load = [&](uint32_t i0, uint64_t raw[4]) {
+        if (E32) {  // two words per 64-bit slot: docs i0 + 2k and i0 + 2k + 1 in the low / high half of raw[k]
+            uint32_t w[8];
+            load_u32x4(P.enc32, min(i0, last4), w);
+            load_u32x4(P.enc32, min(i0 + 4, last4), w + 4);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) raw[k] = (uint64_t)w[2 * k] | (uint64_t)w[2 * k + 1] << 32;
+        } else {
+            load_i64x4((const int64_t*)P.col, min(i0, last4), (int64_t*)raw);
+        }
+    };
+    auto hash4 = [&](uint32_t i0, const uint64_t raw[4], int half) {
         if (i0 >= w1) return;
         const uint32_t lim = w1 - i0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint64_t h = hll_fast_hash<KIND>(P, raw[j]);
-            if ((uint32_t)j < lim && (h & zmask) == 0) {
-                const uint32_t rl = hll_run_len(h, P.p);
-                const uint32_t idx = hll_index(h, P.p);
+            uint32_t rl = 0, idx = 0;
+            bool t;
+            if (E32) {
+                const uint32_t e = hll_enc32_entry((uint32_t)(raw[(half * 4 + j) >> 1] >> (32 * (j & 1))), P.p);
+                rl = e >> 24;
+                idx = e & 0xFFFFFFu;
+                t = (uint32_t)j < lim && rl > F;
+            } else {
+                const uint64_t h = hll_fast_hash<KIND>(P, raw[j]);
+                t = (uint32_t)j < lim && (h & zmask) == 0;
+                if (t) {
+                    rl = hll_run_len(h, P.p);
+                    idx = hll_index(h, P.p);
+                }
+            }
+            if (t) {
                 const uint32_t bi = idx / kHllPerByte;
                 const uint32_t byte = nib[bi];
                 const uint32_t sh = (idx % kHllPerByte) * kHllBits;
@@ -398,28 +425,32 @@ __global__ __launch_bounds__(kHllLdsWG) void hll_registers_lds_kernel(HllParams 
     };
     // ESGPU_HLL_NBUF buffers, each reloaded right after it is hashed: no register copies (which would wait for the
     // loads); the prologue issues them in the loop's order (the loop head's wait counts merge both paths)
+    auto take = [&](uint32_t i0, const uint64_t raw[4]) {
+        hash4(i0, raw, 0);
+        if (E32) hash4(i0 + 4, raw, 1);
+    };
     uint64_t a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
     load(w0 + t4, a);
     __builtin_amdgcn_sched_barrier(0);
-    load(w0 + kHllLdsIter + t4, b);
+    load(w0 + kIt + t4, b);
 #if ESGPU_HLL_NBUF == 3
     uint64_t c[4] = {0, 0, 0, 0};
     __builtin_amdgcn_sched_barrier(0);
-    load(w0 + 2 * kHllLdsIter + t4, c);
-    for (uint32_t base = w0; base < w1; base += 3 * kHllLdsIter) {
-        hash4(base + t4, a);
-        load(base + 3 * kHllLdsIter + t4, a);
-        hash4(base + kHllLdsIter + t4, b);
-        load(base + 4 * kHllLdsIter + t4, b);
-        hash4(base + 2 * kHllLdsIter + t4, c);
-        load(base + 5 * kHllLdsIter + t4, c);
+    load(w0 + 2 * kIt + t4, c);
+    for (uint32_t base = w0; base < w1; base += 3 * kIt) {
+        take(base + t4, a);
+        load(base + 3 * kIt + t4, a);
+        take(base + kIt + t4, b);
+        load(base + 4 * kIt + t4, b);
+        take(base + 2 * kIt + t4, c);
+        load(base + 5 * kIt + t4, c);
     }
 #else
-    for (uint32_t base = w0; base < w1; base += 2 * kHllLdsIter) {
-        hash4(base + t4, a);
-        load(base + 2 * kHllLdsIter + t4, a);
-        hash4(base + kHllLdsIter + t4, b);
-        load(base + 3 * kHllLdsIter + t4, b);
+    for (uint32_t base = w0; base < w1; base += 2 * kIt) {
+        take(base + t4, a);
+        load(base + 2 * kIt + t4, a);
+        take(base + kIt + t4, b);
+        load(base + 3 * kIt + t4, b);
     }
 #endif
     if (!logm) return;
@@ -490,7 +521,43 @@ __device__ __forceinline__ void hll_fs_flush(const HllParams& P, uint32_t* rlog,
     __syncthreads();
 }
 
+// the enc32 form of one hash (HllParams.enc32): its top kP2 bits and min(nlz(h << kP2), 64 - kP2)
+__device__ __forceinline__ uint32_t hll_enc32(uint64_t h) {
+    const uint32_t z = (uint32_t)clz64(h << kP2);
+    return (uint32_t)(h >> (64 - kP2)) << 7 | min(z, 64u - kP2);
+}
+// index and run length of an enc32 word, as hll_index / hll_run_len of its hash (p <= kP2): the kP2 - p bits below the
+// index decide the run length if any is set (decodeRunLen's even case, HyperLogLogPlusPlus.java:349-357), else it is
+// kP2 - p plus the stored count plus one (the odd case; the count is clamped at 64 - kP2 as runLen clamps at 64 - p)
+__device__ __forceinline__ uint32_t hll_enc32_entry(uint32_t v, int p) {
+    const uint32_t e = v >> 7, s = (uint32_t)(kP2 - p);
+    const uint32_t low = s ? (e & ((1u << s) - 1u)) : 0u;
+    const uint32_t rl = low ? (uint32_t)__builtin_clz(low) - (32u - s) + 1u : s + (v & 127u) + 1u;
+    return rl << 24 | (e >> s);
+}
+
 template <int KIND>
+__global__ __launch_bounds__(256) void hll_enc32_kernel(const void* col, uint32_t n, uint32_t* out) {
+    HllParams P{};
+    const uint32_t i0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+    if (i0 >= n) return;  // n is a multiple of 4 (the column's padding)
+    int64_t raw[4];
+    load_i64x4((const int64_t*)col, i0, raw);
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = hll_enc32(hll_fast_hash<KIND>(P, (uint64_t)raw[j]));
+    *(uint4*)(out + i0) = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+void launch_hll_enc32(const void* col, int kind, uint32_t n_pad, uint32_t* out, hipStream_t st) {
+    const dim3 g((n_pad / 4 + 255) / 256);
+    if (n_pad == 0) return;
+    if (kind == HLL_F64) hipLaunchKernelGGL(hll_enc32_kernel<HLL_F64>, g, dim3(256), 0, st, col, n_pad, out);
+    else hipLaunchKernelGGL(hll_enc32_kernel<HLL_I64>, g, dim3(256), 0, st, col, n_pad, out);
+}
+
+// E32: the enc32 words (4 bytes per doc) instead of the values, 8 docs per thread and buffer (the same bytes in flight)
+template <int KIND, bool E32>
 __global__ __launch_bounds__(kHllFsWG) void hll_fs_kernel(HllParams P, uint32_t per_wg, uint32_t check_iters) {
     extern __shared__ __attribute__((aligned(16))) uint32_t fs_lds[];
     uint32_t* rlog = fs_lds;                // [kHllFsLog] (rl << 24 | idx)
@@ -506,21 +573,40 @@ __global__ __launch_bounds__(kHllFsWG) void hll_fs_kernel(HllParams P, uint32_t 
     const uint32_t w1 = min(P.n_docs, w0 + per_wg);
     __syncthreads();
     if (w0 >= w1) return;  // workgroup-uniform
-    const uint32_t t4 = threadIdx.x * 4;
+    constexpr uint32_t kPer = E32 ? 8u : 4u;  // docs per thread and buffer
+    constexpr uint32_t kIt = kHllFsWG * kPer;
+    const uint32_t t4 = threadIdx.x * kPer;
     const uint32_t last4 = (w1 - 1) & ~3u;  // unconditional loads (see hll_registers_lds_kernel)
-    auto load = [&](uint32_t i0, uint64_t raw[4]) { load_i64x4((const int64_t*)P.col, min(i0, last4), (int64_t*)raw); };
+    auto load = [&](uint32_t i0, uint64_t raw[4]) {
+        if (E32) {  // two words per 64-bit slot: docs i0 + 2k and i0 + 2k + 1 in the low / high half of raw[k]
+            uint32_t w[8];
+            load_u32x4(P.enc32, min(i0, last4), w);
+            load_u32x4(P.enc32, min(i0 + 4, last4), w + 4);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) raw[k] = (uint64_t)w[2 * k] | (uint64_t)w[2 * k + 1] << 32;
+        } else {
+            load_i64x4((const int64_t*)P.col, min(i0, last4), (int64_t*)raw);
+        }
+    };
     // the thread's 4 hashes, then ONE log reservation per wave for all of the wave's entries (one returning LDS atomic
     // and one wait per 256 docs instead of one per doc slot); called by every thread of the workgroup
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t lt = (1ull << lane) - 1ull;
-    auto hash4 = [&](uint32_t i0, const uint64_t raw[4]) {
+    auto hash4 = [&](uint32_t i0, const uint64_t raw[4], int half) {
         const uint32_t lim = i0 < w1 ? w1 - i0 : 0u;
         uint32_t e[4], hit = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint64_t h = hll_fast_hash<KIND>(P, raw[j]);
-            const bool t = (uint32_t)j < lim && (h & zmask) == 0;
-            e[j] = (hll_run_len(h, P.p) << 24) | hll_index(h, P.p);
+            bool t;
+            if (E32) {
+                const uint32_t v = (uint32_t)(raw[(half * 4 + j) >> 1] >> (32 * (j & 1)));
+                e[j] = hll_enc32_entry(v, P.p);
+                t = (uint32_t)j < lim && (e[j] >> 24) > G;
+            } else {
+                const uint64_t h = hll_fast_hash<KIND>(P, raw[j]);
+                t = (uint32_t)j < lim && (h & zmask) == 0;
+                e[j] = (hll_run_len(h, P.p) << 24) | hll_index(h, P.p);
+            }
             hit |= (t ? 1u : 0u) << j;
         }
         const uint64_t m0 = __ballot(hit & 1u), m1 = __ballot(hit & 2u), m2 = __ballot(hit & 4u), m3 = __ballot(hit & 8u);
@@ -540,28 +626,33 @@ __global__ __launch_bounds__(kHllFsWG) void hll_fs_kernel(HllParams P, uint32_t 
             else atomicMax(&P.regs[e[j] & 0xFFFFFFu], e[j] >> 24);  // never expected: flushed at half full
         }
     };
+    // one buffer's docs: 4 (values) or 8 (enc32 words, two hash4 rounds)
+    auto take = [&](uint32_t i0, const uint64_t raw[4]) {
+        hash4(i0, raw, 0);
+        if (E32) hash4(i0 + 4, raw, 1);
+    };
     uint64_t a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
     load(w0 + t4, a);
     __builtin_amdgcn_sched_barrier(0);
-    load(w0 + kHllFsIter + t4, b);
+    load(w0 + kIt + t4, b);
     uint32_t it = 0;
 #if ESGPU_HLL_FS_NBUF == 3
     uint64_t c[4] = {0, 0, 0, 0};
     __builtin_amdgcn_sched_barrier(0);
-    load(w0 + 2 * kHllFsIter + t4, c);
-    for (uint32_t base = w0; base < w1; base += 3 * kHllFsIter) {
-        hash4(base + t4, a);
-        load(base + 3 * kHllFsIter + t4, a);
-        hash4(base + kHllFsIter + t4, b);
-        load(base + 4 * kHllFsIter + t4, b);
-        hash4(base + 2 * kHllFsIter + t4, c);
-        load(base + 5 * kHllFsIter + t4, c);
+    load(w0 + 2 * kIt + t4, c);
+    for (uint32_t base = w0; base < w1; base += 3 * kIt) {
+        take(base + t4, a);
+        load(base + 3 * kIt + t4, a);
+        take(base + kIt + t4, b);
+        load(base + 4 * kIt + t4, b);
+        take(base + 2 * kIt + t4, c);
+        load(base + 5 * kIt + t4, c);
 #else
-    for (uint32_t base = w0; base < w1; base += 2 * kHllFsIter) {
-        hash4(base + t4, a);
-        load(base + 2 * kHllFsIter + t4, a);
-        hash4(base + kHllFsIter + t4, b);
-        load(base + 3 * kHllFsIter + t4, b);
+    for (uint32_t base = w0; base < w1; base += 2 * kIt) {
+        take(base + t4, a);
+        load(base + 2 * kIt + t4, a);
+        take(base + kIt + t4, b);
+        load(base + 3 * kIt + t4, b);
 #endif
         if (++it == check_iters) {  // workgroup-uniform: every thread runs the same iterations
             it = 0;
@@ -895,19 +986,23 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
         static int per_cu = 0;
         if (!per_cu) {
             int b = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, hll_fs_kernel<HLL_I64>, kHllFsWG, hll_fs_lds_bytes()) != hipSuccess || b < 1)
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, hll_fs_kernel<HLL_I64, false>, kHllFsWG, hll_fs_lds_bytes()) != hipSuccess || b < 1)
                 b = 1;
             per_cu = b;
         }
         const uint64_t docs_per_check = ((uint64_t)kHllFsLog / 4) << (p.fs_f - 1);
-        uint32_t wgs = std::max(1u, std::min(cus * (uint32_t)per_cu, n / (kHllFsIter * ESGPU_HLL_FS_NBUF)));
+        const bool e32 = p.enc32 != nullptr && p.p <= kP2;
+        const uint32_t it_docs = kHllFsIter * (e32 ? 2u : 1u);  // docs per buffer and workgroup
+        uint32_t wgs = std::max(1u, std::min(cus * (uint32_t)per_cu, n / (it_docs * ESGPU_HLL_FS_NBUF)));
         const uint32_t per = ((n + wgs - 1) / wgs + 3) & ~3u;
         wgs = (n + per - 1) / per;
-        const uint32_t check = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, docs_per_check / (ESGPU_HLL_FS_NBUF * kHllFsIter)));
-        if (p.kind == HLL_I64)
-            hipLaunchKernelGGL(hll_fs_kernel<HLL_I64>, dim3(wgs), dim3(kHllFsWG), hll_fs_lds_bytes(), st, p, per, check);
+        const uint32_t check = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, docs_per_check / (ESGPU_HLL_FS_NBUF * it_docs)));
+        if (e32)
+            hipLaunchKernelGGL((hll_fs_kernel<HLL_I64, true>), dim3(wgs), dim3(kHllFsWG), hll_fs_lds_bytes(), st, p, per, check);
+        else if (p.kind == HLL_I64)
+            hipLaunchKernelGGL((hll_fs_kernel<HLL_I64, false>), dim3(wgs), dim3(kHllFsWG), hll_fs_lds_bytes(), st, p, per, check);
         else
-            hipLaunchKernelGGL(hll_fs_kernel<HLL_F64>, dim3(wgs), dim3(kHllFsWG), hll_fs_lds_bytes(), st, p, per, check);
+            hipLaunchKernelGGL((hll_fs_kernel<HLL_F64, false>), dim3(wgs), dim3(kHllFsWG), hll_fs_lds_bytes(), st, p, per, check);
         hipLaunchKernelGGL(hll_p0_gather_kernel, dim3(hll_p0_ranges(m)), dim3(1024), 0, st, p, 1);
         tail(p);
         return;
@@ -948,10 +1043,12 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
             uint32_t lw = std::max(1u, std::min(cus * per_cu, span / (kHllLdsIter * 4)));
             const uint32_t lper = ((span + lw - 1) / lw + 3) & ~3u;
             lw = (span + lper - 1) / lper;
-            if (p.kind == HLL_I64)
-                hipLaunchKernelGGL(hll_registers_lds_kernel<HLL_I64>, dim3(lw), dim3(kHllLdsWG), hll_lds_bytes(m, logr), st, q, cuts[ph], cuts[ph + 1], lper, fl);
+            if (q.enc32 && q.p <= kP2)
+                hipLaunchKernelGGL((hll_registers_lds_kernel<HLL_I64, true>), dim3(lw), dim3(kHllLdsWG), hll_lds_bytes(m, logr), st, q, cuts[ph], cuts[ph + 1], lper, fl);
+            else if (p.kind == HLL_I64)
+                hipLaunchKernelGGL((hll_registers_lds_kernel<HLL_I64, false>), dim3(lw), dim3(kHllLdsWG), hll_lds_bytes(m, logr), st, q, cuts[ph], cuts[ph + 1], lper, fl);
             else
-                hipLaunchKernelGGL(hll_registers_lds_kernel<HLL_F64>, dim3(lw), dim3(kHllLdsWG), hll_lds_bytes(m, logr), st, q, cuts[ph], cuts[ph + 1], lper, fl);
+                hipLaunchKernelGGL((hll_registers_lds_kernel<HLL_F64, false>), dim3(lw), dim3(kHllLdsWG), hll_lds_bytes(m, logr), st, q, cuts[ph], cuts[ph + 1], lper, fl);
         } else if (fast && p.kind == HLL_I64)
             hipLaunchKernelGGL(hll_registers_fast_kernel<HLL_I64>, dim3(wgs), dim3(kHllWG), 0, st, q, cuts[ph], cuts[ph + 1], per, fl);
         else if (fast && p.kind == HLL_F64)

@@ -186,6 +186,10 @@ struct HllParams {
     uint32_t fs_cap;
     unsigned int* fs_buf;
     unsigned int* unres;
+    // the floored stream's input in 4 bytes per doc instead of the 8-byte values (null: hash the values): per doc its
+    // hash's top kP2 = 25 bits and min(nlz(hash << 25), 39) -- the quantities HyperLogLogPlusPlus.encodeHash keeps
+    // (HyperLogLogPlusPlus.java:335-346), from which index and run length follow exactly for any p <= 25 (hll_enc32)
+    const uint32_t* enc32;
 };
 // floored stream: the floor F (kept hashes have run length >= F, a fraction 2^-(F-1) of the stream) for a request whose
 // registers will have seen `total` values when this segment is done: the largest F for which the expected number of
@@ -318,6 +322,8 @@ size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocn
 // resident workgroups per CU (hk: 0 none, 1 affine, 2 table; vk: bit 0 double histogram column, bit 1 double metric)
 int collect_occupancy(bool ord, int hk, int met, size_t lds, int vk, bool wide = false);
 void launch_hll(const HllParams& p, uint32_t cus, hipStream_t s);
+// the HllParams.enc32 form of a dense long / double column (n_pad entries: the column's padding included)
+void launch_hll_enc32(const void* col, int kind, uint32_t n_pad, uint32_t* out, hipStream_t s);
 
 // ---- multi-valued (CSR) columns, esgpu_kernels_multi.hip ----
 // K1/K4/K5/K6/K7 for SortedSet / SortedNumeric doc values: one doc per thread, every (ordinal x deduplicated key)

@@ -323,6 +323,9 @@ struct DevColumn {
     bool wide_released = false;
     const void* ord16_src = nullptr;
     bool d32_done = false, d16_done = false, b16_done = false;
+    // the floored HLL stream's 4-byte words of a dense long / double column (ensure_hll_enc32, HllParams.enc32)
+    DevBuf hll32;
+    bool hll32_done = false;
     // distinct values of the column, estimated from the HLL registers of an earlier request that collected this segment
     // alone and unfiltered (-1: none yet) -- picks the floored stream's floor (collect_hll); any value is correct
     // (shared: a plan that collected the segment keeps it alive for its build, whatever happens to the segment meanwhile)
@@ -3398,6 +3401,27 @@ static const DevColumn* ensure_b16(esgpu_ctx* c, const DevColumn* col, const esg
     return m;
 }
 
+// the enc32 words of a dense single-valued long / double column for the floored HLL stream (null: over the budget; cached
+// with the column like the compact columns, built once under the context lock)
+static const uint32_t* ensure_hll_enc32(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st) {
+    DevColumn* m = const_cast<DevColumn*>(col);
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (m->hll32_done) return m->hll32.as<uint32_t>();
+    m->hll32_done = true;
+    if (col->type == ESGPU_COL_ORD_U32 || col->multi || col->present.p) return nullptr;  // longs, unsigned longs, doubles
+    try {
+        m->hll32.alloc(c, (size_t)s->n_pad * 4);
+    } catch (const EsError&) {
+        m->hll32.release();
+        return nullptr;
+    }
+    const void* v = col->type == ESGPU_COL_F64 ? col->values.p : wide_i64_locked(c, m, s, st);
+    launch_hll_enc32(v, col->type == ESGPU_COL_F64 ? HLL_F64 : HLL_I64, s->n_pad, m->hll32.as<uint32_t>(), st);
+    HIPX(hipGetLastError());
+    HIPX(hipStreamSynchronize(st));
+    return m->hll32.as<uint32_t>();
+}
+
 static const uint16_t* ensure_d16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st) {
     DevColumn* m = const_cast<DevColumn*>(col);
     std::lock_guard<std::mutex> lk(c->mu);
@@ -3568,6 +3592,14 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
             H.fs_cap = cap;
             H.fs_buf = pl.fs_buf.as<unsigned int>();
             H.unres = pl.lc_count.as<unsigned int>() + 6;
+        }
+        // the floored stream and the LDS register phases read 4 bytes per doc (HllParams.enc32); phase 0 of a request's
+        // first 4 * 2^p values and the LC / tail pass still hash the values.  ESGPU_HLL_E32=0: the values (A/B runs)
+        static const bool e32_on = [] { const char* e = std::getenv("ESGPU_HLL_E32"); return !(e && *e == '0'); }();
+        if (e32_on && dense && pl.p <= kP2) H.enc32 = ensure_hll_enc32(p->ctx, col, s, p->stream);
+        if (H.enc32) {
+            const uint64_t n = s->max_doc, cold = F || pl.hll_seen >= (uint64_t)m * H.cut0 ? 0 : (uint64_t)m * H.cut0 - pl.hll_seen;
+            bytes = 4 * n + 4 * std::min(n, cold);  // phase 0's values are 8 bytes
         }
     }
     H.lc_mask = pl.lc_mask;
