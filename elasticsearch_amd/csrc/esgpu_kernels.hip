@@ -931,7 +931,7 @@ uint32_t hll_fs_cap(uint64_t n, int p, uint32_t f) {
     return (uint32_t)std::min(c, 4.0e9) & ~3u;
 }
 
-void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
+bool launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
     const uint32_t n = p.n_docs;
     const uint32_t m = 1u << p.p;
     // phases [0, 4m), then x4 each: every register has seen ~4 hashes after the first cut, so the floor (min
@@ -1004,13 +1004,13 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
         else
             hipLaunchKernelGGL((hll_fs_kernel<HLL_F64, false>), dim3(wgs), dim3(kHllFsWG), hll_fs_lds_bytes(), st, p, per, check);
         hipLaunchKernelGGL(hll_p0_gather_kernel, dim3(hll_p0_ranges(m)), dim3(1024), 0, st, p, 1);
-        tail(p);
-        return;
+        tail(p);  // its raises (registers below the floor) keep the gather's floors and snapshot lower bounds
+        return true;
     }
     HllParams q = p;  // the phases (fs_f = 0 for their gathers)
     q.fs_f = 0;
     const bool warm = p.seen >= (uint64_t)m * cut0;  // the registers already passed the first cut
-    if (warm) refresh();
+    if (warm && !p.snap_ok) refresh();
 #ifndef ESGPU_HLL_P0
 #define ESGPU_HLL_P0 1
 #endif
@@ -1069,7 +1069,8 @@ void launch_hll(const HllParams& p, uint32_t cus, hipStream_t st) {
         (void)hipMemsetAsync(p.nonzero, 0, 4, st);  // recount over the registers (they accumulate across segments)
         hipLaunchKernelGGL(hll_nonzero_kernel, dim3(floor_grid), dim3(1024), 0, st, (const unsigned int*)p.regs, m, p.nonzero);
     }
-    tail(q);
+    tail(q);  // fs_f = 0: reads the registers only
+    return counted;  // the last phase's gather wrote the floors and snapshot of the final registers
 }
 
 // ------------------------------------------------------------------------------------------------------------

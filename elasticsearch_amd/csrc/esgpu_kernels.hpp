@@ -190,6 +190,10 @@ struct HllParams {
     // hash's top kP2 = 25 bits and min(nlz(hash << 25), 39) -- the quantities HyperLogLogPlusPlus.encodeHash keeps
     // (HyperLogLogPlusPlus.java:335-346), from which index and run length follow exactly for any p <= 25 (hll_enc32)
     const uint32_t* enc32;
+    // the group floors and snapshot already hold lower bounds of the registers as they stand (this request's previous
+    // segment ended with a gather, which writes them; later raises keep them lower bounds): a warm segment skips its
+    // refresh launch
+    int32_t snap_ok;
 };
 // floored stream: the floor F (kept hashes have run length >= F, a fraction 2^-(F-1) of the stream) for a request whose
 // registers will have seen `total` values when this segment is done: the largest F for which the expected number of
@@ -321,7 +325,9 @@ void launch_zone_keys(const CollectParams& p, int64_t* out, hipStream_t s, unsig
 size_t collect_lds_bytes(uint32_t T, uint32_t W, int met, int vcnt_mode, int ocnt_mode, uint32_t ncopies = 1, bool pi = false);
 // resident workgroups per CU (hk: 0 none, 1 affine, 2 table; vk: bit 0 double histogram column, bit 1 double metric)
 int collect_occupancy(bool ord, int hk, int met, size_t lds, int vk, bool wide = false);
-void launch_hll(const HllParams& p, uint32_t cus, hipStream_t s);
+// returns whether the group floors and snapshot are left as lower bounds of the registers (HllParams.snap_ok for the
+// request's next segment)
+bool launch_hll(const HllParams& p, uint32_t cus, hipStream_t s);
 // the HllParams.enc32 form of a dense long / double column (n_pad entries: the column's padding included)
 void launch_hll_enc32(const void* col, int kind, uint32_t n_pad, uint32_t* out, hipStream_t s);
 

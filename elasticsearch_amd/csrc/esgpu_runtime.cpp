@@ -996,6 +996,7 @@ struct Pipeline {
     DevBuf lc_first;                 // [lc_mask + 1] u64: insertion order of each LC set entry (HllParams.lc_first)
     uint32_t lc_mask = 0, lc_threshold = 0;
     uint64_t hll_seen = 0;           // values hashed into the registers by earlier segments of this request
+    bool hll_snap_ok = false;        // the last launch_hll left the group floors and snapshot as register lower bounds
     // the request's first segment, when it was collected dense (its registers alone then estimate its distinct values at
     // build), the segments collected, and the largest distinct estimate among them
     std::shared_ptr<std::atomic<double>> hll_d1;
@@ -3607,6 +3608,7 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
     H.lc_first = pl.lc_first.as<unsigned long long>();
     H.pos_base = (uint64_t)p->seg_seq << 40;
     H.seen = pl.hll_seen;
+    H.snap_ok = pl.hll_seen > 0 && pl.hll_snap_ok;
     if (H.n_docs == 0) return false;
     if (pl.hll_seen == 0) {
         const bool dense1 = !H.accept && H.npred == 0 && !H.present && !col->multi && H.kind != HLL_ORD;
@@ -3619,7 +3621,7 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
     pl.hll_seen += H.n_docs;
     pl.lc_dirty = true;
     HIPX(hipEventRecord(pl.e0, p->stream));
-    launch_hll(H, (uint32_t)p->ctx->cus, p->stream);
+    pl.hll_snap_ok = launch_hll(H, (uint32_t)p->ctx->cus, p->stream);
     HIPX(hipGetLastError());
     HIPX(hipEventRecord(pl.e1, p->stream));
     p->last_bytes += bytes;
@@ -5382,6 +5384,7 @@ extern "C" int esgpu_plan_reset(esgpu_plan* p) {
                 pl.h_regs.clear();
                 pl.any_value = false;
                 pl.hll_seen = 0;
+                pl.hll_snap_ok = false;
                 pl.hll_d1.reset();
                 pl.hll_nseg = 0;
                 continue;
