@@ -3583,7 +3583,11 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
             return e && *e ? (uint64_t)std::atoll(e) : (uint64_t)1024;
         }();
         const bool fs_size = (uint64_t)H.n_docs <= fs_max_per_reg * m;
-        uint32_t F = fs_mode && dense && fs_size && dknown >= 0 ? hll_fs_floor((uint64_t)dknown, pl.p, fs_minf) : 0u;
+        // a warm segment (a later segment of the request, the registers past the first cut) takes the one LDS phase
+        // that remains: 0.098 ms + its gather at 125M docs against the stream's 0.135 ms + its gather
+        // (profiles/r5/hll32); a raised floor (fs_mode > 1, the tail pass's test leg) keeps the stream
+        const bool fs_warm_ok = pl.hll_seen < (uint64_t)m * H.cut0 || fs_mode > 1;
+        uint32_t F = fs_mode && dense && fs_size && fs_warm_ok && dknown >= 0 ? hll_fs_floor((uint64_t)dknown, pl.p, fs_minf) : 0u;
         if (F && fs_mode > 1) F = std::min<uint32_t>(F + (uint32_t)fs_mode - 1, 64u - (uint32_t)pl.p);
         if (F) {
             const uint32_t cap = hll_fs_cap(H.n_docs, pl.p, F);
