@@ -1000,6 +1000,10 @@ struct Pipeline {
     // the request's first segment, when it was collected dense (its registers alone then estimate its distinct values at
     // build), the segments collected, and the largest distinct estimate among them
     std::shared_ptr<std::atomic<double>> hll_d1;
+    // the registers right after that first segment, kept when more segments may follow and its distinct count is not
+    // known yet: estimated at build, so the segment's next request can take the floored stream
+    DevBuf hll_r1;
+    bool hll_r1_pending = false;
     int hll_nseg = 0;
     double hll_dmax = 0.0;
     bool lc_dirty = true;            // lc_set / lc_first may hold entries (cleared at reset only then)
@@ -3627,6 +3631,12 @@ static bool collect_hll(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, con
     HIPX(hipEventRecord(pl.e0, p->stream));
     pl.hll_snap_ok = launch_hll(H, (uint32_t)p->ctx->cus, p->stream);
     HIPX(hipGetLastError());
+    if (pl.hll_nseg == 1 && pl.hll_d1 && pl.hll_d1->load() < 0 && pl.p >= 12) {
+        const size_t rb = (size_t)4 << pl.p;
+        if (pl.hll_r1.bytes < rb) pl.hll_r1.alloc(p->ctx, rb);
+        HIPX(hipMemcpyAsync(pl.hll_r1.p, pl.regs.p, rb, hipMemcpyDeviceToDevice, p->stream));
+        pl.hll_r1_pending = true;
+    }
     HIPX(hipEventRecord(pl.e1, p->stream));
     p->last_bytes += bytes;
     p->last_path = 3;
@@ -3811,6 +3821,18 @@ extern "C" int esgpu_plan_post_collection(esgpu_plan* p) {
                 if (pl.hll_nseg == 1 && pl.hll_d1 && pl.hll_d1->load() < 0) {
                     // the raw HyperLogLog estimate of the segment's distinct values (once per segment: the floored
                     // stream's floor on later requests)
+                    double z = 0.0;
+                    for (uint32_t i = 0; i < m; ++i) z += std::ldexp(1.0, -(int)r[i]);
+                    const double alpha = 0.7213 / (1.0 + 1.079 / m);
+                    pl.hll_d1->store(alpha * (double)m * (double)m / z);
+                }
+            }
+            if (pl.hll_r1_pending) {  // a merged request: the first segment's own registers estimate its distinct values
+                pl.hll_r1_pending = false;
+                if (pl.hll_nseg > 1 && pl.hll_d1 && pl.hll_d1->load() < 0) {
+                    d2h_u64(p, p->h_dst[0], pl.hll_r1.p, (size_t)m / 2);
+                    const uint32_t* r = p->h_dst[0].as<uint32_t>();
+                    bsync(p);
                     double z = 0.0;
                     for (uint32_t i = 0; i < m; ++i) z += std::ldexp(1.0, -(int)r[i]);
                     const double alpha = 0.7213 / (1.0 + 1.079 / m);
@@ -5389,6 +5411,7 @@ extern "C" int esgpu_plan_reset(esgpu_plan* p) {
                 pl.any_value = false;
                 pl.hll_seen = 0;
                 pl.hll_snap_ok = false;
+                pl.hll_r1_pending = false;
                 pl.hll_d1.reset();
                 pl.hll_nseg = 0;
                 continue;
