@@ -668,7 +668,7 @@ __device__ __forceinline__ void runs_reset(Runs<NR>& R) {
 // the hot ordinal's run into its LDS cell (before a window moves, and at the end)
 template <int MET, int NR>
 __device__ __forceinline__ void pi_hot_flush(const CollectParams& P, const Acc& a, Runs<NR>& R, uint32_t T) {
-    if (R.hslot != ~0u) {
+    if (R.hslot != ~0u && R.hpk) {
         const uint32_t c = R.hslot * T + P.hot_t;
         atomicAdd(&a.pk[c + a.coff], R.hpk);
         if (MET >= 2) {
@@ -1154,6 +1154,113 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
     }
 }
 
+// Packed-cell raw-load kernels over block-delta keys (VK bits 64 | 8192), a full zone block whose docs all round to one
+// key (99.4 % of the north star's blocks at 1B docs): the key slot is wave-uniform, so a doc's cell is slot * T + its
+// ordinal and nothing else is computed per doc -- no key arithmetic, no per-doc slot selects, no tail mask (the caller
+// takes this path for full blocks only), and the packed add's high word is a constant: pk_shift >= 33 (pi_fits: a
+// workgroup range holds < 2^31 docs), so `one + delta` is the pair {delta, one >> 32}.  NH = 1 or 2 Doc4 halves of one
+// step, processed together (their LDS reads issued before the adds).
+#ifndef ESGPU_PI_UFAST  // (A/B) 0: the general per-doc path for these blocks too
+#define ESGPU_PI_UFAST 1
+#endif
+#ifndef ESGPU_PI_HOTU  // (A/B) the segment's most frequent ordinal counted and summed in registers in uniform blocks
+#define ESGPU_PI_HOTU 0
+#endif
+#ifndef ESGPU_PI_MMU  // (A/B) uniform blocks' (min, max) updates: 2 = one divergent region per doc (as ESGPU_PI_MMCHECK 2),
+#define ESGPU_PI_MMU 2  // 3 = branch-free -- every lane issues both atomics, lanes whose bounds do not move on a spare word
+#endif
+template <int MET, int VK, int NH, int NR>
+__device__ __forceinline__ void pi_uniform(const CollectParams& P, const Acc& a, const Doc4& h0, const Doc4& h1, uint32_t T,
+                                           uint32_t win0, Runs<NR>& run, uint32_t mw, bool outer) {
+    constexpr int N = 4 * NH;
+    const uint32_t k = h0.ukey;  // wave-uniform (zone_ukey: scalar loads)
+    const uint32_t sl = k - win0;
+    const bool in = k < P.H && sl < (mw ? mw : P.W);
+    uint32_t t[N], dv[N];
+    uint32_t okm = (1u << N) - 1u;  // bit j: doc j passes the folded accept bitset (VK bit 512)
+#pragma unroll
+    for (int hh = 0; hh < NH; ++hh) {
+        const Doc4& h = hh == 0 ? h0 : h1;
+        t[4 * hh + 0] = h.raw[0] & 0xFFFFu; t[4 * hh + 1] = h.raw[0] >> 16;
+        t[4 * hh + 2] = h.raw[1] & 0xFFFFu; t[4 * hh + 3] = h.raw[1] >> 16;
+        dv[4 * hh + 0] = h.raw[6] & 0xFFFFu; dv[4 * hh + 1] = h.raw[6] >> 16;
+        dv[4 * hh + 2] = h.raw[7] & 0xFFFFu; dv[4 * hh + 3] = h.raw[7] >> 16;
+        if constexpr ((VK & 512) != 0) okm &= ~((~(uint32_t)(h.racc >> (h.doc0 & 63)) & 0xFu) << (4 * hh));
+    }
+    // outer counts (wave-uniform mode): per-term counts need every doc; a per-key count is the wave's passing docs
+    if (P.ocnt_mode == OCNT_TERMS) {
+        if (outer)
+#pragma unroll
+            for (int j = 0; j < N; ++j)
+                if (((okm >> j) & 1) && t[j] < T) atomicAdd(&a.ocnt32[t[j]], 1u);
+    } else if (P.ocnt_mode == OCNT_HIST) {
+        if (in) {
+            const uint32_t tot = wave_sum_u32((uint32_t)__builtin_popcount(okm));
+            if ((threadIdx.x & 63) == 0 && tot) atomicAdd(&a.ocnt32[sl], tot);
+        }
+    }
+    if (!in) return;
+    const uint32_t cb = sl * T;  // the block's row of cells
+    const uint32_t onehi = (uint32_t)(1ull << (P.pk_shift - 32));
+    bool hit[N], hpk[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        hit[j] = ((okm >> j) & 1) && t[j] < T;  // (a missing ordinal, 0xFFFF, is >= T)
+        hpk[j] = hit[j];
+    }
+#if ESGPU_PI_HOTU
+    if (sl != run.hslot) {  // (uniform) the hot ordinal's register run moves to this key
+        pi_hot_flush<MET>(P, a, run, T);
+        run.hslot = sl;
+    }
+    {
+        const uint32_t ht = P.hot_t;
+        uint32_t hc = 0, hs = 0;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const bool ho = hit[j] && t[j] == ht;
+            hc += ho ? 1u : 0u;
+            hs += ho ? dv[j] : 0u;
+            hpk[j] = hit[j] && !ho;
+        }
+        run.hpk += ((unsigned long long)hc << P.pk_shift) + hs;
+    }
+#endif
+    uint32_t mlo[N], mhi[N];
+    if (MET >= 2) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const u32x2_t m = *reinterpret_cast<const u32x2_t*>(a.mm + 2 * (hit[j] ? cb + t[j] : 0u));
+            mlo[j] = m.x;
+            mhi[j] = m.y;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j)  // (a miss adds into the lane's spare word)
+        atomicAdd(hpk[j] ? &a.pk[cb + t[j] + a.coff] : a.pkd, join64(dv[j], onehi));
+    if (MET >= 2) {
+#if ESGPU_PI_MMU == 3
+        uint32_t* spare = reinterpret_cast<uint32_t*>(a.pkd);
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const bool mv = hit[j] && (dv[j] < mlo[j] || dv[j] > mhi[j]);
+            uint32_t* w = mv ? &a.mm[2 * (cb + t[j])] : spare;
+            atomicMin(w, dv[j]);
+            atomicMax(w + 1, dv[j]);
+        }
+#else
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const bool mv = hit[j] && (dv[j] < mlo[j] || dv[j] > mhi[j]);
+            if (mv) {
+                atomicMin(&a.mm[2 * (cb + t[j])], dv[j]);
+                atomicMax(&a.mm[2 * (cb + t[j]) + 1], dv[j]);
+            }
+        }
+#endif
+    }
+}
+
 // packed integer cells (VK bit 64): decoded into the grid's u64 counts, f64 sums (the exact integer sum of the cell's
 // values, count * base + sum of deltas) and order-preserving extrema of (double) values -- (double) is monotonic on
 // longs, so the min / max of the casts are the casts of the min / max
@@ -1342,6 +1449,8 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
     // compiler keeps them in the LDS address space (ds_* instructions).  A generic pointer would compile to flat_*
     // accesses, and each flat load waits for vmcnt(0): the prefetched loads of the next iteration.
     constexpr bool PI = MET > 0 && (VK & 64) != 0;  // packed integer cells
+    // ... over block-delta keys: full single-key zone blocks take pi_uniform
+    constexpr bool kPIU = ESGPU_PI_UFAST != 0 && PI && HIST && !HORD && (VKL & 8192) != 0 && kRawPI<MET, VKL, HIST>;
     Acc s;
     s.sum_lo = nullptr; s.sq_lo = nullptr;
     if constexpr (PI) {  // collect_lds_bytes(pi = true) mirrors this carve
@@ -1474,7 +1583,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
     auto slide_to = [&](uint32_t k0) {
         if (dirty) {
             if (!ORD) runs_flush<MET, kMS, runs_for<MET, VKL>(), kIntRuns<ORD, MET, VKL>>(P, s, run);
-            if constexpr (PI && ESGPU_PI_HOT) pi_hot_flush<MET>(P, s, run, T);
+            if constexpr (PI && (ESGPU_PI_HOT || ESGPU_PI_HOTU)) pi_hot_flush<MET>(P, s, run, T);
             if constexpr (PI) flush_window_pi<MET, WGS>(P, s, T, W, win0, ncp);
             else flush_window<MET, kMS, WGS>(P, s, T, W, win0, ncp);
         }
@@ -1528,6 +1637,17 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
                 }
             }
         }
+        if constexpr (kPIU) {
+            // packed cells, a full zone block of one key (wave-uniform test): the uniform-slot path
+            const Doc4* qa;
+            const Doc4* qz;
+            if constexpr (WIDE8) { qa = &q.a; qz = &q.b; } else { qa = &q; qz = &q; }
+            if (use_lds && qa->ukey != kNoUKey && (uint32_t)__builtin_amdgcn_readlane((int)qz->doc0, 63) + 4u <= P.n_docs) {
+                pi_uniform<MET, VKL, WIDE8 ? 2 : 1>(P, s, *qa, *qz, T, win0, run, npass > 1 ? W : 0u, pass == 0);
+                dirty = true;
+                goto prefetch;
+            }
+        }
         if (use_lds) {
             if constexpr (WIDE8) {
                 process4<ORD, HIST, MET, true, KT, kMS, HORD, VKL>(P, s, q.a, T, base, win0, run, npass > 1 ? W : 0u, pass == 0);
@@ -1546,6 +1666,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
         }
         // prefetch kBuf iterations ahead along the schedule (next block of the group, the group's next pass, or the
         // next group)
+    prefetch:
         uint32_t nit = it + kBuf, nb = cb;
         if (nit >= (uint32_t)kItersPerBlockW) {
             nit -= kItersPerBlockW;
@@ -1586,7 +1707,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
 #endif
     if (P.lds_mode && (dirty || !(HIST && P.windowed)) && !ESGPU_FLUSH_DIAG) {
         if (!ORD) runs_flush<MET, kMS, runs_for<MET, VKL>(), kIntRuns<ORD, MET, VKL>>(P, s, run);
-        if constexpr (PI && ESGPU_PI_HOT) pi_hot_flush<MET>(P, s, run, T);
+        if constexpr (PI && (ESGPU_PI_HOT || ESGPU_PI_HOTU)) pi_hot_flush<MET>(P, s, run, T);
         if constexpr (PI) flush_window_pi<MET, WGS>(P, s, T, W, win0, ncp);
         else flush_window<MET, kMS, WGS>(P, s, T, W, win0, ncp);
     }

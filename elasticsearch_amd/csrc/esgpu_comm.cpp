@@ -96,6 +96,16 @@ struct RcclCollective : Collective {
         allgather_bytes += bytes * nranks;
         ++collectives;
     }
+    void allreduce_dev(void* d_buf, uint64_t count, int dt, int op, void* stream) override {
+        if (!count) return;
+        Clock clk(*this);
+        HIPX(hipSetDevice(ctx->device));
+        const ncclDataType_t t = dt == ESGPU_DT_U8 ? ncclUint8 : dt == ESGPU_DT_I64 ? ncclInt64 : dt == ESGPU_DT_U64 ? ncclUint64 : ncclFloat64;
+        const ncclRedOp_t o = op == ESGPU_RED_SUM ? ncclSum : op == ESGPU_RED_MIN ? ncclMin : ncclMax;
+        NCCLX(ncclAllReduce(d_buf, d_buf, count, t, o, comm, (hipStream_t)stream));  // in place, on the caller's stream
+        allreduce_bytes += count * dt_size(dt);
+        ++collectives;
+    }
 };
 
 // a caller's transport (esgpu_comm_init_host)
@@ -125,6 +135,40 @@ struct HostCollective : Collective {
         allgather(hi, ho, bytes);
         HIPX(hipMemcpyAsync(d_out, ho, bytes * nranks, hipMemcpyHostToDevice, st));
         HIPX(hipStreamSynchronize(st));  // the staging buffer is reused by the next call
+    }
+    void allreduce_dev(void* d_buf, uint64_t count, int dt, int op, void* stream) override {
+        if (!count) return;
+        hipStream_t st = (hipStream_t)stream;
+        const size_t bytes = count * dt_size(dt);
+        void* h = h_in.ensure(bytes);
+        HIPX(hipMemcpyAsync(h, d_buf, bytes, hipMemcpyDeviceToHost, st));
+        HIPX(hipStreamSynchronize(st));
+        allreduce(h, count, dt, op);
+        HIPX(hipMemcpyAsync(d_buf, h, bytes, hipMemcpyHostToDevice, st));
+        HIPX(hipStreamSynchronize(st));
+    }
+};
+
+// a device buffer of the in-process transport (no context: its ranks' contexts are their own), grown on demand
+struct RawDev {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int dev = 0;
+    void* ensure_raw(size_t n) {
+        if (n > bytes) {
+            if (p) HIPX(hipFree(p));
+            p = nullptr;
+            HIPX(hipGetDevice(&dev));
+            HIPX(hipMalloc(&p, n));
+            bytes = n;
+        }
+        return p;
+    }
+    ~RawDev() {
+        if (p) {
+            (void)hipSetDevice(dev);
+            (void)hipFree(p);
+        }
     }
 };
 
@@ -231,6 +275,44 @@ struct LocalCollective : Collective {
         allgather_bytes += bytes * nranks;
         ++collectives;
     }
+    RawDev d_stage, d_red;
+    void allreduce_dev(void* d_buf, uint64_t count, int dt, int op, void* stream) override {
+        if (!count) return;
+        Clock clk(*this);
+        hipStream_t st = (hipStream_t)stream;
+        const size_t bytes = count * dt_size(dt);
+        if (!ready) HIPX(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+        HIPX(hipEventRecord(ready, st));
+        int d = 0;
+        HIPX(hipGetDevice(&d));
+        g->src[rank] = d_buf;
+        g->ready[rank] = ready;
+        g->dev[rank] = d;
+        g->barrier();
+        bool one_device = nranks <= esgpu::kColoMaxShards;
+        for (int r = 0; r < nranks; ++r) {
+            one_device = one_device && g->dev[r] == d;
+            if (r != rank) HIPX(hipStreamWaitEvent(st, g->ready[r], 0));
+        }
+        // every rank reduces all operands (rank order, as the host transport does) into its own scratch, and writes its
+        // buffer only after every rank has read every operand
+        void* red = d_red.ensure_raw(bytes);
+        std::vector<const void*> srcs(g->src.begin(), g->src.end());
+        if (!one_device) {  // operands on other devices: copied here first
+            uint8_t* stage = (uint8_t*)d_stage.ensure_raw(bytes * nranks);
+            for (int r = 0; r < nranks; ++r) {
+                HIPX(hipMemcpyAsync(stage + (size_t)r * bytes, g->src[r], bytes, hipMemcpyDeviceToDevice, st));
+                srcs[r] = stage + (size_t)r * bytes;
+            }
+        }
+        launch_reduce_bufs(srcs.data(), nranks, count, dt, op, red, st);
+        HIPX(hipGetLastError());
+        HIPX(hipStreamSynchronize(st));
+        g->barrier();
+        HIPX(hipMemcpyAsync(d_buf, red, bytes, hipMemcpyDeviceToDevice, st));
+        allreduce_bytes += bytes;
+        ++collectives;
+    }
 };
 
 }  // namespace
@@ -290,7 +372,16 @@ extern "C" int esgpu_comm_init_local(const char* group, int32_t nranks, int32_t 
             std::lock_guard<std::mutex> lk(g_local_mu);
             std::weak_ptr<LocalGroup>& w = g_local_groups[group];
             g = w.lock();
-            if (!g || g->n != nranks) {
+            bool broken = false;
+            if (g) {
+                std::lock_guard<std::mutex> glk(g->mu);
+                broken = g->broken;
+            }
+            if (g && !broken) {
+                // the ranks of one live group must agree on its size: replacing it would strand the ranks already in it
+                require(g->n == nranks, ESGPU_ERR_INVALID, "in-process communicator: the group is alive with another rank count");
+            } else {
+                // a new group, or a name whose group broke (a rank timed out; its ranks all fail): the name is reusable
                 g = std::make_shared<LocalGroup>();
                 g->n = nranks;
                 g->src.assign(nranks, nullptr);

@@ -1415,6 +1415,139 @@ void launch_gather_bufs(const void* const* srcs, int n, size_t bytes, void* dst,
     hipLaunchKernelGGL(gather_bufs_kernel, dim3(grid), dim3(256), 0, st, G);
 }
 
+// the in-process transport's all-reduce: dst[i] = src[0][i] (op) src[1][i] (op) ... in rank order (dtype: 0 u8, 1 i64,
+// 2 u64, 3 f64; op: 0 sum, 1 min, 2 max -- include/esgpu.h ESGPU_DT_* / ESGPU_RED_*)
+struct ReduceBufs {
+    const void* src[kColoMaxShards];
+    void* dst;
+    uint64_t count;
+    uint32_t n;
+    int dt, op;
+};
+template <class T>
+__device__ __forceinline__ T red_op(T a, T b, int op) {
+    return op == 0 ? (T)(a + b) : op == 1 ? (b < a ? b : a) : (b > a ? b : a);
+}
+template <class T>
+__device__ void reduce_bufs_t(const ReduceBufs& R) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < R.count; i += (uint64_t)gridDim.x * 256) {
+        T a = ((const T*)R.src[0])[i];
+        for (uint32_t r = 1; r < R.n; ++r) a = red_op(a, ((const T*)R.src[r])[i], R.op);
+        ((T*)R.dst)[i] = a;
+    }
+}
+__global__ __launch_bounds__(256) void reduce_bufs_kernel(ReduceBufs R) {
+    switch (R.dt) {
+        case 0: reduce_bufs_t<uint8_t>(R); break;
+        case 1: reduce_bufs_t<long long>(R); break;
+        case 2: reduce_bufs_t<unsigned long long>(R); break;
+        default: reduce_bufs_t<double>(R); break;
+    }
+}
+void launch_reduce_bufs(const void* const* srcs, int n, uint64_t count, int dt, int op, void* dst, hipStream_t st) {
+    if (n <= 0 || count == 0) return;
+    ReduceBufs R{};
+    for (int r = 0; r < n && r < kColoMaxShards; ++r) R.src[r] = srcs[r];
+    R.dst = dst;
+    R.count = count;
+    R.n = (uint32_t)std::min(n, kColoMaxShards);
+    R.dt = dt;
+    R.op = op;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((count + 255) / 256, 2048);
+    hipLaunchKernelGGL(reduce_bufs_kernel, dim3(grid), dim3(256), 0, st, R);
+}
+
+// ---- the reduce across ranks of a top-level cardinality (esgpu_comm_build_reduce) --------------------------------
+// this rank's local shard plans' u32 registers maxed into one u8 array (HyperLogLogPlusPlus.merge's register max,
+// HyperLogLogPlusPlus.java:223-228) followed by the 64-byte tail the all-reduce (max) carries: [0] some local shard
+// collected a value, [1] some local shard is in HYPERLOGLOG (post_collection's decision from its counters), bytes 8-15 /
+// 16-23 the request's shape hash and its complement (after a max over the ranks, equal hashes read back as h and ~h);
+// and every local plan's two counters copied to pinned memory (lc_out[2 * i ...]).
+__global__ __launch_bounds__(256) void xr_card_pack_kernel(XrCardPack K) {
+    const uint32_t m = K.m;
+    if (blockIdx.x == 0 && threadIdx.x < 2 * K.n) {
+        const uint32_t s = threadIdx.x / 2;
+        K.lc_out[threadIdx.x] = K.cnt[s] ? K.cnt[s][threadIdx.x % 2] : 0u;
+    }
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < m + kXrCardTail; i += gridDim.x * 256) {
+        if (i < m) {
+            uint32_t v = 0;
+            for (uint32_t s = 0; s < K.n; ++s)
+                if (K.regs[s]) v = max(v, K.regs[s][i]);
+            K.out[i] = (uint8_t)v;
+        } else {
+            const uint32_t t = i - m;
+            uint8_t b = 0;
+            if (t == 0 || t == 1) {
+                for (uint32_t s = 0; s < K.n; ++s) {
+                    if (!K.cnt[s]) continue;
+                    const uint32_t c0 = K.cnt[s][0], c1 = K.cnt[s][1];
+                    if (t == 0 && (c0 > 0 || c1 > 0)) b = 1;
+                    if (t == 1 && !(c1 <= K.thr && c0 <= K.thr)) b = 1;
+                }
+            } else if (t >= 8 && t < 16) {
+                b = (uint8_t)(K.hash >> (8 * (t - 8)));
+            } else if (t >= 16 && t < 24) {
+                b = (uint8_t)(~K.hash >> (8 * (t - 16)));
+            }
+            K.out[i] = b;
+        }
+    }
+}
+void launch_xr_card_pack(const XrCardPack& K, hipStream_t st) {
+    const uint32_t total = K.m + kXrCardTail;
+    hipLaunchKernelGGL(xr_card_pack_kernel, dim3(std::min<uint32_t>(1024, (total + 255) / 256)), dim3(256), 0, st, K);
+}
+// the all-reduced registers + tail into pinned memory, and the non-zero registers counted into nz (zeroed before)
+__global__ __launch_bounds__(256) void xr_card_finish_kernel(const uint8_t* regs, uint32_t m, unsigned long long* dst,
+                                                              uint32_t* nz) {
+    const uint32_t words = (m + kXrCardTail) / 8;
+    uint32_t c = 0;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < words; i += gridDim.x * 256) {
+        const unsigned long long w = reinterpret_cast<const unsigned long long*>(regs)[i];
+        dst[i] = w;
+        if (i < m / 8)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) c += ((w >> (8 * k)) & 0xFF) != 0;
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(nz, c);
+}
+void launch_xr_card_finish(const uint8_t* regs, uint32_t m, unsigned long long* dst, uint32_t* nz, hipStream_t st) {
+    const uint32_t words = (m + kXrCardTail) / 8;
+    hipLaunchKernelGGL(xr_card_finish_kernel, dim3(std::min<uint32_t>(256, (words + 255) / 256)), dim3(256), 0, st, regs, m,
+                       dst, nz);
+}
+
+// ---- the reduce across ranks of a plain terms aggregation (config 3) ----------------------------------------------
+// a shard's GPU top-k output (K3: k keys, count << 32 | ~ordinal for count-descending order, then the sum of every
+// ordinal's count) turned into the selection record the other ranks all-gather: {picks, other-doc count,
+// count << 32 | ordinal ...} -- what build_terms_root makes of the same keys on the host (picks end at the first zero
+// key; other = the sum minus the picks' counts)
+__global__ void xr_terms_record_kernel(const unsigned long long* keys, uint32_t kk, uint32_t k_req, int order,
+                                       unsigned long long* rec, uint32_t K) {
+    if (threadIdx.x != 0) return;
+    unsigned long long picks = 0, taken = 0;
+    for (uint32_t i = 0; i < k_req && i < K; ++i) {
+        const unsigned long long key = keys[i];
+        if (key == 0) break;
+        const uint32_t lo = (uint32_t)key;
+        const uint32_t ord = order == 3 /* ESGPU_ORDER_TERM_DESC */ ? lo : 0xFFFFFFFFu - lo;
+        const unsigned long long hi = (key >> 32) & 0x7FFFFFFFull;
+        const unsigned long long cnt = order == 1 /* ESGPU_ORDER_COUNT_ASC */ ? 0x7FFFFFFFull - hi : hi;
+        rec[2 + picks] = (cnt << 32) | ord;
+        taken += cnt;
+        ++picks;
+    }
+    for (uint32_t i = (uint32_t)picks; i < K; ++i) rec[2 + i] = 0;
+    rec[0] = picks;
+    rec[1] = keys[kk] - taken;
+}
+void launch_xr_terms_record(const unsigned long long* keys, uint32_t kk, uint32_t k_req, int order, unsigned long long* rec,
+                            uint32_t K, hipStream_t st) {
+    hipLaunchKernelGGL(xr_terms_record_kernel, dim3(1), dim3(64), 0, st, keys, kk, k_req, order, rec, K);
+}
+
 void launch_colo_merge(const ColoParams& p, hipStream_t st) {
     if (p.R == 0 || p.Hm == 0) return;
     hipLaunchKernelGGL(colo_merge_kernel, dim3((p.Hm + 255) / 256, p.R), dim3(256), 0, st, p);

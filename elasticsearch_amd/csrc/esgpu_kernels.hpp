@@ -291,6 +291,27 @@ void launch_colo_pack(const ColoPackParams& p, hipStream_t s);
 // the in-process transport's all-gather on one device: rank r's `bytes` (a multiple of 8) from srcs[r] into dst + r * bytes,
 // one launch for every rank (n <= kColoMaxShards)
 void launch_gather_bufs(const void* const* srcs, int n, size_t bytes, void* dst, hipStream_t s);
+// dst = the n buffers (count elements of dtype ESGPU_DT_*) combined element-wise by op ESGPU_RED_*, in rank order
+void launch_reduce_bufs(const void* const* srcs, int n, uint64_t count, int dt, int op, void* dst, hipStream_t s);
+// the reduce across ranks of a top-level cardinality (esgpu_comm_build_reduce): the local plans' u32 registers maxed into
+// out[0, m) as bytes, then a kXrCardTail-byte tail (present / HYPERLOGLOG flags, the shape hash and its complement) that
+// the all-reduce (max) carries; every plan's two counters (LC hashes inserted, non-zero registers) to lc_out[2 * s ...]
+constexpr uint32_t kXrCardTail = 64;
+struct XrCardPack {
+    const unsigned int* regs[kColoMaxShards];  // null: the plan collected nothing
+    const unsigned int* cnt[kColoMaxShards];   // Pipeline.lc_count: [0] LC hashes, [1] non-zero registers
+    uint32_t n, m, thr;
+    unsigned long long hash;
+    uint8_t* out;                              // device, m + kXrCardTail bytes
+    uint32_t* lc_out;                          // pinned (device-mapped), 2 * n words
+};
+void launch_xr_card_pack(const XrCardPack& K, hipStream_t s);
+// the all-reduced bytes (m + kXrCardTail) copied to dst (pinned, device-mapped) and the non-zero registers added to *nz
+void launch_xr_card_finish(const uint8_t* regs, uint32_t m, unsigned long long* dst, uint32_t* nz, hipStream_t s);
+// a shard's GPU top-k keys (k_req wanted of kk slots, then the sum of all counts at keys[kk]) as the selection record
+// {picks, other-doc count, count << 32 | ordinal ...} (2 + K words)
+void launch_xr_terms_record(const unsigned long long* keys, uint32_t kk, uint32_t k_req, int order, unsigned long long* rec,
+                            uint32_t K, hipStream_t s);
 // the co-located reduce's selection input: every shard's per-ordinal doc counts, summed over the [H][T] grid rows,
 // written to out[shard][Tmax] (pinned, device-mapped) by one launch over all the shards
 struct ColoTotals {

@@ -126,6 +126,9 @@ struct Collective {
     // device operands, enqueued on `stream` (a hipStream_t): RCCL gathers device to device; a host transport stages
     // through pinned memory
     virtual void allgather_dev(const void* d_in, void* d_out, uint64_t bytes, void* stream) = 0;
+    // in place on a device buffer, enqueued on `stream`: RCCL reduces device to device (ncclAllReduce); the in-process
+    // transport reduces the ranks' buffers in rank order with one kernel; a host transport stages through pinned memory
+    virtual void allreduce_dev(void* d_buf, uint64_t count, int dtype, int op, void* stream) = 0;
 };
 // InternalAggregations.reduce over every rank's shard results, the shards in rank-major order (rank r's `locals` are
 // global shards r * n_local ...).  Fixed-shape partials are combined by all-reduce: top-level histograms with numeric

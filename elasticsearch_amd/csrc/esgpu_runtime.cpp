@@ -320,7 +320,9 @@ struct DevColumn {
     DevBuf b16, b16_base;
     // esgpu_segment_release_wide: the upload-width values of a single-valued long column with a compact copy were
     // released; wide_i64 rebuilds them (losslessly, from the deltas) for a kernel that reads them, and keeps them
-    bool wide_released = false;
+    // released by esgpu_segment_release_wide, rebuilt on first use (wide_i64): written under the context lock, read
+    // without it by the collect path -- an atomic so that a rebuilt column's pointer is published before the flag clears
+    std::atomic<bool> wide_released{false};
     const void* ord16_src = nullptr;
     bool d32_done = false, d16_done = false, b16_done = false;
     // the floored HLL stream's 4-byte words of a dense long / double column (ensure_hll_enc32, HllParams.enc32)
@@ -1086,7 +1088,7 @@ struct esgpu_plan {
     // the co-located reduce across ranks (esgpu_comm_build_reduce): local and all-gathered selection records, the packed
     // rows sent and received, the records on the host, the pack's descriptors; the event other local plans wait on
     Scratch s_xr_picks, s_xr_allpicks, s_xr_send, s_xr_recv;
-    PinnedBuf h_xr_picks, h_xr_meta;
+    PinnedBuf h_xr_picks, h_xr_meta, h_xr_hdr;
     hipEvent_t ev_xr = nullptr;
     int32_t last_path = 0;
     // per-request scratch, reused across requests
@@ -3338,19 +3340,19 @@ static uint32_t sampled_hot_ord(esgpu_ctx* c, const DevColumn* col, const esgpu_
 // deltas (value = vmin + delta: lossless for every present value) on the first kernel that reads them, and kept
 // (the caller holds c->mu)
 static const void* wide_i64_locked(esgpu_ctx* c, DevColumn* m, const esgpu_segment* s, hipStream_t st) {
-    if (!m->wide_released || m->values.p) return m->values.p;
+    if (!m->wide_released.load(std::memory_order_relaxed) || m->values.p) return m->values.p;
     m->values.alloc(c, (size_t)s->n_pad * 8);
     if (m->d32.p) launch_expand_d32(m->d32.as<uint32_t>(), s->n_pad, m->vmin, m->values.as<int64_t>(), st);
     else if (m->b16.p) launch_expand_b16(m->b16.as<uint16_t>(), m->b16_base.as<int64_t>(), s->max_doc, s->n_pad, m->values.as<int64_t>(), st);
     else launch_expand_d16(m->d16.as<uint16_t>(), s->n_pad, m->vmin, m->values.as<int64_t>(), st);
     HIPX(hipGetLastError());
     HIPX(hipStreamSynchronize(st));
-    m->wide_released = false;
+    m->wide_released.store(false, std::memory_order_release);  // (after values.p is set)
     return m->values.p;
 }
 static const void* wide_i64(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st) {
     if (!col) return nullptr;
-    if (!col->wide_released) return col->values.p;
+    if (!col->wide_released.load(std::memory_order_acquire)) return col->values.p;
     std::lock_guard<std::mutex> lk(c->mu);
     return wide_i64_locked(c, const_cast<DevColumn*>(col), s, st);
 }
@@ -5347,10 +5349,13 @@ extern "C" int esgpu_plan_build(esgpu_plan* p, esgpu_result** out) {
             for (int ch : p->specs[r].children) {
                 if (p->specs[ch].s.type == ESGPU_AGG_FILTER) { fb.subs.push_back(build_filter(ch)); continue; }
                 const Group& g = p->groups[gi++];
-                // sub-aggregators are wrapped by asMultiBucketAggregator (AggregatorFactories.java:75): a filter that
-                // collected no doc never created its bucket-0 aggregator, so buildAggregation(0) is
-                // first.buildEmptyAggregation() (AggregatorFactory.java:215-227) -- terms with min_doc_count 0 list
-                // no zero-count terms then
+                // a terms child of a filter that matched no doc builds empty: bucket 0 of the asMultiBucketAggregator
+                // wrapper holds `first` (AggregatorFactory.java:129), whose leaf collector is created only when a doc is
+                // collected into the bucket, so GlobalOrdinalsStringTermsAggregator never set globalOrds and its
+                // buildAggregation returns buildEmptyAggregation() (GlobalOrdinalsStringTermsAggregator.java:147-149)
+                // -- with min_doc_count 0 it lists no zero-count terms.  The GPU plan's terms are always that
+                // aggregator (keyword fields through global ordinals: terms over numeric fields are refused at create);
+                // the map-mode StringTermsAggregator would instead list zero-count terms from every leaf (:110).
                 if (dc == 0 && p->specs[g.root].s.type == ESGPU_AGG_TERMS) {
                     Block e = terms_shell(p, g.root, child_protos(p, g));
                     e.append_empty();
@@ -6124,6 +6129,259 @@ static Block xr_reduce_terms(esgpu_plan* p0, const unsigned long long* recs, int
 
 constexpr int kXrHeader = 8 + 2 * kColoMaxShards;  // header words per rank
 
+static uint64_t fnv64(uint64_t h, uint64_t v) {
+    for (int i = 0; i < 8; ++i) {
+        h ^= (v >> (8 * i)) & 0xFF;
+        h *= 0x100000001b3ULL;
+    }
+    return h;
+}
+// p0's stream waits for the other local plans' streams (their collects) without a host wait
+static void xr_join_streams(esgpu_plan* const* plans, int n) {
+    for (int i = 1; i < n; ++i) {
+        esgpu_plan* p = plans[i];
+        if (!p->ev_xr) HIPX(hipEventCreateWithFlags(&p->ev_xr, hipEventDisableTiming));
+        HIPX(hipEventRecord(p->ev_xr, p->stream));
+        HIPX(hipStreamWaitEvent(plans[0]->stream, p->ev_xr, 0));
+    }
+}
+// ... and the other way round: the local plans' next collects wait for p0's stream (which read their grids)
+static void xr_release_streams(esgpu_plan* const* plans, int n) {
+    esgpu_plan* p0 = plans[0];
+    if (!p0->ev_xr) HIPX(hipEventCreateWithFlags(&p0->ev_xr, hipEventDisableTiming));
+    HIPX(hipEventRecord(p0->ev_xr, p0->stream));
+    for (int i = 1; i < n; ++i) HIPX(hipStreamWaitEvent(plans[i]->stream, p0->ev_xr, 0));
+}
+
+// ---- top-level cardinality across ranks (config 4) ----
+// A request whose only aggregation is a top-level cardinality: InternalCardinality.doReduce over every shard
+// (InternalCardinality.java:103-126; HyperLogLogPlusPlus.merge, HyperLogLogPlusPlus.java:201-230) is a register max
+// whenever the merged sketch ends in HYPERLOGLOG -- any shard in HYPERLOGLOG, or more non-zero merged registers than the
+// linear-counting threshold (every distinct encoded hash raises one register, so the union of the shards' hash sets is
+// at least that large).  The device registers of a shard in LINEAR_COUNTING hold every hash too, which is what the
+// merge's upgradeToHll re-collects.  One all-reduce (max, u8) of [registers | tail] straight from device memory on p0's
+// stream, no host staging: the tail carries the present / HYPERLOGLOG flags and the request's shape hash (as h and ~h:
+// after a max over the ranks they read back as each other's complement only if every rank sent the same hash).  Only
+// a request that ends in LINEAR_COUNTING (every shard in it, a small union) goes to the builds and reduce_across.
+static bool xr_card_shape(esgpu_plan* const* plans, int n) {
+    for (int i = 0; i < n; ++i) {
+        const esgpu_plan* p = plans[i];
+        if (p->tops.size() != 1 || p->groups.size() != 1 || p->specs[p->tops[0]].s.type != ESGPU_AGG_CARDINALITY) return false;
+        const Group& g = p->groups[0];
+        if (g.pipes.size() != 1 || p->pipes[g.pipes[0]].kind != 1) return false;
+    }
+    return true;
+}
+// returns false when the merged sketch may end in LINEAR_COUNTING (every rank decides alike from the reduced bytes)
+static bool xr_card(Collective& C, esgpu_plan* const* plans, int n, int32_t root, ResultHolder& res) {
+    esgpu_plan* p0 = plans[0];
+    hipStream_t st = p0->stream;
+    const int spec = p0->tops[0];
+    const uint32_t pr = (uint32_t)p0->specs[spec].precision;
+    require(pr >= 4 && pr <= 18, ESGPU_ERR_INVALID, "precision out of range");
+    const uint32_t m = 1u << pr;
+    const uint32_t thr = (uint32_t)((float)(m / 4) * 0.75f);  // Hashset threshold (HyperLogLogPlusPlus.java:437-440)
+    // a fresh segment's one-time distinct estimate (post_collection: its later requests' floored-stream floor) reads that
+    // plan's own registers on the host -- such a plan takes its post_collection first, once per segment
+    for (int i = 0; i < n; ++i) {
+        Pipeline& pl = plans[i]->pipes[plans[i]->groups[0].pipes[0]];
+        if (pl.allocated && pl.hll_d1 && pl.hll_d1->load() < 0 && (pl.hll_nseg == 1 || pl.hll_r1_pending)) {
+            const int rc = esgpu_plan_post_collection(plans[i]);
+            if (rc != ESGPU_OK) throw EsError(rc, g_err);
+        }
+    }
+    xr_join_streams(plans, n);
+    XrCardPack K{};
+    uint64_t h = fnv64(fnv64(fnv64(0xcbf29ce484222325ULL, 0xCA4D), pr), (uint64_t)n);
+    for (int i = 0; i < n; ++i) {
+        Pipeline& pl = plans[i]->pipes[plans[i]->groups[0].pipes[0]];
+        if (!pl.allocated) continue;
+        require(pl.p == (int)pr, ESGPU_ERR_DEVICE, "internal: cardinality precision differs between plans");
+        K.regs[i] = pl.regs.as<unsigned int>();
+        K.cnt[i] = pl.lc_count.as<unsigned int>();
+    }
+    K.n = (uint32_t)n;
+    K.m = m;
+    K.thr = thr;
+    K.hash = h;
+    const size_t bytes = (size_t)m + kXrCardTail;
+    K.out = (uint8_t*)p0->s_xr_send.ensure(p0->ctx, bytes);
+    PinnedBuf& hp = p0->h_xr_picks;  // [registers | tail] [non-zero count, pad] [2 counters per local plan]
+    char* hbase = (char*)hp.ensure(bytes + 8 + 8 * (size_t)n);
+    K.lc_out = (uint32_t*)((char*)hp.dev() + bytes + 8);
+    uint32_t* dnz = (uint32_t*)p0->s_xr_picks.ensure(p0->ctx, 8);
+    HIPX(hipMemsetAsync(dnz, 0, 8, st));
+    launch_xr_card_pack(K, st);
+    HIPX(hipGetLastError());
+    C.allreduce_dev(K.out, bytes, ESGPU_DT_U8, ESGPU_RED_MAX, st);
+    launch_xr_card_finish(K.out, m, (unsigned long long*)hp.dev(), dnz, st);
+    HIPX(hipGetLastError());
+    launch_copy_u64((const unsigned long long*)dnz, (unsigned long long*)((char*)hp.dev() + bytes), 1, st);
+    HIPX(hipGetLastError());
+    xr_release_streams(plans, n);
+    HIPX(hipStreamSynchronize(st));
+    const uint8_t* regs = (const uint8_t*)hbase;
+    const uint8_t* tail = regs + m;
+    uint64_t hmax = 0, cmax = 0;
+    for (int k = 0; k < 8; ++k) {
+        hmax |= (uint64_t)tail[8 + k] << (8 * k);
+        cmax |= (uint64_t)tail[16 + k] << (8 * k);
+    }
+    require(cmax == ~hmax, ESGPU_ERR_INVALID, "reduce across ranks: the ranks run different requests");
+    const uint32_t* lc = (const uint32_t*)(hbase + bytes + 8);
+    for (int i = 0; i < n; ++i) {  // the next reset clears a plan's LC set only where its pass inserted hashes
+        Pipeline& pl = plans[i]->pipes[plans[i]->groups[0].pipes[0]];
+        if (pl.allocated) pl.lc_dirty = pl.lc_dirty || lc[2 * i] > 0;
+    }
+    const uint32_t nz = *(const uint32_t*)(hbase + bytes);
+    const bool present = tail[0] != 0, hll = tail[1] != 0 || nz > thr;
+    if (present && !hll) return false;
+    if (root >= 0 && root != C.rank) return true;  // the result on the root only
+    const SpecNode& sn = p0->specs[spec];
+    Block r;
+    r.type = ESGPU_AGG_CARDINALITY;
+    r.name = sn.name;
+    set_format(r, sn);
+    r.precision = (int32_t)pr;
+    if (!present) {  // no shard collected a value: the empty sketch
+        r.append_empty();
+    } else {
+        ++r.n;
+        r.hll_present.push_back(1);
+        r.hll_mode.push_back(1);
+        r.regs.emplace_back(regs, regs + m);
+        r.lc.emplace_back();
+    }
+    res.aggs.push_back(std::move(r));
+    return true;
+}
+
+// ---- a plain terms aggregation across ranks (config 3) ----
+// terms without sub-aggregations in a count or term order (InternalTerms.doReduce, InternalTerms.java:165-246): every
+// local shard's selection record {picks, other-doc count, count << 32 | ordinal ...} is made on its own stream -- the GPU
+// top-k (K3, count orders over more than 65,536 ordinals: build_terms_root's selection) or colo_select (up to
+// kColoSelMax ordinals) -- and the ranks all-gather [header | records] from device memory in one collective; the
+// doReduce then runs once per rank over the records (xr_reduce_terms).  Ranks that cannot make a record (another
+// dictionary, an order or size outside both selections) say so in the header, and every rank then builds and reduces.
+constexpr int kXrTermsHdr = 8;
+static bool xr_terms_shape(esgpu_plan* const* plans, int n) {
+    for (int i = 0; i < n; ++i) {
+        const esgpu_plan* p = plans[i];
+        if (p->tops.size() != 1 || p->groups.size() != 1) return false;
+        const Group& g = p->groups[0];
+        if (p->specs[g.root].s.type != ESGPU_AGG_TERMS || !g.kids.empty() || g.pipes.size() != 1 || g.fspec >= 0) return false;
+        const int32_t o = p->specs[g.root].s.order;
+        if (o < ESGPU_ORDER_COUNT_DESC || o > ESGPU_ORDER_TERM_DESC) return false;
+    }
+    return true;
+}
+static bool xr_terms(Collective& C, esgpu_plan* const* plans, int n, int32_t root, ResultHolder& res) {
+    esgpu_plan* p0 = plans[0];
+    hipStream_t st = p0->stream;
+    const int W = C.nranks, S = W * n;
+    const SpecNode& tn = p0->specs[p0->groups[0].root];
+    const uint32_t K = (uint32_t)std::min<int64_t>(std::max<int64_t>(tn.s.shard_size, 0), kTopkMax);  // request-level
+    const uint32_t rec = 2 + K, words = kXrTermsHdr + (uint32_t)n * rec;
+    const bool count_order = tn.s.order == ESGPU_ORDER_COUNT_DESC || tn.s.order == ESGPU_ORDER_COUNT_ASC;
+    unsigned long long* send = (unsigned long long*)p0->s_xr_send.ensure(p0->ctx, (size_t)words * 8);
+    PinnedBuf& hh = p0->h_xr_meta;
+    uint64_t* hdr = (uint64_t*)hh.ensure(kXrTermsHdr * 8);
+    std::memset(hdr, 0, kXrTermsHdr * 8);
+    const Pipeline& A = p0->pipes[p0->groups[0].pipes[0]];
+    bool ok = tn.s.shard_size >= 1 && (int64_t)K == tn.s.shard_size;
+    ok = ok && A.allocated && A.tdict != nullptr && A.H == 1;
+    for (int i = 0; ok && i < n; ++i) {
+        const Pipeline& B = plans[i]->pipes[plans[i]->groups[0].pipes[0]];
+        ok = B.allocated && B.H == 1 && B.value_count == A.value_count && same_dict(A.tdict, B.tdict) &&
+             plans[i]->docs_seen < (1ull << 31);
+    }
+    const bool topk = ok && count_order && A.value_count > 65536;
+    ok = ok && (topk || A.value_count <= kColoSelMax);
+    if (ok && topk) {
+        for (int i = 0; i < n; ++i) {  // each shard's K3 on its own stream, its record into p0's send buffer
+            esgpu_plan* p = plans[i];
+            const Pipeline& P0 = p->pipes[p->groups[0].pipes[0]];
+            const uint64_t k_req = std::min<uint64_t>(P0.value_count, (uint64_t)std::max<int64_t>(tn.s.shard_size, 0));
+            const uint32_t kk = (uint32_t)std::max<uint64_t>(k_req, 1);
+            TopkParams T{};  // (build_terms_root's K3 parameters)
+            T.counts = P0.ocnt_mode == OCNT_TERMS || P0.ocnt_mode == OCNT_TERMS_DERIVED ? P0.g_ocnt.as<unsigned long long>()
+                                                                                         : P0.g_cnt.as<unsigned long long>();
+            T.counts32 = P0.cnt32 ? P0.g_cnt.as<unsigned int>() : nullptr;
+            T.T = (uint32_t)P0.value_count;
+            T.order = tn.s.order;
+            T.min_doc_count = tn.s.min_doc_count;
+            T.shard_min_doc_count = tn.s.shard_min_doc_count;
+            T.k = kk;
+            T.n_wg = std::min<uint32_t>(512, (T.T + 4095) / 4096);
+            T.cand = (unsigned long long*)p->s_cand.ensure(p->ctx, (size_t)T.T * 8);
+            uint32_t* hs = (uint32_t*)p->s_hist.ensure(p->ctx, (2048 + 2) * 4);
+            T.hist = hs;
+            T.sel = hs + 2048;
+            unsigned long long* dk = (unsigned long long*)p->s_keys.ensure(p->ctx, ((size_t)kk + 1) * 8);
+            T.out_keys = dk;
+            T.out_sum = dk + kk;
+            HIPX(hipMemsetAsync(T.out_sum, 0, 8, p->stream));
+            launch_topk(T, p->stream);
+            HIPX(hipGetLastError());
+            if (p != p0) {  // the record is written on p0's stream once this shard's top-k is done
+                if (!p->ev_xr) HIPX(hipEventCreateWithFlags(&p->ev_xr, hipEventDisableTiming));
+                HIPX(hipEventRecord(p->ev_xr, p->stream));
+                HIPX(hipStreamWaitEvent(st, p->ev_xr, 0));
+            }
+            launch_xr_terms_record(dk, kk, (uint32_t)k_req, tn.s.order, send + kXrTermsHdr + (size_t)i * rec, K, st);
+            HIPX(hipGetLastError());
+        }
+    } else if (ok) {  // up to kColoSelMax ordinals: the co-located reduce's device selection
+        ColoSelection sel = colo_selection(plans, n);  // (waits for the local collects)
+        ok = sel.dev && sel.S.K == K;
+        if (ok) {
+            unsigned long long* dtot = (unsigned long long*)p0->s_colo_tot.ensure(p0->ctx, std::max<size_t>((size_t)n * sel.Tmax * 8, 8));
+            launch_colo_totals((const ColoTotals*)p0->h_colo_meta.dev(), (uint32_t)n, sel.Tmax, dtot, st);
+            HIPX(hipGetLastError());
+            launch_colo_select(dtot, (const ColoTotals*)p0->h_colo_meta.dev(), (uint32_t)n, sel.Tmax, sel.S, send + kXrTermsHdr, st);
+            HIPX(hipGetLastError());
+        }
+    }
+    hdr[0] = ok ? 1 : 0;
+    hdr[1] = (uint64_t)n;
+    hdr[2] = ok ? A.tdict->identity : 0;
+    hdr[3] = ok ? A.value_count : 0;
+    hdr[4] = K;
+    HIPX(hipMemcpyAsync(send, hh.p, kXrTermsHdr * 8, hipMemcpyHostToDevice, st));
+    unsigned long long* dall = (unsigned long long*)p0->s_xr_allpicks.ensure(p0->ctx, (size_t)words * W * 8);
+    C.allgather_dev(send, dall, (uint64_t)words * 8, st);
+    PinnedBuf& hp = p0->h_xr_picks;
+    hp.ensure((size_t)words * W * 8);
+    launch_copy_u64(dall, (unsigned long long*)hp.dev(), (size_t)words * W, st);
+    HIPX(hipGetLastError());
+    xr_release_streams(plans, n);
+    HIPX(hipStreamSynchronize(st));
+    for (int i = 0; i < n; ++i) {  // the hot/cold counting's capacity word (a bug, never data), as post_collection checks it
+        esgpu_plan* p = plans[i];
+        if (!p->hc_check) continue;
+        if (p != p0) HIPX(hipStreamSynchronize(p->stream));
+        p->hc_check = false;
+        volatile uint32_t* err = p->h_hcerr.as<volatile uint32_t>();
+        const uint32_t e = *err;
+        *err = 0;
+        require(e == 0, ESGPU_ERR_DEVICE, "hot/cold counting: partition capacity exceeded");
+    }
+    const uint64_t* all = hp.as<uint64_t>();
+    bool dev = true;
+    for (int r = 0; r < W && dev; ++r) {
+        const uint64_t* h = all + (size_t)r * words;
+        dev = h[0] == 1 && h[1] == (uint64_t)n && h[2] == all[2] && h[3] == all[3] && h[4] == K;
+    }
+    if (!dev) return false;
+    if (root >= 0 && root != C.rank) return true;
+    std::vector<unsigned long long> recs((size_t)S * rec);
+    for (int s = 0; s < S; ++s)
+        std::memcpy(recs.data() + (size_t)s * rec, all + (size_t)(s / n) * words + kXrTermsHdr + (size_t)(s % n) * rec, (size_t)rec * 8);
+    std::vector<std::vector<uint32_t>> won;
+    res.aggs.push_back(xr_reduce_terms(p0, recs.data(), S, rec, (uint32_t)all[3], won));
+    return true;
+}
+
 extern "C" int esgpu_comm_build_reduce(esgpu_comm* cm, esgpu_plan* const* plans, int32_t n, int32_t root,
                                        esgpu_result** out) {
     tune_host_heap();
@@ -6131,6 +6389,7 @@ extern "C" int esgpu_comm_build_reduce(esgpu_comm* cm, esgpu_plan* const* plans,
         require(cm && plans && out && n >= 1 && n <= kColoMaxShards, ESGPU_ERR_INVALID, "build_reduce needs 1..64 local plans");
         for (int i = 0; i < n; ++i) require(plans[i] != nullptr, ESGPU_ERR_INVALID, "null plan");
         Collective& C = comm_collective(cm);
+        require(root < C.nranks, ESGPU_ERR_INVALID, "build_reduce root is not a rank of the communicator");
         const double t_start = now_ms();
         C.allreduce_bytes = C.allgather_bytes = 0;
         C.collectives = 0;
@@ -6139,20 +6398,39 @@ extern "C" int esgpu_comm_build_reduce(esgpu_comm* cm, esgpu_plan* const* plans,
         esgpu_plan* p0 = plans[0];
         hipStream_t st = p0->stream;
         HIPX(hipSetDevice(p0->ctx->device));
-        // ---- this rank's part of the header ----
-        std::vector<uint64_t> hdr(kXrHeader, 0), all((size_t)kXrHeader * W, 0);
+        // shapes with a device exchange of their own (decided from the request alone: every rank takes the same branch)
+        {
+            std::unique_ptr<ResultHolder> res(new ResultHolder());
+            bool done = false;
+            if (S <= kColoMaxShards && xr_card_shape(plans, n)) done = xr_card(C, plans, n, root, *res);
+            else if (S <= kColoMaxShards && xr_terms_shape(plans, n)) done = xr_terms(C, plans, n, root, *res);
+            if (done) {
+                C.last_path = 1;
+                C.last_host_ms = now_ms() - t_start;
+                res->export_view();
+                *out = &res.release()->pub;
+                return;
+            }
+        }
+        // ---- this rank's header and selection records, all-gathered in one collective from device memory ----
+        // (the record size is the request's: every rank sends the same number of words, eligible or not)
+        std::vector<uint64_t> hdr(kXrHeader, 0);
         bool ok = S <= kColoMaxShards && colo_eligible(plans, n, false, true) && !p0->groups[0].kids.empty();
         for (int i = 0; ok && i < n; ++i) {
             ok = !plans[i]->hc_check;
             for (const Pipeline& pl : plans[i]->pipes) ok = ok && pl.kind != 1;
         }
+        const SpecNode& tn_root = p0->specs[p0->groups[0].root];
+        const uint32_t K = tn_root.s.type == ESGPU_AGG_TERMS
+                               ? (uint32_t)std::min<int64_t>(std::max<int64_t>(tn_root.s.shard_size, 0), kColoSelMax) : 0u;
+        const uint32_t rec = 2 + K, words = kXrHeader + (uint32_t)n * rec;
         ColoSelection sel;
         double t_host = t_start;  // the device path's host time is counted once this rank's collects have finished
         if (ok) {
             sel = colo_selection(plans, n);  // waits for the other local plans' collects
             HIPX(hipStreamSynchronize(st));  // ... and p0's
             t_host = now_ms();
-            ok = sel.dev;
+            ok = sel.dev && sel.S.K == K;
         }
         int nl = 0;
         if (ok) {
@@ -6178,12 +6456,30 @@ extern "C" int esgpu_comm_build_reduce(esgpu_comm* cm, esgpu_plan* const* plans,
         static const bool trace = std::getenv("ESGPU_TRACE_XR") != nullptr;
         std::vector<std::pair<const char*, double>> marks{{"host", t_host}};
         auto mark = [&](const char* w) { if (trace) marks.emplace_back(w, now_ms()); };
-        C.allgather(hdr.data(), all.data(), hdr.size() * 8);
-        mark("header");
+        unsigned long long* dsend = (unsigned long long*)p0->s_xr_picks.ensure(p0->ctx, (size_t)words * 8);
+        if (ok) {  // ---- 1. the local selections on the device, into the send buffer behind the header ----
+            unsigned long long* dtot = (unsigned long long*)p0->s_colo_tot.ensure(p0->ctx, std::max<size_t>((size_t)n * sel.Tmax * 8, 8));
+            launch_colo_totals((const ColoTotals*)p0->h_colo_meta.dev(), (uint32_t)n, sel.Tmax, dtot, st);
+            HIPX(hipGetLastError());
+            launch_colo_select(dtot, (const ColoTotals*)p0->h_colo_meta.dev(), (uint32_t)n, sel.Tmax, sel.S, dsend + kXrHeader, st);
+            HIPX(hipGetLastError());
+        }
+        PinnedBuf& hh = p0->h_xr_hdr;
+        std::memcpy(hh.ensure(kXrHeader * 8), hdr.data(), kXrHeader * 8);
+        HIPX(hipMemcpyAsync(dsend, hh.p, kXrHeader * 8, hipMemcpyHostToDevice, st));
+        unsigned long long* dall = (unsigned long long*)p0->s_xr_allpicks.ensure(p0->ctx, (size_t)words * W * 8);
+        C.allgather_dev(dsend, dall, (uint64_t)words * 8, st);
+        PinnedBuf& hp = p0->h_xr_picks;
+        hp.ensure((size_t)words * W * 8);
+        launch_copy_u64(dall, (unsigned long long*)hp.dev(), (size_t)words * W, st);
+        HIPX(hipGetLastError());
+        HIPX(hipStreamSynchronize(st));
+        mark("records");
+        const uint64_t* all = hp.as<uint64_t>();
         // ---- one decision on every rank: the device path, or builds + reduce_across ----
         bool dev = true;
         for (int r = 0; r < W && dev; ++r) {
-            const uint64_t* h = all.data() + (size_t)r * kXrHeader;
+            const uint64_t* h = all + (size_t)r * words;
             dev = h[0] == 1 && h[1] == (uint64_t)n && h[2] == all[2] && h[3] == all[3] && h[4] == all[4] && h[5] == all[5];
         }
         int64_t kmin = INT64_MAX, kmax = INT64_MIN;
@@ -6192,7 +6488,7 @@ extern "C" int esgpu_comm_build_reduce(esgpu_comm* cm, esgpu_plan* const* plans,
         std::vector<uint32_t> sH(S);
         if (dev) {
             for (int s = 0; s < S; ++s) {
-                const uint64_t* h = all.data() + (size_t)(s / n) * kXrHeader + 8 + 2 * (s % n);
+                const uint64_t* h = all + (size_t)(s / n) * words + 8 + 2 * (s % n);
                 skey0[s] = (int64_t)h[0];
                 sH[s] = (uint32_t)h[1];
                 kmin = std::min<int64_t>(kmin, skey0[s]);
@@ -6223,26 +6519,14 @@ extern "C" int esgpu_comm_build_reduce(esgpu_comm* cm, esgpu_plan* const* plans,
             *out = &res.release()->pub;
             return;
         }
-        // ---- 1. the local selections on the device, all-gathered device to device ----
-        const uint32_t K = sel.S.K, rec = 2 + K;
-        unsigned long long* dtot = (unsigned long long*)p0->s_colo_tot.ensure(p0->ctx, std::max<size_t>((size_t)n * sel.Tmax * 8, 8));
-        launch_colo_totals((const ColoTotals*)p0->h_colo_meta.dev(), (uint32_t)n, sel.Tmax, dtot, st);
-        HIPX(hipGetLastError());
-        unsigned long long* dpk = (unsigned long long*)p0->s_xr_picks.ensure(p0->ctx, (size_t)n * rec * 8);
-        launch_colo_select(dtot, (const ColoTotals*)p0->h_colo_meta.dev(), (uint32_t)n, sel.Tmax, sel.S, dpk, st);
-        HIPX(hipGetLastError());
-        unsigned long long* dall = (unsigned long long*)p0->s_xr_allpicks.ensure(p0->ctx, (size_t)S * rec * 8);
-        C.allgather_dev(dpk, dall, (uint64_t)n * rec * 8, st);
-        PinnedBuf& hp = p0->h_xr_picks;
-        hp.ensure((size_t)S * rec * 8);
-        launch_copy_u64(dall, (unsigned long long*)hp.dev(), (size_t)S * rec, st);
-        HIPX(hipGetLastError());
-        HIPX(hipStreamSynchronize(st));
-        mark("records");
+        std::vector<unsigned long long> recs((size_t)S * rec);
+        for (int s = 0; s < S; ++s)
+            std::memcpy(recs.data() + (size_t)s * rec, all + (size_t)(s / n) * words + kXrHeader + (size_t)(s % n) * rec,
+                        (size_t)rec * 8);
+        const uint64_t dict_n = all[3];
         // ---- 2. InternalTerms.doReduce over every shard's skeleton ----
-        const unsigned long long* picks = hp.as<unsigned long long>();
         std::vector<std::vector<uint32_t>> won;
-        res->aggs.push_back(xr_reduce_terms(p0, picks, S, rec, (uint32_t)all[3], won));
+        res->aggs.push_back(xr_reduce_terms(p0, recs.data(), S, rec, (uint32_t)dict_n, won));
         for (int i = 0; i < n; ++i) plans[i]->posted = true;
         Block& tb = res->aggs[0];
         const uint32_t R = (uint32_t)tb.nbuckets();

@@ -9,6 +9,10 @@ the shards' own builds (and to the oracle), for every transport:
   * RCCL with one rank (two local shards);
   * gloo between two processes sharing this GPU (Communicator.over_process_group: the host transport).
 Shapes the co-located reduce does not take fall back to builds + esgpu_comm_reduce (path 0), with the same result.
+Two shapes have device exchanges of their own (round 6): a plain terms aggregation (config 3: each shard's GPU top-k or
+device selection made into a record, [header | records] all-gathered in one collective) and a top-level cardinality
+(config 4: one all-reduce (max) of the u8 registers from device memory); a cardinality that may end in
+LINEAR_COUNTING falls back (path 0).
 """
 import json
 import os
@@ -50,16 +54,36 @@ SHAPES = {
                                 NS_FIELDS, None, True),
     "terms_stats_fallback": (lambda: [AB.terms("hosts").field("host").size(5).subAggregation(AB.stats("s").field("response_time_ms"))],
                              NS_FIELDS, None, False),
+    # config 3: 10M url ordinals, the GPU top-k's keys made into records on the device
+    "config3_urls": (lambda: [AB.terms("urls").field("url").size(10)], ("url",), None, True),
+    "urls_count_asc_errors": (lambda: [AB.terms("urls").field("url").size(4).shardSize(9).order(ea.Order.count(True))
+                                       .showTermDocCountError(True)], ("url",), None, True),
+    # plain terms over 1,000 hosts: the co-located device selection (count and term orders)
+    "hosts_plain": (lambda: [AB.terms("hosts").field("host").size(5)], ("host",), None, True),
+    "hosts_plain_term_desc": (lambda: [AB.terms("hosts").field("host").size(6).order(ea.Order.term(False))], ("host",), None, True),
+    # config 4: a sketch in HYPERLOGLOG on every shard
+    "config4_card": (lambda: [AB.cardinality("ips").field("client_ip.hash").precisionThreshold(40000)], ("client_ip.hash",),
+                     None, True),
+    "card_p14_hll": (lambda: [AB.cardinality("ips").field("client_ip.hash").precisionThreshold(1000)], ("client_ip.hash",),
+                     None, True),
+    # every shard in LINEAR_COUNTING and a small union: builds + reduce (path 0)
+    "card_lc_fallback": (lambda: [AB.cardinality("ips").field("client_ip.hash").precisionThreshold(40000)], ("client_ip.hash",),
+                         None, False, 3_000),
 }
 DOCS = 1_500_000
 
 
+def _docs(shape):
+    t = SHAPES[shape]
+    return t[4] if len(t) > 4 else DOCS
+
+
 def _expected(shape, nshards):
-    aggs_f, fields, filters, _ = SHAPES[shape]
+    aggs_f, fields, filters = SHAPES[shape][:3]
     eng = ea.Engine(0)
     res = []
     for s in range(nshards):
-        seg = eng.synthetic_segment(DOCS + 1000 * s, fields=fields, shard=s)
+        seg = eng.synthetic_segment(_docs(shape) + 1000 * s, fields=fields, shard=s)
         plan = eng.plan(aggs_f(), filters=filters, number_of_shards=nshards)
         plan.collect(seg)
         res.append(plan.build())
@@ -71,13 +95,13 @@ def _expected(shape, nshards):
 
 
 def _rank(shape, world, rank, n_local, group, out, root):
-    aggs_f, fields, filters, _ = SHAPES[shape]
+    aggs_f, fields, filters = SHAPES[shape][:3]
     eng = ea.Engine(0)
     comm = ea.Communicator.local(group, world, rank)
     segs, plans = [], []
     for i in range(n_local):
         s = rank * n_local + i
-        segs.append(eng.synthetic_segment(DOCS + 1000 * s, fields=fields, shard=s))
+        segs.append(eng.synthetic_segment(_docs(shape) + 1000 * s, fields=fields, shard=s))
         plans.append(eng.plan(aggs_f(), filters=filters, number_of_shards=world * n_local))
     for rep in range(2):  # a second request on the same plans (reset, collect again)
         for p, seg in zip(plans, segs):
@@ -130,15 +154,16 @@ def test_local_ranks_match_reduce_of_builds(shape, world, n_local):
                 assert_same(other, want, f"rank {r}")
 
 
-def test_local_ranks_every_rank_gets_the_result():
-    want = _expected("north_star", 4)
-    out = _run_local("north_star", 4, 1, root=-1)
+@pytest.mark.parametrize("shape", ["north_star", "config3_urls", "config4_card"])
+def test_local_ranks_every_rank_gets_the_result(shape):
+    want = _expected(shape, 4)
+    out = _run_local(shape, 4, 1, root=-1)
     for r in range(4):
         assert_same(out[(r, 1)][0], want, f"rank {r}")
 
 
 def test_local_ranks_against_the_oracle():
-    aggs_f, fields, filters, _ = SHAPES["config5"]
+    aggs_f, fields, filters = SHAPES["config5"][:3]
     world = 4
     shards = [(synthetic_columns(fields, DOCS + 1000 * s, shard=s), DOCS + 1000 * s) for s in range(world)]
     want = O.run(shards, aggs_f(), filters=filters, number_of_shards=world)["reduced"]
@@ -146,18 +171,22 @@ def test_local_ranks_against_the_oracle():
     assert_same(out[(0, 0)][0], want, "config5 vs oracle")
 
 
-def test_rccl_one_rank_device_exchange(engine):
-    """RCCL with one rank and two local shards: the selection records and rows go through ncclAllGather."""
-    aggs_f, fields, _, _ = SHAPES["north_star"]
-    want = _expected("north_star", 2)
+@pytest.mark.parametrize("shape", ["north_star", "config3_urls", "config4_card"])
+def test_rccl_one_rank_device_exchange(engine, shape):
+    """RCCL with one rank and two local shards: the selection records and rows go through ncclAllGather, the
+    cardinality registers through ncclAllReduce (max)."""
+    aggs_f, fields = SHAPES[shape][:2]
+    want = _expected(shape, 2)
     comm = ea.Communicator(engine, 1, 0, ea.Communicator.unique_id())
-    segs = [engine.synthetic_segment(DOCS + 1000 * s, fields=fields, shard=s) for s in range(2)]
+    segs = [engine.synthetic_segment(_docs(shape) + 1000 * s, fields=fields, shard=s) for s in range(2)]
     plans = [engine.plan(aggs_f(), number_of_shards=2) for _ in range(2)]
-    for p, s in zip(plans, segs):
-        p.collect(s)
-    got = comm.build_reduce(plans, root=0).to_dict()
-    assert comm.last_build_reduce()[0] == 1
-    assert_same(got, want, "rccl one rank")
+    for rep in range(2):
+        for p, s in zip(plans, segs):
+            p.reset()
+            p.collect(s)
+        got = comm.build_reduce(plans, root=0).to_dict()
+        assert comm.last_build_reduce()[0] == 1
+        assert_same(got, want, f"rccl one rank {shape} rep{rep}")
     comm.close()
     for p in plans:
         p.close()
@@ -165,14 +194,14 @@ def test_rccl_one_rank_device_exchange(engine):
         s.close()
 
 
-def _gloo_worker(rank, world, port, path):
+def _gloo_worker(rank, world, port, path, shape="north_star"):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    aggs_f, fields, _, _ = SHAPES["north_star"]
+    aggs_f, fields = SHAPES[shape][:2]
     eng = ea.Engine(0)
     comm = ea.Communicator.over_process_group()
-    seg = eng.synthetic_segment(DOCS + 1000 * rank, fields=fields, shard=rank)
+    seg = eng.synthetic_segment(_docs(shape) + 1000 * rank, fields=fields, shard=rank)
     plan = eng.plan(aggs_f(), number_of_shards=world)
     plan.collect(seg)
     r = comm.build_reduce([plan], root=0)
@@ -186,18 +215,19 @@ def _gloo_worker(rank, world, port, path):
     dist.destroy_process_group()
 
 
-def test_gloo_two_processes_host_transport():
+@pytest.mark.parametrize("shape", ["north_star", "config3_urls", "config4_card"])
+def test_gloo_two_processes_host_transport(shape):
     import socket
 
     import torch.multiprocessing as mp
-    want = _expected("north_star", 2)
+    want = _expected(shape, 2)
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "r0.json")
-        mp.start_processes(_gloo_worker, args=(2, port, path), nprocs=2, join=True, start_method="spawn")
+        mp.start_processes(_gloo_worker, args=(2, port, path, shape), nprocs=2, join=True, start_method="spawn")
         with open(path) as f:
             got = json.load(f)
     assert got["path"] == 1
-    assert_same(got["result"], want, "gloo world 2")
+    assert_same(got["result"], want, f"gloo world 2 {shape}")

@@ -183,6 +183,10 @@ for s in $STEPS; do
                       ESGPU_LIBRARY=$so run "kbench_$v${KBENCH_TAG:-}" 600 python3 "$R/tools/kbench.py" --docs 1000000000 --reps 5 \
                           ${KBENCH_ONLY:+--only $KBENCH_ONLY} ${KBENCH_ARGS:-}
                   done ;;
+        ranksim) # per-rank host time of esgpu_comm_build_reduce, 8 in-process ranks on this GPU, 125M docs per rank
+              for w in ${RANKSIM_ONLY:-north_star config3 config4 config5}; do
+                  run "ranksim_$w" 300 python3 "$R/tools/rank_sim.py" --workload $w --ranks 8 --docs 125000000 --reqs 20 || exit 1
+              done ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done

@@ -26,6 +26,10 @@ from elasticsearch_amd import QueryBuilders as QB  # noqa: E402
 
 def request(workload):
     hour = AB.dateHistogram("per_hour").field("@timestamp").interval("1h")
+    if workload == "config3":
+        return [AB.terms("urls").field("url").size(10)], ("url",), None
+    if workload == "config4":
+        return [AB.cardinality("ips").field("client_ip.hash").precisionThreshold(40000)], ("client_ip.hash",), None
     if workload == "config5":
         return ([AB.terms("hosts").field("host").size(10).subAggregation(hour.subAggregation(AB.avg("rt").field("response_time_ms")))],
                 ("status", "bytes", "host", "@timestamp", "response_time_ms"),
@@ -36,7 +40,7 @@ def request(workload):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="north_star", choices=["north_star", "config5"])
+    ap.add_argument("--workload", default="north_star", choices=["north_star", "config3", "config4", "config5"])
     ap.add_argument("--ranks", type=int, default=8)
     ap.add_argument("--docs", type=int, default=125_000_000)
     ap.add_argument("--reqs", type=int, default=20)
@@ -77,7 +81,8 @@ def main():
                 if r == 0 and i == a.warmup + a.reqs - 1:
                     wall["t1"] = time.perf_counter()
                     d = res.to_dict()
-                    wall["buckets"] = len(d["hosts"]["buckets"])
+                    top = next(iter(d.values()))
+                    wall["buckets"] = len(top["buckets"]) if "buckets" in top else top.get("value")
             comm.close()
             plan.close()
             seg.close()
@@ -100,7 +105,7 @@ def main():
         "host_ms_per_request_root": round(per_rank[0], 4),
         "host_ms_per_request_max_rank": round(max(per_rank), 4),
         "wall_ms_per_request": round((wall["t1"] - wall["t0"]) * 1e3 / a.reqs, 3),
-        "terms_buckets": wall.get("buckets"),
+        "terms_buckets_or_value": wall.get("buckets"),
     }))
 
 
