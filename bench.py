@@ -230,13 +230,18 @@ def main():
     # same result as reducing every shard build); with several ranks each rank's shards go to the cross-rank reduce
     # with several ranks, a shape the device merge takes goes to the device-resident reduce across ranks
     # (esgpu_comm_build_reduce: device selections and rows exchanged device to device, the merge on rank 0)
-    colo = (units_per_request > 1 or world > 1) and not merged and not args.no_colo
+    colo = units_per_request > 1 and not merged and not args.no_colo
     if colo:
         probe_plans = [engine.plan(aggs, filters=filters, number_of_shards=shards) for _ in range(max(units_per_request, 2))]
         colo = ea.colocated(probe_plans)  # a shape the device merge takes (else the builds run on worker threads)
         for pp in probe_plans:
             pp.close()
-    xr = colo and world > 1
+    # several ranks: every request goes to esgpu_comm_build_reduce, which exchanges device buffers for the co-located
+    # shapes (north star, config 5), plain terms (config 3) and top-level cardinality (config 4), and builds + reduces
+    # every other shape across the ranks
+    xr = world > 1 and not args.no_colo
+    if xr:
+        colo = units_per_request > 1
     if colo:
         args.scheme = "sets"  # one plan per shard: a request's plans are all alive at its reduce
     # plan sets: one plan per unit (a shard, or all of a fixed-shape request's shards); `inflight` sets alternate, so
@@ -263,7 +268,7 @@ def main():
                 kernel_bytes[0] += nbytes
 
     host_ms = {"build": 0.0, "reduce": 0.0}
-    if colo:
+    if colo or xr:
         host_ms = {"build_reduce": 0.0}
     # A request's shard builds run on worker threads -- Elasticsearch runs one SEARCH thread per shard of a request --
     # and the coordinating reduce of a request on its own worker (a coordinating node merges one request while the
@@ -306,9 +311,9 @@ def main():
             futs = []
             for unit, p in enumerate(sets[r % depth]):
                 launch(p, unit, False)
-                if not colo:
+                if not (colo or xr):
                     futs.append(builders.submit(build_unit, p))
-            pend.append(reducer.submit(colo_request, sets[r % depth]) if colo else reducer.submit(reduce_request, futs))
+            pend.append(reducer.submit(colo_request, sets[r % depth]) if colo or xr else reducer.submit(reduce_request, futs))
         while pend:
             final = pend.popleft().result()
 
@@ -348,6 +353,9 @@ def main():
         for r in range(n_requests):
             if r + 1 < n_requests:
                 launch(plans[(r + 1) % depth], 0, False)
+            if xr:
+                final = comm.build_reduce([plans[r % depth]], root=0)
+                continue
             part = plans[r % depth].build()
             final = comm.reduce([part]) if comm else ea.reduce([part])
 
@@ -357,7 +365,7 @@ def main():
         nonlocal final
         p = sets[0][0]
         for _ in range(n_requests):
-            if colo:  # the request's shards collected one after the other, then built and reduced in one call
+            if colo or xr:  # the request's shards collected one after the other, then built and reduced in one call
                 for unit, pu in enumerate(sets[0]):
                     launch(pu, unit, True)
                 final = colo_request(sets[0])
@@ -413,7 +421,7 @@ def main():
         # the compact columns (16-bit ordinals, 32-bit timestamp deltas: DESIGN §3) of each segment of this GPU, built on
         # its first collect and cached with it -- their build time and HBM footprint, outside the timed region
         p = sets[0][0]
-        first, hbm = [], []
+        first, hbm, cold = [], [], []
         for seg in segs:
             p.reset()
             h0 = engine.hbm_used()
@@ -422,14 +430,25 @@ def main():
             k_ms, _, _ = p.last_collect_stats()
             first.append((time.perf_counter() - t0) * 1e3 - k_ms)
             hbm.append(engine.hbm_used() - h0)
-        p.build()
+            p.build()
+            cold.append((time.perf_counter() - t0) * 1e3)  # a request on the cold segment: products, collect, build
         if sum(hbm) >= 2 * args.docs * len(segs):  # at least 2 B per doc: compact columns were built
-            precomputed = {"what": "compact columns of the segment (u16 ordinals, timestamp block deltas or u32 deltas, "
-                                   "u16 / u32 metric deltas; cached with it; the first segment's figure includes the plan's grid)",
+            what = ("compact columns of the segment (u16 ordinals, timestamp block deltas or u32 deltas, u16 / u32 metric "
+                    "deltas; cached with it; the first segment's figure includes the plan's grid)")
+            if args.workload == "config4":
+                what = ("HLL++ encodeHash words of the murmur3 field, 4 B per doc (the hash's index bits and its run-length "
+                        "count past them, HyperLogLogPlusPlus.java:335-346: what the register updates read instead of the "
+                        "8-B hashes), built on the segment's first request and cached with it; the first segment's figure "
+                        "includes the plan's registers and sets")
+            precomputed = {"what": what,
                            "build_ms_per_segment": round(sum(first) / len(first), 3),
-                           "hbm_bytes_per_segment": int(sum(hbm) / len(hbm))}
+                           "hbm_bytes_per_segment": int(sum(hbm) / len(hbm)),
+                           # one request on a segment whose products are not built yet (they are built inside it)
+                           "cold_first_request_ms": round(sum(cold) / len(cold), 3)}
     if args.scheme == "auto":
         args.scheme = "inline" if units_per_request == 1 and not colo and inflight > 1 else "rotate"
+    if xr and args.scheme == "rotate":  # (rotating plans build units one by one: the cross-rank call takes a request's plans)
+        args.scheme = "sets"
     pipelined = {"inline": run_inline, "rotate": run_rotate}.get(args.scheme, run)
     pipelined(args.warmup, inflight)
     elapsed = timed(pipelined, args.steps, inflight)
@@ -512,9 +531,9 @@ def main():
             "data": "synthetic (deterministic splitmix64 log docs generated in HBM, seed 0x5EEDE1A5, shard = global shard id)",
             "config": {"workload": args.workload, "request": desc, "docs_per_shard": args.docs, "shards": shards,
                        "shards_per_gpu": per_gpu, "docs_total": docs_total,
-                       "collect": "merged (one plan per GPU)" if merged else
-                                  ("per shard, device-resident reduce across ranks (esgpu_comm_build_reduce)" if xr else
-                                   "per shard, co-located reduce (esgpu_plans_build_reduce)" if colo else "per shard"),
+                       "collect": ("merged (one plan per GPU)" if merged else "per shard") +
+                                  (", reduce across ranks through esgpu_comm_build_reduce" if xr else
+                                   ", co-located reduce (esgpu_plans_build_reduce)" if colo else ""),
                        "parallelism": f"{per_gpu} shard(s) per GPU x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,

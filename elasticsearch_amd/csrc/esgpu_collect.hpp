@@ -1637,18 +1637,24 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
                 }
             }
         }
+        bool uni = false;  // packed cells, a full zone block of one key (wave-uniform test): the uniform-slot path
         if constexpr (kPIU) {
-            // packed cells, a full zone block of one key (wave-uniform test): the uniform-slot path
             const Doc4* qa;
             const Doc4* qz;
             if constexpr (WIDE8) { qa = &q.a; qz = &q.b; } else { qa = &q; qz = &q; }
-            if (use_lds && qa->ukey != kNoUKey && (uint32_t)__builtin_amdgcn_readlane((int)qz->doc0, 63) + 4u <= P.n_docs) {
-                pi_uniform<MET, VKL, WIDE8 ? 2 : 1>(P, s, *qa, *qz, T, win0, run, npass > 1 ? W : 0u, pass == 0);
+            uni = use_lds && qa->ukey != kNoUKey && (uint32_t)__builtin_amdgcn_readlane((int)qz->doc0, 63) + 4u <= P.n_docs;
+            if (uni) {
+                if constexpr (WIDE8 && MET >= 2) {  // (the (min, max) regions: one half at a time -- registers)
+                    pi_uniform<MET, VKL, 1>(P, s, *qa, *qa, T, win0, run, npass > 1 ? W : 0u, pass == 0);
+                    pi_uniform<MET, VKL, 1>(P, s, *qz, *qz, T, win0, run, npass > 1 ? W : 0u, pass == 0);
+                } else {
+                    pi_uniform<MET, VKL, WIDE8 ? 2 : 1>(P, s, *qa, *qz, T, win0, run, npass > 1 ? W : 0u, pass == 0);
+                }
                 dirty = true;
-                goto prefetch;
             }
         }
-        if (use_lds) {
+        if (uni) {
+        } else if (use_lds) {
             if constexpr (WIDE8) {
                 process4<ORD, HIST, MET, true, KT, kMS, HORD, VKL>(P, s, q.a, T, base, win0, run, npass > 1 ? W : 0u, pass == 0);
                 process4<ORD, HIST, MET, true, KT, kMS, HORD, VKL>(P, s, q.b, T, base, win0, run, npass > 1 ? W : 0u, pass == 0);
@@ -1666,7 +1672,6 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
         }
         // prefetch kBuf iterations ahead along the schedule (next block of the group, the group's next pass, or the
         // next group)
-    prefetch:
         uint32_t nit = it + kBuf, nb = cb;
         if (nit >= (uint32_t)kItersPerBlockW) {
             nit -= kItersPerBlockW;
