@@ -196,6 +196,12 @@ __device__ __forceinline__ void load_keys_raw(const CollectParams& P, uint32_t d
         raw[4] = b.x; raw[5] = b.y;
 #endif
     } else {
+        if constexpr ((VK & 16384) != 0) {  // single-key zone blocks read no 32-bit delta either (VK bit 16384)
+            if (uk != kNoUKey) {
+                raw[2] = 0; raw[3] = 0; raw[4] = 0; raw[5] = 0;
+                return;
+            }
+        }
         const u32x4_t t = load16(P.hv32 + doc0);
         raw[2] = t.x; raw[3] = t.y; raw[4] = t.z; raw[5] = t.w;
     }
@@ -220,6 +226,11 @@ constexpr bool kRawH = (VK & 1024) != 0;
 // of squared deltas, min / max delta): exact, and a third of the VALU work of the f64 runs; decoded at the run's flush
 template <bool ORD, int MET, int VK>
 constexpr bool kIntRuns = !ORD && MET > 0 && (VK & 2048) != 0;
+// raw-load kernels whose key column is block deltas (VK bit 8192) or 32-bit deltas (bit 32): single-key zone blocks take
+// their key from the zone map (zone_ukey) and read no timestamp
+template <bool ORD, bool HIST, int MET, int VK>
+constexpr bool kUKeyK = HIST && ((VK & 8192) != 0 || (VK & (32 | 16384)) == (32 | 16384)) &&
+                        (kRawPI<MET, VK, HIST> || kRawH<ORD, MET, VK>);
 
 template <bool ORD, bool HIST, int MET, int VK>
 __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0, Doc4& d, uint32_t uk = kNoUKey) {
@@ -371,9 +382,16 @@ __device__ __forceinline__ void load_docs8(const CollectParams& P, uint32_t doc0
                 d.a.raw[4] = bs.x; d.a.raw[5] = bs.y; d.b.raw[4] = bs.x; d.b.raw[5] = bs.y;
             }
         } else {
-            const u32x4_t t0 = load16(P.hv32 + doc0), t1 = load16(P.hv32 + doc0 + 4);
-            d.a.raw[2] = t0.x; d.a.raw[3] = t0.y; d.a.raw[4] = t0.z; d.a.raw[5] = t0.w;
-            d.b.raw[2] = t1.x; d.b.raw[3] = t1.y; d.b.raw[4] = t1.z; d.b.raw[5] = t1.w;
+            bool skip = false;
+            if constexpr ((VK & 16384) != 0) skip = uk != kNoUKey;  // a single-key block (VK bit 16384): no delta read
+            if (skip) {
+                d.a.raw[2] = d.a.raw[3] = d.a.raw[4] = d.a.raw[5] = 0u;
+                d.b.raw[2] = d.b.raw[3] = d.b.raw[4] = d.b.raw[5] = 0u;
+            } else {
+                const u32x4_t t0 = load16(P.hv32 + doc0), t1 = load16(P.hv32 + doc0 + 4);
+                d.a.raw[2] = t0.x; d.a.raw[3] = t0.y; d.a.raw[4] = t0.z; d.a.raw[5] = t0.w;
+                d.b.raw[2] = t1.x; d.b.raw[3] = t1.y; d.b.raw[4] = t1.z; d.b.raw[5] = t1.w;
+            }
         }
     }
     if constexpr (MET > 0 && (kRawPI<MET, VK, HIST> || (VK & 2048) != 0)) {  // 16-bit metric deltas
@@ -842,7 +860,7 @@ __device__ __forceinline__ void unpack_docs(const CollectParams& P, Doc4& d) {
     // is below 0xFFFF
     d.ord[0] = d.raw[0] & 0xFFFFu; d.ord[1] = d.raw[0] >> 16; d.ord[2] = d.raw[1] & 0xFFFFu; d.ord[3] = d.raw[1] >> 16;
     if constexpr (HIST) {
-        if ((VK & 8192) == 0 || d.ukey == kNoUKey) unpack_keys_raw<VK>(P, d.raw, d.hv);
+        if (d.ukey == kNoUKey) unpack_keys_raw<VK>(P, d.raw, d.hv);  // (zone_ukey: kNoUKey on the other kernels)
         d.hpres = 0xFu;
     }
     d.mvd[0] = d.raw[6] & 0xFFFFu; d.mvd[1] = d.raw[6] >> 16; d.mvd[2] = d.raw[7] & 0xFFFFu; d.mvd[3] = d.raw[7] >> 16;
@@ -866,7 +884,7 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
             for (int j = 0; j < 4; ++j) du.ord[j] = x[j] == 0xFFFFu ? kMissingOrd : x[j];
         }
         if constexpr (HIST) {
-            if ((VK & 8192) == 0 || du.ukey == kNoUKey) unpack_keys_raw<VK>(P, du.raw, du.hv);
+            if (du.ukey == kNoUKey) unpack_keys_raw<VK>(P, du.raw, du.hv);
             du.hpres = 0xFu;
         }
         if constexpr (MET > 0 && (VK & 2048) != 0) {  // integer runs: the 16-bit deltas as they are
@@ -881,8 +899,9 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
     const Doc4& d = kRawPI<MET, VK, HIST> || kRawH<ORD, MET, VK> ? du : d_in;
     uint32_t slot[kVec];
     bool hv_ok[kVec];
-    // block-delta kernels: a zone block whose docs all share one key takes it for every doc (wave-uniform branch)
-    const bool ublock = (VK & 8192) != 0 && HIST && d.ukey != kNoUKey;
+    // raw-load kernels over block deltas or 32-bit deltas: a zone block whose docs all share one key takes it for every
+    // doc (wave-uniform branch)
+    const bool ublock = kUKeyK<ORD, HIST, MET, VK> && d.ukey != kNoUKey;
     if (ublock) {
         const uint32_t k = d.ukey;  // grid key index, or kOutUKey (outside the grid: no doc counts)
         const uint32_t sl = LDS ? k - win0 : k;
@@ -1163,9 +1182,9 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
 #ifndef ESGPU_PI_UFAST  // (A/B) 0: the general per-doc path for these blocks too
 #define ESGPU_PI_UFAST 1
 #endif
-#ifndef ESGPU_PI_HOTU  // (A/B) the segment's most frequent ordinal counted and summed in registers in uniform blocks
-#define ESGPU_PI_HOTU 0
-#endif
+#ifndef ESGPU_PI_HOTU  // the segment's most frequent ordinal counted and summed in registers in uniform blocks: 2 = with
+#define ESGPU_PI_HOTU 2  // (min, max) leaves only (north star 1.104 -> 1.046 ms at 1B, r6f: its LDS adds were the kernel's
+#endif                   // limit; avg grids, which are not LDS-bound, measured 5 % slower with it), 1 = always, 0 = never
 #ifndef ESGPU_PI_MMU  // (A/B) uniform blocks' (min, max) updates: 2 = one divergent region per doc (as ESGPU_PI_MMCHECK 2),
 #define ESGPU_PI_MMU 2  // 3 = branch-free -- every lane issues both atomics, lanes whose bounds do not move on a spare word
 #endif
@@ -1205,10 +1224,11 @@ __device__ __forceinline__ void pi_uniform(const CollectParams& P, const Acc& a,
     bool hit[N], hpk[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-        hit[j] = ((okm >> j) & 1) && t[j] < T;  // (a missing ordinal, 0xFFFF, is >= T)
+        hit[j] = (((okm >> j) & 1) != 0) & (t[j] < T);  // (a missing ordinal, 0xFFFF, is >= T)
         hpk[j] = hit[j];
     }
-#if ESGPU_PI_HOTU
+    constexpr bool kHot = ESGPU_PI_HOTU == 1 || (ESGPU_PI_HOTU == 2 && MET >= 2);
+    if constexpr (kHot) {
     if (sl != run.hslot) {  // (uniform) the hot ordinal's register run moves to this key
         pi_hot_flush<MET>(P, a, run, T);
         run.hslot = sl;
@@ -1225,7 +1245,7 @@ __device__ __forceinline__ void pi_uniform(const CollectParams& P, const Acc& a,
         }
         run.hpk += ((unsigned long long)hc << P.pk_shift) + hs;
     }
-#endif
+    }
     uint32_t mlo[N], mhi[N];
     if (MET >= 2) {
 #pragma unroll
@@ -1243,7 +1263,7 @@ __device__ __forceinline__ void pi_uniform(const CollectParams& P, const Acc& a,
         uint32_t* spare = reinterpret_cast<uint32_t*>(a.pkd);
 #pragma unroll
         for (int j = 0; j < N; ++j) {
-            const bool mv = hit[j] && (dv[j] < mlo[j] || dv[j] > mhi[j]);
+            const bool mv = hit[j] & ((dv[j] < mlo[j]) | (dv[j] > mhi[j]));
             uint32_t* w = mv ? &a.mm[2 * (cb + t[j])] : spare;
             atomicMin(w, dv[j]);
             atomicMax(w + 1, dv[j]);
@@ -1251,7 +1271,8 @@ __device__ __forceinline__ void pi_uniform(const CollectParams& P, const Acc& a,
 #else
 #pragma unroll
         for (int j = 0; j < N; ++j) {
-            const bool mv = hit[j] && (dv[j] < mlo[j] || dv[j] > mhi[j]);
+            // (bitwise: one divergent region per doc -- a short-circuit && nests a second one around the comparisons)
+            const bool mv = hit[j] & ((dv[j] < mlo[j]) | (dv[j] > mhi[j]));
             if (mv) {
                 atomicMin(&a.mm[2 * (cb + t[j])], dv[j]);
                 atomicMax(&a.mm[2 * (cb + t[j]) + 1], dv[j]);
@@ -1450,7 +1471,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
     // accesses, and each flat load waits for vmcnt(0): the prefetched loads of the next iteration.
     constexpr bool PI = MET > 0 && (VK & 64) != 0;  // packed integer cells
     // ... over block-delta keys: full single-key zone blocks take pi_uniform
-    constexpr bool kPIU = ESGPU_PI_UFAST != 0 && PI && HIST && !HORD && (VKL & 8192) != 0 && kRawPI<MET, VKL, HIST>;
+    constexpr bool kPIU = ESGPU_PI_UFAST != 0 && PI && HIST && !HORD && kUKeyK<ORD, HIST, MET, VKL> && kRawPI<MET, VKL, HIST>;
     Acc s;
     s.sum_lo = nullptr; s.sq_lo = nullptr;
     if constexpr (PI) {  // collect_lds_bytes(pi = true) mirrors this carve
@@ -1557,7 +1578,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
     // block-delta kernels: the zone block's key when all its docs share one (zone_keys ranges, two scalar loads per
     // block and wave), the block's timestamps then left unread
     auto zone_ukey = [&](uint32_t blk) -> uint32_t {
-        if constexpr ((VKL & 8192) == 0 || !HIST) {
+        if constexpr (!kUKeyK<ORD, HIST, MET, VKL>) {
             return kNoUKey;
         } else {
             const uint32_t b = __builtin_amdgcn_readfirstlane(blk);
@@ -1783,7 +1804,7 @@ static auto with_vk0(bool hv_f64, bool mv_f64, F f) {
 // over a long column.
 template <bool ORD, int HK, int MET, class F>
 static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, bool t16, bool pi, bool m32, bool m16, bool acc,
-                    bool raw, bool runs1, F f) {
+                    bool raw, bool runs1, bool uk32, F f) {
     // t16: the key column is read as block deltas (VK bit 8192 in place of 32) -- by the raw-load kernels only; the host
     // picks it only for a launch that takes one of them (t32 is then set as well)
     // VK bit 128, a compact long metric (u32 deltas, values restored in the loader): histogram-only grids over compact
@@ -1793,6 +1814,11 @@ static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, boo
             if (raw && m16 && runs1 && t16) return f(std::integral_constant<int, 8192 | 128 | 1024 | 2048 | 4096>{});
             if (raw && m16 && t16) return f(std::integral_constant<int, 8192 | 128 | 1024 | 2048>{});
             if (raw && t16) return f(std::integral_constant<int, 8192 | 128 | 1024>{});
+            if (raw && uk32) {  // (32-bit deltas skipping single-key zone blocks)
+                if (m16 && runs1) return f(std::integral_constant<int, 16384 | 32 | 128 | 1024 | 2048 | 4096>{});
+                if (m16) return f(std::integral_constant<int, 16384 | 32 | 128 | 1024 | 2048>{});
+                return f(std::integral_constant<int, 16384 | 32 | 128 | 1024>{});
+            }
             if (raw && m16 && runs1) return f(std::integral_constant<int, 32 | 128 | 1024 | 2048 | 4096>{});
             if (raw && m16) return f(std::integral_constant<int, 32 | 128 | 1024 | 2048>{});
             if (raw) return f(std::integral_constant<int, 32 | 128 | 1024>{});
@@ -1801,12 +1827,14 @@ static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, boo
     }
     if constexpr (MET == 0 && !ORD && HK == 1) {
         if (raw && t16 && !hv_f64) return f(std::integral_constant<int, 8192 | 1024>{});
+        if (raw && t32 && uk32 && !hv_f64) return f(std::integral_constant<int, 16384 | 32 | 1024>{});
         if (raw && t32 && !hv_f64) return f(std::integral_constant<int, 32 | 1024>{});
     }
     if constexpr (MET == 0 && ORD && (HK == 0 || HK == 1)) {  // counting terms grids over 16-bit ordinals
         if (raw && c16 && !dord) {
             if constexpr (HK == 1) {
                 if (t16 && !hv_f64) return f(std::integral_constant<int, 16 | 8192 | 1024>{});
+                if (t32 && uk32 && !hv_f64) return f(std::integral_constant<int, 16384 | 48 | 1024>{});
                 if (t32 && !hv_f64) return f(std::integral_constant<int, 48 | 1024>{});
             } else {
                 return f(std::integral_constant<int, 16 | 1024>{});
@@ -1832,6 +1860,8 @@ static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, boo
                 if (t32 && !hv_f64) {
                     if (c16 && m16 && acc && t16) return f(std::integral_constant<int, 16 | 8192 | 64 | 256 | 512>{});
                     if (c16 && m16 && t16) return f(std::integral_constant<int, 16 | 8192 | 64 | 256>{});
+                    if (c16 && m16 && acc && uk32) return f(std::integral_constant<int, 16384 | 48 | 64 | 256 | 512>{});
+                    if (c16 && m16 && uk32) return f(std::integral_constant<int, 16384 | 48 | 64 | 256>{});
                     if (c16 && m16 && acc) return f(std::integral_constant<int, 48 | 64 | 256 | 512>{});
                     if (c16 && m16) return f(std::integral_constant<int, 48 | 64 | 256>{});
                     if (c16) return f(std::integral_constant<int, 48 | 64>{});
@@ -1878,7 +1908,7 @@ template <bool ORD, int HK, int MET>
 static void launch_t(const CollectParams& p, bool wide, uint32_t grid, size_t lds, hipStream_t st) {
     with_vk<ORD, HK, MET>(p.hv_f64 != 0, p.mv_f64 != 0, p.ord_src != nullptr, p.ord16 != nullptr,
                           p.hv32 != nullptr || p.hv16 != nullptr, p.hv16 != nullptr, (p.mv32 || p.mv16) && p.pk_shift != 0, (p.mv32 || p.mv16) && p.pk_shift == 0, p.mv16 != nullptr,
-                          p.accept != nullptr, p.raw_dense != 0, p.runs1 != 0, [&](auto vk) {
+                          p.accept != nullptr, p.raw_dense != 0, p.runs1 != 0, p.ukey32 != 0, [&](auto vk) {
         return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
             hipLaunchKernelGGL((collect_kernel<ORD, HK, MET, decltype(vk)::value, decltype(wg)::value>), dim3(grid),
                                dim3(decltype(wg)::value), lds, st, p);
@@ -1901,7 +1931,8 @@ template <bool ORD, int HK, int MET>
 static int occ_t(size_t lds, int vkbits, bool wide) {
     return with_vk<ORD, HK, MET>((vkbits & 1) != 0, (vkbits & 2) != 0, (vkbits & 8) != 0, (vkbits & 16) != 0,
                                  (vkbits & (32 | 8192)) != 0, (vkbits & 8192) != 0, (vkbits & 64) != 0, (vkbits & 128) != 0, (vkbits & 256) != 0,
-                                 (vkbits & 512) != 0, (vkbits & 1024) != 0, (vkbits & 4096) != 0, [&](auto vk) {
+                                 (vkbits & 512) != 0, (vkbits & 1024) != 0, (vkbits & 4096) != 0, (vkbits & 16384) != 0,
+                                 [&](auto vk) {
         return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
             int n = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(

@@ -110,6 +110,8 @@ struct CollectParams {
     uint32_t hot_t;      // the segment's most frequent ordinal (a sampled hint; kMissingOrd: none) -- ESGPU_PI_HOT builds
     int32_t raw_dense;   // histogram-only grid over dense compact columns, no filter: the raw-load kernels (VK bit 1024)
     int32_t runs1;       // integer runs over time-sorted data: one run accumulator per thread (VK bit 4096)
+    int32_t ukey32;      // raw-load kernels over 32-bit timestamp deltas skip single-key zone blocks (VK bit 16384:
+                         // roughly time-ordered data whose blocks mostly hold one key; block deltas always do)
     int32_t vcnt_mode;   // separate value counts (metric column has missing values)
     int32_t ocnt_mode;   // separate outer-level doc counts (inner dimension column has missing values)
     uint32_t ncopies;    // terms-only LDS grids: copies of the additive cells (count, value count, sum, sum of squares);

@@ -1059,6 +1059,8 @@ struct Group {
     std::vector<ChildSrc> kids;      // bucket root: its children in request order
 };
 
+constexpr uint32_t kZuSlots = 64;  // zone-skip counters per collect call (esgpu_plan.s_zu)
+
 struct esgpu_plan {
     esgpu_ctx* ctx = nullptr;
     hipStream_t stream = nullptr;
@@ -1102,6 +1104,7 @@ struct esgpu_plan {
     Scratch s_zu;
     PinnedBuf zu_host;
     uint32_t zu_n = 0;
+    uint8_t zu_w[kZuSlots] = {};  // ... and the timestamp bytes per doc of each launch (2: block deltas, 4: 32-bit deltas)
     DevBuf d_claim;            // collect kernel's chunk-claim counter pair (zeroed once; every launch leaves it zero)
     Scratch s_hcur, s_hused, s_hslab;  // hot/cold counting: overflow cursors, static-region fills, hot slabs
     PinnedBuf h_hcerr;         // hot/cold counting: capacity-violation word (written by the scatter kernel)
@@ -1682,7 +1685,7 @@ static bool int_runs_on();
 static bool runs1_on();
 static bool b16_on(const esgpu_ctx* c);
 static bool pi_cells(const esgpu_ctx* c);
-static uint32_t pi_copies();
+static uint32_t pi_copies(int met);
 static const uint16_t* ensure_ord16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
 static const uint32_t* ensure_d32(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
 static const uint16_t* ensure_d16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
@@ -3085,7 +3088,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
             const size_t b = collect_lds_bytes(LT, W, L_met, L_vcnt, L_ocnt, nc, pi);
             if (b <= kLdsPair) { P.ncopies = nc; lds = b; break; }
         }
-    } else if (pi && P.lds_mode && L_HIST && pi_copies() > 1 && !wide) {
+    } else if (pi && P.lds_mode && L_HIST && pi_copies(L_met) > 1 && !wide) {
         // packed cells are 16 B instead of 28: a time-sorted window of 2 keys leaves room for lane-rotated copies of the
         // count + sum words (the Zipf-head terms of a wave otherwise queue on one LDS address)
         if (P.windowed && W > 2) {
@@ -3093,7 +3096,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
             P.W = W;
             lds = collect_lds_bytes(LT, W, L_met, L_vcnt, L_ocnt, 1, pi);
         }
-        for (uint32_t nc = pi_copies(); nc > 1; --nc) {
+        for (uint32_t nc = pi_copies(L_met); nc > 1; --nc) {
             const size_t b = collect_lds_bytes(LT, W, L_met, L_vcnt, L_ocnt, nc, pi);
             if (b <= kLdsPair) { P.ncopies = nc; lds = b; break; }
         }
@@ -3141,9 +3144,15 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     // integer runs over time-sorted data (90 % of the blocks span less than one interval): one run per thread; roughly
     // time-ordered data alternates between neighbouring keys and keeps three
     P.runs1 = m32 && P.mv16 && hc && pl.interval > 0 && hc->zspan < pl.interval && runs1_on() ? 1 : 0;
+    // raw-load kernels over 32-bit timestamp deltas (block deltas did not apply: runs spanning 2^16 ms or more) skip the
+    // single-key zone blocks' deltas where most blocks hold one key (90 % of the blocks span less than one interval:
+    // roughly time-ordered data displaced by minutes); with wider displacement the skip's conditional load costs more
+    // than it saves (north star at +-1 h: 2.06 -> 2.40 ms, r6c)
+    P.ukey32 = L_HIST && !P.hv16 && P.hv32 && ((pi && P.ord16 && P.mv16) || P.raw_dense) && !P.kstart && hc &&
+               pl.interval > 0 && hc->zspan < pl.interval ? 1 : 0;
     const int vk = (P.hv_f64 ? 1 : 0) | (P.mv_f64 ? 2 : 0) | (P.ord_src ? 8 : 0) | (P.ord16 ? 16 : 0) | (P.hv32 ? 32 : 0) |
                    (pi ? 64 : 0) | (m32 ? 128 : 0) | (P.mv16 ? 256 : 0) | (fold ? 512 : 0) | (P.raw_dense ? 1024 : 0) |
-                   (P.runs1 ? 4096 : 0) | (P.hv16 ? 8192 : 0);
+                   (P.runs1 ? 4096 : 0) | (P.hv16 ? 8192 : 0) | (P.ukey32 ? 16384 : 0);
     const uint64_t occ_key = ((uint64_t)lds << 24) | ((uint64_t)wide << 23) | ((uint64_t)vk << 8) | ((uint64_t)L_met << 4) |
                              ((uint64_t)hk << 1) | (L_ORD ? 1 : 0);
     if (pl.occ_key != occ_key) {
@@ -3200,11 +3209,12 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         P.claim = (unsigned int*)p->d_claim.p;
         grid = slots;
     }
-    if ((P.lds_mode && P.windowed) || P.hv16) {  // (block-delta kernels read the timestamps of multi-key blocks only)
+    // the raw-load kernels over block deltas or 32-bit deltas read the timestamps of multi-key zone blocks only
+    const bool raw_keys = L_HIST && (P.hv16 || P.ukey32);
+    if ((P.lds_mode && P.windowed) || raw_keys) {
         P.zkey = (const int64_t*)p->s_zkey.ensure(p->ctx, (size_t)std::max(P.n_blocks, 1u) * 16);
         unsigned long long* ud = nullptr;
-        constexpr uint32_t kZuSlots = 64;
-        if (P.hv16 && p->zu_n < kZuSlots) {
+        if (raw_keys && p->zu_n < kZuSlots) {
             ud = (unsigned long long*)p->s_zu.ensure(p->ctx, kZuSlots * 8) + p->zu_n;
             HIPX(hipMemsetAsync(ud, 0, 8, p->stream));
         }
@@ -3213,6 +3223,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         if (ud) {
             uint64_t* h = (uint64_t*)p->zu_host.ensure(kZuSlots * 8);
             HIPX(hipMemcpyAsync(h + p->zu_n, ud, 8, hipMemcpyDeviceToHost, p->stream));
+            p->zu_w[p->zu_n] = P.hv16 ? 2 : 4;  // timestamp bytes per doc the skipped blocks did not read
             ++p->zu_n;
         }
     }
@@ -3276,18 +3287,19 @@ static bool dyn_claim_on() {
     return dyn_claim != 0;
 }
 // packed integer metric cells (CollectParams.pk_shift; ESGPU_PI=0: the f64 cells, for A/B runs) and the lane-rotated
-// copies of their count + sum words under a time window (ESGPU_PI_COPIES, 1 = none)
+// copies of their count + sum words under a time window (ESGPU_PI_COPIES, 1 = none; default: 2 for avg leaves -- the
+// Zipf-head terms' adds on one LDS word are their limit, terms{dh{avg}} 0.843 -> 0.790 ms at 1B, config 5 1.998 -> 1.928
+// ms, r6f -- and 1 with min / max, where the hot term's register run takes those adds instead)
 #ifndef ESGPU_PI_COPIES
-#define ESGPU_PI_COPIES 1
+#define ESGPU_PI_COPIES 0
 #endif
 static bool pi_cells(const esgpu_ctx* c) { return c->opt_pi.load() != 0; }
-static uint32_t pi_copies() {
-    static const uint32_t n = [] {
+static uint32_t pi_copies(int met) {
+    static const int v = [] {
         const char* e = std::getenv("ESGPU_PI_COPIES");
-        const int v = e && *e ? std::atoi(e) : ESGPU_PI_COPIES;
-        return (uint32_t)std::min(std::max(v, 1), 4);
+        return e && *e ? std::atoi(e) : ESGPU_PI_COPIES;
     }();
-    return n;
+    return v > 0 ? (uint32_t)std::min(v, 4) : met == 1 ? 2u : 1u;
 }
 
 // Compact columns: a segment's ordinals and timestamps need fewer bits than their upload width -- Lucene
@@ -3732,8 +3744,8 @@ extern "C" int esgpu_plan_last_collect_stats(const esgpu_plan* cp, double* kerne
             if (p->zu_n) {  // the timestamps of single-key zone blocks were not read
                 HIPX(hipStreamSynchronize(p->stream));
                 uint64_t ud = 0;
-                for (uint32_t i = 0; i < p->zu_n; ++i) ud += ((const uint64_t*)p->zu_host.p)[i];
-                p->last_bytes -= std::min<uint64_t>(p->last_bytes, 2 * ud);
+                for (uint32_t i = 0; i < p->zu_n; ++i) ud += ((const uint64_t*)p->zu_host.p)[i] * p->zu_w[i];
+                p->last_bytes -= std::min<uint64_t>(p->last_bytes, ud);
                 p->zu_n = 0;
             }
         }
@@ -6067,50 +6079,68 @@ static Block xr_reduce_terms(esgpu_plan* p0, const unsigned long long* recs, int
     const Pipeline& P0 = p0->pipes[g.pipes[0]];
     Block out = terms_shell(p0, g.root, {});
     int64_t sumErr = 0, other = 0;
-    std::vector<int64_t> cnt(T, 0), err(T, 0);
-    std::vector<uint8_t> seen(T, 0);
-    std::vector<uint32_t> ords;
+    // the shards' picks as (ordinal, shard) entries, grouped by ordinal: sparse in the S x K picks, not dense in the
+    // dictionary (10M ordinals for config 3)
+    struct Pick { uint32_t ord, shard; int64_t count; };
+    std::vector<Pick> picks;
+    std::vector<int64_t> shardErr(S, 0);
     won.assign(S, {});
     for (int s = 0; s < S; ++s) {
         const unsigned long long* o = recs + (size_t)s * rec;
         const uint64_t np = o[0];
+        require(np <= rec - 2, ESGPU_ERR_DEVICE, "internal: selection record overflows its row");
         other += (int64_t)o[1];
         int64_t thisErr;  // InternalTerms: the shard's doc count error
         if ((int64_t)np < out.shard_size || out.order == ESGPU_ORDER_TERM_ASC || out.order == ESGPU_ORDER_TERM_DESC) thisErr = 0;
         else if (out.order == ESGPU_ORDER_COUNT_DESC) thisErr = (int64_t)(o[2 + np - 1] >> 32);  // its last bucket's count
         else thisErr = -1;
+        shardErr[s] = thisErr;
         if (sumErr != -1) sumErr = thisErr == -1 ? -1 : sumErr + thisErr;
         won[s].resize(np);
         for (uint64_t j = 0; j < np; ++j) {
             const uint32_t ord = (uint32_t)o[2 + j];
             require(ord < T, ESGPU_ERR_DEVICE, "internal: selection record ordinal out of range");
             won[s][j] = ord;
-            if (!seen[ord]) { seen[ord] = 1; ords.push_back(ord); }
-            cnt[ord] += (int64_t)(o[2 + j] >> 32);
-            if (err[ord] != -1) err[ord] = thisErr == -1 ? -1 : err[ord] + thisErr;  // Bucket.reduce
+            picks.push_back({ord, (uint32_t)s, (int64_t)(o[2 + j] >> 32)});
         }
         std::sort(won[s].begin(), won[s].end());
     }
+    std::sort(picks.begin(), picks.end(), [](const Pick& a, const Pick& b) { return a.ord != b.ord ? a.ord < b.ord : a.shard < b.shard; });
+    std::vector<uint32_t> ords;
+    std::vector<int64_t> tcnt, terr;  // per distinct ordinal (parallel to ords)
+    for (size_t i = 0; i < picks.size();) {
+        const uint32_t ord = picks[i].ord;
+        int64_t c = 0, e = 0;
+        for (; i < picks.size() && picks[i].ord == ord; ++i) {
+            c += picks[i].count;
+            const int64_t te = shardErr[picks[i].shard];
+            if (e != -1) e = te == -1 ? -1 : e + te;  // Bucket.reduce
+        }
+        ords.push_back(ord);
+        tcnt.push_back(c);
+        terr.push_back(e);
+    }
     const size_t nb = ords.size();
-    std::vector<uint32_t> keep;
+    std::vector<uint32_t> keep;  // indices into ords
     keep.reserve(nb);
-    for (uint32_t o : ords) {
-        if (err[o] != -1) err[o] = sumErr == -1 ? -1 : sumErr - err[o];
-        if (cnt[o] >= out.min_doc_count) keep.push_back(o);
+    for (size_t i = 0; i < nb; ++i) {
+        if (terr[i] != -1) terr[i] = sumErr == -1 ? -1 : sumErr - terr[i];
+        if (tcnt[i] >= out.min_doc_count) keep.push_back((uint32_t)i);
     }
     const size_t size = std::min<size_t>((size_t)std::max(out.required_size, 0), nb);
     const int32_t order = out.order;
-    auto less = [&](uint32_t a, uint32_t b) {  // cmp_terms with the ordinal as the term
+    auto less = [&](uint32_t x, uint32_t y) {  // cmp_terms with the ordinal as the term
+        const uint32_t a = ords[x], b = ords[y];
         switch (order) {
-            case ESGPU_ORDER_COUNT_DESC: return cnt[a] != cnt[b] ? cnt[a] > cnt[b] : a < b;
-            case ESGPU_ORDER_COUNT_ASC: return cnt[a] != cnt[b] ? cnt[a] < cnt[b] : a < b;
+            case ESGPU_ORDER_COUNT_DESC: return tcnt[x] != tcnt[y] ? tcnt[x] > tcnt[y] : a < b;
+            case ESGPU_ORDER_COUNT_ASC: return tcnt[x] != tcnt[y] ? tcnt[x] < tcnt[y] : a < b;
             case ESGPU_ORDER_TERM_DESC: return a > b;
             default: return a < b;
         }
     };
     if (keep.size() > size) {
         std::partial_sort(keep.begin(), keep.begin() + size, keep.end(), less);
-        for (size_t i = size; i < keep.size(); ++i) other += cnt[keep[i]];
+        for (size_t i = size; i < keep.size(); ++i) other += tcnt[keep[i]];
         keep.resize(size);
     } else {
         std::sort(keep.begin(), keep.end(), less);
@@ -6118,10 +6148,10 @@ static Block xr_reduce_terms(esgpu_plan* p0, const unsigned long long* recs, int
     ++out.n;
     out.doc_count_error.push_back(sumErr == -1 ? -1 : (S == 1 ? 0 : sumErr));
     out.other_doc_count.push_back(other);
-    for (uint32_t o : keep) {
-        const std::string term = plan_term(p0, P0, o);
-        push_bucket(out, o, &term, cnt[o]);
-        out.berr.back() = err[o];
+    for (uint32_t i : keep) {
+        const std::string term = plan_term(p0, P0, ords[i]);
+        push_bucket(out, ords[i], &term, tcnt[i]);
+        out.berr.back() = terr[i];
     }
     end_instance(out);
     return out;

@@ -47,7 +47,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-align", dest="align", action="store_false",
                     help="do not wait for every rank's collect before the reduce")
+    ap.add_argument("--rccl", action="store_true",
+                    help="one rank over an RCCL communicator (the collectives on the device, no in-process barriers or "
+                         "stream waits): the library's own host time per request on the path a GPU per rank takes")
     a = ap.parse_args()
+    if a.rccl:
+        a.ranks = 1
     aggs, fields, filters = request(a.workload)
     W = a.ranks
     host_ms = [[] for _ in range(W)]
@@ -59,7 +64,8 @@ def main():
     def rank(r):
         try:
             eng = ea.Engine(0)
-            comm = ea.Communicator.local("rank_sim", W, r)
+            comm = (ea.Communicator(eng, 1, 0, ea.Communicator.unique_id()) if a.rccl
+                    else ea.Communicator.local("rank_sim", W, r))
             seg = eng.synthetic_segment(a.docs, fields=fields, shard=r)
             plan = eng.plan(aggs, filters=filters, number_of_shards=W)
             ready.wait()
@@ -100,7 +106,7 @@ def main():
         sys.exit(1)
     per_rank = [statistics.median(h) for h in host_ms]
     print(json.dumps({
-        "workload": a.workload, "ranks": W, "aligned": a.align, "docs_per_shard": a.docs, "requests": a.reqs, "paths": sorted(paths),
+        "workload": a.workload, "ranks": W, "transport": "rccl" if a.rccl else "in-process", "aligned": a.align, "docs_per_shard": a.docs, "requests": a.reqs, "paths": sorted(paths),
         "host_ms_per_request_median_by_rank": [round(x, 4) for x in per_rank],
         "host_ms_per_request_root": round(per_rank[0], 4),
         "host_ms_per_request_max_rank": round(max(per_rank), 4),
