@@ -650,15 +650,19 @@ __device__ __forceinline__ void run_flush(const CollectParams& P, const Acc& a, 
 template <int MET, int VK = 0> constexpr int runs_for() {
     return MET == 0 ? 1 : (VK & 4096) != 0 ? 1 : (VK & 2048) != 0 ? ESGPU_INT_RUNS_NR : ESGPU_RUNS;
 }
+#ifndef ESGPU_PI_NHOT  // hot ordinals with register runs in the packed-cell kernels (CollectParams.hot_t, up to 4)
+#define ESGPU_PI_NHOT 1
+#endif
+constexpr int kNHot = ESGPU_PI_NHOT;
 template <int NR>
 struct Runs {
     Run r[NR];
     uint32_t victim;
-    // packed integer cells (VK bit 64) with ESGPU_PI_HOT: the segment's most frequent ordinal (CollectParams.hot_t)
-    // accumulated in registers for its current key slot -- the Zipf head's docs leave the LDS atomics, whose same-address
-    // conflicts they caused
-    uint32_t hslot, hlo, hhi;
-    unsigned long long hpk;
+    // packed integer cells (VK bit 64): the segment's most frequent ordinals (CollectParams.hot_t) accumulated in
+    // registers for the current key slot -- the Zipf head's docs leave the LDS atomics, whose same-address conflicts they
+    // caused (ESGPU_PI_HOTU in the uniform-key path, ESGPU_PI_HOT per doc)
+    uint32_t hslot, hlo[kNHot], hhi[kNHot];
+    uint32_t hcnt[kNHot], hsum[kNHot];  // docs and their delta sum (a lane holds < 65,536 docs of a workgroup range)
 };
 template <int NR>
 __device__ __forceinline__ void runs_reset(Runs<NR>& R) {
@@ -666,9 +670,13 @@ __device__ __forceinline__ void runs_reset(Runs<NR>& R) {
     for (int k = 0; k < NR; ++k) run_reset(R.r[k]);
     R.victim = 0;
     R.hslot = ~0u;
-    R.hlo = ~0u;
-    R.hhi = 0u;
-    R.hpk = 0ull;
+#pragma unroll
+    for (int k = 0; k < kNHot; ++k) {
+        R.hlo[k] = ~0u;
+        R.hhi[k] = 0u;
+        R.hcnt[k] = 0u;
+        R.hsum[k] = 0u;
+    }
 }
 #ifndef ESGPU_PI_HOT
 #define ESGPU_PI_HOT 0
@@ -686,18 +694,22 @@ __device__ __forceinline__ void runs_reset(Runs<NR>& R) {
 // the hot ordinal's run into its LDS cell (before a window moves, and at the end)
 template <int MET, int NR>
 __device__ __forceinline__ void pi_hot_flush(const CollectParams& P, const Acc& a, Runs<NR>& R, uint32_t T) {
-    if (R.hslot != ~0u && R.hpk) {
-        const uint32_t c = R.hslot * T + P.hot_t;
-        atomicAdd(&a.pk[c + a.coff], R.hpk);
-        if (MET >= 2) {
-            if (R.hlo < a.mm[2 * c]) atomicMin(&a.mm[2 * c], R.hlo);
-            if (R.hhi > a.mm[2 * c + 1]) atomicMax(&a.mm[2 * c + 1], R.hhi);
+#pragma unroll
+    for (int k = 0; k < kNHot; ++k) {
+        if (R.hslot != ~0u && R.hcnt[k]) {
+            const uint32_t c = R.hslot * T + P.hot_t[k];
+            atomicAdd(&a.pk[c + a.coff], ((unsigned long long)R.hcnt[k] << P.pk_shift) + R.hsum[k]);
+            if (MET >= 2) {
+                if (R.hlo[k] < a.mm[2 * c]) atomicMin(&a.mm[2 * c], R.hlo[k]);
+                if (R.hhi[k] > a.mm[2 * c + 1]) atomicMax(&a.mm[2 * c + 1], R.hhi[k]);
+            }
         }
+        R.hlo[k] = ~0u;
+        R.hhi[k] = 0u;
+        R.hcnt[k] = 0u;
+        R.hsum[k] = 0u;
     }
     R.hslot = ~0u;
-    R.hlo = ~0u;
-    R.hhi = 0u;
-    R.hpk = 0ull;
 }
 template <int MET, int MS, int NR, bool INT = false>
 __device__ __forceinline__ void runs_flush(const CollectParams& P, const Acc& a, Runs<NR>& R) {
@@ -1030,7 +1042,8 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
         }
         // separate outer counts: one wave-uniform branch per 4 docs (inside the doc loop the compiler kept each doc's
         // masked atomic and its exec bookkeeping even when the mode counts nothing: ~10 scalar instructions per doc)
-        if (P.ocnt_mode == OCNT_TERMS) {
+        if ((VK & 32768) != 0) {  // (no per-doc outer counts: VK bit 32768)
+        } else if (P.ocnt_mode == OCNT_TERMS) {
             if (outer)
 #pragma unroll
                 for (int j = 0; j < kVec; ++j)
@@ -1044,14 +1057,15 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
 #if ESGPU_PI_HOT
 #pragma unroll
         for (int j = 0; j < kVec; ++j) {
-            if (!((hit >> j) & 1) || d.ord[j] != P.hot_t) continue;
+            if (!((hit >> j) & 1) || d.ord[j] != P.hot_t[0]) continue;
             if (slot[j] != run.hslot) {
                 pi_hot_flush<MET>(P, a, run, T);
                 run.hslot = slot[j];
             }
-            run.hpk += one + d.mvd[j];
-            run.hlo = min(run.hlo, d.mvd[j]);
-            run.hhi = max(run.hhi, d.mvd[j]);
+            run.hcnt[0] += 1u;
+            run.hsum[0] += d.mvd[j];
+            run.hlo[0] = min(run.hlo[0], d.mvd[j]);
+            run.hhi[0] = max(run.hhi[0], d.mvd[j]);
             hit &= ~(1u << j);
         }
 #endif
@@ -1185,6 +1199,9 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
 #ifndef ESGPU_PI_HOTU  // the segment's most frequent ordinal counted and summed in registers in uniform blocks: 2 = with
 #define ESGPU_PI_HOTU 2  // (min, max) leaves only (north star 1.104 -> 1.046 ms at 1B, r6f: its LDS adds were the kernel's
 #endif                   // limit; avg grids, which are not LDS-bound, measured 5 % slower with it), 1 = always, 0 = never
+#ifndef ESGPU_PI_HOTMM  // (A/B) the hot ordinal's register run keeps its (min, max) too (no LDS read for its docs)
+#define ESGPU_PI_HOTMM 0  // (measured slower: north star 1.081 -> 1.133 ms at 1B, r6h -- its VALU cost; 2 or 3 hot ordinals 1.54 / 1.91)
+#endif
 #ifndef ESGPU_PI_MMU  // (A/B) uniform blocks' (min, max) updates: 2 = one divergent region per doc (as ESGPU_PI_MMCHECK 2),
 #define ESGPU_PI_MMU 2  // 3 = branch-free -- every lane issues both atomics, lanes whose bounds do not move on a spare word
 #endif
@@ -1207,7 +1224,9 @@ __device__ __forceinline__ void pi_uniform(const CollectParams& P, const Acc& a,
         if constexpr ((VK & 512) != 0) okm &= ~((~(uint32_t)(h.racc >> (h.doc0 & 63)) & 0xFu) << (4 * hh));
     }
     // outer counts (wave-uniform mode): per-term counts need every doc; a per-key count is the wave's passing docs
-    if (P.ocnt_mode == OCNT_TERMS) {
+    // (VK bit 32768: the plan's outer counts are not counted per doc -- derived from the cells at the flush)
+    if ((VK & 32768) != 0) {
+    } else if (P.ocnt_mode == OCNT_TERMS) {
         if (outer)
 #pragma unroll
             for (int j = 0; j < N; ++j)
@@ -1234,23 +1253,34 @@ __device__ __forceinline__ void pi_uniform(const CollectParams& P, const Acc& a,
         run.hslot = sl;
     }
     {
-        const uint32_t ht = P.hot_t;
-        uint32_t hc = 0, hs = 0;
 #pragma unroll
-        for (int j = 0; j < N; ++j) {
-            const bool ho = hit[j] && t[j] == ht;
-            hc += ho ? 1u : 0u;
-            hs += ho ? dv[j] : 0u;
-            hpk[j] = hit[j] && !ho;
+        for (int k = 0; k < kNHot; ++k) {
+            const uint32_t ht = P.hot_t[k];
+            uint32_t hc = run.hcnt[k], hs = run.hsum[k], hl = run.hlo[k], hh = run.hhi[k];
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                const bool ho = hit[j] & (t[j] == ht);
+                hc += ho ? 1u : 0u;
+                hs += ho ? dv[j] : 0u;
+                if (MET >= 2 && ESGPU_PI_HOTMM) {  // ... and its extrema: the hot docs leave the (min, max) reads too
+                    hl = min(hl, ho ? dv[j] : ~0u);
+                    hh = max(hh, ho ? dv[j] : 0u);
+                    hit[j] = hit[j] & !ho;
+                }
+                hpk[j] = hpk[j] & !ho;
+            }
+            run.hcnt[k] = hc;
+            run.hsum[k] = hs;
+            run.hlo[k] = hl;
+            run.hhi[k] = hh;
         }
-        run.hpk += ((unsigned long long)hc << P.pk_shift) + hs;
     }
     }
     uint32_t mlo[N], mhi[N];
     if (MET >= 2) {
 #pragma unroll
-        for (int j = 0; j < N; ++j) {
-            const u32x2_t m = *reinterpret_cast<const u32x2_t*>(a.mm + 2 * (hit[j] ? cb + t[j] : 0u));
+        for (int j = 0; j < N; ++j) {  // (a doc that hits nothing reads cell 0: one broadcast address)
+            const u32x2_t m = *reinterpret_cast<const u32x2_t*>(hit[j] ? a.mm + 2 * (cb + t[j]) : a.mm);
             mlo[j] = m.x;
             mhi[j] = m.y;
         }
@@ -1604,7 +1634,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
     auto slide_to = [&](uint32_t k0) {
         if (dirty) {
             if (!ORD) runs_flush<MET, kMS, runs_for<MET, VKL>(), kIntRuns<ORD, MET, VKL>>(P, s, run);
-            if constexpr (PI && (ESGPU_PI_HOT || ESGPU_PI_HOTU)) pi_hot_flush<MET>(P, s, run, T);
+            if constexpr (PI && (ESGPU_PI_HOT != 0 || ESGPU_PI_HOTU != 0)) pi_hot_flush<MET>(P, s, run, T);
             if constexpr (PI) flush_window_pi<MET, WGS>(P, s, T, W, win0, ncp);
             else flush_window<MET, kMS, WGS>(P, s, T, W, win0, ncp);
         }
@@ -1733,7 +1763,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
 #endif
     if (P.lds_mode && (dirty || !(HIST && P.windowed)) && !ESGPU_FLUSH_DIAG) {
         if (!ORD) runs_flush<MET, kMS, runs_for<MET, VKL>(), kIntRuns<ORD, MET, VKL>>(P, s, run);
-        if constexpr (PI && (ESGPU_PI_HOT || ESGPU_PI_HOTU)) pi_hot_flush<MET>(P, s, run, T);
+        if constexpr (PI && (ESGPU_PI_HOT != 0 || ESGPU_PI_HOTU != 0)) pi_hot_flush<MET>(P, s, run, T);
         if constexpr (PI) flush_window_pi<MET, WGS>(P, s, T, W, win0, ncp);
         else flush_window<MET, kMS, WGS>(P, s, T, W, win0, ncp);
     }
@@ -1804,7 +1834,7 @@ static auto with_vk0(bool hv_f64, bool mv_f64, F f) {
 // over a long column.
 template <bool ORD, int HK, int MET, class F>
 static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, bool t16, bool pi, bool m32, bool m16, bool acc,
-                    bool raw, bool runs1, bool uk32, F f) {
+                    bool raw, bool runs1, bool uk32, bool noc, F f) {
     // t16: the key column is read as block deltas (VK bit 8192 in place of 32) -- by the raw-load kernels only; the host
     // picks it only for a launch that takes one of them (t32 is then set as well)
     // VK bit 128, a compact long metric (u32 deltas, values restored in the loader): histogram-only grids over compact
@@ -1858,6 +1888,11 @@ static auto with_vk(bool hv_f64, bool mv_f64, bool dord, bool c16, bool t32, boo
         if (pi && !mv_f64 && !dord) {
             if constexpr (HK == 1) {
                 if (t32 && !hv_f64) {
+                    // (+ bit 32768: the plan's outer counts are derived at the flush, none counted per doc)
+                    if (c16 && m16 && acc && t16 && noc) return f(std::integral_constant<int, 32768 | 16 | 8192 | 64 | 256 | 512>{});
+                    if (c16 && m16 && t16 && noc) return f(std::integral_constant<int, 32768 | 16 | 8192 | 64 | 256>{});
+                    if (c16 && m16 && acc && uk32 && noc) return f(std::integral_constant<int, 32768 | 16384 | 48 | 64 | 256 | 512>{});
+                    if (c16 && m16 && uk32 && noc) return f(std::integral_constant<int, 32768 | 16384 | 48 | 64 | 256>{});
                     if (c16 && m16 && acc && t16) return f(std::integral_constant<int, 16 | 8192 | 64 | 256 | 512>{});
                     if (c16 && m16 && t16) return f(std::integral_constant<int, 16 | 8192 | 64 | 256>{});
                     if (c16 && m16 && acc && uk32) return f(std::integral_constant<int, 16384 | 48 | 64 | 256 | 512>{});
@@ -1908,7 +1943,8 @@ template <bool ORD, int HK, int MET>
 static void launch_t(const CollectParams& p, bool wide, uint32_t grid, size_t lds, hipStream_t st) {
     with_vk<ORD, HK, MET>(p.hv_f64 != 0, p.mv_f64 != 0, p.ord_src != nullptr, p.ord16 != nullptr,
                           p.hv32 != nullptr || p.hv16 != nullptr, p.hv16 != nullptr, (p.mv32 || p.mv16) && p.pk_shift != 0, (p.mv32 || p.mv16) && p.pk_shift == 0, p.mv16 != nullptr,
-                          p.accept != nullptr, p.raw_dense != 0, p.runs1 != 0, p.ukey32 != 0, [&](auto vk) {
+                          p.accept != nullptr, p.raw_dense != 0, p.runs1 != 0, p.ukey32 != 0,
+                          p.ocnt_mode != OCNT_TERMS && p.ocnt_mode != OCNT_HIST, [&](auto vk) {
         return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
             hipLaunchKernelGGL((collect_kernel<ORD, HK, MET, decltype(vk)::value, decltype(wg)::value>), dim3(grid),
                                dim3(decltype(wg)::value), lds, st, p);
@@ -1932,7 +1968,7 @@ static int occ_t(size_t lds, int vkbits, bool wide) {
     return with_vk<ORD, HK, MET>((vkbits & 1) != 0, (vkbits & 2) != 0, (vkbits & 8) != 0, (vkbits & 16) != 0,
                                  (vkbits & (32 | 8192)) != 0, (vkbits & 8192) != 0, (vkbits & 64) != 0, (vkbits & 128) != 0, (vkbits & 256) != 0,
                                  (vkbits & 512) != 0, (vkbits & 1024) != 0, (vkbits & 4096) != 0, (vkbits & 16384) != 0,
-                                 [&](auto vk) {
+                                 (vkbits & 32768) != 0, [&](auto vk) {
         return with_wg<ORD, HK, MET>(wide, [&](auto wg) {
             int n = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(

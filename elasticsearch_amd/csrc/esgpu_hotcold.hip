@@ -330,6 +330,7 @@ __global__ __launch_bounds__(kHcWG) void hc_scatter_kernel(HcParams P) {
 // (element g * chunk + i, valid while i < used[g]) followed by the overflow pool (0xFFFF = unused)
 template <bool U16>
 __global__ __launch_bounds__(kHcCountWG) void hc_count_kernel(HcParams P) {
+    if (P.skip && *P.skip) return;  // (the hot slots settled the request's top-k)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t* cnt = (uint32_t*)smem;  // U16: [16384] two 16-bit counters per word, else [32768]
     uint32_t* used = cnt + (U16 ? (1u << kPartShift) / 2 : (1u << kPartShift));  // [G]
@@ -469,7 +470,12 @@ __global__ __launch_bounds__(256) void hc_hot_final_kernel(HcParams P, uint32_t 
         acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
     auto add = [&](uint32_t slot, uint32_t t) {
-        if (!t || slot >= P.hot_n) return;
+        if (slot >= P.hot_n) return;
+        if (P.slot_tot) {  // deferred cold lists: the slot's total (every slot written), folded onto its ordinal later
+            P.slot_tot[slot] = t;
+            return;
+        }
+        if (!t) return;
         const uint32_t o = P.hot_ord[slot];
         if (o < P.T) atomicAdd(&P.counts[o], t);
     };
@@ -659,6 +665,49 @@ __global__ __launch_bounds__(256) void hc_cold_sub_kernel(const uint32_t* rc, co
             if (!(v & kHcHotBit) && v < T) atomicSub(&counts[v], 1u);
         }
     }
+}
+
+// the deferred cold lists' fold: the hot slot totals onto their ordinals (after the overwriting cold count)
+__global__ __launch_bounds__(256) void hc_slot_fold_kernel(HcParams P) {
+    if (P.skip && *P.skip) return;
+    const uint32_t s = blockIdx.x * 256 + threadIdx.x;
+    if (s >= P.hot_n) return;
+    const uint32_t t = P.slot_tot[s], o = P.hot_ord[s];
+    if (t && o < P.T) atomicAdd(&P.counts[o], t);
+}
+void launch_hot_postings(const HcParams& hot, hipStream_t s) {
+    const size_t hlds = (size_t)hc_hot_counters(hot.hot_n) * 4;
+    hipLaunchKernelGGL(hc_hot16_count_kernel<false>, dim3(hot.G), dim3(kHotWG), hlds, s, hot);
+    launch_hot_reduce(hot, s);
+}
+void launch_cold_postings(const HcParams& hot, const HcParams& cold, hipStream_t s) {
+    if (cold.n_pieces) {
+        const size_t clds = (cold.u16_counters ? (1u << kPartShift) / 2 : (1u << kPartShift)) * 4 + (size_t)cold.G * 4;
+        if (cold.u16_counters) hipLaunchKernelGGL(hc_count_kernel<true>, dim3(cold.n_pieces), dim3(kHcCountWG), clds, s, cold);
+        else hipLaunchKernelGGL(hc_count_kernel<false>, dim3(cold.n_pieces), dim3(kHcCountWG), clds, s, cold);
+    }
+    hipLaunchKernelGGL(hc_slot_fold_kernel, dim3((hot.hot_n + 255) / 256), dim3(256), 0, s, hot);
+}
+__global__ void hot_topk_check_kernel(const unsigned long long* hot_keys, uint32_t k, uint32_t k_req, uint64_t max_cold,
+                                      uint64_t docs, int order, uint32_t* skip, unsigned long long* out_keys,
+                                      unsigned long long* out_sum) {
+    __shared__ uint32_t ok;
+    if (threadIdx.x == 0) {
+        // count order descending: the k-th pick present and above every cold ordinal's count (ties go to the smaller
+        // ordinal, which may be cold: strictly above)
+        const unsigned long long last = k_req ? hot_keys[k_req - 1] : 0ull;
+        ok = order == 0 && k_req >= 1 && last != 0 && ((last >> 32) & 0x7FFFFFFFull) > max_cold;
+        *skip = ok;
+    }
+    __syncthreads();
+    if (!ok) return;
+    for (uint32_t i = threadIdx.x; i < k; i += blockDim.x) out_keys[i] = hot_keys[i];
+    if (threadIdx.x == 0) *out_sum = docs;  // the sum of every ordinal's count: the segment's docs with a value
+}
+void launch_hot_topk_check(const unsigned long long* hot_keys, uint32_t k, uint32_t k_req, uint64_t max_cold, uint64_t docs,
+                           int order, uint32_t* skip, unsigned long long* out_keys, unsigned long long* out_sum, hipStream_t s) {
+    hipLaunchKernelGGL(hot_topk_check_kernel, dim3(1), dim3(256), 0, s, hot_keys, k, k_req, max_cold, docs, order, skip,
+                       out_keys, out_sum);
 }
 
 void launch_hotcold_postings(const HcParams& hot, const HcParams& cold, hipStream_t s) {

@@ -2213,6 +2213,7 @@ __device__ __forceinline__ void load_counts4(const TopkParams& P, uint32_t i, un
 }
 
 __global__ __launch_bounds__(1024) void topk_hist_kernel(TopkParams P) {
+    if (P.skip && *P.skip) return;
     __shared__ uint32_t hist[kTopkBins];
     for (uint32_t i = threadIdx.x; i < kTopkBins; i += 1024) hist[i] = 0;
     __syncthreads();
@@ -2235,6 +2236,7 @@ __global__ __launch_bounds__(1024) void topk_hist_kernel(TopkParams P) {
 // one workgroup: suffix sums of the histogram (bins are in key order) -> the highest bin b* whose suffix holds >= k
 // candidates, or 0 when fewer than k are eligible
 __global__ __launch_bounds__(kWG) void topk_thresh_kernel(TopkParams P) {
+    if (P.skip && *P.skip) return;
     __shared__ uint32_t v[kTopkBins];
     __shared__ uint32_t wave_tot[kWG / 64];
     __shared__ uint32_t first;
@@ -2253,6 +2255,7 @@ __global__ __launch_bounds__(kWG) void topk_thresh_kernel(TopkParams P) {
 }
 
 __global__ __launch_bounds__(1024) void topk_compact_kernel(TopkParams P) {
+    if (P.skip && *P.skip) return;
     const uint32_t tb = P.sel[0];
     const int lane = threadIdx.x & 63;
     for (uint32_t i0 = blockIdx.x * 1024 * 4; i0 < P.T; i0 += gridDim.x * 1024 * 4) {
@@ -2268,13 +2271,15 @@ __global__ __launch_bounds__(1024) void topk_compact_kernel(TopkParams P) {
             if (lane == __ffsll((long long)m) - 1) base = atomicAdd(&P.sel[1], (uint32_t)__popcll(m));
             base = __shfl(base, __ffsll((long long)m) - 1, 64);
             if (take)
-                P.cand[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = make_topk_key(P.order, c[j], i + j);
+                P.cand[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] =
+                    make_topk_key(P.order, c[j], P.ord_of ? P.ord_of[i + j] : i + j);
         }
     }
 }
 
 // one workgroup: best k of the n = sel[1] candidate keys, chunked bitonic sort + merge (chunk = pow2 >= n, <= 4096)
 __global__ __launch_bounds__(1024) void topk_final_kernel(TopkParams P) {
+    if (P.skip && *P.skip) return;
     __shared__ unsigned long long chunk[kTopkChunk];
     __shared__ unsigned long long best[2 * kTopkMax];
     const uint32_t n = P.sel[1];
@@ -2343,6 +2348,7 @@ void launch_topk_candidates(const TopkParams& p, hipStream_t s) {
 void launch_topk(const TopkParams& p, hipStream_t s) {
     if (p.order == 0 || p.order == 1) {  // count orders: select, then sort the few candidates
         const uint32_t g = std::max(1u, std::min(p.n_wg, (p.T + 4095) / 4096));
+        // (with p.skip the histogram is cleared even when the kernels return at once: harmless)
         (void)hipMemsetAsync(p.hist, 0, kTopkBins * 4, s);
         hipLaunchKernelGGL(topk_hist_kernel, dim3(g), dim3(1024), 0, s, p);
         hipLaunchKernelGGL(topk_thresh_kernel, dim3(1), dim3(kWG), 0, s, p);

@@ -107,7 +107,8 @@ struct CollectParams {
     const uint16_t* mv16;  // the same deltas in 16 bits when the values span < 2^16 (loader VK bit 256)
     int64_t mv_base;
     uint32_t pk_shift;
-    uint32_t hot_t;      // the segment's most frequent ordinal (a sampled hint; kMissingOrd: none) -- ESGPU_PI_HOT builds
+    uint32_t hot_t[4];   // the segment's most frequent ordinals (a sampled hint; kMissingOrd: none): the packed cells'
+                         // register runs (ESGPU_PI_NHOT of them)
     int32_t raw_dense;   // histogram-only grid over dense compact columns, no filter: the raw-load kernels (VK bit 1024)
     int32_t runs1;       // integer runs over time-sorted data: one run accumulator per thread (VK bit 4096)
     int32_t ukey32;      // raw-load kernels over 32-bit timestamp deltas skip single-key zone blocks (VK bit 16384:
@@ -538,6 +539,9 @@ struct HcParams {
     uint32_t* err;                     // set to 1 on a capacity violation (device-visible host word)
     int32_t u16_counters;              // every cold ordinal's count in the segment < 65536: packed LDS counters
     int32_t overwrite;                 // store the counts instead of adding (the plan's first segment)
+    uint32_t* slot_tot;                // postings hot pass, deferred cold lists: [hot_n] hot slot totals instead of
+                                       // atomics onto counts[hot_ord] (esgpu_runtime.cpp hc_pending)
+    const uint32_t* skip;              // non-null and set: the cold counting and the fold return at once
 };
 __host__ __device__ inline uint32_t hc_hot_counters(uint32_t hot_n) { return hot_n + 3 * (hot_n < kHcHotCopies ? hot_n : kHcHotCopies); }
 // per-workgroup hot slab row: the counters padded to 16 bytes (the reduce reads them as uint4)
@@ -549,6 +553,15 @@ void launch_hotcold(const HcParams& p, hipStream_t s);
 // (HcStats' cold lists): `hot` streams the recoded column and counts only the hot slots (G = hot.G workgroups), `cold`
 // counts the cold lists (one static region per partition, G = 1) with the scatter path's counting pass.
 void launch_hotcold_postings(const HcParams& hot, const HcParams& cold, hipStream_t s);
+// ... in two halves, for a request whose top-k the hot slots may settle alone (count order, the segment's largest cold
+// count below the k-th hot one): the hot pass with its slot totals into hot.slot_tot, and later -- unless *cold.skip --
+// the cold lists counted and the slot totals folded onto their ordinals
+void launch_hot_postings(const HcParams& hot, hipStream_t s);
+void launch_cold_postings(const HcParams& hot, const HcParams& cold, hipStream_t s);
+// the hot slots' top-k settles the request: skip = the k keys all present and the k-th count above max_cold; then the
+// final keys and the count sum (docs) are written where the full top-k would write them
+void launch_hot_topk_check(const unsigned long long* hot_keys, uint32_t k, uint32_t k_req, uint64_t max_cold, uint64_t docs,
+                           int order, uint32_t* skip, unsigned long long* out_keys, unsigned long long* out_sum, hipStream_t s);
 // stats time: the dense partition-ordered cold offsets -> one list per partition starting at pad_begin[p] (a multiple
 // of 64 elements), 0xFFFF between lists
 void launch_hc_pad(const uint16_t* dense, const uint32_t* dense_begin, const uint32_t* pad_begin, uint32_t P,
@@ -577,6 +590,8 @@ struct TopkParams {
     uint32_t n_wg;
     unsigned long long* out_keys;    // [k] winners (0 = none), best first
     unsigned long long* out_sum;     // [1] sum of counts over min_doc_count-eligible terms
+    const uint32_t* ord_of;          // count orders: counts[i] is ordinal ord_of[i]'s (null: ordinal i) -- hot slots
+    const uint32_t* skip;            // non-null and set: every kernel of this top-k returns at once (decided on the device)
 };
 constexpr uint32_t kTopkMax = 1024;
 void launch_topk(const TopkParams& p, hipStream_t s);

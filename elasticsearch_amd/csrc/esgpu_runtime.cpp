@@ -333,7 +333,7 @@ struct DevColumn {
     // (shared: a plan that collected the segment keeps it alive for its build, whatever happens to the segment meanwhile)
     std::shared_ptr<std::atomic<double>> hll_distinct = std::make_shared<std::atomic<double>>(-1.0);
     // the most frequent ordinal of ords() in a sample (a hint for the packed cells' register run; any value is correct)
-    uint32_t hot_ord = 0xFFFFFFFFu;
+    uint32_t hot_ord[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
     const void* hot_src = nullptr;
 
     const DevBuf& ords() const { return gdict ? gvalues : values; }       // what terms aggregations count by
@@ -1109,6 +1109,15 @@ struct esgpu_plan {
     Scratch s_hcur, s_hused, s_hslab;  // hot/cold counting: overflow cursors, static-region fills, hot slabs
     PinnedBuf h_hcerr;         // hot/cold counting: capacity-violation word (written by the scatter kernel)
     bool hc_check = false;     // a hot/cold collect ran since the last post_collection
+    // a single-segment plain terms request in count order on the postings form: the cold lists' counting deferred to
+    // the top-k, which runs it only when the hot slots do not settle the winners (collect_hotcold, hc_topk_launch)
+    struct HcPending {
+        bool on = false;
+        int pipe = -1;
+        HcParams hot{}, cold{};
+        std::shared_ptr<const HcStats> hs;  // keeps the segment statistics' buffers the two passes read
+    } hc_pend;
+    Scratch s_slot_tot, s_hcand, s_hhist, s_hkeys, s_hskip;
     PinnedBuf h_keys;
     hipEvent_t ev_mid = nullptr;
     PinnedBuf h_tcnt, h_rows, h_dst[6];
@@ -1691,7 +1700,7 @@ static const uint32_t* ensure_d32(esgpu_ctx* c, const DevColumn* col, const esgp
 static const uint16_t* ensure_d16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
 static const DevColumn* ensure_b16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
 static const void* wide_i64(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
-static uint32_t sampled_hot_ord(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s);
+static void sampled_hot_ords(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, uint32_t (&out)[4]);
 
 // The pipeline's clauses as device predicates: up to kMaxPreds of them are evaluated inside the collect kernels; with
 // more, all of them (and the accept bitset) are folded first into one doc bitset -- chained filter_bits passes of four
@@ -1926,6 +1935,8 @@ struct HcStats {
     bool u16 = false;            // every cold ordinal's count < 65536: packed 16-bit counters in the counting pass
     uint64_t pbuf_elems = 0;     // partition regions + kHcTile spare elements
     uint64_t hot_docs = 0, docs = 0;
+    uint64_t max_cold = 0;       // the largest count of a cold ordinal in the segment (unfiltered): a request's top-k
+                                 // in count order is settled by the hot slots alone when its k-th count is above it
     bool refused = false;        // outside what the hot/cold kernels handle (cached: the check counts the column)
     // recoded ordinal column (hot ordinals as kHcHotBit | slot); empty: no hot set, or released once the postings form is
     // ready (the hot16 column and the cold lists serve unfiltered requests) and rebuilt from the hot table on the first
@@ -2091,6 +2102,7 @@ static std::shared_ptr<const HcStats> ensure_hc_stats(esgpu_ctx* c, const DevCol
         for (uint32_t m : pmax) max_cold = std::max<uint64_t>(max_cold, m);
     }
     hs->u16 = max_cold < 65536;
+    hs->max_cold = max_cold;
     // layout: per partition, G static regions of `chunk` (its expected share per workgroup) then an overflow pool that
     // covers every way the docs can be spread over the workgroups: a workgroup allocates a new overflow chunk only when
     // its current one is full, so what it leaves unused is under one chunk (sizes: DESIGN.md §5)
@@ -2259,6 +2271,11 @@ static const uint32_t* ensure_rc(esgpu_ctx* c, const HcStats& hs, const DevColum
     return hs.d_rc.as<uint32_t>();
 }
 
+// config 3's deferred cold lists (collect_hotcold / hc_topk_launch; ESGPU_HC_PRUNE=0: always counted, for A/B runs)
+static bool hc_prune_on() {
+    static const bool on = [] { const char* e = std::getenv("ESGPU_HC_PRUNE"); return !(e && *e == '0'); }();
+    return on;
+}
 static bool collect_hotcold(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const DevColumn* oc,
                             const uint64_t* d_accept, const PredDev* pred, int npred, bool first_segment) {
     esgpu_ctx* c = p->ctx;
@@ -2320,13 +2337,37 @@ static bool collect_hotcold(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s,
         Hh.G = std::max(1u, (Hh.n_blocks + Hh.blocks_per_wg - 1) / Hh.blocks_per_wg);
         Hh.hot_slab = Hh.hot_n ? (uint32_t*)p->s_hslab.ensure(c, (size_t)hc_slab_stride(Hh.hot_n) * Hh.G * 4) : nullptr;
         Hh.rc16 = hs->d_hot16.p ? hs->d_hot16.as<uint16_t>() : nullptr;
-        if (Hh.rc16)  // the bytes this form moves: 2 B per doc of hot slots plus 2 B per listed cold doc (not 4 B per doc)
-            p->last_bytes = p->last_bytes - 2ull * s->max_doc + 2ull * (hs->docs - hs->hot_docs);
+        // a plain terms request in count order over one segment: the cold lists wait for the top-k (hc_topk_launch),
+        // which needs them only if some cold ordinal can reach the k-th count
+        const int pipe = (int)(&pl - p->pipes.data());
+        bool defer = hc_prune_on() && first_segment && Hh.rc16 && !d_accept && hs->hot_n;
+        if (defer) {
+            // (one terms aggregation and nothing else: no other reader of these counts)
+            const SpecNode& tn = p->specs[pl.root];
+            const bool plain = p->pipes.size() == 1 && p->groups.size() == 1 && p->groups[0].pipes.size() == 1 &&
+                               p->groups[0].pipes[0] == pipe && p->groups[0].kids.empty();
+            defer = plain && tn.s.type == ESGPU_AGG_TERMS && tn.s.order == ESGPU_ORDER_COUNT_DESC &&
+                    tn.s.shard_size >= 1 && (uint64_t)tn.s.shard_size <= std::min<uint64_t>(hs->hot_n, kTopkMax) &&
+                    pl.value_count > 65536 && pl.H == 1 && pl.ocnt_mode == OCNT_NONE;
+        }
+        if (Hh.rc16) {  // the bytes this form moves: 2 B per doc of hot slots plus 2 B per listed cold doc (not 4 B per doc)
+            p->last_bytes = p->last_bytes - 2ull * s->max_doc + (defer ? 0ull : 2ull * (hs->docs - hs->hot_docs));
+        }
         HIPX(hipEventRecord(pl.e0, st));
-        launch_hotcold_postings(Hh, K, st);
+        if (defer) {
+            Hh.slot_tot = (uint32_t*)p->s_slot_tot.ensure(c, (size_t)hs->hot_n * 4);
+            launch_hot_postings(Hh, st);
+            p->hc_pend.on = true;
+            p->hc_pend.pipe = pipe;
+            p->hc_pend.hot = Hh;
+            p->hc_pend.cold = K;
+            p->hc_pend.hs = hs;
+        } else {
+            launch_hotcold_postings(Hh, K, st);
+        }
         HIPX(hipGetLastError());
         HIPX(hipEventRecord(pl.e1, st));
-        p->last_path = 7;
+        p->last_path = defer ? 8 : 7;
         return true;
     }
     require(hc_scatter_lds_bytes(H.P, H.hot_n) <= 160 * 1024 - 256, ESGPU_ERR_STATE, "hot/cold LDS layout");
@@ -2336,6 +2377,72 @@ static bool collect_hotcold(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s,
     HIPX(hipEventRecord(pl.e1, st));
     p->last_path = 6;
     return true;
+}
+
+// after a sync of the plan's stream: a partition overran the capacity the segment statistics promised (a bug, never data)
+static void hc_check_err(esgpu_plan* p) {
+    if (!p->hc_check) return;
+    p->hc_check = false;
+    volatile uint32_t* err = p->h_hcerr.as<volatile uint32_t>();
+    const uint32_t e = *err;
+    *err = 0;
+    require(e == 0, ESGPU_ERR_DEVICE, "hot/cold counting: partition capacity exceeded");
+}
+
+// the deferred cold lists counted and folded (every reader of the counts but the top-k below: a second segment, a
+// host selection, the co-located reduce)
+static void hc_flush(esgpu_plan* p) {
+    if (!p->hc_pend.on) return;
+    launch_cold_postings(p->hc_pend.hot, p->hc_pend.cold, p->stream);
+    HIPX(hipGetLastError());
+    p->hc_pend = esgpu_plan::HcPending{};
+    p->hc_check = true;  // (the cold counting writes the capacity word)
+}
+
+// K3 over a pipeline's counts (build_terms_root, xr_terms).  With the cold lists deferred: the top-k of the hot slot
+// totals first; when its k-th count is above every cold ordinal's count in the segment (HcStats::max_cold), those are
+// the request's winners and the cold counting, the fold and the full top-k return at once (a device flag, no host
+// round trip); otherwise they run as without the deferral.
+static void hc_topk_launch(esgpu_plan* p, const Pipeline& P0, TopkParams K, uint32_t k_req, hipStream_t st) {
+    const int pipe = (int)(&P0 - p->pipes.data());
+    if (!p->hc_pend.on || p->hc_pend.pipe != pipe) {
+        hc_flush(p);
+        launch_topk(K, st);
+        return;
+    }
+    esgpu_ctx* c = p->ctx;
+    const esgpu_plan::HcPending pend = p->hc_pend;
+    p->hc_pend = esgpu_plan::HcPending{};
+    require(st == p->stream, ESGPU_ERR_STATE, "deferred cold lists on another stream");
+    const uint32_t hot_n = pend.hot.hot_n;
+    TopkParams Hk = K;
+    Hk.counts = nullptr;
+    Hk.counts32 = pend.hot.slot_tot;
+    Hk.ord_of = pend.hot.hot_ord;
+    Hk.T = hot_n;
+    Hk.n_wg = std::min<uint32_t>(512, (hot_n + 4095) / 4096);
+    Hk.cand = (unsigned long long*)p->s_hcand.ensure(c, (size_t)hot_n * 8);
+    uint32_t* hh = (uint32_t*)p->s_hhist.ensure(c, (2048 + 2) * 4);
+    Hk.hist = hh;
+    Hk.sel = hh + 2048;
+    unsigned long long* hk = (unsigned long long*)p->s_hkeys.ensure(c, ((size_t)K.k + 1) * 8);
+    Hk.out_keys = hk;
+    Hk.out_sum = hk + K.k;
+    Hk.skip = nullptr;
+    HIPX(hipMemsetAsync(Hk.out_sum, 0, 8, st));
+    launch_topk(Hk, st);
+    HIPX(hipGetLastError());
+    uint32_t* skip = (uint32_t*)p->s_hskip.ensure(c, 16);
+    launch_hot_topk_check(hk, K.k, k_req, pend.hs->max_cold, pend.hs->docs, K.order, skip, K.out_keys, K.out_sum, st);
+    HIPX(hipGetLastError());
+    HcParams hot = pend.hot, cold = pend.cold;
+    hot.skip = skip;
+    cold.skip = skip;
+    launch_cold_postings(hot, cold, st);
+    HIPX(hipGetLastError());
+    p->hc_check = true;
+    K.skip = skip;
+    launch_topk(K, st);
 }
 
 // algorithmic bytes of one referenced column over a segment: natural width per value, plus the CSR
@@ -2827,7 +2934,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     CollectParams P{};
     P.n_docs = s->max_doc;
     P.n_blocks = s->n_pad / kBlockDocs;
-    P.hot_t = kMissingOrd;
+    for (uint32_t& h : P.hot_t) h = kMissingOrd;
     if (P.n_blocks == 0) return 0;
     P.ord = oc ? oc->ords().as<uint32_t>() : nullptr;
     if (fuse_ords && L_ORD) {
@@ -2979,7 +3086,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
             P.mv32 = d32;
             P.mv16 = d16;
             P.mv_base = mc->vmin;
-            P.hot_t = sampled_hot_ord(p->ctx, oc, s);
+            sampled_hot_ords(p->ctx, oc, s, P.hot_t);
             pi = true;
             // a filtered request (clauses or live docs) takes the packed cells through one folded accept bitset, which
             // is instantiated with the 16-bit columns only (with_vk)
@@ -3152,7 +3259,8 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
                pl.interval > 0 && hc->zspan < pl.interval ? 1 : 0;
     const int vk = (P.hv_f64 ? 1 : 0) | (P.mv_f64 ? 2 : 0) | (P.ord_src ? 8 : 0) | (P.ord16 ? 16 : 0) | (P.hv32 ? 32 : 0) |
                    (pi ? 64 : 0) | (m32 ? 128 : 0) | (P.mv16 ? 256 : 0) | (fold ? 512 : 0) | (P.raw_dense ? 1024 : 0) |
-                   (P.runs1 ? 4096 : 0) | (P.hv16 ? 8192 : 0) | (P.ukey32 ? 16384 : 0);
+                   (P.runs1 ? 4096 : 0) | (P.hv16 ? 8192 : 0) | (P.ukey32 ? 16384 : 0) |
+                   (P.ocnt_mode != OCNT_TERMS && P.ocnt_mode != OCNT_HIST ? 32768 : 0);
     const uint64_t occ_key = ((uint64_t)lds << 24) | ((uint64_t)wide << 23) | ((uint64_t)vk << 8) | ((uint64_t)L_met << 4) |
                              ((uint64_t)hk << 1) | (L_ORD ? 1 : 0);
     if (pl.occ_key != occ_key) {
@@ -3183,7 +3291,11 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         const char* e = std::getenv("ESGPU_HIST_MIN_BPW");
         return (uint32_t)std::max(1, e && *e ? std::atoi(e) : 8);
     }();
-    const uint32_t min_bpw = std::min<uint32_t>(L_ORD ? ESGPU_MIN_BPW : hist_min_bpw, (P.n_blocks + slots - 1) / slots);
+    static const uint32_t ord_min_bpw = [] {  // (ESGPU_MIN_BPW_ENV: A/B runs)
+        const char* e = std::getenv("ESGPU_MIN_BPW_ENV");
+        return (uint32_t)std::max(1, e && *e ? std::atoi(e) : ESGPU_MIN_BPW);
+    }();
+    const uint32_t min_bpw = std::min<uint32_t>(L_ORD ? ord_min_bpw : hist_min_bpw, (P.n_blocks + slots - 1) / slots);
     P.blocks_per_wg = std::max(std::max(1u, bpw), min_bpw);
     if (pi && P.lds_mode && !pi_fits(P.blocks_per_wg)) {  // a packed field could overflow: the f64 cells instead
         pi = false;
@@ -3325,15 +3437,17 @@ static const uint16_t* ensure_ord16(esgpu_ctx* c, const DevColumn* col, const es
     HIPX(hipStreamSynchronize(st));
     return m->ord16.as<uint16_t>();
 }
-// the most frequent ordinal among 64 evenly spaced runs of 4,096 docs (cached with the ordinal buffer)
-static uint32_t sampled_hot_ord(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s) {
+// the 4 most frequent ordinals among 64 evenly spaced runs of 4,096 docs, most frequent first (cached with the ordinal
+// buffer; kMissingOrd where fewer ordinals occur)
+static void sampled_hot_ords(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, uint32_t (&out)[4]) {
     DevColumn* m = const_cast<DevColumn*>(col);
     std::lock_guard<std::mutex> lk(c->mu);
-    if (m->hot_src == col->ords().p) return m->hot_ord;
+    auto give = [&] { for (int k = 0; k < 4; ++k) out[k] = m->hot_ord[k]; };
+    if (m->hot_src == col->ords().p) return give();
     m->hot_src = col->ords().p;
-    m->hot_ord = kMissingOrd;
+    for (uint32_t& h : m->hot_ord) h = kMissingOrd;
     const uint64_t T = col->ord_count();
-    if (!T || T > (1u << 24) || s->max_doc == 0) return m->hot_ord;
+    if (!T || T > (1u << 24) || s->max_doc == 0) return give();
     const uint32_t run = std::min<uint32_t>(4096, s->max_doc), nrun = s->max_doc >= 64u * run ? 64u : 1u;
     std::vector<uint32_t> buf((size_t)run * nrun), hist(T, 0);
     for (uint32_t r = 0; r < nrun; ++r) {
@@ -3342,10 +3456,14 @@ static uint32_t sampled_hot_ord(esgpu_ctx* c, const DevColumn* col, const esgpu_
     }
     HIPX(hipStreamSynchronize(c->stream));
     for (uint32_t o : buf) if (o < T) ++hist[o];
-    uint32_t best = 0;
-    for (uint64_t o = 1; o < T; ++o) if (hist[o] > hist[best]) best = (uint32_t)o;
-    if (hist[best]) m->hot_ord = best;
-    return m->hot_ord;
+    for (int k = 0; k < 4; ++k) {
+        uint32_t best = 0;
+        for (uint64_t o = 1; o < T; ++o) if (hist[o] > hist[best]) best = (uint32_t)o;
+        if (!hist[best]) break;
+        m->hot_ord[k] = best;
+        hist[best] = 0;
+    }
+    give();
 }
 
 // the upload-width values of a long column whose wide buffer esgpu_segment_release_wide released, rebuilt from its compact
@@ -3663,6 +3781,7 @@ extern "C" int esgpu_plan_collect_segment(esgpu_plan* p, const esgpu_segment* s,
         require(!p->posted, ESGPU_ERR_STATE, "collect after postCollection");
         require(s->ctx == p->ctx, ESGPU_ERR_INVALID, "segment belongs to another device context");
         HIPX(hipSetDevice(p->ctx->device));
+        hc_flush(p);  // (a second segment adds to the counts)
         const uint64_t* d_accept = nullptr;
         p->sparse_dead = false;
         if (accept_bits) {
@@ -3794,13 +3913,7 @@ extern "C" int esgpu_plan_post_collection(esgpu_plan* p) {
         require(p != nullptr, ESGPU_ERR_INVALID, "null plan");
         HIPX(hipSetDevice(p->ctx->device));
         bsync(p);
-        if (p->hc_check) {  // a partition overran the capacity the segment statistics promised (a bug, never data)
-            p->hc_check = false;
-            volatile uint32_t* err = p->h_hcerr.as<volatile uint32_t>();
-            const uint32_t e = *err;
-            *err = 0;
-            require(e == 0, ESGPU_ERR_DEVICE, "hot/cold counting: partition capacity exceeded");
-        }
+        hc_check_err(p);
         for (Pipeline& pl : p->pipes) {
             if (pl.kind != 1 || !pl.allocated) continue;
             // [0] = distinct encoded hashes inserted (LC pass), [1] = non-zero registers (register pass)
@@ -4731,6 +4844,7 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
     // (the GPU top-k's keys hold a count in 31 bits: a request over at most 2^31 - 1 docs, i.e. one Lucene shard)
     const bool gpu_topk = !agg_order && P0.value_count > 65536 && k_req <= kTopkMax && (P0.H == 1 || count_order) &&
                           p->docs_seen < (1ull << 31);
+    if (!gpu_topk) hc_flush(p);
     if (P0.cnt32 && !gpu_topk) {  // u32 counts (partitioned / hot-cold paths) widened for the host selection
         unsigned long long* w = (unsigned long long*)p->s_tcnt.ensure(p->ctx, (size_t)T * 8);
         launch_widen_u32(P0.g_cnt.as<unsigned int>(), T, w, st);
@@ -4757,11 +4871,12 @@ static Block build_terms_root(esgpu_plan* p, const Group& g) {
         K.out_keys = dk;
         K.out_sum = dk + kk;
         HIPX(hipMemsetAsync(K.out_sum, 0, 8, st));
-        launch_topk(K, st);
+        hc_topk_launch(p, P0, K, (uint32_t)k_req, st);
         HIPX(hipGetLastError());
         d2h_u64(p, p->h_keys, dk, (size_t)kk + 1);
         const unsigned long long* hk = p->h_keys.as<unsigned long long>();
         bsync(p);
+        hc_check_err(p);
         other = (int64_t)hk[kk];
         for (uint32_t i = 0; i < (uint32_t)k_req; ++i) {
             const unsigned long long key = hk[i];
@@ -5405,6 +5520,7 @@ extern "C" int esgpu_plan_reset(esgpu_plan* p) {
     return guarded([&] {
         require(p != nullptr, ESGPU_ERR_INVALID, "null plan");
         HIPX(hipSetDevice(p->ctx->device));
+        p->hc_pend = esgpu_plan::HcPending{};  // (a request reset before its build: its cold lists are not needed)
         for (Pipeline& pl : p->pipes) {
             // the next request takes its grid shape and term dictionary from its own first segment
             pl.fresh = true;
@@ -6351,7 +6467,7 @@ static bool xr_terms(Collective& C, esgpu_plan* const* plans, int n, int32_t roo
             T.out_keys = dk;
             T.out_sum = dk + kk;
             HIPX(hipMemsetAsync(T.out_sum, 0, 8, p->stream));
-            launch_topk(T, p->stream);
+            hc_topk_launch(p, P0, T, (uint32_t)k_req, p->stream);
             HIPX(hipGetLastError());
             if (p != p0) {  // the record is written on p0's stream once this shard's top-k is done
                 if (!p->ev_xr) HIPX(hipEventCreateWithFlags(&p->ev_xr, hipEventDisableTiming));

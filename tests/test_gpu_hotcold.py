@@ -8,6 +8,8 @@ ordinal with more than 65535 docs (32-bit counters in the counting pass), filter
 use a fraction of the capacities), several segments into one plan, and reuse of the statistics across requests.
 Requests without predicates or accept bits take the postings form (path 7: hot slots from the recoded column, the cold
 docs counted from the segment's partition-ordered cold lists); the others scatter the cold docs per request (path 6).
+A lone terms aggregation in count order over one segment defers the cold lists to its top-k (path 8), which counts
+them only when the hot slots' k-th count does not exceed the segment's largest cold count.
 """
 import numpy as np
 import pytest
@@ -34,7 +36,8 @@ def _check(engine, cols, n, aggs, filters=None, accept=None, reps=1, path_want=N
     for rep in range(reps):  # the second request reuses the segment statistics built by the first
         plan.collect(seg, accept_bits=accept)
         _, _, path = plan.last_collect_stats()
-        assert path == (path_want or (7 if not filters and accept is None else 6)), path
+        # (7 or 8 unfiltered: a lone count-ordered terms aggregation defers the cold lists to its top-k)
+        assert path in ((path_want,) if path_want else (7, 8) if not filters and accept is None else (6,)), path
         res = plan.build()
         assert_same(res.to_dict(), want["shards"][0], f"shard rep{rep}")
         assert_same(reduce([res]).to_dict(), want["reduced"], f"reduced rep{rep}")
@@ -280,3 +283,59 @@ def test_count_width_across_single_and_multi_segments(engine, multi_field, multi
         plan.close()
         for s in segs:
             s.close()
+
+
+def _zipf_cols(seed, n, T, a=1.1):
+    rng = np.random.default_rng(seed)
+    ranks = np.minimum(rng.zipf(a, size=n) - 1, T - 1)
+    ords = (ranks * 7919 + 17) % T
+    ords[rng.random(n) < 0.02] = 0xFFFFFFFF
+    return _cols(ords, T, rng)
+
+
+@pytest.mark.parametrize("size", [1, 10, 200])
+def test_deferred_cold_lists_settled_by_hot_slots(engine, size):
+    """Zipf(1.1) over 400,000 ordinals, one terms aggregation in count order (the config-3 request): the hot slots'
+    top-k is above every cold ordinal's count, so the cold counting and the full top-k are skipped on the device
+    (path 8); the other doc count is the segment's total minus the winners'."""
+    n, T = 2_000_000, 400_000
+    cols = _zipf_cols(106, n, T)
+    _check(engine, cols, n, [AB.terms("c").field("kw").size(size)], reps=2, path_want=8)
+
+
+def test_deferred_cold_lists_counted_when_needed(engine):
+    """Uniform over 200,000 ordinals (the hot set's counts tie with cold ones): the k-th hot count does not exceed
+    the largest cold count, so the deferred cold lists are counted before the full top-k (path 8, same result)."""
+    rng = np.random.default_rng(107)
+    n, T = 1_500_000, 200_000
+    cols = _cols(rng.integers(0, T, size=n), T, rng)
+    _check(engine, cols, n, [AB.terms("c").field("kw").size(40)], reps=2, path_want=8)
+    _check(engine, cols, n, [AB.terms("c").field("kw").size(1000).shardSize(1000)], path_want=8)
+
+
+def test_deferred_cold_lists_second_segment_and_reset(engine):
+    """The first segment defers its cold lists; a second segment's collect counts them first (then adds its own,
+    path 7); a request reset before its build drops them (the next request counts from scratch)."""
+    T = 300_000
+    sizes = [900_000, 1_300_000]
+    cols = [_zipf_cols(108 + k, n, T, 1.1 + 0.1 * k) for k, n in enumerate(sizes)]
+    allc = {"kw": dict(cols[0]["kw"], values=np.concatenate([c["kw"]["values"] for c in cols])),
+            "status": {"type": N.COL_I64, "values": np.concatenate([c["status"]["values"] for c in cols])}}
+    aggs = [AB.terms("c").field("kw").size(15)]
+    want = O.run([(allc, sum(sizes))], aggs)
+    want0 = O.run([(cols[0], sizes[0])], aggs)
+    segs = [engine.upload_segment(c, n) for c, n in zip(cols, sizes)]
+    plan = engine.plan(aggs)
+    plan.collect(segs[0])
+    assert plan.last_collect_stats()[2] == 8
+    plan.reset()
+    for k, s in enumerate(segs):
+        plan.collect(s)
+        assert plan.last_collect_stats()[2] == (8 if k == 0 else 7)
+    assert_same(plan.build().to_dict(), want["shards"][0], "two segments")
+    plan.reset()
+    plan.collect(segs[0])
+    assert_same(plan.build().to_dict(), want0["shards"][0], "one segment after reset")
+    plan.close()
+    for s in segs:
+        s.close()
