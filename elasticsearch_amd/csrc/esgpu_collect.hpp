@@ -574,6 +574,7 @@ struct Run {
     // workgroup range of docs, < 2^19: the sums cannot overflow)
     uint32_t isd, imn, imx;
     unsigned long long isq;
+    uint32_t pmn, pmx;  // ... and the extrema of the packed updates (runs_add_pk) as two 16-bit lanes each
 };
 
 __device__ __forceinline__ void run_reset(Run& r) {
@@ -588,6 +589,8 @@ __device__ __forceinline__ void run_reset(Run& r) {
     r.isq = 0;
     r.imn = ~0u;
     r.imx = 0;
+    r.pmn = ~0u;
+    r.pmx = 0;
 }
 
 // an integer run into its LDS cell: the values are v = mv_base + d, so sum = cnt * base + sum d and sum of squares =
@@ -601,8 +604,10 @@ __device__ __forceinline__ void run_flush_i(const CollectParams& P, const Acc& a
         const long long base = P.mv_base;
         atomicAdd(&a.sum[c], (double)((long long)r.cnt * base + (long long)r.isd));
         if (MET >= 2) {
-            const unsigned long long emn = sortable((double)(base + (long long)r.imn));
-            const unsigned long long emx = sortable((double)(base + (long long)r.imx));
+            const uint32_t imn = min(r.imn, min(r.pmn & 0xFFFFu, r.pmn >> 16));
+            const uint32_t imx = max(r.imx, max(r.pmx & 0xFFFFu, r.pmx >> 16));
+            const unsigned long long emn = sortable((double)(base + (long long)imn));
+            const unsigned long long emx = sortable((double)(base + (long long)imx));
             const unsigned long long cmn = a.mn[MS * c], cmx = a.mx[MS * c];
             if (emn < cmn) atomicMin(&a.mn[MS * c], emn);
             if (emx > cmx) atomicMax(&a.mx[MS * c], emx);
@@ -749,6 +754,33 @@ __device__ __forceinline__ void runs_add_i(const CollectParams& P, const Acc& a,
         }
     }
 }
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+// a thread's 4 docs of a single-key zone block into its one integer run, straight from the two raw words of 16-bit
+// metric deltas: v_dot2_u32_u16 sums the deltas (and, below 46,341, their squares: CollectParams.dot16), v_pk_min/max_u16
+// keep two extrema per word until the flush -- 9 VALU per 4 docs where unpacked they took ~25
+template <int MET, int MS, int NR>
+__device__ __forceinline__ void runs_add_pk(const CollectParams& P, const Acc& a, Runs<NR>& R, uint32_t slot, uint32_t w0,
+                                            uint32_t w1) {
+    static_assert(NR == 1, "one run per thread (VK bit 4096)");
+    Run& r = R.r[0];
+    if (r.slot != slot) {
+        run_flush_i<MET, MS>(P, a, r);
+        r.slot = slot;
+    }
+    const u16x2_t x0 = __builtin_bit_cast(u16x2_t, w0), x1 = __builtin_bit_cast(u16x2_t, w1);
+    const u16x2_t one = {1, 1};
+    r.cnt += 4u;
+    r.isd = __builtin_amdgcn_udot2(x0, one, __builtin_amdgcn_udot2(x1, one, r.isd, false), false);
+    if (MET >= 3)
+        r.isq += (unsigned long long)__builtin_amdgcn_udot2(x0, x0, 0u, false) +
+                 (unsigned long long)__builtin_amdgcn_udot2(x1, x1, 0u, false);
+    if (MET >= 2) {
+        r.pmn = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2_t, r.pmn),
+                                                                        __builtin_elementwise_min(x0, x1)));
+        r.pmx = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2_t, r.pmx),
+                                                                        __builtin_elementwise_max(x0, x1)));
+    }
+}
 template <int MET, int MS, int NR>
 __device__ __forceinline__ void runs_add(const CollectParams& P, const Acc& a, Runs<NR>& R, uint32_t slot, bool mpres, double x) {
     int hit = -1;
@@ -882,6 +914,14 @@ __device__ __forceinline__ void unpack_docs(const CollectParams& P, Doc4& d) {
 template <bool ORD, bool HIST, int MET, bool LDS, bool KT, int MS, bool HORD = false, int VK = 0>
 __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, const Doc4& d_in, uint32_t T, int64_t base,
                                          uint32_t win0, Runs<runs_for<MET, VK>()>& run, uint32_t mw = 0, bool outer = true) {
+    if constexpr (LDS && kIntRuns<ORD, MET, VK> && kUKeyK<ORD, HIST, MET, VK> && runs_for<MET, VK>() == 1) {
+        // a single-key zone block's whole quad (every doc but the segment's last few): the packed run update, no unpack
+        if (d_in.ukey != kNoUKey && P.dot16 && d_in.doc0 + 4 <= P.n_docs) {
+            const uint32_t k = d_in.ukey, sl = k - win0;  // (kOutUKey: outside the grid, no doc counts)
+            if (k < P.H && sl < (mw ? mw : P.W)) runs_add_pk<MET, MS>(P, a, run, sl, d_in.raw[6], d_in.raw[7]);
+            return;
+        }
+    }
     Doc4 du;
     if constexpr (kRawPI<MET, VK, HIST>) {
         du = d_in;

@@ -1691,6 +1691,7 @@ static bool d16_on();
 static bool raw_hist_on();
 static bool dd_forced();
 static bool int_runs_on();
+static bool dot16_on();
 static bool runs1_on();
 static bool b16_on(const esgpu_ctx* c);
 static bool pi_cells(const esgpu_ctx* c);
@@ -3251,6 +3252,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     // integer runs over time-sorted data (90 % of the blocks span less than one interval): one run per thread; roughly
     // time-ordered data alternates between neighbouring keys and keeps three
     P.runs1 = m32 && P.mv16 && hc && pl.interval > 0 && hc->zspan < pl.interval && runs1_on() ? 1 : 0;
+    P.dot16 = P.runs1 && mc && (uint64_t)mc->vmax - (uint64_t)mc->vmin <= 46340 && dot16_on() ? 1 : 0;
     // raw-load kernels over 32-bit timestamp deltas (block deltas did not apply: runs spanning 2^16 ms or more) skip the
     // single-key zone blocks' deltas where most blocks hold one key (90 % of the blocks span less than one interval:
     // roughly time-ordered data displaced by minutes); with wider displacement the skip's conditional load costs more
@@ -3285,11 +3287,11 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     // ESGPU_MIN_BPW blocks per workgroup (fewer, longer ranges than the tail-balancing target) -- small segments
     // otherwise pay about one global atomic per 30 docs.  Histogram-only grids flush only the keys they touched.
     const uint32_t slots = (uint32_t)p->ctx->cus * wg_per_cu;
-    // Histogram-only grids: at least ESGPU_HIST_MIN_BPW (8) blocks per workgroup too -- a workgroup's setup and run
+    // Histogram-only grids: at least ESGPU_HIST_MIN_BPW (16) blocks per workgroup too -- a workgroup's setup and run
     // flushes against one 8,192-doc block left config 2 at 100M docs at 0.119 ms; 8 blocks: 0.090 ms (r5, kbench)
     static const uint32_t hist_min_bpw = [] {
         const char* e = std::getenv("ESGPU_HIST_MIN_BPW");
-        return (uint32_t)std::max(1, e && *e ? std::atoi(e) : 8);
+        return (uint32_t)std::max(1, e && *e ? std::atoi(e) : 16);  // (16: config 2 at 100M 0.0799 -> 0.0754 ms, r6l)
     }();
     static const uint32_t ord_min_bpw = [] {  // (ESGPU_MIN_BPW_ENV: A/B runs)
         const char* e = std::getenv("ESGPU_MIN_BPW_ENV");
@@ -3375,6 +3377,11 @@ static bool replay_compaction() {
     return on;
 }
 // integer run accumulators of histogram-only grids (VK bit 2048; ESGPU_INT_RUNS=0: the f64 runs, for A/B runs)
+// packed run updates for single-key zone blocks (CollectParams.dot16; ESGPU_DOT16=0: the unpacked update, for A/B runs)
+static bool dot16_on() {
+    static const bool on = [] { const char* e = std::getenv("ESGPU_DOT16"); return !(e && *e == '0'); }();
+    return on;
+}
 static bool int_runs_on() {
     static const bool on = [] { const char* e = std::getenv("ESGPU_INT_RUNS"); return !(e && *e == '0'); }();
     return on;
