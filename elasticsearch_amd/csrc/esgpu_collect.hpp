@@ -348,6 +348,9 @@ __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0,
 #ifndef ESGPU_DOCS8  // (r5ab7, 1B docs: north star 1.21 -> 1.19 ms, terms{dh{avg}} 1.09 -> 0.96, config 5 2.36 -> 2.12)
 #define ESGPU_DOCS8 1
 #endif
+#ifndef ESGPU_DOCS8_HI  // ... and the histogram-only integer-run grids over time-sorted data (VK bits 2048 | 4096), whose
+#define ESGPU_DOCS8_HI 0  // single-key blocks' packed run updates (CollectParams.dot16) -- measured level (config 2 at 1B
+#endif                    // 0.606 / 0.614 ms, r6m: SALU per 256 docs 72 -> 50, no faster) and off
 #ifndef ESGPU_DOCS8_H  // ... the raw-load counting grids with a terms dimension (VK bit 1024; r5ab8: terms{date_histogram}
 #define ESGPU_DOCS8_H 1  // 0.96 -> 0.88 ms at 1B; the histogram-only grids measured 7 % slower at 8 and keep 4)
 #endif
@@ -1511,7 +1514,8 @@ template <bool ORD, int MET, int VK, int WGS> constexpr int collect_min_waves() 
 template <bool ORD, int HK, int MET, int VK, int WGS>
 __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void collect_kernel(CollectParams P) {
     constexpr bool WIDE8 = (ESGPU_DOCS8 != 0 && kRawPI<MET, VK, (HK != 0)>) ||  // 8 docs per thread per step (Doc8)
-                           (ESGPU_DOCS8_H != 0 && kRawH<ORD, MET, VK> && ORD);
+                           (ESGPU_DOCS8_H != 0 && kRawH<ORD, MET, VK> && ORD) ||
+                           (ESGPU_DOCS8_HI != 0 && kIntRuns<ORD, MET, VK> && (VK & 4096) != 0 && (HK != 0));
     constexpr int kIterDocsW = WGS * (WIDE8 ? 2 * kVec : kVec);
     constexpr int kItersPerBlockW = kBlockDocs / kIterDocsW;
     constexpr bool HIST = HK != 0;
