@@ -67,7 +67,8 @@ void launch_hc_recode(const uint32_t* ord, uint32_t n, const uint32_t* keys, con
 __global__ void hc_hot16_kernel(const uint32_t* rc, uint32_t n, uint16_t* out) {
     for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < n; d += gridDim.x * blockDim.x) {
         const uint32_t v = rc[d];
-        out[d] = (v & kHcHotBit) && v != kMissingOrd ? (uint16_t)(v & ~kHcHotBit) : (uint16_t)0xFFFFu;
+        // hot slot, 0xFFFE for a cold ordinal (counted as one total by a filtered request's hot pass), 0xFFFF missing
+        out[d] = v == kMissingOrd ? (uint16_t)0xFFFFu : (v & kHcHotBit) ? (uint16_t)(v & ~kHcHotBit) : (uint16_t)0xFFFEu;
     }
 }
 void launch_hc_hot16(const uint32_t* rc, uint32_t n, uint16_t* out, hipStream_t s) {
@@ -76,6 +77,7 @@ void launch_hc_hot16(const uint32_t* rc, uint32_t n, uint16_t* out, hipStream_t 
 }
 
 __global__ void hc_init_kernel(HcParams P) {
+    if (P.skip && *P.skip) return;  // (the hot slots settled the request's top-k: hc_topk_launch)
     for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < P.P; p += gridDim.x * blockDim.x)
         P.ovf_cur[p] = P.part[p].ovf_base;
 }  // P.err is zeroed by the host (after each check), so overruns of every segment of a request accumulate
@@ -110,6 +112,7 @@ size_t hc_scatter_lds_bytes(uint32_t n_parts, uint32_t hot_n) {
 
 template <bool HOT>
 __global__ __launch_bounds__(kHcWG) void hc_scatter_kernel(HcParams P) {
+    if (P.skip && *P.skip) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t NH = HOT ? hc_hot_counters(P.hot_n) : 0u;
     uint32_t* hot = (uint32_t*)smem;                        // [NH] hot counters (slot s < 64: 4 s + lane % 4)
@@ -430,6 +433,7 @@ __global__ __launch_bounds__(kHcCountWG) void hc_count_kernel(HcParams P) {
 // (one thread's four), counter i >= 256 is slot i - 192.
 constexpr uint32_t kHotSplit = 16;
 __global__ __launch_bounds__(256) void hc_hot_reduce_kernel(HcParams P) {
+    if (P.skip && *P.skip) return;
     const uint32_t NH = hc_hot_counters(P.hot_n), stride = hc_slab_stride(P.hot_n);
     const uint32_t base = blockIdx.x * 1024 + threadIdx.x * 4;
     if (base >= NH) return;
@@ -452,6 +456,7 @@ __global__ __launch_bounds__(256) void hc_hot_reduce_kernel(HcParams P) {
     src[(size_t)blockIdx.y * row] = acc;
 }
 __global__ __launch_bounds__(256) void hc_hot_final_kernel(HcParams P, uint32_t Y) {
+    if (P.skip && *P.skip) return;
     const uint32_t NH = hc_hot_counters(P.hot_n), stride = hc_slab_stride(P.hot_n);
     const uint32_t base = (blockIdx.x * 256 + threadIdx.x) * 4;
     if (base >= NH) return;
@@ -578,7 +583,9 @@ __global__ __launch_bounds__(kHotWG) void hc_hot_kernel(HcParams P) {
 // The same pass over the 16-bit hot-slot column (the segment statistics' compressed copy, like Lucene's bit-packed
 // ordinals): 8 docs per 16-byte load, half the bytes of the recoded column
 constexpr uint32_t kHot16TileDocs = kHotWG * kHcIt * 8;
-template <bool ACC>
+// CT: the docs of cold ordinals that pass are counted too (one total, P.cold_tot: a filtered request's other doc count
+// when the hot slots settle its top-k)
+template <bool ACC, bool CT = false>
 __global__ __launch_bounds__(kHotWG) void hc_hot16_count_kernel(HcParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t* hot = (uint32_t*)smem;
@@ -602,6 +609,7 @@ __global__ __launch_bounds__(kHotWG) void hc_hot16_count_kernel(HcParams P) {
             if (ACC) aw[k] = P.accept[d >> 6];
         }
     };
+    uint32_t ncold = 0;
     auto count = [&](uint32_t t0, const uint32_t o[kHcIt][4], const uint64_t aw[kHcIt]) {
         if (t0 >= d_begin + span) return;
 #pragma unroll
@@ -611,8 +619,10 @@ __global__ __launch_bounds__(kHotWG) void hc_hot16_count_kernel(HcParams P) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const uint32_t sl = (o[k][j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-                if (sl != 0xFFFFu && doc0 + j < d_end && ((live >> j) & 1u))
+                const bool in = doc0 + j < d_end && ((live >> j) & 1u);
+                if (sl < 0xFFFEu && in)
                     atomicAdd(&hot[sl < kHcHotCopies ? 4 * sl + (threadIdx.x & 3) : 3 * kHcHotCopies + sl], 1u);
+                if (CT) ncold += (sl == 0xFFFEu && in) ? 1u : 0u;
             }
         }
     };
@@ -632,6 +642,10 @@ __global__ __launch_bounds__(kHotWG) void hc_hot16_count_kernel(HcParams P) {
             count(t0 + 2 * kHot16TileDocs, C, Cw);
             load(t0 + 5 * kHot16TileDocs, C, Cw);
         }
+    }
+    if (CT) {  // one global add per wave
+        const uint32_t wsum = wave_sum_u32(ncold);
+        if ((threadIdx.x & 63) == 0 && wsum) atomicAdd(P.cold_tot, wsum);
     }
     __syncthreads();
     const uint32_t stride = hc_slab_stride(P.hot_n);
@@ -677,7 +691,8 @@ __global__ __launch_bounds__(256) void hc_slot_fold_kernel(HcParams P) {
 }
 void launch_hot_postings(const HcParams& hot, hipStream_t s) {
     const size_t hlds = (size_t)hc_hot_counters(hot.hot_n) * 4;
-    hipLaunchKernelGGL(hc_hot16_count_kernel<false>, dim3(hot.G), dim3(kHotWG), hlds, s, hot);
+    if (hot.accept) hipLaunchKernelGGL((hc_hot16_count_kernel<true, true>), dim3(hot.G), dim3(kHotWG), hlds, s, hot);
+    else hipLaunchKernelGGL(hc_hot16_count_kernel<false>, dim3(hot.G), dim3(kHotWG), hlds, s, hot);
     launch_hot_reduce(hot, s);
 }
 void launch_cold_postings(const HcParams& hot, const HcParams& cold, hipStream_t s) {
@@ -690,8 +705,10 @@ void launch_cold_postings(const HcParams& hot, const HcParams& cold, hipStream_t
 }
 __global__ void hot_topk_check_kernel(const unsigned long long* hot_keys, uint32_t k, uint32_t k_req, uint64_t max_cold,
                                       uint64_t docs, int order, uint32_t* skip, unsigned long long* out_keys,
-                                      unsigned long long* out_sum) {
+                                      unsigned long long* out_sum, const uint32_t* slot_tot, uint32_t hot_n,
+                                      const uint32_t* cold_tot) {
     __shared__ uint32_t ok;
+    __shared__ unsigned long long tot;
     if (threadIdx.x == 0) {
         // count order descending: the k-th pick present and above every cold ordinal's count (ties go to the smaller
         // ordinal, which may be cold: strictly above)
@@ -702,12 +719,24 @@ __global__ void hot_topk_check_kernel(const unsigned long long* hot_keys, uint32
     __syncthreads();
     if (!ok) return;
     for (uint32_t i = threadIdx.x; i < k; i += blockDim.x) out_keys[i] = hot_keys[i];
-    if (threadIdx.x == 0) *out_sum = docs;  // the sum of every ordinal's count: the segment's docs with a value
+    if (!cold_tot) {
+        if (threadIdx.x == 0) *out_sum = docs;  // the sum of every ordinal's count: the segment's docs with a value
+        return;
+    }
+    // a filtered request: its docs with a value that pass = the hot slots' totals + the passing cold docs
+    if (threadIdx.x == 0) tot = *cold_tot;
+    __syncthreads();
+    unsigned long long part = 0;
+    for (uint32_t i = threadIdx.x; i < hot_n; i += blockDim.x) part += slot_tot[i];
+    atomicAdd(&tot, part);
+    __syncthreads();
+    if (threadIdx.x == 0) *out_sum = tot;
 }
 void launch_hot_topk_check(const unsigned long long* hot_keys, uint32_t k, uint32_t k_req, uint64_t max_cold, uint64_t docs,
-                           int order, uint32_t* skip, unsigned long long* out_keys, unsigned long long* out_sum, hipStream_t s) {
+                           int order, uint32_t* skip, unsigned long long* out_keys, unsigned long long* out_sum,
+                           const uint32_t* slot_tot, uint32_t hot_n, const uint32_t* cold_tot, hipStream_t s) {
     hipLaunchKernelGGL(hot_topk_check_kernel, dim3(1), dim3(256), 0, s, hot_keys, k, k_req, max_cold, docs, order, skip,
-                       out_keys, out_sum);
+                       out_keys, out_sum, slot_tot, hot_n, cold_tot);
 }
 
 void launch_hotcold_postings(const HcParams& hot, const HcParams& cold, hipStream_t s) {

@@ -543,7 +543,9 @@ struct HcParams {
     int32_t overwrite;                 // store the counts instead of adding (the plan's first segment)
     uint32_t* slot_tot;                // postings hot pass, deferred cold lists: [hot_n] hot slot totals instead of
                                        // atomics onto counts[hot_ord] (esgpu_runtime.cpp hc_pending)
-    const uint32_t* skip;              // non-null and set: the cold counting and the fold return at once
+    const uint32_t* skip;              // non-null and set: the cold counting, the fold and (a filtered request's fallback)
+                                       // the scatter form return at once
+    uint32_t* cold_tot;                // hot16 pass with accept bits: the passing docs of cold ordinals, one total
 };
 __host__ __device__ inline uint32_t hc_hot_counters(uint32_t hot_n) { return hot_n + 3 * (hot_n < kHcHotCopies ? hot_n : kHcHotCopies); }
 // per-workgroup hot slab row: the counters padded to 16 bytes (the reduce reads them as uint4)
@@ -562,8 +564,10 @@ void launch_hot_postings(const HcParams& hot, hipStream_t s);
 void launch_cold_postings(const HcParams& hot, const HcParams& cold, hipStream_t s);
 // the hot slots' top-k settles the request: skip = the k keys all present and the k-th count above max_cold; then the
 // final keys and the count sum (docs) are written where the full top-k would write them
+// (cold_tot non-null: a filtered request, whose count sum is the hot slot totals plus *cold_tot instead of docs)
 void launch_hot_topk_check(const unsigned long long* hot_keys, uint32_t k, uint32_t k_req, uint64_t max_cold, uint64_t docs,
-                           int order, uint32_t* skip, unsigned long long* out_keys, unsigned long long* out_sum, hipStream_t s);
+                           int order, uint32_t* skip, unsigned long long* out_keys, unsigned long long* out_sum,
+                           const uint32_t* slot_tot, uint32_t hot_n, const uint32_t* cold_tot, hipStream_t s);
 // stats time: the dense partition-ordered cold offsets -> one list per partition starting at pad_begin[p] (a multiple
 // of 64 elements), 0xFFFF between lists
 void launch_hc_pad(const uint16_t* dense, const uint32_t* dense_begin, const uint32_t* pad_begin, uint32_t P,

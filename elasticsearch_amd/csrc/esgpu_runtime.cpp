@@ -1113,11 +1113,12 @@ struct esgpu_plan {
     // the top-k, which runs it only when the hot slots do not settle the winners (collect_hotcold, hc_topk_launch)
     struct HcPending {
         bool on = false;
+        bool filtered = false;  // a filter / accept bits: `cold` is the scatter form's parameters (the fallback)
         int pipe = -1;
         HcParams hot{}, cold{};
         std::shared_ptr<const HcStats> hs;  // keeps the segment statistics' buffers the two passes read
     } hc_pend;
-    Scratch s_slot_tot, s_hcand, s_hhist, s_hkeys, s_hskip;
+    Scratch s_slot_tot, s_hcand, s_hhist, s_hkeys, s_hskip, s_cold_tot, s_hbits;
     PinnedBuf h_keys;
     hipEvent_t ev_mid = nullptr;
     PinnedBuf h_tcnt, h_rows, h_dst[6];
@@ -2277,6 +2278,18 @@ static bool hc_prune_on() {
     static const bool on = [] { const char* e = std::getenv("ESGPU_HC_PRUNE"); return !(e && *e == '0'); }();
     return on;
 }
+// the request shape whose cold docs may wait for the top-k: one terms aggregation and nothing else (no other reader of
+// these counts), in count order descending, shard_size within the hot set and the GPU top-k
+static bool hc_defer_shape(const esgpu_plan* p, const Pipeline& pl, const HcStats& hs) {
+    const int pipe = (int)(&pl - p->pipes.data());
+    const SpecNode& tn = p->specs[pl.root];
+    const bool plain = p->pipes.size() == 1 && p->groups.size() == 1 && p->groups[0].pipes.size() == 1 &&
+                       p->groups[0].pipes[0] == pipe && p->groups[0].kids.empty();
+    return hc_prune_on() && plain && hs.hot_n && hs.d_hot16.p && tn.s.type == ESGPU_AGG_TERMS &&
+           tn.s.order == ESGPU_ORDER_COUNT_DESC && tn.s.shard_size >= 1 &&
+           (uint64_t)tn.s.shard_size <= std::min<uint64_t>(hs.hot_n, kTopkMax) && pl.value_count > 65536 && pl.H == 1 &&
+           pl.ocnt_mode == OCNT_NONE;
+}
 static bool collect_hotcold(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, const DevColumn* oc,
                             const uint64_t* d_accept, const PredDev* pred, int npred, bool first_segment) {
     esgpu_ctx* c = p->ctx;
@@ -2319,6 +2332,57 @@ static bool collect_hotcold(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s,
     // every doc counts (or all but a few: a live-docs bitset with few deletions, sampled on the host at collect) -- hot
     // slots from the column (testing the accept bits), the cold lists, then the dead cold docs taken back out
     const bool live_docs_only = d_accept && d_accept == (const uint64_t*)p->s_accept.buf.p && p->sparse_dead;
+    // the hot pass over the 16-bit hot-slot column: ESGPU_HOT_PER_CU 512-thread workgroups per CU
+    auto hot_params = [&](HcParams& Hh) {
+        const size_t hot_lds = (size_t)hc_hot_counters(Hh.hot_n) * 4;
+        require(hot_lds <= 160 * 1024, ESGPU_ERR_STATE, "hot counters beyond LDS");
+        Hh.G = (uint32_t)c->cus * (uint32_t)std::max<size_t>(1, std::min<size_t>(ESGPU_HOT_PER_CU, 160 * 1024 / (hot_lds + 1024)));
+        Hh.blocks_per_wg = std::max(1u, (Hh.n_blocks + Hh.G - 1) / Hh.G);
+        Hh.G = std::max(1u, (Hh.n_blocks + Hh.blocks_per_wg - 1) / Hh.blocks_per_wg);
+        Hh.rc16 = hs->d_hot16.p ? hs->d_hot16.as<uint16_t>() : nullptr;
+    };
+    const int pipe = (int)(&pl - p->pipes.data());
+    if (first_segment && (npred > 0 || d_accept) && hc_hot16() && hc_defer_shape(p, pl, *hs) &&
+        hc_scatter_lds_bytes(H.P, H.hot_n) <= 160 * 1024 - 256) {
+        // a lone count-ordered terms aggregation under a query filter or accept bits (config 3 filtered, deleted
+        // docs): the request's clauses folded into one accept bitset, then only the hot slots (and one total of the
+        // passing cold docs) counted from the 16-bit hot-slot column; the cold docs are scattered and counted (the
+        // scatter form, from the folded bitset) only if the top-k needs them (hc_topk_launch) -- a cold ordinal's
+        // filtered count is at most its count in the segment, HcStats::max_cold
+        HIPX(hipEventRecord(pl.e0, st));
+        const uint64_t* bits = d_accept;
+        if (npred > 0) {
+            uint64_t* xb = (uint64_t*)p->s_hbits.ensure(c, std::max<size_t>(s->n_pad / 64, 1) * 8);
+            launch_filter_bits4(s->max_doc, d_accept, pred, npred, xb, st);
+            HIPX(hipGetLastError());
+            bits = xb;
+        }
+        HcParams Hh = H;
+        hot_params(Hh);
+        Hh.accept = bits;
+        Hh.npred = 0;
+        Hh.rc = nullptr;
+        const size_t slab = (size_t)hc_slab_stride(H.hot_n) * std::max(H.G, Hh.G) * 4;
+        Hh.hot_slab = H.hot_slab = (uint32_t*)p->s_hslab.ensure(c, slab);
+        Hh.slot_tot = (uint32_t*)p->s_slot_tot.ensure(c, (size_t)hs->hot_n * 4);
+        Hh.cold_tot = (uint32_t*)p->s_cold_tot.ensure(c, 16);
+        HIPX(hipMemsetAsync(Hh.cold_tot, 0, 4, st));
+        launch_hot_postings(Hh, st);
+        HIPX(hipGetLastError());
+        HIPX(hipEventRecord(pl.e1, st));
+        H.accept = bits;  // the fallback: the scatter form from the folded bitset (no clause reads the segment later)
+        H.npred = 0;
+        p->hc_pend.on = true;
+        p->hc_pend.filtered = true;
+        p->hc_pend.pipe = pipe;
+        p->hc_pend.hot = Hh;
+        p->hc_pend.cold = H;
+        p->hc_pend.hs = hs;
+        // bytes: 2 per doc of hot slots instead of 4 of ordinals, the folded bitset read (and written by the fold)
+        p->last_bytes = p->last_bytes - 2ull * s->max_doc + s->n_pad / 8 + (npred > 0 ? s->n_pad / 8 : 0);
+        p->last_path = 9;
+        return true;
+    }
     if (hs->cold_lists && npred == 0 && (!d_accept || live_docs_only)) {
         HcParams K = H;                                 // the cold lists: one static region per partition
         K.accept = nullptr;
@@ -2330,27 +2394,12 @@ static bool collect_hotcold(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s,
         K.pbuf = hs->d_cold.as<uint16_t>();
         K.ovf_cur = hs->d_cold_ovf.as<uint32_t>();
         K.hot_n = 0;
-        HcParams Hh = H;                                // hot pass: ESGPU_HOT_PER_CU 512-thread workgroups per CU
-        const size_t hot_lds = (size_t)hc_hot_counters(Hh.hot_n) * 4;
-        require(hot_lds <= 160 * 1024, ESGPU_ERR_STATE, "hot counters beyond LDS");
-        Hh.G = (uint32_t)c->cus * (uint32_t)std::max<size_t>(1, std::min<size_t>(ESGPU_HOT_PER_CU, 160 * 1024 / (hot_lds + 1024)));
-        Hh.blocks_per_wg = std::max(1u, (Hh.n_blocks + Hh.G - 1) / Hh.G);
-        Hh.G = std::max(1u, (Hh.n_blocks + Hh.blocks_per_wg - 1) / Hh.blocks_per_wg);
+        HcParams Hh = H;
+        hot_params(Hh);
         Hh.hot_slab = Hh.hot_n ? (uint32_t*)p->s_hslab.ensure(c, (size_t)hc_slab_stride(Hh.hot_n) * Hh.G * 4) : nullptr;
-        Hh.rc16 = hs->d_hot16.p ? hs->d_hot16.as<uint16_t>() : nullptr;
         // a plain terms request in count order over one segment: the cold lists wait for the top-k (hc_topk_launch),
         // which needs them only if some cold ordinal can reach the k-th count
-        const int pipe = (int)(&pl - p->pipes.data());
-        bool defer = hc_prune_on() && first_segment && Hh.rc16 && !d_accept && hs->hot_n;
-        if (defer) {
-            // (one terms aggregation and nothing else: no other reader of these counts)
-            const SpecNode& tn = p->specs[pl.root];
-            const bool plain = p->pipes.size() == 1 && p->groups.size() == 1 && p->groups[0].pipes.size() == 1 &&
-                               p->groups[0].pipes[0] == pipe && p->groups[0].kids.empty();
-            defer = plain && tn.s.type == ESGPU_AGG_TERMS && tn.s.order == ESGPU_ORDER_COUNT_DESC &&
-                    tn.s.shard_size >= 1 && (uint64_t)tn.s.shard_size <= std::min<uint64_t>(hs->hot_n, kTopkMax) &&
-                    pl.value_count > 65536 && pl.H == 1 && pl.ocnt_mode == OCNT_NONE;
-        }
+        const bool defer = first_segment && Hh.rc16 && !d_accept && hc_defer_shape(p, pl, *hs);
         if (Hh.rc16) {  // the bytes this form moves: 2 B per doc of hot slots plus 2 B per listed cold doc (not 4 B per doc)
             p->last_bytes = p->last_bytes - 2ull * s->max_doc + (defer ? 0ull : 2ull * (hs->docs - hs->hot_docs));
         }
@@ -2394,7 +2443,8 @@ static void hc_check_err(esgpu_plan* p) {
 // host selection, the co-located reduce)
 static void hc_flush(esgpu_plan* p) {
     if (!p->hc_pend.on) return;
-    launch_cold_postings(p->hc_pend.hot, p->hc_pend.cold, p->stream);
+    if (p->hc_pend.filtered) launch_hotcold(p->hc_pend.cold, p->stream);  // the scatter form, hot slots included
+    else launch_cold_postings(p->hc_pend.hot, p->hc_pend.cold, p->stream);
     HIPX(hipGetLastError());
     p->hc_pend = esgpu_plan::HcPending{};
     p->hc_check = true;  // (the cold counting writes the capacity word)
@@ -2434,12 +2484,14 @@ static void hc_topk_launch(esgpu_plan* p, const Pipeline& P0, TopkParams K, uint
     launch_topk(Hk, st);
     HIPX(hipGetLastError());
     uint32_t* skip = (uint32_t*)p->s_hskip.ensure(c, 16);
-    launch_hot_topk_check(hk, K.k, k_req, pend.hs->max_cold, pend.hs->docs, K.order, skip, K.out_keys, K.out_sum, st);
+    launch_hot_topk_check(hk, K.k, k_req, pend.hs->max_cold, pend.hs->docs, K.order, skip, K.out_keys, K.out_sum,
+                          pend.hot.slot_tot, hot_n, pend.filtered ? pend.hot.cold_tot : nullptr, st);
     HIPX(hipGetLastError());
     HcParams hot = pend.hot, cold = pend.cold;
     hot.skip = skip;
     cold.skip = skip;
-    launch_cold_postings(hot, cold, st);
+    if (pend.filtered) launch_hotcold(cold, st);  // (every kernel of the scatter form returns at once when settled)
+    else launch_cold_postings(hot, cold, st);
     HIPX(hipGetLastError());
     p->hc_check = true;
     K.skip = skip;

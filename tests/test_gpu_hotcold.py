@@ -9,7 +9,9 @@ use a fraction of the capacities), several segments into one plan, and reuse of 
 Requests without predicates or accept bits take the postings form (path 7: hot slots from the recoded column, the cold
 docs counted from the segment's partition-ordered cold lists); the others scatter the cold docs per request (path 6).
 A lone terms aggregation in count order over one segment defers the cold lists to its top-k (path 8), which counts
-them only when the hot slots' k-th count does not exceed the segment's largest cold count.
+them only when the hot slots' k-th count does not exceed the segment's largest cold count; filtered (query clauses or
+accept bits) it counts the hot slots and one total of the passing cold docs from the hot-slot column (path 9) and
+scatters the cold docs only when the top-k needs them.
 """
 import numpy as np
 import pytest
@@ -37,7 +39,8 @@ def _check(engine, cols, n, aggs, filters=None, accept=None, reps=1, path_want=N
         plan.collect(seg, accept_bits=accept)
         _, _, path = plan.last_collect_stats()
         # (7 or 8 unfiltered: a lone count-ordered terms aggregation defers the cold lists to its top-k)
-        assert path in ((path_want,) if path_want else (7, 8) if not filters and accept is None else (6,)), path
+        # (a lone count-ordered terms aggregation filtered: 9, the hot slots from the hot-slot column first)
+        assert path in ((path_want,) if path_want else (7, 8) if not filters and accept is None else (6, 9)), path
         res = plan.build()
         assert_same(res.to_dict(), want["shards"][0], f"shard rep{rep}")
         assert_same(reduce([res]).to_dict(), want["reduced"], f"reduced rep{rep}")
@@ -195,9 +198,10 @@ def test_live_docs_two_segments_postings(engine):
     want = O.run([(allc, sum(sizes))], aggs, accept=[bits_from_mask(np.concatenate(masks))])
     segs = [engine.upload_segment(c, n) for c, n in zip(cols, sizes)]
     plan = engine.plan(aggs)
-    for seg, m in zip(segs, masks):
+    for k, (seg, m) in enumerate(zip(segs, masks)):
         plan.collect(seg, accept_bits=bits_from_mask(m))
-        assert plan.last_collect_stats()[2] == 7
+        # (the first segment defers to the top-k, path 9; the second segment's collect counts it first)
+        assert plan.last_collect_stats()[2] == (9 if k == 0 else 7)
     assert_same(plan.build().to_dict(), want["shards"][0], "shard")
     plan.close()
     for seg in segs:
@@ -339,3 +343,32 @@ def test_deferred_cold_lists_second_segment_and_reset(engine):
     plan.close()
     for s in segs:
         s.close()
+
+
+@pytest.mark.parametrize("size", [3, 10, 100])
+def test_filtered_deferred_settled(engine, size):
+    """Config 3 under a range filter keeping ~75 % and under a live-docs bitset clearing 20 %: Zipf(1.1) head terms
+    settle the top-k from the hot slots (path 9); the other doc count is the passing hot docs plus the passing cold
+    docs counted beside them."""
+    n, T = 2_000_000, 400_000
+    cols = _zipf_cols(109, n, T)
+    aggs = [AB.terms("c").field("kw").size(size)]
+    _check(engine, cols, n, aggs, filters=[QB.rangeQuery("status").gte(1)], reps=2, path_want=9)
+    rng = np.random.default_rng(110)
+    _check(engine, cols, n, aggs, accept=bits_from_mask(rng.random(n) >= 0.2), reps=2, path_want=9)
+    _check(engine, cols, n, aggs, filters=[QB.rangeQuery("status").lte(2)],
+           accept=bits_from_mask(rng.random(n) >= 0.3), path_want=9)
+
+
+def test_filtered_deferred_fallback(engine):
+    """A filter whose passing docs are mostly cold: the hot slots' k-th count does not exceed the largest cold count,
+    so the scatter form counts the request (path 9's fallback, decided on the device); and a filter that keeps no doc."""
+    rng = np.random.default_rng(111)
+    n, T = 1_500_000, 200_000
+    cols = _cols(rng.integers(0, T, size=n), T, rng)
+    _check(engine, cols, n, [AB.terms("c").field("kw").size(25)], filters=[QB.rangeQuery("status").gte(2)], reps=2,
+           path_want=9)
+    zcols = _zipf_cols(112, n, T)
+    _check(engine, zcols, n, [AB.terms("c").field("kw").size(5)], filters=[QB.rangeQuery("status").gte(9)], path_want=9)
+    _check(engine, zcols, n, [AB.terms("c").field("kw").size(5).minDocCount(50_000)],
+           filters=[QB.rangeQuery("status").gte(1)], path_want=9)
