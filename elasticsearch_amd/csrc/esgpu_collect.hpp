@@ -994,6 +994,29 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
             }
         }
     }
+    if constexpr (LDS && kIntRuns<ORD, MET, VK> && (VK & 4096) == 0) {
+        // roughly time-ordered data (the blocks span more than one key: no runs1): a thread's consecutive docs alternate
+        // between neighbouring keys and its three runs thrash -- each doc goes straight to its key's LDS cells instead,
+        // in the lane's rotated copy (CollectParams.hdirect, ncopies); the values are exact integers, so the cells'
+        // f64 sums equal the runs' (and the reference's sequential additions below 2^53)
+        if (P.hdirect) {
+#pragma unroll
+            for (int j = 0; j < kVec; ++j) {
+                if (!((d.ok >> j) & 1) || !hv_ok[j]) continue;
+                const uint32_t c = slot[j] + a.coff;
+                const double x = (double)(P.mv_base + (int64_t)d.mvd[j]);
+                atomicAdd(&a.cnt32[c], 1u);
+                atomicAdd(&a.sum[c], x);
+                if (MET >= 3) atomicAdd(&a.sq[c], x * x);
+                if (MET >= 2) {
+                    const unsigned long long e = sortable(x);
+                    if (e < a.mn[MS * slot[j]]) atomicMin(&a.mn[MS * slot[j]], e);
+                    if (e > a.mx[MS * slot[j]]) atomicMax(&a.mx[MS * slot[j]], e);
+                }
+            }
+            return;
+        }
+    }
     if constexpr (LDS && kIntRuns<ORD, MET, VK>) {
         // integer runs: a thread's 4 docs that all pass and share one slot (time-sorted data: nearly always) are combined
         // into one run update; otherwise one update per doc
@@ -1538,7 +1561,8 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
     g.coff = 0;
     g.ocnt64 = P.g_ocnt;
     g.pk = nullptr; g.mm = nullptr; g.pkd = nullptr;
-    const uint32_t ncp = ORD ? max(P.ncopies, 1u) : 1u;  // additive cell copies (grids with a terms dimension)
+    // additive cell copies: grids with a terms dimension, and the per-doc integer-run grids (CollectParams.hdirect)
+    const uint32_t ncp = (ORD || (kIntRuns<ORD, MET, VK> && (VK & 4096) == 0)) ? max(P.ncopies, 1u) : 1u;
 
     // LDS window view.  Every pointer is derived from `smem` alone -- never merged with a global pointer -- so the
     // compiler keeps them in the LDS address space (ds_* instructions).  A generic pointer would compile to flat_*

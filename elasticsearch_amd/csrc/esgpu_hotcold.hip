@@ -159,7 +159,8 @@ __global__ __launch_bounds__(kHcWG) void hc_scatter_kernel(HcParams P) {
     const uint32_t b_end = min(b_begin + P.blocks_per_wg, P.n_blocks);
     const uint32_t d_begin = b_begin * kBlockDocs;
     const uint32_t d_end = min(b_end * kBlockDocs, P.n_docs);
-    const uint32_t d_last = P.n_blocks * kBlockDocs - 4;  // loads past the range re-read the segment's last quad
+    // loads past the range re-read the workgroup's own last quad (an L2 hit), not the next workgroup's docs from HBM
+    const uint32_t d_last = (b_end > b_begin ? b_end : P.n_blocks) * kBlockDocs - 4;
     const uint32_t tid4 = threadIdx.x * 4;
     auto load = [&](uint32_t t0, uint32_t o[kHcIt][4]) {
 #pragma unroll
@@ -531,7 +532,7 @@ __global__ __launch_bounds__(kHotWG) void hc_hot_kernel(HcParams P) {
     const uint32_t d_begin = b_begin * kBlockDocs;
     const uint32_t d_end = min(b_end * kBlockDocs, P.n_docs);
     const uint32_t span = b_end > b_begin ? (b_end - b_begin) * kBlockDocs : 0u;
-    const uint32_t d_last = P.n_blocks * kBlockDocs - 4;
+    const uint32_t d_last = (b_end > b_begin ? b_end : P.n_blocks) * kBlockDocs - 4;  // (the workgroup's own last quad)
     const uint32_t tid4 = threadIdx.x * 4;
     auto load = [&](uint32_t t0, uint32_t o[kHcIt][4], uint64_t aw[kHcIt]) {
 #pragma unroll
@@ -598,7 +599,7 @@ __global__ __launch_bounds__(kHotWG) void hc_hot16_count_kernel(HcParams P) {
     const uint32_t d_begin = b_begin * kBlockDocs;
     const uint32_t d_end = min(b_end * kBlockDocs, P.n_docs);
     const uint32_t span = b_end > b_begin ? (b_end - b_begin) * kBlockDocs : 0u;
-    const uint32_t d_last = P.n_blocks * kBlockDocs - 8;
+    const uint32_t d_last = (b_end > b_begin ? b_end : P.n_blocks) * kBlockDocs - 8;  // (the workgroup's own last 8 docs)
     const uint32_t tid8 = threadIdx.x * 8;
     auto load = [&](uint32_t t0, uint32_t o[kHcIt][4], uint64_t aw[kHcIt]) {
 #pragma unroll

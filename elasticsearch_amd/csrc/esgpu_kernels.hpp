@@ -111,6 +111,8 @@ struct CollectParams {
                          // register runs (ESGPU_PI_NHOT of them)
     int32_t raw_dense;   // histogram-only grid over dense compact columns, no filter: the raw-load kernels (VK bit 1024)
     int32_t runs1;       // integer runs over time-sorted data: one run accumulator per thread (VK bit 4096)
+    int32_t hdirect;     // histogram-only integer-run grids over roughly time-ordered data (no runs1): every doc straight
+                         // into its key's LDS cells, lane-rotated copies (ncopies) instead of three thrashing runs
     int32_t dot16;       // ... whose metric deltas stay below 46,341 (a pair's squares fit 32 bits): single-key zone
                          // blocks update the run from the raw 16-bit words with packed dot / min / max instructions
     int32_t ukey32;      // raw-load kernels over 32-bit timestamp deltas skip single-key zone blocks (VK bit 16384:

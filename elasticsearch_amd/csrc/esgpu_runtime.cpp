@@ -1693,6 +1693,7 @@ static bool raw_hist_on();
 static bool dd_forced();
 static bool int_runs_on();
 static bool dot16_on();
+static uint32_t hdirect_copies();
 static bool runs1_on();
 static bool b16_on(const esgpu_ctx* c);
 static bool pi_cells(const esgpu_ctx* c);
@@ -3305,6 +3306,16 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     // time-ordered data alternates between neighbouring keys and keeps three
     P.runs1 = m32 && P.mv16 && hc && pl.interval > 0 && hc->zspan < pl.interval && runs1_on() ? 1 : 0;
     P.dot16 = P.runs1 && mc && (uint64_t)mc->vmax - (uint64_t)mc->vmin <= 46340 && dot16_on() ? 1 : 0;
+    // ... and without runs1 (roughly time-ordered data), each doc straight into its key's LDS cells, in lane-rotated
+    // copies while they fit two workgroups per CU (ESGPU_HDIRECT=0: the three integer runs, for A/B runs)
+    P.hdirect = 0;
+    if (m32 && P.mv16 && !L_ORD && L_HIST && L_met > 0 && P.lds_mode && !P.runs1 && hdirect_copies() > 0) {
+        P.hdirect = 1;
+        for (uint32_t nc = hdirect_copies(); nc > 1; nc /= 2) {
+            const size_t b = collect_lds_bytes(LT, P.W, L_met, L_vcnt, L_ocnt, nc, pi);
+            if (b <= kLdsPair) { P.ncopies = nc; lds = b; break; }
+        }
+    }
     // raw-load kernels over 32-bit timestamp deltas (block deltas did not apply: runs spanning 2^16 ms or more) skip the
     // single-key zone blocks' deltas where most blocks hold one key (90 % of the blocks span less than one interval:
     // roughly time-ordered data displaced by minutes); with wider displacement the skip's conditional load costs more
@@ -3429,6 +3440,14 @@ static bool replay_compaction() {
     return on;
 }
 // integer run accumulators of histogram-only grids (VK bit 2048; ESGPU_INT_RUNS=0: the f64 runs, for A/B runs)
+// per-doc LDS cells for histogram-only integer-run grids over roughly time-ordered data (CollectParams.hdirect):
+// ESGPU_HDIRECT = the lane-rotated copies to try (0: off, the three integer runs).  Off: measured slower (config 2 at
+// +-1 h jitter, 1B docs: 2.96 ms with the runs, 4.76 ms with 2 or 4 copies, r6p -- the wave's docs land on ~3 keys, and
+// its f64 LDS atomics on those few addresses serialise)
+static uint32_t hdirect_copies() {
+    static const uint32_t n = [] { const char* e = std::getenv("ESGPU_HDIRECT"); return (uint32_t)(e && *e ? std::atoi(e) : 0); }();
+    return n;
+}
 // packed run updates for single-key zone blocks (CollectParams.dot16; ESGPU_DOT16=0: the unpacked update, for A/B runs)
 static bool dot16_on() {
     static const bool on = [] { const char* e = std::getenv("ESGPU_DOT16"); return !(e && *e == '0'); }();

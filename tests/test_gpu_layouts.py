@@ -211,6 +211,32 @@ def test_block_delta_keys(engine, t0, per_run, expect_block, jitter):
     seg.close()
 
 
+@pytest.mark.parametrize("jitter", [60_000, 3_600_000])
+def test_jittered_timestamps(engine, jitter):
+    """Roughly time-ordered data (merged segments: docs displaced by up to +-1 min / +-1 h; one day, 3M docs): every run
+    of 2,048 docs then spans >= 2^16 ms, so the key column is read as 32-bit deltas.  At +-1 min most zone blocks still
+    round to one hour (their deltas skipped, VK bit 16384; one integer run per thread); at +-1 h they span three, so
+    the histogram-only integer grids send each doc straight to its key's lane-rotated LDS cells (CollectParams.hdirect)
+    and the packed-cell grids take their per-doc path -- every leaf against the oracle, 1 h and 5 min keys."""
+    rng = np.random.default_rng(61)
+    n = 3_000_000 + 333
+    cols = _log_segment(rng, n, 1_441_065_600_000, 86_400_000)
+    cols["@timestamp"]["values"] = cols["@timestamp"]["values"] + rng.integers(-jitter, jitter + 1, size=n)
+    dh = lambda i: AB.dateHistogram("d").field("@timestamp").interval(i)  # noqa: E731
+    aggs = [dh("1h").subAggregation(AB.extendedStats("e").field("rt")),
+            dh("1h").subAggregation(AB.stats("s").field("rt")),
+            dh("1h").subAggregation(AB.avg("a").field("rt")),
+            dh("5m").subAggregation(AB.extendedStats("e").field("rt")),
+            AB.terms("h").field("host").size(5).subAggregation(dh("1h").subAggregation(AB.stats("s").field("rt"))),
+            AB.terms("h").field("host").size(5).subAggregation(dh("1h").subAggregation(AB.avg("a").field("rt")))]
+    seg = engine.upload_segment(cols, n)
+    for k, a in enumerate(aggs):
+        want = O.run([(cols, n)], [a])
+        r, _ = _run(engine, seg, [a])
+        assert_same(r.to_dict(), want["shards"][0], f"jitter {jitter} agg {k}")
+    seg.close()
+
+
 def _log_segment(rng, n, t0, span_ms, nterms=300, metric=None):
     ranks = np.minimum(rng.zipf(1.2, size=n) - 1, nterms - 1)
     cols = {
