@@ -972,6 +972,7 @@ struct Pipeline {
     // three bucket levels (two terms and one histogram): the ordinal dimension is the pair of the two terms fields,
     // ord = a * vcB + b (ord_field = a's field, ord_field2 = b's), derived per segment into ord_col
     bool cnt32 = false;              // g_cnt holds u32 counts (written by the partitioned / hot-cold terms paths)
+    bool zero_pending = false;       // g_cnt not zeroed since the plan's reset yet (zero_counts)
     bool comp = false;
     int comp_spec2 = -1;
     // terms under terms whose [outer x inner] grid is over the dense budget (ESGPU_DEFER_CELLS, default 2^31 cells):
@@ -1538,6 +1539,20 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
     });
 }
 
+// The grid's doc counts are zeroed lazily after a reset: a request whose first segment takes a hot / cold path stores
+// every counter (HcParams::overwrite) -- or, settled by its hot slots, never reads them -- and needs no zeroing pass
+// (80 MB at 10M ordinals, 28 us per config-3 shard request); every other path, and a build with no collect, zeroes
+// them first.
+static void zero_counts(esgpu_plan* p, Pipeline& pl) {
+    if (!pl.zero_pending) return;
+    pl.zero_pending = false;
+    if (!pl.allocated || !pl.g_cnt.p) return;
+    HIPX(hipMemsetAsync(pl.g_cnt.p, 0, (size_t)pl.T * pl.H * 8, p->stream));
+}
+static void zero_all_counts(esgpu_plan* p) {
+    for (Pipeline& pl : p->pipes) zero_counts(p, pl);
+}
+
 static void alloc_grid(esgpu_plan* p, Pipeline& pl) {
     esgpu_ctx* c = p->ctx;
     const size_t cells = (size_t)pl.T * pl.H;
@@ -1550,6 +1565,7 @@ static void alloc_grid(esgpu_plan* p, Pipeline& pl) {
     };
     need(pl.g_cnt, true, cells * 8);
     HIPX(hipMemsetAsync(pl.g_cnt.p, 0, cells * 8, p->stream));
+    pl.zero_pending = false;
     const size_t no = pl.ocnt_mode == OCNT_HIST ? pl.H : pl.T;
     need(pl.g_ocnt, pl.ocnt_mode != OCNT_NONE, no * 8);
     if (pl.ocnt_mode != OCNT_NONE) HIPX(hipMemsetAsync(pl.g_ocnt.p, 0, pl.g_ocnt.bytes, p->stream));
@@ -2883,6 +2899,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     // an unmapped metric field collects nothing (ValuesSource null => NO_OP collector); counts stay separate
     const int met_launch = mc ? pl.met : 0;
     const bool first_segment = pl.fresh;
+    if (!first_segment) zero_counts(p, pl);  // (a first segment that launched nothing left them pending)
     // ---- shape the grid ----
     if (pl.fresh) {  // first segment since create / reset: the grid shape and the dictionary are taken from it
         pl.kt_lo = 0;
@@ -3087,6 +3104,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     if (multi && !inner_missing) count_width(p, pl, s, false, first_segment);
     if (multi) {
         need_wide(true);
+        zero_counts(p, pl);
         const bool ok = collect_multi(p, pl, s, P, L_ORD ? oc : nullptr, L_HIST ? hc : nullptr, inner_missing ? nullptr : mc,
                                       L_met, d_accept);
         dd_fold();
@@ -3267,7 +3285,12 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         p->last_bytes += bytes_per_doc * (uint64_t)s->max_doc + (d_accept ? ((uint64_t)s->max_doc + 7) / 8 : 0);
         count_width(p, pl, s, true, first_segment);
         // (the hot/cold form keeps statistics per ordinal column: not for a column derived per request)
-        if (ESGPU_HOTCOLD && !pl.comp && collect_hotcold(p, pl, s, oc, d_accept, P.pred, P.npred, first_segment)) return 1;
+        if (ESGPU_HOTCOLD && !pl.comp && collect_hotcold(p, pl, s, oc, d_accept, P.pred, P.npred, first_segment)) {
+            if (first_segment) pl.zero_pending = false;  // (every counter stored, or never read: HcParams::overwrite)
+            else zero_counts(p, pl);
+            return 1;
+        }
+        zero_counts(p, pl);
         return collect_partitioned(p, pl, s, oc, d_accept, P.pred, P.npred) ? 1 : 0;
     }
     if (!inner_missing) count_width(p, pl, s, false, first_segment);
@@ -3413,6 +3436,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         P.accept = bits;
         P.npred = 0;
     }
+    zero_counts(p, pl);
     launch_collect(P, L_ORD, L_HIST, L_met, wide, grid, lds, p->stream);
     HIPX(hipGetLastError());
     HIPX(hipEventRecord(pl.e1, p->stream));
@@ -5521,6 +5545,7 @@ static Block build_cardinality(esgpu_plan* p, Pipeline& pl) {
 extern "C" int esgpu_plan_build(esgpu_plan* p, esgpu_result** out) {
     return guarded([&] {
         require(p && out, ESGPU_ERR_INVALID, "null argument");
+        zero_all_counts(p);  // (a pipeline no segment reached since the reset)
         const double t0 = now_ms();
         p->b_wait = 0;
         p->b_trace = std::getenv("ESGPU_TRACE_BUILD") != nullptr;
@@ -5645,7 +5670,7 @@ extern "C" int esgpu_plan_reset(esgpu_plan* p) {
                 fl.v[fl.count] = v;
                 if (++fl.count == kFillSpans) { launch_fill_multi(fl, p->stream); fl.count = 0; }
             };
-            span(pl.g_cnt.p, cells, 0ull);
+            pl.zero_pending = pl.g_cnt.p != nullptr;  // (zero_counts: at the request's first collect or build)
             if (pl.g_ocnt.p) {
                 if (pl.g_ocnt.bytes % 8 == 0) span(pl.g_ocnt.p, pl.g_ocnt.bytes / 8, 0ull);
                 else HIPX(hipMemsetAsync(pl.g_ocnt.p, 0, pl.g_ocnt.bytes, p->stream));
@@ -6039,6 +6064,7 @@ extern "C" int esgpu_plans_build_reduce(esgpu_plan* const* plans, int32_t n, esg
     tune_host_heap();
     return guarded([&] {
         require(plans && out && n >= 1, ESGPU_ERR_INVALID, "build_reduce needs at least one plan");
+        for (int i = 0; i < n; ++i) if (plans[i]) zero_all_counts(plans[i]);
         std::vector<std::unique_ptr<ResultHolder, void (*)(ResultHolder*)>> parts;
         const bool colo = colo_eligible(plans, n) && std::getenv("ESGPU_COLO") == nullptr;
         const bool merged_shape = colo && !plans[0]->groups[0].kids.empty();
@@ -6612,6 +6638,7 @@ extern "C" int esgpu_comm_build_reduce(esgpu_comm* cm, esgpu_plan* const* plans,
     return guarded([&] {
         require(cm && plans && out && n >= 1 && n <= kColoMaxShards, ESGPU_ERR_INVALID, "build_reduce needs 1..64 local plans");
         for (int i = 0; i < n; ++i) require(plans[i] != nullptr, ESGPU_ERR_INVALID, "null plan");
+        for (int i = 0; i < n; ++i) zero_all_counts(plans[i]);
         Collective& C = comm_collective(cm);
         require(root < C.nranks, ESGPU_ERR_INVALID, "build_reduce root is not a rank of the communicator");
         const double t_start = now_ms();
