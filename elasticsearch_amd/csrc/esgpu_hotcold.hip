@@ -682,6 +682,91 @@ __global__ __launch_bounds__(256) void hc_cold_sub_kernel(const uint32_t* rc, co
     }
 }
 
+// ---- replay over the hot inner terms (ReplayHotParams) ----
+size_t replay_hot_lds(uint32_t k, uint32_t Hh, uint32_t slot_map_n) {
+    return (size_t)replay_hot_stride(k, Hh) * 4 + (((size_t)slot_map_n + 15) & ~(size_t)15);
+}
+constexpr int kRhWG = 512;
+constexpr int kRhIt = 2;  // 16-byte loads of each column per thread per tile
+constexpr uint32_t kRhTileDocs = kRhWG * kRhIt * 8;
+__global__ __launch_bounds__(kRhWG) void replay_hot_kernel(ReplayHotParams P) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t stride = replay_hot_stride(P.k, P.Hh);
+    uint32_t* cnt = (uint32_t*)smem;                 // [k][Hh], then [k] missing-term counts
+    uint8_t* map = smem + (size_t)stride * 4;        // [slot_map_n]
+    for (uint32_t i = threadIdx.x; i < stride; i += kRhWG) cnt[i] = 0u;
+    for (uint32_t i = threadIdx.x; i < P.slot_map_n; i += kRhWG) map[i] = P.slot_map[i];
+    __syncthreads();
+    const uint32_t w = blockIdx.x;
+    const uint32_t b_begin = min(w * P.blocks_per_wg, P.n_blocks);
+    const uint32_t b_end = min(b_begin + P.blocks_per_wg, P.n_blocks);
+    const uint32_t d_begin = b_begin * kBlockDocs;
+    const uint32_t d_end = min(b_end * kBlockDocs, P.n_docs);
+    const uint32_t span = b_end > b_begin ? (b_end - b_begin) * kBlockDocs : 0u;
+    const uint32_t d_last = (b_end > b_begin ? b_end : P.n_blocks) * kBlockDocs - 8;  // (the workgroup's own last 8 docs)
+    const uint32_t tid8 = threadIdx.x * 8;
+    const uint32_t Hh = P.Hh, nmap = P.slot_map_n, k = P.k;
+    const bool acc = P.accept != nullptr;
+    auto load = [&](uint32_t t0, u32x4_t a[kRhIt], u32x4_t h[kRhIt], uint64_t aw[kRhIt]) {
+#pragma unroll
+        for (int it = 0; it < kRhIt; ++it) {
+            const uint32_t d = min(t0 + it * (kRhWG * 8) + tid8, d_last);
+            a[it] = load16(P.a16 + d);
+            h[it] = load16(P.hot16 + d);
+            aw[it] = acc ? P.accept[d >> 6] : ~0ull;
+        }
+    };
+    auto count = [&](uint32_t t0, const u32x4_t a[kRhIt], const u32x4_t h[kRhIt], const uint64_t aw[kRhIt]) {
+        if (t0 >= d_begin + span) return;
+#pragma unroll
+        for (int it = 0; it < kRhIt; ++it) {
+            const uint32_t doc0 = t0 + it * (kRhWG * 8) + tid8;
+            const uint32_t live = (uint32_t)(aw[it] >> (doc0 & 63)) & 0xFFu;
+            const uint32_t aw4[4] = {a[it].x, a[it].y, a[it].z, a[it].w}, hw4[4] = {h[it].x, h[it].y, h[it].z, h[it].w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t o = (aw4[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                const uint32_t sl = (hw4[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                const uint32_t s = o < nmap ? map[o] : 0xFFu;
+                if (s < k && doc0 + j < d_end && ((live >> j) & 1u)) {
+                    if (sl < Hh) atomicAdd(&cnt[s * Hh + sl], 1u);
+                    else if (sl == 0xFFFFu) atomicAdd(&cnt[k * Hh + s], 1u);
+                }
+            }
+        }
+    };
+    if (span) {
+        u32x4_t A[kRhIt], Ah[kRhIt], B[kRhIt], Bh[kRhIt];
+        uint64_t Aw[kRhIt], Bw[kRhIt];
+        load(d_begin, A, Ah, Aw);
+        load(d_begin + kRhTileDocs, B, Bh, Bw);
+        for (uint32_t t0 = d_begin; t0 < d_begin + span; t0 += 2 * kRhTileDocs) {
+            count(t0, A, Ah, Aw);
+            load(t0 + 2 * kRhTileDocs, A, Ah, Aw);
+            count(t0 + kRhTileDocs, B, Bh, Bw);
+            load(t0 + 3 * kRhTileDocs, B, Bh, Bw);
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < stride; i += kRhWG) P.slab[(size_t)w * stride + i] = cnt[i];
+}
+__global__ __launch_bounds__(256) void replay_hot_sum_kernel(ReplayHotParams P) {
+    const uint32_t stride = replay_hot_stride(P.k, P.Hh);
+    const uint32_t i = (blockIdx.x * 256 + threadIdx.x) * 4;
+    if (i >= stride) return;
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    for (uint32_t g = 0; g < P.G; ++g) {
+        const uint4 v = *reinterpret_cast<const uint4*>(P.slab + (size_t)g * stride + i);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    *reinterpret_cast<uint4*>(P.out + i) = acc;
+}
+void launch_replay_hot(const ReplayHotParams& p, hipStream_t s) {
+    hipLaunchKernelGGL(replay_hot_kernel, dim3(p.G), dim3(kRhWG), replay_hot_lds(p.k, p.Hh, p.slot_map_n), s, p);
+    const uint32_t stride = replay_hot_stride(p.k, p.Hh);
+    hipLaunchKernelGGL(replay_hot_sum_kernel, dim3((stride / 4 + 255) / 256), dim3(256), 0, s, p);
+}
+
 // the deferred cold lists' fold: the hot slot totals onto their ordinals (after the overwriting cold count)
 __global__ __launch_bounds__(256) void hc_slot_fold_kernel(HcParams P) {
     if (P.skip && *P.skip) return;

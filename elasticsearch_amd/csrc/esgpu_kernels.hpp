@@ -439,6 +439,23 @@ struct ReplayCompactParams {
 };
 constexpr uint32_t kReplayMaxBatches = 1024, kReplayBatchShift = 20, kReplayFillStride = 64;
 void launch_replay_compact(const ReplayCompactParams& p, hipStream_t s);
+// The breadth-first replay of a count-ordered terms child over its segment's hot inner terms (replay_hot): one pass
+// counts, per outer winner, its docs on each of the inner field's Hh most frequent terms (the statistics' hot slots,
+// most frequent first) in LDS, and the docs whose inner term is missing; a per-workgroup slab row is summed after.
+struct ReplayHotParams {
+    uint32_t n_docs, n_blocks, blocks_per_wg, G;
+    const uint16_t* a16;         // outer ordinals, 16 bits (0xFFFF missing)
+    const uint16_t* hot16;       // inner hot slot (0xFFFE a colder term, 0xFFFF missing)
+    const uint8_t* slot_map;     // [slot_map_n] outer ordinal -> winner index (0xFF: not a winner)
+    uint32_t slot_map_n;
+    const uint64_t* accept;      // the request's folded clauses and live docs (null: every doc)
+    uint32_t k, Hh;              // winners (< 255), hot slots counted per winner
+    uint32_t* slab;              // [G][stride]: k * Hh counts, then k missing-term counts
+    uint32_t* out;               // [stride] the sums
+};
+__host__ __device__ inline uint32_t replay_hot_stride(uint32_t k, uint32_t Hh) { return ((k * Hh + k) + 3u) & ~3u; }  // slab row words
+size_t replay_hot_lds(uint32_t k, uint32_t Hh, uint32_t slot_map_n);
+void launch_replay_hot(const ReplayHotParams& p, hipStream_t s);
 void launch_comp_ords(const uint32_t* a, const uint32_t* b, uint32_t n_pad, uint32_t na, uint32_t nb, const uint32_t* amap,
                       uint32_t amap_n, uint32_t* out, hipStream_t st);
 void launch_hist_ords(const int64_t* v, const uint64_t* present, uint32_t n_docs, uint32_t n_pad, bool f64, int64_t interval,

@@ -1954,6 +1954,7 @@ struct HcStats {
     bool u16 = false;            // every cold ordinal's count < 65536: packed 16-bit counters in the counting pass
     uint64_t pbuf_elems = 0;     // partition regions + kHcTile spare elements
     uint64_t hot_docs = 0, docs = 0;
+    std::vector<uint32_t> hot_cnt;  // each hot slot's count in the segment (most frequent first)
     uint64_t max_cold = 0;       // the largest count of a cold ordinal in the segment (unfiltered): a request's top-k
                                  // in count order is settled by the hot slots alone when its k-th count is above it
     bool refused = false;        // outside what the hot/cold kernels handle (cached: the check counts the column)
@@ -2055,7 +2056,7 @@ static std::shared_ptr<const HcStats> ensure_hc_stats(esgpu_ctx* c, const DevCol
         H = (uint32_t)std::max<int64_t>(0, hot_fit(kLdsCu));
     }
     // hot set: the H most frequent ordinals (ties by ordinal), slot 0 the most frequent
-    std::vector<uint32_t> hot;
+    std::vector<uint32_t> hot, hot_cnt;
     uint64_t hot_total = 0, total = 0;
     {
         DevBuf dcand, dmeta;
@@ -2090,16 +2091,19 @@ static std::shared_ptr<const HcStats> ensure_hc_stats(esgpu_ctx* c, const DevCol
                 const uint64_t cntv = (keys[i] >> 32) & 0x7FFFFFFFull;
                 if (cntv == 0) break;
                 hot.push_back(0xFFFFFFFFu - (uint32_t)keys[i]);
+                hot_cnt.push_back((uint32_t)cntv);
                 hot_total += cntv;
             }
         }
         if (hot_total * 20 < total) {  // under 5 % of the docs: the recoded copy would not pay for itself
             hot.clear();
+            hot_cnt.clear();
             hot_total = 0;
         }
     }
     hs->docs = total;
     hs->hot_n = (uint32_t)hot.size();
+    hs->hot_cnt = hot_cnt;
     hs->hot_docs = hot_total;
     std::vector<uint64_t> cold(P, 0);
     uint64_t max_cold = 0;
@@ -4693,6 +4697,123 @@ static bool replay_compact(esgpu_plan* p, const ChildSrc& kid, const std::vector
     return true;
 }
 
+// The replay of a count-only child in count order over the inner field's hot terms (ReplayHotParams): with one retained
+// segment, the inner field's statistics (HcStats: hot slots most frequent first, each slot's count, the largest cold
+// count) bound every term outside the first Hh hot slots by the count of slot Hh (or the largest cold count).  One pass
+// counts each winner's docs on those Hh slots (in LDS) and its docs without an inner term; per winner the GPU top-k
+// (K3) over its Hh slots, mapped to ordinals, gives the winners' inner terms whenever its k-th count is above that bound
+// -- no other term can reach it (ties go to the smaller ordinal, which may be outside: strictly above) -- and the other
+// doc count is the winner's doc count less its missing-term docs and its picks.  False when it does not apply or some
+// winner is not settled: the full replay then runs (ESGPU_REPLAY_HOT=0: always).
+static bool replay_hot(esgpu_plan* p, const ChildSrc& kid, const std::vector<TermPick>& top, uint64_t T_outer, ReplaySel& rs) {
+    static const bool on = [] { const char* e = std::getenv("ESGPU_REPLAY_HOT"); return !(e && *e == '0'); }();
+    if (!on || kid.rpipes.size() != 1 || !kid.rgrand.empty() || p->dsegs.size() != 1) return false;
+    const SpecNode& tn2 = p->specs[kid.spec];
+    Pipeline& R0 = p->pipes[kid.rpipes[0]];
+    if (tn2.s.order != ESGPU_ORDER_COUNT_DESC || R0.met != 0 || !R0.cards.empty() || tn2.s.shard_size < 1) return false;
+    const uint32_t k = (uint32_t)top.size();
+    if (k == 0 || k >= 255) return false;
+    for (const TermPick& tp : top) if (tp.count < 0) return false;
+    esgpu_ctx* c = p->ctx;
+    hipStream_t st = p->stream;
+    const esgpu_plan::DeferredSeg& d = p->dsegs[0];
+    const DevColumn* a = d.s->col(R0.ord_field.c_str());
+    const DevColumn* b = d.s->col(R0.ord_field2.c_str());
+    if (!a || !b || a->multi || b->multi || T_outer > 65535 || a->ord_count() > 65535 || b->ord_count() <= 65536) return false;
+    const uint16_t* a16 = ensure_ord16(c, a, d.s, st);
+    if (!a16) return false;
+    std::shared_ptr<const HcStats> hs = ensure_hc_stats(c, b, d.s, (uint32_t)b->ord_count(), st);
+    if (!hs || !hs->hot_n || !hs->d_hot16.p || hs->hot_cnt.size() != hs->hot_n) return false;
+    const uint32_t kk = (uint32_t)std::min<uint64_t>(b->ord_count(), (uint64_t)tn2.s.shard_size);
+    // the hot slots per winner that fit LDS beside the outer ordinal -> winner map
+    const size_t budget = 156 * 1024;
+    const uint32_t nmap = (uint32_t)std::max<uint64_t>(T_outer, 1);
+    uint32_t Hh = std::min<uint32_t>(hs->hot_n, 65534);
+    while (Hh > 0 && replay_hot_lds(k, Hh, nmap) > budget) Hh = Hh > 64 ? Hh - 64 : 0;
+    if (Hh < kk || kk > kTopkMax) return false;
+    const uint64_t bound = Hh < hs->hot_n ? (uint64_t)hs->hot_cnt[Hh] : hs->max_cold;
+    // the request's clauses (as the collect applied them) and live docs, folded into one bitset
+    const uint64_t* acc = d.accept >= 0 ? p->d_daccept[d.accept].as<uint64_t>() : nullptr;
+    PredDev pred[4];
+    int32_t npred = 0;
+    uint64_t bytes = 0;
+    set_preds(p, R0, d.s, pred, &npred, &bytes, &acc);
+    if (npred > 0) {
+        uint64_t* xb = (uint64_t*)p->s_hbits.ensure(c, std::max<size_t>(d.s->n_pad / 64, 1) * 8);
+        launch_filter_bits4(d.s->max_doc, acc, pred, npred, xb, st);
+        HIPX(hipGetLastError());
+        acc = xb;
+    }
+    std::vector<uint8_t> map(nmap, 0xFF);
+    for (uint32_t w = 0; w < k; ++w) if (top[w].ord < nmap) map[top[w].ord] = (uint8_t)w;
+    ReplayHotParams Q{};
+    Q.n_docs = d.s->max_doc;
+    Q.n_blocks = d.s->n_pad / kBlockDocs;
+    Q.G = std::max(1u, std::min<uint32_t>((uint32_t)c->cus, Q.n_blocks));
+    Q.blocks_per_wg = (Q.n_blocks + Q.G - 1) / Q.G;
+    Q.G = std::max(1u, (Q.n_blocks + Q.blocks_per_wg - 1) / Q.blocks_per_wg);
+    Q.a16 = a16;
+    Q.hot16 = hs->d_hot16.as<uint16_t>();
+    Q.slot_map_n = nmap;
+    Q.accept = acc;
+    Q.k = k;
+    Q.Hh = Hh;
+    const uint32_t stride = replay_hot_stride(k, Hh);
+    unsigned char* meta = (unsigned char*)p->s_rmeta.ensure(c, (((size_t)nmap + 15) & ~(size_t)15) + (size_t)stride * 4);
+    Q.slot_map = meta;
+    Q.out = (uint32_t*)(meta + (((size_t)nmap + 15) & ~(size_t)15));
+    Q.slab = (uint32_t*)p->s_rregion.ensure(c, (size_t)Q.G * stride * 4);
+    HIPX(hipMemcpyAsync(meta, map.data(), nmap, hipMemcpyHostToDevice, st));
+    launch_replay_hot(Q, st);
+    HIPX(hipGetLastError());
+    // per winner: K3 over its Hh slot counts, keys mapped to the inner ordinals
+    unsigned long long* dk = (unsigned long long*)p->s_rkeys.ensure(c, (size_t)k * (kk + 1) * 8);
+    HIPX(hipMemsetAsync(dk, 0, (size_t)k * (kk + 1) * 8, st));
+    const uint32_t n_wg = std::min<uint32_t>(512, (Hh + 4095) / 4096);
+    unsigned long long* cand = (unsigned long long*)p->s_cand.ensure(c, (size_t)Hh * 8);
+    uint32_t* hh = (uint32_t*)p->s_hist.ensure(c, (2048 + 2) * 4);
+    for (uint32_t w = 0; w < k; ++w) {
+        TopkParams K{};
+        K.counts32 = Q.out + (size_t)w * Hh;
+        K.ord_of = hs->d_hot_ord.as<uint32_t>();
+        K.T = Hh;
+        K.order = tn2.s.order;
+        K.min_doc_count = tn2.s.min_doc_count;
+        K.shard_min_doc_count = tn2.s.shard_min_doc_count;
+        K.k = kk;
+        K.n_wg = n_wg;
+        K.cand = cand;
+        K.hist = hh;
+        K.sel = hh + 2048;
+        K.out_keys = dk + (size_t)w * (kk + 1);
+        K.out_sum = K.out_keys + kk;
+        launch_topk(K, st);
+        HIPX(hipGetLastError());
+    }
+    d2h_u64(p, p->h_rkeys, dk, (size_t)k * (kk + 1));
+    uint32_t* hmiss = (uint32_t*)p->h_rfill.ensure((size_t)k * 4 + 16);
+    HIPX(hipMemcpyAsync(hmiss, Q.out + (size_t)k * Hh, (size_t)k * 4, hipMemcpyDeviceToHost, st));
+    bsync(p);
+    const unsigned long long* hk = p->h_rkeys.as<unsigned long long>();
+    for (uint32_t w = 0; w < k; ++w) {
+        const unsigned long long last = hk[(size_t)w * (kk + 1) + kk - 1];
+        if (last == 0 || ((last >> 32) & 0x7FFFFFFFull) <= bound) return false;  // not settled: the full replay
+    }
+    for (uint32_t w = 0; w < k; ++w) {
+        const unsigned long long* ki = hk + (size_t)w * (kk + 1);
+        rs.other[w] = top[w].count - (int64_t)hmiss[w];
+        for (uint32_t j = 0; j < kk; ++j) {
+            TermPick tp;
+            tp.ord = 0xFFFFFFFFu - (uint32_t)ki[j];
+            tp.count = (int64_t)((ki[j] >> 32) & 0x7FFFFFFFull);
+            rs.other[w] -= tp.count;
+            rs.cell[w].push_back(0);  // (no gather: the counts came with the keys)
+            rs.picks[w].push_back(tp);
+        }
+    }
+    return true;
+}
+
 // TermsAggregator breadth_first (A/bucket/terms/TermsAggregator.java:161 shouldDefer; BestBucketsDeferringCollector
 // .prepareSelectedBuckets :127-166, replayed from GlobalOrdinalsStringTermsAggregator.buildAggregation :195-196): the
 // child's collectors run again over the retained segments, each doc counted in its outer bucket's winner slot when that
@@ -4708,6 +4829,7 @@ static ReplaySel replay_child(esgpu_plan* p, const ChildSrc& kid, const std::vec
     rs.other.assign(k, 0);
     rs.cell.resize(k);
     if (!k || kid.rpipes.empty()) return rs;
+    if (replay_hot(p, kid, top, T_outer, rs)) return rs;
     hipStream_t st = p->stream;
     const SpecNode& tn2 = p->specs[kid.spec];
     const Pipeline& B0 = p->pipes[kid.pipes[0]];

@@ -18,11 +18,13 @@ from helpers import assert_same, bits_from_mask, synthetic_columns
 pytestmark = pytest.mark.gpu
 
 
-def _segment(seed, n, t_a=300, t_b=2000):
+def _segment(seed, n, t_a=300, t_b=2000, uniform_b=False):
     rng = np.random.default_rng(seed)
     a = ((np.minimum(rng.zipf(1.3, size=n) - 1, t_a - 1) * 7919 + 13) % t_a).astype(np.uint32)
     a[rng.random(n) < 0.03] = 0xFFFFFFFF
     b = ((np.minimum(rng.zipf(1.1, size=n) - 1, t_b - 1) * 104729 + 7) % t_b).astype(np.uint32)
+    if uniform_b:
+        b = rng.integers(0, t_b, size=n).astype(np.uint32)
     b[rng.random(n) < 0.05] = 0xFFFFFFFF
     num = rng.integers(0, 1000, size=n).astype(np.int64)
     present = rng.random(n) >= 0.1
@@ -48,8 +50,9 @@ def _concat(segs):
 
 
 def _run(engine, aggs, segs_per_shard=1, shards=2, n=120_000, t_b=2000, filters=None, deletes=0.0, close_early=False,
-         replayed=True):
-    cols = [[_segment(70 + 10 * s + j, n, t_b=t_b) for j in range(segs_per_shard)] for s in range(shards)]
+         replayed=True, uniform_b=False):
+    cols = [[_segment(70 + 10 * s + j, n, t_b=t_b, uniform_b=uniform_b) for j in range(segs_per_shard)]
+            for s in range(shards)]
     masks = [[np.random.default_rng(900 + 10 * s + j).random(n) >= deletes for j in range(segs_per_shard)]
              for s in range(shards)]
     lookups = {f: {t: i for i, t in enumerate(cols[0][0][f]["terms"])} for f in ("a", "b")}
@@ -184,3 +187,22 @@ def test_replayed_inner_shard_size_over_1024(engine, forced, order):
     inner.order(Order.count(False) if order == "count" else Order.term(True) if order == "term" else Order.count(True))
     aggs = [AB.terms("A").field("a").size(3).subAggregation(inner)]
     _run(engine, aggs, t_b=100_000, n=200_000, shards=1)
+
+
+@pytest.mark.parametrize("size,min_doc", [(3, 1), (10, 1), (60, 1), (5, 40)])
+def test_replayed_over_hot_inner_terms(engine, forced, size, min_doc):
+    """A count-ordered, count-only inner terms over 150,000 Zipf ordinals in one retained segment (the forced replay at
+    its real shape): each winner's inner terms come from one pass over the inner field's hot slots whenever its k-th
+    count is above every colder term's count in the segment (replay_hot), else from the full replay -- under a query
+    filter and live docs, with inner min_doc_count, against the oracle."""
+    inner = AB.terms("B").field("b").size(size).minDocCount(min_doc)
+    aggs = [AB.terms("A").field("a").size(4).subAggregation(inner)]
+    _run(engine, aggs, t_b=150_000, n=300_000, shards=2)
+    _run(engine, aggs, t_b=150_000, n=300_000, shards=1, filters=[QB.termQuery("status", 200)], deletes=0.05)
+
+
+def test_replayed_hot_inner_terms_unsettled(engine, forced):
+    """Uniform inner terms: the hot slots do not settle the winners' inner top-k (their counts tie with colder terms),
+    so the full replay runs -- the same result."""
+    aggs = [AB.terms("A").field("a").size(3).subAggregation(AB.terms("B").field("b").size(4))]
+    _run(engine, aggs, t_b=120_000, n=250_000, shards=1, uniform_b=True)
