@@ -1268,6 +1268,9 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
 #ifndef ESGPU_PI_HOTMM  // (A/B) the hot ordinal's register run keeps its (min, max) too (no LDS read for its docs)
 #define ESGPU_PI_HOTMM 0  // (measured slower: north star 1.081 -> 1.133 ms at 1B, r6h -- its VALU cost; 2 or 3 hot ordinals 1.54 / 1.91)
 #endif
+#ifndef ESGPU_PI_HOTPK  // the hot ordinal's count and sum by packed 16-bit compares and v_dot2 (0: per-doc selects, A/B)
+#define ESGPU_PI_HOTPK 1
+#endif
 #ifndef ESGPU_PI_MMU  // (A/B) uniform blocks' (min, max) updates: 2 = one divergent region per doc (as ESGPU_PI_MMCHECK 2),
 #define ESGPU_PI_MMU 2  // 3 = branch-free -- every lane issues both atomics, lanes whose bounds do not move on a spare word
 #endif
@@ -1318,7 +1321,21 @@ __device__ __forceinline__ void pi_uniform(const CollectParams& P, const Acc& a,
         pi_hot_flush<MET>(P, a, run, T);
         run.hslot = sl;
     }
-    {
+    if constexpr (ESGPU_PI_HOTPK && NH == 1 && kNHot == 1 && !ESGPU_PI_HOTMM && (VK & 512) == 0) {
+        // packed: the hot ordinal's docs among the 4 found as zero 16-bit halves of (ordinals ^ hot), their count and
+        // delta sum by v_dot2_u32_u16 (a doc equal to the hot ordinal is below T: no hit test needed without a bitset)
+        // (no hot ordinal, kMissingOrd: 0xFFFE halves, which no 16-bit ordinal or missing value (0xFFFF) equals)
+        const uint32_t ht = P.hot_t[0], htp = ht < T ? (ht | (ht << 16)) : 0xFFFEFFFEu;
+        const u16x2_t one = {1, 1};
+        const u16x2_t e0 = one - __builtin_elementwise_min(__builtin_bit_cast(u16x2_t, h0.raw[0] ^ htp), one);
+        const u16x2_t e1 = one - __builtin_elementwise_min(__builtin_bit_cast(u16x2_t, h0.raw[1] ^ htp), one);
+        run.hcnt[0] = __builtin_amdgcn_udot2(e0, one, __builtin_amdgcn_udot2(e1, one, run.hcnt[0], false), false);
+        run.hsum[0] = __builtin_amdgcn_udot2(e0, __builtin_bit_cast(u16x2_t, h0.raw[6]),
+                                             __builtin_amdgcn_udot2(e1, __builtin_bit_cast(u16x2_t, h0.raw[7]), run.hsum[0], false),
+                                             false);
+#pragma unroll
+        for (int j = 0; j < N; ++j) hpk[j] = hpk[j] & (t[j] != ht);
+    } else {
 #pragma unroll
         for (int k = 0; k < kNHot; ++k) {
             const uint32_t ht = P.hot_t[k];

@@ -1733,6 +1733,23 @@ void launch_fill_multi(const FillList& l, hipStream_t st) {
     hipLaunchKernelGGL(fill_multi_kernel, dim3((uint32_t)grid), dim3(256), 0, st, l);
 }
 
+__global__ __launch_bounds__(256) void copy_multi_kernel(CopyList L) {
+    const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
+    for (int k = 0; k < L.count; ++k) {
+        const unsigned long long* __restrict__ s = L.src[k];
+        unsigned long long* __restrict__ d = L.dst[k];
+        for (size_t i = g; i < L.n[k]; i += stride) d[i] = s[i];
+    }
+}
+void launch_copy_multi(const CopyList& l, hipStream_t st) {
+    uint64_t mx = 0;
+    for (int k = 0; k < l.count; ++k) mx = l.n[k] > mx ? l.n[k] : mx;
+    if (mx == 0) return;
+    size_t grid = (mx + 255) / 256;
+    if (grid > 4096) grid = 4096;
+    hipLaunchKernelGGL(copy_multi_kernel, dim3((uint32_t)grid), dim3(256), 0, st, l);
+}
+
 void launch_fill_u64(unsigned long long* p, size_t n, unsigned long long v, hipStream_t st) {
     if (n == 0) return;
     size_t grid = (n + 255) / 256;

@@ -487,6 +487,14 @@ struct FillList {
     int32_t count;
 };
 void launch_fill_multi(const FillList& l, hipStream_t s);
+// several device -> pinned-host copies in one launch (the build's grid arrays: one launch instead of one per array)
+struct CopyList {
+    const unsigned long long* src[kFillSpans];
+    unsigned long long* dst[kFillSpans];
+    uint64_t n[kFillSpans];
+    int32_t count;
+};
+void launch_copy_multi(const CopyList& l, hipStream_t s);
 
 }  // namespace esgpu
 

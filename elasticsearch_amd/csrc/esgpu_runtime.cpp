@@ -3425,8 +3425,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         launch_zone_keys(P, const_cast<int64_t*>(P.zkey), p->stream, ud);
         HIPX(hipGetLastError());
         if (ud) {
-            uint64_t* h = (uint64_t*)p->zu_host.ensure(kZuSlots * 8);
-            HIPX(hipMemcpyAsync(h + p->zu_n, ud, 8, hipMemcpyDeviceToHost, p->stream));
+            // (read by esgpu_plan_last_collect_stats: no per-collect copy to the host on the request's path)
             p->zu_w[p->zu_n] = P.hv16 ? 2 : 4;  // timestamp bytes per doc the skipped blocks did not read
             ++p->zu_n;
         }
@@ -3967,6 +3966,9 @@ extern "C" int esgpu_plan_last_collect_stats(const esgpu_plan* cp, double* kerne
             }
             p->last_ms = total;
             if (p->zu_n) {  // the timestamps of single-key zone blocks were not read
+                p->zu_host.ensure(kZuSlots * 8);
+                launch_copy_u64(p->s_zu.as<unsigned long long>(), (unsigned long long*)p->zu_host.dev(), p->zu_n, p->stream);
+                HIPX(hipGetLastError());
                 HIPX(hipStreamSynchronize(p->stream));
                 uint64_t ud = 0;
                 for (uint32_t i = 0; i < p->zu_n; ++i) ud += ((const uint64_t*)p->zu_host.p)[i] * p->zu_w[i];
@@ -4376,8 +4378,21 @@ static void fetch_grid(esgpu_plan* p, Pipeline& pl) {
         HIPX(hipGetLastError());
         src[0] = w;
     }
-    for (int a = 0; a < 6; ++a)
-        if (src[a]) d2h_u64(p, pl.h_cells[a], src[a], cells);
+    // the small arrays in one copy launch (config 2: five 721-cell arrays), large ones by DMA
+    CopyList cl{};
+    for (int a = 0; a < 6; ++a) {
+        if (!src[a]) continue;
+        if (cells * 8 > (4u << 20) || cells == 0) { d2h_u64(p, pl.h_cells[a], src[a], cells); continue; }
+        pl.h_cells[a].ensure(cells * 8);
+        cl.src[cl.count] = (const unsigned long long*)src[a];
+        cl.dst[cl.count] = (unsigned long long*)pl.h_cells[a].dev();
+        cl.n[cl.count] = cells;
+        ++cl.count;
+    }
+    if (cl.count) {
+        launch_copy_multi(cl, p->stream);
+        HIPX(hipGetLastError());
+    }
     point_cells(pl, src);
 }
 

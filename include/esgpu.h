@@ -373,7 +373,10 @@ int esgpu_plan_build(esgpu_plan* plan, esgpu_result** out);
 int esgpu_plan_reset(esgpu_plan* plan);
 int esgpu_plan_destroy(esgpu_plan* plan);
 /* Timing of the last collect_segment's dominant kernel (HIP events on the plan's stream), in milliseconds,
- * and the algorithmic bytes it read (SURVEY §8(d) formula). */
+ * and the algorithmic bytes it read (SURVEY §8(d) formula).  path: the collect form -- 0 grid in global memory,
+ * 1 LDS grid, 2 LDS key window, 3 HLL registers, 4 partitioned terms counting, 5 multi-valued (CSR) columns, 6 hot/cold
+ * terms scatter form, 7 hot/cold postings form, 8 hot slots only (cold lists deferred to the top-k), 9 hot slots of a
+ * filtered request (the scatter form deferred to the top-k). */
 int esgpu_plan_last_collect_stats(const esgpu_plan* plan, double* kernel_ms, uint64_t* algorithmic_bytes,
                                   int32_t* path);
 /* Wall time of the last esgpu_plan_build and the part of it spent waiting on the plan's stream (gathers and copies of
