@@ -2928,6 +2928,28 @@ __global__ __launch_bounds__(256) void hist_ords_kernel(const int64_t* v, const 
         out[d] = o;
     }
 }
+__global__ __launch_bounds__(256) void hist_ords_multi_kernel(const int64_t* v, const uint64_t* off, uint32_t n_docs, int f64,
+                                                              int64_t interval, int64_t offset, int64_t key0, uint32_t nkeys,
+                                                              uint32_t* out) {
+    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < n_docs; d += gridDim.x * blockDim.x) {
+        int64_t prev = 0;
+        bool first = true;
+        for (uint64_t i = off[d]; i < off[d + 1]; ++i) {
+            const int64_t x = f64 ? java_long(bits_dbl((uint64_t)v[i])) : v[i];
+            const int64_t k = floor_div64(x - offset, interval) - key0;
+            const bool dup = !first && k == prev;  // (a doc's values are sorted: its keys are too)
+            first = false;
+            prev = k;
+            out[i] = !dup && k >= 0 && k < (int64_t)nkeys ? (uint32_t)k : 0xFFFFFFFFu;
+        }
+    }
+}
+void launch_hist_ords_multi(const int64_t* v, const uint64_t* offsets, uint32_t n_docs, bool f64, int64_t interval,
+                            int64_t offset, int64_t key0, uint32_t nkeys, uint32_t* out, hipStream_t st) {
+    if (n_docs == 0) return;
+    hipLaunchKernelGGL(hist_ords_multi_kernel, dim3(std::min<uint32_t>(8192, (n_docs + 255) / 256)), dim3(256), 0, st, v,
+                       offsets, n_docs, f64 ? 1 : 0, interval, offset, key0, nkeys, out);
+}
 void launch_hist_ords(const int64_t* v, const uint64_t* present, uint32_t n_docs, uint32_t n_pad, bool f64, int64_t interval,
                       int64_t offset, int64_t key0, uint32_t nkeys, uint32_t* out, hipStream_t st) {
     if (n_pad == 0) return;

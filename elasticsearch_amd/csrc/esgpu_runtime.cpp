@@ -298,6 +298,7 @@ struct DevColumn {
     DevBuf values;   // padded to a multiple of kBlockDocs entries
     DevBuf present;  // optional
     DevBuf offsets;  // multi-valued: CSR offsets [max_doc + 1] (values hold n_values entries, padded)
+    const uint64_t* off_view = nullptr;  // a derived multi-valued column: its source's offsets (not owned)
     uint64_t n_values = 0;
     DevBuf zmin, zmax;
     int64_t vmin = INT64_MAX, vmax = INT64_MIN;  // over present values (I64 columns)
@@ -2544,7 +2545,7 @@ static bool collect_multi(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s, C
         P.accept = bits;
         P.npred = 0;
     }
-    P.ord_off = (oc && oc->multi) ? oc->offsets.as<uint64_t>() : nullptr;
+    P.ord_off = (oc && oc->multi) ? (oc->off_view ? oc->off_view : oc->offsets.as<uint64_t>()) : nullptr;
     P.hv_off = (hc && hc->multi) ? hc->offsets.as<uint64_t>() : nullptr;
     P.mv_off = (mc && mc->multi) ? mc->offsets.as<uint64_t>() : nullptr;
     if (P.ocnt_mode == OCNT_TERMS_DERIVED) P.ocnt_mode = OCNT_TERMS;  // outer counts per doc, never from the cells
@@ -2624,7 +2625,9 @@ static const DevColumn* derive_hist_ords(esgpu_plan* p, Pipeline& pl, const esgp
     if (!src) return nullptr;
     require(src->type == ESGPU_COL_I64 || src->type == ESGPU_COL_F64, ESGPU_ERR_UNSUPPORTED,
             "histogram over a keyword field runs on the CPU path");
-    require(!src->multi, ESGPU_ERR_UNSUPPORTED, "a multi-valued inner histogram field runs on the CPU path");
+    // a multi-valued inner field: one key index per value, in the source's CSR layout (collect_multi_kernel)
+    require(!src->multi || pl.cards.empty(), ESGPU_ERR_UNSUPPORTED,
+            "cardinality under a multi-valued inner histogram runs on the CPU path");
     const bool has = src->vmin <= src->vmax;
     const int64_t kmin = has ? floor_div64(src->vmin - pl.ord_offset, pl.ord_interval) : 0;
     const int64_t kmax = has ? floor_div64(src->vmax - pl.ord_offset, pl.ord_interval) : -1;
@@ -2651,7 +2654,9 @@ static const DevColumn* derive_hist_ords(esgpu_plan* p, Pipeline& pl, const esgp
     DevColumn& d = *pl.ord_col;
     d.name = pl.ord_field;
     d.type = ESGPU_COL_ORD_U32;
-    d.multi = false;
+    d.multi = src->multi;
+    d.n_values = src->multi ? src->n_values : 0;
+    d.off_view = src->multi ? src->offsets.as<uint64_t>() : nullptr;
     d.value_count = std::max<uint32_t>(pl.ord_keys, 1);
     if (materialize) materialize_hist_ords(p, pl, s);
     return &d;
@@ -2699,6 +2704,15 @@ static const DevColumn* derive_comp_ords(esgpu_plan* p, Pipeline& pl, const esgp
 static void materialize_hist_ords(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s) {
     const DevColumn* src = s->col(pl.ord_field.c_str());
     DevColumn& d = *pl.ord_col;
+    if (src->multi) {  // HistogramAggregator.collect: each value's key, a doc's repeated keys once (values are sorted)
+        const size_t nv = std::max<size_t>(src->n_values, 1);
+        if (d.values.bytes < nv * 4) d.values.alloc(p->ctx, nv * 4);
+        launch_hist_ords_multi((const int64_t*)wide_i64(p->ctx, src, s, p->stream), src->offsets.as<uint64_t>(), s->max_doc,
+                               src->type == ESGPU_COL_F64, pl.ord_interval, pl.ord_offset, pl.ord_key0, pl.ord_keys,
+                               d.values.as<uint32_t>(), p->stream);
+        HIPX(hipGetLastError());
+        return;
+    }
     if (d.values.bytes < (size_t)s->n_pad * 4) d.values.alloc(p->ctx, (size_t)s->n_pad * 4);
     launch_hist_ords((const int64_t*)wide_i64(p->ctx, src, s, p->stream), src->present.as<uint64_t>(), s->max_doc, s->n_pad,
                      src->type == ESGPU_COL_F64,

@@ -161,3 +161,38 @@ def test_later_segment_widens_inner_keys(engine, first):
     plan.close()
     for s in segs:
         s.close()
+
+
+def _multi_values(rng, n, lo, hi, f64=False, max_per_doc=3):
+    """a SortedNumeric field: 0..max_per_doc values per doc, sorted within the doc"""
+    per = rng.integers(0, max_per_doc + 1, size=n)
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(per)
+    vals = rng.integers(lo, hi, size=int(offs[-1])).astype(np.int64)
+    order = np.lexsort((vals, np.repeat(np.arange(n), per)))  # each doc's values sorted (SortedNumericDocValues)
+    vals = vals[order]
+    if f64:
+        vals = (vals.astype(np.float64) + 0.25)
+    return vals, offs
+
+
+@pytest.mark.parametrize("f64", [False, True])
+def test_multi_valued_inner_histogram(engine, f64):
+    """A multi-valued inner histogram field (SortedNumeric, several latencies per doc): each value's key, a doc's
+    repeated keys once (HistogramAggregator.collect over sorted values), counted in the CSR collect kernel from a key
+    index per value -- doc counts, avg / extended_stats leaves and inner empty buckets against the oracle."""
+    rng = np.random.default_rng(77)
+    n = 200_000
+    cols = synthetic_columns(("@timestamp", "bytes"), n)
+    vals, offs = _multi_values(rng, n, 0, 2000, f64=f64)
+    cols["lat"] = {"type": N.COL_F64 if f64 else N.COL_I64, "values": vals, "offsets": offs}
+    aggs = [AB.dateHistogram("d").field("@timestamp").interval("1d").minDocCount(1).subAggregation(
+                AB.histogram("lat").field("lat").interval(250).minDocCount(0)
+                .subAggregation(AB.avg("b").field("bytes")).subAggregation(AB.extendedStats("x").field("bytes")))]
+    want = O.run([(cols, n)], aggs)
+    seg = engine.upload_segment(cols, n)
+    plan = engine.plan(aggs)
+    plan.collect(seg)
+    assert_same(plan.build().to_dict(), want["shards"][0], "shard")
+    plan.close()
+    seg.close()
