@@ -2944,6 +2944,46 @@ __global__ __launch_bounds__(256) void hist_ords_multi_kernel(const int64_t* v, 
         }
     }
 }
+__device__ __forceinline__ uint32_t table_key(const int64_t* starts, uint32_t nsteps, const uint32_t* slot, uint32_t nkeys,
+                                              int64_t x) {
+    if (nsteps == 0 || x < starts[0]) return 0xFFFFFFFFu;
+    uint32_t lo = 0, hi = nsteps;  // starts[lo] <= x < starts[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (starts[mid] <= x) lo = mid; else hi = mid;
+    }
+    const uint32_t k = slot ? slot[lo] : lo;
+    return k < nkeys ? k : 0xFFFFFFFFu;
+}
+__global__ __launch_bounds__(256) void hist_ords_table_kernel(const int64_t* v, const uint64_t* present, const uint64_t* off,
+                                                              uint32_t n_docs, uint32_t n_pad, int f64, const int64_t* starts,
+                                                              uint32_t nsteps, const uint32_t* slot, uint32_t nkeys,
+                                                              uint32_t* out) {
+    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < (off ? n_docs : n_pad); d += gridDim.x * blockDim.x) {
+        if (!off) {
+            uint32_t o = 0xFFFFFFFFu;
+            if (d < n_docs && (!present || ((present[d >> 6] >> (d & 63)) & 1)))
+                o = table_key(starts, nsteps, slot, nkeys, f64 ? java_long(bits_dbl((uint64_t)v[d])) : v[d]);
+            out[d] = o;
+            continue;
+        }
+        uint32_t prev = 0xFFFFFFFFu;
+        for (uint64_t i = off[d]; i < off[d + 1]; ++i) {  // a doc's repeated keys once (HistogramAggregator.collect)
+            const uint32_t k = table_key(starts, nsteps, slot, nkeys, f64 ? java_long(bits_dbl((uint64_t)v[i])) : v[i]);
+            const bool dup = i > off[d] && k == prev;
+            prev = k;
+            out[i] = dup ? 0xFFFFFFFFu : k;
+        }
+    }
+}
+void launch_hist_ords_table(const int64_t* v, const uint64_t* present, const uint64_t* offsets, uint32_t n_docs, uint32_t n_pad,
+                            bool f64, const int64_t* starts, uint32_t nsteps, const uint32_t* slot, uint32_t nkeys,
+                            uint32_t* out, hipStream_t st) {
+    const uint32_t n = offsets ? n_docs : n_pad;
+    if (n == 0) return;
+    hipLaunchKernelGGL(hist_ords_table_kernel, dim3(std::min<uint32_t>(8192, (n + 255) / 256)), dim3(256), 0, st, v, present,
+                       offsets, n_docs, n_pad, f64 ? 1 : 0, starts, nsteps, slot, nkeys, out);
+}
 void launch_hist_ords_multi(const int64_t* v, const uint64_t* offsets, uint32_t n_docs, bool f64, int64_t interval,
                             int64_t offset, int64_t key0, uint32_t nkeys, uint32_t* out, hipStream_t st) {
     if (n_docs == 0) return;

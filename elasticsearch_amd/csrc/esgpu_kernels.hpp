@@ -458,6 +458,11 @@ size_t replay_hot_lds(uint32_t k, uint32_t Hh, uint32_t slot_map_n);
 void launch_replay_hot(const ReplayHotParams& p, hipStream_t s);
 void launch_comp_ords(const uint32_t* a, const uint32_t* b, uint32_t n_pad, uint32_t na, uint32_t nb, const uint32_t* amap,
                       uint32_t amap_n, uint32_t* out, hipStream_t st);
+// ... with a calendar / DST rounding: each value's step in the bucket table (starts ascending), its key slot (slot[step],
+// or the step itself when null); single-valued (offsets null: one per doc, padded docs included) or CSR
+void launch_hist_ords_table(const int64_t* v, const uint64_t* present, const uint64_t* offsets, uint32_t n_docs, uint32_t n_pad,
+                            bool f64, const int64_t* starts, uint32_t nsteps, const uint32_t* slot, uint32_t nkeys,
+                            uint32_t* out, hipStream_t st);
 // ... over a multi-valued field: one key index per value (CSR, the source's offsets), a doc's repeated keys kMissingOrd
 void launch_hist_ords_multi(const int64_t* v, const uint64_t* offsets, uint32_t n_docs, bool f64, int64_t interval,
                             int64_t offset, int64_t key0, uint32_t nkeys, uint32_t* out, hipStream_t st);

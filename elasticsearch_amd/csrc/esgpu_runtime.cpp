@@ -953,6 +953,14 @@ struct Pipeline {
     bool ord_hist = false;
     int64_t ord_interval = 1, ord_offset = 0, ord_key0 = 0;
     uint32_t ord_keys = 0;
+    // ... or a calendar / DST rounding (ord_table): the bucket table over the request's inner values (key_table: step
+    // starts, sorted keys, step -> key slot), the key index being the slot of the value's step
+    bool ord_table = false;
+    Rounding ord_rnd;
+    int64_t ot_lo = 0, ot_hi = -1;
+    std::vector<int64_t> ot_start, ot_key;
+    std::vector<uint32_t> ot_slot;
+    DevBuf d_ostart, d_oslot;
     std::shared_ptr<DevColumn> ord_col;
     int met = 0;                     // 0 none, 1 avg, 2 stats, 3 extended
     int64_t interval = 1, offset = 0;  // affine roundings: key = floor((v - offset) / interval) * interval + offset
@@ -1187,8 +1195,11 @@ static int add_pipeline(esgpu_plan* p, int root, int fspec, int outer, int inner
             } catch (const std::invalid_argument& e) {
                 throw EsError(ESGPU_ERR_INVALID, std::string(e.what()) + " for histogram aggregation [" + n.name + "]");
             }
-            require(r.affine(&pl.ord_interval, &pl.ord_offset), ESGPU_ERR_UNSUPPORTED,
-                    "a calendar or DST rounding of an inner histogram runs on the CPU path");
+            if (!r.affine(&pl.ord_interval, &pl.ord_offset)) {  // calendar units, DST zones: a bucket table
+                pl.ord_table = true;
+                pl.ord_rnd = r;
+                pl.ord_interval = 0;
+            }
         } else {
             pl.hist_spec = b;
             pl.hist_field = n.field;
@@ -2629,6 +2640,48 @@ static const DevColumn* derive_hist_ords(esgpu_plan* p, Pipeline& pl, const esgp
     require(!src->multi || pl.cards.empty(), ESGPU_ERR_UNSUPPORTED,
             "cardinality under a multi-valued inner histogram runs on the CPU path");
     const bool has = src->vmin <= src->vmax;
+    if (pl.ord_table) {  // the bucket table grows to cover every segment's values; the grid's columns follow its keys
+        if (pl.fresh) {
+            pl.ot_lo = 0;
+            pl.ot_hi = -1;
+            pl.ot_start.clear();
+            pl.ot_key.clear();
+            pl.ot_slot.clear();
+            pl.ord_keys = 0;
+        }
+        if (has && !(pl.ot_lo <= pl.ot_hi && src->vmin >= pl.ot_lo && src->vmax <= pl.ot_hi)) {
+            int64_t lo = src->vmin, hi = src->vmax;
+            if (pl.ot_lo <= pl.ot_hi) { lo = std::min(lo, pl.ot_lo); hi = std::max(hi, pl.ot_hi); }
+            std::vector<int64_t> starts, keys;
+            std::vector<uint32_t> slot;
+            require(pl.ord_rnd.key_table(lo, hi, 65536, starts, keys, slot) && keys.size() <= 65536, ESGPU_ERR_UNSUPPORTED,
+                    "an inner histogram over 65536 keys runs on the CPU path");
+            int64_t shift = 0;
+            if (!pl.ot_key.empty()) {
+                auto it = std::lower_bound(keys.begin(), keys.end(), pl.ot_key.front());
+                require(it != keys.end() && *it == pl.ot_key.front(), ESGPU_ERR_DEVICE, "inner bucket table is not a superset");
+                shift = it - keys.begin();
+            }
+            const uint32_t old = pl.ord_keys;
+            pl.ot_lo = lo;
+            pl.ot_hi = hi;
+            pl.ot_start = std::move(starts);
+            pl.ot_key = std::move(keys);
+            pl.ot_slot = std::move(slot);
+            pl.ord_keys = (uint32_t)pl.ot_key.size();
+            pl.d_ostart.alloc(p->ctx, std::max<size_t>(pl.ot_start.size(), 1) * 8);
+            HIPX(hipMemcpyAsync(pl.d_ostart.p, pl.ot_start.data(), pl.ot_start.size() * 8, hipMemcpyHostToDevice, p->stream));
+            pl.d_oslot.release();
+            if (!pl.ot_slot.empty()) {
+                pl.d_oslot.alloc(p->ctx, pl.ot_slot.size() * 4);
+                HIPX(hipMemcpyAsync(pl.d_oslot.p, pl.ot_slot.data(), pl.ot_slot.size() * 4, hipMemcpyHostToDevice, p->stream));
+            }
+            HIPX(hipStreamSynchronize(p->stream));  // (the host tables are replaced by the next widening)
+            // earlier segments of the request: their columns move to the new keys' positions
+            if (!pl.fresh && pl.allocated && (old ? (shift != 0 || pl.ord_keys != old) : pl.T != pl.ord_keys))
+                regrid_cols(p, pl, pl.ord_keys, old ? shift : 0);
+        }
+    } else {
     const int64_t kmin = has ? floor_div64(src->vmin - pl.ord_offset, pl.ord_interval) : 0;
     const int64_t kmax = has ? floor_div64(src->vmax - pl.ord_offset, pl.ord_interval) : -1;
     if (pl.fresh || pl.ord_keys == 0) {
@@ -2649,6 +2702,7 @@ static const DevColumn* derive_hist_ords(esgpu_plan* p, Pipeline& pl, const esgp
         pl.ord_key0 = nk0;
         pl.ord_keys = (uint32_t)(nk1 - nk0 + 1);
         if (pl.allocated) regrid_cols(p, pl, pl.ord_keys, shift);
+    }
     }
     if (!pl.ord_col) pl.ord_col = std::make_shared<DevColumn>();
     DevColumn& d = *pl.ord_col;
@@ -2704,6 +2758,16 @@ static const DevColumn* derive_comp_ords(esgpu_plan* p, Pipeline& pl, const esgp
 static void materialize_hist_ords(esgpu_plan* p, Pipeline& pl, const esgpu_segment* s) {
     const DevColumn* src = s->col(pl.ord_field.c_str());
     DevColumn& d = *pl.ord_col;
+    if (pl.ord_table) {  // each value's step in the bucket table, its key slot
+        const size_t nv = src->multi ? std::max<size_t>(src->n_values, 1) : (size_t)s->n_pad;
+        if (d.values.bytes < nv * 4) d.values.alloc(p->ctx, nv * 4);
+        launch_hist_ords_table((const int64_t*)wide_i64(p->ctx, src, s, p->stream), src->present.as<uint64_t>(),
+                               src->multi ? src->offsets.as<uint64_t>() : nullptr, s->max_doc, s->n_pad,
+                               src->type == ESGPU_COL_F64, pl.d_ostart.as<int64_t>(), (uint32_t)pl.ot_start.size(),
+                               pl.d_oslot.p ? pl.d_oslot.as<uint32_t>() : nullptr, pl.ord_keys, d.values.as<uint32_t>(), p->stream);
+        HIPX(hipGetLastError());
+        return;
+    }
     if (src->multi) {  // HistogramAggregator.collect: each value's key, a doc's repeated keys once (values are sorted)
         const size_t nv = std::max<size_t>(src->n_values, 1);
         if (d.values.bytes < nv * 4) d.values.alloc(p->ctx, nv * 4);
@@ -5605,7 +5669,8 @@ static Block build_hist_root(esgpu_plan* p, const Group& g) {
                     for (uint32_t t = 0; t < B0.T; ++t) {  // HistogramAggregator.buildAggregation: keys ascending
                         const int64_t c = (int64_t)B0.hc.cnt[row + t];
                         if (c == 0) continue;
-                        push_bucket(sub, (B0.ord_key0 + (int64_t)t) * B0.ord_interval + B0.ord_offset, nullptr, c);
+                        push_bucket(sub, B0.ord_table ? B0.ot_key[t] : (B0.ord_key0 + (int64_t)t) * B0.ord_interval + B0.ord_offset,
+                                    nullptr, c);
                         for (size_t gj = 0; gj < kid.grand.size(); ++gj)
                             append_leaf(p, p->pipes[kid.grand[gj].pipe], kid.grand[gj].leaf, row + t, sub.subs[gj]);
                     }

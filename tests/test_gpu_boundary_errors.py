@@ -27,7 +27,7 @@ def _plan_and_collect(engine, aggs, fields, n=100_000):
         seg.close()
 
 
-@pytest.mark.parametrize("case", ["metric_ordered_terms_under_high_cardinality_terms", "calendar_histogram_under_histogram",
+@pytest.mark.parametrize("case", ["metric_ordered_terms_under_high_cardinality_terms", "four_bucket_levels",
                                   "three_bucket_levels"])
 def test_unsupported_shapes_raise(engine, case):
     if case == "metric_ordered_terms_under_high_cardinality_terms":
@@ -35,10 +35,11 @@ def test_unsupported_shapes_raise(engine, case):
         aggs = [AB.terms("hosts").field("host").subAggregation(AB.terms("urls").field("url").order(
             Order.aggregation("rt", True)).subAggregation(AB.avg("rt").field("response_time_ms")))]
         fields = ("host", "url", "response_time_ms")
-    elif case == "calendar_histogram_under_histogram":  # the inner key index needs an affine rounding
-        aggs = [AB.histogram("b").field("bytes").interval(4096).subAggregation(
-            AB.dateHistogram("m").field("@timestamp").interval("month"))]
-        fields = ("@timestamp", "bytes")
+    elif case == "four_bucket_levels":  # (a calendar inner histogram is collected since round 6: bucket table)
+        aggs = [AB.terms("hosts").field("host").subAggregation(AB.terms("urls").field("url").subAggregation(
+            AB.dateHistogram("h").field("@timestamp").interval("1h").subAggregation(
+                AB.histogram("b").field("bytes").interval(1024))))]
+        fields = ("host", "url", "@timestamp", "bytes")
     else:
         aggs = [AB.terms("hosts").field("host").subAggregation(
             AB.dateHistogram("h").field("@timestamp").interval("1h").subAggregation(
@@ -50,8 +51,9 @@ def test_unsupported_shapes_raise(engine, case):
 
 def test_engine_usable_after_unsupported(engine):
     with pytest.raises(N.UnsupportedOnGpu):
-        _plan_and_collect(engine, [AB.histogram("b").field("bytes").interval(4096).subAggregation(
-            AB.dateHistogram("m").field("@timestamp").interval("month"))], ("@timestamp", "bytes"))
+        _plan_and_collect(engine, [AB.terms("hosts").field("host").subAggregation(
+            AB.dateHistogram("h").field("@timestamp").interval("1h").subAggregation(
+                AB.histogram("b").field("bytes").interval(1024)))], ("host", "@timestamp", "bytes"))
     aggs = [AB.terms("hosts").field("host").subAggregation(AB.stats("rt").field("response_time_ms"))]
     seg = engine.synthetic_segment(50_000, fields=("host", "response_time_ms"))
     plan = engine.plan(aggs)

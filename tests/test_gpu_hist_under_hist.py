@@ -61,12 +61,62 @@ def test_inner_date_histogram_fixed_zone_and_double_field(engine):
     _both(engine, aggs, exact=False)
 
 
-def test_inner_calendar_rounding_refused(engine):
-    """a DST zone or a calendar unit is not affine: the plan refuses it (the plugin keeps the stock aggregator)"""
-    aggs = [AB.histogram("b").field("bytes").interval(100000).subAggregation(
-        AB.dateHistogram("m").field("@timestamp").interval("month"))]
-    with pytest.raises(N.UnsupportedOnGpu):
-        engine.plan(aggs)
+@pytest.mark.parametrize("interval,zone,shift_days", [("month", None, 0), ("week", "Europe/Berlin", 50),
+                                                      ("1h", "America/New_York", 55), ("quarter", "+05:30", 15),
+                                                      ("day", "Australia/Lord_Howe", 20), ("1h", "Europe/Berlin", 50)])
+def test_inner_calendar_and_dst_rounding(engine, interval, zone, shift_days):
+    """A calendar unit or a DST zone is not affine: the inner date_histogram's key index comes from a bucket table over
+    the request's values (Rounding.key_table: step starts, sorted keys, a DST fall-back's repeated local hour mapped to
+    its first bucket), each doc's step found by binary search -- against the oracle, with min_doc_count 0 and stats;
+    the timestamps shifted so the month spans the zone's transition (Berlin and New York fall back in late October /
+    early November 2015, Lord Howe moves 30 min forward on October 4)."""
+    dh = AB.dateHistogram("m").field("@timestamp").interval(interval).minDocCount(0)
+    if zone:
+        dh.timeZone(zone)
+    aggs = [AB.histogram("b").field("bytes").interval(250000).subAggregation(dh.subAggregation(
+        AB.stats("s").field("response_time_ms")))]
+    n, shards = 200_000, 2
+    data = []
+    for sh in range(shards):
+        cols = synthetic_columns(FIELDS, n, shard=sh)
+        cols["@timestamp"]["values"] = cols["@timestamp"]["values"] + shift_days * 86_400_000
+        data.append((cols, n))
+    want = O.run(data, aggs, number_of_shards=shards)
+    plan = engine.plan(aggs, number_of_shards=shards)
+    results = []
+    for sh, (cols, _) in enumerate(data):
+        seg = engine.upload_segment(cols, n)
+        plan.reset()
+        plan.collect(seg)
+        r = plan.build()
+        assert_same(r.to_dict(), want["shards"][sh], f"shard{sh}")
+        results.append(r)
+        seg.close()
+    assert_same(reduce(results).to_dict(), want["reduced"], "reduced")
+    plan.close()
+
+
+def test_inner_calendar_rounding_two_segments_widen_table(engine):
+    """A later segment whose timestamps lie before and after the first's: the inner bucket table grows on both sides and
+    the grid's columns move to the new keys' positions."""
+    n = 150_000
+    c0 = synthetic_columns(FIELDS, n, shard=0)
+    c1 = synthetic_columns(FIELDS, n, shard=1)
+    c0["@timestamp"]["values"] = c0["@timestamp"]["values"] + 40 * 86_400_000  # a later month range
+    c1["@timestamp"]["values"] = c1["@timestamp"]["values"] - 20 * 86_400_000
+    aggs = [AB.histogram("b").field("bytes").interval(500000).subAggregation(
+        AB.dateHistogram("m").field("@timestamp").interval("month").timeZone("Europe/Berlin").subAggregation(
+            AB.avg("a").field("response_time_ms")))]
+    allc = {f: dict(c0[f], values=np.concatenate([c0[f]["values"], c1[f]["values"]])) for f in FIELDS}
+    want = O.run([(allc, 2 * n)], aggs)
+    plan = engine.plan(aggs)
+    segs = [engine.upload_segment(c, n) for c in (c0, c1)]
+    for sg in segs:
+        plan.collect(sg)
+    assert_same(plan.build().to_dict(), want["shards"][0], "two segments")
+    plan.close()
+    for sg in segs:
+        sg.close()
 
 
 def test_inner_field_missing_in_a_segment(engine):
