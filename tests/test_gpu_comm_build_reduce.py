@@ -56,6 +56,9 @@ SHAPES = {
                              NS_FIELDS, None, False),
     # config 3: 10M url ordinals, the GPU top-k's keys made into records on the device
     "config3_urls": (lambda: [AB.terms("urls").field("url").size(10)], ("url",), None, True),
+    # ... under a range filter: each shard's hot slots from the folded bitset, the scatter form deferred to the top-k
+    "config3_urls_filtered": (lambda: [AB.terms("urls").field("url").size(10)], ("url", "bytes"),
+                              [QB.rangeQuery("bytes").lt(800000)], True),
     "urls_count_asc_errors": (lambda: [AB.terms("urls").field("url").size(4).shardSize(9).order(ea.Order.count(True))
                                        .showTermDocCountError(True)], ("url",), None, True),
     # plain terms over 1,000 hosts: the co-located device selection (count and term orders)
