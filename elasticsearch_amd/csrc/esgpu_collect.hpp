@@ -1883,9 +1883,13 @@ __global__ __launch_bounds__(256) void zone_keys_kernel(CollectParams P, int64_t
         const uint64_t d0 = (uint64_t)b * kBlockDocs;
         if (kmn == kmx && d0 < P.n_docs) ud = min((uint64_t)kBlockDocs, (uint64_t)P.n_docs - d0);
     }
-    if (udocs) {
+    if (udocs) {  // the workgroup's single-key docs into its own word (no shared counter: one atomic per wave on one
+                  // address had made this kernel 26 us at 1B docs)
+        __shared__ unsigned long long wsum[4];
         for (int o = 32; o > 0; o >>= 1) ud += __shfl_xor(ud, o, 64);
-        if ((threadIdx.x & 63) == 0 && ud) atomicAdd(udocs, ud);
+        if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = ud;
+        __syncthreads();
+        if (threadIdx.x == 0) udocs[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
     }
 }
 

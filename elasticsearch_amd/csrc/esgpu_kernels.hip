@@ -1720,15 +1720,24 @@ __global__ __launch_bounds__(256) void fill_multi_kernel(FillList L) {
     for (int k = 0; k < L.count; ++k) {
         unsigned long long* p = L.p[k];
         const unsigned long long v = L.v[k];
-        for (size_t i = g; i < L.n[k]; i += stride) p[i] = v;
+        const size_t n = L.n[k];
+        if (((uintptr_t)p & 15) == 0) {  // 16-byte stores (the grid arrays are 256-byte aligned), then the odd tail word
+            const uint4 w = make_uint4((uint32_t)v, (uint32_t)(v >> 32), (uint32_t)v, (uint32_t)(v >> 32));
+            for (size_t i = g; i < n / 2; i += stride) reinterpret_cast<uint4*>(p)[i] = w;
+            if (g == 0 && (n & 1)) p[n - 1] = v;
+        } else {
+            for (size_t i = g; i < n; i += stride) p[i] = v;
+        }
     }
 }
 void launch_fill_multi(const FillList& l, hipStream_t st) {
     uint64_t total = 0;
     for (int k = 0; k < l.count; ++k) total += l.n[k];
     if (total == 0) return;
-    size_t grid = (total / (uint64_t)l.count + 255) / 256;
-    if (grid > 4096) grid = 4096;
+    // a few workgroups per CU looping over the spans (one thread per pair of words, per span, had spent more on
+    // dispatching ~2,800 workgroups than on the stores: 13 us for the north star's 29 MB)
+    size_t grid = (total / (uint64_t)l.count / 2 + 255) / 256;
+    if (grid > 1024) grid = 1024;
     if (grid == 0) grid = 1;
     hipLaunchKernelGGL(fill_multi_kernel, dim3((uint32_t)grid), dim3(256), 0, st, l);
 }

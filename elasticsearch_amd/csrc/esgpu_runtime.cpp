@@ -1070,6 +1070,7 @@ struct Group {
 };
 
 constexpr uint32_t kZuSlots = 64;  // zone-skip counters per collect call (esgpu_plan.s_zu)
+constexpr uint32_t kZuMaxWG = 2048;  // ... each one word per zone-keys workgroup (a segment has < 2^19 blocks)
 
 struct esgpu_plan {
     esgpu_ctx* ctx = nullptr;
@@ -1115,6 +1116,7 @@ struct esgpu_plan {
     PinnedBuf zu_host;
     uint32_t zu_n = 0;
     uint8_t zu_w[kZuSlots] = {};  // ... and the timestamp bytes per doc of each launch (2: block deltas, 4: 32-bit deltas)
+    uint32_t zu_g[kZuSlots] = {};  // ... and its zone-keys workgroups (words written)
     DevBuf d_claim;            // collect kernel's chunk-claim counter pair (zeroed once; every launch leaves it zero)
     Scratch s_hcur, s_hused, s_hslab;  // hot/cold counting: overflow cursors, static-region fills, hot slabs
     PinnedBuf h_hcerr;         // hot/cold counting: capacity-violation word (written by the scatter kernel)
@@ -3496,9 +3498,9 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
     if ((P.lds_mode && P.windowed) || raw_keys) {
         P.zkey = (const int64_t*)p->s_zkey.ensure(p->ctx, (size_t)std::max(P.n_blocks, 1u) * 16);
         unsigned long long* ud = nullptr;
-        if (raw_keys && p->zu_n < kZuSlots) {
-            ud = (unsigned long long*)p->s_zu.ensure(p->ctx, kZuSlots * 8) + p->zu_n;
-            HIPX(hipMemsetAsync(ud, 0, 8, p->stream));
+        if (raw_keys && p->zu_n < kZuSlots && (P.n_blocks + 255) / 256 <= kZuMaxWG) {
+            ud = (unsigned long long*)p->s_zu.ensure(p->ctx, (size_t)kZuSlots * kZuMaxWG * 8) + (size_t)p->zu_n * kZuMaxWG;
+            p->zu_g[p->zu_n] = (P.n_blocks + 255) / 256;  // (every workgroup writes its word: no zeroing)
         }
         launch_zone_keys(P, const_cast<int64_t*>(P.zkey), p->stream, ud);
         HIPX(hipGetLastError());
@@ -4044,12 +4046,18 @@ extern "C" int esgpu_plan_last_collect_stats(const esgpu_plan* cp, double* kerne
             }
             p->last_ms = total;
             if (p->zu_n) {  // the timestamps of single-key zone blocks were not read
-                p->zu_host.ensure(kZuSlots * 8);
-                launch_copy_u64(p->s_zu.as<unsigned long long>(), (unsigned long long*)p->zu_host.dev(), p->zu_n, p->stream);
+                p->zu_host.ensure((size_t)kZuSlots * kZuMaxWG * 8);
+                for (uint32_t i = 0; i < p->zu_n; ++i)
+                    launch_copy_u64(p->s_zu.as<unsigned long long>() + (size_t)i * kZuMaxWG,
+                                    (unsigned long long*)p->zu_host.dev() + (size_t)i * kZuMaxWG, p->zu_g[i], p->stream);
                 HIPX(hipGetLastError());
                 HIPX(hipStreamSynchronize(p->stream));
                 uint64_t ud = 0;
-                for (uint32_t i = 0; i < p->zu_n; ++i) ud += ((const uint64_t*)p->zu_host.p)[i] * p->zu_w[i];
+                for (uint32_t i = 0; i < p->zu_n; ++i) {
+                    uint64_t w = 0;
+                    for (uint32_t g = 0; g < p->zu_g[i]; ++g) w += ((const uint64_t*)p->zu_host.p)[(size_t)i * kZuMaxWG + g];
+                    ud += w * p->zu_w[i];
+                }
                 p->last_bytes -= std::min<uint64_t>(p->last_bytes, ud);
                 p->zu_n = 0;
             }
