@@ -51,7 +51,7 @@ constexpr uint32_t kGroup = kGroupBlocks;  // blocks per multi-pass group (esgpu
 struct Doc4 {
     // raw-loaded packed-cell kernels (kRawPI): the loads' words as they arrive, unpacked only when the docs are processed
     // (a conversion right after the load would wait for it there, a full memory latency per buffer reload)
-    uint32_t raw[10];
+    uint32_t raw[11];  // ([10]: the block-delta key column's high bytes, 4 docs)
     uint64_t racc;
     uint32_t doc0;
     // block-delta kernels (VK bit 8192): the grid key every doc of this buffer's zone block has (its zone-map range
@@ -170,23 +170,26 @@ constexpr bool kRawPI = MET > 0 && (VK & 64) != 0 && (VK & 16) != 0 && (VK & 256
 // minimum of its run of 2^kB16Shift docs (one 8-byte word per run, the same for all 4 docs of a thread)
 constexpr uint32_t kNoUKey = 0xFFFFFFFFu, kOutUKey = 0xFFFFFFFEu;  // per-doc keys / one key outside the grid
 template <int VK>
-__device__ __forceinline__ void load_keys_raw(const CollectParams& P, uint32_t doc0, uint32_t (&raw)[10], uint32_t uk) {
+__device__ __forceinline__ void load_keys_raw(const CollectParams& P, uint32_t doc0, uint32_t (&raw)[11], uint32_t uk) {
     if constexpr ((VK & 8192) != 0) {
         // a block whose docs all round to one key reads no timestamp: every lane loads the column's first word (one
         // cache line per wave, in place of a branch around the load -- a load under a branch makes the compiler wait
         // for the other buffers' loads)
 #if ESGPU_B16_NOLOAD  // timing experiment only (wrong keys in multi-key blocks): no timestamp or base loads at all
-        raw[2] = doc0; raw[3] = doc0; raw[4] = 0; raw[5] = 0;
+        raw[2] = doc0; raw[3] = doc0; raw[4] = 0; raw[5] = 0; raw[10] = 0;
         return;
 #endif
 #if ESGPU_B16_BRANCH  // (A/B) the single-key blocks' loads skipped under a wave-uniform branch
         if (uk != kNoUKey) {
-            raw[2] = 0; raw[3] = 0; raw[4] = 0; raw[5] = 0;
+            raw[2] = 0; raw[3] = 0; raw[4] = 0; raw[5] = 0; raw[10] = 0;
             return;
         }
 #endif
         const u32x2_t t = load8(P.hv16 + (uk == kNoUKey ? doc0 : 0u));
         raw[2] = t.x; raw[3] = t.y;
+        // bits 16..23 of the deltas (24-bit runs): the high-byte plane, or -- for a column whose every run spans < 2^16 --
+        // the column's first word for all lanes (hv8_mask 0; the bytes are masked off by hv8_and = 0)
+        raw[10] = *reinterpret_cast<const uint32_t*>(P.hv8 + (doc0 & P.hv8_mask));
 #if ESGPU_B16_SCALAR
         // a wave's 256 docs lie in one run: its base is a scalar load
         const int64_t b = P.hv16_base[__builtin_amdgcn_readfirstlane(doc0 >> kB16Shift)];
@@ -207,11 +210,14 @@ __device__ __forceinline__ void load_keys_raw(const CollectParams& P, uint32_t d
     }
 }
 template <int VK>
-__device__ __forceinline__ void unpack_keys_raw(const CollectParams& P, const uint32_t (&raw)[10], int64_t (&hv)[4]) {
+__device__ __forceinline__ void unpack_keys_raw(const CollectParams& P, const uint32_t (&raw)[11], int64_t (&hv)[4]) {
     if constexpr ((VK & 8192) != 0) {
         const int64_t b = (int64_t)join64(raw[4], raw[5]);
-        hv[0] = b + (int64_t)(raw[2] & 0xFFFFu); hv[1] = b + (int64_t)(raw[2] >> 16);
-        hv[2] = b + (int64_t)(raw[3] & 0xFFFFu); hv[3] = b + (int64_t)(raw[3] >> 16);
+        const uint32_t h = raw[10] & (P.hv8_and * 0x01010101u);
+        hv[0] = b + (int64_t)((raw[2] & 0xFFFFu) | ((h & 0xFFu) << 16));
+        hv[1] = b + (int64_t)((raw[2] >> 16) | ((h & 0xFF00u) << 8));
+        hv[2] = b + (int64_t)((raw[3] & 0xFFFFu) | ((h >> 16 & 0xFFu) << 16));
+        hv[3] = b + (int64_t)((raw[3] >> 16) | ((h >> 24) << 16));
     } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) hv[j] = P.hv_base + (int64_t)raw[2 + j];
@@ -376,12 +382,14 @@ __device__ __forceinline__ void load_docs8(const CollectParams& P, uint32_t doc0
             skip = uk != kNoUKey;  // a single-key block: no timestamp is read (wave-uniform branch)
 #endif
             if (skip) {
-                d.a.raw[2] = d.a.raw[3] = d.a.raw[4] = d.a.raw[5] = 0u;
-                d.b.raw[2] = d.b.raw[3] = d.b.raw[4] = d.b.raw[5] = 0u;
+                d.a.raw[2] = d.a.raw[3] = d.a.raw[4] = d.a.raw[5] = d.a.raw[10] = 0u;
+                d.b.raw[2] = d.b.raw[3] = d.b.raw[4] = d.b.raw[5] = d.b.raw[10] = 0u;
             } else {
                 const u32x4_t t = load16(P.hv16 + (uk == kNoUKey ? doc0 : 0u));
                 const u32x2_t bs = load8(P.hv16_base + (doc0 >> kB16Shift));  // (8 docs never straddle a run)
+                const u32x2_t h = load8(P.hv8 + (doc0 & P.hv8_mask));          // (see load_keys_raw)
                 d.a.raw[2] = t.x; d.a.raw[3] = t.y; d.b.raw[2] = t.z; d.b.raw[3] = t.w;
+                d.a.raw[10] = h.x; d.b.raw[10] = h.y;
                 d.a.raw[4] = bs.x; d.a.raw[5] = bs.y; d.b.raw[4] = bs.x; d.b.raw[5] = bs.y;
             }
         } else {
@@ -655,8 +663,14 @@ __device__ __forceinline__ void run_flush(const CollectParams& P, const Acc& a, 
 #endif
 // VK bit 4096 (with 2048): time-sorted data (a block's keys span less than one interval: CollectParams.runs1) -- one integer
 // run per thread, a third of the registers and no run lookup (config 2 at 1B docs: 1.46 -> 1.12 ms, r5d)
+// Integer runs over roughly time-ordered data (VK bit 2048 without 4096): the docs go to four window accumulators per
+// thread instead of three runs (ESGPU_WIN4=0: the runs, for A/B) -- see win_add
+#ifndef ESGPU_WIN4
+#define ESGPU_WIN4 1
+#endif
+template <int MET, int VK> constexpr bool kWin4 = ESGPU_WIN4 != 0 && MET > 0 && (VK & 2048) != 0 && (VK & 4096) == 0;
 template <int MET, int VK = 0> constexpr int runs_for() {
-    return MET == 0 ? 1 : (VK & 4096) != 0 ? 1 : (VK & 2048) != 0 ? ESGPU_INT_RUNS_NR : ESGPU_RUNS;
+    return MET == 0 ? 1 : (VK & 4096) != 0 ? 1 : kWin4<MET, VK> ? 1 : (VK & 2048) != 0 ? ESGPU_INT_RUNS_NR : ESGPU_RUNS;
 }
 #ifndef ESGPU_PI_NHOT  // hot ordinals with register runs in the packed-cell kernels (CollectParams.hot_t, up to 4)
 #define ESGPU_PI_NHOT 1
@@ -671,13 +685,27 @@ struct Runs {
     // caused (ESGPU_PI_HOTU in the uniform-key path, ESGPU_PI_HOT per doc)
     uint32_t hslot, hlo[kNHot], hhi[kNHot];
     uint32_t hcnt[kNHot], hsum[kNHot];  // docs and their delta sum (a lane holds < 65,536 docs of a workgroup range)
+    // window accumulators (kWin4): key slots wb .. wb + 3 -- per slot the docs, delta sum and squared-delta sum, and the
+    // delta extrema as 16-bit pairs (slots 0/1 in wmn[0] / wmx[0], 2/3 in [1]); wb = kWinEmpty: none
+    uint32_t wb, wc[4], ws[4], wmn[2], wmx[2];
+    unsigned long long wq[4];
 };
+constexpr uint32_t kWinEmpty = 0x80000000u;  // (slots are < 2^31: slot - kWinEmpty is never a window offset)
 template <int NR>
 __device__ __forceinline__ void runs_reset(Runs<NR>& R) {
 #pragma unroll
     for (int k = 0; k < NR; ++k) run_reset(R.r[k]);
     R.victim = 0;
     R.hslot = ~0u;
+    R.wb = kWinEmpty;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        R.wc[k] = 0u;
+        R.ws[k] = 0u;
+        R.wq[k] = 0ull;
+    }
+    R.wmn[0] = R.wmn[1] = ~0u;
+    R.wmx[0] = R.wmx[1] = 0u;
 #pragma unroll
     for (int k = 0; k < kNHot; ++k) {
         R.hlo[k] = ~0u;
@@ -719,8 +747,36 @@ __device__ __forceinline__ void pi_hot_flush(const CollectParams& P, const Acc& 
     }
     R.hslot = ~0u;
 }
-template <int MET, int MS, int NR, bool INT = false>
+// the window accumulators into their LDS cells (each slot with docs as one integer run), then emptied
+template <int MET, int MS, int NR>
+__device__ __forceinline__ void win_flush(const CollectParams& P, const Acc& a, Runs<NR>& R) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (R.wc[k]) {
+            Run r;
+            run_reset(r);
+            r.slot = R.wb + (uint32_t)k;
+            r.cnt = R.wc[k];
+            r.isd = R.ws[k];
+            r.isq = R.wq[k];
+            r.imn = (R.wmn[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+            r.imx = (R.wmx[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+            run_flush_i<MET, MS>(P, a, r);
+        }
+        R.wc[k] = 0u;
+        R.ws[k] = 0u;
+        R.wq[k] = 0ull;
+    }
+    R.wmn[0] = R.wmn[1] = ~0u;
+    R.wmx[0] = R.wmx[1] = 0u;
+    R.wb = kWinEmpty;
+}
+template <int MET, int MS, int NR, bool INT = false, bool WIN = false>
 __device__ __forceinline__ void runs_flush(const CollectParams& P, const Acc& a, Runs<NR>& R) {
+    if constexpr (WIN) {
+        win_flush<MET, MS>(P, a, R);
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
         if constexpr (INT) run_flush_i<MET, MS>(P, a, R.r[k]);
@@ -783,6 +839,43 @@ __device__ __forceinline__ void runs_add_pk(const CollectParams& P, const Acc& a
         r.pmx = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2_t, r.pmx),
                                                                         __builtin_elementwise_max(x0, x1)));
     }
+}
+// one doc (v: it passes and has a key) into window slot o = slot - wb (o < 4 when v): the slot's 0/1 weight e multiplies
+// the delta into each sum (v_mad), so a doc costs ~30 VALU where the three runs' hit search and predicated updates took
+// ~110 (config 2 at ±1 h, SQ counters r6ac: 446 VALU per wave per 256 docs)
+template <int MET, int NR>
+__device__ __forceinline__ void win_add(Runs<NR>& R, uint32_t o, uint32_t x, bool v) {
+    const uint32_t oh = v ? 1u << ((o & 3u) << 3) : 0u;  // one-hot byte of the slot
+    const uint32_t xx = x * x;                              // (x < 2^16)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t e = (oh >> (8 * k)) & 0xFFu;
+        R.wc[k] += e;
+        R.ws[k] += x * e;
+        if (MET >= 3) R.wq[k] += (unsigned long long)xx * e;
+    }
+    if (MET >= 2) {
+        const uint32_t sh = (o & 1u) << 4;
+        const uint32_t xm = (x << sh) | (0xFFFF0000u >> sh), xM = x << sh;  // the other half: min / max identities
+        const bool h0 = v && o < 2u, h1 = v && o >= 2u;
+        const u16x2_t m = __builtin_bit_cast(u16x2_t, xm), M = __builtin_bit_cast(u16x2_t, xM);
+        const uint32_t n0 = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2_t, R.wmn[0]), m));
+        const uint32_t n1 = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2_t, R.wmn[1]), m));
+        const uint32_t x0 = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2_t, R.wmx[0]), M));
+        const uint32_t x1 = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2_t, R.wmx[1]), M));
+        R.wmn[0] = h0 ? n0 : R.wmn[0];
+        R.wmn[1] = h1 ? n1 : R.wmn[1];
+        R.wmx[0] = h0 ? x0 : R.wmx[0];
+        R.wmx[1] = h1 ? x1 : R.wmx[1];
+    }
+}
+// a doc whose slot is outside the window: flush it and re-base -- new keys above put the slot at the top (the keys of
+// roughly time-ordered data drift upwards), below at the bottom, a first doc one above the bottom
+template <int MET, int MS, int NR>
+__device__ __forceinline__ void win_rebase(const CollectParams& P, const Acc& a, Runs<NR>& R, uint32_t slot) {
+    const uint32_t old = R.wb;
+    win_flush<MET, MS>(P, a, R);
+    R.wb = old == kWinEmpty ? (slot ? slot - 1u : 0u) : slot > old ? (slot >= 3u ? slot - 3u : 0u) : slot;
 }
 template <int MET, int MS, int NR>
 __device__ __forceinline__ void runs_add(const CollectParams& P, const Acc& a, Runs<NR>& R, uint32_t slot, bool mpres, double x) {
@@ -917,7 +1010,7 @@ __device__ __forceinline__ void unpack_docs(const CollectParams& P, Doc4& d) {
 template <bool ORD, bool HIST, int MET, bool LDS, bool KT, int MS, bool HORD = false, int VK = 0>
 __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, const Doc4& d_in, uint32_t T, int64_t base,
                                          uint32_t win0, Runs<runs_for<MET, VK>()>& run, uint32_t mw = 0, bool outer = true) {
-    if constexpr (LDS && kIntRuns<ORD, MET, VK> && kUKeyK<ORD, HIST, MET, VK> && runs_for<MET, VK>() == 1) {
+    if constexpr (LDS && kIntRuns<ORD, MET, VK> && kUKeyK<ORD, HIST, MET, VK> && (VK & 4096) != 0) {
         // a single-key zone block's whole quad (every doc but the segment's last few): the packed run update, no unpack
         if (d_in.ukey != kNoUKey && P.dot16 && d_in.doc0 + 4 <= P.n_docs) {
             const uint32_t k = d_in.ukey, sl = k - win0;  // (kOutUKey: outside the grid, no doc counts)
@@ -1016,6 +1109,28 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
             }
             return;
         }
+    }
+    if constexpr (LDS && kIntRuns<ORD, MET, VK> && kWin4<MET, VK>) {
+        uint32_t vm = 0;
+        bool miss = false;
+#pragma unroll
+        for (int j = 0; j < kVec; ++j) {
+            const bool v = ((d.ok >> j) & 1) && hv_ok[j];
+            vm |= (uint32_t)v << j;
+            miss = miss || (v && slot[j] - run.wb >= 4u);
+        }
+        if (miss) {  // (rare: a lane's keys left its window) one doc at a time, re-basing where needed
+#pragma unroll
+            for (int j = 0; j < kVec; ++j) {
+                if (!((vm >> j) & 1)) continue;
+                if (slot[j] - run.wb >= 4u) win_rebase<MET, MS>(P, a, run, slot[j]);
+                win_add<MET>(run, slot[j] - run.wb, d.mvd[j], true);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < kVec; ++j) win_add<MET>(run, slot[j] - run.wb, d.mvd[j], (vm >> j) & 1);
+        }
+        return;
     }
     if constexpr (LDS && kIntRuns<ORD, MET, VK>) {
         // integer runs: a thread's 4 docs that all pass and share one slot (time-sorted data: nearly always) are combined
@@ -1718,7 +1833,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
     uint32_t pass = 0, npass = 1;                        // npass > 1: a multi-pass group
     auto slide_to = [&](uint32_t k0) {
         if (dirty) {
-            if (!ORD) runs_flush<MET, kMS, runs_for<MET, VKL>(), kIntRuns<ORD, MET, VKL>>(P, s, run);
+            if (!ORD) runs_flush<MET, kMS, runs_for<MET, VKL>(), kIntRuns<ORD, MET, VKL>, kWin4<MET, VKL>>(P, s, run);
             if constexpr (PI && (ESGPU_PI_HOT != 0 || ESGPU_PI_HOTU != 0)) pi_hot_flush<MET>(P, s, run, T);
             if constexpr (PI) flush_window_pi<MET, WGS>(P, s, T, W, win0, ncp);
             else flush_window<MET, kMS, WGS>(P, s, T, W, win0, ncp);
@@ -1847,7 +1962,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
 #define ESGPU_FLUSH_DIAG 0
 #endif
     if (P.lds_mode && (dirty || !(HIST && P.windowed)) && !ESGPU_FLUSH_DIAG) {
-        if (!ORD) runs_flush<MET, kMS, runs_for<MET, VKL>(), kIntRuns<ORD, MET, VKL>>(P, s, run);
+        if (!ORD) runs_flush<MET, kMS, runs_for<MET, VKL>(), kIntRuns<ORD, MET, VKL>, kWin4<MET, VKL>>(P, s, run);
         if constexpr (PI && (ESGPU_PI_HOT != 0 || ESGPU_PI_HOTU != 0)) pi_hot_flush<MET>(P, s, run, T);
         if constexpr (PI) flush_window_pi<MET, WGS>(P, s, T, W, win0, ncp);
         else flush_window<MET, kMS, WGS>(P, s, T, W, win0, ncp);

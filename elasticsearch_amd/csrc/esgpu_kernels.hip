@@ -1589,7 +1589,8 @@ void launch_expand_d16(const uint16_t* d, uint32_t n, int64_t base, int64_t* out
 
 // one workgroup per run of kB16Docs docs: the run's minimum over its live docs, and every doc's delta over it
 __global__ __launch_bounds__(256) void block_delta16_kernel(const int64_t* __restrict__ v, uint32_t n_docs, uint16_t* __restrict__ d,
-                                                            int64_t* __restrict__ base, unsigned int* __restrict__ bad) {
+                                                            uint8_t* __restrict__ hi, int64_t* __restrict__ base,
+                                                            unsigned int* __restrict__ bad) {
     __shared__ long long smn[4], smx[4];
     const uint32_t c0 = blockIdx.x << kB16Shift;
     long long mn = 0x7FFFFFFFFFFFFFFFll, mx = -0x7FFFFFFFFFFFFFFFll - 1;
@@ -1610,24 +1611,32 @@ __global__ __launch_bounds__(256) void block_delta16_kernel(const int64_t* __res
     const bool any = c0 < n_docs;
     if (threadIdx.x == 0) {
         base[blockIdx.x] = any ? mn : 0;
-        if (any && (unsigned long long)mx - (unsigned long long)mn >= 65536ull) atomicOr(bad, 1u);
+        const unsigned long long span = (unsigned long long)mx - (unsigned long long)mn;
+        if (any && span >= 65536ull) atomicOr(bad, span >= (1ull << 24) ? 3u : 1u);
     }
-    for (uint32_t i = c0 + threadIdx.x; i < c0 + kB16Docs; i += 256)
-        d[i] = i < n_docs ? (uint16_t)((unsigned long long)v[i] - (unsigned long long)mn) : (uint16_t)0;
+    for (uint32_t i = c0 + threadIdx.x; i < c0 + kB16Docs; i += 256) {
+        const uint32_t x = i < n_docs ? (uint32_t)((unsigned long long)v[i] - (unsigned long long)mn) : 0u;
+        d[i] = (uint16_t)x;
+        if (hi) hi[i] = (uint8_t)(x >> 16);
+    }
 }
-void launch_block_delta16(const int64_t* v, uint32_t n_docs, uint32_t n_pad, uint16_t* d, int64_t* base, unsigned int* bad,
-                          hipStream_t st) {
+void launch_block_delta16(const int64_t* v, uint32_t n_docs, uint32_t n_pad, uint16_t* d, uint8_t* hi, int64_t* base,
+                          unsigned int* bad, hipStream_t st) {
     const uint32_t runs = n_pad >> kB16Shift;
-    if (runs) hipLaunchKernelGGL(block_delta16_kernel, dim3(runs), dim3(256), 0, st, v, n_docs, d, base, bad);
+    if (runs) hipLaunchKernelGGL(block_delta16_kernel, dim3(runs), dim3(256), 0, st, v, n_docs, d, hi, base, bad);
 }
-__global__ __launch_bounds__(256) void expand_b16_kernel(const uint16_t* __restrict__ d, const int64_t* __restrict__ base,
-                                                         uint32_t n_docs, uint32_t n, int64_t* __restrict__ out) {
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
-        out[i] = i < n_docs ? (int64_t)((uint64_t)base[i >> kB16Shift] + (uint64_t)d[i]) : 0;  // the upload pads with 0
+__global__ __launch_bounds__(256) void expand_b16_kernel(const uint16_t* __restrict__ d, const uint8_t* __restrict__ hi,
+                                                         const int64_t* __restrict__ base, uint32_t n_docs, uint32_t n,
+                                                         int64_t* __restrict__ out) {
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const uint64_t x = (uint64_t)d[i] | (hi ? (uint64_t)hi[i] << 16 : 0ull);
+        out[i] = i < n_docs ? (int64_t)((uint64_t)base[i >> kB16Shift] + x) : 0;  // the upload pads with 0
+    }
 }
-void launch_expand_b16(const uint16_t* d, const int64_t* base, uint32_t n_docs, uint32_t n_pad, int64_t* out, hipStream_t st) {
+void launch_expand_b16(const uint16_t* d, const uint8_t* hi, const int64_t* base, uint32_t n_docs, uint32_t n_pad, int64_t* out,
+                       hipStream_t st) {
     if (n_pad) hipLaunchKernelGGL(expand_b16_kernel, dim3(std::min<uint32_t>((n_pad + 255) / 256, 8192)), dim3(256), 0, st,
-                                  d, base, n_docs, n_pad, out);
+                                  d, hi, base, n_docs, n_pad, out);
 }
 
 __global__ __launch_bounds__(256) void dd_fold_kernel(double* __restrict__ hi, double* __restrict__ lo, size_t n) {

@@ -71,6 +71,10 @@ struct CollectParams {
     // 2^kB16Shift docs spans < 2^16, as the run's minimum (hv16_base) plus a 16-bit delta per doc -- 2 B per timestamp
     const uint16_t* hv16;
     const int64_t* hv16_base;
+    // ... runs spanning < 2^24 (roughly time-ordered data): bits 16..23 of each delta in a byte plane (hv8, hv8_mask
+    // ~0, hv8_and 0xFF); a column of 16-bit runs has no plane: hv8 = any readable word, hv8_mask = hv8_and = 0
+    const uint8_t* hv8;
+    uint32_t hv8_mask, hv8_and;
     // histogram under histogram, fused (loader VK bit 8): the terms dimension is the inner histogram's key index,
     // derived from its i64 / f64 column as t = (v - ord_base) / ord_div when 0 <= v - ord_base < ord_span (a 32-bit
     // magic division; ord_span = keys x interval < 2^32), else missing -- no materialised ordinal column
@@ -477,12 +481,15 @@ void launch_gather_rows(const GatherParams& p, hipStream_t s);
 // a long column's upload-width values rebuilt from its compact deltas (value = base + delta)
 void launch_expand_d32(const uint32_t* d, uint32_t n, int64_t base, int64_t* out, hipStream_t s);
 void launch_expand_d16(const uint16_t* d, uint32_t n, int64_t base, int64_t* out, hipStream_t s);
-// block-delta columns (CollectParams.hv16): runs of kB16Docs docs, each the run's minimum plus 16-bit deltas.  The build
-// sets *bad when a run spans 2^16 or more (the caller then keeps the 32-bit deltas); docs >= n_docs get delta 0
+// block-delta columns (CollectParams.hv16): runs of kB16Docs docs, each the run's minimum plus 16-bit deltas, and with a
+// high-byte plane (hi, may be null) bits 16..23 of each delta.  The build ORs into *bad 1 when a run spans 2^16 or more
+// (the plane is needed) and 2 when one spans 2^24 or more (the caller then keeps the 32-bit deltas); docs >= n_docs get
+// delta 0
 constexpr uint32_t kB16Shift = 11, kB16Docs = 1u << kB16Shift;
-void launch_block_delta16(const int64_t* v, uint32_t n_docs, uint32_t n_pad, uint16_t* d, int64_t* base, unsigned int* bad,
-                          hipStream_t st);
-void launch_expand_b16(const uint16_t* d, const int64_t* base, uint32_t n_docs, uint32_t n_pad, int64_t* out, hipStream_t st);
+void launch_block_delta16(const int64_t* v, uint32_t n_docs, uint32_t n_pad, uint16_t* d, uint8_t* hi, int64_t* base,
+                          unsigned int* bad, hipStream_t st);
+void launch_expand_b16(const uint16_t* d, const uint8_t* hi, const int64_t* base, uint32_t n_docs, uint32_t n_pad, int64_t* out,
+                       hipStream_t st);
 // g_sum / g_sq += their compensated low parts, which are cleared (after every collect launch that used them)
 void launch_dd_fold(double* hi, double* lo, size_t n, hipStream_t s);
 void launch_fill_u64(unsigned long long* p, size_t n, unsigned long long v, hipStream_t s);

@@ -317,8 +317,10 @@ struct DevColumn {
     // the ords() buffer it was made from -- and a long column's values as 32-bit deltas over vmin while vmax - vmin < 2^32
     DevBuf ord16, d32, d16;  // d16: the same deltas in 16 bits while vmax - vmin < 2^16 (ensure_d16)
     // block deltas of a dense key column (ensure_b16): per run of kB16Docs docs its minimum (b16_base) and a 16-bit delta
-    // per doc, when every run spans < 2^16 -- time-sorted timestamps at any density above ~1 doc per 32 ms
-    DevBuf b16, b16_base;
+    // per doc, when every run spans < 2^16 -- time-sorted timestamps at any density above ~1 doc per 32 ms -- and, when
+    // some run spans 2^16 or more but none 2^24 (roughly time-ordered data: ±1 h of displacement), bits 16..23 of every
+    // delta in a byte plane (b16_hi): 3 B per timestamp (Lucene's per-block bit packing, at 16 or 24 bits)
+    DevBuf b16, b16_base, b16_hi;
     // esgpu_segment_release_wide: the upload-width values of a single-valued long column with a compact copy were
     // released; wide_i64 rebuilds them (losslessly, from the deltas) for a kernel that reads them, and keeps them
     // released by esgpu_segment_release_wide, rebuilt on first use (wide_i64): written under the context lock, read
@@ -1732,6 +1734,7 @@ static const uint16_t* ensure_ord16(esgpu_ctx* c, const DevColumn* col, const es
 static const uint32_t* ensure_d32(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
 static const uint16_t* ensure_d16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
 static const DevColumn* ensure_b16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
+static int b24_mode();
 static const void* wide_i64(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st);
 static void sampled_hot_ords(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, uint32_t (&out)[4]);
 
@@ -3401,9 +3404,18 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         P.hv16 = nullptr;
         P.hv16_base = nullptr;
         P.hv32 = nullptr;
-        if ((pi && P.ord16 && P.mv16) || (P.raw_dense && hk_launch == 1)) {
+        // 24-bit runs where most zone blocks hold one key (their timestamps are not read: ±1 min of displacement, north
+        // star 1.28 -> 1.05 ms at 1B, r6ab); with wider displacement every block is multi-key, the kernel is bound by its
+        // per-doc work rather than by the bytes, and the 32-bit deltas' simpler unpack measured faster (±1 h: 2.12
+        // against 2.27 ms)
+        const bool b24_fits = !t16->b16_hi.p || b24_mode() == 2 || (pl.interval > 0 && !P.kstart && hc->zspan < pl.interval);
+        if (((pi && P.ord16 && P.mv16) || (P.raw_dense && hk_launch == 1)) && b24_fits) {
             P.hv16 = t16->b16.as<uint16_t>();
             P.hv16_base = t16->b16_base.as<int64_t>();
+            const bool b24 = t16->b16_hi.p != nullptr;
+            P.hv8 = b24 ? t16->b16_hi.as<uint8_t>() : (const uint8_t*)t16->b16.p;
+            P.hv8_mask = b24 ? 0xFFFFFFFFu : 0u;
+            P.hv8_and = b24 ? 0xFFu : 0u;
         } else {
             P.hv32 = ensure_d32(p->ctx, hc, s, p->stream);
             require(P.hv32 != nullptr, ESGPU_ERR_DEVICE, "out of device memory for the key column's deltas");
@@ -3478,7 +3490,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         goto relaunch;
     }
     if (pi || m32) bytes_per_doc -= P.mv16 ? 6 : 4;
-    if (P.hv16) bytes_per_doc -= 6;            // (+ one 8-byte base per run, below)
+    if (P.hv16) bytes_per_doc -= P.hv8_and ? 5 : 6;  // (+ one 8-byte base per run, below)
     else if (t16 && P.hv32) bytes_per_doc -= 4;
     uint32_t grid = (P.n_blocks + P.blocks_per_wg - 1) / P.blocks_per_wg;
     // dynamic chunk claiming: one resident wave of workgroups, each flushing its LDS cells once, taking chunks of
@@ -3506,7 +3518,7 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         HIPX(hipGetLastError());
         if (ud) {
             // (read by esgpu_plan_last_collect_stats: no per-collect copy to the host on the request's path)
-            p->zu_w[p->zu_n] = P.hv16 ? 2 : 4;  // timestamp bytes per doc the skipped blocks did not read
+            p->zu_w[p->zu_n] = P.hv16 ? (P.hv8_and ? 3 : 2) : 4;  // timestamp bytes per doc the skipped blocks did not read
             ++p->zu_n;
         }
     }
@@ -3571,6 +3583,16 @@ static bool runs1_on() {
 }
 // block-delta timestamps on the raw-load kernels (ensure_b16; ESGPU_OPT_BLOCK_DELTAS)
 static bool b16_on(const esgpu_ctx* c) { return c->opt_b16.load() != 0; }
+// ESGPU_B24=0: a column with a run spanning 2^16 or more keeps the 32-bit deltas (no 24-bit runs; A/B); 2: the 24-bit
+// runs whatever the zone span (A/B of the gate below)
+static int b24_mode() {
+    static const int m = [] {
+        const char* e = std::getenv("ESGPU_B24");
+        return e && e[0] == '0' ? 0 : e && e[0] == '2' ? 2 : 1;
+    }();
+    return m;
+}
+static bool b24_on() { return b24_mode() != 0; }
 // ESGPU_DD=1: every metric grid takes the compensated flushes, exact data or not (tests of those paths on integer data)
 static bool dd_forced() {
     static const bool on = [] { const char* e = std::getenv("ESGPU_DD"); return e && *e == '1'; }();
@@ -3658,7 +3680,8 @@ static const void* wide_i64_locked(esgpu_ctx* c, DevColumn* m, const esgpu_segme
     if (!m->wide_released.load(std::memory_order_relaxed) || m->values.p) return m->values.p;
     m->values.alloc(c, (size_t)s->n_pad * 8);
     if (m->d32.p) launch_expand_d32(m->d32.as<uint32_t>(), s->n_pad, m->vmin, m->values.as<int64_t>(), st);
-    else if (m->b16.p) launch_expand_b16(m->b16.as<uint16_t>(), m->b16_base.as<int64_t>(), s->max_doc, s->n_pad, m->values.as<int64_t>(), st);
+    else if (m->b16.p) launch_expand_b16(m->b16.as<uint16_t>(), m->b16_hi.as<uint8_t>(), m->b16_base.as<int64_t>(), s->max_doc, s->n_pad,
+                                         m->values.as<int64_t>(), st);
     else launch_expand_d16(m->d16.as<uint16_t>(), s->n_pad, m->vmin, m->values.as<int64_t>(), st);
     HIPX(hipGetLastError());
     HIPX(hipStreamSynchronize(st));
@@ -3689,8 +3712,8 @@ static const uint32_t* ensure_d32(esgpu_ctx* c, const DevColumn* col, const esgp
     return m->d32.as<uint32_t>();
 }
 
-// the block deltas of a dense single-valued long column (null when some run of kB16Docs docs spans 2^16 or more: the
-// column is not sorted enough; the verdict is cached)
+// the block deltas of a dense single-valued long column (null when some run of kB16Docs docs spans 2^24 or more, or 2^16
+// with ESGPU_B24=0: the column is not sorted enough; the verdict is cached)
 static const DevColumn* ensure_b16(esgpu_ctx* c, const DevColumn* col, const esgpu_segment* s, hipStream_t st) {
     DevColumn* m = const_cast<DevColumn*>(col);
     std::lock_guard<std::mutex> lk(c->mu);
@@ -3698,28 +3721,33 @@ static const DevColumn* ensure_b16(esgpu_ctx* c, const DevColumn* col, const esg
     m->b16_done = true;
     if (col->type != ESGPU_COL_I64 || col->multi || col->present.p || s->n_pad % kB16Docs) return nullptr;
     const uint32_t runs = s->n_pad >> kB16Shift;
+    const bool b24 = b24_on();
     try {
         m->b16.alloc(c, (size_t)s->n_pad * 2);
         m->b16_base.alloc(c, (size_t)std::max<uint32_t>(runs, 1) * 8);
+        if (b24) m->b16_hi.alloc(c, (size_t)s->n_pad);
     } catch (const EsError&) {
         m->b16.release();
         m->b16_base.release();
+        m->b16_hi.release();
         return nullptr;
     }
     DevBuf flag;
     flag.alloc(c, 4);
     HIPX(hipMemsetAsync(flag.p, 0, 4, st));
     launch_block_delta16((const int64_t*)wide_i64_locked(c, m, s, st), s->max_doc, s->n_pad, m->b16.as<uint16_t>(),
-                         m->b16_base.as<int64_t>(), flag.as<unsigned int>(), st);
+                         m->b16_hi.as<uint8_t>(), m->b16_base.as<int64_t>(), flag.as<unsigned int>(), st);
     HIPX(hipGetLastError());
     unsigned int bad = 0;
     HIPX(hipMemcpyAsync(&bad, flag.p, 4, hipMemcpyDeviceToHost, st));
     HIPX(hipStreamSynchronize(st));
-    if (bad) {
+    if ((bad & 2) || (bad && !b24)) {
         m->b16.release();
         m->b16_base.release();
+        m->b16_hi.release();
         return nullptr;
     }
+    if (!bad) m->b16_hi.release();  // (every run spans < 2^16: no plane)
     return m;
 }
 
