@@ -158,17 +158,20 @@ def _dense_ts(rng, n, t0, per_run_span):
     return (t0 + np.floor(np.arange(n) * step) + rng.integers(0, max(int(step), 1), size=n)).astype(np.int64)
 
 
-@pytest.mark.parametrize("t0,per_run,expect_block,jitter", [
-    (1_441_065_600_000, 30_000, True, 0),      # dense logs
-    (-3_600_000 * 5, 30_000, True, 0),          # before the epoch: negative keys and bases
-    (1_441_065_600_000, 66_000, False, 0),      # some run spans >= 2^16 ms: the 32-bit deltas instead
-    (1_441_065_600_000, 20_000, True, 20_000),  # merged-segment order: docs displaced by up to 20 s, runs still < 2^16
+@pytest.mark.parametrize("t0,per_run,layout,jitter", [
+    (1_441_065_600_000, 30_000, "b16", 0),      # dense logs
+    (-3_600_000 * 5, 30_000, "b16", 0),          # before the epoch: negative keys and bases
+    (1_441_065_600_000, 66_000, "b24", 0),      # some run spans >= 2^16 ms: 24-bit runs (a zone block spans < 5 min)
+    (1_441_065_600_000, 2_000_000, "d32", 0),   # runs < 2^24 ms but every zone block spans several keys: 32-bit deltas
+    (1_441_065_600_000, 20_000, "b16", 20_000),  # merged-segment order: docs displaced by up to 20 s, runs still < 2^16
+    (1_441_065_600_000, 20_000, "b24", 60_000),  # ... by up to 1 min: 24-bit runs, most zone blocks still single-key
 ])
-def test_block_delta_keys(engine, t0, per_run, expect_block, jitter):
+def test_block_delta_keys(engine, t0, per_run, layout, jitter):
     """Block-delta timestamps on every raw-load kernel that takes them -- packed cells (terms{date_histogram{stats}},
     unfiltered and through a folded filter), integer runs (date_histogram{extended_stats}), counting grids
     (date_histogram, terms{date_histogram}) -- over a ragged last run (n not a multiple of 2,048), against the oracle;
-    then the upload-width timestamps released and rebuilt from the block deltas (a calendar histogram reads them)."""
+    16-bit runs, 24-bit runs (a high-byte plane) and the 32-bit deltas where the zone blocks span several keys; then the
+    upload-width timestamps released and rebuilt from the block deltas (a calendar histogram reads them)."""
     rng = np.random.default_rng(50 + per_run)
     n = 2_000_000 + 777
     cols = _log_segment(rng, n, 0, 1)
@@ -188,15 +191,18 @@ def test_block_delta_keys(engine, t0, per_run, expect_block, jitter):
         r, nbytes = _run(engine, seg, [a])
         got.update(r.to_dict())
     assert_same(got, want["shards"][0], "block deltas")
-    # the key column's bytes: 2 B per doc + the run words on the block-delta layout (less the single-key zone blocks'
-    # timestamps: a block spans ~120 s here, 60 % of them within one 5-minute key), else 4 B
+    # the key column's bytes: 2 B (3 B with the high-byte plane) per doc + the run words on the block-delta layouts (less
+    # the single-key zone blocks' timestamps: a block spans ~120 s in the dense case, 60 % of them within one 5-minute
+    # key), else 4 B
     r, nbytes = _run(engine, seg, [aggs[2]])
-    if expect_block:
+    if layout == "b24":  # 3 B per doc of the multi-key zone blocks
+        assert run_bytes(n) + 0.5 * n < nbytes <= run_bytes(n) + 3 * n, nbytes / n
+    elif layout == "d32":
+        assert 3.9 * n < nbytes <= 4 * n + 64, nbytes / n
+    elif layout == "b16":
         assert run_bytes(n) < nbytes <= run_bytes(n) + 2 * n, nbytes / n
         if not jitter:
             assert run_bytes(n) + 0.4 * n < nbytes < run_bytes(n) + 1.2 * n, nbytes / n
-    else:  # the 32-bit deltas, of the multi-key zone blocks only (a block spans ~264 s: ~12 % hold one 5-minute key)
-        assert 2 * n < nbytes < 4 * n, nbytes / n
     accept = bits_from_mask(rng.random(n) >= 0.25)
     fw = O.run([(cols, n)], aggs[:1], accept=[accept])
     plan = engine.plan(aggs[:1])
@@ -214,10 +220,10 @@ def test_block_delta_keys(engine, t0, per_run, expect_block, jitter):
 @pytest.mark.parametrize("jitter", [60_000, 3_600_000])
 def test_jittered_timestamps(engine, jitter):
     """Roughly time-ordered data (merged segments: docs displaced by up to +-1 min / +-1 h; one day, 3M docs): every run
-    of 2,048 docs then spans >= 2^16 ms, so the key column is read as 32-bit deltas.  At +-1 min most zone blocks still
-    round to one hour (their deltas skipped, VK bit 16384; one integer run per thread); at +-1 h they span three, so
-    the histogram-only integer grids send each doc straight to its key's lane-rotated LDS cells (CollectParams.hdirect)
-    and the packed-cell grids take their per-doc path -- every leaf against the oracle, 1 h and 5 min keys."""
+    of 2,048 docs then spans >= 2^16 ms.  At +-1 min most zone blocks still round to one hour: the key column is read as
+    24-bit block deltas (the high-byte plane) with the single-key blocks skipped, one integer run per thread; at +-1 h
+    they span three keys: the 32-bit deltas, the histogram-only integer grids' window accumulators (kWin4) and the
+    packed-cell grids' per-doc path -- every leaf against the oracle, 1 h and 5 min keys."""
     rng = np.random.default_rng(61)
     n = 3_000_000 + 333
     cols = _log_segment(rng, n, 1_441_065_600_000, 86_400_000)
