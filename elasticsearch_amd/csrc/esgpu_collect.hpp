@@ -355,8 +355,8 @@ __device__ __forceinline__ void load_docs(const CollectParams& P, uint32_t doc0,
 #define ESGPU_DOCS8 1
 #endif
 #ifndef ESGPU_DOCS8_HI  // ... and the histogram-only integer-run grids over time-sorted data (VK bits 2048 | 4096), whose
-#define ESGPU_DOCS8_HI 0  // single-key blocks' packed run updates (CollectParams.dot16) -- measured level (config 2 at 1B
-#endif                    // 0.606 / 0.614 ms, r6m: SALU per 256 docs 72 -> 50, no faster) and off
+#define ESGPU_DOCS8_HI 1  // single-key blocks' packed run updates (CollectParams.dot16): level at 4 waves per SIMD (r6m),
+#endif                    // with 6 (ESGPU_HIST_RUNS1_WAVES) config 2 0.622 -> 0.523 ms at 1B (r6ag)
 #ifndef ESGPU_DOCS8_H  // ... the raw-load counting grids with a terms dimension (VK bit 1024; r5ab8: terms{date_histogram}
 #define ESGPU_DOCS8_H 1  // 0.96 -> 0.88 ms at 1B; the histogram-only grids measured 7 % slower at 8 and keep 4)
 #endif
@@ -1660,9 +1660,14 @@ __device__ __forceinline__ uint32_t claim_chunk(unsigned int* claim) {
 #ifndef ESGPU_HIST_MET_WAVES  // raw-load histogram-only grids with a metric: waves per SIMD
 #define ESGPU_HIST_MET_WAVES 4
 #endif
+#ifndef ESGPU_HIST_RUNS1_WAVES  // ... of them the one-run integer grids over time-sorted data (VK bits 2048 | 4096): the
+#define ESGPU_HIST_RUNS1_WAVES 6  // stream's bytes in flight scale with the waves (6 with 8 docs per thread: config 2
+#endif                            // 0.622 -> 0.523 ms at 1B, 0.0816 -> 0.0703 ms at 100M; the ±1 h window kernels at 6:
+                                  // 2.35 -> 4.49 ms, r6ag -- they keep 4)
 template <bool ORD, int MET, int VK, int WGS> constexpr int collect_min_waves() {
     return (VK & 64) && WGS == 512                    ? ESGPU_PI_WAVES
            : !ORD && (VK & 1024) && WGS == 512 && MET == 0 ? ESGPU_HIST_WAVES
+           : !ORD && (VK & 1024) && WGS == 512 && MET > 0 && (VK & 2048) && (VK & 4096) ? ESGPU_HIST_RUNS1_WAVES
            : !ORD && (VK & 1024) && WGS == 512        ? ESGPU_HIST_MET_WAVES
                                                      : 4;
 }

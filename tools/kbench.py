@@ -30,6 +30,8 @@ def variants():
         "date_hist": ([AB.dateHistogram("h").field("@timestamp").interval("1h")], None),
         "config2_dh_ext": ([AB.dateHistogram("h").field("@timestamp").interval("1h").subAggregation(
             AB.extendedStats("rt").field("response_time_ms"))], None),
+        "dh_stats": ([AB.dateHistogram("h").field("@timestamp").interval("1h").subAggregation(
+            AB.stats("rt").field("response_time_ms"))], None),
         "terms_dh": ([AB.terms("hosts").field("host").subAggregation(AB.dateHistogram("h").field("@timestamp").interval("1h"))], None),
         "config1_terms_stats": ([AB.terms("hosts").field("host").subAggregation(AB.stats("rt").field("response_time_ms"))], None),
         "north_star": ([ns(AB.stats("rt").field("response_time_ms"))], None),
