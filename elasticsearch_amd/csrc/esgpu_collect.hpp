@@ -1292,7 +1292,25 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
             if ((hit >> j) & 1) atomicAdd(&a.pk[cell[j] + a.coff], one + d.mvd[j]);
 #endif
         if (MET >= 2) {
-#if ESGPU_PI_MMCHECK == 2
+#if ESGPU_PI_MMCHECK == 4
+            // one divergent loop over the lane's moving bounds (ESGPU_PI_MMU 4)
+            uint32_t need = 0;
+#pragma unroll
+            for (int j = 0; j < kVec; ++j)
+                need |= (uint32_t)(((hit >> j) & 1) && (d.mvd[j] < mlo[j] || d.mvd[j] > mhi[j])) << j;
+            while (need) {
+                const uint32_t j0 = (uint32_t)__builtin_ctz(need);
+                need &= need - 1u;
+                uint32_t c = 0, x = 0;
+#pragma unroll
+                for (int j = 0; j < kVec; ++j) {
+                    c = j0 == (uint32_t)j ? cell[j] : c;
+                    x = j0 == (uint32_t)j ? d.mvd[j] : x;
+                }
+                atomicMin(&a.mm[2 * c], x);
+                atomicMax(&a.mm[2 * c + 1], x);
+            }
+#elif ESGPU_PI_MMCHECK == 2
             // one divergent region per doc: both atomics where either bound moves (the other is then a no-op)
 #pragma unroll
             for (int j = 0; j < kVec; ++j) {
@@ -1387,8 +1405,8 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
 #define ESGPU_PI_HOTPK 1
 #endif
 #ifndef ESGPU_PI_MMU  // (A/B) uniform blocks' (min, max) updates: 2 = one divergent region per doc (as ESGPU_PI_MMCHECK 2),
-#define ESGPU_PI_MMU 2  // 3 = branch-free -- every lane issues both atomics, lanes whose bounds do not move on a spare word
-#endif
+#define ESGPU_PI_MMU 2  // 3 = branch-free -- every lane issues both atomics, lanes whose bounds do not move on a spare word;
+#endif                  // 4 = one divergent loop per lane over its moving bounds (north star 1.03 -> 1.06 ms, r6aj)
 template <int MET, int VK, int NH, int NR>
 __device__ __forceinline__ void pi_uniform(const CollectParams& P, const Acc& a, const Doc4& h0, const Doc4& h1, uint32_t T,
                                            uint32_t win0, Runs<NR>& run, uint32_t mw, bool outer) {
@@ -1487,7 +1505,25 @@ __device__ __forceinline__ void pi_uniform(const CollectParams& P, const Acc& a,
     for (int j = 0; j < N; ++j)  // (a miss adds into the lane's spare word)
         atomicAdd(hpk[j] ? &a.pk[cb + t[j] + a.coff] : a.pkd, join64(dv[j], onehi));
     if (MET >= 2) {
-#if ESGPU_PI_MMU == 3
+#if ESGPU_PI_MMU == 4
+        // one divergent loop over the lane's moving bounds (most lanes have none: ~1 iteration where the per-doc regions
+        // issued the two atomics for up to N docs)
+        uint32_t need = 0;
+#pragma unroll
+        for (int j = 0; j < N; ++j) need |= (uint32_t)(hit[j] & ((dv[j] < mlo[j]) | (dv[j] > mhi[j]))) << j;
+        while (need) {
+            const uint32_t j0 = (uint32_t)__builtin_ctz(need);
+            need &= need - 1u;
+            uint32_t c = 0, x = 0;
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                c = j0 == (uint32_t)j ? t[j] : c;
+                x = j0 == (uint32_t)j ? dv[j] : x;
+            }
+            atomicMin(&a.mm[2 * (cb + c)], x);
+            atomicMax(&a.mm[2 * (cb + c) + 1], x);
+        }
+#elif ESGPU_PI_MMU == 3
         uint32_t* spare = reinterpret_cast<uint32_t*>(a.pkd);
 #pragma unroll
         for (int j = 0; j < N; ++j) {
