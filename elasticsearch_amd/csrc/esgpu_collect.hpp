@@ -972,6 +972,9 @@ __device__ __forceinline__ void runs_add_n(const CollectParams& P, const Acc& a,
 #define ESGPU_RUN4 0  // slower (config 2 at 1B docs 2.15 -> 2.62 ms, date_histogram 1.03 -> 1.14 ms): off, kept for A/B
 #endif
 
+#ifndef ESGPU_ORDH_HOT  // counting ORD x histogram raw-load grids: the segment's most frequent ordinal counted in a
+#define ESGPU_ORDH_HOT 0  // register in single-key zone blocks (cnt_hot_flush), its docs off the LDS atomics -- measured
+#endif                    // slower (terms{date_histogram} 0.885 -> 1.046 ms at 1B, r6am): A/B option, off
 #ifndef ESGPU_COMBINE4  // counting ORD x histogram grids: combine a thread's equal keys before the LDS atomics
 #define ESGPU_COMBINE4 1
 #endif
@@ -1007,6 +1010,15 @@ __device__ __forceinline__ void unpack_docs(const CollectParams& P, Doc4& d) {
     d.mpres = 0xFu;
 }
 
+// counting ORD x histogram raw-load grids with single-key zone blocks: the hot ordinal's register count (ESGPU_ORDH_HOT)
+template <bool ORD, bool HIST, int MET, int VK>
+constexpr bool kOrdHHot = ESGPU_ORDH_HOT != 0 && ORD && HIST && MET == 0 && kUKeyK<ORD, HIST, MET, VK>;
+template <int NR>
+__device__ __forceinline__ void cnt_hot_flush(const Acc& a, Runs<NR>& R, uint32_t T, uint32_t ht) {
+    if (R.hslot != ~0u && R.hcnt[0]) atomicAdd(&a.cnt32[R.hslot * T + ht + a.coff], R.hcnt[0]);
+    R.hcnt[0] = 0u;
+    R.hslot = ~0u;
+}
 template <bool ORD, bool HIST, int MET, bool LDS, bool KT, int MS, bool HORD = false, int VK = 0>
 __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, const Doc4& d_in, uint32_t T, int64_t base,
                                          uint32_t win0, Runs<runs_for<MET, VK>()>& run, uint32_t mw = 0, bool outer = true) {
@@ -1350,6 +1362,23 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
             const uint32_t t = d.ord[j];
             hk[j] = hit ? slot[j] : ~0u;
             cell[j] = hit && t != kMissingOrd && t < T ? slot[j] * T + t : ~0u;
+        }
+        if constexpr (kOrdHHot<ORD, HIST, MET, VK>) {
+            // a single-key zone block (wave-uniform): the hot ordinal's docs into the lane's register count for the key
+            // -- the Zipf head's same-address LDS atomics were the grid's conflicts
+            const uint32_t ht = P.hot_t[0];
+            if (ublock && ht < T) {
+                if (slot[0] != run.hslot) {
+                    cnt_hot_flush(a, run, T, ht);
+                    run.hslot = slot[0];
+                }
+#pragma unroll
+                for (int j = 0; j < kVec; ++j) {
+                    const bool h = cell[j] != ~0u && d.ord[j] == ht;
+                    run.hcnt[0] += h ? 1u : 0u;
+                    cell[j] = h ? ~0u : cell[j];
+                }
+            }
         }
         if (P.ocnt_mode == OCNT_HIST) {
             uint32_t key = ~0u, n = 0;
@@ -1700,8 +1729,12 @@ __device__ __forceinline__ uint32_t claim_chunk(unsigned int* claim) {
 #define ESGPU_HIST_RUNS1_WAVES 6  // stream's bytes in flight scale with the waves (6 with 8 docs per thread: config 2
 #endif                            // 0.622 -> 0.523 ms at 1B, 0.0816 -> 0.0703 ms at 100M; the ±1 h window kernels at 6:
                                   // 2.35 -> 4.49 ms, r6ag -- they keep 4)
+#ifndef ESGPU_ORDH_WAVES  // raw-load counting grids with a terms dimension (terms{date_histogram}, VK bit 1024): waves per SIMD
+#define ESGPU_ORDH_WAVES 4
+#endif
 template <bool ORD, int MET, int VK, int WGS> constexpr int collect_min_waves() {
     return (VK & 64) && WGS == 512                    ? ESGPU_PI_WAVES
+           : ORD && (VK & 1024) && WGS == 512 && MET == 0 ? ESGPU_ORDH_WAVES
            : !ORD && (VK & 1024) && WGS == 512 && MET == 0 ? ESGPU_HIST_WAVES
            : !ORD && (VK & 1024) && WGS == 512 && MET > 0 && (VK & 2048) && (VK & 4096) ? ESGPU_HIST_RUNS1_WAVES
            : !ORD && (VK & 1024) && WGS == 512        ? ESGPU_HIST_MET_WAVES
@@ -1876,6 +1909,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
         if (dirty) {
             if (!ORD) runs_flush<MET, kMS, runs_for<MET, VKL>(), kIntRuns<ORD, MET, VKL>, kWin4<MET, VKL>>(P, s, run);
             if constexpr (PI && (ESGPU_PI_HOT != 0 || ESGPU_PI_HOTU != 0)) pi_hot_flush<MET>(P, s, run, T);
+            if constexpr (kOrdHHot<ORD, HIST, MET, VKL>) cnt_hot_flush(s, run, T, P.hot_t[0]);
             if constexpr (PI) flush_window_pi<MET, WGS>(P, s, T, W, win0, ncp);
             else flush_window<MET, kMS, WGS>(P, s, T, W, win0, ncp);
         }
@@ -2005,6 +2039,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
     if (P.lds_mode && (dirty || !(HIST && P.windowed)) && !ESGPU_FLUSH_DIAG) {
         if (!ORD) runs_flush<MET, kMS, runs_for<MET, VKL>(), kIntRuns<ORD, MET, VKL>, kWin4<MET, VKL>>(P, s, run);
         if constexpr (PI && (ESGPU_PI_HOT != 0 || ESGPU_PI_HOTU != 0)) pi_hot_flush<MET>(P, s, run, T);
+        if constexpr (kOrdHHot<ORD, HIST, MET, VKL>) cnt_hot_flush(s, run, T, P.hot_t[0]);
         if constexpr (PI) flush_window_pi<MET, WGS>(P, s, T, W, win0, ncp);
         else flush_window<MET, kMS, WGS>(P, s, T, W, win0, ncp);
     }

@@ -3206,6 +3206,9 @@ static int collect_grid_cells(esgpu_plan* p, Pipeline& pl, const esgpu_segment* 
         if (L_ORD && P.ord && plain_ord && !oc->multi && oc->ord_count() < 0xFFFFu) {
             P.ord16 = ensure_ord16(p->ctx, oc, s, p->stream);
             if (P.ord16) bytes_per_doc -= 2;
+            // counting terms x histogram grids: the hot ordinal the kernel counts in registers in single-key zone blocks
+            // (ESGPU_ORDH_HOT; the packed-cell grids take theirs below)
+            if (P.ord16 && L_HIST && L_met == 0) sampled_hot_ords(p->ctx, oc, s, P.hot_t);
         }
         if (L_HIST && hc && !pl.inner_terms && !P.kstart && hc->type == ESGPU_COL_I64 && !hc->multi && hc->vmin <= hc->vmax &&
             (uint64_t)hc->vmax - (uint64_t)hc->vmin < (1ull << 32)) {
