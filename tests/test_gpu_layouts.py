@@ -243,6 +243,32 @@ def test_jittered_timestamps(engine, jitter):
     seg.close()
 
 
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_window_accumulators_fuzz(engine, seed):
+    """Window accumulators (kWin4: histogram-only integer grids over roughly time-ordered data, four key slots per
+    thread) under displacement that moves a thread's keys both ways: ±1 h to ±3 h jitter, 0.1 % of the docs thrown
+    days away (each one a re-base below or above the window and back), metric deltas up to the 16-bit edge, a ragged
+    last block -- extended_stats / stats / avg per key against the oracle, 1 h and 20 min keys."""
+    rng = np.random.default_rng(700 + seed)
+    n = 1_500_000 + 4099 * seed + 13
+    t0 = 1_441_065_600_000
+    ts = np.sort(rng.integers(t0, t0 + 3 * 86_400_000, size=n)).astype(np.int64)
+    ts += rng.integers(-(1 + seed) * 3_600_000, (1 + seed) * 3_600_000 + 1, size=n)
+    far = rng.random(n) < 0.001
+    ts[far] += rng.integers(-2 * 86_400_000, 2 * 86_400_000 + 1, size=int(far.sum()))
+    cols = _log_segment(rng, n, 0, 1, metric=rng.integers(0, 65536, size=n))
+    cols["@timestamp"]["values"] = ts
+    dh = lambda i: AB.dateHistogram("d").field("@timestamp").interval(i)  # noqa: E731
+    aggs = [dh("1h").subAggregation(AB.extendedStats("e").field("rt")),
+            dh("20m").subAggregation(AB.stats("s").field("rt")),
+            dh("1h").subAggregation(AB.avg("a").field("rt"))]
+    seg = engine.upload_segment(cols, n)
+    for k, a in enumerate(aggs):
+        r, _ = _run(engine, seg, [a])
+        assert_same(r.to_dict(), O.run([(cols, n)], [a])["shards"][0], f"seed {seed} agg {k}")
+    seg.close()
+
+
 def _log_segment(rng, n, t0, span_ms, nterms=300, metric=None):
     ranks = np.minimum(rng.zipf(1.2, size=n) - 1, nterms - 1)
     cols = {
