@@ -1559,6 +1559,14 @@ extern "C" int esgpu_plan_create(esgpu_ctx* c, const esgpu_agg_spec* specs, int3
 // every counter (HcParams::overwrite) -- or, settled by its hot slots, never reads them -- and needs no zeroing pass
 // (80 MB at 10M ordinals, 28 us per config-3 shard request); every other path, and a build with no collect, zeroes
 // them first.
+// ESGPU_EAGER_ZERO=0: a small grid's counts are zeroed at the first collect too (A/B)
+static bool eager_zero_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("ESGPU_EAGER_ZERO");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 static void zero_counts(esgpu_plan* p, Pipeline& pl) {
     if (!pl.zero_pending) return;
     pl.zero_pending = false;
@@ -5925,7 +5933,14 @@ extern "C" int esgpu_plan_reset(esgpu_plan* p) {
                 fl.v[fl.count] = v;
                 if (++fl.count == kFillSpans) { launch_fill_multi(fl, p->stream); fl.count = 0; }
             };
-            pl.zero_pending = pl.g_cnt.p != nullptr;  // (zero_counts: at the request's first collect or build)
+            // the counts: with the other arrays in this launch where the grid is small (the north star's 5.8 MB: one
+            // launch fewer ahead of the next collect), else at the request's first collect or build (zero_counts: a
+            // high-cardinality terms grid's first hot/cold segment writes its counts itself)
+            pl.zero_pending = pl.g_cnt.p != nullptr;
+            if (pl.zero_pending && eager_zero_on() && !pl.cnt32 && (size_t)pl.T * pl.H * 8 <= (16u << 20)) {
+                span(pl.g_cnt.p, (size_t)pl.T * pl.H, 0ull);
+                pl.zero_pending = false;
+            }
             if (pl.g_ocnt.p) {
                 if (pl.g_ocnt.bytes % 8 == 0) span(pl.g_ocnt.p, pl.g_ocnt.bytes / 8, 0ull);
                 else HIPX(hipMemsetAsync(pl.g_ocnt.p, 0, pl.g_ocnt.bytes, p->stream));
