@@ -1435,7 +1435,8 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
 #endif
 #ifndef ESGPU_PI_MMU  // (A/B) uniform blocks' (min, max) updates: 2 = one divergent region per doc (as ESGPU_PI_MMCHECK 2),
 #define ESGPU_PI_MMU 2  // 3 = branch-free -- every lane issues both atomics, lanes whose bounds do not move on a spare word;
-#endif                  // 4 = one divergent loop per lane over its moving bounds (north star 1.03 -> 1.06 ms, r6aj)
+#endif                  // 4 = one divergent loop per lane over its moving bounds (north star 1.03 -> 1.06 ms, r6aj);
+                        // 5 = one region per pair of docs, four unconditional atomics (0.99-1.02 -> 1.03-1.04 ms, r6au)
 template <int MET, int VK, int NH, int NR>
 __device__ __forceinline__ void pi_uniform(const CollectParams& P, const Acc& a, const Doc4& h0, const Doc4& h1, uint32_t T,
                                            uint32_t win0, Runs<NR>& run, uint32_t mw, bool outer) {
@@ -1534,7 +1535,24 @@ __device__ __forceinline__ void pi_uniform(const CollectParams& P, const Acc& a,
     for (int j = 0; j < N; ++j)  // (a miss adds into the lane's spare word)
         atomicAdd(hpk[j] ? &a.pk[cb + t[j] + a.coff] : a.pkd, join64(dv[j], onehi));
     if (MET >= 2) {
-#if ESGPU_PI_MMU == 4
+#if ESGPU_PI_MMU == 5
+        // one divergent region per pair of docs, its four atomics unconditional (a doc whose bounds stay on the lane's
+        // spare word)
+        uint32_t* spare = reinterpret_cast<uint32_t*>(a.pkd);
+#pragma unroll
+        for (int j = 0; j < N; j += 2) {
+            const bool m0 = hit[j] & ((dv[j] < mlo[j]) | (dv[j] > mhi[j]));
+            const bool m1 = hit[j + 1] & ((dv[j + 1] < mlo[j + 1]) | (dv[j + 1] > mhi[j + 1]));
+            if (m0 | m1) {
+                uint32_t* w0 = m0 ? &a.mm[2 * (cb + t[j])] : spare;
+                uint32_t* w1 = m1 ? &a.mm[2 * (cb + t[j + 1])] : spare;
+                atomicMin(w0, dv[j]);
+                atomicMax(w0 + 1, dv[j]);
+                atomicMin(w1, dv[j + 1]);
+                atomicMax(w1 + 1, dv[j + 1]);
+            }
+        }
+#elif ESGPU_PI_MMU == 4
         // one divergent loop over the lane's moving bounds (most lanes have none: ~1 iteration where the per-doc regions
         // issued the two atomics for up to N docs)
         uint32_t need = 0;
