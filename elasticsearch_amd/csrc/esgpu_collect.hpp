@@ -669,6 +669,12 @@ __device__ __forceinline__ void run_flush(const CollectParams& P, const Acc& a, 
 #define ESGPU_WIN4 1
 #endif
 template <int MET, int VK> constexpr bool kWin4 = ESGPU_WIN4 != 0 && MET > 0 && (VK & 2048) != 0 && (VK & 4096) == 0;
+#ifndef ESGPU_WIN_MK  // ... and the multi-key zone blocks of the one-run grids with single-key blocks (kWinMK): off --
+#define ESGPU_WIN_MK 0  // the accumulators' registers spill those kernels at 6 waves per SIMD (config 2 sorted 0.53 ->
+#endif                  // 3.66 ms, r6aw)
+template <bool ORD, bool HIST, int MET, int VK>
+constexpr bool kWinMK = ESGPU_WIN_MK != 0 && !ORD && MET > 0 && (VK & 2048) != 0 && (VK & 4096) != 0 &&
+                        kUKeyK<ORD, HIST, MET, VK>;
 template <int MET, int VK = 0> constexpr int runs_for() {
     return MET == 0 ? 1 : (VK & 4096) != 0 ? 1 : kWin4<MET, VK> ? 1 : (VK & 2048) != 0 ? ESGPU_INT_RUNS_NR : ESGPU_RUNS;
 }
@@ -773,10 +779,7 @@ __device__ __forceinline__ void win_flush(const CollectParams& P, const Acc& a, 
 }
 template <int MET, int MS, int NR, bool INT = false, bool WIN = false>
 __device__ __forceinline__ void runs_flush(const CollectParams& P, const Acc& a, Runs<NR>& R) {
-    if constexpr (WIN) {
-        win_flush<MET, MS>(P, a, R);
-        return;
-    }
+    if constexpr (WIN) win_flush<MET, MS>(P, a, R);
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
         if constexpr (INT) run_flush_i<MET, MS>(P, a, R.r[k]);
@@ -1122,7 +1125,12 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
             return;
         }
     }
-    if constexpr (LDS && kIntRuns<ORD, MET, VK> && kWin4<MET, VK>) {
+    // one-run grids over time-sorted data with single-key zone blocks (kWinMK): a multi-key block's quads (an hour
+    // boundary inside the block) go to the window accumulators too -- the one run flushed on every key change there, a
+    // wave's flushes on two LDS addresses
+    bool winq = kWin4<MET, VK>;
+    if constexpr (kWinMK<ORD, HIST, MET, VK>) winq = !ublock;
+    if constexpr (LDS && kIntRuns<ORD, MET, VK> && (kWin4<MET, VK> || kWinMK<ORD, HIST, MET, VK>)) if (winq) {
         uint32_t vm = 0;
         bool miss = false;
 #pragma unroll
@@ -1925,7 +1933,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
     uint32_t pass = 0, npass = 1;                        // npass > 1: a multi-pass group
     auto slide_to = [&](uint32_t k0) {
         if (dirty) {
-            if (!ORD) runs_flush<MET, kMS, runs_for<MET, VKL>(), kIntRuns<ORD, MET, VKL>, kWin4<MET, VKL>>(P, s, run);
+            if (!ORD) runs_flush<MET, kMS, runs_for<MET, VKL>(), kIntRuns<ORD, MET, VKL>, kWin4<MET, VKL> || kWinMK<ORD, HIST, MET, VKL>>(P, s, run);
             if constexpr (PI && (ESGPU_PI_HOT != 0 || ESGPU_PI_HOTU != 0)) pi_hot_flush<MET>(P, s, run, T);
             if constexpr (kOrdHHot<ORD, HIST, MET, VKL>) cnt_hot_flush(s, run, T, P.hot_t[0]);
             if constexpr (PI) flush_window_pi<MET, WGS>(P, s, T, W, win0, ncp);
@@ -2055,7 +2063,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
 #define ESGPU_FLUSH_DIAG 0
 #endif
     if (P.lds_mode && (dirty || !(HIST && P.windowed)) && !ESGPU_FLUSH_DIAG) {
-        if (!ORD) runs_flush<MET, kMS, runs_for<MET, VKL>(), kIntRuns<ORD, MET, VKL>, kWin4<MET, VKL>>(P, s, run);
+        if (!ORD) runs_flush<MET, kMS, runs_for<MET, VKL>(), kIntRuns<ORD, MET, VKL>, kWin4<MET, VKL> || kWinMK<ORD, HIST, MET, VKL>>(P, s, run);
         if constexpr (PI && (ESGPU_PI_HOT != 0 || ESGPU_PI_HOTU != 0)) pi_hot_flush<MET>(P, s, run, T);
         if constexpr (kOrdHHot<ORD, HIST, MET, VKL>) cnt_hot_flush(s, run, T, P.hot_t[0]);
         if constexpr (PI) flush_window_pi<MET, WGS>(P, s, T, W, win0, ncp);
