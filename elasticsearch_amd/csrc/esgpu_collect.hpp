@@ -671,10 +671,15 @@ __device__ __forceinline__ void run_flush(const CollectParams& P, const Acc& a, 
 template <int MET, int VK> constexpr bool kWin4 = ESGPU_WIN4 != 0 && MET > 0 && (VK & 2048) != 0 && (VK & 4096) == 0;
 #ifndef ESGPU_WIN_MK  // ... and the multi-key zone blocks of the one-run grids with single-key blocks (kWinMK): off --
 #define ESGPU_WIN_MK 0  // the accumulators' registers spill those kernels at 6 waves per SIMD (config 2 sorted 0.53 ->
-#endif                  // 3.66 ms, r6aw)
+#endif                  // 3.66 ms with four slots, r6aw; 2.59 ms with two, r6ay)
 template <bool ORD, bool HIST, int MET, int VK>
 constexpr bool kWinMK = ESGPU_WIN_MK != 0 && !ORD && MET > 0 && (VK & 2048) != 0 && (VK & 4096) != 0 &&
                         kUKeyK<ORD, HIST, MET, VK>;
+#ifndef ESGPU_WIN_MK_SLOTS  // key slots of the multi-key-block windows (kWinMK): 2 (an hour boundary inside a block)
+#define ESGPU_WIN_MK_SLOTS 2
+#endif
+template <bool ORD, bool HIST, int MET, int VK>
+constexpr int kWinSlots = kWinMK<ORD, HIST, MET, VK> ? ESGPU_WIN_MK_SLOTS : 4;
 template <int MET, int VK = 0> constexpr int runs_for() {
     return MET == 0 ? 1 : (VK & 4096) != 0 ? 1 : kWin4<MET, VK> ? 1 : (VK & 2048) != 0 ? ESGPU_INT_RUNS_NR : ESGPU_RUNS;
 }
@@ -754,10 +759,10 @@ __device__ __forceinline__ void pi_hot_flush(const CollectParams& P, const Acc& 
     R.hslot = ~0u;
 }
 // the window accumulators into their LDS cells (each slot with docs as one integer run), then emptied
-template <int MET, int MS, int NR>
+template <int MET, int MS, int NR, int S = 4>
 __device__ __forceinline__ void win_flush(const CollectParams& P, const Acc& a, Runs<NR>& R) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < S; ++k) {
         if (R.wc[k]) {
             Run r;
             run_reset(r);
@@ -777,9 +782,9 @@ __device__ __forceinline__ void win_flush(const CollectParams& P, const Acc& a, 
     R.wmx[0] = R.wmx[1] = 0u;
     R.wb = kWinEmpty;
 }
-template <int MET, int MS, int NR, bool INT = false, bool WIN = false>
+template <int MET, int MS, int NR, bool INT = false, bool WIN = false, int WS = 4>
 __device__ __forceinline__ void runs_flush(const CollectParams& P, const Acc& a, Runs<NR>& R) {
-    if constexpr (WIN) win_flush<MET, MS>(P, a, R);
+    if constexpr (WIN) win_flush<MET, MS, NR, WS>(P, a, R);
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
         if constexpr (INT) run_flush_i<MET, MS>(P, a, R.r[k]);
@@ -846,12 +851,12 @@ __device__ __forceinline__ void runs_add_pk(const CollectParams& P, const Acc& a
 // one doc (v: it passes and has a key) into window slot o = slot - wb (o < 4 when v): the slot's 0/1 weight e multiplies
 // the delta into each sum (v_mad), so a doc costs ~30 VALU where the three runs' hit search and predicated updates took
 // ~110 (config 2 at ±1 h, SQ counters r6ac: 446 VALU per wave per 256 docs)
-template <int MET, int NR>
+template <int MET, int NR, int S = 4>
 __device__ __forceinline__ void win_add(Runs<NR>& R, uint32_t o, uint32_t x, bool v) {
     const uint32_t oh = v ? 1u << ((o & 3u) << 3) : 0u;  // one-hot byte of the slot
     const uint32_t xx = x * x;                              // (x < 2^16)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < S; ++k) {
         const uint32_t e = (oh >> (8 * k)) & 0xFFu;
         R.wc[k] += e;
         R.ws[k] += x * e;
@@ -860,7 +865,7 @@ __device__ __forceinline__ void win_add(Runs<NR>& R, uint32_t o, uint32_t x, boo
     if (MET >= 2) {
         const uint32_t sh = (o & 1u) << 4;
         const uint32_t xm = (x << sh) | (0xFFFF0000u >> sh), xM = x << sh;  // the other half: min / max identities
-        const bool h0 = v && o < 2u, h1 = v && o >= 2u;
+        const bool h0 = v && o < 2u, h1 = S > 2 && v && o >= 2u;
         const u16x2_t m = __builtin_bit_cast(u16x2_t, xm), M = __builtin_bit_cast(u16x2_t, xM);
         const uint32_t n0 = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2_t, R.wmn[0]), m));
         const uint32_t n1 = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2_t, R.wmn[1]), m));
@@ -874,11 +879,12 @@ __device__ __forceinline__ void win_add(Runs<NR>& R, uint32_t o, uint32_t x, boo
 }
 // a doc whose slot is outside the window: flush it and re-base -- new keys above put the slot at the top (the keys of
 // roughly time-ordered data drift upwards), below at the bottom, a first doc one above the bottom
-template <int MET, int MS, int NR>
+template <int MET, int MS, int NR, int S = 4>
 __device__ __forceinline__ void win_rebase(const CollectParams& P, const Acc& a, Runs<NR>& R, uint32_t slot) {
     const uint32_t old = R.wb;
-    win_flush<MET, MS>(P, a, R);
-    R.wb = old == kWinEmpty ? (slot ? slot - 1u : 0u) : slot > old ? (slot >= 3u ? slot - 3u : 0u) : slot;
+    win_flush<MET, MS, NR, S>(P, a, R);
+    constexpr uint32_t top = S - 1;
+    R.wb = old == kWinEmpty ? (S > 2 && slot ? slot - 1u : slot) : slot > old ? (slot >= top ? slot - top : 0u) : slot;
 }
 template <int MET, int MS, int NR>
 __device__ __forceinline__ void runs_add(const CollectParams& P, const Acc& a, Runs<NR>& R, uint32_t slot, bool mpres, double x) {
@@ -1129,6 +1135,7 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
     // boundary inside the block) go to the window accumulators too -- the one run flushed on every key change there, a
     // wave's flushes on two LDS addresses
     bool winq = kWin4<MET, VK>;
+    constexpr int WS = kWinSlots<ORD, HIST, MET, VK>;
     if constexpr (kWinMK<ORD, HIST, MET, VK>) winq = !ublock;
     if constexpr (LDS && kIntRuns<ORD, MET, VK> && (kWin4<MET, VK> || kWinMK<ORD, HIST, MET, VK>)) if (winq) {
         uint32_t vm = 0;
@@ -1137,18 +1144,18 @@ __device__ __forceinline__ void process4(const CollectParams& P, const Acc& a, c
         for (int j = 0; j < kVec; ++j) {
             const bool v = ((d.ok >> j) & 1) && hv_ok[j];
             vm |= (uint32_t)v << j;
-            miss = miss || (v && slot[j] - run.wb >= 4u);
+            miss = miss || (v && slot[j] - run.wb >= (uint32_t)WS);
         }
         if (miss) {  // (rare: a lane's keys left its window) one doc at a time, re-basing where needed
 #pragma unroll
             for (int j = 0; j < kVec; ++j) {
                 if (!((vm >> j) & 1)) continue;
-                if (slot[j] - run.wb >= 4u) win_rebase<MET, MS>(P, a, run, slot[j]);
-                win_add<MET>(run, slot[j] - run.wb, d.mvd[j], true);
+                if (slot[j] - run.wb >= (uint32_t)WS) win_rebase<MET, MS, runs_for<MET, VK>(), WS>(P, a, run, slot[j]);
+                win_add<MET, runs_for<MET, VK>(), WS>(run, slot[j] - run.wb, d.mvd[j], true);
             }
         } else {
 #pragma unroll
-            for (int j = 0; j < kVec; ++j) win_add<MET>(run, slot[j] - run.wb, d.mvd[j], (vm >> j) & 1);
+            for (int j = 0; j < kVec; ++j) win_add<MET, runs_for<MET, VK>(), WS>(run, slot[j] - run.wb, d.mvd[j], (vm >> j) & 1);
         }
         return;
     }
@@ -1933,7 +1940,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
     uint32_t pass = 0, npass = 1;                        // npass > 1: a multi-pass group
     auto slide_to = [&](uint32_t k0) {
         if (dirty) {
-            if (!ORD) runs_flush<MET, kMS, runs_for<MET, VKL>(), kIntRuns<ORD, MET, VKL>, kWin4<MET, VKL> || kWinMK<ORD, HIST, MET, VKL>>(P, s, run);
+            if (!ORD) runs_flush<MET, kMS, runs_for<MET, VKL>(), kIntRuns<ORD, MET, VKL>, kWin4<MET, VKL> || kWinMK<ORD, HIST, MET, VKL>, kWinSlots<ORD, HIST, MET, VKL>>(P, s, run);
             if constexpr (PI && (ESGPU_PI_HOT != 0 || ESGPU_PI_HOTU != 0)) pi_hot_flush<MET>(P, s, run, T);
             if constexpr (kOrdHHot<ORD, HIST, MET, VKL>) cnt_hot_flush(s, run, T, P.hot_t[0]);
             if constexpr (PI) flush_window_pi<MET, WGS>(P, s, T, W, win0, ncp);
@@ -2063,7 +2070,7 @@ __global__ __launch_bounds__(WGS, (collect_min_waves<ORD, MET, VK, WGS>())) void
 #define ESGPU_FLUSH_DIAG 0
 #endif
     if (P.lds_mode && (dirty || !(HIST && P.windowed)) && !ESGPU_FLUSH_DIAG) {
-        if (!ORD) runs_flush<MET, kMS, runs_for<MET, VKL>(), kIntRuns<ORD, MET, VKL>, kWin4<MET, VKL> || kWinMK<ORD, HIST, MET, VKL>>(P, s, run);
+        if (!ORD) runs_flush<MET, kMS, runs_for<MET, VKL>(), kIntRuns<ORD, MET, VKL>, kWin4<MET, VKL> || kWinMK<ORD, HIST, MET, VKL>, kWinSlots<ORD, HIST, MET, VKL>>(P, s, run);
         if constexpr (PI && (ESGPU_PI_HOT != 0 || ESGPU_PI_HOTU != 0)) pi_hot_flush<MET>(P, s, run, T);
         if constexpr (kOrdHHot<ORD, HIST, MET, VKL>) cnt_hot_flush(s, run, T, P.hot_t[0]);
         if constexpr (PI) flush_window_pi<MET, WGS>(P, s, T, W, win0, ncp);
